@@ -1,0 +1,255 @@
+/*
+ * mpx.h — C ABI of the MI355X batched Multi-Paxos acceptor/learner engine.
+ *
+ * This header is the drop-in boundary for the hot path of yuchenkan/multi-paxos
+ * (SURVEY.md §8(b)).  The reference host talks to its protocol core through
+ *
+ *   paxos::NetWork::OnReceiveMessage(const char *msg, unsigned len)
+ *       multi/paxos.h:202, multi/paxos.cpp:1714-1717     (inbound bytes)
+ *   paxos::NetWork::SendMessageTCP / SendMessageUDP(ip, port, msg)
+ *       multi/paxos.h:199-200                            (outbound bytes)
+ *   paxos::StateMachine::Execute(const std::string &)
+ *       multi/paxos.h:219                                (in-order apply)
+ *   member: NetWork::OnReceive / Send, StateMachine::Apply
+ *       member/paxos.h:169,180-181
+ *
+ * and the engine replaces the per-message handlers behind them
+ * (OnPrepare/OnAccept/OnCommit/OnPrepareReply/OnAcceptReply/OnReject,
+ * multi/paxos.cpp:858-1623; member/paxos.cpp:1029-1818) with HIP kernels
+ * over structure-of-arrays state in HBM.
+ *
+ * Conventions
+ *   - plain C types only; every function returns int (MPX_OK = 0, <0 error);
+ *   - a handle is single-threaded (like the reference's one paxos thread per
+ *     node, multi/paxos.cpp:345); one HIP stream per engine;
+ *   - the caller keeps ownership of every buffer it passes in (the reference's
+ *     OnReceiveMessage copies into a std::string, multi/paxos.cpp:1716);
+ *   - where the reference would ASSERT-crash (multi/paxos.h:110) the engine
+ *     records the first violation (mpx_last_violation) and keeps going.
+ *
+ * Wire vocabulary: messages are the reference's packed little-endian structs
+ * (SURVEY.md Appendix A).  Two engine-local record types describe what the
+ * proposer control plane of the reference did at that point in the node's
+ * processing order (it is out of scope):
+ *   MPX_MSG_P_START  {u32 type=16, u64 ballot}            StartPrepare, multi/paxos.cpp:1233-1248
+ *                                                        (+ AcceptRejected's batch clear, :1328-1343)
+ *   MPX_MSG_P_BATCH  {u32 type=17, u64 accept_id, u32 len, {u64 iid, Value}*}
+ *                                                        a new AcceptingValues, multi/paxos.cpp:1299-1326
+ */
+#ifndef MPX_H
+#define MPX_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPX_ABI_VERSION 1u
+
+/* ---- status codes ------------------------------------------------------ */
+enum {
+    MPX_OK            = 0,
+    MPX_E_INVAL       = -1,   /* bad argument                                   */
+    MPX_E_NOMEM       = -2,   /* host or device allocation failed               */
+    MPX_E_HIP         = -3,   /* a HIP runtime call failed                      */
+    MPX_E_DECODE      = -4,   /* malformed wire message (unknown type, short)   */
+    MPX_E_RANGE       = -5,   /* value outside what the engine encodes          */
+    MPX_E_STATE       = -6,   /* call not valid in the engine's current state   */
+    MPX_E_NODEVICE    = -7,   /* no usable GPU (the engine never falls back)    */
+    MPX_E_COMM        = -8,   /* RCCL failure                                   */
+    MPX_E_VALUE       = -9    /* two different Values share (proposer,value_id) */
+};
+
+/* ---- wire message types (multi/paxos.cpp:742,831,847,1283,1346,1430,1482) */
+enum {
+    MPX_MSG_PREPARE       = 0,
+    MPX_MSG_PREPARE_REPLY = 1,
+    MPX_MSG_REJECT        = 2,
+    MPX_MSG_ACCEPT        = 3,
+    MPX_MSG_ACCEPT_REPLY  = 4,
+    MPX_MSG_COMMIT        = 5,   /* member: LEARN       (member/paxos.cpp:611) */
+    MPX_MSG_COMMIT_REPLY  = 6,   /* member: LEARN_REPLY (member/paxos.cpp:612) */
+    MPX_MSG_P_START       = 16,  /* engine-local proposer marker, see above   */
+    MPX_MSG_P_BATCH       = 17
+};
+
+enum { MPX_SEM_MULTI = 0, MPX_SEM_MEMBER = 1 };
+
+/* Largest node count: votes are one 64-bit acceptor mask per batch. */
+#define MPX_MAX_NODES 64u
+
+/*
+ * Value handles.  A reference Value is (u32 proposer, u64 value_id, bool noop,
+ * payload) and (proposer, value_id) names it uniquely (multi/paxos.cpp:439).
+ * On the device a Value is the 64-bit handle
+ *     proposer << 48 | noop << 47 | value_id
+ * (proposer < 2^14, value_id < 2^47, else MPX_E_RANGE); payload bytes stay in
+ * a host table and are checked to be unique per handle at ingest (MPX_E_VALUE).
+ */
+#define MPX_HANDLE(proposer, noop, value_id) \
+    (((uint64_t)(proposer) << 48) | ((uint64_t)((noop) ? 1 : 0) << 47) | (uint64_t)(value_id))
+#define MPX_HANDLE_PROPOSER(h) ((uint32_t)(((h) >> 48) & 0x3FFFu))
+#define MPX_HANDLE_NOOP(h)     ((unsigned)(((h) >> 47) & 1u))
+#define MPX_HANDLE_VALUE_ID(h) ((h) & ((1ull << 47) - 1))
+/* mpx_read_chosen / mpx_read_node_state mark present entries with this bit */
+#define MPX_PRESENT (1ull << 63)
+
+/* member semantics: one entry per membership epoch (member/paxos.cpp:1864-1964)
+ * An acceptor drops PREPARE/ACCEPT whose version differs from its own
+ * (member/paxos.cpp:1702,1744); the quorum is |acceptors|/2+1 (:1171,1327). */
+typedef struct mpx_epoch {
+    uint32_t version;
+    uint32_t pad;
+    uint64_t acceptor_mask;   /* bit i set: node i is an acceptor in this epoch */
+} mpx_epoch;
+
+typedef struct mpx_config {
+    uint32_t abi_version;      /* MPX_ABI_VERSION                                  */
+    uint32_t num_nodes;        /* node ids 0..num_nodes-1 (multi: all roles)       */
+    uint32_t semantics;        /* MPX_SEM_MULTI | MPX_SEM_MEMBER                   */
+    int32_t  device;           /* HIP device ordinal                               */
+    uint64_t shard_begin;      /* this engine owns instances [shard_begin,         */
+    uint64_t shard_end;        /*                              shard_end)          */
+    uint32_t num_epochs;       /* member only                                      */
+    uint32_t flags;            /* reserved, 0                                      */
+    const mpx_epoch *epochs;   /* member only, indexed by version                  */
+} mpx_config;
+
+typedef struct mpx_engine mpx_engine;
+
+/* Counters of the last run.  B_alg = 16 P + 24 A + 16 L. */
+typedef struct mpx_stats {
+    uint64_t chosen;           /* C: distinct instances whose accept votes first
+                                  reached quorum (multi/paxos.cpp:1416)           */
+    uint64_t promise_entries;  /* P: entries in granted PREPARE_REPLYs           */
+    uint64_t accept_apps;      /* A: granted (acceptor, instance) applications    */
+    uint64_t commit_apps;      /* L: (learner, instance) commit applications     */
+    uint64_t messages;         /* records processed                               */
+    uint64_t violations;       /* reference ASSERTs that would have fired         */
+    uint64_t chosen_digest;    /* order-independent digest of the chosen log      */
+    uint64_t state_digest;     /* ... of every node's final acceptor/learner state */
+    uint64_t scalar_digest;    /* ... of every node's promised / max_seen         */
+    uint64_t device_ns;        /* device time of the last run (first..last kernel) */
+    uint64_t apply_ns;         /* device time of the acceptor/learner kernel      */
+    uint64_t ingest_ns;        /* host ingest + H2D of the last submit batch       */
+    uint64_t bytes_alg;        /* 16 P + 24 A + 16 L                               */
+    uint64_t reserved[3];
+} mpx_stats;
+
+typedef struct mpx_violation {
+    uint64_t code;             /* MPX_V_*                                          */
+    uint32_t node;
+    uint32_t pad;
+    uint64_t seq;              /* record index in the node's stream               */
+    uint64_t iid;
+} mpx_violation;
+
+enum {
+    MPX_V_NONE          = 0,
+    MPX_V_COMMIT_VALUE  = 1,   /* re-commit with another Value, multi/paxos.cpp:1508-1509 */
+    MPX_V_CHOSEN_VALUE  = 2,   /* two chosen batches disagree on an instance (safety)     */
+    MPX_V_BAD_NODE      = 3,   /* reply from a node not in the set, multi/paxos.cpp:1040,1414 */
+    MPX_V_DUP_IID       = 4,   /* an instance twice in one message / overlapping ranges   */
+    MPX_V_BATCH_BEFORE_QUORUM = 5, /* P_BATCH while preparing, multi/paxos.cpp:1054   */
+    MPX_V_LEARN_VALUE   = 6    /* member: accept/learn differs from learned value         */
+};
+
+/* ---- lifecycle ----------------------------------------------------------- */
+int  mpx_version(void);
+int  mpx_device_count(int *count);
+int  mpx_create(const mpx_config *cfg, mpx_engine **out);
+int  mpx_destroy(mpx_engine *eng);
+
+/* ---- inbound: batched NetWork::OnReceiveMessage -------------------------- *
+ * Appends `count` records to node `node`'s receive stream in arrival order.
+ * Record i is bytes[offsets[i] .. offsets[i+1]) (offsets has count+1 entries).
+ * Decoding and instance bucketing happen here, on the host (the reference
+ * decodes in the handlers: ExtractInstanceValues etc., multi/paxos.cpp:523-711).
+ */
+int  mpx_submit(mpx_engine *eng, uint32_t node, const uint8_t *bytes,
+                const uint64_t *offsets, uint64_t count);
+/* Convenience: submit every node of an MPXT trace container (see mpx_trace_*). */
+int  mpx_submit_trace(mpx_engine *eng, const uint8_t *trace, uint64_t size);
+
+/* Apply everything submitted since the last run (state carries over). */
+int  mpx_run(mpx_engine *eng);
+/* Drop all acceptor/learner/proposer state back to genesis (the PaxosImpl
+ * ctor state, multi/paxos.cpp:323-346).  The resident trace is kept. */
+int  mpx_reset_state(mpx_engine *eng);
+/* One bench step: reset_state + replay the whole resident trace, no host
+ * synchronisation (kernels queued on the engine's stream). */
+int  mpx_step(mpx_engine *eng);
+int  mpx_sync(mpx_engine *eng);
+
+/* ---- outbound ------------------------------------------------------------ */
+/* Replies generated by the acceptor/learner handlers of the last run, in the
+ * reference's generation order per node (types 1,2,4,6; multi/paxos.cpp:
+ * 888-899,1391-1403,1577-1582).  The callback gets a pointer valid for the
+ * duration of the call (the reference passes a const std::string&). */
+typedef void (*mpx_send_fn)(void *user, uint32_t src, uint32_t dst,
+                            const uint8_t *bytes, uint32_t len);
+int  mpx_drain_sends(mpx_engine *eng, mpx_send_fn fn, void *user);
+
+/* chosen log: out[i] = MPX_PRESENT | handle, or 0 if instance first+i is not
+ * chosen yet (instances outside the shard are an error). */
+int  mpx_read_chosen(mpx_engine *eng, uint64_t first, uint64_t count, uint64_t *out);
+/* per-node scalars: promised_proposal_id_ and max_proposal_id_
+ * (multi/paxos.cpp:492,460) */
+int  mpx_read_node_scalars(mpx_engine *eng, uint32_t node,
+                           uint64_t *promised, uint64_t *max_seen);
+/* per-node per-instance state; any output pointer may be NULL.
+ * acc_value / com_value carry MPX_PRESENT when the entry exists. */
+int  mpx_read_node_state(mpx_engine *eng, uint32_t node, uint64_t first, uint64_t count,
+                         uint64_t *acc_ballot, uint64_t *acc_value,
+                         uint64_t *com_ballot, uint64_t *com_value);
+int  mpx_stats_get(mpx_engine *eng, mpx_stats *out);
+int  mpx_last_violation(mpx_engine *eng, mpx_violation *out);
+/* Canonical result dump (format "MPXR"): the byte format
+ * the CPU oracle and the reference driver also write, so parity is a
+ * byte comparison.  *out is malloc'ed; free with mpx_free. */
+int  mpx_dump_result(mpx_engine *eng, uint8_t **out, uint64_t *size);
+/* Encoded reference Value bytes (multi/paxos.cpp:556-598) for a handle. */
+int  mpx_value_bytes(mpx_engine *eng, uint64_t handle, uint8_t *buf,
+                     uint32_t cap, uint32_t *len);
+void mpx_free(void *p);
+
+/* ---- synthetic traces (host generator, deterministic) --------------------- */
+typedef struct mpx_gen_params {
+    uint32_t kind;             /* MPX_GEN_CLEAN | MPX_GEN_FAULTY | MPX_GEN_MEMBER  */
+    uint32_t num_nodes;
+    uint64_t num_instances;    /* M                                                */
+    uint64_t seed;
+    uint32_t batch;            /* instances per ACCEPT/COMMIT (clean: fixed)       */
+    uint32_t proposers;        /* competing proposers (faulty)                     */
+    uint32_t drop_rate;        /* per 10000, HijackSend model multi/main.cpp:116-132 */
+    uint32_t dup_rate;         /* per 10000, duplicates up to depth 3              */
+    uint32_t max_delay;        /* delay U[0,max_delay) ticks: reordering           */
+    uint32_t noop_permille;    /* faulty: share of noop gap-fill values            */
+    uint64_t shard_begin;      /* emit only instance entries in [begin,end);       */
+    uint64_t shard_end;        /*   headers are replicated       */
+} mpx_gen_params;
+
+enum { MPX_GEN_CLEAN = 0, MPX_GEN_FAULTY = 1, MPX_GEN_MEMBER = 2 };
+
+/* Build an MPXT trace container in host memory (free with mpx_free). */
+int  mpx_trace_generate(const mpx_gen_params *p, uint8_t **out, uint64_t *size);
+/* Materialise the clean trace of `p` directly in HBM (GPU generator kernel;
+ * same content as mpx_trace_generate for MPX_GEN_CLEAN, restricted to the
+ * engine's shard).  Replaces the resident trace. */
+int  mpx_load_clean_device(mpx_engine *eng, const mpx_gen_params *p);
+
+/* ---- multi-GPU: RCCL over xGMI, summary all-gather only -- */
+#define MPX_UID_BYTES 128
+int  mpx_comm_unique_id(uint8_t out[MPX_UID_BYTES]);
+int  mpx_comm_init(mpx_engine *eng, const uint8_t uid[MPX_UID_BYTES],
+                   int rank, int nranks);
+/* All-gather every rank's 64-word run summary (mpx_stats words + per-node
+ * scalars) over RCCL on the engine's stream; out holds nranks*64 words. */
+int  mpx_allgather_summary(mpx_engine *eng, uint64_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPX_H */

@@ -1,0 +1,704 @@
+/*
+ * mpx_oracle.c — CPU restatement of the reference's acceptor / learner /
+ * proposer-aggregation handlers.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This file is the parity checker for the MI355X engine.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it; the
+ * product path (multi-paxos_amd/) never links or calls it.
+ *
+ * Parity pin: every behaviour below is checked against the reference's own
+ * handlers (multi/paxos.cpp compiled in place from /root/reference by
+ * oracle/Makefile into oracle/_ref/libmpx_ref.so) on the committed golden
+ * traces under tests/golden/ (tests/test_oracle.py), and against the
+ * reference's UNITTEST codec vectors (multi/paxos.cpp:1753-1777).
+ *
+ * Input : an MPXT trace container (DESIGN.md §Trace container): per node the
+ *         ordered receive stream, records are the reference's packed wire
+ *         messages plus the engine-local proposer markers P_START / P_BATCH.
+ * Output: an MPXR canonical result — the same bytes the
+ *         engine's mpx_dump_result and the reference driver produce.
+ *
+ * Everything is sequential, one node after another, one record after another,
+ * exactly the reference's processing order (PaxosImpl::Loop, paxos.cpp:1654).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef uint8_t u8;
+
+/* ---- little-endian access (the reference memcpy's host structs; x86) ---- */
+static u32 rd32(const u8 *p) { u32 v; memcpy(&v, p, 4); return v; }
+static u64 rd64(const u8 *p) { u64 v; memcpy(&v, p, 8); return v; }
+
+/* ---- growable byte buffer ------------------------------------------------ */
+typedef struct { u8 *p; size_t n, cap; int oom; } buf_t;
+static void bput(buf_t *b, const void *src, size_t n)
+{
+    if (b->oom) return;
+    if (b->n + n > b->cap) {
+        size_t c = b->cap ? b->cap : 256;
+        while (c < b->n + n) c *= 2;
+        u8 *q = (u8 *)realloc(b->p, c);
+        if (!q) { b->oom = 1; return; }
+        b->p = q; b->cap = c;
+    }
+    memcpy(b->p + b->n, src, n);
+    b->n += n;
+}
+static void bput32(buf_t *b, u32 v) { bput(b, &v, 4); }
+static void bput64(buf_t *b, u64 v) { bput(b, &v, 8); }
+
+/* ---- u64 -> (a,b) open-addressing map, linear probing, backward-shift delete */
+typedef struct { u64 key, a, b; } ent_t;
+typedef struct { ent_t *e; u8 *used; size_t cap, n; } map_t;
+
+static size_t hslot(u64 k, size_t cap)
+{
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdull; k ^= k >> 33;
+    return (size_t)(k & (cap - 1));
+}
+static int map_grow(map_t *m)
+{
+    size_t nc = m->cap ? m->cap * 2 : 64;
+    ent_t *ne = (ent_t *)calloc(nc, sizeof(ent_t));
+    u8 *nu = (u8 *)calloc(nc, 1);
+    if (!ne || !nu) { free(ne); free(nu); return -1; }
+    for (size_t i = 0; i < m->cap; ++i) if (m->used[i]) {
+        size_t s = hslot(m->e[i].key, nc);
+        while (nu[s]) s = (s + 1) & (nc - 1);
+        nu[s] = 1; ne[s] = m->e[i];
+    }
+    free(m->e); free(m->used);
+    m->e = ne; m->used = nu; m->cap = nc;
+    return 0;
+}
+static ent_t *map_find(const map_t *m, u64 k)
+{
+    if (!m->cap) return NULL;
+    size_t s = hslot(k, m->cap);
+    while (m->used[s]) { if (m->e[s].key == k) return &m->e[s]; s = (s + 1) & (m->cap - 1); }
+    return NULL;
+}
+static ent_t *map_put(map_t *m, u64 k, u64 a, u64 b)
+{
+    if ((m->n + 1) * 2 > m->cap && map_grow(m)) return NULL;
+    size_t s = hslot(k, m->cap);
+    while (m->used[s]) {
+        if (m->e[s].key == k) { m->e[s].a = a; m->e[s].b = b; return &m->e[s]; }
+        s = (s + 1) & (m->cap - 1);
+    }
+    m->used[s] = 1; m->e[s].key = k; m->e[s].a = a; m->e[s].b = b; m->n++;
+    return &m->e[s];
+}
+static void map_del(map_t *m, u64 k)
+{
+    if (!m->cap) return;
+    size_t s = hslot(k, m->cap);
+    while (m->used[s] && m->e[s].key != k) s = (s + 1) & (m->cap - 1);
+    if (!m->used[s]) return;
+    m->used[s] = 0; m->n--;
+    size_t j = s;
+    for (;;) {
+        j = (j + 1) & (m->cap - 1);
+        if (!m->used[j]) break;
+        size_t h = hslot(m->e[j].key, m->cap);
+        /* can entry j move into hole s? (cyclic distance test) */
+        if (((j - h) & (m->cap - 1)) >= ((j - s) & (m->cap - 1))) {
+            m->e[s] = m->e[j]; m->used[s] = 1; m->used[j] = 0; s = j;
+        }
+    }
+}
+static void map_clear(map_t *m) { if (m->cap) memset(m->used, 0, m->cap); m->n = 0; }
+static void map_free(map_t *m) { free(m->e); free(m->used); memset(m, 0, sizeof *m); }
+
+static int cmp_ent(const void *x, const void *y)
+{
+    u64 a = ((const ent_t *)x)->key, b = ((const ent_t *)y)->key;
+    return a < b ? -1 : a > b;
+}
+/* entries of a map, sorted by key (std::map iteration order) */
+static ent_t *map_sorted(const map_t *m, size_t *n)
+{
+    ent_t *v = (ent_t *)malloc((m->n ? m->n : 1) * sizeof(ent_t));
+    size_t k = 0;
+    if (!v) { *n = 0; return NULL; }
+    for (size_t i = 0; i < m->cap; ++i) if (m->used[i]) v[k++] = m->e[i];
+    qsort(v, k, sizeof(ent_t), cmp_ent);
+    *n = k;
+    return v;
+}
+
+/* ---- Values ---------------------------------------------------------------
+ * A Value is (u32 proposer, u64 value_id, bool noop, membership | payload),
+ * encoded as in FillValue / ExtractValue (multi/paxos.cpp:556-644).  Its
+ * handle is proposer<<48 | noop<<47 | value_id (include/mpx.h); the canonical
+ * re-encoded bytes are interned per handle so PREPARE_REPLY can be rebuilt the
+ * way FillAcceptedValues does (multi/paxos.cpp:657-669). */
+typedef struct { u64 handle; size_t off; u32 len; u32 exec_off; u32 exec_len; } valrec_t;
+typedef struct { map_t idx; valrec_t *v; size_t n, cap; buf_t bytes; } vtab_t;
+
+enum { OK = 0, E_DECODE = -4, E_RANGE = -5, E_VALUE = -9, E_NOMEM = -2 };
+
+/* Parse one Value at p (avail bytes).  Returns bytes used (>0) or <0. */
+static long parse_value(vtab_t *t, const u8 *p, size_t avail, u64 *handle)
+{
+    if (avail < 13) return E_DECODE;
+    u32 proposer = rd32(p);
+    u64 value_id = rd64(p + 4);
+    int noop = p[12] != 0;
+    size_t used;
+    u8 canon[64];
+    buf_t enc = {0};
+    size_t exec_from = 0, exec_len = 0;       /* what Execute() would receive */
+    if (proposer >= (1u << 14) || value_id >= (1ull << 47)) return E_RANGE;
+    bput32(&enc, proposer); bput64(&enc, value_id);
+    u8 bnoop = (u8)noop; bput(&enc, &bnoop, 1);
+    if (noop) {
+        used = 13;
+    } else {
+        if (avail < 14) { free(enc.p); return E_DECODE; }
+        u8 member = p[13] != 0;
+        bput(&enc, &member, 1);
+        if (member) {
+            if (avail < 19) { free(enc.p); return E_DECODE; }
+            u32 id = rd32(p + 14);
+            u8 add = p[18] != 0;
+            bput32(&enc, id); bput(&enc, &add, 1);
+            if (add) {
+                if (avail < 23) { free(enc.p); return E_DECODE; }
+                u32 iplen = rd32(p + 19);
+                if (avail < 25 + (size_t)iplen) { free(enc.p); return E_DECODE; }
+                bput32(&enc, iplen); bput(&enc, p + 23, iplen);
+                u8 port[2]; memcpy(port, p + 23 + iplen, 2); bput(&enc, port, 2);
+                used = 25 + iplen;
+            } else {
+                used = 19;
+            }
+            /* multi executes value_.value_ for membership values: the empty
+             * string (the membership branch is #if 0, paxos.cpp:1592-1617) */
+        } else {
+            if (avail < 18) { free(enc.p); return E_DECODE; }
+            u32 len = rd32(p + 14);
+            if (avail < 18 + (size_t)len) { free(enc.p); return E_DECODE; }
+            bput32(&enc, len); exec_from = enc.n; exec_len = len;
+            bput(&enc, p + 18, len);
+            used = 18 + len;
+        }
+    }
+    (void)canon;
+    if (enc.oom) { free(enc.p); return E_NOMEM; }
+    u64 h = ((u64)proposer << 48) | ((u64)noop << 47) | value_id;
+    ent_t *e = map_find(&t->idx, h);
+    if (e) {
+        valrec_t *r = &t->v[e->a];
+        if (r->len != enc.n || memcmp(t->bytes.p + r->off, enc.p, enc.n)) { free(enc.p); return E_VALUE; }
+    } else {
+        if (t->n == t->cap) {
+            size_t c = t->cap ? t->cap * 2 : 64;
+            valrec_t *q = (valrec_t *)realloc(t->v, c * sizeof(valrec_t));
+            if (!q) { free(enc.p); return E_NOMEM; }
+            t->v = q; t->cap = c;
+        }
+        valrec_t *r = &t->v[t->n];
+        r->handle = h; r->off = t->bytes.n; r->len = (u32)enc.n;
+        r->exec_off = (u32)exec_from; r->exec_len = (u32)exec_len;
+        bput(&t->bytes, enc.p, enc.n);
+        if (!map_put(&t->idx, h, t->n, 0)) { free(enc.p); return E_NOMEM; }
+        t->n++;
+    }
+    free(enc.p);
+    *handle = h;
+    return (long)used;
+}
+static const valrec_t *vt_get(const vtab_t *t, u64 h)
+{
+    ent_t *e = map_find(&t->idx, h);
+    return e ? &t->v[e->a] : NULL;
+}
+
+/* ---- digests (shared definition with the engine) ----- */
+static u64 mix64(u64 x)
+{
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    x ^= x >> 31; return x;
+}
+
+/* ---- per-node state ------------------------------------------------------- */
+typedef struct {
+    u64 batch_id;
+    u64 mask;
+    int live;
+    size_t ent_off, ent_n;      /* entries (iid, handle) in node's batch pool  */
+} batch_t;
+
+typedef struct {
+    u32 index;
+    /* acceptor (multi/paxos.cpp:492-495) */
+    u64 promised, max_seen;
+    map_t acc;                  /* iid -> (ballot, handle): accepted_values_   */
+    map_t com;                  /* iid -> (ballot, handle): committed_values_  */
+    u64 next_apply;             /* next_id_to_apply_, paxos.cpp:501            */
+    /* proposer aggregation (paxos.cpp:470-486) */
+    u64 proposal_id;
+    int preparing;              /* prepare_retry_timeout_ != NULL              */
+    u64 promised_set;           /* prepare_promised_                          */
+    map_t pre;                  /* pre_accepted_values_                       */
+    batch_t *batches; size_t nb, cb;
+    map_t batch_idx;            /* accept_id -> index in batches              */
+    u64 *bent; size_t nbent, cbent;   /* batch entry pool (iid, handle) pairs  */
+    /* outputs */
+    buf_t sends, events_q, events_c, exec;
+    u64 n_sends, n_q, n_c, n_exec;
+    u64 P, A, L;
+    u64 violations;
+} node_t;
+
+typedef struct {
+    u32 N, sem;
+    u64 M;
+    vtab_t vt;
+    node_t *nodes;
+    u64 first_violation[4];     /* code, node, seq, iid */
+} ctx_t;
+
+static void violate(ctx_t *c, node_t *n, u64 code, u64 seq, u64 iid)
+{
+    n->violations++;
+    if (!c->first_violation[0]) {
+        c->first_violation[0] = code; c->first_violation[1] = n->index;
+        c->first_violation[2] = seq;  c->first_violation[3] = iid;
+    }
+}
+
+static void emit(node_t *n, u32 dst, const buf_t *m)
+{
+    bput32(&n->sends, dst);
+    bput32(&n->sends, (u32)m->n);
+    bput(&n->sends, m->p, m->n);
+    n->n_sends++;
+}
+
+static void encode_value(buf_t *b, const vtab_t *t, u64 h)
+{
+    const valrec_t *r = vt_get(t, h);
+    if (r) bput(b, t->bytes.p + r->off, r->len);
+}
+
+/* OnPrepare + FilterAcceptedValues, multi/paxos.cpp:858-922 */
+static int on_prepare(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 20) return E_DECODE;
+    u32 proposer = rd32(m + 4);
+    u64 id = rd64(m + 8);
+    u32 rlen = rd32(m + 16);
+    if (rlen % 16 || 20 + (size_t)rlen > len) return E_DECODE;
+    if (id > n->max_seen) n->max_seen = id;                     /* :862-863 */
+    if (proposer >= c->N) violate(c, n, 3, seq, 0);
+    if (id > n->promised) {                                      /* :865 */
+        n->promised = id;
+        size_t nr = rlen / 16;
+        /* ExtractAvailableInstanceIDs inserts ranges into a std::set; a
+         * repeated pair is an ASSERT (:536) */
+        for (size_t i = 0; i < nr; ++i)
+            for (size_t j = 0; j < i; ++j)
+                if (rd64(m + 20 + 16 * i) == rd64(m + 20 + 16 * j) &&
+                    rd64(m + 28 + 16 * i) == rd64(m + 28 + 16 * j)) violate(c, n, 4, seq, 0);
+        size_t na, nc;
+        ent_t *va = map_sorted(&n->acc, &na);
+        ent_t *vc = map_sorted(&n->com, &nc);
+        /* union of accepted and committed entries inside the ranges, iid
+         * sorted (FilterAcceptedInstances, :902-910).  Tag: accept ballot or
+         * commit ballot. */
+        size_t cap = na + nc + 1, k = 0;
+        ent_t *out = (ent_t *)malloc(cap * sizeof(ent_t));
+        if (!out || !va || !vc) { free(out); free(va); free(vc); return E_NOMEM; }
+        for (size_t r = 0; r < nr; ++r) {
+            u64 a = rd64(m + 20 + 16 * r), b = rd64(m + 28 + 16 * r);
+            for (size_t i = 0; i < na; ++i) if (va[i].key >= a && va[i].key < b) out[k++] = va[i];
+            for (size_t i = 0; i < nc; ++i) if (vc[i].key >= a && vc[i].key < b) out[k++] = vc[i];
+        }
+        qsort(out, k, sizeof(ent_t), cmp_ent);
+        for (size_t i = 1; i < k; ++i) if (out[i].key == out[i - 1].key) violate(c, n, 4, seq, out[i].key);
+        buf_t body = {0};
+        for (size_t i = 0; i < k; ++i) {
+            bput64(&body, out[i].key);
+            bput64(&body, out[i].a);
+            encode_value(&body, &c->vt, out[i].b);
+        }
+        buf_t r = {0};
+        bput32(&r, 1); bput32(&r, n->index); bput64(&r, id); bput32(&r, (u32)body.n);
+        bput(&r, body.p, body.n);
+        emit(n, proposer, &r);
+        n->P += k;
+        free(r.p); free(body.p); free(out); free(va); free(vc);
+    } else if (id < n->promised) {                               /* :894 */
+        buf_t r = {0};
+        bput32(&r, 2); bput64(&r, n->max_seen);
+        emit(n, proposer, &r);
+        free(r.p);
+    }                                                            /* ==: silent */
+    return OK;
+}
+
+/* OnAccept, multi/paxos.cpp:1359-1404 */
+static int on_accept(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 28) return E_DECODE;
+    u32 proposer = rd32(m + 4);
+    u64 accept = rd64(m + 8);
+    u64 id = rd64(m + 16);
+    u32 vlen = rd32(m + 24);
+    if (28 + (size_t)vlen > len) return E_DECODE;
+    if (id > n->max_seen) n->max_seen = id;                     /* :1363 */
+    if (proposer >= c->N) violate(c, n, 3, seq, 0);
+    if (id >= n->promised) {                                     /* :1366 */
+        size_t cur = 28, end = 28 + vlen;
+        map_t seen = {0};
+        while (cur < end) {
+            if (end - cur < 8) { map_free(&seen); return E_DECODE; }
+            u64 iid = rd64(m + cur); cur += 8;
+            u64 h;
+            long u = parse_value(&c->vt, m + cur, end - cur, &h);
+            if (u < 0) { map_free(&seen); return (int)u; }
+            cur += (size_t)u;
+            if (map_find(&seen, iid)) violate(c, n, 4, seq, iid);   /* :552 */
+            map_put(&seen, iid, 0, 0);
+            if (!map_find(&n->com, iid)) {                      /* :1380 */
+                map_put(&n->acc, iid, id, h);                   /* :1387 overwrite */
+                n->A++;
+            }
+        }
+        map_free(&seen);
+        buf_t r = {0};
+        bput32(&r, 4); bput32(&r, n->index); bput64(&r, id); bput64(&r, accept);
+        emit(n, proposer, &r);
+        free(r.p);
+    } else {
+        buf_t r = {0};
+        bput32(&r, 2); bput64(&r, n->max_seen);
+        emit(n, proposer, &r);
+        free(r.p);
+    }
+    return OK;
+}
+
+/* OnCommit, learner part: multi/paxos.cpp:1494-1518,1572-1622 */
+static int on_commit(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 28) return E_DECODE;
+    u32 committer = rd32(m + 4);
+    u64 commit = rd64(m + 8);
+    u64 id = rd64(m + 16);
+    u32 vlen = rd32(m + 24);
+    if (28 + (size_t)vlen > len) return E_DECODE;
+    if (committer >= c->N) violate(c, n, 3, seq, 0);
+    size_t cur = 28, end = 28 + vlen;
+    map_t seen = {0};
+    while (cur < end) {
+        if (end - cur < 8) { map_free(&seen); return E_DECODE; }
+        u64 iid = rd64(m + cur); cur += 8;
+        u64 h;
+        long u = parse_value(&c->vt, m + cur, end - cur, &h);
+        if (u < 0) { map_free(&seen); return (int)u; }
+        cur += (size_t)u;
+        if (map_find(&seen, iid)) violate(c, n, 4, seq, iid);
+        map_put(&seen, iid, 0, 0);
+        map_del(&n->acc, iid);                                  /* :1501-1502 */
+        ent_t *e = map_find(&n->com, iid);
+        if (e) {
+            if (e->b != h) violate(c, n, 1, seq, iid);          /* :1508-1509 */
+        } else {
+            map_put(&n->com, iid, id, h);                       /* :1515 first wins */
+        }
+        n->L++;
+    }
+    map_free(&seen);
+    buf_t r = {0};
+    bput32(&r, 6); bput32(&r, n->index); bput64(&r, commit);   /* :1577-1582 */
+    emit(n, committer, &r);
+    free(r.p);
+    /* in-order apply, skipping noops (:1584-1620) */
+    for (;;) {
+        ent_t *e = map_find(&n->com, n->next_apply);
+        if (!e) break;
+        n->next_apply++;
+        u64 h = e->b;
+        if ((h >> 47) & 1) continue;
+        const valrec_t *r2 = vt_get(&c->vt, h);
+        u32 el = r2 ? r2->exec_len : 0;
+        bput32(&n->exec, el);
+        if (el) bput(&n->exec, c->vt.bytes.p + r2->off + r2->exec_off, el);
+        n->n_exec++;
+    }
+    return OK;
+}
+
+/* OnPrepareReply + UpdateByPreAcceptedValues, multi/paxos.cpp:1036-1057,1201-1223 */
+static int on_prepare_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 20) return E_DECODE;
+    u32 acceptor = rd32(m + 4);
+    u64 id = rd64(m + 8);
+    u32 vlen = rd32(m + 16);
+    if (20 + (size_t)vlen > len) return E_DECODE;
+    if (!n->preparing || id != n->proposal_id) return OK;        /* :1038 */
+    if (acceptor >= c->N) { violate(c, n, 3, seq, 0); return OK; }  /* :1040 */
+    n->promised_set |= 1ull << acceptor;
+    size_t cur = 20, end = 20 + vlen;
+    map_t seen = {0};
+    while (cur < end) {
+        if (end - cur < 16) { map_free(&seen); return E_DECODE; }
+        u64 iid = rd64(m + cur), pid = rd64(m + cur + 8); cur += 16;
+        u64 h;
+        long u = parse_value(&c->vt, m + cur, end - cur, &h);
+        if (u < 0) { map_free(&seen); return (int)u; }
+        cur += (size_t)u;
+        if (map_find(&seen, iid)) violate(c, n, 4, seq, iid);   /* :677 */
+        map_put(&seen, iid, 0, 0);
+        ent_t *e = map_find(&n->pre, iid);
+        if (e) { if (pid > e->a) { e->a = pid; e->b = h; } }   /* strict >, :1218 */
+        else map_put(&n->pre, iid, pid, h);
+    }
+    map_free(&seen);
+    if ((u64)__builtin_popcountll(n->promised_set) >= c->N / 2 + 1) {   /* :1047 */
+        size_t k;
+        ent_t *v = map_sorted(&n->pre, &k);
+        bput64(&n->events_q, seq);
+        bput64(&n->events_q, n->proposal_id);
+        bput64(&n->events_q, k);
+        for (size_t i = 0; i < k; ++i) {
+            bput64(&n->events_q, v[i].key);
+            bput64(&n->events_q, v[i].a);
+            bput64(&n->events_q, v[i].b);
+        }
+        n->n_q++;
+        free(v);
+        for (size_t i = 0; i < n->nb; ++i)                      /* :1054 */
+            if (n->batches[i].live) { violate(c, n, 5, seq, 0); break; }
+        n->promised_set = 0;
+        n->preparing = 0;
+        map_clear(&n->pre);                                     /* :1105 */
+    }
+    return OK;
+}
+
+/* OnAcceptReply, multi/paxos.cpp:1406-1427 */
+static int on_accept_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 24) return E_DECODE;
+    u32 acceptor = rd32(m + 4);
+    u64 id = rd64(m + 8);
+    u64 accept = rd64(m + 16);
+    if (id != n->proposal_id) return OK;                        /* :1408 */
+    ent_t *e = map_find(&n->batch_idx, accept);
+    if (!e || !n->batches[e->a].live) return OK;                /* :1410 */
+    if (acceptor >= c->N) { violate(c, n, 3, seq, 0); return OK; }  /* :1414 */
+    batch_t *b = &n->batches[e->a];
+    b->mask |= 1ull << acceptor;
+    if ((u64)__builtin_popcountll(b->mask) >= c->N / 2 + 1) {   /* :1416 */
+        bput64(&n->events_c, seq);
+        bput64(&n->events_c, accept);
+        n->n_c++;
+        b->live = 0;                                            /* :1423-1425 */
+    }
+    return OK;
+}
+
+/* P_START marker: StartPrepare (paxos.cpp:1233-1248) after RestartPrepare or
+ * AcceptRejected (:1328-1343): new ballot, preparing, empty promise set and
+ * pre-accepted map, no outstanding accept batches. */
+static int on_p_start(node_t *n, const u8 *m, size_t len)
+{
+    if (len < 12) return E_DECODE;
+    n->proposal_id = rd64(m + 4);
+    n->preparing = 1;
+    n->promised_set = 0;
+    map_clear(&n->pre);
+    for (size_t i = 0; i < n->nb; ++i) n->batches[i].live = 0;
+    return OK;
+}
+
+/* P_BATCH marker: a new AcceptingValues (paxos.cpp:1299-1326) */
+static int on_p_batch(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 16) return E_DECODE;
+    u64 bid = rd64(m + 4);
+    u32 vlen = rd32(m + 12);
+    if (16 + (size_t)vlen > len) return E_DECODE;
+    if (n->nb == n->cb) {
+        size_t cc = n->cb ? n->cb * 2 : 16;
+        batch_t *q = (batch_t *)realloc(n->batches, cc * sizeof(batch_t));
+        if (!q) return E_NOMEM;
+        n->batches = q; n->cb = cc;
+    }
+    batch_t *b = &n->batches[n->nb];
+    b->batch_id = bid; b->mask = 0; b->live = 1;
+    b->ent_off = n->nbent; b->ent_n = 0;
+    size_t cur = 16, end = 16 + vlen;
+    while (cur < end) {
+        if (end - cur < 8) return E_DECODE;
+        u64 iid = rd64(m + cur); cur += 8;
+        u64 h;
+        long u = parse_value(&c->vt, m + cur, end - cur, &h);
+        if (u < 0) return (int)u;
+        cur += (size_t)u;
+        if (n->nbent + 2 > n->cbent) {
+            size_t cc = n->cbent ? n->cbent * 2 : 64;
+            u64 *q = (u64 *)realloc(n->bent, cc * sizeof(u64));
+            if (!q) return E_NOMEM;
+            n->bent = q; n->cbent = cc;
+        }
+        n->bent[n->nbent++] = iid;
+        n->bent[n->nbent++] = h;
+        b->ent_n++;
+    }
+    (void)seq;
+    map_put(&n->batch_idx, bid, n->nb, 0);
+    n->nb++;
+    return OK;
+}
+
+static int process(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 4) return E_DECODE;
+    switch (rd32(m)) {                                          /* GetMsgType, :736 */
+    case 0:  return on_prepare(c, n, m, len, seq);
+    case 1:  return on_prepare_reply(c, n, m, len, seq);
+    case 2:                                                     /* OnReject, :1225 */
+        if (len < 12) return E_DECODE;
+        if (n->max_seen < rd64(m + 4)) n->max_seen = rd64(m + 4);
+        return OK;
+    case 3:  return on_accept(c, n, m, len, seq);
+    case 4:  return on_accept_reply(c, n, m, len, seq);
+    case 5:  return on_commit(c, n, m, len, seq);
+    case 6:  return len < 16 ? E_DECODE : OK;                   /* OnCommitReply: out of scope */
+    case 16: return on_p_start(n, m, len);
+    case 17: return on_p_batch(c, n, m, len, seq);
+    default: return E_DECODE;                                   /* ASSERT(false), :1672 */
+    }
+}
+
+/* ---- container -------------------------------------------------------------*/
+#define HDR 40
+
+static int dump(ctx_t *c, u8 **out, u64 *size, u64 *stats)
+{
+    buf_t r = {0};
+    bput(&r, "MPXR", 4);
+    bput32(&r, 1); bput32(&r, c->N); bput32(&r, c->sem);
+    map_t chosen = {0};
+    u64 C = 0, P = 0, A = 0, L = 0, V = 0;
+    u64 dstate = 0, dscal = 0, dchosen = 0;
+    for (u32 i = 0; i < c->N; ++i) {
+        node_t *n = &c->nodes[i];
+        bput64(&r, n->promised); bput64(&r, n->max_seen);
+        dscal += mix64(mix64((u64)i * 0x9E3779B97F4A7C15ull ^ n->promised) ^ n->max_seen);
+        size_t na, nc;
+        ent_t *va = map_sorted(&n->acc, &na);
+        ent_t *vc = map_sorted(&n->com, &nc);
+        bput64(&r, (u64)(na + nc));
+        size_t ia = 0, ic = 0;
+        while (ia < na || ic < nc) {
+            int take_a = ic >= nc || (ia < na && va[ia].key < vc[ic].key);
+            ent_t *e = take_a ? &va[ia++] : &vc[ic++];
+            u64 kind = take_a ? 1 : 2;
+            bput64(&r, e->key); bput64(&r, kind); bput64(&r, e->a); bput64(&r, e->b);
+            dstate += mix64(mix64(mix64(e->key + (u64)i * 0x9E3779B97F4A7C15ull) ^ e->a)
+                            ^ (e->b + kind * 0xD6E8FEB86659FD93ull));
+        }
+        free(va); free(vc);
+        bput64(&r, n->n_sends); bput(&r, n->sends.p, n->sends.n);
+        bput64(&r, n->n_q); bput(&r, n->events_q.p, n->events_q.n);
+        bput64(&r, n->n_c); bput(&r, n->events_c.p, n->events_c.n);
+        bput64(&r, n->n_exec); bput(&r, n->exec.p, n->exec.n);
+        P += n->P; A += n->A; L += n->L; V += n->violations;
+    }
+    /* chosen log: union of the entries of every chosen batch, first wins;
+     * a second batch with another value for an instance breaks safety */
+    for (u32 i = 0; i < c->N; ++i) {
+        node_t *n = &c->nodes[i];
+        for (u64 k = 0; k < n->n_c; ++k) {
+            u64 bid = rd64(n->events_c.p + 16 * k + 8);
+            ent_t *e = map_find(&n->batch_idx, bid);
+            if (!e) continue;
+            batch_t *b = &n->batches[e->a];
+            for (size_t j = 0; j < b->ent_n; ++j) {
+                u64 iid = n->bent[b->ent_off + 2 * j], h = n->bent[b->ent_off + 2 * j + 1];
+                ent_t *x = map_find(&chosen, iid);
+                if (x) { if (x->a != h) { violate(c, n, 2, 0, iid); V++; } }
+                else { map_put(&chosen, iid, h, 0); C++; dchosen += mix64(mix64(iid) ^ h); }
+            }
+        }
+    }
+    size_t nch;
+    ent_t *vch = map_sorted(&chosen, &nch);
+    bput64(&r, (u64)nch);
+    for (size_t i = 0; i < nch; ++i) { bput64(&r, vch[i].key); bput64(&r, vch[i].a); }
+    free(vch);
+    map_free(&chosen);
+    if (stats) {
+        stats[0] = C; stats[1] = P; stats[2] = A; stats[3] = L; stats[4] = V;
+        stats[5] = dchosen; stats[6] = dstate; stats[7] = dscal;
+    }
+    if (r.oom) { free(r.p); return E_NOMEM; }
+    *out = r.p; *size = r.n;
+    return OK;
+}
+
+/*
+ * mpxo_run: process an MPXT trace, write the MPXR result.
+ *   stats (optional, 8 words): C, P, A, L, violations, chosen_digest,
+ *                              state_digest, scalar_digest
+ *   viol  (optional, 4 words): first violation code, node, seq, iid
+ * Returns 0 or a negative mpx status code.
+ */
+int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
+{
+    if (size < HDR || memcmp(trace, "MPXT", 4)) return E_DECODE;
+    ctx_t c;
+    memset(&c, 0, sizeof c);
+    c.N = rd32(trace + 8);
+    c.sem = rd32(trace + 12);
+    c.M = rd64(trace + 16);
+    u32 ne = rd32(trace + 24);
+    if (c.N == 0 || c.N > 64 || c.sem != 0) return -1;   /* member: oracle/mpx_oracle_member (later) */
+    size_t pos = HDR + (size_t)ne * 16;
+    c.nodes = (node_t *)calloc(c.N, sizeof(node_t));
+    if (!c.nodes) return E_NOMEM;
+    int rc = OK;
+    for (u32 i = 0; i < c.N && rc == OK; ++i) {
+        node_t *n = &c.nodes[i];
+        n->index = i;
+        if (pos + 16 > size) { rc = E_DECODE; break; }
+        u64 cnt = rd64(trace + pos), nbytes = rd64(trace + pos + 8);
+        pos += 16;
+        const u8 *offs = trace + pos;
+        if (pos + 8 * (cnt + 1) + nbytes > size) { rc = E_DECODE; break; }
+        const u8 *bytes = trace + pos + 8 * (cnt + 1);
+        for (u64 k = 0; k < cnt && rc == OK; ++k) {
+            u64 a = rd64(offs + 8 * k), b = rd64(offs + 8 * (k + 1));
+            if (b < a || b > nbytes) { rc = E_DECODE; break; }
+            rc = process(&c, n, bytes + a, (size_t)(b - a), k);
+        }
+        pos += 8 * (cnt + 1) + nbytes;
+        pos = (pos + 7) & ~(size_t)7;
+    }
+    if (rc == OK) rc = dump(&c, out, out_size, stats);
+    if (viol) memcpy(viol, c.first_violation, sizeof c.first_violation);
+    for (u32 i = 0; i < c.N; ++i) {
+        node_t *n = &c.nodes[i];
+        map_free(&n->acc); map_free(&n->com); map_free(&n->pre); map_free(&n->batch_idx);
+        free(n->batches); free(n->bent);
+        free(n->sends.p); free(n->events_q.p); free(n->events_c.p); free(n->exec.p);
+    }
+    free(c.nodes);
+    map_free(&c.vt.idx); free(c.vt.v); free(c.vt.bytes.p);
+    return rc;
+}
+
+void mpxo_free(void *p) { free(p); }

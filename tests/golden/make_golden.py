@@ -1,0 +1,57 @@
+"""Regenerate the golden fixtures under tests/golden/ (run in the build container).
+
+Each fixture is a trace (.mpxt: MPXT container of per-node receive streams)
+and the result the REFERENCE's own handlers produce for it (.mpxr: canonical
+MPXR dump), computed by oracle/_ref/libmpx_ref.so — multi/paxos.cpp compiled
+in place from /root/reference (oracle/Makefile, oracle/ref_multi_driver.cpp).
+The reference itself cannot travel; these vectors are what the oracle and the
+engine are pinned against (tests/test_oracle.py, tests/test_engine_gpu.py).
+
+    python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from fuzztrace import fuzz_trace  # noqa: E402
+from handmade import handmade_traces  # noqa: E402
+from oracles import ref_available, ref_run  # noqa: E402
+
+
+def main():
+    if not ref_available():
+        sys.exit("oracle/_ref/libmpx_ref.so missing: run `make -C oracle` where /root/reference exists")
+    cases = {}
+    for name, trace in handmade_traces().items():
+        cases[name] = trace
+    for seed in range(48):
+        cases["fuzz_%03d" % seed] = fuzz_trace(seed)
+    for seed in range(4):
+        cases["fuzz_big_%d" % seed] = fuzz_trace(10_000 + seed, n_nodes=5, n_inst=200, n_msgs=600)
+    extra = os.path.join(HERE, "extra_traces")
+    if os.path.isdir(extra):
+        for fn in sorted(os.listdir(extra)):
+            if fn.endswith(".mpxt"):
+                with open(os.path.join(extra, fn), "rb") as f:
+                    cases[fn[:-5]] = f.read()
+    index = {}
+    for name, trace in sorted(cases.items()):
+        result, stats = ref_run(trace)
+        with open(os.path.join(HERE, name + ".mpxt"), "wb") as f:
+            f.write(trace)
+        with open(os.path.join(HERE, name + ".mpxr"), "wb") as f:
+            f.write(result)
+        index[name] = {"C": stats[0], "P": stats[1], "A": stats[2], "L": stats[3],
+                       "trace_sha1": hashlib.sha1(trace).hexdigest(),
+                       "result_sha1": hashlib.sha1(result).hexdigest()}
+    with open(os.path.join(HERE, "index.json"), "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True)
+    print("wrote %d fixtures" % len(index))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,99 @@
+"""Wire encoder for hand-made traces (test helper).
+
+Encodes the reference's packed little-endian messages (SURVEY.md Appendix A;
+multi/paxos.cpp:741-755,830-856,1282-1297,1345-1357,1429-1444,1481-1492) and
+the Value codec (FillValue, multi/paxos.cpp:556-598), plus the engine-local
+proposer markers P_START / P_BATCH (include/mpx.h), and packs per-node
+receive streams into an MPXT trace container (DESIGN.md §Trace container).
+"""
+import struct
+
+U64_MAX_EXCL = (1 << 64) - 1   # AvailableInstanceIDs starts as [0, 2^64-1), multi/paxos.cpp:259
+
+
+def value(proposer, value_id, payload=None, noop=False):
+    """FillValue: u32 proposer, u64 value_id, bool noop, [bool member=0, u32 len, bytes]."""
+    b = struct.pack("<IQ?", proposer, value_id, noop)
+    if noop:
+        return b
+    if isinstance(payload, str):
+        payload = payload.encode()
+    return b + struct.pack("<?I", False, len(payload)) + payload
+
+
+def value_member(proposer, value_id, node_id, ip=None, port=0):
+    """Membership-change Value (multi codec keeps it even though proposing is #if 0)."""
+    b = struct.pack("<IQ??I", proposer, value_id, False, True, node_id)
+    if ip is None:
+        return b + struct.pack("<?", False)
+    ip = ip.encode()
+    return b + struct.pack("<?I", True, len(ip)) + ip + struct.pack("<H", port)
+
+
+def handle(proposer, value_id, noop=False):
+    return (proposer << 48) | (int(bool(noop)) << 47) | value_id
+
+
+def prepare(proposer, ballot, ranges=((0, U64_MAX_EXCL),)):
+    body = b"".join(struct.pack("<QQ", a, b) for a, b in ranges)
+    return struct.pack("<IIQI", 0, proposer, ballot, len(body)) + body
+
+
+def prepare_reply(acceptor, ballot, entries=()):
+    """entries: (iid, pid, value_bytes)"""
+    body = b"".join(struct.pack("<QQ", i, p) + v for i, p, v in entries)
+    return struct.pack("<IIQI", 1, acceptor, ballot, len(body)) + body
+
+
+def reject(max_id):
+    return struct.pack("<IQ", 2, max_id)
+
+
+def accept(proposer, accept_id, ballot, entries):
+    """entries: (iid, value_bytes)"""
+    body = b"".join(struct.pack("<Q", i) + v for i, v in entries)
+    return struct.pack("<IIQQI", 3, proposer, accept_id, ballot, len(body)) + body
+
+
+def accept_reply(acceptor, ballot, accept_id):
+    return struct.pack("<IIQQ", 4, acceptor, ballot, accept_id)
+
+
+def commit(committer, commit_id, ballot, entries):
+    body = b"".join(struct.pack("<Q", i) + v for i, v in entries)
+    return struct.pack("<IIQQI", 5, committer, commit_id, ballot, len(body)) + body
+
+
+def commit_reply(learner, commit_id):
+    return struct.pack("<IIQ", 6, learner, commit_id)
+
+
+def p_start(ballot):
+    return struct.pack("<IQ", 16, ballot)
+
+
+def p_batch(batch_id, entries):
+    body = b"".join(struct.pack("<Q", i) + v for i, v in entries)
+    return struct.pack("<IQI", 17, batch_id, len(body)) + body
+
+
+def container(streams, num_instances=0, semantics=0, epochs=()):
+    """streams: list (per node) of lists of message bytes, in processing order."""
+    out = bytearray(b"MPXT")
+    out += struct.pack("<III", 1, len(streams), semantics)
+    out += struct.pack("<QII", num_instances, len(epochs), 0)
+    out += struct.pack("<Q", 0)
+    assert len(out) == 40
+    for ver, mask in epochs:
+        out += struct.pack("<IIQ", ver, 0, mask)
+    for msgs in streams:
+        offs = [0]
+        for m in msgs:
+            offs.append(offs[-1] + len(m))
+        out += struct.pack("<QQ", len(msgs), offs[-1])
+        out += struct.pack("<%dQ" % len(offs), *offs)
+        for m in msgs:
+            out += m
+        while len(out) % 8:
+            out += b"\0"
+    return bytes(out)

@@ -1,0 +1,77 @@
+"""ctypes loaders for the parity checkers (TEST INFRASTRUCTURE).
+
+  oracle/_build/libmpx_oracle.so : C restatement (oracle/mpx_oracle.c)
+  oracle/_ref/libmpx_ref.so      : the reference's own handlers (oracle/ref_multi_driver.cpp)
+
+Both take an MPXT trace and return the canonical MPXR result bytes.
+"""
+import ctypes
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libmpx_oracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libmpx_ref.so")
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+def _load(path, fn):
+    lib = ctypes.CDLL(path)
+    f = getattr(lib, fn)
+    return lib, f
+
+
+class _Runner:
+    def __init__(self, path, fn, nstats, has_viol):
+        self.lib = ctypes.CDLL(path)
+        self.fn = getattr(self.lib, fn)
+        self.nstats = nstats
+        self.has_viol = has_viol
+        argt = [ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(_u8p),
+                ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        if has_viol:
+            argt.append(ctypes.POINTER(ctypes.c_uint64))
+        self.fn.argtypes = argt
+        self.fn.restype = ctypes.c_int
+        self.libc = ctypes.CDLL(None)
+        self.libc.free.argtypes = [ctypes.c_void_p]
+
+    def __call__(self, trace):
+        out = _u8p()
+        size = ctypes.c_uint64()
+        stats = (ctypes.c_uint64 * 8)()
+        args = [trace, len(trace), ctypes.byref(out), ctypes.byref(size), stats]
+        viol = (ctypes.c_uint64 * 4)()
+        if self.has_viol:
+            args.append(viol)
+        rc = self.fn(*args)
+        if rc != 0:
+            raise RuntimeError("%s failed: %d" % (self.fn.__name__, rc))
+        data = ctypes.string_at(out, size.value)
+        self.libc.free(out)
+        return data, list(stats)[: self.nstats], list(viol)
+
+
+_oracle = None
+_ref = None
+
+
+def oracle_run(trace):
+    """-> (mpxr bytes, [C,P,A,L,V,chosen_digest,state_digest,scalar_digest], violation[4])"""
+    global _oracle
+    if _oracle is None:
+        _oracle = _Runner(ORACLE_SO, "mpxo_run", 8, True)
+    return _oracle(trace)
+
+
+def ref_available():
+    return os.path.exists(REF_SO)
+
+
+def ref_run(trace):
+    """-> (mpxr bytes, [C,P,A,L])"""
+    global _ref
+    if _ref is None:
+        _ref = _Runner(REF_SO, "mpxref_run", 4, False)
+    data, stats, _ = _ref(trace)
+    return data, stats
