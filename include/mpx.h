@@ -182,6 +182,10 @@ int  mpx_reset_state(mpx_engine *eng);
  * synchronisation (kernels queued on the engine's stream). */
 int  mpx_step(mpx_engine *eng);
 int  mpx_sync(mpx_engine *eng);
+/* Device timings (HIP events on the engine's stream) of the runs/steps since
+ * the previous call: per run the acceptor/learner kernel (k_apply) and the
+ * whole run, in milliseconds.  Writes at most `max` pairs, *n = pairs written. */
+int  mpx_timings(mpx_engine *eng, uint32_t max, double *apply_ms, double *run_ms, uint32_t *n);
 
 /* ---- outbound ------------------------------------------------------------ */
 /* Replies generated by the acceptor/learner handlers of the last run, in the

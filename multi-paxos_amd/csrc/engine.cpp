@@ -1,0 +1,747 @@
+// engine.cpp — the C ABI (include/mpx.h) over the HIP kernels.
+//
+// Host responsibilities: decode + bucket submitted records (ingest.cpp), keep
+// the trace resident in HBM, queue a run (kernels.hip) on the engine's stream,
+// and turn device results back into the reference's vocabulary (sends,
+// canonical MPXR dump).  There is no CPU execution path: without a GPU every
+// compute entry point returns MPX_E_NODEVICE.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gen.hpp"
+#include "ingest.hpp"
+#include "mpx.h"
+#include "mpx_internal.hpp"
+
+using namespace mpx;
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    int alloc(size_t n)
+    {
+        if (n <= bytes && p) return MPX_OK;
+        if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
+        if (!n) return MPX_OK;
+        if (hipMalloc(&p, n) != hipSuccess) { p = nullptr; return MPX_E_NOMEM; }
+        bytes = n;
+        return MPX_OK;
+    }
+    template <typename T> T *as() const { return (T *)p; }
+};
+
+template <typename T> int upload(DevBuf &b, const std::vector<T> &v, hipStream_t s)
+{
+    int rc = b.alloc(std::max<size_t>(v.size() * sizeof(T), 8));
+    if (rc) return rc;
+    if (!v.empty() && hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s) != hipSuccess)
+        return MPX_E_HIP;
+    return MPX_OK;
+}
+
+struct StepEvents { hipEvent_t e[4]; };
+
+}  // namespace
+
+struct mpx_engine {
+    mpx_config cfg{};
+    std::vector<mpx_epoch> epochs;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t num_cus = 256;
+    ValueTable vt;
+    std::vector<NodeStream> nodes;
+    IngestViolation iv;
+    HostTrace ht;
+    bool dirty = true;
+    bool device_trace = false;       // trace materialised by a device generator
+    uint64_t shard_len = 0;
+    uint32_t NB = 0;
+    // device buffers
+    DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, m_flags, m_maxseen;
+    DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
+    DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
+    DevBuf f_off, frags, ev_off, ev_msg, pl_off, pl_msg;
+    DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
+    DevBuf st, st_valid, chosen, chosen_valid;
+    DevBuf out, out_cursor, partials, viol, summary;
+    uint64_t out_cap = 0;
+    DevView view{};
+    LaunchGeom geom{};
+    uint64_t num_msgs = 0;
+    // results of the last synchronised run
+    std::vector<uint64_t> last_summary;
+    mpx_stats stats{};
+    // timing
+    std::vector<StepEvents> ev_pool;
+    size_t ev_used = 0;
+    // comm
+    ncclComm_t comm = nullptr;
+    int rank = 0, nranks = 1;
+    DevBuf gather_buf;
+};
+
+static int hip_ok(hipError_t e) { return e == hipSuccess ? MPX_OK : MPX_E_HIP; }
+#define TRY(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
+#define HTRY(x) do { if ((x) != hipSuccess) return MPX_E_HIP; } while (0)
+
+static uint64_t now_ns()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+        std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+extern "C" int mpx_version(void) { return (int)MPX_ABI_VERSION; }
+
+extern "C" int mpx_device_count(int *count)
+{
+    if (!count) return MPX_E_INVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return MPX_OK;
+}
+
+extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
+{
+    if (!cfg || !out) return MPX_E_INVAL;
+    if (cfg->abi_version != MPX_ABI_VERSION) return MPX_E_INVAL;
+    if (!cfg->num_nodes || cfg->num_nodes > MPX_MAX_NODES) return MPX_E_INVAL;
+    if (cfg->shard_end <= cfg->shard_begin) return MPX_E_INVAL;
+    if (cfg->semantics != MPX_SEM_MULTI) return MPX_E_INVAL;    // member semantics: DESIGN.md §Next
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPX_E_NODEVICE;
+    if (cfg->device < 0 || cfg->device >= n) return MPX_E_NODEVICE;
+    std::unique_ptr<mpx_engine> e(new mpx_engine);
+    e->cfg = *cfg;
+    if (cfg->epochs && cfg->num_epochs) e->epochs.assign(cfg->epochs, cfg->epochs + cfg->num_epochs);
+    e->cfg.epochs = nullptr;
+    e->device = cfg->device;
+    HTRY(hipSetDevice(e->device));
+    HTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, e->device) == hipSuccess && prop.multiProcessorCount > 0)
+        e->num_cus = (uint32_t)prop.multiProcessorCount;
+    e->nodes.resize(cfg->num_nodes);
+    e->shard_len = cfg->shard_end - cfg->shard_begin;
+    e->NB = (uint32_t)((e->shard_len + BS - 1) >> BSH);
+    if ((uint64_t)e->NB * cfg->num_nodes > (1ull << 40)) return MPX_E_RANGE;
+    *out = e.release();
+    return MPX_OK;
+}
+
+extern "C" int mpx_destroy(mpx_engine *e)
+{
+    if (!e) return MPX_E_INVAL;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (auto &s : e->ev_pool) for (auto ev : s.e) (void)hipEventDestroy(ev);
+    if (e->comm) ncclCommDestroy(e->comm);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return MPX_OK;
+}
+
+extern "C" int mpx_submit(mpx_engine *e, uint32_t node, const uint8_t *bytes, const uint64_t *offsets, uint64_t count)
+{
+    if (!e || node >= e->cfg.num_nodes || (count && (!bytes || !offsets))) return MPX_E_INVAL;
+    if (e->device_trace) return MPX_E_STATE;
+    const uint64_t t0 = now_ns();
+    NodeStream &ns = e->nodes[node];
+    for (uint64_t i = 0; i < count; ++i) {
+        if (offsets[i + 1] < offsets[i]) return MPX_E_INVAL;
+        int rc = decode_record(e->vt, ns, node, e->cfg.num_nodes, bytes + offsets[i], (size_t)(offsets[i + 1] - offsets[i]),
+                               e->cfg.shard_begin, e->cfg.shard_end, e->iv);
+        if (rc) return rc;
+    }
+    e->dirty = true;
+    e->stats.ingest_ns += now_ns() - t0;
+    return MPX_OK;
+}
+
+static inline uint32_t rd32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
+static inline uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
+
+extern "C" int mpx_submit_trace(mpx_engine *e, const uint8_t *t, uint64_t size)
+{
+    if (!e || !t || size < 40 || std::memcmp(t, "MPXT", 4)) return MPX_E_INVAL;
+    const uint32_t N = rd32(t + 8), ne = rd32(t + 24);
+    if (N != e->cfg.num_nodes) return MPX_E_INVAL;
+    size_t pos = 40 + (size_t)ne * 16;
+    for (uint32_t n = 0; n < N; ++n) {
+        if (pos + 16 > size) return MPX_E_DECODE;
+        const uint64_t cnt = rd64(t + pos), nb = rd64(t + pos + 8);
+        pos += 16;
+        if (pos + 8 * (cnt + 1) + nb > size) return MPX_E_DECODE;
+        std::vector<uint64_t> offs(cnt + 1);
+        std::memcpy(offs.data(), t + pos, 8 * (cnt + 1));
+        TRY(mpx_submit(e, n, t + pos + 8 * (cnt + 1), offs.data(), cnt));
+        pos += 8 * (cnt + 1) + nb;
+        pos = (pos + 7) & ~(size_t)7;
+    }
+    return MPX_OK;
+}
+
+// allocate state / output buffers and fill the kernel view
+static int finish_view(mpx_engine *e)
+{
+    const uint32_t N = e->cfg.num_nodes;
+    DevView &v = e->view;
+    v.N = N;
+    v.quorum = N / 2 + 1;                          // nodes_.size() / 2 + 1, paxos.cpp:1047,1416
+    v.NB = e->NB;
+    v.semantics = e->cfg.semantics;
+    v.shard_begin = e->cfg.shard_begin;
+    v.shard_len = e->shard_len;
+    v.num_msgs = e->num_msgs;
+    TRY(e->st.alloc((size_t)N * e->shard_len * 16));
+    TRY(e->st_valid.alloc((size_t)N * e->NB));
+    TRY(e->chosen.alloc(e->shard_len * 8));
+    TRY(e->chosen_valid.alloc(e->NB));
+    const uint64_t npairs = (uint64_t)N * e->NB;
+    e->geom.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npairs, (uint64_t)e->num_cus * 8));
+    e->geom.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 4));
+    TRY(e->partials.alloc(8ull * 8 * (e->geom.apply_wgs + e->geom.chosen_wgs)));
+    TRY(e->viol.alloc(sizeof(DevViolation)));
+    TRY(e->summary.alloc(64 * 8));
+    TRY(e->out_cursor.alloc(8));
+    if (!e->out_cap) e->out_cap = 1 << 16;
+    TRY(e->out.alloc(e->out_cap * sizeof(OutRec)));
+    TRY(e->node_scal.alloc(16ull * N));
+    v.st = e->st.as<uint64_t>();
+    v.st_valid = e->st_valid.as<uint8_t>();
+    v.chosen = e->chosen.as<uint64_t>();
+    v.chosen_valid = e->chosen_valid.as<uint8_t>();
+    v.out = e->out.as<OutRec>();
+    v.out_cursor = e->out_cursor.as<unsigned long long>();
+    v.out_cap = e->out_cap;
+    v.partials = e->partials.as<unsigned long long>();
+    v.viol = e->viol.as<DevViolation>();
+    v.summary = e->summary.as<unsigned long long>();
+    v.node_scal = e->node_scal.as<uint64_t>();
+    return MPX_OK;
+}
+
+static int upload_trace(mpx_engine *e)
+{
+    const uint64_t t0 = now_ns();
+    TRY(build_trace(e->nodes, e->cfg.shard_begin, e->shard_len, e->ht));
+    HostTrace &h = e->ht;
+    hipStream_t s = e->stream;
+    TRY(upload(e->m_type, h.m_type, s)); TRY(upload(e->m_src, h.m_src, s));
+    TRY(upload(e->m_ballot, h.m_ballot, s)); TRY(upload(e->m_aux, h.m_aux, s));
+    TRY(upload(e->m_ent, h.m_ent, s)); TRY(upload(e->m_cnt, h.m_cnt, s));
+    TRY(upload(e->m_node, h.m_node, s)); TRY(upload(e->node_off, h.node_off, s));
+    TRY(e->m_flags.alloc(std::max<size_t>(h.m_type.size(), 8)));
+    TRY(e->m_maxseen.alloc(std::max<size_t>(h.m_type.size() * 8, 8)));
+    TRY(upload(e->chunk_node, h.chunk_node, s)); TRY(upload(e->chunk_beg, h.chunk_beg, s));
+    TRY(upload(e->chunk_end, h.chunk_end, s)); TRY(upload(e->node_chunk_off, h.node_chunk_off, s));
+    TRY(e->chunk_agg.alloc(std::max<size_t>(16 * h.chunk_node.size(), 16)));
+    TRY(e->chunk_carry.alloc(std::max<size_t>(16 * h.chunk_node.size(), 16)));
+    TRY(upload(e->e_val, h.e_val, s)); TRY(upload(e->e_slot, h.e_slot, s));
+    TRY(upload(e->r_pid, h.r_pid, s)); TRY(upload(e->r_val, h.r_val, s)); TRY(upload(e->r_slot, h.r_slot, s));
+    TRY(upload(e->g_a, h.g_a, s)); TRY(upload(e->g_b, h.g_b, s));
+    TRY(upload(e->f_off, h.f_off, s)); TRY(upload(e->frags, h.frags, s));
+    TRY(upload(e->ev_off, h.ev_off, s)); TRY(upload(e->ev_msg, h.ev_msg, s));
+    TRY(upload(e->pl_off, h.pl_off, s)); TRY(upload(e->pl_msg, h.pl_msg, s));
+    TRY(upload(e->b_msg, h.b_msg, s)); TRY(upload(e->b_pstart, h.b_pstart, s));
+    TRY(upload(e->b_rep_off, h.b_rep_off, s)); TRY(upload(e->b_rep, h.b_rep, s));
+    TRY(e->b_chosen.alloc(std::max<size_t>(4 * h.b_msg.size(), 4)));
+    TRY(upload(e->cf_off, h.cf_off, s)); TRY(upload(e->cfrags, h.cfrags, s));
+    e->num_msgs = h.m_type.size();
+    DevView &v = e->view;
+    v.m_type = e->m_type.as<uint8_t>(); v.m_src = e->m_src.as<uint32_t>();
+    v.m_ballot = e->m_ballot.as<uint64_t>(); v.m_aux = e->m_aux.as<uint64_t>();
+    v.m_ent = e->m_ent.as<uint64_t>(); v.m_cnt = e->m_cnt.as<uint32_t>();
+    v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
+    v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
+    v.num_chunks = (uint32_t)h.chunk_node.size();
+    v.chunk_node = e->chunk_node.as<uint32_t>(); v.chunk_beg = e->chunk_beg.as<uint64_t>();
+    v.chunk_end = e->chunk_end.as<uint64_t>(); v.node_chunk_off = e->node_chunk_off.as<uint32_t>();
+    v.chunk_agg = e->chunk_agg.as<uint64_t>(); v.chunk_carry = e->chunk_carry.as<uint64_t>();
+    v.e_val = e->e_val.as<uint64_t>(); v.e_slot = e->e_slot.as<uint8_t>();
+    v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
+    v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
+    v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
+    v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>();
+    v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
+    v.num_batches = (uint32_t)h.b_msg.size();
+    v.b_msg = e->b_msg.as<uint32_t>(); v.b_pstart = e->b_pstart.as<uint32_t>();
+    v.b_rep_off = e->b_rep_off.as<uint64_t>(); v.b_rep = e->b_rep.as<uint32_t>();
+    v.b_chosen = e->b_chosen.as<uint32_t>();
+    v.cf_off = e->cf_off.as<uint64_t>(); v.cfrags = e->cfrags.as<Frag>();
+    TRY(finish_view(e));
+    HTRY(hipStreamSynchronize(s));
+    e->dirty = false;
+    e->stats.ingest_ns += now_ns() - t0;
+    return MPX_OK;
+}
+
+static StepEvents *next_events(mpx_engine *e)
+{
+    if (e->ev_used == e->ev_pool.size()) {
+        StepEvents se;
+        for (auto &x : se.e)
+            if (hipEventCreate(&x) != hipSuccess) return nullptr;
+        e->ev_pool.push_back(se);
+    }
+    return &e->ev_pool[e->ev_used++];
+}
+
+static int queue_run(mpx_engine *e)
+{
+    HTRY(hipSetDevice(e->device));
+    if (e->dirty && !e->device_trace) TRY(upload_trace(e));
+    StepEvents *ev = next_events(e);
+    if (!ev) return MPX_E_HIP;
+    int rc = launch_run(e->view, e->stream, e->geom, ev->e[0], ev->e[1], ev->e[2], ev->e[3]);
+    return rc ? MPX_E_HIP : MPX_OK;
+}
+
+static int collect(mpx_engine *e)
+{
+    HTRY(hipStreamSynchronize(e->stream));
+    e->last_summary.assign(64, 0);
+    HTRY(hipMemcpy(e->last_summary.data(), e->summary.p, 64 * 8, hipMemcpyDeviceToHost));
+    uint64_t cursor = 0;
+    HTRY(hipMemcpy(&cursor, e->out_cursor.p, 8, hipMemcpyDeviceToHost));
+    if (cursor > e->out_cap) {
+        // snapshot output overflowed: grow and run again (runs are deterministic)
+        e->out_cap = cursor + cursor / 4;
+        TRY(e->out.alloc(e->out_cap * sizeof(OutRec)));
+        e->view.out = e->out.as<OutRec>();
+        e->view.out_cap = e->out_cap;
+        TRY(queue_run(e));
+        return collect(e);
+    }
+    const auto &s = e->last_summary;
+    mpx_stats &st = e->stats;
+    st.chosen = s[SW_C]; st.promise_entries = s[SW_P]; st.accept_apps = s[SW_A]; st.commit_apps = s[SW_L];
+    st.messages = s[SW_MSGS]; st.violations = s[SW_V] + e->iv.count;
+    st.chosen_digest = s[SW_DCHOSEN]; st.state_digest = s[SW_DSTATE]; st.scalar_digest = s[SW_DSCAL];
+    st.bytes_alg = 16 * st.promise_entries + 24 * st.accept_apps + 16 * st.commit_apps;
+    if (e->ev_used) {
+        StepEvents &x = e->ev_pool[e->ev_used - 1];
+        float a = 0, r = 0;
+        (void)hipEventElapsedTime(&a, x.e[1], x.e[2]);
+        (void)hipEventElapsedTime(&r, x.e[0], x.e[3]);
+        st.apply_ns = (uint64_t)(a * 1e6);
+        st.device_ns = (uint64_t)(r * 1e6);
+    }
+    return MPX_OK;
+}
+
+extern "C" int mpx_run(mpx_engine *e)
+{
+    if (!e) return MPX_E_INVAL;
+    TRY(queue_run(e));
+    return collect(e);
+}
+
+extern "C" int mpx_step(mpx_engine *e)
+{
+    if (!e) return MPX_E_INVAL;
+    return queue_run(e);
+}
+
+extern "C" int mpx_sync(mpx_engine *e)
+{
+    if (!e) return MPX_E_INVAL;
+    return collect(e);
+}
+
+extern "C" int mpx_reset_state(mpx_engine *e)
+{
+    if (!e) return MPX_E_INVAL;
+    HTRY(hipSetDevice(e->device));
+    if (e->st_valid.p) HTRY(hipMemsetAsync(e->st_valid.p, 0, e->st_valid.bytes, e->stream));
+    if (e->chosen_valid.p) HTRY(hipMemsetAsync(e->chosen_valid.p, 0, e->chosen_valid.bytes, e->stream));
+    if (e->node_scal.p) HTRY(hipMemsetAsync(e->node_scal.p, 0, e->node_scal.bytes, e->stream));
+    HTRY(hipStreamSynchronize(e->stream));
+    e->last_summary.clear();
+    return MPX_OK;
+}
+
+extern "C" int mpx_timings(mpx_engine *e, uint32_t max, double *apply_ms, double *run_ms, uint32_t *n)
+{
+    if (!e || !n) return MPX_E_INVAL;
+    HTRY(hipStreamSynchronize(e->stream));
+    uint32_t k = 0;
+    for (size_t i = 0; i < e->ev_used && k < max; ++i, ++k) {
+        float a = 0, r = 0;
+        (void)hipEventElapsedTime(&a, e->ev_pool[i].e[1], e->ev_pool[i].e[2]);
+        (void)hipEventElapsedTime(&r, e->ev_pool[i].e[0], e->ev_pool[i].e[3]);
+        if (apply_ms) apply_ms[k] = a;
+        if (run_ms) run_ms[k] = r;
+    }
+    *n = k;
+    e->ev_used = 0;
+    return MPX_OK;
+}
+
+// ---------------------------------------------------------------- readback --
+template <typename T> static int d2h(std::vector<T> &v, const DevBuf &b, size_t n, size_t off = 0)
+{
+    v.resize(n);
+    if (!n) return MPX_OK;
+    return hip_ok(hipMemcpy(v.data(), (const char *)b.p + off * sizeof(T), n * sizeof(T), hipMemcpyDeviceToHost));
+}
+
+static bool have_results(const mpx_engine *e) { return !e->last_summary.empty(); }
+
+extern "C" int mpx_read_chosen(mpx_engine *e, uint64_t first, uint64_t count, uint64_t *out)
+{
+    if (!e || (count && !out)) return MPX_E_INVAL;
+    if (first < e->cfg.shard_begin || first + count > e->cfg.shard_end) return MPX_E_RANGE;
+    if (!count) return MPX_OK;
+    if (!have_results(e)) { std::memset(out, 0, count * 8); return MPX_OK; }
+    HTRY(hipSetDevice(e->device));
+    const uint64_t l0 = first - e->cfg.shard_begin;
+    const uint64_t b0 = l0 >> BSH, b1 = (l0 + count - 1) >> BSH;
+    std::vector<uint8_t> valid;
+    TRY(d2h(valid, e->chosen_valid, b1 - b0 + 1, b0));
+    HTRY(hipMemcpy(out, (const char *)e->chosen.p + l0 * 8, count * 8, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < count; ++i)
+        if (!valid[((l0 + i) >> BSH) - b0]) out[i] = 0;
+    return MPX_OK;
+}
+
+extern "C" int mpx_read_node_scalars(mpx_engine *e, uint32_t node, uint64_t *promised, uint64_t *max_seen)
+{
+    if (!e || node >= e->cfg.num_nodes) return MPX_E_INVAL;
+    uint64_t v[2] = {0, 0};
+    if (have_results(e)) {
+        HTRY(hipSetDevice(e->device));
+        HTRY(hipMemcpy(v, (const char *)e->node_scal.p + 16ull * node, 16, hipMemcpyDeviceToHost));
+    }
+    if (promised) *promised = v[0];
+    if (max_seen) *max_seen = v[1];
+    return MPX_OK;
+}
+
+extern "C" int mpx_read_node_state(mpx_engine *e, uint32_t node, uint64_t first, uint64_t count,
+                                   uint64_t *acc_ballot, uint64_t *acc_value, uint64_t *com_ballot, uint64_t *com_value)
+{
+    if (!e || node >= e->cfg.num_nodes) return MPX_E_INVAL;
+    if (first < e->cfg.shard_begin || first + count > e->cfg.shard_end) return MPX_E_RANGE;
+    if (!count) return MPX_OK;
+    std::vector<uint64_t> st(2 * count, 0);
+    std::vector<uint8_t> valid;
+    const uint64_t l0 = first - e->cfg.shard_begin;
+    const uint64_t b0 = l0 >> BSH, b1 = (l0 + count - 1) >> BSH;
+    if (have_results(e)) {
+        HTRY(hipSetDevice(e->device));
+        TRY(d2h(valid, e->st_valid, b1 - b0 + 1, (size_t)node * e->NB + b0));
+        HTRY(hipMemcpy(st.data(), (const char *)e->st.p + 16 * ((uint64_t)node * e->shard_len + l0), 16 * count,
+                       hipMemcpyDeviceToHost));
+    } else {
+        valid.assign(b1 - b0 + 1, 0);
+    }
+    for (uint64_t i = 0; i < count; ++i) {
+        uint64_t b = st[2 * i], w = st[2 * i + 1];
+        if (!valid[((l0 + i) >> BSH) - b0]) b = w = 0;
+        const bool com = (w & W_PRESENT) && (w & W_COMMITTED);
+        const bool acc = (w & W_PRESENT) && !(w & W_COMMITTED);
+        if (acc_ballot) acc_ballot[i] = acc ? b : 0;
+        if (acc_value) acc_value[i] = acc ? (MPX_PRESENT | (w & W_HANDLE)) : 0;
+        if (com_ballot) com_ballot[i] = com ? b : 0;
+        if (com_value) com_value[i] = com ? (MPX_PRESENT | (w & W_HANDLE)) : 0;
+    }
+    return MPX_OK;
+}
+
+extern "C" int mpx_stats_get(mpx_engine *e, mpx_stats *out)
+{
+    if (!e || !out) return MPX_E_INVAL;
+    *out = e->stats;
+    return MPX_OK;
+}
+
+extern "C" int mpx_last_violation(mpx_engine *e, mpx_violation *out)
+{
+    if (!e || !out) return MPX_E_INVAL;
+    std::memset(out, 0, sizeof *out);
+    if (e->iv.code) {
+        out->code = e->iv.code; out->node = (uint32_t)e->iv.node; out->seq = e->iv.seq; out->iid = e->iv.iid;
+        return MPX_OK;
+    }
+    if (e->viol.p && have_results(e)) {
+        DevViolation d;
+        HTRY(hipMemcpy(&d, e->viol.p, sizeof d, hipMemcpyDeviceToHost));
+        out->code = d.code; out->node = (uint32_t)d.node; out->seq = d.seq; out->iid = d.iid;
+    }
+    return MPX_OK;
+}
+
+extern "C" int mpx_value_bytes(mpx_engine *e, uint64_t handle, uint8_t *buf, uint32_t cap, uint32_t *len)
+{
+    if (!e || !len) return MPX_E_INVAL;
+    std::string s;
+    if (!e->vt.encode(handle & ~MPX_PRESENT, s)) return MPX_E_RANGE;
+    *len = (uint32_t)s.size();
+    if (buf && cap) std::memcpy(buf, s.data(), std::min<size_t>(cap, s.size()));
+    return MPX_OK;
+}
+
+extern "C" void mpx_free(void *p) { std::free(p); }
+
+// ------------------------------------------------- sends / canonical dump --
+template <typename T> static inline void app(std::string &s, T v) { s.append((const char *)&v, sizeof v); }
+
+struct Results {
+    std::vector<uint8_t> flags;
+    std::vector<uint64_t> maxseen, scal;
+    std::vector<OutRec> out;
+    std::vector<uint32_t> b_chosen;
+    std::map<uint32_t, std::vector<const OutRec *>> by_msg[2];
+};
+
+static int fetch_results(mpx_engine *e, Results &r)
+{
+    if (!have_results(e)) return MPX_E_STATE;
+    if (e->device_trace) return MPX_E_STATE;      // synthetic device traces have no host headers
+    HTRY(hipSetDevice(e->device));
+    const size_t G = e->ht.m_type.size();
+    TRY(d2h(r.flags, e->m_flags, G));
+    TRY(d2h(r.maxseen, e->m_maxseen, G));
+    TRY(d2h(r.scal, e->node_scal, 2ull * e->cfg.num_nodes));
+    uint64_t cursor = 0;
+    HTRY(hipMemcpy(&cursor, e->out_cursor.p, 8, hipMemcpyDeviceToHost));
+    TRY(d2h(r.out, e->out, std::min<uint64_t>(cursor, e->out_cap)));
+    TRY(d2h(r.b_chosen, e->b_chosen, e->ht.b_msg.size()));
+    for (auto &o : r.out) r.by_msg[o.kind & 1][o.msg].push_back(&o);
+    for (int k = 0; k < 2; ++k)
+        for (auto &x : r.by_msg[k])
+            std::sort(x.second.begin(), x.second.end(), [](const OutRec *a, const OutRec *b) { return a->iid < b->iid; });
+    return MPX_OK;
+}
+
+// the replies the reference's acceptor / learner handlers send for message g
+// of node n, in generation order (paxos.cpp:888-899,1391-1403,1577-1582)
+static void reply_of(const mpx_engine *e, const Results &r, uint32_t n, uint64_t g, uint32_t &dst, std::string &m)
+{
+    const HostTrace &h = e->ht;
+    const uint8_t t = h.m_type[g], f = r.flags[g];
+    m.clear();
+    dst = h.m_src[g];
+    if (t == MPX_MSG_PREPARE) {
+        if (f & F_GRANTED) {
+            std::string body;
+            auto it = r.by_msg[0].find((uint32_t)g);
+            if (it != r.by_msg[0].end())
+                for (const OutRec *o : it->second) {
+                    app<uint64_t>(body, o->iid);
+                    app<uint64_t>(body, o->ballot);
+                    e->vt.encode(o->handle, body);
+                }
+            app<uint32_t>(m, MPX_MSG_PREPARE_REPLY); app<uint32_t>(m, n); app<uint64_t>(m, h.m_ballot[g]);
+            app<uint32_t>(m, (uint32_t)body.size());
+            m += body;
+        } else if (f & F_REJECT) {
+            app<uint32_t>(m, MPX_MSG_REJECT); app<uint64_t>(m, r.maxseen[g]);
+        }
+    } else if (t == MPX_MSG_ACCEPT) {
+        if (f & F_GRANTED) {
+            app<uint32_t>(m, MPX_MSG_ACCEPT_REPLY); app<uint32_t>(m, n);
+            app<uint64_t>(m, h.m_ballot[g]); app<uint64_t>(m, h.m_aux[g]);
+        } else {
+            app<uint32_t>(m, MPX_MSG_REJECT); app<uint64_t>(m, r.maxseen[g]);
+        }
+    } else if (t == MPX_MSG_COMMIT) {
+        app<uint32_t>(m, MPX_MSG_COMMIT_REPLY); app<uint32_t>(m, n); app<uint64_t>(m, h.m_aux[g]);
+    }
+}
+
+extern "C" int mpx_drain_sends(mpx_engine *e, mpx_send_fn fn, void *user)
+{
+    if (!e || !fn) return MPX_E_INVAL;
+    Results r;
+    TRY(fetch_results(e, r));
+    std::string m;
+    for (uint32_t n = 0; n < e->cfg.num_nodes; ++n)
+        for (uint64_t g = e->ht.node_off[n]; g < e->ht.node_off[n + 1]; ++g) {
+            uint32_t dst;
+            reply_of(e, r, n, g, dst, m);
+            if (!m.empty()) fn(user, n, dst, (const uint8_t *)m.data(), (uint32_t)m.size());
+        }
+    return MPX_OK;
+}
+
+extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    Results r;
+    TRY(fetch_results(e, r));
+    const uint32_t N = e->cfg.num_nodes;
+    const HostTrace &h = e->ht;
+    std::string d;
+    d.append("MPXR", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, N); app<uint32_t>(d, e->cfg.semantics);
+    std::vector<uint64_t> st;
+    std::vector<uint8_t> valid;
+    TRY(d2h(valid, e->st_valid, (size_t)N * e->NB));
+    std::vector<uint64_t> chosen;
+    std::vector<uint8_t> cvalid;
+    TRY(d2h(chosen, e->chosen, e->shard_len));
+    TRY(d2h(cvalid, e->chosen_valid, e->NB));
+    std::string m;
+    for (uint32_t n = 0; n < N; ++n) {
+        app<uint64_t>(d, r.scal[2 * n]);
+        app<uint64_t>(d, r.scal[2 * n + 1]);
+        TRY(d2h(st, e->st, 2 * e->shard_len, 2 * (size_t)n * e->shard_len));
+        std::string sec;
+        uint64_t cnt = 0;
+        std::vector<std::pair<uint64_t, uint64_t>> committed;   // for the executor
+        for (uint64_t li = 0; li < e->shard_len; ++li) {
+            if (!valid[(size_t)n * e->NB + (li >> BSH)]) { li |= BS - 1; continue; }
+            const uint64_t b = st[2 * li], w = st[2 * li + 1];
+            if (!(w & W_PRESENT)) continue;
+            const uint64_t kind = (w & W_COMMITTED) ? 2 : 1;
+            app<uint64_t>(sec, e->cfg.shard_begin + li); app<uint64_t>(sec, kind);
+            app<uint64_t>(sec, b); app<uint64_t>(sec, w & W_HANDLE);
+            ++cnt;
+        }
+        app<uint64_t>(d, cnt);
+        d += sec;
+        // sends
+        sec.clear(); cnt = 0;
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
+            uint32_t dst;
+            reply_of(e, r, n, g, dst, m);
+            if (m.empty()) continue;
+            app<uint32_t>(sec, dst); app<uint32_t>(sec, (uint32_t)m.size()); sec += m;
+            ++cnt;
+        }
+        app<uint64_t>(d, cnt);
+        d += sec;
+        // promise quorum events
+        sec.clear(); cnt = 0;
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
+            if (h.m_type[g] != MPX_MSG_PREPARE_REPLY || !(r.flags[g] & F_QUORUM)) continue;
+            app<uint64_t>(sec, g - h.node_off[n]);
+            app<uint64_t>(sec, h.m_ballot[g]);
+            auto it = r.by_msg[1].find((uint32_t)g);
+            const uint64_t k = it == r.by_msg[1].end() ? 0 : it->second.size();
+            app<uint64_t>(sec, k);
+            if (k)
+                for (const OutRec *o : it->second) { app<uint64_t>(sec, o->iid); app<uint64_t>(sec, o->ballot); app<uint64_t>(sec, o->handle); }
+            ++cnt;
+        }
+        app<uint64_t>(d, cnt);
+        d += sec;
+        // chosen batch events, in the order of the replies that chose them
+        std::vector<std::pair<uint32_t, uint64_t>> ch;
+        for (size_t j = 0; j < h.b_msg.size(); ++j)
+            if (h.m_node[h.b_msg[j]] == n && r.b_chosen[j] != NONE32) ch.push_back({r.b_chosen[j], h.m_aux[h.b_msg[j]]});
+        std::sort(ch.begin(), ch.end());
+        app<uint64_t>(d, ch.size());
+        for (auto &c : ch) { app<uint64_t>(d, c.first - h.node_off[n]); app<uint64_t>(d, c.second); }
+        // executor: committed prefix from the shard's first instance (paxos.cpp:1584-1620)
+        sec.clear(); cnt = 0;
+        std::string payload;
+        for (uint64_t li = 0; li < e->shard_len; ++li) {
+            if (!valid[(size_t)n * e->NB + (li >> BSH)]) break;
+            const uint64_t w = st[2 * li + 1];
+            if (!(w & W_PRESENT) || !(w & W_COMMITTED)) break;
+            const uint64_t hd = w & W_HANDLE;
+            if (MPX_HANDLE_NOOP(hd)) continue;
+            e->vt.exec_payload(hd, payload);
+            app<uint32_t>(sec, (uint32_t)payload.size());
+            sec += payload;
+            ++cnt;
+        }
+        app<uint64_t>(d, cnt);
+        d += sec;
+    }
+    uint64_t cnt = 0;
+    std::string sec;
+    for (uint64_t li = 0; li < e->shard_len; ++li) {
+        if (!cvalid[li >> BSH]) { li |= BS - 1; continue; }
+        if (!(chosen[li] & W_PRESENT)) continue;
+        app<uint64_t>(sec, e->cfg.shard_begin + li);
+        app<uint64_t>(sec, chosen[li] & W_HANDLE);
+        ++cnt;
+    }
+    app<uint64_t>(d, cnt);
+    d += sec;
+    *out = (uint8_t *)std::malloc(d.size());
+    if (!*out) return MPX_E_NOMEM;
+    std::memcpy(*out, d.data(), d.size());
+    *size = d.size();
+    return MPX_OK;
+}
+
+// -------------------------------------------------------------- generators --
+extern "C" int mpx_trace_generate(const mpx_gen_params *p, uint8_t **out, uint64_t *size)
+{
+    if (!p || !out || !size) return MPX_E_INVAL;
+    std::string t;
+    int rc;
+    if (p->kind == MPX_GEN_CLEAN) rc = gen_clean(*p, t);
+    else if (p->kind == MPX_GEN_FAULTY) rc = gen_faulty(*p, t);
+    else rc = MPX_E_INVAL;
+    if (rc) return rc;
+    *out = (uint8_t *)std::malloc(t.size());
+    if (!*out) return MPX_E_NOMEM;
+    std::memcpy(*out, t.data(), t.size());
+    *size = t.size();
+    return MPX_OK;
+}
+
+extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
+{
+    if (!e || !p) return MPX_E_INVAL;
+    return MPX_E_STATE;   // device generator: DESIGN.md §Next (first round uses host traces)
+}
+
+// ------------------------------------------------------------------- RCCL --
+extern "C" int mpx_comm_unique_id(uint8_t out[MPX_UID_BYTES])
+{
+    static_assert(sizeof(ncclUniqueId) <= MPX_UID_BYTES, "uid size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return MPX_E_COMM;
+    std::memset(out, 0, MPX_UID_BYTES);
+    std::memcpy(out, &id, sizeof id);
+    return MPX_OK;
+}
+
+extern "C" int mpx_comm_init(mpx_engine *e, const uint8_t uid[MPX_UID_BYTES], int rank, int nranks)
+{
+    if (!e || !uid || rank < 0 || rank >= nranks) return MPX_E_INVAL;
+    HTRY(hipSetDevice(e->device));
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof id);
+    if (ncclCommInitRank(&e->comm, nranks, id, rank) != ncclSuccess) return MPX_E_COMM;
+    e->rank = rank;
+    e->nranks = nranks;
+    TRY(e->gather_buf.alloc(64ull * 8 * nranks));
+    return MPX_OK;
+}
+
+extern "C" int mpx_allgather_summary(mpx_engine *e, uint64_t *out)
+{
+    if (!e || !out) return MPX_E_INVAL;
+    if (!e->summary.p) return MPX_E_STATE;
+    HTRY(hipSetDevice(e->device));
+    if (e->comm) {
+        if (ncclAllGather(e->summary.p, e->gather_buf.p, 64, ncclUint64, e->comm, e->stream) != ncclSuccess)
+            return MPX_E_COMM;
+        HTRY(hipMemcpyAsync(out, e->gather_buf.p, 64ull * 8 * e->nranks, hipMemcpyDeviceToHost, e->stream));
+    } else {
+        HTRY(hipMemcpyAsync(out, e->summary.p, 64 * 8, hipMemcpyDeviceToHost, e->stream));
+    }
+    HTRY(hipStreamSynchronize(e->stream));
+    return MPX_OK;
+}

@@ -1,0 +1,75 @@
+// ingest.hpp — host side of mpx_submit: wire decode into SoA, value table,
+// instance bucketing into fragments.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "mpx_internal.hpp"
+
+namespace mpx {
+
+// Interned reference Values: handle -> canonical FillValue bytes
+// (multi/paxos.cpp:556-598) and what StateMachine::Execute receives.
+struct ValueTable {
+    struct Rec { uint64_t off; uint32_t len; uint32_t exec_off; uint32_t exec_len; };
+    std::unordered_map<uint64_t, Rec> idx;
+    std::string bytes;
+    // synthetic resolver for device-generated clean traces: value_id v of
+    // proposer 0 is the decimal string of v-1
+    bool synthetic_clean = false;
+    // parse one Value; returns bytes used (>0) or a negative MPX_E_* code
+    long parse(const uint8_t *p, size_t avail, uint64_t *handle);
+    bool encode(uint64_t handle, std::string &out) const;    // canonical bytes
+    bool exec_payload(uint64_t handle, std::string &out) const;
+    void clear() { idx.clear(); bytes.clear(); synthetic_clean = false; }
+};
+
+// One node's decoded receive stream (submission order).
+struct NodeStream {
+    std::vector<uint8_t> type;
+    std::vector<uint32_t> src;
+    std::vector<uint64_t> ballot, aux, ent;
+    std::vector<uint32_t> cnt;
+    std::vector<uint64_t> e_iid, e_val;           // ACCEPT / COMMIT / P_BATCH entries (in shard)
+    std::vector<uint64_t> r_iid, r_pid, r_val;    // PREPARE_REPLY entries (in shard)
+    std::vector<uint64_t> g_a, g_b;               // PREPARE ranges (all), sorted by start
+    void clear() { *this = NodeStream(); }
+};
+
+struct IngestViolation { uint64_t code = 0, node = 0, seq = 0, iid = 0, count = 0; };
+
+// Flattened, bucketed host copy of the trace — mirrors the device arrays.
+struct HostTrace {
+    uint32_t N = 0, NB = 0;
+    uint64_t shard_begin = 0, shard_len = 0;
+    std::vector<uint8_t> m_type;
+    std::vector<uint32_t> m_src, m_cnt, m_node;
+    std::vector<uint64_t> m_ballot, m_aux, m_ent;
+    std::vector<uint64_t> node_off;
+    std::vector<uint32_t> chunk_node, node_chunk_off;
+    std::vector<uint64_t> chunk_beg, chunk_end;
+    std::vector<uint64_t> e_val, e_iid, r_pid, r_val, r_iid, g_a, g_b;
+    std::vector<uint8_t> e_slot, r_slot;
+    bool any_sparse = false;
+    std::vector<uint64_t> f_off;
+    std::vector<Frag> frags;
+    std::vector<uint64_t> ev_off, pl_off;
+    std::vector<uint32_t> ev_msg, pl_msg;
+    std::vector<uint32_t> b_msg, b_pstart, b_rep;
+    std::vector<uint64_t> b_rep_off;
+    std::vector<uint64_t> cf_off;
+    std::vector<Frag> cfrags;
+};
+
+// Decode one record of `node`'s stream into `ns`.  Entries outside
+// [shard_begin, shard_end) are dropped, headers are always kept.
+int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, const uint8_t *m, size_t len,
+                  uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol);
+
+// Flatten node streams and build every index the kernels walk.
+int build_trace(const std::vector<NodeStream> &nodes, uint64_t shard_begin, uint64_t shard_len,
+                HostTrace &ht);
+
+}  // namespace mpx

@@ -1,0 +1,177 @@
+// mpx_internal.hpp — shared layout of the engine (host ingest, launch code, kernels).
+//
+// HBM layout (DESIGN.md §Data layout):
+//   * messages, all nodes flattened in processing order: SoA headers
+//     m_type u8 | m_src u32 | m_ballot u64 | m_aux u64 | m_ent u64 | m_cnt u32
+//   * entry pools: e_val u64 (+ e_slot u8 when a fragment is sparse) for
+//     ACCEPT / COMMIT / P_BATCH; r_pid,r_val u64 (+ r_slot) for PREPARE_REPLY;
+//     g_a,g_b u64 prepare ranges
+//   * fragments: every entry-carrying message split into runs that fall in one
+//     256-instance bucket, listed per (node, bucket) in processing order (CSR)
+//   * state: one 16-byte slot per (node, instance) = {ballot, word}
+//       word = PRESENT | COMMITTED? | handle  — accepted and committed entries
+//       of a node are disjoint (OnCommit erases accepted_values_,
+//       multi/paxos.cpp:1501; OnAccept skips committed, :1380), so one slot
+//       holds either.
+#pragma once
+#include <cstdint>
+#include <cstddef>
+
+#include "mpx.h"
+
+#ifdef __HIP__
+#define MPX_HD __host__ __device__
+#else
+#define MPX_HD
+#endif
+
+namespace mpx {
+
+constexpr uint32_t BSH = 8;                  // bucket = 256 instances
+constexpr uint32_t BS = 1u << BSH;
+constexpr uint32_t SCAN_CHUNK = 1024;        // header-scan chunk (messages)
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+
+constexpr uint64_t W_PRESENT = 1ull << 63;
+constexpr uint64_t W_COMMITTED = 1ull << 62;
+constexpr uint64_t W_HANDLE = (1ull << 62) - 1;
+
+// m_flags bits, written by the header scan / proposer kernels
+enum : uint8_t {
+    F_GRANTED = 1,    // PREPARE id > promised, ACCEPT id >= promised (paxos.cpp:865,1366)
+    F_REJECT = 2,     // reply REJECT(max_seen) (paxos.cpp:894,1398)
+    F_COUNTED = 4,    // PREPARE_REPLY merged into pre_accepted (paxos.cpp:1038-1045)
+    F_QUORUM = 8,     // PREPARE_REPLY that reached the promise quorum (paxos.cpp:1047)
+    F_BADNODE = 16
+};
+
+// fragment kinds (Frag::flags >> 4)
+enum : uint8_t { K_ACCEPT = 0, K_COMMIT = 1, K_PREPLY = 2, K_BATCH = 3 };
+enum : uint8_t { FR_DENSE = 1 };
+
+struct Frag {
+    uint64_t entry;      // first entry in its pool
+    uint32_t msg;        // global message index (K_BATCH in chosen lists: batch index)
+    uint16_t count;      // entries in this bucket run (<= 256)
+    uint8_t start;       // bucket-local slot of the first entry (dense runs)
+    uint8_t flags;       // FR_DENSE | kind << 4
+};
+static_assert(sizeof(Frag) == 16, "Frag is 16 bytes");
+
+// snapshot output record: an entry of a granted PREPARE_REPLY (kind 0) or of
+// a promise-quorum merged map (kind 1)
+struct OutRec {
+    uint32_t msg;
+    uint32_t kind;
+    uint64_t iid;
+    uint64_t ballot;
+    uint64_t handle;
+};
+
+// violation record written once (first code wins) + count
+struct DevViolation {
+    unsigned long long code, node, seq, iid, count;
+};
+
+// Everything a kernel needs, passed by value (kernarg).
+struct DevView {
+    uint32_t N, quorum, NB, semantics;
+    uint64_t shard_begin, shard_len;
+    uint64_t num_msgs;
+    // messages
+    const uint8_t *m_type;
+    const uint32_t *m_src;
+    const uint64_t *m_ballot;
+    const uint64_t *m_aux;
+    const uint64_t *m_ent;
+    const uint32_t *m_cnt;
+    const uint32_t *m_node;         // node of each message
+    const uint64_t *node_off;       // N+1
+    uint8_t *m_flags;
+    uint64_t *m_maxseen;
+    // header scan
+    uint32_t num_chunks;
+    const uint32_t *chunk_node;
+    const uint64_t *chunk_beg;      // global msg index of chunk start
+    const uint64_t *chunk_end;
+    const uint32_t *node_chunk_off; // N+1
+    uint64_t *chunk_agg;            // 2 per chunk: pmax, smax
+    uint64_t *chunk_carry;          // 2 per chunk: exclusive prefix
+    uint64_t *node_scal;            // 2 per node: promised, max_seen
+    // pools
+    const uint64_t *e_val;
+    const uint8_t *e_slot;
+    const uint64_t *r_pid;
+    const uint64_t *r_val;
+    const uint8_t *r_slot;
+    const uint64_t *g_a;
+    const uint64_t *g_b;
+    // fragment lists
+    const uint64_t *f_off;          // N*NB+1
+    const Frag *frags;
+    const uint64_t *ev_off;         // N+1
+    const uint32_t *ev_msg;
+    const uint64_t *pl_off;         // N+1
+    const uint32_t *pl_msg;
+    // batches
+    uint32_t num_batches;
+    const uint32_t *b_msg;
+    const uint32_t *b_pstart;
+    const uint64_t *b_rep_off;
+    const uint32_t *b_rep;
+    uint32_t *b_chosen;             // global msg index of the quorum reply, NONE32
+    const uint64_t *cf_off;         // NB+1
+    const Frag *cfrags;
+    // state
+    uint64_t *st;                   // 2 words per (node, instance)
+    uint8_t *st_valid;              // per (node, bucket)
+    uint64_t *chosen;               // per instance
+    uint8_t *chosen_valid;          // per bucket
+    // outputs
+    OutRec *out;
+    unsigned long long *out_cursor;
+    uint64_t out_cap;
+    unsigned long long *partials;   // 8 words per apply workgroup, then chosen workgroups
+    DevViolation *viol;
+    unsigned long long *summary;    // 64 words
+};
+
+constexpr uint32_t APPLY_WGS_MAX = 2048;
+constexpr uint32_t CHOSEN_WGS_MAX = 1024;
+// partial counter slots
+enum { PC_A = 0, PC_L, PC_P, PC_Q, PC_C, PC_DSTATE, PC_DCHOSEN, PC_MSGS };
+// summary words (mpx_allgather_summary)
+enum { SW_C = 0, SW_P, SW_A, SW_L, SW_MSGS, SW_V, SW_DCHOSEN, SW_DSTATE, SW_DSCAL, SW_Q,
+       SW_NODE_SCAL = 16 };   // then promised, max_seen per node (up to 24 nodes summarised)
+
+MPX_HD inline uint64_t mix64(uint64_t x)
+{
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    x ^= x >> 31; return x;
+}
+MPX_HD inline uint64_t state_digest(uint32_t node, uint64_t iid, uint64_t kind,
+                                                 uint64_t ballot, uint64_t handle)
+{
+    return mix64(mix64(mix64(iid + (uint64_t)node * 0x9E3779B97F4A7C15ull) ^ ballot) ^
+                 (handle + kind * 0xD6E8FEB86659FD93ull));
+}
+MPX_HD inline uint64_t chosen_digest(uint64_t iid, uint64_t handle)
+{
+    return mix64(mix64(iid) ^ handle);
+}
+MPX_HD inline uint64_t scalar_digest(uint32_t node, uint64_t promised, uint64_t max_seen)
+{
+    return mix64(mix64((uint64_t)node * 0x9E3779B97F4A7C15ull ^ promised) ^ max_seen);
+}
+
+// kernels (kernels.hip); every launcher queues on `stream`, returns hipError_t as int
+struct LaunchGeom { uint32_t apply_wgs, chosen_wgs; };
+int launch_run(const DevView &v, void *stream, LaunchGeom g, void *ev_begin, void *ev_apply0,
+               void *ev_apply1, void *ev_end);
+int launch_gen_clean(const DevView &v, void *stream, uint64_t M, uint32_t batch, uint32_t N,
+                     uint64_t *m_ballot_w, uint8_t *m_type_w, uint32_t *m_src_w, uint64_t *m_aux_w,
+                     uint64_t *m_ent_w, uint32_t *m_cnt_w, uint32_t *m_node_w, uint64_t *e_val_w,
+                     Frag *frags_w, Frag *cfrags_w, uint32_t *b_rep_w);
+
+}  // namespace mpx

@@ -1,0 +1,298 @@
+"""ctypes binding of libmpx.so (include/mpx.h) — the host mirror used by the
+tests, bench.py and __graft_entry__.
+
+The reference's host drives its protocol core through NetWork::OnReceiveMessage
+/ SendMessage* / StateMachine::Execute (multi/paxos.h:193-222); `Engine`
+exposes the batched equivalents: submit (OnReceiveMessage), run, drain_sends
+(SendMessage*), dump (canonical result) and the state readbacks.
+
+There is no Python or CPU fallback: without the built library or without a
+GPU every compute call raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libmpx.so")
+INCLUDE_H = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "mpx.h")
+
+ABI_VERSION = 1
+SEM_MULTI, SEM_MEMBER = 0, 1
+GEN_CLEAN, GEN_FAULTY, GEN_MEMBER = 0, 1, 2
+PRESENT = 1 << 63
+UID_BYTES = 128
+
+ERRORS = {0: "OK", -1: "E_INVAL", -2: "E_NOMEM", -3: "E_HIP", -4: "E_DECODE", -5: "E_RANGE",
+          -6: "E_STATE", -7: "E_NODEVICE", -8: "E_COMM", -9: "E_VALUE"}
+
+
+class MpxError(RuntimeError):
+    def __init__(self, fn, rc):
+        super().__init__("%s failed: %s (%d)" % (fn, ERRORS.get(rc, "?"), rc))
+        self.rc = rc
+
+
+class Epoch(ctypes.Structure):
+    _fields_ = [("version", ctypes.c_uint32), ("pad", ctypes.c_uint32), ("acceptor_mask", ctypes.c_uint64)]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_uint32), ("num_nodes", ctypes.c_uint32),
+                ("semantics", ctypes.c_uint32), ("device", ctypes.c_int32),
+                ("shard_begin", ctypes.c_uint64), ("shard_end", ctypes.c_uint64),
+                ("num_epochs", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("epochs", ctypes.POINTER(Epoch))]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "chosen", "promise_entries", "accept_apps", "commit_apps", "messages", "violations",
+        "chosen_digest", "state_digest", "scalar_digest", "device_ns", "apply_ns", "ingest_ns",
+        "bytes_alg", "r0", "r1", "r2")]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if not f.startswith("r")}
+
+
+class Violation(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_uint64), ("node", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+                ("seq", ctypes.c_uint64), ("iid", ctypes.c_uint64)]
+
+
+class GenParams(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("num_nodes", ctypes.c_uint32),
+                ("num_instances", ctypes.c_uint64), ("seed", ctypes.c_uint64),
+                ("batch", ctypes.c_uint32), ("proposers", ctypes.c_uint32),
+                ("drop_rate", ctypes.c_uint32), ("dup_rate", ctypes.c_uint32),
+                ("max_delay", ctypes.c_uint32), ("noop_permille", ctypes.c_uint32),
+                ("shard_begin", ctypes.c_uint64), ("shard_end", ctypes.c_uint64)]
+
+
+SEND_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                           ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint32)
+
+_lib = None
+
+
+def lib():
+    """Load libmpx.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError("libmpx.so not built: run `make -C multi-paxos_amd` (%s)" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        P = ctypes.POINTER
+        u8p, u64p = P(ctypes.c_uint8), P(ctypes.c_uint64)
+        vp = ctypes.c_void_p
+        sig = {
+            "mpx_version": [],
+            "mpx_device_count": [P(ctypes.c_int)],
+            "mpx_create": [P(Config), P(vp)],
+            "mpx_destroy": [vp],
+            "mpx_submit": [vp, ctypes.c_uint32, ctypes.c_char_p, u64p, ctypes.c_uint64],
+            "mpx_submit_trace": [vp, ctypes.c_char_p, ctypes.c_uint64],
+            "mpx_run": [vp], "mpx_reset_state": [vp], "mpx_step": [vp], "mpx_sync": [vp],
+            "mpx_timings": [vp, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_uint32)],
+            "mpx_drain_sends": [vp, SEND_FN, vp],
+            "mpx_read_chosen": [vp, ctypes.c_uint64, ctypes.c_uint64, u64p],
+            "mpx_read_node_scalars": [vp, ctypes.c_uint32, u64p, u64p],
+            "mpx_read_node_state": [vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, u64p, u64p, u64p, u64p],
+            "mpx_stats_get": [vp, P(Stats)],
+            "mpx_last_violation": [vp, P(Violation)],
+            "mpx_dump_result": [vp, P(u8p), u64p],
+            "mpx_value_bytes": [vp, ctypes.c_uint64, u8p, ctypes.c_uint32, P(ctypes.c_uint32)],
+            "mpx_trace_generate": [P(GenParams), P(u8p), u64p],
+            "mpx_load_clean_device": [vp, P(GenParams)],
+            "mpx_comm_unique_id": [u8p],
+            "mpx_comm_init": [vp, u8p, ctypes.c_int, ctypes.c_int],
+            "mpx_allgather_summary": [vp, u64p],
+        }
+        for name, args in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = ctypes.c_int
+        L.mpx_free.argtypes = [vp]
+        L.mpx_free.restype = None
+        _lib = L
+    return _lib
+
+
+def _ck(name, rc):
+    if rc != 0:
+        raise MpxError(name, rc)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _ck("mpx_device_count", lib().mpx_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def _take(ptr, size):
+    data = ctypes.string_at(ptr, size)
+    lib().mpx_free(ptr)
+    return data
+
+
+def generate_trace(kind=GEN_CLEAN, num_nodes=5, num_instances=1 << 10, seed=0, batch=256,
+                   proposers=1, drop_rate=0, dup_rate=0, max_delay=0, noop_permille=0,
+                   shard_begin=0, shard_end=0):
+    """Deterministic synthetic MPXT trace (host generator in libmpx)."""
+    p = GenParams(kind, num_nodes, num_instances, seed, batch, proposers, drop_rate, dup_rate,
+                  max_delay, noop_permille, shard_begin, shard_end)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    size = ctypes.c_uint64()
+    _ck("mpx_trace_generate", lib().mpx_trace_generate(ctypes.byref(p), ctypes.byref(out), ctypes.byref(size)))
+    return _take(out, size.value)
+
+
+def trace_header(trace):
+    import struct
+    assert trace[:4] == b"MPXT"
+    _, n, sem, m = struct.unpack_from("<IIIQ", trace, 4)
+    return {"num_nodes": n, "semantics": sem, "num_instances": m}
+
+
+class Engine:
+    """One engine = one GPU, one instance shard [shard_begin, shard_end)."""
+
+    def __init__(self, num_nodes, shard_begin=0, shard_end=None, device=0, semantics=SEM_MULTI, epochs=()):
+        L = lib()
+        if shard_end is None:
+            raise ValueError("shard_end required")
+        self._epochs = (Epoch * max(len(epochs), 1))(*[Epoch(v, 0, m) for v, m in epochs])
+        cfg = Config(ABI_VERSION, num_nodes, semantics, device, shard_begin, shard_end,
+                     len(epochs), 0, self._epochs if epochs else None)
+        h = ctypes.c_void_p()
+        _ck("mpx_create", L.mpx_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.num_nodes = num_nodes
+        self.shard_begin, self.shard_end = shard_begin, shard_end
+
+    @classmethod
+    def for_trace(cls, trace, device=0):
+        hd = trace_header(trace)
+        e = cls(hd["num_nodes"], 0, max(hd["num_instances"], 1), device=device, semantics=hd["semantics"])
+        e.submit_trace(trace)
+        return e
+
+    def close(self):
+        if self.h:
+            lib().mpx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # inbound
+    def submit(self, node, messages):
+        blob = b"".join(messages)
+        offs = [0]
+        for m in messages:
+            offs.append(offs[-1] + len(m))
+        arr = (ctypes.c_uint64 * len(offs))(*offs)
+        _ck("mpx_submit", lib().mpx_submit(self.h, node, blob, arr, len(messages)))
+
+    def submit_trace(self, trace):
+        _ck("mpx_submit_trace", lib().mpx_submit_trace(self.h, trace, len(trace)))
+
+    def load_clean_device(self, **kw):
+        p = GenParams(GEN_CLEAN, kw.get("num_nodes", self.num_nodes), kw["num_instances"], kw.get("seed", 0),
+                      kw.get("batch", 256), 1, 0, 0, 0, 0, self.shard_begin, self.shard_end)
+        _ck("mpx_load_clean_device", lib().mpx_load_clean_device(self.h, ctypes.byref(p)))
+
+    # execution
+    def run(self):
+        _ck("mpx_run", lib().mpx_run(self.h))
+        return self.stats()
+
+    def step(self):
+        _ck("mpx_step", lib().mpx_step(self.h))
+
+    def sync(self):
+        _ck("mpx_sync", lib().mpx_sync(self.h))
+
+    def reset_state(self):
+        _ck("mpx_reset_state", lib().mpx_reset_state(self.h))
+
+    def timings(self, max_n=4096):
+        a = (ctypes.c_double * max_n)()
+        r = (ctypes.c_double * max_n)()
+        n = ctypes.c_uint32()
+        _ck("mpx_timings", lib().mpx_timings(self.h, max_n, a, r, ctypes.byref(n)))
+        return list(a[: n.value]), list(r[: n.value])
+
+    # results
+    def stats(self):
+        s = Stats()
+        _ck("mpx_stats_get", lib().mpx_stats_get(self.h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def violation(self):
+        v = Violation()
+        _ck("mpx_last_violation", lib().mpx_last_violation(self.h, ctypes.byref(v)))
+        return {"code": v.code, "node": v.node, "seq": v.seq, "iid": v.iid}
+
+    def dump(self):
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_dump_result", lib().mpx_dump_result(self.h, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
+    def drain_sends(self):
+        sends = []
+
+        def cb(_u, src, dst, p, n):
+            sends.append((src, dst, ctypes.string_at(p, n)))
+
+        f = SEND_FN(cb)
+        _ck("mpx_drain_sends", lib().mpx_drain_sends(self.h, f, None))
+        return sends
+
+    def read_chosen(self, first, count):
+        out = (ctypes.c_uint64 * count)()
+        _ck("mpx_read_chosen", lib().mpx_read_chosen(self.h, first, count, out))
+        return list(out)
+
+    def read_node_scalars(self, node):
+        p, m = ctypes.c_uint64(), ctypes.c_uint64()
+        _ck("mpx_read_node_scalars", lib().mpx_read_node_scalars(self.h, node, ctypes.byref(p), ctypes.byref(m)))
+        return p.value, m.value
+
+    def read_node_state(self, node, first, count):
+        arrs = [(ctypes.c_uint64 * count)() for _ in range(4)]
+        _ck("mpx_read_node_state", lib().mpx_read_node_state(self.h, node, first, count, *arrs))
+        return [list(a) for a in arrs]
+
+    # multi-GPU
+    @staticmethod
+    def comm_unique_id():
+        buf = (ctypes.c_uint8 * UID_BYTES)()
+        _ck("mpx_comm_unique_id", lib().mpx_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid, rank, nranks):
+        buf = (ctypes.c_uint8 * UID_BYTES).from_buffer_copy(uid)
+        _ck("mpx_comm_init", lib().mpx_comm_init(self.h, buf, rank, nranks))
+        self.nranks = nranks
+
+    def allgather_summary(self, nranks=1):
+        out = (ctypes.c_uint64 * (64 * nranks))()
+        _ck("mpx_allgather_summary", lib().mpx_allgather_summary(self.h, out))
+        return [list(out[64 * r: 64 * (r + 1)]) for r in range(nranks)]
+
+
+def declared_symbols(header=INCLUDE_H):
+    """Function names declared in include/mpx.h."""
+    import re
+    txt = open(header).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void)\s+(mpx_\w+)\s*\(", txt, re.M)))
