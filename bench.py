@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Benchmark: quorum decisions/s of the MI355X Multi-Paxos engine (BASELINE.json metric).
+
+Workload (config.workload): C4 — 2^27 instances x 9 acceptors, clean single
+round (one proposer, ballot 1<<16, 256 instances per ACCEPT/COMMIT), the trace
+materialised in HBM by the device generator before timing.  The instance space
+is sharded contiguously over the ranks (strong scaling: the whole C4 trace at
+every N); each rank owns one GPU.
+
+One step = one pass of the hot path over the resident trace from genesis
+state: header scan, promise quorum, accept-vote quorum, acceptor/learner apply
+(k_apply), chosen log, counters, and — for N > 1 — the RCCL all-gather of the
+64-word per-shard summary.  decisions/s = chosen instances per step (summed
+over ranks) / max-over-ranks step time.
+
+roofline: the dominant kernel is k_apply; achieved = B_alg per launch
+(16 P + 24 A + 16 L = 40 B per acceptor-instance here) /
+its mean duration from HIP events on the engine's stream.  traffic = HBM bytes
+per launch from rocprofv3 PMC (profiles/, tools/pmc_traffic.py) or null.
+
+cpu_baseline: the reference's own handlers (multi/paxos.cpp compiled -O2 in
+oracle/_ref, kind "reference") on a bounded sample of the same clean stream,
+rank 0 at N=1 only.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import ctypes
+import glob
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "multi-paxos_amd"))
+
+import mpx  # noqa: E402
+
+METRIC = "quorum decisions/sec (instances chosen/s) + achieved HBM GB/s, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip-level table
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--instances", type=int, default=1 << 27, help="M (C4: 2^27)")
+    ap.add_argument("--nodes", type=int, default=9, help="acceptors N (C4: 9)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the cpu_baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist      # gloo on the CPU: rendezvous, barrier, max-reduce only
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def allreduce_max(pg, x):
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def broadcast_bytes(pg, data, rank):
+    if pg is None:
+        return data
+    obj = [data if rank == 0 else None]
+    pg.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def latest_pmc(n_nodes, instances, world):
+    """HBM bytes per k_apply launch from the newest profiles/*pmc*.json of this config."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("nodes") == n_nodes and d.get("instances") == instances and d.get("gpus", 1) == world:
+            best = d
+    return best
+
+
+def cpu_baseline(args, budget_s):
+    """Reference handlers (oracle/_ref) on host cores: node 1's accept+commit stream of a clean trace."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libmpx_ref.so")
+    kind = "reference"
+    if not os.path.exists(ref_so):
+        return None
+    lib = ctypes.CDLL(ref_so)
+    fn = lib.mpxref_time_node
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+    fn.restype = ctypes.c_int64
+    sample_m = 1 << 16
+    trace = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=args.nodes, num_instances=sample_m, batch=256)
+    # calibrate one pass, then size the sample to the budget
+    t0 = time.perf_counter()
+    fn(trace, len(trace), 1, 1)
+    one = time.perf_counter() - t0
+    threads = max(1, min(16, os.cpu_count() or 1))
+    reps = max(1, int(budget_s / max(one, 1e-6)))
+    done = [0] * threads
+
+    def work(i):
+        done[i] = fn(trace, len(trace), 1, reps)
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    apps = threads * reps * sample_m            # (acceptor, instance) accept+commit applications
+    # one decision needs every acceptor's accept + commit application: N of them
+    decisions = apps / args.nodes
+    return {"value": decisions / dt, "unit": "decisions/s", "cores": threads, "kind": kind,
+            "sample": "reference multi/paxos.cpp handlers (-O2) on node 1's stream of a clean C4-shaped trace: "
+                      "%d instances x %d passes x %d threads, accept+commit (OnAccept/OnCommit), %.1f s wall; "
+                      "decisions/s = acceptor-instance applications/s / N=%d" % (sample_m, reps, threads, dt, args.nodes),
+            "node_instance_apps_per_s": apps / dt}
+
+
+def main():
+    args = parse()
+    world, rank, local, pg = dist_setup(args)
+    if args.gpus != world and world > 1:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    M, N = args.instances, args.nodes
+    # contiguous instance shards, aligned to the 256-instance bucket
+    per = ((M + world - 1) // world + 255) // 256 * 256
+    sb, se = min(M, rank * per), min(M, (rank + 1) * per)
+    eng = mpx.Engine(N, sb, se, device=local)
+    if world > 1:
+        uid = broadcast_bytes(pg, mpx.Engine.comm_unique_id() if rank == 0 else None, rank)
+        eng.comm_init(uid, rank, world)
+    t_gen = time.perf_counter()
+    eng.load_clean_device(num_instances=M, batch=256)
+    t_gen = time.perf_counter() - t_gen
+
+    for _ in range(args.warmup):
+        eng.step()
+    eng.sync()
+    eng.timings()                                   # drop warmup timings
+
+    barrier(pg)
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step()
+    eng.sync()
+    dt = time.perf_counter() - t0
+    barrier(pg)
+    dt_max = allreduce_max(pg, dt)
+
+    st = eng.stats()
+    apply_ms, run_ms = eng.timings()
+    summ = eng.allgather_summary(world)
+    chosen_total = sum(s[0] for s in summ)
+    viol_total = sum(s[5] for s in summ)
+    assert chosen_total == M, "chosen %d != %d instances" % (chosen_total, M)
+    assert viol_total == 0
+    # every rank computes the same per-acceptor scalars from the replicated headers
+    assert all(s[8] == summ[0][8] for s in summ), "per-acceptor scalars differ across shards"
+
+    value = chosen_total * args.steps / dt_max
+    ms_per_step = dt_max / args.steps * 1e3
+    apply_mean = sum(apply_ms) / max(len(apply_ms), 1)
+    bytes_alg = st["bytes_alg"]                     # this rank's 16P + 24A + 16L per launch
+    achieved = bytes_alg / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
+    pmc = latest_pmc(N, M, world)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, args.cpu_seconds)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "decisions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (device-generated clean trace, decoded+bucketed in HBM before timing)",
+            "config": {"workload": "C4: 2^27 instances x 9 acceptors, clean single round, batch 256, "
+                                   "instance-sharded over the GPUs" if (M, N) == (1 << 27, 9) else
+                                   "clean: %d instances x %d acceptors, batch 256" % (M, N),
+                       "instances": M, "acceptors": N, "batch": 256, "shard_per_gpu": se - sb,
+                       "parallelism": "instance-shard x%d (RCCL all-gather of 64-word summaries)" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_apply", "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_alg},
+            "cpu_baseline": cpu,
+            "hbm_gbps_alg_step": bytes_alg * world / (dt_max / args.steps) / 1e9,
+            "decisions_per_step": chosen_total,
+            "run_ms_device": sum(run_ms) / max(len(run_ms), 1),
+            "trace_materialise_s": t_gen,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -307,7 +307,12 @@ static int queue_run(mpx_engine *e)
     StepEvents *ev = next_events(e);
     if (!ev) return MPX_E_HIP;
     int rc = launch_run(e->view, e->stream, e->geom, ev->e[0], ev->e[1], ev->e[2], ev->e[3]);
-    return rc ? MPX_E_HIP : MPX_OK;
+    if (rc) return MPX_E_HIP;
+    // the one cross-GPU exchange: every rank's 64-word summary, over RCCL on
+    // the same stream, no host synchronisation
+    if (e->comm && ncclAllGather(e->summary.p, e->gather_buf.p, 64, ncclUint64, e->comm, e->stream) != ncclSuccess)
+        return MPX_E_COMM;
+    return MPX_OK;
 }
 
 static int collect(mpx_engine *e)
@@ -500,6 +505,8 @@ extern "C" void mpx_free(void *p) { std::free(p); }
 // ------------------------------------------------- sends / canonical dump --
 template <typename T> static inline void app(std::string &s, T v) { s.append((const char *)&v, sizeof v); }
 
+static int ensure_host_headers(mpx_engine *e);
+
 struct Results {
     std::vector<uint8_t> flags;
     std::vector<uint64_t> maxseen, scal;
@@ -511,8 +518,8 @@ struct Results {
 static int fetch_results(mpx_engine *e, Results &r)
 {
     if (!have_results(e)) return MPX_E_STATE;
-    if (e->device_trace) return MPX_E_STATE;      // synthetic device traces have no host headers
     HTRY(hipSetDevice(e->device));
+    TRY(ensure_host_headers(e));
     const size_t G = e->ht.m_type.size();
     TRY(d2h(r.flags, e->m_flags, G));
     TRY(d2h(r.maxseen, e->m_maxseen, G));
@@ -703,7 +710,116 @@ extern "C" int mpx_trace_generate(const mpx_gen_params *p, uint8_t **out, uint64
 extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
 {
     if (!e || !p) return MPX_E_INVAL;
-    return MPX_E_STATE;   // device generator: DESIGN.md §Next (first round uses host traces)
+    if (p->kind != MPX_GEN_CLEAN || p->num_nodes != e->cfg.num_nodes) return MPX_E_INVAL;
+    if ((p->batch && p->batch != BS) || (e->cfg.shard_begin & (BS - 1))) return MPX_E_INVAL;
+    if (e->cfg.shard_end > p->num_instances) return MPX_E_INVAL;
+    HTRY(hipSetDevice(e->device));
+    const uint64_t t0 = now_ns();
+    const uint32_t N = e->cfg.num_nodes;
+    const uint64_t sb = e->cfg.shard_begin, se = e->cfg.shard_end, L = se - sb;
+    const uint64_t k0 = sb >> BSH, K = e->NB;                   // kept batches = shard buckets
+    const uint64_t G0 = 2 + N + K * (3 + 2ull * N), G1 = 1 + 2 * K;
+    const uint64_t G = G0 + (uint64_t)(N - 1) * G1;
+    const uint64_t E = (2ull * N + 1) * L;
+    if (G >= NONE32) return MPX_E_RANGE;
+    const uint64_t ballot = 1ull << 16;                         // (1 << 16) | node 0
+    // host-side small tables
+    HostTrace &h = e->ht;
+    h = HostTrace();
+    h.N = N; h.NB = e->NB; h.shard_begin = sb; h.shard_len = L;
+    h.node_off.resize(N + 1);
+    for (uint32_t n = 0; n <= N; ++n) h.node_off[n] = n == 0 ? 0 : G0 + (uint64_t)(n - 1) * G1;
+    h.node_chunk_off.assign(N + 1, 0);
+    for (uint32_t n = 0; n < N; ++n) {
+        h.node_chunk_off[n] = (uint32_t)h.chunk_node.size();
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; g += SCAN_CHUNK) {
+            h.chunk_node.push_back(n);
+            h.chunk_beg.push_back(g);
+            h.chunk_end.push_back(std::min<uint64_t>(g + SCAN_CHUNK, h.node_off[n + 1]));
+        }
+    }
+    h.node_chunk_off[N] = (uint32_t)h.chunk_node.size();
+    h.g_a.assign(N, 0); h.g_b.assign(N, ~0ull);
+    h.ev_off.assign(N + 1, 0); h.pl_off.assign(N + 1, 0);
+    for (uint32_t k = 0; k < N + 2; ++k) h.ev_msg.push_back(k);
+    h.pl_msg.push_back(0);
+    for (uint32_t k = 0; k < N; ++k) h.pl_msg.push_back(2 + k);
+    h.ev_off[1] = N + 2; h.pl_off[1] = N + 1;
+    for (uint32_t n = 1; n < N; ++n) {
+        h.ev_msg.push_back((uint32_t)h.node_off[n]);
+        h.ev_off[n + 1] = h.ev_off[n] + 1;
+        h.pl_off[n + 1] = h.pl_off[n];
+    }
+    hipStream_t s = e->stream;
+    TRY(e->m_type.alloc(G)); TRY(e->m_src.alloc(4 * G)); TRY(e->m_ballot.alloc(8 * G)); TRY(e->m_aux.alloc(8 * G));
+    TRY(e->m_ent.alloc(8 * G)); TRY(e->m_cnt.alloc(4 * G)); TRY(e->m_node.alloc(4 * G));
+    TRY(e->m_flags.alloc(G)); TRY(e->m_maxseen.alloc(8 * G));
+    TRY(upload(e->node_off, h.node_off, s));
+    TRY(upload(e->chunk_node, h.chunk_node, s)); TRY(upload(e->chunk_beg, h.chunk_beg, s));
+    TRY(upload(e->chunk_end, h.chunk_end, s)); TRY(upload(e->node_chunk_off, h.node_chunk_off, s));
+    TRY(e->chunk_agg.alloc(std::max<size_t>(16 * h.chunk_node.size(), 16)));
+    TRY(e->chunk_carry.alloc(std::max<size_t>(16 * h.chunk_node.size(), 16)));
+    TRY(e->e_val.alloc(std::max<uint64_t>(8 * E, 8)));
+    TRY(e->e_slot.alloc(8)); TRY(e->r_pid.alloc(8)); TRY(e->r_val.alloc(8)); TRY(e->r_slot.alloc(8));
+    TRY(upload(e->g_a, h.g_a, s)); TRY(upload(e->g_b, h.g_b, s));
+    TRY(e->f_off.alloc(8 * ((uint64_t)N * e->NB + 1))); TRY(e->frags.alloc(sizeof(Frag) * 2 * (uint64_t)N * e->NB + 16));
+    TRY(upload(e->ev_off, h.ev_off, s)); TRY(upload(e->ev_msg, h.ev_msg, s));
+    TRY(upload(e->pl_off, h.pl_off, s)); TRY(upload(e->pl_msg, h.pl_msg, s));
+    TRY(e->b_msg.alloc(4 * K + 4)); TRY(e->b_pstart.alloc(4 * K + 4)); TRY(e->b_rep_off.alloc(8 * (K + 1)));
+    TRY(e->b_rep.alloc(4 * (uint64_t)N * K + 4)); TRY(e->b_chosen.alloc(4 * K + 4));
+    TRY(e->cf_off.alloc(8 * (K + 1))); TRY(e->cfrags.alloc(sizeof(Frag) * K + 16));
+    if (launch_gen_clean(s, N, K, k0, sb, se, G0, G1, 3 * L, ballot, e->NB,
+                         e->m_type.as<uint8_t>(), e->m_src.as<uint32_t>(), e->m_ballot.as<uint64_t>(),
+                         e->m_aux.as<uint64_t>(), e->m_ent.as<uint64_t>(), e->m_cnt.as<uint32_t>(),
+                         e->m_node.as<uint32_t>(), e->e_val.as<uint64_t>(), e->frags.as<Frag>(),
+                         e->f_off.as<uint64_t>(), e->b_msg.as<uint32_t>(), e->b_pstart.as<uint32_t>(),
+                         e->b_rep_off.as<uint64_t>(), e->b_rep.as<uint32_t>(), e->cf_off.as<uint64_t>(),
+                         e->cfrags.as<Frag>()) != 0)
+        return MPX_E_HIP;
+    HTRY(hipStreamSynchronize(s));
+    e->num_msgs = G;
+    DevView &v = e->view;
+    v.m_type = e->m_type.as<uint8_t>(); v.m_src = e->m_src.as<uint32_t>();
+    v.m_ballot = e->m_ballot.as<uint64_t>(); v.m_aux = e->m_aux.as<uint64_t>();
+    v.m_ent = e->m_ent.as<uint64_t>(); v.m_cnt = e->m_cnt.as<uint32_t>();
+    v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
+    v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
+    v.num_chunks = (uint32_t)h.chunk_node.size();
+    v.chunk_node = e->chunk_node.as<uint32_t>(); v.chunk_beg = e->chunk_beg.as<uint64_t>();
+    v.chunk_end = e->chunk_end.as<uint64_t>(); v.node_chunk_off = e->node_chunk_off.as<uint32_t>();
+    v.chunk_agg = e->chunk_agg.as<uint64_t>(); v.chunk_carry = e->chunk_carry.as<uint64_t>();
+    v.e_val = e->e_val.as<uint64_t>(); v.e_slot = e->e_slot.as<uint8_t>();
+    v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
+    v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
+    v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
+    v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>();
+    v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
+    v.num_batches = (uint32_t)K;
+    v.b_msg = e->b_msg.as<uint32_t>(); v.b_pstart = e->b_pstart.as<uint32_t>();
+    v.b_rep_off = e->b_rep_off.as<uint64_t>(); v.b_rep = e->b_rep.as<uint32_t>();
+    v.b_chosen = e->b_chosen.as<uint32_t>();
+    v.cf_off = e->cf_off.as<uint64_t>(); v.cfrags = e->cfrags.as<Frag>();
+    TRY(finish_view(e));
+    for (auto &ns : e->nodes) ns.clear();
+    e->vt.clear();
+    e->vt.synthetic_clean = true;
+    e->device_trace = true;
+    e->dirty = false;
+    e->stats.ingest_ns = now_ns() - t0;
+    return MPX_OK;
+}
+
+// Host copies of the device-generated headers, for drain / dump (small traces).
+static int ensure_host_headers(mpx_engine *e)
+{
+    if (!e->device_trace || e->ht.m_type.size() == e->num_msgs) return MPX_OK;
+    HostTrace &h = e->ht;
+    const size_t G = e->num_msgs;
+    TRY(d2h(h.m_type, e->m_type, G)); TRY(d2h(h.m_src, e->m_src, G));
+    TRY(d2h(h.m_ballot, e->m_ballot, G)); TRY(d2h(h.m_aux, e->m_aux, G));
+    TRY(d2h(h.m_node, e->m_node, G));
+    TRY(d2h(h.b_msg, e->b_msg, e->view.num_batches));
+    return MPX_OK;
 }
 
 // ------------------------------------------------------------------- RCCL --
@@ -736,8 +852,7 @@ extern "C" int mpx_allgather_summary(mpx_engine *e, uint64_t *out)
     if (!e->summary.p) return MPX_E_STATE;
     HTRY(hipSetDevice(e->device));
     if (e->comm) {
-        if (ncclAllGather(e->summary.p, e->gather_buf.p, 64, ncclUint64, e->comm, e->stream) != ncclSuccess)
-            return MPX_E_COMM;
+        // gathered by the last queued run/step
         HTRY(hipMemcpyAsync(out, e->gather_buf.p, 64ull * 8 * e->nranks, hipMemcpyDeviceToHost, e->stream));
     } else {
         HTRY(hipMemcpyAsync(out, e->summary.p, 64 * 8, hipMemcpyDeviceToHost, e->stream));

@@ -169,9 +169,10 @@ MPX_HD inline uint64_t scalar_digest(uint32_t node, uint64_t promised, uint64_t 
 struct LaunchGeom { uint32_t apply_wgs, chosen_wgs; };
 int launch_run(const DevView &v, void *stream, LaunchGeom g, void *ev_begin, void *ev_apply0,
                void *ev_apply1, void *ev_end);
-int launch_gen_clean(const DevView &v, void *stream, uint64_t M, uint32_t batch, uint32_t N,
-                     uint64_t *m_ballot_w, uint8_t *m_type_w, uint32_t *m_src_w, uint64_t *m_aux_w,
-                     uint64_t *m_ent_w, uint32_t *m_cnt_w, uint32_t *m_node_w, uint64_t *e_val_w,
-                     Frag *frags_w, Frag *cfrags_w, uint32_t *b_rep_w);
+int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
+                     uint64_t G0, uint64_t G1, uint64_t E0, uint64_t ballot, uint32_t NB,
+                     uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,
+                     uint32_t *node, uint64_t *e_val, Frag *frags, uint64_t *f_off, uint32_t *b_msg,
+                     uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep, uint64_t *cf_off, Frag *cfrags);
 
 }  // namespace mpx

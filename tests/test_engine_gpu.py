@@ -101,3 +101,59 @@ def test_repeated_runs_are_identical():
         assert e.dump() == d1
     for k in ("chosen", "state_digest", "chosen_digest", "accept_apps"):
         assert a[k] == b[k]
+
+
+@pytest.mark.parametrize("n,m", [(5, 4096), (9, 256 * 37), (2, 256)])
+def test_device_generator_matches_host(n, m):
+    """The HBM-materialised clean trace (mpx_load_clean_device) gives the same
+    result bytes as the host trace through mpx_submit, and the oracle's."""
+    t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=256)
+    want, ostats, _ = oracle_run(t)
+    with mpx.Engine(n, 0, m) as e:
+        e.load_clean_device(num_instances=m)
+        st = e.run()
+        got = e.dump()
+    assert got == want, mpxr.diff(got, want)
+    assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
+            st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
+
+
+@pytest.mark.parametrize("shards", [2, 3, 8])
+def test_sharded_device_generator_sums_to_whole(shards):
+    """Instance sharding: per-shard counters and digests add
+    up to the single-engine run; per-acceptor scalars agree on every shard."""
+    n, m = 9, 256 * 64
+    with mpx.Engine(n, 0, m) as e:
+        e.load_clean_device(num_instances=m)
+        whole = e.run()
+    per = m // shards // 256 * 256
+    bounds = [(i * per, m if i == shards - 1 else (i + 1) * per) for i in range(shards)]
+    tot = {k: 0 for k in ("chosen", "accept_apps", "commit_apps", "chosen_digest", "state_digest")}
+    for sb, se in bounds:
+        with mpx.Engine(n, sb, se) as e:
+            e.load_clean_device(num_instances=m)
+            st = e.run()
+            assert st["scalar_digest"] == whole["scalar_digest"]
+            for k in tot:
+                tot[k] = (tot[k] + st[k]) % (1 << 64)
+            ch = e.read_chosen(sb, se - sb)
+            assert ch == [mpx.PRESENT | (i + 1) for i in range(sb, se)]
+    for k in tot:
+        assert tot[k] == whole[k] % (1 << 64), k
+
+
+def test_host_sharded_ingest_matches_oracle_restricted():
+    """Host ingest with a shard: state / chosen entries equal the oracle's, restricted to the shard."""
+    name = "fuzz_big_1"
+    trace = _read(name, ".mpxt")
+    full = mpxr.parse(_read(name, ".mpxr"))
+    n = len(full["nodes"])
+    sb, se = 64, 150
+    with mpx.Engine(n, sb, se) as e:
+        e.submit_trace(trace)
+        e.run()
+        part = mpxr.parse(e.dump())
+    for a, b in zip(part["nodes"], full["nodes"]):
+        assert a["state"] == [s for s in b["state"] if sb <= s[0] < se]
+        assert (a["promised"], a["max_seen"]) == (b["promised"], b["max_seen"])
+    assert part["chosen"] == [c for c in full["chosen"] if sb <= c[0] < se]
