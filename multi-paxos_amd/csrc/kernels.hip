@@ -210,6 +210,26 @@ __global__ void k_votes(DevView v)
 }
 
 // ------------------------------------------------------------- apply ----
+// Wave-level helpers: descriptors are loaded one per lane and then broadcast
+// with v_readlane, so one (node, bucket) pair costs three dependent memory
+// round trips — (1) CSR offsets, (2) fragment / event descriptors, (3) the
+// scan's per-message flags + the entry values — and (1) of the next pair is
+// already in flight while the current one is processed.
+__device__ inline uint64_t rl64(uint64_t x, uint32_t i)
+{
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, i);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), i);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint32_t rl32(uint32_t x, uint32_t i) { return __builtin_amdgcn_readlane(x, i); }
+__device__ inline void wave_lds_fence()
+{
+    // LDS instructions of one wave execute in order; keep the compiler from
+    // reordering the scatter / gather around this point
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __device__ inline void emit(const DevView &v, bool want, uint32_t msg, uint32_t kind, uint64_t iid,
                             uint64_t ballot, uint64_t handle)
 {
@@ -217,9 +237,10 @@ __device__ inline void emit(const DevView &v, bool want, uint32_t msg, uint32_t 
     if (!m) return;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
+    const uint32_t first = (uint32_t)(__ffsll((long long)m) - 1);
     unsigned long long base = 0;
-    if (lane == (uint32_t)(__ffsll((long long)m) - 1)) base = atomicAdd(v.out_cursor, (unsigned long long)__popcll(m));
-    base = __shfl(base, __ffsll((long long)m) - 1, 64);
+    if (lane == first) base = atomicAdd(v.out_cursor, (unsigned long long)__popcll(m));
+    base = __shfl(base, first, 64);
     if (want && base + rank < v.out_cap) {
         OutRec r;
         r.msg = msg; r.kind = kind; r.iid = iid; r.ballot = ballot; r.handle = handle;
@@ -227,195 +248,329 @@ __device__ inline void emit(const DevView &v, bool want, uint32_t msg, uint32_t 
     }
 }
 
-// A workgroup owns one (node, bucket) pair at a time, one thread per instance
-// slot; the pair's fragments and the node's snapshot events are walked in
-// message order, so every instance sees its events in the reference's order.
+constexpr uint32_t SPL = BS / 64;
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));          // slots per lane: slot = lane + 64 * j
+
+// slots of this lane that fragment (start, count, dense) covers: k[j] = entry
+// offset within the fragment or -1.  Sparse runs scatter through the wave's
+// own LDS row.
+__device__ inline void frag_slots(uint16_t *lidx, const uint8_t *slots, uint64_t entry, uint32_t count,
+                                  uint32_t start, bool dense, int (&k)[SPL])
+{
+    const uint32_t lane = threadIdx.x & 63;
+    if (dense) {
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) {
+            const int d = (int)(lane + 64 * j) - (int)start;
+            k[j] = (d >= 0 && d < (int)count) ? d : -1;
+        }
+        return;
+    }
+    for (uint32_t q = lane; q < count; q += 64) lidx[slots[entry + q]] = (uint16_t)q;
+    wave_lds_fence();
+#pragma unroll
+    for (uint32_t j = 0; j < SPL; ++j) {
+        const uint16_t x = lidx[lane + 64 * j];
+        k[j] = x == 0xFFFF ? -1 : (int)x;
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (uint32_t j = 0; j < SPL; ++j) lidx[lane + 64 * j] = 0xFFFF;
+    wave_lds_fence();
+}
+
+// One wave owns one (node, bucket) pair at a time: its 256 instance slots are
+// 4 per lane.  The pair's fragments and the node's snapshot events are walked
+// in message order, so every instance sees its events in the reference's order.
 __global__ __launch_bounds__(256) void k_apply(DevView v)
 {
-    __shared__ uint16_t lidx[256];
+    __shared__ uint16_t lidx_all[4][BS];
+    __shared__ u64x2 pre_all[4][BS];           // pre-accepted merge (pid, PRESENT|handle): rare, kept in LDS
     __shared__ unsigned long long red[4][8];
-    const uint32_t t = threadIdx.x;
-    lidx[t] = 0xFFFF;
-    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint16_t *lidx = lidx_all[wv];
+    u64x2 *pre = pre_all[wv];
+#pragma unroll
+    for (uint32_t j = 0; j < SPL; ++j) lidx[lane + 64 * j] = 0xFFFF;
+    wave_lds_fence();
     unsigned long long cA = 0, cL = 0, cP = 0, cQ = 0, dig = 0;
     const uint64_t npairs = (uint64_t)v.N * v.NB;
-    for (uint64_t p = blockIdx.x; p < npairs; p += gridDim.x) {
+    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    const uint64_t *__restrict__ e_val = v.e_val;
+    const uint64_t *__restrict__ f_off = v.f_off;
+    const uint64_t *__restrict__ ev_off = v.ev_off;
+
+    auto rt1 = [&](uint64_t q) -> uint64_t {
+        if (q >= npairs || lane > 3) return 0;
+        const uint32_t n = (uint32_t)(q / v.NB);
+        return lane < 2 ? f_off[q + lane] : ev_off[n + lane - 2];
+    };
+    uint64_t p = (uint64_t)blockIdx.x * 4 + wv;
+    uint64_t nxt = rt1(p);
+    for (; p < npairs; p += stride) {
         const uint32_t n = (uint32_t)(p / v.NB);
         const uint32_t b = (uint32_t)(p - (uint64_t)n * v.NB);
-        const uint64_t li = ((uint64_t)b << BSH) + t;
-        const bool in = li < v.shard_len;
-        const uint64_t iid = v.shard_begin + li;
-        uint64_t sb = 0, sw = 0, pb = 0, pw = 0;
-        uint64_t fi = v.f_off[p];
-        const uint64_t fe = v.f_off[p + 1];
-        uint64_t ei = v.ev_off[n];
-        const uint64_t ee = v.ev_off[n + 1];
+        uint64_t fi = rl64(nxt, 0), fe = rl64(nxt, 1), ei = rl64(nxt, 2), ee = rl64(nxt, 3);
+        nxt = rt1(p + stride);
+        const uint64_t li0 = (uint64_t)b << BSH;
+        uint64_t sb[SPL], sw[SPL];
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) { sb[j] = sw[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
+
         while (fi < fe || ei < ee) {
-            const uint32_t fm = fi < fe ? v.frags[fi].msg : NONE32;
-            const uint32_t em = ei < ee ? v.ev_msg[ei] : NONE32;
-            if (fm <= em) {
-                const Frag F = v.frags[fi++];
-                const uint32_t kind = F.flags >> 4;
-                const uint8_t fl = v.m_flags[F.msg];
-                int k = -1;
-                if (F.flags & FR_DENSE) {
-                    const int d = (int)t - (int)F.start;
-                    if (d >= 0 && d < (int)F.count) k = d;
+            const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
+            const uint32_t ne = (uint32_t)(ee - ei < 64 ? ee - ei : 64);
+            // (2) descriptors, one per lane
+            uint64_t fw0 = 0, fw1 = NONE32;
+            if (lane < nf) {
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
+                fw0 = x.x; fw1 = x.y;
+            }
+            const uint32_t evm = lane < ne ? v.ev_msg[ei + lane] : NONE32;
+            // (3) scan results for those messages; entry values of the first
+            //     two dense entry fragments (accept + commit of the bucket)
+            const uint32_t fmsg = (uint32_t)fw1;
+            uint32_t fflag = 0;
+            uint64_t fbal = 0;
+            if (lane < nf) { fflag = v.m_flags[fmsg]; fbal = v.m_ballot[fmsg]; }
+            uint32_t einfo = 0;
+            if (lane < ne) einfo = (uint32_t)v.m_type[evm] | ((uint32_t)v.m_flags[evm] << 8);
+            uint64_t pv[2][SPL];
+#pragma unroll
+            for (uint32_t a = 0; a < 2; ++a) {
+                const uint64_t w1 = a < nf ? rl64(fw1, a) : 0;
+                const uint64_t ent = a < nf ? rl64(fw0, a) : 0;
+                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                const uint32_t fl = (uint32_t)(w1 >> 56);
+                const bool pre = a < nf && (fl & FR_DENSE) && (fl >> 4) != K_PREPLY;
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) {
+                    const int d = (int)(lane + 64 * j) - (int)st0;
+                    pv[a][j] = (pre && d >= 0 && d < (int)cnt) ? e_val[ent + d] : 0;
+                }
+            }
+            // merge-walk fragments and events by message index
+            uint32_t a = 0, c = 0;
+            for (;;) {
+                const bool fmore = a < nf, emore = c < ne;
+                if ((!fmore && fi + nf < fe) || (!emore && ei + ne < ee) || (!fmore && !emore)) break;
+                const uint32_t fm = fmore ? rl32(fmsg, a) : NONE32;
+                const uint32_t em = emore ? rl32(evm, c) : NONE32;
+                if (fm <= em) {
+                    const uint64_t ent = rl64(fw0, a), w1 = rl64(fw1, a);
+                    const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                    const uint32_t fl = (uint32_t)(w1 >> 56), kind = fl >> 4;
+                    const uint32_t mf = rl32(fflag, a);
+                    const uint64_t ballot = rl64(fbal, a);
+                    const bool dense = fl & FR_DENSE;
+                    int k[SPL];
+                    frag_slots(lidx, kind == K_PREPLY ? v.r_slot : v.e_slot, ent, cnt, st0, dense, k);
+                    uint64_t val[SPL];
+                    if (kind != K_PREPLY && dense && a < 2) {
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) val[j] = a == 0 ? pv[0][j] : pv[1][j];
+                    } else {
+                        const uint64_t *src = kind == K_PREPLY ? v.r_val : e_val;
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) val[j] = k[j] >= 0 ? src[ent + k[j]] : 0;
+                    }
+                    if (kind == K_ACCEPT) {
+                        if (mf & F_GRANTED) {
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j)
+                                if (k[j] >= 0 && !(sw[j] & W_COMMITTED)) {           // :1380
+                                    sb[j] = ballot;                                   // :1387
+                                    sw[j] = W_PRESENT | val[j];
+                                    ++cA;
+                                }
+                        }
+                    } else if (kind == K_COMMIT) {
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j)
+                            if (k[j] >= 0) {
+                                if (sw[j] & W_COMMITTED) {                            // :1508
+                                    if ((sw[j] & W_HANDLE) != val[j])
+                                        record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
+                                                         v.shard_begin + li0 + lane + 64 * j);
+                                } else {
+                                    sb[j] = ballot;                                   // :1515
+                                    sw[j] = W_PRESENT | W_COMMITTED | val[j];
+                                }
+                                ++cL;
+                            }
+                    } else if (kind == K_PREPLY) {
+                        if (mf & F_COUNTED) {
+#pragma unroll 1
+                            for (uint32_t j = 0; j < SPL; ++j)
+                                if (k[j] >= 0) {
+                                    const uint64_t pid = v.r_pid[ent + k[j]];
+                                    const u64x2 cur = pre[lane + 64 * j];
+                                    if (!cur.y || pid > cur.x) pre[lane + 64 * j] = u64x2{pid, W_PRESENT | val[j]};   // :1216-1221
+                                }
+                        }
+                    }
+                    ++a;
                 } else {
-                    const uint8_t *slots = kind == K_PREPLY ? v.r_slot : v.e_slot;
-                    if (t < F.count) lidx[slots[F.entry + t]] = (uint16_t)t;
-                    __syncthreads();
-                    k = lidx[t] == 0xFFFF ? -1 : (int)lidx[t];
-                    __syncthreads();
-                    lidx[t] = 0xFFFF;
-                    __syncthreads();
-                }
-                if (kind == K_ACCEPT) {
-                    if ((fl & F_GRANTED) && k >= 0) {
-                        const uint64_t val = v.e_val[F.entry + k];
-                        if (!(sw & W_COMMITTED)) {                          // :1380
-                            sb = v.m_ballot[F.msg];                        // :1387
-                            sw = W_PRESENT | val;
-                            ++cA;
-                        }
-                    }
-                } else if (kind == K_COMMIT) {
-                    if (k >= 0) {
-                        const uint64_t val = v.e_val[F.entry + k];
-                        if (sw & W_COMMITTED) {                             // :1508
-                            if ((sw & W_HANDLE) != val) {
-                                const uint32_t g = F.msg;
-                                record_violation(v, MPX_V_COMMIT_VALUE, n, g - v.node_off[n], iid);
+                    const uint32_t g = em;
+                    const uint32_t info = rl32(einfo, c);
+                    const uint32_t t8 = info & 0xFF, fl = info >> 8;
+                    if (t8 == MPX_MSG_PREPARE) {
+                        bool have = false;
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) have |= (sw[j] & W_PRESENT) != 0;
+                        if ((fl & F_GRANTED) && __ballot(have)) {
+                            // FilterAcceptedValues over the prepare's ranges (:902-922);
+                            // ranges sorted by start and disjoint (ingest)
+                            const uint64_t r0 = v.m_ent[g];
+                            const uint32_t nr = v.m_cnt[g];
+#pragma unroll 1
+                            for (uint32_t j = 0; j < SPL; ++j) {
+                                const uint64_t li = li0 + lane + 64 * j;
+                                const uint64_t iid = v.shard_begin + li;
+                                bool hit = false;
+                                if (nr && li < v.shard_len && (sw[j] & W_PRESENT)) {
+                                    uint32_t lo = 0, hi = nr;       // last range with a <= iid
+                                    while (lo < hi) {
+                                        const uint32_t mid = (lo + hi) >> 1;
+                                        if (v.g_a[r0 + mid] <= iid) lo = mid + 1; else hi = mid;
+                                    }
+                                    hit = lo > 0 && iid < v.g_b[r0 + lo - 1];
+                                }
+                                emit(v, hit, g, 0, iid, sb[j], sw[j] & W_HANDLE);
+                                cP += hit;
                             }
-                        } else {
-                            sb = v.m_ballot[F.msg];                        // :1515
-                            sw = W_PRESENT | W_COMMITTED | val;
                         }
-                        ++cL;
-                    }
-                } else if (kind == K_PREPLY) {
-                    if ((fl & F_COUNTED) && k >= 0) {
-                        const uint64_t pid = v.r_pid[F.entry + k];
-                        const uint64_t val = v.r_val[F.entry + k];
-                        if (!pw || pid > pb) { pb = pid; pw = W_PRESENT | val; }   // :1216-1221
-                    }
-                }
-            } else {
-                const uint32_t g = em;
-                ++ei;
-                const uint8_t t8 = v.m_type[g];
-                const uint8_t fl = v.m_flags[g];
-                if (t8 == MPX_MSG_PREPARE) {
-                    if (fl & F_GRANTED) {
-                        // FilterAcceptedValues over the prepare's ranges (:902-922);
-                        // ranges are sorted by start and disjoint (ingest)
-                        const uint64_t r0 = v.m_ent[g];
-                        const uint32_t nr = v.m_cnt[g];
-                        bool hit = false;
-                        if (nr && in && (sw & W_PRESENT)) {
-                            uint32_t lo = 0, hi = nr;          // last range with a <= iid
-                            while (lo < hi) {
-                                const uint32_t mid = (lo + hi) >> 1;
-                                if (v.g_a[r0 + mid] <= iid) lo = mid + 1; else hi = mid;
-                            }
-                            hit = lo > 0 && iid < v.g_b[r0 + lo - 1];
+                    } else if (t8 == MPX_MSG_P_START) {
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) pre[lane + 64 * j] = u64x2{0, 0};
+                    } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
+#pragma unroll 1
+                        for (uint32_t j = 0; j < SPL; ++j) {
+                            const uint64_t li = li0 + lane + 64 * j;
+                            const u64x2 cur = pre[lane + 64 * j];
+                            const bool hit = li < v.shard_len && cur.y;
+                            emit(v, hit, g, 1, v.shard_begin + li, cur.x, cur.y & W_HANDLE);
+                            cQ += hit;
+                            pre[lane + 64 * j] = u64x2{0, 0};                        // :1105
                         }
-                        emit(v, hit, g, 0, iid, sb, sw & W_HANDLE);
-                        cP += hit;
                     }
-                } else if (t8 == MPX_MSG_P_START) {
-                    pb = pw = 0;
-                } else if (t8 == MPX_MSG_PREPARE_REPLY) {
-                    if (fl & F_QUORUM) {
-                        const bool hit = in && pw;
-                        emit(v, hit, g, 1, iid, pb, pw & W_HANDLE);
-                        cQ += hit;
-                        pb = pw = 0;                                  // :1105
-                    }
+                    ++c;
                 }
             }
+            fi += a;
+            ei += c;
         }
-        const int any = __syncthreads_or(sw != 0);
-        if (any) {
-            if (in) {
-                uint64_t *s = v.st + 2 * ((uint64_t)n * v.shard_len + li);
-                *reinterpret_cast<ulonglong2 *>(s) = make_ulonglong2(sb, sw);
+        bool have = false;
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) have |= sw[j] != 0;
+        if (__ballot(have)) {
+#pragma unroll
+            for (uint32_t j = 0; j < SPL; ++j) {
+                const uint64_t li = li0 + lane + 64 * j;
+                if (li < v.shard_len) {
+                    uint64_t *s = v.st + 2 * ((uint64_t)n * v.shard_len + li);
+                    u64x2 w; w.x = sb[j]; w.y = sw[j];
+                    __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(s));
+                }
+                if (sw[j])
+                    dig += state_digest(n, v.shard_begin + li, (sw[j] & W_COMMITTED) ? 2 : 1, sb[j], sw[j] & W_HANDLE);
             }
-            if (t == 0) v.st_valid[p] = 1;
-            if (sw) dig += state_digest(n, iid, (sw & W_COMMITTED) ? 2 : 1, sb, sw & W_HANDLE);
+            if (lane == 0) v.st_valid[p] = 1;
         }
     }
     // workgroup reduction of the counters
-    unsigned long long c[5] = {cA, cL, cP, cQ, dig};
+    unsigned long long cc[5] = {cA, cL, cP, cQ, dig};
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-        unsigned long long x = c[i];
+        unsigned long long x = cc[i];
         for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-        c[i] = x;
+        cc[i] = x;
     }
-    if ((t & 63) == 0) {
+    if (lane == 0) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) red[t >> 6][i] = c[i];
+        for (int i = 0; i < 5; ++i) red[wv][i] = cc[i];
     }
     __syncthreads();
-    if (t < 5) {
+    if (threadIdx.x < 5) {
+        const uint32_t t = threadIdx.x;
         unsigned long long s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         const int slot = t == 0 ? PC_A : t == 1 ? PC_L : t == 2 ? PC_P : t == 3 ? PC_Q : PC_DSTATE;
         v.partials[8 * blockIdx.x + slot] = s;
     }
 }
 
-// Chosen log per bucket: every batch whose votes reached quorum contributes
-// its instances; the first one wins, later ones must agree (safety).
+// Chosen log, one wave per bucket: every batch whose votes reached quorum
+// contributes its instances; the first one wins, later ones must agree (safety).
 __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base)
 {
-    __shared__ uint16_t lidx[256];
+    __shared__ uint16_t lidx_all[4][BS];
     __shared__ unsigned long long red[4][2];
-    const uint32_t t = threadIdx.x;
-    lidx[t] = 0xFFFF;
-    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint16_t *lidx = lidx_all[wv];
+#pragma unroll
+    for (uint32_t j = 0; j < SPL; ++j) lidx[lane + 64 * j] = 0xFFFF;
+    wave_lds_fence();
     unsigned long long cC = 0, dig = 0;
-    for (uint64_t b = blockIdx.x; b < v.NB; b += gridDim.x) {
-        const uint64_t li = (b << BSH) + t;
-        const uint64_t iid = v.shard_begin + li;
-        uint64_t cv = 0;
-        for (uint64_t f = v.cf_off[b]; f < v.cf_off[b + 1]; ++f) {
-            const Frag F = v.cfrags[f];
-            const bool live = v.b_chosen[F.msg] != NONE32;
-            int k = -1;
-            if (F.flags & FR_DENSE) {
-                const int d = (int)t - (int)F.start;
-                if (d >= 0 && d < (int)F.count) k = d;
-            } else {
-                if (t < F.count) lidx[v.e_slot[F.entry + t]] = (uint16_t)t;
-                __syncthreads();
-                k = lidx[t] == 0xFFFF ? -1 : (int)lidx[t];
-                __syncthreads();
-                lidx[t] = 0xFFFF;
-                __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    for (uint64_t b = (uint64_t)blockIdx.x * 4 + wv; b < v.NB; b += stride) {
+        const uint64_t li0 = b << BSH;
+        uint64_t off = lane < 2 ? v.cf_off[b + lane] : 0;
+        uint64_t fi = rl64(off, 0);
+        const uint64_t fe = rl64(off, 1);
+        uint64_t cv[SPL];
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) cv[j] = 0;
+        while (fi < fe) {
+            const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
+            uint64_t fw0 = 0, fw1 = 0;
+            if (lane < nf) {
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.cfrags + fi + lane);
+                fw0 = x.x; fw1 = x.y;
             }
-            if (live && k >= 0) {
-                const uint64_t val = v.e_val[F.entry + k];
-                if (!cv) { cv = W_PRESENT | val; ++cC; dig += chosen_digest(iid, val); }
-                else if ((cv & W_HANDLE) != val) record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, iid);
+            const uint32_t live = lane < nf ? (v.b_chosen[(uint32_t)fw1] != NONE32) : 0;
+            for (uint32_t a = 0; a < nf; ++a) {
+                if (!rl32(live, a)) continue;
+                const uint64_t ent = rl64(fw0, a), w1 = rl64(fw1, a);
+                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                const bool dense = (w1 >> 56) & FR_DENSE;
+                int k[SPL];
+                frag_slots(lidx, v.e_slot, ent, cnt, st0, dense, k);
+                uint64_t val[SPL];
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) val[j] = k[j] >= 0 ? v.e_val[ent + k[j]] : 0;
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) {
+                    if (k[j] < 0) continue;
+                    const uint64_t iid = v.shard_begin + li0 + lane + 64 * j;
+                    if (!cv[j]) { cv[j] = W_PRESENT | val[j]; ++cC; dig += chosen_digest(iid, val[j]); }
+                    else if ((cv[j] & W_HANDLE) != val[j]) record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, iid);
+                }
             }
+            fi += nf;
         }
-        const int any = __syncthreads_or(cv != 0);
-        if (any) {
-            if (li < v.shard_len) v.chosen[li] = cv;
-            if (t == 0) v.chosen_valid[b] = 1;
+        bool have = false;
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) have |= cv[j] != 0;
+        if (__ballot(have)) {
+#pragma unroll
+            for (uint32_t j = 0; j < SPL; ++j) {
+                const uint64_t li = li0 + lane + 64 * j;
+                if (li < v.shard_len) __builtin_nontemporal_store(cv[j], v.chosen + li);
+            }
+            if (lane == 0) v.chosen_valid[b] = 1;
         }
     }
-    unsigned long long c[2] = {cC, dig};
+    unsigned long long cc[2] = {cC, dig};
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        unsigned long long x = c[i];
+        unsigned long long x = cc[i];
         for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-        c[i] = x;
+        cc[i] = x;
     }
-    if ((t & 63) == 0) { red[t >> 6][0] = c[0]; red[t >> 6][1] = c[1]; }
+    if (lane == 0) { red[wv][0] = cc[0]; red[wv][1] = cc[1]; }
     __syncthreads();
-    if (t < 2) {
+    if (threadIdx.x < 2) {
+        const uint32_t t = threadIdx.x;
         unsigned long long s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         v.partials[8 * (partial_base + blockIdx.x) + (t == 0 ? PC_C : PC_DCHOSEN)] = s;
     }
