@@ -70,7 +70,7 @@ struct mpx_engine {
     uint64_t shard_len = 0;
     uint32_t NB = 0;
     // device buffers
-    DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, m_flags, m_maxseen;
+    DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, n_after_prepare, m_flags, m_maxseen;
     DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
     DevBuf f_off, frags, ev_off, ev_msg, pl_off, pl_msg;
@@ -211,9 +211,12 @@ static int finish_view(mpx_engine *e)
     TRY(e->chosen.alloc(e->shard_len * 8));
     TRY(e->chosen_valid.alloc(e->NB));
     const uint64_t npairs = (uint64_t)N * e->NB;
-    e->geom.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npairs, (uint64_t)e->num_cus * 8));
+    // resident grid: k_apply_fast holds 5 waves/SIMD (94 VGPRs) = 5 workgroups
+    // of 4 waves per CU; a grid matched to residency measured best (ab_apply.py)
+    e->geom.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npairs, (uint64_t)e->num_cus * 5));
     e->geom.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 4));
-    TRY(e->partials.alloc(8ull * 8 * (e->geom.apply_wgs + e->geom.chosen_wgs)));
+
+    TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + e->geom.chosen_wgs)));
     TRY(e->viol.alloc(sizeof(DevViolation)));
     TRY(e->summary.alloc(64 * 8));
     TRY(e->out_cursor.alloc(8));
@@ -244,6 +247,7 @@ static int upload_trace(mpx_engine *e)
     TRY(upload(e->m_ballot, h.m_ballot, s)); TRY(upload(e->m_aux, h.m_aux, s));
     TRY(upload(e->m_ent, h.m_ent, s)); TRY(upload(e->m_cnt, h.m_cnt, s));
     TRY(upload(e->m_node, h.m_node, s)); TRY(upload(e->node_off, h.node_off, s));
+    TRY(upload(e->n_after_prepare, h.n_after_prepare, s));
     TRY(e->m_flags.alloc(std::max<size_t>(h.m_type.size(), 8)));
     TRY(e->m_maxseen.alloc(std::max<size_t>(h.m_type.size() * 8, 8)));
     TRY(upload(e->chunk_node, h.chunk_node, s)); TRY(upload(e->chunk_beg, h.chunk_beg, s));
@@ -266,6 +270,7 @@ static int upload_trace(mpx_engine *e)
     v.m_ballot = e->m_ballot.as<uint64_t>(); v.m_aux = e->m_aux.as<uint64_t>();
     v.m_ent = e->m_ent.as<uint64_t>(); v.m_cnt = e->m_cnt.as<uint32_t>();
     v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
+    v.n_after_prepare = e->n_after_prepare.as<uint32_t>();
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
     v.num_chunks = (uint32_t)h.chunk_node.size();
     v.chunk_node = e->chunk_node.as<uint32_t>(); v.chunk_beg = e->chunk_beg.as<uint64_t>();
@@ -306,7 +311,16 @@ static int queue_run(mpx_engine *e)
     if (e->dirty && !e->device_trace) TRY(upload_trace(e));
     StepEvents *ev = next_events(e);
     if (!ev) return MPX_E_HIP;
-    int rc = launch_run(e->view, e->stream, e->geom, ev->e[0], ev->e[1], ev->e[2], ev->e[3]);
+    // k_apply build variant / grid for A/B measurements (tools/ab_apply.py);
+    // the defaults are the measured best
+    LaunchGeom g = e->geom;
+    if (const char *x = std::getenv("MPX_APPLY_VARIANT")) g.variant = (uint32_t)std::atoi(x);
+    if (const char *x = std::getenv("MPX_APPLY_WGS_PER_CU")) {
+        const uint64_t np = (uint64_t)e->cfg.num_nodes * e->NB;
+        g.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(np, (uint64_t)e->num_cus * std::atoi(x)));
+        if (g.apply_wgs > e->num_cus * 16) g.apply_wgs = e->num_cus * 16;   // partials are sized for 16 per CU
+    }
+    int rc = launch_run(e->view, e->stream, g, ev->e[0], ev->e[1], ev->e[2], ev->e[3]);
     if (rc) return MPX_E_HIP;
     // the one cross-GPU exchange: every rank's 64-word summary, over RCCL on
     // the same stream, no host synchronisation
@@ -740,6 +754,8 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     }
     h.node_chunk_off[N] = (uint32_t)h.chunk_node.size();
     h.g_a.assign(N, 0); h.g_b.assign(N, ~0ull);
+    h.n_after_prepare.resize(N);
+    for (uint32_t n = 0; n < N; ++n) h.n_after_prepare[n] = (uint32_t)(n == 0 ? 2 : h.node_off[n] + 1);
     h.ev_off.assign(N + 1, 0); h.pl_off.assign(N + 1, 0);
     for (uint32_t k = 0; k < N + 2; ++k) h.ev_msg.push_back(k);
     h.pl_msg.push_back(0);
@@ -755,6 +771,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     TRY(e->m_ent.alloc(8 * G)); TRY(e->m_cnt.alloc(4 * G)); TRY(e->m_node.alloc(4 * G));
     TRY(e->m_flags.alloc(G)); TRY(e->m_maxseen.alloc(8 * G));
     TRY(upload(e->node_off, h.node_off, s));
+    TRY(upload(e->n_after_prepare, h.n_after_prepare, s));
     TRY(upload(e->chunk_node, h.chunk_node, s)); TRY(upload(e->chunk_beg, h.chunk_beg, s));
     TRY(upload(e->chunk_end, h.chunk_end, s)); TRY(upload(e->node_chunk_off, h.node_chunk_off, s));
     TRY(e->chunk_agg.alloc(std::max<size_t>(16 * h.chunk_node.size(), 16)));
@@ -783,6 +800,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.m_ballot = e->m_ballot.as<uint64_t>(); v.m_aux = e->m_aux.as<uint64_t>();
     v.m_ent = e->m_ent.as<uint64_t>(); v.m_cnt = e->m_cnt.as<uint32_t>();
     v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
+    v.n_after_prepare = e->n_after_prepare.as<uint32_t>();
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
     v.num_chunks = (uint32_t)h.chunk_node.size();
     v.chunk_node = e->chunk_node.as<uint32_t>(); v.chunk_beg = e->chunk_beg.as<uint64_t>();

@@ -331,6 +331,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     ht.e_val.reserve(E); ht.e_iid.reserve(E); ht.r_pid.reserve(R); ht.r_val.reserve(R); ht.r_iid.reserve(R);
     ht.g_a.reserve(GR); ht.g_b.reserve(GR);
     ht.node_off.assign(N + 1, 0);
+    ht.n_after_prepare.assign(N, 0);
 
     struct FragKey { uint64_t key; Frag f; };
     std::vector<uint64_t> fcount(N * NB + 1, 0), cfcount(NB + 1, 0);
@@ -365,6 +366,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             ht.m_cnt.push_back(ns.cnt[k]);
             ht.m_node.push_back(n);
             if (t == MPX_MSG_PREPARE || t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START) { ev.push_back(g); ev_cnt[n]++; }
+            if (t == MPX_MSG_PREPARE) ht.n_after_prepare[n] = g + 1;
             if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START) { pl.push_back(g); pl_cnt[n]++; }
             if (t == MPX_MSG_P_START) pstart = g;
             if (t == MPX_MSG_P_BATCH) {

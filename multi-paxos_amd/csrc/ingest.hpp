@@ -48,6 +48,7 @@ struct HostTrace {
     std::vector<uint32_t> m_src, m_cnt, m_node;
     std::vector<uint64_t> m_ballot, m_aux, m_ent;
     std::vector<uint64_t> node_off;
+    std::vector<uint32_t> n_after_prepare;          // 1 + global index of the node's last PREPARE, 0: none
     std::vector<uint32_t> chunk_node, node_chunk_off;
     std::vector<uint64_t> chunk_beg, chunk_end;
     std::vector<uint64_t> e_val, e_iid, r_pid, r_val, r_iid, g_a, g_b;

@@ -282,7 +282,167 @@ __device__ inline void frag_slots(uint16_t *lidx, const uint8_t *slots, uint64_t
 // One wave owns one (node, bucket) pair at a time: its 256 instance slots are
 // 4 per lane.  The pair's fragments and the node's snapshot events are walked
 // in message order, so every instance sees its events in the reference's order.
-__global__ __launch_bounds__(256) void k_apply(DevView v)
+// Fast-path predicate, evaluated identically by both apply kernels so every
+// (node, bucket) pair is processed exactly once: all fragments are dense
+// ACCEPT / COMMIT runs (fit one 64-descriptor window) and the node has no
+// PREPARE after the pair's first fragment.  Such a pair never emits: its
+// snapshots see empty state and it has no pre-accepted merge, so the events
+// can be skipped without changing any output.
+__device__ inline bool pair_is_fast(const DevView &v, uint32_t n, uint64_t nfrag, uint64_t fw1)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    if (nfrag == 0 || nfrag > 64) return false;
+    const uint32_t fl = (uint32_t)(fw1 >> 56);
+    const bool ok = lane >= nfrag || ((fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT));
+    const uint32_t first_msg = rl32((uint32_t)fw1, 0);
+    return __ballot(!ok) == 0 && first_msg >= v.n_after_prepare[n];
+}
+
+// Lean acceptor/learner apply for fast pairs: one wave per pair, slots
+// {2l, 2l+1, 128+2l, 129+2l} of lane l so full 256-entry runs move with
+// 16-byte loads and stores.  Values of two fragments are loaded before either
+// is applied, so a bucket's accept + commit cost one memory round trip.
+__device__ inline void fast_load(const uint64_t *__restrict__ e_val, uint64_t ent, uint64_t w1, bool skip,
+                                 uint32_t lane, uint64_t &v0, uint64_t &v1, uint64_t &v2, uint64_t &v3, uint32_t &inm)
+{
+    const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+    inm = 0;
+    v0 = v1 = v2 = v3 = 0;
+    if (skip) return;
+    if (st0 == 0 && cnt == BS && !(ent & 1)) {
+        const u64x2 x0 = *reinterpret_cast<const u64x2 *>(e_val + ent + 2 * lane);
+        const u64x2 x1 = *reinterpret_cast<const u64x2 *>(e_val + ent + 128 + 2 * lane);
+        v0 = x0.x; v1 = x0.y; v2 = x1.x; v3 = x1.y;
+        inm = 0xF;
+        return;
+    }
+    const int d0 = (int)(2 * lane) - (int)st0;
+    const int d2 = (int)(128 + 2 * lane) - (int)st0;
+    if (d0 >= 0 && d0 < (int)cnt) { v0 = e_val[ent + d0]; inm |= 1; }
+    if (d0 + 1 >= 0 && d0 + 1 < (int)cnt) { v1 = e_val[ent + d0 + 1]; inm |= 2; }
+    if (d2 >= 0 && d2 < (int)cnt) { v2 = e_val[ent + d2]; inm |= 4; }
+    if (d2 + 1 >= 0 && d2 + 1 < (int)cnt) { v3 = e_val[ent + d2 + 1]; inm |= 8; }
+}
+
+// apply one fragment's values to one slot; returns 1 on a re-commit with another Value
+__device__ inline uint32_t fast_apply(bool commit, uint64_t ballot, uint64_t val, bool in, uint64_t &sb, uint64_t &sw,
+                                      uint32_t &cA, uint32_t &cL)
+{
+    if (!in) return 0;
+    if (!commit) {
+        if (!(sw & W_COMMITTED)) { sb = ballot; sw = W_PRESENT | val; ++cA; }         // :1380-1387
+        return 0;
+    }
+    ++cL;
+    if (sw & W_COMMITTED) return (sw & W_HANDLE) != val;                               // :1508
+    sb = ballot; sw = W_PRESENT | W_COMMITTED | val;                                   // :1515
+    return 0;
+}
+
+template <int WAVES_PER_EU>
+__global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
+{
+    __shared__ unsigned long long red[4][4];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t cA = 0, cL = 0;
+    unsigned long long dig = 0;
+    const uint64_t npairs = (uint64_t)v.N * v.NB;
+    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    const uint64_t *__restrict__ e_val = v.e_val;
+    uint64_t p = (uint64_t)blockIdx.x * 4 + wv;
+    // software pipeline: CSR offsets two pairs ahead, descriptors one ahead
+    uint64_t off_cur = (p < npairs && lane < 2) ? v.f_off[p + lane] : 0;
+    uint64_t off_nxt = (p + stride < npairs && lane < 2) ? v.f_off[p + stride + lane] : 0;
+    uint64_t nw0 = 0, nw1 = NONE32;
+    {
+        const uint64_t fi = rl64(off_cur, 0), fe = rl64(off_cur, 1);
+        if (lane < fe - fi && lane < 64) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
+            nw0 = x.x; nw1 = x.y;
+        }
+    }
+    for (; p < npairs; p += stride) {
+        const uint32_t n = (uint32_t)(p / v.NB);
+        const uint32_t b = (uint32_t)(p - (uint64_t)n * v.NB);
+        const uint64_t nfrag = rl64(off_cur, 1) - rl64(off_cur, 0);
+        const uint64_t fw0 = nw0, fw1 = nw1;
+        {
+            const uint64_t fi = rl64(off_nxt, 0), fe = rl64(off_nxt, 1);
+            nw0 = 0; nw1 = NONE32;
+            if (lane < fe - fi && lane < 64) {
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
+                nw0 = x.x; nw1 = x.y;
+            }
+        }
+        off_cur = off_nxt;
+        off_nxt = (p + 2 * stride < npairs && lane < 2) ? v.f_off[p + 2 * stride + lane] : 0;
+        if (!pair_is_fast(v, n, nfrag, fw1)) continue;
+        const uint32_t fmsg = (uint32_t)fw1;
+        const uint32_t fflag = lane < nfrag ? v.m_flags[fmsg] : 0;
+        const uint64_t fbal = lane < nfrag ? v.m_ballot[fmsg] : 0;
+        uint64_t sb0 = 0, sb1 = 0, sb2 = 0, sb3 = 0, sw0 = 0, sw1 = 0, sw2 = 0, sw3 = 0;
+        uint32_t bad = 0;
+        for (uint32_t a = 0; a < (uint32_t)nfrag; a += 2) {
+            const bool two = a + 1 < (uint32_t)nfrag;
+            const uint64_t wa = rl64(fw1, a), wb = two ? rl64(fw1, a + 1) : 0;
+            const bool ca = (wa >> 60) == K_COMMIT, cb = (wb >> 60) == K_COMMIT;
+            const bool ska = !ca && !(rl32(fflag, a) & F_GRANTED);
+            const bool skb = !two || (!cb && !(rl32(fflag, a + 1) & F_GRANTED));
+            uint64_t a0, a1, a2, a3, b0, b1, b2, b3;
+            uint32_t ma, mb;
+            fast_load(e_val, rl64(fw0, a), wa, ska, lane, a0, a1, a2, a3, ma);
+            fast_load(e_val, two ? rl64(fw0, a + 1) : 0, wb, skb, lane, b0, b1, b2, b3, mb);
+            const uint64_t ba = rl64(fbal, a), bb = two ? rl64(fbal, a + 1) : 0;
+            bad |= fast_apply(ca, ba, a0, ma & 1, sb0, sw0, cA, cL);
+            bad |= fast_apply(ca, ba, a1, ma & 2, sb1, sw1, cA, cL);
+            bad |= fast_apply(ca, ba, a2, ma & 4, sb2, sw2, cA, cL);
+            bad |= fast_apply(ca, ba, a3, ma & 8, sb3, sw3, cA, cL);
+            bad |= fast_apply(cb, bb, b0, mb & 1, sb0, sw0, cA, cL);
+            bad |= fast_apply(cb, bb, b1, mb & 2, sb1, sw1, cA, cL);
+            bad |= fast_apply(cb, bb, b2, mb & 4, sb2, sw2, cA, cL);
+            bad |= fast_apply(cb, bb, b3, mb & 8, sb3, sw3, cA, cL);
+        }
+        const uint64_t li0 = (uint64_t)b << BSH;
+        if (bad) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, v.shard_begin + li0);
+        uint64_t *srow = v.st + 2 * ((uint64_t)n * v.shard_len + li0);
+        const uint32_t s0 = 2 * lane, s2 = 128 + 2 * lane;
+        u64x2 w;
+        if (li0 + BS <= v.shard_len) {
+            w.x = sb0; w.y = sw0; __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(srow + 2 * s0));
+            w.x = sb1; w.y = sw1; __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(srow + 2 * s0 + 2));
+            w.x = sb2; w.y = sw2; __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(srow + 2 * s2));
+            w.x = sb3; w.y = sw3; __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(srow + 2 * s2 + 2));
+        } else {
+            if (li0 + s0 < v.shard_len) { w.x = sb0; w.y = sw0; *reinterpret_cast<u64x2 *>(srow + 2 * s0) = w; }
+            if (li0 + s0 + 1 < v.shard_len) { w.x = sb1; w.y = sw1; *reinterpret_cast<u64x2 *>(srow + 2 * s0 + 2) = w; }
+            if (li0 + s2 < v.shard_len) { w.x = sb2; w.y = sw2; *reinterpret_cast<u64x2 *>(srow + 2 * s2) = w; }
+            if (li0 + s2 + 1 < v.shard_len) { w.x = sb3; w.y = sw3; *reinterpret_cast<u64x2 *>(srow + 2 * s2 + 2) = w; }
+        }
+        const uint64_t ib = v.shard_begin + li0;
+        if (sw0) dig += state_digest(n, ib + s0, (sw0 & W_COMMITTED) ? 2 : 1, sb0, sw0 & W_HANDLE);
+        if (sw1) dig += state_digest(n, ib + s0 + 1, (sw1 & W_COMMITTED) ? 2 : 1, sb1, sw1 & W_HANDLE);
+        if (sw2) dig += state_digest(n, ib + s2, (sw2 & W_COMMITTED) ? 2 : 1, sb2, sw2 & W_HANDLE);
+        if (sw3) dig += state_digest(n, ib + s2 + 1, (sw3 & W_COMMITTED) ? 2 : 1, sb3, sw3 & W_HANDLE);
+        if (lane == 0) v.st_valid[p] = 1;
+    }
+    unsigned long long cc[3] = {cA, cL, dig};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        unsigned long long x = cc[i];
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        cc[i] = x;
+    }
+    if (lane == 0) { red[wv][0] = cc[0]; red[wv][1] = cc[1]; red[wv][2] = cc[2]; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const uint32_t t = threadIdx.x;
+        unsigned long long s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+        v.partials[8 * blockIdx.x + (t == 0 ? PC_A : t == 1 ? PC_L : PC_DSTATE)] += s;
+    }
+}
+
+template <int WAVES_PER_EU, bool PREFETCH_VALUES>
+__global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 {
     __shared__ uint16_t lidx_all[4][BS];
     __shared__ u64x2 pre_all[4][BS];           // pre-accepted merge (pid, PRESENT|handle): rare, kept in LDS
@@ -293,7 +453,8 @@ __global__ __launch_bounds__(256) void k_apply(DevView v)
 #pragma unroll
     for (uint32_t j = 0; j < SPL; ++j) lidx[lane + 64 * j] = 0xFFFF;
     wave_lds_fence();
-    unsigned long long cA = 0, cL = 0, cP = 0, cQ = 0, dig = 0;
+    uint32_t cA = 0, cL = 0, cP = 0, cQ = 0;    // per-lane counts stay far below 2^32
+    unsigned long long dig = 0;
     const uint64_t npairs = (uint64_t)v.N * v.NB;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
@@ -305,28 +466,54 @@ __global__ __launch_bounds__(256) void k_apply(DevView v)
         const uint32_t n = (uint32_t)(q / v.NB);
         return lane < 2 ? f_off[q + lane] : ev_off[n + lane - 2];
     };
+    // software pipeline over this wave's pairs p, p+stride, p+2*stride:
+    //   (1) CSR offsets two pairs ahead, (2) first descriptor window one pair
+    //   ahead, (3) flags + entry values of the current pair
+    struct Win { uint64_t fw0, fw1; uint32_t evm; };
+    auto rt2 = [&](uint64_t off) -> Win {
+        Win w{0, NONE32, NONE32};
+        const uint64_t fi = rl64(off, 0), fe = rl64(off, 1), ei = rl64(off, 2), ee = rl64(off, 3);
+        if (lane < fe - fi && lane < 64) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
+            w.fw0 = x.x; w.fw1 = x.y;
+        }
+        if (lane < ee - ei && lane < 64) w.evm = v.ev_msg[ei + lane];
+        return w;
+    };
     uint64_t p = (uint64_t)blockIdx.x * 4 + wv;
-    uint64_t nxt = rt1(p);
+    uint64_t off_cur = rt1(p);
+    uint64_t off_nxt = rt1(p + stride);
+    Win win_nxt = rt2(off_cur);
     for (; p < npairs; p += stride) {
         const uint32_t n = (uint32_t)(p / v.NB);
         const uint32_t b = (uint32_t)(p - (uint64_t)n * v.NB);
-        uint64_t fi = rl64(nxt, 0), fe = rl64(nxt, 1), ei = rl64(nxt, 2), ee = rl64(nxt, 3);
-        nxt = rt1(p + stride);
+        uint64_t fi = rl64(off_cur, 0), fe = rl64(off_cur, 1), ei = rl64(off_cur, 2), ee = rl64(off_cur, 3);
+        Win win = win_nxt;
+        win_nxt = rt2(off_nxt);                  // next pair's descriptors in flight
+        off_cur = off_nxt;
+        off_nxt = rt1(p + 2 * stride);
+        if (fi == fe || pair_is_fast(v, n, fe - fi, win.fw1)) continue;   // empty pairs leave no state
         const uint64_t li0 = (uint64_t)b << BSH;
         uint64_t sb[SPL], sw[SPL];
 #pragma unroll
         for (uint32_t j = 0; j < SPL; ++j) { sb[j] = sw[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
 
+        bool first = true;
         while (fi < fe || ei < ee) {
             const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
             const uint32_t ne = (uint32_t)(ee - ei < 64 ? ee - ei : 64);
-            // (2) descriptors, one per lane
-            uint64_t fw0 = 0, fw1 = NONE32;
-            if (lane < nf) {
-                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
-                fw0 = x.x; fw1 = x.y;
+            // (2) descriptors, one per lane (prefetched for the first window)
+            uint64_t fw0 = win.fw0, fw1 = win.fw1;
+            uint32_t evm = win.evm;
+            if (!first) {
+                fw0 = 0; fw1 = NONE32;
+                if (lane < nf) {
+                    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
+                    fw0 = x.x; fw1 = x.y;
+                }
+                evm = lane < ne ? v.ev_msg[ei + lane] : NONE32;
             }
-            const uint32_t evm = lane < ne ? v.ev_msg[ei + lane] : NONE32;
+            first = false;
             // (3) scan results for those messages; entry values of the first
             //     two dense entry fragments (accept + commit of the bucket)
             const uint32_t fmsg = (uint32_t)fw1;
@@ -342,7 +529,7 @@ __global__ __launch_bounds__(256) void k_apply(DevView v)
                 const uint64_t ent = a < nf ? rl64(fw0, a) : 0;
                 const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
                 const uint32_t fl = (uint32_t)(w1 >> 56);
-                const bool pre = a < nf && (fl & FR_DENSE) && (fl >> 4) != K_PREPLY;
+                const bool pre = PREFETCH_VALUES && a < nf && (fl & FR_DENSE) && (fl >> 4) != K_PREPLY;
 #pragma unroll
                 for (uint32_t j = 0; j < SPL; ++j) {
                     const int d = (int)(lane + 64 * j) - (int)st0;
@@ -366,7 +553,7 @@ __global__ __launch_bounds__(256) void k_apply(DevView v)
                     int k[SPL];
                     frag_slots(lidx, kind == K_PREPLY ? v.r_slot : v.e_slot, ent, cnt, st0, dense, k);
                     uint64_t val[SPL];
-                    if (kind != K_PREPLY && dense && a < 2) {
+                    if (PREFETCH_VALUES && kind != K_PREPLY && dense && a < 2) {
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) val[j] = a == 0 ? pv[0][j] : pv[1][j];
                     } else {
@@ -495,7 +682,7 @@ __global__ __launch_bounds__(256) void k_apply(DevView v)
         const uint32_t t = threadIdx.x;
         unsigned long long s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         const int slot = t == 0 ? PC_A : t == 1 ? PC_L : t == 2 ? PC_P : t == 3 ? PC_Q : PC_DSTATE;
-        v.partials[8 * blockIdx.x + slot] = s;
+        v.partials[8 * blockIdx.x + slot] += s;
     }
 }
 
@@ -642,8 +829,13 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
     hipLaunchKernelGGL(k_proposer, dim3(cdiv(v.N, 64)), dim3(64), 0, s, v);
     if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
     if (ev_apply0) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
-    hipLaunchKernelGGL(k_apply, dim3(g.apply_wgs), dim3(256), 0, s, v);
+    switch (g.variant) {
+    case 1: hipLaunchKernelGGL((k_apply_fast<4>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+    case 2: hipLaunchKernelGGL((k_apply_fast<6>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+    default: hipLaunchKernelGGL((k_apply_fast<1>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+    }
     if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
+    hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, v, n_partials);
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, s);

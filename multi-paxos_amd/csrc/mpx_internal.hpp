@@ -87,6 +87,7 @@ struct DevView {
     const uint32_t *m_cnt;
     const uint32_t *m_node;         // node of each message
     const uint64_t *node_off;       // N+1
+    const uint32_t *n_after_prepare; // per node: 1 + index of its last PREPARE (0: none)
     uint8_t *m_flags;
     uint64_t *m_maxseen;
     // header scan
@@ -166,7 +167,7 @@ MPX_HD inline uint64_t scalar_digest(uint32_t node, uint64_t promised, uint64_t 
 }
 
 // kernels (kernels.hip); every launcher queues on `stream`, returns hipError_t as int
-struct LaunchGeom { uint32_t apply_wgs, chosen_wgs; };
+struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, variant; };
 int launch_run(const DevView &v, void *stream, LaunchGeom g, void *ev_begin, void *ev_apply0,
                void *ev_apply1, void *ev_end);
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
