@@ -73,7 +73,7 @@ struct mpx_engine {
     DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, n_after_prepare, m_flags, m_maxseen;
     DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
-    DevBuf f_off, frags, ev_off, ev_msg, pl_off, pl_msg;
+    DevBuf f_off, frags, gp_list, ev_off, ev_msg, pl_off, pl_msg;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
     DevBuf st, st_valid, chosen, chosen_valid;
     DevBuf out, out_cursor, partials, viol, summary;
@@ -257,7 +257,7 @@ static int upload_trace(mpx_engine *e)
     TRY(upload(e->e_val, h.e_val, s)); TRY(upload(e->e_slot, h.e_slot, s));
     TRY(upload(e->r_pid, h.r_pid, s)); TRY(upload(e->r_val, h.r_val, s)); TRY(upload(e->r_slot, h.r_slot, s));
     TRY(upload(e->g_a, h.g_a, s)); TRY(upload(e->g_b, h.g_b, s));
-    TRY(upload(e->f_off, h.f_off, s)); TRY(upload(e->frags, h.frags, s));
+    TRY(upload(e->f_off, h.f_off, s)); TRY(upload(e->frags, h.frags, s)); TRY(upload(e->gp_list, h.gp_list, s));
     TRY(upload(e->ev_off, h.ev_off, s)); TRY(upload(e->ev_msg, h.ev_msg, s));
     TRY(upload(e->pl_off, h.pl_off, s)); TRY(upload(e->pl_msg, h.pl_msg, s));
     TRY(upload(e->b_msg, h.b_msg, s)); TRY(upload(e->b_pstart, h.b_pstart, s));
@@ -280,6 +280,7 @@ static int upload_trace(mpx_engine *e)
     v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
+    v.num_gp = h.gp_list.size(); v.gp_list = e->gp_list.as<uint64_t>();
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
     v.num_batches = (uint32_t)h.b_msg.size();
@@ -810,6 +811,8 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
+    TRY(e->gp_list.alloc(8));
+    v.num_gp = 0; v.gp_list = e->gp_list.as<uint64_t>();    // clean trace: every pair is a fast pair
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
     v.num_batches = (uint32_t)K;

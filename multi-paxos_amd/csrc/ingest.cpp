@@ -436,6 +436,19 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         std::vector<uint64_t> pos(ht.cf_off.begin(), ht.cf_off.end() - 1);
         for (auto &x : cfr) ht.cfrags[pos[x.key]++] = x.f;
     }
+    // pairs the lean dense kernel cannot take (same predicate as pair_is_fast
+    // in kernels.hip): they go to the general kernel's work list
+    for (uint32_t n = 0; n < N; ++n)
+        for (uint64_t b = 0; b < NB; ++b) {
+            const uint64_t p = (uint64_t)n * NB + b, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
+            if (!nf) continue;
+            bool fast = nf <= 64 && ht.frags[f0].msg >= ht.n_after_prepare[n];
+            for (uint64_t f = f0; fast && f < f0 + nf; ++f) {
+                const uint8_t fl = ht.frags[f].flags;
+                fast = (fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT);
+            }
+            if (!fast) ht.gp_list.push_back(p);
+        }
     // slots for sparse fragments
     if (ht.any_sparse) {
         ht.e_slot.resize(ht.e_iid.size());

@@ -56,6 +56,7 @@ struct HostTrace {
     bool any_sparse = false;
     std::vector<uint64_t> f_off;
     std::vector<Frag> frags;
+    std::vector<uint64_t> gp_list;                  // (node, bucket) pairs for the general apply kernel
     std::vector<uint64_t> ev_off, pl_off;
     std::vector<uint32_t> ev_msg, pl_msg;
     std::vector<uint32_t> b_msg, b_pstart, b_rep;

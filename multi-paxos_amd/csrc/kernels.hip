@@ -455,20 +455,22 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     wave_lds_fence();
     uint32_t cA = 0, cL = 0, cP = 0, cQ = 0;    // per-lane counts stay far below 2^32
     unsigned long long dig = 0;
-    const uint64_t npairs = (uint64_t)v.N * v.NB;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
     const uint64_t *__restrict__ f_off = v.f_off;
     const uint64_t *__restrict__ ev_off = v.ev_off;
 
-    auto rt1 = [&](uint64_t q) -> uint64_t {
-        if (q >= npairs || lane > 3) return 0;
+    // work list: the pairs the lean kernel does not take (ingest.cpp)
+    auto rt1 = [&](uint64_t i) -> uint64_t {
+        if (i >= v.num_gp || lane > 4) return 0;
+        const uint64_t q = v.gp_list[i];
+        if (lane == 4) return q;
         const uint32_t n = (uint32_t)(q / v.NB);
         return lane < 2 ? f_off[q + lane] : ev_off[n + lane - 2];
     };
-    // software pipeline over this wave's pairs p, p+stride, p+2*stride:
-    //   (1) CSR offsets two pairs ahead, (2) first descriptor window one pair
-    //   ahead, (3) flags + entry values of the current pair
+    // software pipeline over this wave's work items: (1) CSR offsets two
+    // items ahead, (2) first descriptor window one item ahead, (3) flags +
+    // entry values of the current item
     struct Win { uint64_t fw0, fw1; uint32_t evm; };
     auto rt2 = [&](uint64_t off) -> Win {
         Win w{0, NONE32, NONE32};
@@ -480,19 +482,19 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         if (lane < ee - ei && lane < 64) w.evm = v.ev_msg[ei + lane];
         return w;
     };
-    uint64_t p = (uint64_t)blockIdx.x * 4 + wv;
-    uint64_t off_cur = rt1(p);
-    uint64_t off_nxt = rt1(p + stride);
+    uint64_t it = (uint64_t)blockIdx.x * 4 + wv;
+    uint64_t off_cur = rt1(it);
+    uint64_t off_nxt = rt1(it + stride);
     Win win_nxt = rt2(off_cur);
-    for (; p < npairs; p += stride) {
+    for (; it < v.num_gp; it += stride) {
+        const uint64_t p = rl64(off_cur, 4);
         const uint32_t n = (uint32_t)(p / v.NB);
         const uint32_t b = (uint32_t)(p - (uint64_t)n * v.NB);
         uint64_t fi = rl64(off_cur, 0), fe = rl64(off_cur, 1), ei = rl64(off_cur, 2), ee = rl64(off_cur, 3);
         Win win = win_nxt;
-        win_nxt = rt2(off_nxt);                  // next pair's descriptors in flight
+        win_nxt = rt2(off_nxt);                  // next item's descriptors in flight
         off_cur = off_nxt;
-        off_nxt = rt1(p + 2 * stride);
-        if (fi == fe || pair_is_fast(v, n, fe - fi, win.fw1)) continue;   // empty pairs leave no state
+        off_nxt = rt1(it + 2 * stride);
         const uint64_t li0 = (uint64_t)b << BSH;
         uint64_t sb[SPL], sw[SPL];
 #pragma unroll
@@ -835,7 +837,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
     default: hipLaunchKernelGGL((k_apply_fast<1>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
     }
     if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-    hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+    if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, v, n_partials);
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, s);

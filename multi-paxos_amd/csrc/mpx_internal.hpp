@@ -110,6 +110,8 @@ struct DevView {
     // fragment lists
     const uint64_t *f_off;          // N*NB+1
     const Frag *frags;
+    uint64_t num_gp;                // pairs for the general apply kernel
+    const uint64_t *gp_list;
     const uint64_t *ev_off;         // N+1
     const uint32_t *ev_msg;
     const uint64_t *pl_off;         // N+1
