@@ -38,6 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "multi-paxos_amd"))
 
 import mpx  # noqa: E402
+from mpx import dist as mdist  # noqa: E402
 
 METRIC = "quorum decisions/sec (instances chosen/s) + achieved HBM GB/s, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip-level table
@@ -150,9 +151,7 @@ def main():
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
     M, N = args.instances, args.nodes
-    # contiguous instance shards, aligned to the 256-instance bucket
-    per = ((M + world - 1) // world + 255) // 256 * 256
-    sb, se = min(M, rank * per), min(M, (rank + 1) * per)
+    sb, se = mdist.shard_bounds(M, world, rank)       # contiguous, bucket-aligned instance shard
     eng = mpx.Engine(N, sb, se, device=local)
     if world > 1:
         uid = broadcast_bytes(pg, mpx.Engine.comm_unique_id() if rank == 0 else None, rank)
@@ -178,13 +177,10 @@ def main():
 
     st = eng.stats()
     apply_ms, run_ms = eng.timings()
-    summ = eng.allgather_summary(world)
-    chosen_total = sum(s[0] for s in summ)
-    viol_total = sum(s[5] for s in summ)
+    tot = mdist.combine(eng.allgather_summary(world))   # also checks per-acceptor scalars agree
+    chosen_total = tot["chosen"]
     assert chosen_total == M, "chosen %d != %d instances" % (chosen_total, M)
-    assert viol_total == 0
-    # every rank computes the same per-acceptor scalars from the replicated headers
-    assert all(s[8] == summ[0][8] for s in summ), "per-acceptor scalars differ across shards"
+    assert tot["violations"] == 0
 
     value = chosen_total * args.steps / dt_max
     ms_per_step = dt_max / args.steps * 1e3

@@ -1,0 +1,49 @@
+"""Instance sharding and the cross-rank summary.
+
+Paxos instances are independent, so the instance space is split into
+contiguous, bucket-aligned shards, one per GPU; per-acceptor scalars depend
+only on replicated headers.  The one exchange is an all-gather of each rank's
+64-word summary (layout = SW_* in multi-paxos_amd/csrc/mpx_internal.hpp).
+"""
+MASK64 = (1 << 64) - 1
+SW_C, SW_P, SW_A, SW_L, SW_MSGS, SW_V, SW_DCHOSEN, SW_DSTATE, SW_DSCAL, SW_Q = range(10)
+SUMMARY_WORDS = 64
+BUCKET = 256
+
+
+def shard_bounds(num_instances, world, rank, align=BUCKET):
+    """[begin, end) of `rank`'s contiguous shard (strong scaling: the whole M at every world size)."""
+    per = ((num_instances + world - 1) // world + align - 1) // align * align
+    return min(num_instances, rank * per), min(num_instances, (rank + 1) * per)
+
+
+def summary_from_oracle(stats, num_msgs=0):
+    """64-word summary from the CPU oracle's [C,P,A,L,V,chosen_digest,state_digest,scalar_digest]."""
+    s = [0] * SUMMARY_WORDS
+    s[SW_C], s[SW_P], s[SW_A], s[SW_L], s[SW_V] = stats[0], stats[1], stats[2], stats[3], stats[4]
+    s[SW_DCHOSEN], s[SW_DSTATE], s[SW_DSCAL] = stats[5], stats[6], stats[7]
+    s[SW_MSGS] = num_msgs
+    return s
+
+
+def combine(summaries):
+    """Whole-job totals from every rank's summary.  Counters add, digests add
+    mod 2^64 (they are sums of per-entry hashes), per-acceptor scalars must be
+    identical on every shard (replicated headers)."""
+    if not summaries:
+        raise ValueError("no summaries")
+    scal = {s[SW_DSCAL] for s in summaries}
+    if len(scal) != 1:
+        raise AssertionError("per-acceptor scalars differ across shards: %r" % sorted(scal))
+    out = {
+        "chosen": sum(s[SW_C] for s in summaries),
+        "promise_entries": sum(s[SW_P] for s in summaries),
+        "accept_apps": sum(s[SW_A] for s in summaries),
+        "commit_apps": sum(s[SW_L] for s in summaries),
+        "violations": sum(s[SW_V] for s in summaries),
+        "chosen_digest": sum(s[SW_DCHOSEN] for s in summaries) & MASK64,
+        "state_digest": sum(s[SW_DSTATE] for s in summaries) & MASK64,
+        "scalar_digest": summaries[0][SW_DSCAL],
+    }
+    out["bytes_alg"] = 16 * out["promise_entries"] + 24 * out["accept_apps"] + 16 * out["commit_apps"]
+    return out

@@ -1,0 +1,79 @@
+"""The N>1 decomposition on CPU: world_size-2 gloo, one process per shard.
+
+Each rank generates its shard's trace (headers replicated, entries of its
+instances only — what every GPU rank holds), runs the CPU oracle on it, and the
+64-word summaries are all-gathered over gloo and combined with the same code
+bench.py uses.  The combination must equal the oracle over the whole trace:
+counters add, digests add mod 2^64, per-acceptor scalars agree on every rank.
+"""
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import mpx
+from mpx import dist as mdist
+from oracles import oracle_run
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, n, m, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sb, se = mdist.shard_bounds(m, world, rank)
+        t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=256,
+                               shard_begin=sb, shard_end=se)
+        _, stats, _ = oracle_run(t)
+        mine = mdist.summary_from_oracle(stats)
+        allsum = [None] * world
+        dist.all_gather_object(allsum, mine)
+        if rank == 0:
+            q.put(mdist.combine(allsum))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,m", [(2, 9, 256 * 40), (2, 5, 1000), (3, 3, 256 * 7 + 5)])
+def test_sharded_oracle_combines_to_whole(world, n, m):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, n, m, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, whole, _ = oracle_run(mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=256))
+    assert [got["chosen"], got["promise_entries"], got["accept_apps"], got["commit_apps"], got["violations"],
+            got["chosen_digest"], got["state_digest"], got["scalar_digest"]] == whole
+    assert got["chosen"] == m
+
+
+def test_shard_bounds_cover_and_align():
+    for m in (1, 255, 256, 1000, 1 << 20, (1 << 27) + 3):
+        for w in (1, 2, 3, 4, 8):
+            b = [mdist.shard_bounds(m, w, r) for r in range(w)]
+            assert b[0][0] == 0 and b[-1][1] == m
+            for (a0, a1), (c0, c1) in zip(b, b[1:]):
+                assert a1 == c0
+            for a0, a1 in b:
+                assert a0 <= a1 and (a0 % 256 == 0 or a0 == a1 == m)   # trailing ranks may be empty
+
+
+def test_combine_rejects_disagreeing_scalars():
+    a = [0] * 64
+    b = [0] * 64
+    b[mdist.SW_DSCAL] = 1
+    with pytest.raises(AssertionError):
+        mdist.combine([a, b])
