@@ -61,7 +61,9 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     pg = None
-    if world > 1:
+    # under torchrun (WORLD_SIZE set) the distributed path runs even at N=1, so
+    # the rendezvous / RCCL communicator / all-gather code is exercised
+    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:
         import torch.distributed as dist      # gloo on the CPU: rendezvous, barrier, max-reduce only
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -153,7 +155,7 @@ def main():
     M, N = args.instances, args.nodes
     sb, se = mdist.shard_bounds(M, world, rank)       # contiguous, bucket-aligned instance shard
     eng = mpx.Engine(N, sb, se, device=local)
-    if world > 1:
+    if pg is not None:
         uid = broadcast_bytes(pg, mpx.Engine.comm_unique_id() if rank == 0 else None, rank)
         eng.comm_init(uid, rank, world)
     t_gen = time.perf_counter()
@@ -215,7 +217,7 @@ def main():
                        "parallelism": "instance-shard x%d (RCCL all-gather of 64-word summaries)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_apply", "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_alg},
+                         "kernel": "k_apply_fast", "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_alg},
             "cpu_baseline": cpu,
             "hbm_gbps_alg_step": bytes_alg * world / (dt_max / args.steps) / 1e9,
             "decisions_per_step": chosen_total,

@@ -155,6 +155,3 @@ int gen_clean(const mpx_gen_params &p, std::string &out)
 }
 
 }  // namespace mpx
-namespace mpx {
-int gen_faulty(const mpx_gen_params &, std::string &) { return MPX_E_INVAL; }
-}

@@ -21,6 +21,9 @@ from fuzztrace import fuzz_trace  # noqa: E402
 from handmade import handmade_traces  # noqa: E402
 from oracles import ref_available, ref_run  # noqa: E402
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "multi-paxos_amd"))
+import mpx  # noqa: E402  (host generators only: no GPU needed)
+
 
 def main():
     if not ref_available():
@@ -32,6 +35,13 @@ def main():
         cases["fuzz_%03d" % seed] = fuzz_trace(seed)
     for seed in range(4):
         cases["fuzz_big_%d" % seed] = fuzz_trace(10_000 + seed, n_nodes=5, n_inst=200, n_msgs=600)
+    # C2-shaped clean traces and C3-shaped contended, lossy traces at fixture size
+    cases["c2_clean_n5"] = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=5, num_instances=1000, batch=256)
+    cases["c2_clean_n9_b100"] = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=9, num_instances=777, batch=100)
+    for seed in range(4):
+        cases["c3_faulty_%d" % seed] = mpx.generate_trace(
+            mpx.GEN_FAULTY, num_nodes=7, num_instances=300, seed=seed, batch=32, proposers=3,
+            drop_rate=500, dup_rate=1000, max_delay=500)
     extra = os.path.join(HERE, "extra_traces")
     if os.path.isdir(extra):
         for fn in sorted(os.listdir(extra)):

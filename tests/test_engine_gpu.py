@@ -157,3 +157,36 @@ def test_host_sharded_ingest_matches_oracle_restricted():
         assert a["state"] == [s for s in b["state"] if sb <= s[0] < se]
         assert (a["promised"], a["max_seen"]) == (b["promised"], b["max_seen"])
     assert part["chosen"] == [c for c in full["chosen"] if sb <= c[0] < se]
+
+
+@pytest.mark.parametrize("seed,m,p,b", [(11, 1 << 12, 3, 64), (12, 3000, 2, 256), (13, 1 << 13, 3, 17)])
+def test_engine_matches_oracle_c3_faulty(seed, m, p, b):
+    """C3 shape: 7 acceptors, competing proposers, drop 5 % / dup 10 % (<=3) /
+    delay U[0,500) (multi/debug.conf.sample:1) — multi-ballot promise phases,
+    promise replies with entries, rejects, duplicates, reordering."""
+    t = mpx.generate_trace(mpx.GEN_FAULTY, num_nodes=7, num_instances=m, seed=seed, batch=b, proposers=p,
+                           drop_rate=500, dup_rate=1000, max_delay=500)
+    want, ostats, _ = oracle_run(t)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        got = e.dump()
+    assert got == want, mpxr.diff(got, want)
+    assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
+            st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
+    assert st["promise_entries"] > 0 and st["violations"] == 0
+
+
+def test_rccl_single_rank_allgather():
+    """The RCCL path of a step (communicator + summary all-gather on the engine stream), one rank."""
+    n, m = 9, 256 * 64
+    with mpx.Engine(n, 0, m) as e:
+        e.comm_init(mpx.Engine.comm_unique_id(), 0, 1)
+        e.load_clean_device(num_instances=m)
+        e.step()
+        e.sync()
+        st = e.stats()
+        summ = e.allgather_summary(1)
+    from mpx import dist as mdist
+    tot = mdist.combine(summ)
+    assert tot["chosen"] == m == st["chosen"]
+    assert tot["state_digest"] == st["state_digest"]
