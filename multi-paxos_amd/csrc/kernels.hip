@@ -300,45 +300,9 @@ __device__ inline bool pair_is_fast(const DevView &v, uint32_t n, uint64_t nfrag
 
 // Lean acceptor/learner apply for fast pairs: one wave per pair, slots
 // {2l, 2l+1, 128+2l, 129+2l} of lane l so full 256-entry runs move with
-// 16-byte loads and stores.  Values of two fragments are loaded before either
-// is applied, so a bucket's accept + commit cost one memory round trip.
-__device__ inline void fast_load(const uint64_t *__restrict__ e_val, uint64_t ent, uint64_t w1, bool skip,
-                                 uint32_t lane, uint64_t &v0, uint64_t &v1, uint64_t &v2, uint64_t &v3, uint32_t &inm)
-{
-    const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
-    inm = 0;
-    v0 = v1 = v2 = v3 = 0;
-    if (skip) return;
-    if (st0 == 0 && cnt == BS && !(ent & 1)) {
-        const u64x2 x0 = *reinterpret_cast<const u64x2 *>(e_val + ent + 2 * lane);
-        const u64x2 x1 = *reinterpret_cast<const u64x2 *>(e_val + ent + 128 + 2 * lane);
-        v0 = x0.x; v1 = x0.y; v2 = x1.x; v3 = x1.y;
-        inm = 0xF;
-        return;
-    }
-    const int d0 = (int)(2 * lane) - (int)st0;
-    const int d2 = (int)(128 + 2 * lane) - (int)st0;
-    if (d0 >= 0 && d0 < (int)cnt) { v0 = e_val[ent + d0]; inm |= 1; }
-    if (d0 + 1 >= 0 && d0 + 1 < (int)cnt) { v1 = e_val[ent + d0 + 1]; inm |= 2; }
-    if (d2 >= 0 && d2 < (int)cnt) { v2 = e_val[ent + d2]; inm |= 4; }
-    if (d2 + 1 >= 0 && d2 + 1 < (int)cnt) { v3 = e_val[ent + d2 + 1]; inm |= 8; }
-}
-
-// apply one fragment's values to one slot; returns 1 on a re-commit with another Value
-__device__ inline uint32_t fast_apply(bool commit, uint64_t ballot, uint64_t val, bool in, uint64_t &sb, uint64_t &sw,
-                                      uint32_t &cA, uint32_t &cL)
-{
-    if (!in) return 0;
-    if (!commit) {
-        if (!(sw & W_COMMITTED)) { sb = ballot; sw = W_PRESENT | val; ++cA; }         // :1380-1387
-        return 0;
-    }
-    ++cL;
-    if (sw & W_COMMITTED) return (sw & W_HANDLE) != val;                               // :1508
-    sb = ballot; sw = W_PRESENT | W_COMMITTED | val;                                   // :1515
-    return 0;
-}
-
+// 16-byte loads and stores.  Only the Value that fixes each slot's final state
+// is loaded (pass 1 below), so a clean bucket's accept + commit cost one
+// 8-byte value read per slot instead of two.
 template <int WAVES_PER_EU>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
 {
@@ -380,30 +344,95 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         const uint32_t fmsg = (uint32_t)fw1;
         const uint32_t fflag = lane < nfrag ? v.m_flags[fmsg] : 0;
         const uint64_t fbal = lane < nfrag ? v.m_ballot[fmsg] : 0;
+        // Pass 1, descriptors only: per slot the fragment that fixes its final
+        // state — the first COMMIT covering it (first commit wins, :1515, and
+        // later accepts skip committed slots, :1380), else the last granted
+        // ACCEPT (:1387) — and the counters.  A fast pair has no snapshot
+        // events, so values of overwritten accepts never reach an output and
+        // are not loaded.
+        uint32_t src = 0xFFFFFFFFu;            // 8 bits per slot: fragment index, 0xFF none
+        uint32_t com = 0;                      // bit j: slot j committed
+        uint32_t recommit = 0;                 // a later COMMIT covers a committed slot
+        for (uint32_t a = 0; a < (uint32_t)nfrag; ++a) {
+            const uint64_t w1 = rl64(fw1, a);
+            const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+            const bool commit = (w1 >> 60) == K_COMMIT;
+            if (!commit && !(rl32(fflag, a) & F_GRANTED)) continue;
+#pragma unroll
+            for (uint32_t j = 0; j < SPL; ++j) {
+                const uint32_t s = j < 2 ? 2 * lane + j : 128 + 2 * lane + (j - 2);
+                if (s < st0 || s >= st0 + cnt) continue;
+                if (commit) {
+                    ++cL;
+                    if ((com >> j) & 1) recommit = 1;
+                    else { com |= 1u << j; src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j)); }
+                } else if (!((com >> j) & 1)) {
+                    ++cA;
+                    src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j));
+                }
+            }
+        }
+        // Pass 2: one value load per slot, from its fixing fragment; 16-byte
+        // loads when every slot of the wave reads one full run
+        uint64_t val[SPL] = {0, 0, 0, 0};
         uint64_t sb0 = 0, sb1 = 0, sb2 = 0, sb3 = 0, sw0 = 0, sw1 = 0, sw2 = 0, sw3 = 0;
+        const uint32_t a0 = src & 0xFF;
+        const bool same = src == (a0 | (a0 << 8) | (a0 << 16) | (a0 << 24)) && a0 != 0xFF;
+        const uint32_t a_u = __builtin_amdgcn_readfirstlane(a0);
+        const bool uni = __ballot(!same || a0 != a_u) == 0;
+        bool full = false;
+        uint64_t ent_u = 0, w1_u = 0;
+        if (uni) {
+            w1_u = rl64(fw1, a_u);
+            ent_u = rl64(fw0, a_u);
+            full = ((w1_u >> 48) & 0xFF) == 0 && ((w1_u >> 32) & 0xFFFF) == BS && !(ent_u & 1);
+        }
+        if (full) {
+            // every slot fixed by one full run: ballot and committed bit are wave-uniform
+            const u64x2 x0 = *reinterpret_cast<const u64x2 *>(e_val + ent_u + 2 * lane);
+            const u64x2 x1 = *reinterpret_cast<const u64x2 *>(e_val + ent_u + 128 + 2 * lane);
+            val[0] = x0.x; val[1] = x0.y; val[2] = x1.x; val[3] = x1.y;
+            const uint64_t bu = rl64(fbal, a_u);
+            const uint64_t tag = W_PRESENT | ((w1_u >> 60) == K_COMMIT ? W_COMMITTED : 0);
+            sb0 = sb1 = sb2 = sb3 = bu;
+            sw0 = tag | x0.x; sw1 = tag | x0.y; sw2 = tag | x1.x; sw3 = tag | x1.y;
+        } else {
+            // per-lane fragment index: fetch its descriptor with a lane-indexed
+            // shuffle, issued by every lane (a bpermute from an inactive lane reads 0)
+#define MPX_SLOT(J, SB, SW)                                                                   \
+            {                                                                                 \
+                const uint32_t fa = (src >> (8 * J)) & 0xFF;                                  \
+                const uint32_t s = J < 2 ? 2 * lane + J : 128 + 2 * lane + (J - 2);           \
+                const uint64_t ent = __shfl(fw0, (int)(fa & 63), 64);                         \
+                const uint64_t w1 = __shfl(fw1, (int)(fa & 63), 64);                          \
+                const uint64_t bj = __shfl(fbal, (int)(fa & 63), 64);                         \
+                if (fa != 0xFF) {                                                             \
+                    val[J] = e_val[ent + (s - ((uint32_t)(w1 >> 48) & 0xFF))];                \
+                    SB = bj;                                                                  \
+                    SW = W_PRESENT | (((com >> J) & 1) ? W_COMMITTED : 0) | val[J];           \
+                }                                                                             \
+            }
+            MPX_SLOT(0, sb0, sw0) MPX_SLOT(1, sb1, sw1) MPX_SLOT(2, sb2, sw2) MPX_SLOT(3, sb3, sw3)
+#undef MPX_SLOT
+        }
+        // re-commit check (rare): every later COMMIT must carry the committed Value (:1508)
         uint32_t bad = 0;
-        for (uint32_t a = 0; a < (uint32_t)nfrag; a += 2) {
-            const bool two = a + 1 < (uint32_t)nfrag;
-            const uint64_t wa = rl64(fw1, a), wb = two ? rl64(fw1, a + 1) : 0;
-            const bool ca = (wa >> 60) == K_COMMIT, cb = (wb >> 60) == K_COMMIT;
-            const bool ska = !ca && !(rl32(fflag, a) & F_GRANTED);
-            const bool skb = !two || (!cb && !(rl32(fflag, a + 1) & F_GRANTED));
-            uint64_t a0, a1, a2, a3, b0, b1, b2, b3;
-            uint32_t ma, mb;
-            fast_load(e_val, rl64(fw0, a), wa, ska, lane, a0, a1, a2, a3, ma);
-            fast_load(e_val, two ? rl64(fw0, a + 1) : 0, wb, skb, lane, b0, b1, b2, b3, mb);
-            const uint64_t ba = rl64(fbal, a), bb = two ? rl64(fbal, a + 1) : 0;
-            bad |= fast_apply(ca, ba, a0, ma & 1, sb0, sw0, cA, cL);
-            bad |= fast_apply(ca, ba, a1, ma & 2, sb1, sw1, cA, cL);
-            bad |= fast_apply(ca, ba, a2, ma & 4, sb2, sw2, cA, cL);
-            bad |= fast_apply(ca, ba, a3, ma & 8, sb3, sw3, cA, cL);
-            bad |= fast_apply(cb, bb, b0, mb & 1, sb0, sw0, cA, cL);
-            bad |= fast_apply(cb, bb, b1, mb & 2, sb1, sw1, cA, cL);
-            bad |= fast_apply(cb, bb, b2, mb & 4, sb2, sw2, cA, cL);
-            bad |= fast_apply(cb, bb, b3, mb & 8, sb3, sw3, cA, cL);
+        if (__ballot(recommit)) {
+            for (uint32_t a = 0; a < (uint32_t)nfrag; ++a) {
+                const uint64_t w1 = rl64(fw1, a);
+                if ((w1 >> 60) != K_COMMIT) continue;
+                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                const uint64_t ent = rl64(fw0, a);
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) {
+                    const uint32_t s = j < 2 ? 2 * lane + j : 128 + 2 * lane + (j - 2);
+                    if (s < st0 || s >= st0 + cnt || ((src >> (8 * j)) & 0xFF) == a) continue;
+                    if (e_val[ent + (s - st0)] != val[j]) bad = 1;
+                }
+            }
         }
         const uint64_t li0 = (uint64_t)b << BSH;
-        if (bad) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, v.shard_begin + li0);
+        if (__ballot(bad) && lane == 0) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, v.shard_begin + li0);
         uint64_t *srow = v.st + 2 * ((uint64_t)n * v.shard_len + li0);
         const uint32_t s0 = 2 * lane, s2 = 128 + 2 * lane;
         u64x2 w;
