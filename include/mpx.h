@@ -35,6 +35,20 @@
  *                                                        (+ AcceptRejected's batch clear, :1328-1343)
  *   MPX_MSG_P_BATCH  {u32 type=17, u64 accept_id, u32 len, {u64 iid, Value}*}
  *                                                        a new AcceptingValues, multi/paxos.cpp:1299-1326
+ *                    (member: entries are {u64 iid, u64 pid, Value_m}, member/paxos.cpp:1158-1160)
+ * and, for member semantics only, where the node applied a learned membership
+ * change (NodeImpl::ChangeMemberships, member/paxos.cpp:1864-1964):
+ *   MPX_MSG_E_EPOCH  {u32 type=18, u32 epoch}            the node moves to epochs[epoch]
+ * Member E_EPOCH semantics:
+ *   - the node's version_ becomes epochs[epoch].version; PREPARE / ACCEPT
+ *     with another version are dropped silently (member/paxos.cpp:1702,1744);
+ *   - acceptor role lost: the Acceptor object and its state are deleted
+ *     (:1952-1957); gained: a fresh Acceptor (:1897-1901);
+ *   - proposer role lost: the Proposer is deleted (:1927-1930); gained, or
+ *     kept while the acceptor set changed (AcceptorsChanged, :1291-1322): the
+ *     proposer is idle (no promise round, no batches) until its next P_START;
+ *   - quorum for replies is |acceptors of the node's epoch|/2+1 (:1171,1327),
+ *     and a reply from a non-acceptor is an ASSERT (:1163,1324).
  */
 #ifndef MPX_H
 #define MPX_H
@@ -72,7 +86,8 @@ enum {
     MPX_MSG_COMMIT        = 5,   /* member: LEARN       (member/paxos.cpp:611) */
     MPX_MSG_COMMIT_REPLY  = 6,   /* member: LEARN_REPLY (member/paxos.cpp:612) */
     MPX_MSG_P_START       = 16,  /* engine-local proposer marker, see above   */
-    MPX_MSG_P_BATCH       = 17
+    MPX_MSG_P_BATCH       = 17,
+    MPX_MSG_E_EPOCH       = 18   /* member only */
 };
 
 enum { MPX_SEM_MULTI = 0, MPX_SEM_MEMBER = 1 };
@@ -96,13 +111,17 @@ enum { MPX_SEM_MULTI = 0, MPX_SEM_MEMBER = 1 };
 /* mpx_read_chosen / mpx_read_node_state mark present entries with this bit */
 #define MPX_PRESENT (1ull << 63)
 
-/* member semantics: one entry per membership epoch (member/paxos.cpp:1864-1964)
- * An acceptor drops PREPARE/ACCEPT whose version differs from its own
- * (member/paxos.cpp:1702,1744); the quorum is |acceptors|/2+1 (:1171,1327). */
+/* member semantics: one entry per membership epoch — the node sets after one
+ * step of NodeImpl::ChangeMemberships (member/paxos.cpp:1864-1964).  Every
+ * node starts in epoch 0 (Loop: {first} is learner, proposer and acceptor,
+ * member/paxos.cpp:738-747).  An acceptor drops PREPARE/ACCEPT whose version
+ * differs from its own (:1702,1744); the quorum is |acceptors|/2+1 (:1171,1327).
+ * In an MPXT container each entry is 24 bytes, in this layout. */
 typedef struct mpx_epoch {
-    uint32_t version;
-    uint32_t pad;
-    uint64_t acceptor_mask;   /* bit i set: node i is an acceptor in this epoch */
+    uint32_t version;         /* NodeImpl::version_ in this epoch               */
+    uint32_t flags;           /* 0                                              */
+    uint64_t acceptor_mask;   /* bit i set: node i is an acceptor (acceptors_)  */
+    uint64_t proposer_mask;   /* bit i set: node i runs a Proposer (proposers_) */
 } mpx_epoch;
 
 typedef struct mpx_config {
@@ -114,7 +133,7 @@ typedef struct mpx_config {
     uint64_t shard_end;        /*                              shard_end)          */
     uint32_t num_epochs;       /* member only                                      */
     uint32_t flags;            /* reserved, 0                                      */
-    const mpx_epoch *epochs;   /* member only, indexed by version                  */
+    const mpx_epoch *epochs;   /* member only, indexed by E_EPOCH's epoch          */
 } mpx_config;
 
 typedef struct mpx_engine mpx_engine;
@@ -153,7 +172,8 @@ enum {
     MPX_V_BAD_NODE      = 3,   /* reply from a node not in the set, multi/paxos.cpp:1040,1414 */
     MPX_V_DUP_IID       = 4,   /* an instance twice in one message / overlapping ranges   */
     MPX_V_BATCH_BEFORE_QUORUM = 5, /* P_BATCH while preparing, multi/paxos.cpp:1054   */
-    MPX_V_LEARN_VALUE   = 6    /* member: accept/learn differs from learned value         */
+    MPX_V_LEARN_VALUE   = 6    /* member: accept/learn differs from the learned Value,
+                                  member/paxos.cpp:1767-1769,1398-1399           */
 };
 
 /* ---- lifecycle ----------------------------------------------------------- */

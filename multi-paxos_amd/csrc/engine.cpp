@@ -179,7 +179,7 @@ extern "C" int mpx_submit_trace(mpx_engine *e, const uint8_t *t, uint64_t size)
     if (!e || !t || size < 40 || std::memcmp(t, "MPXT", 4)) return MPX_E_INVAL;
     const uint32_t N = rd32(t + 8), ne = rd32(t + 24);
     if (N != e->cfg.num_nodes) return MPX_E_INVAL;
-    size_t pos = 40 + (size_t)ne * 16;
+    size_t pos = 40 + (size_t)ne * 24;
     for (uint32_t n = 0; n < N; ++n) {
         if (pos + 16 > size) return MPX_E_DECODE;
         const uint64_t cnt = rd64(t + pos), nb = rd64(t + pos + 8);
@@ -713,6 +713,7 @@ extern "C" int mpx_trace_generate(const mpx_gen_params *p, uint8_t **out, uint64
     int rc;
     if (p->kind == MPX_GEN_CLEAN) rc = gen_clean(*p, t);
     else if (p->kind == MPX_GEN_FAULTY) rc = gen_faulty(*p, t);
+    else if (p->kind == MPX_GEN_MEMBER) rc = gen_member(*p, t);
     else rc = MPX_E_INVAL;
     if (rc) return rc;
     *out = (uint8_t *)std::malloc(t.size());

@@ -14,7 +14,7 @@ namespace mpx {
 
 template <typename T> static inline void app(std::string &s, T v) { s.append((const char *)&v, sizeof v); }
 
-void TraceWriter::begin(uint32_t N, uint32_t semantics, uint64_t M, const std::vector<std::pair<uint32_t, uint64_t>> &epochs)
+void TraceWriter::begin(uint32_t N, uint32_t semantics, uint64_t M, const std::vector<mpx_epoch> &epochs)
 {
     out.clear();
     out.append("MPXT", 4);
@@ -25,7 +25,7 @@ void TraceWriter::begin(uint32_t N, uint32_t semantics, uint64_t M, const std::v
     app<uint32_t>(out, (uint32_t)epochs.size());
     app<uint32_t>(out, 0);
     app<uint64_t>(out, 0);
-    for (auto &e : epochs) { app<uint32_t>(out, e.first); app<uint32_t>(out, 0); app<uint64_t>(out, e.second); }
+    for (auto &e : epochs) { app<uint32_t>(out, e.version); app<uint32_t>(out, e.flags); app<uint64_t>(out, e.acceptor_mask); app<uint64_t>(out, e.proposer_mask); }
 }
 
 void TraceWriter::node(const std::vector<std::string> &msgs)

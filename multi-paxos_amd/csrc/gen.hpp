@@ -11,7 +11,7 @@ namespace mpx {
 
 struct TraceWriter {
     std::string out;
-    void begin(uint32_t N, uint32_t semantics, uint64_t M, const std::vector<std::pair<uint32_t, uint64_t>> &epochs);
+    void begin(uint32_t N, uint32_t semantics, uint64_t M, const std::vector<mpx_epoch> &epochs);
     void node(const std::vector<std::string> &msgs);
 };
 
@@ -28,5 +28,6 @@ std::string msg_p_batch(uint64_t batch, const std::string &body);
 
 int gen_clean(const mpx_gen_params &p, std::string &out);
 int gen_faulty(const mpx_gen_params &p, std::string &out);
+int gen_member(const mpx_gen_params &p, std::string &out);
 
 }  // namespace mpx

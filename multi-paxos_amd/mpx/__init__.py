@@ -33,7 +33,8 @@ class MpxError(RuntimeError):
 
 
 class Epoch(ctypes.Structure):
-    _fields_ = [("version", ctypes.c_uint32), ("pad", ctypes.c_uint32), ("acceptor_mask", ctypes.c_uint64)]
+    _fields_ = [("version", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("acceptor_mask", ctypes.c_uint64),
+                ("proposer_mask", ctypes.c_uint64)]
 
 
 class Config(ctypes.Structure):
@@ -160,7 +161,7 @@ class Engine:
         L = lib()
         if shard_end is None:
             raise ValueError("shard_end required")
-        self._epochs = (Epoch * max(len(epochs), 1))(*[Epoch(v, 0, m) for v, m in epochs])
+        self._epochs = (Epoch * max(len(epochs), 1))(*[Epoch(v, 0, a, p) for v, a, p in epochs])
         cfg = Config(ABI_VERSION, num_nodes, semantics, device, shard_begin, shard_end,
                      len(epochs), 0, self._epochs if epochs else None)
         h = ctypes.c_void_p()

@@ -220,6 +220,69 @@ static const valrec_t *vt_get(const vtab_t *t, u64 h)
     return e ? &t->v[e->a] : NULL;
 }
 
+/* member Value_m (member/paxos.cpp:330-408): u32 proposer, u64 value_id,
+ * u8 noop; unless noop: u8 membership, then either u32 count + count x
+ * {u32 node, u32 type} or u32 len + payload, then u32 cblen + cb.  What
+ * StateMachine::Apply receives is the payload (Learner::Apply, :1062-1073). */
+static long parse_value_m(vtab_t *t, const u8 *p, size_t avail, u64 *handle, int *membership)
+{
+    if (avail < 13) return E_DECODE;
+    u32 proposer = rd32(p);
+    u64 value_id = rd64(p + 4);
+    int noop = p[12] != 0;
+    size_t used = 13, exec_from = 0, exec_len = 0;
+    *membership = 0;
+    if (proposer >= (1u << 14) || value_id >= (1ull << 47)) return E_RANGE;
+    if (!noop) {
+        if (avail < 18) return E_DECODE;
+        int mem = p[13] != 0;
+        u32 n = rd32(p + 14);
+        used = 18;
+        if (mem) {
+            if ((avail - used) / 8 < n) return E_DECODE;
+            used += 8 * (size_t)n;
+            *membership = 1;
+        } else {
+            if (avail - used < n) return E_DECODE;
+            exec_from = used; exec_len = n;
+            used += n;
+        }
+        if (avail - used < 4) return E_DECODE;
+        u32 cbl = rd32(p + used);
+        used += 4;
+        if (avail - used < cbl) return E_DECODE;
+        used += cbl;
+    }
+    /* canonical bytes = the wire bytes with bools normalised to 0/1 */
+    buf_t enc = {0};
+    bput(&enc, p, used);
+    if (enc.oom) return E_NOMEM;
+    enc.p[12] = (u8)noop;
+    if (!noop) enc.p[13] = (u8)*membership;
+    u64 h = ((u64)proposer << 48) | ((u64)noop << 47) | value_id;
+    ent_t *e = map_find(&t->idx, h);
+    if (e) {
+        valrec_t *r = &t->v[e->a];
+        if (r->len != enc.n || memcmp(t->bytes.p + r->off, enc.p, enc.n)) { free(enc.p); return E_VALUE; }
+    } else {
+        if (t->n == t->cap) {
+            size_t c = t->cap ? t->cap * 2 : 64;
+            valrec_t *q = (valrec_t *)realloc(t->v, c * sizeof(valrec_t));
+            if (!q) { free(enc.p); return E_NOMEM; }
+            t->v = q; t->cap = c;
+        }
+        valrec_t *r = &t->v[t->n];
+        r->handle = h; r->off = t->bytes.n; r->len = (u32)enc.n;
+        r->exec_off = *membership ? 0xFFFFFFFFu : (u32)exec_from; r->exec_len = (u32)exec_len;
+        bput(&t->bytes, enc.p, enc.n);
+        if (!map_put(&t->idx, h, t->n, 0)) { free(enc.p); return E_NOMEM; }
+        t->n++;
+    }
+    free(enc.p);
+    *handle = h;
+    return (long)used;
+}
+
 /* ---- digests (shared definition with the engine) ----- */
 static u64 mix64(u64 x)
 {
@@ -251,6 +314,9 @@ typedef struct {
     batch_t *batches; size_t nb, cb;
     map_t batch_idx;            /* accept_id -> index in batches              */
     u64 *bent; size_t nbent, cbent;   /* batch entry pool (iid, handle) pairs  */
+    /* member roles (member/paxos.cpp:737-747,1864-1964) */
+    u32 epoch;
+    int acc_exists, prop_exists;
     /* outputs */
     buf_t sends, events_q, events_c, exec;
     u64 n_sends, n_q, n_c, n_exec;
@@ -258,9 +324,13 @@ typedef struct {
     u64 violations;
 } node_t;
 
+typedef struct { u32 version; u64 amask, pmask; } epoch_t;
+
 typedef struct {
     u32 N, sem;
     u64 M;
+    u32 ne;
+    epoch_t *ep;
     vtab_t vt;
     node_t *nodes;
     u64 first_violation[4];     /* code, node, seq, iid */
@@ -583,6 +653,335 @@ static int process(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     }
 }
 
+
+/* ======================= member semantics (member/paxos.cpp) ===============
+ * Node roles follow the E_EPOCH markers against the epoch table (include/mpx.h):
+ * Loop dispatches PREPARE/ACCEPT only to an existing Acceptor and replies only
+ * to an existing Proposer (:749-790); LEARN always reaches the Learner. */
+
+/* entries {u64 iid, u64 pid, Value_m}* of ACCEPT / LEARN / PREPARE_REPLY /
+ * member P_BATCH (ExtractProposalValues, :421-433); a repeated iid is its ASSERT */
+typedef struct { u64 iid, pid, h; } pent_t;
+static int parse_pvalues(ctx_t *c, node_t *n, const u8 *m, size_t beg, size_t end, u64 seq,
+                         int report, pent_t **out, size_t *k)
+{
+    size_t cap = 16, cnt = 0, cur = beg;
+    pent_t *v = (pent_t *)malloc(cap * sizeof(pent_t));
+    map_t seen = {0};
+    if (!v) return E_NOMEM;
+    while (cur < end) {
+        if (end - cur < 16) { free(v); map_free(&seen); return E_DECODE; }
+        u64 iid = rd64(m + cur), pid = rd64(m + cur + 8);
+        cur += 16;
+        u64 h; int mem;
+        long u = parse_value_m(&c->vt, m + cur, end - cur, &h, &mem);
+        if (u < 0) { free(v); map_free(&seen); return (int)u; }
+        cur += (size_t)u;
+        if (map_find(&seen, iid)) { if (report) violate(c, n, 4, seq, iid); continue; }   /* :429-431 */
+        map_put(&seen, iid, 0, 0);
+        if (cnt == cap) {
+            cap *= 2;
+            pent_t *q = (pent_t *)realloc(v, cap * sizeof(pent_t));
+            if (!q) { free(v); map_free(&seen); return E_NOMEM; }
+            v = q;
+        }
+        v[cnt].iid = iid; v[cnt].pid = pid; v[cnt].h = h; cnt++;
+    }
+    map_free(&seen);
+    *out = v; *k = cnt;
+    return OK;
+}
+
+static int m_reject(node_t *n, u32 dst)
+{
+    buf_t r = {0};
+    bput32(&r, 2); bput64(&r, n->max_seen);                 /* RejectMsg, :882-888 */
+    emit(n, dst, &r);
+    free(r.p);
+    return OK;
+}
+
+/* Acceptor::OnPrepare + FilterAcceptedValues, member/paxos.cpp:1700-1741,1796-1818 */
+static int m_on_prepare(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 24) return E_DECODE;
+    u32 version = rd32(m + 4), proposer = rd32(m + 8);
+    u64 id = rd64(m + 12);
+    u32 rlen = rd32(m + 20);
+    if (rlen % 16 || 24 + (size_t)rlen > len) return E_DECODE;
+    if (!n->acc_exists) return OK;                          /* Loop: if (acceptor_) */
+    if (version != c->ep[n->epoch].version) return OK;      /* :1702 */
+    if (id > n->max_seen) n->max_seen = id;                 /* :1708-1709 */
+    if (proposer >= c->N) violate(c, n, 3, seq, 0);
+    if (id > n->promised) {                                 /* :1711 */
+        n->promised = id;
+        size_t nr = rlen / 16;
+        for (size_t i = 0; i < nr; ++i)                     /* range set insert ASSERT, :290 */
+            for (size_t j = 0; j < i; ++j)
+                if (rd64(m + 24 + 16 * i) == rd64(m + 24 + 16 * j) &&
+                    rd64(m + 32 + 16 * i) == rd64(m + 32 + 16 * j)) violate(c, n, 4, seq, 0);
+        size_t na, nc;
+        ent_t *va = map_sorted(&n->acc, &na);
+        ent_t *vc = map_sorted(&n->com, &nc);
+        size_t k = 0;
+        ent_t *out = (ent_t *)malloc((na + nc + 1) * nr * sizeof(ent_t) + sizeof(ent_t));
+        if (!out || !va || !vc) { free(out); free(va); free(vc); return E_NOMEM; }
+        /* accepted then learned per range, into one iid-keyed map (:1806-1816) */
+        for (size_t r = 0; r < nr; ++r) {
+            u64 a = rd64(m + 24 + 16 * r), b = rd64(m + 32 + 16 * r);
+            for (size_t i = 0; i < na; ++i) if (va[i].key >= a && va[i].key < b) out[k++] = va[i];
+            for (size_t i = 0; i < nc; ++i) if (vc[i].key >= a && vc[i].key < b) out[k++] = vc[i];
+        }
+        qsort(out, k, sizeof(ent_t), cmp_ent);
+        size_t w = 0;
+        for (size_t i = 0; i < k; ++i) {
+            if (w && out[i].key == out[w - 1].key) { violate(c, n, 4, seq, out[i].key); continue; }
+            out[w++] = out[i];
+        }
+        buf_t body = {0};
+        for (size_t i = 0; i < w; ++i) {
+            bput64(&body, out[i].key);
+            bput64(&body, out[i].a);
+            encode_value(&body, &c->vt, out[i].b);
+        }
+        buf_t r = {0};
+        bput32(&r, 1); bput32(&r, n->index); bput64(&r, id); bput32(&r, (u32)body.n);   /* :1726-1730 */
+        bput(&r, body.p, body.n);
+        emit(n, proposer, &r);
+        n->P += w;
+        free(r.p); free(body.p); free(out); free(va); free(vc);
+    } else if (id < n->promised) {                          /* :1734 */
+        m_reject(n, proposer);
+    }
+    return OK;
+}
+
+/* Acceptor::OnAccept, member/paxos.cpp:1742-1784: insert (first value sticks) */
+static int m_on_accept(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 32) return E_DECODE;
+    u32 version = rd32(m + 4), proposer = rd32(m + 8);
+    u64 accept = rd64(m + 12), id = rd64(m + 20);
+    u32 vlen = rd32(m + 28);
+    if (32 + (size_t)vlen > len) return E_DECODE;
+    if (!n->acc_exists) return OK;
+    if (version != c->ep[n->epoch].version) return OK;      /* :1744 */
+    if (id > n->max_seen) n->max_seen = id;                 /* :1750-1751 */
+    if (proposer >= c->N) violate(c, n, 3, seq, 0);
+    if (id >= n->promised) {                                /* :1753 */
+        pent_t *v; size_t k;
+        int rc = parse_pvalues(c, n, m, 32, 32 + vlen, seq, 1, &v, &k);
+        if (rc) return rc;
+        for (size_t i = 0; i < k; ++i) {
+            ent_t *l = map_find(&n->com, v[i].iid);
+            if (l) {                                        /* :1767-1769 */
+                if (l->b != v[i].h) violate(c, n, 6, seq, v[i].iid);
+            } else if (!map_find(&n->acc, v[i].iid)) {      /* std::map::insert, :1765 */
+                map_put(&n->acc, v[i].iid, v[i].pid, v[i].h);
+                n->A++;
+            }
+        }
+        free(v);
+        buf_t r = {0};
+        bput32(&r, 4); bput32(&r, n->index); bput64(&r, accept);   /* AcceptReplyMsg, :1771 */
+        emit(n, proposer, &r);
+        free(r.p);
+    } else {
+        m_reject(n, proposer);
+    }
+    return OK;
+}
+
+/* Learner::OnLearn (+ Proposer::OnLearn's equality ASSERT, Acceptor::OnLearn),
+ * member/paxos.cpp:1029-1060,1396-1400,1786-1793 */
+static int m_on_learn(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 20) return E_DECODE;
+    u32 proposer = rd32(m + 4);
+    u64 learn = rd64(m + 8);
+    u32 vlen = rd32(m + 16);
+    if (20 + (size_t)vlen > len) return E_DECODE;
+    pent_t *v; size_t k;
+    int rc = parse_pvalues(c, n, m, 20, 20 + vlen, seq, 1, &v, &k);
+    if (rc) return rc;
+    if (proposer >= c->N) violate(c, n, 3, seq, 0);
+    for (size_t i = 0; i < k; ++i) {
+        ent_t *l = map_find(&n->com, v[i].iid);
+        if (l) {
+            if (n->prop_exists && l->b != v[i].h) violate(c, n, 6, seq, v[i].iid);   /* :1398-1399 */
+        }
+        map_del(&n->acc, v[i].iid);                         /* :1790-1791 */
+        if (!l) map_put(&n->com, v[i].iid, v[i].pid, v[i].h);   /* insert, :1040 */
+        n->L++;
+    }
+    free(v);
+    for (;;) {                                              /* :1042-1053 */
+        ent_t *e = map_find(&n->com, n->next_apply);
+        if (!e) break;
+        n->next_apply++;
+        u64 h = e->b;
+        if ((h >> 47) & 1) continue;                        /* noop, :1064 */
+        const valrec_t *r2 = vt_get(&c->vt, h);
+        if (r2 && r2->exec_off == 0xFFFFFFFFu) continue;    /* membership: ChangeMemberships, :1066-1069 */
+        u32 el = r2 ? r2->exec_len : 0;
+        bput32(&n->exec, el);
+        if (el) bput(&n->exec, c->vt.bytes.p + r2->off + r2->exec_off, el);
+        n->n_exec++;
+    }
+    buf_t r = {0};
+    bput32(&r, 6); bput32(&r, n->index); bput64(&r, learn);   /* LearnReplyMsg, :1055-1059 */
+    emit(n, proposer, &r);
+    free(r.p);
+    return OK;
+}
+
+/* Proposer::OnPrepareReply + UpdateByPreAcceptedValues, member/paxos.cpp:1158-1182,1571-1586 */
+static int m_on_prepare_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 20) return E_DECODE;
+    u32 acceptor = rd32(m + 4);
+    u64 id = rd64(m + 8);
+    u32 vlen = rd32(m + 16);
+    if (20 + (size_t)vlen > len) return E_DECODE;
+    pent_t *v; size_t k;
+    const int live = n->prop_exists && n->preparing && id == n->proposal_id;     /* :1160 */
+    int rc = parse_pvalues(c, n, m, 20, 20 + vlen, seq, live, &v, &k);
+    if (rc) return rc;
+    const epoch_t *ep = &c->ep[n->epoch];
+    if (!live) { free(v); return OK; }
+    if (acceptor >= 64 || !((ep->amask >> acceptor) & 1)) { violate(c, n, 3, seq, 0); free(v); return OK; }   /* :1163 */
+    n->promised_set |= 1ull << acceptor;
+    for (size_t i = 0; i < k; ++i) {
+        ent_t *e = map_find(&n->pre, v[i].iid);
+        if (e) { if (v[i].pid > e->a) { e->a = v[i].pid; e->b = v[i].h; } }   /* strict >, :1580 */
+        else map_put(&n->pre, v[i].iid, v[i].pid, v[i].h);
+    }
+    free(v);
+    if ((u64)__builtin_popcountll(n->promised_set) >= (u64)__builtin_popcountll(ep->amask) / 2 + 1) {   /* :1171 */
+        size_t q;
+        ent_t *pv = map_sorted(&n->pre, &q);
+        bput64(&n->events_q, seq);
+        bput64(&n->events_q, n->proposal_id);
+        bput64(&n->events_q, q);
+        for (size_t i = 0; i < q; ++i) {
+            bput64(&n->events_q, pv[i].key);
+            bput64(&n->events_q, pv[i].a);
+            bput64(&n->events_q, pv[i].b);
+        }
+        n->n_q++;
+        free(pv);
+        for (size_t i = 0; i < n->nb; ++i)                 /* :1182 */
+            if (n->batches[i].live) { violate(c, n, 5, seq, 0); break; }
+        n->promised_set = 0;
+        n->preparing = 0;
+        map_clear(&n->pre);
+    }
+    return OK;
+}
+
+/* Proposer::OnAcceptReply, member/paxos.cpp:1317-1343: matched by batch id only */
+static int m_on_accept_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 16) return E_DECODE;
+    u32 acceptor = rd32(m + 4);
+    u64 accept = rd64(m + 8);
+    if (!n->prop_exists) return OK;
+    ent_t *e = map_find(&n->batch_idx, accept);
+    if (!e || !n->batches[e->a].live) return OK;            /* :1319 */
+    const epoch_t *ep = &c->ep[n->epoch];
+    if (acceptor >= 64 || !((ep->amask >> acceptor) & 1)) { violate(c, n, 3, seq, 0); return OK; }   /* :1324 */
+    batch_t *b = &n->batches[e->a];
+    b->mask |= 1ull << acceptor;
+    if ((u64)__builtin_popcountll(b->mask) >= (u64)__builtin_popcountll(ep->amask) / 2 + 1) {   /* :1327 */
+        bput64(&n->events_c, seq);
+        bput64(&n->events_c, accept);
+        n->n_c++;
+        b->live = 0;                                        /* :1340-1342 */
+    }
+    return OK;
+}
+
+/* member P_BATCH: entries carry their proposal id like AcceptingValues' map */
+static int m_on_p_batch(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 16) return E_DECODE;
+    u64 bid = rd64(m + 4);
+    u32 vlen = rd32(m + 12);
+    if (16 + (size_t)vlen > len) return E_DECODE;
+    pent_t *v; size_t k;
+    int rc = parse_pvalues(c, n, m, 16, 16 + vlen, seq, 0, &v, &k);
+    if (rc) return rc;
+    if (!n->prop_exists) { free(v); return OK; }
+    if (n->nb == n->cb) {
+        size_t cc = n->cb ? n->cb * 2 : 16;
+        batch_t *q = (batch_t *)realloc(n->batches, cc * sizeof(batch_t));
+        if (!q) { free(v); return E_NOMEM; }
+        n->batches = q; n->cb = cc;
+    }
+    batch_t *b = &n->batches[n->nb];
+    b->batch_id = bid; b->mask = 0; b->live = 1;
+    b->ent_off = n->nbent; b->ent_n = k;
+    if (n->nbent + 2 * k > n->cbent) {
+        size_t cc = n->cbent ? n->cbent : 64;
+        while (cc < n->nbent + 2 * k) cc *= 2;
+        u64 *q = (u64 *)realloc(n->bent, cc * sizeof(u64));
+        if (!q) { free(v); return E_NOMEM; }
+        n->bent = q; n->cbent = cc;
+    }
+    for (size_t i = 0; i < k; ++i) { n->bent[n->nbent++] = v[i].iid; n->bent[n->nbent++] = v[i].h; }
+    free(v);
+    map_put(&n->batch_idx, bid, n->nb, 0);
+    n->nb++;
+    return OK;
+}
+
+/* E_EPOCH marker: one step of ChangeMemberships as seen by this node */
+static int m_on_epoch(ctx_t *c, node_t *n, const u8 *m, size_t len)
+{
+    if (len < 8) return E_DECODE;
+    u32 e = rd32(m + 4);
+    if (e >= c->ne) return E_DECODE;
+    const epoch_t *o = &c->ep[n->epoch], *x = &c->ep[e];
+    int acc = (int)((x->amask >> n->index) & 1), prop = (int)((x->pmask >> n->index) & 1);
+    if (n->acc_exists != acc) {                             /* new / delete Acceptor, :1897-1901,1952-1957 */
+        map_clear(&n->acc);
+        n->promised = n->max_seen = 0;
+        n->acc_exists = acc;
+    }
+    if (n->prop_exists != prop || (prop && o->amask != x->amask)) {
+        /* Proposer deleted (:1927-1930), created (:1879-1883), or
+         * AcceptorsChanged (:1291-1322): idle until the next P_START */
+        n->preparing = 0;
+        n->promised_set = 0;
+        map_clear(&n->pre);
+        for (size_t i = 0; i < n->nb; ++i) n->batches[i].live = 0;
+        n->prop_exists = prop;
+    }
+    n->epoch = e;
+    return OK;
+}
+
+static int process_member(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 4) return E_DECODE;
+    switch (rd32(m)) {
+    case 0:  return m_on_prepare(c, n, m, len, seq);
+    case 1:  return m_on_prepare_reply(c, n, m, len, seq);
+    case 2:  return len < 12 ? E_DECODE : OK;              /* Proposer::OnReject: proposer-side max only */
+    case 3:  return m_on_accept(c, n, m, len, seq);
+    case 4:  return m_on_accept_reply(c, n, m, len, seq);
+    case 5:  return m_on_learn(c, n, m, len, seq);
+    case 6:  return len < 16 ? E_DECODE : OK;              /* OnLearnReply: out of scope */
+    case 16:
+        if (len < 12) return E_DECODE;
+        if (n->prop_exists) on_p_start(n, m, len);
+        return OK;
+    case 17: return m_on_p_batch(c, n, m, len, seq);
+    case 18: return m_on_epoch(c, n, m, len);
+    default: return E_DECODE;
+    }
+}
+
 /* ---- container -------------------------------------------------------------*/
 #define HDR 40
 
@@ -666,14 +1065,26 @@ int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64
     c.sem = rd32(trace + 12);
     c.M = rd64(trace + 16);
     u32 ne = rd32(trace + 24);
-    if (c.N == 0 || c.N > 64 || c.sem != 0) return -1;   /* member: oracle/mpx_oracle_member (later) */
-    size_t pos = HDR + (size_t)ne * 16;
+    if (c.N == 0 || c.N > 64 || c.sem > 1) return -1;
+    if (c.sem == 1 && (ne == 0 || size < HDR + (u64)ne * 24)) return E_DECODE;
+    size_t pos = HDR + (size_t)ne * 24;
     c.nodes = (node_t *)calloc(c.N, sizeof(node_t));
-    if (!c.nodes) return E_NOMEM;
+    c.ne = ne;
+    c.ep = (epoch_t *)calloc(ne ? ne : 1, sizeof(epoch_t));
+    if (!c.nodes || !c.ep) { free(c.nodes); free(c.ep); return E_NOMEM; }
+    for (u32 e = 0; e < ne; ++e) {
+        c.ep[e].version = rd32(trace + HDR + 24 * e);
+        c.ep[e].amask = rd64(trace + HDR + 24 * e + 8);
+        c.ep[e].pmask = rd64(trace + HDR + 24 * e + 16);
+    }
     int rc = OK;
     for (u32 i = 0; i < c.N && rc == OK; ++i) {
         node_t *n = &c.nodes[i];
         n->index = i;
+        if (c.sem == 1) {                                  /* genesis roles: epoch 0 */
+            n->acc_exists = (int)((c.ep[0].amask >> i) & 1);
+            n->prop_exists = (int)((c.ep[0].pmask >> i) & 1);
+        }
         if (pos + 16 > size) { rc = E_DECODE; break; }
         u64 cnt = rd64(trace + pos), nbytes = rd64(trace + pos + 8);
         pos += 16;
@@ -683,7 +1094,8 @@ int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64
         for (u64 k = 0; k < cnt && rc == OK; ++k) {
             u64 a = rd64(offs + 8 * k), b = rd64(offs + 8 * (k + 1));
             if (b < a || b > nbytes) { rc = E_DECODE; break; }
-            rc = process(&c, n, bytes + a, (size_t)(b - a), k);
+            rc = c.sem ? process_member(&c, n, bytes + a, (size_t)(b - a), k)
+                       : process(&c, n, bytes + a, (size_t)(b - a), k);
         }
         pos += 8 * (cnt + 1) + nbytes;
         pos = (pos + 7) & ~(size_t)7;
@@ -697,6 +1109,7 @@ int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64
         free(n->sends.p); free(n->events_q.p); free(n->events_c.p); free(n->exec.p);
     }
     free(c.nodes);
+    free(c.ep);
     map_free(&c.vt.idx); free(c.vt.v); free(c.vt.bytes.p);
     return rc;
 }

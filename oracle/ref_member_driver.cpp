@@ -1,0 +1,427 @@
+// ref_member_driver.cpp — drives the REFERENCE's own member handlers.  TEST INFRASTRUCTURE ONLY.
+//
+// Built by oracle/Makefile into oracle/_ref/libmpx_ref_member.so, only where
+// /root/reference exists.  The reference source is compiled where it lies:
+// this translation unit #includes /root/reference/member/paxos.cpp; nothing of
+// it is copied here.
+//
+// Technique: `private` is widened; every node is a real
+// NodeImpl whose Acceptor / Learner / Proposer objects are the reference's, and
+// each record of the node's stream is dispatched exactly as NodeImpl::Loop does
+// (member/paxos.cpp:749-790), single-threaded: NodeImpl::Init (which starts the
+// paxos thread) is never called.  The abstract platform interfaces of indet.h
+// (Thread, SpinLock, AtomicBool, Clock) get trivial single-thread
+// implementations; NetWork::Send is captured, StateMachine::Apply recorded.
+//
+// Membership: the reference applies learned membership Values itself
+// (Learner::Apply -> NodeImpl::ChangeMemberships, :1062-1073,1864-1964).  The
+// trace's E_EPOCH markers are CHECKED against what it did: before every
+// non-marker record the node's version_, acceptors_, proposer_ and acceptor_
+// must equal the marker-driven epoch (else mpxref_member_run returns -11).
+// Proposer control plane (out of scope) is held still as in the multi driver:
+// P_START / P_BATCH set what StartPrepare / Accept would, a proposer that was
+// created or saw its acceptor set change is made idle at the marker (the engine
+// model, include/mpx.h), and batches / learns its own decision code creates are
+// discarded (their sends are proposer broadcasts, not in-scope replies).
+//
+// Output: the canonical MPXR result.
+
+#include <string.h>
+#include <stdarg.h>
+#include <stdlib.h>
+#include <stdio.h>
+#include <stdint.h>
+#include <set>
+#include <map>
+#include <list>
+#include <deque>
+#include <vector>
+#include <string>
+#include <algorithm>
+#include <sstream>
+
+#define private public
+#define protected public
+#include "/root/reference/member/paxos.cpp"
+#undef private
+#undef protected
+
+namespace {
+
+typedef unsigned long long u64;
+
+struct DLock : public SpinLock {
+    void Lock(const Thread *) {}
+    void Unlock() {}
+};
+struct DBool : public AtomicBool {
+    explicit DBool(bool b) : AtomicBool(b) {}
+    void Set(bool b, const Thread *) { b_ = b; }
+    bool Get(const Thread *) { return b_; }
+};
+struct DThread : public Thread {
+    DThread() : Thread(std::vector<ThreadID>(1, 0), "ref", "/tmp", Rand(0), 0) {}
+    void USleep(unsigned long long) {}
+    void Sleep(unsigned long long) {}
+    SpinLock *NewSpinLock(const std::string &) { return new DLock; }
+    AtomicBool *NewAtomicBool(bool b, const std::string &) { return new DBool(b); }
+    Thread *NewThread(const std::vector<ThreadID> &, const std::string &, const std::string &, const Rand &,
+                      unsigned long long) { return new DThread; }
+    FILE *OpenClockLog(const std::string &) { return NULL; }
+};
+struct FrozenClock : public Clock {
+    TimeStamp Now(const Thread *) { return 1000; }
+};
+
+struct Sent { uint32_t dst; std::string bytes; };
+
+struct CapNet : public paxos::NetWork {
+    std::vector<Sent> *out;
+    void Send(Thread *, paxos::NodeID node, const std::string &msg) { out->push_back(Sent{node, msg}); }
+};
+struct RecSM : public paxos::StateMachine {
+    std::vector<std::string> executed;
+    bool Apply(Thread *, const std::string &v, std::string *) { executed.push_back(v); return true; }
+};
+
+u64 handle_of(const paxos::Value &v) { return ((u64)v.proposer_ << 48) | ((u64)(v.noop_ ? 1 : 0) << 47) | v.value_id_; }
+
+template <typename T> void put(std::string &b, T v) { b.append((const char *)&v, sizeof v); }
+uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+u64 rd64(const uint8_t *p) { u64 v; memcpy(&v, p, 8); return v; }
+
+struct Epoch { uint32_t version; u64 amask, pmask; };
+
+typedef std::map<paxos::InstanceID, paxos::ProposalValue> PVMap;
+
+struct Node {
+    paxos::NodeImpl *impl;
+    CapNet net;
+    RecSM sm;
+    std::vector<Sent> sends;
+    std::string events_q; u64 n_q = 0;
+    std::string events_c; u64 n_c = 0;
+    std::map<paxos::AcceptingID, std::map<paxos::InstanceID, u64> > batch_values;
+    paxos::Proposer *prefilled = NULL;
+    std::map<paxos::ValueID, paxos::ProposedValue> own_values;   // Values this node proposed (its LEARNs)
+    std::map<paxos::InstanceID, paxos::ValueID> own_iids;
+    uint32_t epoch = 0;
+    u64 P = 0, A = 0, L = 0;
+};
+
+DThread *g_thread;
+paxos::PrepareRetryTimeout *g_dummy_prt;
+
+u64 set_mask(const std::set<paxos::NodeID> &s)
+{
+    u64 m = 0;
+    for (paxos::NodeID x : s) if (x < 64) m |= 1ull << x;
+    return m;
+}
+
+// reference node == marker-driven epoch?
+bool consistent(const Node &n, uint32_t id, const Epoch &e)
+{
+    const paxos::NodeImpl *p = n.impl;
+    return p->version_ == e.version && set_mask(p->acceptors_) == e.amask &&
+           (p->acceptor_ != NULL) == (bool)((e.amask >> id) & 1) &&
+           (p->proposer_ != NULL) == (bool)((e.pmask >> id) & 1);
+}
+
+// Proposer bookkeeping Propose() would have filled (Proposer::OnLearn asserts
+// on it, member/paxos.cpp:1402-1424): the Values this node proposed, at the
+// instance each was first learned at.
+void prefill(Node &n)
+{
+    paxos::Proposer *p = n.impl->proposer_;
+    if (!p || p == n.prefilled) return;
+    n.prefilled = p;
+    const PVMap &learned = n.impl->learner_.learned_values_;
+    for (auto &e : n.own_iids) {
+        if (learned.count(e.first)) continue;
+        p->unlearned_proposed_values_.insert(std::make_pair(e.second, n.own_values[e.second]));
+        p->initial_proposals_.insert(e);
+    }
+}
+
+void make_idle(paxos::Proposer *p)
+{
+    if (p->prepare_delay_) { p->prepare_delay_->Cancel(); p->prepare_delay_ = NULL; }
+    if (p->prepare_retry_timeout_) { p->prepare_retry_timeout_->Cancel(); p->prepare_retry_timeout_ = NULL; }
+    p->prepare_promised_.clear();
+    p->pre_accepted_values_.clear();
+    for (auto &e : p->accepting_values_) e.second->retry_timeout_->Cancel();
+    p->accepting_values_.clear();
+}
+
+void discard_new_batches(paxos::Proposer *p, const std::set<paxos::AcceptingID> &before)
+{
+    if (!p) return;
+    for (auto it = p->accepting_values_.begin(); it != p->accepting_values_.end();) {
+        if (!before.count(it->first)) {
+            it->second->retry_timeout_->Cancel();
+            it = p->accepting_values_.erase(it);
+        } else ++it;
+    }
+}
+
+int parse_pvalues(Logger *lg, const uint8_t *buf, uint32_t len, PVMap *out)
+{
+    paxos::ExtractProposalValues(lg, g_thread, (const char *)buf, len, out);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size,
+                                 uint64_t *stats)
+{
+    if (size < 40 || memcmp(trace, "MPXT", 4)) return -4;
+    uint32_t N = rd32(trace + 8), sem = rd32(trace + 12), ne = rd32(trace + 24);
+    if (sem != 1 || N == 0 || N > 64 || ne == 0) return -1;
+    std::vector<Epoch> ep(ne);
+    for (uint32_t e = 0; e < ne; ++e) {
+        ep[e].version = rd32(trace + 40 + 24 * e);
+        ep[e].amask = rd64(trace + 48 + 24 * e);
+        ep[e].pmask = rd64(trace + 56 + 24 * e);
+    }
+    // the reference starts every node in {first} (NodeImpl::Loop, :738-747)
+    if (ep[0].amask == 0 || (ep[0].amask & (ep[0].amask - 1)) || ep[0].pmask != ep[0].amask || ep[0].version != 0)
+        return -1;
+    const uint32_t first = (uint32_t)__builtin_ctzll(ep[0].amask);
+
+    // Platform objects outlive the call on purpose (the leaked NodeImpls and
+    // their queued timeouts point into them), like the multi driver.
+    if (!g_thread) g_thread = new DThread;
+    FrozenClock &clock = *new FrozenClock;
+    Logger &logger = *new Logger(new DLock, &clock, 7);   // above CRITICAL: silent (ASSERT still crashes)
+    Timer &timer = *new Timer(&logger);
+    Rand &rand = *new Rand(0);
+    paxos::Callback &cb = *new paxos::Callback;
+    paxos::Config cfg;
+
+    std::vector<const uint8_t *> offs(N), bytes(N);
+    std::vector<u64> cnt(N);
+    size_t pos = 40 + (size_t)ne * 24;
+    for (uint32_t i = 0; i < N; ++i) {
+        if (pos + 16 > size) return -4;
+        cnt[i] = rd64(trace + pos);
+        u64 nb = rd64(trace + pos + 8);
+        pos += 16;
+        offs[i] = trace + pos;
+        bytes[i] = trace + pos + 8 * (cnt[i] + 1);
+        pos += 8 * (cnt[i] + 1) + nb;
+        pos = (pos + 7) & ~(size_t)7;
+        if (pos > size + 7) return -4;
+    }
+
+    std::vector<Node> ns(N);
+    for (uint32_t i = 0; i < N; ++i) {
+        Node &n = ns[i];
+        n.net.out = &n.sends;
+        n.impl = new paxos::NodeImpl(g_thread, i, first, &logger, &clock, &timer, &rand, &cb, &n.net, &n.sm, cfg);
+        n.impl->thread_ = g_thread;
+        n.net.node_ = n.impl;
+        // own Values, first learned position
+        for (u64 k = 0; k < cnt[i]; ++k) {
+            const uint8_t *m = bytes[i] + rd64(offs[i] + 8 * k);
+            if (rd32(m) != 5) continue;
+            PVMap vals;
+            parse_pvalues(&logger, m + 20, rd32(m + 16), &vals);
+            for (auto &e : vals) {
+                const paxos::Value &v = e.second.value_;
+                if (v.proposer_ != i || v.noop_ || n.own_values.count(v.value_id_)) continue;
+                paxos::ProposedValue pv;
+                pv.membership_changes_ = v.membership_changes_ ? new std::vector<paxos::MembershipChange>(*v.membership_changes_) : NULL;
+                pv.value_ = v.value_;
+                pv.cb_ = v.cb_;
+                n.own_values[v.value_id_] = pv;
+                n.own_iids[e.first] = v.value_id_;
+            }
+        }
+        // NodeImpl::Loop prologue (:738-747)
+        paxos::NodeImpl *p = n.impl;
+        p->learners_.insert(first);
+        p->proposers_.insert(first);
+        p->acceptors_.insert(first);
+        if (first == i) {
+            p->proposer_ = new paxos::Proposer(p);
+            p->acceptor_ = new paxos::Acceptor(p);
+            make_idle(p->proposer_);     // the engine model: idle until P_START
+            prefill(n);
+        }
+    }
+    if (!g_dummy_prt) g_dummy_prt = new paxos::PrepareRetryTimeout(NULL, 1000000);
+
+    for (uint32_t i = 0; i < N; ++i) {
+        Node &n = ns[i];
+        paxos::NodeImpl *ni = n.impl;
+        for (u64 k = 0; k < cnt[i]; ++k) {
+            u64 a = rd64(offs[i] + 8 * k), b = rd64(offs[i] + 8 * k + 8);
+            const uint8_t *m = bytes[i] + a;
+            if (b - a < 4) return -4;
+            uint32_t type = rd32(m);
+            if (type != 18 && !consistent(n, i, ep[n.epoch])) return -11;   // an E_EPOCH marker is missing
+            size_t before = n.sends.size();
+            paxos::Proposer *pr = ni->proposer_;
+            std::set<paxos::AcceptingID> before_b;
+            if (pr) for (auto &e : pr->accepting_values_) before_b.insert(e.first);
+            switch (type) {
+            case 0:
+                if (ni->acceptor_) ni->acceptor_->OnPrepare((const paxos::PrepareMsg *)m);
+                break;
+            case 1: {
+                if (!pr) break;
+                const paxos::PrepareReplyMsg *msg = (const paxos::PrepareReplyMsg *)m;
+                bool live = pr->prepare_retry_timeout_ && msg->id_ == pr->proposal_id_;
+                bool quorum_next = live && [&] {
+                    std::set<paxos::NodeID> s = pr->prepare_promised_;
+                    s.insert(msg->acceptor_);
+                    return s.size() >= ni->acceptors_.size() / 2 + 1;
+                }();
+                if (quorum_next) {
+                    // snapshot the merged map with the reference's own merge
+                    PVMap saved(pr->pre_accepted_values_);
+                    PVMap vals;
+                    parse_pvalues(&logger, (const uint8_t *)msg->values_, msg->len_, &vals);
+                    pr->UpdateByPreAcceptedValues(vals);
+                    put<u64>(n.events_q, k); put<u64>(n.events_q, pr->proposal_id_);
+                    put<u64>(n.events_q, pr->pre_accepted_values_.size());
+                    for (auto &e : pr->pre_accepted_values_) {
+                        put<u64>(n.events_q, e.first);
+                        put<u64>(n.events_q, e.second.proposal_id_);
+                        put<u64>(n.events_q, handle_of(e.second.value_));
+                    }
+                    n.n_q++;
+                    pr->pre_accepted_values_.swap(saved);
+                }
+                pr->OnPrepareReply(msg);
+                discard_new_batches(pr, before_b);
+                break;
+            }
+            case 2:
+                if (pr) pr->OnReject((const paxos::RejectMsg *)m);
+                break;
+            case 3: {
+                paxos::Acceptor *ac = ni->acceptor_;
+                if (!ac) break;
+                const paxos::AcceptMsg *msg = (const paxos::AcceptMsg *)m;
+                if (msg->version_ == ni->version_ && msg->id_ >= ac->promised_proposal_id_) {
+                    PVMap vals;
+                    parse_pvalues(&logger, (const uint8_t *)msg->values_, msg->len_, &vals);
+                    const PVMap &learned = ni->learner_.learned_values_;
+                    for (auto &e : vals)
+                        if (!learned.count(e.first) && !ac->accepted_values_.count(e.first)) n.A++;
+                }
+                ac->OnAccept(msg);
+                break;
+            }
+            case 4: {
+                if (!pr) break;
+                const paxos::AcceptReplyMsg *msg = (const paxos::AcceptReplyMsg *)m;
+                bool live = pr->accepting_values_.count(msg->accept_) != 0;
+                pr->OnAcceptReply(msg);
+                if (live && !pr->accepting_values_.count(msg->accept_)) {
+                    put<u64>(n.events_c, k); put<u64>(n.events_c, msg->accept_);
+                    n.n_c++;
+                }
+                break;
+            }
+            case 5: {
+                const paxos::LearnMsg *msg = (const paxos::LearnMsg *)m;
+                n.L += [&] { PVMap v; parse_pvalues(&logger, (const uint8_t *)msg->values_, msg->len_, &v); return (u64)v.size(); }();
+                ni->learner_.OnLearn(msg);
+                discard_new_batches(ni->proposer_ == pr ? pr : NULL, before_b);
+                break;
+            }
+            case 6:
+                break;     // OnLearnReply: learn-retry bookkeeping, out of scope
+            case 16:       // P_START
+                if (pr) {
+                    make_idle(pr);
+                    pr->proposal_id_ = rd64(m + 4);
+                    pr->prepare_retry_timeout_ = g_dummy_prt;
+                }
+                break;
+            case 17: {     // P_BATCH
+                if (!pr) break;
+                u64 bid = rd64(m + 4);
+                PVMap vals;
+                parse_pvalues(&logger, m + 16, rd32(m + 12), &vals);
+                paxos::AcceptingValues *acc = new paxos::AcceptingValues(bid, vals);
+                acc->retry_timeout_ = new paxos::AcceptRetryTimeout(pr, acc, 1000000);
+                pr->accepting_values_[bid] = acc;
+                for (auto &e : vals) n.batch_values[bid][e.first] = handle_of(e.second.value_);
+                break;
+            }
+            case 18: {     // E_EPOCH
+                uint32_t e = rd32(m + 4);
+                if (e >= ne) return -4;
+                const Epoch &o = ep[n.epoch], &x = ep[e];
+                bool was = (o.pmask >> i) & 1, now = (x.pmask >> i) & 1;
+                n.epoch = e;
+                if (now && ni->proposer_ && (!was || o.amask != x.amask)) make_idle(ni->proposer_);
+                prefill(n);
+                break;
+            }
+            default: return -4;
+            }
+            // keep only the acceptor / learner replies (types 1,2,4,6)
+            std::vector<Sent> keep(n.sends.begin(), n.sends.begin() + before);
+            for (size_t j = before; j < n.sends.size(); ++j) {
+                uint32_t t = rd32((const uint8_t *)n.sends[j].bytes.data());
+                if (t == 1 || t == 2 || t == 4 || t == 6) keep.push_back(n.sends[j]);
+                if (t == 1) {
+                    const paxos::PrepareReplyMsg *r = (const paxos::PrepareReplyMsg *)n.sends[j].bytes.data();
+                    PVMap vals;
+                    parse_pvalues(&logger, (const uint8_t *)r->values_, r->len_, &vals);
+                    n.P += vals.size();
+                }
+            }
+            n.sends.swap(keep);
+        }
+        if (!consistent(n, i, ep[n.epoch])) return -11;
+    }
+
+    // canonical MPXR dump
+    std::string r;
+    r.append("MPXR", 4);
+    put<uint32_t>(r, 1); put<uint32_t>(r, N); put<uint32_t>(r, 1);
+    u64 P = 0, A = 0, L = 0;
+    std::map<u64, u64> chosen;
+    for (uint32_t i = 0; i < N; ++i) {
+        Node &n = ns[i];
+        paxos::NodeImpl *ni = n.impl;
+        paxos::Acceptor *ac = ni->acceptor_;
+        put<u64>(r, ac ? ac->promised_proposal_id_ : 0);
+        put<u64>(r, ac ? ac->max_proposal_id_ : 0);
+        std::map<u64, std::pair<u64, const paxos::ProposalValue *> > st;
+        if (ac) for (auto &e : ac->accepted_values_) st[e.first] = std::make_pair(1ull, &e.second);
+        for (auto &e : ni->learner_.learned_values_) st[e.first] = std::make_pair(2ull, &e.second);
+        put<u64>(r, st.size());
+        for (auto &e : st) {
+            put<u64>(r, e.first); put<u64>(r, e.second.first);
+            put<u64>(r, e.second.second->proposal_id_); put<u64>(r, handle_of(e.second.second->value_));
+        }
+        put<u64>(r, n.sends.size());
+        for (auto &s : n.sends) { put<uint32_t>(r, s.dst); put<uint32_t>(r, (uint32_t)s.bytes.size()); r += s.bytes; }
+        put<u64>(r, n.n_q); r += n.events_q;
+        put<u64>(r, n.n_c); r += n.events_c;
+        put<u64>(r, n.sm.executed.size());
+        for (auto &s : n.sm.executed) { put<uint32_t>(r, (uint32_t)s.size()); r += s; }
+        P += n.P; A += n.A; L += n.L;
+        for (u64 k = 0; k < n.n_c; ++k) {
+            u64 bid = rd64((const uint8_t *)n.events_c.data() + 16 * k + 8);
+            for (auto &e : n.batch_values[bid]) chosen.insert(e);
+        }
+    }
+    put<u64>(r, chosen.size());
+    for (auto &e : chosen) { put<u64>(r, e.first); put<u64>(r, e.second); }
+    if (stats) { stats[0] = chosen.size(); stats[1] = P; stats[2] = A; stats[3] = L; }
+    *out = (uint8_t *)malloc(r.size());
+    if (!*out) return -2;
+    memcpy(*out, r.data(), r.size());
+    *out_size = r.size();
+    // NodeImpl objects are leaked on purpose (their dtors expect a joined thread).
+    return 0;
+}

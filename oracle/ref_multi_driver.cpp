@@ -133,7 +133,7 @@ extern "C" int mpxref_run(const uint8_t *trace, uint64_t size, uint8_t **out, ui
     // locate node sections
     std::vector<const uint8_t *> offs(N), bytes(N);
     std::vector<u64> cnt(N);
-    size_t pos = 40 + (size_t)ne * 16;
+    size_t pos = 40 + (size_t)ne * 24;
     for (uint32_t i = 0; i < N; ++i) {
         if (pos + 16 > size) return -4;
         cnt[i] = rd64(trace + pos);
@@ -345,7 +345,7 @@ extern "C" int64_t mpxref_time_node(const uint8_t *trace, uint64_t size, uint32_
     paxos::Paxos::Config cfg;
     paxos::NodeInfoMap nodes;
     for (uint32_t i = 0; i < N; ++i) nodes.insert(std::make_pair(i, paxos::NodeInfo("0.0.0.0", (unsigned short)i)));
-    size_t pos = 40 + (size_t)ne * 16;
+    size_t pos = 40 + (size_t)ne * 24;
     const uint8_t *offs = NULL, *bytes = NULL;
     u64 cnt = 0;
     for (uint32_t i = 0; i <= node && i < N; ++i) {

@@ -3,7 +3,9 @@
 Each fixture is a trace (.mpxt: MPXT container of per-node receive streams)
 and the result the REFERENCE's own handlers produce for it (.mpxr: canonical
 MPXR dump), computed by oracle/_ref/libmpx_ref.so — multi/paxos.cpp compiled
-in place from /root/reference (oracle/Makefile, oracle/ref_multi_driver.cpp).
+in place from /root/reference (oracle/Makefile, oracle/ref_multi_driver.cpp) —
+or, for member-semantics traces (mm_*, c5_*), by oracle/_ref/libmpx_ref_member.so
+(member/paxos.cpp, oracle/ref_member_driver.cpp).
 The reference itself cannot travel; these vectors are what the oracle and the
 engine are pinned against (tests/test_oracle.py, tests/test_engine_gpu.py).
 
@@ -19,6 +21,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 from fuzztrace import fuzz_trace  # noqa: E402
 from handmade import handmade_traces  # noqa: E402
+from handmade_member import member_traces  # noqa: E402
 from oracles import ref_available, ref_run  # noqa: E402
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "multi-paxos_amd"))
@@ -42,6 +45,15 @@ def main():
         cases["c3_faulty_%d" % seed] = mpx.generate_trace(
             mpx.GEN_FAULTY, num_nodes=7, num_instances=300, seed=seed, batch=32, proposers=3,
             drop_rate=500, dup_rate=1000, max_delay=500)
+    # member semantics (reference: member/paxos.cpp via oracle/_ref/libmpx_ref_member.so)
+    for name, trace in member_traces().items():
+        cases[name] = trace
+    for seed, (U, M, B, drop, dup, noop) in enumerate([(3, 64, 4, 0, 0, 0), (4, 200, 8, 0, 0, 0),
+                                                       (8, 1000, 16, 500, 100, 15), (8, 2000, 64, 1000, 300, 50),
+                                                       (6, 1500, 32, 0, 200, 0)]):
+        cases["c5_member_%d" % seed] = mpx.generate_trace(
+            mpx.GEN_MEMBER, num_nodes=U, num_instances=M, seed=seed, batch=B, drop_rate=drop,
+            dup_rate=dup, max_delay=64, noop_permille=noop)
     extra = os.path.join(HERE, "extra_traces")
     if os.path.isdir(extra):
         for fn in sorted(os.listdir(extra)):

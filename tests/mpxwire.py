@@ -78,14 +78,15 @@ def p_batch(batch_id, entries):
 
 
 def container(streams, num_instances=0, semantics=0, epochs=()):
-    """streams: list (per node) of lists of message bytes, in processing order."""
+    """streams: list (per node) of lists of message bytes, in processing order.
+    epochs (member): (version, acceptor_mask, proposer_mask) per epoch."""
     out = bytearray(b"MPXT")
     out += struct.pack("<III", 1, len(streams), semantics)
     out += struct.pack("<QII", num_instances, len(epochs), 0)
     out += struct.pack("<Q", 0)
     assert len(out) == 40
-    for ver, mask in epochs:
-        out += struct.pack("<IIQ", ver, 0, mask)
+    for ver, amask, pmask in epochs:
+        out += struct.pack("<IIQQ", ver, 0, amask, pmask)
     for msgs in streams:
         offs = [0]
         for m in msgs:
@@ -97,3 +98,68 @@ def container(streams, num_instances=0, semantics=0, epochs=()):
         while len(out) % 8:
             out += b"\0"
     return bytes(out)
+
+
+# ---- member semantics (member/paxos.cpp:321-440,846-932) ----------------------
+ADD_LEARNER, LEARNER_TO_PROPOSER, PROPOSER_TO_ACCEPTOR = 0, 1, 2
+DEL_LEARNER, PROPOSER_TO_LEARNER, ACCEPTOR_TO_PROPOSER = 3, 4, 5
+
+
+def mvalue(proposer, value_id, payload=None, cb=b"", noop=False, changes=None):
+    """FillValue (member): u32 proposer, u64 value_id, bool noop; unless noop:
+    bool membership, then u32 count + {u32 node, u32 type}* or u32 len + bytes;
+    then u32 cblen + cb."""
+    b = struct.pack("<IQ?", proposer, value_id, noop)
+    if noop:
+        return b
+    if isinstance(payload, str):
+        payload = payload.encode()
+    if isinstance(cb, str):
+        cb = cb.encode()
+    if changes is not None:
+        b += struct.pack("<?I", True, len(changes)) + b"".join(struct.pack("<II", n, t) for n, t in changes)
+    else:
+        b += struct.pack("<?I", False, len(payload)) + payload
+    return b + struct.pack("<I", len(cb)) + cb
+
+
+def m_entries(entries):
+    """(iid, pid, value_bytes) -> {u64 iid, u64 pid, Value_m}*"""
+    return b"".join(struct.pack("<QQ", i, p) + v for i, p, v in entries)
+
+
+def m_prepare(version, proposer, ballot, ranges=((0, U64_MAX_EXCL),)):
+    body = b"".join(struct.pack("<QQ", a, b) for a, b in ranges)
+    return struct.pack("<IIIQI", 0, version, proposer, ballot, len(body)) + body
+
+
+def m_prepare_reply(acceptor, ballot, entries=()):
+    body = m_entries(entries)
+    return struct.pack("<IIQI", 1, acceptor, ballot, len(body)) + body
+
+
+def m_accept(version, proposer, accept_id, ballot, entries):
+    body = m_entries(entries)
+    return struct.pack("<IIIQQI", 3, version, proposer, accept_id, ballot, len(body)) + body
+
+
+def m_accept_reply(acceptor, accept_id):
+    return struct.pack("<IIQ", 4, acceptor, accept_id)
+
+
+def m_learn(proposer, learn_id, entries):
+    body = m_entries(entries)
+    return struct.pack("<IIQI", 5, proposer, learn_id, len(body)) + body
+
+
+def m_learn_reply(learner, learn_id):
+    return struct.pack("<IIQ", 6, learner, learn_id)
+
+
+def m_p_batch(batch_id, entries):
+    body = m_entries(entries)
+    return struct.pack("<IQI", 17, batch_id, len(body)) + body
+
+
+def e_epoch(epoch):
+    return struct.pack("<II", 18, epoch)

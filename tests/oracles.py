@@ -2,6 +2,7 @@
 
   oracle/_build/libmpx_oracle.so : C restatement (oracle/mpx_oracle.c)
   oracle/_ref/libmpx_ref.so      : the reference's own handlers (oracle/ref_multi_driver.cpp)
+  oracle/_ref/libmpx_ref_member.so : the same for member/paxos.cpp (oracle/ref_member_driver.cpp)
 
 Both take an MPXT trace and return the canonical MPXR result bytes.
 """
@@ -11,6 +12,7 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libmpx_oracle.so")
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libmpx_ref.so")
+REF_MEMBER_SO = os.path.join(ROOT, "oracle", "_ref", "libmpx_ref_member.so")
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 
@@ -54,6 +56,7 @@ class _Runner:
 
 _oracle = None
 _ref = None
+_ref_member = None
 
 
 def oracle_run(trace):
@@ -65,12 +68,17 @@ def oracle_run(trace):
 
 
 def ref_available():
-    return os.path.exists(REF_SO)
+    return os.path.exists(REF_SO) and os.path.exists(REF_MEMBER_SO)
 
 
 def ref_run(trace):
-    """-> (mpxr bytes, [C,P,A,L])"""
-    global _ref
+    """-> (mpxr bytes, [C,P,A,L]); multi or member driver by the trace's semantics"""
+    global _ref, _ref_member
+    if trace[12:16] == b"\x01\x00\x00\x00":
+        if _ref_member is None:
+            _ref_member = _Runner(REF_MEMBER_SO, "mpxref_member_run", 4, False)
+        data, stats, _ = _ref_member(trace)
+        return data, stats
     if _ref is None:
         _ref = _Runner(REF_SO, "mpxref_run", 4, False)
     data, stats, _ = _ref(trace)

@@ -56,3 +56,56 @@ def test_oracle_matches_reference_live(seed):
 def test_oracle_rejects_unknown_type():
     with pytest.raises(RuntimeError):
         oracle_run(container([[struct.pack("<I", 9)]], 1))
+
+
+# ---- member semantics (member/paxos.cpp) -----------------------------------------
+import sys as _sys  # noqa: E402
+_sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "multi-paxos_amd"))
+import mpx as _mpx  # noqa: E402  (host generator only)
+from handmade_member import member_violation_traces, Member  # noqa: E402
+from mpxwire import e_epoch, m_learn, m_prepare  # noqa: E402
+
+
+@pytest.mark.ref
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("seed", range(200, 216))
+def test_member_oracle_matches_reference_live(seed):
+    U = 3 + seed % 6
+    trace = _mpx.generate_trace(_mpx.GEN_MEMBER, num_nodes=U, num_instances=300 + 37 * seed % 500, seed=seed,
+                                batch=1 + seed % 40, drop_rate=(seed % 3) * 700, dup_rate=(seed % 4) * 150,
+                                max_delay=32, noop_permille=seed % 30)
+    got, stats, viol = oracle_run(trace)
+    want, rstats = ref_run(trace)
+    assert got == want, mpxr.diff(got, want)
+    assert stats[:4] == rstats and stats[4] == 0
+
+
+def test_member_violations_recorded():
+    got, stats, viol = oracle_run(member_violation_traces()["mm_violations"])
+    # learned-value mismatch (Proposer::OnLearn :1398), accept of a learned instance
+    # with another Value (:1767), PREPARE_REPLY from a non-acceptor (:1163)
+    assert stats[4] == 3
+    assert viol[:2] == [6, 0]
+
+
+@pytest.mark.ref
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+def test_member_reference_checks_epoch_markers():
+    # node 1 learns AddAcceptor(1) but the trace omits its E_EPOCH marker: the
+    # reference driver refuses the trace (the epoch table would be a lie)
+    m = Member(2, 2)
+    m.streams[0] += [m_learn(0, 1, m.boot), e_epoch(1)]
+    m.streams[1] += [m_learn(0, 1, m.boot), m_prepare(1, 0, 5 << 16)]
+    with pytest.raises(RuntimeError, match="-11"):
+        ref_run(m.trace())
+
+
+def test_member_epoch_gates_roles():
+    # a node outside epoch 0's acceptor set ignores PREPARE; after E_EPOCH it answers
+    m = Member(2, 2)
+    m.streams[1] += [m_prepare(1, 0, 7 << 16), m_learn(0, 1, m.boot), e_epoch(1), m_prepare(1, 0, 7 << 16)]
+    got, stats, _ = oracle_run(m.trace())
+    res = mpxr.parse(got)
+    node1 = res["nodes"][1]
+    assert node1["promised"] == 7 << 16
+    assert [s[1][:4] for s in node1["sends"]][-1] == struct.pack("<I", 1)
