@@ -71,6 +71,7 @@ struct mpx_engine {
     uint32_t NB = 0;
     // device buffers
     DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, n_after_prepare, m_flags, m_maxseen;
+    DevBuf m_gate, e_pid, ep_amask;
     DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
     DevBuf f_off, frags, gp_list, ev_off, ev_msg, pl_off, pl_msg;
@@ -120,7 +121,8 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
     if (cfg->abi_version != MPX_ABI_VERSION) return MPX_E_INVAL;
     if (!cfg->num_nodes || cfg->num_nodes > MPX_MAX_NODES) return MPX_E_INVAL;
     if (cfg->shard_end <= cfg->shard_begin) return MPX_E_INVAL;
-    if (cfg->semantics != MPX_SEM_MULTI) return MPX_E_INVAL;    // member semantics: DESIGN.md §Next
+    if (cfg->semantics != MPX_SEM_MULTI && cfg->semantics != MPX_SEM_MEMBER) return MPX_E_INVAL;
+    if (cfg->semantics == MPX_SEM_MULTI && cfg->num_epochs) return MPX_E_INVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPX_E_NODEVICE;
     if (cfg->device < 0 || cfg->device >= n) return MPX_E_NODEVICE;
@@ -135,6 +137,7 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
     if (hipGetDeviceProperties(&prop, e->device) == hipSuccess && prop.multiProcessorCount > 0)
         e->num_cus = (uint32_t)prop.multiProcessorCount;
     e->nodes.resize(cfg->num_nodes);
+    e->vt.member = cfg->semantics == MPX_SEM_MEMBER;
     e->shard_len = cfg->shard_end - cfg->shard_begin;
     e->NB = (uint32_t)((e->shard_len + BS - 1) >> BSH);
     if ((uint64_t)e->NB * cfg->num_nodes > (1ull << 40)) return MPX_E_RANGE;
@@ -160,10 +163,13 @@ extern "C" int mpx_submit(mpx_engine *e, uint32_t node, const uint8_t *bytes, co
     if (e->device_trace) return MPX_E_STATE;
     const uint64_t t0 = now_ns();
     NodeStream &ns = e->nodes[node];
+    const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
     for (uint64_t i = 0; i < count; ++i) {
         if (offsets[i + 1] < offsets[i]) return MPX_E_INVAL;
-        int rc = decode_record(e->vt, ns, node, e->cfg.num_nodes, bytes + offsets[i], (size_t)(offsets[i + 1] - offsets[i]),
-                               e->cfg.shard_begin, e->cfg.shard_end, e->iv);
+        const uint8_t *m = bytes + offsets[i];
+        const size_t len = (size_t)(offsets[i + 1] - offsets[i]);
+        int rc = member ? decode_record_member(e->vt, ns, node, m, len, e->cfg.shard_begin, e->cfg.shard_end, e->iv)
+                        : decode_record(e->vt, ns, node, e->cfg.num_nodes, m, len, e->cfg.shard_begin, e->cfg.shard_end, e->iv);
         if (rc) return rc;
     }
     e->dirty = true;
@@ -177,8 +183,17 @@ static inline uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8
 extern "C" int mpx_submit_trace(mpx_engine *e, const uint8_t *t, uint64_t size)
 {
     if (!e || !t || size < 40 || std::memcmp(t, "MPXT", 4)) return MPX_E_INVAL;
-    const uint32_t N = rd32(t + 8), ne = rd32(t + 24);
-    if (N != e->cfg.num_nodes) return MPX_E_INVAL;
+    const uint32_t N = rd32(t + 8), sem = rd32(t + 12), ne = rd32(t + 24);
+    if (N != e->cfg.num_nodes || sem != e->cfg.semantics) return MPX_E_INVAL;
+    if (size < 40 + (uint64_t)ne * 24) return MPX_E_DECODE;
+    if (ne) {
+        // the container's epoch table: adopted by an engine created without
+        // one, else it must be the same table
+        std::vector<mpx_epoch> ep(ne);
+        std::memcpy(ep.data(), t + 40, (size_t)ne * 24);
+        if (e->epochs.empty()) e->epochs = ep;
+        else if (e->epochs.size() != ep.size() || std::memcmp(e->epochs.data(), ep.data(), (size_t)ne * 24)) return MPX_E_INVAL;
+    }
     size_t pos = 40 + (size_t)ne * 24;
     for (uint32_t n = 0; n < N; ++n) {
         if (pos + 16 > size) return MPX_E_DECODE;
@@ -240,9 +255,18 @@ static int finish_view(mpx_engine *e)
 static int upload_trace(mpx_engine *e)
 {
     const uint64_t t0 = now_ns();
-    TRY(build_trace(e->nodes, e->cfg.shard_begin, e->shard_len, e->ht));
+    const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
+    if (member && e->epochs.empty()) return MPX_E_STATE;        // no epoch table yet
+    TRY(build_trace(e->nodes, e->cfg.shard_begin, e->shard_len, member ? e->epochs : std::vector<mpx_epoch>(), e->ht));
     HostTrace &h = e->ht;
     hipStream_t s = e->stream;
+    {
+        std::vector<uint64_t> am;
+        for (auto &x : e->epochs) am.push_back(x.acceptor_mask);
+        TRY(upload(e->ep_amask, am, s));
+        TRY(upload(e->m_gate, h.m_gate, s));
+        TRY(upload(e->e_pid, h.e_pid, s));
+    }
     TRY(upload(e->m_type, h.m_type, s)); TRY(upload(e->m_src, h.m_src, s));
     TRY(upload(e->m_ballot, h.m_ballot, s)); TRY(upload(e->m_aux, h.m_aux, s));
     TRY(upload(e->m_ent, h.m_ent, s)); TRY(upload(e->m_cnt, h.m_cnt, s));
@@ -272,6 +296,8 @@ static int upload_trace(mpx_engine *e)
     v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
     v.n_after_prepare = e->n_after_prepare.as<uint32_t>();
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
+    v.m_gate = e->m_gate.as<uint32_t>(); v.e_pid = e->e_pid.as<uint64_t>();
+    v.ep_amask = e->ep_amask.as<uint64_t>(); v.num_epochs = (uint32_t)e->epochs.size();
     v.num_chunks = (uint32_t)h.chunk_node.size();
     v.chunk_node = e->chunk_node.as<uint32_t>(); v.chunk_beg = e->chunk_beg.as<uint64_t>();
     v.chunk_end = e->chunk_end.as<uint64_t>(); v.node_chunk_off = e->node_chunk_off.as<uint32_t>();
@@ -577,8 +603,9 @@ static void reply_of(const mpx_engine *e, const Results &r, uint32_t n, uint64_t
     } else if (t == MPX_MSG_ACCEPT) {
         if (f & F_GRANTED) {
             app<uint32_t>(m, MPX_MSG_ACCEPT_REPLY); app<uint32_t>(m, n);
-            app<uint64_t>(m, h.m_ballot[g]); app<uint64_t>(m, h.m_aux[g]);
-        } else {
+            if (e->cfg.semantics == MPX_SEM_MULTI) app<uint64_t>(m, h.m_ballot[g]);   // member: no ballot, :900-908
+            app<uint64_t>(m, h.m_aux[g]);
+        } else if (f & F_REJECT) {
             app<uint32_t>(m, MPX_MSG_REJECT); app<uint64_t>(m, r.maxseen[g]);
         }
     } else if (t == MPX_MSG_COMMIT) {
@@ -679,7 +706,7 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
             if (!(w & W_PRESENT) || !(w & W_COMMITTED)) break;
             const uint64_t hd = w & W_HANDLE;
             if (MPX_HANDLE_NOOP(hd)) continue;
-            e->vt.exec_payload(hd, payload);
+            if (!e->vt.exec_payload(hd, payload)) continue;         // member: a membership Value
             app<uint32_t>(sec, (uint32_t)payload.size());
             sec += payload;
             ++cnt;
@@ -726,7 +753,7 @@ extern "C" int mpx_trace_generate(const mpx_gen_params *p, uint8_t **out, uint64
 extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
 {
     if (!e || !p) return MPX_E_INVAL;
-    if (p->kind != MPX_GEN_CLEAN || p->num_nodes != e->cfg.num_nodes) return MPX_E_INVAL;
+    if (p->kind != MPX_GEN_CLEAN || p->num_nodes != e->cfg.num_nodes || e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_INVAL;
     if ((p->batch && p->batch != BS) || (e->cfg.shard_begin & (BS - 1))) return MPX_E_INVAL;
     if (e->cfg.shard_end > p->num_instances) return MPX_E_INVAL;
     HTRY(hipSetDevice(e->device));
@@ -804,6 +831,8 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
     v.n_after_prepare = e->n_after_prepare.as<uint32_t>();
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
+    v.m_gate = e->m_gate.as<uint32_t>(); v.e_pid = e->e_pid.as<uint64_t>();
+    v.ep_amask = e->ep_amask.as<uint64_t>(); v.num_epochs = (uint32_t)e->epochs.size();
     v.num_chunks = (uint32_t)h.chunk_node.size();
     v.chunk_node = e->chunk_node.as<uint32_t>(); v.chunk_beg = e->chunk_beg.as<uint64_t>();
     v.chunk_end = e->chunk_end.as<uint64_t>(); v.node_chunk_off = e->node_chunk_off.as<uint32_t>();

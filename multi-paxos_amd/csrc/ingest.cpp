@@ -19,10 +19,68 @@ static inline uint32_t rd32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4
 static inline uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 template <typename T> static inline void app(std::string &s, T v) { s.append((const char *)&v, sizeof v); }
 
+// member Value_m (FillValue / ExtractValue, member/paxos.cpp:330-408): the
+// multi layout plus a membership change list {u32 node, u32 type}* in place of
+// the payload and a u32-length cb after it.  Canonical bytes = wire bytes with
+// the bools normalised; membership Values are not executed (Learner::Apply,
+// :1062-1073), marked by exec_off = NONE32.
+static long parse_member(const uint8_t *p, size_t avail, std::string &enc, uint32_t &exec_off, uint32_t &exec_len)
+{
+    const bool noop = p[12] != 0;
+    size_t used = 13;
+    exec_off = exec_len = 0;
+    if (!noop) {
+        if (avail < 18) return MPX_E_DECODE;
+        const bool mem = p[13] != 0;
+        const uint32_t n = rd32(p + 14);
+        used = 18;
+        if (mem) {
+            if ((avail - used) / 8 < n) return MPX_E_DECODE;
+            used += 8 * (size_t)n;
+            exec_off = NONE32;
+        } else {
+            if (avail - used < n) return MPX_E_DECODE;
+            exec_off = (uint32_t)used;
+            exec_len = n;
+            used += n;
+        }
+        if (avail - used < 4) return MPX_E_DECODE;
+        const uint32_t cbl = rd32(p + used);
+        used += 4;
+        if (avail - used < cbl) return MPX_E_DECODE;
+        used += cbl;
+    }
+    enc.assign((const char *)p, used);
+    enc[12] = noop ? 1 : 0;
+    if (!noop) enc[13] = exec_off == NONE32 ? 1 : 0;
+    return (long)used;
+}
+
 long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle)
 {
     // FillValue / ExtractValue layout, multi/paxos.cpp:556-644
     if (avail < 13) return MPX_E_DECODE;
+    if (member) {
+        const uint32_t proposer = rd32(p);
+        const uint64_t value_id = rd64(p + 4);
+        if (proposer >= (1u << 14) || value_id >= (1ull << 47)) return MPX_E_RANGE;
+        std::string enc;
+        uint32_t eo, el;
+        const long used = parse_member(p, avail, enc, eo, el);
+        if (used < 0) return used;
+        const uint64_t h = MPX_HANDLE(proposer, p[12] != 0, value_id);
+        auto it = idx.find(h);
+        if (it != idx.end()) {
+            const Rec &r = it->second;
+            if (r.len != enc.size() || std::memcmp(bytes.data() + r.off, enc.data(), enc.size()) != 0)
+                return MPX_E_VALUE;
+        } else {
+            idx.emplace(h, Rec{bytes.size(), (uint32_t)enc.size(), eo, el});
+            bytes += enc;
+        }
+        *handle = h;
+        return used;
+    }
     const uint32_t proposer = rd32(p);
     const uint64_t value_id = rd64(p + 4);
     const bool noop = p[12] != 0;
@@ -104,6 +162,7 @@ bool ValueTable::exec_payload(uint64_t h, std::string &out) const
 {
     auto it = idx.find(h);
     if (it != idx.end()) {
+        if (it->second.exec_off == NONE32) return false;     // member: ChangeMemberships
         out.assign(bytes.data() + it->second.off + it->second.exec_off, it->second.exec_len);
         return true;
     }
@@ -113,6 +172,8 @@ bool ValueTable::exec_payload(uint64_t h, std::string &out) const
     }
     return false;
 }
+
+#define TRY_RC(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
 
 static void flag(IngestViolation &v, uint64_t code, uint64_t node, uint64_t seq, uint64_t iid)
 {
@@ -296,6 +357,136 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
     return MPX_OK;
 }
 
+int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const uint8_t *m, size_t len,
+                         uint64_t sb, uint64_t se, IngestViolation &viol)
+{
+    if (len < 4) return MPX_E_DECODE;
+    const uint32_t t = rd32(m);
+    const uint64_t seq = ns.type.size();
+    uint32_t src = 0, ver = 0;
+    uint64_t ballot = 0, aux = 0, ent = 0;
+    uint32_t cnt = 0;
+    auto keep_shard = [&](size_t first) {
+        size_t w = first;
+        for (size_t k = first; k < ns.e_iid.size(); ++k)
+            if (ns.e_iid[k] >= sb && ns.e_iid[k] < se) {
+                ns.e_iid[w] = ns.e_iid[k]; ns.e_val[w] = ns.e_val[k]; ns.e_pid[w] = ns.e_pid[k];
+                ++w;
+            }
+        ns.e_iid.resize(w); ns.e_val.resize(w); ns.e_pid.resize(w);
+        return (uint32_t)(w - first);
+    };
+    // {u64 iid, u64 pid, Value_m}* (ExtractProposalValues, member/paxos.cpp:421-433)
+    auto entries = [&](const uint8_t *b, size_t l) -> int {
+        const size_t first = ns.e_iid.size();
+        size_t n_all; bool dup;
+        int rc = decode_entries(vt, b, l, true, ns.e_iid, ns.e_pid, ns.e_val, n_all, dup);
+        if (rc) return rc;
+        if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
+        ent = first;
+        cnt = keep_shard(first);
+        return MPX_OK;
+    };
+    switch (t) {
+    case MPX_MSG_PREPARE: {                       // PrepareMsg, member/paxos.cpp:847-859
+        if (len < 24) return MPX_E_DECODE;
+        ver = rd32(m + 4); src = rd32(m + 8); ballot = rd64(m + 12);
+        const uint32_t rl = rd32(m + 20);
+        if (rl % 16 || 24 + (size_t)rl > len) return MPX_E_DECODE;
+        ent = ns.g_a.size();
+        const uint32_t nr = rl / 16;
+        std::vector<std::pair<uint64_t, uint64_t>> r(nr);
+        for (uint32_t k = 0; k < nr; ++k) r[k] = {rd64(m + 24 + 16 * k), rd64(m + 32 + 16 * k)};
+        std::sort(r.begin(), r.end());
+        for (uint32_t k = 0; k < nr; ++k) {
+            if (k && r[k] == r[k - 1]) flag(viol, MPX_V_DUP_IID, node, seq, r[k].first);
+            if (r[k].first >= r[k].second) continue;
+            if (cnt && r[k].first < ns.g_b.back()) { ns.g_b.back() = std::max(ns.g_b.back(), r[k].second); continue; }
+            ns.g_a.push_back(r[k].first);
+            ns.g_b.push_back(r[k].second);
+            ++cnt;
+        }
+        break;
+    }
+    case MPX_MSG_PREPARE_REPLY: {                 // PrepareReplyMsg, :861-872
+        if (len < 20) return MPX_E_DECODE;
+        src = rd32(m + 4); ballot = rd64(m + 8);
+        const uint32_t vl = rd32(m + 16);
+        if (20 + (size_t)vl > len) return MPX_E_DECODE;
+        const size_t first = ns.r_iid.size();
+        size_t n_all; bool dup;
+        int rc = decode_entries(vt, m + 20, vl, true, ns.r_iid, ns.r_pid, ns.r_val, n_all, dup);
+        if (rc) return rc;
+        if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
+        ent = first;
+        size_t w = first;
+        for (size_t k = first; k < ns.r_iid.size(); ++k)
+            if (ns.r_iid[k] >= sb && ns.r_iid[k] < se) {
+                ns.r_iid[w] = ns.r_iid[k]; ns.r_val[w] = ns.r_val[k]; ns.r_pid[w] = ns.r_pid[k];
+                ++w;
+            }
+        ns.r_iid.resize(w); ns.r_val.resize(w); ns.r_pid.resize(w);
+        cnt = (uint32_t)(w - first);
+        break;
+    }
+    case MPX_MSG_REJECT:                          // RejectMsg, :874-881
+        if (len < 12) return MPX_E_DECODE;
+        ballot = rd64(m + 4);
+        break;
+    case MPX_MSG_ACCEPT: {                        // AcceptMsg, :883-898
+        if (len < 32) return MPX_E_DECODE;
+        ver = rd32(m + 4); src = rd32(m + 8); aux = rd64(m + 12); ballot = rd64(m + 20);
+        const uint32_t vl = rd32(m + 28);
+        if (32 + (size_t)vl > len) return MPX_E_DECODE;
+        TRY_RC(entries(m + 32, vl));
+        break;
+    }
+    case MPX_MSG_ACCEPT_REPLY:                    // AcceptReplyMsg, :900-908
+        if (len < 16) return MPX_E_DECODE;
+        src = rd32(m + 4); aux = rd64(m + 8);
+        break;
+    case MPX_MSG_COMMIT: {                        // LearnMsg, :910-921
+        if (len < 20) return MPX_E_DECODE;
+        src = rd32(m + 4); aux = rd64(m + 8);
+        const uint32_t vl = rd32(m + 16);
+        if (20 + (size_t)vl > len) return MPX_E_DECODE;
+        TRY_RC(entries(m + 20, vl));
+        break;
+    }
+    case MPX_MSG_COMMIT_REPLY:                    // LearnReplyMsg, :923-931
+        if (len < 16) return MPX_E_DECODE;
+        src = rd32(m + 4); aux = rd64(m + 8);
+        break;
+    case MPX_MSG_P_START:
+        if (len < 12) return MPX_E_DECODE;
+        ballot = rd64(m + 4);
+        break;
+    case MPX_MSG_P_BATCH: {
+        if (len < 16) return MPX_E_DECODE;
+        aux = rd64(m + 4);
+        const uint32_t vl = rd32(m + 12);
+        if (16 + (size_t)vl > len) return MPX_E_DECODE;
+        TRY_RC(entries(m + 16, vl));
+        break;
+    }
+    case MPX_MSG_E_EPOCH:
+        if (len < 8) return MPX_E_DECODE;
+        ver = rd32(m + 4);
+        break;
+    default:
+        return MPX_E_DECODE;
+    }
+    if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && ballot > LOW56) return MPX_E_RANGE;   // see G_SEG
+    ns.type.push_back((uint8_t)t);
+    ns.src.push_back(src);
+    ns.ballot.push_back(ballot);
+    ns.aux.push_back(aux);
+    ns.ent.push_back(ent);
+    ns.cnt.push_back(cnt);
+    ns.ver.push_back(ver);
+    return MPX_OK;
+}
+
 // Cut entries [first, first+count) of one message (sorted by iid, inside the
 // shard) into per-bucket runs.
 template <typename F>
@@ -314,8 +505,10 @@ static void cut_runs(const uint64_t *iid, uint64_t first, uint32_t count, uint64
     }
 }
 
-int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen, HostTrace &ht)
+int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen,
+                const std::vector<mpx_epoch> &epochs, HostTrace &ht)
 {
+    const bool member = !epochs.empty();
     ht = HostTrace();
     const uint32_t N = (uint32_t)nodes.size();
     ht.N = N;
@@ -345,15 +538,41 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         const uint64_t ebase = ht.e_val.size(), rbase = ht.r_val.size(), gbase = ht.g_a.size();
         ht.e_val.insert(ht.e_val.end(), ns.e_val.begin(), ns.e_val.end());
         ht.e_iid.insert(ht.e_iid.end(), ns.e_iid.begin(), ns.e_iid.end());
+        ht.e_pid.insert(ht.e_pid.end(), ns.e_pid.begin(), ns.e_pid.end());
         ht.r_pid.insert(ht.r_pid.end(), ns.r_pid.begin(), ns.r_pid.end());
         ht.r_val.insert(ht.r_val.end(), ns.r_val.begin(), ns.r_val.end());
         ht.r_iid.insert(ht.r_iid.end(), ns.r_iid.begin(), ns.r_iid.end());
         ht.g_a.insert(ht.g_a.end(), ns.g_a.begin(), ns.g_a.end());
         ht.g_b.insert(ht.g_b.end(), ns.g_b.begin(), ns.g_b.end());
         uint32_t pstart = NONE32;                       // epoch of the batches that follow
+        // member roles of node n along its stream (include/mpx.h E_EPOCH)
+        uint32_t ep = 0, seg = 1;
+        bool acc = member && ((epochs[0].acceptor_mask >> n) & 1);
+        bool prop = member && ((epochs[0].proposer_mask >> n) & 1);
         for (size_t k = 0; k < ns.type.size(); ++k) {
             const uint32_t g = (uint32_t)ht.m_type.size();
             const uint8_t t = ns.type[k];
+            if (member) {
+                uint32_t gate = 0;
+                if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
+                    gate = acc && ns.ver[k] == epochs[ep].version ? seg : 0;
+                } else if (t == MPX_MSG_E_EPOCH) {
+                    const uint32_t x = ns.ver[k];
+                    if (x >= epochs.size()) return MPX_E_DECODE;
+                    const bool a2 = (epochs[x].acceptor_mask >> n) & 1, p2 = (epochs[x].proposer_mask >> n) & 1;
+                    if (a2 != acc) { ++seg; gate |= G_ACCCLR; }
+                    if (p2 != prop || (p2 && epochs[x].acceptor_mask != epochs[ep].acceptor_mask)) gate |= G_PRECLR;
+                    if (seg > G_SEG) return MPX_E_RANGE;
+                    gate |= seg;
+                    acc = a2; prop = p2; ep = x;
+                } else if (t == MPX_MSG_COMMIT) {
+                    gate = prop ? G_PROP : 0;
+                } else if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_ACCEPT_REPLY || t == MPX_MSG_P_START ||
+                           t == MPX_MSG_P_BATCH) {
+                    gate = prop ? (ep + 1) << G_EPOCH_SHIFT : 0;
+                }
+                ht.m_gate.push_back(gate);
+            }
             uint64_t ent = ns.ent[k];
             if (t == MPX_MSG_PREPARE) ent += gbase;
             else if (t == MPX_MSG_PREPARE_REPLY) ent += rbase;
@@ -365,9 +584,11 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             ht.m_ent.push_back(ent);
             ht.m_cnt.push_back(ns.cnt[k]);
             ht.m_node.push_back(n);
-            if (t == MPX_MSG_PREPARE || t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START) { ev.push_back(g); ev_cnt[n]++; }
+            if (t == MPX_MSG_PREPARE || t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_E_EPOCH) {
+                ev.push_back(g); ev_cnt[n]++;
+            }
             if (t == MPX_MSG_PREPARE) ht.n_after_prepare[n] = g + 1;
-            if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START) { pl.push_back(g); pl_cnt[n]++; }
+            if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_E_EPOCH) { pl.push_back(g); pl_cnt[n]++; }
             if (t == MPX_MSG_P_START) pstart = g;
             if (t == MPX_MSG_P_BATCH) {
                 ht.b_msg.push_back(g);
@@ -407,9 +628,13 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             uint32_t jn = j;
             for (uint64_t g = ht.node_off[n]; g < ht.node_off[n + 1]; ++g) {
                 const uint8_t t = ht.m_type[g];
-                if (t == MPX_MSG_P_START) live.clear();
-                else if (t == MPX_MSG_P_BATCH) live[ht.m_aux[g]] = jn++;
-                else if (t == MPX_MSG_ACCEPT_REPLY) {
+                // member: only a node with a Proposer keeps batches / counts
+                // replies (Loop, member/paxos.cpp:763-790); an idle proposer has none
+                const bool off = member && t != MPX_MSG_E_EPOCH && !(ht.m_gate[g] >> G_EPOCH_SHIFT);
+                if (t == MPX_MSG_P_START) { if (!off) live.clear(); }
+                else if (t == MPX_MSG_E_EPOCH) { if (ht.m_gate[g] & G_PRECLR) live.clear(); }
+                else if (t == MPX_MSG_P_BATCH) { if (off) ++jn; else live[ht.m_aux[g]] = jn++; }
+                else if (t == MPX_MSG_ACCEPT_REPLY && !off) {
                     auto it = live.find(ht.m_aux[g]);
                     if (it != live.end()) reps[it->second].push_back((uint32_t)g);
                 }
@@ -442,7 +667,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         for (uint64_t b = 0; b < NB; ++b) {
             const uint64_t p = (uint64_t)n * NB + b, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
             if (!nf) continue;
-            bool fast = nf <= 64 && ht.frags[f0].msg >= ht.n_after_prepare[n];
+            bool fast = !member && nf <= 64 && ht.frags[f0].msg >= ht.n_after_prepare[n];
             for (uint64_t f = f0; fast && f < f0 + nf; ++f) {
                 const uint8_t fl = ht.frags[f].flags;
                 fast = (fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT);

@@ -6,6 +6,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include "mpx.h"
+
 #include "mpx_internal.hpp"
 
 namespace mpx {
@@ -19,9 +21,13 @@ struct ValueTable {
     // synthetic resolver for device-generated clean traces: value_id v of
     // proposer 0 is the decimal string of v-1
     bool synthetic_clean = false;
+    // member Value_m codec (member/paxos.cpp:321-408): + cb, membership list
+    bool member = false;
     // parse one Value; returns bytes used (>0) or a negative MPX_E_* code
     long parse(const uint8_t *p, size_t avail, uint64_t *handle);
     bool encode(uint64_t handle, std::string &out) const;    // canonical bytes
+    // what StateMachine::Execute / Apply receives; false for unknown handles
+    // and for member membership Values (applied by ChangeMemberships instead)
     bool exec_payload(uint64_t handle, std::string &out) const;
     void clear() { idx.clear(); bytes.clear(); synthetic_clean = false; }
 };
@@ -33,6 +39,8 @@ struct NodeStream {
     std::vector<uint64_t> ballot, aux, ent;
     std::vector<uint32_t> cnt;
     std::vector<uint64_t> e_iid, e_val;           // ACCEPT / COMMIT / P_BATCH entries (in shard)
+    std::vector<uint64_t> e_pid;                  // member: their proposal ids
+    std::vector<uint32_t> ver;                    // member: PREPARE / ACCEPT version, E_EPOCH epoch
     std::vector<uint64_t> r_iid, r_pid, r_val;    // PREPARE_REPLY entries (in shard)
     std::vector<uint64_t> g_a, g_b;               // PREPARE ranges (all), sorted by start
     void clear() { *this = NodeStream(); }
@@ -45,13 +53,13 @@ struct HostTrace {
     uint32_t N = 0, NB = 0;
     uint64_t shard_begin = 0, shard_len = 0;
     std::vector<uint8_t> m_type;
-    std::vector<uint32_t> m_src, m_cnt, m_node;
+    std::vector<uint32_t> m_src, m_cnt, m_node, m_gate;
     std::vector<uint64_t> m_ballot, m_aux, m_ent;
     std::vector<uint64_t> node_off;
     std::vector<uint32_t> n_after_prepare;          // 1 + global index of the node's last PREPARE, 0: none
     std::vector<uint32_t> chunk_node, node_chunk_off;
     std::vector<uint64_t> chunk_beg, chunk_end;
-    std::vector<uint64_t> e_val, e_iid, r_pid, r_val, r_iid, g_a, g_b;
+    std::vector<uint64_t> e_val, e_iid, e_pid, r_pid, r_val, r_iid, g_a, g_b;
     std::vector<uint8_t> e_slot, r_slot;
     bool any_sparse = false;
     std::vector<uint64_t> f_off;
@@ -69,9 +77,13 @@ struct HostTrace {
 // [shard_begin, shard_end) are dropped, headers are always kept.
 int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, const uint8_t *m, size_t len,
                   uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol);
+// member semantics wire formats (member/paxos.cpp:846-932)
+int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const uint8_t *m, size_t len,
+                         uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol);
 
-// Flatten node streams and build every index the kernels walk.
+// Flatten node streams and build every index the kernels walk.  `epochs`
+// non-empty selects member semantics (role / version gates, E_EPOCH events).
 int build_trace(const std::vector<NodeStream> &nodes, uint64_t shard_begin, uint64_t shard_len,
-                HostTrace &ht);
+                const std::vector<mpx_epoch> &epochs, HostTrace &ht);
 
 }  // namespace mpx

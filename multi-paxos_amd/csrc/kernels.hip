@@ -68,6 +68,22 @@ __device__ inline void msg_contrib(const DevView &v, uint64_t g, uint64_t &p, ui
 {
     uint8_t t = v.m_type[g];
     uint64_t b = v.m_ballot[g];
+    if (v.semantics == MPX_SEM_MEMBER) {
+        // keys (incarnation << 56 | ballot): the Acceptor's own promised /
+        // max_proposal_id_ restart with every new Acceptor (member/paxos.cpp:
+        // 1700-1760); REJECT only feeds the proposer's max (:1221-1225)
+        const uint32_t gt = v.m_gate[g];
+        const uint64_t key = (uint64_t)(gt & G_SEG) << SEG_SHIFT;
+        if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && (gt & G_SEG)) {
+            s = key | b;
+            p = t == MPX_MSG_PREPARE ? s : 0;
+        } else if (t == MPX_MSG_E_EPOCH) {
+            p = s = key;
+        } else {
+            p = s = 0;
+        }
+        return;
+    }
     p = t == MPX_MSG_PREPARE ? b : 0;
     s = (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT || t == MPX_MSG_REJECT) ? b : 0;
 }
@@ -109,6 +125,7 @@ __global__ __launch_bounds__(256) void k_scan_node(DevView v)
         carry_p = carry_p > tp ? carry_p : tp;
         carry_s = carry_s > ts ? carry_s : ts;
     }
+    if (v.semantics == MPX_SEM_MEMBER) { carry_p &= LOW56; carry_s &= LOW56; }   // current incarnation
     if (threadIdx.x == 0) { v.node_scal[2 * n] = carry_p; v.node_scal[2 * n + 1] = carry_s; }
 }
 
@@ -135,6 +152,39 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
     uint64_t cp = v.chunk_carry[2 * c], cs = v.chunk_carry[2 * c + 1];
     uint64_t run_p = ep > cp ? ep : cp;      // promised before message g0
     uint64_t run_s = es > cs ? es : cs;
+    if (v.semantics == MPX_SEM_MEMBER) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t g = g0 + i;
+            if (g >= end) break;
+            const uint8_t t = v.m_type[g];
+            const uint64_t id = v.m_ballot[g];
+            const uint32_t gt = v.m_gate[g];
+            run_s = run_s > s[i] ? run_s : s[i];
+            uint8_t f = 0;
+            if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && (gt & G_SEG)) {
+                const uint64_t seg = gt & G_SEG;
+                const uint64_t prom = (run_p >> SEG_SHIFT) == seg ? (run_p & LOW56) : 0;
+                if (t == MPX_MSG_PREPARE) {
+                    if (id > prom) f = F_GRANTED;                       // :1711
+                    else if (id < prom) f = F_REJECT;                   // :1734
+                } else {
+                    f = id >= prom ? F_GRANTED : F_REJECT;              // :1753
+                }
+                if (v.m_src[g] >= v.N) f |= F_BADNODE;
+                if (f & F_REJECT) v.m_maxseen[g] = run_s & LOW56;       // same incarnation: s[i] is in run_s
+            } else if (t == MPX_MSG_E_EPOCH) {
+                f = ((gt & G_ACCCLR) ? F_ACCCLR : 0) | ((gt & G_PRECLR) ? F_PRECLR : 0);
+            } else if (t == MPX_MSG_COMMIT) {
+                f = (gt & G_PROP) ? F_PROP : 0;
+                if (v.m_src[g] >= v.N) f |= F_BADNODE;
+            }
+            v.m_flags[g] = f;
+            if (f & F_BADNODE) record_violation(v, MPX_V_BAD_NODE, v.m_node[g], g - v.node_off[v.m_node[g]], 0);
+            run_p = run_p > p[i] ? run_p : p[i];
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint64_t g = g0 + i;
@@ -167,9 +217,30 @@ __global__ void k_proposer(DevView v)
     if (n >= v.N) return;
     uint64_t ballot = 0, mask = 0;         // proposal_id_ = 0 at genesis (:338)
     bool preparing = false;                // prepare_retry_timeout_ = NULL
+    const bool member = v.semantics == MPX_SEM_MEMBER;
     for (uint64_t i = v.pl_off[n]; i < v.pl_off[n + 1]; ++i) {
         const uint32_t g = v.pl_msg[i];
         const uint8_t t = v.m_type[g];
+        if (member) {
+            // Proposer::OnPrepareReply, member/paxos.cpp:1158-1182: only an
+            // existing Proposer; quorum |acceptors|/2+1 of the node's epoch
+            const uint32_t gt = v.m_gate[g];
+            if (t == MPX_MSG_E_EPOCH) {
+                if (gt & G_PRECLR) { preparing = false; mask = 0; }
+                continue;
+            }
+            if (!(gt >> G_EPOCH_SHIFT)) continue;
+            if (t == MPX_MSG_P_START) { ballot = v.m_ballot[g]; preparing = true; mask = 0; continue; }
+            if (!preparing || v.m_ballot[g] != ballot) continue;             // :1160
+            const uint64_t am = v.ep_amask[(gt >> G_EPOCH_SHIFT) - 1];
+            const uint32_t a = v.m_src[g];
+            if (a >= 64 || !((am >> a) & 1)) { record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0); continue; }
+            uint8_t f = F_COUNTED;
+            mask |= 1ull << a;
+            if ((uint32_t)__popcll(mask) >= (uint32_t)__popcll(am) / 2 + 1) { f |= F_QUORUM; preparing = false; mask = 0; }
+            v.m_flags[g] |= f;
+            continue;
+        }
         if (t == MPX_MSG_P_START) {
             ballot = v.m_ballot[g]; preparing = true; mask = 0;
         } else if (preparing && v.m_ballot[g] == ballot) {      // :1038
@@ -194,8 +265,23 @@ __global__ void k_votes(DevView v)
     const uint64_t ballot = ps == NONE32 ? 0 : v.m_ballot[ps];
     uint64_t mask = 0;
     uint32_t chosen = NONE32;
+    const bool member = v.semantics == MPX_SEM_MEMBER;
     for (uint64_t r = v.b_rep_off[j]; r < v.b_rep_off[j + 1]; ++r) {
         const uint32_t g = v.b_rep[r];
+        if (member) {
+            // Proposer::OnAcceptReply, member/paxos.cpp:1317-1343: matched by
+            // batch id only; quorum of the node's epoch at the reply
+            const uint64_t am = v.ep_amask[(v.m_gate[g] >> G_EPOCH_SHIFT) - 1];
+            const uint32_t a = v.m_src[g];
+            if (a >= 64 || !((am >> a) & 1)) {
+                const uint32_t n = v.m_node[g];
+                record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0);
+                continue;
+            }
+            mask |= 1ull << a;
+            if ((uint32_t)__popcll(mask) >= (uint32_t)__popcll(am) / 2 + 1) { chosen = g; break; }
+            continue;
+        }
         if (v.m_ballot[g] != ballot) continue;                  // :1408
         const uint32_t a = v.m_src[g];
         if (a >= v.N) {
@@ -484,6 +570,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     wave_lds_fence();
     uint32_t cA = 0, cL = 0, cP = 0, cQ = 0;    // per-lane counts stay far below 2^32
     unsigned long long dig = 0;
+    const bool member = v.semantics == MPX_SEM_MEMBER;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
     const uint64_t *__restrict__ f_off = v.f_off;
@@ -592,7 +679,33 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) val[j] = k[j] >= 0 ? src[ent + k[j]] : 0;
                     }
-                    if (kind == K_ACCEPT) {
+                    if (member && (kind == K_ACCEPT || kind == K_COMMIT)) {
+                        // member: accept and learn are std::map::insert — the first
+                        // Value and its proposal id stick (member/paxos.cpp:1765,1040);
+                        // a learned instance is not accepted (:1763-1769) and a learn
+                        // erases the accepted entry (:1786-1793)
+                        const bool learn = kind == K_COMMIT;
+                        if (learn || (mf & F_GRANTED)) {
+                            const uint32_t seq = rl32(fmsg, a) - (uint32_t)v.node_off[n];
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j) {
+                                if (k[j] < 0) continue;
+                                const uint64_t pid = v.e_pid[ent + k[j]];
+                                if (sw[j] & W_COMMITTED) {
+                                    if ((sw[j] & W_HANDLE) != val[j] && (!learn || (mf & F_PROP)))
+                                        record_violation(v, MPX_V_LEARN_VALUE, n, seq, v.shard_begin + li0 + lane + 64 * j);
+                                } else if (learn) {
+                                    sb[j] = pid;
+                                    sw[j] = W_PRESENT | W_COMMITTED | val[j];
+                                } else if (!(sw[j] & W_PRESENT)) {
+                                    sb[j] = pid;
+                                    sw[j] = W_PRESENT | val[j];
+                                    ++cA;
+                                }
+                                cL += learn;
+                            }
+                        }
+                    } else if (kind == K_ACCEPT) {
                         if (mf & F_GRANTED) {
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
@@ -658,9 +771,20 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 cP += hit;
                             }
                         }
-                    } else if (t8 == MPX_MSG_P_START) {
+                    } else if (t8 == MPX_MSG_P_START || (t8 == MPX_MSG_E_EPOCH && (fl & F_PRECLR))) {
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) pre[lane + 64 * j] = u64x2{0, 0};
+                        if (t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j)
+                                if (!(sw[j] & W_COMMITTED)) sb[j] = sw[j] = 0;
+                        }
+                    } else if (t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
+                        // the Acceptor is deleted / recreated: its accepted values go
+                        // (member/paxos.cpp:1952-1957); learned ones stay with the Learner
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j)
+                            if (!(sw[j] & W_COMMITTED)) sb[j] = sw[j] = 0;
                     } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
 #pragma unroll 1
                         for (uint32_t j = 0; j < SPL; ++j) {
@@ -860,13 +984,19 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
     hipLaunchKernelGGL(k_proposer, dim3(cdiv(v.N, 64)), dim3(64), 0, s, v);
     if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
     if (ev_apply0) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
-    switch (g.variant) {
-    case 1: hipLaunchKernelGGL((k_apply_fast<4>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-    case 2: hipLaunchKernelGGL((k_apply_fast<6>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-    default: hipLaunchKernelGGL((k_apply_fast<1>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+    if (v.semantics == MPX_SEM_MEMBER) {
+        // member: every pair walks the general kernel (insert semantics, epoch events)
+        if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+        if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
+    } else {
+        switch (g.variant) {
+        case 1: hipLaunchKernelGGL((k_apply_fast<4>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        case 2: hipLaunchKernelGGL((k_apply_fast<6>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        default: hipLaunchKernelGGL((k_apply_fast<1>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        }
+        if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
+        if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
     }
-    if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-    if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, v, n_partials);
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, s);

@@ -42,8 +42,27 @@ enum : uint8_t {
     F_REJECT = 2,     // reply REJECT(max_seen) (paxos.cpp:894,1398)
     F_COUNTED = 4,    // PREPARE_REPLY merged into pre_accepted (paxos.cpp:1038-1045)
     F_QUORUM = 8,     // PREPARE_REPLY that reached the promise quorum (paxos.cpp:1047)
-    F_BADNODE = 16
+    F_BADNODE = 16,
+    // member semantics (copied from m_gate by the header scan)
+    F_ACCCLR = 32,    // E_EPOCH: the node's Acceptor is deleted or recreated (member/paxos.cpp:1897-1901,1952-1957)
+    F_PRECLR = 64,    // E_EPOCH: its Proposer is deleted, created or sees new acceptors (idle)
+    F_PROP = 128      // LEARN: the node has a Proposer (Proposer::OnLearn's ASSERT, :1398)
 };
+
+// member semantics: per-message role / version gate, computed at ingest from
+// the E_EPOCH markers and the epoch table (include/mpx.h):
+//   PREPARE / ACCEPT : acceptor incarnation (1..255) when the node has an
+//                      Acceptor of the message's version, 0 = dropped
+//                      (Loop :749-756, version filter :1702,1744)
+//   E_EPOCH          : the node's new incarnation | G_ACCCLR | G_PRECLR
+//   LEARN            : G_PROP when the node has a Proposer
+//   PREPARE_REPLY / ACCEPT_REPLY / P_START / P_BATCH :
+//                      (epoch + 1) << G_EPOCH_SHIFT when the node has a Proposer
+// The header scan runs over (incarnation << 56 | ballot), so one prefix max
+// restarts at every new Acceptor; member ballots must stay below 2^56.
+enum : uint32_t { G_SEG = 0xFF, G_ACCCLR = 1u << 8, G_PRECLR = 1u << 9, G_PROP = 1u << 10, G_EPOCH_SHIFT = 16 };
+constexpr uint64_t SEG_SHIFT = 56;
+constexpr uint64_t LOW56 = (1ull << 56) - 1;
 
 // fragment kinds (Frag::flags >> 4)
 enum : uint8_t { K_ACCEPT = 0, K_COMMIT = 1, K_PREPLY = 2, K_BATCH = 3 };
@@ -90,6 +109,11 @@ struct DevView {
     const uint32_t *n_after_prepare; // per node: 1 + index of its last PREPARE (0: none)
     uint8_t *m_flags;
     uint64_t *m_maxseen;
+    // member semantics
+    const uint32_t *m_gate;         // per message, see G_*
+    const uint64_t *e_pid;          // per ACCEPT / LEARN entry: its proposal id
+    const uint64_t *ep_amask;       // per epoch: acceptor set
+    uint32_t num_epochs;
     // header scan
     uint32_t num_chunks;
     const uint32_t *chunk_node;

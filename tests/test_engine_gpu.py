@@ -190,3 +190,57 @@ def test_rccl_single_rank_allgather():
     tot = mdist.combine(summ)
     assert tot["chosen"] == m == st["chosen"]
     assert tot["state_digest"] == st["state_digest"]
+
+
+# ---- member semantics (member/paxos.cpp) ----
+@pytest.mark.parametrize("seed,u,m,b,drop,dup", [(21, 8, 1 << 12, 64, 500, 100), (22, 5, 3000, 17, 1000, 300),
+                                                  (23, 8, 1 << 14, 256, 0, 100), (24, 3, 500, 1, 0, 0)])
+def test_engine_matches_oracle_c5_member(seed, u, m, b, drop, dup):
+    """C5 shape: AddAcceptor(1..U-1) then DelAcceptor(1..U-1) (member/main.cpp:119-141),
+    version filter, insert semantics, per-epoch quorums, catch-up learns, stale in-flight ACCEPTs."""
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=u, num_instances=m, seed=seed, batch=b,
+                           drop_rate=drop, dup_rate=dup, max_delay=64, noop_permille=15)
+    want, ostats, _ = oracle_run(t)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        got = e.dump()
+    assert got == want, mpxr.diff(got, want)
+    assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
+            st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
+    assert st["chosen"] == m and st["violations"] == 0
+
+
+def test_engine_member_violations():
+    from handmade_member import member_violation_traces
+    t = member_violation_traces()["mm_violations"]
+    want, ostats, oviol = oracle_run(t)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        got = e.dump()
+        v = e.violation()
+    assert got == want, mpxr.diff(got, want)
+    assert st["violations"] == ostats[4] == 3
+    assert v["code"] in (3, 6)
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+def test_engine_member_sharded_matches_oracle_restricted(shards):
+    """Instance shards of a member trace: headers (and so roles, versions, scalars,
+    quorums) are replicated, entries split; per-shard state == the oracle's, restricted."""
+    m = 2000
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=6, num_instances=m, seed=31, batch=40,
+                           drop_rate=300, dup_rate=200, max_delay=32)
+    full = mpxr.parse(oracle_run(t)[0])
+    from mpx import dist as mdist
+    for r in range(shards):
+        sb, se = mdist.shard_bounds(m, shards, r)
+        if sb == se:
+            continue
+        with mpx.Engine(6, sb, se, semantics=mpx.SEM_MEMBER) as e:
+            e.submit_trace(t)
+            e.run()
+            part = mpxr.parse(e.dump())
+        for a, b in zip(part["nodes"], full["nodes"]):
+            assert a["state"] == [s for s in b["state"] if sb <= s[0] < se]
+            assert (a["promised"], a["max_seen"]) == (b["promised"], b["max_seen"])
+        assert part["chosen"] == [c for c in full["chosen"] if sb <= c[0] < se]
