@@ -11,6 +11,7 @@ engine are pinned against (tests/test_oracle.py, tests/test_engine_gpu.py).
 
     python tests/golden/make_golden.py
 """
+import glob
 import hashlib
 import json
 import os
@@ -23,6 +24,7 @@ from fuzztrace import fuzz_trace  # noqa: E402
 from handmade import handmade_traces  # noqa: E402
 from handmade_member import member_traces  # noqa: E402
 from oracles import ref_available, ref_run  # noqa: E402
+import demotrace  # noqa: E402
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "multi-paxos_amd"))
 import mpx  # noqa: E402  (host generators only: no GPU needed)
@@ -54,6 +56,9 @@ def main():
         cases["c5_member_%d" % seed] = mpx.generate_trace(
             mpx.GEN_MEMBER, num_nodes=U, num_instances=M, seed=seed, batch=B, drop_rate=drop,
             dup_rate=dup, max_delay=64, noop_permille=noop)
+    # C1: the reference's own demo, captured by capture_demo.py (tests/demotrace.py, test_demo.py)
+    for path in sorted(glob.glob(os.path.join(HERE, "demo", "*.log.gz"))):
+        cases[os.path.basename(path)[:-len(".log.gz")]] = demotrace.to_trace(demotrace.read_log(path))
     extra = os.path.join(HERE, "extra_traces")
     if os.path.isdir(extra):
         for fn in sorted(os.listdir(extra)):
