@@ -13,10 +13,18 @@ state: header scan, promise quorum, accept-vote quorum, acceptor/learner apply
 64-word per-shard summary.  decisions/s = chosen instances per step (summed
 over ranks) / max-over-ranks step time.
 
-roofline: the dominant kernel is k_apply; achieved = B_alg per launch
-(16 P + 24 A + 16 L = 40 B per acceptor-instance here) /
-its mean duration from HIP events on the engine's stream.  traffic = HBM bytes
-per launch from rocprofv3 PMC (profiles/, tools/pmc_traffic.py) or null.
+roofline: the dominant kernel is k_apply_fast (acceptor/learner apply + the
+chosen log).  achieved = the compulsory bytes of one launch (DESIGN.md §4:
+16 B state slot written per (acceptor, instance), 8 B Value read and 8 B
+chosen-log entry written per instance — the trace stores each broadcast
+once) / its mean duration from HIP events on the engine's stream.  The
+SURVEY.md §8(d) model (16 P + 24 A + 16 L, which charges every acceptor for
+its own copy of each message) is reported beside it.  traffic = HBM bytes per
+launch from rocprofv3 PMC (profiles/, tools/pmc_traffic.py) or null.
+
+Verification: steps leave the order-independent digests off (mpx_step); after
+the timed region one digested run (mpx_run) is checked against the closed-form
+final state of the clean trace (oracle mpxo_clean_expect), per rank.
 
 cpu_baseline: the reference's own handlers (multi/paxos.cpp compiled -O2 in
 oracle/_ref, kind "reference") on a bounded sample of the same clean stream,
@@ -106,6 +114,19 @@ def latest_pmc(n_nodes, instances, world):
     return best
 
 
+def clean_expect(n_nodes, sb, se, ballot=1 << 16):
+    """(state_digest, chosen_digest) of the clean trace's final state over [sb, se) — closed form, oracle C."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libmpx_oracle.so"))
+    f = lib.mpxo_clean_expect
+    f.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    if f(n_nodes, sb, se, ballot, threads, ctypes.byref(a), ctypes.byref(b)) != 0:
+        raise RuntimeError("mpxo_clean_expect failed")
+    return a.value, b.value
+
+
 def cpu_baseline(args, budget_s):
     """Reference handlers (oracle/_ref) on host cores: node 1's accept+commit stream of a clean trace."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -183,12 +204,21 @@ def main():
     chosen_total = tot["chosen"]
     assert chosen_total == M, "chosen %d != %d instances" % (chosen_total, M)
     assert tot["violations"] == 0
+    # verification, outside the timed region: one digested run vs the closed form
+    chk = eng.run()
+    eng.timings()
+    want_state, want_chosen = clean_expect(N, sb, se)
+    verified = (chk["state_digest"] == want_state and chk["chosen_digest"] == want_chosen and
+                chk["accept_apps"] == N * (se - sb) == chk["commit_apps"] and chk["chosen"] == se - sb)
+    assert verified, "digests / counters differ from the clean trace's closed form"
 
     value = chosen_total * args.steps / dt_max
     ms_per_step = dt_max / args.steps * 1e3
     apply_mean = sum(apply_ms) / max(len(apply_ms), 1)
-    bytes_alg = st["bytes_alg"]                     # this rank's 16P + 24A + 16L per launch
-    achieved = bytes_alg / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
+    bytes_survey = st["bytes_alg"]                  # this rank's 16P + 24A + 16L per launch
+    L = se - sb
+    bytes_min = 16 * N * L + 8 * L + 8 * L          # state slots + Values once + chosen log
+    achieved = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
     pmc = latest_pmc(N, M, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
 
@@ -217,9 +247,13 @@ def main():
                        "parallelism": "instance-shard x%d (RCCL all-gather of 64-word summaries)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_apply_fast", "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_alg},
+                         "kernel": "k_apply_fast", "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_min,
+                         "bytes_survey_model_per_launch": bytes_survey,
+                         "survey_model_gbps": bytes_survey / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0},
             "cpu_baseline": cpu,
-            "hbm_gbps_alg_step": bytes_alg * world / (dt_max / args.steps) / 1e9,
+            "verified": {"digests_vs_closed_form": verified, "state_digest": chk["state_digest"],
+                         "chosen_digest": chk["chosen_digest"]},
+            "hbm_gbps_alg_step": bytes_min * world / (dt_max / args.steps) / 1e9,
             "decisions_per_step": chosen_total,
             "run_ms_device": sum(run_ms) / max(len(run_ms), 1),
             "trace_materialise_s": t_gen,

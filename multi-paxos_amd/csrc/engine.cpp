@@ -332,7 +332,7 @@ static StepEvents *next_events(mpx_engine *e)
     return &e->ev_pool[e->ev_used++];
 }
 
-static int queue_run(mpx_engine *e)
+static int queue_run(mpx_engine *e, bool digest)
 {
     HTRY(hipSetDevice(e->device));
     if (e->dirty && !e->device_trace) TRY(upload_trace(e));
@@ -342,6 +342,9 @@ static int queue_run(mpx_engine *e)
     // the defaults are the measured best
     LaunchGeom g = e->geom;
     if (const char *x = std::getenv("MPX_APPLY_VARIANT")) g.variant = (uint32_t)std::atoi(x);
+    e->view.digest = digest ? 1 : 0;
+    e->view.knobs = 0;
+    if (const char *x = std::getenv("MPX_KNOBS")) e->view.knobs = (uint32_t)std::atoi(x);
     if (const char *x = std::getenv("MPX_APPLY_WGS_PER_CU")) {
         const uint64_t np = (uint64_t)e->cfg.num_nodes * e->NB;
         g.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(np, (uint64_t)e->num_cus * std::atoi(x)));
@@ -369,7 +372,7 @@ static int collect(mpx_engine *e)
         TRY(e->out.alloc(e->out_cap * sizeof(OutRec)));
         e->view.out = e->out.as<OutRec>();
         e->view.out_cap = e->out_cap;
-        TRY(queue_run(e));
+        TRY(queue_run(e, e->view.digest != 0));
         return collect(e);
     }
     const auto &s = e->last_summary;
@@ -392,14 +395,14 @@ static int collect(mpx_engine *e)
 extern "C" int mpx_run(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
-    TRY(queue_run(e));
+    TRY(queue_run(e, true));
     return collect(e);
 }
 
 extern "C" int mpx_step(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
-    return queue_run(e);
+    return queue_run(e, false);
 }
 
 extern "C" int mpx_sync(mpx_engine *e)
@@ -763,7 +766,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     const uint64_t k0 = sb >> BSH, K = e->NB;                   // kept batches = shard buckets
     const uint64_t G0 = 2 + N + K * (3 + 2ull * N), G1 = 1 + 2 * K;
     const uint64_t G = G0 + (uint64_t)(N - 1) * G1;
-    const uint64_t E = (2ull * N + 1) * L;
+    const uint64_t E = L;                                       // one shared run per batch
     if (G >= NONE32) return MPX_E_RANGE;
     const uint64_t ballot = 1ull << 16;                         // (1 << 16) | node 0
     // host-side small tables
@@ -814,7 +817,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     TRY(e->b_msg.alloc(4 * K + 4)); TRY(e->b_pstart.alloc(4 * K + 4)); TRY(e->b_rep_off.alloc(8 * (K + 1)));
     TRY(e->b_rep.alloc(4 * (uint64_t)N * K + 4)); TRY(e->b_chosen.alloc(4 * K + 4));
     TRY(e->cf_off.alloc(8 * (K + 1))); TRY(e->cfrags.alloc(sizeof(Frag) * K + 16));
-    if (launch_gen_clean(s, N, K, k0, sb, se, G0, G1, 3 * L, ballot, e->NB,
+    if (launch_gen_clean(s, N, K, k0, sb, se, G0, G1, ballot, e->NB,
                          e->m_type.as<uint8_t>(), e->m_src.as<uint32_t>(), e->m_ballot.as<uint64_t>(),
                          e->m_aux.as<uint64_t>(), e->m_ent.as<uint64_t>(), e->m_cnt.as<uint32_t>(),
                          e->m_node.as<uint32_t>(), e->e_val.as<uint64_t>(), e->frags.as<Frag>(),

@@ -13,7 +13,10 @@
 //   node 0 : P_START, PREPARE, N x PREPARE_REPLY, then per kept batch
 //            P_BATCH, ACCEPT, N x ACCEPT_REPLY, COMMIT, N x COMMIT_REPLY
 //   node i : PREPARE, then per kept batch ACCEPT, COMMIT
-//   entries: node 0 per batch P_BATCH | ACCEPT | COMMIT, node i ACCEPT | COMMIT
+//   entries: one run per batch, shared by its P_BATCH, ACCEPT and COMMIT at
+//            every node (the content-addressed pool of ingest.cpp: a
+//            broadcast is stored once), so e_val[i - sb] = handle of i
+//   pairs:   f_off / frags indexed bucket-major, q = bucket * N + node
 #include <hip/hip_runtime.h>
 #include "mpx_internal.hpp"
 
@@ -26,7 +29,6 @@ struct CleanGeo {
     uint64_t sb, se;     // shard, se clamped to M
     uint64_t G0;         // messages of node 0
     uint64_t G1;         // messages of node i > 0
-    uint64_t E0;         // entries of node 0
     uint64_t ballot;
 };
 
@@ -43,7 +45,6 @@ __device__ inline uint64_t batch_pre(const CleanGeo &c, uint64_t j)   // in-shar
     return m > c.sb ? m - c.sb : 0;
 }
 __device__ inline uint64_t node_msg0(const CleanGeo &c, uint32_t n) { return n == 0 ? 0 : c.G0 + (uint64_t)(n - 1) * c.G1; }
-__device__ inline uint64_t node_ent0(const CleanGeo &c, uint32_t n) { return n == 0 ? 0 : c.E0 + (uint64_t)(n - 1) * 2 * (c.se - c.sb); }
 
 // one thread per message
 __global__ void k_gen_msgs(CleanGeo c, uint8_t *type, uint32_t *src, uint64_t *ballot, uint64_t *aux,
@@ -63,53 +64,39 @@ __global__ void k_gen_msgs(CleanGeo c, uint8_t *type, uint32_t *src, uint64_t *b
         else if (k < 2 + N) { t = MPX_MSG_PREPARE_REPLY; s = (uint32_t)(k - 2); b = c.ballot; }
         else {
             const uint64_t r = k - 2 - N, j = r / (3 + 2 * N), o = r % (3 + 2 * N);
-            const uint64_t bc = batch_cnt(c, j), be = 3 * batch_pre(c, j);
+            const uint64_t bc = batch_cnt(c, j), be = batch_pre(c, j);
             a = c.k0 + j + 1;
             if (o == 0) { t = MPX_MSG_P_BATCH; e = be; ct = (uint32_t)bc; }
-            else if (o == 1) { t = MPX_MSG_ACCEPT; b = c.ballot; e = be + bc; ct = (uint32_t)bc; }
+            else if (o == 1) { t = MPX_MSG_ACCEPT; b = c.ballot; e = be; ct = (uint32_t)bc; }
             else if (o < 2 + N) { t = MPX_MSG_ACCEPT_REPLY; s = (uint32_t)(o - 2); b = c.ballot; }
-            else if (o == 2 + N) { t = MPX_MSG_COMMIT; b = c.ballot; e = be + 2 * bc; ct = (uint32_t)bc; }
+            else if (o == 2 + N) { t = MPX_MSG_COMMIT; b = c.ballot; e = be; ct = (uint32_t)bc; }
             else { t = MPX_MSG_COMMIT_REPLY; s = (uint32_t)(o - 3 - N); }
         }
     } else {
         if (k == 0) { t = MPX_MSG_PREPARE; b = c.ballot; e = n; ct = 1; }
         else {
             const uint64_t j = (k - 1) / 2;
-            const uint64_t bc = batch_cnt(c, j), be = node_ent0(c, n) + 2 * batch_pre(c, j);
+            const uint64_t bc = batch_cnt(c, j), be = batch_pre(c, j);
             a = c.k0 + j + 1;
             b = c.ballot;
-            if ((k - 1) % 2 == 0) { t = MPX_MSG_ACCEPT; e = be; }
-            else { t = MPX_MSG_COMMIT; e = be + bc; }
+            t = (k - 1) % 2 == 0 ? MPX_MSG_ACCEPT : MPX_MSG_COMMIT;
+            e = be;
             ct = (uint32_t)bc;
         }
     }
     type[g] = t; src[g] = s; ballot[g] = b; aux[g] = a; ent[g] = e; cnt[g] = ct; node[g] = n;
 }
 
-// one thread per (node, in-shard instance): every entry of the clean trace
+// one thread per in-shard instance: the shared entry pool (batch runs are
+// contiguous and in instance order, so entry li holds instance sb + li)
 __global__ void k_gen_entries(CleanGeo c, uint64_t *e_val)
 {
-    const uint64_t L = c.se - c.sb;
-    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= (uint64_t)c.N * L) return;
-    const uint32_t n = (uint32_t)(x / L);
-    const uint64_t li = x % L;
-    const uint64_t iid = c.sb + li;
-    const uint64_t j = (iid >> 8) - c.k0;
-    const uint64_t bc = batch_cnt(c, j);
-    const uint64_t lo = (c.k0 + j) * 256;
-    const uint64_t pos = iid - (lo > c.sb ? lo : c.sb);     // position inside the batch's in-shard run
-    const uint64_t h = MPX_HANDLE(0, 0, iid + 1);
-    if (n == 0) {
-        const uint64_t be = 3 * batch_pre(c, j);
-        e_val[be + pos] = h; e_val[be + bc + pos] = h; e_val[be + 2 * bc + pos] = h;
-    } else {
-        const uint64_t be = node_ent0(c, n) + 2 * batch_pre(c, j);
-        e_val[be + pos] = h; e_val[be + bc + pos] = h;
-    }
+    const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= c.se - c.sb) return;
+    e_val[li] = MPX_HANDLE(0, 0, c.sb + li + 1);
 }
 
-// one thread per (node, bucket): two fragments (ACCEPT, COMMIT) and f_off
+// one thread per (bucket, node) pair q = bucket * N + node: two fragments (ACCEPT, COMMIT) and f_off
 __global__ void k_gen_frags(CleanGeo c, uint32_t NB, Frag *frags, uint64_t *f_off)
 {
     const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -117,20 +104,19 @@ __global__ void k_gen_frags(CleanGeo c, uint32_t NB, Frag *frags, uint64_t *f_of
     if (x > np) return;
     f_off[x] = 2 * x;
     if (x == np) return;
-    const uint32_t n = (uint32_t)(x / NB);
-    const uint64_t j = x % NB;
-    const uint64_t bc = batch_cnt(c, j);
     const uint32_t N = c.N;
-    uint64_t acc_msg, com_msg, acc_ent, com_ent;
+    const uint32_t n = (uint32_t)(x % N);
+    const uint64_t j = x / N;
+    const uint64_t bc = batch_cnt(c, j);
+    uint64_t acc_msg, com_msg;
     if (n == 0) {
         const uint64_t base = 2 + N + j * (3 + 2 * N);
         acc_msg = base + 1; com_msg = base + 2 + N;
-        acc_ent = 3 * batch_pre(c, j) + bc; com_ent = acc_ent + bc;
     } else {
         const uint64_t base = node_msg0(c, n) + 1 + 2 * j;
         acc_msg = base; com_msg = base + 1;
-        acc_ent = node_ent0(c, n) + 2 * batch_pre(c, j); com_ent = acc_ent + bc;
     }
+    const uint64_t acc_ent = batch_pre(c, j), com_ent = acc_ent;
     const uint8_t start = (uint8_t)((c.k0 + j) * 256 > c.sb ? 0 : (c.sb & 255));
     Frag fa{acc_ent, (uint32_t)acc_msg, (uint16_t)bc, start, (uint8_t)(FR_DENSE | (K_ACCEPT << 4))};
     Frag fc{com_ent, (uint32_t)com_msg, (uint16_t)bc, start, (uint8_t)(FR_DENSE | (K_COMMIT << 4))};
@@ -154,23 +140,23 @@ __global__ void k_gen_batches(CleanGeo c, uint32_t *b_msg, uint32_t *b_pstart, u
     for (uint32_t i = 0; i < N; ++i) b_rep[(uint64_t)N * j + i] = (uint32_t)(base + 2 + i);
     const uint64_t bc = batch_cnt(c, j);
     const uint8_t start = (uint8_t)((c.k0 + j) * 256 > c.sb ? 0 : (c.sb & 255));
-    Frag f{3 * batch_pre(c, j), (uint32_t)j, (uint16_t)bc, start, (uint8_t)(FR_DENSE | (K_BATCH << 4))};
+    Frag f{batch_pre(c, j), (uint32_t)j, (uint16_t)bc, start, (uint8_t)(FR_DENSE | (K_BATCH << 4))};
     cfrags[j] = f;
 }
 
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 int launch_gen_clean(void *stream_, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
-                        uint64_t G0, uint64_t G1, uint64_t E0, uint64_t ballot, uint32_t NB,
+                        uint64_t G0, uint64_t G1, uint64_t ballot, uint32_t NB,
                         uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,
                         uint32_t *node, uint64_t *e_val, Frag *frags, uint64_t *f_off, uint32_t *b_msg,
                         uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep, uint64_t *cf_off, Frag *cfrags)
 {
     hipStream_t s = (hipStream_t)stream_;
-    CleanGeo c{N, K, k0, sb, se, G0, G1, E0, ballot};
+    CleanGeo c{N, K, k0, sb, se, G0, G1, ballot};
     const uint64_t G = G0 + (uint64_t)(N - 1) * G1;
     hipLaunchKernelGGL(k_gen_msgs, dim3(cdiv(G, 256)), dim3(256), 0, s, c, type, src, bal, aux, ent, cnt, node);
-    hipLaunchKernelGGL(k_gen_entries, dim3(cdiv((uint64_t)N * (se - sb), 256)), dim3(256), 0, s, c, e_val);
+    hipLaunchKernelGGL(k_gen_entries, dim3(cdiv(se - sb, 256)), dim3(256), 0, s, c, e_val);
     hipLaunchKernelGGL(k_gen_frags, dim3(cdiv((uint64_t)N * NB + 1, 256)), dim3(256), 0, s, c, NB, frags, f_off);
     hipLaunchKernelGGL(k_gen_batches, dim3(cdiv(K + 1, 256)), dim3(256), 0, s, c, b_msg, b_pstart, b_rep_off, b_rep,
                        cf_off, cfrags);

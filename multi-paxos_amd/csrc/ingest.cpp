@@ -505,6 +505,41 @@ static void cut_runs(const uint64_t *iid, uint64_t first, uint32_t count, uint64
     }
 }
 
+// Content-addressed entry pool.  A broadcast reaches every node as identical
+// bytes (the proposer sends one string to all, multi/paxos.cpp:1322-1323,
+// 1474-1476), and a P_BATCH carries the same entries as its ACCEPT; storing
+// each distinct entry list once lets the apply kernel read a bucket's Values
+// once for all nodes (DESIGN.md §Data layout).  Lists are compared in full,
+// the hash only picks the candidates.
+struct EntryPool {
+    std::unordered_multimap<uint64_t, uint64_t> idx;    // hash -> offset in ht.e_*
+    uint64_t intern(const NodeStream &ns, uint64_t first, uint32_t cnt, HostTrace &ht)
+    {
+        const bool pid = !ns.e_pid.empty();
+        uint64_t h = mix64(cnt + 0x51ull);
+        for (uint32_t i = 0; i < cnt; ++i) {
+            h = mix64(h ^ ns.e_iid[first + i]) + ns.e_val[first + i];
+            if (pid) h = mix64(h ^ ns.e_pid[first + i]);
+        }
+        auto r = idx.equal_range(h);
+        for (auto it = r.first; it != r.second; ++it) {
+            const uint64_t o = it->second;
+            if (o + cnt > ht.e_iid.size()) continue;
+            bool same = true;
+            for (uint32_t i = 0; same && i < cnt; ++i)
+                same = ht.e_iid[o + i] == ns.e_iid[first + i] && ht.e_val[o + i] == ns.e_val[first + i] &&
+                       (!pid || ht.e_pid[o + i] == ns.e_pid[first + i]);
+            if (same) return o;
+        }
+        const uint64_t o = ht.e_iid.size();
+        ht.e_iid.insert(ht.e_iid.end(), ns.e_iid.begin() + first, ns.e_iid.begin() + first + cnt);
+        ht.e_val.insert(ht.e_val.end(), ns.e_val.begin() + first, ns.e_val.begin() + first + cnt);
+        if (pid) ht.e_pid.insert(ht.e_pid.end(), ns.e_pid.begin() + first, ns.e_pid.begin() + first + cnt);
+        idx.emplace(h, o);
+        return o;
+    }
+};
+
 int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen,
                 const std::vector<mpx_epoch> &epochs, HostTrace &ht)
 {
@@ -526,6 +561,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     ht.node_off.assign(N + 1, 0);
     ht.n_after_prepare.assign(N, 0);
 
+    EntryPool pool;
     struct FragKey { uint64_t key; Frag f; };
     std::vector<uint64_t> fcount(N * NB + 1, 0), cfcount(NB + 1, 0);
     std::vector<FragKey> fr, cfr;
@@ -535,10 +571,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     for (uint32_t n = 0; n < N; ++n) {
         const NodeStream &ns = nodes[n];
         ht.node_off[n] = ht.m_type.size();
-        const uint64_t ebase = ht.e_val.size(), rbase = ht.r_val.size(), gbase = ht.g_a.size();
-        ht.e_val.insert(ht.e_val.end(), ns.e_val.begin(), ns.e_val.end());
-        ht.e_iid.insert(ht.e_iid.end(), ns.e_iid.begin(), ns.e_iid.end());
-        ht.e_pid.insert(ht.e_pid.end(), ns.e_pid.begin(), ns.e_pid.end());
+        const uint64_t rbase = ht.r_val.size(), gbase = ht.g_a.size();
         ht.r_pid.insert(ht.r_pid.end(), ns.r_pid.begin(), ns.r_pid.end());
         ht.r_val.insert(ht.r_val.end(), ns.r_val.begin(), ns.r_val.end());
         ht.r_iid.insert(ht.r_iid.end(), ns.r_iid.begin(), ns.r_iid.end());
@@ -576,7 +609,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             uint64_t ent = ns.ent[k];
             if (t == MPX_MSG_PREPARE) ent += gbase;
             else if (t == MPX_MSG_PREPARE_REPLY) ent += rbase;
-            else if (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_P_BATCH) ent += ebase;
+            else if (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_P_BATCH) ent = pool.intern(ns, ent, ns.cnt[k], ht);
             ht.m_type.push_back(t);
             ht.m_src.push_back(ns.src[k]);
             ht.m_ballot.push_back(ns.ballot[k]);
@@ -600,8 +633,8 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                 cut_runs(iid, ent, ns.cnt[k], sb, [&](uint64_t b, uint64_t e0, uint32_t c, uint8_t st, bool dense) {
                     Frag f{e0, g, (uint16_t)c, st, (uint8_t)((dense ? FR_DENSE : 0) | (kind << 4))};
                     if (!dense) ht.any_sparse = true;
-                    fr.push_back({(uint64_t)n * NB + b, f});
-                    fcount[(uint64_t)n * NB + b]++;
+                    fr.push_back({b * N + n, f});            // pair index: bucket-major
+                    fcount[b * N + n]++;
                 });
             }
             if (t == MPX_MSG_P_BATCH) {
@@ -661,13 +694,15 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         std::vector<uint64_t> pos(ht.cf_off.begin(), ht.cf_off.end() - 1);
         for (auto &x : cfr) ht.cfrags[pos[x.key]++] = x.f;
     }
-    // pairs the lean dense kernel cannot take (same predicate as pair_is_fast
-    // in kernels.hip): they go to the general kernel's work list
-    for (uint32_t n = 0; n < N; ++n)
-        for (uint64_t b = 0; b < NB; ++b) {
-            const uint64_t p = (uint64_t)n * NB + b, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
+    // pairs the lean kernel cannot take (same predicate as k_apply_fast in
+    // kernels.hip): they go to the general kernel's work list
+    for (uint64_t b = 0; b < NB; ++b)
+        for (uint32_t n = 0; n < N; ++n) {
+            const uint64_t p = b * N + n, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
             if (!nf) continue;
-            bool fast = !member && nf <= 64 && ht.frags[f0].msg >= ht.n_after_prepare[n];
+            const uint64_t bucket_frags = ht.f_off[(b + 1) * N] - ht.f_off[b * N];
+            bool fast = !member && N <= FAST_MAX_NODES && bucket_frags <= FAST_MAX_FRAGS &&
+                        ht.frags[f0].msg >= ht.n_after_prepare[n];
             for (uint64_t f = f0; fast && f < f0 + nf; ++f) {
                 const uint8_t fl = ht.frags[f].flags;
                 fast = (fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT);

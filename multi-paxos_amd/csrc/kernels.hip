@@ -365,197 +365,360 @@ __device__ inline void frag_slots(uint16_t *lidx, const uint8_t *slots, uint64_t
     wave_lds_fence();
 }
 
-// One wave owns one (node, bucket) pair at a time: its 256 instance slots are
-// 4 per lane.  The pair's fragments and the node's snapshot events are walked
-// in message order, so every instance sees its events in the reference's order.
-// Fast-path predicate, evaluated identically by both apply kernels so every
-// (node, bucket) pair is processed exactly once: all fragments are dense
-// ACCEPT / COMMIT runs (fit one 64-descriptor window) and the node has no
-// PREPARE after the pair's first fragment.  Such a pair never emits: its
-// snapshots see empty state and it has no pre-accepted merge, so the events
-// can be skipped without changing any output.
-__device__ inline bool pair_is_fast(const DevView &v, uint32_t n, uint64_t nfrag, uint64_t fw1)
+// Chosen log of one bucket, general walk: every batch whose votes reached
+// quorum contributes its instances (OnAcceptReply -> Commit, multi/paxos.cpp:
+// 1416-1421); the first one wins, later ones must agree (safety).
+__device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx, unsigned long long &cC,
+                                   unsigned long long &dig)
 {
     const uint32_t lane = threadIdx.x & 63;
-    if (nfrag == 0 || nfrag > 64) return false;
-    const uint32_t fl = (uint32_t)(fw1 >> 56);
-    const bool ok = lane >= nfrag || ((fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT));
-    const uint32_t first_msg = rl32((uint32_t)fw1, 0);
-    return __ballot(!ok) == 0 && first_msg >= v.n_after_prepare[n];
+    const uint64_t li0 = b << BSH;
+    uint64_t off = lane < 2 ? v.cf_off[b + lane] : 0;
+    uint64_t fi = rl64(off, 0);
+    const uint64_t fe = rl64(off, 1);
+    uint64_t cv[SPL];
+#pragma unroll
+    for (uint32_t j = 0; j < SPL; ++j) cv[j] = 0;
+    while (fi < fe) {
+        const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
+        uint64_t fw0 = 0, fw1 = 0;
+        if (lane < nf) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.cfrags + fi + lane);
+            fw0 = x.x; fw1 = x.y;
+        }
+        const uint32_t live = lane < nf ? (v.b_chosen[(uint32_t)fw1] != NONE32) : 0;
+        for (uint32_t a = 0; a < nf; ++a) {
+            if (!rl32(live, a)) continue;
+            const uint64_t ent = rl64(fw0, a), w1 = rl64(fw1, a);
+            const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+            const bool dense = (w1 >> 56) & FR_DENSE;
+            int k[SPL];
+            frag_slots(lidx, v.e_slot, ent, cnt, st0, dense, k);
+            uint64_t val[SPL];
+#pragma unroll
+            for (uint32_t j = 0; j < SPL; ++j) val[j] = k[j] >= 0 ? v.e_val[ent + k[j]] : 0;
+#pragma unroll
+            for (uint32_t j = 0; j < SPL; ++j) {
+                if (k[j] < 0) continue;
+                const uint64_t iid = v.shard_begin + li0 + lane + 64 * j;
+                if (!cv[j]) { cv[j] = W_PRESENT | val[j]; ++cC; if (v.digest) dig += chosen_digest(iid, val[j]); }
+                else if ((cv[j] & W_HANDLE) != val[j]) record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, iid);
+            }
+        }
+        fi += nf;
+    }
+    bool have = false;
+#pragma unroll
+    for (uint32_t j = 0; j < SPL; ++j) have |= cv[j] != 0;
+    if (__ballot(have)) {
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) {
+            const uint64_t li = li0 + lane + 64 * j;
+            if (li < v.shard_len) v.chosen[li] = cv[j];
+        }
+        if (lane == 0) v.chosen_valid[b] = 1;
+    }
 }
 
-// Lean acceptor/learner apply for fast pairs: one wave per pair, slots
-// {2l, 2l+1, 128+2l, 129+2l} of lane l so full 256-entry runs move with
-// 16-byte loads and stores.  Only the Value that fixes each slot's final state
-// is loaded (pass 1 below), so a clean bucket's accept + commit cost one
-// 8-byte value read per slot instead of two.
+// Wave id with consecutive ids on one XCD: workgroups are dealt round-robin
+// over the 8 XCDs (blockIdx % 8), so id = xcd * (waves per XCD) + local id.
+// Neighbouring buckets then share their XCD's L2 (headers, descriptors).
+__device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
+{
+    if ((gridDim.x & 7) || (knobs & 1)) return (uint64_t)blockIdx.x * 4 + wv;
+    const uint64_t per = (uint64_t)(gridDim.x >> 3) * 4;
+    return (uint64_t)(blockIdx.x & 7) * per + (uint64_t)(blockIdx.x >> 3) * 4 + wv;
+}
+
+// Lean acceptor/learner apply, one bucket at a time, plus the chosen log.
+//
+// A wave owns a bucket and applies its N (node, bucket) pairs.  The pairs are
+// bucket-major in the CSR, so the whole bucket is three lane-parallel loads:
+// the N+1 CSR offsets, all its fragment descriptors (lane i = fragment i, at
+// most 64) and the scan results (flags, ballot) of their messages; the chosen
+// log's descriptors ride along.  These are issued one / two buckets ahead, so
+// a bucket costs about one memory round trip however many nodes it has.
+// Lane l holds slots {2l, 2l+1, 128+2l, 129+2l}, so a full 256-entry run moves
+// with 16-byte loads and stores.  Per slot only the Value that fixes its final
+// state is loaded (pass 1), and a run already in registers — the same
+// broadcast at the previous node, stored once in the content-addressed pool —
+// is not loaded again: a clean bucket reads its Values once for all N
+// acceptors and for the chosen log, written from the same registers when the
+// bucket's one live batch is that run (chosen_valid[b] = 1; k_chosen walks
+// every other bucket).
+//
+// A pair is taken here iff (same predicate as ingest.cpp's work list):
+// N <= FAST_MAX_NODES, the bucket has at most FAST_MAX_FRAGS fragments, the pair's fragments are all dense
+// ACCEPT / COMMIT runs and its node has no PREPARE after the first of them —
+// its snapshot events see empty state, so skipping them changes no output.
 template <int WAVES_PER_EU>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
 {
-    __shared__ unsigned long long red[4][4];
+    __shared__ unsigned long long red[4][5];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t cA = 0, cL = 0;
-    unsigned long long dig = 0;
-    const uint64_t npairs = (uint64_t)v.N * v.NB;
-    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    unsigned long long dig = 0, cC = 0, cdig = 0;
+    const uint32_t N = v.N;
+    const uint64_t NB = v.NB;
+    if (N > FAST_MAX_NODES) return;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
-    uint64_t p = (uint64_t)blockIdx.x * 4 + wv;
-    // software pipeline: CSR offsets two pairs ahead, descriptors one ahead
-    uint64_t off_cur = (p < npairs && lane < 2) ? v.f_off[p + lane] : 0;
-    uint64_t off_nxt = (p + stride < npairs && lane < 2) ? v.f_off[p + stride + lane] : 0;
-    uint64_t nw0 = 0, nw1 = NONE32;
-    {
-        const uint64_t fi = rl64(off_cur, 0), fe = rl64(off_cur, 1);
-        if (lane < fe - fi && lane < 64) {
-            const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
-            nw0 = x.x; nw1 = x.y;
+    const uint32_t nap = lane < N ? v.n_after_prepare[lane] : 0;
+    // stage 1 (two buckets ahead): CSR offsets of the bucket's pairs in lanes
+    // 0..N, of its chosen-log fragments in lanes 62..63
+    auto ld_off = [&](uint64_t b) -> uint64_t {
+        if (b >= NB) return 0;
+        if (lane <= N) return v.f_off[b * N + lane];
+        return lane >= 62 ? v.cf_off[b + lane - 62] : 0;
+    };
+    // stage 2 (one bucket ahead): fragment descriptors, lane i = fragment i
+    // (at most FAST_MAX_FRAGS), lane 63 = the chosen-log fragment if it is the only one
+    auto ld_frags = [&](uint64_t off, uint64_t &w0, uint64_t &w1) {
+        const uint64_t fi = rl64(off, 0), fe = rl64(off, N);
+        const uint64_t ci = rl64(off, 62), ce = rl64(off, 63);
+        w0 = 0; w1 = NONE32;
+        const Frag *src = nullptr;
+        if (fe - fi <= FAST_MAX_FRAGS && lane < fe - fi) src = v.frags + fi + lane;
+        else if (lane == 63 && ce - ci == 1) src = v.cfrags + ci;
+        if (src) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(src);
+            w0 = x.x; w1 = x.y;
         }
-    }
-    for (; p < npairs; p += stride) {
-        const uint32_t n = (uint32_t)(p / v.NB);
-        const uint32_t b = (uint32_t)(p - (uint64_t)n * v.NB);
-        const uint64_t nfrag = rl64(off_cur, 1) - rl64(off_cur, 0);
+    };
+    uint64_t b_c = xcd_wave_id(wv, v.knobs);
+    uint64_t off_c = ld_off(b_c), off_n = ld_off(b_c + nwaves);
+    uint64_t nw0, nw1;
+    ld_frags(off_c, nw0, nw1);
+    uint64_t cache_ent = ~0ull;                // entry offset of the full run held in cval
+    uint64_t cval[SPL] = {0, 0, 0, 0};
+    for (; b_c < NB; b_c += nwaves) {
+        const uint64_t b = b_c;
+        const uint64_t off = off_c;
         const uint64_t fw0 = nw0, fw1 = nw1;
-        {
-            const uint64_t fi = rl64(off_nxt, 0), fe = rl64(off_nxt, 1);
-            nw0 = 0; nw1 = NONE32;
-            if (lane < fe - fi && lane < 64) {
-                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
-                nw0 = x.x; nw1 = x.y;
-            }
-        }
-        off_cur = off_nxt;
-        off_nxt = (p + 2 * stride < npairs && lane < 2) ? v.f_off[p + 2 * stride + lane] : 0;
-        if (!pair_is_fast(v, n, nfrag, fw1)) continue;
+        // next bucket's descriptors, the one after's offsets
+        ld_frags(off_n, nw0, nw1);
+        off_c = off_n;
+        off_n = ld_off(b + 2 * nwaves);
+        // stage 3: scan results of this bucket's fragment messages; lane 63:
+        // whether the chosen-log fragment's batch reached its quorum
+        const uint64_t f_base = rl64(off, 0);
+        const uint32_t total = (uint32_t)(rl64(off, N) - f_base);
+        if (total > FAST_MAX_FRAGS) continue;  // every pair is on the general work list
         const uint32_t fmsg = (uint32_t)fw1;
-        const uint32_t fflag = lane < nfrag ? v.m_flags[fmsg] : 0;
-        const uint64_t fbal = lane < nfrag ? v.m_ballot[fmsg] : 0;
-        // Pass 1, descriptors only: per slot the fragment that fixes its final
-        // state — the first COMMIT covering it (first commit wins, :1515, and
-        // later accepts skip committed slots, :1380), else the last granted
-        // ACCEPT (:1387) — and the counters.  A fast pair has no snapshot
-        // events, so values of overwritten accepts never reach an output and
-        // are not loaded.
-        uint32_t src = 0xFFFFFFFFu;            // 8 bits per slot: fragment index, 0xFF none
-        uint32_t com = 0;                      // bit j: slot j committed
-        uint32_t recommit = 0;                 // a later COMMIT covers a committed slot
-        for (uint32_t a = 0; a < (uint32_t)nfrag; ++a) {
-            const uint64_t w1 = rl64(fw1, a);
-            const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
-            const bool commit = (w1 >> 60) == K_COMMIT;
-            if (!commit && !(rl32(fflag, a) & F_GRANTED)) continue;
-#pragma unroll
-            for (uint32_t j = 0; j < SPL; ++j) {
-                const uint32_t s = j < 2 ? 2 * lane + j : 128 + 2 * lane + (j - 2);
-                if (s < st0 || s >= st0 + cnt) continue;
-                if (commit) {
-                    ++cL;
-                    if ((com >> j) & 1) recommit = 1;
-                    else { com |= 1u << j; src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j)); }
-                } else if (!((com >> j) & 1)) {
-                    ++cA;
-                    src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j));
-                }
-            }
-        }
-        // Pass 2: one value load per slot, from its fixing fragment; 16-byte
-        // loads when every slot of the wave reads one full run
-        uint64_t val[SPL] = {0, 0, 0, 0};
-        uint64_t sb0 = 0, sb1 = 0, sb2 = 0, sb3 = 0, sw0 = 0, sw1 = 0, sw2 = 0, sw3 = 0;
-        const uint32_t a0 = src & 0xFF;
-        const bool same = src == (a0 | (a0 << 8) | (a0 << 16) | (a0 << 24)) && a0 != 0xFF;
-        const uint32_t a_u = __builtin_amdgcn_readfirstlane(a0);
-        const bool uni = __ballot(!same || a0 != a_u) == 0;
-        bool full = false;
-        uint64_t ent_u = 0, w1_u = 0;
-        if (uni) {
-            w1_u = rl64(fw1, a_u);
-            ent_u = rl64(fw0, a_u);
-            full = ((w1_u >> 48) & 0xFF) == 0 && ((w1_u >> 32) & 0xFFFF) == BS && !(ent_u & 1);
-        }
-        if (full) {
-            // every slot fixed by one full run: ballot and committed bit are wave-uniform
-            const u64x2 x0 = *reinterpret_cast<const u64x2 *>(e_val + ent_u + 2 * lane);
-            const u64x2 x1 = *reinterpret_cast<const u64x2 *>(e_val + ent_u + 128 + 2 * lane);
-            val[0] = x0.x; val[1] = x0.y; val[2] = x1.x; val[3] = x1.y;
-            const uint64_t bu = rl64(fbal, a_u);
-            const uint64_t tag = W_PRESENT | ((w1_u >> 60) == K_COMMIT ? W_COMMITTED : 0);
-            sb0 = sb1 = sb2 = sb3 = bu;
-            sw0 = tag | x0.x; sw1 = tag | x0.y; sw2 = tag | x1.x; sw3 = tag | x1.y;
-        } else {
-            // per-lane fragment index: fetch its descriptor with a lane-indexed
-            // shuffle, issued by every lane (a bpermute from an inactive lane reads 0)
-#define MPX_SLOT(J, SB, SW)                                                                   \
-            {                                                                                 \
-                const uint32_t fa = (src >> (8 * J)) & 0xFF;                                  \
-                const uint32_t s = J < 2 ? 2 * lane + J : 128 + 2 * lane + (J - 2);           \
-                const uint64_t ent = __shfl(fw0, (int)(fa & 63), 64);                         \
-                const uint64_t w1 = __shfl(fw1, (int)(fa & 63), 64);                          \
-                const uint64_t bj = __shfl(fbal, (int)(fa & 63), 64);                         \
-                if (fa != 0xFF) {                                                             \
-                    val[J] = e_val[ent + (s - ((uint32_t)(w1 >> 48) & 0xFF))];                \
-                    SB = bj;                                                                  \
-                    SW = W_PRESENT | (((com >> J) & 1) ? W_COMMITTED : 0) | val[J];           \
-                }                                                                             \
-            }
-            MPX_SLOT(0, sb0, sw0) MPX_SLOT(1, sb1, sw1) MPX_SLOT(2, sb2, sw2) MPX_SLOT(3, sb3, sw3)
-#undef MPX_SLOT
-        }
-        // re-commit check (rare): every later COMMIT must carry the committed Value (:1508)
-        uint32_t bad = 0;
-        if (__ballot(recommit)) {
-            for (uint32_t a = 0; a < (uint32_t)nfrag; ++a) {
-                const uint64_t w1 = rl64(fw1, a);
-                if ((w1 >> 60) != K_COMMIT) continue;
-                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
-                const uint64_t ent = rl64(fw0, a);
-#pragma unroll
-                for (uint32_t j = 0; j < SPL; ++j) {
-                    const uint32_t s = j < 2 ? 2 * lane + j : 128 + 2 * lane + (j - 2);
-                    if (s < st0 || s >= st0 + cnt || ((src >> (8 * j)) & 0xFF) == a) continue;
-                    if (e_val[ent + (s - st0)] != val[j]) bad = 1;
-                }
-            }
-        }
-        const uint64_t li0 = (uint64_t)b << BSH;
-        if (__ballot(bad) && lane == 0) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, v.shard_begin + li0);
-        uint64_t *srow = v.st + 2 * ((uint64_t)n * v.shard_len + li0);
-        const uint32_t s0 = 2 * lane, s2 = 128 + 2 * lane;
-        u64x2 w;
-        if (li0 + BS <= v.shard_len) {
-            w.x = sb0; w.y = sw0; __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(srow + 2 * s0));
-            w.x = sb1; w.y = sw1; __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(srow + 2 * s0 + 2));
-            w.x = sb2; w.y = sw2; __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(srow + 2 * s2));
-            w.x = sb3; w.y = sw3; __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(srow + 2 * s2 + 2));
-        } else {
-            if (li0 + s0 < v.shard_len) { w.x = sb0; w.y = sw0; *reinterpret_cast<u64x2 *>(srow + 2 * s0) = w; }
-            if (li0 + s0 + 1 < v.shard_len) { w.x = sb1; w.y = sw1; *reinterpret_cast<u64x2 *>(srow + 2 * s0 + 2) = w; }
-            if (li0 + s2 < v.shard_len) { w.x = sb2; w.y = sw2; *reinterpret_cast<u64x2 *>(srow + 2 * s2) = w; }
-            if (li0 + s2 + 1 < v.shard_len) { w.x = sb3; w.y = sw3; *reinterpret_cast<u64x2 *>(srow + 2 * s2 + 2) = w; }
-        }
+        uint32_t fflag = 0;
+        uint64_t fbal = 0;
+        if (lane < total) { fflag = v.m_flags[fmsg]; fbal = v.m_ballot[fmsg]; }
+        else if (lane == 63 && fmsg != NONE32) fflag = v.b_chosen[fmsg] != NONE32;
+        // One wait per bucket, before its stores: vmcnt counts stores too
+        // (gfx9), and a wait inside the node loop on these registers would
+        // drain every node's stores (vmcnt(0) vmcnt, expcnt / lgkmcnt free).
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        // lanes whose fragment disqualifies its pair from the lean path
+        const uint32_t fl = (uint32_t)(fw1 >> 56);
+        const uint64_t badm = __ballot(lane < total && !((fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT)));
+        // lanes whose fragment is a full, 16-byte aligned run: a pair made only
+        // of those treats all 256 slots alike (uniform path below)
+        const uint64_t fullm = __ballot(lane < total && ((fw1 >> 48) & 0xFF) == 0 && ((fw1 >> 32) & 0xFFFF) == BS &&
+                                        !(fw0 & 1));
+        const uint64_t li0 = b << BSH;
         const uint64_t ib = v.shard_begin + li0;
-        if (sw0) dig += state_digest(n, ib + s0, (sw0 & W_COMMITTED) ? 2 : 1, sb0, sw0 & W_HANDLE);
-        if (sw1) dig += state_digest(n, ib + s0 + 1, (sw1 & W_COMMITTED) ? 2 : 1, sb1, sw1 & W_HANDLE);
-        if (sw2) dig += state_digest(n, ib + s2, (sw2 & W_COMMITTED) ? 2 : 1, sb2, sw2 & W_HANDLE);
-        if (sw3) dig += state_digest(n, ib + s2 + 1, (sw3 & W_COMMITTED) ? 2 : 1, sb3, sw3 & W_HANDLE);
-        if (lane == 0) v.st_valid[p] = 1;
-    }
-    unsigned long long cc[3] = {cA, cL, dig};
+        const uint32_t s0 = 2 * lane, s2 = 128 + 2 * lane;
+        for (uint32_t n = 0; n < N; ++n) {
+            const uint32_t f0 = (uint32_t)(rl64(off, n) - f_base), f1 = (uint32_t)(rl64(off, n + 1) - f_base);
+            if (f1 == f0) continue;
+            const uint64_t rng = (f1 - f0 >= 64 ? ~0ull : ((1ull << (f1 - f0)) - 1)) << f0;
+            if ((badm & rng) || rl32(fmsg, f0) < rl32(nap, n)) continue;
+            uint64_t sb0 = 0, sb1 = 0, sb2 = 0, sb3 = 0, sw0 = 0, sw1 = 0, sw2 = 0, sw3 = 0;
+            uint32_t bad = 0;
+            bool done = false;
+            if ((fullm & rng) == rng) {
+                // Uniform pair: every fragment covers all 256 slots, so the walk
+                // below is wave-uniform (scalar): the fixing fragment is the first
+                // COMMIT (:1515; later accepts skip it, :1380), else the last
+                // granted ACCEPT (:1387).  A second COMMIT needs the per-slot
+                // Value check (:1508): left to the per-slot path.
+                uint32_t fix = NONE32, nA = 0, nL = 0;
+                bool comm = false, again = false;
+                for (uint32_t a = f0; a < f1; ++a) {
+                    const bool commit = (rl64(fw1, a) >> 60) == K_COMMIT;
+                    if (commit) { ++nL; if (comm) again = true; else { comm = true; fix = a; } }
+                    else if (!comm && (rl32(fflag, a) & F_GRANTED)) { ++nA; fix = a; }
+                }
+                if (!again) {
+                    cA += nA * SPL;
+                    cL += nL * SPL;
+                    if (fix != NONE32) {
+                        const uint64_t ent = rl64(fw0, fix);
+                        if (ent != cache_ent || (v.knobs & 4)) {
+                            const u64x2 x0 = *reinterpret_cast<const u64x2 *>(e_val + ent + 2 * lane);
+                            const u64x2 x1 = *reinterpret_cast<const u64x2 *>(e_val + ent + 128 + 2 * lane);
+                            cval[0] = x0.x; cval[1] = x0.y; cval[2] = x1.x; cval[3] = x1.y;
+                            cache_ent = ent;
+                        }
+                        const uint64_t bu = rl64(fbal, fix);
+                        const uint64_t tag = W_PRESENT | (comm ? W_COMMITTED : 0);
+                        sb0 = sb1 = sb2 = sb3 = bu;
+                        sw0 = tag | cval[0]; sw1 = tag | cval[1]; sw2 = tag | cval[2]; sw3 = tag | cval[3];
+                    }
+                    done = true;
+                }
+            }
+            if (!done) {
+                // Pass 1, descriptors only: per slot the fragment that fixes its final
+                // state — the first COMMIT covering it (first commit wins, :1515, and
+                // later accepts skip committed slots, :1380), else the last granted
+                // ACCEPT (:1387) — and the counters.  Values of overwritten accepts
+                // never reach an output (no snapshot events here) and are not loaded.
+                uint32_t src = 0xFFFFFFFFu;            // 8 bits per slot: fragment lane, 0xFF none
+                uint32_t com = 0;                      // bit j: slot j committed
+                uint32_t recommit = 0;                 // a later COMMIT covers a committed slot
+                for (uint32_t a = f0; a < f1; ++a) {
+                    const uint64_t w1 = rl64(fw1, a);
+                    const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                    const bool commit = (w1 >> 60) == K_COMMIT;
+                    if (!commit && !(rl32(fflag, a) & F_GRANTED)) continue;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+                    for (uint32_t j = 0; j < SPL; ++j) {
+                        const uint32_t s = j < 2 ? 2 * lane + j : 128 + 2 * lane + (j - 2);
+                        if (s < st0 || s >= st0 + cnt) continue;
+                        if (commit) {
+                            ++cL;
+                            if ((com >> j) & 1) recommit = 1;
+                            else { com |= 1u << j; src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j)); }
+                        } else if (!((com >> j) & 1)) {
+                            ++cA;
+                            src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j));
+                        }
+                    }
+                }
+                // Pass 2: one value load per slot, from its fixing fragment; a full
+                // run fixing every slot is one pair of 16-byte loads per lane, or
+                // none when that run is the one already in registers
+                uint64_t val[SPL] = {0, 0, 0, 0};
+                const uint32_t a0 = src & 0xFF;
+                const bool same = src == (a0 | (a0 << 8) | (a0 << 16) | (a0 << 24)) && a0 != 0xFF;
+                const uint32_t a_u = __builtin_amdgcn_readfirstlane(a0);
+                const bool uni = __ballot(!same || a0 != a_u) == 0;
+                bool full = false;
+                uint64_t ent_u = 0, w1_u = 0;
+                if (uni) {
+                    w1_u = rl64(fw1, a_u);
+                    ent_u = rl64(fw0, a_u);
+                    full = ((w1_u >> 48) & 0xFF) == 0 && ((w1_u >> 32) & 0xFFFF) == BS && !(ent_u & 1);
+                }
+                if (full) {
+                    // every slot fixed by one full run: ballot and committed bit are wave-uniform
+                    if (ent_u != cache_ent || (v.knobs & 4)) {
+                        const u64x2 x0 = *reinterpret_cast<const u64x2 *>(e_val + ent_u + 2 * lane);
+                        const u64x2 x1 = *reinterpret_cast<const u64x2 *>(e_val + ent_u + 128 + 2 * lane);
+                        cval[0] = x0.x; cval[1] = x0.y; cval[2] = x1.x; cval[3] = x1.y;
+                        cache_ent = ent_u;
+                    }
+#pragma unroll
+                    for (uint32_t j = 0; j < SPL; ++j) val[j] = cval[j];
+                    const uint64_t bu = rl64(fbal, a_u);
+                    const uint64_t tag = W_PRESENT | ((w1_u >> 60) == K_COMMIT ? W_COMMITTED : 0);
+                    sb0 = sb1 = sb2 = sb3 = bu;
+                    sw0 = tag | val[0]; sw1 = tag | val[1]; sw2 = tag | val[2]; sw3 = tag | val[3];
+                } else {
+                    // per-lane fragment lane: fetch its descriptor with a lane-indexed
+                    // shuffle, issued by every lane (a bpermute from an inactive lane reads 0)
+#define MPX_SLOT(J, SB, SW)                                                                   \
+                    {                                                                             \
+                        const uint32_t fa = (src >> (8 * J)) & 0xFF;                              \
+                        const uint32_t s = J < 2 ? 2 * lane + J : 128 + 2 * lane + (J - 2);       \
+                        const uint64_t ent = __shfl(fw0, (int)(fa & 63), 64);                     \
+                        const uint64_t w1 = __shfl(fw1, (int)(fa & 63), 64);                      \
+                        const uint64_t bj = __shfl(fbal, (int)(fa & 63), 64);                     \
+                        if (fa != 0xFF) {                                                         \
+                            val[J] = e_val[ent + (s - ((uint32_t)(w1 >> 48) & 0xFF))];            \
+                            SB = bj;                                                              \
+                            SW = W_PRESENT | (((com >> J) & 1) ? W_COMMITTED : 0) | val[J];       \
+                        }                                                                         \
+                    }
+                    MPX_SLOT(0, sb0, sw0) MPX_SLOT(1, sb1, sw1) MPX_SLOT(2, sb2, sw2) MPX_SLOT(3, sb3, sw3)
+#undef MPX_SLOT
+                }
+                // re-commit check (rare): every later COMMIT must carry the committed Value (:1508)
+                if (__ballot(recommit)) {
+                    for (uint32_t a = f0; a < f1; ++a) {
+                        const uint64_t w1 = rl64(fw1, a);
+                        if ((w1 >> 60) != K_COMMIT) continue;
+                        const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                        const uint64_t ent = rl64(fw0, a);
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) {
+                            const uint32_t s = j < 2 ? 2 * lane + j : 128 + 2 * lane + (j - 2);
+                            if (s < st0 || s >= st0 + cnt || ((src >> (8 * j)) & 0xFF) == a) continue;
+                            if (e_val[ent + (s - st0)] != val[j]) bad = 1;
+                        }
+                    }
+                }
+            }
+            if (__ballot(bad) && lane == 0) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, ib);
+            uint64_t *srow = v.st + 2 * ((uint64_t)n * v.shard_len + li0);
+            u64x2 w;
+            if (v.knobs & 16) {
+                // experiment: no state stores
+            } else if (li0 + BS <= v.shard_len) {
+                w.x = sb0; w.y = sw0; *reinterpret_cast<u64x2 *>(srow + 2 * s0) = w;
+                w.x = sb1; w.y = sw1; *reinterpret_cast<u64x2 *>(srow + 2 * s0 + 2) = w;
+                w.x = sb2; w.y = sw2; *reinterpret_cast<u64x2 *>(srow + 2 * s2) = w;
+                w.x = sb3; w.y = sw3; *reinterpret_cast<u64x2 *>(srow + 2 * s2 + 2) = w;
+            } else {
+                if (li0 + s0 < v.shard_len) { w.x = sb0; w.y = sw0; *reinterpret_cast<u64x2 *>(srow + 2 * s0) = w; }
+                if (li0 + s0 + 1 < v.shard_len) { w.x = sb1; w.y = sw1; *reinterpret_cast<u64x2 *>(srow + 2 * s0 + 2) = w; }
+                if (li0 + s2 < v.shard_len) { w.x = sb2; w.y = sw2; *reinterpret_cast<u64x2 *>(srow + 2 * s2) = w; }
+                if (li0 + s2 + 1 < v.shard_len) { w.x = sb3; w.y = sw3; *reinterpret_cast<u64x2 *>(srow + 2 * s2 + 2) = w; }
+            }
+            if (v.digest) {
+                if (sw0) dig += state_digest(n, ib + s0, (sw0 & W_COMMITTED) ? 2 : 1, sb0, sw0 & W_HANDLE);
+                if (sw1) dig += state_digest(n, ib + s0 + 1, (sw1 & W_COMMITTED) ? 2 : 1, sb1, sw1 & W_HANDLE);
+                if (sw2) dig += state_digest(n, ib + s2, (sw2 & W_COMMITTED) ? 2 : 1, sb2, sw2 & W_HANDLE);
+                if (sw3) dig += state_digest(n, ib + s2 + 1, (sw3 & W_COMMITTED) ? 2 : 1, sb3, sw3 & W_HANDLE);
+            }
+            if (lane == 0) v.st_valid[(uint64_t)n * NB + b] = 1;
+        }
+        // the bucket's chosen log from the registers, when its one live batch is the cached run
+        const uint64_t c0 = rl64(fw0, 63), c1 = rl64(fw1, 63);
+        if (rl32(fflag, 63) && c0 == cache_ent && ((c1 >> 48) & 0xFF) == 0 && ((c1 >> 32) & 0xFFFF) == BS &&
+            li0 + BS <= v.shard_len) {
+            u64x2 w;
+            w.x = W_PRESENT | cval[0]; w.y = W_PRESENT | cval[1];
+            *reinterpret_cast<u64x2 *>(v.chosen + li0 + s0) = w;
+            w.x = W_PRESENT | cval[2]; w.y = W_PRESENT | cval[3];
+            *reinterpret_cast<u64x2 *>(v.chosen + li0 + s2) = w;
+            cC += SPL;
+            if (v.digest)
+                cdig += chosen_digest(ib + s0, cval[0]) + chosen_digest(ib + s0 + 1, cval[1]) +
+                        chosen_digest(ib + s2, cval[2]) + chosen_digest(ib + s2 + 1, cval[3]);
+            if (lane == 0) v.chosen_valid[b] = 1;
+        }
+    }
+    unsigned long long cc[5] = {cA, cL, dig, cC, cdig};
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
         unsigned long long x = cc[i];
         for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
         cc[i] = x;
     }
-    if (lane == 0) { red[wv][0] = cc[0]; red[wv][1] = cc[1]; red[wv][2] = cc[2]; }
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) red[wv][i] = cc[i];
+    }
     __syncthreads();
-    if (threadIdx.x < 3) {
+    if (threadIdx.x < 5) {
         const uint32_t t = threadIdx.x;
         unsigned long long s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
-        v.partials[8 * blockIdx.x + (t == 0 ? PC_A : t == 1 ? PC_L : PC_DSTATE)] += s;
+        const int slot = t == 0 ? PC_A : t == 1 ? PC_L : t == 2 ? PC_DSTATE : t == 3 ? PC_C : PC_DCHOSEN;
+        v.partials[8 * blockIdx.x + slot] += s;
     }
 }
 
+// General apply: one wave owns one (node, bucket) pair of the host-built work
+// list at a time, its 256 instance slots 4 per lane.  The pair's fragments and
+// the node's snapshot events are walked in message order, so every instance
+// sees its events in the reference's order.
 template <int WAVES_PER_EU, bool PREFETCH_VALUES>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 {
@@ -579,9 +742,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     // work list: the pairs the lean kernel does not take (ingest.cpp)
     auto rt1 = [&](uint64_t i) -> uint64_t {
         if (i >= v.num_gp || lane > 4) return 0;
-        const uint64_t q = v.gp_list[i];
+        const uint64_t q = v.gp_list[i];                // pair, bucket-major
         if (lane == 4) return q;
-        const uint32_t n = (uint32_t)(q / v.NB);
+        const uint32_t n = (uint32_t)(q % v.N);
         return lane < 2 ? f_off[q + lane] : ev_off[n + lane - 2];
     };
     // software pipeline over this wave's work items: (1) CSR offsets two
@@ -603,9 +766,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     uint64_t off_nxt = rt1(it + stride);
     Win win_nxt = rt2(off_cur);
     for (; it < v.num_gp; it += stride) {
-        const uint64_t p = rl64(off_cur, 4);
-        const uint32_t n = (uint32_t)(p / v.NB);
-        const uint32_t b = (uint32_t)(p - (uint64_t)n * v.NB);
+        const uint64_t q = rl64(off_cur, 4);
+        const uint32_t b = (uint32_t)(q / v.N);
+        const uint32_t n = (uint32_t)(q - (uint64_t)b * v.N);
         uint64_t fi = rl64(off_cur, 0), fe = rl64(off_cur, 1), ei = rl64(off_cur, 2), ee = rl64(off_cur, 3);
         Win win = win_nxt;
         win_nxt = rt2(off_nxt);                  // next item's descriptors in flight
@@ -812,12 +975,12 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                 if (li < v.shard_len) {
                     uint64_t *s = v.st + 2 * ((uint64_t)n * v.shard_len + li);
                     u64x2 w; w.x = sb[j]; w.y = sw[j];
-                    __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(s));
+                    *reinterpret_cast<u64x2 *>(s) = w;
                 }
                 if (sw[j])
-                    dig += state_digest(n, v.shard_begin + li, (sw[j] & W_COMMITTED) ? 2 : 1, sb[j], sw[j] & W_HANDLE);
+                    if (v.digest) dig += state_digest(n, v.shard_begin + li, (sw[j] & W_COMMITTED) ? 2 : 1, sb[j], sw[j] & W_HANDLE);
             }
-            if (lane == 0) v.st_valid[p] = 1;
+            if (lane == 0) v.st_valid[(uint64_t)n * v.NB + b] = 1;
         }
     }
     // workgroup reduction of the counters
@@ -841,8 +1004,8 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     }
 }
 
-// Chosen log, one wave per bucket: every batch whose votes reached quorum
-// contributes its instances; the first one wins, later ones must agree (safety).
+// Chosen log, one wave per bucket, for the buckets k_apply_fast did not
+// write from registers (multi) or every bucket (member: chosen_valid is 0).
 __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base)
 {
     __shared__ uint16_t lidx_all[4][BS];
@@ -854,54 +1017,8 @@ __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base
     wave_lds_fence();
     unsigned long long cC = 0, dig = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
-    for (uint64_t b = (uint64_t)blockIdx.x * 4 + wv; b < v.NB; b += stride) {
-        const uint64_t li0 = b << BSH;
-        uint64_t off = lane < 2 ? v.cf_off[b + lane] : 0;
-        uint64_t fi = rl64(off, 0);
-        const uint64_t fe = rl64(off, 1);
-        uint64_t cv[SPL];
-#pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) cv[j] = 0;
-        while (fi < fe) {
-            const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
-            uint64_t fw0 = 0, fw1 = 0;
-            if (lane < nf) {
-                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.cfrags + fi + lane);
-                fw0 = x.x; fw1 = x.y;
-            }
-            const uint32_t live = lane < nf ? (v.b_chosen[(uint32_t)fw1] != NONE32) : 0;
-            for (uint32_t a = 0; a < nf; ++a) {
-                if (!rl32(live, a)) continue;
-                const uint64_t ent = rl64(fw0, a), w1 = rl64(fw1, a);
-                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
-                const bool dense = (w1 >> 56) & FR_DENSE;
-                int k[SPL];
-                frag_slots(lidx, v.e_slot, ent, cnt, st0, dense, k);
-                uint64_t val[SPL];
-#pragma unroll
-                for (uint32_t j = 0; j < SPL; ++j) val[j] = k[j] >= 0 ? v.e_val[ent + k[j]] : 0;
-#pragma unroll
-                for (uint32_t j = 0; j < SPL; ++j) {
-                    if (k[j] < 0) continue;
-                    const uint64_t iid = v.shard_begin + li0 + lane + 64 * j;
-                    if (!cv[j]) { cv[j] = W_PRESENT | val[j]; ++cC; dig += chosen_digest(iid, val[j]); }
-                    else if ((cv[j] & W_HANDLE) != val[j]) record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, iid);
-                }
-            }
-            fi += nf;
-        }
-        bool have = false;
-#pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) have |= cv[j] != 0;
-        if (__ballot(have)) {
-#pragma unroll
-            for (uint32_t j = 0; j < SPL; ++j) {
-                const uint64_t li = li0 + lane + 64 * j;
-                if (li < v.shard_len) __builtin_nontemporal_store(cv[j], v.chosen + li);
-            }
-            if (lane == 0) v.chosen_valid[b] = 1;
-        }
-    }
+    for (uint64_t b = xcd_wave_id(wv); b < v.NB; b += stride)
+        if (!v.chosen_valid[b]) chosen_walk(v, b, lidx, cC, dig);
     unsigned long long cc[2] = {cC, dig};
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -989,9 +1106,10 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
         if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
     } else {
+        // multi: the lean kernel also writes the chosen log of clean buckets
         switch (g.variant) {
         case 1: hipLaunchKernelGGL((k_apply_fast<4>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-        case 2: hipLaunchKernelGGL((k_apply_fast<6>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        case 2: hipLaunchKernelGGL((k_apply_fast<5>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         default: hipLaunchKernelGGL((k_apply_fast<1>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         }
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);

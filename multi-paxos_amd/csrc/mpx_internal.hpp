@@ -4,10 +4,13 @@
 //   * messages, all nodes flattened in processing order: SoA headers
 //     m_type u8 | m_src u32 | m_ballot u64 | m_aux u64 | m_ent u64 | m_cnt u32
 //   * entry pools: e_val u64 (+ e_slot u8 when a fragment is sparse) for
-//     ACCEPT / COMMIT / P_BATCH; r_pid,r_val u64 (+ r_slot) for PREPARE_REPLY;
-//     g_a,g_b u64 prepare ranges
+//     ACCEPT / COMMIT / P_BATCH, content-addressed: an entry list that reaches
+//     several nodes (a broadcast, its P_BATCH, duplicates) is stored once;
+//     r_pid,r_val u64 (+ r_slot) for PREPARE_REPLY; g_a,g_b u64 prepare ranges
 //   * fragments: every entry-carrying message split into runs that fall in one
-//     256-instance bucket, listed per (node, bucket) in processing order (CSR)
+//     256-instance bucket, listed per pair in processing order (CSR); pairs are
+//     bucket-major, q = bucket * N + node, so one wave can walk a bucket's
+//     nodes and reuse the shared Values
 //   * state: one 16-byte slot per (node, instance) = {ballot, word}
 //       word = PRESENT | COMMITTED? | handle  — accepted and committed entries
 //       of a node are disjoint (OnCommit erases accepted_values_,
@@ -95,6 +98,9 @@ struct DevViolation {
 // Everything a kernel needs, passed by value (kernarg).
 struct DevView {
     uint32_t N, quorum, NB, semantics;
+    uint32_t knobs;                 // experiment switches (MPX_KNOBS, tools/ab_apply.py), 0 = default
+    uint32_t digest;                // 1: accumulate the order-independent state / chosen digests
+                                    //    (mpx_run; verification only, mpx_step leaves them 0)
     uint64_t shard_begin, shard_len;
     uint64_t num_msgs;
     // messages
@@ -132,7 +138,7 @@ struct DevView {
     const uint64_t *g_a;
     const uint64_t *g_b;
     // fragment lists
-    const uint64_t *f_off;          // N*NB+1
+    const uint64_t *f_off;          // N*NB+1, pair q = bucket * N + node
     const Frag *frags;
     uint64_t num_gp;                // pairs for the general apply kernel
     const uint64_t *gp_list;
@@ -151,7 +157,7 @@ struct DevView {
     const Frag *cfrags;
     // state
     uint64_t *st;                   // 2 words per (node, instance)
-    uint8_t *st_valid;              // per (node, bucket)
+    uint8_t *st_valid;              // per (node, bucket): node * NB + bucket
     uint64_t *chosen;               // per instance
     uint8_t *chosen_valid;          // per bucket
     // outputs
@@ -163,6 +169,11 @@ struct DevView {
     unsigned long long *summary;    // 64 words
 };
 
+// k_apply_fast takes a bucket's pairs only when its CSR offsets (N+1, plus two
+// chosen-log offsets) and its fragments (plus the chosen-log one) fit one
+// wave's lanes (kernels.hip, ingest.cpp work list)
+constexpr uint32_t FAST_MAX_NODES = 61;
+constexpr uint32_t FAST_MAX_FRAGS = 63;
 constexpr uint32_t APPLY_WGS_MAX = 2048;
 constexpr uint32_t CHOSEN_WGS_MAX = 1024;
 // partial counter slots
@@ -197,7 +208,7 @@ struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, variant; };
 int launch_run(const DevView &v, void *stream, LaunchGeom g, void *ev_begin, void *ev_apply0,
                void *ev_apply1, void *ev_end);
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
-                     uint64_t G0, uint64_t G1, uint64_t E0, uint64_t ballot, uint32_t NB,
+                     uint64_t G0, uint64_t G1, uint64_t ballot, uint32_t NB,
                      uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,
                      uint32_t *node, uint64_t *e_val, Frag *frags, uint64_t *f_off, uint32_t *b_msg,
                      uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep, uint64_t *cf_off, Frag *cfrags);

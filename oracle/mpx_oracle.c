@@ -141,7 +141,7 @@ static ent_t *map_sorted(const map_t *m, size_t *n)
 typedef struct { u64 handle; size_t off; u32 len; u32 exec_off; u32 exec_len; } valrec_t;
 typedef struct { map_t idx; valrec_t *v; size_t n, cap; buf_t bytes; } vtab_t;
 
-enum { OK = 0, E_DECODE = -4, E_RANGE = -5, E_VALUE = -9, E_NOMEM = -2 };
+enum { OK = 0, E_INVAL = -1, E_DECODE = -4, E_RANGE = -5, E_VALUE = -9, E_NOMEM = -2 };
 
 /* Parse one Value at p (avail bytes).  Returns bytes used (>0) or <0. */
 static long parse_value(vtab_t *t, const u8 *p, size_t avail, u64 *handle)
@@ -1115,3 +1115,50 @@ int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64
 }
 
 void mpxo_free(void *p) { free(p); }
+
+/* ---- closed form for the clean trace (bench verification) -----------------
+ * The clean generator (one proposer, ballot B, every instance proposed once,
+ * every ACCEPT granted, every COMMIT delivered) ends
+ * with every node holding committed_values_[i] = (B, handle(0, 0, i + 1))
+ * (OnCommit, multi/paxos.cpp:1494-1518) and the chosen log = the same
+ * handles.  This sums the digests (dump() above) of that final state over
+ * instances [sb, se) without replaying the trace, so bench.py can check a
+ * 2^27-instance run; `threads` POSIX threads split the instances. */
+#include <pthread.h>
+typedef struct { u64 N, lo, hi, ballot, ds, dc; } clean_job_t;
+
+static void *clean_job(void *arg)
+{
+    clean_job_t *j = (clean_job_t *)arg;
+    u64 ds = 0, dc = 0;
+    for (u64 iid = j->lo; iid < j->hi; ++iid) {
+        const u64 h = (iid + 1);                              /* MPX_HANDLE(0, 0, iid + 1) */
+        dc += mix64(mix64(iid) ^ h);
+        for (u64 i = 0; i < j->N; ++i)
+            ds += mix64(mix64(mix64(iid + i * 0x9E3779B97F4A7C15ull) ^ j->ballot) ^ (h + 2 * 0xD6E8FEB86659FD93ull));
+    }
+    j->ds = ds; j->dc = dc;
+    return NULL;
+}
+
+int mpxo_clean_expect(u32 N, u64 sb, u64 se, u64 ballot, u32 threads, u64 *state_digest, u64 *chosen_digest)
+{
+    if (!threads || threads > 256 || se < sb || !state_digest || !chosen_digest) return E_INVAL;
+    clean_job_t jobs[256];
+    pthread_t tid[256];
+    const u64 span = (se - sb + threads - 1) / threads;
+    for (u32 t = 0; t < threads; ++t) {
+        u64 lo = sb + t * span, hi = lo + span;
+        if (lo > se) lo = se;
+        if (hi > se) hi = se;
+        jobs[t] = (clean_job_t){N, lo, hi, ballot, 0, 0};
+        if (pthread_create(&tid[t], NULL, clean_job, &jobs[t])) return E_NOMEM;
+    }
+    u64 ds = 0, dc = 0;
+    for (u32 t = 0; t < threads; ++t) {
+        pthread_join(tid[t], NULL);
+        ds += jobs[t].ds; dc += jobs[t].dc;
+    }
+    *state_digest = ds; *chosen_digest = dc;
+    return OK;
+}

@@ -109,3 +109,27 @@ def test_member_epoch_gates_roles():
     node1 = res["nodes"][1]
     assert node1["promised"] == 7 << 16
     assert [s[1][:4] for s in node1["sends"]][-1] == struct.pack("<I", 1)
+
+
+@pytest.mark.parametrize("n,m,sb,se", [(5, 3000, 0, 3000), (9, 256 * 40, 0, 256 * 40), (9, 256 * 40, 256 * 8, 256 * 24),
+                                       (3, 777, 0, 777)])
+def test_clean_closed_form_matches_oracle(n, m, sb, se):
+    """bench.py verifies its full-size run against mpxo_clean_expect: pin that closed form to the oracle's
+    replay of the same clean trace (digests restricted to the shard via the state entries)."""
+    import ctypes
+    import mpxr
+    from oracles import ORACLE_SO
+    t = _mpx.generate_trace(_mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=256)
+    res, st, _ = oracle_run(t)
+    lib = ctypes.CDLL(ORACLE_SO)
+    f = lib.mpxo_clean_expect
+    f.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    assert f(n, sb, se, 1 << 16, 3, ctypes.byref(a), ctypes.byref(b)) == 0
+    if (sb, se) == (0, m):
+        assert (a.value, b.value) == (st[6], st[5])
+    # shard: every node's state in [sb, se) is (ballot 1<<16, committed, handle iid+1)
+    R = mpxr.parse(res)
+    for nd in R["nodes"]:
+        assert [s for s in nd["state"] if sb <= s[0] < se] == [(i, 2, 1 << 16, i + 1) for i in range(sb, se)]
