@@ -15,12 +15,14 @@ over ranks) / max-over-ranks step time.
 
 roofline: the dominant kernel is k_apply_fast (acceptor/learner apply + the
 chosen log).  achieved = the compulsory bytes of one launch (DESIGN.md §4:
-16 B state slot written per (acceptor, instance), 8 B Value read and 8 B
-chosen-log entry written per instance — the trace stores each broadcast
-once) / its mean duration from HIP events on the engine's stream.  The
-SURVEY.md §8(d) model (16 P + 24 A + 16 L, which charges every acceptor for
-its own copy of each message) is reported beside it.  traffic = HBM bytes per
-launch from rocprofv3 PMC (profiles/, tools/pmc_traffic.py) or null.
+one 8-byte state slot written per (acceptor, instance), one 4-byte chosen-log
+entry per instance, one 16-byte fragment descriptor read per (acceptor,
+bucket, message) — slots reference the Value in the resident entry pool, so
+no Value is read or copied) / its mean duration from HIP events on the
+engine's stream.  The SURVEY.md §8(d) model (16 P + 24 A + 16 L, which charges
+every acceptor a 16-byte slot plus a read of its own copy of each message) is
+reported beside it.  traffic = HBM bytes per launch from rocprofv3 PMC
+(profiles/, tools/pmc_traffic.py) or null.
 
 Verification: steps leave the order-independent digests off (mpx_step); after
 the timed region one digested run (mpx_run) is checked against the closed-form
@@ -217,7 +219,8 @@ def main():
     apply_mean = sum(apply_ms) / max(len(apply_ms), 1)
     bytes_survey = st["bytes_alg"]                  # this rank's 16P + 24A + 16L per launch
     L = se - sb
-    bytes_min = 16 * N * L + 8 * L + 8 * L          # state slots + Values once + chosen log
+    # 8-B state slots + 4-B chosen log + the ACCEPT and COMMIT descriptors of every (node, bucket)
+    bytes_min = 8 * N * L + 4 * L + 2 * 16 * N * ((L + 255) // 256)
     achieved = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
     pmc = latest_pmc(N, M, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None

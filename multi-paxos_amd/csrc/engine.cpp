@@ -77,6 +77,7 @@ struct mpx_engine {
     DevBuf f_off, frags, gp_list, ev_off, ev_msg, pl_off, pl_msg;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
     DevBuf st, st_valid, chosen, chosen_valid;
+    DevBuf decode_buf;                      // readback scratch (k_decode)
     DevBuf out, out_cursor, partials, viol, summary;
     uint64_t out_cap = 0;
     DevView view{};
@@ -221,14 +222,14 @@ static int finish_view(mpx_engine *e)
     v.shard_begin = e->cfg.shard_begin;
     v.shard_len = e->shard_len;
     v.num_msgs = e->num_msgs;
-    TRY(e->st.alloc((size_t)N * e->shard_len * 16));
+    TRY(e->st.alloc((size_t)N * e->shard_len * 8));
     TRY(e->st_valid.alloc((size_t)N * e->NB));
-    TRY(e->chosen.alloc(e->shard_len * 8));
+    TRY(e->chosen.alloc(e->shard_len * 4));
     TRY(e->chosen_valid.alloc(e->NB));
     const uint64_t npairs = (uint64_t)N * e->NB;
-    // resident grid: k_apply_fast holds 5 waves/SIMD (94 VGPRs) = 5 workgroups
-    // of 4 waves per CU; a grid matched to residency measured best (ab_apply.py)
-    e->geom.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npairs, (uint64_t)e->num_cus * 5));
+    // k_apply_fast holds 5 waves/SIMD (82 VGPRs); 8 workgroups of 4 waves per
+    // CU measured best on C4 (tools/ab_apply.py: 2.17 ms vs 2.31 ms at 5)
+    e->geom.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npairs, (uint64_t)e->num_cus * 8));
     e->geom.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 4));
 
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + e->geom.chosen_wgs)));
@@ -240,7 +241,7 @@ static int finish_view(mpx_engine *e)
     TRY(e->node_scal.alloc(16ull * N));
     v.st = e->st.as<uint64_t>();
     v.st_valid = e->st_valid.as<uint8_t>();
-    v.chosen = e->chosen.as<uint64_t>();
+    v.chosen = e->chosen.as<uint32_t>();
     v.chosen_valid = e->chosen_valid.as<uint8_t>();
     v.out = e->out.as<OutRec>();
     v.out_cursor = e->out_cursor.as<unsigned long long>();
@@ -450,20 +451,27 @@ template <typename T> static int d2h(std::vector<T> &v, const DevBuf &b, size_t 
 
 static bool have_results(const mpx_engine *e) { return !e->last_summary.empty(); }
 
+// count slots of node n (n == N: the chosen log) from shard offset l0, decoded
+// on the device into {ballot, PRESENT | COMMITTED? | handle} pairs
+static int decode_slots(mpx_engine *e, uint32_t n, uint64_t l0, uint64_t count, std::vector<uint64_t> &out)
+{
+    out.assign(2 * count, 0);
+    if (!count || !have_results(e)) return MPX_OK;
+    HTRY(hipSetDevice(e->device));
+    TRY(e->decode_buf.alloc(16 * count));
+    if (launch_decode(e->view, e->stream, n, l0, count, e->decode_buf.as<uint64_t>()) != 0) return MPX_E_HIP;
+    HTRY(hipStreamSynchronize(e->stream));
+    return d2h(out, e->decode_buf, 2 * count);
+}
+
 extern "C" int mpx_read_chosen(mpx_engine *e, uint64_t first, uint64_t count, uint64_t *out)
 {
     if (!e || (count && !out)) return MPX_E_INVAL;
     if (first < e->cfg.shard_begin || first + count > e->cfg.shard_end) return MPX_E_RANGE;
     if (!count) return MPX_OK;
-    if (!have_results(e)) { std::memset(out, 0, count * 8); return MPX_OK; }
-    HTRY(hipSetDevice(e->device));
-    const uint64_t l0 = first - e->cfg.shard_begin;
-    const uint64_t b0 = l0 >> BSH, b1 = (l0 + count - 1) >> BSH;
-    std::vector<uint8_t> valid;
-    TRY(d2h(valid, e->chosen_valid, b1 - b0 + 1, b0));
-    HTRY(hipMemcpy(out, (const char *)e->chosen.p + l0 * 8, count * 8, hipMemcpyDeviceToHost));
-    for (uint64_t i = 0; i < count; ++i)
-        if (!valid[((l0 + i) >> BSH) - b0]) out[i] = 0;
+    std::vector<uint64_t> d;
+    TRY(decode_slots(e, e->cfg.num_nodes, first - e->cfg.shard_begin, count, d));
+    for (uint64_t i = 0; i < count; ++i) out[i] = d[2 * i + 1];
     return MPX_OK;
 }
 
@@ -486,21 +494,10 @@ extern "C" int mpx_read_node_state(mpx_engine *e, uint32_t node, uint64_t first,
     if (!e || node >= e->cfg.num_nodes) return MPX_E_INVAL;
     if (first < e->cfg.shard_begin || first + count > e->cfg.shard_end) return MPX_E_RANGE;
     if (!count) return MPX_OK;
-    std::vector<uint64_t> st(2 * count, 0);
-    std::vector<uint8_t> valid;
-    const uint64_t l0 = first - e->cfg.shard_begin;
-    const uint64_t b0 = l0 >> BSH, b1 = (l0 + count - 1) >> BSH;
-    if (have_results(e)) {
-        HTRY(hipSetDevice(e->device));
-        TRY(d2h(valid, e->st_valid, b1 - b0 + 1, (size_t)node * e->NB + b0));
-        HTRY(hipMemcpy(st.data(), (const char *)e->st.p + 16 * ((uint64_t)node * e->shard_len + l0), 16 * count,
-                       hipMemcpyDeviceToHost));
-    } else {
-        valid.assign(b1 - b0 + 1, 0);
-    }
+    std::vector<uint64_t> st;
+    TRY(decode_slots(e, node, first - e->cfg.shard_begin, count, st));
     for (uint64_t i = 0; i < count; ++i) {
-        uint64_t b = st[2 * i], w = st[2 * i + 1];
-        if (!valid[((l0 + i) >> BSH) - b0]) b = w = 0;
+        const uint64_t b = st[2 * i], w = st[2 * i + 1];
         const bool com = (w & W_PRESENT) && (w & W_COMMITTED);
         const bool acc = (w & W_PRESENT) && !(w & W_COMMITTED);
         if (acc_ballot) acc_ballot[i] = acc ? b : 0;
@@ -642,22 +639,14 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
     d.append("MPXR", 4);
     app<uint32_t>(d, 1); app<uint32_t>(d, N); app<uint32_t>(d, e->cfg.semantics);
     std::vector<uint64_t> st;
-    std::vector<uint8_t> valid;
-    TRY(d2h(valid, e->st_valid, (size_t)N * e->NB));
-    std::vector<uint64_t> chosen;
-    std::vector<uint8_t> cvalid;
-    TRY(d2h(chosen, e->chosen, e->shard_len));
-    TRY(d2h(cvalid, e->chosen_valid, e->NB));
     std::string m;
     for (uint32_t n = 0; n < N; ++n) {
         app<uint64_t>(d, r.scal[2 * n]);
         app<uint64_t>(d, r.scal[2 * n + 1]);
-        TRY(d2h(st, e->st, 2 * e->shard_len, 2 * (size_t)n * e->shard_len));
+        TRY(decode_slots(e, n, 0, e->shard_len, st));
         std::string sec;
         uint64_t cnt = 0;
-        std::vector<std::pair<uint64_t, uint64_t>> committed;   // for the executor
         for (uint64_t li = 0; li < e->shard_len; ++li) {
-            if (!valid[(size_t)n * e->NB + (li >> BSH)]) { li |= BS - 1; continue; }
             const uint64_t b = st[2 * li], w = st[2 * li + 1];
             if (!(w & W_PRESENT)) continue;
             const uint64_t kind = (w & W_COMMITTED) ? 2 : 1;
@@ -704,7 +693,6 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
         sec.clear(); cnt = 0;
         std::string payload;
         for (uint64_t li = 0; li < e->shard_len; ++li) {
-            if (!valid[(size_t)n * e->NB + (li >> BSH)]) break;
             const uint64_t w = st[2 * li + 1];
             if (!(w & W_PRESENT) || !(w & W_COMMITTED)) break;
             const uint64_t hd = w & W_HANDLE;
@@ -719,11 +707,11 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
     }
     uint64_t cnt = 0;
     std::string sec;
+    TRY(decode_slots(e, N, 0, e->shard_len, st));
     for (uint64_t li = 0; li < e->shard_len; ++li) {
-        if (!cvalid[li >> BSH]) { li |= BS - 1; continue; }
-        if (!(chosen[li] & W_PRESENT)) continue;
+        if (!(st[2 * li + 1] & W_PRESENT)) continue;
         app<uint64_t>(sec, e->cfg.shard_begin + li);
-        app<uint64_t>(sec, chosen[li] & W_HANDLE);
+        app<uint64_t>(sec, st[2 * li + 1] & W_HANDLE);
         ++cnt;
     }
     app<uint64_t>(d, cnt);
@@ -767,7 +755,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     const uint64_t G0 = 2 + N + K * (3 + 2ull * N), G1 = 1 + 2 * K;
     const uint64_t G = G0 + (uint64_t)(N - 1) * G1;
     const uint64_t E = L;                                       // one shared run per batch
-    if (G >= NONE32) return MPX_E_RANGE;
+    if (G >= NONE32 || E > MAX_ENTRIES) return MPX_E_RANGE;
     const uint64_t ballot = 1ull << 16;                         // (1 << 16) | node 0
     // host-side small tables
     HostTrace &h = e->ht;

@@ -553,7 +553,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     const uint64_t NB = ht.NB;
     uint64_t G = 0, E = 0, R = 0, GR = 0;
     for (auto &ns : nodes) { G += ns.type.size(); E += ns.e_iid.size(); R += ns.r_iid.size(); GR += ns.g_a.size(); }
-    if (G >= NONE32) return MPX_E_RANGE;
+    if (G >= NONE32 || E > MAX_ENTRIES) return MPX_E_RANGE;     // 8-byte state slots (mpx_internal.hpp)
     ht.m_type.reserve(G); ht.m_src.reserve(G); ht.m_cnt.reserve(G); ht.m_node.reserve(G);
     ht.m_ballot.reserve(G); ht.m_aux.reserve(G); ht.m_ent.reserve(G);
     ht.e_val.reserve(E); ht.e_iid.reserve(E); ht.r_pid.reserve(R); ht.r_val.reserve(R); ht.r_iid.reserve(R);

@@ -376,9 +376,10 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
     uint64_t off = lane < 2 ? v.cf_off[b + lane] : 0;
     uint64_t fi = rl64(off, 0);
     const uint64_t fe = rl64(off, 1);
-    uint64_t cv[SPL];
+    uint32_t cv[SPL];                          // entry + 1 of the first chosen Value
+    uint64_t ch[SPL];                          // its handle (agreement check)
 #pragma unroll
-    for (uint32_t j = 0; j < SPL; ++j) cv[j] = 0;
+    for (uint32_t j = 0; j < SPL; ++j) { cv[j] = 0; ch[j] = 0; }
     while (fi < fe) {
         const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
         uint64_t fw0 = 0, fw1 = 0;
@@ -401,8 +402,10 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
             for (uint32_t j = 0; j < SPL; ++j) {
                 if (k[j] < 0) continue;
                 const uint64_t iid = v.shard_begin + li0 + lane + 64 * j;
-                if (!cv[j]) { cv[j] = W_PRESENT | val[j]; ++cC; if (v.digest) dig += chosen_digest(iid, val[j]); }
-                else if ((cv[j] & W_HANDLE) != val[j]) record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, iid);
+                if (!cv[j]) {
+                    cv[j] = (uint32_t)(ent + k[j] + 1); ch[j] = val[j]; ++cC;
+                    if (v.digest) dig += chosen_digest(iid, val[j]);
+                } else if (ch[j] != val[j]) record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, iid);
             }
         }
         fi += nf;
@@ -420,6 +423,27 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
     }
 }
 
+// A state slot back to {ballot, PRESENT | COMMITTED? | handle}
+// (mpx_internal.hpp): the fixing message's type and header ballot (member:
+// the entry's proposal id), the Value handle from the entry pool
+__device__ inline void decode_slot(const DevView &v, uint64_t s, uint64_t &ballot, uint64_t &word)
+{
+    ballot = word = 0;
+    if (!s) return;
+    const uint32_t g = slot_msg(s);
+    const uint64_t ent = slot_ent(s);
+    ballot = v.semantics == MPX_SEM_MEMBER ? v.e_pid[ent] : v.m_ballot[g];
+    word = W_PRESENT | (v.m_type[g] == MPX_MSG_COMMIT ? W_COMMITTED : 0) | v.e_val[ent];
+}
+
+__device__ inline uint64_t slot_digest(const DevView &v, uint32_t n, uint64_t iid, uint64_t s)
+{
+    if (!s) return 0;
+    uint64_t b, w;
+    decode_slot(v, s, b, w);
+    return state_digest(n, iid, (w & W_COMMITTED) ? 2 : 1, b, w & W_HANDLE);
+}
+
 // Wave id with consecutive ids on one XCD: workgroups are dealt round-robin
 // over the 8 XCDs (blockIdx % 8), so id = xcd * (waves per XCD) + local id.
 // Neighbouring buckets then share their XCD's L2 (headers, descriptors).
@@ -435,23 +459,27 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // A wave owns a bucket and applies its N (node, bucket) pairs.  The pairs are
 // bucket-major in the CSR, so the whole bucket is three lane-parallel loads:
 // the N+1 CSR offsets, all its fragment descriptors (lane i = fragment i, at
-// most 64) and the scan results (flags, ballot) of their messages; the chosen
-// log's descriptors ride along.  These are issued one / two buckets ahead, so
-// a bucket costs about one memory round trip however many nodes it has.
-// Lane l holds slots {2l, 2l+1, 128+2l, 129+2l}, so a full 256-entry run moves
-// with 16-byte loads and stores.  Per slot only the Value that fixes its final
-// state is loaded (pass 1), and a run already in registers — the same
-// broadcast at the previous node, stored once in the content-addressed pool —
-// is not loaded again: a clean bucket reads its Values once for all N
-// acceptors and for the chosen log, written from the same registers when the
-// bucket's one live batch is that run (chosen_valid[b] = 1; k_chosen walks
-// every other bucket).
+// most 64) and the scan flags of their messages; the chosen log's descriptor
+// rides along.  These are issued one / two buckets ahead, so a bucket costs
+// about one memory round trip however many nodes it has.
+//
+// Per slot only the fragment that fixes its final state matters: the first
+// COMMIT covering it (first commit wins, multi/paxos.cpp:1515, and later
+// accepts skip committed slots, :1380), else the last granted ACCEPT (:1387).
+// The slot is written as (that message, its entry) — 8 bytes, no Value load
+// (mpx_internal.hpp) — so a pair is one pass over ≤ 63 descriptors in
+// registers and two 16-byte stores per lane (lane l: slots {2l, 2l+1} and
+// {128+2l, 129+2l}, 1 KiB contiguous per wave instruction).  The chosen log of
+// a bucket whose one live batch is a full run is written the same way.  Value
+// loads happen only for the re-commit check (:1508, rare) and in digest runs.
 //
 // A pair is taken here iff (same predicate as ingest.cpp's work list):
 // N <= FAST_MAX_NODES, the bucket has at most FAST_MAX_FRAGS fragments, the pair's fragments are all dense
 // ACCEPT / COMMIT runs and its node has no PREPARE after the first of them —
 // its snapshot events see empty state, so skipping them changes no output.
-template <int WAVES_PER_EU>
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+template <int WAVES_PER_EU, bool DIGEST>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
 {
     __shared__ unsigned long long red[4][5];
@@ -489,8 +517,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
     uint64_t off_c = ld_off(b_c), off_n = ld_off(b_c + nwaves);
     uint64_t nw0, nw1;
     ld_frags(off_c, nw0, nw1);
-    uint64_t cache_ent = ~0ull;                // entry offset of the full run held in cval
-    uint64_t cval[SPL] = {0, 0, 0, 0};
+    const uint32_t s0 = 2 * lane, s2 = 128 + 2 * lane;
     for (; b_c < NB; b_c += nwaves) {
         const uint64_t b = b_c;
         const uint64_t off = off_c;
@@ -499,15 +526,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         ld_frags(off_n, nw0, nw1);
         off_c = off_n;
         off_n = ld_off(b + 2 * nwaves);
-        // stage 3: scan results of this bucket's fragment messages; lane 63:
+        // stage 3: scan flags of this bucket's fragment messages; lane 63:
         // whether the chosen-log fragment's batch reached its quorum
         const uint64_t f_base = rl64(off, 0);
         const uint32_t total = (uint32_t)(rl64(off, N) - f_base);
         if (total > FAST_MAX_FRAGS) continue;  // every pair is on the general work list
         const uint32_t fmsg = (uint32_t)fw1;
         uint32_t fflag = 0;
-        uint64_t fbal = 0;
-        if (lane < total) { fflag = v.m_flags[fmsg]; fbal = v.m_ballot[fmsg]; }
+        if (lane < total) fflag = v.m_flags[fmsg];
         else if (lane == 63 && fmsg != NONE32) fflag = v.b_chosen[fmsg] != NONE32;
         // One wait per bucket, before its stores: vmcnt counts stores too
         // (gfx9), and a wait inside the node loop on these registers would
@@ -516,26 +542,22 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         // lanes whose fragment disqualifies its pair from the lean path
         const uint32_t fl = (uint32_t)(fw1 >> 56);
         const uint64_t badm = __ballot(lane < total && !((fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT)));
-        // lanes whose fragment is a full, 16-byte aligned run: a pair made only
-        // of those treats all 256 slots alike (uniform path below)
-        const uint64_t fullm = __ballot(lane < total && ((fw1 >> 48) & 0xFF) == 0 && ((fw1 >> 32) & 0xFFFF) == BS &&
-                                        !(fw0 & 1));
+        // lanes whose fragment is a full run: a pair made only of those treats
+        // all 256 slots alike (uniform path below)
+        const uint64_t fullm = __ballot(lane < total && ((fw1 >> 48) & 0xFF) == 0 && ((fw1 >> 32) & 0xFFFF) == BS);
         const uint64_t li0 = b << BSH;
         const uint64_t ib = v.shard_begin + li0;
-        const uint32_t s0 = 2 * lane, s2 = 128 + 2 * lane;
         for (uint32_t n = 0; n < N; ++n) {
             const uint32_t f0 = (uint32_t)(rl64(off, n) - f_base), f1 = (uint32_t)(rl64(off, n + 1) - f_base);
             if (f1 == f0) continue;
             const uint64_t rng = (f1 - f0 >= 64 ? ~0ull : ((1ull << (f1 - f0)) - 1)) << f0;
             if ((badm & rng) || rl32(fmsg, f0) < rl32(nap, n)) continue;
-            uint64_t sb0 = 0, sb1 = 0, sb2 = 0, sb3 = 0, sw0 = 0, sw1 = 0, sw2 = 0, sw3 = 0;
+            uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the lane's four slots
             uint32_t bad = 0;
             bool done = false;
             if ((fullm & rng) == rng) {
                 // Uniform pair: every fragment covers all 256 slots, so the walk
-                // below is wave-uniform (scalar): the fixing fragment is the first
-                // COMMIT (:1515; later accepts skip it, :1380), else the last
-                // granted ACCEPT (:1387).  A second COMMIT needs the per-slot
+                // is wave-uniform (scalar).  A second COMMIT needs the per-slot
                 // Value check (:1508): left to the per-slot path.
                 uint32_t fix = NONE32, nA = 0, nL = 0;
                 bool comm = false, again = false;
@@ -548,29 +570,17 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
                     cA += nA * SPL;
                     cL += nL * SPL;
                     if (fix != NONE32) {
-                        const uint64_t ent = rl64(fw0, fix);
-                        if (ent != cache_ent || (v.knobs & 4)) {
-                            const u64x2 x0 = *reinterpret_cast<const u64x2 *>(e_val + ent + 2 * lane);
-                            const u64x2 x1 = *reinterpret_cast<const u64x2 *>(e_val + ent + 128 + 2 * lane);
-                            cval[0] = x0.x; cval[1] = x0.y; cval[2] = x1.x; cval[3] = x1.y;
-                            cache_ent = ent;
-                        }
-                        const uint64_t bu = rl64(fbal, fix);
-                        const uint64_t tag = W_PRESENT | (comm ? W_COMMITTED : 0);
-                        sb0 = sb1 = sb2 = sb3 = bu;
-                        sw0 = tag | cval[0]; sw1 = tag | cval[1]; sw2 = tag | cval[2]; sw3 = tag | cval[3];
+                        const uint64_t base = slot_of(rl32(fmsg, fix), rl64(fw0, fix));
+                        q0 = base + s0; q1 = base + s0 + 1; q2 = base + s2; q3 = base + s2 + 1;
                     }
                     done = true;
                 }
             }
             if (!done) {
-                // Pass 1, descriptors only: per slot the fragment that fixes its final
-                // state — the first COMMIT covering it (first commit wins, :1515, and
-                // later accepts skip committed slots, :1380), else the last granted
-                // ACCEPT (:1387) — and the counters.  Values of overwritten accepts
-                // never reach an output (no snapshot events here) and are not loaded.
-                uint32_t src = 0xFFFFFFFFu;            // 8 bits per slot: fragment lane, 0xFF none
-                uint32_t com = 0;                      // bit j: slot j committed
+                // Per slot: the fixing fragment (8 bits per slot: its lane, 0xFF
+                // none), the committed bit and the counters
+                uint32_t src = 0xFFFFFFFFu;
+                uint32_t com = 0;
                 uint32_t recommit = 0;                 // a later COMMIT covers a committed slot
                 for (uint32_t a = f0; a < f1; ++a) {
                     const uint64_t w1 = rl64(fw1, a);
@@ -591,56 +601,21 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
                         }
                     }
                 }
-                // Pass 2: one value load per slot, from its fixing fragment; a full
-                // run fixing every slot is one pair of 16-byte loads per lane, or
-                // none when that run is the one already in registers
-                uint64_t val[SPL] = {0, 0, 0, 0};
-                const uint32_t a0 = src & 0xFF;
-                const bool same = src == (a0 | (a0 << 8) | (a0 << 16) | (a0 << 24)) && a0 != 0xFF;
-                const uint32_t a_u = __builtin_amdgcn_readfirstlane(a0);
-                const bool uni = __ballot(!same || a0 != a_u) == 0;
-                bool full = false;
-                uint64_t ent_u = 0, w1_u = 0;
-                if (uni) {
-                    w1_u = rl64(fw1, a_u);
-                    ent_u = rl64(fw0, a_u);
-                    full = ((w1_u >> 48) & 0xFF) == 0 && ((w1_u >> 32) & 0xFFFF) == BS && !(ent_u & 1);
+                // the slot from its fixing fragment's descriptor, fetched with a
+                // lane-indexed shuffle issued by every lane
+#define MPX_SLOT(J, Q)                                                                        \
+                {                                                                             \
+                    const uint32_t fa = (src >> (8 * J)) & 0xFF;                              \
+                    const uint32_t s = J < 2 ? 2 * lane + J : 128 + 2 * lane + (J - 2);       \
+                    const uint64_t ent = __shfl(fw0, (int)(fa & 63), 64);                     \
+                    const uint64_t w1 = __shfl(fw1, (int)(fa & 63), 64);                      \
+                    if (fa != 0xFF) Q = slot_of((uint32_t)w1, ent + (s - ((uint32_t)(w1 >> 48) & 0xFF))); \
                 }
-                if (full) {
-                    // every slot fixed by one full run: ballot and committed bit are wave-uniform
-                    if (ent_u != cache_ent || (v.knobs & 4)) {
-                        const u64x2 x0 = *reinterpret_cast<const u64x2 *>(e_val + ent_u + 2 * lane);
-                        const u64x2 x1 = *reinterpret_cast<const u64x2 *>(e_val + ent_u + 128 + 2 * lane);
-                        cval[0] = x0.x; cval[1] = x0.y; cval[2] = x1.x; cval[3] = x1.y;
-                        cache_ent = ent_u;
-                    }
-#pragma unroll
-                    for (uint32_t j = 0; j < SPL; ++j) val[j] = cval[j];
-                    const uint64_t bu = rl64(fbal, a_u);
-                    const uint64_t tag = W_PRESENT | ((w1_u >> 60) == K_COMMIT ? W_COMMITTED : 0);
-                    sb0 = sb1 = sb2 = sb3 = bu;
-                    sw0 = tag | val[0]; sw1 = tag | val[1]; sw2 = tag | val[2]; sw3 = tag | val[3];
-                } else {
-                    // per-lane fragment lane: fetch its descriptor with a lane-indexed
-                    // shuffle, issued by every lane (a bpermute from an inactive lane reads 0)
-#define MPX_SLOT(J, SB, SW)                                                                   \
-                    {                                                                             \
-                        const uint32_t fa = (src >> (8 * J)) & 0xFF;                              \
-                        const uint32_t s = J < 2 ? 2 * lane + J : 128 + 2 * lane + (J - 2);       \
-                        const uint64_t ent = __shfl(fw0, (int)(fa & 63), 64);                     \
-                        const uint64_t w1 = __shfl(fw1, (int)(fa & 63), 64);                      \
-                        const uint64_t bj = __shfl(fbal, (int)(fa & 63), 64);                     \
-                        if (fa != 0xFF) {                                                         \
-                            val[J] = e_val[ent + (s - ((uint32_t)(w1 >> 48) & 0xFF))];            \
-                            SB = bj;                                                              \
-                            SW = W_PRESENT | (((com >> J) & 1) ? W_COMMITTED : 0) | val[J];       \
-                        }                                                                         \
-                    }
-                    MPX_SLOT(0, sb0, sw0) MPX_SLOT(1, sb1, sw1) MPX_SLOT(2, sb2, sw2) MPX_SLOT(3, sb3, sw3)
+                MPX_SLOT(0, q0) MPX_SLOT(1, q1) MPX_SLOT(2, q2) MPX_SLOT(3, q3)
 #undef MPX_SLOT
-                }
                 // re-commit check (rare): every later COMMIT must carry the committed Value (:1508)
                 if (__ballot(recommit)) {
+                    const uint64_t q[SPL] = {q0, q1, q2, q3};
                     for (uint32_t a = f0; a < f1; ++a) {
                         const uint64_t w1 = rl64(fw1, a);
                         if ((w1 >> 60) != K_COMMIT) continue;
@@ -650,48 +625,39 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
                         for (uint32_t j = 0; j < SPL; ++j) {
                             const uint32_t s = j < 2 ? 2 * lane + j : 128 + 2 * lane + (j - 2);
                             if (s < st0 || s >= st0 + cnt || ((src >> (8 * j)) & 0xFF) == a) continue;
-                            if (e_val[ent + (s - st0)] != val[j]) bad = 1;
+                            if (e_val[ent + (s - st0)] != e_val[slot_ent(q[j])]) bad = 1;
                         }
                     }
                 }
             }
             if (__ballot(bad) && lane == 0) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, ib);
-            uint64_t *srow = v.st + 2 * ((uint64_t)n * v.shard_len + li0);
-            u64x2 w;
+            uint64_t *srow = v.st + (uint64_t)n * v.shard_len + li0;
             if (v.knobs & 16) {
                 // experiment: no state stores
             } else if (li0 + BS <= v.shard_len) {
-                w.x = sb0; w.y = sw0; *reinterpret_cast<u64x2 *>(srow + 2 * s0) = w;
-                w.x = sb1; w.y = sw1; *reinterpret_cast<u64x2 *>(srow + 2 * s0 + 2) = w;
-                w.x = sb2; w.y = sw2; *reinterpret_cast<u64x2 *>(srow + 2 * s2) = w;
-                w.x = sb3; w.y = sw3; *reinterpret_cast<u64x2 *>(srow + 2 * s2 + 2) = w;
+                *reinterpret_cast<u64x2 *>(srow + s0) = u64x2{q0, q1};
+                *reinterpret_cast<u64x2 *>(srow + s2) = u64x2{q2, q3};
             } else {
-                if (li0 + s0 < v.shard_len) { w.x = sb0; w.y = sw0; *reinterpret_cast<u64x2 *>(srow + 2 * s0) = w; }
-                if (li0 + s0 + 1 < v.shard_len) { w.x = sb1; w.y = sw1; *reinterpret_cast<u64x2 *>(srow + 2 * s0 + 2) = w; }
-                if (li0 + s2 < v.shard_len) { w.x = sb2; w.y = sw2; *reinterpret_cast<u64x2 *>(srow + 2 * s2) = w; }
-                if (li0 + s2 + 1 < v.shard_len) { w.x = sb3; w.y = sw3; *reinterpret_cast<u64x2 *>(srow + 2 * s2 + 2) = w; }
+                if (li0 + s0 < v.shard_len) srow[s0] = q0;
+                if (li0 + s0 + 1 < v.shard_len) srow[s0 + 1] = q1;
+                if (li0 + s2 < v.shard_len) srow[s2] = q2;
+                if (li0 + s2 + 1 < v.shard_len) srow[s2 + 1] = q3;
             }
-            if (v.digest) {
-                if (sw0) dig += state_digest(n, ib + s0, (sw0 & W_COMMITTED) ? 2 : 1, sb0, sw0 & W_HANDLE);
-                if (sw1) dig += state_digest(n, ib + s0 + 1, (sw1 & W_COMMITTED) ? 2 : 1, sb1, sw1 & W_HANDLE);
-                if (sw2) dig += state_digest(n, ib + s2, (sw2 & W_COMMITTED) ? 2 : 1, sb2, sw2 & W_HANDLE);
-                if (sw3) dig += state_digest(n, ib + s2 + 1, (sw3 & W_COMMITTED) ? 2 : 1, sb3, sw3 & W_HANDLE);
-            }
+            if (DIGEST)
+                dig += slot_digest(v, n, ib + s0, q0) + slot_digest(v, n, ib + s0 + 1, q1) +
+                       slot_digest(v, n, ib + s2, q2) + slot_digest(v, n, ib + s2 + 1, q3);
             if (lane == 0) v.st_valid[(uint64_t)n * NB + b] = 1;
         }
-        // the bucket's chosen log from the registers, when its one live batch is the cached run
+        // the bucket's chosen log, when its one live batch is a full run
         const uint64_t c0 = rl64(fw0, 63), c1 = rl64(fw1, 63);
-        if (rl32(fflag, 63) && c0 == cache_ent && ((c1 >> 48) & 0xFF) == 0 && ((c1 >> 32) & 0xFFFF) == BS &&
-            li0 + BS <= v.shard_len) {
-            u64x2 w;
-            w.x = W_PRESENT | cval[0]; w.y = W_PRESENT | cval[1];
-            *reinterpret_cast<u64x2 *>(v.chosen + li0 + s0) = w;
-            w.x = W_PRESENT | cval[2]; w.y = W_PRESENT | cval[3];
-            *reinterpret_cast<u64x2 *>(v.chosen + li0 + s2) = w;
+        if (rl32(fflag, 63) && ((c1 >> 48) & 0xFF) == 0 && ((c1 >> 32) & 0xFFFF) == BS && li0 + BS <= v.shard_len) {
+            const uint32_t cb = (uint32_t)c0 + 1;
+            *reinterpret_cast<u32x2 *>(v.chosen + li0 + s0) = u32x2{cb + s0, cb + s0 + 1};
+            *reinterpret_cast<u32x2 *>(v.chosen + li0 + s2) = u32x2{cb + s2, cb + s2 + 1};
             cC += SPL;
-            if (v.digest)
-                cdig += chosen_digest(ib + s0, cval[0]) + chosen_digest(ib + s0 + 1, cval[1]) +
-                        chosen_digest(ib + s2, cval[2]) + chosen_digest(ib + s2 + 1, cval[3]);
+            if (DIGEST)
+                cdig += chosen_digest(ib + s0, e_val[c0 + s0]) + chosen_digest(ib + s0 + 1, e_val[c0 + s0 + 1]) +
+                        chosen_digest(ib + s2, e_val[c0 + s2]) + chosen_digest(ib + s2 + 1, e_val[c0 + s2 + 1]);
             if (lane == 0) v.chosen_valid[b] = 1;
         }
     }
@@ -775,9 +741,10 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         off_cur = off_nxt;
         off_nxt = rt1(it + 2 * stride);
         const uint64_t li0 = (uint64_t)b << BSH;
-        uint64_t sb[SPL], sw[SPL];
+        uint64_t sb[SPL], sw[SPL];               // decoded state (checks, snapshots, digest)
+        uint64_t sm[SPL];                        // the slot as stored: (msg, entry)
 #pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) { sb[j] = sw[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
+        for (uint32_t j = 0; j < SPL; ++j) { sb[j] = sw[j] = sm[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
 
         bool first = true;
         while (fi < fe || ei < ee) {
@@ -860,9 +827,11 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 } else if (learn) {
                                     sb[j] = pid;
                                     sw[j] = W_PRESENT | W_COMMITTED | val[j];
+                                    sm[j] = slot_of(rl32(fmsg, a), ent + k[j]);
                                 } else if (!(sw[j] & W_PRESENT)) {
                                     sb[j] = pid;
                                     sw[j] = W_PRESENT | val[j];
+                                    sm[j] = slot_of(rl32(fmsg, a), ent + k[j]);
                                     ++cA;
                                 }
                                 cL += learn;
@@ -875,6 +844,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 if (k[j] >= 0 && !(sw[j] & W_COMMITTED)) {           // :1380
                                     sb[j] = ballot;                                   // :1387
                                     sw[j] = W_PRESENT | val[j];
+                                    sm[j] = slot_of(rl32(fmsg, a), ent + k[j]);
                                     ++cA;
                                 }
                         }
@@ -889,6 +859,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 } else {
                                     sb[j] = ballot;                                   // :1515
                                     sw[j] = W_PRESENT | W_COMMITTED | val[j];
+                                    sm[j] = slot_of(rl32(fmsg, a), ent + k[j]);
                                 }
                                 ++cL;
                             }
@@ -940,14 +911,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                         if (t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
-                                if (!(sw[j] & W_COMMITTED)) sb[j] = sw[j] = 0;
+                                if (!(sw[j] & W_COMMITTED)) sb[j] = sw[j] = sm[j] = 0;
                         }
                     } else if (t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
                         // the Acceptor is deleted / recreated: its accepted values go
                         // (member/paxos.cpp:1952-1957); learned ones stay with the Learner
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j)
-                            if (!(sw[j] & W_COMMITTED)) sb[j] = sw[j] = 0;
+                            if (!(sw[j] & W_COMMITTED)) sb[j] = sw[j] = sm[j] = 0;
                     } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
 #pragma unroll 1
                         for (uint32_t j = 0; j < SPL; ++j) {
@@ -972,11 +943,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 #pragma unroll
             for (uint32_t j = 0; j < SPL; ++j) {
                 const uint64_t li = li0 + lane + 64 * j;
-                if (li < v.shard_len) {
-                    uint64_t *s = v.st + 2 * ((uint64_t)n * v.shard_len + li);
-                    u64x2 w; w.x = sb[j]; w.y = sw[j];
-                    *reinterpret_cast<u64x2 *>(s) = w;
-                }
+                if (li < v.shard_len) v.st[(uint64_t)n * v.shard_len + li] = sm[j];
                 if (sw[j])
                     if (v.digest) dig += state_digest(n, v.shard_begin + li, (sw[j] & W_COMMITTED) ? 2 : 1, sb[j], sw[j] & W_HANDLE);
             }
@@ -1083,6 +1050,31 @@ __global__ void k_reset(DevView v, uint32_t n_partials)
 
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
+// Readback (mpx_read_node_state / mpx_read_chosen / mpx_dump_result): slots of
+// one node, or the chosen log (node >= N), to {ballot, word} pairs
+__global__ __launch_bounds__(256) void k_decode(DevView v, uint32_t node, uint64_t l0, uint64_t count, uint64_t *out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    const uint64_t li = l0 + i;
+    uint64_t b = 0, w = 0;
+    if (node >= v.N) {
+        const uint32_t c = v.chosen_valid[li >> BSH] ? v.chosen[li] : 0;
+        if (c) w = W_PRESENT | v.e_val[c - 1];
+    } else if (v.st_valid[(uint64_t)node * v.NB + (li >> BSH)]) {
+        decode_slot(v, v.st[(uint64_t)node * v.shard_len + li], b, w);
+    }
+    out[2 * i] = b;
+    out[2 * i + 1] = w;
+}
+
+int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, uint64_t count, uint64_t *out)
+{
+    if (!count) return 0;
+    hipLaunchKernelGGL(k_decode, dim3(cdiv(count, 256)), dim3(256), 0, (hipStream_t)stream, v, node, l0, count, out);
+    return (int)hipGetLastError();
+}
+
 int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, void *ev_apply0,
                void *ev_apply1, void *ev_end)
 {
@@ -1107,10 +1099,13 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
     } else {
         // multi: the lean kernel also writes the chosen log of clean buckets
-        switch (g.variant) {
-        case 1: hipLaunchKernelGGL((k_apply_fast<4>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-        case 2: hipLaunchKernelGGL((k_apply_fast<5>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-        default: hipLaunchKernelGGL((k_apply_fast<1>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        // digest runs (verification) take their own instantiation, so the
+        // timed kernel carries no digest code
+        if (v.digest) hipLaunchKernelGGL((k_apply_fast<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+        else switch (g.variant) {
+        case 1: hipLaunchKernelGGL((k_apply_fast<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        case 2: hipLaunchKernelGGL((k_apply_fast<5, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         }
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);

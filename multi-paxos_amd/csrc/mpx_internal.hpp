@@ -11,11 +11,16 @@
 //     256-instance bucket, listed per pair in processing order (CSR); pairs are
 //     bucket-major, q = bucket * N + node, so one wave can walk a bucket's
 //     nodes and reuse the shared Values
-//   * state: one 16-byte slot per (node, instance) = {ballot, word}
-//       word = PRESENT | COMMITTED? | handle  — accepted and committed entries
-//       of a node are disjoint (OnCommit erases accepted_values_,
-//       multi/paxos.cpp:1501; OnAccept skips committed, :1380), so one slot
-//       holds either.
+//   * state: one 8-byte slot per (node, instance) = (msg + 1) << 32 | entry,
+//       0 = empty: the message that fixed the slot and the entry-pool index of
+//       its Value.  The message's type says accepted or committed, its header
+//       ballot is the tag (multi; member: the entry's proposal id e_pid), the
+//       pool holds the Value handle — AcceptedValue(id, value) by reference to
+//       the resident trace (k_decode turns a slot back into {ballot, word}).
+//       Accepted and committed entries of a node are disjoint (OnCommit erases
+//       accepted_values_, multi/paxos.cpp:1501; OnAccept skips committed,
+//       :1380), so one slot holds either.
+//   * chosen log: one u32 per instance = entry + 1 of the chosen Value, 0 = none
 #pragma once
 #include <cstdint>
 #include <cstddef>
@@ -38,6 +43,12 @@ constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr uint64_t W_PRESENT = 1ull << 63;
 constexpr uint64_t W_COMMITTED = 1ull << 62;
 constexpr uint64_t W_HANDLE = (1ull << 62) - 1;
+
+// state slot encoding (see the layout note above); entries and messages < 2^32 - 1
+MPX_HD inline uint64_t slot_of(uint32_t msg, uint64_t ent) { return ((uint64_t)(msg + 1) << 32) | ent; }
+MPX_HD inline uint32_t slot_msg(uint64_t s) { return (uint32_t)(s >> 32) - 1; }
+MPX_HD inline uint64_t slot_ent(uint64_t s) { return s & 0xFFFFFFFFull; }
+constexpr uint64_t MAX_ENTRIES = 0xFFFFFFFEull;
 
 // m_flags bits, written by the header scan / proposer kernels
 enum : uint8_t {
@@ -156,9 +167,9 @@ struct DevView {
     const uint64_t *cf_off;         // NB+1
     const Frag *cfrags;
     // state
-    uint64_t *st;                   // 2 words per (node, instance)
+    uint64_t *st;                   // one slot per (node, instance), node-major
     uint8_t *st_valid;              // per (node, bucket): node * NB + bucket
-    uint64_t *chosen;               // per instance
+    uint32_t *chosen;               // per instance: entry + 1
     uint8_t *chosen_valid;          // per bucket
     // outputs
     OutRec *out;
@@ -207,6 +218,10 @@ MPX_HD inline uint64_t scalar_digest(uint32_t node, uint64_t promised, uint64_t 
 struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, variant; };
 int launch_run(const DevView &v, void *stream, LaunchGeom g, void *ev_begin, void *ev_apply0,
                void *ev_apply1, void *ev_end);
+// readback: count slots of node `node` (node >= N: the chosen log) from shard
+// offset l0 -> out, 2 words each {ballot, PRESENT | COMMITTED? | handle}
+// (chosen: {0, PRESENT | handle}); unwritten buckets read as empty
+int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, uint64_t count, uint64_t *out);
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
                      uint64_t G0, uint64_t G1, uint64_t ballot, uint32_t NB,
                      uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,
