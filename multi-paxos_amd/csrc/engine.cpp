@@ -222,7 +222,7 @@ static int finish_view(mpx_engine *e)
     v.shard_begin = e->cfg.shard_begin;
     v.shard_len = e->shard_len;
     v.num_msgs = e->num_msgs;
-    TRY(e->st.alloc((size_t)N * e->shard_len * 8));
+    TRY(e->st.alloc((size_t)N * e->shard_len * 4));
     TRY(e->st_valid.alloc((size_t)N * e->NB));
     TRY(e->chosen.alloc(e->shard_len * 4));
     TRY(e->chosen_valid.alloc(e->NB));
@@ -239,7 +239,7 @@ static int finish_view(mpx_engine *e)
     if (!e->out_cap) e->out_cap = 1 << 16;
     TRY(e->out.alloc(e->out_cap * sizeof(OutRec)));
     TRY(e->node_scal.alloc(16ull * N));
-    v.st = e->st.as<uint64_t>();
+    v.st = e->st.as<uint32_t>();
     v.st_valid = e->st_valid.as<uint8_t>();
     v.chosen = e->chosen.as<uint32_t>();
     v.chosen_valid = e->chosen_valid.as<uint8_t>();
@@ -755,7 +755,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     const uint64_t G0 = 2 + N + K * (3 + 2ull * N), G1 = 1 + 2 * K;
     const uint64_t G = G0 + (uint64_t)(N - 1) * G1;
     const uint64_t E = L;                                       // one shared run per batch
-    if (G >= NONE32 || E > MAX_ENTRIES) return MPX_E_RANGE;
+    if (G >= NONE32 || E > MAX_ENTRIES || 2ull * N * K > MAX_FRAGS) return MPX_E_RANGE;
     const uint64_t ballot = 1ull << 16;                         // (1 << 16) | node 0
     // host-side small tables
     HostTrace &h = e->ht;

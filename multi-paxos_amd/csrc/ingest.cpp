@@ -553,7 +553,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     const uint64_t NB = ht.NB;
     uint64_t G = 0, E = 0, R = 0, GR = 0;
     for (auto &ns : nodes) { G += ns.type.size(); E += ns.e_iid.size(); R += ns.r_iid.size(); GR += ns.g_a.size(); }
-    if (G >= NONE32 || E > MAX_ENTRIES) return MPX_E_RANGE;     // 8-byte state slots (mpx_internal.hpp)
+    if (G >= NONE32 || E > MAX_ENTRIES) return MPX_E_RANGE;     // chosen log (mpx_internal.hpp)
     ht.m_type.reserve(G); ht.m_src.reserve(G); ht.m_cnt.reserve(G); ht.m_node.reserve(G);
     ht.m_ballot.reserve(G); ht.m_aux.reserve(G); ht.m_ent.reserve(G);
     ht.e_val.reserve(E); ht.e_iid.reserve(E); ht.r_pid.reserve(R); ht.r_val.reserve(R); ht.r_iid.reserve(R);
@@ -682,6 +682,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     // fragment CSR per (node, bucket), stable (keeps message order)
     ht.f_off.assign(N * NB + 1, 0);
     for (uint64_t i = 0; i < N * NB; ++i) ht.f_off[i + 1] = ht.f_off[i] + fcount[i];
+    if (fr.size() > MAX_FRAGS) return MPX_E_RANGE;             // 4-byte state slots (mpx_internal.hpp)
     ht.frags.resize(fr.size());
     {
         std::vector<uint64_t> pos(ht.f_off.begin(), ht.f_off.end() - 1);

@@ -424,23 +424,27 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
 }
 
 // A state slot back to {ballot, PRESENT | COMMITTED? | handle}
-// (mpx_internal.hpp): the fixing message's type and header ballot (member:
-// the entry's proposal id), the Value handle from the entry pool
-__device__ inline void decode_slot(const DevView &v, uint64_t s, uint64_t &ballot, uint64_t &word)
+// (mpx_internal.hpp): the fixing fragment's message type and header ballot
+// (member: the entry's proposal id), the Value handle of its entry at bucket
+// position s (sparse runs: found in the run's slot list)
+__device__ inline void decode_slot(const DevView &v, uint32_t q, uint32_t s, uint64_t &ballot, uint64_t &word)
 {
     ballot = word = 0;
-    if (!s) return;
-    const uint32_t g = slot_msg(s);
-    const uint64_t ent = slot_ent(s);
-    ballot = v.semantics == MPX_SEM_MEMBER ? v.e_pid[ent] : v.m_ballot[g];
-    word = W_PRESENT | (v.m_type[g] == MPX_MSG_COMMIT ? W_COMMITTED : 0) | v.e_val[ent];
+    if (!q) return;
+    const Frag f = v.frags[q - 1];
+    uint64_t ent = f.entry + (s - f.start);
+    if (!(f.flags & FR_DENSE))
+        for (uint32_t k = 0; k < f.count; ++k)
+            if (v.e_slot[f.entry + k] == s) { ent = f.entry + k; break; }
+    ballot = v.semantics == MPX_SEM_MEMBER ? v.e_pid[ent] : v.m_ballot[f.msg];
+    word = W_PRESENT | ((f.flags >> 4) == K_COMMIT ? W_COMMITTED : 0) | v.e_val[ent];
 }
 
-__device__ inline uint64_t slot_digest(const DevView &v, uint32_t n, uint64_t iid, uint64_t s)
+__device__ inline uint64_t slot_digest(const DevView &v, uint32_t n, uint64_t iid, uint32_t q)
 {
-    if (!s) return 0;
+    if (!q) return 0;
     uint64_t b, w;
-    decode_slot(v, s, b, w);
+    decode_slot(v, q, (uint32_t)(iid - v.shard_begin) & (BS - 1), b, w);
     return state_digest(n, iid, (w & W_COMMITTED) ? 2 : 1, b, w & W_HANDLE);
 }
 
@@ -454,211 +458,283 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
     return (uint64_t)(blockIdx.x & 7) * per + (uint64_t)(blockIdx.x >> 3) * 4 + wv;
 }
 
-// Lean acceptor/learner apply, one bucket at a time, plus the chosen log.
-//
-// A wave owns a bucket and applies its N (node, bucket) pairs.  The pairs are
-// bucket-major in the CSR, so the whole bucket is three lane-parallel loads:
-// the N+1 CSR offsets, all its fragment descriptors (lane i = fragment i, at
-// most 64) and the scan flags of their messages; the chosen log's descriptor
-// rides along.  These are issued one / two buckets ahead, so a bucket costs
-// about one memory round trip however many nodes it has.
+// Lean acceptor/learner apply plus the chosen log, G consecutive buckets per
+// wave step (fast_group: G * N + 1 <= 64, at most 4).
 //
 // Per slot only the fragment that fixes its final state matters: the first
 // COMMIT covering it (first commit wins, multi/paxos.cpp:1515, and later
 // accepts skip committed slots, :1380), else the last granted ACCEPT (:1387).
-// The slot is written as (that message, its entry) — 8 bytes, no Value load
-// (mpx_internal.hpp) — so a pair is one pass over ≤ 63 descriptors in
-// registers and two 16-byte stores per lane (lane l: slots {2l, 2l+1} and
-// {128+2l, 129+2l}, 1 KiB contiguous per wave instruction).  The chosen log of
-// a bucket whose one live batch is a full run is written the same way.  Value
+// The slot is written as that fragment's index — 4 bytes, no Value load
+// (mpx_internal.hpp).
+//
+// Lane p < G*N owns pair (bucket b0 + p / N, node p % N); pairs are
+// bucket-major in the CSR, so a step's offsets are one contiguous load.  Each
+// pair lane loads its first FAST_PAIR_FRAGS descriptors and their scan flags
+// itself and plans its pair in registers: when all its fragments are full
+// runs (the clean case) the fixing fragment is wave-uniform per pair and the
+// pair is one 16-byte store per lane — lane l holds slots 4l..4l+3, so a
+// node row gets G KiB of contiguous stores per step.  The three dependent
+// loads (offsets, descriptors, flags) are issued two / one / zero steps ahead,
+// so a step waits once for memory (vmcnt also counts stores on gfx9, so
+// every wait drains the step's stores: fewer, larger steps amortise it).
+// Pairs with partial runs, a re-commit or more fragments take the per-slot
+// path (descriptors loaded for that bucket, lane i = fragment i).  The
+// chosen log of a bucket whose one live batch is a full run is written the
+// same way (entry + 1 per slot); k_chosen walks every other bucket.  Value
 // loads happen only for the re-commit check (:1508, rare) and in digest runs.
 //
 // A pair is taken here iff (same predicate as ingest.cpp's work list):
 // N <= FAST_MAX_NODES, the bucket has at most FAST_MAX_FRAGS fragments, the pair's fragments are all dense
 // ACCEPT / COMMIT runs and its node has no PREPARE after the first of them —
 // its snapshot events see empty state, so skipping them changes no output.
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t FAST_PAIR_FRAGS = 2;      // descriptors a pair lane prefetches
+__host__ __device__ inline uint32_t fast_group(uint32_t N) { return N ? (63 / N < 4 ? 63 / N : 4) : 1; }
+
+__device__ inline bool frag_lean(uint64_t w1)
+{
+    const uint32_t fl = (uint32_t)(w1 >> 56);
+    return (fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT);
+}
+__device__ inline bool frag_full(uint64_t w1) { return ((w1 >> 48) & 0xFF) == 0 && ((w1 >> 32) & 0xFFFF) == BS; }
 
 template <int WAVES_PER_EU, bool DIGEST>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
 {
+    constexpr uint32_t F = FAST_PAIR_FRAGS;
     __shared__ unsigned long long red[4][5];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t cA = 0, cL = 0;
-    unsigned long long dig = 0, cC = 0, cdig = 0;
+    unsigned long long cA = 0, cL = 0, dig = 0, cC = 0, cdig = 0;
     const uint32_t N = v.N;
     const uint64_t NB = v.NB;
     if (N > FAST_MAX_NODES) return;
+    const uint32_t G = fast_group(N), GN = G * N;
+    const uint64_t steps = (NB + G - 1) / G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
-    const uint32_t nap = lane < N ? v.n_after_prepare[lane] : 0;
-    // stage 1 (two buckets ahead): CSR offsets of the bucket's pairs in lanes
-    // 0..N, of its chosen-log fragments in lanes 62..63
-    auto ld_off = [&](uint64_t b) -> uint64_t {
-        if (b >= NB) return 0;
-        if (lane <= N) return v.f_off[b * N + lane];
-        return lane >= 62 ? v.cf_off[b + lane - 62] : 0;
+    const uint32_t pg = lane / N, pn = lane - pg * N;    // pair of lane (lane < GN)
+    const uint32_t nap = lane < GN ? v.n_after_prepare[pn] : 0;
+    const uint32_t s0 = 4 * lane;                        // the lane's slots s0..s0+3
+
+    // stage 1 (two steps ahead): pair CSR offsets (lanes 0..nb*N), chosen-log
+    // CSR offsets (lanes 0..nb)
+    auto ld_off = [&](uint64_t st, uint64_t &oa, uint64_t &oc) {
+        oa = oc = 0;
+        if (st >= steps) return;
+        const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
+        if (lane <= nb * N) oa = v.f_off[b0 * N + lane];
+        if (lane <= nb) oc = v.cf_off[b0 + lane];
     };
-    // stage 2 (one bucket ahead): fragment descriptors, lane i = fragment i
-    // (at most FAST_MAX_FRAGS), lane 63 = the chosen-log fragment if it is the only one
-    auto ld_frags = [&](uint64_t off, uint64_t &w0, uint64_t &w1) {
-        const uint64_t fi = rl64(off, 0), fe = rl64(off, N);
-        const uint64_t ci = rl64(off, 62), ce = rl64(off, 63);
-        w0 = 0; w1 = NONE32;
-        const Frag *src = nullptr;
-        if (fe - fi <= FAST_MAX_FRAGS && lane < fe - fi) src = v.frags + fi + lane;
-        else if (lane == 63 && ce - ci == 1) src = v.cfrags + ci;
-        if (src) {
-            const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(src);
-            w0 = x.x; w1 = x.y;
+    // stage 2 (one step ahead): each pair's first F descriptors, each
+    // bucket's chosen-log descriptor when it is the only one
+    auto ld_desc = [&](uint64_t st, uint64_t oa, uint64_t oc, uint64_t (&e)[F], uint64_t (&w)[F], uint64_t &ce,
+                       uint64_t &cw) {
+        const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64);
+        const uint64_t c1 = __shfl(oc, (int)((lane + 1) & 63), 64);
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) { e[k] = 0; w[k] = NONE32; }
+        ce = 0; cw = NONE32;
+        if (st >= steps) return;
+        const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
+        if (lane < nb * N) {
+            const uint64_t len = o1 - oa;
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k)
+                if (k < len) {
+                    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + oa + k);
+                    e[k] = x.x; w[k] = x.y;
+                }
+        }
+        if (lane < nb && c1 - oc == 1) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.cfrags + oc);
+            ce = x.x; cw = x.y;
         }
     };
-    uint64_t b_c = xcd_wave_id(wv, v.knobs);
-    uint64_t off_c = ld_off(b_c), off_n = ld_off(b_c + nwaves);
-    uint64_t nw0, nw1;
-    ld_frags(off_c, nw0, nw1);
-    const uint32_t s0 = 2 * lane, s2 = 128 + 2 * lane;
-    for (; b_c < NB; b_c += nwaves) {
-        const uint64_t b = b_c;
-        const uint64_t off = off_c;
-        const uint64_t fw0 = nw0, fw1 = nw1;
-        // next bucket's descriptors, the one after's offsets
-        ld_frags(off_n, nw0, nw1);
-        off_c = off_n;
-        off_n = ld_off(b + 2 * nwaves);
-        // stage 3: scan flags of this bucket's fragment messages; lane 63:
-        // whether the chosen-log fragment's batch reached its quorum
-        const uint64_t f_base = rl64(off, 0);
-        const uint32_t total = (uint32_t)(rl64(off, N) - f_base);
-        if (total > FAST_MAX_FRAGS) continue;  // every pair is on the general work list
-        const uint32_t fmsg = (uint32_t)fw1;
-        uint32_t fflag = 0;
-        if (lane < total) fflag = v.m_flags[fmsg];
-        else if (lane == 63 && fmsg != NONE32) fflag = v.b_chosen[fmsg] != NONE32;
-        // One wait per bucket, before its stores: vmcnt counts stores too
-        // (gfx9), and a wait inside the node loop on these registers would
-        // drain every node's stores (vmcnt(0) vmcnt, expcnt / lgkmcnt free).
+
+    uint64_t st_c = xcd_wave_id(wv, v.knobs);
+    uint64_t oa_c, oc_c, oa_n, oc_n;
+    ld_off(st_c, oa_c, oc_c);
+    ld_off(st_c + nwaves, oa_n, oc_n);
+    uint64_t ne[F], nw[F], nce, ncw;
+    ld_desc(st_c, oa_c, oc_c, ne, nw, nce, ncw);
+    for (; st_c < steps; st_c += nwaves) {
+        const uint64_t st = st_c;
+        const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
+        const uint64_t oa = oa_c, oc = oc_c;
+        uint64_t e[F], w[F];
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) { e[k] = ne[k]; w[k] = nw[k]; }
+        const uint64_t ce = nce, cw = ncw;
+        // the next step's descriptors, the one after's offsets
+        ld_desc(st + nwaves, oa_n, oc_n, ne, nw, nce, ncw);
+        oa_c = oa_n; oc_c = oc_n;
+        ld_off(st + 2 * nwaves, oa_n, oc_n);
+        // stage 3: scan flags of this step's fragment messages, quorum of the
+        // chosen-log batch
+        uint32_t fg[F];
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) fg[k] = (uint32_t)w[k] != NONE32 ? v.m_flags[(uint32_t)w[k]] : 0;
+        const uint32_t clive = (uint32_t)cw != NONE32 ? v.b_chosen[(uint32_t)cw] != NONE32 : 0;
+        // One wait per step, before its stores (vmcnt(0); expcnt / lgkmcnt free).
         __builtin_amdgcn_s_waitcnt(0x0F70);
-        // lanes whose fragment disqualifies its pair from the lean path
-        const uint32_t fl = (uint32_t)(fw1 >> 56);
-        const uint64_t badm = __ballot(lane < total && !((fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT)));
-        // lanes whose fragment is a full run: a pair made only of those treats
-        // all 256 slots alike (uniform path below)
-        const uint64_t fullm = __ballot(lane < total && ((fw1 >> 48) & 0xFF) == 0 && ((fw1 >> 32) & 0xFFFF) == BS);
-        const uint64_t li0 = b << BSH;
-        const uint64_t ib = v.shard_begin + li0;
+
+        // plan, one pair per lane
+        const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64);
+        const uint64_t bb = __shfl(oa, (int)((pg * N) & 63), 64);           // bucket's first fragment
+        const uint64_t be = __shfl(oa, (int)((pg * N + N) & 63), 64);       // and its end
+        const bool pair = lane < nb * N;
+        const uint32_t len = pair ? (uint32_t)(o1 - oa) : 0;
+        const bool in_list = len && be - bb <= FAST_MAX_FRAGS;              // else: general work list
+        bool elig = in_list && len <= F, full = true, again = false, comm = false;
+        uint32_t fix = NONE32, nA = 0, nL = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) {
+            if (k >= len) continue;
+            elig = elig && frag_lean(w[k]);
+            full = full && frag_full(w[k]);
+            if ((w[k] >> 60) == K_COMMIT) { ++nL; if (comm) again = true; else { comm = true; fix = k; } }
+            else if (!comm && (fg[k] & F_GRANTED)) { ++nA; fix = k; }
+        }
+        elig = elig && (uint32_t)w[0] >= nap;
+        const bool uni = elig && full && !again;
+        const uint64_t uni_m = __ballot(uni);
+        const uint64_t slow_m = __ballot((elig && !uni) || (in_list && len > F));
+        if (uni) { cA += nA * BS; cL += nL * BS; }
+        const uint32_t qv = fix == NONE32 ? 0 : (uint32_t)(oa + fix + 1);
+        if (elig) v.st_valid[(uint64_t)pn * NB + b0 + pg] = 1;
+
+        // uniform pairs, node-major so each row gets its G buckets back to back
+        const bool whole = (b0 + nb) * BS <= v.shard_len;
         for (uint32_t n = 0; n < N; ++n) {
-            const uint32_t f0 = (uint32_t)(rl64(off, n) - f_base), f1 = (uint32_t)(rl64(off, n + 1) - f_base);
-            if (f1 == f0) continue;
-            const uint64_t rng = (f1 - f0 >= 64 ? ~0ull : ((1ull << (f1 - f0)) - 1)) << f0;
-            if ((badm & rng) || rl32(fmsg, f0) < rl32(nap, n)) continue;
-            uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the lane's four slots
-            uint32_t bad = 0;
-            bool done = false;
-            if ((fullm & rng) == rng) {
-                // Uniform pair: every fragment covers all 256 slots, so the walk
-                // is wave-uniform (scalar).  A second COMMIT needs the per-slot
-                // Value check (:1508): left to the per-slot path.
-                uint32_t fix = NONE32, nA = 0, nL = 0;
-                bool comm = false, again = false;
-                for (uint32_t a = f0; a < f1; ++a) {
-                    const bool commit = (rl64(fw1, a) >> 60) == K_COMMIT;
-                    if (commit) { ++nL; if (comm) again = true; else { comm = true; fix = a; } }
-                    else if (!comm && (rl32(fflag, a) & F_GRANTED)) { ++nA; fix = a; }
+            uint32_t *row = v.st + (uint64_t)n * v.shard_len + b0 * BS;
+            for (uint32_t g = 0; g < nb; ++g) {
+                const uint32_t p = g * N + n;
+                if (!((uni_m >> p) & 1)) continue;
+                const uint32_t q = rl32(qv, p);
+                if (v.knobs & 16) {
+                    // experiment: no state stores
+                } else if (whole) {
+                    *reinterpret_cast<u32x4 *>(row + g * BS + s0) = u32x4{q, q, q, q};
+                } else {
+#pragma unroll
+                    for (uint32_t j = 0; j < SPL; ++j)
+                        if ((b0 + g) * BS + s0 + j < v.shard_len) row[g * BS + s0 + j] = q;
                 }
-                if (!again) {
-                    cA += nA * SPL;
-                    cL += nL * SPL;
-                    if (fix != NONE32) {
-                        const uint64_t base = slot_of(rl32(fmsg, fix), rl64(fw0, fix));
-                        q0 = base + s0; q1 = base + s0 + 1; q2 = base + s2; q3 = base + s2 + 1;
+                if (DIGEST)
+#pragma unroll
+                    for (uint32_t j = 0; j < SPL; ++j) dig += slot_digest(v, n, v.shard_begin + (b0 + g) * BS + s0 + j, q);
+            }
+        }
+
+        // per-slot path (rare): the pair's bucket window, lane i = fragment i
+        for (uint64_t m = slow_m; m; m &= m - 1) {
+            const uint32_t p = (uint32_t)__builtin_ctzll(m);
+            const uint32_t g = p / N, n = p - g * N;
+            const uint64_t b = b0 + g, li0 = b << BSH, ib = v.shard_begin + li0;
+            const uint64_t f_base = rl64(oa, g * N);
+            const uint32_t total = (uint32_t)(rl64(oa, g * N + N) - f_base);
+            const uint32_t f0 = (uint32_t)(rl64(oa, p) - f_base), f1 = (uint32_t)(rl64(oa, p + 1) - f_base);
+            uint64_t fw0 = 0, fw1 = NONE32;
+            uint32_t fflag = 0;
+            if (lane < total) {
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + f_base + lane);
+                fw0 = x.x; fw1 = x.y;
+                fflag = v.m_flags[(uint32_t)fw1];
+            }
+            // eligibility of a pair with more fragments than a lane prefetches
+            const uint64_t rng = ((f1 - f0 >= 64) ? ~0ull : ((1ull << (f1 - f0)) - 1)) << f0;
+            const uint64_t badm = __ballot(lane < total && !frag_lean(fw1));
+            if ((badm & rng) || rl32((uint32_t)fw1, f0) < v.n_after_prepare[n]) continue;
+            if (lane == 0) v.st_valid[(uint64_t)n * NB + b] = 1;
+            uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the lane's four slots
+            uint32_t bad = 0;
+            // per slot: the fixing fragment (8 bits per slot: its lane, 0xFF
+            // none), the committed bit and the counters
+            uint32_t src = 0xFFFFFFFFu;
+            uint32_t com = 0;
+            uint32_t recommit = 0;                     // a later COMMIT covers a committed slot
+            for (uint32_t a = f0; a < f1; ++a) {
+                const uint64_t w1 = rl64(fw1, a);
+                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                const bool commit = (w1 >> 60) == K_COMMIT;
+                if (!commit && !(rl32(fflag, a) & F_GRANTED)) continue;
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) {
+                    const uint32_t s = s0 + j;
+                    if (s < st0 || s >= st0 + cnt) continue;
+                    if (commit) {
+                        ++cL;
+                        if ((com >> j) & 1) recommit = 1;
+                        else { com |= 1u << j; src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j)); }
+                    } else if (!((com >> j) & 1)) {
+                        ++cA;
+                        src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j));
                     }
-                    done = true;
                 }
             }
-            if (!done) {
-                // Per slot: the fixing fragment (8 bits per slot: its lane, 0xFF
-                // none), the committed bit and the counters
-                uint32_t src = 0xFFFFFFFFu;
-                uint32_t com = 0;
-                uint32_t recommit = 0;                 // a later COMMIT covers a committed slot
+#define MPX_SLOT(J, Q)                                                                        \
+            {                                                                                 \
+                const uint32_t fa = (src >> (8 * J)) & 0xFF;                                  \
+                if (fa != 0xFF) Q = (uint32_t)(f_base + fa + 1);                              \
+            }
+            MPX_SLOT(0, q0) MPX_SLOT(1, q1) MPX_SLOT(2, q2) MPX_SLOT(3, q3)
+#undef MPX_SLOT
+            // re-commit check: every later COMMIT must carry the committed Value (:1508)
+            if (__ballot(recommit)) {
+                uint64_t cval[SPL];                    // the committed Value of slot j
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) {
+                    const uint32_t fa = (src >> (8 * j)) & 0xFF;
+                    const uint64_t ent = __shfl(fw0, (int)(fa & 63), 64);
+                    const uint64_t w1 = __shfl(fw1, (int)(fa & 63), 64);
+                    cval[j] = fa != 0xFF ? e_val[ent + (s0 + j - ((uint32_t)(w1 >> 48) & 0xFF))] : 0;
+                }
                 for (uint32_t a = f0; a < f1; ++a) {
                     const uint64_t w1 = rl64(fw1, a);
+                    if ((w1 >> 60) != K_COMMIT) continue;
                     const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
-                    const bool commit = (w1 >> 60) == K_COMMIT;
-                    if (!commit && !(rl32(fflag, a) & F_GRANTED)) continue;
+                    const uint64_t ent = rl64(fw0, a);
 #pragma unroll
                     for (uint32_t j = 0; j < SPL; ++j) {
-                        const uint32_t s = j < 2 ? 2 * lane + j : 128 + 2 * lane + (j - 2);
-                        if (s < st0 || s >= st0 + cnt) continue;
-                        if (commit) {
-                            ++cL;
-                            if ((com >> j) & 1) recommit = 1;
-                            else { com |= 1u << j; src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j)); }
-                        } else if (!((com >> j) & 1)) {
-                            ++cA;
-                            src = (src & ~(0xFFu << (8 * j))) | (a << (8 * j));
-                        }
-                    }
-                }
-                // the slot from its fixing fragment's descriptor, fetched with a
-                // lane-indexed shuffle issued by every lane
-#define MPX_SLOT(J, Q)                                                                        \
-                {                                                                             \
-                    const uint32_t fa = (src >> (8 * J)) & 0xFF;                              \
-                    const uint32_t s = J < 2 ? 2 * lane + J : 128 + 2 * lane + (J - 2);       \
-                    const uint64_t ent = __shfl(fw0, (int)(fa & 63), 64);                     \
-                    const uint64_t w1 = __shfl(fw1, (int)(fa & 63), 64);                      \
-                    if (fa != 0xFF) Q = slot_of((uint32_t)w1, ent + (s - ((uint32_t)(w1 >> 48) & 0xFF))); \
-                }
-                MPX_SLOT(0, q0) MPX_SLOT(1, q1) MPX_SLOT(2, q2) MPX_SLOT(3, q3)
-#undef MPX_SLOT
-                // re-commit check (rare): every later COMMIT must carry the committed Value (:1508)
-                if (__ballot(recommit)) {
-                    const uint64_t q[SPL] = {q0, q1, q2, q3};
-                    for (uint32_t a = f0; a < f1; ++a) {
-                        const uint64_t w1 = rl64(fw1, a);
-                        if ((w1 >> 60) != K_COMMIT) continue;
-                        const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
-                        const uint64_t ent = rl64(fw0, a);
-#pragma unroll
-                        for (uint32_t j = 0; j < SPL; ++j) {
-                            const uint32_t s = j < 2 ? 2 * lane + j : 128 + 2 * lane + (j - 2);
-                            if (s < st0 || s >= st0 + cnt || ((src >> (8 * j)) & 0xFF) == a) continue;
-                            if (e_val[ent + (s - st0)] != e_val[slot_ent(q[j])]) bad = 1;
-                        }
+                        const uint32_t s = s0 + j;
+                        if (s < st0 || s >= st0 + cnt || ((src >> (8 * j)) & 0xFF) == a) continue;
+                        if (e_val[ent + (s - st0)] != cval[j]) bad = 1;
                     }
                 }
             }
             if (__ballot(bad) && lane == 0) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, ib);
-            uint64_t *srow = v.st + (uint64_t)n * v.shard_len + li0;
+            uint32_t *srow = v.st + (uint64_t)n * v.shard_len + li0;
             if (v.knobs & 16) {
                 // experiment: no state stores
             } else if (li0 + BS <= v.shard_len) {
-                *reinterpret_cast<u64x2 *>(srow + s0) = u64x2{q0, q1};
-                *reinterpret_cast<u64x2 *>(srow + s2) = u64x2{q2, q3};
+                *reinterpret_cast<u32x4 *>(srow + s0) = u32x4{q0, q1, q2, q3};
             } else {
                 if (li0 + s0 < v.shard_len) srow[s0] = q0;
                 if (li0 + s0 + 1 < v.shard_len) srow[s0 + 1] = q1;
-                if (li0 + s2 < v.shard_len) srow[s2] = q2;
-                if (li0 + s2 + 1 < v.shard_len) srow[s2 + 1] = q3;
+                if (li0 + s0 + 2 < v.shard_len) srow[s0 + 2] = q2;
+                if (li0 + s0 + 3 < v.shard_len) srow[s0 + 3] = q3;
             }
             if (DIGEST)
                 dig += slot_digest(v, n, ib + s0, q0) + slot_digest(v, n, ib + s0 + 1, q1) +
-                       slot_digest(v, n, ib + s2, q2) + slot_digest(v, n, ib + s2 + 1, q3);
-            if (lane == 0) v.st_valid[(uint64_t)n * NB + b] = 1;
+                       slot_digest(v, n, ib + s0 + 2, q2) + slot_digest(v, n, ib + s0 + 3, q3);
         }
-        // the bucket's chosen log, when its one live batch is a full run
-        const uint64_t c0 = rl64(fw0, 63), c1 = rl64(fw1, 63);
-        if (rl32(fflag, 63) && ((c1 >> 48) & 0xFF) == 0 && ((c1 >> 32) & 0xFFFF) == BS && li0 + BS <= v.shard_len) {
-            const uint32_t cb = (uint32_t)c0 + 1;
-            *reinterpret_cast<u32x2 *>(v.chosen + li0 + s0) = u32x2{cb + s0, cb + s0 + 1};
-            *reinterpret_cast<u32x2 *>(v.chosen + li0 + s2) = u32x2{cb + s2, cb + s2 + 1};
+
+        // chosen log of the buckets whose one live batch is a full run
+        const bool cok = clive && frag_full(cw) && (b0 + lane + 1) * BS <= v.shard_len;
+        const uint64_t cok_m = __ballot(cok);
+        const uint32_t qc = (uint32_t)ce + 1;
+        if (cok) v.chosen_valid[b0 + lane] = 1;
+        for (uint64_t m = cok_m; m; m &= m - 1) {
+            const uint32_t g = (uint32_t)__builtin_ctzll(m);
+            const uint32_t cb = rl32(qc, g) + s0;
+            const uint64_t li0 = (b0 + g) << BSH;
+            *reinterpret_cast<u32x4 *>(v.chosen + li0 + s0) = u32x4{cb, cb + 1, cb + 2, cb + 3};
             cC += SPL;
-            if (DIGEST)
-                cdig += chosen_digest(ib + s0, e_val[c0 + s0]) + chosen_digest(ib + s0 + 1, e_val[c0 + s0 + 1]) +
-                        chosen_digest(ib + s2, e_val[c0 + s2]) + chosen_digest(ib + s2 + 1, e_val[c0 + s2 + 1]);
-            if (lane == 0) v.chosen_valid[b] = 1;
+            if (DIGEST) {
+                const uint64_t c0 = rl64(ce, g), ib = v.shard_begin + li0;
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) cdig += chosen_digest(ib + s0 + j, e_val[c0 + s0 + j]);
+            }
         }
     }
     unsigned long long cc[5] = {cA, cL, dig, cC, cdig};
@@ -742,7 +818,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         off_nxt = rt1(it + 2 * stride);
         const uint64_t li0 = (uint64_t)b << BSH;
         uint64_t sb[SPL], sw[SPL];               // decoded state (checks, snapshots, digest)
-        uint64_t sm[SPL];                        // the slot as stored: (msg, entry)
+        uint32_t sm[SPL];                        // the slot as stored: fixing fragment + 1
 #pragma unroll
         for (uint32_t j = 0; j < SPL; ++j) { sb[j] = sw[j] = sm[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
 
@@ -827,11 +903,11 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 } else if (learn) {
                                     sb[j] = pid;
                                     sw[j] = W_PRESENT | W_COMMITTED | val[j];
-                                    sm[j] = slot_of(rl32(fmsg, a), ent + k[j]);
+                                    sm[j] = (uint32_t)(fi + a + 1);
                                 } else if (!(sw[j] & W_PRESENT)) {
                                     sb[j] = pid;
                                     sw[j] = W_PRESENT | val[j];
-                                    sm[j] = slot_of(rl32(fmsg, a), ent + k[j]);
+                                    sm[j] = (uint32_t)(fi + a + 1);
                                     ++cA;
                                 }
                                 cL += learn;
@@ -844,7 +920,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 if (k[j] >= 0 && !(sw[j] & W_COMMITTED)) {           // :1380
                                     sb[j] = ballot;                                   // :1387
                                     sw[j] = W_PRESENT | val[j];
-                                    sm[j] = slot_of(rl32(fmsg, a), ent + k[j]);
+                                    sm[j] = (uint32_t)(fi + a + 1);
                                     ++cA;
                                 }
                         }
@@ -859,7 +935,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 } else {
                                     sb[j] = ballot;                                   // :1515
                                     sw[j] = W_PRESENT | W_COMMITTED | val[j];
-                                    sm[j] = slot_of(rl32(fmsg, a), ent + k[j]);
+                                    sm[j] = (uint32_t)(fi + a + 1);
                                 }
                                 ++cL;
                             }
@@ -984,8 +1060,17 @@ __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base
     wave_lds_fence();
     unsigned long long cC = 0, dig = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
-    for (uint64_t b = xcd_wave_id(wv); b < v.NB; b += stride)
-        if (!v.chosen_valid[b]) chosen_walk(v, b, lidx, cC, dig);
+    // 64 buckets per wave step: one lane-parallel load of their chosen_valid
+    // bytes, then a walk of only the buckets k_apply_fast left
+    for (uint64_t c = xcd_wave_id(wv); 64 * c < v.NB; c += stride) {
+        const uint64_t b0 = 64 * c;
+        uint64_t todo = __ballot(b0 + lane < v.NB && !v.chosen_valid[b0 + lane]);
+        while (todo) {
+            const uint32_t i = (uint32_t)__builtin_ctzll(todo);
+            todo &= todo - 1;
+            chosen_walk(v, b0 + i, lidx, cC, dig);
+        }
+    }
     unsigned long long cc[2] = {cC, dig};
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1062,7 +1147,7 @@ __global__ __launch_bounds__(256) void k_decode(DevView v, uint32_t node, uint64
         const uint32_t c = v.chosen_valid[li >> BSH] ? v.chosen[li] : 0;
         if (c) w = W_PRESENT | v.e_val[c - 1];
     } else if (v.st_valid[(uint64_t)node * v.NB + (li >> BSH)]) {
-        decode_slot(v, v.st[(uint64_t)node * v.shard_len + li], b, w);
+        decode_slot(v, v.st[(uint64_t)node * v.shard_len + li], (uint32_t)li & (BS - 1), b, w);
     }
     out[2 * i] = b;
     out[2 * i + 1] = w;

@@ -11,15 +11,15 @@
 //     256-instance bucket, listed per pair in processing order (CSR); pairs are
 //     bucket-major, q = bucket * N + node, so one wave can walk a bucket's
 //     nodes and reuse the shared Values
-//   * state: one 8-byte slot per (node, instance) = (msg + 1) << 32 | entry,
-//       0 = empty: the message that fixed the slot and the entry-pool index of
-//       its Value.  The message's type says accepted or committed, its header
-//       ballot is the tag (multi; member: the entry's proposal id e_pid), the
-//       pool holds the Value handle — AcceptedValue(id, value) by reference to
-//       the resident trace (k_decode turns a slot back into {ballot, word}).
-//       Accepted and committed entries of a node are disjoint (OnCommit erases
-//       accepted_values_, multi/paxos.cpp:1501; OnAccept skips committed,
-//       :1380), so one slot holds either.
+//   * state: one 4-byte slot per (node, instance) = fragment + 1, 0 = empty:
+//       the message run (fragment) that fixed the slot.  Its message's type
+//       says accepted or committed, its header ballot is the tag (multi;
+//       member: the entry's proposal id e_pid) and its entry at the slot's
+//       position holds the Value handle — AcceptedValue(id, value) by
+//       reference to the resident trace; k_decode turns a slot back into
+//       {ballot, word}.  Accepted and committed entries of a node are disjoint
+//       (OnCommit erases accepted_values_, multi/paxos.cpp:1501; OnAccept skips
+//       committed, :1380), so one slot holds either.
 //   * chosen log: one u32 per instance = entry + 1 of the chosen Value, 0 = none
 #pragma once
 #include <cstdint>
@@ -44,11 +44,10 @@ constexpr uint64_t W_PRESENT = 1ull << 63;
 constexpr uint64_t W_COMMITTED = 1ull << 62;
 constexpr uint64_t W_HANDLE = (1ull << 62) - 1;
 
-// state slot encoding (see the layout note above); entries and messages < 2^32 - 1
-MPX_HD inline uint64_t slot_of(uint32_t msg, uint64_t ent) { return ((uint64_t)(msg + 1) << 32) | ent; }
-MPX_HD inline uint32_t slot_msg(uint64_t s) { return (uint32_t)(s >> 32) - 1; }
-MPX_HD inline uint64_t slot_ent(uint64_t s) { return s & 0xFFFFFFFFull; }
+// state slot / chosen-log encoding (see the layout note above): fragments and
+// entries stay below 2^32 - 1
 constexpr uint64_t MAX_ENTRIES = 0xFFFFFFFEull;
+constexpr uint64_t MAX_FRAGS = 0xFFFFFFFEull;
 
 // m_flags bits, written by the header scan / proposer kernels
 enum : uint8_t {
@@ -167,7 +166,7 @@ struct DevView {
     const uint64_t *cf_off;         // NB+1
     const Frag *cfrags;
     // state
-    uint64_t *st;                   // one slot per (node, instance), node-major
+    uint32_t *st;                   // one slot per (node, instance), node-major
     uint8_t *st_valid;              // per (node, bucket): node * NB + bucket
     uint32_t *chosen;               // per instance: entry + 1
     uint8_t *chosen_valid;          // per bucket
