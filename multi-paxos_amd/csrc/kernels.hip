@@ -30,6 +30,15 @@ __device__ inline void record_violation(const DevView &v, uint64_t code, uint64_
     }
 }
 
+// wave-uniform read of lane i
+__device__ inline uint64_t rl64(uint64_t x, uint32_t i)
+{
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, i);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), i);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint32_t rl32(uint32_t x, uint32_t i) { return __builtin_amdgcn_readlane(x, i); }
+
 // ---------------------------------------------------------------- scans --
 // wave64 inclusive max scan
 __device__ inline uint64_t wave_scan_max(uint64_t x)
@@ -63,16 +72,14 @@ __device__ inline uint64_t block_excl_max(uint64_t x, uint64_t *lds4, uint64_t *
     return excl;
 }
 
-// contribution of one message to promised (p) and max_seen (s)
-__device__ inline void msg_contrib(const DevView &v, uint64_t g, uint64_t &p, uint64_t &s)
+// contribution of one message (type t, ballot b, member gate gt) to promised
+// (p) and max_seen (s)
+__device__ inline void contrib(bool member, uint8_t t, uint64_t b, uint32_t gt, uint64_t &p, uint64_t &s)
 {
-    uint8_t t = v.m_type[g];
-    uint64_t b = v.m_ballot[g];
-    if (v.semantics == MPX_SEM_MEMBER) {
+    if (member) {
         // keys (incarnation << 56 | ballot): the Acceptor's own promised /
         // max_proposal_id_ restart with every new Acceptor (member/paxos.cpp:
         // 1700-1760); REJECT only feeds the proposer's max (:1221-1225)
-        const uint32_t gt = v.m_gate[g];
         const uint64_t key = (uint64_t)(gt & G_SEG) << SEG_SHIFT;
         if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && (gt & G_SEG)) {
             s = key | b;
@@ -88,22 +95,57 @@ __device__ inline void msg_contrib(const DevView &v, uint64_t g, uint64_t &p, ui
     s = (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT || t == MPX_MSG_REJECT) ? b : 0;
 }
 
+__device__ inline uint64_t wave_max(uint64_t x)
+{
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) {
+        const uint64_t y = __shfl_xor(x, d, 64);
+        x = x > y ? x : y;
+    }
+    return x;
+}
+
+constexpr uint32_t SCAN_ROUNDS = SCAN_CHUNK / 256;   // rounds of 64 messages per wave
+
+// Chunk aggregates: max of PREPARE ids and of max_seen contributions over
+// SCAN_CHUNK messages (order-free, so plain coalesced loads)
+template <bool MEMBER>
 __global__ __launch_bounds__(256) void k_scan_chunk(DevView v)
 {
-    __shared__ uint64_t l[8];
-    const uint32_t c = blockIdx.x;
+    __shared__ uint64_t l[2][4];
+    const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
-    uint64_t pm = 0, sm = 0;
-    for (uint64_t g = beg + threadIdx.x; g < end; g += 256) {
-        uint64_t p, s;
-        msg_contrib(v, g, p, s);
-        pm = pm > p ? pm : p;
-        sm = sm > s ? sm : s;
+    constexpr bool member = MEMBER;
+    uint64_t lp = 0, ls = 0;
+    uint8_t ty[SCAN_ROUNDS];
+    uint64_t ba[SCAN_ROUNDS];
+    uint32_t ga[SCAN_ROUNDS];
+#pragma unroll
+    for (uint32_t i = 0; i < SCAN_ROUNDS; ++i) {          // all loads in flight at once
+        const uint64_t g = beg + threadIdx.x + 256ull * i;
+        ty[i] = 0xFF; ba[i] = 0; ga[i] = 0;
+        if (g < end) {
+            ty[i] = v.m_type[g]; ba[i] = v.m_ballot[g];
+            if (member) ga[i] = v.m_gate[g];
+        }
     }
-    uint64_t tp, ts;
-    block_excl_max(pm, l, &tp);
-    block_excl_max(sm, l + 4, &ts);
-    if (threadIdx.x == 0) { v.chunk_agg[2 * c] = tp; v.chunk_agg[2 * c + 1] = ts; }
+#pragma unroll
+    for (uint32_t i = 0; i < SCAN_ROUNDS; ++i) {
+        uint64_t p, s;
+        contrib(member, ty[i], ba[i], ga[i], p, s);
+        lp = lp > p ? lp : p;
+        ls = ls > s ? ls : s;
+    }
+    lp = wave_max(lp);
+    ls = wave_max(ls);
+    if (lane == 0) { l[0][w] = lp; l[1][w] = ls; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t tp = 0, ts = 0;
+        for (int i = 0; i < 4; ++i) { tp = tp > l[0][i] ? tp : l[0][i]; ts = ts > l[1][i] ? ts : l[1][i]; }
+        v.chunk_agg[2 * c] = tp;
+        v.chunk_agg[2 * c + 1] = ts;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_scan_node(DevView v)
@@ -129,82 +171,108 @@ __global__ __launch_bounds__(256) void k_scan_node(DevView v)
     if (threadIdx.x == 0) { v.node_scal[2 * n] = carry_p; v.node_scal[2 * n + 1] = carry_s; }
 }
 
-// per message: granted / reject flags, max_seen carried by REJECTs.
-// Chunk = 1024 messages, 4 consecutive per thread.
+// Per message: granted / reject flags, max_seen carried by REJECTs.  Wave w of
+// the chunk's block owns SCAN_CHUNK / 4 consecutive messages, 64 per round
+// (coalesced), kept in registers between the two phases: (1) wave maxima ->
+// the wave's carry-in, (2) per round the promised value before each message
+// (an exclusive wave scan, only in rounds that hold a PREPARE) and, in rounds
+// with a REJECT, the inclusive max_seen scan.
+template <bool MEMBER>
 __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
 {
-    __shared__ uint64_t l[8];
-    const uint32_t c = blockIdx.x;
+    __shared__ uint64_t l[2][4];
+    const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
-    const uint64_t g0 = beg + 4ull * threadIdx.x;
-    uint64_t p[4], s[4];
-    uint64_t tp = 0, ts = 0;
+    const uint64_t wb = beg + (uint64_t)w * (SCAN_CHUNK / 4) + lane;
+    constexpr bool member = MEMBER;
+    uint8_t ty[SCAN_ROUNDS];
+    uint64_t ba[SCAN_ROUNDS];
+    uint32_t sr[SCAN_ROUNDS], ga[SCAN_ROUNDS];
+    uint64_t lp = 0, ls = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        p[i] = s[i] = 0;
-        if (g0 + i < end) msg_contrib(v, g0 + i, p[i], s[i]);
+    for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {             // all loads in flight at once
+        const uint64_t g = wb + 64 * r;
+        ty[r] = 0xFF; ba[r] = 0; sr[r] = 0; ga[r] = 0;
+        if (g < end) {
+            ty[r] = v.m_type[g]; ba[r] = v.m_ballot[g]; sr[r] = v.m_src[g];
+            if (member) ga[r] = v.m_gate[g];
+        }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { tp = tp > p[i] ? tp : p[i]; ts = ts > s[i] ? ts : s[i]; }
-    uint64_t bt;
-    uint64_t ep = block_excl_max(tp, l, &bt);
-    uint64_t es = block_excl_max(ts, l + 4, &bt);
-    uint64_t cp = v.chunk_carry[2 * c], cs = v.chunk_carry[2 * c + 1];
-    uint64_t run_p = ep > cp ? ep : cp;      // promised before message g0
-    uint64_t run_s = es > cs ? es : cs;
-    if (v.semantics == MPX_SEM_MEMBER) {
+    for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
+        uint64_t p, s;
+        contrib(member, ty[r], ba[r], ga[r], p, s);
+        lp = lp > p ? lp : p;
+        ls = ls > s ? ls : s;
+    }
+    lp = wave_max(lp);
+    ls = wave_max(ls);
+    if (lane == 0) { l[0][w] = lp; l[1][w] = ls; }
+    __syncthreads();
+    uint64_t cp = v.chunk_carry[2 * c], cs = v.chunk_carry[2 * c + 1];   // wave-uniform running maxima
+    for (uint32_t i = 0; i < w; ++i) { cp = cp > l[0][i] ? cp : l[0][i]; cs = cs > l[1][i] ? cs : l[1][i]; }
+    ls = 0;                                    // this lane's max_seen contributions since cs
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint64_t g = g0 + i;
-            if (g >= end) break;
-            const uint8_t t = v.m_type[g];
-            const uint64_t id = v.m_ballot[g];
-            const uint32_t gt = v.m_gate[g];
-            run_s = run_s > s[i] ? run_s : s[i];
-            uint8_t f = 0;
+    for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
+        const uint64_t g = wb + 64 * r;
+        if (!__ballot(g < end)) break;
+        const uint8_t t = ty[r];
+        const uint64_t id = ba[r];
+        const uint32_t gt = ga[r];
+        uint64_t p, s;
+        contrib(member, t, id, gt, p, s);
+        // promised before this message
+        uint64_t prom = cp;
+        if (__ballot(p != 0)) {
+            uint64_t x = wave_scan_max(p);
+            cp = cp > rl64(x, 63) ? cp : rl64(x, 63);
+            x = __shfl_up(x, 1, 64);
+            if (lane == 0) x = 0;
+            prom = prom > x ? prom : x;
+        }
+        uint8_t f = 0;
+        bool chk_src = false;
+        if (member) {
             if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && (gt & G_SEG)) {
                 const uint64_t seg = gt & G_SEG;
-                const uint64_t prom = (run_p >> SEG_SHIFT) == seg ? (run_p & LOW56) : 0;
+                const uint64_t pr = (prom >> SEG_SHIFT) == seg ? (prom & LOW56) : 0;
                 if (t == MPX_MSG_PREPARE) {
-                    if (id > prom) f = F_GRANTED;                       // :1711
-                    else if (id < prom) f = F_REJECT;                   // :1734
+                    if (id > pr) f = F_GRANTED;                         // :1711
+                    else if (id < pr) f = F_REJECT;                     // :1734
                 } else {
-                    f = id >= prom ? F_GRANTED : F_REJECT;              // :1753
+                    f = id >= pr ? F_GRANTED : F_REJECT;                // :1753
                 }
-                if (v.m_src[g] >= v.N) f |= F_BADNODE;
-                if (f & F_REJECT) v.m_maxseen[g] = run_s & LOW56;       // same incarnation: s[i] is in run_s
+                chk_src = true;
             } else if (t == MPX_MSG_E_EPOCH) {
                 f = ((gt & G_ACCCLR) ? F_ACCCLR : 0) | ((gt & G_PRECLR) ? F_PRECLR : 0);
             } else if (t == MPX_MSG_COMMIT) {
                 f = (gt & G_PROP) ? F_PROP : 0;
-                if (v.m_src[g] >= v.N) f |= F_BADNODE;
+                chk_src = true;
             }
+        } else {
+            if (t == MPX_MSG_PREPARE) {
+                if (id > prom) f = F_GRANTED;                           // :865
+                else if (id < prom) f = F_REJECT;                       // :894
+            } else if (t == MPX_MSG_ACCEPT) {
+                f = id >= prom ? F_GRANTED : F_REJECT;                  // :1366
+            }
+            chk_src = t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT;
+        }
+        if (chk_src && sr[r] >= v.N) f |= F_BADNODE;
+        // max_seen after this message, for the REJECTs it carries (:894,1398)
+        if (__ballot(f & F_REJECT)) {
+            const uint64_t pre = wave_max(ls);
+            cs = cs > pre ? cs : pre;
+            ls = 0;
+            uint64_t x = wave_scan_max(s);
+            x = x > cs ? x : cs;
+            if (f & F_REJECT) v.m_maxseen[g] = member ? x & LOW56 : x;
+        }
+        ls = ls > s ? ls : s;
+        if (g < end) {
             v.m_flags[g] = f;
             if (f & F_BADNODE) record_violation(v, MPX_V_BAD_NODE, v.m_node[g], g - v.node_off[v.m_node[g]], 0);
-            run_p = run_p > p[i] ? run_p : p[i];
         }
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint64_t g = g0 + i;
-        if (g >= end) break;
-        const uint8_t t = v.m_type[g];
-        const uint64_t id = v.m_ballot[g];
-        run_s = run_s > s[i] ? run_s : s[i];   // max_seen after this message
-        uint8_t f = 0;
-        if (t == MPX_MSG_PREPARE) {
-            if (id > run_p) f = F_GRANTED;                        // :865
-            else if (id < run_p) f = F_REJECT;                    // :894
-        } else if (t == MPX_MSG_ACCEPT) {
-            f = id >= run_p ? F_GRANTED : F_REJECT;               // :1366
-        }
-        if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT) && v.m_src[g] >= v.N)
-            f |= F_BADNODE;
-        v.m_flags[g] = f;
-        if (f & F_REJECT) v.m_maxseen[g] = run_s;
-        if (f & F_BADNODE) record_violation(v, MPX_V_BAD_NODE, v.m_node[g], g - v.node_off[v.m_node[g]], 0);
-        run_p = run_p > p[i] ? run_p : p[i];
     }
 }
 
@@ -266,7 +334,37 @@ __global__ void k_votes(DevView v)
     uint64_t mask = 0;
     uint32_t chosen = NONE32;
     const bool member = v.semantics == MPX_SEM_MEMBER;
-    for (uint64_t r = v.b_rep_off[j]; r < v.b_rep_off[j + 1]; ++r) {
+    uint64_t r = v.b_rep_off[j];
+    const uint64_t re = v.b_rep_off[j + 1];
+    if (!member) {
+        // the first VOTE_PREFETCH replies: indices, then ballots and sources,
+        // each level issued at once (three memory round trips, not one per reply)
+        constexpr uint32_t VP = 8;
+        uint32_t gi[VP];
+        uint64_t bal[VP];
+        uint32_t src[VP];
+#pragma unroll
+        for (uint32_t k = 0; k < VP; ++k) gi[k] = r + k < re ? v.b_rep[r + k] : NONE32;
+#pragma unroll
+        for (uint32_t k = 0; k < VP; ++k) {
+            bal[k] = gi[k] != NONE32 ? v.m_ballot[gi[k]] : 0;
+            src[k] = gi[k] != NONE32 ? v.m_src[gi[k]] : 0;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < VP; ++k) {
+            if (gi[k] == NONE32 || chosen != NONE32) continue;
+            if (bal[k] != ballot) continue;                       // :1408
+            if (src[k] >= v.N) {
+                const uint32_t n = v.m_node[gi[k]];
+                record_violation(v, MPX_V_BAD_NODE, n, gi[k] - v.node_off[n], 0);
+                continue;
+            }
+            mask |= 1ull << src[k];
+            if ((uint32_t)__popcll(mask) >= v.quorum) chosen = gi[k];   // :1416
+        }
+        r = chosen == NONE32 && re - r > VP ? r + VP : re;
+    }
+    for (; r < re; ++r) {
         const uint32_t g = v.b_rep[r];
         if (member) {
             // Proposer::OnAcceptReply, member/paxos.cpp:1317-1343: matched by
@@ -301,13 +399,6 @@ __global__ void k_votes(DevView v)
 // round trips — (1) CSR offsets, (2) fragment / event descriptors, (3) the
 // scan's per-message flags + the entry values — and (1) of the next pair is
 // already in flight while the current one is processed.
-__device__ inline uint64_t rl64(uint64_t x, uint32_t i)
-{
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, i);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), i);
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ inline uint32_t rl32(uint32_t x, uint32_t i) { return __builtin_amdgcn_readlane(x, i); }
 __device__ inline void wave_lds_fence()
 {
     // LDS instructions of one wave execute in order; keep the compiler from
@@ -1171,9 +1262,11 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, s);
     hipLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s, v, n_partials);
     if (v.num_chunks) {
-        hipLaunchKernelGGL(k_scan_chunk, dim3(v.num_chunks), dim3(256), 0, s, v);
+        if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_chunk<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
+        else hipLaunchKernelGGL(k_scan_chunk<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
         hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);
-        hipLaunchKernelGGL(k_scan_apply, dim3(v.num_chunks), dim3(256), 0, s, v);
+        if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
+        else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
     }
     hipLaunchKernelGGL(k_proposer, dim3(cdiv(v.N, 64)), dim3(64), 0, s, v);
     if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);

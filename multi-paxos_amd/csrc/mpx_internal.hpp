@@ -37,7 +37,7 @@ namespace mpx {
 
 constexpr uint32_t BSH = 8;                  // bucket = 256 instances
 constexpr uint32_t BS = 1u << BSH;
-constexpr uint32_t SCAN_CHUNK = 1024;        // header-scan chunk (messages)
+constexpr uint32_t SCAN_CHUNK = 4096;        // header-scan chunk (messages): 16 per thread
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 
 constexpr uint64_t W_PRESENT = 1ull << 63;
