@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void k_scan_node(DevView v)
 
 // Per message: granted / reject flags, max_seen carried by REJECTs.  Wave w of
 // the chunk's block owns SCAN_CHUNK / 4 consecutive messages, 64 per round
-// (coalesced), kept in registers between the two phases: (1) wave maxima ->
+// (coalesced), staged in LDS between the two phases: (1) wave maxima ->
 // the wave's carry-in, (2) per round the promised value before each message
 // (an exclusive wave scan, only in rounds that hold a PREPARE) and, in rounds
 // with a REJECT, the inclusive max_seen scan.
@@ -181,9 +181,13 @@ template <bool MEMBER>
 __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
 {
     __shared__ uint64_t l[2][4];
+    __shared__ uint64_t lba[SCAN_CHUNK];        // phase 2 reads its rounds back from LDS,
+    __shared__ uint8_t lty[SCAN_CHUNK];         // so the round loop needs few registers
+    __shared__ uint32_t lga[MEMBER ? SCAN_CHUNK : 1];
     const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
     const uint64_t wb = beg + (uint64_t)w * (SCAN_CHUNK / 4) + lane;
+    const uint32_t lb = w * (SCAN_CHUNK / 4) + lane;
     constexpr bool member = MEMBER;
     uint8_t ty[SCAN_ROUNDS];
     uint64_t ba[SCAN_ROUNDS];
@@ -198,12 +202,17 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
             if (member) ga[r] = v.m_gate[g];
         }
     }
+    uint32_t badsrc = 0;                        // one bad-node bit per round
 #pragma unroll
     for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
         uint64_t p, s;
         contrib(member, ty[r], ba[r], ga[r], p, s);
         lp = lp > p ? lp : p;
         ls = ls > s ? ls : s;
+        badsrc |= (sr[r] >= v.N ? 1u : 0u) << r;
+        lty[lb + 64 * r] = ty[r];
+        lba[lb + 64 * r] = ba[r];
+        if (member) lga[lb + 64 * r] = ga[r];
     }
     lp = wave_max(lp);
     ls = wave_max(ls);
@@ -212,13 +221,13 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
     uint64_t cp = v.chunk_carry[2 * c], cs = v.chunk_carry[2 * c + 1];   // wave-uniform running maxima
     for (uint32_t i = 0; i < w; ++i) { cp = cp > l[0][i] ? cp : l[0][i]; cs = cs > l[1][i] ? cs : l[1][i]; }
     ls = 0;                                    // this lane's max_seen contributions since cs
-#pragma unroll
+#pragma unroll 1
     for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
         const uint64_t g = wb + 64 * r;
         if (!__ballot(g < end)) break;
-        const uint8_t t = ty[r];
-        const uint64_t id = ba[r];
-        const uint32_t gt = ga[r];
+        const uint8_t t = lty[lb + 64 * r];    // written by this lane: no barrier needed
+        const uint64_t id = lba[lb + 64 * r];
+        const uint32_t gt = member ? lga[lb + 64 * r] : 0;
         uint64_t p, s;
         contrib(member, t, id, gt, p, s);
         // promised before this message
@@ -258,7 +267,7 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
             }
             chk_src = t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT;
         }
-        if (chk_src && sr[r] >= v.N) f |= F_BADNODE;
+        if (chk_src && ((badsrc >> r) & 1)) f |= F_BADNODE;
         // max_seen after this message, for the REJECTs it carries (:894,1398)
         if (__ballot(f & F_REJECT)) {
             const uint64_t pre = wave_max(ls);

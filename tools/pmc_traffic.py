@@ -59,7 +59,8 @@ def main():
         fk, wk = sum(f) / len(f), sum(w) / len(w)
         out["kernels"][name] = {"dispatches": len(f), "FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk,
                                 "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024}
-    apply = [v for k, v in out["kernels"].items() if "k_apply_fast" in k]
+    # the timed instantiation (digest runs use k_apply_fast<..., true>)
+    apply = [v for k, v in out["kernels"].items() if "k_apply_fast" in k and "false" in k]
     out["hbm_bytes_per_launch"] = apply[0]["hbm_bytes_per_launch"] if apply else None
     out["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"
     # written under gpurun_out/ (merged back from the GPU box); copy into profiles/ to commit
