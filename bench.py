@@ -13,13 +13,17 @@ state: header scan, promise quorum, accept-vote quorum, acceptor/learner apply
 64-word per-shard summary.  decisions/s = chosen instances per step (summed
 over ranks) / max-over-ranks step time.
 
-roofline: the dominant kernel is k_apply_fast (acceptor/learner apply + the
-chosen log).  achieved = the compulsory bytes of one launch (DESIGN.md §4:
-one 4-byte state slot written per (acceptor, instance), one 4-byte chosen-log
-entry per instance, one 16-byte fragment descriptor read per (acceptor,
-bucket, message) — a slot names the message run that fixed it, whose entry
-in the resident pool holds the Value, so no Value is read or copied) / its mean duration from HIP events on the
-engine's stream.  The SURVEY.md §8(d) model (16 P + 24 A + 16 L, which charges
+roofline: the dominant unit is the apply phase — k_plan (one thread per
+(acceptor, bucket) pair decides which message run fixes it), k_store (streams
+the slots and the chosen log) and k_apply_fast's per-slot pairs (none in C4:
+it exits at once) — bracketed by HIP events on the engine's stream; k_store is
+≈92 % of it (profiles/).  achieved = the phase's compulsory bytes (DESIGN.md
+§4: one 4-byte state slot written per (acceptor, instance), one 4-byte
+chosen-log entry per instance, one 16-byte fragment descriptor read per
+(acceptor, bucket, message), and the 4-byte plan word per (row, bucket) written
+and read back — a slot names the message run that fixed it, whose entry in the
+resident pool holds the Value, so no Value is read or copied) / its mean
+duration.  The SURVEY.md §8(d) model (16 P + 24 A + 16 L, which charges
 every acceptor a 16-byte slot plus a read of its own copy of each message) is
 reported beside it.  traffic = HBM bytes per launch from rocprofv3 PMC
 (profiles/, tools/pmc_traffic.py) or null.
@@ -220,7 +224,9 @@ def main():
     bytes_survey = st["bytes_alg"]                  # this rank's 16P + 24A + 16L per launch
     L = se - sb
     # 4-B state slots + 4-B chosen log + the ACCEPT and COMMIT descriptors of every (node, bucket)
-    bytes_min = 4 * N * L + 4 * L + 2 * 16 * N * ((L + 255) // 256)
+    # + the plan word of every (row, bucket), written by k_plan and read by k_store
+    nb = (L + 255) // 256
+    bytes_min = 4 * N * L + 4 * L + 2 * 16 * N * nb + 2 * 4 * (N + 1) * nb
     achieved = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
     pmc = latest_pmc(N, M, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
@@ -250,7 +256,8 @@ def main():
                        "parallelism": "instance-shard x%d (RCCL all-gather of 64-word summaries)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_apply_fast", "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_min,
+                         "kernel": "apply phase: k_plan + k_store + k_apply_fast<1,false,true>",
+                         "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_min,
                          "bytes_survey_model_per_launch": bytes_survey,
                          "survey_model_gbps": bytes_survey / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0},
             "cpu_baseline": cpu,

@@ -76,7 +76,7 @@ struct mpx_engine {
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
     DevBuf f_off, frags, gp_list, ev_off, ev_msg, pl_off, pl_msg;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
-    DevBuf st, st_valid, chosen, chosen_valid;
+    DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy;
     DevBuf decode_buf;                      // readback scratch (k_decode)
     DevBuf out, out_cursor, partials, viol, summary;
     uint64_t out_cap = 0;
@@ -226,11 +226,15 @@ static int finish_view(mpx_engine *e)
     TRY(e->st_valid.alloc((size_t)N * e->NB));
     TRY(e->chosen.alloc(e->shard_len * 4));
     TRY(e->chosen_valid.alloc(e->NB));
+    TRY(e->plan.alloc((size_t)(N + 1) * e->NB * 4));
+    TRY(e->fast_rest.alloc(8));
+    TRY(e->store_dummy.alloc(64 * 1024));
     const uint64_t npairs = (uint64_t)N * e->NB;
     // k_apply_fast holds 5 waves/SIMD (82 VGPRs); 8 workgroups of 4 waves per
     // CU measured best on C4 (tools/ab_apply.py: 2.17 ms vs 2.31 ms at 5)
     e->geom.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npairs, (uint64_t)e->num_cus * 8));
     e->geom.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 4));
+    e->geom.store_wgs = e->num_cus * 8;     // k_store: 8 workgroups of 4 waves per CU
 
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + e->geom.chosen_wgs)));
     TRY(e->viol.alloc(sizeof(DevViolation)));
@@ -243,6 +247,9 @@ static int finish_view(mpx_engine *e)
     v.st_valid = e->st_valid.as<uint8_t>();
     v.chosen = e->chosen.as<uint32_t>();
     v.chosen_valid = e->chosen_valid.as<uint8_t>();
+    v.plan = e->plan.as<uint32_t>();
+    v.fast_rest = e->fast_rest.as<uint32_t>();
+    v.store_dummy = e->store_dummy.as<uint32_t>();
     v.out = e->out.as<OutRec>();
     v.out_cursor = e->out_cursor.as<unsigned long long>();
     v.out_cap = e->out_cap;
@@ -346,6 +353,7 @@ static int queue_run(mpx_engine *e, bool digest)
     e->view.digest = digest ? 1 : 0;
     e->view.knobs = 0;
     if (const char *x = std::getenv("MPX_KNOBS")) e->view.knobs = (uint32_t)std::atoi(x);
+    if (const char *x = std::getenv("MPX_STORE_WGS_PER_CU")) g.store_wgs = std::max<uint32_t>(1, e->num_cus * (uint32_t)std::atoi(x));
     if (const char *x = std::getenv("MPX_APPLY_WGS_PER_CU")) {
         const uint64_t np = (uint64_t)e->cfg.num_nodes * e->NB;
         g.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(np, (uint64_t)e->num_cus * std::atoi(x)));

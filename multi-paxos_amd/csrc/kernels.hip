@@ -583,13 +583,20 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // same way (entry + 1 per slot); k_chosen walks every other bucket.  Value
 // loads happen only for the re-commit check (:1508, rare) and in digest runs.
 //
+// State and chosen-log stores are non-temporal (written once per run, read
+// back only by k_decode): tools/bw_probe2.hip measures this store pattern with
+// one wait per step at 5.3 TB/s cached vs 5.7 TB/s nt on MI355X.
+//
 // A pair is taken here iff (same predicate as ingest.cpp's work list):
 // N <= FAST_MAX_NODES, the bucket has at most FAST_MAX_FRAGS fragments, the pair's fragments are all dense
 // ACCEPT / COMMIT runs and its node has no PREPARE after the first of them —
 // its snapshot events see empty state, so skipping them changes no output.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t FAST_PAIR_FRAGS = 2;      // descriptors a pair lane prefetches
-__host__ __device__ inline uint32_t fast_group(uint32_t N) { return N ? (63 / N < 4 ? 63 / N : 4) : 1; }
+__host__ __device__ inline uint32_t fast_group(uint32_t N, uint32_t cap = 4)
+{
+    return N ? (63 / N < cap ? 63 / N : cap) : 1;
+}
 
 __device__ inline bool frag_lean(uint64_t w1)
 {
@@ -598,7 +605,7 @@ __device__ inline bool frag_lean(uint64_t w1)
 }
 __device__ inline bool frag_full(uint64_t w1) { return ((w1 >> 48) & 0xFF) == 0 && ((w1 >> 32) & 0xFFFF) == BS; }
 
-template <int WAVES_PER_EU, bool DIGEST>
+template <int WAVES_PER_EU, bool DIGEST, bool AFTER_STORE = false>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
 {
     constexpr uint32_t F = FAST_PAIR_FRAGS;
@@ -608,7 +615,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
     const uint32_t N = v.N;
     const uint64_t NB = v.NB;
     if (N > FAST_MAX_NODES) return;
-    const uint32_t G = fast_group(N), GN = G * N;
+    // after k_plan + k_store only the pairs k_plan counted are left
+    if (AFTER_STORE && *v.fast_rest == 0) return;
+    const uint32_t G = fast_group(N, (v.knobs >> 8) & 15 ? (v.knobs >> 8) & 15 : 4), GN = G * N;
     const uint64_t steps = (NB + G - 1) / G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
@@ -676,7 +685,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         for (uint32_t k = 0; k < F; ++k) fg[k] = (uint32_t)w[k] != NONE32 ? v.m_flags[(uint32_t)w[k]] : 0;
         const uint32_t clive = (uint32_t)cw != NONE32 ? v.b_chosen[(uint32_t)cw] != NONE32 : 0;
         // One wait per step, before its stores (vmcnt(0); expcnt / lgkmcnt free).
-        __builtin_amdgcn_s_waitcnt(0x0F70);
+        if (!(v.knobs & 32)) __builtin_amdgcn_s_waitcnt(0x0F70);
 
         // plan, one pair per lane
         const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64);
@@ -699,7 +708,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         const bool uni = elig && full && !again;
         const uint64_t uni_m = __ballot(uni);
         const uint64_t slow_m = __ballot((elig && !uni) || (in_list && len > F));
-        if (uni) { cA += nA * BS; cL += nL * BS; }
+        // AFTER_STORE: k_plan counted and k_store wrote the uniform pairs of whole buckets
+        const bool stored = AFTER_STORE && (b0 + pg + 1) * BS <= v.shard_len;
+        if (uni && !stored) { cA += nA * BS; cL += nL * BS; }
         const uint32_t qv = fix == NONE32 ? 0 : (uint32_t)(oa + fix + 1);
         if (elig) v.st_valid[(uint64_t)pn * NB + b0 + pg] = 1;
 
@@ -710,11 +721,12 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             for (uint32_t g = 0; g < nb; ++g) {
                 const uint32_t p = g * N + n;
                 if (!((uni_m >> p) & 1)) continue;
+                if (AFTER_STORE && (b0 + g + 1) * BS <= v.shard_len) continue;
                 const uint32_t q = rl32(qv, p);
                 if (v.knobs & 16) {
                     // experiment: no state stores
                 } else if (whole) {
-                    *reinterpret_cast<u32x4 *>(row + g * BS + s0) = u32x4{q, q, q, q};
+                    __builtin_nontemporal_store(u32x4{q, q, q, q}, reinterpret_cast<u32x4 *>(row + g * BS + s0));
                 } else {
 #pragma unroll
                     for (uint32_t j = 0; j < SPL; ++j)
@@ -807,7 +819,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             if (v.knobs & 16) {
                 // experiment: no state stores
             } else if (li0 + BS <= v.shard_len) {
-                *reinterpret_cast<u32x4 *>(srow + s0) = u32x4{q0, q1, q2, q3};
+                __builtin_nontemporal_store(u32x4{q0, q1, q2, q3}, reinterpret_cast<u32x4 *>(srow + s0));
             } else {
                 if (li0 + s0 < v.shard_len) srow[s0] = q0;
                 if (li0 + s0 + 1 < v.shard_len) srow[s0 + 1] = q1;
@@ -820,7 +832,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         }
 
         // chosen log of the buckets whose one live batch is a full run
-        const bool cok = clive && frag_full(cw) && (b0 + lane + 1) * BS <= v.shard_len;
+        const bool cok = !AFTER_STORE && clive && frag_full(cw) && (b0 + lane + 1) * BS <= v.shard_len;
         const uint64_t cok_m = __ballot(cok);
         const uint32_t qc = (uint32_t)ce + 1;
         if (cok) v.chosen_valid[b0 + lane] = 1;
@@ -828,7 +840,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             const uint32_t g = (uint32_t)__builtin_ctzll(m);
             const uint32_t cb = rl32(qc, g) + s0;
             const uint64_t li0 = (b0 + g) << BSH;
-            *reinterpret_cast<u32x4 *>(v.chosen + li0 + s0) = u32x4{cb, cb + 1, cb + 2, cb + 3};
+            __builtin_nontemporal_store(u32x4{cb, cb + 1, cb + 2, cb + 3}, reinterpret_cast<u32x4 *>(v.chosen + li0 + s0));
             cC += SPL;
             if (DIGEST) {
                 const uint64_t c0 = rl64(ce, g), ib = v.shard_begin + li0;
@@ -854,6 +866,169 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         unsigned long long s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         const int slot = t == 0 ? PC_A : t == 1 ? PC_L : t == 2 ? PC_DSTATE : t == 3 ? PC_C : PC_DCHOSEN;
         v.partials[8 * blockIdx.x + slot] += s;
+    }
+}
+
+__device__ inline uint64_t frag_w1(const Frag *f) { return reinterpret_cast<const uint64_t *>(f)[1]; }
+constexpr uint32_t PLAN_SKIP = 0xFFFFFFFFu;   // fragment indices + 1 stay below (MPX_E_RANGE)
+
+// Apply split in two (the default for multi runs): k_plan decides every pair
+// with one thread per pair — the same plan as k_apply_fast's pair lanes, but
+// with no per-step chain, so its gathers (CSR offsets, two descriptors, two
+// scan flags) all overlap — and k_store streams the result.  A (node, bucket)
+// pair whose fragments are full dense runs is fixed by one fragment, so its
+// plan word is that fragment's index + 1 and k_store writes it over the whole
+// 1 KiB of slots; the chosen log of a bucket with one live full batch is row N
+// (entry + 1 + slot).  Pairs that need the per-slot path, or a partial last
+// bucket, are counted in fast_rest and left to k_apply_fast<.., AFTER_STORE>.
+__global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
+{
+    constexpr uint32_t F = FAST_PAIR_FRAGS;
+    __shared__ unsigned long long red[4][3];
+    __shared__ uint32_t rest_w[4];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t N = v.N;
+    const uint64_t NB = v.NB, np = (uint64_t)N * NB;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    unsigned long long cA = 0, cL = 0, cC = 0;
+    uint32_t rest = 0;
+    if (i < np) {
+        const uint64_t b = i / N;
+        const uint32_t n = (uint32_t)(i - b * N);
+        const uint64_t oa = v.f_off[i], o1 = v.f_off[i + 1];
+        const uint64_t bb = v.f_off[b * N], be = v.f_off[b * N + N];
+        const uint32_t len = (uint32_t)(o1 - oa);
+        const bool in_list = len && be - bb <= FAST_MAX_FRAGS;
+        uint64_t w[F];
+        uint32_t fg[F];
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) w[k] = k < len ? frag_w1(v.frags + oa + k) : (uint64_t)NONE32;
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) fg[k] = k < len ? v.m_flags[(uint32_t)w[k]] : 0;
+        bool elig = in_list && len <= F, full = true, again = false, comm = false;
+        uint32_t fix = NONE32, nA = 0, nL = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) {
+            if (k >= len) continue;
+            elig = elig && frag_lean(w[k]);
+            full = full && frag_full(w[k]);
+            if ((w[k] >> 60) == K_COMMIT) { ++nL; if (comm) again = true; else { comm = true; fix = k; } }
+            else if (!comm && (fg[k] & F_GRANTED)) { ++nA; fix = k; }
+        }
+        elig = elig && len && (uint32_t)w[0] >= v.n_after_prepare[n];
+        const bool uni = elig && full && !again;
+        const bool whole = (b + 1) * BS <= v.shard_len;
+        uint32_t q = PLAN_SKIP;
+        if (uni && whole) {
+            q = fix == NONE32 ? 0 : (uint32_t)(oa + fix + 1);
+            v.st_valid[(uint64_t)n * NB + b] = 1;
+            cA = nA * BS; cL = nL * BS;
+        } else if (elig || (in_list && len > F)) {
+            rest = 1;
+        }
+        v.plan[(uint64_t)n * NB + b] = q;
+    }
+    if (i < NB) {
+        const uint64_t oc = v.cf_off[i], c1 = v.cf_off[i + 1];
+        uint32_t q = PLAN_SKIP;
+        if (c1 - oc == 1) {
+            const uint64_t ce = v.cfrags[oc].entry, cw = frag_w1(v.cfrags + oc);
+            if (v.b_chosen[(uint32_t)cw] != NONE32 && frag_full(cw) && (i + 1) * BS <= v.shard_len) {
+                q = (uint32_t)ce + 1;
+                v.chosen_valid[i] = 1;
+                cC = BS;
+            }
+        }
+        v.plan[(uint64_t)N * NB + i] = q;
+    }
+    unsigned long long cc[3] = {cA, cL, cC};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        unsigned long long x = cc[k];
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        cc[k] = x;
+    }
+    const uint64_t rm = __ballot(rest);
+    if (lane == 0) {
+        red[wv][0] = cc[0]; red[wv][1] = cc[1]; red[wv][2] = cc[2];
+        rest_w[wv] = (uint32_t)__builtin_popcountll(rm);
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const uint32_t t = threadIdx.x;
+        const unsigned long long x = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+        const int slot = t == 0 ? PC_A : t == 1 ? PC_L : PC_C;
+        if (x) atomicAdd(&v.partials[8 * (blockIdx.x % apply_wgs) + slot], x);
+    } else if (threadIdx.x == 3) {
+        const uint32_t r = rest_w[0] + rest_w[1] + rest_w[2] + rest_w[3];
+        if (r) atomicAdd(v.fast_rest, r);
+    }
+}
+
+// Streams the plan: a wave takes a chunk of C whole buckets of one
+// row (state row n or the chosen log) and writes C KiB contiguous,
+// one 16-byte non-temporal store per lane per bucket, 4 slots per lane.  The
+// chunk's plan words are loaded one chunk ahead and the inner loop has no
+// branch — a PLAN_SKIP bucket's store goes to a scratch sink — so the only
+// wait per chunk is for that one load, with the previous chunk's stores still
+// in flight (vmcnt counts stores on gfx9: a data-dependent store count would
+// force a full drain instead).  Buckets past the last whole chunk of a row
+// take a plain tail loop.
+template <uint32_t C>
+__global__ __launch_bounds__(256) void k_store(DevView v)
+{
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t N = v.N, rows = N + 1;
+    const uint64_t NB = v.NB;
+    const uint64_t whole = v.shard_len >> BSH;            // buckets wholly inside the shard
+    const uint64_t cpr = whole / C, chunks = (uint64_t)rows * cpr;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    const uint64_t wid = xcd_wave_id(wv);
+    const uint32_t s0 = 4 * lane;
+    uint32_t *const sink = v.store_dummy + (wid & 63) * BS + s0;
+    // chunk c = (row r, k-th chunk of the row), advanced incrementally; the
+    // plan load is unconditional (lanes >= C repeat lanes 0..C-1, a finished
+    // wave re-reads the last chunk) so the compiler can count it exactly
+    uint32_t r = 0, k = 0;
+    if (cpr) { r = (uint32_t)(wid / cpr); k = (uint32_t)(wid - (uint64_t)r * cpr); }
+    const uint32_t step_r = cpr ? (uint32_t)(nwaves / cpr) : 0, step_k = cpr ? (uint32_t)(nwaves - (uint64_t)step_r * cpr) : 0;
+    auto advance = [&](uint32_t &rr, uint32_t &kk) {
+        rr += step_r; kk += step_k;
+        if (kk >= cpr) { kk -= (uint32_t)cpr; ++rr; }
+    };
+    auto plan_ptr = [&](uint32_t rr, uint32_t kk) -> const uint32_t * {
+        const bool live = rr < rows;
+        return v.plan + (live ? (uint64_t)rr * NB + (uint64_t)kk * C : 0) + (lane & (C - 1));
+    };
+    uint32_t rn = r, kn = k;
+    uint32_t qn = chunks ? *plan_ptr(rn, kn) : PLAN_SKIP;
+    // settled before the loop: the loop-carried plan word then has one pending
+    // source, the in-loop load, which waits as vmcnt(C) (its C stores in flight)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    for (uint64_t c = wid; c < chunks; c += nwaves) {
+        const uint32_t qw = qn;
+        const uint32_t rc = rn, kc = kn;
+        advance(rn, kn);
+        qn = *plan_ptr(rn, kn);
+        const uint32_t inc = rc == N ? 1u : 0u;
+        uint32_t *const base = (rc == N ? v.chosen : v.st + (uint64_t)rc * v.shard_len) + ((uint64_t)kc * C << BSH) + s0;
+#pragma unroll
+        for (uint32_t j = 0; j < C; ++j) {
+            const uint32_t q = __builtin_amdgcn_readlane(qw, j);
+            const uint32_t x = q + inc * s0;
+            uint32_t *const dst = q == PLAN_SKIP ? sink : base + j * BS;
+            __builtin_nontemporal_store(u32x4{x, x + inc, x + 2 * inc, x + 3 * inc}, reinterpret_cast<u32x4 *>(dst));
+        }
+    }
+    // tail: the whole buckets after each row's last full chunk
+    const uint64_t tpr = whole - cpr * C, tails = (uint64_t)rows * tpr;
+    for (uint64_t t = wid; t < tails; t += nwaves) {
+        const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
+        const uint32_t q = v.plan[r * NB + b];
+        if (q == PLAN_SKIP) continue;
+        const uint32_t inc = r == N ? 1u : 0u, x = q + inc * s0;
+        uint32_t *const dst = (r == N ? v.chosen : v.st + r * v.shard_len) + (b << BSH) + s0;
+        __builtin_nontemporal_store(u32x4{x, x + inc, x + 2 * inc, x + 3 * inc}, reinterpret_cast<u32x4 *>(dst));
     }
 }
 
@@ -1229,6 +1404,7 @@ __global__ void k_reset(DevView v, uint32_t n_partials)
     if (i < 8ull * n_partials) v.partials[i] = 0;
     if (i == 0) {
         *v.out_cursor = 0;
+        *v.fast_rest = 0;
         v.viol->code = v.viol->node = v.viol->seq = v.viol->iid = v.viol->count = 0;
     }
 }
@@ -1289,7 +1465,16 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
         // digest runs (verification) take their own instantiation, so the
         // timed kernel carries no digest code
         if (v.digest) hipLaunchKernelGGL((k_apply_fast<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-        else switch (g.variant) {
+        else if (!(v.knobs & 64) && v.N <= FAST_MAX_NODES) {
+            // plan + stream, then the per-slot pairs (knob 64: the one-kernel form)
+            hipLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s, v, g.apply_wgs);
+            switch ((v.knobs >> 12) & 3) {   // chunk size A/B (tools/ab_apply.py)
+            case 1: hipLaunchKernelGGL(k_store<16>, dim3(g.store_wgs), dim3(256), 0, s, v); break;
+            case 2: hipLaunchKernelGGL(k_store<48>, dim3(g.store_wgs), dim3(256), 0, s, v); break;
+            default: hipLaunchKernelGGL(k_store<32>, dim3(g.store_wgs), dim3(256), 0, s, v); break;
+            }
+            hipLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+        } else switch (g.variant) {
         case 1: hipLaunchKernelGGL((k_apply_fast<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         case 2: hipLaunchKernelGGL((k_apply_fast<5, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;

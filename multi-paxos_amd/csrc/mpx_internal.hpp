@@ -170,6 +170,10 @@ struct DevView {
     uint8_t *st_valid;              // per (node, bucket): node * NB + bucket
     uint32_t *chosen;               // per instance: entry + 1
     uint8_t *chosen_valid;          // per bucket
+    uint32_t *plan;                 // (N + 1) * NB: the value k_store writes over a whole (row, bucket),
+                                    // rows 0..N-1 state, row N chosen log; PLAN_SKIP = not by k_store
+    uint32_t *fast_rest;            // pairs k_plan leaves to k_apply_fast (0: it exits at once)
+    uint32_t *store_dummy;          // 64 KiB sink for k_store's skipped (row, bucket) stores
     // outputs
     OutRec *out;
     unsigned long long *out_cursor;
@@ -214,7 +218,7 @@ MPX_HD inline uint64_t scalar_digest(uint32_t node, uint64_t promised, uint64_t 
 }
 
 // kernels (kernels.hip); every launcher queues on `stream`, returns hipError_t as int
-struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, variant; };
+struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, variant, store_wgs; };
 int launch_run(const DevView &v, void *stream, LaunchGeom g, void *ev_begin, void *ev_apply0,
                void *ev_apply1, void *ev_end);
 // readback: count slots of node `node` (node >= N: the chosen log) from shard

@@ -33,13 +33,29 @@ def _need_gpu():
         pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
 
 
+COUNTERS = ("chosen", "promise_entries", "accept_apps", "commit_apps", "violations")
+
+
+def _step_path(e, want, st_run):
+    """The timed path (mpx_step: k_plan + k_store + k_apply_fast's remaining
+    pairs, no digest code) gives the same result bytes and counters as the
+    digested mpx_run (one-kernel k_apply_fast)."""
+    e.step()
+    e.sync()
+    st = e.stats()
+    got = e.dump()
+    assert got == want, mpxr.diff(got, want)
+    assert [st[k] for k in COUNTERS] == [st_run[k] for k in COUNTERS]
+
+
 @pytest.mark.parametrize("name", sorted(INDEX))
 def test_engine_matches_reference_golden(name):
     trace, want = _read(name, ".mpxt"), _read(name, ".mpxr")
     with mpx.Engine.for_trace(trace) as e:
         st = e.run()
         got = e.dump()
-    assert got == want, mpxr.diff(got, want)
+        assert got == want, mpxr.diff(got, want)
+        _step_path(e, want, st)
     meta = INDEX[name]
     assert (st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"]) == \
         (meta["C"], meta["P"], meta["A"], meta["L"])
@@ -63,6 +79,7 @@ def test_engine_matches_oracle_clean(n, m, b):
             assert not any(av) and not any(ab)
             assert all(x == 1 << 16 for x in cb)
             assert e.read_node_scalars(node) == (1 << 16, 1 << 16)
+        _step_path(e, want, st)
 
 
 def test_engine_c2_full_size_digests():
@@ -73,6 +90,8 @@ def test_engine_c2_full_size_digests():
     _, ostats, _ = oracle_run(t)
     with mpx.Engine.for_trace(t) as e:
         st = e.run()
+        d_run = e.dump()
+        _step_path(e, d_run, st)
     assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
     assert st["chosen"] == m and st["bytes_alg"] == 40 * n * m
@@ -170,6 +189,7 @@ def test_engine_matches_oracle_c3_faulty(seed, m, p, b):
     with mpx.Engine.for_trace(t) as e:
         st = e.run()
         got = e.dump()
+        _step_path(e, want, st)
     assert got == want, mpxr.diff(got, want)
     assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats

@@ -19,7 +19,7 @@ __device__ inline uint64_t xcd_id(uint32_t wv)
 
 // item = C consecutive 1-KiB buckets; R rows; LOAD: one dependent 16-B load
 // per lane from `meta` (two levels) + vmcnt(0) before the item's stores
-template <int C, bool LOAD>
+template <int C, bool LOAD, bool NT = false>
 __global__ __launch_bounds__(256) void k_rows(uint32_t *st, const uint64_t *meta, uint64_t NB, uint32_t R,
                                               uint64_t L, unsigned long long *sink)
 {
@@ -40,13 +40,18 @@ __global__ __launch_bounds__(256) void k_rows(uint32_t *st, const uint64_t *meta
             uint32_t *row = st + (uint64_t)r * L + it * C * 256;
 #pragma unroll
             for (int c = 0; c < C; ++c)
-                *reinterpret_cast<u32x4 *>(row + c * 256 + 4 * lane) = u32x4{q, q + 1, q + 2, q + r};
+            {
+                u32x4 *dst = reinterpret_cast<u32x4 *>(row + c * 256 + 4 * lane);
+                const u32x4 val = u32x4{q, q + 1, q + 2, q + r};
+                if (NT) __builtin_nontemporal_store(val, dst);
+                else *dst = val;
+            }
         }
     }
     if (acc == 0x123456789ull) *sink = acc;
 }
 
-template <int C, bool LOAD>
+template <int C, bool LOAD, bool NT = false>
 static void run(const char *name, uint32_t *st, const uint64_t *meta, uint64_t NB, uint32_t R, uint64_t L,
                 unsigned long long *sink, int cus)
 {
@@ -57,7 +62,7 @@ static void run(const char *name, uint32_t *st, const uint64_t *meta, uint64_t N
         float best = 1e9f;
         for (int r = 0; r < 4; ++r) {
             hipEventRecord(a);
-            hipLaunchKernelGGL((k_rows<C, LOAD>), dim3(grid), dim3(256), 0, 0, st, meta, NB, R, L, sink);
+            hipLaunchKernelGGL((k_rows<C, LOAD, NT>), dim3(grid), dim3(256), 0, 0, st, meta, NB, R, L, sink);
             hipEventRecord(b);
             hipEventSynchronize(b);
             float ms = 0;
@@ -91,6 +96,25 @@ int main()
     run<1, true>("1 KiB/row, load+wait", st, meta, NB, R, L, sink, cus);
     run<2, true>("2 KiB/row, load+wait", st, meta, NB, R, L, sink, cus);
     run<4, true>("4 KiB/row, load+wait", st, meta, NB, R, L, sink, cus);
+    run<1, false, true>("1 KiB/row, no load, nt", st, meta, NB, R, L, sink, cus);
+    run<4, false, true>("4 KiB/row, no load, nt", st, meta, NB, R, L, sink, cus);
+    run<1, true, true>("1 KiB/row, load+wait, nt", st, meta, NB, R, L, sink, cus);
+    run<4, true, true>("4 KiB/row, load+wait, nt", st, meta, NB, R, L, sink, cus);
+    {
+        hipEvent_t a, b;
+        hipEventCreate(&a); hipEventCreate(&b);
+        float best = 1e9f;
+        for (int r = 0; r < 4; ++r) {
+            hipEventRecord(a);
+            hipMemsetD32Async((hipDeviceptr_t)st, r, (size_t)R * L, 0);
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms = 0;
+            hipEventElapsedTime(&ms, a, b);
+            if (r && ms < best) best = ms;
+        }
+        printf("%-28s          : %.3f ms  %.2f TB/s\n", "hipMemsetD32", best, (double)R * L * 4 / (best * 1e-3) / 1e12);
+    }
     hipFree(st); hipFree(meta); hipFree(sink);
     return 0;
 }

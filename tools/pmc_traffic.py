@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""HBM traffic per k_apply launch from rocprofv3 PMC counters (run on the GPU box).
+"""HBM traffic per apply phase (k_plan + k_store + k_apply_fast) from rocprofv3 PMC counters (run on the GPU box).
 
 Follows MI355X_MICROARCH.md §HBM / §rocprofv3 PMC slots:
   * FETCH_SIZE (3 TCC slots) and WRITE_SIZE (2) do not fit one pass together:
@@ -59,9 +59,12 @@ def main():
         fk, wk = sum(f) / len(f), sum(w) / len(w)
         out["kernels"][name] = {"dispatches": len(f), "FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk,
                                 "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024}
-    # the timed instantiation (digest runs use k_apply_fast<..., true>)
-    apply = [v for k, v in out["kernels"].items() if "k_apply_fast" in k and "false" in k]
-    out["hbm_bytes_per_launch"] = apply[0]["hbm_bytes_per_launch"] if apply else None
+    # the timed apply phase: k_plan + k_store + k_apply_fast<1, false, true>
+    # (digest runs use the one-kernel k_apply_fast<..., true, false>)
+    phase = [v for k, v in out["kernels"].items()
+             if "k_plan" in k or "k_store" in k or ("k_apply_fast" in k and "true>" in k and "false" in k)]
+    out["apply_phase_kernels"] = [k for k, v in out["kernels"].items() if v in phase]
+    out["hbm_bytes_per_launch"] = sum(v["hbm_bytes_per_launch"] for v in phase) if phase else None
     out["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"
     # written under gpurun_out/ (merged back from the GPU box); copy into profiles/ to commit
     path = os.path.join(a.outdir, "%s_pmc.json" % a.tag)
