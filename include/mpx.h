@@ -221,6 +221,15 @@ int  mpx_drain_sends(mpx_engine *eng, mpx_send_fn fn, void *user);
 int  mpx_read_chosen(mpx_engine *eng, uint64_t first, uint64_t count, uint64_t *out);
 /* per-node scalars: promised_proposal_id_ and max_proposal_id_
  * (multi/paxos.cpp:492,460) */
+/* In-order executor of one node, on the device (replaces the
+ * apply loop of PaxosImpl::OnCommit, multi/paxos.cpp:1584-1622, and the
+ * member Learner's, member/paxos.cpp:1042-1053): *frontier = the node's
+ * next_id_to_apply_ (first instance of the shard not committed there),
+ * *count = Values executed below it (noops and member membership Values
+ * skipped), handles[0 .. min(count, cap)) = their handles in instance order
+ * (payload bytes: mpx_value_bytes).  handles may be NULL when cap is 0. */
+int  mpx_read_executed(mpx_engine *eng, uint32_t node, uint64_t *frontier,
+                       uint64_t *count, uint64_t *handles, uint64_t cap);
 int  mpx_read_node_scalars(mpx_engine *eng, uint32_t node,
                            uint64_t *promised, uint64_t *max_seen);
 /* per-node per-instance state; any output pointer may be NULL.

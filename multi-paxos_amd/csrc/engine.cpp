@@ -76,7 +76,7 @@ struct mpx_engine {
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
     DevBuf f_off, frags, gp_list, ev_off, ev_msg, pl_off, pl_msg;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
-    DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy;
+    DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy, exec_aux, exec_out;
     DevBuf decode_buf;                      // readback scratch (k_decode)
     DevBuf out, out_cursor, partials, viol, summary;
     uint64_t out_cap = 0;
@@ -472,6 +472,56 @@ static int decode_slots(mpx_engine *e, uint32_t n, uint64_t l0, uint64_t count, 
     return d2h(out, e->decode_buf, 2 * count);
 }
 
+// In-order executor of node n on the device (kernels.hip k_exec_*): the
+// frontier (shard-local index of the first instance not committed here, i.e.
+// next_id_to_apply_ - shard_begin, multi/paxos.cpp:1584-1622) and the handles
+// of the Values it executed, in instance order, noops skipped (:1601-1606).
+// Membership Values are skipped too (member/paxos.cpp:1042-1053: only client
+// Values reach Apply); that filter needs the host value table.
+static int gpu_executed(mpx_engine *e, uint32_t n, uint64_t &frontier, std::vector<uint64_t> &handles)
+{
+    frontier = 0;
+    handles.clear();
+    if (!have_results(e)) return MPX_OK;
+    HTRY(hipSetDevice(e->device));
+    const uint64_t NB = e->NB;
+    TRY(e->exec_aux.alloc(8 * (2 * NB + 2)));
+    unsigned long long *aux = e->exec_aux.as<unsigned long long>();
+    if (launch_exec(e->view, e->stream, n, aux, nullptr) != 0) return MPX_E_HIP;
+    unsigned long long total = 0, fr = 0;
+    HTRY(hipMemcpyAsync(&fr, aux, 8, hipMemcpyDeviceToHost, e->stream));
+    HTRY(hipMemcpyAsync(&total, aux + 1 + 2 * NB, 8, hipMemcpyDeviceToHost, e->stream));
+    HTRY(hipStreamSynchronize(e->stream));
+    frontier = fr;
+    if (total) {
+        TRY(e->exec_out.alloc(8 * total));
+        if (launch_exec(e->view, e->stream, n, aux, e->exec_out.as<uint64_t>()) != 0) return MPX_E_HIP;
+        HTRY(hipStreamSynchronize(e->stream));
+        TRY(d2h(handles, e->exec_out, total));
+    }
+    {   // Values with no executable payload (membership changes) are not executed
+        std::string payload;
+        size_t k = 0;
+        for (uint64_t h : handles)
+            if (e->vt.exec_payload(h, payload)) handles[k++] = h;
+        handles.resize(k);
+    }
+    return MPX_OK;
+}
+
+extern "C" int mpx_read_executed(mpx_engine *e, uint32_t node, uint64_t *frontier, uint64_t *count,
+                                 uint64_t *handles, uint64_t cap)
+{
+    if (!e || node >= e->cfg.num_nodes || (cap && !handles)) return MPX_E_INVAL;
+    uint64_t fr;
+    std::vector<uint64_t> h;
+    TRY(gpu_executed(e, node, fr, h));
+    if (frontier) *frontier = e->cfg.shard_begin + fr;
+    if (count) *count = h.size();
+    for (uint64_t i = 0; i < h.size() && i < cap; ++i) handles[i] = h[i];
+    return MPX_OK;
+}
+
 extern "C" int mpx_read_chosen(mpx_engine *e, uint64_t first, uint64_t count, uint64_t *out)
 {
     if (!e || (count && !out)) return MPX_E_INVAL;
@@ -697,15 +747,15 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
         std::sort(ch.begin(), ch.end());
         app<uint64_t>(d, ch.size());
         for (auto &c : ch) { app<uint64_t>(d, c.first - h.node_off[n]); app<uint64_t>(d, c.second); }
-        // executor: committed prefix from the shard's first instance (paxos.cpp:1584-1620)
+        // executor: committed prefix from the shard's first instance (paxos.cpp:1584-1620),
+        // computed on the device (gpu_executed); the host only looks up payload bytes
         sec.clear(); cnt = 0;
         std::string payload;
-        for (uint64_t li = 0; li < e->shard_len; ++li) {
-            const uint64_t w = st[2 * li + 1];
-            if (!(w & W_PRESENT) || !(w & W_COMMITTED)) break;
-            const uint64_t hd = w & W_HANDLE;
-            if (MPX_HANDLE_NOOP(hd)) continue;
-            if (!e->vt.exec_payload(hd, payload)) continue;         // member: a membership Value
+        uint64_t frontier;
+        std::vector<uint64_t> executed;
+        TRY(gpu_executed(e, n, frontier, executed));
+        for (uint64_t hd : executed) {
+            if (!e->vt.exec_payload(hd, payload)) return MPX_E_VALUE;   // filtered in gpu_executed
             app<uint32_t>(sec, (uint32_t)payload.size());
             sec += payload;
             ++cnt;

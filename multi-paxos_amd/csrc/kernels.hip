@@ -1429,6 +1429,105 @@ __global__ __launch_bounds__(256) void k_decode(DevView v, uint32_t node, uint64
     out[2 * i + 1] = w;
 }
 
+// ---- in-order executor: multi/paxos.cpp:1584-1622 applies
+// next_id_to_apply_ forward while the instance is committed, skipping noops
+// (:1601-1606); member/paxos.cpp:1042-1053 the same over learned_.  On the GPU
+// the frontier is the first shard slot of the node that is not committed (a
+// min-reduction), and the executed Values are the non-noop handles below it,
+// compacted in instance order by a count / scan / scatter over buckets.
+// aux layout: [0] frontier, [1 .. NB] bucket counts, [NB + 1 .. 2 NB + 1] offsets
+__device__ inline uint64_t exec_word(const DevView &v, uint32_t node, uint64_t li)
+{
+    if (!v.st_valid[(uint64_t)node * v.NB + (li >> BSH)]) return 0;
+    uint64_t b, w;
+    decode_slot(v, v.st[(uint64_t)node * v.shard_len + li], (uint32_t)li & (BS - 1), b, w);
+    return w;
+}
+
+__global__ __launch_bounds__(256) void k_exec_frontier(DevView v, uint32_t node, unsigned long long *aux)
+{
+    const uint64_t li = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool gap = li < v.shard_len && !(exec_word(v, node, li) & W_COMMITTED);
+    const uint64_t m = __ballot(gap);
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicMin(&aux[0], (unsigned long long)li);
+}
+
+// one workgroup per bucket: executed slots (below the frontier, not a noop)
+__device__ inline bool exec_take(const DevView &v, uint32_t node, uint64_t li, uint64_t frontier, uint64_t &h)
+{
+    if (li >= frontier) return false;
+    h = exec_word(v, node, li) & W_HANDLE;
+    return !((h >> 47) & 1);                   // MPX_HANDLE_NOOP
+}
+
+__global__ __launch_bounds__(256) void k_exec_count(DevView v, uint32_t node, unsigned long long *aux)
+{
+    __shared__ uint32_t wc[4];
+    const uint64_t li = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint64_t h;
+    const uint64_t m = __ballot(exec_take(v, node, li, aux[0], h));
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = (uint32_t)__builtin_popcountll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) aux[1 + blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+// exclusive scan of the NB bucket counts, one workgroup of 1024, carried over chunks
+__global__ __launch_bounds__(1024) void k_exec_scan(DevView v, unsigned long long *aux)
+{
+    __shared__ unsigned long long sh[1024];
+    const uint64_t NB = v.NB;
+    const uint32_t t = threadIdx.x;
+    unsigned long long carry = 0;
+    for (uint64_t base = 0; base < NB; base += 1024) {
+        const unsigned long long x = base + t < NB ? aux[1 + base + t] : 0;
+        sh[t] = x;
+        __syncthreads();
+        for (uint32_t d = 1; d < 1024; d <<= 1) {
+            const unsigned long long y = t >= d ? sh[t - d] : 0;
+            __syncthreads();
+            sh[t] += y;
+            __syncthreads();
+        }
+        if (base + t < NB) aux[1 + NB + base + t] = carry + sh[t] - x;
+        carry += sh[1023];
+        __syncthreads();
+    }
+    if (t == 0) aux[1 + 2 * NB] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_exec_scatter(DevView v, uint32_t node, const unsigned long long *aux,
+                                                     uint64_t *out)
+{
+    __shared__ uint32_t wc[4];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t li = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint64_t h = 0;
+    const bool take = exec_take(v, node, li, aux[0], h);
+    const uint64_t m = __ballot(take);
+    if (lane == 0) wc[wv] = (uint32_t)__builtin_popcountll(m);
+    __syncthreads();
+    uint64_t at = aux[1 + v.NB + blockIdx.x] + __builtin_popcountll(m & ((1ull << lane) - 1));
+    for (uint32_t k = 0; k < wv; ++k) at += wc[k];
+    if (take) out[at] = h;
+}
+
+int launch_exec(const DevView &v, void *stream_, uint32_t node, unsigned long long *aux, uint64_t *out)
+{
+    hipStream_t s = (hipStream_t)stream_;
+    const uint32_t blocks = cdiv(v.shard_len, 256);
+    if (!out) {
+        const unsigned long long init = v.shard_len;
+        if (hipMemcpyAsync(aux, &init, 8, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+        if (!blocks) return 0;
+        hipLaunchKernelGGL(k_exec_frontier, dim3(blocks), dim3(256), 0, s, v, node, aux);
+        hipLaunchKernelGGL(k_exec_count, dim3(blocks), dim3(256), 0, s, v, node, aux);
+        hipLaunchKernelGGL(k_exec_scan, dim3(1), dim3(1024), 0, s, v, aux);
+    } else if (blocks) {
+        hipLaunchKernelGGL(k_exec_scatter, dim3(blocks), dim3(256), 0, s, v, node, aux, out);
+    }
+    return (int)hipGetLastError();
+}
+
 int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, uint64_t count, uint64_t *out)
 {
     if (!count) return 0;

@@ -225,6 +225,10 @@ int launch_run(const DevView &v, void *stream, LaunchGeom g, void *ev_begin, voi
 // offset l0 -> out, 2 words each {ballot, PRESENT | COMMITTED? | handle}
 // (chosen: {0, PRESENT | handle}); unwritten buckets read as empty
 int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, uint64_t count, uint64_t *out);
+// in-order executor of one node: out == nullptr queues frontier / count / scan
+// into aux (2 NB + 2 words: frontier, counts, offsets, total); then with out
+// (total words) the scatter of the executed handles in instance order
+int launch_exec(const DevView &v, void *stream, uint32_t node, unsigned long long *aux, uint64_t *out);
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
                      uint64_t G0, uint64_t G1, uint64_t ballot, uint32_t NB,
                      uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,

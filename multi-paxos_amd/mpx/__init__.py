@@ -97,6 +97,7 @@ def lib():
             "mpx_drain_sends": [vp, SEND_FN, vp],
             "mpx_read_chosen": [vp, ctypes.c_uint64, ctypes.c_uint64, u64p],
             "mpx_read_node_scalars": [vp, ctypes.c_uint32, u64p, u64p],
+            "mpx_read_executed": [vp, ctypes.c_uint32, u64p, u64p, u64p, ctypes.c_uint64],
             "mpx_read_node_state": [vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, u64p, u64p, u64p, u64p],
             "mpx_stats_get": [vp, P(Stats)],
             "mpx_last_violation": [vp, P(Violation)],
@@ -268,6 +269,16 @@ class Engine:
         p, m = ctypes.c_uint64(), ctypes.c_uint64()
         _ck("mpx_read_node_scalars", lib().mpx_read_node_scalars(self.h, node, ctypes.byref(p), ctypes.byref(m)))
         return p.value, m.value
+
+    def read_executed(self, node):
+        """(next_id_to_apply_, [handles executed in instance order]) of one node,
+        computed on the device (mpx_read_executed; multi/paxos.cpp:1584-1622)."""
+        fr, cnt = ctypes.c_uint64(), ctypes.c_uint64()
+        _ck("mpx_read_executed", lib().mpx_read_executed(self.h, node, ctypes.byref(fr), ctypes.byref(cnt), None, 0))
+        out = (ctypes.c_uint64 * max(cnt.value, 1))()
+        _ck("mpx_read_executed", lib().mpx_read_executed(self.h, node, ctypes.byref(fr), ctypes.byref(cnt), out,
+                                                         cnt.value))
+        return fr.value, list(out[: cnt.value])
 
     def read_node_state(self, node, first, count):
         arrs = [(ctypes.c_uint64 * count)() for _ in range(4)]

@@ -48,6 +48,24 @@ def _step_path(e, want, st_run):
     assert [st[k] for k in COUNTERS] == [st_run[k] for k in COUNTERS]
 
 
+def _executed_ok(e, want):
+    """mpx_read_executed (device frontier + compaction) against the executed
+    payloads of the expected MPXR (reference / oracle), node by node."""
+    parsed = mpxr.parse(want)
+    for n, nd in enumerate(parsed["nodes"]):
+        committed = {iid: h for iid, kind, _b, h in nd["state"] if kind == 2}
+        front = 0
+        while front in committed:
+            front += 1
+        below = [committed[i] for i in range(front) if not (committed[i] >> 47) & 1]
+        fr, handles = e.read_executed(n)
+        assert fr == front, (n, fr, front)
+        # membership Values are not executed: a subsequence of `below`, as many as the expected payloads
+        it = iter(below)
+        assert all(h in it for h in handles), n
+        assert len(handles) == len(nd["executed"]), n
+
+
 @pytest.mark.parametrize("name", sorted(INDEX))
 def test_engine_matches_reference_golden(name):
     trace, want = _read(name, ".mpxt"), _read(name, ".mpxr")
@@ -55,6 +73,7 @@ def test_engine_matches_reference_golden(name):
         st = e.run()
         got = e.dump()
         assert got == want, mpxr.diff(got, want)
+        _executed_ok(e, want)
         _step_path(e, want, st)
     meta = INDEX[name]
     assert (st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"]) == \
@@ -79,6 +98,8 @@ def test_engine_matches_oracle_clean(n, m, b):
             assert not any(av) and not any(ab)
             assert all(x == 1 << 16 for x in cb)
             assert e.read_node_scalars(node) == (1 << 16, 1 << 16)
+            fr, hs = e.read_executed(node)                  # every instance committed, none a noop
+            assert fr == m and hs == [c & ~mpx.PRESENT for c in ch]
         _step_path(e, want, st)
 
 
