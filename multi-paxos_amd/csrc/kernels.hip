@@ -974,7 +974,7 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
 // in flight (vmcnt counts stores on gfx9: a data-dependent store count would
 // force a full drain instead).  Buckets past the last whole chunk of a row
 // take a plain tail loop.
-template <uint32_t C>
+template <uint32_t C, bool NT = true>
 __global__ __launch_bounds__(256) void k_store(DevView v)
 {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -983,7 +983,7 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
     const uint64_t whole = v.shard_len >> BSH;            // buckets wholly inside the shard
     const uint64_t cpr = whole / C, chunks = (uint64_t)rows * cpr;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
-    const uint64_t wid = xcd_wave_id(wv);
+    const uint64_t wid = xcd_wave_id(wv, v.knobs);
     const uint32_t s0 = 4 * lane;
     uint32_t *const sink = v.store_dummy + (wid & 63) * BS + s0;
     // chunk c = (row r, k-th chunk of the row), advanced incrementally; the
@@ -1017,7 +1017,8 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
             const uint32_t q = __builtin_amdgcn_readlane(qw, j);
             const uint32_t x = q + inc * s0;
             uint32_t *const dst = q == PLAN_SKIP ? sink : base + j * BS;
-            __builtin_nontemporal_store(u32x4{x, x + inc, x + 2 * inc, x + 3 * inc}, reinterpret_cast<u32x4 *>(dst));
+            if (NT) __builtin_nontemporal_store(u32x4{x, x + inc, x + 2 * inc, x + 3 * inc}, reinterpret_cast<u32x4 *>(dst));
+            else *reinterpret_cast<u32x4 *>(dst) = u32x4{x, x + inc, x + 2 * inc, x + 3 * inc};
         }
     }
     // tail: the whole buckets after each row's last full chunk
@@ -1570,6 +1571,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
             switch ((v.knobs >> 12) & 3) {   // chunk size A/B (tools/ab_apply.py)
             case 1: hipLaunchKernelGGL(k_store<16>, dim3(g.store_wgs), dim3(256), 0, s, v); break;
             case 2: hipLaunchKernelGGL(k_store<48>, dim3(g.store_wgs), dim3(256), 0, s, v); break;
+            case 3: hipLaunchKernelGGL((k_store<32, false>), dim3(g.store_wgs), dim3(256), 0, s, v); break;
             default: hipLaunchKernelGGL(k_store<32>, dim3(g.store_wgs), dim3(256), 0, s, v); break;
             }
             hipLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);

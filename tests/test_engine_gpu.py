@@ -80,7 +80,9 @@ def test_engine_matches_reference_golden(name):
         (meta["C"], meta["P"], meta["A"], meta["L"])
 
 
-@pytest.mark.parametrize("n,m,b", [(5, 4096, 256), (3, 1000, 100), (7, 5000, 37), (1, 10, 256), (64, 300, 256)])
+# (9, 256 * 70 + 100): k_store's full 32-bucket chunks, its tail buckets and a partial last bucket
+@pytest.mark.parametrize("n,m,b", [(5, 4096, 256), (3, 1000, 100), (7, 5000, 37), (1, 10, 256), (64, 300, 256),
+                                   (9, 256 * 70 + 100, 256)])
 def test_engine_matches_oracle_clean(n, m, b):
     t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=b)
     want, ostats, _ = oracle_run(t)
@@ -153,6 +155,7 @@ def test_device_generator_matches_host(n, m):
         e.load_clean_device(num_instances=m)
         st = e.run()
         got = e.dump()
+        _step_path(e, want, st)
     assert got == want, mpxr.diff(got, want)
     assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
@@ -178,6 +181,8 @@ def test_sharded_device_generator_sums_to_whole(shards):
                 tot[k] = (tot[k] + st[k]) % (1 << 64)
             ch = e.read_chosen(sb, se - sb)
             assert ch == [mpx.PRESENT | (i + 1) for i in range(sb, se)]
+            _step_path(e, e.dump(), st)
+            assert e.read_chosen(sb, se - sb) == ch
     for k in tot:
         assert tot[k] == whole[k] % (1 << 64), k
 
