@@ -17,8 +17,8 @@ roofline: the dominant unit is the apply phase — k_plan (one thread per
 (acceptor, bucket) pair decides which message run fixes it), k_store (streams
 the slots and the chosen log) and k_apply_fast's per-slot pairs (none in C4:
 it exits at once) — bracketed by HIP events on the engine's stream; k_store is
-≈92 % of it (profiles/).  achieved = the phase's compulsory bytes (DESIGN.md
-§4: one 4-byte state slot written per (acceptor, instance), one 4-byte
+most of it (profiles/).  achieved = the phase's compulsory bytes (DESIGN.md
+§4: one 2-byte state slot written per (acceptor, instance), one 4-byte
 chosen-log entry per instance, one 16-byte fragment descriptor read per
 (acceptor, bucket, message), and the 4-byte plan word per (row, bucket) written
 and read back — a slot names the message run that fixed it, whose entry in the
@@ -44,6 +44,7 @@ import ctypes
 import glob
 import json
 import os
+import re
 import sys
 import threading
 import time
@@ -110,7 +111,10 @@ def broadcast_bytes(pg, data, rank):
 def latest_pmc(n_nodes, instances, world):
     """HBM bytes per k_apply launch from the newest profiles/*pmc*.json of this config."""
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    def natural(path):                              # r01_v10 after r01_v9
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=natural):
         try:
             d = json.load(open(path))
         except Exception:
@@ -223,10 +227,10 @@ def main():
     apply_mean = sum(apply_ms) / max(len(apply_ms), 1)
     bytes_survey = st["bytes_alg"]                  # this rank's 16P + 24A + 16L per launch
     L = se - sb
-    # 4-B state slots + 4-B chosen log + the ACCEPT and COMMIT descriptors of every (node, bucket)
+    # 2-B state slots + 4-B chosen log + the ACCEPT and COMMIT descriptors of every (node, bucket)
     # + the plan word of every (row, bucket), written by k_plan and read by k_store
     nb = (L + 255) // 256
-    bytes_min = 4 * N * L + 4 * L + 2 * 16 * N * nb + 2 * 4 * (N + 1) * nb
+    bytes_min = 2 * N * L + 4 * L + 2 * 16 * N * nb + 2 * 4 * (N + 1) * nb
     achieved = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
     pmc = latest_pmc(N, M, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None

@@ -222,7 +222,7 @@ static int finish_view(mpx_engine *e)
     v.shard_begin = e->cfg.shard_begin;
     v.shard_len = e->shard_len;
     v.num_msgs = e->num_msgs;
-    TRY(e->st.alloc((size_t)N * e->shard_len * 4));
+    TRY(e->st.alloc((size_t)N * e->shard_len * sizeof(slot_t)));
     TRY(e->st_valid.alloc((size_t)N * e->NB));
     TRY(e->chosen.alloc(e->shard_len * 4));
     TRY(e->chosen_valid.alloc(e->NB));
@@ -243,7 +243,7 @@ static int finish_view(mpx_engine *e)
     if (!e->out_cap) e->out_cap = 1 << 16;
     TRY(e->out.alloc(e->out_cap * sizeof(OutRec)));
     TRY(e->node_scal.alloc(16ull * N));
-    v.st = e->st.as<uint32_t>();
+    v.st = e->st.as<slot_t>();
     v.st_valid = e->st_valid.as<uint8_t>();
     v.chosen = e->chosen.as<uint32_t>();
     v.chosen_valid = e->chosen_valid.as<uint8_t>();

@@ -681,7 +681,10 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
 
     // fragment CSR per (node, bucket), stable (keeps message order)
     ht.f_off.assign(N * NB + 1, 0);
-    for (uint64_t i = 0; i < N * NB; ++i) ht.f_off[i + 1] = ht.f_off[i] + fcount[i];
+    for (uint64_t i = 0; i < N * NB; ++i) {
+        ht.f_off[i + 1] = ht.f_off[i] + fcount[i];
+        if (fcount[i] > MAX_PAIR_FRAGS) return MPX_E_RANGE;   // 2-byte state slots (mpx_internal.hpp)
+    }
     if (fr.size() > MAX_FRAGS) return MPX_E_RANGE;             // 4-byte state slots (mpx_internal.hpp)
     ht.frags.resize(fr.size());
     {

@@ -540,6 +540,13 @@ __device__ inline void decode_slot(const DevView &v, uint32_t q, uint32_t s, uin
     word = W_PRESENT | ((f.flags >> 4) == K_COMMIT ? W_COMMITTED : 0) | v.e_val[ent];
 }
 
+// the stored 2-byte slot of (node, shard index li) as a global fragment index + 1
+__device__ inline uint32_t slot_global(const DevView &v, uint32_t node, uint64_t li)
+{
+    const uint32_t s = v.st[(uint64_t)node * v.shard_len + li];
+    return s ? (uint32_t)(v.f_off[(li >> BSH) * v.N + node] + s) : 0;
+}
+
 __device__ inline uint64_t slot_digest(const DevView &v, uint32_t n, uint64_t iid, uint32_t q)
 {
     if (!q) return 0;
@@ -592,6 +599,7 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // ACCEPT / COMMIT runs and its node has no PREPARE after the first of them —
 // its snapshot events see empty state, so skipping them changes no output.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t FAST_PAIR_FRAGS = 2;      // descriptors a pair lane prefetches
 __host__ __device__ inline uint32_t fast_group(uint32_t N, uint32_t cap = 4)
 {
@@ -711,26 +719,28 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         // AFTER_STORE: k_plan counted and k_store wrote the uniform pairs of whole buckets
         const bool stored = AFTER_STORE && (b0 + pg + 1) * BS <= v.shard_len;
         if (uni && !stored) { cA += nA * BS; cL += nL * BS; }
-        const uint32_t qv = fix == NONE32 ? 0 : (uint32_t)(oa + fix + 1);
+        const uint32_t qv = fix == NONE32 ? 0 : (uint32_t)(oa + fix + 1);   // global fragment + 1
+        const uint32_t ql = fix == NONE32 ? 0 : fix + 1;                     // as stored: pair-local
         if (elig) v.st_valid[(uint64_t)pn * NB + b0 + pg] = 1;
 
         // uniform pairs, node-major so each row gets its G buckets back to back
         const bool whole = (b0 + nb) * BS <= v.shard_len;
         for (uint32_t n = 0; n < N; ++n) {
-            uint32_t *row = v.st + (uint64_t)n * v.shard_len + b0 * BS;
+            slot_t *row = v.st + (uint64_t)n * v.shard_len + b0 * BS;
             for (uint32_t g = 0; g < nb; ++g) {
                 const uint32_t p = g * N + n;
                 if (!((uni_m >> p) & 1)) continue;
                 if (AFTER_STORE && (b0 + g + 1) * BS <= v.shard_len) continue;
                 const uint32_t q = rl32(qv, p);
+                const slot_t sq = (slot_t)rl32(ql, p);
                 if (v.knobs & 16) {
                     // experiment: no state stores
                 } else if (whole) {
-                    __builtin_nontemporal_store(u32x4{q, q, q, q}, reinterpret_cast<u32x4 *>(row + g * BS + s0));
+                    __builtin_nontemporal_store(u16x4{sq, sq, sq, sq}, reinterpret_cast<u16x4 *>(row + g * BS + s0));
                 } else {
 #pragma unroll
                     for (uint32_t j = 0; j < SPL; ++j)
-                        if ((b0 + g) * BS + s0 + j < v.shard_len) row[g * BS + s0 + j] = q;
+                        if ((b0 + g) * BS + s0 + j < v.shard_len) row[g * BS + s0 + j] = sq;
                 }
                 if (DIGEST)
 #pragma unroll
@@ -815,16 +825,19 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
                 }
             }
             if (__ballot(bad) && lane == 0) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, ib);
-            uint32_t *srow = v.st + (uint64_t)n * v.shard_len + li0;
+            slot_t *srow = v.st + (uint64_t)n * v.shard_len + li0;
+            const uint64_t pbase = f_base + f0;        // the pair's first fragment
+            const slot_t l0 = q0 ? (slot_t)(q0 - pbase) : 0, l1 = q1 ? (slot_t)(q1 - pbase) : 0,
+                         l2 = q2 ? (slot_t)(q2 - pbase) : 0, l3 = q3 ? (slot_t)(q3 - pbase) : 0;
             if (v.knobs & 16) {
                 // experiment: no state stores
             } else if (li0 + BS <= v.shard_len) {
-                __builtin_nontemporal_store(u32x4{q0, q1, q2, q3}, reinterpret_cast<u32x4 *>(srow + s0));
+                __builtin_nontemporal_store(u16x4{l0, l1, l2, l3}, reinterpret_cast<u16x4 *>(srow + s0));
             } else {
-                if (li0 + s0 < v.shard_len) srow[s0] = q0;
-                if (li0 + s0 + 1 < v.shard_len) srow[s0 + 1] = q1;
-                if (li0 + s0 + 2 < v.shard_len) srow[s0 + 2] = q2;
-                if (li0 + s0 + 3 < v.shard_len) srow[s0 + 3] = q3;
+                if (li0 + s0 < v.shard_len) srow[s0] = l0;
+                if (li0 + s0 + 1 < v.shard_len) srow[s0 + 1] = l1;
+                if (li0 + s0 + 2 < v.shard_len) srow[s0 + 2] = l2;
+                if (li0 + s0 + 3 < v.shard_len) srow[s0 + 3] = l3;
             }
             if (DIGEST)
                 dig += slot_digest(v, n, ib + s0, q0) + slot_digest(v, n, ib + s0 + 1, q1) +
@@ -920,7 +933,7 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
         const bool whole = (b + 1) * BS <= v.shard_len;
         uint32_t q = PLAN_SKIP;
         if (uni && whole) {
-            q = fix == NONE32 ? 0 : (uint32_t)(oa + fix + 1);
+            q = fix == NONE32 ? 0 : fix + 1;             // the slot as stored: pair-local fragment + 1
             v.st_valid[(uint64_t)n * NB + b] = 1;
             cA = nA * BS; cL = nL * BS;
         } else if (elig || (in_list && len > F)) {
@@ -965,71 +978,86 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
     }
 }
 
-// Streams the plan: a wave takes a chunk of C whole buckets of one
-// row (state row n or the chosen log) and writes C KiB contiguous,
-// one 16-byte non-temporal store per lane per bucket, 4 slots per lane.  The
-// chunk's plan words are loaded one chunk ahead and the inner loop has no
-// branch — a PLAN_SKIP bucket's store goes to a scratch sink — so the only
-// wait per chunk is for that one load, with the previous chunk's stores still
-// in flight (vmcnt counts stores on gfx9: a data-dependent store count would
-// force a full drain instead).  Buckets past the last whole chunk of a row
-// take a plain tail loop.
-template <uint32_t C, bool NT = true>
-__global__ __launch_bounds__(256) void k_store(DevView v)
+// Streams the plan: a wave takes a chunk of C whole buckets of one row — a
+// state row (2-byte slots: 512 B per bucket) or the chosen log (4-byte
+// entries: 1 KiB per bucket) — and writes it contiguously, one non-temporal
+// store per lane per bucket, 4 slots per lane.  The chunk's plan words are
+// loaded one chunk ahead and the inner loop has no branch — a PLAN_SKIP
+// bucket's store goes to a scratch sink — so the only wait per chunk is for
+// that one load, with the previous chunk's C stores still in flight (vmcnt
+// counts stores on gfx9: a data-dependent store count would force a full drain
+// instead).  A wave walks chunks c = wid, wid + nwaves, ... over the state rows
+// and then the chosen-log row; buckets past the last whole chunk of a row take
+// a plain tail loop.
+template <uint32_t C, bool NT, typename T, typename V>
+__device__ inline uint64_t store_chunks(const DevView &v, uint64_t c, const uint64_t c_base, const uint64_t c_end,
+                                        const uint64_t cpr, const uint32_t prow0, T *const base0, const uint64_t stride,
+                                        const uint32_t inc, T *const sink, const uint64_t nwaves)
 {
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t N = v.N, rows = N + 1;
-    const uint64_t NB = v.NB;
-    const uint64_t whole = v.shard_len >> BSH;            // buckets wholly inside the shard
-    const uint64_t cpr = whole / C, chunks = (uint64_t)rows * cpr;
-    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
-    const uint64_t wid = xcd_wave_id(wv, v.knobs);
-    const uint32_t s0 = 4 * lane;
-    uint32_t *const sink = v.store_dummy + (wid & 63) * BS + s0;
-    // chunk c = (row r, k-th chunk of the row), advanced incrementally; the
-    // plan load is unconditional (lanes >= C repeat lanes 0..C-1, a finished
-    // wave re-reads the last chunk) so the compiler can count it exactly
-    uint32_t r = 0, k = 0;
-    if (cpr) { r = (uint32_t)(wid / cpr); k = (uint32_t)(wid - (uint64_t)r * cpr); }
-    const uint32_t step_r = cpr ? (uint32_t)(nwaves / cpr) : 0, step_k = cpr ? (uint32_t)(nwaves - (uint64_t)step_r * cpr) : 0;
-    auto advance = [&](uint32_t &rr, uint32_t &kk) {
-        rr += step_r; kk += step_k;
-        if (kk >= cpr) { kk -= (uint32_t)cpr; ++rr; }
+    if (c >= c_end) return c;
+    const uint32_t lane = threadIdx.x & 63, s0 = 4 * lane;
+    const uint64_t rel = c - c_base;
+    uint32_t rn = (uint32_t)(rel / cpr), kn = (uint32_t)(rel - (uint64_t)rn * cpr);
+    const uint32_t step_r = (uint32_t)(nwaves / cpr), step_k = (uint32_t)(nwaves - (uint64_t)step_r * cpr);
+    // unconditional plan load (lanes >= C repeat lanes 0..C-1; past the end:
+    // a valid dummy address) so the compiler can count it exactly
+    auto ptr = [&](uint64_t cc, uint32_t rr, uint32_t kk) -> const uint32_t * {
+        const uint64_t o = cc < c_end ? (uint64_t)(prow0 + rr) * v.NB + (uint64_t)kk * C : (uint64_t)prow0 * v.NB;
+        return v.plan + o + (lane & (C - 1));
     };
-    auto plan_ptr = [&](uint32_t rr, uint32_t kk) -> const uint32_t * {
-        const bool live = rr < rows;
-        return v.plan + (live ? (uint64_t)rr * NB + (uint64_t)kk * C : 0) + (lane & (C - 1));
-    };
-    uint32_t rn = r, kn = k;
-    uint32_t qn = chunks ? *plan_ptr(rn, kn) : PLAN_SKIP;
+    uint32_t qn = *ptr(c, rn, kn);
     // settled before the loop: the loop-carried plan word then has one pending
     // source, the in-loop load, which waits as vmcnt(C) (its C stores in flight)
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    for (uint64_t c = wid; c < chunks; c += nwaves) {
-        const uint32_t qw = qn;
-        const uint32_t rc = rn, kc = kn;
-        advance(rn, kn);
-        qn = *plan_ptr(rn, kn);
-        const uint32_t inc = rc == N ? 1u : 0u;
-        uint32_t *const base = (rc == N ? v.chosen : v.st + (uint64_t)rc * v.shard_len) + ((uint64_t)kc * C << BSH) + s0;
+    for (; c < c_end; c += nwaves) {
+        const uint32_t qw = qn, rc = rn, kc = kn;
+        rn += step_r; kn += step_k;
+        if (kn >= cpr) { kn -= (uint32_t)cpr; ++rn; }
+        qn = *ptr(c + nwaves, rn, kn);
+        T *const base = base0 + (uint64_t)rc * stride + ((uint64_t)kc * C << BSH) + s0;
 #pragma unroll
         for (uint32_t j = 0; j < C; ++j) {
             const uint32_t q = __builtin_amdgcn_readlane(qw, j);
-            const uint32_t x = q + inc * s0;
-            uint32_t *const dst = q == PLAN_SKIP ? sink : base + j * BS;
-            if (NT) __builtin_nontemporal_store(u32x4{x, x + inc, x + 2 * inc, x + 3 * inc}, reinterpret_cast<u32x4 *>(dst));
-            else *reinterpret_cast<u32x4 *>(dst) = u32x4{x, x + inc, x + 2 * inc, x + 3 * inc};
+            const T x = (T)(q + inc * s0);
+            T *const dst = q == PLAN_SKIP ? sink : base + j * BS;
+            const V val = V{x, (T)(x + inc), (T)(x + 2 * inc), (T)(x + 3 * inc)};
+            if (NT) __builtin_nontemporal_store(val, reinterpret_cast<V *>(dst));
+            else *reinterpret_cast<V *>(dst) = val;
         }
     }
+    return c;
+}
+
+template <uint32_t C, bool NT = true>
+__global__ __launch_bounds__(256) void k_store(DevView v)
+{
+    // wave-uniform chunk walk in scalar registers (readfirstlane): the row
+    // address math stays off the VGPRs the plan load writes
+    const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t N = v.N;
+    const uint64_t NB = v.NB;
+    const uint64_t whole = v.shard_len >> BSH;            // buckets wholly inside the shard
+    const uint64_t cpr = whole / C, S = (uint64_t)N * cpr;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    const uint64_t wid = xcd_wave_id(wv, v.knobs);
+    const uint32_t s0 = 4 * lane;
+    uint32_t *const sink = v.store_dummy + (wid & 63) * BS;
+    const uint64_t c = store_chunks<C, NT, slot_t, u16x4>(v, wid, 0, S, cpr, 0, v.st, v.shard_len, 0,
+                                                          reinterpret_cast<slot_t *>(sink) + s0, nwaves);
+    store_chunks<C, NT, uint32_t, u32x4>(v, c, S, S + cpr, cpr, N, v.chosen, 0, 1, sink + s0, nwaves);
     // tail: the whole buckets after each row's last full chunk
-    const uint64_t tpr = whole - cpr * C, tails = (uint64_t)rows * tpr;
+    const uint64_t tpr = whole - cpr * C, tails = (uint64_t)(N + 1) * tpr;
     for (uint64_t t = wid; t < tails; t += nwaves) {
         const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
         const uint32_t q = v.plan[r * NB + b];
         if (q == PLAN_SKIP) continue;
-        const uint32_t inc = r == N ? 1u : 0u, x = q + inc * s0;
-        uint32_t *const dst = (r == N ? v.chosen : v.st + r * v.shard_len) + (b << BSH) + s0;
-        __builtin_nontemporal_store(u32x4{x, x + inc, x + 2 * inc, x + 3 * inc}, reinterpret_cast<u32x4 *>(dst));
+        if (r == N) {
+            const uint32_t x = q + s0;
+            __builtin_nontemporal_store(u32x4{x, x + 1, x + 2, x + 3}, reinterpret_cast<u32x4 *>(v.chosen + (b << BSH) + s0));
+        } else {
+            const slot_t x = (slot_t)q;
+            __builtin_nontemporal_store(u16x4{x, x, x, x}, reinterpret_cast<u16x4 *>(v.st + r * v.shard_len + (b << BSH) + s0));
+        }
     }
 }
 
@@ -1088,6 +1116,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         const uint32_t b = (uint32_t)(q / v.N);
         const uint32_t n = (uint32_t)(q - (uint64_t)b * v.N);
         uint64_t fi = rl64(off_cur, 0), fe = rl64(off_cur, 1), ei = rl64(off_cur, 2), ee = rl64(off_cur, 3);
+        const uint64_t pbase = fi;               // the pair's first fragment (slots are pair-local)
         Win win = win_nxt;
         win_nxt = rt2(off_nxt);                  // next item's descriptors in flight
         off_cur = off_nxt;
@@ -1295,7 +1324,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 #pragma unroll
             for (uint32_t j = 0; j < SPL; ++j) {
                 const uint64_t li = li0 + lane + 64 * j;
-                if (li < v.shard_len) v.st[(uint64_t)n * v.shard_len + li] = sm[j];
+                if (li < v.shard_len) v.st[(uint64_t)n * v.shard_len + li] = sm[j] ? (slot_t)(sm[j] - pbase) : 0;
                 if (sw[j])
                     if (v.digest) dig += state_digest(n, v.shard_begin + li, (sw[j] & W_COMMITTED) ? 2 : 1, sb[j], sw[j] & W_HANDLE);
             }
@@ -1424,7 +1453,7 @@ __global__ __launch_bounds__(256) void k_decode(DevView v, uint32_t node, uint64
         const uint32_t c = v.chosen_valid[li >> BSH] ? v.chosen[li] : 0;
         if (c) w = W_PRESENT | v.e_val[c - 1];
     } else if (v.st_valid[(uint64_t)node * v.NB + (li >> BSH)]) {
-        decode_slot(v, v.st[(uint64_t)node * v.shard_len + li], (uint32_t)li & (BS - 1), b, w);
+        decode_slot(v, slot_global(v, node, li), (uint32_t)li & (BS - 1), b, w);
     }
     out[2 * i] = b;
     out[2 * i + 1] = w;
@@ -1441,7 +1470,7 @@ __device__ inline uint64_t exec_word(const DevView &v, uint32_t node, uint64_t l
 {
     if (!v.st_valid[(uint64_t)node * v.NB + (li >> BSH)]) return 0;
     uint64_t b, w;
-    decode_slot(v, v.st[(uint64_t)node * v.shard_len + li], (uint32_t)li & (BS - 1), b, w);
+    decode_slot(v, slot_global(v, node, li), (uint32_t)li & (BS - 1), b, w);
     return w;
 }
 

@@ -11,7 +11,8 @@
 //     256-instance bucket, listed per pair in processing order (CSR); pairs are
 //     bucket-major, q = bucket * N + node, so one wave can walk a bucket's
 //     nodes and reuse the shared Values
-//   * state: one 4-byte slot per (node, instance) = fragment + 1, 0 = empty:
+//   * state: one 2-byte slot per (node, instance) = fragment + 1 counted from
+//       the pair's first fragment (f_off[bucket * N + node]), 0 = empty:
 //       the message run (fragment) that fixed the slot.  Its message's type
 //       says accepted or committed, its header ballot is the tag (multi;
 //       member: the entry's proposal id e_pid) and its entry at the slot's
@@ -48,6 +49,9 @@ constexpr uint64_t W_HANDLE = (1ull << 62) - 1;
 // entries stay below 2^32 - 1
 constexpr uint64_t MAX_ENTRIES = 0xFFFFFFFEull;
 constexpr uint64_t MAX_FRAGS = 0xFFFFFFFEull;
+// 2-byte state slots hold the pair-local fragment index + 1
+constexpr uint64_t MAX_PAIR_FRAGS = 0xFFFEull;
+typedef uint16_t slot_t;
 
 // m_flags bits, written by the header scan / proposer kernels
 enum : uint8_t {
@@ -166,7 +170,7 @@ struct DevView {
     const uint64_t *cf_off;         // NB+1
     const Frag *cfrags;
     // state
-    uint32_t *st;                   // one slot per (node, instance), node-major
+    slot_t *st;                     // one 2-byte slot per (node, instance), node-major
     uint8_t *st_valid;              // per (node, bucket): node * NB + bucket
     uint32_t *chosen;               // per instance: entry + 1
     uint8_t *chosen_valid;          // per bucket
