@@ -222,9 +222,8 @@ static int finish_view(mpx_engine *e)
     v.shard_begin = e->cfg.shard_begin;
     v.shard_len = e->shard_len;
     v.num_msgs = e->num_msgs;
-    TRY(e->st.alloc((size_t)N * e->shard_len * sizeof(slot_t)));
+    TRY(e->st.alloc((size_t)(N + 1) * e->shard_len * sizeof(slot_t)));   // row N: the chosen log
     TRY(e->st_valid.alloc((size_t)N * e->NB));
-    TRY(e->chosen.alloc(e->shard_len * 4));
     TRY(e->chosen_valid.alloc(e->NB));
     TRY(e->plan.alloc((size_t)(N + 1) * e->NB * 4));
     TRY(e->fast_rest.alloc(8));
@@ -245,7 +244,7 @@ static int finish_view(mpx_engine *e)
     TRY(e->node_scal.alloc(16ull * N));
     v.st = e->st.as<slot_t>();
     v.st_valid = e->st_valid.as<uint8_t>();
-    v.chosen = e->chosen.as<uint32_t>();
+    v.chosen = e->st.as<slot_t>() + (size_t)N * e->shard_len;
     v.chosen_valid = e->chosen_valid.as<uint8_t>();
     v.plan = e->plan.as<uint32_t>();
     v.fast_rest = e->fast_rest.as<uint32_t>();

@@ -692,7 +692,10 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         for (auto &x : fr) ht.frags[pos[x.key]++] = x.f;
     }
     ht.cf_off.assign(NB + 1, 0);
-    for (uint64_t i = 0; i < NB; ++i) ht.cf_off[i + 1] = ht.cf_off[i] + cfcount[i];
+    for (uint64_t i = 0; i < NB; ++i) {
+        ht.cf_off[i + 1] = ht.cf_off[i] + cfcount[i];
+        if (cfcount[i] > MAX_PAIR_FRAGS) return MPX_E_RANGE;  // 2-byte chosen log (mpx_internal.hpp)
+    }
     ht.cfrags.resize(cfr.size());
     {
         std::vector<uint64_t> pos(ht.cf_off.begin(), ht.cf_off.end() - 1);

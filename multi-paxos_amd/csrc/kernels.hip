@@ -475,8 +475,8 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
     const uint64_t li0 = b << BSH;
     uint64_t off = lane < 2 ? v.cf_off[b + lane] : 0;
     uint64_t fi = rl64(off, 0);
-    const uint64_t fe = rl64(off, 1);
-    uint32_t cv[SPL];                          // entry + 1 of the first chosen Value
+    const uint64_t fe = rl64(off, 1), cbase = fi;
+    uint32_t cv[SPL];                          // bucket-local chosen fragment + 1 of the first chosen Value
     uint64_t ch[SPL];                          // its handle (agreement check)
 #pragma unroll
     for (uint32_t j = 0; j < SPL; ++j) { cv[j] = 0; ch[j] = 0; }
@@ -503,7 +503,7 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
                 if (k[j] < 0) continue;
                 const uint64_t iid = v.shard_begin + li0 + lane + 64 * j;
                 if (!cv[j]) {
-                    cv[j] = (uint32_t)(ent + k[j] + 1); ch[j] = val[j]; ++cC;
+                    cv[j] = (uint32_t)(fi + a - cbase + 1); ch[j] = val[j]; ++cC;
                     if (v.digest) dig += chosen_digest(iid, val[j]);
                 } else if (ch[j] != val[j]) record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, iid);
             }
@@ -517,7 +517,7 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
 #pragma unroll
         for (uint32_t j = 0; j < SPL; ++j) {
             const uint64_t li = li0 + lane + 64 * j;
-            if (li < v.shard_len) v.chosen[li] = cv[j];
+            if (li < v.shard_len) v.chosen[li] = (slot_t)cv[j];
         }
         if (lane == 0) v.chosen_valid[b] = 1;
     }
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
     for (; st_c < steps; st_c += nwaves) {
         const uint64_t st = st_c;
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
-        const uint64_t oa = oa_c, oc = oc_c;
+        const uint64_t oa = oa_c;
         uint64_t e[F], w[F];
 #pragma unroll
         for (uint32_t k = 0; k < F; ++k) { e[k] = ne[k]; w[k] = nw[k]; }
@@ -847,13 +847,12 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         // chosen log of the buckets whose one live batch is a full run
         const bool cok = !AFTER_STORE && clive && frag_full(cw) && (b0 + lane + 1) * BS <= v.shard_len;
         const uint64_t cok_m = __ballot(cok);
-        const uint32_t qc = (uint32_t)ce + 1;
         if (cok) v.chosen_valid[b0 + lane] = 1;
         for (uint64_t m = cok_m; m; m &= m - 1) {
             const uint32_t g = (uint32_t)__builtin_ctzll(m);
-            const uint32_t cb = rl32(qc, g) + s0;
             const uint64_t li0 = (b0 + g) << BSH;
-            __builtin_nontemporal_store(u32x4{cb, cb + 1, cb + 2, cb + 3}, reinterpret_cast<u32x4 *>(v.chosen + li0 + s0));
+            // the bucket's only chosen fragment: local index 0, stored + 1
+            __builtin_nontemporal_store(u16x4{1, 1, 1, 1}, reinterpret_cast<u16x4 *>(v.chosen + li0 + s0));
             cC += SPL;
             if (DIGEST) {
                 const uint64_t c0 = rl64(ce, g), ib = v.shard_begin + li0;
@@ -945,9 +944,9 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
         const uint64_t oc = v.cf_off[i], c1 = v.cf_off[i + 1];
         uint32_t q = PLAN_SKIP;
         if (c1 - oc == 1) {
-            const uint64_t ce = v.cfrags[oc].entry, cw = frag_w1(v.cfrags + oc);
+            const uint64_t cw = frag_w1(v.cfrags + oc);
             if (v.b_chosen[(uint32_t)cw] != NONE32 && frag_full(cw) && (i + 1) * BS <= v.shard_len) {
-                q = (uint32_t)ce + 1;
+                q = 1;                                   // its only chosen fragment, + 1
                 v.chosen_valid[i] = 1;
                 cC = BS;
             }
@@ -1037,27 +1036,21 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
     const uint32_t N = v.N;
     const uint64_t NB = v.NB;
     const uint64_t whole = v.shard_len >> BSH;            // buckets wholly inside the shard
-    const uint64_t cpr = whole / C, S = (uint64_t)N * cpr;
+    const uint64_t cpr = whole / C, S = (uint64_t)(N + 1) * cpr;   // rows 0..N-1 state, row N chosen log
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
     const uint64_t wid = xcd_wave_id(wv, v.knobs);
     const uint32_t s0 = 4 * lane;
     uint32_t *const sink = v.store_dummy + (wid & 63) * BS;
-    const uint64_t c = store_chunks<C, NT, slot_t, u16x4>(v, wid, 0, S, cpr, 0, v.st, v.shard_len, 0,
-                                                          reinterpret_cast<slot_t *>(sink) + s0, nwaves);
-    store_chunks<C, NT, uint32_t, u32x4>(v, c, S, S + cpr, cpr, N, v.chosen, 0, 1, sink + s0, nwaves);
+    store_chunks<C, NT, slot_t, u16x4>(v, wid, 0, S, cpr, 0, v.st, v.shard_len, 0,
+                                       reinterpret_cast<slot_t *>(sink) + s0, nwaves);
     // tail: the whole buckets after each row's last full chunk
     const uint64_t tpr = whole - cpr * C, tails = (uint64_t)(N + 1) * tpr;
     for (uint64_t t = wid; t < tails; t += nwaves) {
         const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
         const uint32_t q = v.plan[r * NB + b];
         if (q == PLAN_SKIP) continue;
-        if (r == N) {
-            const uint32_t x = q + s0;
-            __builtin_nontemporal_store(u32x4{x, x + 1, x + 2, x + 3}, reinterpret_cast<u32x4 *>(v.chosen + (b << BSH) + s0));
-        } else {
-            const slot_t x = (slot_t)q;
-            __builtin_nontemporal_store(u16x4{x, x, x, x}, reinterpret_cast<u16x4 *>(v.st + r * v.shard_len + (b << BSH) + s0));
-        }
+        const slot_t x = (slot_t)q;
+        __builtin_nontemporal_store(u16x4{x, x, x, x}, reinterpret_cast<u16x4 *>(v.st + r * v.shard_len + (b << BSH) + s0));
     }
 }
 
@@ -1451,7 +1444,16 @@ __global__ __launch_bounds__(256) void k_decode(DevView v, uint32_t node, uint64
     uint64_t b = 0, w = 0;
     if (node >= v.N) {
         const uint32_t c = v.chosen_valid[li >> BSH] ? v.chosen[li] : 0;
-        if (c) w = W_PRESENT | v.e_val[c - 1];
+        if (c) {
+            // the bucket's chosen fragment c - 1 and its entry at this slot
+            const Frag f = v.cfrags[v.cf_off[li >> BSH] + c - 1];
+            const uint32_t sl = (uint32_t)li & (BS - 1);
+            uint64_t ent = f.entry + (sl - f.start);
+            if (!(f.flags & FR_DENSE))
+                for (uint32_t k = 0; k < f.count; ++k)
+                    if (v.e_slot[f.entry + k] == sl) { ent = f.entry + k; break; }
+            w = W_PRESENT | v.e_val[ent];
+        }
     } else if (v.st_valid[(uint64_t)node * v.NB + (li >> BSH)]) {
         decode_slot(v, slot_global(v, node, li), (uint32_t)li & (BS - 1), b, w);
     }

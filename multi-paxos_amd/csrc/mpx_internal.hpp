@@ -21,7 +21,9 @@
 //       {ballot, word}.  Accepted and committed entries of a node are disjoint
 //       (OnCommit erases accepted_values_, multi/paxos.cpp:1501; OnAccept skips
 //       committed, :1380), so one slot holds either.
-//   * chosen log: one u32 per instance = entry + 1 of the chosen Value, 0 = none
+//   * chosen log: one u16 per instance = index + 1 of the chosen batch's run
+//       among its bucket's chosen fragments (cf_off), 0 = none; stored as
+//       row N of the state array so k_store streams both alike
 #pragma once
 #include <cstdint>
 #include <cstddef>
@@ -172,7 +174,7 @@ struct DevView {
     // state
     slot_t *st;                     // one 2-byte slot per (node, instance), node-major
     uint8_t *st_valid;              // per (node, bucket): node * NB + bucket
-    uint32_t *chosen;               // per instance: entry + 1
+    slot_t *chosen;                 // per instance: the bucket's chosen fragment (cf_off) + 1; row N of st
     uint8_t *chosen_valid;          // per bucket
     uint32_t *plan;                 // (N + 1) * NB: the value k_store writes over a whole (row, bucket),
                                     // rows 0..N-1 state, row N chosen log; PLAN_SKIP = not by k_store
