@@ -571,7 +571,7 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // Per slot only the fragment that fixes its final state matters: the first
 // COMMIT covering it (first commit wins, multi/paxos.cpp:1515, and later
 // accepts skip committed slots, :1380), else the last granted ACCEPT (:1387).
-// The slot is written as that fragment's index — 4 bytes, no Value load
+// The slot is written as that fragment's pair-local index + 1 — 2 bytes, no Value load
 // (mpx_internal.hpp).
 //
 // Lane p < G*N owns pair (bucket b0 + p / N, node p % N); pairs are
@@ -978,16 +978,15 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
 }
 
 // Streams the plan: a wave takes a chunk of C whole buckets of one row — a
-// state row (2-byte slots: 512 B per bucket) or the chosen log (4-byte
-// entries: 1 KiB per bucket) — and writes it contiguously, one non-temporal
+// state row or the chosen log (row N), 2-byte slots, 512 B per bucket — and
+// writes it contiguously, one non-temporal
 // store per lane per bucket, 4 slots per lane.  The chunk's plan words are
 // loaded one chunk ahead and the inner loop has no branch — a PLAN_SKIP
 // bucket's store goes to a scratch sink — so the only wait per chunk is for
 // that one load, with the previous chunk's C stores still in flight (vmcnt
 // counts stores on gfx9: a data-dependent store count would force a full drain
-// instead).  A wave walks chunks c = wid, wid + nwaves, ... over the state rows
-// and then the chosen-log row; buckets past the last whole chunk of a row take
-// a plain tail loop.
+// instead).  A wave walks chunks c = wid, wid + nwaves, ... over the N + 1
+// rows; buckets past the last whole chunk of a row take a plain tail loop.
 template <uint32_t C, bool NT, typename T, typename V>
 __device__ inline uint64_t store_chunks(const DevView &v, uint64_t c, const uint64_t c_base, const uint64_t c_end,
                                         const uint64_t cpr, const uint32_t prow0, T *const base0, const uint64_t stride,
