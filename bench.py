@@ -18,7 +18,7 @@ roofline: the dominant unit is the apply phase — k_plan (one thread per
 the slots and the chosen log) and k_apply_fast's per-slot pairs (none in C4:
 it exits at once) — bracketed by HIP events on the engine's stream; k_store is
 most of it (profiles/).  achieved = the phase's compulsory bytes (DESIGN.md
-§4: one 2-byte state slot written per (acceptor, instance), one 2-byte
+§4: one 1-byte state slot written per (acceptor, instance), one 1-byte
 chosen-log entry per instance, one 16-byte fragment descriptor read per
 (acceptor, bucket, message), and the 4-byte plan word per (row, bucket) written
 and read back — a slot names the message run that fixed it, whose entry in the
@@ -227,10 +227,11 @@ def main():
     apply_mean = sum(apply_ms) / max(len(apply_ms), 1)
     bytes_survey = st["bytes_alg"]                  # this rank's 16P + 24A + 16L per launch
     L = se - sb
-    # 2-B state slots + 2-B chosen log + the ACCEPT and COMMIT descriptors of every (node, bucket)
+    # 1-B state slots + 1-B chosen log (the device-generated clean trace has 2 runs per pair, so
+    # mpx_load_clean_device picks 1-byte slots) + the ACCEPT and COMMIT descriptors of every (node, bucket)
     # + the plan word of every (row, bucket), written by k_plan and read by k_store
     nb = (L + 255) // 256
-    bytes_min = 2 * N * L + 2 * L + 2 * 16 * N * nb + 2 * 4 * (N + 1) * nb
+    bytes_min = 1 * N * L + 1 * L + 2 * 16 * N * nb + 2 * 4 * (N + 1) * nb
     achieved = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
     pmc = latest_pmc(N, M, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None

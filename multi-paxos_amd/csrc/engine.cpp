@@ -222,7 +222,11 @@ static int finish_view(mpx_engine *e)
     v.shard_begin = e->cfg.shard_begin;
     v.shard_len = e->shard_len;
     v.num_msgs = e->num_msgs;
-    TRY(e->st.alloc((size_t)(N + 1) * e->shard_len * sizeof(slot_t)));   // row N: the chosen log
+    // slot width: 1 byte when every pair / bucket has few enough fragments for a
+    // 1-byte pair-local index (set by the trace loader), MPX_SLOT_BYTES=2 forces 2
+    if (const char *x = std::getenv("MPX_SLOT_BYTES")) if (std::atoi(x) == 2) v.slot_w = 2;
+    if (v.slot_w != 1) v.slot_w = 2;
+    TRY(e->st.alloc((size_t)(N + 1) * e->shard_len * v.slot_w));   // row N: the chosen log
     TRY(e->st_valid.alloc((size_t)N * e->NB));
     TRY(e->chosen_valid.alloc(e->NB));
     TRY(e->plan.alloc((size_t)(N + 1) * e->NB * 4));
@@ -242,10 +246,9 @@ static int finish_view(mpx_engine *e)
     if (!e->out_cap) e->out_cap = 1 << 16;
     TRY(e->out.alloc(e->out_cap * sizeof(OutRec)));
     TRY(e->node_scal.alloc(16ull * N));
-    v.st = e->st.as<slot_t>();
+    v.st = e->st.p;
     v.st_valid = e->st_valid.as<uint8_t>();
-    v.chosen = e->st.as<slot_t>() + (size_t)N * e->shard_len;
-    v.chosen_valid = e->chosen_valid.as<uint8_t>();
+        v.chosen_valid = e->chosen_valid.as<uint8_t>();
     v.plan = e->plan.as<uint32_t>();
     v.fast_rest = e->fast_rest.as<uint32_t>();
     v.store_dummy = e->store_dummy.as<uint32_t>();
@@ -321,6 +324,12 @@ static int upload_trace(mpx_engine *e)
     v.b_rep_off = e->b_rep_off.as<uint64_t>(); v.b_rep = e->b_rep.as<uint32_t>();
     v.b_chosen = e->b_chosen.as<uint32_t>();
     v.cf_off = e->cf_off.as<uint64_t>(); v.cfrags = e->cfrags.as<Frag>();
+    {
+        uint64_t mx = 0;
+        for (size_t i = 0; i + 1 < h.f_off.size(); ++i) mx = std::max<uint64_t>(mx, h.f_off[i + 1] - h.f_off[i]);
+        for (size_t i = 0; i + 1 < h.cf_off.size(); ++i) mx = std::max<uint64_t>(mx, h.cf_off[i + 1] - h.cf_off[i]);
+        v.slot_w = mx <= MAX_PAIR_FRAGS_1 ? 1 : 2;
+    }
     TRY(finish_view(e));
     HTRY(hipStreamSynchronize(s));
     e->dirty = false;
@@ -898,6 +907,9 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.b_rep_off = e->b_rep_off.as<uint64_t>(); v.b_rep = e->b_rep.as<uint32_t>();
     v.b_chosen = e->b_chosen.as<uint32_t>();
     v.cf_off = e->cf_off.as<uint64_t>(); v.cfrags = e->cfrags.as<Frag>();
+    // clean geometry, batch = bucket = 256: a pair holds one ACCEPT and one COMMIT run,
+    // a bucket's chosen list one run
+    v.slot_w = 1;
     TRY(finish_view(e));
     for (auto &ns : e->nodes) ns.clear();
     e->vt.clear();

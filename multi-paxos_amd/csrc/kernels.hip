@@ -20,6 +20,30 @@
 
 namespace mpx {
 
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+// slot array access, slot_w bytes per slot (element index i = row * shard_len + li)
+typedef unsigned char u8x4 __attribute__((ext_vector_type(4)));
+__device__ inline uint32_t st_get(const DevView &v, uint64_t i)
+{
+    return v.slot_w == 1 ? (uint32_t)static_cast<const uint8_t *>(v.st)[i] : (uint32_t)static_cast<const uint16_t *>(v.st)[i];
+}
+__device__ inline void st_put(const DevView &v, uint64_t i, uint32_t x)
+{
+    if (v.slot_w == 1) static_cast<uint8_t *>(v.st)[i] = (uint8_t)x;
+    else static_cast<uint16_t *>(v.st)[i] = (uint16_t)x;
+}
+// four consecutive slots i..i+3 (i a multiple of 4), non-temporal
+__device__ inline void st_put4(const DevView &v, uint64_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    if (v.slot_w == 1)
+        __builtin_nontemporal_store(u8x4{(uint8_t)a, (uint8_t)b, (uint8_t)c, (uint8_t)d},
+                                    reinterpret_cast<u8x4 *>(static_cast<uint8_t *>(v.st) + i));
+    else
+        __builtin_nontemporal_store(u16x4{(uint16_t)a, (uint16_t)b, (uint16_t)c, (uint16_t)d},
+                                    reinterpret_cast<u16x4 *>(static_cast<uint16_t *>(v.st) + i));
+}
+
+
 __device__ inline void record_violation(const DevView &v, uint64_t code, uint64_t node, uint64_t seq, uint64_t iid)
 {
     atomicAdd(&v.viol->count, 1ull);
@@ -517,7 +541,7 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
 #pragma unroll
         for (uint32_t j = 0; j < SPL; ++j) {
             const uint64_t li = li0 + lane + 64 * j;
-            if (li < v.shard_len) v.chosen[li] = (slot_t)cv[j];
+            if (li < v.shard_len) st_put(v, (uint64_t)v.N * v.shard_len + li, cv[j]);
         }
         if (lane == 0) v.chosen_valid[b] = 1;
     }
@@ -540,10 +564,10 @@ __device__ inline void decode_slot(const DevView &v, uint32_t q, uint32_t s, uin
     word = W_PRESENT | ((f.flags >> 4) == K_COMMIT ? W_COMMITTED : 0) | v.e_val[ent];
 }
 
-// the stored 2-byte slot of (node, shard index li) as a global fragment index + 1
+// the stored slot of (node, shard index li) as a global fragment index + 1
 __device__ inline uint32_t slot_global(const DevView &v, uint32_t node, uint64_t li)
 {
-    const uint32_t s = v.st[(uint64_t)node * v.shard_len + li];
+    const uint32_t s = st_get(v, (uint64_t)node * v.shard_len + li);
     return s ? (uint32_t)(v.f_off[(li >> BSH) * v.N + node] + s) : 0;
 }
 
@@ -599,7 +623,6 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // ACCEPT / COMMIT runs and its node has no PREPARE after the first of them —
 // its snapshot events see empty state, so skipping them changes no output.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t FAST_PAIR_FRAGS = 2;      // descriptors a pair lane prefetches
 __host__ __device__ inline uint32_t fast_group(uint32_t N, uint32_t cap = 4)
 {
@@ -726,21 +749,21 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         // uniform pairs, node-major so each row gets its G buckets back to back
         const bool whole = (b0 + nb) * BS <= v.shard_len;
         for (uint32_t n = 0; n < N; ++n) {
-            slot_t *row = v.st + (uint64_t)n * v.shard_len + b0 * BS;
+            const uint64_t row = (uint64_t)n * v.shard_len + b0 * BS;
             for (uint32_t g = 0; g < nb; ++g) {
                 const uint32_t p = g * N + n;
                 if (!((uni_m >> p) & 1)) continue;
                 if (AFTER_STORE && (b0 + g + 1) * BS <= v.shard_len) continue;
                 const uint32_t q = rl32(qv, p);
-                const slot_t sq = (slot_t)rl32(ql, p);
+                const uint32_t sq = rl32(ql, p);
                 if (v.knobs & 16) {
                     // experiment: no state stores
                 } else if (whole) {
-                    __builtin_nontemporal_store(u16x4{sq, sq, sq, sq}, reinterpret_cast<u16x4 *>(row + g * BS + s0));
+                    st_put4(v, row + g * BS + s0, sq, sq, sq, sq);
                 } else {
 #pragma unroll
                     for (uint32_t j = 0; j < SPL; ++j)
-                        if ((b0 + g) * BS + s0 + j < v.shard_len) row[g * BS + s0 + j] = sq;
+                        if ((b0 + g) * BS + s0 + j < v.shard_len) st_put(v, row + g * BS + s0 + j, sq);
                 }
                 if (DIGEST)
 #pragma unroll
@@ -825,19 +848,19 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
                 }
             }
             if (__ballot(bad) && lane == 0) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, ib);
-            slot_t *srow = v.st + (uint64_t)n * v.shard_len + li0;
+            const uint64_t srow = (uint64_t)n * v.shard_len + li0;
             const uint64_t pbase = f_base + f0;        // the pair's first fragment
-            const slot_t l0 = q0 ? (slot_t)(q0 - pbase) : 0, l1 = q1 ? (slot_t)(q1 - pbase) : 0,
-                         l2 = q2 ? (slot_t)(q2 - pbase) : 0, l3 = q3 ? (slot_t)(q3 - pbase) : 0;
+            const uint32_t l0 = q0 ? (uint32_t)(q0 - pbase) : 0, l1 = q1 ? (uint32_t)(q1 - pbase) : 0,
+                           l2 = q2 ? (uint32_t)(q2 - pbase) : 0, l3 = q3 ? (uint32_t)(q3 - pbase) : 0;
             if (v.knobs & 16) {
                 // experiment: no state stores
             } else if (li0 + BS <= v.shard_len) {
-                __builtin_nontemporal_store(u16x4{l0, l1, l2, l3}, reinterpret_cast<u16x4 *>(srow + s0));
+                st_put4(v, srow + s0, l0, l1, l2, l3);
             } else {
-                if (li0 + s0 < v.shard_len) srow[s0] = l0;
-                if (li0 + s0 + 1 < v.shard_len) srow[s0 + 1] = l1;
-                if (li0 + s0 + 2 < v.shard_len) srow[s0 + 2] = l2;
-                if (li0 + s0 + 3 < v.shard_len) srow[s0 + 3] = l3;
+                if (li0 + s0 < v.shard_len) st_put(v, srow + s0, l0);
+                if (li0 + s0 + 1 < v.shard_len) st_put(v, srow + s0 + 1, l1);
+                if (li0 + s0 + 2 < v.shard_len) st_put(v, srow + s0 + 2, l2);
+                if (li0 + s0 + 3 < v.shard_len) st_put(v, srow + s0 + 3, l3);
             }
             if (DIGEST)
                 dig += slot_digest(v, n, ib + s0, q0) + slot_digest(v, n, ib + s0 + 1, q1) +
@@ -852,7 +875,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             const uint32_t g = (uint32_t)__builtin_ctzll(m);
             const uint64_t li0 = (b0 + g) << BSH;
             // the bucket's only chosen fragment: local index 0, stored + 1
-            __builtin_nontemporal_store(u16x4{1, 1, 1, 1}, reinterpret_cast<u16x4 *>(v.chosen + li0 + s0));
+            st_put4(v, (uint64_t)N * v.shard_len + li0 + s0, 1, 1, 1, 1);
             cC += SPL;
             if (DIGEST) {
                 const uint64_t c0 = rl64(ce, g), ib = v.shard_begin + li0;
@@ -1026,7 +1049,7 @@ __device__ inline uint64_t store_chunks(const DevView &v, uint64_t c, const uint
     return c;
 }
 
-template <uint32_t C, bool NT = true>
+template <uint32_t C, bool NT, typename T, typename V>
 __global__ __launch_bounds__(256) void k_store(DevView v)
 {
     // wave-uniform chunk walk in scalar registers (readfirstlane): the row
@@ -1040,16 +1063,16 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
     const uint64_t wid = xcd_wave_id(wv, v.knobs);
     const uint32_t s0 = 4 * lane;
     uint32_t *const sink = v.store_dummy + (wid & 63) * BS;
-    store_chunks<C, NT, slot_t, u16x4>(v, wid, 0, S, cpr, 0, v.st, v.shard_len, 0,
-                                       reinterpret_cast<slot_t *>(sink) + s0, nwaves);
+    T *const st = static_cast<T *>(v.st);
+    store_chunks<C, NT, T, V>(v, wid, 0, S, cpr, 0, st, v.shard_len, 0, reinterpret_cast<T *>(sink) + s0, nwaves);
     // tail: the whole buckets after each row's last full chunk
     const uint64_t tpr = whole - cpr * C, tails = (uint64_t)(N + 1) * tpr;
     for (uint64_t t = wid; t < tails; t += nwaves) {
         const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
         const uint32_t q = v.plan[r * NB + b];
         if (q == PLAN_SKIP) continue;
-        const slot_t x = (slot_t)q;
-        __builtin_nontemporal_store(u16x4{x, x, x, x}, reinterpret_cast<u16x4 *>(v.st + r * v.shard_len + (b << BSH) + s0));
+        const T x = (T)q;
+        __builtin_nontemporal_store(V{x, x, x, x}, reinterpret_cast<V *>(st + r * v.shard_len + (b << BSH) + s0));
     }
 }
 
@@ -1316,7 +1339,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 #pragma unroll
             for (uint32_t j = 0; j < SPL; ++j) {
                 const uint64_t li = li0 + lane + 64 * j;
-                if (li < v.shard_len) v.st[(uint64_t)n * v.shard_len + li] = sm[j] ? (slot_t)(sm[j] - pbase) : 0;
+                if (li < v.shard_len) st_put(v, (uint64_t)n * v.shard_len + li, sm[j] ? (uint32_t)(sm[j] - pbase) : 0);
                 if (sw[j])
                     if (v.digest) dig += state_digest(n, v.shard_begin + li, (sw[j] & W_COMMITTED) ? 2 : 1, sb[j], sw[j] & W_HANDLE);
             }
@@ -1442,7 +1465,7 @@ __global__ __launch_bounds__(256) void k_decode(DevView v, uint32_t node, uint64
     const uint64_t li = l0 + i;
     uint64_t b = 0, w = 0;
     if (node >= v.N) {
-        const uint32_t c = v.chosen_valid[li >> BSH] ? v.chosen[li] : 0;
+        const uint32_t c = v.chosen_valid[li >> BSH] ? st_get(v, (uint64_t)v.N * v.shard_len + li) : 0;
         if (c) {
             // the bucket's chosen fragment c - 1 and its entry at this slot
             const Frag f = v.cfrags[v.cf_off[li >> BSH] + c - 1];
@@ -1598,12 +1621,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
         else if (!(v.knobs & 64) && v.N <= FAST_MAX_NODES) {
             // plan + stream, then the per-slot pairs (knob 64: the one-kernel form)
             hipLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s, v, g.apply_wgs);
-            switch ((v.knobs >> 12) & 3) {   // chunk size A/B (tools/ab_apply.py)
-            case 1: hipLaunchKernelGGL(k_store<16>, dim3(g.store_wgs), dim3(256), 0, s, v); break;
-            case 2: hipLaunchKernelGGL(k_store<48>, dim3(g.store_wgs), dim3(256), 0, s, v); break;
-            case 3: hipLaunchKernelGGL((k_store<32, false>), dim3(g.store_wgs), dim3(256), 0, s, v); break;
-            default: hipLaunchKernelGGL(k_store<32>, dim3(g.store_wgs), dim3(256), 0, s, v); break;
-            }
+            if (v.slot_w == 1) hipLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
+            else hipLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
             hipLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
         } else switch (g.variant) {
         case 1: hipLaunchKernelGGL((k_apply_fast<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;

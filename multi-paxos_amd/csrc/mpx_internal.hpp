@@ -11,7 +11,7 @@
 //     256-instance bucket, listed per pair in processing order (CSR); pairs are
 //     bucket-major, q = bucket * N + node, so one wave can walk a bucket's
 //     nodes and reuse the shared Values
-//   * state: one 2-byte slot per (node, instance) = fragment + 1 counted from
+//   * state: one 1- or 2-byte slot (slot_w) per (node, instance) = fragment + 1 counted from
 //       the pair's first fragment (f_off[bucket * N + node]), 0 = empty:
 //       the message run (fragment) that fixed the slot.  Its message's type
 //       says accepted or committed, its header ballot is the tag (multi;
@@ -21,7 +21,7 @@
 //       {ballot, word}.  Accepted and committed entries of a node are disjoint
 //       (OnCommit erases accepted_values_, multi/paxos.cpp:1501; OnAccept skips
 //       committed, :1380), so one slot holds either.
-//   * chosen log: one u16 per instance = index + 1 of the chosen batch's run
+//   * chosen log: one slot per instance = index + 1 of the chosen batch's run
 //       among its bucket's chosen fragments (cf_off), 0 = none; stored as
 //       row N of the state array so k_store streams both alike
 #pragma once
@@ -53,6 +53,7 @@ constexpr uint64_t MAX_ENTRIES = 0xFFFFFFFEull;
 constexpr uint64_t MAX_FRAGS = 0xFFFFFFFEull;
 // 2-byte state slots hold the pair-local fragment index + 1
 constexpr uint64_t MAX_PAIR_FRAGS = 0xFFFEull;
+constexpr uint64_t MAX_PAIR_FRAGS_1 = 0xFEull;   // 1-byte slots when every pair fits
 typedef uint16_t slot_t;
 
 // m_flags bits, written by the header scan / proposer kernels
@@ -172,9 +173,10 @@ struct DevView {
     const uint64_t *cf_off;         // NB+1
     const Frag *cfrags;
     // state
-    slot_t *st;                     // one 2-byte slot per (node, instance), node-major
+    void *st;                       // one slot per (node, instance), node-major, slot_w bytes each
+    uint32_t slot_w;                // 1 when every pair / bucket has <= MAX_PAIR_FRAGS_1 fragments, else 2
     uint8_t *st_valid;              // per (node, bucket): node * NB + bucket
-    slot_t *chosen;                 // per instance: the bucket's chosen fragment (cf_off) + 1; row N of st
+    // chosen log: row N of st (per instance: the bucket's chosen fragment (cf_off) + 1)
     uint8_t *chosen_valid;          // per bucket
     uint32_t *plan;                 // (N + 1) * NB: the value k_store writes over a whole (row, bucket),
                                     // rows 0..N-1 state, row N chosen log; PLAN_SKIP = not by k_store

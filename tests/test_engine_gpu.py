@@ -81,6 +81,33 @@ def test_engine_matches_reference_golden(name):
 
 
 # (9, 256 * 70 + 100): k_store's full 32-bucket chunks, its tail buckets and a partial last bucket
+@pytest.mark.parametrize("name", ["fuzz_big_0", "fuzz_big_1", "hm_commit_tags", "hm_promise_merge", "c2_clean_n9_b100", "c5_member_0", "demo5_s3",
+                                  "c3_faulty_0", "mm_aggregate"])
+def test_two_byte_slots_match(name, monkeypatch):
+    """Traces whose pairs all fit 1-byte slots run with 2-byte slots too when
+    forced (MPX_SLOT_BYTES=2): the same result bytes on both apply paths."""
+    if name not in INDEX:
+        pytest.skip("no golden " + name)
+    monkeypatch.setenv("MPX_SLOT_BYTES", "2")
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxr")
+    with mpx.Engine.for_trace(trace) as e:
+        st = e.run()
+        got = e.dump()
+        assert got == want, mpxr.diff(got, want)
+        _step_path(e, want, st)
+
+
+def test_wide_pairs_take_two_byte_slots():
+    """Batch 1: a pair holds up to 512 runs (> 254), so the engine switches to
+    2-byte slots by itself; result bytes still equal the oracle's."""
+    t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=3, num_instances=700, batch=1)
+    want, ostats, _ = oracle_run(t)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        assert e.dump() == want
+        _step_path(e, want, st)
+
+
 @pytest.mark.parametrize("n,m,b", [(5, 4096, 256), (3, 1000, 100), (7, 5000, 37), (1, 10, 256), (64, 300, 256),
                                    (9, 256 * 70 + 100, 256)])
 def test_engine_matches_oracle_clean(n, m, b):
