@@ -1076,6 +1076,61 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
     }
 }
 
+// 1-byte slots: a 256-B bucket row is too small a unit for one wave store, so
+// a wave takes a chunk of 64 whole buckets (16 KiB of one row) and writes it as
+// 16 contiguous KiB-stores: lane l of store j covers bytes 16l..16l+15 of
+// buckets 4j..4j+3, its plan word fetched with a cross-lane shuffle (LDS
+// permute, lgkmcnt) from the chunk's 64 plan words, which are loaded one chunk
+// ahead as in k_store (the loop waits vmcnt(16): the previous chunk's stores
+// stay in flight).  Tail buckets of a row go through the per-bucket loop.
+template <bool NT>
+__global__ __launch_bounds__(256) void k_store8(DevView v)
+{
+    constexpr uint32_t C = 64;
+    const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t N = v.N;
+    const uint64_t NB = v.NB;
+    const uint64_t whole = v.shard_len >> BSH;
+    const uint64_t cpr = whole / C, S = (uint64_t)(N + 1) * cpr;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    const uint64_t wid = xcd_wave_id(wv, v.knobs);
+    uint8_t *const st = static_cast<uint8_t *>(v.st);
+    uint8_t *const sink = reinterpret_cast<uint8_t *>(v.store_dummy) + (wid & 63) * 1024 + 16 * lane;
+    if (wid < S) {
+        uint32_t rn = (uint32_t)(wid / cpr), kn = (uint32_t)(wid - (uint64_t)rn * cpr);
+        const uint32_t step_r = (uint32_t)(nwaves / cpr), step_k = (uint32_t)(nwaves - (uint64_t)step_r * cpr);
+        auto ptr = [&](uint64_t cc, uint32_t rr, uint32_t kk) -> const uint32_t * {
+            return v.plan + (cc < S ? (uint64_t)rr * NB + (uint64_t)kk * C : 0) + lane;
+        };
+        uint32_t qn = *ptr(wid, rn, kn);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        for (uint64_t c = wid; c < S; c += nwaves) {
+            const uint32_t qw = qn, rc = rn, kc = kn;
+            rn += step_r; kn += step_k;
+            if (kn >= cpr) { kn -= (uint32_t)cpr; ++rn; }
+            qn = *ptr(c + nwaves, rn, kn);
+            uint8_t *const base = st + (uint64_t)rc * v.shard_len + ((uint64_t)kc * C << BSH) + 16 * lane;
+#pragma unroll
+            for (uint32_t j = 0; j < C / 4; ++j) {
+                const uint32_t q = (uint32_t)__shfl((int)qw, (int)(4 * j + (lane >> 4)), 64);
+                const uint32_t x = (q & 0xFF) * 0x01010101u;
+                uint8_t *const dst = q == PLAN_SKIP ? sink : base + 1024 * j;
+                if (NT) __builtin_nontemporal_store(u32x4{x, x, x, x}, reinterpret_cast<u32x4 *>(dst));
+                else *reinterpret_cast<u32x4 *>(dst) = u32x4{x, x, x, x};
+            }
+        }
+    }
+    const uint32_t s0 = 4 * lane;
+    const uint64_t tpr = whole - cpr * C, tails = (uint64_t)(N + 1) * tpr;
+    for (uint64_t t = wid; t < tails; t += nwaves) {
+        const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
+        const uint32_t q = v.plan[r * NB + b];
+        if (q == PLAN_SKIP) continue;
+        const uint8_t x = (uint8_t)q;
+        __builtin_nontemporal_store(u8x4{x, x, x, x}, reinterpret_cast<u8x4 *>(st + r * v.shard_len + (b << BSH) + s0));
+    }
+}
+
 // General apply: one wave owns one (node, bucket) pair of the host-built work
 // list at a time, its 256 instance slots 4 per lane.  The pair's fragments and
 // the node's snapshot events are walked in message order, so every instance
@@ -1621,7 +1676,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
         else if (!(v.knobs & 64) && v.N <= FAST_MAX_NODES) {
             // plan + stream, then the per-slot pairs (knob 64: the one-kernel form)
             hipLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s, v, g.apply_wgs);
-            if (v.slot_w == 1) hipLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
+            if (v.slot_w == 1 && (v.knobs & 128)) hipLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
+            else if (v.slot_w == 1) hipLaunchKernelGGL(k_store8<true>, dim3(g.store_wgs), dim3(256), 0, s, v);
             else hipLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
             hipLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
         } else switch (g.variant) {
