@@ -939,7 +939,8 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
 #pragma unroll
         for (uint32_t k = 0; k < F; ++k) w[k] = k < len ? frag_w1(v.frags + oa + k) : (uint64_t)NONE32;
 #pragma unroll
-        for (uint32_t k = 0; k < F; ++k) fg[k] = k < len ? v.m_flags[(uint32_t)w[k]] : 0;
+        for (uint32_t k = 0; k < F; ++k)   // a COMMIT run's scan flag is never read
+            fg[k] = k < len && (w[k] >> 60) != K_COMMIT ? v.m_flags[(uint32_t)w[k]] : 0;
         bool elig = in_list && len <= F, full = true, again = false, comm = false;
         uint32_t fix = NONE32, nA = 0, nL = 0;
 #pragma unroll
