@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void k_scan_node(DevView v)
 template <bool MEMBER>
 __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
 {
-    __shared__ uint64_t l[2][4];
+    __shared__ uint64_t l[2][4], lc[2][4];
     __shared__ uint64_t lba[SCAN_CHUNK];        // phase 2 reads its rounds back from LDS,
     __shared__ uint8_t lty[SCAN_CHUNK];         // so the round loop needs few registers
     __shared__ uint32_t lga[MEMBER ? SCAN_CHUNK : 1];
@@ -238,11 +238,32 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
         lba[lb + 64 * r] = ba[r];
         if (member) lga[lb + 64 * r] = ga[r];
     }
+    // carry-in = max over the node's earlier chunk aggregates (k_scan_chunk),
+    // read here from L2 instead of a separate per-node scan kernel
+    const uint32_t cn = v.chunk_node[c];
+    const uint32_t c0 = v.node_chunk_off[cn], c1 = v.node_chunk_off[cn + 1];
+    uint64_t xp = 0, xs = 0;
+    for (uint32_t k = c0 + threadIdx.x; k < c; k += 256) {
+        const uint64_t ap = v.chunk_agg[2 * k], as = v.chunk_agg[2 * k + 1];
+        xp = xp > ap ? xp : ap;
+        xs = xs > as ? xs : as;
+    }
+    xp = wave_max(xp);
+    xs = wave_max(xs);
     lp = wave_max(lp);
     ls = wave_max(ls);
-    if (lane == 0) { l[0][w] = lp; l[1][w] = ls; }
+    if (lane == 0) { l[0][w] = lp; l[1][w] = ls; lc[0][w] = xp; lc[1][w] = xs; }
     __syncthreads();
-    uint64_t cp = v.chunk_carry[2 * c], cs = v.chunk_carry[2 * c + 1];   // wave-uniform running maxima
+    uint64_t cp = 0, cs = 0;                   // wave-uniform running maxima
+    for (uint32_t i = 0; i < 4; ++i) { cp = cp > lc[0][i] ? cp : lc[0][i]; cs = cs > lc[1][i] ? cs : lc[1][i]; }
+    if (c == c1 - 1 && threadIdx.x == 0) {
+        // the node's last chunk: its promised / max_seen after the whole stream
+        uint64_t tp = cp, ts = cs;
+        for (uint32_t i = 0; i < 4; ++i) { tp = tp > l[0][i] ? tp : l[0][i]; ts = ts > l[1][i] ? ts : l[1][i]; }
+        if (member) { tp &= LOW56; ts &= LOW56; }   // current incarnation
+        v.node_scal[2 * cn] = tp;
+        v.node_scal[2 * cn + 1] = ts;
+    }
     for (uint32_t i = 0; i < w; ++i) { cp = cp > l[0][i] ? cp : l[0][i]; cs = cs > l[1][i] ? cs : l[1][i]; }
     ls = 0;                                    // this lane's max_seen contributions since cs
 #pragma unroll 1
@@ -1503,6 +1524,7 @@ __global__ void k_reset(DevView v, uint32_t n_partials)
     if (i < np) v.st_valid[i] = 0;
     if (i < v.NB) v.chosen_valid[i] = 0;
     if (i < 8ull * n_partials) v.partials[i] = 0;
+    if (i < 2ull * v.N) v.node_scal[i] = 0;    // nodes without messages keep promised = max_seen = 0
     if (i == 0) {
         *v.out_cursor = 0;
         *v.fast_rest = 0;
@@ -1653,12 +1675,13 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
     uint64_t reset_n = (uint64_t)v.N * v.NB;
     if (v.NB > reset_n) reset_n = v.NB;
     if (8ull * n_partials > reset_n) reset_n = 8ull * n_partials;
+    if (2ull * v.N > reset_n) reset_n = 2ull * v.N;
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, s);
     hipLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s, v, n_partials);
     if (v.num_chunks) {
         if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_chunk<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
         else hipLaunchKernelGGL(k_scan_chunk<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
-        hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);
+        if (v.knobs & 1024) hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);   // A/B: old per-node scan
         if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
         else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
     }
