@@ -1099,16 +1099,16 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
 }
 
 // 1-byte slots: a 256-B bucket row is too small a unit for one wave store, so
-// a wave takes a chunk of 64 whole buckets (16 KiB of one row) and writes it as
-// 16 contiguous KiB-stores: lane l of store j covers bytes 16l..16l+15 of
-// buckets 4j..4j+3, its plan word fetched with a cross-lane shuffle (LDS
-// permute, lgkmcnt) from the chunk's 64 plan words, which are loaded one chunk
-// ahead as in k_store (the loop waits vmcnt(16): the previous chunk's stores
-// stay in flight).  Tail buckets of a row go through the per-bucket loop.
-template <bool NT>
+// a wave takes a chunk of C (default 128) whole buckets (C / 4 KiB of one row)
+// and writes it as C / 4 contiguous KiB-stores: lane l of store j covers bytes
+// 16l..16l+15 of buckets 4j..4j+3, its plan word fetched with a cross-lane
+// shuffle (LDS permute, lgkmcnt) from the chunk's plan words (one or two per
+// lane), which are loaded one chunk ahead as in k_store (the loop waits
+// vmcnt(C / 4): the previous chunk's stores stay in flight).  Tail buckets of a row go through the per-bucket loop.
+template <bool NT, uint32_t C = 64>
 __global__ __launch_bounds__(256) void k_store8(DevView v)
 {
-    constexpr uint32_t C = 64;
+    static_assert(C == 64 || C == 128, "one or two plan words per lane");
     const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t N = v.N;
     const uint64_t NB = v.NB;
@@ -1124,17 +1124,18 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
         auto ptr = [&](uint64_t cc, uint32_t rr, uint32_t kk) -> const uint32_t * {
             return v.plan + (cc < S ? (uint64_t)rr * NB + (uint64_t)kk * C : 0) + lane;
         };
-        uint32_t qn = *ptr(wid, rn, kn);
+        uint32_t qn = *ptr(wid, rn, kn), qn1 = C == 128 ? ptr(wid, rn, kn)[64] : 0;
         __builtin_amdgcn_s_waitcnt(0x0F70);
         for (uint64_t c = wid; c < S; c += nwaves) {
-            const uint32_t qw = qn, rc = rn, kc = kn;
+            const uint32_t qw = qn, qw1 = qn1, rc = rn, kc = kn;
             rn += step_r; kn += step_k;
             if (kn >= cpr) { kn -= (uint32_t)cpr; ++rn; }
             qn = *ptr(c + nwaves, rn, kn);
+            if (C == 128) qn1 = ptr(c + nwaves, rn, kn)[64];
             uint8_t *const base = st + (uint64_t)rc * v.shard_len + ((uint64_t)kc * C << BSH) + 16 * lane;
 #pragma unroll
             for (uint32_t j = 0; j < C / 4; ++j) {
-                const uint32_t q = (uint32_t)__shfl((int)qw, (int)(4 * j + (lane >> 4)), 64);
+                const uint32_t q = (uint32_t)__shfl((int)(j < 16 ? qw : qw1), (int)((4 * j + (lane >> 4)) & 63), 64);
                 const uint32_t x = (q & 0xFF) * 0x01010101u;
                 uint8_t *const dst = q == PLAN_SKIP ? sink : base + 1024 * j;
                 if (NT) __builtin_nontemporal_store(u32x4{x, x, x, x}, reinterpret_cast<u32x4 *>(dst));
@@ -1701,7 +1702,9 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
             // plan + stream, then the per-slot pairs (knob 64: the one-kernel form)
             hipLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s, v, g.apply_wgs);
             if (v.slot_w == 1 && (v.knobs & 128)) hipLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
-            else if (v.slot_w == 1) hipLaunchKernelGGL(k_store8<true>, dim3(g.store_wgs), dim3(256), 0, s, v);
+            // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64
+            else if (v.slot_w == 1 && (v.knobs & 2048)) hipLaunchKernelGGL((k_store8<true, 64>), dim3(g.store_wgs), dim3(256), 0, s, v);
+            else if (v.slot_w == 1) hipLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, v);
             else hipLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
             hipLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
         } else switch (g.variant) {
