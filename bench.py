@@ -214,10 +214,15 @@ def main():
     chosen_total = tot["chosen"]
     assert chosen_total == M, "chosen %d != %d instances" % (chosen_total, M)
     assert tot["violations"] == 0
-    # verification, outside the timed region: one digested run vs the closed form
+    # verification, outside the timed region: (1) the state the last TIMED step's kernels
+    # (k_plan + k_store8) wrote, digested by a separate device pass; (2) one digested run
+    want_state, want_chosen = clean_expect(N, sb, se)
+    step_state, step_chosen = eng.state_digest()
+    step_ok = (step_state, step_chosen) == (want_state, want_chosen) and \
+        st["accept_apps"] == N * (se - sb) == st["commit_apps"]
+    assert step_ok, "the timed step's final state differs from the clean trace's closed form"
     chk = eng.run()
     eng.timings()
-    want_state, want_chosen = clean_expect(N, sb, se)
     verified = (chk["state_digest"] == want_state and chk["chosen_digest"] == want_chosen and
                 chk["accept_apps"] == N * (se - sb) == chk["commit_apps"] and chk["chosen"] == se - sb)
     assert verified, "digests / counters differ from the clean trace's closed form"
@@ -266,8 +271,9 @@ def main():
                          "bytes_survey_model_per_launch": bytes_survey,
                          "survey_model_gbps": bytes_survey / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0},
             "cpu_baseline": cpu,
-            "verified": {"digests_vs_closed_form": verified, "state_digest": chk["state_digest"],
-                         "chosen_digest": chk["chosen_digest"]},
+            "verified": {"step_state_digest_vs_closed_form": step_ok, "step_state_digest": step_state,
+                         "step_chosen_digest": step_chosen, "run_digests_vs_closed_form": verified,
+                         "state_digest": chk["state_digest"], "chosen_digest": chk["chosen_digest"]},
             "hbm_gbps_alg_step": bytes_min * world / (dt_max / args.steps) / 1e9,
             "decisions_per_step": chosen_total,
             "run_ms_device": sum(run_ms) / max(len(run_ms), 1),

@@ -238,6 +238,11 @@ int  mpx_read_node_state(mpx_engine *eng, uint32_t node, uint64_t first, uint64_
                          uint64_t *acc_ballot, uint64_t *acc_value,
                          uint64_t *com_ballot, uint64_t *com_value);
 int  mpx_stats_get(mpx_engine *eng, mpx_stats *out);
+/* Order-independent digests (the mpx_stats.state_digest / chosen_digest
+ * definitions) of the acceptor/learner state and chosen log the last run OR
+ * step left in HBM, computed by a separate device pass.  mpx_step carries no
+ * digest code, so this is how a caller verifies what the timed kernels wrote. */
+int  mpx_state_digest(mpx_engine *eng, uint64_t *state_digest, uint64_t *chosen_digest);
 int  mpx_last_violation(mpx_engine *eng, mpx_violation *out);
 /* Canonical result dump (format "MPXR"): the byte format
  * the CPU oracle and the reference driver also write, so parity is a

@@ -222,6 +222,10 @@ static int finish_view(mpx_engine *e)
     v.shard_begin = e->cfg.shard_begin;
     v.shard_len = e->shard_len;
     v.num_msgs = e->num_msgs;
+    v.scan_node_pass = 0;
+    for (size_t n = 0; n + 1 < e->ht.node_chunk_off.size(); ++n)
+        if (e->ht.node_chunk_off[n + 1] - e->ht.node_chunk_off[n] > SCAN_INLINE_CHUNKS) v.scan_node_pass = 1;
+    if (const char *x = std::getenv("MPX_SCAN_NODE_PASS")) v.scan_node_pass = std::atoi(x) ? 1 : 0;
     // slot width: 1 byte when every pair / bucket has few enough fragments for a
     // 1-byte pair-local index (set by the trace loader), MPX_SLOT_BYTES=2 forces 2
     if (const char *x = std::getenv("MPX_SLOT_BYTES")) if (std::atoi(x) == 2) v.slot_w = 2;
@@ -578,6 +582,22 @@ extern "C" int mpx_stats_get(mpx_engine *e, mpx_stats *out)
 {
     if (!e || !out) return MPX_E_INVAL;
     *out = e->stats;
+    return MPX_OK;
+}
+
+extern "C" int mpx_state_digest(mpx_engine *e, uint64_t *state_digest, uint64_t *chosen_digest)
+{
+    if (!e || !state_digest || !chosen_digest) return MPX_E_INVAL;
+    if (!e->st.p) return MPX_E_STATE;
+    HTRY(hipSetDevice(e->device));
+    TRY(e->exec_aux.alloc(std::max<size_t>(e->exec_aux.bytes, 16)));
+    unsigned long long *aux = e->exec_aux.as<unsigned long long>();
+    if (launch_state_digest(e->view, e->stream, aux) != 0) return MPX_E_HIP;
+    unsigned long long d[2] = {0, 0};
+    HTRY(hipMemcpyAsync(d, aux, 16, hipMemcpyDeviceToHost, e->stream));
+    HTRY(hipStreamSynchronize(e->stream));
+    *state_digest = d[0];
+    *chosen_digest = d[1];
     return MPX_OK;
 }
 

@@ -240,13 +240,19 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
     }
     // carry-in = max over the node's earlier chunk aggregates (k_scan_chunk),
     // read here from L2 instead of a separate per-node scan kernel
+    // — O(chunks^2) per node, so a node with more than SCAN_INLINE_CHUNKS
+    // chunks reads the carry k_scan_node computed instead (v.scan_node_pass)
     const uint32_t cn = v.chunk_node[c];
     const uint32_t c0 = v.node_chunk_off[cn], c1 = v.node_chunk_off[cn + 1];
     uint64_t xp = 0, xs = 0;
-    for (uint32_t k = c0 + threadIdx.x; k < c; k += 256) {
-        const uint64_t ap = v.chunk_agg[2 * k], as = v.chunk_agg[2 * k + 1];
-        xp = xp > ap ? xp : ap;
-        xs = xs > as ? xs : as;
+    if (v.scan_node_pass) {
+        if (threadIdx.x == 0) { xp = v.chunk_carry[2 * c]; xs = v.chunk_carry[2 * c + 1]; }
+    } else {
+        for (uint32_t k = c0 + threadIdx.x; k < c; k += 256) {
+            const uint64_t ap = v.chunk_agg[2 * k], as = v.chunk_agg[2 * k + 1];
+            xp = xp > ap ? xp : ap;
+            xs = xs > as ? xs : as;
+        }
     }
     xp = wave_max(xp);
     xs = wave_max(xs);
@@ -1562,6 +1568,49 @@ __global__ __launch_bounds__(256) void k_decode(DevView v, uint32_t node, uint64
     out[2 * i + 1] = w;
 }
 
+// Order-independent digests of the state the last run / step left in HBM
+// (mpx_state_digest): every (node, instance) slot decoded as k_decode does,
+// plus the chosen log.  The timed step carries no digest code; this pass
+// verifies what its kernels (k_plan + k_store8, or k_apply) wrote, at any size.
+__global__ __launch_bounds__(256) void k_state_digest(DevView v, unsigned long long *out)
+{
+    const uint64_t total = (uint64_t)(v.N + 1) * v.shard_len;
+    unsigned long long ds = 0, dc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t row = (uint32_t)(i / v.shard_len);
+        const uint64_t li = i - (uint64_t)row * v.shard_len;
+        const uint64_t iid = v.shard_begin + li;
+        if (row < v.N) {
+            if (v.st_valid[(uint64_t)row * v.NB + (li >> BSH)]) ds += slot_digest(v, row, iid, slot_global(v, row, li));
+        } else if (v.chosen_valid[li >> BSH]) {
+            const uint32_t c = st_get(v, (uint64_t)v.N * v.shard_len + li);
+            if (c) {
+                const Frag f = v.cfrags[v.cf_off[li >> BSH] + c - 1];
+                const uint32_t sl = (uint32_t)li & (BS - 1);
+                uint64_t ent = f.entry + (sl - f.start);
+                if (!(f.flags & FR_DENSE))
+                    for (uint32_t k = 0; k < f.count; ++k)
+                        if (v.e_slot[f.entry + k] == sl) { ent = f.entry + k; break; }
+                dc += chosen_digest(iid, v.e_val[ent]);
+            }
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) { ds += __shfl_xor(ds, d, 64); dc += __shfl_xor(dc, d, 64); }
+    if ((threadIdx.x & 63) == 0) {
+        if (ds) atomicAdd(&out[0], ds);
+        if (dc) atomicAdd(&out[1], dc);
+    }
+}
+
+int launch_state_digest(const DevView &v, void *stream, unsigned long long *out)
+{
+    const uint64_t total = (uint64_t)(v.N + 1) * v.shard_len;
+    const uint64_t blocks = total / 256 + 1 < 16384 ? total / 256 + 1 : 16384;
+    if (hipMemsetAsync(out, 0, 16, (hipStream_t)stream) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_state_digest, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, v, out);
+    return (int)hipGetLastError();
+}
+
 // ---- in-order executor: multi/paxos.cpp:1584-1622 applies
 // next_id_to_apply_ forward while the instance is committed, skipping noops
 // (:1601-1606); member/paxos.cpp:1042-1053 the same over learned_.  On the GPU
@@ -1682,7 +1731,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
     if (v.num_chunks) {
         if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_chunk<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
         else hipLaunchKernelGGL(k_scan_chunk<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
-        if (v.knobs & 1024) hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);   // A/B: old per-node scan
+        if (v.scan_node_pass) hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);   // long node streams
         if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
         else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
     }

@@ -41,6 +41,9 @@ namespace mpx {
 constexpr uint32_t BSH = 8;                  // bucket = 256 instances
 constexpr uint32_t BS = 1u << BSH;
 constexpr uint32_t SCAN_CHUNK = 4096;        // header-scan chunk (messages): 16 per thread
+// k_scan_apply re-reduces a node's earlier chunk aggregates inline (O(chunks^2)
+// per node) up to this many chunks per node; longer streams take k_scan_node
+constexpr uint32_t SCAN_INLINE_CHUNKS = 512;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 
 constexpr uint64_t W_PRESENT = 1ull << 63;
@@ -144,7 +147,8 @@ struct DevView {
     const uint64_t *chunk_end;
     const uint32_t *node_chunk_off; // N+1
     uint64_t *chunk_agg;            // 2 per chunk: pmax, smax
-    uint64_t *chunk_carry;          // 2 per chunk: exclusive prefix
+    uint64_t *chunk_carry;          // 2 per chunk: exclusive prefix (k_scan_node)
+    uint32_t scan_node_pass;        // 1: a node has > SCAN_INLINE_CHUNKS chunks, carry-in from k_scan_node
     uint64_t *node_scal;            // 2 per node: promised, max_seen
     // pools
     const uint64_t *e_val;
@@ -237,6 +241,8 @@ int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, ui
 // into aux (2 NB + 2 words: frontier, counts, offsets, total); then with out
 // (total words) the scatter of the executed handles in instance order
 int launch_exec(const DevView &v, void *stream, uint32_t node, unsigned long long *aux, uint64_t *out);
+// digests of the resident state / chosen log -> out[0], out[1] (16 bytes, device)
+int launch_state_digest(const DevView &v, void *stream, unsigned long long *out);
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
                      uint64_t G0, uint64_t G1, uint64_t ballot, uint32_t NB,
                      uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,

@@ -100,6 +100,7 @@ def lib():
             "mpx_read_executed": [vp, ctypes.c_uint32, u64p, u64p, u64p, ctypes.c_uint64],
             "mpx_read_node_state": [vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, u64p, u64p, u64p, u64p],
             "mpx_stats_get": [vp, P(Stats)],
+            "mpx_state_digest": [vp, u64p, u64p],
             "mpx_last_violation": [vp, P(Violation)],
             "mpx_dump_result": [vp, P(u8p), u64p],
             "mpx_value_bytes": [vp, ctypes.c_uint64, u8p, ctypes.c_uint32, P(ctypes.c_uint32)],
@@ -238,6 +239,12 @@ class Engine:
         s = Stats()
         _ck("mpx_stats_get", lib().mpx_stats_get(self.h, ctypes.byref(s)))
         return s.as_dict()
+
+    def state_digest(self):
+        """(state_digest, chosen_digest) of what the last run/step left in HBM (separate device pass)."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _ck("mpx_state_digest", lib().mpx_state_digest(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def violation(self):
         v = Violation()

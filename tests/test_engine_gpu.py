@@ -43,6 +43,8 @@ def _step_path(e, want, st_run):
     e.step()
     e.sync()
     st = e.stats()
+    # what the step's kernels left in HBM, digested by a separate pass
+    assert e.state_digest() == (st_run["state_digest"], st_run["chosen_digest"])
     got = e.dump()
     assert got == want, mpxr.diff(got, want)
     assert [st[k] for k in COUNTERS] == [st_run[k] for k in COUNTERS]
@@ -317,3 +319,71 @@ def test_engine_member_sharded_matches_oracle_restricted(shards):
             assert a["state"] == [s for s in b["state"] if sb <= s[0] < se]
             assert (a["promised"], a["max_seen"]) == (b["promised"], b["max_seen"])
         assert part["chosen"] == [c for c in full["chosen"] if sb <= c[0] < se]
+
+
+def _clean_with_extra_runs(n, m, extra):
+    """A clean batch-256 trace (gen_clean's shape) where node 1 also receives, for
+    each bucket k in `extra`, a partial ACCEPT from proposer 2 at the leader's
+    ballot before the bucket's own ACCEPT (granted, then overwritten) and a partial
+    ACCEPT after its COMMIT (skipped: committed, multi/paxos.cpp:1380) — pairs
+    with more than two runs inside the store chunks, next to uniform ones."""
+    from mpxwire import accept, accept_reply, commit, commit_reply, container, p_batch, p_start, prepare, \
+        prepare_reply, value
+    b0 = 1 << 16
+    s0 = [p_start(b0), prepare(0, b0)] + [prepare_reply(i, b0) for i in range(n)]
+    si = [[prepare(0, b0)] for _ in range(1, n)]
+    for k in range((m + 255) // 256):
+        ent = [(i, value(0, i + 1, str(i))) for i in range(256 * k, min(m, 256 * k + 256))]
+        acc, com = accept(0, k + 1, b0, ent), commit(0, k + 1, b0, ent)
+        s0 += [p_batch(k + 1, ent), acc] + [accept_reply(i, b0, k + 1) for i in range(n)] + [com] + \
+            [commit_reply(i, k + 1) for i in range(n)]
+        for j in range(1, n):
+            if j == 1 and k in extra:
+                part = [(i, value(2, 10 ** 6 + i, "x%d" % i)) for i in range(256 * k + 10, 256 * k + 50)]
+                si[j - 1] += [accept(2, 7000 + k, b0, part), acc, com, accept(2, 8000 + k, b0, part)]
+            else:
+                si[j - 1] += [acc, com]
+    return container([s0] + si, m)
+
+
+@pytest.mark.parametrize("extra", [(), (3, 70, 100, 127, 200, 300)])
+def test_store_chunks_tails_and_partial_pairs(extra):
+    """1-byte slots with two whole 128-bucket store chunks per row, 70 tail buckets and a
+    partial last bucket; optionally pairs of 4 runs inside the chunks (plan word
+    PLAN_SKIP in both of a lane's plan words) left to the per-slot path."""
+    n, m = 3, 256 * (2 * 128 + 70) + 100
+    t = _clean_with_extra_runs(n, m, set(extra))
+    want, ostats, _ = oracle_run(t)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        assert e.dump() == want
+        _step_path(e, want, st)
+    assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
+            st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
+
+
+@pytest.mark.parametrize("env", [("MPX_SCAN_NODE_PASS", "1"), ("MPX_KNOBS", "2048")])
+@pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "demo_s0"])
+def test_kept_alternative_paths(name, env, monkeypatch):
+    """The kept alternatives stay correct: the separate per-node scan pass (taken
+    automatically beyond SCAN_INLINE_CHUNKS chunks per node) and 64-bucket k_store8 chunks."""
+    if name not in INDEX:
+        pytest.skip("no golden " + name)
+    monkeypatch.setenv(*env)
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxr")
+    with mpx.Engine.for_trace(trace) as e:
+        st = e.run()
+        assert e.dump() == want
+        _step_path(e, want, st)
+
+
+def test_clean_long_node_stream_scan_node_pass():
+    """A node stream of more than SCAN_INLINE_CHUNKS header-scan chunks takes the
+    k_scan_node pass by itself; the result equals the oracle's either way."""
+    n, m = 2, 320000                         # batch 1: node 0 gets 7 records per instance -> 547 chunks of 4096
+    t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=1)
+    _, ostats, _ = oracle_run(t)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+    assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
+            st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
