@@ -68,7 +68,79 @@ def parse():
     ap.add_argument("--nodes", type=int, default=9, help="acceptors N (C4: 9)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c3-instances", type=int, default=1 << 24, help="C3 general-path leg: M (2^24); 0 = skip")
+    ap.add_argument("--c3-steps", type=int, default=5)
+    ap.add_argument("--c3-only", action="store_true", help="only the C3 leg (profiling)")
     return ap.parse_args()
+
+
+# C3 (BASELINE.json configs[2]): 7 acceptors, 3 competing proposers, the
+# HijackSend fault model of multi/debug.conf.sample:1 (drop 500, dup 1000 per 10^4, delay U[0,500)),
+# batches of U[1,256] instances
+C3 = dict(num_nodes=7, seed=0, batch=256, proposers=3, drop_rate=500, dup_rate=1000, max_delay=500)
+
+
+def c3_leg(args):
+    """The general path on C3: every pair goes through k_apply (multi-ballot promise phases,
+    promise replies with entries, rejects, duplicates, reordering).  The trace is generated
+    and ingested through mpx_submit_trace before timing (host work, reported apart); a step
+    is the same mpx_step the C4 line times.  roofline on SURVEY §8(d)'s bytes
+    (16 P + 24 A + 16 L from the engine's counters) over the apply phase."""
+    m = args.c3_instances
+    t0 = time.perf_counter()
+    trace = mpx.generate_trace(mpx.GEN_FAULTY, num_instances=m, **C3)
+    t_gen = time.perf_counter() - t0
+    hd = mpx.trace_header(trace)
+    trace_bytes = len(trace)
+    eng = mpx.Engine(hd["num_nodes"], 0, max(hd["num_instances"], 1))
+    t0 = time.perf_counter()
+    eng.submit_trace(trace)
+    t_ingest = time.perf_counter() - t0
+    del trace
+    t0 = time.perf_counter()
+    chk = eng.run()                                 # upload + one digested run (verification)
+    t_first = time.perf_counter() - t0
+    eng.timings()
+    for _ in range(2):
+        eng.step()
+    eng.sync()
+    eng.timings()
+    t0 = time.perf_counter()
+    for _ in range(args.c3_steps):
+        eng.step()
+    eng.sync()
+    dt = time.perf_counter() - t0
+    st = eng.stats()
+    ph = eng.timings_detail()
+    step_digests = eng.state_digest()
+    step_ok = step_digests == (chk["state_digest"], chk["chosen_digest"]) and \
+        all(st[k] == chk[k] for k in ("chosen", "promise_entries", "accept_apps", "commit_apps", "violations"))
+    assert step_ok, "C3: the timed step's state differs from the digested run's"
+    assert st["violations"] == 0
+    mean = lambda k: sum(p[k] for p in ph) / max(len(ph), 1)
+    general_ms, fast_ms = mean("general_apply"), mean("fast_apply")
+    apply_ms = general_ms + fast_ms
+    b_alg = 16 * st["promise_entries"] + 24 * st["accept_apps"] + 16 * st["commit_apps"]
+    achieved = b_alg / (apply_ms * 1e-3) / 1e9 if apply_ms else 0.0
+    ms_step = dt / args.c3_steps * 1e3
+    return {
+        "workload": "C3: 2^%d instances x 7 acceptors, 3 competing proposers, drop 5%% / dup 10%% (<=3) / "
+                    "delay U[0,500) (multi/debug.conf.sample:1), batch U[1,256]" % (m.bit_length() - 1),
+        "instances_proposed": m, "instances": hd["num_instances"], "acceptors": hd["num_nodes"],
+        "decisions_per_step": st["chosen"], "ms_per_step": ms_step,
+        "value": st["chosen"] / (ms_step * 1e-3), "unit": "decisions/s",
+        "counters": {k: st[k] for k in ("chosen", "promise_entries", "accept_apps", "commit_apps", "messages")},
+        "phases_ms": {k: mean(k) for k in mpx.Engine.PHASES},
+        "roofline": {"bound": "hbm", "kernel": "apply phase (k_apply: general pairs; k_plan/k_store/k_apply_fast: "
+                                               "clean pairs)",
+                     "bytes_alg_per_launch": b_alg, "bytes_model": "SURVEY §8(d): 16 P + 24 A + 16 L",
+                     "kernel_ms": apply_ms, "general_ms": general_ms, "fast_ms": fast_ms,
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS},
+        "verified": {"step_state_digest_vs_run": step_ok, "state_digest": chk["state_digest"],
+                     "chosen_digest": chk["chosen_digest"]},
+        "host": {"generate_s": t_gen, "ingest_s": t_ingest, "upload_and_first_run_s": t_first,
+                 "trace_bytes": trace_bytes},
+    }
 
 
 def dist_setup(args):
@@ -180,6 +252,9 @@ def cpu_baseline(args, budget_s):
 
 def main():
     args = parse()
+    if args.c3_only:
+        print(json.dumps({"c3": c3_leg(args)}), flush=True)
+        return
     world, rank, local, pg = dist_setup(args)
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
@@ -246,6 +321,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, args.cpu_seconds)
+        c3 = c3_leg(args) if world == 1 and args.c3_instances else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -271,6 +347,7 @@ def main():
                          "bytes_survey_model_per_launch": bytes_survey,
                          "survey_model_gbps": bytes_survey / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0},
             "cpu_baseline": cpu,
+            "c3": c3,
             "verified": {"step_state_digest_vs_closed_form": step_ok, "step_state_digest": step_state,
                          "step_chosen_digest": step_chosen, "run_digests_vs_closed_form": verified,
                          "state_digest": chk["state_digest"], "chosen_digest": chk["chosen_digest"]},

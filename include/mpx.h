@@ -206,6 +206,11 @@ int  mpx_sync(mpx_engine *eng);
  * the previous call: per run the acceptor/learner kernel (k_apply) and the
  * whole run, in milliseconds.  Writes at most `max` pairs, *n = pairs written. */
 int  mpx_timings(mpx_engine *eng, uint32_t max, double *apply_ms, double *run_ms, uint32_t *n);
+/* The same runs/steps split into phases, 5 doubles (ms) per run: whole run,
+ * header scan + promise / vote quorums, plan + store + fast apply (clean
+ * pairs), general apply (k_apply: every other pair), chosen log + counters.
+ * apply_ms of mpx_timings = phases 2 + 3.  Consumes the timings like mpx_timings. */
+int  mpx_timings_detail(mpx_engine *eng, uint32_t max, double *phases, uint32_t *n);
 
 /* ---- outbound ------------------------------------------------------------ */
 /* Replies generated by the acceptor/learner handlers of the last run, in the

@@ -51,7 +51,7 @@ template <typename T> int upload(DevBuf &b, const std::vector<T> &v, hipStream_t
     return MPX_OK;
 }
 
-struct StepEvents { hipEvent_t e[4]; };
+struct StepEvents { hipEvent_t e[5]; };   // launch_run's event points
 
 }  // namespace
 
@@ -371,7 +371,8 @@ static int queue_run(mpx_engine *e, bool digest)
         g.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(np, (uint64_t)e->num_cus * std::atoi(x)));
         if (g.apply_wgs > e->num_cus * 16) g.apply_wgs = e->num_cus * 16;   // partials are sized for 16 per CU
     }
-    int rc = launch_run(e->view, e->stream, g, ev->e[0], ev->e[1], ev->e[2], ev->e[3]);
+    void *evp[5] = {ev->e[0], ev->e[1], ev->e[2], ev->e[3], ev->e[4]};
+    int rc = launch_run(e->view, e->stream, g, evp);
     if (rc) return MPX_E_HIP;
     // the one cross-GPU exchange: every rank's 64-word summary, over RCCL on
     // the same stream, no host synchronisation
@@ -405,8 +406,8 @@ static int collect(mpx_engine *e)
     if (e->ev_used) {
         StepEvents &x = e->ev_pool[e->ev_used - 1];
         float a = 0, r = 0;
-        (void)hipEventElapsedTime(&a, x.e[1], x.e[2]);
-        (void)hipEventElapsedTime(&r, x.e[0], x.e[3]);
+        (void)hipEventElapsedTime(&a, x.e[1], x.e[3]);
+        (void)hipEventElapsedTime(&r, x.e[0], x.e[4]);
         st.apply_ns = (uint64_t)(a * 1e6);
         st.device_ns = (uint64_t)(r * 1e6);
     }
@@ -451,10 +452,27 @@ extern "C" int mpx_timings(mpx_engine *e, uint32_t max, double *apply_ms, double
     uint32_t k = 0;
     for (size_t i = 0; i < e->ev_used && k < max; ++i, ++k) {
         float a = 0, r = 0;
-        (void)hipEventElapsedTime(&a, e->ev_pool[i].e[1], e->ev_pool[i].e[2]);
-        (void)hipEventElapsedTime(&r, e->ev_pool[i].e[0], e->ev_pool[i].e[3]);
+        (void)hipEventElapsedTime(&a, e->ev_pool[i].e[1], e->ev_pool[i].e[3]);
+        (void)hipEventElapsedTime(&r, e->ev_pool[i].e[0], e->ev_pool[i].e[4]);
         if (apply_ms) apply_ms[k] = a;
         if (run_ms) run_ms[k] = r;
+    }
+    *n = k;
+    e->ev_used = 0;
+    return MPX_OK;
+}
+
+extern "C" int mpx_timings_detail(mpx_engine *e, uint32_t max, double *phases, uint32_t *n)
+{
+    if (!e || !n || (max && !phases)) return MPX_E_INVAL;
+    HTRY(hipStreamSynchronize(e->stream));
+    uint32_t k = 0;
+    for (size_t i = 0; i < e->ev_used && k < max; ++i, ++k) {
+        const hipEvent_t *x = e->ev_pool[i].e;
+        float t[5] = {0, 0, 0, 0, 0};
+        (void)hipEventElapsedTime(&t[0], x[0], x[4]);
+        for (int j = 0; j < 4; ++j) (void)hipEventElapsedTime(&t[j + 1], x[j], x[j + 1]);
+        for (int j = 0; j < 5; ++j) phases[5 * k + j] = t[j];
     }
     *n = k;
     e->ev_used = 0;

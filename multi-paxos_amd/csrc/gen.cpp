@@ -41,6 +41,15 @@ void TraceWriter::node(const std::vector<std::string> &msgs)
     while (out.size() % 8) out.push_back('\0');
 }
 
+void TraceWriter::node_raw(const std::string &bytes, const std::vector<uint64_t> &offs)
+{
+    app<uint64_t>(out, offs.size() - 1);
+    app<uint64_t>(out, bytes.size());
+    out.append((const char *)offs.data(), 8 * offs.size());
+    out += bytes;
+    while (out.size() % 8) out.push_back('\0');
+}
+
 // ---- wire encoders ----
 void enc_value(std::string &s, uint32_t proposer, uint64_t value_id, bool noop, const std::string &payload)
 {

@@ -13,6 +13,8 @@ struct TraceWriter {
     std::string out;
     void begin(uint32_t N, uint32_t semantics, uint64_t M, const std::vector<mpx_epoch> &epochs);
     void node(const std::vector<std::string> &msgs);
+    // one node's stream already concatenated: bytes, offs[count + 1] (offs[0] = 0)
+    void node_raw(const std::string &bytes, const std::vector<uint64_t> &offs);
 };
 
 void enc_value(std::string &s, uint32_t proposer, uint64_t value_id, bool noop, const std::string &payload);

@@ -1717,9 +1717,9 @@ int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, ui
     return (int)hipGetLastError();
 }
 
-int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, void *ev_apply0,
-               void *ev_apply1, void *ev_end)
+int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
 {
+    void *ev_begin = ev[0], *ev_apply0 = ev[1], *ev_apply1 = ev[2], *ev_general = ev[3], *ev_end = ev[4];
     hipStream_t s = (hipStream_t)stream_;
     const uint32_t n_partials = g.apply_wgs + g.chosen_wgs;
     uint64_t reset_n = (uint64_t)v.N * v.NB;
@@ -1740,8 +1740,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
     if (ev_apply0) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
     if (v.semantics == MPX_SEM_MEMBER) {
         // member: every pair walks the general kernel (insert semantics, epoch events)
-        if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
+        if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
     } else {
         // multi: the lean kernel also writes the chosen log of clean buckets
         // digest runs (verification) take their own instantiation, so the
@@ -1764,6 +1764,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *ev_begin, vo
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
     }
+    if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, v, n_partials);
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, s);

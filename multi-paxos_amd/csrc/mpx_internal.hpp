@@ -231,8 +231,10 @@ MPX_HD inline uint64_t scalar_digest(uint32_t node, uint64_t promised, uint64_t 
 
 // kernels (kernels.hip); every launcher queues on `stream`, returns hipError_t as int
 struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, variant, store_wgs; };
-int launch_run(const DevView &v, void *stream, LaunchGeom g, void *ev_begin, void *ev_apply0,
-               void *ev_apply1, void *ev_end);
+// ev (hipEvent_t, each may be null): begin, apply phase start (after the header
+// scan / quorum kernels), after the plan / store / fast-apply kernels, after the
+// general k_apply, end
+int launch_run(const DevView &v, void *stream, LaunchGeom g, void *const ev[5]);
 // readback: count slots of node `node` (node >= N: the chosen log) from shard
 // offset l0 -> out, 2 words each {ballot, PRESENT | COMMITTED? | handle}
 // (chosen: {0, PRESENT | handle}); unwritten buckets read as empty

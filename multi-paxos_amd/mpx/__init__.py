@@ -94,6 +94,7 @@ def lib():
             "mpx_submit_trace": [vp, ctypes.c_char_p, ctypes.c_uint64],
             "mpx_run": [vp], "mpx_reset_state": [vp], "mpx_step": [vp], "mpx_sync": [vp],
             "mpx_timings": [vp, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_uint32)],
+            "mpx_timings_detail": [vp, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_uint32)],
             "mpx_drain_sends": [vp, SEND_FN, vp],
             "mpx_read_chosen": [vp, ctypes.c_uint64, ctypes.c_uint64, u64p],
             "mpx_read_node_scalars": [vp, ctypes.c_uint32, u64p, u64p],
@@ -233,6 +234,15 @@ class Engine:
         n = ctypes.c_uint32()
         _ck("mpx_timings", lib().mpx_timings(self.h, max_n, a, r, ctypes.byref(n)))
         return list(a[: n.value]), list(r[: n.value])
+
+    PHASES = ("run", "scan", "fast_apply", "general_apply", "tail")
+
+    def timings_detail(self, max_n=4096):
+        """Per run/step since the last timings call: dict of phase -> ms (mpx_timings_detail)."""
+        a = (ctypes.c_double * (5 * max_n))()
+        n = ctypes.c_uint32()
+        _ck("mpx_timings_detail", lib().mpx_timings_detail(self.h, max_n, a, ctypes.byref(n)))
+        return [dict(zip(self.PHASES, a[5 * i: 5 * i + 5])) for i in range(n.value)]
 
     # results
     def stats(self):

@@ -25,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stdio.h>
+#include <pthread.h>
 
 typedef uint64_t u64;
 typedef uint32_t u32;
@@ -35,21 +36,23 @@ static u32 rd32(const u8 *p) { u32 v; memcpy(&v, p, 4); return v; }
 static u64 rd64(const u8 *p) { u64 v; memcpy(&v, p, 8); return v; }
 
 /* ---- growable byte buffer ------------------------------------------------ */
-typedef struct { u8 *p; size_t n, cap; int oom; } buf_t;
+typedef struct { u8 *p; size_t n, cap; int oom; int ext; } buf_t;   /* ext: p is caller storage, not owned */
 static void bput(buf_t *b, const void *src, size_t n)
 {
     if (b->oom) return;
     if (b->n + n > b->cap) {
         size_t c = b->cap ? b->cap : 256;
         while (c < b->n + n) c *= 2;
-        u8 *q = (u8 *)realloc(b->p, c);
+        u8 *q = (u8 *)(b->ext ? malloc(c) : realloc(b->p, c));
         if (!q) { b->oom = 1; return; }
-        b->p = q; b->cap = c;
+        if (b->ext && b->n) memcpy(q, b->p, b->n);
+        b->p = q; b->cap = c; b->ext = 0;
     }
     memcpy(b->p + b->n, src, n);
     b->n += n;
 }
 static void bput32(buf_t *b, u32 v) { bput(b, &v, 4); }
+static void bfree(buf_t *b) { if (!b->ext) free(b->p); }
 static void bput64(buf_t *b, u64 v) { bput(b, &v, 8); }
 
 /* ---- u64 -> (a,b) open-addressing map, linear probing, backward-shift delete */
@@ -144,6 +147,8 @@ typedef struct { map_t idx; valrec_t *v; size_t n, cap; buf_t bytes; } vtab_t;
 enum { OK = 0, E_INVAL = -1, E_DECODE = -4, E_RANGE = -5, E_VALUE = -9, E_NOMEM = -2 };
 
 /* Parse one Value at p (avail bytes).  Returns bytes used (>0) or <0. */
+/* Parse one Value at p (avail bytes).  Returns bytes used (>0) or <0.
+ * t == NULL: length and handle only (an entry outside the oracle's shard). */
 static long parse_value(vtab_t *t, const u8 *p, size_t avail, u64 *handle)
 {
     if (avail < 13) return E_DECODE;
@@ -151,8 +156,8 @@ static long parse_value(vtab_t *t, const u8 *p, size_t avail, u64 *handle)
     u64 value_id = rd64(p + 4);
     int noop = p[12] != 0;
     size_t used;
-    u8 canon[64];
-    buf_t enc = {0};
+    u8 sbuf[256];
+    buf_t enc = {sbuf, 0, sizeof sbuf, 0, 1};
     size_t exec_from = 0, exec_len = 0;       /* what Execute() would receive */
     if (proposer >= (1u << 14) || value_id >= (1ull << 47)) return E_RANGE;
     bput32(&enc, proposer); bput64(&enc, value_id);
@@ -160,18 +165,18 @@ static long parse_value(vtab_t *t, const u8 *p, size_t avail, u64 *handle)
     if (noop) {
         used = 13;
     } else {
-        if (avail < 14) { free(enc.p); return E_DECODE; }
+        if (avail < 14) { bfree(&enc); return E_DECODE; }
         u8 member = p[13] != 0;
         bput(&enc, &member, 1);
         if (member) {
-            if (avail < 19) { free(enc.p); return E_DECODE; }
+            if (avail < 19) { bfree(&enc); return E_DECODE; }
             u32 id = rd32(p + 14);
             u8 add = p[18] != 0;
             bput32(&enc, id); bput(&enc, &add, 1);
             if (add) {
-                if (avail < 23) { free(enc.p); return E_DECODE; }
+                if (avail < 23) { bfree(&enc); return E_DECODE; }
                 u32 iplen = rd32(p + 19);
-                if (avail < 25 + (size_t)iplen) { free(enc.p); return E_DECODE; }
+                if (avail < 25 + (size_t)iplen) { bfree(&enc); return E_DECODE; }
                 bput32(&enc, iplen); bput(&enc, p + 23, iplen);
                 u8 port[2]; memcpy(port, p + 23 + iplen, 2); bput(&enc, port, 2);
                 used = 25 + iplen;
@@ -181,36 +186,36 @@ static long parse_value(vtab_t *t, const u8 *p, size_t avail, u64 *handle)
             /* multi executes value_.value_ for membership values: the empty
              * string (the membership branch is #if 0, paxos.cpp:1592-1617) */
         } else {
-            if (avail < 18) { free(enc.p); return E_DECODE; }
+            if (avail < 18) { bfree(&enc); return E_DECODE; }
             u32 len = rd32(p + 14);
-            if (avail < 18 + (size_t)len) { free(enc.p); return E_DECODE; }
+            if (avail < 18 + (size_t)len) { bfree(&enc); return E_DECODE; }
             bput32(&enc, len); exec_from = enc.n; exec_len = len;
             bput(&enc, p + 18, len);
             used = 18 + len;
         }
     }
-    (void)canon;
-    if (enc.oom) { free(enc.p); return E_NOMEM; }
+    if (enc.oom) { bfree(&enc); return E_NOMEM; }
     u64 h = ((u64)proposer << 48) | ((u64)noop << 47) | value_id;
+    if (!t) { bfree(&enc); *handle = h; return (long)used; }   /* outside the shard: not interned */
     ent_t *e = map_find(&t->idx, h);
     if (e) {
         valrec_t *r = &t->v[e->a];
-        if (r->len != enc.n || memcmp(t->bytes.p + r->off, enc.p, enc.n)) { free(enc.p); return E_VALUE; }
+        if (r->len != enc.n || memcmp(t->bytes.p + r->off, enc.p, enc.n)) { bfree(&enc); return E_VALUE; }
     } else {
         if (t->n == t->cap) {
             size_t c = t->cap ? t->cap * 2 : 64;
             valrec_t *q = (valrec_t *)realloc(t->v, c * sizeof(valrec_t));
-            if (!q) { free(enc.p); return E_NOMEM; }
+            if (!q) { bfree(&enc); return E_NOMEM; }
             t->v = q; t->cap = c;
         }
         valrec_t *r = &t->v[t->n];
         r->handle = h; r->off = t->bytes.n; r->len = (u32)enc.n;
         r->exec_off = (u32)exec_from; r->exec_len = (u32)exec_len;
         bput(&t->bytes, enc.p, enc.n);
-        if (!map_put(&t->idx, h, t->n, 0)) { free(enc.p); return E_NOMEM; }
+        if (!map_put(&t->idx, h, t->n, 0)) { bfree(&enc); return E_NOMEM; }
         t->n++;
     }
-    free(enc.p);
+    bfree(&enc);
     *handle = h;
     return (long)used;
 }
@@ -254,31 +259,33 @@ static long parse_value_m(vtab_t *t, const u8 *p, size_t avail, u64 *handle, int
         used += cbl;
     }
     /* canonical bytes = the wire bytes with bools normalised to 0/1 */
-    buf_t enc = {0};
+    u64 h = ((u64)proposer << 48) | ((u64)noop << 47) | value_id;
+    if (!t) { *handle = h; return (long)used; }             /* outside the shard: not interned */
+    u8 sbuf[256];
+    buf_t enc = {sbuf, 0, sizeof sbuf, 0, 1};
     bput(&enc, p, used);
     if (enc.oom) return E_NOMEM;
     enc.p[12] = (u8)noop;
     if (!noop) enc.p[13] = (u8)*membership;
-    u64 h = ((u64)proposer << 48) | ((u64)noop << 47) | value_id;
     ent_t *e = map_find(&t->idx, h);
     if (e) {
         valrec_t *r = &t->v[e->a];
-        if (r->len != enc.n || memcmp(t->bytes.p + r->off, enc.p, enc.n)) { free(enc.p); return E_VALUE; }
+        if (r->len != enc.n || memcmp(t->bytes.p + r->off, enc.p, enc.n)) { bfree(&enc); return E_VALUE; }
     } else {
         if (t->n == t->cap) {
             size_t c = t->cap ? t->cap * 2 : 64;
             valrec_t *q = (valrec_t *)realloc(t->v, c * sizeof(valrec_t));
-            if (!q) { free(enc.p); return E_NOMEM; }
+            if (!q) { bfree(&enc); return E_NOMEM; }
             t->v = q; t->cap = c;
         }
         valrec_t *r = &t->v[t->n];
         r->handle = h; r->off = t->bytes.n; r->len = (u32)enc.n;
         r->exec_off = *membership ? 0xFFFFFFFFu : (u32)exec_from; r->exec_len = (u32)exec_len;
         bput(&t->bytes, enc.p, enc.n);
-        if (!map_put(&t->idx, h, t->n, 0)) { free(enc.p); return E_NOMEM; }
+        if (!map_put(&t->idx, h, t->n, 0)) { bfree(&enc); return E_NOMEM; }
         t->n++;
     }
-    free(enc.p);
+    bfree(&enc);
     *handle = h;
     return (long)used;
 }
@@ -322,6 +329,12 @@ typedef struct {
     u64 n_sends, n_q, n_c, n_exec;
     u64 P, A, L;
     u64 violations;
+    /* presence bitmap of accepted ∪ committed keys below the trace's instance
+     * count M: FilterAcceptedValues' range scans walk it instead of sorting
+     * both maps per PREPARE (O(window / 64), not O(state)).  `big`: a key >= M
+     * was stored, this node then takes the full sorted scan. */
+    u64 *pres;
+    int big;
 } node_t;
 
 typedef struct { u32 version; u64 amask, pmask; } epoch_t;
@@ -334,7 +347,10 @@ typedef struct {
     vtab_t vt;
     node_t *nodes;
     u64 first_violation[4];     /* code, node, seq, iid */
+    u64 sb, se;                 /* instance shard: entries outside are skipped (engine ingest) */
+    map_t seen;                 /* per-message duplicate-iid check, reused */
 } ctx_t;
+#define IN_SHARD(c, iid) ((iid) >= (c)->sb && (iid) < (c)->se)
 
 static void violate(ctx_t *c, node_t *n, u64 code, u64 seq, u64 iid)
 {
@@ -351,6 +367,81 @@ static void emit(node_t *n, u32 dst, const buf_t *m)
     bput32(&n->sends, (u32)m->n);
     bput(&n->sends, m->p, m->n);
     n->n_sends++;
+}
+
+/* ---- presence bitmap (see node_t) ---- */
+static void pres_add(ctx_t *c, node_t *n, u64 k)
+{
+    if (k >= c->M || c->M > (1ull << 36)) { n->big = 1; return; }
+    if (!n->pres) {
+        n->pres = (u64 *)calloc((size_t)((c->M + 63) >> 6), 8);
+        if (!n->pres) { n->big = 1; return; }
+    }
+    n->pres[k >> 6] |= 1ull << (k & 63);
+}
+/* after an erase: clear the bit when the key is in neither map */
+static void pres_drop(ctx_t *c, node_t *n, u64 k)
+{
+    if (k < c->M && n->pres && !map_find(&n->acc, k) && !map_find(&n->com, k))
+        n->pres[k >> 6] &= ~(1ull << (k & 63));
+}
+/* first set bit in [i, e) or e */
+static u64 pres_next(const node_t *n, u64 i, u64 e)
+{
+    while (i < e) {
+        u64 w = n->pres[i >> 6] & (~0ull << (i & 63));
+        if (w) { u64 r = (i & ~63ull) + (u64)__builtin_ctzll(w); return r < e ? r : e; }
+        i = (i | 63) + 1;
+    }
+    return e;
+}
+static int push_ent(ent_t **v, size_t *k, size_t *cap, const ent_t *x)
+{
+    if (*k == *cap) {
+        size_t nc = *cap ? 2 * *cap : 64;
+        ent_t *q = (ent_t *)realloc(*v, nc * sizeof(ent_t));
+        if (!q) return -1;
+        *v = q; *cap = nc;
+    }
+    (*v)[(*k)++] = *x;
+    return 0;
+}
+/* FilterAcceptedValues' candidates for the ranges of a PREPARE (nr ranges of
+ * 16 bytes at rg): per range the accepted entries inside it, then the
+ * committed ones, each iid ascending — what the caller then sorts by iid.
+ * Returns the count (*out malloc'ed) or -1. */
+static long range_entries(ctx_t *c, node_t *n, const u8 *rg, size_t nr, ent_t **out)
+{
+    size_t k = 0, cap = 0;
+    ent_t *v = NULL;
+    if (n->big || !n->pres) {
+        size_t na, nc;
+        ent_t *va = map_sorted(&n->acc, &na);
+        ent_t *vc = map_sorted(&n->com, &nc);
+        if (!va || !vc) { free(va); free(vc); return -1; }
+        for (size_t r = 0; r < nr; ++r) {
+            u64 a = rd64(rg + 16 * r), b = rd64(rg + 16 * r + 8);
+            for (size_t i = 0; i < na; ++i) if (va[i].key >= a && va[i].key < b && push_ent(&v, &k, &cap, &va[i])) goto oom;
+            for (size_t i = 0; i < nc; ++i) if (vc[i].key >= a && vc[i].key < b && push_ent(&v, &k, &cap, &vc[i])) goto oom;
+        }
+        free(va); free(vc);
+        *out = v;
+        return (long)k;
+    oom:
+        free(va); free(vc); free(v);
+        return -1;
+    }
+    for (size_t r = 0; r < nr; ++r) {
+        u64 a = rd64(rg + 16 * r), b = rd64(rg + 16 * r + 8);
+        u64 e = b < c->M ? b : c->M;
+        for (int pass = 0; pass < 2; ++pass)
+            for (u64 i = pres_next(n, a, e); i < e; i = pres_next(n, i + 1, e)) {
+                const ent_t *x = map_find(pass ? &n->com : &n->acc, i);
+                if (x && push_ent(&v, &k, &cap, x)) { free(v); return -1; }
+            }
+    }
+    *out = v;
+    return (long)k;
 }
 
 static void encode_value(buf_t *b, const vtab_t *t, u64 h)
@@ -378,20 +469,13 @@ static int on_prepare(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
             for (size_t j = 0; j < i; ++j)
                 if (rd64(m + 20 + 16 * i) == rd64(m + 20 + 16 * j) &&
                     rd64(m + 28 + 16 * i) == rd64(m + 28 + 16 * j)) violate(c, n, 4, seq, 0);
-        size_t na, nc;
-        ent_t *va = map_sorted(&n->acc, &na);
-        ent_t *vc = map_sorted(&n->com, &nc);
         /* union of accepted and committed entries inside the ranges, iid
          * sorted (FilterAcceptedInstances, :902-910).  Tag: accept ballot or
          * commit ballot. */
-        size_t cap = na + nc + 1, k = 0;
-        ent_t *out = (ent_t *)malloc(cap * sizeof(ent_t));
-        if (!out || !va || !vc) { free(out); free(va); free(vc); return E_NOMEM; }
-        for (size_t r = 0; r < nr; ++r) {
-            u64 a = rd64(m + 20 + 16 * r), b = rd64(m + 28 + 16 * r);
-            for (size_t i = 0; i < na; ++i) if (va[i].key >= a && va[i].key < b) out[k++] = va[i];
-            for (size_t i = 0; i < nc; ++i) if (vc[i].key >= a && vc[i].key < b) out[k++] = vc[i];
-        }
+        ent_t *out = NULL;
+        long kk = range_entries(c, n, m + 20, nr, &out);
+        if (kk < 0) return E_NOMEM;
+        size_t k = (size_t)kk;
         qsort(out, k, sizeof(ent_t), cmp_ent);
         for (size_t i = 1; i < k; ++i) if (out[i].key == out[i - 1].key) violate(c, n, 4, seq, out[i].key);
         buf_t body = {0};
@@ -405,7 +489,7 @@ static int on_prepare(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         bput(&r, body.p, body.n);
         emit(n, proposer, &r);
         n->P += k;
-        free(r.p); free(body.p); free(out); free(va); free(vc);
+        free(r.p); free(body.p); free(out);
     } else if (id < n->promised) {                               /* :894 */
         buf_t r = {0};
         bput32(&r, 2); bput64(&r, n->max_seen);
@@ -428,22 +512,24 @@ static int on_accept(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     if (proposer >= c->N) violate(c, n, 3, seq, 0);
     if (id >= n->promised) {                                     /* :1366 */
         size_t cur = 28, end = 28 + vlen;
-        map_t seen = {0};
+        map_clear(&c->seen);
         while (cur < end) {
-            if (end - cur < 8) { map_free(&seen); return E_DECODE; }
+            if (end - cur < 8) { return E_DECODE; }
             u64 iid = rd64(m + cur); cur += 8;
             u64 h;
-            long u = parse_value(&c->vt, m + cur, end - cur, &h);
-            if (u < 0) { map_free(&seen); return (int)u; }
+            long u = parse_value(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h);
+            if (u < 0) { return (int)u; }
             cur += (size_t)u;
-            if (map_find(&seen, iid)) violate(c, n, 4, seq, iid);   /* :552 */
-            map_put(&seen, iid, 0, 0);
+            if (!IN_SHARD(c, iid)) continue;
+            if (map_find(&c->seen, iid)) violate(c, n, 4, seq, iid);   /* :552 */
+            map_put(&c->seen, iid, 0, 0);
             if (!map_find(&n->com, iid)) {                      /* :1380 */
                 map_put(&n->acc, iid, id, h);                   /* :1387 overwrite */
+                pres_add(c, n, iid);
                 n->A++;
             }
         }
-        map_free(&seen);
+       
         buf_t r = {0};
         bput32(&r, 4); bput32(&r, n->index); bput64(&r, id); bput64(&r, accept);
         emit(n, proposer, &r);
@@ -468,26 +554,29 @@ static int on_commit(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     if (28 + (size_t)vlen > len) return E_DECODE;
     if (committer >= c->N) violate(c, n, 3, seq, 0);
     size_t cur = 28, end = 28 + vlen;
-    map_t seen = {0};
+    map_clear(&c->seen);
     while (cur < end) {
-        if (end - cur < 8) { map_free(&seen); return E_DECODE; }
+        if (end - cur < 8) { return E_DECODE; }
         u64 iid = rd64(m + cur); cur += 8;
         u64 h;
-        long u = parse_value(&c->vt, m + cur, end - cur, &h);
-        if (u < 0) { map_free(&seen); return (int)u; }
+        long u = parse_value(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h);
+        if (u < 0) { return (int)u; }
         cur += (size_t)u;
-        if (map_find(&seen, iid)) violate(c, n, 4, seq, iid);
-        map_put(&seen, iid, 0, 0);
+        if (!IN_SHARD(c, iid)) continue;
+        if (map_find(&c->seen, iid)) violate(c, n, 4, seq, iid);
+        map_put(&c->seen, iid, 0, 0);
         map_del(&n->acc, iid);                                  /* :1501-1502 */
+        pres_drop(c, n, iid);
         ent_t *e = map_find(&n->com, iid);
         if (e) {
             if (e->b != h) violate(c, n, 1, seq, iid);          /* :1508-1509 */
         } else {
             map_put(&n->com, iid, id, h);                       /* :1515 first wins */
+            pres_add(c, n, iid);
         }
         n->L++;
     }
-    map_free(&seen);
+   
     buf_t r = {0};
     bput32(&r, 6); bput32(&r, n->index); bput64(&r, commit);   /* :1577-1582 */
     emit(n, committer, &r);
@@ -520,21 +609,22 @@ static int on_prepare_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 se
     if (acceptor >= c->N) { violate(c, n, 3, seq, 0); return OK; }  /* :1040 */
     n->promised_set |= 1ull << acceptor;
     size_t cur = 20, end = 20 + vlen;
-    map_t seen = {0};
+    map_clear(&c->seen);
     while (cur < end) {
-        if (end - cur < 16) { map_free(&seen); return E_DECODE; }
+        if (end - cur < 16) { return E_DECODE; }
         u64 iid = rd64(m + cur), pid = rd64(m + cur + 8); cur += 16;
         u64 h;
-        long u = parse_value(&c->vt, m + cur, end - cur, &h);
-        if (u < 0) { map_free(&seen); return (int)u; }
+        long u = parse_value(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h);
+        if (u < 0) { return (int)u; }
         cur += (size_t)u;
-        if (map_find(&seen, iid)) violate(c, n, 4, seq, iid);   /* :677 */
-        map_put(&seen, iid, 0, 0);
+        if (!IN_SHARD(c, iid)) continue;
+        if (map_find(&c->seen, iid)) violate(c, n, 4, seq, iid);   /* :677 */
+        map_put(&c->seen, iid, 0, 0);
         ent_t *e = map_find(&n->pre, iid);
         if (e) { if (pid > e->a) { e->a = pid; e->b = h; } }   /* strict >, :1218 */
         else map_put(&n->pre, iid, pid, h);
     }
-    map_free(&seen);
+   
     if ((u64)__builtin_popcountll(n->promised_set) >= c->N / 2 + 1) {   /* :1047 */
         size_t k;
         ent_t *v = map_sorted(&n->pre, &k);
@@ -614,9 +704,10 @@ static int on_p_batch(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         if (end - cur < 8) return E_DECODE;
         u64 iid = rd64(m + cur); cur += 8;
         u64 h;
-        long u = parse_value(&c->vt, m + cur, end - cur, &h);
+        long u = parse_value(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h);
         if (u < 0) return (int)u;
         cur += (size_t)u;
+        if (!IN_SHARD(c, iid)) continue;
         if (n->nbent + 2 > n->cbent) {
             size_t cc = n->cbent ? n->cbent * 2 : 64;
             u64 *q = (u64 *)realloc(n->bent, cc * sizeof(u64));
@@ -667,27 +758,28 @@ static int parse_pvalues(ctx_t *c, node_t *n, const u8 *m, size_t beg, size_t en
 {
     size_t cap = 16, cnt = 0, cur = beg;
     pent_t *v = (pent_t *)malloc(cap * sizeof(pent_t));
-    map_t seen = {0};
+    map_clear(&c->seen);
     if (!v) return E_NOMEM;
     while (cur < end) {
-        if (end - cur < 16) { free(v); map_free(&seen); return E_DECODE; }
+        if (end - cur < 16) { free(v); return E_DECODE; }
         u64 iid = rd64(m + cur), pid = rd64(m + cur + 8);
         cur += 16;
         u64 h; int mem;
-        long u = parse_value_m(&c->vt, m + cur, end - cur, &h, &mem);
-        if (u < 0) { free(v); map_free(&seen); return (int)u; }
+        long u = parse_value_m(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h, &mem);
+        if (u < 0) { free(v); return (int)u; }
         cur += (size_t)u;
-        if (map_find(&seen, iid)) { if (report) violate(c, n, 4, seq, iid); continue; }   /* :429-431 */
-        map_put(&seen, iid, 0, 0);
+        if (!IN_SHARD(c, iid)) continue;
+        if (map_find(&c->seen, iid)) { if (report) violate(c, n, 4, seq, iid); continue; }   /* :429-431 */
+        map_put(&c->seen, iid, 0, 0);
         if (cnt == cap) {
             cap *= 2;
             pent_t *q = (pent_t *)realloc(v, cap * sizeof(pent_t));
-            if (!q) { free(v); map_free(&seen); return E_NOMEM; }
+            if (!q) { free(v); return E_NOMEM; }
             v = q;
         }
         v[cnt].iid = iid; v[cnt].pid = pid; v[cnt].h = h; cnt++;
     }
-    map_free(&seen);
+   
     *out = v; *k = cnt;
     return OK;
 }
@@ -720,18 +812,11 @@ static int m_on_prepare(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
             for (size_t j = 0; j < i; ++j)
                 if (rd64(m + 24 + 16 * i) == rd64(m + 24 + 16 * j) &&
                     rd64(m + 32 + 16 * i) == rd64(m + 32 + 16 * j)) violate(c, n, 4, seq, 0);
-        size_t na, nc;
-        ent_t *va = map_sorted(&n->acc, &na);
-        ent_t *vc = map_sorted(&n->com, &nc);
-        size_t k = 0;
-        ent_t *out = (ent_t *)malloc((na + nc + 1) * nr * sizeof(ent_t) + sizeof(ent_t));
-        if (!out || !va || !vc) { free(out); free(va); free(vc); return E_NOMEM; }
         /* accepted then learned per range, into one iid-keyed map (:1806-1816) */
-        for (size_t r = 0; r < nr; ++r) {
-            u64 a = rd64(m + 24 + 16 * r), b = rd64(m + 32 + 16 * r);
-            for (size_t i = 0; i < na; ++i) if (va[i].key >= a && va[i].key < b) out[k++] = va[i];
-            for (size_t i = 0; i < nc; ++i) if (vc[i].key >= a && vc[i].key < b) out[k++] = vc[i];
-        }
+        ent_t *out = NULL;
+        long kk = range_entries(c, n, m + 24, nr, &out);
+        if (kk < 0) return E_NOMEM;
+        size_t k = (size_t)kk;
         qsort(out, k, sizeof(ent_t), cmp_ent);
         size_t w = 0;
         for (size_t i = 0; i < k; ++i) {
@@ -749,7 +834,7 @@ static int m_on_prepare(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         bput(&r, body.p, body.n);
         emit(n, proposer, &r);
         n->P += w;
-        free(r.p); free(body.p); free(out); free(va); free(vc);
+        free(r.p); free(body.p); free(out);
     } else if (id < n->promised) {                          /* :1734 */
         m_reject(n, proposer);
     }
@@ -778,6 +863,7 @@ static int m_on_accept(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
                 if (l->b != v[i].h) violate(c, n, 6, seq, v[i].iid);
             } else if (!map_find(&n->acc, v[i].iid)) {      /* std::map::insert, :1765 */
                 map_put(&n->acc, v[i].iid, v[i].pid, v[i].h);
+                pres_add(c, n, v[i].iid);
                 n->A++;
             }
         }
@@ -812,6 +898,7 @@ static int m_on_learn(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         }
         map_del(&n->acc, v[i].iid);                         /* :1790-1791 */
         if (!l) map_put(&n->com, v[i].iid, v[i].pid, v[i].h);   /* insert, :1040 */
+        if (!l) pres_add(c, n, v[i].iid); else pres_drop(c, n, v[i].iid);
         n->L++;
     }
     free(v);
@@ -944,6 +1031,9 @@ static int m_on_epoch(ctx_t *c, node_t *n, const u8 *m, size_t len)
     const epoch_t *o = &c->ep[n->epoch], *x = &c->ep[e];
     int acc = (int)((x->amask >> n->index) & 1), prop = (int)((x->pmask >> n->index) & 1);
     if (n->acc_exists != acc) {                             /* new / delete Acceptor, :1897-1901,1952-1957 */
+        for (size_t i = 0; i < n->acc.cap && n->pres; ++i)   /* keys only accepted leave the bitmap */
+            if (n->acc.used[i] && n->acc.e[i].key < c->M && !map_find(&n->com, n->acc.e[i].key))
+                n->pres[n->acc.e[i].key >> 6] &= ~(1ull << (n->acc.e[i].key & 63));
         map_clear(&n->acc);
         n->promised = n->max_seen = 0;
         n->acc_exists = acc;
@@ -985,36 +1075,52 @@ static int process_member(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
 /* ---- container -------------------------------------------------------------*/
 #define HDR 40
 
+/* out == NULL: counters and digests only (no MPXR bytes, state not sorted) */
 static int dump(ctx_t *c, u8 **out, u64 *size, u64 *stats)
 {
     buf_t r = {0};
-    bput(&r, "MPXR", 4);
-    bput32(&r, 1); bput32(&r, c->N); bput32(&r, c->sem);
+    const int want = out != NULL;
+    if (want) bput(&r, "MPXR", 4);
+    if (want) { bput32(&r, 1); bput32(&r, c->N); bput32(&r, c->sem); }
     map_t chosen = {0};
     u64 C = 0, P = 0, A = 0, L = 0, V = 0;
     u64 dstate = 0, dscal = 0, dchosen = 0;
     for (u32 i = 0; i < c->N; ++i) {
         node_t *n = &c->nodes[i];
-        bput64(&r, n->promised); bput64(&r, n->max_seen);
+        if (want) { bput64(&r, n->promised); bput64(&r, n->max_seen); }
         dscal += mix64(mix64((u64)i * 0x9E3779B97F4A7C15ull ^ n->promised) ^ n->max_seen);
+        if (!want) {
+            for (int pass = 0; pass < 2; ++pass) {
+                const map_t *mp = pass ? &n->com : &n->acc;
+                const u64 kind = pass ? 2 : 1;
+                for (size_t j = 0; j < mp->cap; ++j) {
+                    if (!mp->used[j]) continue;
+                    const ent_t *e = &mp->e[j];
+                    dstate += mix64(mix64(mix64(e->key + (u64)i * 0x9E3779B97F4A7C15ull) ^ e->a)
+                                    ^ (e->b + kind * 0xD6E8FEB86659FD93ull));
+                }
+            }
+            P += n->P; A += n->A; L += n->L; V += n->violations;
+            continue;
+        }
         size_t na, nc;
         ent_t *va = map_sorted(&n->acc, &na);
         ent_t *vc = map_sorted(&n->com, &nc);
-        bput64(&r, (u64)(na + nc));
+        if (want) bput64(&r, (u64)(na + nc));
         size_t ia = 0, ic = 0;
         while (ia < na || ic < nc) {
             int take_a = ic >= nc || (ia < na && va[ia].key < vc[ic].key);
             ent_t *e = take_a ? &va[ia++] : &vc[ic++];
             u64 kind = take_a ? 1 : 2;
-            bput64(&r, e->key); bput64(&r, kind); bput64(&r, e->a); bput64(&r, e->b);
+            if (want) { bput64(&r, e->key); bput64(&r, kind); bput64(&r, e->a); bput64(&r, e->b); }
             dstate += mix64(mix64(mix64(e->key + (u64)i * 0x9E3779B97F4A7C15ull) ^ e->a)
                             ^ (e->b + kind * 0xD6E8FEB86659FD93ull));
         }
         free(va); free(vc);
-        bput64(&r, n->n_sends); bput(&r, n->sends.p, n->sends.n);
-        bput64(&r, n->n_q); bput(&r, n->events_q.p, n->events_q.n);
-        bput64(&r, n->n_c); bput(&r, n->events_c.p, n->events_c.n);
-        bput64(&r, n->n_exec); bput(&r, n->exec.p, n->exec.n);
+        if (want) { bput64(&r, n->n_sends); bput(&r, n->sends.p, n->sends.n); }
+        if (want) { bput64(&r, n->n_q); bput(&r, n->events_q.p, n->events_q.n); }
+        if (want) { bput64(&r, n->n_c); bput(&r, n->events_c.p, n->events_c.n); }
+        if (want) { bput64(&r, n->n_exec); bput(&r, n->exec.p, n->exec.n); }
         P += n->P; A += n->A; L += n->L; V += n->violations;
     }
     /* chosen log: union of the entries of every chosen batch, first wins;
@@ -1034,16 +1140,19 @@ static int dump(ctx_t *c, u8 **out, u64 *size, u64 *stats)
             }
         }
     }
-    size_t nch;
-    ent_t *vch = map_sorted(&chosen, &nch);
-    bput64(&r, (u64)nch);
-    for (size_t i = 0; i < nch; ++i) { bput64(&r, vch[i].key); bput64(&r, vch[i].a); }
-    free(vch);
+    if (want) {
+        size_t nch;
+        ent_t *vch = map_sorted(&chosen, &nch);
+        bput64(&r, (u64)nch);
+        for (size_t i = 0; i < nch; ++i) { bput64(&r, vch[i].key); bput64(&r, vch[i].a); }
+        free(vch);
+    }
     map_free(&chosen);
     if (stats) {
         stats[0] = C; stats[1] = P; stats[2] = A; stats[3] = L; stats[4] = V;
         stats[5] = dchosen; stats[6] = dstate; stats[7] = dscal;
     }
+    if (!want) return OK;
     if (r.oom) { free(r.p); return E_NOMEM; }
     *out = r.p; *size = r.n;
     return OK;
@@ -1056,11 +1165,12 @@ static int dump(ctx_t *c, u8 **out, u64 *size, u64 *stats)
  *   viol  (optional, 4 words): first violation code, node, seq, iid
  * Returns 0 or a negative mpx status code.
  */
-int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
+static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
 {
     if (size < HDR || memcmp(trace, "MPXT", 4)) return E_DECODE;
     ctx_t c;
     memset(&c, 0, sizeof c);
+    c.sb = sb; c.se = se;
     c.N = rd32(trace + 8);
     c.sem = rd32(trace + 12);
     c.M = rd64(trace + 16);
@@ -1105,12 +1215,74 @@ int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64
     for (u32 i = 0; i < c.N; ++i) {
         node_t *n = &c.nodes[i];
         map_free(&n->acc); map_free(&n->com); map_free(&n->pre); map_free(&n->batch_idx);
+        free(n->pres);
         free(n->batches); free(n->bent);
         free(n->sends.p); free(n->events_q.p); free(n->events_c.p); free(n->exec.p);
     }
     free(c.nodes);
     free(c.ep);
     map_free(&c.vt.idx); free(c.vt.v); free(c.vt.bytes.p);
+    map_free(&c.seen);
+    return rc;
+}
+
+int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
+{
+    return run_shard(trace, size, 0, ~0ull, out, out_size, stats, viol);
+}
+
+/*
+ * mpxo_run_shard: the same over the instance shard [sb, se) only — entries
+ * outside it are skipped, headers are processed as a whole (what one GPU rank
+ * ingests).  out may be NULL (counters / digests only).
+ */
+int mpxo_run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
+{
+    return run_shard(trace, size, sb, se, out, out_size, stats, viol);
+}
+
+/*
+ * mpxo_run_sharded: counters and digests of the whole trace from `shards`
+ * instance shards of [0, M) run on `threads` host threads — instances are
+ * independent given the headers, so counters and digests add up and the
+ * per-node scalars (scalar digest) agree on every shard (E_STATE otherwise).
+ * stats as in mpxo_run; returns the first error.
+ */
+typedef struct { const u8 *t; u64 size, sb, se; u64 stats[8]; int rc; } shard_job_t;
+static void *shard_job(void *arg)
+{
+    shard_job_t *j = (shard_job_t *)arg;
+    j->rc = run_shard(j->t, j->size, j->sb, j->se, NULL, NULL, j->stats, NULL);
+    return NULL;
+}
+int mpxo_run_sharded(const u8 *trace, u64 size, u32 shards, u32 threads, u64 *stats)
+{
+    if (size < HDR || !shards || shards > 4096 || !threads || !stats) return E_INVAL;
+    const u64 M = rd64(trace + 16);
+    const u64 per = ((M + shards - 1) / shards + 255) / 256 * 256;
+    shard_job_t *jobs = (shard_job_t *)calloc(shards, sizeof(shard_job_t));
+    pthread_t *tid = (pthread_t *)calloc(threads, sizeof(pthread_t));
+    if (!jobs || !tid) { free(jobs); free(tid); return E_NOMEM; }
+    for (u32 k = 0; k < shards; ++k) {
+        jobs[k].t = trace; jobs[k].size = size;
+        jobs[k].sb = (u64)k * per < M ? (u64)k * per : M;
+        jobs[k].se = k + 1 == shards ? ~0ull : ((u64)(k + 1) * per < M ? (u64)(k + 1) * per : M);
+    }
+    int rc = OK;
+    for (u32 base = 0; base < shards; base += threads) {
+        u32 nt = shards - base < threads ? shards - base : threads;
+        for (u32 k = 0; k < nt; ++k)
+            if (pthread_create(&tid[k], NULL, shard_job, &jobs[base + k])) { shard_job(&jobs[base + k]); tid[k] = 0; }
+        for (u32 k = 0; k < nt; ++k) if (tid[k]) pthread_join(tid[k], NULL);
+    }
+    memset(stats, 0, 8 * sizeof(u64));
+    for (u32 k = 0; k < shards; ++k) {
+        if (jobs[k].rc && rc == OK) rc = jobs[k].rc;
+        for (int w = 0; w < 7; ++w) stats[w] += jobs[k].stats[w];
+        if (k && jobs[k].stats[7] != jobs[0].stats[7] && rc == OK) rc = -6;   /* scalars must agree */
+    }
+    stats[7] = jobs[0].stats[7];
+    free(jobs); free(tid);
     return rc;
 }
 
@@ -1124,7 +1296,6 @@ void mpxo_free(void *p) { free(p); }
  * handles.  This sums the digests (dump() above) of that final state over
  * instances [sb, se) without replaying the trace, so bench.py can check a
  * 2^27-instance run; `threads` POSIX threads split the instances. */
-#include <pthread.h>
 typedef struct { u64 N, lo, hi, ballot, ds, dc; } clean_job_t;
 
 static void *clean_job(void *arg)

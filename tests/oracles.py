@@ -83,3 +83,27 @@ def ref_run(trace):
         _ref = _Runner(REF_SO, "mpxref_run", 4, False)
     data, stats, _ = _ref(trace)
     return data, stats
+
+
+_sharded = None
+
+
+def oracle_run_sharded(trace, shards=16, threads=None):
+    """Counters + digests of the whole trace from `shards` instance shards of
+    the CPU oracle on host threads (oracle mpxo_run_sharded: instances are
+    independent given the replicated headers, so counters / digests add and
+    per-node scalars agree) -> [C,P,A,L,V,chosen_digest,state_digest,scalar_digest]."""
+    global _sharded
+    if _sharded is None:
+        lib = ctypes.CDLL(ORACLE_SO)
+        f = lib.mpxo_run_sharded
+        f.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                      ctypes.POINTER(ctypes.c_uint64)]
+        f.restype = ctypes.c_int
+        _sharded = (lib, f)
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    stats = (ctypes.c_uint64 * 8)()
+    rc = _sharded[1](trace, len(trace), shards, threads, stats)
+    if rc != 0:
+        raise RuntimeError("mpxo_run_sharded failed: %d" % rc)
+    return list(stats)
