@@ -80,6 +80,10 @@ def parse():
 C3 = dict(num_nodes=7, seed=0, batch=256, proposers=3, drop_rate=500, dup_rate=1000, max_delay=500)
 
 
+def log(msg):
+    print("[bench] " + msg, file=sys.stderr, flush=True)
+
+
 def c3_leg(args):
     """The general path on C3: every pair goes through k_apply (multi-ballot promise phases,
     promise replies with entries, rejects, duplicates, reordering).  The trace is generated
@@ -90,16 +94,19 @@ def c3_leg(args):
     t0 = time.perf_counter()
     trace = mpx.generate_trace(mpx.GEN_FAULTY, num_instances=m, **C3)
     t_gen = time.perf_counter() - t0
+    log("c3: generated %.1f MB in %.1f s" % (len(trace) / 1e6, t_gen))
     hd = mpx.trace_header(trace)
     trace_bytes = len(trace)
     eng = mpx.Engine(hd["num_nodes"], 0, max(hd["num_instances"], 1))
     t0 = time.perf_counter()
     eng.submit_trace(trace)
     t_ingest = time.perf_counter() - t0
+    log("c3: ingested in %.1f s" % t_ingest)
     del trace
     t0 = time.perf_counter()
     chk = eng.run()                                 # upload + one digested run (verification)
     t_first = time.perf_counter() - t0
+    log("c3: upload + first run %.1f s" % t_first)
     eng.timings()
     for _ in range(2):
         eng.step()

@@ -70,7 +70,7 @@ struct mpx_engine {
     uint64_t shard_len = 0;
     uint32_t NB = 0;
     // device buffers
-    DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, n_after_prepare, m_flags, m_maxseen;
+    DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, pair_ev, m_flags, m_maxseen;
     DevBuf m_gate, e_pid, ep_amask;
     DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
@@ -285,7 +285,7 @@ static int upload_trace(mpx_engine *e)
     TRY(upload(e->m_ballot, h.m_ballot, s)); TRY(upload(e->m_aux, h.m_aux, s));
     TRY(upload(e->m_ent, h.m_ent, s)); TRY(upload(e->m_cnt, h.m_cnt, s));
     TRY(upload(e->m_node, h.m_node, s)); TRY(upload(e->node_off, h.node_off, s));
-    TRY(upload(e->n_after_prepare, h.n_after_prepare, s));
+    TRY(upload(e->pair_ev, h.pair_ev, s));
     TRY(e->m_flags.alloc(std::max<size_t>(h.m_type.size(), 8)));
     TRY(e->m_maxseen.alloc(std::max<size_t>(h.m_type.size() * 8, 8)));
     TRY(upload(e->chunk_node, h.chunk_node, s)); TRY(upload(e->chunk_beg, h.chunk_beg, s));
@@ -308,7 +308,7 @@ static int upload_trace(mpx_engine *e)
     v.m_ballot = e->m_ballot.as<uint64_t>(); v.m_aux = e->m_aux.as<uint64_t>();
     v.m_ent = e->m_ent.as<uint64_t>(); v.m_cnt = e->m_cnt.as<uint32_t>();
     v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
-    v.n_after_prepare = e->n_after_prepare.as<uint32_t>();
+    v.pair_ev = e->pair_ev.as<uint8_t>();
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
     v.m_gate = e->m_gate.as<uint32_t>(); v.e_pid = e->e_pid.as<uint64_t>();
     v.ep_amask = e->ep_amask.as<uint64_t>(); v.num_epochs = (uint32_t)e->epochs.size();
@@ -878,24 +878,23 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     }
     h.node_chunk_off[N] = (uint32_t)h.chunk_node.size();
     h.g_a.assign(N, 0); h.g_b.assign(N, ~0ull);
-    h.n_after_prepare.resize(N);
-    for (uint32_t n = 0; n < N; ++n) h.n_after_prepare[n] = (uint32_t)(n == 0 ? 2 : h.node_off[n] + 1);
-    h.ev_off.assign(N + 1, 0); h.pl_off.assign(N + 1, 0);
-    for (uint32_t k = 0; k < N + 2; ++k) h.ev_msg.push_back(k);
+    // snapshot events: node 0's PREPARE precedes every fragment and its promise
+    // replies carry no entries, so no pair has events (ingest.cpp's per-pair lists)
+    h.pl_off.assign(N + 1, 0);
     h.pl_msg.push_back(0);
     for (uint32_t k = 0; k < N; ++k) h.pl_msg.push_back(2 + k);
-    h.ev_off[1] = N + 2; h.pl_off[1] = N + 1;
-    for (uint32_t n = 1; n < N; ++n) {
-        h.ev_msg.push_back((uint32_t)h.node_off[n]);
-        h.ev_off[n + 1] = h.ev_off[n] + 1;
-        h.pl_off[n + 1] = h.pl_off[n];
-    }
+    h.pl_off[1] = N + 1;
+    for (uint32_t n = 1; n < N; ++n) h.pl_off[n + 1] = h.pl_off[n];
     hipStream_t s = e->stream;
     TRY(e->m_type.alloc(G)); TRY(e->m_src.alloc(4 * G)); TRY(e->m_ballot.alloc(8 * G)); TRY(e->m_aux.alloc(8 * G));
     TRY(e->m_ent.alloc(8 * G)); TRY(e->m_cnt.alloc(4 * G)); TRY(e->m_node.alloc(4 * G));
     TRY(e->m_flags.alloc(G)); TRY(e->m_maxseen.alloc(8 * G));
     TRY(upload(e->node_off, h.node_off, s));
-    TRY(upload(e->n_after_prepare, h.n_after_prepare, s));
+    TRY(e->pair_ev.alloc(std::max<uint64_t>((uint64_t)N * e->NB, 8)));
+    HTRY(hipMemsetAsync(e->pair_ev.p, 0, e->pair_ev.bytes, s));
+    TRY(e->ev_off.alloc(8 * ((uint64_t)N * e->NB + 1)));
+    HTRY(hipMemsetAsync(e->ev_off.p, 0, e->ev_off.bytes, s));
+    TRY(e->ev_msg.alloc(8));
     TRY(upload(e->chunk_node, h.chunk_node, s)); TRY(upload(e->chunk_beg, h.chunk_beg, s));
     TRY(upload(e->chunk_end, h.chunk_end, s)); TRY(upload(e->node_chunk_off, h.node_chunk_off, s));
     TRY(e->chunk_agg.alloc(std::max<size_t>(16 * h.chunk_node.size(), 16)));
@@ -904,7 +903,6 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     TRY(e->e_slot.alloc(8)); TRY(e->r_pid.alloc(8)); TRY(e->r_val.alloc(8)); TRY(e->r_slot.alloc(8));
     TRY(upload(e->g_a, h.g_a, s)); TRY(upload(e->g_b, h.g_b, s));
     TRY(e->f_off.alloc(8 * ((uint64_t)N * e->NB + 1))); TRY(e->frags.alloc(sizeof(Frag) * 2 * (uint64_t)N * e->NB + 16));
-    TRY(upload(e->ev_off, h.ev_off, s)); TRY(upload(e->ev_msg, h.ev_msg, s));
     TRY(upload(e->pl_off, h.pl_off, s)); TRY(upload(e->pl_msg, h.pl_msg, s));
     TRY(e->b_msg.alloc(4 * K + 4)); TRY(e->b_pstart.alloc(4 * K + 4)); TRY(e->b_rep_off.alloc(8 * (K + 1)));
     TRY(e->b_rep.alloc(4 * (uint64_t)N * K + 4)); TRY(e->b_chosen.alloc(4 * K + 4));
@@ -924,7 +922,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.m_ballot = e->m_ballot.as<uint64_t>(); v.m_aux = e->m_aux.as<uint64_t>();
     v.m_ent = e->m_ent.as<uint64_t>(); v.m_cnt = e->m_cnt.as<uint32_t>();
     v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
-    v.n_after_prepare = e->n_after_prepare.as<uint32_t>();
+    v.pair_ev = e->pair_ev.as<uint8_t>();
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
     v.m_gate = e->m_gate.as<uint32_t>(); v.e_pid = e->e_pid.as<uint64_t>();
     v.ep_amask = e->ep_amask.as<uint64_t>(); v.num_epochs = (uint32_t)e->epochs.size();

@@ -559,14 +559,28 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     ht.e_val.reserve(E); ht.e_iid.reserve(E); ht.r_pid.reserve(R); ht.r_val.reserve(R); ht.r_iid.reserve(R);
     ht.g_a.reserve(GR); ht.g_b.reserve(GR);
     ht.node_off.assign(N + 1, 0);
-    ht.n_after_prepare.assign(N, 0);
 
     EntryPool pool;
     struct FragKey { uint64_t key; Frag f; };
     std::vector<uint64_t> fcount(N * NB + 1, 0), cfcount(NB + 1, 0);
     std::vector<FragKey> fr, cfr;
-    std::vector<uint32_t> ev, pl;
-    std::vector<uint64_t> ev_cnt(N, 0), pl_cnt(N, 0);
+    std::vector<uint32_t> pl;
+    std::vector<uint64_t> pl_cnt(N, 0);
+    // Snapshot events (PREPARE, PREPARE_REPLY, P_START, E_EPOCH) are listed per
+    // (bucket, node) pair, only where they can act on the pair's state:
+    //   PREPARE       FilterAcceptedValues (multi/paxos.cpp:902-922) reads accepted /
+    //                 committed entries: buckets inside its ranges that already hold
+    //                 a fragment of the node (state can exist only after one);
+    //   PREPARE_REPLY the quorum reply emits the merged pre-accepted map (:1047-1105),
+    //   P_START       which it also clears (:1233-1248): buckets with PREPARE_REPLY
+    //                 entries since the node's last P_START;
+    //   E_EPOCH       (member) the same, plus every bucket with state when the node's
+    //                 Acceptor is deleted / recreated (member/paxos.cpp:1897-1901,1952-1957).
+    // So a pair walks O(events that touch it), not every event of its node.
+    std::vector<std::pair<uint64_t, uint32_t>> evp;          // (pair, message)
+    std::vector<uint32_t> first_frag(NB, NONE32);            // per bucket: the node's first fragment message
+    std::vector<uint64_t> touched, round_b;
+    std::vector<uint8_t> in_round(NB, 0);
 
     for (uint32_t n = 0; n < N; ++n) {
         const NodeStream &ns = nodes[n];
@@ -578,6 +592,10 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         ht.g_a.insert(ht.g_a.end(), ns.g_a.begin(), ns.g_a.end());
         ht.g_b.insert(ht.g_b.end(), ns.g_b.begin(), ns.g_b.end());
         uint32_t pstart = NONE32;                       // epoch of the batches that follow
+        for (uint64_t b : touched) first_frag[b] = NONE32;
+        for (uint64_t b : round_b) in_round[b] = 0;
+        touched.clear(); round_b.clear();
+        int64_t maxb = -1;                              // highest bucket with a fragment of this node
         // member roles of node n along its stream (include/mpx.h E_EPOCH)
         uint32_t ep = 0, seg = 1;
         bool acc = member && ((epochs[0].acceptor_mask >> n) & 1);
@@ -617,10 +635,6 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             ht.m_ent.push_back(ent);
             ht.m_cnt.push_back(ns.cnt[k]);
             ht.m_node.push_back(n);
-            if (t == MPX_MSG_PREPARE || t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_E_EPOCH) {
-                ev.push_back(g); ev_cnt[n]++;
-            }
-            if (t == MPX_MSG_PREPARE) ht.n_after_prepare[n] = g + 1;
             if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_E_EPOCH) { pl.push_back(g); pl_cnt[n]++; }
             if (t == MPX_MSG_P_START) pstart = g;
             if (t == MPX_MSG_P_BATCH) {
@@ -635,7 +649,37 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                     if (!dense) ht.any_sparse = true;
                     fr.push_back({b * N + n, f});            // pair index: bucket-major
                     fcount[b * N + n]++;
+                    if (first_frag[b] == NONE32) { first_frag[b] = g; touched.push_back(b); maxb = std::max<int64_t>(maxb, (int64_t)b); }
+                    if (kind == K_PREPLY && !in_round[b]) { in_round[b] = 1; round_b.push_back(b); }
                 });
+            }
+            // snapshot events of this message (after its own fragments: the kernels
+            // merge a message's fragments before its event)
+            auto add_ev = [&](uint64_t b) { evp.push_back({b * N + n, g}); };
+            auto clear_round = [&]() { for (uint64_t b : round_b) in_round[b] = 0; round_b.clear(); };
+            if (t == MPX_MSG_PREPARE && maxb >= 0) {
+                for (uint32_t r = 0; r < ns.cnt[k]; ++r) {
+                    const uint64_t a = ht.g_a[ent + r], e = ht.g_b[ent + r];
+                    if (e <= sb || a >= sb + slen) continue;
+                    const uint64_t lo = (std::max(a, sb) - sb) >> BSH;
+                    const uint64_t hi = std::min<uint64_t>((std::min(e, sb + slen) - sb + BS - 1) >> BSH, (uint64_t)maxb + 1);
+                    for (uint64_t b = lo; b < hi; ++b)
+                        if (first_frag[b] < g) add_ev(b);
+                }
+            } else if (t == MPX_MSG_PREPARE_REPLY) {
+                for (uint64_t b : round_b) add_ev(b);
+            } else if (t == MPX_MSG_P_START) {
+                for (uint64_t b : round_b) add_ev(b);
+                clear_round();
+            } else if (t == MPX_MSG_E_EPOCH) {
+                const uint32_t gate = ht.m_gate.back();
+                if (gate & G_ACCCLR) {
+                    for (uint64_t b = 0; (int64_t)b <= maxb; ++b)
+                        if (first_frag[b] < g) add_ev(b);
+                } else {
+                    for (uint64_t b : round_b) add_ev(b);
+                }
+                if (gate & G_PRECLR) clear_round();
             }
             if (t == MPX_MSG_P_BATCH) {
                 const uint32_t j = (uint32_t)ht.b_msg.size() - 1;
@@ -701,6 +745,20 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         std::vector<uint64_t> pos(ht.cf_off.begin(), ht.cf_off.end() - 1);
         for (auto &x : cfr) ht.cfrags[pos[x.key]++] = x.f;
     }
+    // per-pair event CSR (stable: message order within a pair)
+    ht.ev_off.assign(N * NB + 1, 0);
+    ht.pair_ev.assign(N * NB, 0);
+    for (auto &x : evp) ht.ev_off[x.first + 1]++;
+    for (uint64_t i = 0; i < N * NB; ++i) {
+        ht.pair_ev[i] = ht.ev_off[i + 1] ? 1 : 0;
+        ht.ev_off[i + 1] += ht.ev_off[i];
+    }
+    ht.ev_msg.resize(evp.size());
+    {
+        std::vector<uint64_t> pos(ht.ev_off.begin(), ht.ev_off.end() - 1);
+        for (auto &x : evp) ht.ev_msg[pos[x.first]++] = x.second;
+    }
+    std::vector<std::pair<uint64_t, uint32_t>>().swap(evp);
     // pairs the lean kernel cannot take (same predicate as k_apply_fast in
     // kernels.hip): they go to the general kernel's work list
     for (uint64_t b = 0; b < NB; ++b)
@@ -708,8 +766,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             const uint64_t p = b * N + n, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
             if (!nf) continue;
             const uint64_t bucket_frags = ht.f_off[(b + 1) * N] - ht.f_off[b * N];
-            bool fast = !member && N <= FAST_MAX_NODES && bucket_frags <= FAST_MAX_FRAGS &&
-                        ht.frags[f0].msg >= ht.n_after_prepare[n];
+            bool fast = !member && N <= FAST_MAX_NODES && bucket_frags <= FAST_MAX_FRAGS && !ht.pair_ev[p];
             for (uint64_t f = f0; fast && f < f0 + nf; ++f) {
                 const uint8_t fl = ht.frags[f].flags;
                 fast = (fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT);
@@ -723,11 +780,9 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         ht.r_slot.resize(ht.r_iid.size());
         for (size_t k = 0; k < ht.r_iid.size(); ++k) ht.r_slot[k] = (uint8_t)((ht.r_iid[k] - sb) & (BS - 1));
     }
-    // event / proposer lists
-    ht.ev_off.assign(N + 1, 0);
+    // proposer lists
     ht.pl_off.assign(N + 1, 0);
-    for (uint32_t n = 0; n < N; ++n) { ht.ev_off[n + 1] = ht.ev_off[n] + ev_cnt[n]; ht.pl_off[n + 1] = ht.pl_off[n] + pl_cnt[n]; }
-    ht.ev_msg = std::move(ev);
+    for (uint32_t n = 0; n < N; ++n) ht.pl_off[n + 1] = ht.pl_off[n] + pl_cnt[n];
     ht.pl_msg = std::move(pl);
     // header-scan chunks
     ht.node_chunk_off.assign(N + 1, 0);

@@ -56,7 +56,6 @@ struct HostTrace {
     std::vector<uint32_t> m_src, m_cnt, m_node, m_gate;
     std::vector<uint64_t> m_ballot, m_aux, m_ent;
     std::vector<uint64_t> node_off;
-    std::vector<uint32_t> n_after_prepare;          // 1 + global index of the node's last PREPARE, 0: none
     std::vector<uint32_t> chunk_node, node_chunk_off;
     std::vector<uint64_t> chunk_beg, chunk_end;
     std::vector<uint64_t> e_val, e_iid, e_pid, r_pid, r_val, r_iid, g_a, g_b;
@@ -65,8 +64,9 @@ struct HostTrace {
     std::vector<uint64_t> f_off;
     std::vector<Frag> frags;
     std::vector<uint64_t> gp_list;                  // (node, bucket) pairs for the general apply kernel
-    std::vector<uint64_t> ev_off, pl_off;
+    std::vector<uint64_t> ev_off, pl_off;           // ev_off: per (bucket, node) pair (N * NB + 1); pl_off: per node
     std::vector<uint32_t> ev_msg, pl_msg;
+    std::vector<uint8_t> pair_ev;                   // per pair: 1 when it has snapshot events (not a lean pair)
     std::vector<uint32_t> b_msg, b_pstart, b_rep;
     std::vector<uint64_t> b_rep_off;
     std::vector<uint64_t> cf_off;

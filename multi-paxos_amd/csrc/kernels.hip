@@ -651,6 +651,7 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // its snapshot events see empty state, so skipping them changes no output.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t FAST_PAIR_FRAGS = 2;      // descriptors a pair lane prefetches
+constexpr uint64_t EV_BIT = 1ull << 63;      // k_apply_fast: pair_ev folded into the lane's CSR offset
 __host__ __device__ inline uint32_t fast_group(uint32_t N, uint32_t cap = 4)
 {
     return N ? (63 / N < cap ? 63 / N : cap) : 1;
@@ -675,12 +676,11 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
     if (N > FAST_MAX_NODES) return;
     // after k_plan + k_store only the pairs k_plan counted are left
     if (AFTER_STORE && *v.fast_rest == 0) return;
-    const uint32_t G = fast_group(N, (v.knobs >> 8) & 15 ? (v.knobs >> 8) & 15 : 4), GN = G * N;
+    const uint32_t G = fast_group(N, (v.knobs >> 8) & 15 ? (v.knobs >> 8) & 15 : 4);
     const uint64_t steps = (NB + G - 1) / G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
     const uint32_t pg = lane / N, pn = lane - pg * N;    // pair of lane (lane < GN)
-    const uint32_t nap = lane < GN ? v.n_after_prepare[pn] : 0;
     const uint32_t s0 = 4 * lane;                        // the lane's slots s0..s0+3
 
     // stage 1 (two steps ahead): pair CSR offsets (lanes 0..nb*N), chosen-log
@@ -689,15 +689,16 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         oa = oc = 0;
         if (st >= steps) return;
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
-        if (lane <= nb * N) oa = v.f_off[b0 * N + lane];
+        if (lane <= nb * N) oa = v.f_off[b0 * N + lane] | (lane < nb * N && v.pair_ev[b0 * N + lane] ? EV_BIT : 0);
         if (lane <= nb) oc = v.cf_off[b0 + lane];
     };
     // stage 2 (one step ahead): each pair's first F descriptors, each
     // bucket's chosen-log descriptor when it is the only one
     auto ld_desc = [&](uint64_t st, uint64_t oa, uint64_t oc, uint64_t (&e)[F], uint64_t (&w)[F], uint64_t &ce,
                        uint64_t &cw) {
-        const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64);
+        const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64) & ~EV_BIT;
         const uint64_t c1 = __shfl(oc, (int)((lane + 1) & 63), 64);
+        oa &= ~EV_BIT;
 #pragma unroll
         for (uint32_t k = 0; k < F; ++k) { e[k] = 0; w[k] = NONE32; }
         ce = 0; cw = NONE32;
@@ -727,7 +728,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
     for (; st_c < steps; st_c += nwaves) {
         const uint64_t st = st_c;
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
-        const uint64_t oa = oa_c;
+        const bool pev = (oa_c & EV_BIT) != 0;                 // the pair has snapshot events
+        const uint64_t oa = oa_c & ~EV_BIT;
+        const uint64_t pev_m = __ballot(pev);
         uint64_t e[F], w[F];
 #pragma unroll
         for (uint32_t k = 0; k < F; ++k) { e[k] = ne[k]; w[k] = nw[k]; }
@@ -762,7 +765,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             if ((w[k] >> 60) == K_COMMIT) { ++nL; if (comm) again = true; else { comm = true; fix = k; } }
             else if (!comm && (fg[k] & F_GRANTED)) { ++nA; fix = k; }
         }
-        elig = elig && (uint32_t)w[0] >= nap;
+        elig = elig && !pev;
         const bool uni = elig && full && !again;
         const uint64_t uni_m = __ballot(uni);
         const uint64_t slow_m = __ballot((elig && !uni) || (in_list && len > F));
@@ -816,7 +819,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             // eligibility of a pair with more fragments than a lane prefetches
             const uint64_t rng = ((f1 - f0 >= 64) ? ~0ull : ((1ull << (f1 - f0)) - 1)) << f0;
             const uint64_t badm = __ballot(lane < total && !frag_lean(fw1));
-            if ((badm & rng) || rl32((uint32_t)fw1, f0) < v.n_after_prepare[n]) continue;
+            if ((badm & rng) || ((pev_m >> p) & 1)) continue;
             if (lane == 0) v.st_valid[(uint64_t)n * NB + b] = 1;
             uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the lane's four slots
             uint32_t bad = 0;
@@ -978,7 +981,7 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
             if ((w[k] >> 60) == K_COMMIT) { ++nL; if (comm) again = true; else { comm = true; fix = k; } }
             else if (!comm && (fg[k] & F_GRANTED)) { ++nA; fix = k; }
         }
-        elig = elig && len && (uint32_t)w[0] >= v.n_after_prepare[n];
+        elig = elig && len && !v.pair_ev[i];
         const bool uni = elig && full && !again;
         const bool whole = (b + 1) * BS <= v.shard_len;
         uint32_t q = PLAN_SKIP;
@@ -1189,8 +1192,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         if (i >= v.num_gp || lane > 4) return 0;
         const uint64_t q = v.gp_list[i];                // pair, bucket-major
         if (lane == 4) return q;
-        const uint32_t n = (uint32_t)(q % v.N);
-        return lane < 2 ? f_off[q + lane] : ev_off[n + lane - 2];
+        return lane < 2 ? f_off[q + lane] : ev_off[q + lane - 2];
     };
     // software pipeline over this wave's work items: (1) CSR offsets two
     // items ahead, (2) first descriptor window one item ahead, (3) flags +

@@ -132,7 +132,7 @@ struct DevView {
     const uint32_t *m_cnt;
     const uint32_t *m_node;         // node of each message
     const uint64_t *node_off;       // N+1
-    const uint32_t *n_after_prepare; // per node: 1 + index of its last PREPARE (0: none)
+    const uint8_t *pair_ev;         // per (bucket, node) pair: 1 when snapshot events act on it
     uint8_t *m_flags;
     uint64_t *m_maxseen;
     // member semantics
@@ -163,7 +163,7 @@ struct DevView {
     const Frag *frags;
     uint64_t num_gp;                // pairs for the general apply kernel
     const uint64_t *gp_list;
-    const uint64_t *ev_off;         // N+1
+    const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
     const uint32_t *ev_msg;
     const uint64_t *pl_off;         // N+1
     const uint32_t *pl_msg;

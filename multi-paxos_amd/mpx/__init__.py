@@ -133,7 +133,9 @@ def device_count():
 
 
 def _take(ptr, size):
-    data = ctypes.string_at(ptr, size)
+    # (ctypes.string_at takes a C int size: traces of C3 / C5 at full size exceed 2^31 bytes)
+    addr = ctypes.cast(ptr, ctypes.c_void_p).value
+    data = bytes(memoryview((ctypes.c_char * size).from_address(addr))) if size else b""
     lib().mpx_free(ptr)
     return data
 

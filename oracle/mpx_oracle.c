@@ -335,6 +335,11 @@ typedef struct {
      * was stored, this node then takes the full sorted scan. */
     u64 *pres;
     int big;
+    /* per-node processing state: nodes run on their own threads (run_shard) */
+    vtab_t vt;                  /* Values this node has seen (interned)        */
+    map_t seen;                 /* per-message duplicate-iid check, reused     */
+    u64 first_violation[4];
+    int rc;
 } node_t;
 
 typedef struct { u32 version; u64 amask, pmask; } epoch_t;
@@ -348,16 +353,16 @@ typedef struct {
     node_t *nodes;
     u64 first_violation[4];     /* code, node, seq, iid */
     u64 sb, se;                 /* instance shard: entries outside are skipped (engine ingest) */
-    map_t seen;                 /* per-message duplicate-iid check, reused */
 } ctx_t;
 #define IN_SHARD(c, iid) ((iid) >= (c)->sb && (iid) < (c)->se)
 
 static void violate(ctx_t *c, node_t *n, u64 code, u64 seq, u64 iid)
 {
+    (void)c;
     n->violations++;
-    if (!c->first_violation[0]) {
-        c->first_violation[0] = code; c->first_violation[1] = n->index;
-        c->first_violation[2] = seq;  c->first_violation[3] = iid;
+    if (!n->first_violation[0]) {
+        n->first_violation[0] = code; n->first_violation[1] = n->index;
+        n->first_violation[2] = seq;  n->first_violation[3] = iid;
     }
 }
 
@@ -482,7 +487,7 @@ static int on_prepare(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         for (size_t i = 0; i < k; ++i) {
             bput64(&body, out[i].key);
             bput64(&body, out[i].a);
-            encode_value(&body, &c->vt, out[i].b);
+            encode_value(&body, &n->vt, out[i].b);
         }
         buf_t r = {0};
         bput32(&r, 1); bput32(&r, n->index); bput64(&r, id); bput32(&r, (u32)body.n);
@@ -512,17 +517,17 @@ static int on_accept(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     if (proposer >= c->N) violate(c, n, 3, seq, 0);
     if (id >= n->promised) {                                     /* :1366 */
         size_t cur = 28, end = 28 + vlen;
-        map_clear(&c->seen);
+        map_clear(&n->seen);
         while (cur < end) {
             if (end - cur < 8) { return E_DECODE; }
             u64 iid = rd64(m + cur); cur += 8;
             u64 h;
-            long u = parse_value(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h);
+            long u = parse_value(IN_SHARD(c, iid) ? &n->vt : NULL, m + cur, end - cur, &h);
             if (u < 0) { return (int)u; }
             cur += (size_t)u;
             if (!IN_SHARD(c, iid)) continue;
-            if (map_find(&c->seen, iid)) violate(c, n, 4, seq, iid);   /* :552 */
-            map_put(&c->seen, iid, 0, 0);
+            if (map_find(&n->seen, iid)) violate(c, n, 4, seq, iid);   /* :552 */
+            map_put(&n->seen, iid, 0, 0);
             if (!map_find(&n->com, iid)) {                      /* :1380 */
                 map_put(&n->acc, iid, id, h);                   /* :1387 overwrite */
                 pres_add(c, n, iid);
@@ -554,17 +559,17 @@ static int on_commit(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     if (28 + (size_t)vlen > len) return E_DECODE;
     if (committer >= c->N) violate(c, n, 3, seq, 0);
     size_t cur = 28, end = 28 + vlen;
-    map_clear(&c->seen);
+    map_clear(&n->seen);
     while (cur < end) {
         if (end - cur < 8) { return E_DECODE; }
         u64 iid = rd64(m + cur); cur += 8;
         u64 h;
-        long u = parse_value(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h);
+        long u = parse_value(IN_SHARD(c, iid) ? &n->vt : NULL, m + cur, end - cur, &h);
         if (u < 0) { return (int)u; }
         cur += (size_t)u;
         if (!IN_SHARD(c, iid)) continue;
-        if (map_find(&c->seen, iid)) violate(c, n, 4, seq, iid);
-        map_put(&c->seen, iid, 0, 0);
+        if (map_find(&n->seen, iid)) violate(c, n, 4, seq, iid);
+        map_put(&n->seen, iid, 0, 0);
         map_del(&n->acc, iid);                                  /* :1501-1502 */
         pres_drop(c, n, iid);
         ent_t *e = map_find(&n->com, iid);
@@ -588,10 +593,10 @@ static int on_commit(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         n->next_apply++;
         u64 h = e->b;
         if ((h >> 47) & 1) continue;
-        const valrec_t *r2 = vt_get(&c->vt, h);
+        const valrec_t *r2 = vt_get(&n->vt, h);
         u32 el = r2 ? r2->exec_len : 0;
         bput32(&n->exec, el);
-        if (el) bput(&n->exec, c->vt.bytes.p + r2->off + r2->exec_off, el);
+        if (el) bput(&n->exec, n->vt.bytes.p + r2->off + r2->exec_off, el);
         n->n_exec++;
     }
     return OK;
@@ -609,17 +614,17 @@ static int on_prepare_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 se
     if (acceptor >= c->N) { violate(c, n, 3, seq, 0); return OK; }  /* :1040 */
     n->promised_set |= 1ull << acceptor;
     size_t cur = 20, end = 20 + vlen;
-    map_clear(&c->seen);
+    map_clear(&n->seen);
     while (cur < end) {
         if (end - cur < 16) { return E_DECODE; }
         u64 iid = rd64(m + cur), pid = rd64(m + cur + 8); cur += 16;
         u64 h;
-        long u = parse_value(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h);
+        long u = parse_value(IN_SHARD(c, iid) ? &n->vt : NULL, m + cur, end - cur, &h);
         if (u < 0) { return (int)u; }
         cur += (size_t)u;
         if (!IN_SHARD(c, iid)) continue;
-        if (map_find(&c->seen, iid)) violate(c, n, 4, seq, iid);   /* :677 */
-        map_put(&c->seen, iid, 0, 0);
+        if (map_find(&n->seen, iid)) violate(c, n, 4, seq, iid);   /* :677 */
+        map_put(&n->seen, iid, 0, 0);
         ent_t *e = map_find(&n->pre, iid);
         if (e) { if (pid > e->a) { e->a = pid; e->b = h; } }   /* strict >, :1218 */
         else map_put(&n->pre, iid, pid, h);
@@ -704,7 +709,7 @@ static int on_p_batch(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         if (end - cur < 8) return E_DECODE;
         u64 iid = rd64(m + cur); cur += 8;
         u64 h;
-        long u = parse_value(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h);
+        long u = parse_value(IN_SHARD(c, iid) ? &n->vt : NULL, m + cur, end - cur, &h);
         if (u < 0) return (int)u;
         cur += (size_t)u;
         if (!IN_SHARD(c, iid)) continue;
@@ -758,19 +763,19 @@ static int parse_pvalues(ctx_t *c, node_t *n, const u8 *m, size_t beg, size_t en
 {
     size_t cap = 16, cnt = 0, cur = beg;
     pent_t *v = (pent_t *)malloc(cap * sizeof(pent_t));
-    map_clear(&c->seen);
+    map_clear(&n->seen);
     if (!v) return E_NOMEM;
     while (cur < end) {
         if (end - cur < 16) { free(v); return E_DECODE; }
         u64 iid = rd64(m + cur), pid = rd64(m + cur + 8);
         cur += 16;
         u64 h; int mem;
-        long u = parse_value_m(IN_SHARD(c, iid) ? &c->vt : NULL, m + cur, end - cur, &h, &mem);
+        long u = parse_value_m(IN_SHARD(c, iid) ? &n->vt : NULL, m + cur, end - cur, &h, &mem);
         if (u < 0) { free(v); return (int)u; }
         cur += (size_t)u;
         if (!IN_SHARD(c, iid)) continue;
-        if (map_find(&c->seen, iid)) { if (report) violate(c, n, 4, seq, iid); continue; }   /* :429-431 */
-        map_put(&c->seen, iid, 0, 0);
+        if (map_find(&n->seen, iid)) { if (report) violate(c, n, 4, seq, iid); continue; }   /* :429-431 */
+        map_put(&n->seen, iid, 0, 0);
         if (cnt == cap) {
             cap *= 2;
             pent_t *q = (pent_t *)realloc(v, cap * sizeof(pent_t));
@@ -827,7 +832,7 @@ static int m_on_prepare(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         for (size_t i = 0; i < w; ++i) {
             bput64(&body, out[i].key);
             bput64(&body, out[i].a);
-            encode_value(&body, &c->vt, out[i].b);
+            encode_value(&body, &n->vt, out[i].b);
         }
         buf_t r = {0};
         bput32(&r, 1); bput32(&r, n->index); bput64(&r, id); bput32(&r, (u32)body.n);   /* :1726-1730 */
@@ -908,11 +913,11 @@ static int m_on_learn(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         n->next_apply++;
         u64 h = e->b;
         if ((h >> 47) & 1) continue;                        /* noop, :1064 */
-        const valrec_t *r2 = vt_get(&c->vt, h);
+        const valrec_t *r2 = vt_get(&n->vt, h);
         if (r2 && r2->exec_off == 0xFFFFFFFFu) continue;    /* membership: ChangeMemberships, :1066-1069 */
         u32 el = r2 ? r2->exec_len : 0;
         bput32(&n->exec, el);
-        if (el) bput(&n->exec, c->vt.bytes.p + r2->off + r2->exec_off, el);
+        if (el) bput(&n->exec, n->vt.bytes.p + r2->off + r2->exec_off, el);
         n->n_exec++;
     }
     buf_t r = {0};
@@ -1165,6 +1170,40 @@ static int dump(ctx_t *c, u8 **out, u64 *size, u64 *stats)
  *   viol  (optional, 4 words): first violation code, node, seq, iid
  * Returns 0 or a negative mpx status code.
  */
+typedef struct { ctx_t *c; node_t *n; const u8 *offs, *bytes; u64 cnt, nbytes; } node_job_t;
+static void *node_job(void *arg)
+{
+    node_job_t *j = (node_job_t *)arg;
+    int rc = OK;
+    for (u64 k = 0; k < j->cnt && rc == OK; ++k) {
+        u64 a = rd64(j->offs + 8 * k), b = rd64(j->offs + 8 * (k + 1));
+        if (b < a || b > j->nbytes) { rc = E_DECODE; break; }
+        rc = j->c->sem ? process_member(j->c, j->n, j->bytes + a, (size_t)(b - a), k)
+                       : process(j->c, j->n, j->bytes + a, (size_t)(b - a), k);
+    }
+    j->n->rc = rc;
+    return NULL;
+}
+
+static int check_values(ctx_t *c)
+{
+    map_t all = {0};            /* handle -> node * 2^32 + record */
+    int rc = OK;
+    for (u32 i = 0; i < c->N && rc == OK; ++i) {
+        const vtab_t *t = &c->nodes[i].vt;
+        for (size_t r = 0; r < t->n && rc == OK; ++r) {
+            const valrec_t *x = &t->v[r];
+            ent_t *e = map_find(&all, x->handle);
+            if (!e) { if (!map_put(&all, x->handle, ((u64)i << 32) | r, 0)) rc = E_NOMEM; continue; }
+            const vtab_t *u = &c->nodes[e->a >> 32].vt;
+            const valrec_t *y = &u->v[e->a & 0xFFFFFFFFu];
+            if (x->len != y->len || memcmp(t->bytes.p + x->off, u->bytes.p + y->off, x->len)) rc = E_VALUE;
+        }
+    }
+    map_free(&all);
+    return rc;
+}
+
 static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
 {
     if (size < HDR || memcmp(trace, "MPXT", 4)) return E_DECODE;
@@ -1187,7 +1226,12 @@ static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *o
         c.ep[e].amask = rd64(trace + HDR + 24 * e + 8);
         c.ep[e].pmask = rd64(trace + HDR + 24 * e + 16);
     }
+    /* node streams: located sequentially, processed in parallel — a node's
+     * handlers touch only its own state (the reference runs one paxos thread
+     * per node, multi/paxos.cpp:345), so the result equals node-after-node */
     int rc = OK;
+    node_job_t *jobs = (node_job_t *)calloc(c.N, sizeof(node_job_t));
+    if (!jobs) rc = E_NOMEM;
     for (u32 i = 0; i < c.N && rc == OK; ++i) {
         node_t *n = &c.nodes[i];
         n->index = i;
@@ -1198,18 +1242,29 @@ static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *o
         if (pos + 16 > size) { rc = E_DECODE; break; }
         u64 cnt = rd64(trace + pos), nbytes = rd64(trace + pos + 8);
         pos += 16;
-        const u8 *offs = trace + pos;
         if (pos + 8 * (cnt + 1) + nbytes > size) { rc = E_DECODE; break; }
-        const u8 *bytes = trace + pos + 8 * (cnt + 1);
-        for (u64 k = 0; k < cnt && rc == OK; ++k) {
-            u64 a = rd64(offs + 8 * k), b = rd64(offs + 8 * (k + 1));
-            if (b < a || b > nbytes) { rc = E_DECODE; break; }
-            rc = c.sem ? process_member(&c, n, bytes + a, (size_t)(b - a), k)
-                       : process(&c, n, bytes + a, (size_t)(b - a), k);
-        }
+        jobs[i] = (node_job_t){&c, n, trace + pos, trace + pos + 8 * (cnt + 1), cnt, nbytes};
         pos += 8 * (cnt + 1) + nbytes;
         pos = (pos + 7) & ~(size_t)7;
     }
+    if (rc == OK) {
+        pthread_t *tid = (pthread_t *)calloc(c.N, sizeof(pthread_t));
+        const int par = tid && c.N > 1 && size > (1u << 20);
+        for (u32 i = 0; i < c.N; ++i)
+            if (!par || pthread_create(&tid[i], NULL, node_job, &jobs[i])) { node_job(&jobs[i]); if (tid) tid[i] = 0; }
+        if (par) for (u32 i = 0; i < c.N; ++i) if (tid[i]) pthread_join(tid[i], NULL);
+        free(tid);
+        for (u32 i = 0; i < c.N; ++i) {                    /* first error / violation in node order */
+            if (c.nodes[i].rc && rc == OK) rc = c.nodes[i].rc;
+            if (c.nodes[i].first_violation[0] && !c.first_violation[0])
+                memcpy(c.first_violation, c.nodes[i].first_violation, sizeof c.first_violation);
+        }
+        /* a Value must be the same bytes wherever its (proposer, value_id)
+         * appears (the engine's one value table, MPX_E_VALUE): checked across
+         * the per-node tables for full results */
+        if (rc == OK && out) rc = check_values(&c);
+    }
+    free(jobs);
     if (rc == OK) rc = dump(&c, out, out_size, stats);
     if (viol) memcpy(viol, c.first_violation, sizeof c.first_violation);
     for (u32 i = 0; i < c.N; ++i) {
@@ -1219,10 +1274,13 @@ static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *o
         free(n->batches); free(n->bent);
         free(n->sends.p); free(n->events_q.p); free(n->events_c.p); free(n->exec.p);
     }
+    for (u32 i = 0; i < c.N; ++i) {
+        node_t *n = &c.nodes[i];
+        map_free(&n->vt.idx); free(n->vt.v); free(n->vt.bytes.p);
+        map_free(&n->seen);
+    }
     free(c.nodes);
     free(c.ep);
-    map_free(&c.vt.idx); free(c.vt.v); free(c.vt.bytes.p);
-    map_free(&c.seen);
     return rc;
 }
 

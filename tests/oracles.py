@@ -49,7 +49,8 @@ class _Runner:
         rc = self.fn(*args)
         if rc != 0:
             raise RuntimeError("%s failed: %d" % (self.fn.__name__, rc))
-        data = ctypes.string_at(out, size.value)
+        addr = ctypes.cast(out, ctypes.c_void_p).value
+        data = bytes(memoryview((ctypes.c_char * size.value).from_address(addr))) if size.value else b""
         self.libc.free(out)
         return data, list(stats)[: self.nstats], list(viol)
 

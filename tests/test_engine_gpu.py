@@ -387,3 +387,44 @@ def test_clean_long_node_stream_scan_node_pass():
         st = e.run()
     assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
+
+
+# ---- the stated configs at full size (BASELINE.json configs[2], configs[4]) ----
+STATS_ORDER = ("chosen", "promise_entries", "accept_apps", "commit_apps", "violations",
+               "chosen_digest", "state_digest", "scalar_digest")
+
+
+def _full_size_vs_oracle(kind, **kw):
+    from oracles import oracle_run_sharded
+    t = mpx.generate_trace(kind, **kw)
+    want = oracle_run_sharded(t, shards=1, threads=1)       # node-parallel CPU oracle, digests only
+    e = mpx.Engine.for_trace(t)
+    del t
+    with e:
+        st = e.run()
+        e.step()                                             # the timed path, digested by a separate pass
+        e.sync()
+        step = e.stats()
+        sd = e.state_digest()
+    assert [st[k] for k in STATS_ORDER] == want
+    assert sd == (st["state_digest"], st["chosen_digest"])
+    assert [step[k] for k in STATS_ORDER[:5]] == want[:5]
+    return st
+
+
+def test_c3_full_size_matches_oracle():
+    """C3 at its stated size: 2^24 instances x 7 acceptors, 3 competing proposers,
+    drop 5 % / dup 10 % (<=3) / delay U[0,500) (multi/debug.conf.sample:1), batch U[1,256];
+    every counter and order-independent digest equals the CPU oracle's."""
+    st = _full_size_vs_oracle(mpx.GEN_FAULTY, num_nodes=7, num_instances=1 << 24, seed=0, batch=256,
+                              proposers=3, drop_rate=500, dup_rate=1000, max_delay=500)
+    assert st["chosen"] >= 1 << 24 and st["promise_entries"] > 0 and st["violations"] == 0
+
+
+def test_c5_full_size_matches_oracle():
+    """C5 at its stated size: 2^25 instances, member semantics, acceptor universe 8 —
+    AddAcceptor(1..7) then DelAcceptor(1..7), 15 epochs (member/main.cpp:119-141), 1 % loss,
+    1 % duplicates, stale in-flight ACCEPTs across version changes."""
+    st = _full_size_vs_oracle(mpx.GEN_MEMBER, num_nodes=8, num_instances=1 << 25, seed=0, batch=256,
+                              drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15)
+    assert st["chosen"] == 1 << 25 and st["violations"] == 0
