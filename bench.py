@@ -92,7 +92,7 @@ def c3_leg(args):
     (16 P + 24 A + 16 L from the engine's counters) over the apply phase."""
     m = args.c3_instances
     t0 = time.perf_counter()
-    trace = mpx.generate_trace(mpx.GEN_FAULTY, num_instances=m, **C3)
+    trace = mpx.generate_trace(mpx.GEN_FAULTY, num_instances=m, copy=False, **C3)
     t_gen = time.perf_counter() - t0
     log("c3: generated %.1f MB in %.1f s" % (len(trace) / 1e6, t_gen))
     hd = mpx.trace_header(trace)

@@ -15,6 +15,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gen.hpp"
@@ -196,17 +197,65 @@ extern "C" int mpx_submit_trace(mpx_engine *e, const uint8_t *t, uint64_t size)
         else if (e->epochs.size() != ep.size() || std::memcmp(e->epochs.data(), ep.data(), (size_t)ne * 24)) return MPX_E_INVAL;
     }
     size_t pos = 40 + (size_t)ne * 24;
+    std::vector<size_t> at(N);                      // each node's stream: count word
     for (uint32_t n = 0; n < N; ++n) {
         if (pos + 16 > size) return MPX_E_DECODE;
         const uint64_t cnt = rd64(t + pos), nb = rd64(t + pos + 8);
+        at[n] = pos;
         pos += 16;
         if (pos + 8 * (cnt + 1) + nb > size) return MPX_E_DECODE;
-        std::vector<uint64_t> offs(cnt + 1);
-        std::memcpy(offs.data(), t + pos, 8 * (cnt + 1));
-        TRY(mpx_submit(e, n, t + pos + 8 * (cnt + 1), offs.data(), cnt));
         pos += 8 * (cnt + 1) + nb;
         pos = (pos + 7) & ~(size_t)7;
     }
+    auto stream = [&](uint32_t n, const uint64_t *&offs, const uint8_t *&bytes) {
+        const uint64_t cnt = rd64(t + at[n]);
+        offs = reinterpret_cast<const uint64_t *>(t + at[n] + 16);     // 8-aligned in the container
+        bytes = t + at[n] + 16 + 8 * (cnt + 1);
+        return cnt;
+    };
+    if (N == 1 || size < (1u << 20) || e->device_trace) {
+        for (uint32_t n = 0; n < N; ++n) {
+            const uint64_t *offs; const uint8_t *bytes;
+            const uint64_t cnt = stream(n, offs, bytes);
+            TRY(mpx_submit(e, n, bytes, offs, cnt));
+        }
+        return MPX_OK;
+    }
+    // large traces: the nodes' streams are independent records, decoded on one
+    // host thread each (own value table, merged after; the same MPX_E_VALUE
+    // check across nodes), so ingest scales with the node count
+    const uint64_t t0 = now_ns();
+    std::vector<ValueTable> vts(N);
+    std::vector<IngestViolation> ivs(N);
+    std::vector<int> rcs(N, MPX_OK);
+    const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
+    std::vector<std::thread> th;
+    for (uint32_t n = 0; n < N; ++n) {
+        vts[n].member = member;
+        th.emplace_back([&, n]() {
+            const uint64_t *offs; const uint8_t *bytes;
+            const uint64_t cnt = stream(n, offs, bytes);
+            NodeStream &ns = e->nodes[n];
+            for (uint64_t i = 0; i < cnt && rcs[n] == MPX_OK; ++i) {
+                if (offs[i + 1] < offs[i]) { rcs[n] = MPX_E_INVAL; break; }
+                const uint8_t *m = bytes + offs[i];
+                const size_t len = (size_t)(offs[i + 1] - offs[i]);
+                rcs[n] = member ? decode_record_member(vts[n], ns, n, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n])
+                                : decode_record(vts[n], ns, n, N, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n]);
+            }
+        });
+    }
+    for (auto &x : th) x.join();
+    for (uint32_t n = 0; n < N; ++n) {
+        TRY(rcs[n]);
+        TRY(e->vt.merge(vts[n]));
+        if (ivs[n].count) {                          // first violation in node order
+            if (!e->iv.code) { e->iv.code = ivs[n].code; e->iv.node = ivs[n].node; e->iv.seq = ivs[n].seq; e->iv.iid = ivs[n].iid; }
+            e->iv.count += ivs[n].count;
+        }
+    }
+    e->dirty = true;
+    e->stats.ingest_ns += now_ns() - t0;
     return MPX_OK;
 }
 

@@ -31,6 +31,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -70,6 +71,8 @@ struct Delivery {
     uint64_t lo;                  // PREPARE range start
     std::vector<uint64_t> iids;   // ACCEPT / LEARN entries
     std::vector<uint64_t> pids;
+    // entry bytes, encoded once and shared by every copy of the delivery
+    mutable std::shared_ptr<const std::string> body;
 };
 
 struct Pending { uint64_t due; Delivery d; };
@@ -83,7 +86,8 @@ struct SimNode {
     std::vector<uint64_t> learned_pid;
     uint64_t next_apply = 0, max_learned = 0;
     uint64_t appended = 0;
-    std::vector<std::string> rec;
+    std::string bytes;                        // receive stream: concatenated records
+    std::vector<uint64_t> offs{0};
     std::deque<Pending> later;
 };
 
@@ -120,19 +124,25 @@ struct Gen {
     std::string entries(const std::vector<uint64_t> &iids, const std::vector<uint64_t> &pids) const
     {
         std::string s;
+        s.reserve(iids.size() * 48);
         for (size_t i = 0; i < iids.size(); ++i) { app<uint64_t>(s, iids[i]); app<uint64_t>(s, pids[i]); s += value(iids[i]); }
         return s;
     }
-
-    // the leader's receive stream gets replies at once
-    void to_leader(const std::string &m) { nd[0].rec.push_back(m); nd[0].appended++; }
+    const std::string &body_of(const Delivery &d) const
+    {
+        if (!d.body) d.body = std::make_shared<const std::string>(entries(d.iids, d.pids));
+        return *d.body;
+    }
 
     void append(uint32_t n, const std::string &m)
     {
         SimNode &x = nd[n];
-        x.rec.push_back(m);
+        x.bytes += m;
+        x.offs.push_back(x.bytes.size());
         x.appended++;
     }
+    // the leader's receive stream gets replies at once
+    void to_leader(const std::string &m) { append(0, m); }
 
     // ---- acceptor / learner simulation while writing node n's stream --------
     // returns 1 granted, 0 otherwise
@@ -164,7 +174,7 @@ struct Gen {
             return 0;
         }
         if (d.kind == D_ACCEPT) {
-            std::string body = entries(d.iids, d.pids);
+            const std::string &body = body_of(d);
             app<uint32_t>(m, MPX_MSG_ACCEPT); app<uint32_t>(m, d.version); app<uint32_t>(m, 0);
             app<uint64_t>(m, d.id); app<uint64_t>(m, d.ballot); app<uint32_t>(m, (uint32_t)body.size()); m += body;
             append(n, m);
@@ -182,7 +192,7 @@ struct Gen {
             return 0;
         }
         // LEARN
-        std::string body = entries(d.iids, d.pids);
+        const std::string &body = body_of(d);
         app<uint32_t>(m, MPX_MSG_COMMIT); app<uint32_t>(m, 0); app<uint64_t>(m, d.id);
         app<uint32_t>(m, (uint32_t)body.size()); m += body;
         append(n, m);
@@ -404,7 +414,14 @@ int gen_member(const mpx_gen_params &p, std::string &out)
 
     TraceWriter w;
     w.begin(U, MPX_SEM_MEMBER, g.M, g.ep);
-    for (uint32_t n = 0; n < U; ++n) w.node(g.nd[n].rec);
+    uint64_t total = w.out.size();
+    for (auto &x : g.nd) total += 24 + 8 * x.offs.size() + x.bytes.size();
+    w.out.reserve(total);
+    for (uint32_t n = 0; n < U; ++n) {
+        w.node_raw(g.nd[n].bytes, g.nd[n].offs);
+        std::string().swap(g.nd[n].bytes);
+        std::vector<uint64_t>().swap(g.nd[n].offs);
+    }
     out.swap(w.out);
     return MPX_OK;
 }

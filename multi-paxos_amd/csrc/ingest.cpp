@@ -140,6 +140,23 @@ long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle)
     return (long)used;
 }
 
+int ValueTable::merge(const ValueTable &o)
+{
+    idx.reserve(idx.size() + o.idx.size());
+    for (const auto &kv : o.idx) {
+        const Rec &r = kv.second;
+        auto it = idx.find(kv.first);
+        if (it != idx.end()) {
+            const Rec &q = it->second;
+            if (q.len != r.len || std::memcmp(bytes.data() + q.off, o.bytes.data() + r.off, r.len) != 0) return MPX_E_VALUE;
+            continue;
+        }
+        idx.emplace(kv.first, Rec{bytes.size(), r.len, r.exec_off, r.exec_len});
+        bytes.append(o.bytes, r.off, r.len);
+    }
+    return MPX_OK;
+}
+
 bool ValueTable::encode(uint64_t h, std::string &out) const
 {
     auto it = idx.find(h);
@@ -658,13 +675,18 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             auto add_ev = [&](uint64_t b) { evp.push_back({b * N + n, g}); };
             auto clear_round = [&]() { for (uint64_t b : round_b) in_round[b] = 0; round_b.clear(); };
             if (t == MPX_MSG_PREPARE && maxb >= 0) {
+                uint64_t last_b = 0;                     // ranges are sorted and disjoint: buckets ascend
                 for (uint32_t r = 0; r < ns.cnt[k]; ++r) {
                     const uint64_t a = ht.g_a[ent + r], e = ht.g_b[ent + r];
                     if (e <= sb || a >= sb + slen) continue;
                     const uint64_t lo = (std::max(a, sb) - sb) >> BSH;
                     const uint64_t hi = std::min<uint64_t>((std::min(e, sb + slen) - sb + BS - 1) >> BSH, (uint64_t)maxb + 1);
+                    // several ranges of one PREPARE can meet in a bucket (holes): list it once
                     for (uint64_t b = lo; b < hi; ++b)
-                        if (first_frag[b] < g) add_ev(b);
+                        if (first_frag[b] < g && (evp.empty() || evp.back().second != g || b > last_b)) {
+                            add_ev(b);
+                            last_b = b;
+                        }
                 }
             } else if (t == MPX_MSG_PREPARE_REPLY) {
                 for (uint64_t b : round_b) add_ev(b);

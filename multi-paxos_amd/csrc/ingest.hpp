@@ -30,6 +30,9 @@ struct ValueTable {
     // and for member membership Values (applied by ChangeMemberships instead)
     bool exec_payload(uint64_t handle, std::string &out) const;
     void clear() { idx.clear(); bytes.clear(); synthetic_clean = false; }
+    // add every Value of `o` (decoded on another thread); MPX_E_VALUE when a
+    // handle names different bytes in the two tables
+    int merge(const ValueTable &o);
 };
 
 // One node's decoded receive stream (submission order).

@@ -142,14 +142,23 @@ def _take(ptr, size):
 
 def generate_trace(kind=GEN_CLEAN, num_nodes=5, num_instances=1 << 10, seed=0, batch=256,
                    proposers=1, drop_rate=0, dup_rate=0, max_delay=0, noop_permille=0,
-                   shard_begin=0, shard_end=0):
-    """Deterministic synthetic MPXT trace (host generator in libmpx)."""
+                   shard_begin=0, shard_end=0, copy=True):
+    """Deterministic synthetic MPXT trace (host generator in libmpx).  copy=False
+    returns the generator's own buffer as a ctypes char array (len, slicing, the
+    buffer protocol and every c_char_p argument accept it; freed when collected):
+    C3 / C5 at full size are 15-20 GB, and a bytes copy would double that."""
     p = GenParams(kind, num_nodes, num_instances, seed, batch, proposers, drop_rate, dup_rate,
                   max_delay, noop_permille, shard_begin, shard_end)
     out = ctypes.POINTER(ctypes.c_uint8)()
     size = ctypes.c_uint64()
     _ck("mpx_trace_generate", lib().mpx_trace_generate(ctypes.byref(p), ctypes.byref(out), ctypes.byref(size)))
-    return _take(out, size.value)
+    if copy:
+        return _take(out, size.value)
+    import weakref
+    addr = ctypes.cast(out, ctypes.c_void_p).value
+    arr = (ctypes.c_char * size.value).from_address(addr)
+    weakref.finalize(arr, lib().mpx_free, addr)
+    return arr
 
 
 def trace_header(trace):

@@ -395,13 +395,20 @@ STATS_ORDER = ("chosen", "promise_entries", "accept_apps", "commit_apps", "viola
 
 
 def _full_size_vs_oracle(kind, **kw):
+    import time
     from oracles import oracle_run_sharded
-    t = mpx.generate_trace(kind, **kw)
+    t0 = time.time()
+    log = lambda m: print("[full-size] %s: %s (%.0f s)" % (kw.get("num_instances"), m, time.time() - t0), flush=True)
+    t = mpx.generate_trace(kind, copy=False, **kw)           # the generator's buffer, no bytes copy
+    log("generated %.1f GB" % (len(t) / 1e9))
     want = oracle_run_sharded(t, shards=1, threads=1)       # node-parallel CPU oracle, digests only
+    log("oracle")
     e = mpx.Engine.for_trace(t)
     del t
+    log("ingested")
     with e:
         st = e.run()
+        log("run")
         e.step()                                             # the timed path, digested by a separate pass
         e.sync()
         step = e.stats()
