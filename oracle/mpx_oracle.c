@@ -116,6 +116,10 @@ static void map_del(map_t *m, u64 k)
     }
 }
 static void map_clear(map_t *m) { if (m->cap) memset(m->used, 0, m->cap); m->n = 0; }
+static void map_free(map_t *m);
+/* per-message scratch map: after a large message (a catch-up LEARN carries
+ * every learned Value) release it rather than clear its whole table per message */
+static void map_reset(map_t *m) { if (m->cap > 4096) map_free(m); else map_clear(m); }
 static void map_free(map_t *m) { free(m->e); free(m->used); memset(m, 0, sizeof *m); }
 
 static int cmp_ent(const void *x, const void *y)
@@ -517,7 +521,7 @@ static int on_accept(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     if (proposer >= c->N) violate(c, n, 3, seq, 0);
     if (id >= n->promised) {                                     /* :1366 */
         size_t cur = 28, end = 28 + vlen;
-        map_clear(&n->seen);
+        map_reset(&n->seen);
         while (cur < end) {
             if (end - cur < 8) { return E_DECODE; }
             u64 iid = rd64(m + cur); cur += 8;
@@ -559,7 +563,7 @@ static int on_commit(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     if (28 + (size_t)vlen > len) return E_DECODE;
     if (committer >= c->N) violate(c, n, 3, seq, 0);
     size_t cur = 28, end = 28 + vlen;
-    map_clear(&n->seen);
+    map_reset(&n->seen);
     while (cur < end) {
         if (end - cur < 8) { return E_DECODE; }
         u64 iid = rd64(m + cur); cur += 8;
@@ -614,7 +618,7 @@ static int on_prepare_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 se
     if (acceptor >= c->N) { violate(c, n, 3, seq, 0); return OK; }  /* :1040 */
     n->promised_set |= 1ull << acceptor;
     size_t cur = 20, end = 20 + vlen;
-    map_clear(&n->seen);
+    map_reset(&n->seen);
     while (cur < end) {
         if (end - cur < 16) { return E_DECODE; }
         u64 iid = rd64(m + cur), pid = rd64(m + cur + 8); cur += 16;
@@ -763,7 +767,7 @@ static int parse_pvalues(ctx_t *c, node_t *n, const u8 *m, size_t beg, size_t en
 {
     size_t cap = 16, cnt = 0, cur = beg;
     pent_t *v = (pent_t *)malloc(cap * sizeof(pent_t));
-    map_clear(&n->seen);
+    map_reset(&n->seen);
     if (!v) return E_NOMEM;
     while (cur < end) {
         if (end - cur < 16) { free(v); return E_DECODE; }
