@@ -528,9 +528,10 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
     uint64_t fi = rl64(off, 0);
     const uint64_t fe = rl64(off, 1), cbase = fi;
     uint32_t cv[SPL];                          // bucket-local chosen fragment + 1 of the first chosen Value
-    uint64_t ch[SPL];                          // its handle (agreement check)
+    uint32_t ce[SPL];                          // its entry index (agreement check: Values compared
+                                               // only when two chosen runs name different entries)
 #pragma unroll
-    for (uint32_t j = 0; j < SPL; ++j) { cv[j] = 0; ch[j] = 0; }
+    for (uint32_t j = 0; j < SPL; ++j) { cv[j] = 0; ce[j] = 0; }
     while (fi < fe) {
         const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
         uint64_t fw0 = 0, fw1 = 0;
@@ -546,17 +547,15 @@ __device__ inline void chosen_walk(const DevView &v, uint64_t b, uint16_t *lidx,
             const bool dense = (w1 >> 56) & FR_DENSE;
             int k[SPL];
             frag_slots(lidx, v.e_slot, ent, cnt, st0, dense, k);
-            uint64_t val[SPL];
-#pragma unroll
-            for (uint32_t j = 0; j < SPL; ++j) val[j] = k[j] >= 0 ? v.e_val[ent + k[j]] : 0;
 #pragma unroll
             for (uint32_t j = 0; j < SPL; ++j) {
                 if (k[j] < 0) continue;
                 const uint64_t iid = v.shard_begin + li0 + lane + 64 * j;
+                const uint32_t x = (uint32_t)(ent + k[j]);
                 if (!cv[j]) {
-                    cv[j] = (uint32_t)(fi + a - cbase + 1); ch[j] = val[j]; ++cC;
-                    if (v.digest) dig += chosen_digest(iid, val[j]);
-                } else if (ch[j] != val[j]) record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, iid);
+                    cv[j] = (uint32_t)(fi + a - cbase + 1); ce[j] = x; ++cC;
+                    if (v.digest) dig += chosen_digest(iid, v.e_val[x]);
+                } else if (ce[j] != x && v.e_val[ce[j]] != v.e_val[x]) record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, iid);
             }
         }
         fi += nf;
@@ -1165,13 +1164,23 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
 
 // General apply: one wave owns one (node, bucket) pair of the host-built work
 // list at a time, its 256 instance slots 4 per lane.  The pair's fragments and
-// the node's snapshot events are walked in message order, so every instance
-// sees its events in the reference's order.
-template <int WAVES_PER_EU, bool PREFETCH_VALUES>
+// its snapshot events (ingest.cpp: only the events that can act on this pair)
+// are walked in message order, so every instance sees its events in the
+// reference's order.
+//
+// A slot's state is held as the entry index of its Value in the resident pool
+// (AcceptedValue by reference, mpx_internal.hpp), never the Value itself: a
+// fragment costs no memory access beyond its window's descriptors, scan flags
+// and header ballots, loaded lane-parallel 64 fragments at a time.  Values are
+// read only where the reference looks at them: the re-commit / learned-Value
+// checks when the two entry indices differ (the pool is content-addressed, so a
+// duplicate or retried COMMIT carries the same entries), and the snapshots a
+// granted PREPARE or a promise quorum emits.
+template <int WAVES_PER_EU>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 {
     __shared__ uint16_t lidx_all[4][BS];
-    __shared__ u64x2 pre_all[4][BS];           // pre-accepted merge (pid, PRESENT|handle): rare, kept in LDS
+    __shared__ u64x2 pre_all[4][BS];           // pre-accepted merge (pid, PRESENT | r-entry): rare, kept in LDS
     __shared__ unsigned long long red[4][8];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint16_t *lidx = lidx_all[wv];
@@ -1186,6 +1195,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     const uint64_t *__restrict__ e_val = v.e_val;
     const uint64_t *__restrict__ f_off = v.f_off;
     const uint64_t *__restrict__ ev_off = v.ev_off;
+    constexpr uint32_t S_PRESENT = 1, S_COMMITTED = 2;
 
     // work list: the pairs the lean kernel does not take (ingest.cpp)
     auto rt1 = [&](uint64_t i) -> uint64_t {
@@ -1196,7 +1206,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     };
     // software pipeline over this wave's work items: (1) CSR offsets two
     // items ahead, (2) first descriptor window one item ahead, (3) flags +
-    // entry values of the current item
+    // ballots of the current item
     struct Win { uint64_t fw0, fw1; uint32_t evm; };
     auto rt2 = [&](uint64_t off) -> Win {
         Win w{0, NONE32, NONE32};
@@ -1223,10 +1233,10 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         off_cur = off_nxt;
         off_nxt = rt1(it + 2 * stride);
         const uint64_t li0 = (uint64_t)b << BSH;
-        uint64_t sb[SPL], sw[SPL];               // decoded state (checks, snapshots, digest)
-        uint32_t sm[SPL];                        // the slot as stored: fixing fragment + 1
+        uint64_t sb[SPL];                        // ballot (multi: accept / commit id; member: proposal id)
+        uint32_t sf[SPL], se[SPL], sm[SPL];      // S_* flags, Value entry index, fixing fragment + 1
 #pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) { sb[j] = sw[j] = sm[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
+        for (uint32_t j = 0; j < SPL; ++j) { sb[j] = 0; sf[j] = se[j] = sm[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
 
         bool first = true;
         while (fi < fe || ei < ee) {
@@ -1244,28 +1254,13 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                 evm = lane < ne ? v.ev_msg[ei + lane] : NONE32;
             }
             first = false;
-            // (3) scan results for those messages; entry values of the first
-            //     two dense entry fragments (accept + commit of the bucket)
+            // (3) scan results and ballots of those messages
             const uint32_t fmsg = (uint32_t)fw1;
             uint32_t fflag = 0;
             uint64_t fbal = 0;
             if (lane < nf) { fflag = v.m_flags[fmsg]; fbal = v.m_ballot[fmsg]; }
             uint32_t einfo = 0;
             if (lane < ne) einfo = (uint32_t)v.m_type[evm] | ((uint32_t)v.m_flags[evm] << 8);
-            uint64_t pv[2][SPL];
-#pragma unroll
-            for (uint32_t a = 0; a < 2; ++a) {
-                const uint64_t w1 = a < nf ? rl64(fw1, a) : 0;
-                const uint64_t ent = a < nf ? rl64(fw0, a) : 0;
-                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
-                const uint32_t fl = (uint32_t)(w1 >> 56);
-                const bool pre = PREFETCH_VALUES && a < nf && (fl & FR_DENSE) && (fl >> 4) != K_PREPLY;
-#pragma unroll
-                for (uint32_t j = 0; j < SPL; ++j) {
-                    const int d = (int)(lane + 64 * j) - (int)st0;
-                    pv[a][j] = (pre && d >= 0 && d < (int)cnt) ? e_val[ent + d] : 0;
-                }
-            }
             // merge-walk fragments and events by message index
             uint32_t a = 0, c = 0;
             for (;;) {
@@ -1280,17 +1275,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                     const uint32_t mf = rl32(fflag, a);
                     const uint64_t ballot = rl64(fbal, a);
                     const bool dense = fl & FR_DENSE;
+                    const uint32_t fq = (uint32_t)(fi + a + 1);
                     int k[SPL];
                     frag_slots(lidx, kind == K_PREPLY ? v.r_slot : v.e_slot, ent, cnt, st0, dense, k);
-                    uint64_t val[SPL];
-                    if (PREFETCH_VALUES && kind != K_PREPLY && dense && a < 2) {
-#pragma unroll
-                        for (uint32_t j = 0; j < SPL; ++j) val[j] = a == 0 ? pv[0][j] : pv[1][j];
-                    } else {
-                        const uint64_t *src = kind == K_PREPLY ? v.r_val : e_val;
-#pragma unroll
-                        for (uint32_t j = 0; j < SPL; ++j) val[j] = k[j] >= 0 ? src[ent + k[j]] : 0;
-                    }
                     if (member && (kind == K_ACCEPT || kind == K_COMMIT)) {
                         // member: accept and learn are std::map::insert — the first
                         // Value and its proposal id stick (member/paxos.cpp:1765,1040);
@@ -1302,18 +1289,16 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j) {
                                 if (k[j] < 0) continue;
-                                const uint64_t pid = v.e_pid[ent + k[j]];
-                                if (sw[j] & W_COMMITTED) {
-                                    if ((sw[j] & W_HANDLE) != val[j] && (!learn || (mf & F_PROP)))
+                                const uint32_t x = (uint32_t)(ent + k[j]);
+                                if (sf[j] & S_COMMITTED) {
+                                    if (se[j] != x && e_val[se[j]] != e_val[x] && (!learn || (mf & F_PROP)))
                                         record_violation(v, MPX_V_LEARN_VALUE, n, seq, v.shard_begin + li0 + lane + 64 * j);
                                 } else if (learn) {
-                                    sb[j] = pid;
-                                    sw[j] = W_PRESENT | W_COMMITTED | val[j];
-                                    sm[j] = (uint32_t)(fi + a + 1);
-                                } else if (!(sw[j] & W_PRESENT)) {
-                                    sb[j] = pid;
-                                    sw[j] = W_PRESENT | val[j];
-                                    sm[j] = (uint32_t)(fi + a + 1);
+                                    sb[j] = v.e_pid[x];
+                                    sf[j] = S_PRESENT | S_COMMITTED; se[j] = x; sm[j] = fq;
+                                } else if (!(sf[j] & S_PRESENT)) {
+                                    sb[j] = v.e_pid[x];
+                                    sf[j] = S_PRESENT; se[j] = x; sm[j] = fq;
                                     ++cA;
                                 }
                                 cL += learn;
@@ -1323,10 +1308,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                         if (mf & F_GRANTED) {
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
-                                if (k[j] >= 0 && !(sw[j] & W_COMMITTED)) {           // :1380
+                                if (k[j] >= 0 && !(sf[j] & S_COMMITTED)) {           // :1380
                                     sb[j] = ballot;                                   // :1387
-                                    sw[j] = W_PRESENT | val[j];
-                                    sm[j] = (uint32_t)(fi + a + 1);
+                                    sf[j] = S_PRESENT; se[j] = (uint32_t)(ent + k[j]); sm[j] = fq;
                                     ++cA;
                                 }
                         }
@@ -1334,14 +1318,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j)
                             if (k[j] >= 0) {
-                                if (sw[j] & W_COMMITTED) {                            // :1508
-                                    if ((sw[j] & W_HANDLE) != val[j])
+                                const uint32_t x = (uint32_t)(ent + k[j]);
+                                if (sf[j] & S_COMMITTED) {                            // :1508
+                                    if (se[j] != x && e_val[se[j]] != e_val[x])
                                         record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
                                                          v.shard_begin + li0 + lane + 64 * j);
                                 } else {
                                     sb[j] = ballot;                                   // :1515
-                                    sw[j] = W_PRESENT | W_COMMITTED | val[j];
-                                    sm[j] = (uint32_t)(fi + a + 1);
+                                    sf[j] = S_PRESENT | S_COMMITTED; se[j] = x; sm[j] = fq;
                                 }
                                 ++cL;
                             }
@@ -1352,7 +1336,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 if (k[j] >= 0) {
                                     const uint64_t pid = v.r_pid[ent + k[j]];
                                     const u64x2 cur = pre[lane + 64 * j];
-                                    if (!cur.y || pid > cur.x) pre[lane + 64 * j] = u64x2{pid, W_PRESENT | val[j]};   // :1216-1221
+                                    if (!cur.y || pid > cur.x) pre[lane + 64 * j] = u64x2{pid, W_PRESENT | (ent + k[j])};   // :1216-1221
                                 }
                         }
                     }
@@ -1364,7 +1348,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                     if (t8 == MPX_MSG_PREPARE) {
                         bool have = false;
 #pragma unroll
-                        for (uint32_t j = 0; j < SPL; ++j) have |= (sw[j] & W_PRESENT) != 0;
+                        for (uint32_t j = 0; j < SPL; ++j) have |= (sf[j] & S_PRESENT) != 0;
                         if ((fl & F_GRANTED) && __ballot(have)) {
                             // FilterAcceptedValues over the prepare's ranges (:902-922);
                             // ranges sorted by start and disjoint (ingest)
@@ -1375,7 +1359,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 const uint64_t li = li0 + lane + 64 * j;
                                 const uint64_t iid = v.shard_begin + li;
                                 bool hit = false;
-                                if (nr && li < v.shard_len && (sw[j] & W_PRESENT)) {
+                                if (nr && li < v.shard_len && (sf[j] & S_PRESENT)) {
                                     uint32_t lo = 0, hi = nr;       // last range with a <= iid
                                     while (lo < hi) {
                                         const uint32_t mid = (lo + hi) >> 1;
@@ -1383,7 +1367,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                     }
                                     hit = lo > 0 && iid < v.g_b[r0 + lo - 1];
                                 }
-                                emit(v, hit, g, 0, iid, sb[j], sw[j] & W_HANDLE);
+                                emit(v, hit, g, 0, iid, sb[j], hit ? e_val[se[j]] : 0);
                                 cP += hit;
                             }
                         }
@@ -1393,21 +1377,21 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                         if (t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
-                                if (!(sw[j] & W_COMMITTED)) sb[j] = sw[j] = sm[j] = 0;
+                                if (!(sf[j] & S_COMMITTED)) { sb[j] = 0; sf[j] = se[j] = sm[j] = 0; }
                         }
                     } else if (t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
                         // the Acceptor is deleted / recreated: its accepted values go
                         // (member/paxos.cpp:1952-1957); learned ones stay with the Learner
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j)
-                            if (!(sw[j] & W_COMMITTED)) sb[j] = sw[j] = sm[j] = 0;
+                            if (!(sf[j] & S_COMMITTED)) { sb[j] = 0; sf[j] = se[j] = sm[j] = 0; }
                     } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
 #pragma unroll 1
                         for (uint32_t j = 0; j < SPL; ++j) {
                             const uint64_t li = li0 + lane + 64 * j;
                             const u64x2 cur = pre[lane + 64 * j];
                             const bool hit = li < v.shard_len && cur.y;
-                            emit(v, hit, g, 1, v.shard_begin + li, cur.x, cur.y & W_HANDLE);
+                            emit(v, hit, g, 1, v.shard_begin + li, cur.x, hit ? v.r_val[cur.y & ~W_PRESENT] : 0);
                             cQ += hit;
                             pre[lane + 64 * j] = u64x2{0, 0};                        // :1105
                         }
@@ -1420,14 +1404,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         }
         bool have = false;
 #pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) have |= sw[j] != 0;
+        for (uint32_t j = 0; j < SPL; ++j) have |= sf[j] != 0;
         if (__ballot(have)) {
 #pragma unroll
             for (uint32_t j = 0; j < SPL; ++j) {
                 const uint64_t li = li0 + lane + 64 * j;
                 if (li < v.shard_len) st_put(v, (uint64_t)n * v.shard_len + li, sm[j] ? (uint32_t)(sm[j] - pbase) : 0);
-                if (sw[j])
-                    if (v.digest) dig += state_digest(n, v.shard_begin + li, (sw[j] & W_COMMITTED) ? 2 : 1, sb[j], sw[j] & W_HANDLE);
+                if (sf[j] && v.digest)
+                    dig += state_digest(n, v.shard_begin + li, (sf[j] & S_COMMITTED) ? 2 : 1, sb[j], e_val[se[j]]);
             }
             if (lane == 0) v.st_valid[(uint64_t)n * v.NB + b] = 1;
         }
@@ -1743,7 +1727,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (v.semantics == MPX_SEM_MEMBER) {
         // member: every pair walks the general kernel (insert semantics, epoch events)
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-        if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+        if (v.num_gp) hipLaunchKernelGGL((k_apply<1>), dim3(g.apply_wgs), dim3(256), 0, s, v);
     } else {
         // multi: the lean kernel also writes the chosen log of clean buckets
         // digest runs (verification) take their own instantiation, so the
@@ -1764,7 +1748,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         }
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-        if (v.num_gp) hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+        if (v.num_gp) hipLaunchKernelGGL((k_apply<1>), dim3(g.apply_wgs), dim3(256), 0, s, v);
     }
     if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
