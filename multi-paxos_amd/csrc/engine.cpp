@@ -295,9 +295,9 @@ static int finish_view(mpx_engine *e)
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + e->geom.chosen_wgs)));
     TRY(e->viol.alloc(sizeof(DevViolation)));
     TRY(e->summary.alloc(64 * 8));
-    TRY(e->out_cursor.alloc(8));
-    if (!e->out_cap) e->out_cap = 1 << 16;
-    TRY(e->out.alloc(e->out_cap * sizeof(OutRec)));
+    TRY(e->out_cursor.alloc(8ull * OUT_STRIDE * OUT_SUBS));
+    if (!e->out_cap) e->out_cap = 1 << 12;               // records per sub-buffer
+    TRY(e->out.alloc(OUT_SUBS * e->out_cap * sizeof(OutRec)));
     TRY(e->node_scal.alloc(16ull * N));
     v.st = e->st.p;
     v.st_valid = e->st_valid.as<uint8_t>();
@@ -436,11 +436,15 @@ static int collect(mpx_engine *e)
     e->last_summary.assign(64, 0);
     HTRY(hipMemcpy(e->last_summary.data(), e->summary.p, 64 * 8, hipMemcpyDeviceToHost));
     uint64_t cursor = 0;
-    HTRY(hipMemcpy(&cursor, e->out_cursor.p, 8, hipMemcpyDeviceToHost));
+    {
+        std::vector<uint64_t> cur(OUT_STRIDE * OUT_SUBS);
+        HTRY(hipMemcpy(cur.data(), e->out_cursor.p, 8 * cur.size(), hipMemcpyDeviceToHost));
+        for (uint32_t s = 0; s < OUT_SUBS; ++s) cursor = std::max<uint64_t>(cursor, cur[OUT_STRIDE * s]);
+    }
     if (cursor > e->out_cap) {
-        // snapshot output overflowed: grow and run again (runs are deterministic)
+        // a snapshot sub-buffer overflowed: grow and run again (runs are deterministic)
         e->out_cap = cursor + cursor / 4;
-        TRY(e->out.alloc(e->out_cap * sizeof(OutRec)));
+        TRY(e->out.alloc(OUT_SUBS * e->out_cap * sizeof(OutRec)));
         e->view.out = e->out.as<OutRec>();
         e->view.out_cap = e->out_cap;
         TRY(queue_run(e, e->view.digest != 0));
@@ -718,9 +722,16 @@ static int fetch_results(mpx_engine *e, Results &r)
     TRY(d2h(r.flags, e->m_flags, G));
     TRY(d2h(r.maxseen, e->m_maxseen, G));
     TRY(d2h(r.scal, e->node_scal, 2ull * e->cfg.num_nodes));
-    uint64_t cursor = 0;
-    HTRY(hipMemcpy(&cursor, e->out_cursor.p, 8, hipMemcpyDeviceToHost));
-    TRY(d2h(r.out, e->out, std::min<uint64_t>(cursor, e->out_cap)));
+    {
+        std::vector<uint64_t> cur(OUT_STRIDE * OUT_SUBS);
+        HTRY(hipMemcpy(cur.data(), e->out_cursor.p, 8 * cur.size(), hipMemcpyDeviceToHost));
+        std::vector<OutRec> part;
+        for (uint32_t s = 0; s < OUT_SUBS; ++s) {
+            const uint64_t k = std::min<uint64_t>(cur[OUT_STRIDE * s], e->out_cap);
+            TRY(d2h(part, e->out, k, (size_t)s * e->out_cap));
+            r.out.insert(r.out.end(), part.begin(), part.end());
+        }
+    }
     TRY(d2h(r.b_chosen, e->b_chosen, e->ht.b_msg.size()));
     for (auto &o : r.out) r.by_msg[o.kind & 1][o.msg].push_back(&o);
     for (int k = 0; k < 2; ++k)

@@ -337,50 +337,75 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
 }
 
 // --------------------------------------------------------- proposer side --
-// Promise quorum per node: serial over the node's (few) P_START and
-// PREPARE_REPLY records.  One lane per node.
-__global__ void k_proposer(DevView v)
+// Promise quorum per node (OnPrepareReply, multi/paxos.cpp:1036-1057): one
+// wave per node walks its P_START / PREPARE_REPLY (/ E_EPOCH) records 64 at a
+// time — each window's headers are loaded lane-parallel, the quorum state
+// machine then runs serially on wave-uniform registers, and each lane writes
+// its own record's flags.  (A lane-serial walk paid a dependent global load per
+// record: 10 ms for C3's 2^24 trace.)
+__global__ __launch_bounds__(64) void k_proposer(DevView v)
 {
-    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = blockIdx.x, lane = threadIdx.x;
     if (n >= v.N) return;
     uint64_t ballot = 0, mask = 0;         // proposal_id_ = 0 at genesis (:338)
     bool preparing = false;                // prepare_retry_timeout_ = NULL
     const bool member = v.semantics == MPX_SEM_MEMBER;
-    for (uint64_t i = v.pl_off[n]; i < v.pl_off[n + 1]; ++i) {
-        const uint32_t g = v.pl_msg[i];
-        const uint8_t t = v.m_type[g];
-        if (member) {
-            // Proposer::OnPrepareReply, member/paxos.cpp:1158-1182: only an
-            // existing Proposer; quorum |acceptors|/2+1 of the node's epoch
-            const uint32_t gt = v.m_gate[g];
-            if (t == MPX_MSG_E_EPOCH) {
-                if (gt & G_PRECLR) { preparing = false; mask = 0; }
+    const uint64_t i0 = v.pl_off[n], i1 = v.pl_off[n + 1];
+    for (uint64_t base = i0; base < i1; base += 64) {
+        const uint32_t cnt = (uint32_t)(i1 - base < 64 ? i1 - base : 64);
+        uint32_t g = 0, t = 0xFF, src = 0, gt = 0;
+        uint64_t b = 0, am = 0;
+        if (lane < cnt) {
+            g = v.pl_msg[base + lane];
+            t = v.m_type[g]; b = v.m_ballot[g]; src = v.m_src[g];
+            if (member) {
+                gt = v.m_gate[g];
+                if (gt >> G_EPOCH_SHIFT) am = v.ep_amask[(gt >> G_EPOCH_SHIFT) - 1];
+            }
+        }
+        uint32_t mine = 0;                 // flags for this lane's record
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const uint32_t tk = rl32(t, k);
+            const uint64_t bk = rl64(b, k);
+            uint32_t f = 0;
+            if (member) {
+                // Proposer::OnPrepareReply, member/paxos.cpp:1158-1182: only an
+                // existing Proposer; quorum |acceptors|/2+1 of the node's epoch
+                const uint32_t gk = rl32(gt, k);
+                if (tk == MPX_MSG_E_EPOCH) {
+                    if (gk & G_PRECLR) { preparing = false; mask = 0; }
+                    continue;
+                }
+                if (!(gk >> G_EPOCH_SHIFT)) continue;
+                if (tk == MPX_MSG_P_START) { ballot = bk; preparing = true; mask = 0; continue; }
+                if (!preparing || bk != ballot) continue;                      // :1160
+                const uint64_t amk = rl64(am, k);
+                const uint32_t a = rl32(src, k);
+                if (a >= 64 || !((amk >> a) & 1)) {
+                    if (lane == 0) record_violation(v, MPX_V_BAD_NODE, n, rl32(g, k) - v.node_off[n], 0);
+                    continue;
+                }
+                f = F_COUNTED;
+                mask |= 1ull << a;
+                if ((uint32_t)__popcll(mask) >= (uint32_t)__popcll(amk) / 2 + 1) { f |= F_QUORUM; preparing = false; mask = 0; }
+            } else if (tk == MPX_MSG_P_START) {
+                ballot = bk; preparing = true; mask = 0;
                 continue;
+            } else if (preparing && bk == ballot) {      // :1038
+                const uint32_t a = rl32(src, k);
+                if (a >= v.N) {
+                    if (lane == 0) record_violation(v, MPX_V_BAD_NODE, n, rl32(g, k) - v.node_off[n], 0);
+                    continue;
+                }
+                f = F_COUNTED;
+                mask |= 1ull << a;
+                if ((uint32_t)__popcll(mask) >= v.quorum) {          // :1047
+                    f |= F_QUORUM; preparing = false; mask = 0;
+                }
             }
-            if (!(gt >> G_EPOCH_SHIFT)) continue;
-            if (t == MPX_MSG_P_START) { ballot = v.m_ballot[g]; preparing = true; mask = 0; continue; }
-            if (!preparing || v.m_ballot[g] != ballot) continue;             // :1160
-            const uint64_t am = v.ep_amask[(gt >> G_EPOCH_SHIFT) - 1];
-            const uint32_t a = v.m_src[g];
-            if (a >= 64 || !((am >> a) & 1)) { record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0); continue; }
-            uint8_t f = F_COUNTED;
-            mask |= 1ull << a;
-            if ((uint32_t)__popcll(mask) >= (uint32_t)__popcll(am) / 2 + 1) { f |= F_QUORUM; preparing = false; mask = 0; }
-            v.m_flags[g] |= f;
-            continue;
+            if (lane == k) mine = f;
         }
-        if (t == MPX_MSG_P_START) {
-            ballot = v.m_ballot[g]; preparing = true; mask = 0;
-        } else if (preparing && v.m_ballot[g] == ballot) {      // :1038
-            const uint32_t a = v.m_src[g];
-            if (a >= v.N) { record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0); continue; }
-            uint8_t f = F_COUNTED;
-            mask |= 1ull << a;
-            if ((uint32_t)__popcll(mask) >= v.quorum) {          // :1047
-                f |= F_QUORUM; preparing = false; mask = 0;
-            }
-            v.m_flags[g] |= f;
-        }
+        if (mine) v.m_flags[g] |= (uint8_t)mine;
     }
 }
 
@@ -467,25 +492,38 @@ __device__ inline void wave_lds_fence()
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ inline void emit(const DevView &v, bool want, uint32_t msg, uint32_t kind, uint64_t iid,
-                            uint64_t ballot, uint64_t handle)
+// Snapshot records of one event of a pair: lane l's slot j is emitted when
+// want[j]; one append (atomicAdd on the wave's sub-buffer cursor) per event.
+constexpr uint32_t SPL_ = 4;
+__device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uint32_t msg, uint32_t kind,
+                                 uint64_t iid0, const uint64_t (&ballot)[SPL_], const uint64_t (&handle)[SPL_])
 {
-    const uint64_t m = __ballot(want);
-    if (!m) return;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
-    const uint32_t first = (uint32_t)(__ffsll((long long)m) - 1);
+    uint64_t m[SPL_];
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SPL_; ++j) { m[j] = __ballot(want[j]); tot += (uint32_t)__popcll(m[j]); }
+    if (!tot) return;
+    const uint32_t sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (OUT_SUBS - 1);
     unsigned long long base = 0;
-    if (lane == first) base = atomicAdd(v.out_cursor, (unsigned long long)__popcll(m));
-    base = __shfl(base, first, 64);
-    if (want && base + rank < v.out_cap) {
-        OutRec r;
-        r.msg = msg; r.kind = kind; r.iid = iid; r.ballot = ballot; r.handle = handle;
-        v.out[base + rank] = r;
+    if (lane == 0) base = atomicAdd(&v.out_cursor[OUT_STRIDE * sub], (unsigned long long)tot);
+    base = __shfl(base, 0, 64);
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t off = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SPL_; ++j) {
+        const uint64_t at = base + off + (uint64_t)__popcll(m[j] & below);
+        if (want[j] && at < v.out_cap) {
+            OutRec r;
+            r.msg = msg; r.kind = kind; r.iid = iid0 + lane + 64 * j; r.ballot = ballot[j]; r.handle = handle[j];
+            v.out[(uint64_t)sub * v.out_cap + at] = r;
+        }
+        off += (uint32_t)__popcll(m[j]);
     }
 }
 
 constexpr uint32_t SPL = BS / 64;
+static_assert(SPL == SPL_, "4 slots per lane");
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));          // slots per lane: slot = lane + 64 * j
 
 // slots of this lane that fragment (start, count, dense) covers: k[j] = entry
@@ -1345,31 +1383,44 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                     const uint32_t g = em;
                     const uint32_t info = rl32(einfo, c);
                     const uint32_t t8 = info & 0xFF, fl = info >> 8;
-                    if (t8 == MPX_MSG_PREPARE) {
+                    if (t8 == MPX_MSG_PREPARE && !(v.knobs & 4096)) {   // knob 4096: experiment, no snapshots
                         bool have = false;
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) have |= (sf[j] & S_PRESENT) != 0;
                         if ((fl & F_GRANTED) && __ballot(have)) {
                             // FilterAcceptedValues over the prepare's ranges (:902-922);
-                            // ranges sorted by start and disjoint (ingest)
+                            // ranges sorted by start and disjoint (ingest): one
+                            // wave-uniform search for the bucket's first range, then
+                            // the few ranges that meet the bucket
                             const uint64_t r0 = v.m_ent[g];
                             const uint32_t nr = v.m_cnt[g];
-#pragma unroll 1
-                            for (uint32_t j = 0; j < SPL; ++j) {
-                                const uint64_t li = li0 + lane + 64 * j;
-                                const uint64_t iid = v.shard_begin + li;
-                                bool hit = false;
-                                if (nr && li < v.shard_len && (sf[j] & S_PRESENT)) {
-                                    uint32_t lo = 0, hi = nr;       // last range with a <= iid
-                                    while (lo < hi) {
-                                        const uint32_t mid = (lo + hi) >> 1;
-                                        if (v.g_a[r0 + mid] <= iid) lo = mid + 1; else hi = mid;
-                                    }
-                                    hit = lo > 0 && iid < v.g_b[r0 + lo - 1];
-                                }
-                                emit(v, hit, g, 0, iid, sb[j], hit ? e_val[se[j]] : 0);
-                                cP += hit;
+                            const uint64_t blo = v.shard_begin + li0, bhi = blo + BS;
+                            uint32_t lo = 0, hi = nr;       // last range with a <= blo
+                            while (lo < hi) {
+                                const uint32_t mid = (lo + hi) >> 1;
+                                if (v.g_a[r0 + mid] <= blo) lo = mid + 1; else hi = mid;
                             }
+                            bool hit[SPL];
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j) hit[j] = false;
+                            for (uint32_t r = lo ? lo - 1 : 0; r < nr; ++r) {
+                                const uint64_t ra = v.g_a[r0 + r], rb = v.g_b[r0 + r];
+                                if (ra >= bhi) break;
+                                if (rb <= blo) continue;
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j) {
+                                    const uint64_t iid = blo + lane + 64 * j;
+                                    hit[j] |= iid >= ra && iid < rb;
+                                }
+                            }
+                            uint64_t hv[SPL];
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j) {
+                                hit[j] = hit[j] && li0 + lane + 64 * j < v.shard_len && (sf[j] & S_PRESENT);
+                                hv[j] = hit[j] ? e_val[se[j]] : 0;
+                                cP += hit[j];
+                            }
+                            emit_rows(v, hit, g, 0, blo, sb, hv);
                         }
                     } else if (t8 == MPX_MSG_P_START || (t8 == MPX_MSG_E_EPOCH && (fl & F_PRECLR))) {
 #pragma unroll
@@ -1386,15 +1437,18 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                         for (uint32_t j = 0; j < SPL; ++j)
                             if (!(sf[j] & S_COMMITTED)) { sb[j] = 0; sf[j] = se[j] = sm[j] = 0; }
                     } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
-#pragma unroll 1
+                        bool hit[SPL];
+                        uint64_t pb[SPL], hv[SPL];
+#pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) {
-                            const uint64_t li = li0 + lane + 64 * j;
                             const u64x2 cur = pre[lane + 64 * j];
-                            const bool hit = li < v.shard_len && cur.y;
-                            emit(v, hit, g, 1, v.shard_begin + li, cur.x, hit ? v.r_val[cur.y & ~W_PRESENT] : 0);
-                            cQ += hit;
+                            hit[j] = li0 + lane + 64 * j < v.shard_len && cur.y;
+                            pb[j] = cur.x;
+                            hv[j] = hit[j] ? v.r_val[cur.y & ~W_PRESENT] : 0;
+                            cQ += hit[j];
                             pre[lane + 64 * j] = u64x2{0, 0};                        // :1105
                         }
+                        emit_rows(v, hit, g, 1, v.shard_begin + li0, pb, hv);
                     }
                     ++c;
                 }
@@ -1518,8 +1572,8 @@ __global__ void k_reset(DevView v, uint32_t n_partials)
     if (i < v.NB) v.chosen_valid[i] = 0;
     if (i < 8ull * n_partials) v.partials[i] = 0;
     if (i < 2ull * v.N) v.node_scal[i] = 0;    // nodes without messages keep promised = max_seen = 0
+    if (i < OUT_SUBS) v.out_cursor[OUT_STRIDE * i] = 0;
     if (i == 0) {
-        *v.out_cursor = 0;
         *v.fast_rest = 0;
         v.viol->code = v.viol->node = v.viol->seq = v.viol->iid = v.viol->count = 0;
     }
@@ -1721,7 +1775,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
         else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
     }
-    hipLaunchKernelGGL(k_proposer, dim3(cdiv(v.N, 64)), dim3(64), 0, s, v);
+    hipLaunchKernelGGL(k_proposer, dim3(v.N), dim3(64), 0, s, v);
     if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
     if (ev_apply0) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
     if (v.semantics == MPX_SEM_MEMBER) {

@@ -110,6 +110,12 @@ struct OutRec {
     uint64_t handle;
 };
 
+// snapshot output: OUT_SUBS sub-buffers with their own cursors, a wave appends
+// to sub (wave id mod OUT_SUBS) — the host sorts records by message and iid, so
+// their order is free and the append needs no single global atomic
+constexpr uint32_t OUT_SUBS = 64;
+constexpr uint32_t OUT_STRIDE = 16;
+
 // violation record written once (first code wins) + count
 struct DevViolation {
     unsigned long long code, node, seq, iid, count;
@@ -188,8 +194,8 @@ struct DevView {
     uint32_t *store_dummy;          // 64 KiB sink for k_store's skipped (row, bucket) stores
     // outputs
     OutRec *out;
-    unsigned long long *out_cursor;
-    uint64_t out_cap;
+    unsigned long long *out_cursor;  // OUT_SUBS cursors, one per 128-byte line (stride OUT_STRIDE words)
+    uint64_t out_cap;               // records per sub-buffer: sub s owns out[s * out_cap .. (s + 1) * out_cap)
     unsigned long long *partials;   // 8 words per apply workgroup, then chosen workgroups
     DevViolation *viol;
     unsigned long long *summary;    // 64 words
