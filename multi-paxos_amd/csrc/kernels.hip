@@ -337,75 +337,90 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
 }
 
 // --------------------------------------------------------- proposer side --
-// Promise quorum per node (OnPrepareReply, multi/paxos.cpp:1036-1057): one
-// wave per node walks its P_START / PREPARE_REPLY (/ E_EPOCH) records 64 at a
-// time — each window's headers are loaded lane-parallel, the quorum state
-// machine then runs serially on wave-uniform registers, and each lane writes
-// its own record's flags.  (A lane-serial walk paid a dependent global load per
-// record: 10 ms for C3's 2^24 trace.)
+// Promise quorum per node (OnPrepareReply, multi/paxos.cpp:1036-1057; member
+// Proposer::OnPrepareReply, member/paxos.cpp:1158-1182): one wave per node over
+// its P_START / PREPARE_REPLY (/ E_EPOCH) records, 64 per window, all lanes at
+// once.  A P_START (a gated one in member) starts a round — new ballot,
+// preparing, empty promise set — and a member E_EPOCH that resets the proposer
+// ends one (idle until the next P_START); each record's round is the last such
+// head at or before it in the window, or the state carried in.  A reply
+// counts while its round is preparing and its ballot is the round's (:1038);
+// the promise set up to it is a segmented OR scan of the counted replies'
+// acceptor bits, and the round's quorum reply is its first reply whose set
+// reaches |acceptors|/2+1 (:1047) — later replies of the round are not counted.
+__device__ inline uint64_t shfl64(uint64_t x, int src)
+{
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(x >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint64_t shfl64_up(uint64_t x, uint32_t d)
+{
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, d, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __global__ __launch_bounds__(64) void k_proposer(DevView v)
 {
     const uint32_t n = blockIdx.x, lane = threadIdx.x;
     if (n >= v.N) return;
-    uint64_t ballot = 0, mask = 0;         // proposal_id_ = 0 at genesis (:338)
-    bool preparing = false;                // prepare_retry_timeout_ = NULL
+    uint64_t cb = 0, cmask = 0;            // proposal_id_ = 0 at genesis (:338)
+    bool cprep = false;                    // prepare_retry_timeout_ = NULL
     const bool member = v.semantics == MPX_SEM_MEMBER;
+    const uint64_t le = ~0ull >> (63 - lane);                  // lanes 0..lane
+    const uint64_t all_nodes = v.N >= 64 ? ~0ull : ((1ull << v.N) - 1);
     const uint64_t i0 = v.pl_off[n], i1 = v.pl_off[n + 1];
     for (uint64_t base = i0; base < i1; base += 64) {
         const uint32_t cnt = (uint32_t)(i1 - base < 64 ? i1 - base : 64);
+        const bool valid = lane < cnt;
         uint32_t g = 0, t = 0xFF, src = 0, gt = 0;
-        uint64_t b = 0, am = 0;
-        if (lane < cnt) {
+        uint64_t b = 0, am = all_nodes;
+        if (valid) {
             g = v.pl_msg[base + lane];
             t = v.m_type[g]; b = v.m_ballot[g]; src = v.m_src[g];
             if (member) {
                 gt = v.m_gate[g];
-                if (gt >> G_EPOCH_SHIFT) am = v.ep_amask[(gt >> G_EPOCH_SHIFT) - 1];
+                am = (gt >> G_EPOCH_SHIFT) ? v.ep_amask[(gt >> G_EPOCH_SHIFT) - 1] : 0;
             }
         }
-        uint32_t mine = 0;                 // flags for this lane's record
-        for (uint32_t k = 0; k < cnt; ++k) {
-            const uint32_t tk = rl32(t, k);
-            const uint64_t bk = rl64(b, k);
-            uint32_t f = 0;
-            if (member) {
-                // Proposer::OnPrepareReply, member/paxos.cpp:1158-1182: only an
-                // existing Proposer; quorum |acceptors|/2+1 of the node's epoch
-                const uint32_t gk = rl32(gt, k);
-                if (tk == MPX_MSG_E_EPOCH) {
-                    if (gk & G_PRECLR) { preparing = false; mask = 0; }
-                    continue;
-                }
-                if (!(gk >> G_EPOCH_SHIFT)) continue;
-                if (tk == MPX_MSG_P_START) { ballot = bk; preparing = true; mask = 0; continue; }
-                if (!preparing || bk != ballot) continue;                      // :1160
-                const uint64_t amk = rl64(am, k);
-                const uint32_t a = rl32(src, k);
-                if (a >= 64 || !((amk >> a) & 1)) {
-                    if (lane == 0) record_violation(v, MPX_V_BAD_NODE, n, rl32(g, k) - v.node_off[n], 0);
-                    continue;
-                }
-                f = F_COUNTED;
-                mask |= 1ull << a;
-                if ((uint32_t)__popcll(mask) >= (uint32_t)__popcll(amk) / 2 + 1) { f |= F_QUORUM; preparing = false; mask = 0; }
-            } else if (tk == MPX_MSG_P_START) {
-                ballot = bk; preparing = true; mask = 0;
-                continue;
-            } else if (preparing && bk == ballot) {      // :1038
-                const uint32_t a = rl32(src, k);
-                if (a >= v.N) {
-                    if (lane == 0) record_violation(v, MPX_V_BAD_NODE, n, rl32(g, k) - v.node_off[n], 0);
-                    continue;
-                }
-                f = F_COUNTED;
-                mask |= 1ull << a;
-                if ((uint32_t)__popcll(mask) >= v.quorum) {          // :1047
-                    f |= F_QUORUM; preparing = false; mask = 0;
-                }
-            }
-            if (lane == k) mine = f;
+        const bool gated = !member || (gt >> G_EPOCH_SHIFT) != 0;
+        const bool ps = valid && gated && t == MPX_MSG_P_START;                     // round head: preparing
+        const bool ec = valid && member && t == MPX_MSG_E_EPOCH && (gt & G_PRECLR); // round head: idle
+        const bool rep = valid && gated && t == MPX_MSG_PREPARE_REPLY;
+        const uint64_t heads = __ballot(ps || ec), psm = __ballot(ps);
+        const uint64_t hm = heads & le;
+        const int sh = hm ? 63 - __builtin_clzll(hm) : -1;                         // this record's round head
+        const uint64_t rb = sh >= 0 ? shfl64(b, sh) : cb;
+        const bool prep0 = sh >= 0 ? ((psm >> sh) & 1) != 0 : cprep;
+        const uint64_t mask0 = sh >= 0 ? 0 : cmask;
+        const bool m1 = rep && prep0 && b == rb;                                    // :1038 / :1160
+        const bool bad = m1 && (src >= 64 || !((am >> src) & 1));                  // :1040 / :1163
+        const bool match = m1 && !bad;
+        // segmented inclusive OR scan of the counted replies' acceptor bits
+        uint64_t x = match ? 1ull << src : 0;
+        bool f = ps || ec;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t y = shfl64_up(x, d);
+            const bool fy = __shfl_up((int)f, d, 64) != 0;
+            if (lane >= d && !f) { x |= y; f = f || fy; }
         }
-        if (mine) v.m_flags[g] |= (uint8_t)mine;
+        const uint64_t incl = x | mask0;
+        const uint32_t Q = member ? (uint32_t)__popcll(am) / 2 + 1 : v.quorum;
+        const bool cand = match && (uint32_t)__popcll(incl) >= Q;
+        const uint64_t cm = __ballot(cand);
+        const uint64_t seg = le & ~((sh > 0 ? (1ull << sh) : 1ull) - 1);           // lanes sh..lane (or 0..lane)
+        const uint64_t cseg = cm & seg;
+        const uint32_t fc = cseg ? (uint32_t)__builtin_ctzll(cseg) : 64;          // the round's quorum reply
+        uint32_t fl = 0;
+        if (match && fc >= lane) fl = F_COUNTED | (fc == lane ? F_QUORUM : 0);
+        if (bad && fc > lane) record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0);
+        if (fl) v.m_flags[g] |= (uint8_t)fl;
+        // carry the last record's round into the next window
+        const uint32_t L = cnt - 1;
+        if (psm) cb = rl64(b, 63 - __builtin_clzll(psm));
+        const bool prepL = rl32((uint32_t)prep0, L) && !rl32((uint32_t)(cseg != 0), L);
+        cprep = prepL;
+        cmask = prepL ? rl64(incl, L) : 0;
     }
 }
 
