@@ -344,7 +344,17 @@ static int upload_trace(mpx_engine *e)
     TRY(upload(e->e_val, h.e_val, s)); TRY(upload(e->e_slot, h.e_slot, s));
     TRY(upload(e->r_pid, h.r_pid, s)); TRY(upload(e->r_val, h.r_val, s)); TRY(upload(e->r_slot, h.r_slot, s));
     TRY(upload(e->g_a, h.g_a, s)); TRY(upload(e->g_b, h.g_b, s));
-    TRY(upload(e->f_off, h.f_off, s)); TRY(upload(e->frags, h.frags, s)); TRY(upload(e->gp_list, h.gp_list, s));
+    TRY(upload(e->f_off, h.f_off, s)); TRY(upload(e->frags, h.frags, s));
+    {   // work items of the general k_apply: {f_off[q], f_off[q + 1], ev_off[q], ev_off[q + 1], q}
+        std::vector<uint64_t> gd(GP_WORDS * h.gp_list.size(), 0);
+        for (size_t i = 0; i < h.gp_list.size(); ++i) {
+            const uint64_t q = h.gp_list[i];
+            uint64_t *w = &gd[GP_WORDS * i];
+            w[0] = h.f_off[q]; w[1] = h.f_off[q + 1]; w[2] = h.ev_off[q]; w[3] = h.ev_off[q + 1]; w[4] = q;
+        }
+        TRY(upload(e->gp_list, gd, s));
+        HTRY(hipStreamSynchronize(s));                 // gd is a local
+    }
     TRY(upload(e->ev_off, h.ev_off, s)); TRY(upload(e->ev_msg, h.ev_msg, s));
     TRY(upload(e->pl_off, h.pl_off, s)); TRY(upload(e->pl_msg, h.pl_msg, s));
     TRY(upload(e->b_msg, h.b_msg, s)); TRY(upload(e->b_pstart, h.b_pstart, s));
@@ -708,9 +718,9 @@ static int ensure_host_headers(mpx_engine *e);
 struct Results {
     std::vector<uint8_t> flags;
     std::vector<uint64_t> maxseen, scal;
-    std::vector<OutRec> out;
+    std::vector<OutEnt> out;
     std::vector<uint32_t> b_chosen;
-    std::map<uint32_t, std::vector<const OutRec *>> by_msg[2];
+    std::map<uint32_t, std::vector<const OutEnt *>> by_msg[2];
 };
 
 static int fetch_results(mpx_engine *e, Results &r)
@@ -726,17 +736,37 @@ static int fetch_results(mpx_engine *e, Results &r)
         std::vector<uint64_t> cur(OUT_STRIDE * OUT_SUBS);
         HTRY(hipMemcpy(cur.data(), e->out_cursor.p, 8 * cur.size(), hipMemcpyDeviceToHost));
         std::vector<OutRec> part;
+        const HostTrace &h = e->ht;
+        const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
         for (uint32_t s = 0; s < OUT_SUBS; ++s) {
             const uint64_t k = std::min<uint64_t>(cur[OUT_STRIDE * s], e->out_cap);
             TRY(d2h(part, e->out, k, (size_t)s * e->out_cap));
-            r.out.insert(r.out.end(), part.begin(), part.end());
+            for (const OutRec &o : part) {
+                // resolve the reference (mpx_internal.hpp OutRec) against the host trace
+                OutEnt x{o.msg, (o.aux & OUT_K1) ? 1u : 0u, 0, 0, 0};
+                if (x.kind) {
+                    if (o.ref >= h.r_iid.size()) return MPX_E_STATE;
+                    x.iid = h.r_iid[o.ref]; x.ballot = h.r_pid[o.ref]; x.handle = h.r_val[o.ref];
+                } else {
+                    if (o.ref >= h.frags.size()) return MPX_E_STATE;
+                    const Frag &f = h.frags[o.ref];
+                    const uint32_t sl = o.aux & (BS - 1);
+                    uint64_t ent = f.entry + (sl - f.start);
+                    if (!(f.flags & FR_DENSE))
+                        for (uint32_t q = 0; q < f.count; ++q)
+                            if (((h.e_iid[f.entry + q] - e->cfg.shard_begin) & (BS - 1)) == sl) { ent = f.entry + q; break; }
+                    x.iid = h.e_iid[ent]; x.handle = h.e_val[ent];
+                    x.ballot = member ? h.e_pid[ent] : h.m_ballot[f.msg];
+                }
+                r.out.push_back(x);
+            }
         }
     }
     TRY(d2h(r.b_chosen, e->b_chosen, e->ht.b_msg.size()));
     for (auto &o : r.out) r.by_msg[o.kind & 1][o.msg].push_back(&o);
     for (int k = 0; k < 2; ++k)
         for (auto &x : r.by_msg[k])
-            std::sort(x.second.begin(), x.second.end(), [](const OutRec *a, const OutRec *b) { return a->iid < b->iid; });
+            std::sort(x.second.begin(), x.second.end(), [](const OutEnt *a, const OutEnt *b) { return a->iid < b->iid; });
     return MPX_OK;
 }
 
@@ -753,7 +783,7 @@ static void reply_of(const mpx_engine *e, const Results &r, uint32_t n, uint64_t
             std::string body;
             auto it = r.by_msg[0].find((uint32_t)g);
             if (it != r.by_msg[0].end())
-                for (const OutRec *o : it->second) {
+                for (const OutEnt *o : it->second) {
                     app<uint64_t>(body, o->iid);
                     app<uint64_t>(body, o->ballot);
                     e->vt.encode(o->handle, body);
@@ -841,7 +871,7 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
             const uint64_t k = it == r.by_msg[1].end() ? 0 : it->second.size();
             app<uint64_t>(sec, k);
             if (k)
-                for (const OutRec *o : it->second) { app<uint64_t>(sec, o->iid); app<uint64_t>(sec, o->ballot); app<uint64_t>(sec, o->handle); }
+                for (const OutEnt *o : it->second) { app<uint64_t>(sec, o->iid); app<uint64_t>(sec, o->ballot); app<uint64_t>(sec, o->handle); }
             ++cnt;
         }
         app<uint64_t>(d, cnt);

@@ -508,10 +508,11 @@ __device__ inline void wave_lds_fence()
 }
 
 // Snapshot records of one event of a pair: lane l's slot j is emitted when
-// want[j]; one append (atomicAdd on the wave's sub-buffer cursor) per event.
+// want[j] (record: ref[j], aux = slot | kind); one append (atomicAdd on the
+// wave's sub-buffer cursor) per event.
 constexpr uint32_t SPL_ = 4;
-__device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uint32_t msg, uint32_t kind,
-                                 uint64_t iid0, const uint64_t (&ballot)[SPL_], const uint64_t (&handle)[SPL_])
+__device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uint32_t msg, uint32_t kind_aux,
+                                 const uint32_t (&ref)[SPL_])
 {
     const uint32_t lane = threadIdx.x & 63;
     uint64_t m[SPL_];
@@ -530,7 +531,7 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
         const uint64_t at = base + off + (uint64_t)__popcll(m[j] & below);
         if (want[j] && at < v.out_cap) {
             OutRec r;
-            r.msg = msg; r.kind = kind; r.iid = iid0 + lane + 64 * j; r.ballot = ballot[j]; r.handle = handle[j];
+            r.msg = msg; r.ref = ref[j]; r.aux = kind_aux | (lane + 64 * j);
             v.out[(uint64_t)sub * v.out_cap + at] = r;
         }
         off += (uint32_t)__popcll(m[j]);
@@ -1229,7 +1230,8 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
 // checks when the two entry indices differ (the pool is content-addressed, so a
 // duplicate or retried COMMIT carries the same entries), and the snapshots a
 // granted PREPARE or a promise quorum emits.
-template <int WAVES_PER_EU>
+// DIGEST: the digested verification run (mpx_run) — the only user of the slot's ballot
+template <int WAVES_PER_EU, bool DIGEST>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 {
     __shared__ uint16_t lidx_all[4][BS];
@@ -1246,20 +1248,17 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     const bool member = v.semantics == MPX_SEM_MEMBER;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
-    const uint64_t *__restrict__ f_off = v.f_off;
-    const uint64_t *__restrict__ ev_off = v.ev_off;
     constexpr uint32_t S_PRESENT = 1, S_COMMITTED = 2;
 
-    // work list: the pairs the lean kernel does not take (ingest.cpp)
+    // work list: the pairs the lean kernel does not take (ingest.cpp), GP_WORDS
+    // per item.  Three-stage software pipeline over this wave's items, issued at
+    // the top of item i so each stage's loads had a whole item to land: (1) the
+    // item's CSR ranges three items ahead, (2) its first descriptor window two
+    // ahead, (3) that window's scan flags one ahead — one wait per item.
     auto rt1 = [&](uint64_t i) -> uint64_t {
         if (i >= v.num_gp || lane > 4) return 0;
-        const uint64_t q = v.gp_list[i];                // pair, bucket-major
-        if (lane == 4) return q;
-        return lane < 2 ? f_off[q + lane] : ev_off[q + lane - 2];
+        return v.gp_list[GP_WORDS * i + lane];          // lanes 0..4: fi, fe, ei, ee, q
     };
-    // software pipeline over this wave's work items: (1) CSR offsets two
-    // items ahead, (2) first descriptor window one item ahead, (3) flags +
-    // ballots of the current item
     struct Win { uint64_t fw0, fw1; uint32_t evm; };
     auto rt2 = [&](uint64_t off) -> Win {
         Win w{0, NONE32, NONE32};
@@ -1271,49 +1270,64 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         if (lane < ee - ei && lane < 64) w.evm = v.ev_msg[ei + lane];
         return w;
     };
+    struct Flg { uint32_t fflag, einfo; uint64_t fbal; };
+    auto rt3 = [&](const Win &w) -> Flg {
+        Flg f{0, 0, 0};
+        if ((uint32_t)w.fw1 != NONE32) {
+            f.fflag = v.m_flags[(uint32_t)w.fw1];
+            if (DIGEST) f.fbal = v.m_ballot[(uint32_t)w.fw1];
+        }
+        if (w.evm != NONE32) f.einfo = (uint32_t)v.m_type[w.evm] | ((uint32_t)v.m_flags[w.evm] << 8);
+        return f;
+    };
     uint64_t it = (uint64_t)blockIdx.x * 4 + wv;
-    uint64_t off_cur = rt1(it);
-    uint64_t off_nxt = rt1(it + stride);
-    Win win_nxt = rt2(off_cur);
+    uint64_t off0 = rt1(it), off1 = rt1(it + stride), off2 = rt1(it + 2 * stride);
+    Win win0 = rt2(off0), win1 = rt2(off1);
+    Flg flg0 = rt3(win0);
     for (; it < v.num_gp; it += stride) {
-        const uint64_t q = rl64(off_cur, 4);
+        const uint64_t off_c = off0;
+        const Win win = win0;
+        const Flg flg = flg0;
+        flg0 = rt3(win1);                        // item i + 1
+        win0 = win1; win1 = rt2(off2);           // item i + 2
+        off0 = off1; off1 = off2; off2 = rt1(it + 3 * stride);   // item i + 3
+        const uint64_t q = rl64(off_c, 4);
         const uint32_t b = (uint32_t)(q / v.N);
         const uint32_t n = (uint32_t)(q - (uint64_t)b * v.N);
-        uint64_t fi = rl64(off_cur, 0), fe = rl64(off_cur, 1), ei = rl64(off_cur, 2), ee = rl64(off_cur, 3);
+        uint64_t fi = rl64(off_c, 0), fe = rl64(off_c, 1), ei = rl64(off_c, 2), ee = rl64(off_c, 3);
         const uint64_t pbase = fi;               // the pair's first fragment (slots are pair-local)
-        Win win = win_nxt;
-        win_nxt = rt2(off_nxt);                  // next item's descriptors in flight
-        off_cur = off_nxt;
-        off_nxt = rt1(it + 2 * stride);
         const uint64_t li0 = (uint64_t)b << BSH;
-        uint64_t sb[SPL];                        // ballot (multi: accept / commit id; member: proposal id)
-        uint32_t sf[SPL], se[SPL], sm[SPL];      // S_* flags, Value entry index, fixing fragment + 1
+        uint64_t sb[DIGEST ? SPL : 1];           // ballot (multi: accept / commit id; member: proposal id)
+        uint32_t sfl = 0;                        // S_* flags of slot j in byte j
+        uint32_t se[SPL], sm[SPL];               // Value entry index, fixing fragment + 1
+#define SF(j) ((sfl >> (8 * (j))) & 0xFF)
+#define SF_SET(j, x) (sfl = (sfl & ~(0xFFu << (8 * (j)))) | ((uint32_t)(x) << (8 * (j))))
 #pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) { sb[j] = 0; sf[j] = se[j] = sm[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
+        for (uint32_t j = 0; j < SPL; ++j) { if (DIGEST) sb[j] = 0; se[j] = sm[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
 
         bool first = true;
         while (fi < fe || ei < ee) {
             const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
             const uint32_t ne = (uint32_t)(ee - ei < 64 ? ee - ei : 64);
-            // (2) descriptors, one per lane (prefetched for the first window)
+            // descriptors (one per lane) and their scan flags: the pipelined
+            // first window, then loaded here for the rare longer pairs
             uint64_t fw0 = win.fw0, fw1 = win.fw1;
             uint32_t evm = win.evm;
+            uint32_t fflag = flg.fflag, einfo = flg.einfo;
+            uint64_t fbal = flg.fbal;
             if (!first) {
-                fw0 = 0; fw1 = NONE32;
+                Win w2{0, NONE32, NONE32};
                 if (lane < nf) {
                     const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
-                    fw0 = x.x; fw1 = x.y;
+                    w2.fw0 = x.x; w2.fw1 = x.y;
                 }
-                evm = lane < ne ? v.ev_msg[ei + lane] : NONE32;
+                if (lane < ne) w2.evm = v.ev_msg[ei + lane];
+                const Flg f2 = rt3(w2);
+                fw0 = w2.fw0; fw1 = w2.fw1; evm = w2.evm;
+                fflag = f2.fflag; einfo = f2.einfo; fbal = f2.fbal;
             }
             first = false;
-            // (3) scan results and ballots of those messages
             const uint32_t fmsg = (uint32_t)fw1;
-            uint32_t fflag = 0;
-            uint64_t fbal = 0;
-            if (lane < nf) { fflag = v.m_flags[fmsg]; fbal = v.m_ballot[fmsg]; }
-            uint32_t einfo = 0;
-            if (lane < ne) einfo = (uint32_t)v.m_type[evm] | ((uint32_t)v.m_flags[evm] << 8);
             // merge-walk fragments and events by message index
             uint32_t a = 0, c = 0;
             for (;;) {
@@ -1326,7 +1340,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                     const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
                     const uint32_t fl = (uint32_t)(w1 >> 56), kind = fl >> 4;
                     const uint32_t mf = rl32(fflag, a);
-                    const uint64_t ballot = rl64(fbal, a);
+                    const uint64_t ballot = DIGEST ? rl64(fbal, a) : 0;
                     const bool dense = fl & FR_DENSE;
                     const uint32_t fq = (uint32_t)(fi + a + 1);
                     int k[SPL];
@@ -1343,15 +1357,15 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                             for (uint32_t j = 0; j < SPL; ++j) {
                                 if (k[j] < 0) continue;
                                 const uint32_t x = (uint32_t)(ent + k[j]);
-                                if (sf[j] & S_COMMITTED) {
+                                if (SF(j) & S_COMMITTED) {
                                     if (se[j] != x && e_val[se[j]] != e_val[x] && (!learn || (mf & F_PROP)))
                                         record_violation(v, MPX_V_LEARN_VALUE, n, seq, v.shard_begin + li0 + lane + 64 * j);
                                 } else if (learn) {
-                                    sb[j] = v.e_pid[x];
-                                    sf[j] = S_PRESENT | S_COMMITTED; se[j] = x; sm[j] = fq;
-                                } else if (!(sf[j] & S_PRESENT)) {
-                                    sb[j] = v.e_pid[x];
-                                    sf[j] = S_PRESENT; se[j] = x; sm[j] = fq;
+                                    if (DIGEST) sb[j] = v.e_pid[x];
+                                    SF_SET(j, S_PRESENT | S_COMMITTED); se[j] = x; sm[j] = fq;
+                                } else if (!(SF(j) & S_PRESENT)) {
+                                    if (DIGEST) sb[j] = v.e_pid[x];
+                                    SF_SET(j, S_PRESENT); se[j] = x; sm[j] = fq;
                                     ++cA;
                                 }
                                 cL += learn;
@@ -1361,9 +1375,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                         if (mf & F_GRANTED) {
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
-                                if (k[j] >= 0 && !(sf[j] & S_COMMITTED)) {           // :1380
-                                    sb[j] = ballot;                                   // :1387
-                                    sf[j] = S_PRESENT; se[j] = (uint32_t)(ent + k[j]); sm[j] = fq;
+                                if (k[j] >= 0 && !(SF(j) & S_COMMITTED)) {           // :1380
+                                    if (DIGEST) sb[j] = ballot;                                   // :1387
+                                    SF_SET(j, S_PRESENT); se[j] = (uint32_t)(ent + k[j]); sm[j] = fq;
                                     ++cA;
                                 }
                         }
@@ -1372,13 +1386,13 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                         for (uint32_t j = 0; j < SPL; ++j)
                             if (k[j] >= 0) {
                                 const uint32_t x = (uint32_t)(ent + k[j]);
-                                if (sf[j] & S_COMMITTED) {                            // :1508
+                                if (SF(j) & S_COMMITTED) {                            // :1508
                                     if (se[j] != x && e_val[se[j]] != e_val[x])
                                         record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
                                                          v.shard_begin + li0 + lane + 64 * j);
                                 } else {
-                                    sb[j] = ballot;                                   // :1515
-                                    sf[j] = S_PRESENT | S_COMMITTED; se[j] = x; sm[j] = fq;
+                                    if (DIGEST) sb[j] = ballot;                                   // :1515
+                                    SF_SET(j, S_PRESENT | S_COMMITTED); se[j] = x; sm[j] = fq;
                                 }
                                 ++cL;
                             }
@@ -1401,7 +1415,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                     if (t8 == MPX_MSG_PREPARE && !(v.knobs & 4096)) {   // knob 4096: experiment, no snapshots
                         bool have = false;
 #pragma unroll
-                        for (uint32_t j = 0; j < SPL; ++j) have |= (sf[j] & S_PRESENT) != 0;
+                        for (uint32_t j = 0; j < SPL; ++j) have |= (SF(j) & S_PRESENT) != 0;
                         if ((fl & F_GRANTED) && __ballot(have)) {
                             // FilterAcceptedValues over the prepare's ranges (:902-922);
                             // ranges sorted by start and disjoint (ingest): one
@@ -1428,14 +1442,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                     hit[j] |= iid >= ra && iid < rb;
                                 }
                             }
-                            uint64_t hv[SPL];
+                            uint32_t ref[SPL];
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j) {
-                                hit[j] = hit[j] && li0 + lane + 64 * j < v.shard_len && (sf[j] & S_PRESENT);
-                                hv[j] = hit[j] ? e_val[se[j]] : 0;
+                                hit[j] = hit[j] && li0 + lane + 64 * j < v.shard_len && (SF(j) & S_PRESENT);
+                                ref[j] = sm[j] - 1;                 // the fixing fragment (global)
                                 cP += hit[j];
                             }
-                            emit_rows(v, hit, g, 0, blo, sb, hv);
+                            emit_rows(v, hit, g, 0, ref);
                         }
                     } else if (t8 == MPX_MSG_P_START || (t8 == MPX_MSG_E_EPOCH && (fl & F_PRECLR))) {
 #pragma unroll
@@ -1443,27 +1457,26 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                         if (t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
-                                if (!(sf[j] & S_COMMITTED)) { sb[j] = 0; sf[j] = se[j] = sm[j] = 0; }
+                                if (!(SF(j) & S_COMMITTED)) { if (DIGEST) sb[j] = 0; SF_SET(j, 0); se[j] = sm[j] = 0; }
                         }
                     } else if (t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
                         // the Acceptor is deleted / recreated: its accepted values go
                         // (member/paxos.cpp:1952-1957); learned ones stay with the Learner
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j)
-                            if (!(sf[j] & S_COMMITTED)) { sb[j] = 0; sf[j] = se[j] = sm[j] = 0; }
+                            if (!(SF(j) & S_COMMITTED)) { if (DIGEST) sb[j] = 0; SF_SET(j, 0); se[j] = sm[j] = 0; }
                     } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
                         bool hit[SPL];
-                        uint64_t pb[SPL], hv[SPL];
+                        uint32_t ref[SPL];
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) {
                             const u64x2 cur = pre[lane + 64 * j];
                             hit[j] = li0 + lane + 64 * j < v.shard_len && cur.y;
-                            pb[j] = cur.x;
-                            hv[j] = hit[j] ? v.r_val[cur.y & ~W_PRESENT] : 0;
+                            ref[j] = (uint32_t)(cur.y & ~W_PRESENT);                 // the PREPARE_REPLY entry
                             cQ += hit[j];
                             pre[lane + 64 * j] = u64x2{0, 0};                        // :1105
                         }
-                        emit_rows(v, hit, g, 1, v.shard_begin + li0, pb, hv);
+                        emit_rows(v, hit, g, OUT_K1, ref);
                     }
                     ++c;
                 }
@@ -1473,14 +1486,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         }
         bool have = false;
 #pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) have |= sf[j] != 0;
+        for (uint32_t j = 0; j < SPL; ++j) have |= SF(j) != 0;
         if (__ballot(have)) {
 #pragma unroll
             for (uint32_t j = 0; j < SPL; ++j) {
                 const uint64_t li = li0 + lane + 64 * j;
                 if (li < v.shard_len) st_put(v, (uint64_t)n * v.shard_len + li, sm[j] ? (uint32_t)(sm[j] - pbase) : 0);
-                if (sf[j] && v.digest)
-                    dig += state_digest(n, v.shard_begin + li, (sf[j] & S_COMMITTED) ? 2 : 1, sb[j], e_val[se[j]]);
+                if (DIGEST && SF(j))
+                    dig += state_digest(n, v.shard_begin + li, (SF(j) & S_COMMITTED) ? 2 : 1, sb[DIGEST ? j : 0], e_val[se[j]]);
             }
             if (lane == 0) v.st_valid[(uint64_t)n * v.NB + b] = 1;
         }
@@ -1504,6 +1517,8 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
         const int slot = t == 0 ? PC_A : t == 1 ? PC_L : t == 2 ? PC_P : t == 3 ? PC_Q : PC_DSTATE;
         v.partials[8 * blockIdx.x + slot] += s;
     }
+#undef SF
+#undef SF_SET
 }
 
 // Chosen log, one wave per bucket, for the buckets k_apply_fast did not
@@ -1796,7 +1811,9 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (v.semantics == MPX_SEM_MEMBER) {
         // member: every pair walks the general kernel (insert semantics, epoch events)
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-        if (v.num_gp) hipLaunchKernelGGL((k_apply<1>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+                   else if (g.variant == 4) hipLaunchKernelGGL((k_apply<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+                   else hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); }
     } else {
         // multi: the lean kernel also writes the chosen log of clean buckets
         // digest runs (verification) take their own instantiation, so the
@@ -1817,7 +1834,9 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         }
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-        if (v.num_gp) hipLaunchKernelGGL((k_apply<1>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+                   else if (g.variant == 4) hipLaunchKernelGGL((k_apply<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+                   else hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); }
     }
     if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);

@@ -100,9 +100,23 @@ struct Frag {
 };
 static_assert(sizeof(Frag) == 16, "Frag is 16 bytes");
 
-// snapshot output record: an entry of a granted PREPARE_REPLY (kind 0) or of
-// a promise-quorum merged map (kind 1)
+// snapshot output record (12 bytes): an entry of a granted PREPARE_REPLY
+// (kind 0: FilterAcceptedValues, multi/paxos.cpp:902-922) or of a
+// promise-quorum merged map (kind 1: :1047-1105), by reference to the resident
+// trace — the host resolves iid, tag and Value (fetch_results):
+//   kind 0: ref = global index of the fragment that fixed the slot, aux = slot
+//           in its bucket (the entry at that slot: iid, Value; its message's
+//           ballot, member: the entry's proposal id)
+//   kind 1: ref = PREPARE_REPLY entry index (r_iid, r_pid, r_val), aux = OUT_K1
 struct OutRec {
+    uint32_t msg;
+    uint32_t ref;
+    uint32_t aux;
+};
+static_assert(sizeof(OutRec) == 12, "OutRec is 12 bytes");
+constexpr uint32_t OUT_K1 = 0x100;
+// host form of a snapshot record
+struct OutEnt {
     uint32_t msg;
     uint32_t kind;
     uint64_t iid;
@@ -114,6 +128,7 @@ struct OutRec {
 // to sub (wave id mod OUT_SUBS) — the host sorts records by message and iid, so
 // their order is free and the append needs no single global atomic
 constexpr uint32_t OUT_SUBS = 64;
+constexpr uint32_t GP_WORDS = 8;
 constexpr uint32_t OUT_STRIDE = 16;
 
 // violation record written once (first code wins) + count
@@ -168,7 +183,8 @@ struct DevView {
     const uint64_t *f_off;          // N*NB+1, pair q = bucket * N + node
     const Frag *frags;
     uint64_t num_gp;                // pairs for the general apply kernel
-    const uint64_t *gp_list;
+    const uint64_t *gp_list;        // general-apply work items, GP_WORDS each: the pair's fragment CSR
+                                    // range, its event CSR range, the pair q (one coalesced load per item)
     const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
     const uint32_t *ev_msg;
     const uint64_t *pl_off;         // N+1

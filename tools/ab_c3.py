@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--log2", type=int, default=22)
     ap.add_argument("--knobs", default="0")
     ap.add_argument("--wgs", default="8")
+    ap.add_argument("--variants", default="0", help="MPX_APPLY_VARIANT values (4: k_apply at 4 waves/SIMD)")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=3)
     a = ap.parse_args()
@@ -28,23 +29,25 @@ def main():
     del t
     base = e.run()
     e.timings()
-    arms = [(k, w) for k in a.knobs.split(",") for w in a.wgs.split(",")]
+    arms = [(k, w, x) for k in a.knobs.split(",") for w in a.wgs.split(",") for x in a.variants.split(",")]
     res = {arm: [] for arm in arms}
     for _ in range(a.rounds):
-        for k, w in arms:
+        for k, w, x in arms:
             os.environ["MPX_KNOBS"] = k
             os.environ["MPX_APPLY_WGS_PER_CU"] = w
+            os.environ["MPX_APPLY_VARIANT"] = x
             for _ in range(a.steps):
                 e.step()
             e.sync()
-            res[(k, w)].extend(e.timings_detail())
+            res[(k, w, x)].extend(e.timings_detail())
     os.environ["MPX_KNOBS"] = "0"
+    os.environ["MPX_APPLY_VARIANT"] = "0"
     chk = e.run()
     assert chk["state_digest"] == base["state_digest"]
     for arm in arms:
         ph = res[arm]
         med = {p: statistics.median(x[p] for x in ph) for p in mpx.Engine.PHASES}
-        print("knobs %s wgs/cu %s: " % arm + " ".join("%s %.3f" % (p, med[p]) for p in mpx.Engine.PHASES), flush=True)
+        print("knobs %s wgs/cu %s variant %s: " % arm + " ".join("%s %.3f" % (p, med[p]) for p in mpx.Engine.PHASES), flush=True)
 
 
 if __name__ == "__main__":

@@ -11,6 +11,7 @@ The result goes to gpurun_out/pmc/<tag>_pmc.json; committed copies live in
 profiles/, where bench.py picks them up as roofline.traffic.
 
     python tools/pmc_traffic.py --tag r01 [bench args...]
+    python tools/pmc_traffic.py --tag r02_c3 --c3 --sq     (C3 general path, + SQ wave-state pass)
 """
 import argparse
 import csv
@@ -21,24 +22,29 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# one pass: at most 8 SQ counters (MI355X_MICROARCH.md §rocprofv3 PMC slots); WAIT_ANY +
+# WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES (quad-cycles)
+SQ_COUNTERS = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+               "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VALU", "SQ_INSTS_SALU"]
 
 
-def run_pass(counter, outdir, bench_args):
-    d = os.path.join(outdir, "pmc_" + counter.lower())
-    cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", counter, "-d", d, "-o", "pmc",
+def run_pass(counters, outdir, bench_args, tag):
+    """One rocprofv3 --pmc pass (kernel trace only); {counter: {kernel: [values per dispatch]}}."""
+    d = os.path.join(outdir, "%s_pmc_%s" % (tag, "_".join(c.lower() for c in counters)))
+    cmd = ["timeout", "-s", "KILL", "400", "rocprofv3", "--pmc"] + counters + ["-d", d, "-o", "pmc",
            "--output-format", "csv", "--", sys.executable, os.path.join(ROOT, "bench.py"),
            "--no-cpu-baseline"] + bench_args
     subprocess.check_call(cmd, cwd=ROOT)
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit("no counter_collection.csv under " + d)
-    vals = {}
+    vals = {c: {} for c in counters}
     with open(files[0]) as f:
         for row in csv.DictReader(f):
-            if row.get("Counter_Name") != counter:
+            c = row.get("Counter_Name")
+            if c not in vals:
                 continue
-            name = row.get("Kernel_Name", "")
-            vals.setdefault(name, []).append(float(row["Counter_Value"]))
+            vals[c].setdefault(row.get("Kernel_Name", ""), []).append(float(row["Counter_Value"]))
     return vals
 
 
@@ -48,21 +54,35 @@ def main():
     ap.add_argument("--outdir", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     ap.add_argument("--instances", type=int, default=1 << 27)
     ap.add_argument("--nodes", type=int, default=9)
+    ap.add_argument("--c3", action="store_true", help="the C3 general-path leg (bench.py --c3-only)")
+    ap.add_argument("--sq", action="store_true", help="also one pass of SQ wave-state counters")
     a, rest = ap.parse_known_args()
-    bench_args = ["--steps", "3", "--warmup", "0", "--instances", str(a.instances), "--nodes", str(a.nodes)] + rest
-    fetch = run_pass("FETCH_SIZE", a.outdir, bench_args)
-    write = run_pass("WRITE_SIZE", a.outdir, bench_args)
-    out = {"tag": a.tag, "instances": a.instances, "nodes": a.nodes, "gpus": 1, "kernels": {}}
+    if a.c3:
+        bench_args = ["--c3-only", "--c3-steps", "3"] + rest
+    else:
+        bench_args = ["--steps", "3", "--warmup", "0", "--instances", str(a.instances), "--nodes", str(a.nodes),
+                      "--c3-instances", "0"] + rest
+    fetch = run_pass(["FETCH_SIZE"], a.outdir, bench_args, a.tag)["FETCH_SIZE"]
+    write = run_pass(["WRITE_SIZE"], a.outdir, bench_args, a.tag)["WRITE_SIZE"]
+    sq = run_pass(SQ_COUNTERS, a.outdir, bench_args, a.tag) if a.sq else {}
+    out = {"tag": a.tag, "workload": "C3 2^24 x 7 (bench.py --c3-only)" if a.c3 else "C4",
+           "instances": a.instances, "nodes": a.nodes, "gpus": 1, "kernels": {}}
+    mean = lambda xs: sum(xs) / len(xs) if xs else 0.0
     for name in sorted(set(fetch) | set(write)):
         f = fetch.get(name, [0.0])
         w = write.get(name, [0.0])
-        fk, wk = sum(f) / len(f), sum(w) / len(w)
+        fk, wk = mean(f), mean(w)
         out["kernels"][name] = {"dispatches": len(f), "FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk,
                                 "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024}
+        for c, per in sq.items():
+            if name in per:
+                out["kernels"][name][c] = mean(per[name])
     # the timed apply phase: k_plan + k_store + k_apply_fast<1, false, true>
     # (digest runs use the one-kernel k_apply_fast<..., true, false>)
+    # C3 adds the general k_apply (its digested-run dispatch averages in; digests are a few loads per slot)
     phase = [v for k, v in out["kernels"].items()
-             if "k_plan" in k or "k_store" in k or ("k_apply_fast" in k and "true>" in k and "false" in k)]
+             if "k_plan" in k or "k_store" in k or ("k_apply_fast" in k and "true>" in k and "false" in k)
+             or (a.c3 and "k_apply<" in k)]
     out["apply_phase_kernels"] = [k for k, v in out["kernels"].items() if v in phase]
     out["hbm_bytes_per_launch"] = sum(v["hbm_bytes_per_launch"] for v in phase) if phase else None
     out["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"
