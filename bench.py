@@ -129,6 +129,7 @@ def c3_leg(args):
     apply_ms = general_ms + fast_ms
     b_alg = 16 * st["promise_entries"] + 24 * st["accept_apps"] + 16 * st["commit_apps"]
     achieved = b_alg / (apply_ms * 1e-3) / 1e9 if apply_ms else 0.0
+    pmc = latest_pmc(7, m, 1, workload="C3")
     ms_step = dt / args.c3_steps * 1e3
     return {
         "workload": "C3: 2^%d instances x 7 acceptors, 3 competing proposers, drop 5%% / dup 10%% (<=3) / "
@@ -142,7 +143,11 @@ def c3_leg(args):
                                                "clean pairs)",
                      "bytes_alg_per_launch": b_alg, "bytes_model": "SURVEY §8(d): 16 P + 24 A + 16 L",
                      "kernel_ms": apply_ms, "general_ms": general_ms, "fast_ms": fast_ms,
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS},
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                     "traffic_source": ("profiles/%s_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the apply "
+                                        "phase, bench.py --c3-only; not measured inside this process)" % pmc["tag"])
+                     if pmc else None},
         "verified": {"step_state_digest_vs_run": step_ok, "state_digest": chk["state_digest"],
                      "chosen_digest": chk["chosen_digest"]},
         "host": {"generate_s": t_gen, "ingest_s": t_ingest, "upload_and_first_run_s": t_first,
@@ -187,8 +192,8 @@ def broadcast_bytes(pg, data, rank):
     return obj[0]
 
 
-def latest_pmc(n_nodes, instances, world):
-    """HBM bytes per k_apply launch from the newest profiles/*pmc*.json of this config."""
+def latest_pmc(n_nodes, instances, world, workload="C4"):
+    """HBM bytes per apply-phase launch from the newest profiles/*pmc*.json of this config."""
     best = None
     def natural(path):                              # r01_v10 after r01_v9
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
@@ -198,7 +203,10 @@ def latest_pmc(n_nodes, instances, world):
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("nodes") == n_nodes and d.get("instances") == instances and d.get("gpus", 1) == world:
+        if d.get("workload", "C4").split()[0] != workload:
+            continue
+        if workload == "C3" or (d.get("nodes") == n_nodes and d.get("instances") == instances and
+                                d.get("gpus", 1) == world):
             best = d
     return best
 
@@ -255,6 +263,33 @@ def cpu_baseline(args, budget_s):
                       "%d instances x %d passes x %d threads, accept+commit (OnAccept/OnCommit), %.1f s wall; "
                       "decisions/s = acceptor-instance applications/s / N=%d" % (sample_m, reps, threads, dt, args.nodes),
             "node_instance_apps_per_s": apps / dt}
+
+
+def cpu_port_baseline(args, budget_s):
+    """The build's own CPU restatement (oracle/mpx_oracle.c, gcc -O2) over a clean
+    C4-shaped trace on the host's cores: every node's stream on its own thread, instance shards
+    in parallel (mpxo_run_sharded), counters + digests only.  Not -march=native: the checker is
+    built in the build container and runs on the GPU box's host, whose CPU may differ."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracles import oracle_run_sharded
+    sample_m = 1 << 18
+    trace = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=args.nodes, num_instances=sample_m, batch=256, copy=False)
+    cores = max(1, min(16, os.cpu_count() or 1))      # the box's CPU share per GPU (16)
+    shards = max(1, cores // args.nodes)
+    t0 = time.perf_counter()
+    st = oracle_run_sharded(trace, shards=shards, threads=shards)
+    one = time.perf_counter() - t0
+    assert st[0] == sample_m
+    reps = max(1, int(budget_s / max(one, 1e-6)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        oracle_run_sharded(trace, shards=shards, threads=shards)
+    dt = time.perf_counter() - t0
+    return {"value": reps * sample_m / dt, "unit": "decisions/s", "cores": shards * args.nodes, "kind": "port",
+            "sample": "oracle/mpx_oracle.c (the build's C restatement, -O2) over a clean C4-shaped trace of %d "
+                      "instances x %d acceptors, every node's stream on its own thread x %d instance shards, "
+                      "%d passes in %.1f s (nproc here: %d; 16 = this GPU's host CPU share)"
+                      % (sample_m, args.nodes, shards, reps, dt, os.cpu_count() or 0)}
 
 
 def main():
@@ -322,12 +357,15 @@ def main():
     achieved = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
     pmc = latest_pmc(N, M, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    traffic_src = ("profiles/%s_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of this command, "
+                   "committed; not measured inside this process)" % pmc["tag"]) if pmc else None
 
     out = None
     if rank == 0:
-        cpu = None
+        cpu = cpu_port = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, args.cpu_seconds)
+            cpu_port = cpu_port_baseline(args, args.cpu_seconds / 2)
         c3 = c3_leg(args) if world == 1 and args.c3_instances else None
         out = {
             "metric": METRIC,
@@ -348,12 +386,22 @@ def main():
                        "instances": M, "acceptors": N, "batch": 256, "shard_per_gpu": se - sb,
                        "parallelism": "instance-shard x%d (RCCL all-gather of 64-word summaries)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "apply phase: k_plan + k_store + k_apply_fast<1,false,true>",
                          "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_min,
+                         "bytes_model": "DESIGN.md §4: 1-B slot per (acceptor, instance) + 1-B chosen log + "
+                                        "16-B descriptors + 4-B plan words",
                          "bytes_survey_model_per_launch": bytes_survey,
-                         "survey_model_gbps": bytes_survey / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0},
+                         "survey_model_gbps": bytes_survey / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0,
+                         "frac_survey_model": bytes_survey / (apply_mean * 1e-3) / 1e9 / HBM_PEAK_GBS
+                         if apply_mean else 0.0,
+                         "note": "the clean trace fixes every (acceptor, bucket) pair with one full run, so its apply "
+                                 "phase reduces to one plan word per pair and a byte stream of slots (k_store8): the "
+                                 "survey model's 360 B/instance (16-B slot writes + per-acceptor Value reads) are "
+                                 "never moved, and frac_survey_model > 1 measures representation, not bandwidth; "
+                                 "c3.roofline is the per-slot general path on the survey's bytes"},
             "cpu_baseline": cpu,
+            "cpu_baseline_port": cpu_port,
             "c3": c3,
             "verified": {"step_state_digest_vs_closed_form": step_ok, "step_state_digest": step_state,
                          "step_chosen_digest": step_chosen, "run_digests_vs_closed_form": verified,
