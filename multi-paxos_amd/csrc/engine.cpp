@@ -74,6 +74,7 @@ struct mpx_engine {
     DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, pair_ev, m_flags, m_maxseen;
     DevBuf m_gate, e_pid, ep_amask;
     DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
+    DevBuf sc_type, sc_key, sc_idx, b_rbal, b_rsrc, b_bal;
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
     DevBuf f_off, frags, gp_list, ev_off, ev_msg, pl_off, pl_msg;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
@@ -335,7 +336,9 @@ static int upload_trace(mpx_engine *e)
     TRY(upload(e->m_ent, h.m_ent, s)); TRY(upload(e->m_cnt, h.m_cnt, s));
     TRY(upload(e->m_node, h.m_node, s)); TRY(upload(e->node_off, h.node_off, s));
     TRY(upload(e->pair_ev, h.pair_ev, s));
-    TRY(e->m_flags.alloc(std::max<size_t>(h.m_type.size(), 8)));
+    TRY(upload(e->m_flags, h.m_flags0, s));             // static flags; the steps rewrite the dynamic ones
+    TRY(upload(e->sc_type, h.sc_type, s)); TRY(upload(e->sc_key, h.sc_key, s)); TRY(upload(e->sc_idx, h.sc_idx, s));
+    TRY(upload(e->b_rbal, h.b_rbal, s)); TRY(upload(e->b_rsrc, h.b_rsrc, s)); TRY(upload(e->b_bal, h.b_bal, s));
     TRY(e->m_maxseen.alloc(std::max<size_t>(h.m_type.size() * 8, 8)));
     TRY(upload(e->chunk_node, h.chunk_node, s)); TRY(upload(e->chunk_beg, h.chunk_beg, s));
     TRY(upload(e->chunk_end, h.chunk_end, s)); TRY(upload(e->node_chunk_off, h.node_chunk_off, s));
@@ -385,6 +388,8 @@ static int upload_trace(mpx_engine *e)
     v.num_batches = (uint32_t)h.b_msg.size();
     v.b_msg = e->b_msg.as<uint32_t>(); v.b_pstart = e->b_pstart.as<uint32_t>();
     v.b_rep_off = e->b_rep_off.as<uint64_t>(); v.b_rep = e->b_rep.as<uint32_t>();
+    v.b_rbal = e->b_rbal.as<uint64_t>(); v.b_rsrc = e->b_rsrc.as<uint32_t>(); v.b_bal = e->b_bal.as<uint64_t>();
+    v.sc_type = e->sc_type.as<uint8_t>(); v.sc_key = e->sc_key.as<uint64_t>(); v.sc_idx = e->sc_idx.as<uint32_t>();
     v.b_chosen = e->b_chosen.as<uint32_t>();
     v.cf_off = e->cf_off.as<uint64_t>(); v.cfrags = e->cfrags.as<Frag>();
     {
@@ -957,13 +962,15 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     h.N = N; h.NB = e->NB; h.shard_begin = sb; h.shard_len = L;
     h.node_off.resize(N + 1);
     for (uint32_t n = 0; n <= N; ++n) h.node_off[n] = n == 0 ? 0 : G0 + (uint64_t)(n - 1) * G1;
+    // header-scan stream: per node its PREPARE and K ACCEPTs (gen_device.hip k_gen_scan)
     h.node_chunk_off.assign(N + 1, 0);
     for (uint32_t n = 0; n < N; ++n) {
         h.node_chunk_off[n] = (uint32_t)h.chunk_node.size();
-        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; g += SCAN_CHUNK) {
+        const uint64_t a = (uint64_t)n * (K + 1), b = a + K + 1;
+        for (uint64_t g = a; g < b; g += SCAN_CHUNK) {
             h.chunk_node.push_back(n);
             h.chunk_beg.push_back(g);
-            h.chunk_end.push_back(std::min<uint64_t>(g + SCAN_CHUNK, h.node_off[n + 1]));
+            h.chunk_end.push_back(std::min<uint64_t>(g + SCAN_CHUNK, b));
         }
     }
     h.node_chunk_off[N] = (uint32_t)h.chunk_node.size();
@@ -979,6 +986,11 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     TRY(e->m_type.alloc(G)); TRY(e->m_src.alloc(4 * G)); TRY(e->m_ballot.alloc(8 * G)); TRY(e->m_aux.alloc(8 * G));
     TRY(e->m_ent.alloc(8 * G)); TRY(e->m_cnt.alloc(4 * G)); TRY(e->m_node.alloc(4 * G));
     TRY(e->m_flags.alloc(G)); TRY(e->m_maxseen.alloc(8 * G));
+    HTRY(hipMemsetAsync(e->m_flags.p, 0, G, s));          // no static flags: every source is a node
+    TRY(e->sc_type.alloc((uint64_t)N * (K + 1))); TRY(e->sc_key.alloc(8 * (uint64_t)N * (K + 1)));
+    TRY(e->sc_idx.alloc(4 * (uint64_t)N * (K + 1)));
+    TRY(e->b_rbal.alloc(8 * (uint64_t)N * K + 8)); TRY(e->b_rsrc.alloc(4 * (uint64_t)N * K + 4));
+    TRY(e->b_bal.alloc(8 * K + 8));
     TRY(upload(e->node_off, h.node_off, s));
     TRY(e->pair_ev.alloc(std::max<uint64_t>((uint64_t)N * e->NB, 8)));
     HTRY(hipMemsetAsync(e->pair_ev.p, 0, e->pair_ev.bytes, s));
@@ -1003,7 +1015,9 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
                          e->m_node.as<uint32_t>(), e->e_val.as<uint64_t>(), e->frags.as<Frag>(),
                          e->f_off.as<uint64_t>(), e->b_msg.as<uint32_t>(), e->b_pstart.as<uint32_t>(),
                          e->b_rep_off.as<uint64_t>(), e->b_rep.as<uint32_t>(), e->cf_off.as<uint64_t>(),
-                         e->cfrags.as<Frag>()) != 0)
+                         e->cfrags.as<Frag>(), e->sc_type.as<uint8_t>(), e->sc_key.as<uint64_t>(),
+                         e->sc_idx.as<uint32_t>(), e->b_rbal.as<uint64_t>(), e->b_rsrc.as<uint32_t>(),
+                         e->b_bal.as<uint64_t>()) != 0)
         return MPX_E_HIP;
     HTRY(hipStreamSynchronize(s));
     e->num_msgs = G;
@@ -1031,6 +1045,8 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.num_batches = (uint32_t)K;
     v.b_msg = e->b_msg.as<uint32_t>(); v.b_pstart = e->b_pstart.as<uint32_t>();
     v.b_rep_off = e->b_rep_off.as<uint64_t>(); v.b_rep = e->b_rep.as<uint32_t>();
+    v.b_rbal = e->b_rbal.as<uint64_t>(); v.b_rsrc = e->b_rsrc.as<uint32_t>(); v.b_bal = e->b_bal.as<uint64_t>();
+    v.sc_type = e->sc_type.as<uint8_t>(); v.sc_key = e->sc_key.as<uint64_t>(); v.sc_idx = e->sc_idx.as<uint32_t>();
     v.b_chosen = e->b_chosen.as<uint32_t>();
     v.cf_off = e->cf_off.as<uint64_t>(); v.cfrags = e->cfrags.as<Frag>();
     // clean geometry, batch = bucket = 256: a pair holds one ACCEPT and one COMMIT run,

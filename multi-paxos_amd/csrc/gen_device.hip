@@ -124,9 +124,26 @@ __global__ void k_gen_frags(CleanGeo c, uint32_t NB, Frag *frags, uint64_t *f_of
     frags[2 * x + 1] = fc;
 }
 
-// one thread per batch: proposer marker, vote list, chosen fragment
+// one thread per header-scan record: node n's PREPARE, then its K ACCEPTs
+// (index n * (K + 1) + r; mpx_internal.hpp SC_*)
+__global__ void k_gen_scan(CleanGeo c, uint8_t *sc_type, uint64_t *sc_key, uint32_t *sc_idx)
+{
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= (uint64_t)c.N * (c.K + 1)) return;
+    const uint32_t n = (uint32_t)(x / (c.K + 1));
+    const uint64_t r = x - (uint64_t)n * (c.K + 1);
+    uint64_t g;
+    if (r == 0) g = n == 0 ? 1 : node_msg0(c, n);
+    else if (n == 0) g = 2 + c.N + (r - 1) * (3 + 2 * c.N) + 1;
+    else g = node_msg0(c, n) + 1 + 2 * (r - 1);
+    sc_type[x] = r == 0 ? SC_PREP : SC_ACC;
+    sc_key[x] = c.ballot;
+    sc_idx[x] = (uint32_t)g;
+}
+
+// one thread per batch: proposer marker, vote list (+ the replies' headers), chosen fragment
 __global__ void k_gen_batches(CleanGeo c, uint32_t *b_msg, uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep,
-                              uint64_t *cf_off, Frag *cfrags)
+                              uint64_t *cf_off, Frag *cfrags, uint64_t *b_rbal, uint32_t *b_rsrc, uint64_t *b_bal)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j > c.K) return;
@@ -137,7 +154,12 @@ __global__ void k_gen_batches(CleanGeo c, uint32_t *b_msg, uint32_t *b_pstart, u
     const uint64_t base = 2 + N + j * (3 + 2 * N);
     b_msg[j] = (uint32_t)base;
     b_pstart[j] = 0;
-    for (uint32_t i = 0; i < N; ++i) b_rep[(uint64_t)N * j + i] = (uint32_t)(base + 2 + i);
+    b_bal[j] = c.ballot;
+    for (uint32_t i = 0; i < N; ++i) {
+        b_rep[(uint64_t)N * j + i] = (uint32_t)(base + 2 + i);
+        b_rbal[(uint64_t)N * j + i] = c.ballot;
+        b_rsrc[(uint64_t)N * j + i] = i;
+    }
     const uint64_t bc = batch_cnt(c, j);
     const uint8_t start = (uint8_t)((c.k0 + j) * 256 > c.sb ? 0 : (c.sb & 255));
     Frag f{batch_pre(c, j), (uint32_t)j, (uint16_t)bc, start, (uint8_t)(FR_DENSE | (K_BATCH << 4))};
@@ -150,7 +172,9 @@ int launch_gen_clean(void *stream_, uint32_t N, uint64_t K, uint64_t k0, uint64_
                         uint64_t G0, uint64_t G1, uint64_t ballot, uint32_t NB,
                         uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,
                         uint32_t *node, uint64_t *e_val, Frag *frags, uint64_t *f_off, uint32_t *b_msg,
-                        uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep, uint64_t *cf_off, Frag *cfrags)
+                        uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep, uint64_t *cf_off, Frag *cfrags,
+                        uint8_t *sc_type, uint64_t *sc_key, uint32_t *sc_idx, uint64_t *b_rbal, uint32_t *b_rsrc,
+                        uint64_t *b_bal)
 {
     hipStream_t s = (hipStream_t)stream_;
     CleanGeo c{N, K, k0, sb, se, G0, G1, ballot};
@@ -159,7 +183,8 @@ int launch_gen_clean(void *stream_, uint32_t N, uint64_t K, uint64_t k0, uint64_
     hipLaunchKernelGGL(k_gen_entries, dim3(cdiv(se - sb, 256)), dim3(256), 0, s, c, e_val);
     hipLaunchKernelGGL(k_gen_frags, dim3(cdiv((uint64_t)N * NB + 1, 256)), dim3(256), 0, s, c, NB, frags, f_off);
     hipLaunchKernelGGL(k_gen_batches, dim3(cdiv(K + 1, 256)), dim3(256), 0, s, c, b_msg, b_pstart, b_rep_off, b_rep,
-                       cf_off, cfrags);
+                       cf_off, cfrags, b_rbal, b_rsrc, b_bal);
+    hipLaunchKernelGGL(k_gen_scan, dim3(cdiv((uint64_t)N * (K + 1), 256)), dim3(256), 0, s, c, sc_type, sc_key, sc_idx);
     return (int)hipGetLastError();
 }
 

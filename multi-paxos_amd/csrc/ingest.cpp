@@ -598,6 +598,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     std::vector<uint32_t> first_frag(NB, NONE32);            // per bucket: the node's first fragment message
     std::vector<uint64_t> touched, round_b;
     std::vector<uint8_t> in_round(NB, 0);
+    std::vector<uint64_t> sc_off(N + 1, 0);                 // each node's scan-stream range
 
     for (uint32_t n = 0; n < N; ++n) {
         const NodeStream &ns = nodes[n];
@@ -609,6 +610,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         ht.g_a.insert(ht.g_a.end(), ns.g_a.begin(), ns.g_a.end());
         ht.g_b.insert(ht.g_b.end(), ns.g_b.begin(), ns.g_b.end());
         uint32_t pstart = NONE32;                       // epoch of the batches that follow
+        sc_off[n] = ht.sc_type.size();
         for (uint64_t b : touched) first_frag[b] = NONE32;
         for (uint64_t b : round_b) in_round[b] = 0;
         touched.clear(); round_b.clear();
@@ -652,6 +654,36 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             ht.m_ent.push_back(ent);
             ht.m_cnt.push_back(ns.cnt[k]);
             ht.m_node.push_back(n);
+            {   // header-scan stream and static flags (mpx_internal.hpp SC_*)
+                const uint32_t gate = member ? ht.m_gate.back() : 0;
+                const bool badsrc = ns.src[k] >= N;
+                uint8_t f0 = 0;
+                int sct = -1;
+                uint64_t key = ns.ballot[k];
+                if (member) {
+                    if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && (gate & G_SEG)) {
+                        sct = t == MPX_MSG_PREPARE ? SC_PREP : SC_ACC;
+                        key |= (uint64_t)(gate & G_SEG) << SEG_SHIFT;
+                        if (badsrc) { f0 |= F_BADNODE; sct |= SC_BAD; }
+                    } else if (t == MPX_MSG_E_EPOCH) {
+                        sct = SC_PS;
+                        key = (uint64_t)(gate & G_SEG) << SEG_SHIFT;
+                        f0 = (uint8_t)(((gate & G_ACCCLR) ? F_ACCCLR : 0) | ((gate & G_PRECLR) ? F_PRECLR : 0));
+                    } else if (t == MPX_MSG_COMMIT) {
+                        f0 = (gate & G_PROP) ? F_PROP : 0;
+                        if (badsrc) { f0 |= F_BADNODE; sct = SC_NONE | SC_BAD; }
+                    }
+                } else if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
+                    sct = t == MPX_MSG_PREPARE ? SC_PREP : SC_ACC;
+                    if (badsrc) { f0 |= F_BADNODE; sct |= SC_BAD; }
+                } else if (t == MPX_MSG_REJECT) {
+                    sct = SC_SONLY;
+                } else if (t == MPX_MSG_COMMIT && badsrc) {
+                    f0 = F_BADNODE; sct = SC_NONE | SC_BAD;
+                }
+                ht.m_flags0.push_back(f0);
+                if (sct >= 0) { ht.sc_type.push_back((uint8_t)sct); ht.sc_key.push_back(key); ht.sc_idx.push_back(g); }
+            }
             if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_E_EPOCH) { pl.push_back(g); pl_cnt[n]++; }
             if (t == MPX_MSG_P_START) pstart = g;
             if (t == MPX_MSG_P_BATCH) {
@@ -715,6 +747,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         }
     }
     ht.node_off[N] = ht.m_type.size();
+    sc_off[N] = ht.sc_type.size();
 
     // vote lists: replies attributed to the live batch of the same id, same epoch
     {
@@ -743,6 +776,16 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         for (size_t j = 0; j < reps.size(); ++j) ht.b_rep_off[j + 1] = ht.b_rep_off[j] + reps[j].size();
         ht.b_rep.reserve(ht.b_rep_off.back());
         for (auto &r : reps) ht.b_rep.insert(ht.b_rep.end(), r.begin(), r.end());
+        // the replies' headers beside the list (read in order by k_votes, no gathers)
+        ht.b_rbal.resize(ht.b_rep.size());
+        ht.b_rsrc.resize(ht.b_rep.size());
+        for (size_t r = 0; r < ht.b_rep.size(); ++r) {
+            const uint32_t g = ht.b_rep[r];
+            ht.b_rbal[r] = ht.m_ballot[g];
+            ht.b_rsrc[r] = std::min<uint32_t>(ht.m_src[g], 0xFFFF) | (member ? (ht.m_gate[g] >> G_EPOCH_SHIFT) << 16 : 0);
+        }
+        ht.b_bal.resize(ht.b_msg.size());
+        for (size_t j = 0; j < ht.b_msg.size(); ++j) ht.b_bal[j] = ht.b_pstart[j] == NONE32 ? 0 : ht.m_ballot[ht.b_pstart[j]];
     }
 
     // fragment CSR per (node, bucket), stable (keeps message order)
@@ -806,14 +849,14 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     ht.pl_off.assign(N + 1, 0);
     for (uint32_t n = 0; n < N; ++n) ht.pl_off[n + 1] = ht.pl_off[n] + pl_cnt[n];
     ht.pl_msg = std::move(pl);
-    // header-scan chunks
+    // header-scan chunks, over each node's scan stream
     ht.node_chunk_off.assign(N + 1, 0);
     for (uint32_t n = 0; n < N; ++n) {
         ht.node_chunk_off[n] = (uint32_t)ht.chunk_node.size();
-        for (uint64_t g = ht.node_off[n]; g < ht.node_off[n + 1]; g += SCAN_CHUNK) {
+        for (uint64_t g = sc_off[n]; g < sc_off[n + 1]; g += SCAN_CHUNK) {
             ht.chunk_node.push_back(n);
             ht.chunk_beg.push_back(g);
-            ht.chunk_end.push_back(std::min<uint64_t>(g + SCAN_CHUNK, ht.node_off[n + 1]));
+            ht.chunk_end.push_back(std::min<uint64_t>(g + SCAN_CHUNK, sc_off[n + 1]));
         }
     }
     ht.node_chunk_off[N] = (uint32_t)ht.chunk_node.size();

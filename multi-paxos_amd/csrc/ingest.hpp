@@ -61,6 +61,10 @@ struct HostTrace {
     std::vector<uint64_t> node_off;
     std::vector<uint32_t> chunk_node, node_chunk_off;
     std::vector<uint64_t> chunk_beg, chunk_end;
+    std::vector<uint8_t> sc_type;                   // header-scan stream (mpx_internal.hpp SC_*)
+    std::vector<uint64_t> sc_key;
+    std::vector<uint32_t> sc_idx;
+    std::vector<uint8_t> m_flags0;                  // static message flags (bad source, member role gates)
     std::vector<uint64_t> e_val, e_iid, e_pid, r_pid, r_val, r_iid, g_a, g_b;
     std::vector<uint8_t> e_slot, r_slot;
     bool any_sparse = false;
@@ -70,7 +74,8 @@ struct HostTrace {
     std::vector<uint64_t> ev_off, pl_off;           // ev_off: per (bucket, node) pair (N * NB + 1); pl_off: per node
     std::vector<uint32_t> ev_msg, pl_msg;
     std::vector<uint8_t> pair_ev;                   // per pair: 1 when it has snapshot events (not a lean pair)
-    std::vector<uint32_t> b_msg, b_pstart, b_rep;
+    std::vector<uint32_t> b_msg, b_pstart, b_rep, b_rsrc;
+    std::vector<uint64_t> b_rbal, b_bal;
     std::vector<uint64_t> b_rep_off;
     std::vector<uint64_t> cf_off;
     std::vector<Frag> cfrags;

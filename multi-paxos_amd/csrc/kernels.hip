@@ -63,6 +63,14 @@ __device__ inline uint64_t rl64(uint64_t x, uint32_t i)
 }
 __device__ inline uint32_t rl32(uint32_t x, uint32_t i) { return __builtin_amdgcn_readlane(x, i); }
 
+__device__ inline void wave_lds_fence()
+{
+    // LDS instructions of one wave execute in order; keep the compiler from
+    // reordering the scatter / gather around this point
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // ---------------------------------------------------------------- scans --
 // wave64 inclusive max scan
 __device__ inline uint64_t wave_scan_max(uint64_t x)
@@ -96,27 +104,16 @@ __device__ inline uint64_t block_excl_max(uint64_t x, uint64_t *lds4, uint64_t *
     return excl;
 }
 
-// contribution of one message (type t, ballot b, member gate gt) to promised
-// (p) and max_seen (s)
-__device__ inline void contrib(bool member, uint8_t t, uint64_t b, uint32_t gt, uint64_t &p, uint64_t &s)
+// contribution of one scan record (SC_* type t, key) to promised (p) and
+// max_seen (s): PREPARE ids feed both, ACCEPT ids and REJECT max_ids max_seen
+// (multi/paxos.cpp:862-863,1363-1364,1229-1230); member keys carry the Acceptor
+// incarnation in their top byte, so both restart with each new Acceptor
+// (member/paxos.cpp:1700-1760) and an E_EPOCH record starts the incarnation
+__device__ inline void contrib(uint8_t t, uint64_t key, uint64_t &p, uint64_t &s)
 {
-    if (member) {
-        // keys (incarnation << 56 | ballot): the Acceptor's own promised /
-        // max_proposal_id_ restart with every new Acceptor (member/paxos.cpp:
-        // 1700-1760); REJECT only feeds the proposer's max (:1221-1225)
-        const uint64_t key = (uint64_t)(gt & G_SEG) << SEG_SHIFT;
-        if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && (gt & G_SEG)) {
-            s = key | b;
-            p = t == MPX_MSG_PREPARE ? s : 0;
-        } else if (t == MPX_MSG_E_EPOCH) {
-            p = s = key;
-        } else {
-            p = s = 0;
-        }
-        return;
-    }
-    p = t == MPX_MSG_PREPARE ? b : 0;
-    s = (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT || t == MPX_MSG_REJECT) ? b : 0;
+    const uint32_t k = t & SC_KIND;
+    p = (k == SC_PREP || k == SC_PS) ? key : 0;
+    s = k <= SC_PS ? key : 0;
 }
 
 __device__ inline uint64_t wave_max(uint64_t x)
@@ -129,34 +126,28 @@ __device__ inline uint64_t wave_max(uint64_t x)
     return x;
 }
 
-constexpr uint32_t SCAN_ROUNDS = SCAN_CHUNK / 256;   // rounds of 64 messages per wave
+constexpr uint32_t SCAN_ROUNDS = SCAN_CHUNK / 256;   // rounds of 64 records per wave
 
-// Chunk aggregates: max of PREPARE ids and of max_seen contributions over
-// SCAN_CHUNK messages (order-free, so plain coalesced loads)
-template <bool MEMBER>
+// Chunk aggregates over the header-scan stream: max of the PREPARE ids and of
+// the max_seen contributions of SCAN_CHUNK records (order-free, coalesced)
 __global__ __launch_bounds__(256) void k_scan_chunk(DevView v)
 {
     __shared__ uint64_t l[2][4];
     const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
-    constexpr bool member = MEMBER;
     uint64_t lp = 0, ls = 0;
     uint8_t ty[SCAN_ROUNDS];
-    uint64_t ba[SCAN_ROUNDS];
-    uint32_t ga[SCAN_ROUNDS];
+    uint64_t ky[SCAN_ROUNDS];
 #pragma unroll
     for (uint32_t i = 0; i < SCAN_ROUNDS; ++i) {          // all loads in flight at once
         const uint64_t g = beg + threadIdx.x + 256ull * i;
-        ty[i] = 0xFF; ba[i] = 0; ga[i] = 0;
-        if (g < end) {
-            ty[i] = v.m_type[g]; ba[i] = v.m_ballot[g];
-            if (member) ga[i] = v.m_gate[g];
-        }
+        ty[i] = SC_NONE; ky[i] = 0;
+        if (g < end) { ty[i] = v.sc_type[g]; ky[i] = v.sc_key[g]; }
     }
 #pragma unroll
     for (uint32_t i = 0; i < SCAN_ROUNDS; ++i) {
         uint64_t p, s;
-        contrib(member, ty[i], ba[i], ga[i], p, s);
+        contrib(ty[i], ky[i], p, s);
         lp = lp > p ? lp : p;
         ls = ls > s ? ls : s;
     }
@@ -195,48 +186,41 @@ __global__ __launch_bounds__(256) void k_scan_node(DevView v)
     if (threadIdx.x == 0) { v.node_scal[2 * n] = carry_p; v.node_scal[2 * n + 1] = carry_s; }
 }
 
-// Per message: granted / reject flags, max_seen carried by REJECTs.  Wave w of
-// the chunk's block owns SCAN_CHUNK / 4 consecutive messages, 64 per round
-// (coalesced), staged in LDS between the two phases: (1) wave maxima ->
-// the wave's carry-in, (2) per round the promised value before each message
+// Per scan record: granted / reject flags and the max_seen a REJECT carries.
+// Wave w of the chunk's block owns SCAN_CHUNK / 4 consecutive records, 64 per
+// round (coalesced), staged in LDS between the two phases: (1) wave maxima ->
+// the wave's carry-in, (2) per round the promised value before each record
 // (an exclusive wave scan, only in rounds that hold a PREPARE) and, in rounds
-// with a REJECT, the inclusive max_seen scan.
+// with a REJECT, the inclusive max_seen scan.  Flags go to the record's
+// message (m_flags[sc_idx]); messages outside the stream keep their static flags.
 template <bool MEMBER>
 __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
 {
     __shared__ uint64_t l[2][4], lc[2][4];
-    __shared__ uint64_t lba[SCAN_CHUNK];        // phase 2 reads its rounds back from LDS,
+    __shared__ uint64_t lky[SCAN_CHUNK];        // phase 2 reads its rounds back from LDS,
     __shared__ uint8_t lty[SCAN_CHUNK];         // so the round loop needs few registers
-    __shared__ uint32_t lga[MEMBER ? SCAN_CHUNK : 1];
     const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
     const uint64_t wb = beg + (uint64_t)w * (SCAN_CHUNK / 4) + lane;
     const uint32_t lb = w * (SCAN_CHUNK / 4) + lane;
     constexpr bool member = MEMBER;
     uint8_t ty[SCAN_ROUNDS];
-    uint64_t ba[SCAN_ROUNDS];
-    uint32_t sr[SCAN_ROUNDS], ga[SCAN_ROUNDS];
+    uint64_t ky[SCAN_ROUNDS];
     uint64_t lp = 0, ls = 0;
 #pragma unroll
     for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {             // all loads in flight at once
         const uint64_t g = wb + 64 * r;
-        ty[r] = 0xFF; ba[r] = 0; sr[r] = 0; ga[r] = 0;
-        if (g < end) {
-            ty[r] = v.m_type[g]; ba[r] = v.m_ballot[g]; sr[r] = v.m_src[g];
-            if (member) ga[r] = v.m_gate[g];
-        }
+        ty[r] = SC_NONE; ky[r] = 0;
+        if (g < end) { ty[r] = v.sc_type[g]; ky[r] = v.sc_key[g]; }
     }
-    uint32_t badsrc = 0;                        // one bad-node bit per round
 #pragma unroll
     for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
         uint64_t p, s;
-        contrib(member, ty[r], ba[r], ga[r], p, s);
+        contrib(ty[r], ky[r], p, s);
         lp = lp > p ? lp : p;
         ls = ls > s ? ls : s;
-        badsrc |= (sr[r] >= v.N ? 1u : 0u) << r;
         lty[lb + 64 * r] = ty[r];
-        lba[lb + 64 * r] = ba[r];
-        if (member) lga[lb + 64 * r] = ga[r];
+        lky[lb + 64 * r] = ky[r];
     }
     // carry-in = max over the node's earlier chunk aggregates (k_scan_chunk),
     // read here from L2 instead of a separate per-node scan kernel
@@ -277,11 +261,11 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
         const uint64_t g = wb + 64 * r;
         if (!__ballot(g < end)) break;
         const uint8_t t = lty[lb + 64 * r];    // written by this lane: no barrier needed
-        const uint64_t id = lba[lb + 64 * r];
-        const uint32_t gt = member ? lga[lb + 64 * r] : 0;
+        const uint64_t key = lky[lb + 64 * r];
+        const uint32_t kind = t & SC_KIND;
         uint64_t p, s;
-        contrib(member, t, id, gt, p, s);
-        // promised before this message
+        contrib(t, key, p, s);
+        // promised before this record
         uint64_t prom = cp;
         if (__ballot(p != 0)) {
             uint64_t x = wave_scan_max(p);
@@ -291,47 +275,37 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
             prom = prom > x ? prom : x;
         }
         uint8_t f = 0;
-        bool chk_src = false;
-        if (member) {
-            if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && (gt & G_SEG)) {
-                const uint64_t seg = gt & G_SEG;
-                const uint64_t pr = (prom >> SEG_SHIFT) == seg ? (prom & LOW56) : 0;
-                if (t == MPX_MSG_PREPARE) {
-                    if (id > pr) f = F_GRANTED;                         // :1711
-                    else if (id < pr) f = F_REJECT;                     // :1734
-                } else {
-                    f = id >= pr ? F_GRANTED : F_REJECT;                // :1753
-                }
-                chk_src = true;
-            } else if (t == MPX_MSG_E_EPOCH) {
-                f = ((gt & G_ACCCLR) ? F_ACCCLR : 0) | ((gt & G_PRECLR) ? F_PRECLR : 0);
-            } else if (t == MPX_MSG_COMMIT) {
-                f = (gt & G_PROP) ? F_PROP : 0;
-                chk_src = true;
+        if (kind == SC_PREP || kind == SC_ACC) {
+            uint64_t id = key, pr = prom;
+            if (member) {
+                // the Acceptor's own promise: zero when prom is an earlier incarnation's
+                id = key & LOW56;
+                pr = (prom >> SEG_SHIFT) == (key >> SEG_SHIFT) ? (prom & LOW56) : 0;
             }
-        } else {
-            if (t == MPX_MSG_PREPARE) {
-                if (id > prom) f = F_GRANTED;                           // :865
-                else if (id < prom) f = F_REJECT;                       // :894
-            } else if (t == MPX_MSG_ACCEPT) {
-                f = id >= prom ? F_GRANTED : F_REJECT;                  // :1366
+            if (kind == SC_PREP) {
+                if (id > pr) f = F_GRANTED;                             // :865 / member :1711
+                else if (id < pr) f = F_REJECT;                         // :894 / :1734
+            } else {
+                f = id >= pr ? F_GRANTED : F_REJECT;                    // :1366 / :1753
             }
-            chk_src = t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT;
         }
-        if (chk_src && ((badsrc >> r) & 1)) f |= F_BADNODE;
-        // max_seen after this message, for the REJECTs it carries (:894,1398)
+        // max_seen after this record, for the REJECTs it carries (:894,1398)
         if (__ballot(f & F_REJECT)) {
             const uint64_t pre = wave_max(ls);
             cs = cs > pre ? cs : pre;
             ls = 0;
             uint64_t x = wave_scan_max(s);
             x = x > cs ? x : cs;
-            if (f & F_REJECT) v.m_maxseen[g] = member ? x & LOW56 : x;
+            if (f & F_REJECT) v.m_maxseen[v.sc_idx[g]] = member ? x & LOW56 : x;
         }
         ls = ls > s ? ls : s;
-        if (g < end) {
-            v.m_flags[g] = f;
-            if (f & F_BADNODE) record_violation(v, MPX_V_BAD_NODE, v.m_node[g], g - v.node_off[v.m_node[g]], 0);
+        if (g < end && (kind <= SC_ACC || (t & SC_BAD))) {
+            const uint32_t idx = v.sc_idx[g];
+            if (kind <= SC_ACC) v.m_flags[idx] = f | ((t & SC_BAD) ? F_BADNODE : 0);
+            if (t & SC_BAD) {
+                const uint32_t n = v.m_node[idx];
+                record_violation(v, MPX_V_BAD_NODE, n, idx - v.node_off[n], 0);
+            }
         }
     }
 }
@@ -414,7 +388,7 @@ __global__ __launch_bounds__(64) void k_proposer(DevView v)
         uint32_t fl = 0;
         if (match && fc >= lane) fl = F_COUNTED | (fc == lane ? F_QUORUM : 0);
         if (bad && fc > lane) record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0);
-        if (fl) v.m_flags[g] |= (uint8_t)fl;
+        if (rep) v.m_flags[g] = (uint8_t)fl;    // a reply's flags are this kernel's alone (static ones are 0)
         // carry the last record's round into the next window
         const uint32_t L = cnt - 1;
         if (psm) cb = rl64(b, 63 - __builtin_clzll(psm));
@@ -424,73 +398,56 @@ __global__ __launch_bounds__(64) void k_proposer(DevView v)
     }
 }
 
-// Accept-vote quorum, one lane per batch (AcceptingValues::accepted_ as a mask).
-__global__ void k_votes(DevView v)
+// Accept-vote quorum (OnAcceptReply, multi/paxos.cpp:1406-1427; member
+// Proposer::OnAcceptReply, member/paxos.cpp:1317-1343): AcceptingValues::
+// accepted_ as a 64-bit acceptor mask per batch, chosen at |mask| >= quorum.
+// A wave takes 64 consecutive batches: their vote lists are one contiguous
+// range of the CSR, staged through LDS with coalesced loads of the replies'
+// headers (ballot, acceptor, epoch: laid out beside the list at ingest), then
+// each lane walks its own batch's replies in order from LDS.
+constexpr uint32_t VOTE_LDS = 768;             // reply headers staged per wave
+__global__ __launch_bounds__(256) void k_votes(DevView v)
 {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= v.num_batches) return;
-    const uint32_t ps = v.b_pstart[j];
-    const uint64_t ballot = ps == NONE32 ? 0 : v.m_ballot[ps];
-    uint64_t mask = 0;
-    uint32_t chosen = NONE32;
+    __shared__ uint64_t lbal[4][VOTE_LDS];
+    __shared__ uint32_t lsrc[4][VOTE_LDS];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t j0 = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    if (j0 >= v.num_batches) return;
+    const uint64_t j = j0 + lane;
+    const bool have = j < v.num_batches;
+    const uint64_t jl = j0 + 64 < v.num_batches ? j0 + 64 : v.num_batches;
+    const uint64_t r0 = v.b_rep_off[j0], r1 = v.b_rep_off[jl];
+    const uint64_t rs = have ? v.b_rep_off[j] : r1, re = have ? v.b_rep_off[j + 1] : r1;
+    const uint64_t staged = r1 - r0 < VOTE_LDS ? r1 - r0 : VOTE_LDS;
+    for (uint64_t x = lane; x < staged; x += 64) { lbal[wv][x] = v.b_rbal[r0 + x]; lsrc[wv][x] = v.b_rsrc[r0 + x]; }
+    wave_lds_fence();
+    const uint64_t ballot = have ? v.b_bal[j] : 0;
     const bool member = v.semantics == MPX_SEM_MEMBER;
-    uint64_t r = v.b_rep_off[j];
-    const uint64_t re = v.b_rep_off[j + 1];
-    if (!member) {
-        // the first VOTE_PREFETCH replies: indices, then ballots and sources,
-        // each level issued at once (three memory round trips, not one per reply)
-        constexpr uint32_t VP = 8;
-        uint32_t gi[VP];
-        uint64_t bal[VP];
-        uint32_t src[VP];
-#pragma unroll
-        for (uint32_t k = 0; k < VP; ++k) gi[k] = r + k < re ? v.b_rep[r + k] : NONE32;
-#pragma unroll
-        for (uint32_t k = 0; k < VP; ++k) {
-            bal[k] = gi[k] != NONE32 ? v.m_ballot[gi[k]] : 0;
-            src[k] = gi[k] != NONE32 ? v.m_src[gi[k]] : 0;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < VP; ++k) {
-            if (gi[k] == NONE32 || chosen != NONE32) continue;
-            if (bal[k] != ballot) continue;                       // :1408
-            if (src[k] >= v.N) {
-                const uint32_t n = v.m_node[gi[k]];
-                record_violation(v, MPX_V_BAD_NODE, n, gi[k] - v.node_off[n], 0);
-                continue;
-            }
-            mask |= 1ull << src[k];
-            if ((uint32_t)__popcll(mask) >= v.quorum) chosen = gi[k];   // :1416
-        }
-        r = chosen == NONE32 && re - r > VP ? r + VP : re;
-    }
-    for (; r < re; ++r) {
-        const uint32_t g = v.b_rep[r];
+    uint64_t mask = 0;
+    uint64_t chosen_r = ~0ull;
+    for (uint64_t r = rs; r < re; ++r) {
+        const uint64_t o = r - r0;
+        const uint64_t b = o < VOTE_LDS ? lbal[wv][o] : v.b_rbal[r];
+        const uint32_t x = o < VOTE_LDS ? lsrc[wv][o] : v.b_rsrc[r];
+        const uint32_t a = x & 0xFFFF;
+        uint64_t am;
         if (member) {
-            // Proposer::OnAcceptReply, member/paxos.cpp:1317-1343: matched by
-            // batch id only; quorum of the node's epoch at the reply
-            const uint64_t am = v.ep_amask[(v.m_gate[g] >> G_EPOCH_SHIFT) - 1];
-            const uint32_t a = v.m_src[g];
-            if (a >= 64 || !((am >> a) & 1)) {
-                const uint32_t n = v.m_node[g];
-                record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0);
-                continue;
-            }
-            mask |= 1ull << a;
-            if ((uint32_t)__popcll(mask) >= (uint32_t)__popcll(am) / 2 + 1) { chosen = g; break; }
-            continue;
+            am = v.ep_amask[(x >> 16) - 1];              // the node's acceptors at the reply (:1324-1327)
+        } else {
+            if (b != ballot) continue;                   // :1408
+            am = v.N >= 64 ? ~0ull : ((1ull << v.N) - 1);
         }
-        if (v.m_ballot[g] != ballot) continue;                  // :1408
-        const uint32_t a = v.m_src[g];
-        if (a >= v.N) {
+        if (a >= 64 || !((am >> a) & 1)) {              // :1414 / :1324
+            const uint32_t g = v.b_rep[r];
             const uint32_t n = v.m_node[g];
             record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0);
             continue;
         }
         mask |= 1ull << a;
-        if ((uint32_t)__popcll(mask) >= v.quorum) { chosen = g; break; }   // :1416
+        const uint32_t q = member ? (uint32_t)__popcll(am) / 2 + 1 : v.quorum;
+        if ((uint32_t)__popcll(mask) >= q) { chosen_r = r; break; }   // :1416
     }
-    v.b_chosen[j] = chosen;
+    if (have) v.b_chosen[j] = chosen_r == ~0ull ? NONE32 : v.b_rep[chosen_r];
 }
 
 // ------------------------------------------------------------- apply ----
@@ -499,13 +456,6 @@ __global__ void k_votes(DevView v)
 // round trips — (1) CSR offsets, (2) fragment / event descriptors, (3) the
 // scan's per-message flags + the entry values — and (1) of the next pair is
 // already in flight while the current one is processed.
-__device__ inline void wave_lds_fence()
-{
-    // LDS instructions of one wave execute in order; keep the compiler from
-    // reordering the scatter / gather around this point
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // Snapshot records of one event of a pair: lane l's slot j is emitted when
 // want[j] (record: ref[j], aux = slot | kind); one append (atomicAdd on the
@@ -1799,8 +1749,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, s);
     hipLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s, v, n_partials);
     if (v.num_chunks) {
-        if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_chunk<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
-        else hipLaunchKernelGGL(k_scan_chunk<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
+        hipLaunchKernelGGL(k_scan_chunk, dim3(v.num_chunks), dim3(256), 0, s, v);
         if (v.scan_node_pass) hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);   // long node streams
         if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
         else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);

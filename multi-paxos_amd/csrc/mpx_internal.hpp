@@ -87,6 +87,22 @@ enum : uint32_t { G_SEG = 0xFF, G_ACCCLR = 1u << 8, G_PRECLR = 1u << 9, G_PROP =
 constexpr uint64_t SEG_SHIFT = 56;
 constexpr uint64_t LOW56 = (1ull << 56) - 1;
 
+// Header-scan stream (ingest.cpp, gen_device.hip): per node, in processing
+// order, only the records that move the acceptor scalars promised / max_seen or
+// take a scan flag — PREPARE, ACCEPT, REJECT (multi), E_EPOCH (member), and any
+// record with a bad source (violation) — as {type, key, message index}; the
+// key is the ballot (member: incarnation << 56 | ballot).  The scan reads 13 B
+// per such record instead of every header of the trace.
+enum : uint8_t {
+    SC_PREP = 0,      // p = s = key; granted if id > promised, reject if <      (multi/paxos.cpp:862-894)
+    SC_ACC = 1,       // s = key; granted if id >= promised, else reject        (:1363-1398)
+    SC_SONLY = 2,     // s = key (REJECT's max_id, :1229-1230)
+    SC_PS = 3,        // p = s = key (member E_EPOCH: a new Acceptor incarnation)
+    SC_NONE = 4,      // no contribution (a COMMIT with a bad source)
+    SC_KIND = 7,
+    SC_BAD = 8        // the record's source is not a node: F_BADNODE + violation
+};
+
 // fragment kinds (Frag::flags >> 4)
 enum : uint8_t { K_ACCEPT = 0, K_COMMIT = 1, K_PREPLY = 2, K_BATCH = 3 };
 enum : uint8_t { FR_DENSE = 1 };
@@ -161,10 +177,13 @@ struct DevView {
     const uint64_t *e_pid;          // per ACCEPT / LEARN entry: its proposal id
     const uint64_t *ep_amask;       // per epoch: acceptor set
     uint32_t num_epochs;
-    // header scan
+    // header scan over the scan stream (SC_*): chunks of SCAN_CHUNK records per node
+    const uint8_t *sc_type;
+    const uint64_t *sc_key;
+    const uint32_t *sc_idx;         // global message index of the record
     uint32_t num_chunks;
     const uint32_t *chunk_node;
-    const uint64_t *chunk_beg;      // global msg index of chunk start
+    const uint64_t *chunk_beg;      // scan-stream index of chunk start
     const uint64_t *chunk_end;
     const uint32_t *node_chunk_off; // N+1
     uint64_t *chunk_agg;            // 2 per chunk: pmax, smax
@@ -195,6 +214,9 @@ struct DevView {
     const uint32_t *b_pstart;
     const uint64_t *b_rep_off;
     const uint32_t *b_rep;
+    const uint64_t *b_rbal;         // per vote-list entry: the reply's ballot
+    const uint32_t *b_rsrc;         // ... its acceptor (low 16 bits, clamped) | member: (epoch + 1) << 16
+    const uint64_t *b_bal;          // per batch: the ballot of its proposer round (0: none)
     uint32_t *b_chosen;             // global msg index of the quorum reply, NONE32
     const uint64_t *cf_off;         // NB+1
     const Frag *cfrags;
@@ -271,6 +293,8 @@ int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t
                      uint64_t G0, uint64_t G1, uint64_t ballot, uint32_t NB,
                      uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,
                      uint32_t *node, uint64_t *e_val, Frag *frags, uint64_t *f_off, uint32_t *b_msg,
-                     uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep, uint64_t *cf_off, Frag *cfrags);
+                     uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep, uint64_t *cf_off, Frag *cfrags,
+                     uint8_t *sc_type, uint64_t *sc_key, uint32_t *sc_idx, uint64_t *b_rbal, uint32_t *b_rsrc,
+                     uint64_t *b_bal);
 
 }  // namespace mpx
