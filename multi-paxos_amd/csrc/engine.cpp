@@ -944,17 +944,30 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
 {
     if (!e || !p) return MPX_E_INVAL;
     if (p->kind != MPX_GEN_CLEAN || p->num_nodes != e->cfg.num_nodes || e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_INVAL;
-    if ((p->batch && p->batch != BS) || (e->cfg.shard_begin & (BS - 1))) return MPX_E_INVAL;
+    const uint64_t B = p->batch ? p->batch : BS;               // instances per batch
+    if (B > 0xFFFF || (e->cfg.shard_begin & (BS - 1)) || e->NB == 0) return MPX_E_INVAL;
     if (e->cfg.shard_end > p->num_instances) return MPX_E_INVAL;
     HTRY(hipSetDevice(e->device));
     const uint64_t t0 = now_ns();
     const uint32_t N = e->cfg.num_nodes;
-    const uint64_t sb = e->cfg.shard_begin, se = e->cfg.shard_end, L = se - sb;
-    const uint64_t k0 = sb >> BSH, K = e->NB;                   // kept batches = shard buckets
+    const uint64_t sb = e->cfg.shard_begin, se = e->cfg.shard_end, L = se - sb, NB = e->NB;
+    const uint64_t k0 = sb / B, K = (se - 1) / B - k0 + 1;      // kept batches: those meeting the shard
     const uint64_t G0 = 2 + N + K * (3 + 2ull * N), G1 = 1 + 2 * K;
     const uint64_t G = G0 + (uint64_t)(N - 1) * G1;
     const uint64_t E = L;                                       // one shared run per batch
-    if (G >= NONE32 || E > MAX_ENTRIES || 2ull * N * K > MAX_FRAGS) return MPX_E_RANGE;
+    // per bucket: the batches meeting it (one ACCEPT and one COMMIT run per
+    // node each, one chosen-log run) -> the fragment CSR offsets
+    std::vector<uint64_t> cf_off(NB + 1, 0), f_off(N * NB + 1, 0);
+    uint64_t max_pair = 0;
+    for (uint64_t b = 0; b < NB; ++b) {
+        const uint64_t lo = sb + (b << BSH), hi = std::min(lo + BS, se);
+        const uint64_t nb = (hi - 1) / B - lo / B + 1;
+        cf_off[b + 1] = cf_off[b] + nb;
+        for (uint32_t n = 0; n < N; ++n) f_off[b * N + n] = 2 * (N * cf_off[b] + n * nb);
+        max_pair = std::max(max_pair, 2 * nb);
+    }
+    f_off[N * NB] = 2ull * N * cf_off[NB];
+    if (G >= NONE32 || E > MAX_ENTRIES || f_off[N * NB] > MAX_FRAGS || max_pair > MAX_PAIR_FRAGS) return MPX_E_RANGE;
     const uint64_t ballot = 1ull << 16;                         // (1 << 16) | node 0
     // host-side small tables
     HostTrace &h = e->ht;
@@ -1004,12 +1017,22 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     TRY(e->e_val.alloc(std::max<uint64_t>(8 * E, 8)));
     TRY(e->e_slot.alloc(8)); TRY(e->r_pid.alloc(8)); TRY(e->r_val.alloc(8)); TRY(e->r_slot.alloc(8));
     TRY(upload(e->g_a, h.g_a, s)); TRY(upload(e->g_b, h.g_b, s));
-    TRY(e->f_off.alloc(8 * ((uint64_t)N * e->NB + 1))); TRY(e->frags.alloc(sizeof(Frag) * 2 * (uint64_t)N * e->NB + 16));
+    TRY(upload(e->f_off, f_off, s)); TRY(e->frags.alloc(sizeof(Frag) * f_off[N * NB] + 16));
     TRY(upload(e->pl_off, h.pl_off, s)); TRY(upload(e->pl_msg, h.pl_msg, s));
     TRY(e->b_msg.alloc(4 * K + 4)); TRY(e->b_pstart.alloc(4 * K + 4)); TRY(e->b_rep_off.alloc(8 * (K + 1)));
     TRY(e->b_rep.alloc(4 * (uint64_t)N * K + 4)); TRY(e->b_chosen.alloc(4 * K + 4));
-    TRY(e->cf_off.alloc(8 * (K + 1))); TRY(e->cfrags.alloc(sizeof(Frag) * K + 16));
-    if (launch_gen_clean(s, N, K, k0, sb, se, G0, G1, ballot, e->NB,
+    TRY(upload(e->cf_off, cf_off, s)); TRY(e->cfrags.alloc(sizeof(Frag) * cf_off[NB] + 16));
+    // pairs the lean kernels cannot take (ingest.cpp's predicate: every run is
+    // dense, no snapshot events, so only the node count and run count decide)
+    std::vector<uint64_t> gd;
+    for (uint64_t q = 0; q < N * NB; ++q)
+        if (N > FAST_MAX_NODES || f_off[q + 1] - f_off[q] > FAST_MAX_FRAGS) {
+            const uint64_t w[GP_WORDS] = {f_off[q], f_off[q + 1], 0, 0, q, 0, 0, 0};
+            gd.insert(gd.end(), w, w + GP_WORDS);
+        }
+    if (gd.empty()) TRY(e->gp_list.alloc(8));
+    else TRY(upload(e->gp_list, gd, s));
+    if (launch_gen_clean(s, N, K, k0, sb, se, G0, G1, ballot, B, e->NB,
                          e->m_type.as<uint8_t>(), e->m_src.as<uint32_t>(), e->m_ballot.as<uint64_t>(),
                          e->m_aux.as<uint64_t>(), e->m_ent.as<uint64_t>(), e->m_cnt.as<uint32_t>(),
                          e->m_node.as<uint32_t>(), e->e_val.as<uint64_t>(), e->frags.as<Frag>(),
@@ -1038,8 +1061,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
-    TRY(e->gp_list.alloc(8));
-    v.num_gp = 0; v.gp_list = e->gp_list.as<uint64_t>();    // clean trace: every pair is a fast pair
+    v.num_gp = gd.size() / GP_WORDS; v.gp_list = e->gp_list.as<uint64_t>();
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
     v.num_batches = (uint32_t)K;
@@ -1049,9 +1071,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.sc_type = e->sc_type.as<uint8_t>(); v.sc_key = e->sc_key.as<uint64_t>(); v.sc_idx = e->sc_idx.as<uint32_t>();
     v.b_chosen = e->b_chosen.as<uint32_t>();
     v.cf_off = e->cf_off.as<uint64_t>(); v.cfrags = e->cfrags.as<Frag>();
-    // clean geometry, batch = bucket = 256: a pair holds one ACCEPT and one COMMIT run,
-    // a bucket's chosen list one run
-    v.slot_w = 1;
+    v.slot_w = max_pair <= MAX_PAIR_FRAGS_1 ? 1 : 2;
     TRY(finish_view(e));
     for (auto &ns : e->nodes) ns.clear();
     e->vt.clear();

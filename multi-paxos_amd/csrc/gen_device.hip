@@ -9,14 +9,16 @@
 // those instances; in the clean trace they cannot change this shard's state
 // or scalars (every ACCEPT carries the PREPARE's ballot, already seen).
 //
-// Layout for batch size 256 = bucket size, shard aligned to 256:
+// Layout (batch size B, shard aligned to 256; B = 256 puts one batch per bucket):
 //   node 0 : P_START, PREPARE, N x PREPARE_REPLY, then per kept batch
 //            P_BATCH, ACCEPT, N x ACCEPT_REPLY, COMMIT, N x COMMIT_REPLY
 //   node i : PREPARE, then per kept batch ACCEPT, COMMIT
 //   entries: one run per batch, shared by its P_BATCH, ACCEPT and COMMIT at
 //            every node (the content-addressed pool of ingest.cpp: a
 //            broadcast is stored once), so e_val[i - sb] = handle of i
-//   pairs:   f_off / frags indexed bucket-major, q = bucket * N + node
+//   pairs:   f_off / frags indexed bucket-major, q = bucket * N + node; a pair
+//            holds an ACCEPT and a COMMIT run for every batch meeting its
+//            bucket (f_off / cf_off: prefix counts computed on the host)
 #include <hip/hip_runtime.h>
 #include "mpx_internal.hpp"
 
@@ -30,17 +32,18 @@ struct CleanGeo {
     uint64_t G0;         // messages of node 0
     uint64_t G1;         // messages of node i > 0
     uint64_t ballot;
+    uint64_t B;          // instances per batch
 };
 
 __device__ inline uint64_t batch_cnt(const CleanGeo &c, uint64_t j)
 {
-    const uint64_t lo = (c.k0 + j) * 256, hi = lo + 256;
+    const uint64_t lo = (c.k0 + j) * c.B, hi = lo + c.B;
     const uint64_t a = lo > c.sb ? lo : c.sb, b = hi < c.se ? hi : c.se;
     return b > a ? b - a : 0;
 }
 __device__ inline uint64_t batch_pre(const CleanGeo &c, uint64_t j)   // in-shard entries before batch j
 {
-    const uint64_t x = (c.k0 + j) * 256;
+    const uint64_t x = (c.k0 + j) * c.B;
     const uint64_t m = x < c.se ? x : c.se;
     return m > c.sb ? m - c.sb : 0;
 }
@@ -96,32 +99,43 @@ __global__ void k_gen_entries(CleanGeo c, uint64_t *e_val)
     e_val[li] = MPX_HANDLE(0, 0, c.sb + li + 1);
 }
 
-// one thread per (bucket, node) pair q = bucket * N + node: two fragments (ACCEPT, COMMIT) and f_off
-__global__ void k_gen_frags(CleanGeo c, uint32_t NB, Frag *frags, uint64_t *f_off)
+// one thread per (bucket, node) pair q = bucket * N + node: for every batch
+// meeting the bucket, in message order, its ACCEPT run then its COMMIT run
+// (f_off from the host); the (bucket, 0) thread also writes the bucket's
+// chosen-log runs (cf_off)
+__global__ void k_gen_frags(CleanGeo c, uint32_t NB, Frag *frags, const uint64_t *f_off, Frag *cfrags,
+                            const uint64_t *cf_off)
 {
     const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t np = (uint64_t)c.N * NB;
-    if (x > np) return;
-    f_off[x] = 2 * x;
-    if (x == np) return;
+    if (x >= np) return;
     const uint32_t N = c.N;
     const uint32_t n = (uint32_t)(x % N);
-    const uint64_t j = x / N;
-    const uint64_t bc = batch_cnt(c, j);
-    uint64_t acc_msg, com_msg;
-    if (n == 0) {
-        const uint64_t base = 2 + N + j * (3 + 2 * N);
-        acc_msg = base + 1; com_msg = base + 2 + N;
-    } else {
-        const uint64_t base = node_msg0(c, n) + 1 + 2 * j;
-        acc_msg = base; com_msg = base + 1;
+    const uint64_t b = x / N;
+    const uint64_t lo = c.sb + (b << 8), hi = lo + 256 < c.se ? lo + 256 : c.se;
+    const uint64_t j0 = lo / c.B - c.k0, j1 = (hi - 1) / c.B - c.k0;
+    uint64_t at = f_off[x];
+    for (uint64_t j = j0; j <= j1; ++j) {
+        const uint64_t blo = (c.k0 + j) * c.B, bhi = blo + c.B;
+        const uint64_t a = blo > lo ? blo : lo, e = bhi < hi ? bhi : hi;     // the batch's run in this bucket
+        uint64_t acc_msg, com_msg;
+        if (n == 0) {
+            const uint64_t base = 2 + N + j * (3 + 2 * N);
+            acc_msg = base + 1; com_msg = base + 2 + N;
+        } else {
+            const uint64_t base = node_msg0(c, n) + 1 + 2 * j;
+            acc_msg = base; com_msg = base + 1;
+        }
+        const uint8_t start = (uint8_t)((a - c.sb) & 255);
+        const Frag fa{a - c.sb, (uint32_t)acc_msg, (uint16_t)(e - a), start, (uint8_t)(FR_DENSE | (K_ACCEPT << 4))};
+        const Frag fc{a - c.sb, (uint32_t)com_msg, (uint16_t)(e - a), start, (uint8_t)(FR_DENSE | (K_COMMIT << 4))};
+        frags[at++] = fa;
+        frags[at++] = fc;
+        if (n == 0) {
+            const Frag fb{a - c.sb, (uint32_t)j, (uint16_t)(e - a), start, (uint8_t)(FR_DENSE | (K_BATCH << 4))};
+            cfrags[cf_off[b] + (j - j0)] = fb;
+        }
     }
-    const uint64_t acc_ent = batch_pre(c, j), com_ent = acc_ent;
-    const uint8_t start = (uint8_t)((c.k0 + j) * 256 > c.sb ? 0 : (c.sb & 255));
-    Frag fa{acc_ent, (uint32_t)acc_msg, (uint16_t)bc, start, (uint8_t)(FR_DENSE | (K_ACCEPT << 4))};
-    Frag fc{com_ent, (uint32_t)com_msg, (uint16_t)bc, start, (uint8_t)(FR_DENSE | (K_COMMIT << 4))};
-    frags[2 * x] = fa;
-    frags[2 * x + 1] = fc;
 }
 
 // one thread per header-scan record: node n's PREPARE, then its K ACCEPTs
@@ -141,15 +155,14 @@ __global__ void k_gen_scan(CleanGeo c, uint8_t *sc_type, uint64_t *sc_key, uint3
     sc_idx[x] = (uint32_t)g;
 }
 
-// one thread per batch: proposer marker, vote list (+ the replies' headers), chosen fragment
+// one thread per batch: proposer marker, vote list (+ the replies' headers)
 __global__ void k_gen_batches(CleanGeo c, uint32_t *b_msg, uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep,
-                              uint64_t *cf_off, Frag *cfrags, uint64_t *b_rbal, uint32_t *b_rsrc, uint64_t *b_bal)
+                              uint64_t *b_rbal, uint32_t *b_rsrc, uint64_t *b_bal)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j > c.K) return;
     const uint32_t N = c.N;
     b_rep_off[j] = (uint64_t)N * j;
-    cf_off[j] = j;
     if (j == c.K) return;
     const uint64_t base = 2 + N + j * (3 + 2 * N);
     b_msg[j] = (uint32_t)base;
@@ -160,16 +173,12 @@ __global__ void k_gen_batches(CleanGeo c, uint32_t *b_msg, uint32_t *b_pstart, u
         b_rbal[(uint64_t)N * j + i] = c.ballot;
         b_rsrc[(uint64_t)N * j + i] = i;
     }
-    const uint64_t bc = batch_cnt(c, j);
-    const uint8_t start = (uint8_t)((c.k0 + j) * 256 > c.sb ? 0 : (c.sb & 255));
-    Frag f{batch_pre(c, j), (uint32_t)j, (uint16_t)bc, start, (uint8_t)(FR_DENSE | (K_BATCH << 4))};
-    cfrags[j] = f;
 }
 
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 int launch_gen_clean(void *stream_, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
-                        uint64_t G0, uint64_t G1, uint64_t ballot, uint32_t NB,
+                        uint64_t G0, uint64_t G1, uint64_t ballot, uint64_t B, uint32_t NB,
                         uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,
                         uint32_t *node, uint64_t *e_val, Frag *frags, uint64_t *f_off, uint32_t *b_msg,
                         uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep, uint64_t *cf_off, Frag *cfrags,
@@ -177,13 +186,14 @@ int launch_gen_clean(void *stream_, uint32_t N, uint64_t K, uint64_t k0, uint64_
                         uint64_t *b_bal)
 {
     hipStream_t s = (hipStream_t)stream_;
-    CleanGeo c{N, K, k0, sb, se, G0, G1, ballot};
+    CleanGeo c{N, K, k0, sb, se, G0, G1, ballot, B};
     const uint64_t G = G0 + (uint64_t)(N - 1) * G1;
     hipLaunchKernelGGL(k_gen_msgs, dim3(cdiv(G, 256)), dim3(256), 0, s, c, type, src, bal, aux, ent, cnt, node);
     hipLaunchKernelGGL(k_gen_entries, dim3(cdiv(se - sb, 256)), dim3(256), 0, s, c, e_val);
-    hipLaunchKernelGGL(k_gen_frags, dim3(cdiv((uint64_t)N * NB + 1, 256)), dim3(256), 0, s, c, NB, frags, f_off);
+    hipLaunchKernelGGL(k_gen_frags, dim3(cdiv((uint64_t)N * NB, 256)), dim3(256), 0, s, c, NB, frags, f_off, cfrags,
+                       cf_off);
     hipLaunchKernelGGL(k_gen_batches, dim3(cdiv(K + 1, 256)), dim3(256), 0, s, c, b_msg, b_pstart, b_rep_off, b_rep,
-                       cf_off, cfrags, b_rbal, b_rsrc, b_bal);
+                       b_rbal, b_rsrc, b_bal);
     hipLaunchKernelGGL(k_gen_scan, dim3(cdiv((uint64_t)N * (K + 1), 256)), dim3(256), 0, s, c, sc_type, sc_key, sc_idx);
     return (int)hipGetLastError();
 }

@@ -830,8 +830,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         for (uint32_t n = 0; n < N; ++n) {
             const uint64_t p = b * N + n, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
             if (!nf) continue;
-            const uint64_t bucket_frags = ht.f_off[(b + 1) * N] - ht.f_off[b * N];
-            bool fast = !member && N <= FAST_MAX_NODES && bucket_frags <= FAST_MAX_FRAGS && !ht.pair_ev[p];
+            bool fast = !member && N <= FAST_MAX_NODES && nf <= FAST_MAX_FRAGS && !ht.pair_ev[p];
             for (uint64_t f = f0; fast && f < f0 + nf; ++f) {
                 const uint8_t fl = ht.frags[f].flags;
                 fast = (fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT);

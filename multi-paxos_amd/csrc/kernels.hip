@@ -649,7 +649,7 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // one wait per step at 5.3 TB/s cached vs 5.7 TB/s nt on MI355X.
 //
 // A pair is taken here iff (same predicate as ingest.cpp's work list):
-// N <= FAST_MAX_NODES, the bucket has at most FAST_MAX_FRAGS fragments, the pair's fragments are all dense
+// N <= FAST_MAX_NODES, the pair has at most FAST_MAX_FRAGS fragments, all dense
 // ACCEPT / COMMIT runs and its node has no PREPARE after the first of them —
 // its snapshot events see empty state, so skipping them changes no output.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -753,11 +753,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
 
         // plan, one pair per lane
         const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64);
-        const uint64_t bb = __shfl(oa, (int)((pg * N) & 63), 64);           // bucket's first fragment
-        const uint64_t be = __shfl(oa, (int)((pg * N + N) & 63), 64);       // and its end
         const bool pair = lane < nb * N;
         const uint32_t len = pair ? (uint32_t)(o1 - oa) : 0;
-        const bool in_list = len && be - bb <= FAST_MAX_FRAGS;              // else: general work list
+        const bool in_list = len && len <= FAST_MAX_FRAGS;                  // else: general work list
         bool elig = in_list && len <= F, full = true, again = false, comm = false;
         uint32_t fix = NONE32, nA = 0, nL = 0;
 #pragma unroll
@@ -804,14 +802,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             }
         }
 
-        // per-slot path (rare): the pair's bucket window, lane i = fragment i
+        // per-slot path (rare): the pair's fragments, lane i = fragment i
         for (uint64_t m = slow_m; m; m &= m - 1) {
             const uint32_t p = (uint32_t)__builtin_ctzll(m);
             const uint32_t g = p / N, n = p - g * N;
             const uint64_t b = b0 + g, li0 = b << BSH, ib = v.shard_begin + li0;
-            const uint64_t f_base = rl64(oa, g * N);
-            const uint32_t total = (uint32_t)(rl64(oa, g * N + N) - f_base);
-            const uint32_t f0 = (uint32_t)(rl64(oa, p) - f_base), f1 = (uint32_t)(rl64(oa, p + 1) - f_base);
+            const uint64_t f_base = rl64(oa, p);
+            const uint32_t total = (uint32_t)(rl64(oa, p + 1) - f_base);   // <= FAST_MAX_FRAGS
+            const uint32_t f0 = 0, f1 = total;
             uint64_t fw0 = 0, fw1 = NONE32;
             uint32_t fflag = 0;
             if (lane < total) {
@@ -820,9 +818,8 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
                 fflag = v.m_flags[(uint32_t)fw1];
             }
             // eligibility of a pair with more fragments than a lane prefetches
-            const uint64_t rng = ((f1 - f0 >= 64) ? ~0ull : ((1ull << (f1 - f0)) - 1)) << f0;
             const uint64_t badm = __ballot(lane < total && !frag_lean(fw1));
-            if ((badm & rng) || ((pev_m >> p) & 1)) continue;
+            if (badm || ((pev_m >> p) & 1)) continue;
             if (lane == 0) v.st_valid[(uint64_t)n * NB + b] = 1;
             uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the lane's four slots
             uint32_t bad = 0;
@@ -882,7 +879,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             }
             if (__ballot(bad) && lane == 0) record_violation(v, MPX_V_COMMIT_VALUE, n, 0, ib);
             const uint64_t srow = (uint64_t)n * v.shard_len + li0;
-            const uint64_t pbase = f_base + f0;        // the pair's first fragment
+            const uint64_t pbase = f_base;             // the pair's first fragment
             const uint32_t l0 = q0 ? (uint32_t)(q0 - pbase) : 0, l1 = q1 ? (uint32_t)(q1 - pbase) : 0,
                            l2 = q2 ? (uint32_t)(q2 - pbase) : 0, l3 = q3 ? (uint32_t)(q3 - pbase) : 0;
             if (v.knobs & 16) {
@@ -964,9 +961,8 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
         const uint64_t b = i / N;
         const uint32_t n = (uint32_t)(i - b * N);
         const uint64_t oa = v.f_off[i], o1 = v.f_off[i + 1];
-        const uint64_t bb = v.f_off[b * N], be = v.f_off[b * N + N];
         const uint32_t len = (uint32_t)(o1 - oa);
-        const bool in_list = len && be - bb <= FAST_MAX_FRAGS;
+        const bool in_list = len && len <= FAST_MAX_FRAGS;
         uint64_t w[F];
         uint32_t fg[F];
 #pragma unroll

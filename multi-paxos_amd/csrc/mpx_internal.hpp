@@ -239,9 +239,10 @@ struct DevView {
     unsigned long long *summary;    // 64 words
 };
 
-// k_apply_fast takes a bucket's pairs only when its CSR offsets (N+1, plus two
-// chosen-log offsets) and its fragments (plus the chosen-log one) fit one
-// wave's lanes (kernels.hip, ingest.cpp work list)
+// k_plan / k_apply_fast take a pair only when its bucket's CSR offsets (N+1,
+// plus two chosen-log offsets) fit one wave's lanes and the pair has at most
+// FAST_MAX_FRAGS fragments (its per-slot path: lane i = fragment i); the rest
+// go to k_apply's work list (kernels.hip, ingest.cpp, engine.cpp)
 constexpr uint32_t FAST_MAX_NODES = 61;
 constexpr uint32_t FAST_MAX_FRAGS = 63;
 constexpr uint32_t APPLY_WGS_MAX = 2048;
@@ -289,8 +290,9 @@ int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, ui
 int launch_exec(const DevView &v, void *stream, uint32_t node, unsigned long long *aux, uint64_t *out);
 // digests of the resident state / chosen log -> out[0], out[1] (16 bytes, device)
 int launch_state_digest(const DevView &v, void *stream, unsigned long long *out);
+// f_off / cf_off: host-computed prefix counts (per pair, per bucket), read by the generator
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
-                     uint64_t G0, uint64_t G1, uint64_t ballot, uint32_t NB,
+                     uint64_t G0, uint64_t G1, uint64_t ballot, uint64_t B, uint32_t NB,
                      uint8_t *type, uint32_t *src, uint64_t *bal, uint64_t *aux, uint64_t *ent, uint32_t *cnt,
                      uint32_t *node, uint64_t *e_val, Frag *frags, uint64_t *f_off, uint32_t *b_msg,
                      uint32_t *b_pstart, uint64_t *b_rep_off, uint32_t *b_rep, uint64_t *cf_off, Frag *cfrags,

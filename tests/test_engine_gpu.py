@@ -174,14 +174,18 @@ def test_repeated_runs_are_identical():
         assert a[k] == b[k]
 
 
-@pytest.mark.parametrize("n,m", [(5, 4096), (9, 256 * 37), (2, 256)])
-def test_device_generator_matches_host(n, m):
+# batch != 256: a bucket meets 2-4 batches (partial runs, segmented plan
+# words); batch 7: 38-run pairs; batch 3: 172-run pairs go to k_apply's work list
+@pytest.mark.parametrize("n,m,b", [(5, 4096, 256), (9, 256 * 37, 256), (2, 256, 256), (5, 4096 + 77, 100),
+                                   (9, 256 * 37 + 5, 255), (9, 256 * 40, 100), (3, 1000, 37), (4, 3000, 7),
+                                   (2, 700, 3)])
+def test_device_generator_matches_host(n, m, b):
     """The HBM-materialised clean trace (mpx_load_clean_device) gives the same
     result bytes as the host trace through mpx_submit, and the oracle's."""
-    t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=256)
+    t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=b)
     want, ostats, _ = oracle_run(t)
     with mpx.Engine(n, 0, m) as e:
-        e.load_clean_device(num_instances=m)
+        e.load_clean_device(num_instances=m, batch=b)
         st = e.run()
         got = e.dump()
         _step_path(e, want, st)
@@ -190,20 +194,21 @@ def test_device_generator_matches_host(n, m):
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
 
 
-@pytest.mark.parametrize("shards", [2, 3, 8])
-def test_sharded_device_generator_sums_to_whole(shards):
+@pytest.mark.parametrize("shards,b", [(2, 256), (3, 256), (8, 256), (3, 100), (8, 255)])
+def test_sharded_device_generator_sums_to_whole(shards, b):
     """Instance sharding: per-shard counters and digests add
-    up to the single-engine run; per-acceptor scalars agree on every shard."""
+    up to the single-engine run; per-acceptor scalars agree on every shard
+    (batch 100 / 255: batches straddle the shard boundaries)."""
     n, m = 9, 256 * 64
     with mpx.Engine(n, 0, m) as e:
-        e.load_clean_device(num_instances=m)
+        e.load_clean_device(num_instances=m, batch=b)
         whole = e.run()
     per = m // shards // 256 * 256
     bounds = [(i * per, m if i == shards - 1 else (i + 1) * per) for i in range(shards)]
     tot = {k: 0 for k in ("chosen", "accept_apps", "commit_apps", "chosen_digest", "state_digest")}
     for sb, se in bounds:
         with mpx.Engine(n, sb, se) as e:
-            e.load_clean_device(num_instances=m)
+            e.load_clean_device(num_instances=m, batch=b)
             st = e.run()
             assert st["scalar_digest"] == whole["scalar_digest"]
             for k in tot:
