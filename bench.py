@@ -66,6 +66,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--instances", type=int, default=1 << 27, help="M (C4: 2^27)")
     ap.add_argument("--nodes", type=int, default=9, help="acceptors N (C4: 9)")
+    ap.add_argument("--batch", type=int, default=256, help="instances per ACCEPT / COMMIT batch (C4: 256)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c3-instances", type=int, default=1 << 24, help="C3 general-path leg: M (2^24); 0 = skip")
@@ -307,7 +308,7 @@ def main():
         uid = broadcast_bytes(pg, mpx.Engine.comm_unique_id() if rank == 0 else None, rank)
         eng.comm_init(uid, rank, world)
     t_gen = time.perf_counter()
-    eng.load_clean_device(num_instances=M, batch=256)
+    eng.load_clean_device(num_instances=M, batch=args.batch)
     t_gen = time.perf_counter() - t_gen
 
     for _ in range(args.warmup):
@@ -326,7 +327,10 @@ def main():
     dt_max = allreduce_max(pg, dt)
 
     st = eng.stats()
-    apply_ms, run_ms = eng.timings()
+    ph = eng.timings_detail()                       # per timed step: phase -> ms (HIP events)
+    apply_ms = [p["fast_apply"] + p["general_apply"] for p in ph]
+    run_ms = [p["run"] for p in ph]
+    phases = {k: sum(p[k] for p in ph) / max(len(ph), 1) for k in mpx.Engine.PHASES}
     tot = mdist.combine(eng.allgather_summary(world))   # also checks per-acceptor scalars agree
     chosen_total = tot["chosen"]
     assert chosen_total == M, "chosen %d != %d instances" % (chosen_total, M)
@@ -353,7 +357,9 @@ def main():
     # mpx_load_clean_device picks 1-byte slots) + the ACCEPT and COMMIT descriptors of every (node, bucket)
     # + the plan word of every (row, bucket), written by k_plan and read by k_store
     nb = (L + 255) // 256
-    bytes_min = 1 * N * L + 1 * L + 2 * 16 * N * nb + 2 * 4 * (N + 1) * nb
+    runs = sum(((min(b0 + 256, se) - 1) // args.batch - b0 // args.batch + 1)
+               for b0 in range(sb, se, 256)) if args.batch != 256 else nb   # batch runs meeting each bucket
+    bytes_min = 1 * N * L + 1 * L + 2 * 16 * N * runs + 2 * 8 * (N + 1) * nb
     achieved = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
     pmc = latest_pmc(N, M, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
@@ -381,16 +387,16 @@ def main():
             "dtype": "u64",
             "data": "synthetic (device-generated clean trace, decoded+bucketed in HBM before timing)",
             "config": {"workload": "C4: 2^27 instances x 9 acceptors, clean single round, batch 256, "
-                                   "instance-sharded over the GPUs" if (M, N) == (1 << 27, 9) else
-                                   "clean: %d instances x %d acceptors, batch 256" % (M, N),
-                       "instances": M, "acceptors": N, "batch": 256, "shard_per_gpu": se - sb,
+                                   "instance-sharded over the GPUs" if (M, N, args.batch) == (1 << 27, 9, 256) else
+                                   "clean: %d instances x %d acceptors, batch %d" % (M, N, args.batch),
+                       "instances": M, "acceptors": N, "batch": args.batch, "shard_per_gpu": se - sb,
                        "parallelism": "instance-shard x%d (RCCL all-gather of 64-word summaries)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "apply phase: k_plan + k_store + k_apply_fast<1,false,true>",
                          "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_min,
                          "bytes_model": "DESIGN.md §4: 1-B slot per (acceptor, instance) + 1-B chosen log + "
-                                        "16-B descriptors + 4-B plan words",
+                                        "16-B ACCEPT / COMMIT descriptors per run + 8-B plan words",
                          "bytes_survey_model_per_launch": bytes_survey,
                          "survey_model_gbps": bytes_survey / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0,
                          "frac_survey_model": bytes_survey / (apply_mean * 1e-3) / 1e9 / HBM_PEAK_GBS
@@ -409,6 +415,7 @@ def main():
             "hbm_gbps_alg_step": bytes_min * world / (dt_max / args.steps) / 1e9,
             "decisions_per_step": chosen_total,
             "run_ms_device": sum(run_ms) / max(len(run_ms), 1),
+            "phases_ms": phases,
             "trace_materialise_s": t_gen,
         }
         print(json.dumps(out), flush=True)

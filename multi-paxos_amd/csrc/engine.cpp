@@ -283,7 +283,7 @@ static int finish_view(mpx_engine *e)
     TRY(e->st.alloc((size_t)(N + 1) * e->shard_len * v.slot_w));   // row N: the chosen log
     TRY(e->st_valid.alloc((size_t)N * e->NB));
     TRY(e->chosen_valid.alloc(e->NB));
-    TRY(e->plan.alloc((size_t)(N + 1) * e->NB * 4));
+    TRY(e->plan.alloc((size_t)(N + 1) * e->NB * 8));
     TRY(e->fast_rest.alloc(8));
     TRY(e->store_dummy.alloc(64 * 1024));
     const uint64_t npairs = (uint64_t)N * e->NB;
@@ -303,7 +303,7 @@ static int finish_view(mpx_engine *e)
     v.st = e->st.p;
     v.st_valid = e->st_valid.as<uint8_t>();
         v.chosen_valid = e->chosen_valid.as<uint8_t>();
-    v.plan = e->plan.as<uint32_t>();
+    v.plan = e->plan.as<uint64_t>();
     v.fast_rest = e->fast_rest.as<uint32_t>();
     v.store_dummy = e->store_dummy.as<uint32_t>();
     v.out = e->out.as<OutRec>();

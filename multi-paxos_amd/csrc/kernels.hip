@@ -655,6 +655,8 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t FAST_PAIR_FRAGS = 2;      // descriptors a pair lane prefetches
 constexpr uint64_t EV_BIT = 1ull << 63;      // k_apply_fast: pair_ev folded into the lane's CSR offset
+constexpr uint64_t DONE_BIT = 1ull << 62;    // ... and (AFTER_STORE) "k_plan planned this pair"
+constexpr uint64_t OFF_FLAGS = EV_BIT | DONE_BIT;
 __host__ __device__ inline uint32_t fast_group(uint32_t N, uint32_t cap = 4)
 {
     return N ? (63 / N < cap ? 63 / N : cap) : 1;
@@ -693,15 +695,18 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         if (st >= steps) return;
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
         if (lane <= nb * N) oa = v.f_off[b0 * N + lane] | (lane < nb * N && v.pair_ev[b0 * N + lane] ? EV_BIT : 0);
+        if (AFTER_STORE && lane < nb * N &&   // the plan word's high half (PLAN_SKIP: all ones)
+            reinterpret_cast<const uint32_t *>(v.plan)[2 * ((uint64_t)pn * NB + b0 + pg) + 1] != 0xFFFFFFFFu)
+            oa |= DONE_BIT;
         if (lane <= nb) oc = v.cf_off[b0 + lane];
     };
     // stage 2 (one step ahead): each pair's first F descriptors, each
     // bucket's chosen-log descriptor when it is the only one
     auto ld_desc = [&](uint64_t st, uint64_t oa, uint64_t oc, uint64_t (&e)[F], uint64_t (&w)[F], uint64_t &ce,
                        uint64_t &cw) {
-        const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64) & ~EV_BIT;
+        const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64) & ~OFF_FLAGS;
         const uint64_t c1 = __shfl(oc, (int)((lane + 1) & 63), 64);
-        oa &= ~EV_BIT;
+        oa &= ~OFF_FLAGS;
 #pragma unroll
         for (uint32_t k = 0; k < F; ++k) { e[k] = 0; w[k] = NONE32; }
         ce = 0; cw = NONE32;
@@ -732,7 +737,8 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         const uint64_t st = st_c;
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
         const bool pev = (oa_c & EV_BIT) != 0;                 // the pair has snapshot events
-        const uint64_t oa = oa_c & ~EV_BIT;
+        const bool done = (oa_c & DONE_BIT) != 0;              // k_plan + k_store wrote it
+        const uint64_t oa = oa_c & ~OFF_FLAGS;
         const uint64_t pev_m = __ballot(pev);
         uint64_t e[F], w[F];
 #pragma unroll
@@ -755,7 +761,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64);
         const bool pair = lane < nb * N;
         const uint32_t len = pair ? (uint32_t)(o1 - oa) : 0;
-        const bool in_list = len && len <= FAST_MAX_FRAGS;                  // else: general work list
+        const bool in_list = len && len <= FAST_MAX_FRAGS && !done;         // else: general work list / stored
         bool elig = in_list && len <= F, full = true, again = false, comm = false;
         uint32_t fix = NONE32, nA = 0, nL = 0;
 #pragma unroll
@@ -770,9 +776,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         const bool uni = elig && full && !again;
         const uint64_t uni_m = __ballot(uni);
         const uint64_t slow_m = __ballot((elig && !uni) || (in_list && len > F));
-        // AFTER_STORE: k_plan counted and k_store wrote the uniform pairs of whole buckets
-        const bool stored = AFTER_STORE && (b0 + pg + 1) * BS <= v.shard_len;
-        if (uni && !stored) { cA += nA * BS; cL += nL * BS; }
+        if (uni) { cA += nA * BS; cL += nL * BS; }
         const uint32_t qv = fix == NONE32 ? 0 : (uint32_t)(oa + fix + 1);   // global fragment + 1
         const uint32_t ql = fix == NONE32 ? 0 : fix + 1;                     // as stored: pair-local
         if (elig) v.st_valid[(uint64_t)pn * NB + b0 + pg] = 1;
@@ -784,7 +788,6 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             for (uint32_t g = 0; g < nb; ++g) {
                 const uint32_t p = g * N + n;
                 if (!((uni_m >> p) & 1)) continue;
-                if (AFTER_STORE && (b0 + g + 1) * BS <= v.shard_len) continue;
                 const uint32_t q = rl32(qv, p);
                 const uint32_t sq = rl32(ql, p);
                 if (v.knobs & 16) {
@@ -935,20 +938,74 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
 }
 
 __device__ inline uint64_t frag_w1(const Frag *f) { return reinterpret_cast<const uint64_t *>(f)[1]; }
-constexpr uint32_t PLAN_SKIP = 0xFFFFFFFFu;   // fragment indices + 1 stay below (MPX_E_RANGE)
+
+// Plan words (k_plan -> k_store / k_store8; 64 bits per (row, bucket)): the
+// row's 256 slots as at most four segments of equal value —
+//   bits  0..31  v0..v3, the slot value of segment k (8 bits each)
+//   bits 32..58  s1, s2, s3 (9 bits each): segment k = slots [s_k, s_k+1) with
+//                s_0 = 0, s_4 = 256; unused splits are 256 and unused segments
+//                repeat the last value, so a one-segment word has v0 = .. = v3
+//                and its low half is already four slots' bytes
+// PLAN_SKIP: not k_store's row (k_apply_fast / k_chosen write it).
+constexpr uint64_t PLAN_SKIP = ~0ull;
+constexpr uint32_t PLAN_FRAGS = 8;                          // runs of a pair k_plan still plans
+constexpr uint32_t PLAN_UNI = BS | BS << 9 | BS << 18;      // bits 32..58 of a one-segment word
+
+__device__ inline uint32_t plan_split(uint64_t q, uint32_t k) { return (uint32_t)(q >> (32 + 9 * k)) & 511; }
+__device__ inline uint32_t plan_slot(uint64_t q, uint32_t s)
+{
+    const uint32_t k = (s >= plan_split(q, 0)) + (s >= plan_split(q, 1)) + (s >= plan_split(q, 2));
+    return (uint32_t)(q >> (8 * k)) & 0xFF;
+}
+// one-byte slots p..p+15: every byte picks its segment's value out of the low
+// word with v_perm (selector byte = segment index 0..3 = splits at or below it)
+__device__ inline u32x4 plan_bytes16(uint64_t q, uint32_t p)
+{
+    constexpr uint64_t ONES = 0x0101010101010101ull;
+    const uint32_t V = (uint32_t)q;
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+        const int t = (int)plan_split(q, k) - (int)p;        // window bytes >= t are at or past split k
+        lo += t <= 0 ? ONES : t >= 8 ? 0 : ONES << (8 * t);
+        hi += t <= 8 ? ONES : t >= 16 ? 0 : ONES << (8 * (t - 8));
+    }
+    return u32x4{__builtin_amdgcn_perm(V, V, (uint32_t)lo), __builtin_amdgcn_perm(V, V, (uint32_t)(lo >> 32)),
+                 __builtin_amdgcn_perm(V, V, (uint32_t)hi), __builtin_amdgcn_perm(V, V, (uint32_t)(hi >> 32))};
+}
+// the distinct run boundaries inside (0, 256), sorted into s[0..2] (BS = unused);
+// false once a fourth one appears
+__device__ inline bool plan_add_split(uint32_t x, uint32_t (&s)[3])
+{
+    if (x == 0 || x >= BS || x == s[0] || x == s[1] || x == s[2]) return true;
+    if (s[2] != BS) return false;
+    if (x < s[0]) { s[2] = s[1]; s[1] = s[0]; s[0] = x; }
+    else if (x < s[1]) { s[2] = s[1]; s[1] = x; }
+    else s[2] = x;
+    return true;
+}
+__device__ inline uint64_t plan_pack(const uint32_t (&val)[4], const uint32_t (&s)[3])
+{
+    return (uint64_t)(val[0] | val[1] << 8 | val[2] << 16 | val[3] << 24) |
+           ((uint64_t)s[0] << 32) | ((uint64_t)s[1] << 41) | ((uint64_t)s[2] << 50);
+}
 
 // Apply split in two (the default for multi runs): k_plan decides every pair
-// with one thread per pair — the same plan as k_apply_fast's pair lanes, but
-// with no per-step chain, so its gathers (CSR offsets, two descriptors, two
-// scan flags) all overlap — and k_store streams the result.  A (node, bucket)
-// pair whose fragments are full dense runs is fixed by one fragment, so its
-// plan word is that fragment's index + 1 and k_store writes it over the whole
-// 1 KiB of slots; the chosen log of a bucket with one live full batch is row N
-// (entry + 1 + slot).  Pairs that need the per-slot path, or a partial last
-// bucket, are counted in fast_rest and left to k_apply_fast<.., AFTER_STORE>.
+// with one thread per pair — no per-step chain, so its gathers (CSR offsets,
+// up to PLAN_FRAGS descriptors and scan flags) all overlap — and k_store
+// streams the result.  A (node, bucket) pair whose runs are all dense ACCEPT /
+// COMMIT runs cuts its bucket into segments at the runs' boundaries; in each
+// segment one run fixes every slot (the first COMMIT over it, else the last
+// granted ACCEPT, as in the per-slot path), so up to four segments are one
+// plan word of pair-local fragment + 1 values.  Batch 256 gives one segment,
+// batch 100 / 255 two to four (a bucket meets two to four batches).  The
+// chosen log of a bucket whose live batch runs do not overlap is row N the
+// same way (bucket-local chosen run + 1).  Pairs with more runs or segments, a
+// re-commit (its Value check) or a partial last bucket are counted in
+// fast_rest and left to k_apply_fast<.., AFTER_STORE>.
 __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
 {
-    constexpr uint32_t F = FAST_PAIR_FRAGS;
+    constexpr uint32_t F = PLAN_FRAGS;
     __shared__ unsigned long long red[4][3];
     __shared__ uint32_t rest_w[4];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -962,46 +1019,94 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
         const uint32_t n = (uint32_t)(i - b * N);
         const uint64_t oa = v.f_off[i], o1 = v.f_off[i + 1];
         const uint32_t len = (uint32_t)(o1 - oa);
-        const bool in_list = len && len <= FAST_MAX_FRAGS;
-        uint64_t w[F];
-        uint32_t fg[F];
+        const bool in_list = len && len <= FAST_MAX_FRAGS && !v.pair_ev[i];
+        uint64_t q = PLAN_SKIP;
+        if (in_list && len <= F) {
+            uint64_t w[F];
+            uint32_t fg[F];
 #pragma unroll
-        for (uint32_t k = 0; k < F; ++k) w[k] = k < len ? frag_w1(v.frags + oa + k) : (uint64_t)NONE32;
+            for (uint32_t k = 0; k < F; ++k) w[k] = k < len ? frag_w1(v.frags + oa + k) : 0;
 #pragma unroll
-        for (uint32_t k = 0; k < F; ++k)   // a COMMIT run's scan flag is never read
-            fg[k] = k < len && (w[k] >> 60) != K_COMMIT ? v.m_flags[(uint32_t)w[k]] : 0;
-        bool elig = in_list && len <= F, full = true, again = false, comm = false;
-        uint32_t fix = NONE32, nA = 0, nL = 0;
+            for (uint32_t k = 0; k < F; ++k)   // a COMMIT run's scan flag is never read
+                fg[k] = k < len && (w[k] >> 60) != K_COMMIT ? v.m_flags[(uint32_t)w[k]] : 0;
+            bool ok = (b + 1) * BS <= v.shard_len;
+            uint32_t sp[3] = {BS, BS, BS};
 #pragma unroll
-        for (uint32_t k = 0; k < F; ++k) {
-            if (k >= len) continue;
-            elig = elig && frag_lean(w[k]);
-            full = full && frag_full(w[k]);
-            if ((w[k] >> 60) == K_COMMIT) { ++nL; if (comm) again = true; else { comm = true; fix = k; } }
-            else if (!comm && (fg[k] & F_GRANTED)) { ++nA; fix = k; }
+            for (uint32_t k = 0; k < F; ++k) {
+                if (k >= len) continue;
+                const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
+                ok = ok && frag_lean(w[k]) && plan_add_split(st0, sp) && plan_add_split(st0 + cnt, sp);
+            }
+            uint32_t val[4];
+            unsigned long long a = 0, l = 0;
+#pragma unroll
+            for (uint32_t g = 0; g < 4; ++g) {
+                const uint32_t lo = g ? sp[g - 1] : 0, hi = g < 3 ? sp[g] : BS;
+                if (lo >= BS) { val[g] = val[g - 1]; continue; }
+                bool comm = false;
+                uint32_t fix = NONE32, nA = 0, nL = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < F; ++k) {
+                    if (k >= len) continue;
+                    const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
+                    if (lo < st0 || lo >= st0 + cnt) continue;          // segments lie inside or outside a run
+                    if ((w[k] >> 60) == K_COMMIT) { ++nL; if (comm) ok = false; else { comm = true; fix = k; } }
+                    else if (!comm && (fg[k] & F_GRANTED)) { ++nA; fix = k; }
+                }
+                val[g] = fix == NONE32 ? 0 : fix + 1;               // the slot as stored: pair-local fragment + 1
+                a += (unsigned long long)nA * (hi - lo);
+                l += (unsigned long long)nL * (hi - lo);
+            }
+            if (ok) {
+                q = plan_pack(val, sp);
+                v.st_valid[(uint64_t)n * NB + b] = 1;
+                cA = a; cL = l;
+            }
         }
-        elig = elig && len && !v.pair_ev[i];
-        const bool uni = elig && full && !again;
-        const bool whole = (b + 1) * BS <= v.shard_len;
-        uint32_t q = PLAN_SKIP;
-        if (uni && whole) {
-            q = fix == NONE32 ? 0 : fix + 1;             // the slot as stored: pair-local fragment + 1
-            v.st_valid[(uint64_t)n * NB + b] = 1;
-            cA = nA * BS; cL = nL * BS;
-        } else if (elig || (in_list && len > F)) {
-            rest = 1;
-        }
+        if (q == PLAN_SKIP && in_list) rest = 1;
         v.plan[(uint64_t)n * NB + b] = q;
     }
     if (i < NB) {
         const uint64_t oc = v.cf_off[i], c1 = v.cf_off[i + 1];
-        uint32_t q = PLAN_SKIP;
-        if (c1 - oc == 1) {
-            const uint64_t cw = frag_w1(v.cfrags + oc);
-            if (v.b_chosen[(uint32_t)cw] != NONE32 && frag_full(cw) && (i + 1) * BS <= v.shard_len) {
-                q = 1;                                   // its only chosen fragment, + 1
+        const uint32_t len = (uint32_t)(c1 - oc);
+        uint64_t q = PLAN_SKIP;
+        if (len && len <= F && (i + 1) * BS <= v.shard_len) {
+            uint64_t w[F];
+            uint32_t live[F];
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k) w[k] = k < len ? frag_w1(v.cfrags + oc + k) : 0;
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k) live[k] = k < len ? v.b_chosen[(uint32_t)w[k]] != NONE32 : 0;
+            bool ok = true;
+            uint32_t sp[3] = {BS, BS, BS};
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k) {
+                if (k >= len) continue;
+                const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
+                ok = ok && ((w[k] >> 56) & FR_DENSE) && plan_add_split(st0, sp) && plan_add_split(st0 + cnt, sp);
+            }
+            uint32_t val[4];
+            unsigned long long c = 0;
+#pragma unroll
+            for (uint32_t g = 0; g < 4; ++g) {
+                const uint32_t lo = g ? sp[g - 1] : 0, hi = g < 3 ? sp[g] : BS;
+                if (lo >= BS) { val[g] = val[g - 1]; continue; }
+                uint32_t fix = NONE32;
+#pragma unroll
+                for (uint32_t k = 0; k < F; ++k) {
+                    if (k >= len || !live[k]) continue;
+                    const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
+                    if (lo < st0 || lo >= st0 + cnt) continue;
+                    if (fix != NONE32) ok = false;                    // two chosen runs: k_chosen compares Values
+                    else fix = k;
+                }
+                val[g] = fix == NONE32 ? 0 : fix + 1;
+                if (fix != NONE32) c += hi - lo;
+            }
+            if (ok) {
+                q = plan_pack(val, sp);
                 v.chosen_valid[i] = 1;
-                cC = BS;
+                cC = c;
             }
         }
         v.plan[(uint64_t)N * NB + i] = q;
@@ -1043,7 +1148,7 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
 template <uint32_t C, bool NT, typename T, typename V>
 __device__ inline uint64_t store_chunks(const DevView &v, uint64_t c, const uint64_t c_base, const uint64_t c_end,
                                         const uint64_t cpr, const uint32_t prow0, T *const base0, const uint64_t stride,
-                                        const uint32_t inc, T *const sink, const uint64_t nwaves)
+                                        T *const sink, const uint64_t nwaves)
 {
     if (c >= c_end) return c;
     const uint32_t lane = threadIdx.x & 63, s0 = 4 * lane;
@@ -1052,26 +1157,26 @@ __device__ inline uint64_t store_chunks(const DevView &v, uint64_t c, const uint
     const uint32_t step_r = (uint32_t)(nwaves / cpr), step_k = (uint32_t)(nwaves - (uint64_t)step_r * cpr);
     // unconditional plan load (lanes >= C repeat lanes 0..C-1; past the end:
     // a valid dummy address) so the compiler can count it exactly
-    auto ptr = [&](uint64_t cc, uint32_t rr, uint32_t kk) -> const uint32_t * {
+    auto ptr = [&](uint64_t cc, uint32_t rr, uint32_t kk) -> const uint64_t * {
         const uint64_t o = cc < c_end ? (uint64_t)(prow0 + rr) * v.NB + (uint64_t)kk * C : (uint64_t)prow0 * v.NB;
         return v.plan + o + (lane & (C - 1));
     };
-    uint32_t qn = *ptr(c, rn, kn);
+    uint64_t qn = *ptr(c, rn, kn);
     // settled before the loop: the loop-carried plan word then has one pending
     // source, the in-loop load, which waits as vmcnt(C) (its C stores in flight)
     __builtin_amdgcn_s_waitcnt(0x0F70);
     for (; c < c_end; c += nwaves) {
-        const uint32_t qw = qn, rc = rn, kc = kn;
+        const uint64_t qw = qn;
+        const uint32_t rc = rn, kc = kn;
         rn += step_r; kn += step_k;
         if (kn >= cpr) { kn -= (uint32_t)cpr; ++rn; }
         qn = *ptr(c + nwaves, rn, kn);
         T *const base = base0 + (uint64_t)rc * stride + ((uint64_t)kc * C << BSH) + s0;
 #pragma unroll
         for (uint32_t j = 0; j < C; ++j) {
-            const uint32_t q = __builtin_amdgcn_readlane(qw, j);
-            const T x = (T)(q + inc * s0);
+            const uint64_t q = rl64(qw, j);                 // wave-uniform: the segment math is scalar
             T *const dst = q == PLAN_SKIP ? sink : base + j * BS;
-            const V val = V{x, (T)(x + inc), (T)(x + 2 * inc), (T)(x + 3 * inc)};
+            const V val = V{(T)plan_slot(q, s0), (T)plan_slot(q, s0 + 1), (T)plan_slot(q, s0 + 2), (T)plan_slot(q, s0 + 3)};
             if (NT) __builtin_nontemporal_store(val, reinterpret_cast<V *>(dst));
             else *reinterpret_cast<V *>(dst) = val;
         }
@@ -1094,15 +1199,16 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
     const uint32_t s0 = 4 * lane;
     uint32_t *const sink = v.store_dummy + (wid & 63) * BS;
     T *const st = static_cast<T *>(v.st);
-    store_chunks<C, NT, T, V>(v, wid, 0, S, cpr, 0, st, v.shard_len, 0, reinterpret_cast<T *>(sink) + s0, nwaves);
+    store_chunks<C, NT, T, V>(v, wid, 0, S, cpr, 0, st, v.shard_len, reinterpret_cast<T *>(sink) + s0, nwaves);
     // tail: the whole buckets after each row's last full chunk
     const uint64_t tpr = whole - cpr * C, tails = (uint64_t)(N + 1) * tpr;
     for (uint64_t t = wid; t < tails; t += nwaves) {
         const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
-        const uint32_t q = v.plan[r * NB + b];
+        const uint64_t q = v.plan[r * NB + b];
         if (q == PLAN_SKIP) continue;
-        const T x = (T)q;
-        __builtin_nontemporal_store(V{x, x, x, x}, reinterpret_cast<V *>(st + r * v.shard_len + (b << BSH) + s0));
+        __builtin_nontemporal_store(V{(T)plan_slot(q, s0), (T)plan_slot(q, s0 + 1), (T)plan_slot(q, s0 + 2),
+                                      (T)plan_slot(q, s0 + 3)},
+                                    reinterpret_cast<V *>(st + r * v.shard_len + (b << BSH) + s0));
     }
 }
 
@@ -1112,7 +1218,10 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
 // 16l..16l+15 of buckets 4j..4j+3, its plan word fetched with a cross-lane
 // shuffle (LDS permute, lgkmcnt) from the chunk's plan words (one or two per
 // lane), which are loaded one chunk ahead as in k_store (the loop waits
-// vmcnt(C / 4): the previous chunk's stores stay in flight).  Tail buckets of a row go through the per-bucket loop.
+// vmcnt(C / 4): the previous chunk's stores stay in flight).  When every word
+// of a store is one segment (batch 256) its low half is the 16 bytes; else
+// plan_bytes16 expands the segments.  Tail buckets of a row go through the
+// per-bucket loop.
 template <bool NT, uint32_t C = 64>
 __global__ __launch_bounds__(256) void k_store8(DevView v)
 {
@@ -1126,16 +1235,18 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
     const uint64_t wid = xcd_wave_id(wv, v.knobs);
     uint8_t *const st = static_cast<uint8_t *>(v.st);
     uint8_t *const sink = reinterpret_cast<uint8_t *>(v.store_dummy) + (wid & 63) * 1024 + 16 * lane;
+    const uint32_t p16 = 16 * (lane & 15);                 // the lane's first slot in its bucket
     if (wid < S) {
         uint32_t rn = (uint32_t)(wid / cpr), kn = (uint32_t)(wid - (uint64_t)rn * cpr);
         const uint32_t step_r = (uint32_t)(nwaves / cpr), step_k = (uint32_t)(nwaves - (uint64_t)step_r * cpr);
-        auto ptr = [&](uint64_t cc, uint32_t rr, uint32_t kk) -> const uint32_t * {
+        auto ptr = [&](uint64_t cc, uint32_t rr, uint32_t kk) -> const uint64_t * {
             return v.plan + (cc < S ? (uint64_t)rr * NB + (uint64_t)kk * C : 0) + lane;
         };
-        uint32_t qn = *ptr(wid, rn, kn), qn1 = C == 128 ? ptr(wid, rn, kn)[64] : 0;
+        uint64_t qn = *ptr(wid, rn, kn), qn1 = C == 128 ? ptr(wid, rn, kn)[64] : 0;
         __builtin_amdgcn_s_waitcnt(0x0F70);
         for (uint64_t c = wid; c < S; c += nwaves) {
-            const uint32_t qw = qn, qw1 = qn1, rc = rn, kc = kn;
+            const uint64_t qw = qn, qw1 = qn1;
+            const uint32_t rc = rn, kc = kn;
             rn += step_r; kn += step_k;
             if (kn >= cpr) { kn -= (uint32_t)cpr; ++rn; }
             qn = *ptr(c + nwaves, rn, kn);
@@ -1143,11 +1254,13 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
             uint8_t *const base = st + (uint64_t)rc * v.shard_len + ((uint64_t)kc * C << BSH) + 16 * lane;
 #pragma unroll
             for (uint32_t j = 0; j < C / 4; ++j) {
-                const uint32_t q = (uint32_t)__shfl((int)(j < 16 ? qw : qw1), (int)((4 * j + (lane >> 4)) & 63), 64);
-                const uint32_t x = (q & 0xFF) * 0x01010101u;
+                const uint64_t q = __shfl(j < 16 ? qw : qw1, (int)((4 * j + (lane >> 4)) & 63), 64);
                 uint8_t *const dst = q == PLAN_SKIP ? sink : base + 1024 * j;
-                if (NT) __builtin_nontemporal_store(u32x4{x, x, x, x}, reinterpret_cast<u32x4 *>(dst));
-                else *reinterpret_cast<u32x4 *>(dst) = u32x4{x, x, x, x};
+                u32x4 x;
+                if (__ballot(q != PLAN_SKIP && (uint32_t)(q >> 32) != PLAN_UNI)) x = plan_bytes16(q, p16);
+                else x = u32x4{(uint32_t)q, (uint32_t)q, (uint32_t)q, (uint32_t)q};
+                if (NT) __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(dst));
+                else *reinterpret_cast<u32x4 *>(dst) = x;
             }
         }
     }
@@ -1155,10 +1268,11 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
     const uint64_t tpr = whole - cpr * C, tails = (uint64_t)(N + 1) * tpr;
     for (uint64_t t = wid; t < tails; t += nwaves) {
         const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
-        const uint32_t q = v.plan[r * NB + b];
+        const uint64_t q = v.plan[r * NB + b];
         if (q == PLAN_SKIP) continue;
-        const uint8_t x = (uint8_t)q;
-        __builtin_nontemporal_store(u8x4{x, x, x, x}, reinterpret_cast<u8x4 *>(st + r * v.shard_len + (b << BSH) + s0));
+        __builtin_nontemporal_store(u8x4{(uint8_t)plan_slot(q, s0), (uint8_t)plan_slot(q, s0 + 1),
+                                         (uint8_t)plan_slot(q, s0 + 2), (uint8_t)plan_slot(q, s0 + 3)},
+                                    reinterpret_cast<u8x4 *>(st + r * v.shard_len + (b << BSH) + s0));
     }
 }
 

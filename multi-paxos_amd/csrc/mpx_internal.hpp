@@ -226,7 +226,7 @@ struct DevView {
     uint8_t *st_valid;              // per (node, bucket): node * NB + bucket
     // chosen log: row N of st (per instance: the bucket's chosen fragment (cf_off) + 1)
     uint8_t *chosen_valid;          // per bucket
-    uint32_t *plan;                 // (N + 1) * NB: the value k_store writes over a whole (row, bucket),
+    uint64_t *plan;                 // (N + 1) * NB: the segments k_store writes over a whole (row, bucket),
                                     // rows 0..N-1 state, row N chosen log; PLAN_SKIP = not by k_store
     uint32_t *fast_rest;            // pairs k_plan leaves to k_apply_fast (0: it exits at once)
     uint32_t *store_dummy;          // 64 KiB sink for k_store's skipped (row, bucket) stores
