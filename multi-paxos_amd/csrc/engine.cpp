@@ -76,7 +76,8 @@ struct mpx_engine {
     DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
     DevBuf sc_type, sc_key, sc_idx, b_rbal, b_rsrc, b_bal;
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
-    DevBuf f_off, frags, gp_list, ev_off, ev_msg, pl_off, pl_msg;
+    DevBuf f_off, frags, frag_w1, gp_list, ev_off, ev_msg, pl_off, pl_msg;
+    uint64_t num_frags = 0;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
     DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy, exec_aux, exec_out;
     DevBuf decode_buf;                      // readback scratch (k_decode)
@@ -284,6 +285,9 @@ static int finish_view(mpx_engine *e)
     TRY(e->st_valid.alloc((size_t)N * e->NB));
     TRY(e->chosen_valid.alloc(e->NB));
     TRY(e->plan.alloc((size_t)(N + 1) * e->NB * 8));
+    TRY(e->frag_w1.alloc(std::max<size_t>(8 * e->num_frags, 8)));
+    if (launch_frag_w1(v.frags, e->frag_w1.as<uint64_t>(), e->num_frags, e->stream) != 0) return MPX_E_HIP;
+    v.frag_w1 = e->frag_w1.as<uint64_t>();
     TRY(e->fast_rest.alloc(8));
     TRY(e->store_dummy.alloc(64 * 1024));
     const uint64_t npairs = (uint64_t)N * e->NB;
@@ -382,6 +386,7 @@ static int upload_trace(mpx_engine *e)
     v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
+    e->num_frags = h.frags.size();
     v.num_gp = h.gp_list.size(); v.gp_list = e->gp_list.as<uint64_t>();
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
@@ -1061,6 +1066,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
+    e->num_frags = f_off[N * NB];
     v.num_gp = gd.size() / GP_WORDS; v.gp_list = e->gp_list.as<uint64_t>();
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();

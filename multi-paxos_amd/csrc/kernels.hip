@@ -63,6 +63,15 @@ __device__ inline uint64_t rl64(uint64_t x, uint32_t i)
 }
 __device__ inline uint32_t rl32(uint32_t x, uint32_t i) { return __builtin_amdgcn_readlane(x, i); }
 
+// per-pair arrays (st_valid, the state rows' plan words) are pair-major like
+// the fragment CSR, q = bucket * N + node, so the pair-per-lane kernels write
+// them coalesced; the chosen log's plan words follow at N * NB + bucket
+__device__ inline uint64_t sv_idx(const DevView &v, uint32_t n, uint64_t b) { return b * v.N + n; }
+__device__ inline uint64_t plan_idx(const DevView &v, uint32_t row, uint64_t b)
+{
+    return row < v.N ? b * v.N + row : (uint64_t)v.N * v.NB + b;
+}
+
 __device__ inline void wave_lds_fence()
 {
     // LDS instructions of one wave execute in order; keep the compiler from
@@ -696,7 +705,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
         if (lane <= nb * N) oa = v.f_off[b0 * N + lane] | (lane < nb * N && v.pair_ev[b0 * N + lane] ? EV_BIT : 0);
         if (AFTER_STORE && lane < nb * N &&   // the plan word's high half (PLAN_SKIP: all ones)
-            reinterpret_cast<const uint32_t *>(v.plan)[2 * ((uint64_t)pn * NB + b0 + pg) + 1] != 0xFFFFFFFFu)
+            reinterpret_cast<const uint32_t *>(v.plan)[2 * (b0 * N + lane) + 1] != 0xFFFFFFFFu)
             oa |= DONE_BIT;
         if (lane <= nb) oc = v.cf_off[b0 + lane];
     };
@@ -779,7 +788,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         if (uni) { cA += nA * BS; cL += nL * BS; }
         const uint32_t qv = fix == NONE32 ? 0 : (uint32_t)(oa + fix + 1);   // global fragment + 1
         const uint32_t ql = fix == NONE32 ? 0 : fix + 1;                     // as stored: pair-local
-        if (elig) v.st_valid[(uint64_t)pn * NB + b0 + pg] = 1;
+        if (elig) v.st_valid[b0 * N + lane] = 1;
 
         // uniform pairs, node-major so each row gets its G buckets back to back
         const bool whole = (b0 + nb) * BS <= v.shard_len;
@@ -823,7 +832,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             // eligibility of a pair with more fragments than a lane prefetches
             const uint64_t badm = __ballot(lane < total && !frag_lean(fw1));
             if (badm || ((pev_m >> p) & 1)) continue;
-            if (lane == 0) v.st_valid[(uint64_t)n * NB + b] = 1;
+            if (lane == 0) v.st_valid[sv_idx(v, n, b)] = 1;
             uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the lane's four slots
             uint32_t bad = 0;
             // per slot: the fixing fragment (8 bits per slot: its lane, 0xFF
@@ -949,6 +958,7 @@ __device__ inline uint64_t frag_w1(const Frag *f) { return reinterpret_cast<cons
 // PLAN_SKIP: not k_store's row (k_apply_fast / k_chosen write it).
 constexpr uint64_t PLAN_SKIP = ~0ull;
 constexpr uint32_t PLAN_FRAGS = 8;                          // runs of a pair k_plan still plans
+constexpr uint32_t PLAN_LDS = 512;                          // descriptor words a k_plan wave stages (4 KiB)
 constexpr uint32_t PLAN_UNI = BS | BS << 9 | BS << 18;      // bits 32..58 of a one-segment word
 
 __device__ inline uint32_t plan_split(uint64_t q, uint32_t k) { return (uint32_t)(q >> (32 + 9 * k)) & 511; }
@@ -1008,24 +1018,37 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
     constexpr uint32_t F = PLAN_FRAGS;
     __shared__ unsigned long long red[4][3];
     __shared__ uint32_t rest_w[4];
+    __shared__ uint64_t w_lds[4][PLAN_LDS];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t N = v.N;
     const uint64_t NB = v.NB, np = (uint64_t)N * NB;
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     unsigned long long cA = 0, cL = 0, cC = 0;
     uint32_t rest = 0;
+    // the wave's 64 pairs own one contiguous descriptor range: stream its
+    // second words into LDS with coalesced loads (lane r: words r, r + 64, ..),
+    // then every pair lane reads its runs from there
+    const uint64_t oa = v.f_off[i < np ? i : np], o1 = v.f_off[i < np ? i + 1 : np];
+    const uint64_t wbase = rl64(oa, 0);
+    {
+        const uint64_t wend = rl64(o1, 63);
+        const uint32_t R = (uint32_t)(wend - wbase < PLAN_LDS ? wend - wbase : PLAN_LDS);
+        for (uint32_t r = lane; r < R; r += 64) w_lds[wv][r] = v.frag_w1[wbase + r];
+        wave_lds_fence();
+    }
     if (i < np) {
         const uint64_t b = i / N;
         const uint32_t n = (uint32_t)(i - b * N);
-        const uint64_t oa = v.f_off[i], o1 = v.f_off[i + 1];
         const uint32_t len = (uint32_t)(o1 - oa);
         const bool in_list = len && len <= FAST_MAX_FRAGS && !v.pair_ev[i];
         uint64_t q = PLAN_SKIP;
         if (in_list && len <= F) {
             uint64_t w[F];
             uint32_t fg[F];
+            const uint64_t rel = oa - wbase;                 // past the staged words: global loads (rare)
 #pragma unroll
-            for (uint32_t k = 0; k < F; ++k) w[k] = k < len ? frag_w1(v.frags + oa + k) : 0;
+            for (uint32_t k = 0; k < F; ++k)
+                w[k] = k >= len ? 0 : rel + k < PLAN_LDS ? w_lds[wv][rel + k] : v.frag_w1[oa + k];
 #pragma unroll
             for (uint32_t k = 0; k < F; ++k)   // a COMMIT run's scan flag is never read
                 fg[k] = k < len && (w[k] >> 60) != K_COMMIT ? v.m_flags[(uint32_t)w[k]] : 0;
@@ -1059,12 +1082,12 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
             }
             if (ok) {
                 q = plan_pack(val, sp);
-                v.st_valid[(uint64_t)n * NB + b] = 1;
+                v.st_valid[i] = 1;
                 cA = a; cL = l;
             }
         }
         if (q == PLAN_SKIP && in_list) rest = 1;
-        v.plan[(uint64_t)n * NB + b] = q;
+        v.plan[i] = q;
     }
     if (i < NB) {
         const uint64_t oc = v.cf_off[i], c1 = v.cf_off[i + 1];
@@ -1158,8 +1181,7 @@ __device__ inline uint64_t store_chunks(const DevView &v, uint64_t c, const uint
     // unconditional plan load (lanes >= C repeat lanes 0..C-1; past the end:
     // a valid dummy address) so the compiler can count it exactly
     auto ptr = [&](uint64_t cc, uint32_t rr, uint32_t kk) -> const uint64_t * {
-        const uint64_t o = cc < c_end ? (uint64_t)(prow0 + rr) * v.NB + (uint64_t)kk * C : (uint64_t)prow0 * v.NB;
-        return v.plan + o + (lane & (C - 1));
+        return cc < c_end ? v.plan + plan_idx(v, prow0 + rr, (uint64_t)kk * C + (lane & (C - 1))) : v.plan;
     };
     uint64_t qn = *ptr(c, rn, kn);
     // settled before the loop: the loop-carried plan word then has one pending
@@ -1204,7 +1226,7 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
     const uint64_t tpr = whole - cpr * C, tails = (uint64_t)(N + 1) * tpr;
     for (uint64_t t = wid; t < tails; t += nwaves) {
         const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
-        const uint64_t q = v.plan[r * NB + b];
+        const uint64_t q = v.plan[plan_idx(v, (uint32_t)r, b)];
         if (q == PLAN_SKIP) continue;
         __builtin_nontemporal_store(V{(T)plan_slot(q, s0), (T)plan_slot(q, s0 + 1), (T)plan_slot(q, s0 + 2),
                                       (T)plan_slot(q, s0 + 3)},
@@ -1239,18 +1261,19 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
     if (wid < S) {
         uint32_t rn = (uint32_t)(wid / cpr), kn = (uint32_t)(wid - (uint64_t)rn * cpr);
         const uint32_t step_r = (uint32_t)(nwaves / cpr), step_k = (uint32_t)(nwaves - (uint64_t)step_r * cpr);
-        auto ptr = [&](uint64_t cc, uint32_t rr, uint32_t kk) -> const uint64_t * {
-            return v.plan + (cc < S ? (uint64_t)rr * NB + (uint64_t)kk * C : 0) + lane;
+        // plan words of bucket kk * C + lane (and + 64) of row rr; past the end: a valid dummy
+        auto ld = [&](uint64_t cc, uint32_t rr, uint32_t kk, uint32_t off) -> uint64_t {
+            return v.plan[cc < S ? plan_idx(v, rr, (uint64_t)kk * C + off + lane) : lane];
         };
-        uint64_t qn = *ptr(wid, rn, kn), qn1 = C == 128 ? ptr(wid, rn, kn)[64] : 0;
+        uint64_t qn = ld(wid, rn, kn, 0), qn1 = C == 128 ? ld(wid, rn, kn, 64) : 0;
         __builtin_amdgcn_s_waitcnt(0x0F70);
         for (uint64_t c = wid; c < S; c += nwaves) {
             const uint64_t qw = qn, qw1 = qn1;
             const uint32_t rc = rn, kc = kn;
             rn += step_r; kn += step_k;
             if (kn >= cpr) { kn -= (uint32_t)cpr; ++rn; }
-            qn = *ptr(c + nwaves, rn, kn);
-            if (C == 128) qn1 = ptr(c + nwaves, rn, kn)[64];
+            qn = ld(c + nwaves, rn, kn, 0);
+            if (C == 128) qn1 = ld(c + nwaves, rn, kn, 64);
             uint8_t *const base = st + (uint64_t)rc * v.shard_len + ((uint64_t)kc * C << BSH) + 16 * lane;
 #pragma unroll
             for (uint32_t j = 0; j < C / 4; ++j) {
@@ -1268,7 +1291,7 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
     const uint64_t tpr = whole - cpr * C, tails = (uint64_t)(N + 1) * tpr;
     for (uint64_t t = wid; t < tails; t += nwaves) {
         const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
-        const uint64_t q = v.plan[r * NB + b];
+        const uint64_t q = v.plan[plan_idx(v, (uint32_t)r, b)];
         if (q == PLAN_SKIP) continue;
         __builtin_nontemporal_store(u8x4{(uint8_t)plan_slot(q, s0), (uint8_t)plan_slot(q, s0 + 1),
                                          (uint8_t)plan_slot(q, s0 + 2), (uint8_t)plan_slot(q, s0 + 3)},
@@ -1555,7 +1578,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                 if (DIGEST && SF(j))
                     dig += state_digest(n, v.shard_begin + li, (SF(j) & S_COMMITTED) ? 2 : 1, sb[DIGEST ? j : 0], e_val[se[j]]);
             }
-            if (lane == 0) v.st_valid[(uint64_t)n * v.NB + b] = 1;
+            if (lane == 0) v.st_valid[sv_idx(v, n, b)] = 1;
         }
     }
     // workgroup reduction of the counters
@@ -1691,7 +1714,7 @@ __global__ __launch_bounds__(256) void k_decode(DevView v, uint32_t node, uint64
                     if (v.e_slot[f.entry + k] == sl) { ent = f.entry + k; break; }
             w = W_PRESENT | v.e_val[ent];
         }
-    } else if (v.st_valid[(uint64_t)node * v.NB + (li >> BSH)]) {
+    } else if (v.st_valid[sv_idx(v, node, li >> BSH)]) {
         decode_slot(v, slot_global(v, node, li), (uint32_t)li & (BS - 1), b, w);
     }
     out[2 * i] = b;
@@ -1711,7 +1734,7 @@ __global__ __launch_bounds__(256) void k_state_digest(DevView v, unsigned long l
         const uint64_t li = i - (uint64_t)row * v.shard_len;
         const uint64_t iid = v.shard_begin + li;
         if (row < v.N) {
-            if (v.st_valid[(uint64_t)row * v.NB + (li >> BSH)]) ds += slot_digest(v, row, iid, slot_global(v, row, li));
+            if (v.st_valid[sv_idx(v, row, li >> BSH)]) ds += slot_digest(v, row, iid, slot_global(v, row, li));
         } else if (v.chosen_valid[li >> BSH]) {
             const uint32_t c = st_get(v, (uint64_t)v.N * v.shard_len + li);
             if (c) {
@@ -1750,7 +1773,7 @@ int launch_state_digest(const DevView &v, void *stream, unsigned long long *out)
 // aux layout: [0] frontier, [1 .. NB] bucket counts, [NB + 1 .. 2 NB + 1] offsets
 __device__ inline uint64_t exec_word(const DevView &v, uint32_t node, uint64_t li)
 {
-    if (!v.st_valid[(uint64_t)node * v.NB + (li >> BSH)]) return 0;
+    if (!v.st_valid[sv_idx(v, node, li >> BSH)]) return 0;
     uint64_t b, w;
     decode_slot(v, slot_global(v, node, li), (uint32_t)li & (BS - 1), b, w);
     return w;
@@ -1840,6 +1863,19 @@ int launch_exec(const DevView &v, void *stream_, uint32_t node, unsigned long lo
     return (int)hipGetLastError();
 }
 
+__global__ void k_frag_w1(const Frag *frags, uint64_t *out, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = frag_w1(frags + i);
+}
+
+int launch_frag_w1(const Frag *frags, uint64_t *out, uint64_t n, void *stream)
+{
+    if (!n) return 0;
+    hipLaunchKernelGGL(k_frag_w1, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, frags, out, n);
+    return (int)hipGetLastError();
+}
+
 int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, uint64_t count, uint64_t *out)
 {
     if (!count) return 0;
@@ -1880,6 +1916,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (v.digest) hipLaunchKernelGGL((k_apply_fast<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
         else if (!(v.knobs & 64) && v.N <= FAST_MAX_NODES) {
             // plan + stream, then the per-slot pairs (knob 64: the one-kernel form)
+            // (a persistent software-pipelined k_plan — next group's descriptor words and the
+            // one after's offsets in flight — measured slower: 0.329 vs 0.304 ms apply phase)
             hipLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s, v, g.apply_wgs);
             if (v.slot_w == 1 && (v.knobs & 128)) hipLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
             // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64

@@ -223,10 +223,12 @@ struct DevView {
     // state
     void *st;                       // one slot per (node, instance), node-major, slot_w bytes each
     uint32_t slot_w;                // 1 when every pair / bucket has <= MAX_PAIR_FRAGS_1 fragments, else 2
-    uint8_t *st_valid;              // per (node, bucket): node * NB + bucket
+    uint8_t *st_valid;              // per (node, bucket) pair: bucket * N + node (sv_idx)
     // chosen log: row N of st (per instance: the bucket's chosen fragment (cf_off) + 1)
     uint8_t *chosen_valid;          // per bucket
-    uint64_t *plan;                 // (N + 1) * NB: the segments k_store writes over a whole (row, bucket),
+    const uint64_t *frag_w1;        // frags[i]'s second word (message, count, start, flags): k_plan's
+                                    // half of the descriptor, streamed without the entry words
+    uint64_t *plan;                 // (N + 1) * NB: the segments k_store writes over a whole (row, bucket) (plan_idx),
                                     // rows 0..N-1 state, row N chosen log; PLAN_SKIP = not by k_store
     uint32_t *fast_rest;            // pairs k_plan leaves to k_apply_fast (0: it exits at once)
     uint32_t *store_dummy;          // 64 KiB sink for k_store's skipped (row, bucket) stores
@@ -290,6 +292,8 @@ int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, ui
 int launch_exec(const DevView &v, void *stream, uint32_t node, unsigned long long *aux, uint64_t *out);
 // digests of the resident state / chosen log -> out[0], out[1] (16 bytes, device)
 int launch_state_digest(const DevView &v, void *stream, unsigned long long *out);
+// out[i] = second word of frags[i], i < n (once per trace load)
+int launch_frag_w1(const Frag *frags, uint64_t *out, uint64_t n, void *stream);
 // f_off / cf_off: host-computed prefix counts (per pair, per bucket), read by the generator
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
                      uint64_t G0, uint64_t G1, uint64_t ballot, uint64_t B, uint32_t NB,
