@@ -79,10 +79,10 @@ def main():
                 out["kernels"][name][c] = mean(per[name])
     # the timed apply phase: k_plan + k_store + k_apply_fast<1, false, true>
     # (digest runs use the one-kernel k_apply_fast<..., true, false>)
-    # C3 adds the general k_apply (its digested-run dispatch averages in; digests are a few loads per slot)
+    # C3 adds the general k_apply of the timed steps
     phase = [v for k, v in out["kernels"].items()
              if "k_plan" in k or "k_store" in k or ("k_apply_fast" in k and "true>" in k and "false" in k)
-             or (a.c3 and "k_apply<" in k)]
+             or (a.c3 and "k_apply<" in k and ", false>" in k)]   # not the digested run's <.., true>
     out["apply_phase_kernels"] = [k for k, v in out["kernels"].items() if v in phase]
     out["hbm_bytes_per_launch"] = sum(v["hbm_bytes_per_launch"] for v in phase) if phase else None
     out["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"
