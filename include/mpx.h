@@ -154,7 +154,9 @@ typedef struct mpx_stats {
     uint64_t apply_ns;         /* device time of the acceptor/learner kernel      */
     uint64_t ingest_ns;        /* host ingest + H2D of the last submit batch       */
     uint64_t bytes_alg;        /* 16 P + 24 A + 16 L                               */
-    uint64_t reserved[3];
+    uint64_t skipped;          /* submitted records left out: all their entries
+                                  belong to other shards (header sharding)       */
+    uint64_t reserved[2];
 } mpx_stats;
 
 typedef struct mpx_violation {

@@ -474,6 +474,7 @@ static int collect(mpx_engine *e)
     mpx_stats &st = e->stats;
     st.chosen = s[SW_C]; st.promise_entries = s[SW_P]; st.accept_apps = s[SW_A]; st.commit_apps = s[SW_L];
     st.messages = s[SW_MSGS]; st.violations = s[SW_V] + e->iv.count;
+    st.skipped = e->device_trace ? 0 : e->ht.dropped;
     st.chosen_digest = s[SW_DCHOSEN]; st.state_digest = s[SW_DSTATE]; st.scalar_digest = s[SW_DSCAL];
     st.bytes_alg = 16 * st.promise_entries + 24 * st.accept_apps + 16 * st.commit_apps;
     if (e->ev_used) {
@@ -704,6 +705,12 @@ extern "C" int mpx_last_violation(mpx_engine *e, mpx_violation *out)
         DevViolation d;
         HTRY(hipMemcpy(&d, e->viol.p, sizeof d, hipMemcpyDeviceToHost));
         out->code = d.code; out->node = (uint32_t)d.node; out->seq = d.seq; out->iid = d.iid;
+        // kernels report a message's position among the kept records of its node
+        const HostTrace &h = e->ht;
+        const bool msg_seq = d.code == MPX_V_BAD_NODE || d.code == MPX_V_LEARN_VALUE ||
+                             (d.code == MPX_V_COMMIT_VALUE && d.seq);
+        if (msg_seq && d.node < h.N && h.node_off[d.node] + d.seq < h.m_seq.size())
+            out->seq = h.m_seq[h.node_off[d.node] + d.seq];
     }
     return MPX_OK;
 }
@@ -778,6 +785,13 @@ static int fetch_results(mpx_engine *e, Results &r)
         for (auto &x : r.by_msg[k])
             std::sort(x.second.begin(), x.second.end(), [](const OutEnt *a, const OutEnt *b) { return a->iid < b->iid; });
     return MPX_OK;
+}
+
+// record index of message g in node n's submitted stream (ingest leaves other
+// shards' records out, HostTrace::m_seq; device-generated traces keep all)
+static uint64_t seq_of(const HostTrace &h, uint32_t n, uint64_t g)
+{
+    return h.m_seq.size() > g ? h.m_seq[g] : g - h.node_off[n];
 }
 
 // the replies the reference's acceptor / learner handlers send for message g
@@ -875,7 +889,7 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
         sec.clear(); cnt = 0;
         for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
             if (h.m_type[g] != MPX_MSG_PREPARE_REPLY || !(r.flags[g] & F_QUORUM)) continue;
-            app<uint64_t>(sec, g - h.node_off[n]);
+            app<uint64_t>(sec, seq_of(h, n, g));
             app<uint64_t>(sec, h.m_ballot[g]);
             auto it = r.by_msg[1].find((uint32_t)g);
             const uint64_t k = it == r.by_msg[1].end() ? 0 : it->second.size();
@@ -892,7 +906,7 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
             if (h.m_node[h.b_msg[j]] == n && r.b_chosen[j] != NONE32) ch.push_back({r.b_chosen[j], h.m_aux[h.b_msg[j]]});
         std::sort(ch.begin(), ch.end());
         app<uint64_t>(d, ch.size());
-        for (auto &c : ch) { app<uint64_t>(d, c.first - h.node_off[n]); app<uint64_t>(d, c.second); }
+        for (auto &c : ch) { app<uint64_t>(d, seq_of(h, n, c.first)); app<uint64_t>(d, c.second); }
         // executor: committed prefix from the shard's first instance (paxos.cpp:1584-1620),
         // computed on the device (gpu_executed); the host only looks up payload bytes
         sec.clear(); cnt = 0;

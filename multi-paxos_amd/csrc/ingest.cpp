@@ -256,6 +256,7 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
     uint32_t src = 0;
     uint64_t ballot = 0, aux = 0, ent = 0;
     uint32_t cnt = 0;
+    uint8_t part = 0;                             // entries, none in the shard: another rank's record
     (void)N;
     auto keep_shard = [&](std::vector<uint64_t> &iid, std::vector<uint64_t> *pid, std::vector<uint64_t> &val,
                           size_t first) {
@@ -333,6 +334,7 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
         cnt = (uint32_t)keep_shard(ns.e_iid, nullptr, ns.e_val, first);
+        part = n_all && !cnt;
         break;
     }
     case MPX_MSG_ACCEPT_REPLY:                    // :1345-1357
@@ -360,11 +362,13 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
         cnt = (uint32_t)keep_shard(ns.e_iid, nullptr, ns.e_val, first);
+        part = n_all && !cnt;
         break;
     }
     default:
         return MPX_E_DECODE;                      // ASSERT(false), :1671-1672
     }
+    ns.part.push_back(part);
     ns.type.push_back((uint8_t)t);
     ns.src.push_back(src);
     ns.ballot.push_back(ballot);
@@ -383,6 +387,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
     uint32_t src = 0, ver = 0;
     uint64_t ballot = 0, aux = 0, ent = 0;
     uint32_t cnt = 0;
+    uint8_t part = 0;
     auto keep_shard = [&](size_t first) {
         size_t w = first;
         for (size_t k = first; k < ns.e_iid.size(); ++k)
@@ -402,6 +407,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
         cnt = keep_shard(first);
+        part = n_all && !cnt;
         return MPX_OK;
     };
     switch (t) {
@@ -494,6 +500,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         return MPX_E_DECODE;
     }
     if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && ballot > LOW56) return MPX_E_RANGE;   // see G_SEG
+    ns.part.push_back(part);
     ns.type.push_back((uint8_t)t);
     ns.src.push_back(src);
     ns.ballot.push_back(ballot);
@@ -599,6 +606,11 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     std::vector<uint64_t> touched, round_b;
     std::vector<uint8_t> in_round(NB, 0);
     std::vector<uint64_t> sc_off(N + 1, 0);                 // each node's scan-stream range
+    // vote lists: an ACCEPT_REPLY counts for the live batch of its node with the
+    // same accept id (OnAcceptReply, multi/paxos.cpp:1406-1410); member: only at a
+    // node whose Proposer exists (Loop, member/paxos.cpp:763-790)
+    std::unordered_map<uint64_t, uint32_t> live;
+    std::vector<std::vector<uint32_t>> reps;
 
     for (uint32_t n = 0; n < N; ++n) {
         const NodeStream &ns = nodes[n];
@@ -615,6 +627,8 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         for (uint64_t b : round_b) in_round[b] = 0;
         touched.clear(); round_b.clear();
         int64_t maxb = -1;                              // highest bucket with a fragment of this node
+        live.clear();
+        bool last_virtual = false;                      // the node's last scan record stands for left-out ACCEPTs
         // member roles of node n along its stream (include/mpx.h E_EPOCH)
         uint32_t ep = 0, seg = 1;
         bool acc = member && ((epochs[0].acceptor_mask >> n) & 1);
@@ -622,8 +636,8 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         for (size_t k = 0; k < ns.type.size(); ++k) {
             const uint32_t g = (uint32_t)ht.m_type.size();
             const uint8_t t = ns.type[k];
+            uint32_t gate = 0;
             if (member) {
-                uint32_t gate = 0;
                 if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
                     gate = acc && ns.ver[k] == epochs[ep].version ? seg : 0;
                 } else if (t == MPX_MSG_E_EPOCH) {
@@ -641,8 +655,41 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                            t == MPX_MSG_P_BATCH) {
                     gate = prop ? (ep + 1) << G_EPOCH_SHIFT : 0;
                 }
-                ht.m_gate.push_back(gate);
             }
+            // Header sharding: a record whose entries all belong to
+            // other shards is left out here — ACCEPT / COMMIT / P_BATCH with no
+            // entry in the shard, the ACCEPT_REPLYs of batches not kept, and
+            // COMMIT_REPLYs (no effect on the acceptor / learner path; the shard
+            // at instance 0 keeps them).  Only the scalars see such an ACCEPT:
+            // its ballot stays in the scan stream as a max_seen-only record.
+            const bool off = member && t != MPX_MSG_E_EPOCH && !(gate >> G_EPOCH_SHIFT);
+            bool drop = ns.part[k] != 0 || (t == MPX_MSG_COMMIT_REPLY && sb != 0);
+            int64_t vote_j = -1;
+            if (t == MPX_MSG_P_START) {
+                if (!off) live.clear();
+            } else if (t == MPX_MSG_E_EPOCH) {
+                if (gate & G_PRECLR) live.clear();
+            } else if (t == MPX_MSG_P_BATCH) {
+                if (drop) live.erase(ns.aux[k]);
+                else if (!off) live[ns.aux[k]] = (uint32_t)ht.b_msg.size();
+            } else if (t == MPX_MSG_ACCEPT_REPLY) {
+                auto it = off ? live.end() : live.find(ns.aux[k]);
+                if (it == live.end()) drop = true;   // stale, or its batch is another shard's
+                else vote_j = it->second;
+            }
+            if (drop) {
+                ++ht.dropped;
+                if (t == MPX_MSG_ACCEPT && (!member || (gate & G_SEG))) {
+                    const uint64_t key = ns.ballot[k] | (member ? (uint64_t)(gate & G_SEG) << SEG_SHIFT : 0);
+                    if (last_virtual) ht.sc_key.back() = std::max(ht.sc_key.back(), key);
+                    else { ht.sc_type.push_back(SC_SONLY); ht.sc_key.push_back(key); ht.sc_idx.push_back(0); }
+                    last_virtual = true;
+                }
+                continue;
+            }
+            if (member) ht.m_gate.push_back(gate);
+            ht.m_seq.push_back((uint32_t)k);
+            if (vote_j >= 0) reps[vote_j].push_back(g);
             uint64_t ent = ns.ent[k];
             if (t == MPX_MSG_PREPARE) ent += gbase;
             else if (t == MPX_MSG_PREPARE_REPLY) ent += rbase;
@@ -655,7 +702,6 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             ht.m_cnt.push_back(ns.cnt[k]);
             ht.m_node.push_back(n);
             {   // header-scan stream and static flags (mpx_internal.hpp SC_*)
-                const uint32_t gate = member ? ht.m_gate.back() : 0;
                 const bool badsrc = ns.src[k] >= N;
                 uint8_t f0 = 0;
                 int sct = -1;
@@ -682,13 +728,17 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                     f0 = F_BADNODE; sct = SC_NONE | SC_BAD;
                 }
                 ht.m_flags0.push_back(f0);
-                if (sct >= 0) { ht.sc_type.push_back((uint8_t)sct); ht.sc_key.push_back(key); ht.sc_idx.push_back(g); }
+                if (sct >= 0) {
+                    ht.sc_type.push_back((uint8_t)sct); ht.sc_key.push_back(key); ht.sc_idx.push_back(g);
+                    last_virtual = false;
+                }
             }
             if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_E_EPOCH) { pl.push_back(g); pl_cnt[n]++; }
             if (t == MPX_MSG_P_START) pstart = g;
             if (t == MPX_MSG_P_BATCH) {
                 ht.b_msg.push_back(g);
                 ht.b_pstart.push_back(pstart);
+                reps.emplace_back();
             }
             if (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_PREPARE_REPLY) {
                 const uint8_t kind = t == MPX_MSG_ACCEPT ? K_ACCEPT : t == MPX_MSG_COMMIT ? K_COMMIT : K_PREPLY;
@@ -726,7 +776,6 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                 for (uint64_t b : round_b) add_ev(b);
                 clear_round();
             } else if (t == MPX_MSG_E_EPOCH) {
-                const uint32_t gate = ht.m_gate.back();
                 if (gate & G_ACCCLR) {
                     for (uint64_t b = 0; (int64_t)b <= maxb; ++b)
                         if (first_frag[b] < g) add_ev(b);
@@ -749,29 +798,8 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     ht.node_off[N] = ht.m_type.size();
     sc_off[N] = ht.sc_type.size();
 
-    // vote lists: replies attributed to the live batch of the same id, same epoch
+    // vote lists (attributed in the walk above)
     {
-        std::vector<std::vector<uint32_t>> reps(ht.b_msg.size());
-        for (uint32_t n = 0; n < N; ++n) {
-            std::unordered_map<uint64_t, uint32_t> live;
-            uint32_t j = 0;
-            // batches of node n are contiguous in b_msg, in message order
-            while (j < ht.b_msg.size() && ht.m_node[ht.b_msg[j]] < n) ++j;
-            uint32_t jn = j;
-            for (uint64_t g = ht.node_off[n]; g < ht.node_off[n + 1]; ++g) {
-                const uint8_t t = ht.m_type[g];
-                // member: only a node with a Proposer keeps batches / counts
-                // replies (Loop, member/paxos.cpp:763-790); an idle proposer has none
-                const bool off = member && t != MPX_MSG_E_EPOCH && !(ht.m_gate[g] >> G_EPOCH_SHIFT);
-                if (t == MPX_MSG_P_START) { if (!off) live.clear(); }
-                else if (t == MPX_MSG_E_EPOCH) { if (ht.m_gate[g] & G_PRECLR) live.clear(); }
-                else if (t == MPX_MSG_P_BATCH) { if (off) ++jn; else live[ht.m_aux[g]] = jn++; }
-                else if (t == MPX_MSG_ACCEPT_REPLY && !off) {
-                    auto it = live.find(ht.m_aux[g]);
-                    if (it != live.end()) reps[it->second].push_back((uint32_t)g);
-                }
-            }
-        }
         ht.b_rep_off.assign(ht.b_msg.size() + 1, 0);
         for (size_t j = 0; j < reps.size(); ++j) ht.b_rep_off[j + 1] = ht.b_rep_off[j] + reps[j].size();
         ht.b_rep.reserve(ht.b_rep_off.back());

@@ -46,6 +46,7 @@ struct NodeStream {
     std::vector<uint32_t> ver;                    // member: PREPARE / ACCEPT version, E_EPOCH epoch
     std::vector<uint64_t> r_iid, r_pid, r_val;    // PREPARE_REPLY entries (in shard)
     std::vector<uint64_t> g_a, g_b;               // PREPARE ranges (all), sorted by start
+    std::vector<uint8_t> part;                    // 1: the record carried entries, none in the shard
     void clear() { *this = NodeStream(); }
 };
 
@@ -59,6 +60,8 @@ struct HostTrace {
     std::vector<uint32_t> m_src, m_cnt, m_node, m_gate;
     std::vector<uint64_t> m_ballot, m_aux, m_ent;
     std::vector<uint64_t> node_off;
+    std::vector<uint32_t> m_seq;                    // record index in its node's submitted stream
+    uint64_t dropped = 0;                           // records of other shards left out (header sharding)
     std::vector<uint32_t> chunk_node, node_chunk_off;
     std::vector<uint64_t> chunk_beg, chunk_end;
     std::vector<uint8_t> sc_type;                   // header-scan stream (mpx_internal.hpp SC_*)
@@ -82,7 +85,8 @@ struct HostTrace {
 };
 
 // Decode one record of `node`'s stream into `ns`.  Entries outside
-// [shard_begin, shard_end) are dropped, headers are always kept.
+// [shard_begin, shard_end) are dropped; a record whose entries all lie outside
+// is marked (`part`) and left out by build_trace (header sharding).
 int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, const uint8_t *m, size_t len,
                   uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol);
 // member semantics wire formats (member/paxos.cpp:846-932)

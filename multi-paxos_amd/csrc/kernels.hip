@@ -694,7 +694,6 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
     const uint64_t steps = (NB + G - 1) / G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
-    const uint32_t pg = lane / N, pn = lane - pg * N;    // pair of lane (lane < GN)
     const uint32_t s0 = 4 * lane;                        // the lane's slots s0..s0+3
 
     // stage 1 (two steps ahead): pair CSR offsets (lanes 0..nb*N), chosen-log
@@ -1038,7 +1037,7 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
     }
     if (i < np) {
         const uint64_t b = i / N;
-        const uint32_t n = (uint32_t)(i - b * N);
+
         const uint32_t len = (uint32_t)(o1 - oa);
         const bool in_list = len && len <= FAST_MAX_FRAGS && !v.pair_ev[i];
         uint64_t q = PLAN_SKIP;
@@ -1213,7 +1212,7 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
     // address math stays off the VGPRs the plan load writes
     const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t N = v.N;
-    const uint64_t NB = v.NB;
+
     const uint64_t whole = v.shard_len >> BSH;            // buckets wholly inside the shard
     const uint64_t cpr = whole / C, S = (uint64_t)(N + 1) * cpr;   // rows 0..N-1 state, row N chosen log
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
@@ -1250,7 +1249,7 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
     static_assert(C == 64 || C == 128, "one or two plan words per lane");
     const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t N = v.N;
-    const uint64_t NB = v.NB;
+
     const uint64_t whole = v.shard_len >> BSH;
     const uint64_t cpr = whole / C, S = (uint64_t)(N + 1) * cpr;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;

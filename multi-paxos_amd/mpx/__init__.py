@@ -49,7 +49,7 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "chosen", "promise_entries", "accept_apps", "commit_apps", "messages", "violations",
         "chosen_digest", "state_digest", "scalar_digest", "device_ns", "apply_ns", "ingest_ns",
-        "bytes_alg", "r0", "r1", "r2")]
+        "bytes_alg", "skipped", "r1", "r2")]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if not f.startswith("r")}

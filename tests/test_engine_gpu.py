@@ -221,6 +221,41 @@ def test_sharded_device_generator_sums_to_whole(shards, b):
         assert tot[k] == whole[k] % (1 << 64), k
 
 
+@pytest.mark.parametrize("shards", [2, 4])
+def test_c3_header_sharding(shards):
+    """Header sharding of host-ingested traces: a shard engine leaves out the
+    ACCEPT / COMMIT / P_BATCH records with no entry in its shard (and their
+    replies), keeping only their ballots for the max_seen scan.  State, scalars,
+    promise-quorum events (entries restricted) and chosen batches still equal the
+    oracle's whole run, and each rank processes about total / shards + the
+    replicated headers."""
+    m = 1 << 12
+    t = mpx.generate_trace(mpx.GEN_FAULTY, num_nodes=7, num_instances=m, seed=5, batch=64, proposers=3,
+                           drop_rate=500, dup_rate=1000, max_delay=500)
+    full = mpxr.parse(oracle_run(t)[0])
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+    records = st["messages"] + st["skipped"]
+    from mpx import dist as mdist
+    kept = []
+    for r in range(shards):
+        sb, se = mdist.shard_bounds(m, shards, r)
+        with mpx.Engine(7, sb, se) as e:
+            e.submit_trace(t)
+            st = e.run()
+            part = mpxr.parse(e.dump())
+        assert st["messages"] + st["skipped"] == records
+        kept.append(st["messages"])
+        for a, b in zip(part["nodes"], full["nodes"]):
+            assert a["state"] == [x for x in b["state"] if sb <= x[0] < se]
+            assert (a["promised"], a["max_seen"]) == (b["promised"], b["max_seen"])
+            assert a["quorums"] == [(q, bal, [x for x in ents if sb <= x[0] < se]) for q, bal, ents in b["quorums"]]
+            assert set(a["chosen_batches"]) <= set(b["chosen_batches"])
+        assert part["chosen"] == [c for c in full["chosen"] if sb <= c[0] < se]
+    print("records %d, kept per rank %s" % (records, kept))
+    assert max(kept) < records * (0.75 if shards == 2 else 0.5)
+
+
 def test_host_sharded_ingest_matches_oracle_restricted():
     """Host ingest with a shard: state / chosen entries equal the oracle's, restricted to the shard."""
     name = "fuzz_big_1"
