@@ -37,7 +37,9 @@ oracle/_ref, kind "reference") on a bounded sample of the same clean stream,
 rank 0 at N=1 only.
 
     python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+(the launcher only starts the ranks; rendezvous, barriers and the max-reduce of
+the step time go through FileGroup, the RCCL communicator through mpx_comm_*)
 """
 import argparse
 import ctypes
@@ -156,6 +158,47 @@ def c3_leg(args):
     }
 
 
+class FileGroup:
+    """Rendezvous, barrier, max-reduce and broadcast between the ranks of one node
+    through files (the contract launches every rank on one node; no PyTorch): a
+    directory keyed by the launcher's MASTER_PORT and PID, one file per rank and
+    round, written atomically (write + rename) and polled."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world, self.k = rank, world, 0
+        key = "%s_%d" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+        self.dir = os.path.join("/tmp", "mpx_bench_" + key)
+        os.makedirs(self.dir, exist_ok=True)
+
+    def _put(self, name, data):
+        tmp = os.path.join(self.dir, ".%s.%d" % (name, self.rank))
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, os.path.join(self.dir, name))
+
+    def _get(self, name, timeout=600.0):
+        path = os.path.join(self.dir, name)
+        t0 = time.monotonic()
+        while not os.path.exists(path):
+            if time.monotonic() - t0 > timeout:
+                raise TimeoutError("rendezvous: %s missing after %.0f s" % (path, timeout))
+            time.sleep(0.001)
+        with open(path, "rb") as f:
+            return f.read()
+
+    def exchange(self, data):
+        """All-gather of one bytes object per rank (also the barrier)."""
+        self.k += 1
+        self._put("r%d_%d" % (self.k, self.rank), data)
+        return [self._get("r%d_%d" % (self.k, r)) for r in range(self.world)]
+
+    def close(self):
+        self.exchange(b"")                          # nobody reads the directory after this
+        if self.rank == 0:
+            import shutil
+            shutil.rmtree(self.dir, ignore_errors=True)
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -164,33 +207,26 @@ def dist_setup(args):
     # under torchrun (WORLD_SIZE set) the distributed path runs even at N=1, so
     # the rendezvous / RCCL communicator / all-gather code is exercised
     if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:
-        import torch.distributed as dist      # gloo on the CPU: rendezvous, barrier, max-reduce only
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        pg = dist
+        pg = FileGroup(rank, world)
     return world, rank, local, pg
 
 
 def barrier(pg):
     if pg is not None:
-        pg.barrier()
+        pg.exchange(b"")
 
 
 def allreduce_max(pg, x):
     if pg is None:
         return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
+    import struct
+    return max(struct.unpack("<d", b)[0] for b in pg.exchange(struct.pack("<d", x)))
 
 
 def broadcast_bytes(pg, data, rank):
     if pg is None:
         return data
-    obj = [data if rank == 0 else None]
-    pg.broadcast_object_list(obj, src=0)
-    return obj[0]
+    return pg.exchange(data if rank == 0 else b"")[0]
 
 
 def latest_pmc(n_nodes, instances, world, workload="C4"):
@@ -421,7 +457,7 @@ def main():
         print(json.dumps(out), flush=True)
     eng.close()
     if pg is not None:
-        pg.destroy_process_group()
+        pg.close()
 
 
 if __name__ == "__main__":
