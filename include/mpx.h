@@ -255,6 +255,18 @@ int  mpx_last_violation(mpx_engine *eng, mpx_violation *out);
  * the CPU oracle and the reference driver also write, so parity is a
  * byte comparison.  *out is malloc'ed; free with mpx_free. */
 int  mpx_dump_result(mpx_engine *eng, uint8_t **out, uint64_t *size);
+/* Phase-2 decisions (multi semantics, an engine whose shard
+ * starts at instance 0): for every promise quorum of the last run, the batch
+ * OnPrepareReply builds (multi/paxos.cpp:1056-1130) for a proposer with no
+ * client proposals of its own — every pre-accepted value of an instance the
+ * node has not committed (:1071-1102), then a noop Value(node, ++value_id) for
+ * every other uncommitted instance below the highest committed-or-adopted one
+ * (:1117-1130; value ids count from 1 per node over its quorums).  Computed on
+ * the device from the run's state.  Format MPXD: "MPXD" u32 1, u32 nodes; per
+ * node u64 count, per quorum {u64 seq (record index in the node's stream),
+ * u64 n, {u64 iid, u64 handle} * n, iid ascending}.  *out is malloc'ed; free
+ * with mpx_free.  MPX_E_STATE for member semantics or a shard engine. */
+int  mpx_read_decisions(mpx_engine *eng, uint8_t **out, uint64_t *size);
 /* Encoded reference Value bytes (multi/paxos.cpp:556-598) for a handle. */
 int  mpx_value_bytes(mpx_engine *eng, uint64_t handle, uint8_t *buf,
                      uint32_t cap, uint32_t *len);

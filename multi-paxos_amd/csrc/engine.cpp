@@ -760,8 +760,8 @@ static int fetch_results(mpx_engine *e, Results &r)
             TRY(d2h(part, e->out, k, (size_t)s * e->out_cap));
             for (const OutRec &o : part) {
                 // resolve the reference (mpx_internal.hpp OutRec) against the host trace
-                OutEnt x{o.msg, (o.aux & OUT_K1) ? 1u : 0u, 0, 0, 0};
-                if (x.kind) {
+                OutEnt x{o.msg, ((o.aux & OUT_K1) ? 1u : 0u) | ((o.aux & OUT_CMT) ? 2u : 0u), 0, 0, 0};
+                if (x.kind & 1) {
                     if (o.ref >= h.r_iid.size()) return MPX_E_STATE;
                     x.iid = h.r_iid[o.ref]; x.ballot = h.r_pid[o.ref]; x.handle = h.r_val[o.ref];
                 } else {
@@ -934,6 +934,110 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
     }
     app<uint64_t>(d, cnt);
     d += sec;
+    *out = (uint8_t *)std::malloc(d.size());
+    if (!*out) return MPX_E_NOMEM;
+    std::memcpy(*out, d.data(), d.size());
+    *size = d.size();
+    return MPX_OK;
+}
+
+// ------------------------------------------------- phase-2 decisions (f2) --
+// The batch OnPrepareReply builds at each promise quorum (multi/paxos.cpp:
+// 1056-1130) for a proposer with no client proposals of its own: the device
+// finds, per event, the highest instance the node had committed before it and
+// the instances to noop-fill (kernels.hip k_decide); the adopted values are the
+// quorum's merged map minus what the node had committed (k_apply's records).
+// The host merges the two sorted lists and numbers the noops per node
+// (Value(index_, ++value_id_)).  Format MPXD (include/mpx.h).
+extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->cfg.semantics != MPX_SEM_MULTI || e->cfg.shard_begin != 0) return MPX_E_STATE;
+    Results r;
+    TRY(fetch_results(e, r));
+    const HostTrace &h = e->ht;
+    const uint32_t N = e->cfg.num_nodes;
+    std::vector<uint32_t> en, eg;
+    for (uint32_t n = 0; n < N; ++n)
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g)
+            if (h.m_type[g] == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM)) { en.push_back(n); eg.push_back((uint32_t)g); }
+    const uint32_t E = (uint32_t)en.size();
+    const uint64_t sb = e->cfg.shard_begin;
+    // adopted: the merged entries of instances not committed at the quorum (:1091)
+    std::vector<std::vector<const OutEnt *>> adopted(E);
+    std::vector<uint64_t> ad_off(E + 1, 0), xend(E, 0);
+    std::vector<uint32_t> ad_li;
+    for (uint32_t k = 0; k < E; ++k) {
+        auto it = r.by_msg[1].find(eg[k]);
+        if (it != r.by_msg[1].end())
+            for (const OutEnt *o : it->second)
+                if (!(o->kind & 2)) { adopted[k].push_back(o); ad_li.push_back((uint32_t)(o->iid - sb)); }
+        ad_off[k + 1] = ad_li.size();
+        if (!adopted[k].empty()) xend[k] = adopted[k].back()->iid - sb + 1;
+    }
+    std::vector<uint32_t> noops;
+    std::vector<uint64_t> ev_base(E + 1, 0);
+    if (E) {
+        hipStream_t s = e->stream;
+        DevBuf d_node, d_msg, d_xmax, d_xend, d_adoff, d_adli, d_boff, d_bcnt, d_base, d_tot, d_noop;
+        TRY(upload(d_node, en, s)); TRY(upload(d_msg, eg, s));
+        TRY(d_xmax.alloc(8ull * E)); HTRY(hipMemsetAsync(d_xmax.p, 0, 8ull * E, s));
+        DecideArgs a{};
+        a.E = E; a.ev_node = d_node.as<uint32_t>(); a.ev_msg = d_msg.as<uint32_t>();
+        a.xmax = d_xmax.as<unsigned long long>();
+        if (launch_decide(e->view, s, 0, a) != 0) return MPX_E_HIP;
+        std::vector<uint64_t> xmax;
+        HTRY(hipStreamSynchronize(s));
+        TRY(d2h(xmax, d_xmax, E));
+        std::vector<uint64_t> boff(E + 1, 0);
+        uint64_t maxb = 0;
+        for (uint32_t k = 0; k < E; ++k) {
+            xend[k] = std::min<uint64_t>(std::max(xend[k], xmax[k]), e->shard_len);
+            const uint64_t nb = (xend[k] + 255) / 256;
+            boff[k + 1] = boff[k] + nb;
+            maxb = std::max(maxb, nb);
+        }
+        TRY(upload(d_xend, xend, s)); TRY(upload(d_adoff, ad_off, s)); TRY(upload(d_adli, ad_li, s));
+        TRY(upload(d_boff, boff, s));
+        TRY(d_bcnt.alloc(std::max<uint64_t>(4 * boff[E], 4))); TRY(d_tot.alloc(8ull * E));
+        a.xend = d_xend.as<uint64_t>(); a.ad_off = d_adoff.as<uint64_t>(); a.ad_li = d_adli.as<uint32_t>();
+        a.blk_off = d_boff.as<uint64_t>(); a.blk_cnt = d_bcnt.as<uint32_t>(); a.ev_total = d_tot.as<uint64_t>();
+        a.max_blocks = maxb;
+        if (launch_decide(e->view, s, 1, a) != 0 || launch_decide(e->view, s, 3, a) != 0) return MPX_E_HIP;
+        std::vector<uint64_t> tot;
+        HTRY(hipStreamSynchronize(s));
+        TRY(d2h(tot, d_tot, E));
+        for (uint32_t k = 0; k < E; ++k) ev_base[k + 1] = ev_base[k] + tot[k];
+        TRY(upload(d_base, ev_base, s));
+        TRY(d_noop.alloc(std::max<uint64_t>(4 * ev_base[E], 4)));
+        a.ev_base = d_base.as<uint64_t>(); a.noop_li = d_noop.as<uint32_t>();
+        if (launch_decide(e->view, s, 2, a) != 0) return MPX_E_HIP;
+        HTRY(hipStreamSynchronize(s));
+        TRY(d2h(noops, d_noop, ev_base[E]));
+    }
+    std::string d;
+    d.append("MPXD", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, N);
+    std::vector<uint64_t> vid(N, 0);                     // value_id_ per node (:335, ++ per noop)
+    uint32_t k = 0;
+    for (uint32_t n = 0; n < N; ++n) {
+        const uint32_t k0 = k;
+        while (k < E && en[k] == n) ++k;
+        app<uint64_t>(d, k - k0);
+        for (uint32_t x = k0; x < k; ++x) {
+            app<uint64_t>(d, seq_of(h, n, eg[x]));
+            const auto &ad = adopted[x];
+            app<uint64_t>(d, ad.size() + (ev_base[x + 1] - ev_base[x]));
+            size_t i = 0;
+            uint64_t j = ev_base[x];
+            while (i < ad.size() || j < ev_base[x + 1]) {  // both sorted by instance
+                const uint64_t ai = i < ad.size() ? ad[i]->iid : ~0ull;
+                const uint64_t ni = j < ev_base[x + 1] ? sb + noops[j] : ~0ull;
+                if (ai < ni) { app<uint64_t>(d, ai); app<uint64_t>(d, ad[i]->handle); ++i; }
+                else { app<uint64_t>(d, ni); app<uint64_t>(d, MPX_HANDLE(n, 1, ++vid[n])); ++j; }
+            }
+        }
+    }
     *out = (uint8_t *)std::malloc(d.size());
     if (!*out) return MPX_E_NOMEM;
     std::memcpy(*out, d.data(), d.size());

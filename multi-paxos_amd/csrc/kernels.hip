@@ -471,7 +471,7 @@ __global__ __launch_bounds__(256) void k_votes(DevView v)
 // wave's sub-buffer cursor) per event.
 constexpr uint32_t SPL_ = 4;
 __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uint32_t msg, uint32_t kind_aux,
-                                 const uint32_t (&ref)[SPL_])
+                                 const uint32_t (&ref)[SPL_], const uint32_t *ext = nullptr)
 {
     const uint32_t lane = threadIdx.x & 63;
     uint64_t m[SPL_];
@@ -490,7 +490,7 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
         const uint64_t at = base + off + (uint64_t)__popcll(m[j] & below);
         if (want[j] && at < v.out_cap) {
             OutRec r;
-            r.msg = msg; r.ref = ref[j]; r.aux = kind_aux | (lane + 64 * j);
+            r.msg = msg; r.ref = ref[j]; r.aux = kind_aux | (lane + 64 * j) | (ext ? ext[j] : 0);
             v.out[(uint64_t)sub * v.out_cap + at] = r;
         }
         off += (uint32_t)__popcll(m[j]);
@@ -1549,16 +1549,17 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                             if (!(SF(j) & S_COMMITTED)) { if (DIGEST) sb[j] = 0; SF_SET(j, 0); se[j] = sm[j] = 0; }
                     } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
                         bool hit[SPL];
-                        uint32_t ref[SPL];
+                        uint32_t ref[SPL], ext[SPL];
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) {
                             const u64x2 cur = pre[lane + 64 * j];
                             hit[j] = li0 + lane + 64 * j < v.shard_len && cur.y;
                             ref[j] = (uint32_t)(cur.y & ~W_PRESENT);                 // the PREPARE_REPLY entry
+                            ext[j] = (SF(j) & S_COMMITTED) ? OUT_CMT : 0;            // not adoptable (:1091)
                             cQ += hit[j];
                             pre[lane + 64 * j] = u64x2{0, 0};                        // :1105
                         }
-                        emit_rows(v, hit, g, OUT_K1, ref);
+                        emit_rows(v, hit, g, OUT_K1, ref, ext);
                     }
                     ++c;
                 }
@@ -1872,6 +1873,110 @@ int launch_frag_w1(const Frag *frags, uint64_t *out, uint64_t n, void *stream)
 {
     if (!n) return 0;
     hipLaunchKernelGGL(k_frag_w1, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, frags, out, n);
+    return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------- phase-2 decisions --
+// OnPrepareReply's batch at a promise quorum (multi/paxos.cpp:1056-1130; SURVEY
+// §8 f2): adopt every pre-accepted value of an instance the node has not
+// committed (the quorum's merged map, k_apply's OUT_K1 records without OUT_CMT),
+// then fill every instance of the unproposed set below its last, open range
+// with a noop — the instances not committed before the quorum and not adopted,
+// below 1 + the highest committed-or-adopted instance.  The per-instance work is
+// here; the host only merges the two sorted lists and numbers the noops.
+// the message of the first COMMIT that reached (node n, instance li), NONE32 if none
+__device__ inline uint32_t commit_msg(const DevView &v, uint32_t n, uint64_t li)
+{
+    if (!v.st_valid[sv_idx(v, n, li >> BSH)]) return NONE32;
+    const uint32_t q = slot_global(v, n, li);
+    if (!q) return NONE32;
+    const uint64_t w1 = frag_w1(v.frags + q - 1);
+    return (w1 >> 60) == K_COMMIT ? (uint32_t)w1 : NONE32;
+}
+
+__global__ __launch_bounds__(256) void k_decide(DevView v, uint32_t pass, DecideArgs a)
+{
+    __shared__ uint32_t wc[4];
+    const uint32_t e = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t n = a.ev_node[e], g = a.ev_msg[e];
+    const uint64_t li = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (pass == 0) {
+        uint64_t x = 0;
+        if (li < v.shard_len && commit_msg(v, n, li) < g) x = li + 1;
+        x = wave_max(x);
+        if (lane == 0 && x) atomicMax(&a.xmax[e], (unsigned long long)x);
+        return;
+    }
+    const uint64_t end = a.xend[e];
+    if ((uint64_t)blockIdx.x * 256 >= end) return;           // block-uniform
+    bool fill = false;
+    if (li < end && !(commit_msg(v, n, li) < g)) {
+        const uint64_t a0 = a.ad_off[e], a1 = a.ad_off[e + 1];
+        uint64_t lo = a0, hi = a1;                          // adopted: binary search
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (a.ad_li[mid] < li) lo = mid + 1; else hi = mid;
+        }
+        fill = !(lo < a1 && a.ad_li[lo] == li);
+    }
+    const uint64_t m = __ballot(fill);
+    if (lane == 0) wc[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    const uint64_t bi = a.blk_off[e] + blockIdx.x;
+    if (pass == 1) {
+        if (threadIdx.x == 0) a.blk_cnt[bi] = wc[0] + wc[1] + wc[2] + wc[3];
+        return;
+    }
+    uint32_t before = 0;
+    for (uint32_t i = 0; i < wv; ++i) before += wc[i];
+    if (fill)
+        a.noop_li[a.ev_base[e] + a.blk_cnt[bi] + before + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint32_t)li;
+}
+
+// per event: its block counts -> exclusive offsets (in place), total -> ev_total
+__global__ __launch_bounds__(256) void k_decide_scan(DecideArgs a)
+{
+    __shared__ uint32_t ws[4];
+    const uint32_t e = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t b0 = a.blk_off[e], b1 = a.blk_off[e + 1];
+    uint64_t carry = 0;
+    for (uint64_t base = b0; base < b1; base += 256) {
+        const uint64_t i = base + threadIdx.x;
+        const uint32_t x = i < b1 ? a.blk_cnt[i] : 0;
+        uint32_t inc = x;                                    // wave inclusive scan
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += y;
+        }
+        if (lane == 63) ws[wv] = inc;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+        for (uint32_t k = 0; k < 4; ++k) { if (k < wv) pre += ws[k]; tot += ws[k]; }
+        if (i < b1) a.blk_cnt[i] = (uint32_t)(carry + pre + inc - x);
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.ev_total[e] = carry;
+}
+
+int launch_decide(const DevView &v, void *stream, uint32_t pass, const DecideArgs &a)
+{
+    hipStream_t s = (hipStream_t)stream;
+    if (!a.E) return 0;
+    for (uint32_t e0 = 0; e0 < a.E; e0 += 65535) {           // grid.y limit: events in slices
+        DecideArgs sl = a;
+        sl.E = a.E - e0 < 65535 ? a.E - e0 : 65535;
+        sl.ev_node = a.ev_node + e0; sl.ev_msg = a.ev_msg + e0;
+        sl.xmax = a.xmax + e0; sl.xend = a.xend + e0; sl.ad_off = a.ad_off + e0;
+        sl.blk_off = a.blk_off + e0; sl.ev_base = a.ev_base + e0; sl.ev_total = a.ev_total + e0;
+        if (pass == 3) {
+            hipLaunchKernelGGL(k_decide_scan, dim3(sl.E), dim3(256), 0, s, sl);
+            continue;
+        }
+        const uint64_t blocks = pass == 0 ? cdiv(v.shard_len, 256) : a.max_blocks;
+        if (!blocks) continue;
+        hipLaunchKernelGGL(k_decide, dim3((uint32_t)blocks, sl.E), dim3(256), 0, s, v, pass, sl);
+    }
     return (int)hipGetLastError();
 }
 

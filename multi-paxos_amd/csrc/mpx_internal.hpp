@@ -124,6 +124,8 @@ static_assert(sizeof(Frag) == 16, "Frag is 16 bytes");
 //           in its bucket (the entry at that slot: iid, Value; its message's
 //           ballot, member: the entry's proposal id)
 //   kind 1: ref = PREPARE_REPLY entry index (r_iid, r_pid, r_val), aux = OUT_K1
+//           (| OUT_CMT: the node had committed the instance by then — not
+//           adoptable by the phase-2 batch, multi/paxos.cpp:1091)
 struct OutRec {
     uint32_t msg;
     uint32_t ref;
@@ -131,10 +133,11 @@ struct OutRec {
 };
 static_assert(sizeof(OutRec) == 12, "OutRec is 12 bytes");
 constexpr uint32_t OUT_K1 = 0x100;
+constexpr uint32_t OUT_CMT = 0x200;
 // host form of a snapshot record
 struct OutEnt {
     uint32_t msg;
-    uint32_t kind;
+    uint32_t kind;                  // bit 0: kind; bit 1: OUT_CMT
     uint64_t iid;
     uint64_t ballot;
     uint64_t handle;
@@ -294,6 +297,26 @@ int launch_exec(const DevView &v, void *stream, uint32_t node, unsigned long lon
 int launch_state_digest(const DevView &v, void *stream, unsigned long long *out);
 // out[i] = second word of frags[i], i < n (once per trace load)
 int launch_frag_w1(const Frag *frags, uint64_t *out, uint64_t n, void *stream);
+// Phase-2 decisions (mpx_read_decisions, kernels.hip k_decide*): E promise-quorum
+// events (node, message) over the shard, in four launches —
+//   pass 0: xmax[e] = 1 + the highest instance the event's node had committed
+//           before the event (0: none);
+//   pass 1: (xend[e] = where the noop fill ends; the adopted instances of event
+//           e sorted in ad_li[ad_off[e] .. ad_off[e + 1])) per 256-instance block
+//           below xend the number of instances to fill -> blk_cnt[blk_off[e] + block];
+//   scan:   per event, blk_cnt -> exclusive block offsets in place, total -> ev_total[e];
+//   pass 2: the instances to fill, in instance order -> noop_li[ev_base[e] + ...].
+struct DecideArgs {
+    uint32_t E;
+    const uint32_t *ev_node, *ev_msg;
+    unsigned long long *xmax;
+    const uint64_t *xend, *ad_off, *blk_off, *ev_base;
+    const uint32_t *ad_li;
+    uint32_t *blk_cnt, *noop_li;
+    uint64_t *ev_total;
+    uint64_t max_blocks;            // blocks of the widest event (pass 1 / 2 grid)
+};
+int launch_decide(const DevView &v, void *stream, uint32_t pass, const DecideArgs &a);
 // f_off / cf_off: host-computed prefix counts (per pair, per bucket), read by the generator
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
                      uint64_t G0, uint64_t G1, uint64_t ballot, uint64_t B, uint32_t NB,

@@ -344,6 +344,9 @@ typedef struct {
     map_t seen;                 /* per-message duplicate-iid check, reused     */
     u64 first_violation[4];
     int rc;
+    /* phase-2 decisions (mpxo_decisions): value_id_ (multi/paxos.cpp:335) and the MPXD records */
+    u64 value_id;
+    buf_t dec; u64 n_dec;
 } node_t;
 
 typedef struct { u32 version; u64 amask, pmask; } epoch_t;
@@ -357,6 +360,7 @@ typedef struct {
     node_t *nodes;
     u64 first_violation[4];     /* code, node, seq, iid */
     u64 sb, se;                 /* instance shard: entries outside are skipped (engine ingest) */
+    int want_dec;               /* record the phase-2 batch at every promise quorum (mpxo_decisions) */
 } ctx_t;
 #define IN_SHARD(c, iid) ((iid) >= (c)->sb && (iid) < (c)->se)
 
@@ -606,6 +610,41 @@ static int on_commit(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     return OK;
 }
 
+/* The phase-2 batch OnPrepareReply builds at a promise quorum
+ * (multi/paxos.cpp:1056-1130), for a proposer with no client proposals of its
+ * own (initial_proposals_ / newly_proposed_values_ empty; the driver's state):
+ * unproposed = uncommitted_instance_ids_ = every id not committed here; every
+ * pre-accepted value of an unproposed id is adopted (:1071-1102); then every
+ * range of the unproposed set but the last, open one is filled with noops
+ * Value(index_, ++value_id_) in id order (:1117-1130).  The last range starts
+ * after the highest committed or adopted id, so the fill covers exactly the
+ * unproposed, non-adopted ids below it.  Record: seq, count, {iid, handle}
+ * ascending (the AcceptingValues map order). */
+static void decide(node_t *n, const ent_t *pre, size_t k, u64 seq)
+{
+    u64 X = 0;
+    for (size_t j = 0; j < n->com.cap; ++j)
+        if (n->com.used[j] && n->com.e[j].key + 1 > X) X = n->com.e[j].key + 1;
+    for (size_t i = 0; i < k; ++i)
+        if (!map_find(&n->com, pre[i].key) && pre[i].key + 1 > X) X = pre[i].key + 1;
+    buf_t d = {0};
+    u64 cnt = 0;
+    size_t i = 0;
+    for (u64 id = 0; id < X; ++id) {
+        while (i < k && pre[i].key < id) ++i;
+        if (map_find(&n->com, id)) continue;
+        bput64(&d, id);
+        if (i < k && pre[i].key == id) bput64(&d, pre[i].b);                             /* adopt */
+        else bput64(&d, ((u64)n->index << 48) | (1ull << 47) | ++n->value_id);           /* noop */
+        ++cnt;
+    }
+    bput64(&n->dec, seq);
+    bput64(&n->dec, cnt);
+    bput(&n->dec, d.p, d.n);
+    free(d.p);
+    n->n_dec++;
+}
+
 /* OnPrepareReply + UpdateByPreAcceptedValues, multi/paxos.cpp:1036-1057,1201-1223 */
 static int on_prepare_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
 {
@@ -646,6 +685,7 @@ static int on_prepare_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 se
             bput64(&n->events_q, v[i].b);
         }
         n->n_q++;
+        if (c->want_dec) decide(n, v, k, seq);
         free(v);
         for (size_t i = 0; i < n->nb; ++i)                      /* :1054 */
             if (n->batches[i].live) { violate(c, n, 5, seq, 0); break; }
@@ -1208,12 +1248,14 @@ static int check_values(ctx_t *c)
     return rc;
 }
 
-static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
+static int run_shard_ex(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *out_size, u64 *stats,
+                        u64 *viol, u8 **dec, u64 *dec_size)
 {
     if (size < HDR || memcmp(trace, "MPXT", 4)) return E_DECODE;
     ctx_t c;
     memset(&c, 0, sizeof c);
     c.sb = sb; c.se = se;
+    c.want_dec = dec != NULL;
     c.N = rd32(trace + 8);
     c.sem = rd32(trace + 12);
     c.M = rd64(trace + 16);
@@ -1270,6 +1312,13 @@ static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *o
     }
     free(jobs);
     if (rc == OK) rc = dump(&c, out, out_size, stats);
+    if (rc == OK && dec) {
+        buf_t d = {0};
+        bput(&d, "MPXD", 4); bput32(&d, 1); bput32(&d, c.N);
+        for (u32 i = 0; i < c.N; ++i) { bput64(&d, c.nodes[i].n_dec); bput(&d, c.nodes[i].dec.p, c.nodes[i].dec.n); }
+        if (d.oom) { free(d.p); rc = E_NOMEM; } else { *dec = d.p; *dec_size = d.n; }
+    }
+    for (u32 i = 0; i < c.N; ++i) free(c.nodes[i].dec.p);
     if (viol) memcpy(viol, c.first_violation, sizeof c.first_violation);
     for (u32 i = 0; i < c.N; ++i) {
         node_t *n = &c.nodes[i];
@@ -1288,9 +1337,25 @@ static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *o
     return rc;
 }
 
+static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
+{
+    return run_shard_ex(trace, size, sb, se, out, out_size, stats, viol, NULL, NULL);
+}
+
 int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
 {
     return run_shard(trace, size, 0, ~0ull, out, out_size, stats, viol);
+}
+
+/* mpxo_decisions: the phase-2 batch at every promise quorum (MPXD, DESIGN.md
+ * §f2; multi semantics), what `decide` records over a whole-trace run. */
+int mpxo_decisions(const u8 *trace, u64 size, u8 **out, u64 *out_size)
+{
+    u8 *r = NULL;
+    u64 rs = 0;
+    int rc = run_shard_ex(trace, size, 0, ~0ull, &r, &rs, NULL, NULL, out, out_size);
+    free(r);
+    return rc;
 }
 
 /*

@@ -92,6 +92,7 @@ struct Node {
     std::vector<Send> sends;
     std::string events_q; u64 n_q = 0;
     std::string events_c; u64 n_c = 0;
+    std::string events_d; u64 n_d = 0;                  // the reference's own phase-2 batch per promise quorum
     std::set<paxos::AcceptingID> marker_batches;       // created by P_BATCH markers
     std::map<paxos::AcceptingID, std::map<paxos::InstanceID, paxos::Value> > batch_values;
     u64 P = 0, A = 0, L = 0;
@@ -114,7 +115,35 @@ static void scan_values(const uint8_t *m, size_t len, std::map<u64, paxos::Value
     for (auto &e : av) vals.insert(std::make_pair(handle_of(e.second.value_), e.second.value_));
 }
 
+static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size, uint64_t *stats,
+                    std::string *decisions);
+
 extern "C" int mpxref_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size, uint64_t *stats)
+{
+    return run_impl(trace, size, out, out_size, stats, NULL);
+}
+
+// The reference's own phase-2 decisions (MPXD): per node, per
+// promise quorum {u64 seq, u64 count, {u64 iid, u64 handle} * count}, the batch
+// OnPrepareReply built with this driver's proposer bookkeeping (no client
+// proposals: initial_proposals_ and newly_proposed_values_ stay empty).
+extern "C" int mpxref_decisions(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)
+{
+    uint8_t *r = NULL;
+    uint64_t rs = 0;
+    std::string d;
+    int rc = run_impl(trace, size, &r, &rs, NULL, &d);
+    free(r);
+    if (rc) return rc;
+    *out = (uint8_t *)malloc(d.size() ? d.size() : 1);
+    if (!*out) return -2;
+    memcpy(*out, d.data(), d.size());
+    *out_size = d.size();
+    return 0;
+}
+
+static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size, uint64_t *stats,
+                    std::string *decisions)
 {
     if (size < 40 || memcmp(trace, "MPXT", 4)) return -4;
     uint32_t N = rd32(trace + 8), sem = rd32(trace + 12), ne = rd32(trace + 24);
@@ -207,7 +236,19 @@ extern "C" int mpxref_run(const uint8_t *trace, uint64_t size, uint8_t **out, ui
                     std::set<paxos::AcceptingID> before_b;
                     for (auto &e : p->accepting_values_) before_b.insert(e.first);
                     p->OnPrepareReply(msg);
-                    // discard what the (out-of-scope) decision logic created
+                    // record, then discard, what the reference's decision logic created
+                    // (multi/paxos.cpp:1056-1182: adopt pre-accepted, noop gap fill, ...)
+                    {
+                        std::string d;
+                        u64 cnt_d = 0;
+                        for (auto &e : p->accepting_values_)
+                            if (!before_b.count(e.first))
+                                for (auto &v : e.second->values_) {
+                                    put<u64>(d, v.first); put<u64>(d, handle_of(v.second)); ++cnt_d;
+                                }
+                        put<u64>(n.events_d, k); put<u64>(n.events_d, cnt_d); n.events_d += d;
+                        n.n_d++;
+                    }
                     for (auto it = p->accepting_values_.begin(); it != p->accepting_values_.end();) {
                         if (!before_b.count(it->first)) {
                             it->second->retry_timeout_->Cancel();
@@ -321,6 +362,11 @@ extern "C" int mpxref_run(const uint8_t *trace, uint64_t size, uint8_t **out, ui
     }
     put<u64>(r, chosen.size());
     for (auto &e : chosen) { put<u64>(r, e.first); put<u64>(r, e.second); }
+    if (decisions) {
+        decisions->append("MPXD", 4);
+        put<uint32_t>(*decisions, 1); put<uint32_t>(*decisions, N);
+        for (uint32_t i = 0; i < N; ++i) { put<u64>(*decisions, ns[i].n_d); *decisions += ns[i].events_d; }
+    }
     if (stats) { stats[0] = chosen.size(); stats[1] = P; stats[2] = A; stats[3] = L; }
     *out = (uint8_t *)malloc(r.size());
     if (!*out) return -2;

@@ -108,3 +108,30 @@ def oracle_run_sharded(trace, shards=16, threads=None):
     if rc != 0:
         raise RuntimeError("mpxo_run_sharded failed: %d" % rc)
     return list(stats)
+
+
+def _blob_call(so, fn, trace):
+    lib = ctypes.CDLL(so)
+    f = getattr(lib, fn)
+    f.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                  ctypes.POINTER(ctypes.c_uint64)]
+    f.restype = ctypes.c_int
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    size = ctypes.c_uint64()
+    rc = f(bytes(trace), len(trace), ctypes.byref(out), ctypes.byref(size))
+    if rc != 0:
+        raise RuntimeError("%s failed: %d" % (fn, rc))
+    data = ctypes.string_at(out, size.value)
+    ctypes.CDLL(None).free(out)
+    return data
+
+
+def ref_decisions(trace):
+    """The reference's own phase-2 batch at every promise quorum (MPXD; multi semantics),
+    recorded by oracle/ref_multi_driver.cpp (mpxref_decisions)."""
+    return _blob_call(REF_SO, "mpxref_decisions", trace)
+
+
+def oracle_decisions(trace):
+    """The oracle's restatement of the same decisions (mpxo_decisions)."""
+    return _blob_call(ORACLE_SO, "mpxo_decisions", trace)

@@ -475,3 +475,45 @@ def test_c5_full_size_matches_oracle():
     st = _full_size_vs_oracle(mpx.GEN_MEMBER, num_nodes=8, num_instances=1 << 25, seed=0, batch=256,
                               drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15)
     assert st["chosen"] == 1 << 25 and st["violations"] == 0
+
+
+# ---- phase-2 decisions at promise quorums (multi/paxos.cpp:1056-1130) ----
+DECISIONS = json.load(open(os.path.join(GOLD, "decisions.json")))
+
+
+@pytest.mark.parametrize("name", sorted(DECISIONS))
+def test_engine_decisions_match_reference(name):
+    """The device's phase-2 batch at every promise quorum (adopt the merged
+    pre-accepted values of instances the node has not committed, noop-fill the
+    other uncommitted instances below the highest committed-or-adopted one) ==
+    the batch the reference's own OnPrepareReply built (fixture), on both apply paths."""
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxd")
+    with mpx.Engine.for_trace(trace) as e:
+        e.run()
+        assert e.decisions() == want
+        e.step()
+        e.sync()
+        assert e.decisions() == want
+
+
+@pytest.mark.parametrize("seed,m", [(81, 1 << 12), (82, 3000), (83, 1 << 14)])
+def test_engine_decisions_match_oracle_c3(seed, m):
+    from oracles import oracle_decisions
+    t = mpx.generate_trace(mpx.GEN_FAULTY, num_nodes=7, num_instances=m, seed=seed, batch=64, proposers=3,
+                           drop_rate=500, dup_rate=1000, max_delay=500)
+    want = oracle_decisions(t)
+    with mpx.Engine.for_trace(t) as e:
+        e.run()
+        got = e.decisions()
+    import mpxd
+    assert sum(len(x) for x in mpxd.parse(want)) > 0
+    assert got == want
+
+
+def test_decisions_refused_for_shards_and_member():
+    t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=3, num_instances=1024, batch=256)
+    with mpx.Engine(3, 256, 1024) as e:
+        e.submit_trace(t)
+        e.run()
+        with pytest.raises(mpx.MpxError):
+            e.decisions()

@@ -133,3 +133,30 @@ def test_clean_closed_form_matches_oracle(n, m, sb, se):
     R = mpxr.parse(res)
     for nd in R["nodes"]:
         assert [s for s in nd["state"] if sb <= s[0] < se] == [(i, 2, 1 << 16, i + 1) for i in range(sb, se)]
+
+
+# ---- phase-2 decisions at promise quorums (multi/paxos.cpp:1056-1130) ----
+DECISIONS = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "decisions.json")))
+
+
+@pytest.mark.parametrize("name", sorted(DECISIONS))
+def test_oracle_decisions_match_reference_golden(name):
+    """The oracle's restatement of OnPrepareReply's batch == what the reference's
+    own code built (fixture written by oracle/ref_multi_driver.cpp)."""
+    from oracles import oracle_decisions
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    trace = open(os.path.join(gold, name + ".mpxt"), "rb").read()
+    want = open(os.path.join(gold, name + ".mpxd"), "rb").read()
+    assert oracle_decisions(trace) == want
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_oracle_decisions_match_reference_live(seed):
+    if not ref_available():
+        pytest.skip("reference driver not built (needs /root/reference)")
+    from oracles import oracle_decisions, ref_decisions
+    t = fuzz_trace(50_000 + seed, n_nodes=5, n_inst=120, n_msgs=400)
+    assert oracle_decisions(t) == ref_decisions(t)
+    t = _mpx.generate_trace(_mpx.GEN_FAULTY, num_nodes=7, num_instances=400, seed=70 + seed, batch=32, proposers=3,
+                            drop_rate=500, dup_rate=1000, max_delay=500)
+    assert oracle_decisions(t) == ref_decisions(t)
