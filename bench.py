@@ -193,8 +193,11 @@ class FileGroup:
         return [self._get("r%d_%d" % (self.k, r)) for r in range(self.world)]
 
     def close(self):
-        self.exchange(b"")                          # nobody reads the directory after this
+        self.exchange(b"")
+        self._put("done_%d" % self.rank, b"")       # this rank reads no file of the directory any more
         if self.rank == 0:
+            for r in range(self.world):
+                self._get("done_%d" % r)
             import shutil
             shutil.rmtree(self.dir, ignore_errors=True)
 

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -71,7 +72,7 @@ struct mpx_engine {
     uint64_t shard_len = 0;
     uint32_t NB = 0;
     // device buffers
-    DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, pair_ev, m_flags, m_maxseen;
+    DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, pair_gp, m_flags, m_maxseen;
     DevBuf m_gate, e_pid, ep_amask;
     DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
     DevBuf sc_type, sc_key, sc_idx, b_rbal, b_rsrc, b_bal;
@@ -339,7 +340,7 @@ static int upload_trace(mpx_engine *e)
     TRY(upload(e->m_ballot, h.m_ballot, s)); TRY(upload(e->m_aux, h.m_aux, s));
     TRY(upload(e->m_ent, h.m_ent, s)); TRY(upload(e->m_cnt, h.m_cnt, s));
     TRY(upload(e->m_node, h.m_node, s)); TRY(upload(e->node_off, h.node_off, s));
-    TRY(upload(e->pair_ev, h.pair_ev, s));
+    TRY(upload(e->pair_gp, h.pair_gp, s));
     TRY(upload(e->m_flags, h.m_flags0, s));             // static flags; the steps rewrite the dynamic ones
     TRY(upload(e->sc_type, h.sc_type, s)); TRY(upload(e->sc_key, h.sc_key, s)); TRY(upload(e->sc_idx, h.sc_idx, s));
     TRY(upload(e->b_rbal, h.b_rbal, s)); TRY(upload(e->b_rsrc, h.b_rsrc, s)); TRY(upload(e->b_bal, h.b_bal, s));
@@ -361,6 +362,18 @@ static int upload_trace(mpx_engine *e)
         }
         TRY(upload(e->gp_list, gd, s));
         HTRY(hipStreamSynchronize(s));                 // gd is a local
+        if (std::getenv("MPX_TRACE_STATS")) {          // shape of the general work list (tools)
+            uint64_t fr = 0, ev = 0, mx = 0, pre = 0;
+            for (uint64_t q : h.gp_list) {
+                fr += h.f_off[q + 1] - h.f_off[q]; ev += h.ev_off[q + 1] - h.ev_off[q];
+                mx = std::max<uint64_t>(mx, h.f_off[q + 1] - h.f_off[q]);
+                for (uint64_t f = h.f_off[q]; f < h.f_off[q + 1]; ++f) pre += (h.frags[f].flags >> 4) == K_PREPLY;
+            }
+            std::fprintf(stderr, "[mpx] pairs %llu, general %zu: runs %llu (promise-reply runs %llu, max/pair %llu), "
+                         "events %llu; all runs %zu, messages %zu\n", (unsigned long long)((uint64_t)h.N * h.NB),
+                         h.gp_list.size(), (unsigned long long)fr, (unsigned long long)pre, (unsigned long long)mx,
+                         (unsigned long long)ev, h.frags.size(), h.m_type.size());
+        }
     }
     TRY(upload(e->ev_off, h.ev_off, s)); TRY(upload(e->ev_msg, h.ev_msg, s));
     TRY(upload(e->pl_off, h.pl_off, s)); TRY(upload(e->pl_msg, h.pl_msg, s));
@@ -374,7 +387,7 @@ static int upload_trace(mpx_engine *e)
     v.m_ballot = e->m_ballot.as<uint64_t>(); v.m_aux = e->m_aux.as<uint64_t>();
     v.m_ent = e->m_ent.as<uint64_t>(); v.m_cnt = e->m_cnt.as<uint32_t>();
     v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
-    v.pair_ev = e->pair_ev.as<uint8_t>();
+    v.pair_gp = e->pair_gp.as<uint8_t>();
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
     v.m_gate = e->m_gate.as<uint32_t>(); v.e_pid = e->e_pid.as<uint64_t>();
     v.ep_amask = e->ep_amask.as<uint64_t>(); v.num_epochs = (uint32_t)e->epochs.size();
@@ -1128,8 +1141,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     TRY(e->b_rbal.alloc(8 * (uint64_t)N * K + 8)); TRY(e->b_rsrc.alloc(4 * (uint64_t)N * K + 4));
     TRY(e->b_bal.alloc(8 * K + 8));
     TRY(upload(e->node_off, h.node_off, s));
-    TRY(e->pair_ev.alloc(std::max<uint64_t>((uint64_t)N * e->NB, 8)));
-    HTRY(hipMemsetAsync(e->pair_ev.p, 0, e->pair_ev.bytes, s));
+
     TRY(e->ev_off.alloc(8 * ((uint64_t)N * e->NB + 1)));
     HTRY(hipMemsetAsync(e->ev_off.p, 0, e->ev_off.bytes, s));
     TRY(e->ev_msg.alloc(8));
@@ -1147,14 +1159,19 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     TRY(upload(e->cf_off, cf_off, s)); TRY(e->cfrags.alloc(sizeof(Frag) * cf_off[NB] + 16));
     // pairs the lean kernels cannot take (ingest.cpp's predicate: every run is
     // dense, no snapshot events, so only the node count and run count decide)
+    // (lean: mpx_internal.hpp plan_shape_ok — a pair's batch runs are disjoint and
+    // in order, so its run count and a whole bucket decide)
     std::vector<uint64_t> gd;
+    std::vector<uint8_t> pair_gp(N * NB, 0);
     for (uint64_t q = 0; q < N * NB; ++q)
-        if (N > FAST_MAX_NODES || f_off[q + 1] - f_off[q] > FAST_MAX_FRAGS) {
+        if (f_off[q + 1] > f_off[q] && (N > FAST_MAX_NODES || f_off[q + 1] - f_off[q] > PLAN_FRAGS || (q / N + 1) * BS > L)) {
             const uint64_t w[GP_WORDS] = {f_off[q], f_off[q + 1], 0, 0, q, 0, 0, 0};
             gd.insert(gd.end(), w, w + GP_WORDS);
+            pair_gp[q] = 1;
         }
     if (gd.empty()) TRY(e->gp_list.alloc(8));
     else TRY(upload(e->gp_list, gd, s));
+    TRY(upload(e->pair_gp, pair_gp, s));
     if (launch_gen_clean(s, N, K, k0, sb, se, G0, G1, ballot, B, e->NB,
                          e->m_type.as<uint8_t>(), e->m_src.as<uint32_t>(), e->m_ballot.as<uint64_t>(),
                          e->m_aux.as<uint64_t>(), e->m_ent.as<uint64_t>(), e->m_cnt.as<uint32_t>(),
@@ -1172,7 +1189,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.m_ballot = e->m_ballot.as<uint64_t>(); v.m_aux = e->m_aux.as<uint64_t>();
     v.m_ent = e->m_ent.as<uint64_t>(); v.m_cnt = e->m_cnt.as<uint32_t>();
     v.m_node = e->m_node.as<uint32_t>(); v.node_off = e->node_off.as<uint64_t>();
-    v.pair_ev = e->pair_ev.as<uint8_t>();
+    v.pair_gp = e->pair_gp.as<uint8_t>();
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
     v.m_gate = e->m_gate.as<uint32_t>(); v.e_pid = e->e_pid.as<uint64_t>();
     v.ep_amask = e->ep_amask.as<uint64_t>(); v.num_epochs = (uint32_t)e->epochs.size();

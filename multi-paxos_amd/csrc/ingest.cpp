@@ -852,18 +852,20 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         for (auto &x : evp) ht.ev_msg[pos[x.first]++] = x.second;
     }
     std::vector<std::pair<uint64_t, uint32_t>>().swap(evp);
-    // pairs the lean kernel cannot take (same predicate as k_apply_fast in
-    // kernels.hip): they go to the general kernel's work list
+    // pairs that are not lean (mpx_internal.hpp plan_shape_ok: one plan word of
+    // k_plan) go to the general kernel's work list
+    ht.pair_gp.assign(N * NB, 0);
     for (uint64_t b = 0; b < NB; ++b)
         for (uint32_t n = 0; n < N; ++n) {
             const uint64_t p = b * N + n, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
             if (!nf) continue;
-            bool fast = !member && N <= FAST_MAX_NODES && nf <= FAST_MAX_FRAGS && !ht.pair_ev[p];
-            for (uint64_t f = f0; fast && f < f0 + nf; ++f) {
-                const uint8_t fl = ht.frags[f].flags;
-                fast = (fl & FR_DENSE) && ((fl >> 4) == K_ACCEPT || (fl >> 4) == K_COMMIT);
+            bool fast = !member && N <= FAST_MAX_NODES && nf <= PLAN_FRAGS && !ht.pair_ev[p] && (b + 1) * BS <= slen;
+            if (fast) {
+                uint64_t w1[PLAN_FRAGS];
+                for (uint64_t f = 0; f < nf; ++f) std::memcpy(&w1[f], reinterpret_cast<const uint8_t *>(&ht.frags[f0 + f]) + 8, 8);
+                fast = plan_shape_ok(w1, (uint32_t)nf);
             }
-            if (!fast) ht.gp_list.push_back(p);
+            if (!fast) { ht.gp_list.push_back(p); ht.pair_gp[p] = 1; }
         }
     // slots for sparse fragments
     if (ht.any_sparse) {

@@ -663,7 +663,7 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // its snapshot events see empty state, so skipping them changes no output.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t FAST_PAIR_FRAGS = 2;      // descriptors a pair lane prefetches
-constexpr uint64_t EV_BIT = 1ull << 63;      // k_apply_fast: pair_ev folded into the lane's CSR offset
+constexpr uint64_t EV_BIT = 1ull << 63;      // k_apply_fast: pair_gp folded into the lane's CSR offset
 constexpr uint64_t DONE_BIT = 1ull << 62;    // ... and (AFTER_STORE) "k_plan planned this pair"
 constexpr uint64_t OFF_FLAGS = EV_BIT | DONE_BIT;
 __host__ __device__ inline uint32_t fast_group(uint32_t N, uint32_t cap = 4)
@@ -702,7 +702,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         oa = oc = 0;
         if (st >= steps) return;
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
-        if (lane <= nb * N) oa = v.f_off[b0 * N + lane] | (lane < nb * N && v.pair_ev[b0 * N + lane] ? EV_BIT : 0);
+        if (lane <= nb * N) oa = v.f_off[b0 * N + lane] | (lane < nb * N && v.pair_gp[b0 * N + lane] ? EV_BIT : 0);
         if (AFTER_STORE && lane < nb * N &&   // the plan word's high half (PLAN_SKIP: all ones)
             reinterpret_cast<const uint32_t *>(v.plan)[2 * (b0 * N + lane) + 1] != 0xFFFFFFFFu)
             oa |= DONE_BIT;
@@ -956,7 +956,6 @@ __device__ inline uint64_t frag_w1(const Frag *f) { return reinterpret_cast<cons
 //                and its low half is already four slots' bytes
 // PLAN_SKIP: not k_store's row (k_apply_fast / k_chosen write it).
 constexpr uint64_t PLAN_SKIP = ~0ull;
-constexpr uint32_t PLAN_FRAGS = 8;                          // runs of a pair k_plan still plans
 constexpr uint32_t PLAN_LDS = 512;                          // descriptor words a k_plan wave stages (4 KiB)
 constexpr uint32_t PLAN_UNI = BS | BS << 9 | BS << 18;      // bits 32..58 of a one-segment word
 
@@ -981,17 +980,6 @@ __device__ inline u32x4 plan_bytes16(uint64_t q, uint32_t p)
     }
     return u32x4{__builtin_amdgcn_perm(V, V, (uint32_t)lo), __builtin_amdgcn_perm(V, V, (uint32_t)(lo >> 32)),
                  __builtin_amdgcn_perm(V, V, (uint32_t)hi), __builtin_amdgcn_perm(V, V, (uint32_t)(hi >> 32))};
-}
-// the distinct run boundaries inside (0, 256), sorted into s[0..2] (BS = unused);
-// false once a fourth one appears
-__device__ inline bool plan_add_split(uint32_t x, uint32_t (&s)[3])
-{
-    if (x == 0 || x >= BS || x == s[0] || x == s[1] || x == s[2]) return true;
-    if (s[2] != BS) return false;
-    if (x < s[0]) { s[2] = s[1]; s[1] = s[0]; s[0] = x; }
-    else if (x < s[1]) { s[2] = s[1]; s[1] = x; }
-    else s[2] = x;
-    return true;
 }
 __device__ inline uint64_t plan_pack(const uint32_t (&val)[4], const uint32_t (&s)[3])
 {
@@ -1039,7 +1027,7 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
         const uint64_t b = i / N;
 
         const uint32_t len = (uint32_t)(o1 - oa);
-        const bool in_list = len && len <= FAST_MAX_FRAGS && !v.pair_ev[i];
+        const bool in_list = len && len <= FAST_MAX_FRAGS && !v.pair_gp[i];
         uint64_t q = PLAN_SKIP;
         if (in_list && len <= F) {
             uint64_t w[F];
@@ -1313,7 +1301,9 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
 // duplicate or retried COMMIT carries the same entries), and the snapshots a
 // granted PREPARE or a promise quorum emits.
 // DIGEST: the digested verification run (mpx_run) — the only user of the slot's ballot
-template <int WAVES_PER_EU, bool DIGEST>
+// MEMBER: member semantics (insert-first apply, epoch events) — compiled apart so
+// the multi kernel carries none of it
+template <int WAVES_PER_EU, bool DIGEST, bool MEMBER>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 {
     __shared__ uint16_t lidx_all[4][BS];
@@ -1327,7 +1317,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     wave_lds_fence();
     uint32_t cA = 0, cL = 0, cP = 0, cQ = 0;    // per-lane counts stay far below 2^32
     unsigned long long dig = 0;
-    const bool member = v.semantics == MPX_SEM_MEMBER;
+    constexpr bool member = MEMBER;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
     constexpr uint32_t S_PRESENT = 1, S_COMMITTED = 2;
@@ -1479,7 +1469,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 ++cL;
                             }
                     } else if (kind == K_PREPLY) {
-                        if (mf & F_COUNTED) {
+                        if ((mf & F_COUNTED) && !(v.knobs & 8192)) {       // knob 8192: experiment, no merge
 #pragma unroll 1
                             for (uint32_t j = 0; j < SPL; ++j)
                                 if (k[j] >= 0) {
@@ -1547,7 +1537,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j)
                             if (!(SF(j) & S_COMMITTED)) { if (DIGEST) sb[j] = 0; SF_SET(j, 0); se[j] = sm[j] = 0; }
-                    } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
+                    } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM) && !(v.knobs & 16384)) {   // knob 16384: experiment
                         bool hit[SPL];
                         uint32_t ref[SPL], ext[SPL];
 #pragma unroll
@@ -2010,9 +2000,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (v.semantics == MPX_SEM_MEMBER) {
         // member: every pair walks the general kernel (insert semantics, epoch events)
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-                   else if (g.variant == 4) hipLaunchKernelGGL((k_apply<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-                   else hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); }
+        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+                   else hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v); }
     } else {
         // multi: the lean kernel also writes the chosen log of clean buckets
         // digest runs (verification) take their own instantiation, so the
@@ -2035,9 +2024,9 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         }
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-                   else if (g.variant == 4) hipLaunchKernelGGL((k_apply<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-                   else hipLaunchKernelGGL((k_apply<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); }
+        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+                   else if (g.variant == 4) hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+                   else hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); }
     }
     if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);

@@ -172,7 +172,7 @@ struct DevView {
     const uint32_t *m_cnt;
     const uint32_t *m_node;         // node of each message
     const uint64_t *node_off;       // N+1
-    const uint8_t *pair_ev;         // per (bucket, node) pair: 1 when snapshot events act on it
+    const uint8_t *pair_gp;         // per (bucket, node) pair: 1 = not lean, on k_apply's work list
     uint8_t *m_flags;
     uint64_t *m_maxseen;
     // member semantics
@@ -250,6 +250,42 @@ struct DevView {
 // go to k_apply's work list (kernels.hip, ingest.cpp, engine.cpp)
 constexpr uint32_t FAST_MAX_NODES = 61;
 constexpr uint32_t FAST_MAX_FRAGS = 63;
+// A *lean* pair is one k_plan turns into one plan word (kernels.hip): at most
+// PLAN_FRAGS runs, all dense ACCEPT / COMMIT runs, at most three distinct run
+// boundaries inside the bucket (four segments of equal slots), no instance under
+// two COMMIT runs (a re-commit's Value check), a whole bucket, no snapshot
+// events; ingest.cpp / mpx_load_clean_device put every other pair on the work
+// list of the general k_apply (pair_gp = 1).  All static: no run-time flag enters.
+constexpr uint32_t PLAN_FRAGS = 8;
+// the distinct run boundaries inside (0, 256), sorted into s[0..2] (BS = unused);
+// false once a fourth one appears
+MPX_HD inline bool plan_add_split(uint32_t x, uint32_t (&s)[3])
+{
+    if (x == 0 || x >= BS || x == s[0] || x == s[1] || x == s[2]) return true;
+    if (s[2] != BS) return false;
+    if (x < s[0]) { s[2] = s[1]; s[1] = s[0]; s[0] = x; }
+    else if (x < s[1]) { s[2] = s[1]; s[1] = x; }
+    else s[2] = x;
+    return true;
+}
+// the run shape of a lean pair, from its runs' second descriptor words
+MPX_HD inline bool plan_shape_ok(const uint64_t *w1, uint32_t len)
+{
+    if (!len || len > PLAN_FRAGS) return false;
+    uint32_t sp[3] = {BS, BS, BS};
+    for (uint32_t k = 0; k < len; ++k) {
+        const uint32_t fl = (uint32_t)(w1[k] >> 56), kind = fl >> 4;
+        const uint32_t cnt = (uint32_t)(w1[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w1[k] >> 48) & 0xFF;
+        if (!(fl & FR_DENSE) || (kind != K_ACCEPT && kind != K_COMMIT)) return false;
+        if (!plan_add_split(st0, sp) || !plan_add_split(st0 + cnt, sp)) return false;
+        if (kind == K_COMMIT)
+            for (uint32_t j = 0; j < k; ++j) {
+                const uint32_t c2 = (uint32_t)(w1[j] >> 32) & 0xFFFF, s2 = (uint32_t)(w1[j] >> 48) & 0xFF;
+                if ((w1[j] >> 60) == K_COMMIT && st0 < s2 + c2 && s2 < st0 + cnt) return false;
+            }
+    }
+    return true;
+}
 constexpr uint32_t APPLY_WGS_MAX = 2048;
 constexpr uint32_t CHOSEN_WGS_MAX = 1024;
 // partial counter slots

@@ -79,29 +79,17 @@ def test_combine_rejects_disagreeing_scalars():
         mdist.combine([a, b])
 
 
-def _filegroup_rank(rank, world, port, q):
-    import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    import bench
-    os.environ["MASTER_PORT"] = port
-    g = bench.FileGroup(rank, world)
-    uid = bench.broadcast_bytes(g, b"uid-from-rank-0" if rank == 0 else None, rank)
-    bench.barrier(g)
-    mx = bench.allreduce_max(g, float(rank) * 1.5)
-    g.close()
-    q.put((rank, uid, mx))
-
-
 def test_bench_filegroup_rendezvous():
     """bench.py's N>1 rendezvous (no PyTorch): broadcast, barrier and max-reduce over 3 processes."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = str(40000 + os.getpid() % 10000)
-    procs = [ctx.Process(target=_filegroup_rank, args=(r, 3, port, q)) for r in range(3)]
+    import _filegroup_child                         # a module without torch: the spawned children start fast
+    procs = [ctx.Process(target=_filegroup_child.rank_main, args=(r, 3, port, q)) for r in range(3)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=60) for _ in procs)
+    res = sorted(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(timeout=60)
     assert [r[1] for r in res] == [b"uid-from-rank-0"] * 3
