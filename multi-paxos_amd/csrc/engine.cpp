@@ -77,7 +77,7 @@ struct mpx_engine {
     DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
     DevBuf sc_type, sc_key, sc_idx, b_rbal, b_rsrc, b_bal;
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
-    DevBuf f_off, frags, frag_w1, gp_list, ev_off, ev_msg, pl_off, pl_msg;
+    DevBuf f_off, frags, frag_w1, gp_list, ev_off, ev_msg, ev_aux, pl_off, pl_msg;
     uint64_t num_frags = 0;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
     DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy, exec_aux, exec_out;
@@ -375,7 +375,7 @@ static int upload_trace(mpx_engine *e)
                          (unsigned long long)ev, h.frags.size(), h.m_type.size());
         }
     }
-    TRY(upload(e->ev_off, h.ev_off, s)); TRY(upload(e->ev_msg, h.ev_msg, s));
+    TRY(upload(e->ev_off, h.ev_off, s)); TRY(upload(e->ev_msg, h.ev_msg, s)); TRY(upload(e->ev_aux, h.ev_aux, s));
     TRY(upload(e->pl_off, h.pl_off, s)); TRY(upload(e->pl_msg, h.pl_msg, s));
     TRY(upload(e->b_msg, h.b_msg, s)); TRY(upload(e->b_pstart, h.b_pstart, s));
     TRY(upload(e->b_rep_off, h.b_rep_off, s)); TRY(upload(e->b_rep, h.b_rep, s));
@@ -401,7 +401,7 @@ static int upload_trace(mpx_engine *e)
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
     e->num_frags = h.frags.size();
     v.num_gp = h.gp_list.size(); v.gp_list = e->gp_list.as<uint64_t>();
-    v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>();
+    v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>(); v.ev_aux = e->ev_aux.as<uint64_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
     v.num_batches = (uint32_t)h.b_msg.size();
     v.b_msg = e->b_msg.as<uint32_t>(); v.b_pstart = e->b_pstart.as<uint32_t>();
@@ -1144,7 +1144,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
 
     TRY(e->ev_off.alloc(8 * ((uint64_t)N * e->NB + 1)));
     HTRY(hipMemsetAsync(e->ev_off.p, 0, e->ev_off.bytes, s));
-    TRY(e->ev_msg.alloc(8));
+    TRY(e->ev_msg.alloc(8)); TRY(e->ev_aux.alloc(8));
     TRY(upload(e->chunk_node, h.chunk_node, s)); TRY(upload(e->chunk_beg, h.chunk_beg, s));
     TRY(upload(e->chunk_end, h.chunk_end, s)); TRY(upload(e->node_chunk_off, h.node_chunk_off, s));
     TRY(e->chunk_agg.alloc(std::max<size_t>(16 * h.chunk_node.size(), 16)));
@@ -1203,7 +1203,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
     e->num_frags = f_off[N * NB];
     v.num_gp = gd.size() / GP_WORDS; v.gp_list = e->gp_list.as<uint64_t>();
-    v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>();
+    v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>(); v.ev_aux = e->ev_aux.as<uint64_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
     v.num_batches = (uint32_t)K;
     v.b_msg = e->b_msg.as<uint32_t>(); v.b_pstart = e->b_pstart.as<uint32_t>();

@@ -602,6 +602,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     //                 Acceptor is deleted / recreated (member/paxos.cpp:1897-1901,1952-1957).
     // So a pair walks O(events that touch it), not every event of its node.
     std::vector<std::pair<uint64_t, uint32_t>> evp;          // (pair, message)
+    std::vector<uint64_t> evx;                               // its aux word (PREPARE: the ranges meeting the bucket)
     std::vector<uint32_t> first_frag(NB, NONE32);            // per bucket: the node's first fragment message
     std::vector<uint64_t> touched, round_b;
     std::vector<uint8_t> in_round(NB, 0);
@@ -754,7 +755,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             }
             // snapshot events of this message (after its own fragments: the kernels
             // merge a message's fragments before its event)
-            auto add_ev = [&](uint64_t b) { evp.push_back({b * N + n, g}); };
+            auto add_ev = [&](uint64_t b) { evp.push_back({b * N + n, g}); evx.push_back(0); };
             auto clear_round = [&]() { for (uint64_t b : round_b) in_round[b] = 0; round_b.clear(); };
             if (t == MPX_MSG_PREPARE && maxb >= 0) {
                 uint64_t last_b = 0;                     // ranges are sorted and disjoint: buckets ascend
@@ -763,12 +764,18 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                     if (e <= sb || a >= sb + slen) continue;
                     const uint64_t lo = (std::max(a, sb) - sb) >> BSH;
                     const uint64_t hi = std::min<uint64_t>((std::min(e, sb + slen) - sb + BS - 1) >> BSH, (uint64_t)maxb + 1);
-                    // several ranges of one PREPARE can meet in a bucket (holes): list it once
-                    for (uint64_t b = lo; b < hi; ++b)
-                        if (first_frag[b] < g && (evp.empty() || evp.back().second != g || b > last_b)) {
+                    // several ranges of one PREPARE can meet in a bucket (holes): list it
+                    // once, its aux word = first range (absolute) | ranges meeting it << 32
+                    for (uint64_t b = lo; b < hi; ++b) {
+                        if (first_frag[b] >= g) continue;
+                        if (!evp.empty() && evp.back().second == g && b == last_b && evp.back().first == b * N + n) {
+                            evx.back() += 1ull << 32;
+                        } else if (evp.empty() || evp.back().second != g || b > last_b) {
                             add_ev(b);
+                            evx.back() = (ent + r) | (1ull << 32);
                             last_b = b;
                         }
+                    }
                 }
             } else if (t == MPX_MSG_PREPARE_REPLY) {
                 for (uint64_t b : round_b) add_ev(b);
@@ -847,10 +854,16 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         ht.ev_off[i + 1] += ht.ev_off[i];
     }
     ht.ev_msg.resize(evp.size());
+    ht.ev_aux.resize(evp.size());
     {
         std::vector<uint64_t> pos(ht.ev_off.begin(), ht.ev_off.end() - 1);
-        for (auto &x : evp) ht.ev_msg[pos[x.first]++] = x.second;
+        for (size_t i = 0; i < evp.size(); ++i) {
+            const uint64_t at = pos[evp[i].first]++;
+            ht.ev_msg[at] = evp[i].second;
+            ht.ev_aux[at] = evx[i];
+        }
     }
+    std::vector<uint64_t>().swap(evx);
     std::vector<std::pair<uint64_t, uint32_t>>().swap(evp);
     // pairs that are not lean (mpx_internal.hpp plan_shape_ok: one plan word of
     // k_plan) go to the general kernel's work list

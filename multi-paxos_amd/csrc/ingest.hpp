@@ -76,6 +76,7 @@ struct HostTrace {
     std::vector<uint64_t> gp_list;                  // (node, bucket) pairs for the general apply kernel
     std::vector<uint64_t> ev_off, pl_off;           // ev_off: per (bucket, node) pair (N * NB + 1); pl_off: per node
     std::vector<uint32_t> ev_msg, pl_msg;
+    std::vector<uint64_t> ev_aux;                   // per event: PREPARE's first range meeting the bucket | count << 32
     std::vector<uint8_t> pair_ev;                   // per pair: 1 when it has snapshot events
     std::vector<uint8_t> pair_gp;                   // per pair: 1 when not lean (mpx_internal.hpp plan_shape_ok)
     std::vector<uint32_t> b_msg, b_pstart, b_rep, b_rsrc;

@@ -1489,25 +1489,20 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) have |= (SF(j) & S_PRESENT) != 0;
                         if ((fl & F_GRANTED) && __ballot(have)) {
-                            // FilterAcceptedValues over the prepare's ranges (:902-922);
-                            // ranges sorted by start and disjoint (ingest): one
-                            // wave-uniform search for the bucket's first range, then
-                            // the few ranges that meet the bucket
-                            const uint64_t r0 = v.m_ent[g];
-                            const uint32_t nr = v.m_cnt[g];
-                            const uint64_t blo = v.shard_begin + li0, bhi = blo + BS;
-                            uint32_t lo = 0, hi = nr;       // last range with a <= blo
-                            while (lo < hi) {
-                                const uint32_t mid = (lo + hi) >> 1;
-                                if (v.g_a[r0 + mid] <= blo) lo = mid + 1; else hi = mid;
-                            }
+                            // FilterAcceptedValues over the prepare's ranges (:902-922):
+                            // ingest listed which of them meet this bucket (ev_aux: first
+                            // range | count), loaded one per lane
+                            const uint64_t ax = v.ev_aux[ei + c];
+                            const uint32_t r0 = (uint32_t)ax, nr = (uint32_t)(ax >> 32);
+                            const uint64_t blo = v.shard_begin + li0;
+                            uint64_t la = 0, lb = 0;
+                            if (lane < nr) { la = v.g_a[r0 + lane]; lb = v.g_b[r0 + lane]; }
                             bool hit[SPL];
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j) hit[j] = false;
-                            for (uint32_t r = lo ? lo - 1 : 0; r < nr; ++r) {
-                                const uint64_t ra = v.g_a[r0 + r], rb = v.g_b[r0 + r];
-                                if (ra >= bhi) break;
-                                if (rb <= blo) continue;
+                            for (uint32_t r = 0; r < nr; ++r) {
+                                const uint64_t ra = r < 64 ? rl64(la, r) : v.g_a[r0 + r];
+                                const uint64_t rb = r < 64 ? rl64(lb, r) : v.g_b[r0 + r];
 #pragma unroll
                                 for (uint32_t j = 0; j < SPL; ++j) {
                                     const uint64_t iid = blo + lane + 64 * j;
@@ -1607,15 +1602,17 @@ __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base
     wave_lds_fence();
     unsigned long long cC = 0, dig = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
-    // 64 buckets per wave step: one lane-parallel load of their chosen_valid
-    // bytes, then a walk of only the buckets k_apply_fast left
-    for (uint64_t c = xcd_wave_id(wv); 64 * c < v.NB; c += stride) {
-        const uint64_t b0 = 64 * c;
-        uint64_t todo = __ballot(b0 + lane < v.NB && !v.chosen_valid[b0 + lane]);
+    // 64 buckets per wave step, strided by the wave count (b = base + lane *
+    // stride) so the walks spread over every wave even when few buckets need
+    // one: one lane-parallel load of their chosen_valid bytes, then a walk of
+    // only the buckets k_plan / k_apply_fast left
+    for (uint64_t base = xcd_wave_id(wv); base < v.NB; base += 64 * stride) {
+        const uint64_t bl = base + (uint64_t)lane * stride;
+        uint64_t todo = __ballot(bl < v.NB && !v.chosen_valid[bl]);
         while (todo) {
             const uint32_t i = (uint32_t)__builtin_ctzll(todo);
             todo &= todo - 1;
-            chosen_walk(v, b0 + i, lidx, cC, dig);
+            chosen_walk(v, base + (uint64_t)i * stride, lidx, cC, dig);
         }
     }
     unsigned long long cc[2] = {cC, dig};

@@ -209,6 +209,7 @@ struct DevView {
                                     // range, its event CSR range, the pair q (one coalesced load per item)
     const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
     const uint32_t *ev_msg;
+    const uint64_t *ev_aux;         // per event: PREPARE: first range (g_a index) meeting the bucket | count << 32
     const uint64_t *pl_off;         // N+1
     const uint32_t *pl_msg;
     // batches
