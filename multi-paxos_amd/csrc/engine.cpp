@@ -78,6 +78,7 @@ struct mpx_engine {
     DevBuf sc_type, sc_key, sc_idx, b_rbal, b_rsrc, b_bal;
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
     DevBuf f_off, frags, frag_w1, gp_list, ev_off, ev_msg, ev_aux, pl_off, pl_msg;
+    DevBuf pc_node, pc_node_off, pc_beg, pc_end, pc_head, pc_state;
     uint64_t num_frags = 0;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
     DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy, exec_aux, exec_out;
@@ -286,6 +287,31 @@ static int finish_view(mpx_engine *e)
     TRY(e->st_valid.alloc((size_t)N * e->NB));
     TRY(e->chosen_valid.alloc(e->NB));
     TRY(e->plan.alloc((size_t)(N + 1) * e->NB * 8));
+    {   // promise-quorum chunks over each node's proposer list (k_prop_chunk / k_prop_node)
+        const HostTrace &h = e->ht;
+        uint64_t pc = PROP_CHUNK;                       // MPX_PROP_CHUNK: smaller chunks (tests)
+        if (const char *x = std::getenv("MPX_PROP_CHUNK")) pc = std::max<uint64_t>(1, std::strtoull(x, nullptr, 10));
+        std::vector<uint32_t> pn, pno(N + 1, 0);
+        std::vector<uint64_t> pb, pe;
+        uint32_t multi = 0;
+        for (uint32_t n = 0; n < N && n + 1 < h.pl_off.size(); ++n) {
+            pno[n] = (uint32_t)pn.size();
+            for (uint64_t a = h.pl_off[n]; a < h.pl_off[n + 1]; a += pc) {
+                pn.push_back(n); pb.push_back(a); pe.push_back(std::min<uint64_t>(a + pc, h.pl_off[n + 1]));
+                if (a != h.pl_off[n]) multi = 1;
+            }
+        }
+        pno[N] = (uint32_t)pn.size();
+        v.pc_multi = multi;
+        TRY(upload(e->pc_node, pn, e->stream)); TRY(upload(e->pc_node_off, pno, e->stream));
+        TRY(upload(e->pc_beg, pb, e->stream)); TRY(upload(e->pc_end, pe, e->stream));
+        TRY(e->pc_head.alloc(std::max<size_t>(4 * pn.size(), 4))); TRY(e->pc_state.alloc(std::max<size_t>(24 * pn.size(), 24)));
+        v.num_pc = (uint32_t)pn.size();
+        v.pc_node = e->pc_node.as<uint32_t>(); v.pc_node_off = e->pc_node_off.as<uint32_t>();
+        v.pc_beg = e->pc_beg.as<uint64_t>(); v.pc_end = e->pc_end.as<uint64_t>();
+        v.pc_head = e->pc_head.as<uint32_t>(); v.pc_state = e->pc_state.as<uint64_t>();
+        HTRY(hipStreamSynchronize(e->stream));          // the host vectors are locals
+    }
     TRY(e->frag_w1.alloc(std::max<size_t>(8 * e->num_frags, 8)));
     if (launch_frag_w1(v.frags, e->frag_w1.as<uint64_t>(), e->num_frags, e->stream) != 0) return MPX_E_HIP;
     v.frag_w1 = e->frag_w1.as<uint64_t>();

@@ -342,16 +342,19 @@ __device__ inline uint64_t shfl64_up(uint64_t x, uint32_t d)
     return ((uint64_t)hi << 32) | lo;
 }
 
-__global__ __launch_bounds__(64) void k_proposer(DevView v)
+// The window walk over records [i0, i1) of node n's list.  `known`: the state
+// carried in (cb, cprep, cmask) is the real one; otherwise records before the
+// range's first round head are left alone (their round started in an earlier
+// chunk: k_prop_node walks them).  Returns, in `head`, the offset of the first
+// head from i0 (~0u: none).
+struct PropState { uint64_t cb, cmask; uint32_t cprep, known; };
+__device__ inline void prop_range(const DevView &v, uint32_t n, uint64_t i0, uint64_t i1, PropState &st, uint32_t &head)
 {
-    const uint32_t n = blockIdx.x, lane = threadIdx.x;
-    if (n >= v.N) return;
-    uint64_t cb = 0, cmask = 0;            // proposal_id_ = 0 at genesis (:338)
-    bool cprep = false;                    // prepare_retry_timeout_ = NULL
+    const uint32_t lane = threadIdx.x & 63;
     const bool member = v.semantics == MPX_SEM_MEMBER;
     const uint64_t le = ~0ull >> (63 - lane);                  // lanes 0..lane
     const uint64_t all_nodes = v.N >= 64 ? ~0ull : ((1ull << v.N) - 1);
-    const uint64_t i0 = v.pl_off[n], i1 = v.pl_off[n + 1];
+    head = ~0u;
     for (uint64_t base = i0; base < i1; base += 64) {
         const uint32_t cnt = (uint32_t)(i1 - base < 64 ? i1 - base : 64);
         const bool valid = lane < cnt;
@@ -370,11 +373,13 @@ __global__ __launch_bounds__(64) void k_proposer(DevView v)
         const bool ec = valid && member && t == MPX_MSG_E_EPOCH && (gt & G_PRECLR); // round head: idle
         const bool rep = valid && gated && t == MPX_MSG_PREPARE_REPLY;
         const uint64_t heads = __ballot(ps || ec), psm = __ballot(ps);
+        if (heads && head == ~0u) head = (uint32_t)(base - i0) + (uint32_t)__builtin_ctzll(heads);
         const uint64_t hm = heads & le;
         const int sh = hm ? 63 - __builtin_clzll(hm) : -1;                         // this record's round head
-        const uint64_t rb = sh >= 0 ? shfl64(b, sh) : cb;
-        const bool prep0 = sh >= 0 ? ((psm >> sh) & 1) != 0 : cprep;
-        const uint64_t mask0 = sh >= 0 ? 0 : cmask;
+        const bool mine = sh >= 0 || st.known;                                      // its round's state is known here
+        const uint64_t rb = sh >= 0 ? shfl64(b, sh) : st.cb;
+        const bool prep0 = sh >= 0 ? ((psm >> sh) & 1) != 0 : st.cprep != 0;
+        const uint64_t mask0 = sh >= 0 ? 0 : st.cmask;
         const bool m1 = rep && prep0 && b == rb;                                    // :1038 / :1160
         const bool bad = m1 && (src >= 64 || !((am >> src) & 1));                  // :1040 / :1163
         const bool match = m1 && !bad;
@@ -396,14 +401,54 @@ __global__ __launch_bounds__(64) void k_proposer(DevView v)
         const uint32_t fc = cseg ? (uint32_t)__builtin_ctzll(cseg) : 64;          // the round's quorum reply
         uint32_t fl = 0;
         if (match && fc >= lane) fl = F_COUNTED | (fc == lane ? F_QUORUM : 0);
-        if (bad && fc > lane) record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0);
-        if (rep) v.m_flags[g] = (uint8_t)fl;    // a reply's flags are this kernel's alone (static ones are 0)
+        if (mine && bad && fc > lane) record_violation(v, MPX_V_BAD_NODE, n, g - v.node_off[n], 0);
+        if (mine && rep) v.m_flags[g] = (uint8_t)fl;    // a reply's flags are this kernel's alone (static ones are 0)
         // carry the last record's round into the next window
         const uint32_t L = cnt - 1;
-        if (psm) cb = rl64(b, 63 - __builtin_clzll(psm));
+        if (psm) st.cb = rl64(b, 63 - __builtin_clzll(psm));
         const bool prepL = rl32((uint32_t)prep0, L) && !rl32((uint32_t)(cseg != 0), L);
-        cprep = prepL;
-        cmask = prepL ? rl64(incl, L) : 0;
+        st.cprep = prepL;
+        st.cmask = prepL ? rl64(incl, L) : 0;
+        if (heads) st.known = 1;
+    }
+}
+
+// Promise quorums, pass 1: one wave per chunk of PROP_CHUNK records of a node's
+// list; a node's first chunk starts from the genesis state (proposal_id_ = 0,
+// :338; not preparing), later ones from their first round head — the records
+// before it wait for k_prop_node.  Writes the chunk's first head and its state
+// after the last record (valid when it has a head or is the node's first).
+__global__ __launch_bounds__(64) void k_prop_chunk(DevView v)
+{
+    const uint32_t c = blockIdx.x;
+    const uint32_t n = v.pc_node[c];
+    const uint64_t i0 = v.pc_beg[c], i1 = v.pc_end[c];
+    PropState st{0, 0, 0, i0 == v.pl_off[n] ? 1u : 0u};
+    uint32_t head;
+    prop_range(v, n, i0, i1, st, head);
+    if (threadIdx.x == 0) {
+        v.pc_head[c] = head;
+        v.pc_state[3 * c] = st.cb; v.pc_state[3 * c + 1] = st.cmask; v.pc_state[3 * c + 2] = st.cprep | (st.known << 1);
+    }
+}
+
+// pass 2: one wave per node, its chunks in order: the records before each
+// chunk's first head under the state carried from the chunk before
+__global__ __launch_bounds__(64) void k_prop_node(DevView v)
+{
+    const uint32_t n = blockIdx.x;
+    if (n >= v.N) return;
+    const uint32_t c0 = v.pc_node_off[n], c1 = v.pc_node_off[n + 1];
+    if (c0 == c1) return;
+    PropState st{v.pc_state[3 * c0], v.pc_state[3 * c0 + 1], (uint32_t)(v.pc_state[3 * c0 + 2] & 1), 1};
+    for (uint32_t c = c0 + 1; c < c1; ++c) {
+        const uint64_t i0 = v.pc_beg[c], i1 = v.pc_end[c];
+        const uint32_t h = v.pc_head[c];
+        uint32_t dummy;
+        prop_range(v, n, i0, h == ~0u ? i1 : i0 + h, st, dummy);
+        if (h != ~0u) {
+            st.cb = v.pc_state[3 * c]; st.cmask = v.pc_state[3 * c + 1]; st.cprep = (uint32_t)(v.pc_state[3 * c + 2] & 1);
+        }
     }
 }
 
@@ -1459,7 +1504,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                             if (k[j] >= 0) {
                                 const uint32_t x = (uint32_t)(ent + k[j]);
                                 if (SF(j) & S_COMMITTED) {                            // :1508
-                                    if (se[j] != x && e_val[se[j]] != e_val[x])
+                                    if (se[j] != x && !(v.knobs & 32768) && e_val[se[j]] != e_val[x])   // knob 32768: experiment
                                         record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
                                                          v.shard_begin + li0 + lane + 64 * j);
                                 } else {
@@ -1991,7 +2036,10 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
         else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
     }
-    hipLaunchKernelGGL(k_proposer, dim3(v.N), dim3(64), 0, s, v);
+    if (v.num_pc) {
+        hipLaunchKernelGGL(k_prop_chunk, dim3(v.num_pc), dim3(64), 0, s, v);
+        if (v.pc_multi) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s, v);
+    }
     if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
     if (ev_apply0) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
     if (v.semantics == MPX_SEM_MEMBER) {

@@ -41,6 +41,7 @@ namespace mpx {
 constexpr uint32_t BSH = 8;                  // bucket = 256 instances
 constexpr uint32_t BS = 1u << BSH;
 constexpr uint32_t SCAN_CHUNK = 4096;        // header-scan chunk (messages): 16 per thread
+constexpr uint32_t PROP_CHUNK = 2048;        // promise-quorum chunk (pl records): 32 windows of 64
 // k_scan_apply re-reduces a node's earlier chunk aggregates inline (O(chunks^2)
 // per node) up to this many chunks per node; longer streams take k_scan_node
 constexpr uint32_t SCAN_INLINE_CHUNKS = 512;
@@ -209,6 +210,13 @@ struct DevView {
                                     // range, its event CSR range, the pair q (one coalesced load per item)
     const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
     const uint32_t *ev_msg;
+    // promise-quorum chunks (k_prop_chunk / k_prop_node): PROP_CHUNK records of one
+    // node's pl list each, CSR per node; outputs: first round head, state after
+    uint32_t num_pc, pc_multi;      // pc_multi: some node has more than one chunk (k_prop_node runs)
+    const uint32_t *pc_node, *pc_node_off;
+    const uint64_t *pc_beg, *pc_end;
+    uint32_t *pc_head;
+    uint64_t *pc_state;             // 3 words per chunk: ballot, promise mask, preparing | known << 1
     const uint64_t *ev_aux;         // per event: PREPARE: first range (g_a index) meeting the bucket | count << 32
     const uint64_t *pl_off;         // N+1
     const uint32_t *pl_msg;

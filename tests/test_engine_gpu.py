@@ -402,11 +402,15 @@ def test_store_chunks_tails_and_partial_pairs(extra):
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
 
 
-@pytest.mark.parametrize("env", [("MPX_SCAN_NODE_PASS", "1"), ("MPX_KNOBS", "2048")])
-@pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "demo_s0"])
+@pytest.mark.parametrize("env", [("MPX_SCAN_NODE_PASS", "1"), ("MPX_KNOBS", "2048"), ("MPX_PROP_CHUNK", "64"),
+                                 ("MPX_PROP_CHUNK", "5")])
+@pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "c5_member_3",
+                                  "demo_s0", "demo5_s3", "hm_promise_merge"])
 def test_kept_alternative_paths(name, env, monkeypatch):
     """The kept alternatives stay correct: the separate per-node scan pass (taken
-    automatically beyond SCAN_INLINE_CHUNKS chunks per node) and 64-bucket k_store8 chunks."""
+    automatically beyond SCAN_INLINE_CHUNKS chunks per node), 64-bucket k_store8
+    chunks, and promise-quorum chunks small enough that rounds span chunks
+    (k_prop_chunk's deferred prefixes, k_prop_node's carry)."""
     if name not in INDEX:
         pytest.skip("no golden " + name)
     monkeypatch.setenv(*env)
