@@ -366,8 +366,19 @@ static int upload_trace(mpx_engine *e)
     TRY(upload(e->m_ballot, h.m_ballot, s)); TRY(upload(e->m_aux, h.m_aux, s));
     TRY(upload(e->m_ent, h.m_ent, s)); TRY(upload(e->m_cnt, h.m_cnt, s));
     TRY(upload(e->m_node, h.m_node, s)); TRY(upload(e->node_off, h.node_off, s));
-    TRY(upload(e->pair_gp, h.pair_gp, s));
+    {
+        std::vector<uint8_t> gp(h.pair_gp);
+        gp.resize(gp.size() + 8, 0);                   // dword slack (k_plan_store8)
+        TRY(upload(e->pair_gp, gp, s));
+        HTRY(hipStreamSynchronize(s));
+    }
     TRY(upload(e->m_flags, h.m_flags0, s));             // static flags; the steps rewrite the dynamic ones
+    if (e->m_flags.bytes < h.m_flags0.size() + 8) {    // + a dword of slack: k_plan_store8 reads flags as dwords
+        std::vector<uint8_t> f(h.m_flags0);
+        f.resize(f.size() + 8, 0);
+        TRY(upload(e->m_flags, f, s));
+        HTRY(hipStreamSynchronize(s));
+    }
     TRY(upload(e->sc_type, h.sc_type, s)); TRY(upload(e->sc_key, h.sc_key, s)); TRY(upload(e->sc_idx, h.sc_idx, s));
     TRY(upload(e->b_rbal, h.b_rbal, s)); TRY(upload(e->b_rsrc, h.b_rsrc, s)); TRY(upload(e->b_bal, h.b_bal, s));
     TRY(e->m_maxseen.alloc(std::max<size_t>(h.m_type.size() * 8, 8)));
@@ -1160,7 +1171,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     hipStream_t s = e->stream;
     TRY(e->m_type.alloc(G)); TRY(e->m_src.alloc(4 * G)); TRY(e->m_ballot.alloc(8 * G)); TRY(e->m_aux.alloc(8 * G));
     TRY(e->m_ent.alloc(8 * G)); TRY(e->m_cnt.alloc(4 * G)); TRY(e->m_node.alloc(4 * G));
-    TRY(e->m_flags.alloc(G)); TRY(e->m_maxseen.alloc(8 * G));
+    TRY(e->m_flags.alloc(G + 8)); TRY(e->m_maxseen.alloc(8 * G));
     HTRY(hipMemsetAsync(e->m_flags.p, 0, G, s));          // no static flags: every source is a node
     TRY(e->sc_type.alloc((uint64_t)N * (K + 1))); TRY(e->sc_key.alloc(8 * (uint64_t)N * (K + 1)));
     TRY(e->sc_idx.alloc(4 * (uint64_t)N * (K + 1)));
@@ -1197,6 +1208,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
         }
     if (gd.empty()) TRY(e->gp_list.alloc(8));
     else TRY(upload(e->gp_list, gd, s));
+    pair_gp.resize(pair_gp.size() + 8, 0);             // dword slack (k_plan_store8)
     TRY(upload(e->pair_gp, pair_gp, s));
     if (launch_gen_clean(s, N, K, k0, sb, se, G0, G1, ballot, B, e->NB,
                          e->m_type.as<uint8_t>(), e->m_src.as<uint32_t>(), e->m_ballot.as<uint64_t>(),

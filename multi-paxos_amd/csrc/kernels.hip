@@ -748,8 +748,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         if (st >= steps) return;
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
         if (lane <= nb * N) oa = v.f_off[b0 * N + lane] | (lane < nb * N && v.pair_gp[b0 * N + lane] ? EV_BIT : 0);
-        if (AFTER_STORE && lane < nb * N &&   // the plan word's high half (PLAN_SKIP: all ones)
-            reinterpret_cast<const uint32_t *>(v.plan)[2 * (b0 * N + lane) + 1] != 0xFFFFFFFFu)
+        if (AFTER_STORE && lane < nb * N && v.st_valid[b0 * N + lane])   // set only by k_plan so far
             oa |= DONE_BIT;
         if (lane <= nb) oc = v.cf_off[b0 + lane];
     };
@@ -2054,8 +2053,9 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (v.digest) hipLaunchKernelGGL((k_apply_fast<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
         else if (!(v.knobs & 64) && v.N <= FAST_MAX_NODES) {
             // plan + stream, then the per-slot pairs (knob 64: the one-kernel form)
-            // (a persistent software-pipelined k_plan — next group's descriptor words and the
-            // one after's offsets in flight — measured slower: 0.329 vs 0.304 ms apply phase)
+            // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
+            // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
+            // 0.391 vs 0.304 ms apply phase at C4; the compiler drains vmcnt at its loop head)
             hipLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s, v, g.apply_wgs);
             if (v.slot_w == 1 && (v.knobs & 128)) hipLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
             // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64
