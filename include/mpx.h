@@ -267,6 +267,23 @@ int  mpx_dump_result(mpx_engine *eng, uint8_t **out, uint64_t *size);
  * u64 n, {u64 iid, u64 handle} * n, iid ascending}.  *out is malloc'ed; free
  * with mpx_free.  MPX_E_STATE for member semantics or a shard engine. */
 int  mpx_read_decisions(mpx_engine *eng, uint8_t **out, uint64_t *size);
+/* Commit reliability (multi semantics, an engine that kept
+ * every record — shard starting at 0, nothing left out for another shard):
+ * every CommittingValues each node's proposer created in the last run — at an
+ * accept quorum (OnAcceptReply, multi/paxos.cpp:1416-1421) and at a promise
+ * quorum while it held committed values (OnPrepareReply re-commits all of them,
+ * :1184-1197) — numbered 1, 2, ... per node like committing_id_ (:340), and what
+ * OnCommitReply (:1625-1641) made of it: replied_ as a learner mask and the
+ * reply at which every node had replied (the commit retires; a retry timer,
+ * Commit :1474-1478, resends to the learners not in the mask).  Computed on the
+ * device (k_commits) from the run's accept / promise quorums.  Format MPXC:
+ * "MPXC" u32 1, u32 nodes; per node u64 count, per commit {u64 id, u64
+ * created_seq, u64 kind (0 accept quorum, 1 promise quorum), u64 accept_id
+ * (kind 0, else 0), u64 retired_seq (~0: still open), u64 replied_mask}, seqs
+ * = record indices in the node's stream.  *out is malloc'ed; free with
+ * mpx_free.  MPX_E_STATE for member semantics or a shard engine, MPX_E_RANGE
+ * for a COMMIT_REPLY naming a learner >= 64. */
+int  mpx_read_commits(mpx_engine *eng, uint8_t **out, uint64_t *size);
 /* Encoded reference Value bytes (multi/paxos.cpp:556-598) for a handle. */
 int  mpx_value_bytes(mpx_engine *eng, uint64_t handle, uint8_t *buf,
                      uint32_t cap, uint32_t *len);

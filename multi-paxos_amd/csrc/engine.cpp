@@ -69,6 +69,7 @@ struct mpx_engine {
     HostTrace ht;
     bool dirty = true;
     bool device_trace = false;       // trace materialised by a device generator
+    bool whole = true;               // no record left out for another shard (mpx_read_commits)
     uint64_t shard_len = 0;
     uint32_t NB = 0;
     // device buffers
@@ -353,6 +354,7 @@ static int upload_trace(mpx_engine *e)
     const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
     if (member && e->epochs.empty()) return MPX_E_STATE;        // no epoch table yet
     TRY(build_trace(e->nodes, e->cfg.shard_begin, e->shard_len, member ? e->epochs : std::vector<mpx_epoch>(), e->ht));
+    e->whole = e->cfg.shard_begin == 0 && e->ht.part_dropped == 0;
     HostTrace &h = e->ht;
     hipStream_t s = e->stream;
     {
@@ -1095,6 +1097,124 @@ extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
     return MPX_OK;
 }
 
+// ---------------------------------------------- commit reliability (f4) --
+// The proposer's CommittingValues bookkeeping (multi/paxos.cpp:1184-1197,
+// 1416-1421, 1625-1641).  A node creates commit id ++committing_id_ at every
+// accept quorum (the batch's chosen reply, k_votes) and at every promise quorum
+// where it holds committed values (k_decide pass 0: the highest instance it had
+// committed before the quorum exists); the host ranks those per node in message
+// order.  k_commits walks the COMMIT_REPLYs of each (node, commit id) on the
+// device: replied_ as a learner mask, retired at |replied_| == N.
+// Format MPXC (include/mpx.h).
+extern "C" int mpx_read_commits(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->cfg.semantics != MPX_SEM_MULTI || !e->whole) return MPX_E_STATE;
+    Results r;
+    TRY(fetch_results(e, r));
+    const HostTrace &h = e->ht;
+    const uint32_t N = e->cfg.num_nodes;
+    hipStream_t s = e->stream;
+    // promise quorums: did the node hold a committed value there (xmax > 0)
+    std::vector<uint32_t> qn, qg;
+    for (uint32_t n = 0; n < N; ++n)
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g)
+            if (h.m_type[g] == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM)) { qn.push_back(n); qg.push_back((uint32_t)g); }
+    std::vector<uint64_t> xmax;
+    if (!qn.empty()) {
+        DevBuf d_node, d_msg, d_xmax;
+        TRY(upload(d_node, qn, s)); TRY(upload(d_msg, qg, s));
+        TRY(d_xmax.alloc(8 * qn.size())); HTRY(hipMemsetAsync(d_xmax.p, 0, 8 * qn.size(), s));
+        DecideArgs a{};
+        a.E = (uint32_t)qn.size(); a.ev_node = d_node.as<uint32_t>(); a.ev_msg = d_msg.as<uint32_t>();
+        a.xmax = d_xmax.as<unsigned long long>();
+        if (launch_decide(e->view, s, 0, a) != 0) return MPX_E_HIP;
+        HTRY(hipStreamSynchronize(s));
+        TRY(d2h(xmax, d_xmax, qn.size()));
+    }
+    // commit creation points per node, in message order: (message, accept id | ~0 for a promise quorum)
+    std::vector<std::vector<std::pair<uint32_t, uint64_t>>> cm(N);
+    for (size_t j = 0; j < h.b_msg.size(); ++j)
+        if (r.b_chosen[j] != NONE32) cm[h.m_node[h.b_msg[j]]].push_back({r.b_chosen[j], h.m_aux[h.b_msg[j]]});
+    for (size_t k = 0; k < qn.size(); ++k)
+        if (xmax[k]) cm[qn[k]].push_back({qg[k], ~0ull});
+    std::vector<uint64_t> cm_off(N + 1, 0);
+    std::vector<uint32_t> cm_pos;
+    for (uint32_t n = 0; n < N; ++n) {
+        std::sort(cm[n].begin(), cm[n].end());
+        for (auto &x : cm[n]) cm_pos.push_back(x.first);
+        cm_off[n + 1] = cm_pos.size();
+    }
+    // reply lists: the COMMIT_REPLYs of each (node, commit id), in processing order
+    std::vector<uint64_t> cr_off(1, 0), cr_id;
+    std::vector<uint32_t> cr_msg, cr_src, cr_node;
+    {
+        std::vector<std::vector<uint32_t>> lists;
+        std::map<uint64_t, uint32_t> idx;
+        for (uint32_t n = 0; n < N; ++n) {
+            idx.clear();
+            for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
+                if (h.m_type[g] != MPX_MSG_COMMIT_REPLY) continue;
+                if (h.m_src[g] >= 64) return MPX_E_RANGE;           // replied_ as a 64-bit learner mask
+                auto it = idx.find(h.m_aux[g]);
+                if (it == idx.end()) {
+                    it = idx.emplace(h.m_aux[g], (uint32_t)lists.size()).first;
+                    lists.emplace_back();
+                    cr_id.push_back(h.m_aux[g]);
+                    cr_node.push_back(n);
+                }
+                lists[it->second].push_back((uint32_t)g);
+            }
+        }
+        for (auto &l : lists) {
+            for (uint32_t g : l) { cr_msg.push_back(g); cr_src.push_back(h.m_src[g]); }
+            cr_off.push_back(cr_msg.size());
+        }
+    }
+    const uint32_t L = (uint32_t)cr_id.size();
+    std::vector<uint32_t> ret;
+    std::vector<uint64_t> mask;
+    if (L) {
+        DevBuf d_off, d_id, d_cmoff, d_msg, d_src, d_node, d_pos, d_ret, d_mask;
+        TRY(upload(d_off, cr_off, s)); TRY(upload(d_id, cr_id, s)); TRY(upload(d_cmoff, cm_off, s));
+        TRY(upload(d_msg, cr_msg, s)); TRY(upload(d_src, cr_src, s)); TRY(upload(d_node, cr_node, s));
+        TRY(upload(d_pos, cm_pos, s));
+        TRY(d_ret.alloc(4ull * L)); TRY(d_mask.alloc(8ull * L));
+        CommitArgs a{L, d_off.as<uint64_t>(), d_id.as<uint64_t>(), d_cmoff.as<uint64_t>(), d_msg.as<uint32_t>(),
+                     d_src.as<uint32_t>(), d_node.as<uint32_t>(), d_pos.as<uint32_t>(), d_ret.as<uint32_t>(),
+                     d_mask.as<unsigned long long>()};
+        if (launch_commits(e->view, s, a) != 0) return MPX_E_HIP;
+        HTRY(hipStreamSynchronize(s));
+        TRY(d2h(ret, d_ret, L)); TRY(d2h(mask, d_mask, L));
+    }
+    // per node, per commit id: the list that names it (if any)
+    std::vector<std::map<uint64_t, uint32_t>> by_id(N);
+    for (uint32_t l = 0; l < L; ++l) by_id[cr_node[l]][cr_id[l]] = l;
+    std::string d;
+    d.append("MPXC", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, N);
+    for (uint32_t n = 0; n < N; ++n) {
+        app<uint64_t>(d, cm[n].size());
+        for (size_t k = 0; k < cm[n].size(); ++k) {
+            const uint64_t id = k + 1;
+            auto it = by_id[n].find(id);
+            const bool has = it != by_id[n].end();
+            const uint32_t rg = has ? ret[it->second] : NONE32;
+            app<uint64_t>(d, id);
+            app<uint64_t>(d, seq_of(h, n, cm[n][k].first));
+            app<uint64_t>(d, cm[n][k].second == ~0ull ? 1 : 0);
+            app<uint64_t>(d, cm[n][k].second == ~0ull ? 0 : cm[n][k].second);
+            app<uint64_t>(d, rg == NONE32 ? ~0ull : seq_of(h, n, rg));
+            app<uint64_t>(d, has ? mask[it->second] : 0);
+        }
+    }
+    *out = (uint8_t *)std::malloc(d.size());
+    if (!*out) return MPX_E_NOMEM;
+    std::memcpy(*out, d.data(), d.size());
+    *size = d.size();
+    return MPX_OK;
+}
+
 // -------------------------------------------------------------- generators --
 extern "C" int mpx_trace_generate(const mpx_gen_params *p, uint8_t **out, uint64_t *size)
 {
@@ -1125,6 +1245,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     const uint32_t N = e->cfg.num_nodes;
     const uint64_t sb = e->cfg.shard_begin, se = e->cfg.shard_end, L = se - sb, NB = e->NB;
     const uint64_t k0 = sb / B, K = (se - 1) / B - k0 + 1;      // kept batches: those meeting the shard
+    e->whole = sb == 0 && se == p->num_instances;
     const uint64_t G0 = 2 + N + K * (3 + 2ull * N), G1 = 1 + 2 * K;
     const uint64_t G = G0 + (uint64_t)(N - 1) * G1;
     const uint64_t E = L;                                       // one shared run per batch

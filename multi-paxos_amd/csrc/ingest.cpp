@@ -680,6 +680,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             }
             if (drop) {
                 ++ht.dropped;
+                if (ns.part[k] != 0) ++ht.part_dropped;
                 if (t == MPX_MSG_ACCEPT && (!member || (gate & G_SEG))) {
                     const uint64_t key = ns.ballot[k] | (member ? (uint64_t)(gate & G_SEG) << SEG_SHIFT : 0);
                     if (last_virtual) ht.sc_key.back() = std::max(ht.sc_key.back(), key);

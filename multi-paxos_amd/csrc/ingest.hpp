@@ -62,6 +62,7 @@ struct HostTrace {
     std::vector<uint64_t> node_off;
     std::vector<uint32_t> m_seq;                    // record index in its node's submitted stream
     uint64_t dropped = 0;                           // records of other shards left out (header sharding)
+    uint64_t part_dropped = 0;                      // ... of them, records whose entries all lie in other shards
     std::vector<uint32_t> chunk_node, node_chunk_off;
     std::vector<uint64_t> chunk_beg, chunk_end;
     std::vector<uint8_t> sc_type;                   // header-scan stream (mpx_internal.hpp SC_*)

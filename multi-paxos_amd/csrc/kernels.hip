@@ -2011,6 +2011,42 @@ int launch_decide(const DevView &v, void *stream, uint32_t pass, const DecideArg
     return (int)hipGetLastError();
 }
 
+// ------------------------------------------------- commit reliability --
+// OnCommitReply (multi/paxos.cpp:1625-1641): a COMMIT_REPLY for a
+// CommittingValues that exists (created at an earlier message: the accept
+// quorum, :1418, or a promise quorum of a node holding commits, :1184-1197) and
+// is not yet retired adds its learner to replied_; the commit retires at the
+// reply that makes |replied_| == |nodes_|, and later replies find nothing
+// (:1627).  One lane per (node, commit id) list; the replies' learner ids lie
+// beside the list (no gathers), so a lane reads 8 B per reply.
+__global__ __launch_bounds__(256) void k_commits(DevView v, CommitArgs a)
+{
+    const uint64_t l = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (l >= a.L) return;
+    const uint32_t n = a.cr_node[l];
+    const uint64_t c = a.cr_id[l], c0 = a.cm_off[n], c1 = a.cm_off[n + 1];
+    uint32_t ret = NONE32;
+    unsigned long long mask = 0;
+    if (c >= 1 && c <= c1 - c0) {
+        const uint32_t created = a.cm_pos[c0 + c - 1];
+        for (uint64_t r = a.cr_off[l]; r < a.cr_off[l + 1]; ++r) {
+            const uint32_t g = a.cr_msg[r], learner = a.cr_src[r];
+            if (g < created) continue;                         // no such commit yet (:1627)
+            mask |= 1ull << learner;                           // :1633 (learner < 64: checked by the host)
+            if ((uint32_t)__popcll(mask) == v.N) { ret = g; break; }   // :1635-1640
+        }
+    }
+    a.ret[l] = ret;
+    a.mask[l] = mask;
+}
+
+int launch_commits(const DevView &v, void *stream, const CommitArgs &a)
+{
+    if (!a.L) return 0;
+    hipLaunchKernelGGL(k_commits, dim3(cdiv(a.L, 256)), dim3(256), 0, (hipStream_t)stream, v, a);
+    return (int)hipGetLastError();
+}
+
 int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, uint64_t count, uint64_t *out)
 {
     if (!count) return 0;

@@ -362,6 +362,20 @@ struct DecideArgs {
     uint64_t max_blocks;            // blocks of the widest event (pass 1 / 2 grid)
 };
 int launch_decide(const DevView &v, void *stream, uint32_t pass, const DecideArgs &a);
+// Commit reliability (mpx_read_commits, kernels.hip k_commits):
+// L reply lists, one per (node, commit id named by its COMMIT_REPLYs), each the
+// replies in the node's processing order with their learner ids beside them;
+// per node the messages at which its CommittingValues were created (cm_pos,
+// CSR cm_off, commit id c = position c - 1).  Per list: the message of the reply
+// that completed the replied set (NONE32: open) and the final learner mask.
+struct CommitArgs {
+    uint32_t L;
+    const uint64_t *cr_off, *cr_id, *cm_off;
+    const uint32_t *cr_msg, *cr_src, *cr_node, *cm_pos;
+    uint32_t *ret;
+    unsigned long long *mask;
+};
+int launch_commits(const DevView &v, void *stream, const CommitArgs &a);
 // f_off / cf_off: host-computed prefix counts (per pair, per bucket), read by the generator
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
                      uint64_t G0, uint64_t G1, uint64_t ballot, uint64_t B, uint32_t NB,

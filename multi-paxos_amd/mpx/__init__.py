@@ -105,6 +105,7 @@ def lib():
             "mpx_last_violation": [vp, P(Violation)],
             "mpx_dump_result": [vp, P(u8p), u64p],
             "mpx_read_decisions": [vp, P(u8p), u64p],
+            "mpx_read_commits": [vp, P(u8p), u64p],
             "mpx_value_bytes": [vp, ctypes.c_uint64, u8p, ctypes.c_uint32, P(ctypes.c_uint32)],
             "mpx_trace_generate": [P(GenParams), P(u8p), u64p],
             "mpx_load_clean_device": [vp, P(GenParams)],
@@ -284,6 +285,13 @@ class Engine:
         out = ctypes.POINTER(ctypes.c_uint8)()
         size = ctypes.c_uint64()
         _ck("mpx_read_decisions", lib().mpx_read_decisions(self.h, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
+    def commits(self):
+        """MPXC bytes: every CommittingValues with its OnCommitReply retirement (mpx_read_commits)."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_read_commits", lib().mpx_read_commits(self.h, ctypes.byref(out), ctypes.byref(size)))
         return _take(out, size.value)
 
     def drain_sends(self):

@@ -310,6 +310,14 @@ typedef struct {
     size_t ent_off, ent_n;      /* entries (iid, handle) in node's batch pool  */
 } batch_t;
 
+/* a CommittingValues: id = ++committing_id_ at an accept quorum (kind 0,
+ * multi/paxos.cpp:1418) or at a promise quorum of a node holding committed
+ * values (kind 1: all of them re-committed, :1184-1197); replied_ as a learner
+ * mask; retired at |replied_| == |nodes_| */
+typedef struct {
+    u64 created_seq, kind, accept_id, retired_seq, mask;
+} commit_t;
+
 typedef struct {
     u32 index;
     /* acceptor (multi/paxos.cpp:492-495) */
@@ -347,6 +355,9 @@ typedef struct {
     /* phase-2 decisions (mpxo_decisions): value_id_ (multi/paxos.cpp:335) and the MPXD records */
     u64 value_id;
     buf_t dec; u64 n_dec;
+    /* commit reliability (mpxo_commits): committing_values_
+     * (multi/paxos.cpp:483), one record per CommittingValues in id order */
+    commit_t *cm; size_t ncm, ccm;
 } node_t;
 
 typedef struct { u32 version; u64 amask, pmask; } epoch_t;
@@ -645,6 +656,8 @@ static void decide(node_t *n, const ent_t *pre, size_t k, u64 seq)
     n->n_dec++;
 }
 
+static int new_commit(node_t *n, u64 seq, u64 kind, u64 accept);
+
 /* OnPrepareReply + UpdateByPreAcceptedValues, multi/paxos.cpp:1036-1057,1201-1223 */
 static int on_prepare_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
 {
@@ -689,10 +702,23 @@ static int on_prepare_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 se
         free(v);
         for (size_t i = 0; i < n->nb; ++i)                      /* :1054 */
             if (n->batches[i].live) { violate(c, n, 5, seq, 0); break; }
+        if (n->com.n && new_commit(n, seq, 1, 0)) return E_NOMEM;   /* re-commit everything committed, :1184-1197 */
         n->promised_set = 0;
         n->preparing = 0;
         map_clear(&n->pre);                                     /* :1105 */
     }
+    return OK;
+}
+
+static int new_commit(node_t *n, u64 seq, u64 kind, u64 accept)
+{
+    if (n->ncm == n->ccm) {
+        size_t cc = n->ccm ? n->ccm * 2 : 16;
+        commit_t *q = (commit_t *)realloc(n->cm, cc * sizeof(commit_t));
+        if (!q) return E_NOMEM;
+        n->cm = q; n->ccm = cc;
+    }
+    n->cm[n->ncm++] = (commit_t){seq, kind, accept, ~0ull, 0};
     return OK;
 }
 
@@ -714,7 +740,24 @@ static int on_accept_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq
         bput64(&n->events_c, accept);
         n->n_c++;
         b->live = 0;                                            /* :1423-1425 */
+        if (new_commit(n, seq, 0, accept)) return E_NOMEM;      /* CommittingValues(++committing_id_), :1418-1421 */
     }
+    return OK;
+}
+
+/* OnCommitReply, multi/paxos.cpp:1625-1641: a reply for a live commit adds its
+ * learner to replied_; the commit retires when every node has replied.  A
+ * learner id >= 64 (the engine's mask) is recorded as a violation instead. */
+static int on_commit_reply(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
+{
+    if (len < 16) return E_DECODE;
+    u32 learner = rd32(m + 4);
+    u64 id = rd64(m + 8);
+    if (id == 0 || id > n->ncm || n->cm[id - 1].retired_seq != ~0ull) return OK;   /* :1627 */
+    if (learner >= 64) { violate(c, n, 3, seq, 0); return OK; }
+    commit_t *x = &n->cm[id - 1];
+    x->mask |= 1ull << learner;                                 /* :1633 */
+    if ((u64)__builtin_popcountll(x->mask) == c->N) x->retired_seq = seq;   /* :1635-1640 */
     return OK;
 }
 
@@ -786,7 +829,7 @@ static int process(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     case 3:  return on_accept(c, n, m, len, seq);
     case 4:  return on_accept_reply(c, n, m, len, seq);
     case 5:  return on_commit(c, n, m, len, seq);
-    case 6:  return len < 16 ? E_DECODE : OK;                   /* OnCommitReply: out of scope */
+    case 6:  return on_commit_reply(c, n, m, len, seq);
     case 16: return on_p_start(n, m, len);
     case 17: return on_p_batch(c, n, m, len, seq);
     default: return E_DECODE;                                   /* ASSERT(false), :1672 */
@@ -1249,7 +1292,7 @@ static int check_values(ctx_t *c)
 }
 
 static int run_shard_ex(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *out_size, u64 *stats,
-                        u64 *viol, u8 **dec, u64 *dec_size)
+                        u64 *viol, u8 **dec, u64 *dec_size, u8 **cmt, u64 *cmt_size)
 {
     if (size < HDR || memcmp(trace, "MPXT", 4)) return E_DECODE;
     ctx_t c;
@@ -1318,7 +1361,22 @@ static int run_shard_ex(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64
         for (u32 i = 0; i < c.N; ++i) { bput64(&d, c.nodes[i].n_dec); bput(&d, c.nodes[i].dec.p, c.nodes[i].dec.n); }
         if (d.oom) { free(d.p); rc = E_NOMEM; } else { *dec = d.p; *dec_size = d.n; }
     }
-    for (u32 i = 0; i < c.N; ++i) free(c.nodes[i].dec.p);
+    if (rc == OK && cmt) {
+        /* MPXC (include/mpx.h mpx_read_commits): per node, per commit id */
+        buf_t d = {0};
+        bput(&d, "MPXC", 4); bput32(&d, 1); bput32(&d, c.N);
+        for (u32 i = 0; i < c.N; ++i) {
+            const node_t *n = &c.nodes[i];
+            bput64(&d, n->ncm);
+            for (size_t k = 0; k < n->ncm; ++k) {
+                bput64(&d, k + 1); bput64(&d, n->cm[k].created_seq); bput64(&d, n->cm[k].kind);
+                bput64(&d, n->cm[k].accept_id);
+                bput64(&d, n->cm[k].retired_seq); bput64(&d, n->cm[k].mask);
+            }
+        }
+        if (d.oom) { free(d.p); rc = E_NOMEM; } else { *cmt = d.p; *cmt_size = d.n; }
+    }
+    for (u32 i = 0; i < c.N; ++i) { free(c.nodes[i].dec.p); free(c.nodes[i].cm); }
     if (viol) memcpy(viol, c.first_violation, sizeof c.first_violation);
     for (u32 i = 0; i < c.N; ++i) {
         node_t *n = &c.nodes[i];
@@ -1339,7 +1397,7 @@ static int run_shard_ex(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64
 
 static int run_shard(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
 {
-    return run_shard_ex(trace, size, sb, se, out, out_size, stats, viol, NULL, NULL);
+    return run_shard_ex(trace, size, sb, se, out, out_size, stats, viol, NULL, NULL, NULL, NULL);
 }
 
 int mpxo_run(const u8 *trace, u64 size, u8 **out, u64 *out_size, u64 *stats, u64 *viol)
@@ -1353,7 +1411,20 @@ int mpxo_decisions(const u8 *trace, u64 size, u8 **out, u64 *out_size)
 {
     u8 *r = NULL;
     u64 rs = 0;
-    int rc = run_shard_ex(trace, size, 0, ~0ull, &r, &rs, NULL, NULL, out, out_size);
+    int rc = run_shard_ex(trace, size, 0, ~0ull, &r, &rs, NULL, NULL, out, out_size, NULL, NULL);
+    free(r);
+    return rc;
+}
+
+/* mpxo_commits: the commit-reliability bookkeeping of a whole-trace run (MPXC,
+ * DESIGN.md §f4; multi semantics): per node every CommittingValues with its
+ * creation (accept quorum), accept id, retirement (all nodes replied) and
+ * final replied_ mask. */
+int mpxo_commits(const u8 *trace, u64 size, u8 **out, u64 *out_size)
+{
+    u8 *r = NULL;
+    u64 rs = 0;
+    int rc = run_shard_ex(trace, size, 0, ~0ull, &r, &rs, NULL, NULL, NULL, NULL, out, out_size);
     free(r);
     return rc;
 }

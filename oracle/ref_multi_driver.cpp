@@ -96,6 +96,9 @@ struct Node {
     std::set<paxos::AcceptingID> marker_batches;       // created by P_BATCH markers
     std::map<paxos::AcceptingID, std::map<paxos::InstanceID, paxos::Value> > batch_values;
     u64 P = 0, A = 0, L = 0;
+    // the reference's own CommittingValues bookkeeping (MPXC): per commit id
+    // {created seq, kind (0 accept quorum, 1 promise quorum), accept id, retired seq, replied mask}
+    std::vector<std::vector<u64> > commits;
 };
 
 }  // namespace
@@ -116,11 +119,30 @@ static void scan_values(const uint8_t *m, size_t len, std::map<u64, paxos::Value
 }
 
 static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size, uint64_t *stats,
-                    std::string *decisions);
+                    std::string *decisions, std::string *commits = NULL);
 
 extern "C" int mpxref_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size, uint64_t *stats)
 {
     return run_impl(trace, size, out, out_size, stats, NULL);
+}
+
+// The reference's own commit-reliability bookkeeping (MPXC):
+// every CommittingValues each node created (multi/paxos.cpp:1184-1197,1416-1421),
+// in id order, with the COMMIT_REPLY that retired it (OnCommitReply, :1625-1641)
+// and its replied_ set as a mask (at retirement, or at the end of the trace).
+extern "C" int mpxref_commits(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)
+{
+    uint8_t *r = NULL;
+    uint64_t rs = 0;
+    std::string d;
+    int rc = run_impl(trace, size, &r, &rs, NULL, NULL, &d);
+    free(r);
+    if (rc) return rc;
+    *out = (uint8_t *)malloc(d.size() ? d.size() : 1);
+    if (!*out) return -2;
+    memcpy(*out, d.data(), d.size());
+    *out_size = d.size();
+    return 0;
 }
 
 // The reference's own phase-2 decisions (MPXD): per node, per
@@ -143,7 +165,7 @@ extern "C" int mpxref_decisions(const uint8_t *trace, uint64_t size, uint8_t **o
 }
 
 static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size, uint64_t *stats,
-                    std::string *decisions)
+                    std::string *decisions, std::string *commits)
 {
     if (size < 40 || memcmp(trace, "MPXT", 4)) return -4;
     uint32_t N = rd32(trace + 8), sem = rd32(trace + 12), ne = rd32(trace + 24);
@@ -203,6 +225,17 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
             const uint8_t *m = bytes[i] + a;
             uint32_t type = rd32(m);
             size_t before = n.sends.size();
+            const paxos::CommittingID cid0 = p->committing_id_;
+            u64 retire_id = 0, retire_mask = 0;
+            if (type == 6) {               // OnCommitReply below: the commit it may retire
+                const paxos::CommitReplyMsg *msg = (const paxos::CommitReplyMsg *)m;
+                auto it = p->committing_values_.find(msg->commit_);
+                if (it != p->committing_values_.end()) {
+                    retire_id = msg->commit_;
+                    for (unsigned int x : it->second->replied_) if (x < 64) retire_mask |= 1ull << x;
+                    if (msg->learner_ < 64) retire_mask |= 1ull << msg->learner_;
+                }
+            }
             switch (type) {
             case 0: {
                 // P: entries in a granted reply are counted from the reply itself below
@@ -289,7 +322,7 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
                 p->OnCommit(msg);
                 break;
             }
-            case 6: break;     // OnCommitReply: commit-retry bookkeeping, out of scope
+            case 6: p->OnCommitReply((const paxos::CommitReplyMsg *)m); break;
             case 16: {         // P_START
                 p->proposal_id_ = rd64(m + 4);
                 p->prepare_promised_.clear();
@@ -312,6 +345,14 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
                 break;
             }
             default: return -4;
+            }
+            for (paxos::CommittingID id = cid0 + 1; id <= p->committing_id_; ++id) {
+                const u64 acc = type == 4 ? ((const paxos::AcceptReplyMsg *)m)->accept_ : 0;
+                n.commits.push_back(std::vector<u64>{k, type == 4 ? 0ull : 1ull, acc, ~0ull, 0});
+            }
+            if (retire_id && !p->committing_values_.count(retire_id) && retire_id <= n.commits.size()) {
+                n.commits[retire_id - 1][3] = k;
+                n.commits[retire_id - 1][4] = retire_mask;
             }
             // keep only the acceptor / learner replies (types 1,2,4,6)
             std::vector<Send> keep(n.sends.begin(), n.sends.begin() + before);
@@ -366,6 +407,22 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
         decisions->append("MPXD", 4);
         put<uint32_t>(*decisions, 1); put<uint32_t>(*decisions, N);
         for (uint32_t i = 0; i < N; ++i) { put<u64>(*decisions, ns[i].n_d); *decisions += ns[i].events_d; }
+    }
+    if (commits) {
+        commits->append("MPXC", 4);
+        put<uint32_t>(*commits, 1); put<uint32_t>(*commits, N);
+        for (uint32_t i = 0; i < N; ++i) {
+            Node &n = ns[i];
+            put<u64>(*commits, n.commits.size());
+            for (size_t c = 0; c < n.commits.size(); ++c) {
+                std::vector<u64> &x = n.commits[c];
+                auto it = n.impl->committing_values_.find(c + 1);
+                if (it != n.impl->committing_values_.end())
+                    for (unsigned int y : it->second->replied_) if (y < 64) x[4] |= 1ull << y;
+                put<u64>(*commits, c + 1);
+                for (u64 w : x) put<u64>(*commits, w);
+            }
+        }
     }
     if (stats) { stats[0] = chosen.size(); stats[1] = P; stats[2] = A; stats[3] = L; }
     *out = (uint8_t *)malloc(r.size());

@@ -135,3 +135,15 @@ def ref_decisions(trace):
 def oracle_decisions(trace):
     """The oracle's restatement of the same decisions (mpxo_decisions)."""
     return _blob_call(ORACLE_SO, "mpxo_decisions", trace)
+
+
+def ref_commits(trace):
+    """The reference's own CommittingValues bookkeeping (MPXC; multi semantics):
+    creation at accept / promise quorums, OnCommitReply retirement, replied masks
+    (oracle/ref_multi_driver.cpp mpxref_commits)."""
+    return _blob_call(REF_SO, "mpxref_commits", trace)
+
+
+def oracle_commits(trace):
+    """The oracle's restatement of the same bookkeeping (mpxo_commits)."""
+    return _blob_call(ORACLE_SO, "mpxo_commits", trace)

@@ -561,3 +561,54 @@ def test_incremental_submit_matches_whole(name):
             e.run()
             got = e.dump()
         assert got == want, (frac, mpxr.diff(got, want))
+
+
+# ---- commit reliability (multi/paxos.cpp:1184-1197,1416-1421,1625-1641) ----
+COMMITS = json.load(open(os.path.join(GOLD, "commits.json")))
+
+
+@pytest.mark.parametrize("name", sorted(COMMITS))
+def test_engine_commits_match_reference(name):
+    """Every CommittingValues the device finds (accept quorums from k_votes,
+    promise quorums with committed values from k_decide) and what k_commits makes
+    of its COMMIT_REPLYs == the reference's own bookkeeping (fixture)."""
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxc")
+    with mpx.Engine.for_trace(trace) as e:
+        e.run()
+        assert e.commits() == want
+        e.step()
+        e.sync()
+        assert e.commits() == want
+
+
+@pytest.mark.parametrize("seed,m", [(91, 1 << 12), (92, 1 << 14)])
+def test_engine_commits_match_oracle_c3(seed, m):
+    from oracles import oracle_commits
+    import mpxc
+    t = mpx.generate_trace(mpx.GEN_FAULTY, num_nodes=7, num_instances=m, seed=seed, batch=64, proposers=3,
+                           drop_rate=500, dup_rate=1000, max_delay=500)
+    want = oracle_commits(t)
+    with mpx.Engine.for_trace(t) as e:
+        e.run()
+        got = e.commits()
+    p = mpxc.parse(want)
+    assert sum(1 for x in p for r in x if r[4] != mpxc.OPEN) > 0
+    assert got == want
+
+
+def test_engine_commits_clean_device_trace():
+    """Device-generated clean trace: every batch is chosen and every COMMIT is
+    answered by all N learners, so every commit retires with the full mask."""
+    import mpxc
+    N, M = 5, 1 << 14
+    with mpx.Engine(N, 0, M) as e:
+        e.load_clean_device(num_instances=M, batch=256)
+        e.run()
+        p = mpxc.parse(e.commits())
+    assert len(p[0]) == M // 256 and all(len(x) == 0 for x in p[1:])
+    assert all(r[2] == 0 and r[4] != mpxc.OPEN and r[5] == (1 << N) - 1 for r in p[0])
+    with mpx.Engine(N, 0, M // 2) as e:     # a shard engine drops other shards' batches
+        e.load_clean_device(num_instances=M, batch=256)
+        e.run()
+        with pytest.raises(mpx.MpxError):
+            e.commits()

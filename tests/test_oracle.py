@@ -160,3 +160,38 @@ def test_oracle_decisions_match_reference_live(seed):
     t = _mpx.generate_trace(_mpx.GEN_FAULTY, num_nodes=7, num_instances=400, seed=70 + seed, batch=32, proposers=3,
                             drop_rate=500, dup_rate=1000, max_delay=500)
     assert oracle_decisions(t) == ref_decisions(t)
+
+
+# ---- commit reliability (multi/paxos.cpp:1184-1197,1416-1421,1625-1641) ----
+COMMITS = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "commits.json")))
+
+
+@pytest.mark.parametrize("name", sorted(COMMITS))
+def test_oracle_commits_match_reference_golden(name):
+    """The oracle's CommittingValues bookkeeping (creation at accept / promise
+    quorums, OnCommitReply retirement, replied_ masks) == the reference's own
+    (fixture written by oracle/ref_multi_driver.cpp)."""
+    from oracles import oracle_commits
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    trace = open(os.path.join(gold, name + ".mpxt"), "rb").read()
+    want = open(os.path.join(gold, name + ".mpxc"), "rb").read()
+    assert oracle_commits(trace) == want
+
+
+def test_commit_fixtures_cover_both_kinds_and_retirement():
+    kinds = sum(v["promise_quorum"] for v in COMMITS.values())
+    total = sum(v["commits"] for v in COMMITS.values())
+    retired = sum(v["retired"] for v in COMMITS.values())
+    assert 0 < kinds < total and 0 < retired < total
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_oracle_commits_match_reference_live(seed):
+    if not ref_available():
+        pytest.skip("reference driver not built (needs /root/reference)")
+    from oracles import oracle_commits, ref_commits
+    t = fuzz_trace(60_000 + seed, n_nodes=5, n_inst=120, n_msgs=400)
+    assert oracle_commits(t) == ref_commits(t)
+    t = _mpx.generate_trace(_mpx.GEN_FAULTY, num_nodes=7, num_instances=400, seed=90 + seed, batch=32, proposers=3,
+                            drop_rate=500, dup_rate=1000, max_delay=500)
+    assert oracle_commits(t) == ref_commits(t)
