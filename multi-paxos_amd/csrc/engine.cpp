@@ -74,7 +74,7 @@ struct mpx_engine {
     uint32_t NB = 0;
     // device buffers
     DevBuf m_type, m_src, m_ballot, m_aux, m_ent, m_cnt, m_node, node_off, pair_gp, m_flags, m_maxseen;
-    DevBuf m_gate, e_pid, ep_amask;
+    DevBuf m_gate, e_pid, ep_amask, ep_pmask, ep_ver, m_ver, ee_off, ee_msg, ee_state, sc_ver, sc_off;
     DevBuf chunk_node, chunk_beg, chunk_end, node_chunk_off, chunk_agg, chunk_carry, node_scal;
     DevBuf sc_type, sc_key, sc_idx, b_rbal, b_rsrc, b_bal;
     DevBuf e_val, e_slot, r_pid, r_val, r_slot, g_a, g_b;
@@ -357,12 +357,18 @@ static int upload_trace(mpx_engine *e)
     e->whole = e->cfg.shard_begin == 0 && e->ht.part_dropped == 0;
     HostTrace &h = e->ht;
     hipStream_t s = e->stream;
-    {
-        std::vector<uint64_t> am;
-        for (auto &x : e->epochs) am.push_back(x.acceptor_mask);
-        TRY(upload(e->ep_amask, am, s));
-        TRY(upload(e->m_gate, h.m_gate, s));
+    {   // member: the epoch table and the markers; the gates are computed on the device (k_gate_*)
+        std::vector<uint64_t> am, pm;
+        std::vector<uint32_t> ver;
+        for (auto &x : e->epochs) { am.push_back(x.acceptor_mask); pm.push_back(x.proposer_mask); ver.push_back(x.version); }
+        TRY(upload(e->ep_amask, am, s)); TRY(upload(e->ep_pmask, pm, s)); TRY(upload(e->ep_ver, ver, s));
+        TRY(e->m_gate.alloc(std::max<size_t>(4 * (member ? h.m_type.size() : 0), 4)));
+        TRY(upload(e->m_ver, h.m_ver, s));
+        TRY(upload(e->ee_off, h.ee_off, s)); TRY(upload(e->ee_msg, h.ee_msg, s));
+        TRY(e->ee_state.alloc(std::max<size_t>(4 * h.ee_msg.size(), 4)));
+        TRY(upload(e->sc_ver, h.sc_ver, s)); TRY(upload(e->sc_off, h.sc_off, s));
         TRY(upload(e->e_pid, h.e_pid, s));
+        HTRY(hipStreamSynchronize(s));                 // am / pm / ver are locals
     }
     TRY(upload(e->m_type, h.m_type, s)); TRY(upload(e->m_src, h.m_src, s));
     TRY(upload(e->m_ballot, h.m_ballot, s)); TRY(upload(e->m_aux, h.m_aux, s));
@@ -430,6 +436,10 @@ static int upload_trace(mpx_engine *e)
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
     v.m_gate = e->m_gate.as<uint32_t>(); v.e_pid = e->e_pid.as<uint64_t>();
     v.ep_amask = e->ep_amask.as<uint64_t>(); v.num_epochs = (uint32_t)e->epochs.size();
+    v.ep_pmask = e->ep_pmask.as<uint64_t>(); v.ep_ver = e->ep_ver.as<uint32_t>();
+    v.m_ver = e->m_ver.as<uint32_t>(); v.ee_off = e->ee_off.as<uint64_t>(); v.ee_msg = e->ee_msg.as<uint32_t>();
+    v.ee_state = e->ee_state.as<uint32_t>(); v.sc_ver = e->sc_ver.as<uint32_t>(); v.sc_off = e->sc_off.as<uint64_t>();
+    v.num_sc = h.sc_type.size();
     v.num_chunks = (uint32_t)h.chunk_node.size();
     v.chunk_node = e->chunk_node.as<uint32_t>(); v.chunk_beg = e->chunk_beg.as<uint64_t>();
     v.chunk_end = e->chunk_end.as<uint64_t>(); v.node_chunk_off = e->node_chunk_off.as<uint32_t>();
@@ -1352,6 +1362,10 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.m_flags = e->m_flags.as<uint8_t>(); v.m_maxseen = e->m_maxseen.as<uint64_t>();
     v.m_gate = e->m_gate.as<uint32_t>(); v.e_pid = e->e_pid.as<uint64_t>();
     v.ep_amask = e->ep_amask.as<uint64_t>(); v.num_epochs = (uint32_t)e->epochs.size();
+    v.ep_pmask = e->ep_pmask.as<uint64_t>(); v.ep_ver = e->ep_ver.as<uint32_t>();
+    v.m_ver = e->m_ver.as<uint32_t>(); v.ee_off = e->ee_off.as<uint64_t>(); v.ee_msg = e->ee_msg.as<uint32_t>();
+    v.ee_state = e->ee_state.as<uint32_t>(); v.sc_ver = e->sc_ver.as<uint32_t>(); v.sc_off = e->sc_off.as<uint64_t>();
+    v.num_sc = h.sc_type.size();
     v.num_chunks = (uint32_t)h.chunk_node.size();
     v.chunk_node = e->chunk_node.as<uint32_t>(); v.chunk_beg = e->chunk_beg.as<uint64_t>();
     v.chunk_end = e->chunk_end.as<uint64_t>(); v.node_chunk_off = e->node_chunk_off.as<uint32_t>();

@@ -612,6 +612,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     // node whose Proposer exists (Loop, member/paxos.cpp:763-790)
     std::unordered_map<uint64_t, uint32_t> live;
     std::vector<std::vector<uint32_t>> reps;
+    if (member) ht.ee_off.assign(N + 1, 0);
 
     for (uint32_t n = 0; n < N; ++n) {
         const NodeStream &ns = nodes[n];
@@ -630,66 +631,55 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         int64_t maxb = -1;                              // highest bucket with a fragment of this node
         live.clear();
         bool last_virtual = false;                      // the node's last scan record stands for left-out ACCEPTs
-        // member roles of node n along its stream (include/mpx.h E_EPOCH)
-        uint32_t ep = 0, seg = 1;
-        bool acc = member && ((epochs[0].acceptor_mask >> n) & 1);
-        bool prop = member && ((epochs[0].proposer_mask >> n) & 1);
+        // member semantics: no role or version logic here — the per-message gate
+        // (acceptor incarnation, version filter, proposer presence) is computed on
+        // the device from the E_EPOCH markers and the epoch table (kernels.hip
+        // k_gate_*); ingest only lists the markers and keeps every record
+        if (member) ht.ee_off[n] = ht.ee_msg.size();
         for (size_t k = 0; k < ns.type.size(); ++k) {
             const uint32_t g = (uint32_t)ht.m_type.size();
             const uint8_t t = ns.type[k];
-            uint32_t gate = 0;
-            if (member) {
-                if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
-                    gate = acc && ns.ver[k] == epochs[ep].version ? seg : 0;
-                } else if (t == MPX_MSG_E_EPOCH) {
-                    const uint32_t x = ns.ver[k];
-                    if (x >= epochs.size()) return MPX_E_DECODE;
-                    const bool a2 = (epochs[x].acceptor_mask >> n) & 1, p2 = (epochs[x].proposer_mask >> n) & 1;
-                    if (a2 != acc) { ++seg; gate |= G_ACCCLR; }
-                    if (p2 != prop || (p2 && epochs[x].acceptor_mask != epochs[ep].acceptor_mask)) gate |= G_PRECLR;
-                    if (seg > G_SEG) return MPX_E_RANGE;
-                    gate |= seg;
-                    acc = a2; prop = p2; ep = x;
-                } else if (t == MPX_MSG_COMMIT) {
-                    gate = prop ? G_PROP : 0;
-                } else if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_ACCEPT_REPLY || t == MPX_MSG_P_START ||
-                           t == MPX_MSG_P_BATCH) {
-                    gate = prop ? (ep + 1) << G_EPOCH_SHIFT : 0;
-                }
-            }
+            if (member && t == MPX_MSG_E_EPOCH && ns.ver[k] >= epochs.size()) return MPX_E_DECODE;
             // Header sharding: a record whose entries all belong to
             // other shards is left out here — ACCEPT / COMMIT / P_BATCH with no
             // entry in the shard, the ACCEPT_REPLYs of batches not kept, and
             // COMMIT_REPLYs (no effect on the acceptor / learner path; the shard
             // at instance 0 keeps them).  Only the scalars see such an ACCEPT:
             // its ballot stays in the scan stream as a max_seen-only record.
-            const bool off = member && t != MPX_MSG_E_EPOCH && !(gate >> G_EPOCH_SHIFT);
+            // (member: a batch made while the node has no Proposer, or cut off by a
+            // marker that resets it, is killed on the device — k_gate_votes)
             bool drop = ns.part[k] != 0 || (t == MPX_MSG_COMMIT_REPLY && sb != 0);
             int64_t vote_j = -1;
             if (t == MPX_MSG_P_START) {
-                if (!off) live.clear();
-            } else if (t == MPX_MSG_E_EPOCH) {
-                if (gate & G_PRECLR) live.clear();
+                live.clear();
             } else if (t == MPX_MSG_P_BATCH) {
                 if (drop) live.erase(ns.aux[k]);
-                else if (!off) live[ns.aux[k]] = (uint32_t)ht.b_msg.size();
+                else live[ns.aux[k]] = (uint32_t)ht.b_msg.size();
             } else if (t == MPX_MSG_ACCEPT_REPLY) {
-                auto it = off ? live.end() : live.find(ns.aux[k]);
+                auto it = live.find(ns.aux[k]);
                 if (it == live.end()) drop = true;   // stale, or its batch is another shard's
                 else vote_j = it->second;
             }
             if (drop) {
                 ++ht.dropped;
                 if (ns.part[k] != 0) ++ht.part_dropped;
-                if (t == MPX_MSG_ACCEPT && (!member || (gate & G_SEG))) {
-                    const uint64_t key = ns.ballot[k] | (member ? (uint64_t)(gate & G_SEG) << SEG_SHIFT : 0);
-                    if (last_virtual) ht.sc_key.back() = std::max(ht.sc_key.back(), key);
-                    else { ht.sc_type.push_back(SC_SONLY); ht.sc_key.push_back(key); ht.sc_idx.push_back(0); }
+                if (t == MPX_MSG_ACCEPT && member) {
+                    // member: the device gates it and adds the incarnation (k_gate_scan),
+                    // so it is kept on its own with its version and position
+                    ht.sc_type.push_back(SC_SONLY | SC_VIRT); ht.sc_key.push_back(ns.ballot[k]);
+                    ht.sc_idx.push_back(g); ht.sc_ver.push_back(ns.ver[k]);
+                    last_virtual = false;
+                } else if (t == MPX_MSG_ACCEPT) {
+                    if (last_virtual) ht.sc_key.back() = std::max(ht.sc_key.back(), ns.ballot[k]);
+                    else { ht.sc_type.push_back(SC_SONLY); ht.sc_key.push_back(ns.ballot[k]); ht.sc_idx.push_back(0); }
                     last_virtual = true;
                 }
                 continue;
             }
-            if (member) ht.m_gate.push_back(gate);
+            if (member) {
+                ht.m_ver.push_back(ns.ver[k]);
+                if (t == MPX_MSG_E_EPOCH) ht.ee_msg.push_back(g);
+            }
             ht.m_seq.push_back((uint32_t)k);
             if (vote_j >= 0) reps[vote_j].push_back(g);
             uint64_t ent = ns.ent[k];
@@ -709,17 +699,15 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                 int sct = -1;
                 uint64_t key = ns.ballot[k];
                 if (member) {
-                    if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && (gate & G_SEG)) {
+                    // keys / types finished on the device (k_gate_scan): the raw ballot here
+                    if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
                         sct = t == MPX_MSG_PREPARE ? SC_PREP : SC_ACC;
-                        key |= (uint64_t)(gate & G_SEG) << SEG_SHIFT;
-                        if (badsrc) { f0 |= F_BADNODE; sct |= SC_BAD; }
+                        if (badsrc) sct |= SC_BAD;
                     } else if (t == MPX_MSG_E_EPOCH) {
                         sct = SC_PS;
-                        key = (uint64_t)(gate & G_SEG) << SEG_SHIFT;
-                        f0 = (uint8_t)(((gate & G_ACCCLR) ? F_ACCCLR : 0) | ((gate & G_PRECLR) ? F_PRECLR : 0));
-                    } else if (t == MPX_MSG_COMMIT) {
-                        f0 = (gate & G_PROP) ? F_PROP : 0;
-                        if (badsrc) { f0 |= F_BADNODE; sct = SC_NONE | SC_BAD; }
+                        key = 0;
+                    } else if (t == MPX_MSG_COMMIT && badsrc) {
+                        f0 = F_BADNODE; sct = SC_NONE | SC_BAD;
                     }
                 } else if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
                     sct = t == MPX_MSG_PREPARE ? SC_PREP : SC_ACC;
@@ -732,6 +720,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                 ht.m_flags0.push_back(f0);
                 if (sct >= 0) {
                     ht.sc_type.push_back((uint8_t)sct); ht.sc_key.push_back(key); ht.sc_idx.push_back(g);
+                    if (member) ht.sc_ver.push_back(ns.ver[k]);
                     last_virtual = false;
                 }
             }
@@ -784,13 +773,11 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                 for (uint64_t b : round_b) add_ev(b);
                 clear_round();
             } else if (t == MPX_MSG_E_EPOCH) {
-                if (gate & G_ACCCLR) {
-                    for (uint64_t b = 0; (int64_t)b <= maxb; ++b)
-                        if (first_frag[b] < g) add_ev(b);
-                } else {
-                    for (uint64_t b : round_b) add_ev(b);
-                }
-                if (gate & G_PRECLR) clear_round();
+                // the marker may delete / recreate the Acceptor or reset the Proposer
+                // (decided on the device): every bucket with state of the node gets the
+                // event (round buckets included), and the round stays listed
+                for (uint64_t b = 0; (int64_t)b <= maxb; ++b)
+                    if (first_frag[b] < g) add_ev(b);
             }
             if (t == MPX_MSG_P_BATCH) {
                 const uint32_t j = (uint32_t)ht.b_msg.size() - 1;
@@ -805,6 +792,12 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     }
     ht.node_off[N] = ht.m_type.size();
     sc_off[N] = ht.sc_type.size();
+    if (member) {
+        ht.ee_off[N] = ht.ee_msg.size();
+        ht.sc_off = sc_off;
+        for (uint32_t n = 0; n < N; ++n)       // the device incarnation (G_SEG) counts at most one per marker
+            if (ht.ee_off[n + 1] - ht.ee_off[n] >= G_SEG) return MPX_E_RANGE;
+    }
 
     // vote lists (attributed in the walk above)
     {
@@ -818,7 +811,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         for (size_t r = 0; r < ht.b_rep.size(); ++r) {
             const uint32_t g = ht.b_rep[r];
             ht.b_rbal[r] = ht.m_ballot[g];
-            ht.b_rsrc[r] = std::min<uint32_t>(ht.m_src[g], 0xFFFF) | (member ? (ht.m_gate[g] >> G_EPOCH_SHIFT) << 16 : 0);
+            ht.b_rsrc[r] = std::min<uint32_t>(ht.m_src[g], 0xFFFF);   // member: epoch bits added on the device
         }
         ht.b_bal.resize(ht.b_msg.size());
         for (size_t j = 0; j < ht.b_msg.size(); ++j) ht.b_bal[j] = ht.b_pstart[j] == NONE32 ? 0 : ht.m_ballot[ht.b_pstart[j]];

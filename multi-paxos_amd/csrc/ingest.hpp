@@ -57,7 +57,7 @@ struct HostTrace {
     uint32_t N = 0, NB = 0;
     uint64_t shard_begin = 0, shard_len = 0;
     std::vector<uint8_t> m_type;
-    std::vector<uint32_t> m_src, m_cnt, m_node, m_gate;
+    std::vector<uint32_t> m_src, m_cnt, m_node;
     std::vector<uint64_t> m_ballot, m_aux, m_ent;
     std::vector<uint64_t> node_off;
     std::vector<uint32_t> m_seq;                    // record index in its node's submitted stream
@@ -68,7 +68,12 @@ struct HostTrace {
     std::vector<uint8_t> sc_type;                   // header-scan stream (mpx_internal.hpp SC_*)
     std::vector<uint64_t> sc_key;
     std::vector<uint32_t> sc_idx;
-    std::vector<uint8_t> m_flags0;                  // static message flags (bad source, member role gates)
+    std::vector<uint8_t> m_flags0;                  // static message flags (bad source)
+    // member semantics (gated on the device, kernels.hip k_gate_*): per message its
+    // version (PREPARE / ACCEPT) or epoch (E_EPOCH); per node its E_EPOCH messages;
+    // per scan record its version; per node its scan-stream range
+    std::vector<uint32_t> m_ver, ee_msg, sc_ver;
+    std::vector<uint64_t> ee_off, sc_off;
     std::vector<uint64_t> e_val, e_iid, e_pid, r_pid, r_val, r_iid, g_a, g_b;
     std::vector<uint8_t> e_slot, r_slot;
     bool any_sparse = false;

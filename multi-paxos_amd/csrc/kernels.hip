@@ -135,6 +135,136 @@ __device__ inline uint64_t wave_max(uint64_t x)
     return x;
 }
 
+// ------------------------------------------------- member role gates ----
+// NodeImpl::ChangeMemberships (member/paxos.cpp:1864-1964) as it reaches each
+// node's stream: an E_EPOCH marker moves the node to epochs[x].  The gate of a
+// record follows from the node's roles after the last marker before it —
+//   PREPARE / ACCEPT: the acceptor incarnation when the node has an Acceptor and
+//     the message carries its version (Loop :749-756, :1702,1744), else 0 (dropped);
+//   LEARN: G_PROP when it has a Proposer (Proposer::OnLearn's check, :1398);
+//   replies / P_START / P_BATCH: (epoch + 1) << 16 when it has a Proposer;
+// a marker itself: the new incarnation (bumped when the acceptor role flips:
+// the Acceptor is deleted, :1952-1957, or created, :1897-1901) | G_ACCCLR on that
+// flip | G_PRECLR when the Proposer is deleted, created or sees a new acceptor
+// set (AcceptorsChanged, :1504-1549).  Four passes at the head of every member run.
+__device__ inline uint32_t ee_genesis(const DevView &v, uint32_t n)
+{
+    return (1u << EE_SEG_SHIFT) | (((v.ep_amask[0] >> n) & 1) ? EE_ACC : 0) | (((v.ep_pmask[0] >> n) & 1) ? EE_PROP : 0);
+}
+
+// the node's roles before message g (the state after its last marker < g)
+__device__ inline uint32_t ee_before(const DevView &v, uint32_t n, uint32_t g)
+{
+    uint64_t lo = v.ee_off[n], hi = v.ee_off[n + 1];
+    while (lo < hi) {                                   // first marker >= g
+        const uint64_t mid = (lo + hi) >> 1;
+        if (v.ee_msg[mid] < g) lo = mid + 1; else hi = mid;
+    }
+    return lo > v.ee_off[n] ? v.ee_state[lo - 1] : ee_genesis(v, n);
+}
+
+// pass 1: one lane per node walks its markers in order (few: one per membership step)
+__global__ __launch_bounds__(64) void k_gate_epochs(DevView v)
+{
+    const uint32_t n = blockIdx.x * 64 + threadIdx.x;
+    if (n >= v.N) return;
+    uint32_t st = ee_genesis(v, n);
+    for (uint64_t k = v.ee_off[n]; k < v.ee_off[n + 1]; ++k) {
+        const uint32_t g = v.ee_msg[k], x = v.m_ver[g], ep = st & 0xFFFF;
+        uint32_t seg = (st >> EE_SEG_SHIFT) & G_SEG;
+        const bool acc = st & EE_ACC, prop = st & EE_PROP;
+        const bool a2 = (v.ep_amask[x] >> n) & 1, p2 = (v.ep_pmask[x] >> n) & 1;
+        uint32_t gate = 0;
+        if (a2 != acc) { ++seg; gate |= G_ACCCLR; }
+        if (p2 != prop || (p2 && v.ep_amask[x] != v.ep_amask[ep])) gate |= G_PRECLR;
+        v.m_gate[g] = gate | seg;
+        v.m_flags[g] = (uint8_t)(((gate & G_ACCCLR) ? F_ACCCLR : 0) | ((gate & G_PRECLR) ? F_PRECLR : 0));
+        st = x | (seg << EE_SEG_SHIFT) | (a2 ? EE_ACC : 0) | (p2 ? EE_PROP : 0);
+        v.ee_state[k] = st;
+    }
+}
+
+// pass 2: every other record of the trace
+__global__ __launch_bounds__(256) void k_gate_msgs(DevView v)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= v.num_msgs) return;
+    const uint8_t t = v.m_type[g];
+    if (t == MPX_MSG_E_EPOCH) return;
+    const uint32_t n = v.m_node[g];
+    const uint32_t st = ee_before(v, n, (uint32_t)g), ep = st & 0xFFFF;
+    const bool acc = st & EE_ACC, prop = st & EE_PROP;
+    uint32_t gate = 0;
+    if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
+        gate = acc && v.m_ver[g] == v.ep_ver[ep] ? (st >> EE_SEG_SHIFT) & G_SEG : 0;
+    } else if (t == MPX_MSG_COMMIT) {
+        gate = prop ? G_PROP : 0;
+        if (prop) v.m_flags[g] |= F_PROP;
+    } else if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_ACCEPT_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_P_BATCH) {
+        gate = prop ? (ep + 1) << G_EPOCH_SHIFT : 0;
+    }
+    v.m_gate[g] = gate;
+}
+
+// pass 3: the header-scan stream — a PREPARE / ACCEPT of a node without an
+// Acceptor of its version leaves the stream (SC_NONE), the others (and the
+// left-out ACCEPTs of header sharding, SC_VIRT) take the incarnation in their key,
+// so one prefix max restarts with every new Acceptor; a marker's key is its
+// incarnation.  Idempotent (a rerun finds the same keys and types).
+__global__ __launch_bounds__(256) void k_gate_scan(DevView v, uint64_t num_sc)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= num_sc) return;
+    const uint8_t t = v.sc_type[i];
+    const uint32_t kind = t & SC_KIND;
+    if (kind == SC_PS) {
+        v.sc_key[i] = (uint64_t)(v.m_gate[v.sc_idx[i]] & G_SEG) << SEG_SHIFT;
+        return;
+    }
+    if (!(kind == SC_PREP || kind == SC_ACC || (kind == SC_SONLY && (t & SC_VIRT)))) return;
+    const uint32_t g = v.sc_idx[i];
+    uint32_t n;
+    if (t & SC_VIRT) {                                  // the node whose scan range holds i
+        uint32_t lo = 0, hi = v.N;
+        while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (v.sc_off[mid] <= i) lo = mid; else hi = mid; }
+        n = lo;
+    } else {
+        n = v.m_node[g];
+    }
+    const uint32_t st = ee_before(v, n, g), ep = st & 0xFFFF;
+    if ((st & EE_ACC) && v.sc_ver[i] == v.ep_ver[ep])
+        v.sc_key[i] = (v.sc_key[i] & LOW56) | ((uint64_t)((st >> EE_SEG_SHIFT) & G_SEG) << SEG_SHIFT);
+    else
+        v.sc_type[i] = SC_NONE;                         // dropped silently (:1702,1744)
+}
+
+// pass 4: vote lists — a reply counts only while its node has a Proposer
+// (epoch bits beside the list) and only for a batch made while it had one and
+// not reset since (a marker with G_PRECLR clears accepting_values_)
+__global__ __launch_bounds__(256) void k_gate_votes(DevView v)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= v.num_batches) return;
+    const uint32_t g0 = v.b_msg[j], n = v.m_node[g0];
+    uint32_t kill = NONE32;
+    if (!(v.m_gate[g0] >> G_EPOCH_SHIFT)) {
+        kill = g0;
+    } else {
+        uint64_t lo = v.ee_off[n], hi = v.ee_off[n + 1];
+        while (lo < hi) {                               // first marker after the batch
+            const uint64_t mid = (lo + hi) >> 1;
+            if (v.ee_msg[mid] < g0) lo = mid + 1; else hi = mid;
+        }
+        for (; lo < v.ee_off[n + 1]; ++lo)
+            if (v.m_gate[v.ee_msg[lo]] & G_PRECLR) { kill = v.ee_msg[lo]; break; }
+    }
+    for (uint64_t r = v.b_rep_off[j]; r < v.b_rep_off[j + 1]; ++r) {
+        const uint32_t g = v.b_rep[r];
+        const uint32_t ep = g < kill ? v.m_gate[g] >> G_EPOCH_SHIFT : 0;
+        v.b_rsrc[r] = (v.b_rsrc[r] & 0xFFFF) | (ep << 16);
+    }
+}
+
 constexpr uint32_t SCAN_ROUNDS = SCAN_CHUNK / 256;   // rounds of 64 records per wave
 
 // Chunk aggregates over the header-scan stream: max of the PREPARE ids and of
@@ -486,6 +616,7 @@ __global__ __launch_bounds__(256) void k_votes(DevView v)
         const uint32_t a = x & 0xFFFF;
         uint64_t am;
         if (member) {
+            if (!(x >> 16)) continue;                    // no Proposer, or its batch was cleared (k_gate_votes)
             am = v.ep_amask[(x >> 16) - 1];              // the node's acceptors at the reply (:1324-1327)
         } else {
             if (b != ballot) continue;                   // :1408
@@ -2065,6 +2196,13 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (2ull * v.N > reset_n) reset_n = 2ull * v.N;
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, s);
     hipLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s, v, n_partials);
+    if (v.semantics == MPX_SEM_MEMBER) {
+        // member role / version gates from the E_EPOCH markers (k_gate_*)
+        hipLaunchKernelGGL(k_gate_epochs, dim3(cdiv(v.N, 64)), dim3(64), 0, s, v);
+        if (v.num_msgs) hipLaunchKernelGGL(k_gate_msgs, dim3(cdiv(v.num_msgs, 256)), dim3(256), 0, s, v);
+        if (v.num_sc) hipLaunchKernelGGL(k_gate_scan, dim3(cdiv(v.num_sc, 256)), dim3(256), 0, s, v, v.num_sc);
+        if (v.num_batches) hipLaunchKernelGGL(k_gate_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
+    }
     if (v.num_chunks) {
         hipLaunchKernelGGL(k_scan_chunk, dim3(v.num_chunks), dim3(256), 0, s, v);
         if (v.scan_node_pass) hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);   // long node streams

@@ -67,14 +67,14 @@ enum : uint8_t {
     F_COUNTED = 4,    // PREPARE_REPLY merged into pre_accepted (paxos.cpp:1038-1045)
     F_QUORUM = 8,     // PREPARE_REPLY that reached the promise quorum (paxos.cpp:1047)
     F_BADNODE = 16,
-    // member semantics (copied from m_gate by the header scan)
+    // member semantics (set by k_gate_epochs / k_gate_msgs from the E_EPOCH markers)
     F_ACCCLR = 32,    // E_EPOCH: the node's Acceptor is deleted or recreated (member/paxos.cpp:1897-1901,1952-1957)
     F_PRECLR = 64,    // E_EPOCH: its Proposer is deleted, created or sees new acceptors (idle)
     F_PROP = 128      // LEARN: the node has a Proposer (Proposer::OnLearn's ASSERT, :1398)
 };
 
-// member semantics: per-message role / version gate, computed at ingest from
-// the E_EPOCH markers and the epoch table (include/mpx.h):
+// member semantics: per-message role / version gate, computed on the device
+// (kernels.hip k_gate_*) from the E_EPOCH markers and the epoch table (include/mpx.h):
 //   PREPARE / ACCEPT : acceptor incarnation (1..255) when the node has an
 //                      Acceptor of the message's version, 0 = dropped
 //                      (Loop :749-756, version filter :1702,1744)
@@ -85,6 +85,8 @@ enum : uint8_t {
 // The header scan runs over (incarnation << 56 | ballot), so one prefix max
 // restarts at every new Acceptor; member ballots must stay below 2^56.
 enum : uint32_t { G_SEG = 0xFF, G_ACCCLR = 1u << 8, G_PRECLR = 1u << 9, G_PROP = 1u << 10, G_EPOCH_SHIFT = 16 };
+// ee_state: epoch (low 16 bits) | incarnation << 16 | acceptor << 24 | proposer << 25
+enum : uint32_t { EE_SEG_SHIFT = 16, EE_ACC = 1u << 24, EE_PROP = 1u << 25 };
 constexpr uint64_t SEG_SHIFT = 56;
 constexpr uint64_t LOW56 = (1ull << 56) - 1;
 
@@ -101,7 +103,8 @@ enum : uint8_t {
     SC_PS = 3,        // p = s = key (member E_EPOCH: a new Acceptor incarnation)
     SC_NONE = 4,      // no contribution (a COMMIT with a bad source)
     SC_KIND = 7,
-    SC_BAD = 8        // the record's source is not a node: F_BADNODE + violation
+    SC_BAD = 8,       // the record's source is not a node: F_BADNODE + violation
+    SC_VIRT = 16      // member: a left-out ACCEPT (header sharding), sc_idx = the next kept message
 };
 
 // fragment kinds (Frag::flags >> 4)
@@ -177,13 +180,22 @@ struct DevView {
     uint8_t *m_flags;
     uint64_t *m_maxseen;
     // member semantics
-    const uint32_t *m_gate;         // per message, see G_*
+    uint32_t *m_gate;               // per message, see G_* (written by k_gate_*)
     const uint64_t *e_pid;          // per ACCEPT / LEARN entry: its proposal id
     const uint64_t *ep_amask;       // per epoch: acceptor set
+    const uint64_t *ep_pmask;       // per epoch: proposer set
+    const uint32_t *ep_ver;         // per epoch: NodeImpl::version_
     uint32_t num_epochs;
+    const uint32_t *m_ver;          // per message: PREPARE / ACCEPT version, E_EPOCH epoch
+    const uint64_t *ee_off;         // N + 1: each node's E_EPOCH messages in ee_msg
+    const uint32_t *ee_msg;
+    uint32_t *ee_state;             // per marker: the node's roles after it (k_gate_epochs, EE_*)
+    const uint32_t *sc_ver;         // per scan record: its message's version
+    const uint64_t *sc_off;         // N + 1: each node's scan-stream range
+    uint64_t num_sc;                // scan records
     // header scan over the scan stream (SC_*): chunks of SCAN_CHUNK records per node
-    const uint8_t *sc_type;
-    const uint64_t *sc_key;
+    uint8_t *sc_type;               // member: types / keys finished by k_gate_scan
+    uint64_t *sc_key;
     const uint32_t *sc_idx;         // global message index of the record
     uint32_t num_chunks;
     const uint32_t *chunk_node;
@@ -227,7 +239,7 @@ struct DevView {
     const uint64_t *b_rep_off;
     const uint32_t *b_rep;
     const uint64_t *b_rbal;         // per vote-list entry: the reply's ballot
-    const uint32_t *b_rsrc;         // ... its acceptor (low 16 bits, clamped) | member: (epoch + 1) << 16
+    uint32_t *b_rsrc;               // ... its acceptor (low 16 bits, clamped) | member: (epoch + 1) << 16 (k_gate_votes)
     const uint64_t *b_bal;          // per batch: the ballot of its proposer round (0: none)
     uint32_t *b_chosen;             // global msg index of the quorum reply, NONE32
     const uint64_t *cf_off;         // NB+1
