@@ -414,10 +414,12 @@ static int upload_trace(mpx_engine *e)
                 mx = std::max<uint64_t>(mx, h.f_off[q + 1] - h.f_off[q]);
                 for (uint64_t f = h.f_off[q]; f < h.f_off[q + 1]; ++f) pre += (h.frags[f].flags >> 4) == K_PREPLY;
             }
-            std::fprintf(stderr, "[mpx] pairs %llu, general %zu: runs %llu (promise-reply runs %llu, max/pair %llu), "
-                         "events %llu; all runs %zu, messages %zu\n", (unsigned long long)((uint64_t)h.N * h.NB),
-                         h.gp_list.size(), (unsigned long long)fr, (unsigned long long)pre, (unsigned long long)mx,
-                         (unsigned long long)ev, h.frags.size(), h.m_type.size());
+            uint64_t sfr = 0;
+            for (uint64_t i = 0; i < h.num_gp_simple; ++i) sfr += h.f_off[h.gp_list[i] + 1] - h.f_off[h.gp_list[i]];
+            std::fprintf(stderr, "[mpx] pairs %llu, general %zu (simple %llu, their runs %llu): runs %llu (promise-reply runs %llu, "
+                         "max/pair %llu), events %llu; all runs %zu, messages %zu\n", (unsigned long long)((uint64_t)h.N * h.NB),
+                         h.gp_list.size(), (unsigned long long)h.num_gp_simple, (unsigned long long)sfr, (unsigned long long)fr,
+                         (unsigned long long)pre, (unsigned long long)mx, (unsigned long long)ev, h.frags.size(), h.m_type.size());
         }
     }
     TRY(upload(e->ev_off, h.ev_off, s)); TRY(upload(e->ev_msg, h.ev_msg, s)); TRY(upload(e->ev_aux, h.ev_aux, s));
@@ -449,7 +451,7 @@ static int upload_trace(mpx_engine *e)
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
     e->num_frags = h.frags.size();
-    v.num_gp = h.gp_list.size(); v.gp_list = e->gp_list.as<uint64_t>();
+    v.num_gp = h.gp_list.size(); v.gp_list = e->gp_list.as<uint64_t>(); v.num_gp_simple = h.num_gp_simple;
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>(); v.ev_aux = e->ev_aux.as<uint64_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
     v.num_batches = (uint32_t)h.b_msg.size();
@@ -1375,7 +1377,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
     e->num_frags = f_off[N * NB];
-    v.num_gp = gd.size() / GP_WORDS; v.gp_list = e->gp_list.as<uint64_t>();
+    v.num_gp = gd.size() / GP_WORDS; v.gp_list = e->gp_list.as<uint64_t>(); v.num_gp_simple = 0;
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>(); v.ev_aux = e->ev_aux.as<uint64_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
     v.num_batches = (uint32_t)K;

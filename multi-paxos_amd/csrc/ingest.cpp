@@ -759,10 +759,13 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                     for (uint64_t b = lo; b < hi; ++b) {
                         if (first_frag[b] >= g) continue;
                         if (!evp.empty() && evp.back().second == g && b == last_b && evp.back().first == b * N + n) {
-                            evx.back() += 1ull << 32;
+                            evx.back() = (evx.back() + (1ull << 32)) & ~EVX_ONE;   // a second range: no interval
                         } else if (evp.empty() || evp.back().second != g || b > last_b) {
                             add_ev(b);
-                            evx.back() = (ent + r) | (1ull << 32);
+                            // one range so far: its bucket-local interval too (k_apply needs no range loads)
+                            const uint64_t blo = sb + (b << BSH);
+                            const uint64_t il = std::max(a, blo) - blo, ih = std::min(e, blo + BS) - blo;
+                            evx.back() = (ent + r) | (1ull << 32) | (il << 40) | (ih << 49) | EVX_ONE;
                             last_b = b;
                         }
                     }
@@ -874,6 +877,19 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             }
             if (!fast) { ht.gp_list.push_back(p); ht.pair_gp[p] = 1; }
         }
+    // work-list order: the pairs with no snapshot events and no promise-reply runs
+    // first (multi: k_apply's SIMPLE instantiation takes them), pair order kept
+    ht.num_gp_simple = 0;
+    if (!member) {
+        auto simple = [&](uint64_t p) {
+            if (ht.pair_ev[p]) return false;
+            for (uint64_t f = ht.f_off[p]; f < ht.f_off[p + 1]; ++f)
+                if ((ht.frags[f].flags >> 4) == K_PREPLY) return false;
+            return true;
+        };
+        auto mid = std::stable_partition(ht.gp_list.begin(), ht.gp_list.end(), simple);
+        ht.num_gp_simple = (uint64_t)(mid - ht.gp_list.begin());
+    }
     // slots for sparse fragments
     if (ht.any_sparse) {
         ht.e_slot.resize(ht.e_iid.size());

@@ -1478,8 +1478,12 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
 // DIGEST: the digested verification run (mpx_run) — the only user of the slot's ballot
 // MEMBER: member semantics (insert-first apply, epoch events) — compiled apart so
 // the multi kernel carries none of it
-template <int WAVES_PER_EU, bool DIGEST, bool MEMBER>
-__global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
+// SIMPLE: work items [it0, it1) are pairs with no snapshot events and no
+// promise-reply runs (ingest.cpp lists them first): the walk is ACCEPT / COMMIT
+// runs only, compiled without the event / merge / emission code, so the kernel
+// holds fewer registers and more waves per SIMD hide the descriptor latency
+template <int WAVES_PER_EU, bool DIGEST, bool MEMBER, bool SIMPLE = false>
+__global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t it0, uint64_t it1)
 {
     __shared__ uint16_t lidx_all[4][BS];
     __shared__ u64x2 pre_all[4][BS];           // pre-accepted merge (pid, PRESENT | r-entry): rare, kept in LDS
@@ -1503,18 +1507,19 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
     // item's CSR ranges three items ahead, (2) its first descriptor window two
     // ahead, (3) that window's scan flags one ahead — one wait per item.
     auto rt1 = [&](uint64_t i) -> uint64_t {
-        if (i >= v.num_gp || lane > 4) return 0;
+        if (i >= it1 || lane > 4) return 0;
         return v.gp_list[GP_WORDS * i + lane];          // lanes 0..4: fi, fe, ei, ee, q
     };
-    struct Win { uint64_t fw0, fw1; uint32_t evm; };
+    // the event window carries each event's aux word (PREPARE: its ranges in the bucket)
+    struct Win { uint64_t fw0, fw1; uint32_t evm; uint64_t eax; };
     auto rt2 = [&](uint64_t off) -> Win {
-        Win w{0, NONE32, NONE32};
+        Win w{0, NONE32, NONE32, 0};
         const uint64_t fi = rl64(off, 0), fe = rl64(off, 1), ei = rl64(off, 2), ee = rl64(off, 3);
         if (lane < fe - fi && lane < 64) {
             const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
             w.fw0 = x.x; w.fw1 = x.y;
         }
-        if (lane < ee - ei && lane < 64) w.evm = v.ev_msg[ei + lane];
+        if (!SIMPLE && lane < ee - ei && lane < 64) { w.evm = v.ev_msg[ei + lane]; w.eax = v.ev_aux[ei + lane]; }
         return w;
     };
     struct Flg { uint32_t fflag, einfo; uint64_t fbal; };
@@ -1524,14 +1529,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
             f.fflag = v.m_flags[(uint32_t)w.fw1];
             if (DIGEST) f.fbal = v.m_ballot[(uint32_t)w.fw1];
         }
-        if (w.evm != NONE32) f.einfo = (uint32_t)v.m_type[w.evm] | ((uint32_t)v.m_flags[w.evm] << 8);
+        if (!SIMPLE && w.evm != NONE32) f.einfo = (uint32_t)v.m_type[w.evm] | ((uint32_t)v.m_flags[w.evm] << 8);
         return f;
     };
-    uint64_t it = (uint64_t)blockIdx.x * 4 + wv;
+    uint64_t it = it0 + (uint64_t)blockIdx.x * 4 + wv;
     uint64_t off0 = rt1(it), off1 = rt1(it + stride), off2 = rt1(it + 2 * stride);
     Win win0 = rt2(off0), win1 = rt2(off1);
     Flg flg0 = rt3(win0);
-    for (; it < v.num_gp; it += stride) {
+    for (; it < it1; it += stride) {
         const uint64_t off_c = off0;
         const Win win = win0;
         const Flg flg = flg0;
@@ -1550,27 +1555,27 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
 #define SF(j) ((sfl >> (8 * (j))) & 0xFF)
 #define SF_SET(j, x) (sfl = (sfl & ~(0xFFu << (8 * (j)))) | ((uint32_t)(x) << (8 * (j))))
 #pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) { if (DIGEST) sb[j] = 0; se[j] = sm[j] = 0; pre[lane + 64 * j] = u64x2{0, 0}; }
+        for (uint32_t j = 0; j < SPL; ++j) { if (DIGEST) sb[j] = 0; se[j] = sm[j] = 0; if (!SIMPLE) pre[lane + 64 * j] = u64x2{0, 0}; }
 
         bool first = true;
         while (fi < fe || ei < ee) {
             const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
-            const uint32_t ne = (uint32_t)(ee - ei < 64 ? ee - ei : 64);
+            const uint32_t ne = SIMPLE ? 0 : (uint32_t)(ee - ei < 64 ? ee - ei : 64);
             // descriptors (one per lane) and their scan flags: the pipelined
             // first window, then loaded here for the rare longer pairs
-            uint64_t fw0 = win.fw0, fw1 = win.fw1;
+            uint64_t fw0 = win.fw0, fw1 = win.fw1, eax = win.eax;
             uint32_t evm = win.evm;
             uint32_t fflag = flg.fflag, einfo = flg.einfo;
             uint64_t fbal = flg.fbal;
             if (!first) {
-                Win w2{0, NONE32, NONE32};
+                Win w2{0, NONE32, NONE32, 0};
                 if (lane < nf) {
                     const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
                     w2.fw0 = x.x; w2.fw1 = x.y;
                 }
-                if (lane < ne) w2.evm = v.ev_msg[ei + lane];
+                if (!SIMPLE && lane < ne) { w2.evm = v.ev_msg[ei + lane]; w2.eax = v.ev_aux[ei + lane]; }
                 const Flg f2 = rt3(w2);
-                fw0 = w2.fw0; fw1 = w2.fw1; evm = w2.evm;
+                fw0 = w2.fw0; fw1 = w2.fw1; evm = w2.evm; eax = w2.eax;
                 fflag = f2.fflag; einfo = f2.einfo; fbal = f2.fbal;
             }
             first = false;
@@ -1643,7 +1648,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                                 }
                                 ++cL;
                             }
-                    } else if (kind == K_PREPLY) {
+                    } else if (!SIMPLE && kind == K_PREPLY) {
                         if ((mf & F_COUNTED) && !(v.knobs & 8192)) {       // knob 8192: experiment, no merge
 #pragma unroll 1
                             for (uint32_t j = 0; j < SPL; ++j)
@@ -1655,7 +1660,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                         }
                     }
                     ++a;
-                } else {
+                } else if (!SIMPLE) {
                     const uint32_t g = em;
                     const uint32_t info = rl32(einfo, c);
                     const uint32_t t8 = info & 0xFF, fl = info >> 8;
@@ -1665,23 +1670,30 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v)
                         for (uint32_t j = 0; j < SPL; ++j) have |= (SF(j) & S_PRESENT) != 0;
                         if ((fl & F_GRANTED) && __ballot(have)) {
                             // FilterAcceptedValues over the prepare's ranges (:902-922):
-                            // ingest listed which of them meet this bucket (ev_aux: first
-                            // range | count), loaded one per lane
-                            const uint64_t ax = v.ev_aux[ei + c];
-                            const uint32_t r0 = (uint32_t)ax, nr = (uint32_t)(ax >> 32);
-                            const uint64_t blo = v.shard_begin + li0;
-                            uint64_t la = 0, lb = 0;
-                            if (lane < nr) { la = v.g_a[r0 + lane]; lb = v.g_b[r0 + lane]; }
+                            // ingest listed which of them meet this bucket (ev_aux, in the
+                            // event window: first range | count, or one range's bucket-local
+                            // interval inline — then no range loads at all)
+                            // (knob 131072: A/B against the loaded word and the range loads)
+                            const uint64_t ax = (v.knobs & 131072) ? v.ev_aux[ei + c] & ~EVX_ONE : rl64(eax, c);
                             bool hit[SPL];
+                            if (ax & EVX_ONE) {
+                                const uint32_t il = (uint32_t)(ax >> 40) & 0x1FF, ih = (uint32_t)(ax >> 49) & 0x1FF;
 #pragma unroll
-                            for (uint32_t j = 0; j < SPL; ++j) hit[j] = false;
-                            for (uint32_t r = 0; r < nr; ++r) {
-                                const uint64_t ra = r < 64 ? rl64(la, r) : v.g_a[r0 + r];
-                                const uint64_t rb = r < 64 ? rl64(lb, r) : v.g_b[r0 + r];
+                                for (uint32_t j = 0; j < SPL; ++j) hit[j] = lane + 64 * j >= il && lane + 64 * j < ih;
+                            } else {
+                                const uint32_t r0 = (uint32_t)ax, nr = (uint32_t)(ax >> 32) & 0xFF;
+                                const uint64_t blo = v.shard_begin + li0;
+                                uint64_t la = 0, lb = 0;
+                                if (lane < nr) { la = v.g_a[r0 + lane]; lb = v.g_b[r0 + lane]; }
 #pragma unroll
-                                for (uint32_t j = 0; j < SPL; ++j) {
-                                    const uint64_t iid = blo + lane + 64 * j;
-                                    hit[j] |= iid >= ra && iid < rb;
+                                for (uint32_t j = 0; j < SPL; ++j) hit[j] = false;
+                                for (uint32_t r = 0; r < nr; ++r) {
+                                    const uint64_t ra = rl64(la, r), rb = rl64(lb, r);
+#pragma unroll
+                                    for (uint32_t j = 0; j < SPL; ++j) {
+                                        const uint64_t iid = blo + lane + 64 * j;
+                                        hit[j] |= iid >= ra && iid < rb;
+                                    }
                                 }
                             }
                             uint32_t ref[SPL];
@@ -2218,8 +2230,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (v.semantics == MPX_SEM_MEMBER) {
         // member: every pair walks the general kernel (insert semantics, epoch events)
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-                   else hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v); }
+        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, v.num_gp);
+                   else hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, v.num_gp); }
     } else {
         // multi: the lean kernel also writes the chosen log of clean buckets
         // digest runs (verification) take their own instantiation, so the
@@ -2243,9 +2255,14 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         }
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-                   else if (g.variant == 4) hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-                   else hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); }
+        // the event- and merge-free pairs first (k_apply<..., SIMPLE>), then the rest;
+        // knob 65536: one kernel over the whole list (A/B)
+        const uint64_t ns = (v.knobs & 65536) ? 0 : v.num_gp_simple;
+        if (ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
+                  else hipLaunchKernelGGL((k_apply<1, false, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
+        if (v.num_gp > ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp);
+                   else if (g.variant == 4) hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp);
+                   else hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp); }
     }
     if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);

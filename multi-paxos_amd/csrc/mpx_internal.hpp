@@ -46,6 +46,7 @@ constexpr uint32_t PROP_CHUNK = 2048;        // promise-quorum chunk (pl records
 // per node) up to this many chunks per node; longer streams take k_scan_node
 constexpr uint32_t SCAN_INLINE_CHUNKS = 512;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr uint64_t EVX_ONE = 1ull << 63;     // ev_aux: the PREPARE has one range in the bucket (interval inline)
 
 constexpr uint64_t W_PRESENT = 1ull << 63;
 constexpr uint64_t W_COMMITTED = 1ull << 62;
@@ -218,6 +219,7 @@ struct DevView {
     const uint64_t *f_off;          // N*NB+1, pair q = bucket * N + node
     const Frag *frags;
     uint64_t num_gp;                // pairs for the general apply kernel
+    uint64_t num_gp_simple;         // ... the first of them: no snapshot events, no promise-reply runs (multi)
     const uint64_t *gp_list;        // general-apply work items, GP_WORDS each: the pair's fragment CSR
                                     // range, its event CSR range, the pair q (one coalesced load per item)
     const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
@@ -230,6 +232,7 @@ struct DevView {
     uint32_t *pc_head;
     uint64_t *pc_state;             // 3 words per chunk: ballot, promise mask, preparing | known << 1
     const uint64_t *ev_aux;         // per event: PREPARE: first range (g_a index) meeting the bucket | count << 32
+                                    // (8 bits) | one range: its bucket-local [lo << 40, hi << 49) | EVX_ONE
     const uint64_t *pl_off;         // N+1
     const uint32_t *pl_msg;
     // batches
