@@ -2259,10 +2259,14 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         // knob 65536: one kernel over the whole list (A/B)
         const uint64_t ns = (v.knobs & 65536) ? 0 : v.num_gp_simple;
         if (ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
+                  // (capped at 6 / 8 waves per SIMD: 1.415 / 1.458 vs 1.393 ms general apply, C3 2^24)
                   else hipLaunchKernelGGL((k_apply<1, false, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
         if (v.num_gp > ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp);
-                   else if (g.variant == 4) hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp);
-                   else hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp); }
+                   // 4 waves / SIMD (128 VGPRs, a few spilled) beats the unconstrained 154 VGPRs at 3:
+                   // C3 2^24 general apply 1.394 vs 1.580 ms; 5 and 6 waves spill more (1.87, 2.36 ms);
+                   // variant 1: the unconstrained build (A/B)
+                   else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp);
+                   else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp); }
     }
     if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);

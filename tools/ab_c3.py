@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--log2", type=int, default=22)
     ap.add_argument("--knobs", default="0")
     ap.add_argument("--wgs", default="8")
-    ap.add_argument("--variants", default="0", help="MPX_APPLY_VARIANT values (4: k_apply at 4 waves/SIMD)")
+    ap.add_argument("--variants", default="0", help="MPX_APPLY_VARIANT values (1: the general k_apply unconstrained, 3 waves/SIMD)")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=3)
     a = ap.parse_args()
