@@ -16,6 +16,7 @@ profiles/, where bench.py picks them up as roofline.traffic.
 import argparse
 import csv
 import glob
+import re
 import json
 import os
 import subprocess
@@ -82,7 +83,7 @@ def main():
     # C3 adds the general k_apply of the timed steps
     phase = [v for k, v in out["kernels"].items()
              if "k_plan" in k or "k_store" in k or ("k_apply_fast" in k and "true>" in k and "false" in k)
-             or (a.c3 and "k_apply<" in k and ", false>" in k)]   # not the digested run's <.., true>
+             or (a.c3 and re.search(r"k_apply<\d+, false", k))]   # k_apply<waves, DIGEST, ...>: not the digested run's
     out["apply_phase_kernels"] = [k for k, v in out["kernels"].items() if v in phase]
     out["hbm_bytes_per_launch"] = sum(v["hbm_bytes_per_launch"] for v in phase) if phase else None
     out["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"
