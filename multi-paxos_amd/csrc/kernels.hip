@@ -338,6 +338,7 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
     __shared__ uint64_t l[2][4], lc[2][4];
     __shared__ uint64_t lky[SCAN_CHUNK];        // phase 2 reads its rounds back from LDS,
     __shared__ uint8_t lty[SCAN_CHUNK];         // so the round loop needs few registers
+    __shared__ uint32_t lix[SCAN_CHUNK];        // and no dependent load of the message index per round
     const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
     const uint64_t wb = beg + (uint64_t)w * (SCAN_CHUNK / 4) + lane;
@@ -345,12 +346,13 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
     constexpr bool member = MEMBER;
     uint8_t ty[SCAN_ROUNDS];
     uint64_t ky[SCAN_ROUNDS];
+    uint32_t ix[SCAN_ROUNDS];
     uint64_t lp = 0, ls = 0;
 #pragma unroll
     for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {             // all loads in flight at once
         const uint64_t g = wb + 64 * r;
-        ty[r] = SC_NONE; ky[r] = 0;
-        if (g < end) { ty[r] = v.sc_type[g]; ky[r] = v.sc_key[g]; }
+        ty[r] = SC_NONE; ky[r] = 0; ix[r] = 0;
+        if (g < end) { ty[r] = v.sc_type[g]; ky[r] = v.sc_key[g]; ix[r] = v.sc_idx[g]; }
     }
 #pragma unroll
     for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
@@ -360,6 +362,7 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
         ls = ls > s ? ls : s;
         lty[lb + 64 * r] = ty[r];
         lky[lb + 64 * r] = ky[r];
+        lix[lb + 64 * r] = ix[r];
     }
     // carry-in = max over the node's earlier chunk aggregates (k_scan_chunk),
     // read here from L2 instead of a separate per-node scan kernel
@@ -435,11 +438,11 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
             ls = 0;
             uint64_t x = wave_scan_max(s);
             x = x > cs ? x : cs;
-            if (f & F_REJECT) v.m_maxseen[v.sc_idx[g]] = member ? x & LOW56 : x;
+            if (f & F_REJECT) v.m_maxseen[lix[lb + 64 * r]] = member ? x & LOW56 : x;
         }
         ls = ls > s ? ls : s;
         if (g < end && (kind <= SC_ACC || (t & SC_BAD))) {
-            const uint32_t idx = v.sc_idx[g];
+            const uint32_t idx = lix[lb + 64 * r];
             if (kind <= SC_ACC) v.m_flags[idx] = f | ((t & SC_BAD) ? F_BADNODE : 0);
             if (t & SC_BAD) {
                 const uint32_t n = v.m_node[idx];
@@ -603,7 +606,20 @@ __global__ __launch_bounds__(256) void k_votes(DevView v)
     const uint64_t r0 = v.b_rep_off[j0], r1 = v.b_rep_off[jl];
     const uint64_t rs = have ? v.b_rep_off[j] : r1, re = have ? v.b_rep_off[j + 1] : r1;
     const uint64_t staged = r1 - r0 < VOTE_LDS ? r1 - r0 : VOTE_LDS;
-    for (uint64_t x = lane; x < staged; x += 64) { lbal[wv][x] = v.b_rbal[r0 + x]; lsrc[wv][x] = v.b_rsrc[r0 + x]; }
+    {   // every staging load in flight at once, then the LDS writes
+        constexpr uint32_t K = VOTE_LDS / 64;
+        uint64_t xb[K];
+        uint32_t xs[K];
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint64_t x = lane + 64 * k;
+            xb[k] = 0; xs[k] = 0;
+            if (x < staged) { xb[k] = v.b_rbal[r0 + x]; xs[k] = v.b_rsrc[r0 + x]; }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k)
+            if (lane + 64 * k < staged) { lbal[wv][lane + 64 * k] = xb[k]; lsrc[wv][lane + 64 * k] = xs[k]; }
+    }
     wave_lds_fence();
     const uint64_t ballot = have ? v.b_bal[j] : 0;
     const bool member = v.semantics == MPX_SEM_MEMBER;
@@ -1823,6 +1839,7 @@ __global__ __launch_bounds__(256) void k_reduce(DevView v, uint32_t n_partials)
     __shared__ unsigned long long red[4][8];
     const uint32_t t = threadIdx.x;
     unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 4
     for (uint32_t w = t; w < n_partials; w += 256)
 #pragma unroll
         for (int i = 0; i < 8; ++i) s[i] += v.partials[8 * w + i];
@@ -1855,7 +1872,10 @@ __global__ void k_reset(DevView v, uint32_t n_partials)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t np = (uint64_t)v.N * v.NB;
-    if (i < np) v.st_valid[i] = 0;
+    if (16 * i < np) {                         // st_valid: 16 bytes per thread, byte tail
+        if (16 * i + 16 <= np) *reinterpret_cast<uint4 *>(v.st_valid + 16 * i) = uint4{0, 0, 0, 0};
+        else for (uint64_t k = 16 * i; k < np; ++k) v.st_valid[k] = 0;
+    }
     if (i < v.NB) v.chosen_valid[i] = 0;
     if (i < 8ull * n_partials) v.partials[i] = 0;
     if (i < 2ull * v.N) v.node_scal[i] = 0;    // nodes without messages keep promised = max_seen = 0
@@ -2202,7 +2222,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     void *ev_begin = ev[0], *ev_apply0 = ev[1], *ev_apply1 = ev[2], *ev_general = ev[3], *ev_end = ev[4];
     hipStream_t s = (hipStream_t)stream_;
     const uint32_t n_partials = g.apply_wgs + g.chosen_wgs;
-    uint64_t reset_n = (uint64_t)v.N * v.NB;
+    uint64_t reset_n = ((uint64_t)v.N * v.NB + 15) / 16;
     if (v.NB > reset_n) reset_n = v.NB;
     if (8ull * n_partials > reset_n) reset_n = 8ull * n_partials;
     if (2ull * v.N > reset_n) reset_n = 2ull * v.N;
