@@ -451,7 +451,7 @@ static int upload_trace(mpx_engine *e)
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
     e->num_frags = h.frags.size();
-    v.num_gp = h.gp_list.size(); v.gp_list = e->gp_list.as<uint64_t>(); v.num_gp_simple = h.num_gp_simple;
+    v.num_gp = h.gp_list.size(); v.gp_list = e->gp_list.as<uint64_t>(); v.num_gp_simple = h.num_gp_simple; v.num_gp_snap = h.num_gp_snap;
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>(); v.ev_aux = e->ev_aux.as<uint64_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
     v.num_batches = (uint32_t)h.b_msg.size();
@@ -1377,7 +1377,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
     e->num_frags = f_off[N * NB];
-    v.num_gp = gd.size() / GP_WORDS; v.gp_list = e->gp_list.as<uint64_t>(); v.num_gp_simple = 0;
+    v.num_gp = gd.size() / GP_WORDS; v.gp_list = e->gp_list.as<uint64_t>(); v.num_gp_simple = 0; v.num_gp_snap = 0;
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>(); v.ev_aux = e->ev_aux.as<uint64_t>();
     v.pl_off = e->pl_off.as<uint64_t>(); v.pl_msg = e->pl_msg.as<uint32_t>();
     v.num_batches = (uint32_t)K;

@@ -879,16 +879,19 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         }
     // work-list order: the pairs with no snapshot events and no promise-reply runs
     // first (multi: k_apply's SIMPLE instantiation takes them), pair order kept
-    ht.num_gp_simple = 0;
+    // then those with no promise-reply runs (their events are PREPAREs only; k_apply
+    // AM_SNAP), then the rest (promise rounds)
+    ht.num_gp_simple = ht.num_gp_snap = 0;
     if (!member) {
-        auto simple = [&](uint64_t p) {
-            if (ht.pair_ev[p]) return false;
+        auto no_preply = [&](uint64_t p) {
             for (uint64_t f = ht.f_off[p]; f < ht.f_off[p + 1]; ++f)
                 if ((ht.frags[f].flags >> 4) == K_PREPLY) return false;
             return true;
         };
-        auto mid = std::stable_partition(ht.gp_list.begin(), ht.gp_list.end(), simple);
-        ht.num_gp_simple = (uint64_t)(mid - ht.gp_list.begin());
+        auto mid = std::stable_partition(ht.gp_list.begin(), ht.gp_list.end(), no_preply);
+        ht.num_gp_snap = (uint64_t)(mid - ht.gp_list.begin());
+        auto mid2 = std::stable_partition(ht.gp_list.begin(), mid, [&](uint64_t p) { return !ht.pair_ev[p]; });
+        ht.num_gp_simple = (uint64_t)(mid2 - ht.gp_list.begin());
     }
     // slots for sparse fragments
     if (ht.any_sparse) {

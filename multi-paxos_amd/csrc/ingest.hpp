@@ -81,6 +81,7 @@ struct HostTrace {
     std::vector<Frag> frags;
     std::vector<uint64_t> gp_list;                  // (node, bucket) pairs for the general apply kernel
     uint64_t num_gp_simple = 0;                     // ... the first of them: no events, no promise-reply runs
+    uint64_t num_gp_snap = 0;                       // ... then up to here: no promise-reply runs
     std::vector<uint64_t> ev_off, pl_off;           // ev_off: per (bucket, node) pair (N * NB + 1); pl_off: per node
     std::vector<uint32_t> ev_msg, pl_msg;
     std::vector<uint64_t> ev_aux;                   // per event: PREPARE's first range meeting the bucket | count << 32

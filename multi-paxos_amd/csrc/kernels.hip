@@ -1494,11 +1494,15 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
 // DIGEST: the digested verification run (mpx_run) — the only user of the slot's ballot
 // MEMBER: member semantics (insert-first apply, epoch events) — compiled apart so
 // the multi kernel carries none of it
-// SIMPLE: work items [it0, it1) are pairs with no snapshot events and no
-// promise-reply runs (ingest.cpp lists them first): the walk is ACCEPT / COMMIT
-// runs only, compiled without the event / merge / emission code, so the kernel
-// holds fewer registers and more waves per SIMD hide the descriptor latency
-template <int WAVES_PER_EU, bool DIGEST, bool MEMBER, bool SIMPLE = false>
+// MODE (multi): which work items [it0, it1) the instantiation takes — ingest.cpp
+// orders the list: AM_SIMPLE pairs (no snapshot events, no promise-reply runs:
+// ACCEPT / COMMIT runs only), then AM_SNAP pairs (no promise-reply runs, so their
+// only events are PREPAREs: snapshots), then AM_FULL (promise rounds: merges, round
+// resets, quorum emission).  The narrower ones are compiled without the code they
+// never run, so they hold fewer registers and more waves per SIMD hide the
+// descriptor latency.
+enum { AM_FULL = 0, AM_SIMPLE = 1, AM_SNAP = 2 };
+template <int WAVES_PER_EU, bool DIGEST, bool MEMBER, int MODE = AM_FULL>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t it0, uint64_t it1)
 {
     __shared__ uint16_t lidx_all[4][BS];
@@ -1507,6 +1511,8 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint16_t *lidx = lidx_all[wv];
     u64x2 *pre = pre_all[wv];
+    constexpr bool SIMPLE = MODE == AM_SIMPLE;   // no events at all
+    constexpr bool ROUNDS = MODE == AM_FULL;     // promise-round runs and events
 #pragma unroll
     for (uint32_t j = 0; j < SPL; ++j) lidx[lane + 64 * j] = 0xFFFF;
     wave_lds_fence();
@@ -1571,7 +1577,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
 #define SF(j) ((sfl >> (8 * (j))) & 0xFF)
 #define SF_SET(j, x) (sfl = (sfl & ~(0xFFu << (8 * (j)))) | ((uint32_t)(x) << (8 * (j))))
 #pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) { if (DIGEST) sb[j] = 0; se[j] = sm[j] = 0; if (!SIMPLE) pre[lane + 64 * j] = u64x2{0, 0}; }
+        for (uint32_t j = 0; j < SPL; ++j) { if (DIGEST) sb[j] = 0; se[j] = sm[j] = 0; if (ROUNDS) pre[lane + 64 * j] = u64x2{0, 0}; }
 
         bool first = true;
         while (fi < fe || ei < ee) {
@@ -1664,7 +1670,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                 }
                                 ++cL;
                             }
-                    } else if (!SIMPLE && kind == K_PREPLY) {
+                    } else if (ROUNDS && kind == K_PREPLY) {
                         if ((mf & F_COUNTED) && !(v.knobs & 8192)) {       // knob 8192: experiment, no merge
 #pragma unroll 1
                             for (uint32_t j = 0; j < SPL; ++j)
@@ -1721,6 +1727,8 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             }
                             emit_rows(v, hit, g, 0, ref);
                         }
+                    } else if (!ROUNDS) {
+                        // (AM_SNAP: a pair without promise-reply runs gets no other event)
                     } else if (t8 == MPX_MSG_P_START || (t8 == MPX_MSG_E_EPOCH && (fl & F_PRECLR))) {
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) pre[lane + 64 * j] = u64x2{0, 0};
@@ -2277,16 +2285,22 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         // the event- and merge-free pairs first (k_apply<..., SIMPLE>), then the rest;
         // knob 65536: one kernel over the whole list (A/B)
+        // knob 262144: no AM_SNAP kernel (those pairs go to the full one)
         const uint64_t ns = (v.knobs & 65536) ? 0 : v.num_gp_simple;
-        if (ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
+        const uint64_t nq = (v.knobs & (65536 | 262144)) ? ns : v.num_gp_snap;
+        if (ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
                   // (capped at 6 / 8 waves per SIMD: 1.415 / 1.458 vs 1.393 ms general apply, C3 2^24)
-                  else hipLaunchKernelGGL((k_apply<1, false, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
-        if (v.num_gp > ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp);
+                  else hipLaunchKernelGGL((k_apply<1, false, false, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
+        if (nq > ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq);
+                  // 4 waves / SIMD (128 VGPRs, 4 spilled): 1.324 ms general apply vs 1.469 unconstrained (133 VGPRs,
+                  // 3 waves) and 1.351 without the AM_SNAP split (knob 262144), C3 2^24
+                  else hipLaunchKernelGGL((k_apply<4, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq); }
+        if (v.num_gp > nq) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
                    // 4 waves / SIMD (128 VGPRs, a few spilled) beats the unconstrained 154 VGPRs at 3:
                    // C3 2^24 general apply 1.394 vs 1.580 ms; 5 and 6 waves spill more (1.87, 2.36 ms);
                    // variant 1: the unconstrained build (A/B)
-                   else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp);
-                   else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, v.num_gp); }
+                   else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
+                   else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
     }
     if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
     hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);

@@ -220,6 +220,7 @@ struct DevView {
     const Frag *frags;
     uint64_t num_gp;                // pairs for the general apply kernel
     uint64_t num_gp_simple;         // ... the first of them: no snapshot events, no promise-reply runs (multi)
+    uint64_t num_gp_snap;           // ... then up to here: no promise-reply runs (PREPARE events only)
     const uint64_t *gp_list;        // general-apply work items, GP_WORDS each: the pair's fragment CSR
                                     // range, its event CSR range, the pair q (one coalesced load per item)
     const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
