@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--c3-instances", type=int, default=1 << 24, help="C3 general-path leg: M (2^24); 0 = skip")
     ap.add_argument("--c3-steps", type=int, default=5)
     ap.add_argument("--c3-only", action="store_true", help="only the C3 leg (profiling)")
+    ap.add_argument("--c5-instances", type=int, default=0, help="C5 member-path leg: M (2^25); 0 = skip")
+    ap.add_argument("--c5-steps", type=int, default=5)
+    ap.add_argument("--c5-only", action="store_true", help="only the C5 leg (profiling)")
     return ap.parse_args()
 
 
@@ -81,42 +84,53 @@ def parse():
 # HijackSend fault model of multi/debug.conf.sample:1 (drop 500, dup 1000 per 10^4, delay U[0,500)),
 # batches of U[1,256] instances
 C3 = dict(num_nodes=7, seed=0, batch=256, proposers=3, drop_rate=500, dup_rate=1000, max_delay=500)
+# C5: member semantics, acceptor universe 8, AddAcceptor(1..7) then DelAcceptor(1..7)
+# (member/main.cpp:119-141), 1 % loss / duplicates, stale in-flight ACCEPTs across version changes
+C5 = dict(num_nodes=8, seed=0, batch=256, drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15)
 
 
 def log(msg):
     print("[bench] " + msg, file=sys.stderr, flush=True)
 
 
-def c3_leg(args):
+def c3_leg(args, kind="c3"):
     """The general path on C3: every pair goes through k_apply (multi-ballot promise phases,
     promise replies with entries, rejects, duplicates, reordering).  The trace is generated
     and ingested through mpx_submit_trace before timing (host work, reported apart); a step
     is the same mpx_step the C4 line times.  roofline on SURVEY §8(d)'s bytes
-    (16 P + 24 A + 16 L from the engine's counters) over the apply phase."""
-    m = args.c3_instances
+    (16 P + 24 A + 16 L from the engine's counters) over the apply phase.
+    kind "c5": the same over the C5 member trace (member role gates, insert-first apply,
+    per-epoch quorums: the member instantiation of k_apply)."""
+    member = kind == "c5"
+    m = args.c5_instances if member else args.c3_instances
+    steps = args.c5_steps if member else args.c3_steps
     t0 = time.perf_counter()
-    trace = mpx.generate_trace(mpx.GEN_FAULTY, num_instances=m, copy=False, **C3)
+    if member:
+        trace = mpx.generate_trace(mpx.GEN_MEMBER, num_instances=m, copy=False, **C5)
+    else:
+        trace = mpx.generate_trace(mpx.GEN_FAULTY, num_instances=m, copy=False, **C3)
     t_gen = time.perf_counter() - t0
-    log("c3: generated %.1f MB in %.1f s" % (len(trace) / 1e6, t_gen))
+    log("%s: generated %.1f MB in %.1f s" % (kind, len(trace) / 1e6, t_gen))
     hd = mpx.trace_header(trace)
     trace_bytes = len(trace)
-    eng = mpx.Engine(hd["num_nodes"], 0, max(hd["num_instances"], 1))
+    eng = mpx.Engine.for_trace(trace) if member else mpx.Engine(hd["num_nodes"], 0, max(hd["num_instances"], 1))
     t0 = time.perf_counter()
-    eng.submit_trace(trace)
+    if not member:
+        eng.submit_trace(trace)
     t_ingest = time.perf_counter() - t0
-    log("c3: ingested in %.1f s" % t_ingest)
+    log("%s: ingested in %.1f s" % (kind, t_ingest))
     del trace
     t0 = time.perf_counter()
     chk = eng.run()                                 # upload + one digested run (verification)
     t_first = time.perf_counter() - t0
-    log("c3: upload + first run %.1f s" % t_first)
+    log("%s: upload + first run %.1f s" % (kind, t_first))
     eng.timings()
     for _ in range(2):
         eng.step()
     eng.sync()
     eng.timings()
     t0 = time.perf_counter()
-    for _ in range(args.c3_steps):
+    for _ in range(steps):
         eng.step()
     eng.sync()
     dt = time.perf_counter() - t0
@@ -125,25 +139,31 @@ def c3_leg(args):
     step_digests = eng.state_digest()
     step_ok = step_digests == (chk["state_digest"], chk["chosen_digest"]) and \
         all(st[k] == chk[k] for k in ("chosen", "promise_entries", "accept_apps", "commit_apps", "violations"))
-    assert step_ok, "C3: the timed step's state differs from the digested run's"
+    assert step_ok, "%s: the timed step's state differs from the digested run's" % kind.upper()
     assert st["violations"] == 0
     mean = lambda k: sum(p[k] for p in ph) / max(len(ph), 1)
     general_ms, fast_ms = mean("general_apply"), mean("fast_apply")
     apply_ms = general_ms + fast_ms
     b_alg = 16 * st["promise_entries"] + 24 * st["accept_apps"] + 16 * st["commit_apps"]
     achieved = b_alg / (apply_ms * 1e-3) / 1e9 if apply_ms else 0.0
-    pmc = latest_pmc(7, m, 1, workload="C3")
-    ms_step = dt / args.c3_steps * 1e3
+    pmc = None if member else latest_pmc(7, m, 1, workload="C3")
+    ms_step = dt / steps * 1e3
+    if member:
+        workload = ("C5: 2^%d instances, member semantics, acceptor universe 8, AddAcceptor(1..7) then "
+                    "DelAcceptor(1..7) = 15 epochs (member/main.cpp:119-141), 1%% loss / 1%% duplicates, "
+                    "batch U[1,256]" % (m.bit_length() - 1))
+    else:
+        workload = ("C3: 2^%d instances x 7 acceptors, 3 competing proposers, drop 5%% / dup 10%% (<=3) / "
+                    "delay U[0,500) (multi/debug.conf.sample:1), batch U[1,256]" % (m.bit_length() - 1))
     return {
-        "workload": "C3: 2^%d instances x 7 acceptors, 3 competing proposers, drop 5%% / dup 10%% (<=3) / "
-                    "delay U[0,500) (multi/debug.conf.sample:1), batch U[1,256]" % (m.bit_length() - 1),
+        "workload": workload,
         "instances_proposed": m, "instances": hd["num_instances"], "acceptors": hd["num_nodes"],
         "decisions_per_step": st["chosen"], "ms_per_step": ms_step,
         "value": st["chosen"] / (ms_step * 1e-3), "unit": "decisions/s",
         "counters": {k: st[k] for k in ("chosen", "promise_entries", "accept_apps", "commit_apps", "messages")},
         "phases_ms": {k: mean(k) for k in mpx.Engine.PHASES},
-        "roofline": {"bound": "hbm", "kernel": "apply phase (k_apply: general pairs; k_plan/k_store/k_apply_fast: "
-                                               "clean pairs)",
+        "roofline": {"bound": "hbm", "kernel": "apply phase (k_apply<member>: every pair)" if member else
+                     "apply phase (k_apply: general pairs; k_plan/k_store/k_apply_fast: clean pairs)",
                      "bytes_alg_per_launch": b_alg, "bytes_model": "SURVEY §8(d): 16 P + 24 A + 16 L",
                      "kernel_ms": apply_ms, "general_ms": general_ms, "fast_ms": fast_ms,
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -337,6 +357,9 @@ def main():
     if args.c3_only:
         print(json.dumps({"c3": c3_leg(args)}), flush=True)
         return
+    if args.c5_only:
+        print(json.dumps({"c5": c3_leg(args, "c5")}), flush=True)
+        return
     world, rank, local, pg = dist_setup(args)
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
@@ -412,6 +435,7 @@ def main():
             cpu = cpu_baseline(args, args.cpu_seconds)
             cpu_port = cpu_port_baseline(args, args.cpu_seconds / 2)
         c3 = c3_leg(args) if world == 1 and args.c3_instances else None
+        c5 = c3_leg(args, "c5") if world == 1 and args.c5_instances else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -448,6 +472,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_port": cpu_port,
             "c3": c3,
+            **({"c5": c5} if c5 else {}),
             "verified": {"step_state_digest_vs_closed_form": step_ok, "step_state_digest": step_state,
                          "step_chosen_digest": step_chosen, "run_digests_vs_closed_form": verified,
                          "state_digest": chk["state_digest"], "chosen_digest": chk["chosen_digest"]},

@@ -2259,6 +2259,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         // member: every pair walks the general kernel (insert semantics, epoch events)
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, v.num_gp);
+                   else if (g.variant == 4) hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, v.num_gp);
                    else hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, v.num_gp); }
     } else {
         // multi: the lean kernel also writes the chosen log of clean buckets
