@@ -1207,18 +1207,34 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
     // second words into LDS with coalesced loads (lane r: words r, r + 64, ..),
     // then every pair lane reads its runs from there
     const uint64_t oa = v.f_off[i < np ? i : np], o1 = v.f_off[i < np ? i + 1 : np];
+    const uint8_t gp = i < np ? v.pair_gp[i] : 1;   // issued with the offsets, not after the staging
     const uint64_t wbase = rl64(oa, 0);
     {
+        // the staging loads of a wave's runs all in flight, then the LDS writes
+        // (C4: two runs per pair, 128 words per wave; longer ranges loop)
         const uint64_t wend = rl64(o1, 63);
         const uint32_t R = (uint32_t)(wend - wbase < PLAN_LDS ? wend - wbase : PLAN_LDS);
-        for (uint32_t r = lane; r < R; r += 64) w_lds[wv][r] = v.frag_w1[wbase + r];
+        constexpr uint32_t K = 4;
+        for (uint32_t r0 = 0; r0 < R; r0 += 64 * K) {
+            uint64_t x[K];
+#pragma unroll
+            for (uint32_t k = 0; k < K; ++k) {
+                const uint32_t r = r0 + lane + 64 * k;
+                x[k] = r < R ? v.frag_w1[wbase + r] : 0;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < K; ++k) {
+                const uint32_t r = r0 + lane + 64 * k;
+                if (r < R) w_lds[wv][r] = x[k];
+            }
+        }
         wave_lds_fence();
     }
     if (i < np) {
         const uint64_t b = i / N;
 
         const uint32_t len = (uint32_t)(o1 - oa);
-        const bool in_list = len && len <= FAST_MAX_FRAGS && !v.pair_gp[i];
+        const bool in_list = len && len <= FAST_MAX_FRAGS && !gp;
         uint64_t q = PLAN_SKIP;
         if (in_list && len <= F) {
             uint64_t w[F];
@@ -2272,6 +2288,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
             // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
             // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
             // 0.391 vs 0.304 ms apply phase at C4; the compiler drains vmcnt at its loop head)
+            // (the chosen-log buckets on threads of their own after the pairs: 63.5 vs 61.5 us at C4)
             hipLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s, v, g.apply_wgs);
             if (v.slot_w == 1 && (v.knobs & 128)) hipLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
             // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64
