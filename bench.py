@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--c3-instances", type=int, default=1 << 24, help="C3 general-path leg: M (2^24); 0 = skip")
     ap.add_argument("--c3-steps", type=int, default=5)
     ap.add_argument("--c3-only", action="store_true", help="only the C3 leg (profiling)")
-    ap.add_argument("--c5-instances", type=int, default=0, help="C5 member-path leg: M (2^25); 0 = skip")
+    ap.add_argument("--c5-instances", type=int, default=1 << 25, help="C5 member-path leg: M (2^25); 0 = skip")
     ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--c5-only", action="store_true", help="only the C5 leg (profiling)")
     return ap.parse_args()
@@ -113,10 +113,9 @@ def c3_leg(args, kind="c3"):
     log("%s: generated %.1f MB in %.1f s" % (kind, len(trace) / 1e6, t_gen))
     hd = mpx.trace_header(trace)
     trace_bytes = len(trace)
-    eng = mpx.Engine.for_trace(trace) if member else mpx.Engine(hd["num_nodes"], 0, max(hd["num_instances"], 1))
+    eng = mpx.Engine(hd["num_nodes"], 0, max(hd["num_instances"], 1), semantics=hd["semantics"])
     t0 = time.perf_counter()
-    if not member:
-        eng.submit_trace(trace)
+    eng.submit_trace(trace)                         # (member: the trace's epoch table comes with it)
     t_ingest = time.perf_counter() - t0
     log("%s: ingested in %.1f s" % (kind, t_ingest))
     del trace
@@ -435,7 +434,12 @@ def main():
             cpu = cpu_baseline(args, args.cpu_seconds)
             cpu_port = cpu_port_baseline(args, args.cpu_seconds / 2)
         c3 = c3_leg(args) if world == 1 and args.c3_instances else None
-        c5 = c3_leg(args, "c5") if world == 1 and args.c5_instances else None
+        c5 = None
+        if world == 1 and args.c5_instances:
+            try:                                    # a secondary leg: its failure is reported, not fatal
+                c5 = c3_leg(args, "c5")
+            except Exception as ex:                 # noqa: BLE001
+                c5 = {"error": repr(ex)}
         out = {
             "metric": METRIC,
             "value": value,
