@@ -2312,7 +2312,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                   else hipLaunchKernelGGL((k_apply<1, false, false, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
         if (nq > ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq);
                   // 4 waves / SIMD (128 VGPRs, 4 spilled): 1.324 ms general apply vs 1.469 unconstrained (133 VGPRs,
-                  // 3 waves) and 1.351 without the AM_SNAP split (knob 262144), C3 2^24
+                  // 3 waves), 1.496 at 5 waves (96 VGPRs, 38 spilled) and 1.351 without the AM_SNAP split
+                  // (knob 262144), C3 2^24
                   else hipLaunchKernelGGL((k_apply<4, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq); }
         if (v.num_gp > nq) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
                    // 4 waves / SIMD (128 VGPRs, a few spilled) beats the unconstrained 154 VGPRs at 3:
