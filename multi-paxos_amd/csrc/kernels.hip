@@ -16,6 +16,7 @@
 //   k_reduce     counters, digests -> 64-word summary
 // Everything is integer, HBM-bound; no MFMA.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include "mpx_internal.hpp"
 
 namespace mpx {
@@ -2250,8 +2251,11 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (v.NB > reset_n) reset_n = v.NB;
     if (8ull * n_partials > reset_n) reset_n = 8ull * n_partials;
     if (2ull * v.N > reset_n) reset_n = 2ull * v.N;
-    if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, s);
-    hipLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s, v, n_partials);
+    // Phase events ride on kernel dispatches (hipExtLaunchKernelGGL start / stop events) where a
+    // kernel begins or ends the phase: a separate event record costs a 5-10 us bubble between
+    // dependent kernels (rocprof, C4: 16 us of a 395 us step)
+    hipExtLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s,
+                          (hipEvent_t)ev_begin, (hipEvent_t)nullptr, 0, v, n_partials);
     if (v.semantics == MPX_SEM_MEMBER) {
         // member role / version gates from the E_EPOCH markers (k_gate_*)
         hipLaunchKernelGGL(k_gate_epochs, dim3(cdiv(v.N, 64)), dim3(64), 0, s, v);
@@ -2270,7 +2274,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (v.pc_multi) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s, v);
     }
     if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
-    if (ev_apply0) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
+    const bool plan_path = v.semantics != MPX_SEM_MEMBER && !v.digest && !(v.knobs & 64) && v.N <= FAST_MAX_NODES;
+    if (ev_apply0 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
     if (v.semantics == MPX_SEM_MEMBER) {
         // member: every pair walks the general kernel (insert semantics, epoch events)
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
@@ -2289,19 +2294,21 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
             // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
             // 0.391 vs 0.304 ms apply phase at C4; the compiler drains vmcnt at its loop head)
             // (the chosen-log buckets on threads of their own after the pairs: 63.5 vs 61.5 us at C4)
-            hipLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s, v, g.apply_wgs);
+            hipExtLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s,
+                                  (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
             if (v.slot_w == 1 && (v.knobs & 128)) hipLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
             // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64
             else if (v.slot_w == 1 && (v.knobs & 2048)) hipLaunchKernelGGL((k_store8<true, 64>), dim3(g.store_wgs), dim3(256), 0, s, v);
             else if (v.slot_w == 1) hipLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, v);
             else hipLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
-            hipLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+            hipExtLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s,
+                                  (hipEvent_t)nullptr, (hipEvent_t)ev_apply1, 0, v);
         } else switch (g.variant) {
         case 1: hipLaunchKernelGGL((k_apply_fast<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         case 2: hipLaunchKernelGGL((k_apply_fast<5, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
         }
-        if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
+        if (ev_apply1 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         // the event- and merge-free pairs first (k_apply<..., SIMPLE>), then the rest;
         // knob 65536: one kernel over the whole list (A/B)
         // knob 262144: no AM_SNAP kernel (those pairs go to the full one)
@@ -2322,10 +2329,9 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                    else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
                    else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
     }
-    if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
-    hipLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, v, n_partials);
-    if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, s);
+    hipExtLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general, (hipEvent_t)nullptr, 0,
+                          v, g.apply_wgs);
+    hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
     return (int)hipGetLastError();
 }
 
