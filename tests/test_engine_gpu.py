@@ -403,14 +403,17 @@ def test_store_chunks_tails_and_partial_pairs(extra):
 
 
 @pytest.mark.parametrize("env", [("MPX_SCAN_NODE_PASS", "1"), ("MPX_KNOBS", "2048"), ("MPX_PROP_CHUNK", "64"),
-                                 ("MPX_PROP_CHUNK", "5")])
+                                 ("MPX_PROP_CHUNK", "5"), ("MPX_KNOBS", "65536"), ("MPX_KNOBS", "262144"),
+                                 ("MPX_KNOBS", "131072"), ("MPX_APPLY_VARIANT", "1")])
 @pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "c5_member_3",
                                   "demo_s0", "demo5_s3", "hm_promise_merge"])
 def test_kept_alternative_paths(name, env, monkeypatch):
     """The kept alternatives stay correct: the separate per-node scan pass (taken
     automatically beyond SCAN_INLINE_CHUNKS chunks per node), 64-bucket k_store8
-    chunks, and promise-quorum chunks small enough that rounds span chunks
-    (k_prop_chunk's deferred prefixes, k_prop_node's carry)."""
+    chunks, promise-quorum chunks small enough that rounds span chunks
+    (k_prop_chunk's deferred prefixes, k_prop_node's carry), the general k_apply
+    work list without its SIMPLE / SNAP split, PREPARE ranges loaded instead of
+    the inline interval, and the unconstrained (3-wave) k_apply builds."""
     if name not in INDEX:
         pytest.skip("no golden " + name)
     monkeypatch.setenv(*env)
