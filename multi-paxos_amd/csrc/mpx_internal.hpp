@@ -40,7 +40,7 @@ namespace mpx {
 
 constexpr uint32_t BSH = 8;                  // bucket = 256 instances
 constexpr uint32_t BS = 1u << BSH;
-constexpr uint32_t SCAN_CHUNK = 4096;        // header-scan chunk (messages): 16 per thread
+constexpr uint32_t SCAN_CHUNK = 2048;        // header-scan chunk (messages): 8 per thread
 constexpr uint32_t PROP_CHUNK = 512;         // promise-quorum chunk (pl records): 8 windows of 64 (C3 2^24 scan
                                              // phase 0.112 ms vs 0.128 at 2048, 0.134 at 256)
 // k_scan_apply re-reduces a node's earlier chunk aggregates inline (O(chunks^2)
