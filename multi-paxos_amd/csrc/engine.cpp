@@ -325,7 +325,7 @@ static int finish_view(mpx_engine *e)
     e->geom.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 4));
     e->geom.store_wgs = e->num_cus * 8;     // k_store: 8 workgroups of 4 waves per CU
 
-    TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + e->geom.chosen_wgs)));
+    TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + std::max<uint64_t>(e->geom.chosen_wgs, e->num_cus * 16))));
     TRY(e->viol.alloc(sizeof(DevViolation)));
     TRY(e->summary.alloc(64 * 8));
     TRY(e->out_cursor.alloc(8ull * OUT_STRIDE * OUT_SUBS));
@@ -499,6 +499,9 @@ static int queue_run(mpx_engine *e, bool digest)
     e->view.knobs = 0;
     if (const char *x = std::getenv("MPX_KNOBS")) e->view.knobs = (uint32_t)std::atoi(x);
     if (const char *x = std::getenv("MPX_STORE_WGS_PER_CU")) g.store_wgs = std::max<uint32_t>(1, e->num_cus * (uint32_t)std::atoi(x));
+    if (const char *x = std::getenv("MPX_CHOSEN_WGS_PER_CU"))     // (partials hold 16 per CU for it too)
+        g.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 16),
+                                                                          (uint64_t)e->num_cus * std::atoi(x)));
     if (const char *x = std::getenv("MPX_APPLY_WGS_PER_CU")) {
         const uint64_t np = (uint64_t)e->cfg.num_nodes * e->NB;
         g.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(np, (uint64_t)e->num_cus * std::atoi(x)));
