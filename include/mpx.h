@@ -267,6 +267,29 @@ int  mpx_dump_result(mpx_engine *eng, uint8_t **out, uint64_t *size);
  * u64 n, {u64 iid, u64 handle} * n, iid ascending}.  *out is malloc'ed; free
  * with mpx_free.  MPX_E_STATE for member semantics or a shard engine. */
 int  mpx_read_decisions(mpx_engine *eng, uint8_t **out, uint64_t *size);
+/* Sharded phase-2 decisions (one engine per instance range, shards in rank
+ * order).  The fill of each quorum reaches the highest committed-or-adopted
+ * instance over ALL shards, so it takes one exchange of per-quorum bounds:
+ *  1. mpx_decisions_bounds: per promise quorum of the run (node-major stream
+ *     order, the same list on every shard) the shard's own bound, absolute:
+ *     shard_begin + 1 + its highest committed-or-adopted instance, 0 if none.
+ *     Writes min(cap, count) bounds, *count = the number of quorums.
+ *  2. the caller takes the element-wise maximum over shards (an all-reduce MAX
+ *     of `count` u64) and passes it to mpx_read_decisions_part, which writes
+ *     this shard's adopted entries and noop-fill instances.  Format MPXP:
+ *     "MPXP" u32 1, u32 nodes, u64 shard_begin; then MPXD's body with a noop
+ *     entry's handle ~0 (numbered only once the parts are merged).
+ *  3. mpx_decisions_combine merges the parts (given in shard order) into the
+ *     MPXD mpx_read_decisions writes on one engine holding every instance:
+ *     each quorum's entries concatenated in shard order, noops numbered
+ *     Value(node, ++value_id) per node.  Pure host work.
+ * MPX_E_STATE for member semantics; MPX_E_INVAL for a bound count or parts
+ * that do not match. */
+int  mpx_decisions_bounds(mpx_engine *eng, uint64_t *bounds, uint64_t cap, uint64_t *count);
+int  mpx_read_decisions_part(mpx_engine *eng, const uint64_t *global_bounds, uint64_t count,
+                             uint8_t **out, uint64_t *size);
+int  mpx_decisions_combine(const uint8_t *const *parts, const uint64_t *sizes, uint32_t nparts,
+                           uint8_t **out, uint64_t *size);
 /* Commit reliability (multi semantics, an engine that kept
  * every record — shard starting at 0, nothing left out for another shard):
  * every CommittingValues each node's proposer created in the last run — at an

@@ -1008,6 +1008,98 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
     return MPX_OK;
 }
 
+// Per promise-quorum event of the run (node-major stream order, the same on every
+// shard: the promise headers are replicated): the adopted entries in the shard and
+// the shard's noop-fill instances.  gx == nullptr: the fill ends at the shard's own
+// bound (a whole engine); else at gx[k] (absolute), the maximum of every shard's bound.
+struct DecideEv { uint32_t node, msg; uint64_t bound; std::vector<const OutEnt *> adopted; std::vector<uint64_t> noops; };
+static int decide_core(mpx_engine *e, const Results &r, const uint64_t *gx, uint64_t ngx, bool bounds_only,
+                       std::vector<DecideEv> &evs)
+{
+    const HostTrace &h = e->ht;
+    const uint32_t N = e->cfg.num_nodes;
+    evs.clear();
+    for (uint32_t n = 0; n < N; ++n)
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g)
+            if (h.m_type[g] == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM)) evs.push_back(DecideEv{n, (uint32_t)g, 0, {}, {}});
+    const uint32_t E = (uint32_t)evs.size();
+    if (gx && ngx != E) return MPX_E_INVAL;
+    const uint64_t sb = e->cfg.shard_begin;
+    // adopted: the merged entries of instances not committed at the quorum (:1091)
+    std::vector<uint64_t> ad_off(E + 1, 0), xend(E, 0);
+    std::vector<uint32_t> ad_li, en(E), eg(E);
+    for (uint32_t k = 0; k < E; ++k) {
+        en[k] = evs[k].node; eg[k] = evs[k].msg;
+        auto it = r.by_msg[1].find(eg[k]);
+        if (it != r.by_msg[1].end())
+            for (const OutEnt *o : it->second)
+                if (!(o->kind & 2)) { evs[k].adopted.push_back(o); ad_li.push_back((uint32_t)(o->iid - sb)); }
+        ad_off[k + 1] = ad_li.size();
+        if (!evs[k].adopted.empty()) xend[k] = evs[k].adopted.back()->iid - sb + 1;
+    }
+    if (!E) return MPX_OK;
+    hipStream_t s = e->stream;
+    DevBuf d_node, d_msg, d_xmax, d_xend, d_adoff, d_adli, d_boff, d_bcnt, d_base, d_tot, d_noop;
+    TRY(upload(d_node, en, s)); TRY(upload(d_msg, eg, s));
+    TRY(d_xmax.alloc(8ull * E)); HTRY(hipMemsetAsync(d_xmax.p, 0, 8ull * E, s));
+    DecideArgs a{};
+    a.E = E; a.ev_node = d_node.as<uint32_t>(); a.ev_msg = d_msg.as<uint32_t>();
+    a.xmax = d_xmax.as<unsigned long long>();
+    if (launch_decide(e->view, s, 0, a) != 0) return MPX_E_HIP;
+    std::vector<uint64_t> xmax;
+    HTRY(hipStreamSynchronize(s));
+    TRY(d2h(xmax, d_xmax, E));
+    std::vector<uint64_t> boff(E + 1, 0);
+    uint64_t maxb = 0;
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint64_t own = std::max(xend[k], xmax[k]);            // 1 + the highest committed or adopted (local)
+        evs[k].bound = own ? sb + own : 0;
+        uint64_t end = own;
+        if (gx) end = gx[k] > sb ? gx[k] - sb : 0;                   // the fill reaches the global bound
+        xend[k] = std::min<uint64_t>(end, e->shard_len);
+        const uint64_t nb = (xend[k] + 255) / 256;
+        boff[k + 1] = boff[k] + nb;
+        maxb = std::max(maxb, nb);
+    }
+    if (bounds_only) return MPX_OK;
+    TRY(upload(d_xend, xend, s)); TRY(upload(d_adoff, ad_off, s)); TRY(upload(d_adli, ad_li, s));
+    TRY(upload(d_boff, boff, s));
+    TRY(d_bcnt.alloc(std::max<uint64_t>(4 * boff[E], 4))); TRY(d_tot.alloc(8ull * E));
+    a.xend = d_xend.as<uint64_t>(); a.ad_off = d_adoff.as<uint64_t>(); a.ad_li = d_adli.as<uint32_t>();
+    a.blk_off = d_boff.as<uint64_t>(); a.blk_cnt = d_bcnt.as<uint32_t>(); a.ev_total = d_tot.as<uint64_t>();
+    a.max_blocks = maxb;
+    if (launch_decide(e->view, s, 1, a) != 0 || launch_decide(e->view, s, 3, a) != 0) return MPX_E_HIP;
+    std::vector<uint64_t> tot, ev_base(E + 1, 0);
+    HTRY(hipStreamSynchronize(s));
+    TRY(d2h(tot, d_tot, E));
+    for (uint32_t k = 0; k < E; ++k) ev_base[k + 1] = ev_base[k] + tot[k];
+    TRY(upload(d_base, ev_base, s));
+    TRY(d_noop.alloc(std::max<uint64_t>(4 * ev_base[E], 4)));
+    a.ev_base = d_base.as<uint64_t>(); a.noop_li = d_noop.as<uint32_t>();
+    if (launch_decide(e->view, s, 2, a) != 0) return MPX_E_HIP;
+    std::vector<uint32_t> noops;
+    HTRY(hipStreamSynchronize(s));
+    TRY(d2h(noops, d_noop, ev_base[E]));
+    for (uint32_t k = 0; k < E; ++k)
+        for (uint64_t j = ev_base[k]; j < ev_base[k + 1]; ++j) evs[k].noops.push_back(sb + noops[j]);
+    return MPX_OK;
+}
+
+// one event's batch: adopted and noop entries merged by instance (both sorted);
+// noop handles Value(node, ++value_id_) from vid, or NOOP_SLOT placeholders (parts)
+static constexpr uint64_t NOOP_SLOT = ~0ull;
+static void decide_entries(const DecideEv &ev, uint64_t *vid, std::string &d)
+{
+    app<uint64_t>(d, ev.adopted.size() + ev.noops.size());
+    size_t i = 0, j = 0;
+    while (i < ev.adopted.size() || j < ev.noops.size()) {
+        const uint64_t ai = i < ev.adopted.size() ? ev.adopted[i]->iid : ~0ull;
+        const uint64_t ni = j < ev.noops.size() ? ev.noops[j] : ~0ull;
+        if (ai < ni) { app<uint64_t>(d, ai); app<uint64_t>(d, ev.adopted[i]->handle); ++i; }
+        else { app<uint64_t>(d, ni); app<uint64_t>(d, vid ? MPX_HANDLE(ev.node, 1, ++*vid) : NOOP_SLOT); ++j; }
+    }
+}
+
 // ------------------------------------------------- phase-2 decisions (f2) --
 // The batch OnPrepareReply builds at each promise quorum (multi/paxos.cpp:
 // 1056-1130) for a proposer with no client proposals of its own: the device
@@ -1022,90 +1114,128 @@ extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
     if (e->cfg.semantics != MPX_SEM_MULTI || e->cfg.shard_begin != 0) return MPX_E_STATE;
     Results r;
     TRY(fetch_results(e, r));
-    const HostTrace &h = e->ht;
+    std::vector<DecideEv> evs;
+    TRY(decide_core(e, r, nullptr, 0, false, evs));
     const uint32_t N = e->cfg.num_nodes;
-    std::vector<uint32_t> en, eg;
-    for (uint32_t n = 0; n < N; ++n)
-        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g)
-            if (h.m_type[g] == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM)) { en.push_back(n); eg.push_back((uint32_t)g); }
-    const uint32_t E = (uint32_t)en.size();
-    const uint64_t sb = e->cfg.shard_begin;
-    // adopted: the merged entries of instances not committed at the quorum (:1091)
-    std::vector<std::vector<const OutEnt *>> adopted(E);
-    std::vector<uint64_t> ad_off(E + 1, 0), xend(E, 0);
-    std::vector<uint32_t> ad_li;
-    for (uint32_t k = 0; k < E; ++k) {
-        auto it = r.by_msg[1].find(eg[k]);
-        if (it != r.by_msg[1].end())
-            for (const OutEnt *o : it->second)
-                if (!(o->kind & 2)) { adopted[k].push_back(o); ad_li.push_back((uint32_t)(o->iid - sb)); }
-        ad_off[k + 1] = ad_li.size();
-        if (!adopted[k].empty()) xend[k] = adopted[k].back()->iid - sb + 1;
-    }
-    std::vector<uint32_t> noops;
-    std::vector<uint64_t> ev_base(E + 1, 0);
-    if (E) {
-        hipStream_t s = e->stream;
-        DevBuf d_node, d_msg, d_xmax, d_xend, d_adoff, d_adli, d_boff, d_bcnt, d_base, d_tot, d_noop;
-        TRY(upload(d_node, en, s)); TRY(upload(d_msg, eg, s));
-        TRY(d_xmax.alloc(8ull * E)); HTRY(hipMemsetAsync(d_xmax.p, 0, 8ull * E, s));
-        DecideArgs a{};
-        a.E = E; a.ev_node = d_node.as<uint32_t>(); a.ev_msg = d_msg.as<uint32_t>();
-        a.xmax = d_xmax.as<unsigned long long>();
-        if (launch_decide(e->view, s, 0, a) != 0) return MPX_E_HIP;
-        std::vector<uint64_t> xmax;
-        HTRY(hipStreamSynchronize(s));
-        TRY(d2h(xmax, d_xmax, E));
-        std::vector<uint64_t> boff(E + 1, 0);
-        uint64_t maxb = 0;
-        for (uint32_t k = 0; k < E; ++k) {
-            xend[k] = std::min<uint64_t>(std::max(xend[k], xmax[k]), e->shard_len);
-            const uint64_t nb = (xend[k] + 255) / 256;
-            boff[k + 1] = boff[k] + nb;
-            maxb = std::max(maxb, nb);
-        }
-        TRY(upload(d_xend, xend, s)); TRY(upload(d_adoff, ad_off, s)); TRY(upload(d_adli, ad_li, s));
-        TRY(upload(d_boff, boff, s));
-        TRY(d_bcnt.alloc(std::max<uint64_t>(4 * boff[E], 4))); TRY(d_tot.alloc(8ull * E));
-        a.xend = d_xend.as<uint64_t>(); a.ad_off = d_adoff.as<uint64_t>(); a.ad_li = d_adli.as<uint32_t>();
-        a.blk_off = d_boff.as<uint64_t>(); a.blk_cnt = d_bcnt.as<uint32_t>(); a.ev_total = d_tot.as<uint64_t>();
-        a.max_blocks = maxb;
-        if (launch_decide(e->view, s, 1, a) != 0 || launch_decide(e->view, s, 3, a) != 0) return MPX_E_HIP;
-        std::vector<uint64_t> tot;
-        HTRY(hipStreamSynchronize(s));
-        TRY(d2h(tot, d_tot, E));
-        for (uint32_t k = 0; k < E; ++k) ev_base[k + 1] = ev_base[k] + tot[k];
-        TRY(upload(d_base, ev_base, s));
-        TRY(d_noop.alloc(std::max<uint64_t>(4 * ev_base[E], 4)));
-        a.ev_base = d_base.as<uint64_t>(); a.noop_li = d_noop.as<uint32_t>();
-        if (launch_decide(e->view, s, 2, a) != 0) return MPX_E_HIP;
-        HTRY(hipStreamSynchronize(s));
-        TRY(d2h(noops, d_noop, ev_base[E]));
-    }
     std::string d;
     d.append("MPXD", 4);
     app<uint32_t>(d, 1); app<uint32_t>(d, N);
     std::vector<uint64_t> vid(N, 0);                     // value_id_ per node (:335, ++ per noop)
-    uint32_t k = 0;
+    size_t k = 0;
     for (uint32_t n = 0; n < N; ++n) {
-        const uint32_t k0 = k;
-        while (k < E && en[k] == n) ++k;
+        const size_t k0 = k;
+        while (k < evs.size() && evs[k].node == n) ++k;
         app<uint64_t>(d, k - k0);
-        for (uint32_t x = k0; x < k; ++x) {
-            app<uint64_t>(d, seq_of(h, n, eg[x]));
-            const auto &ad = adopted[x];
-            app<uint64_t>(d, ad.size() + (ev_base[x + 1] - ev_base[x]));
-            size_t i = 0;
-            uint64_t j = ev_base[x];
-            while (i < ad.size() || j < ev_base[x + 1]) {  // both sorted by instance
-                const uint64_t ai = i < ad.size() ? ad[i]->iid : ~0ull;
-                const uint64_t ni = j < ev_base[x + 1] ? sb + noops[j] : ~0ull;
-                if (ai < ni) { app<uint64_t>(d, ai); app<uint64_t>(d, ad[i]->handle); ++i; }
-                else { app<uint64_t>(d, ni); app<uint64_t>(d, MPX_HANDLE(n, 1, ++vid[n])); ++j; }
-            }
+        for (size_t x = k0; x < k; ++x) {
+            app<uint64_t>(d, seq_of(e->ht, n, evs[x].msg));
+            decide_entries(evs[x], &vid[n], d);
         }
     }
     *out = (uint8_t *)std::malloc(d.size());
+    if (!*out) return MPX_E_NOMEM;
+    std::memcpy(*out, d.data(), d.size());
+    *size = d.size();
+    return MPX_OK;
+}
+
+// Sharded form (include/mpx.h): every rank's per-event bound, then its part with
+// the fill cut at the global bound, then the parts merged in shard order.
+extern "C" int mpx_decisions_bounds(mpx_engine *e, uint64_t *bounds, uint64_t cap, uint64_t *count)
+{
+    if (!e || !count || (cap && !bounds)) return MPX_E_INVAL;
+    if (e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
+    Results r;
+    TRY(fetch_results(e, r));
+    std::vector<DecideEv> evs;
+    TRY(decide_core(e, r, nullptr, 0, true, evs));
+    *count = evs.size();
+    for (size_t k = 0; k < evs.size() && k < cap; ++k) bounds[k] = evs[k].bound;
+    return MPX_OK;
+}
+
+extern "C" int mpx_read_decisions_part(mpx_engine *e, const uint64_t *global_bounds, uint64_t count,
+                                       uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size || (count && !global_bounds)) return MPX_E_INVAL;
+    if (e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
+    Results r;
+    TRY(fetch_results(e, r));
+    std::vector<DecideEv> evs;
+    TRY(decide_core(e, r, global_bounds, count, false, evs));
+    const uint32_t N = e->cfg.num_nodes;
+    std::string d;
+    d.append("MPXP", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, N);
+    app<uint64_t>(d, e->cfg.shard_begin);
+    size_t k = 0;
+    for (uint32_t n = 0; n < N; ++n) {
+        const size_t k0 = k;
+        while (k < evs.size() && evs[k].node == n) ++k;
+        app<uint64_t>(d, k - k0);
+        for (size_t x = k0; x < k; ++x) {
+            app<uint64_t>(d, seq_of(e->ht, n, evs[x].msg));
+            decide_entries(evs[x], nullptr, d);
+        }
+    }
+    *out = (uint8_t *)std::malloc(d.size());
+    if (!*out) return MPX_E_NOMEM;
+    std::memcpy(*out, d.data(), d.size());
+    *size = d.size();
+    return MPX_OK;
+}
+
+extern "C" int mpx_decisions_combine(const uint8_t *const *parts, const uint64_t *sizes, uint32_t nparts,
+                                     uint8_t **out, uint64_t *size)
+{
+    if (!parts || !sizes || !nparts || !out || !size) return MPX_E_INVAL;
+    struct P { const uint8_t *p; uint64_t n, pos; uint64_t sb; };
+    std::vector<P> ps(nparts);
+    uint32_t N = 0;
+    for (uint32_t i = 0; i < nparts; ++i) {
+        if (!parts[i] || sizes[i] < 20 || std::memcmp(parts[i], "MPXP", 4)) return MPX_E_INVAL;
+        const uint32_t n = rd32(parts[i] + 8);
+        if (i && n != N) return MPX_E_INVAL;
+        N = n;
+        ps[i] = P{parts[i], sizes[i], 20, rd64(parts[i] + 12)};
+        if (i && ps[i].sb <= ps[i - 1].sb) return MPX_E_INVAL;        // shard order
+    }
+    auto need = [](const P &q, uint64_t b) { return q.pos + b <= q.n; };
+    std::string d;
+    d.append("MPXD", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, N);
+    for (uint32_t node = 0; node < N; ++node) {
+        uint64_t cnt = 0;
+        for (uint32_t i = 0; i < nparts; ++i) {
+            if (!need(ps[i], 8)) return MPX_E_INVAL;
+            const uint64_t c = rd64(ps[i].p + ps[i].pos); ps[i].pos += 8;
+            if (i && c != cnt) return MPX_E_INVAL;                  // the same quorums on every shard
+            cnt = c;
+        }
+        app<uint64_t>(d, cnt);
+        uint64_t vid = 0;                                           // value_id_ of the node (:335)
+        for (uint64_t q = 0; q < cnt; ++q) {
+            std::string ents;
+            uint64_t tot = 0, seq = 0;
+            for (uint32_t i = 0; i < nparts; ++i) {
+                if (!need(ps[i], 16)) return MPX_E_INVAL;
+                const uint64_t sq = rd64(ps[i].p + ps[i].pos), m = rd64(ps[i].p + ps[i].pos + 8);
+                ps[i].pos += 16;
+                if (i && sq != seq) return MPX_E_INVAL;
+                seq = sq;
+                if (!need(ps[i], 16 * m)) return MPX_E_INVAL;
+                for (uint64_t j = 0; j < m; ++j) {
+                    const uint64_t iid = rd64(ps[i].p + ps[i].pos), h = rd64(ps[i].p + ps[i].pos + 8);
+                    ps[i].pos += 16;
+                    app<uint64_t>(ents, iid);
+                    app<uint64_t>(ents, h == NOOP_SLOT ? MPX_HANDLE(node, 1, ++vid) : h);
+                }
+                tot += m;
+            }
+            app<uint64_t>(d, seq); app<uint64_t>(d, tot);
+            d += ents;
+        }
+    }
+    *out = (uint8_t *)std::malloc(d.size() ? d.size() : 1);
     if (!*out) return MPX_E_NOMEM;
     std::memcpy(*out, d.data(), d.size());
     *size = d.size();

@@ -106,6 +106,9 @@ def lib():
             "mpx_dump_result": [vp, P(u8p), u64p],
             "mpx_read_decisions": [vp, P(u8p), u64p],
             "mpx_read_commits": [vp, P(u8p), u64p],
+            "mpx_decisions_bounds": [vp, u64p, ctypes.c_uint64, u64p],
+            "mpx_read_decisions_part": [vp, u64p, ctypes.c_uint64, P(u8p), u64p],
+            "mpx_decisions_combine": [P(u8p), u64p, ctypes.c_uint32, P(u8p), u64p],
             "mpx_value_bytes": [vp, ctypes.c_uint64, u8p, ctypes.c_uint32, P(ctypes.c_uint32)],
             "mpx_trace_generate": [P(GenParams), P(u8p), u64p],
             "mpx_load_clean_device": [vp, P(GenParams)],
@@ -287,6 +290,24 @@ class Engine:
         _ck("mpx_read_decisions", lib().mpx_read_decisions(self.h, ctypes.byref(out), ctypes.byref(size)))
         return _take(out, size.value)
 
+    def decision_bounds(self):
+        """Per promise quorum, this shard's absolute fill bound (mpx_decisions_bounds)."""
+        cnt = ctypes.c_uint64()
+        _ck("mpx_decisions_bounds", lib().mpx_decisions_bounds(self.h, None, 0, ctypes.byref(cnt)))
+        buf = (ctypes.c_uint64 * max(cnt.value, 1))()
+        _ck("mpx_decisions_bounds", lib().mpx_decisions_bounds(self.h, buf, cnt.value, ctypes.byref(cnt)))
+        return list(buf[:cnt.value])
+
+    def decisions_part(self, global_bounds):
+        """MPXP bytes: this shard's part of the decisions, fills cut at the global bounds."""
+        n = len(global_bounds)
+        buf = (ctypes.c_uint64 * max(n, 1))(*global_bounds)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_read_decisions_part",
+            lib().mpx_read_decisions_part(self.h, buf, n, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
     def commits(self):
         """MPXC bytes: every CommittingValues with its OnCommitReply retirement (mpx_read_commits)."""
         out = ctypes.POINTER(ctypes.c_uint8)()
@@ -352,3 +373,15 @@ def declared_symbols(header=INCLUDE_H):
     import re
     txt = open(header).read()
     return sorted(set(re.findall(r"^\s*(?:int|void)\s+(mpx_\w+)\s*\(", txt, re.M)))
+
+
+def decisions_combine(parts):
+    """Merge MPXP parts (shard order) into the whole run's MPXD (mpx_decisions_combine)."""
+    n = len(parts)
+    raw = [ctypes.create_string_buffer(bytes(p), max(len(p), 1)) for p in parts]   # kept alive for the call
+    arr = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in raw])
+    sizes = (ctypes.c_uint64 * n)(*[len(p) for p in parts])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    size = ctypes.c_uint64()
+    _ck("mpx_decisions_combine", lib().mpx_decisions_combine(arr, sizes, n, ctypes.byref(out), ctypes.byref(size)))
+    return _take(out, size.value)

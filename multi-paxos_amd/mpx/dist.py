@@ -4,6 +4,8 @@ Paxos instances are independent, so the instance space is split into
 contiguous, bucket-aligned shards, one per GPU; per-acceptor scalars depend
 only on replicated headers.  The one exchange is an all-gather of each rank's
 64-word summary (layout = SW_* in multi-paxos_amd/csrc/mpx_internal.hpp).
+Phase-2 decisions (f2) add one more: an all-reduce MAX of the per-quorum fill
+bounds, then a gather of the per-shard parts (gather_decisions).
 """
 MASK64 = (1 << 64) - 1
 SW_C, SW_P, SW_A, SW_L, SW_MSGS, SW_V, SW_DCHOSEN, SW_DSTATE, SW_DSCAL, SW_Q = range(10)
@@ -47,3 +49,30 @@ def combine(summaries):
     }
     out["bytes_alg"] = 16 * out["promise_entries"] + 24 * out["accept_apps"] + 16 * out["commit_apps"]
     return out
+
+
+def gather_decisions(engine, device="cpu", group=None):
+    """Phase-2 decisions of a sharded run (include/mpx.h mpx_decisions_bounds /
+    mpx_read_decisions_part / mpx_decisions_combine) over torch.distributed: every
+    rank's per-quorum fill bounds are max-reduced (the noop fill of a quorum reaches
+    the highest committed-or-adopted instance over all shards), each rank writes its
+    part, and rank 0 merges the parts in rank (= shard) order.  Returns the whole
+    run's MPXD on rank 0, None elsewhere.  `device` holds the bound tensor: "cpu"
+    for gloo, the rank's GPU for RCCL."""
+    import torch
+    import torch.distributed as dist
+    from . import decisions_combine
+    mine = engine.decision_bounds()
+    n = torch.tensor([len(mine)], dtype=torch.int64, device=device)
+    lo, hi = n.clone(), n.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    if lo.item() != hi.item():
+        raise RuntimeError("ranks disagree on the promise quorums: %d vs %d" % (lo.item(), hi.item()))
+    b = torch.tensor(mine if mine else [0], dtype=torch.int64, device=device)   # bounds <= 2^63 (instance ids)
+    dist.all_reduce(b, op=dist.ReduceOp.MAX, group=group)
+    part = engine.decisions_part([int(x) for x in b.cpu().tolist()[:len(mine)]])
+    world = dist.get_world_size(group)
+    parts = [None] * world
+    dist.all_gather_object(parts, part, group=group)
+    return decisions_combine(parts) if dist.get_rank(group) == 0 else None

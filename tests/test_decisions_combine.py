@@ -1,0 +1,70 @@
+"""CPU checks of mpx_decisions_combine (include/mpx.h): the
+host-only merge of per-shard decision parts (MPXP) into MPXD.  Parts are cut
+from the reference's own decision fixtures (tests/golden/*.mpxd) at instance
+boundaries, with the fill noops' handles blanked to ~0 as a shard writes them;
+merging them must give the fixture back byte for byte."""
+import json
+import os
+import struct
+
+import pytest
+
+import mpx
+import mpxd
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DECISIONS = sorted(json.load(open(os.path.join(GOLD, "decisions.json"))))
+NOOP_SLOT = (1 << 64) - 1
+
+
+def _handle(node, noop, vid):
+    return (node << 48) | ((1 if noop else 0) << 47) | vid
+
+
+def _parts(buf, cuts):
+    """Split MPXD into MPXP parts at the instance boundaries `cuts` (ascending)."""
+    nodes = mpxd.parse(buf)
+    begins = [0] + list(cuts)
+    out = []
+    for k, sb in enumerate(begins):
+        se = begins[k + 1] if k + 1 < len(begins) else 1 << 63
+        b = bytearray(b"MPXP" + struct.pack("<IIQ", 1, len(nodes), sb))
+        for node, ds in enumerate(nodes):
+            b += struct.pack("<Q", len(ds))
+            vid = 0
+            for seq, ents in ds:
+                mine = []
+                for iid, h in ents:
+                    fill = h == _handle(node, True, vid + 1)      # the next number of the node's fill noops
+                    if fill:
+                        vid += 1
+                    if sb <= iid < se:
+                        mine.append((iid, NOOP_SLOT if fill else h))
+                b += struct.pack("<QQ", seq, len(mine))
+                for iid, h in mine:
+                    b += struct.pack("<QQ", iid, h)
+        out.append(bytes(b))
+    return out
+
+
+@pytest.mark.parametrize("name", DECISIONS)
+def test_combine_restores_reference_decisions(name):
+    want = open(os.path.join(GOLD, name + ".mpxd"), "rb").read()
+    iids = sorted({i for ds in mpxd.parse(want) for _, ents in ds for i, _ in ents})
+    assert mpx.decisions_combine(_parts(want, [])) == want
+    if iids:
+        mid = iids[len(iids) // 2]
+        assert mpx.decisions_combine(_parts(want, [mid])) == want
+        q = [iids[len(iids) * j // 4] for j in (1, 2, 3)]
+        assert mpx.decisions_combine(_parts(want, sorted(set(x for x in q if x > 0)))) == want
+
+
+def test_combine_rejects_mismatched_parts():
+    want = open(os.path.join(GOLD, "fuzz_big_1.mpxd"), "rb").read()
+    a, b = _parts(want, [100])
+    with pytest.raises(mpx.MpxError):
+        mpx.decisions_combine([b, a])                           # not in shard order
+    with pytest.raises(mpx.MpxError):
+        mpx.decisions_combine([a, b[:-8]])                      # truncated
+    with pytest.raises(mpx.MpxError):
+        mpx.decisions_combine([a, b"MPXD" + b[4:]])             # not a part

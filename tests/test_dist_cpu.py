@@ -14,6 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import mpx
+import mpxd
 from mpx import dist as mdist
 from oracles import oracle_run
 
@@ -77,6 +78,55 @@ def test_combine_rejects_disagreeing_scalars():
     b[mdist.SW_DSCAL] = 1
     with pytest.raises(AssertionError):
         mdist.combine([a, b])
+
+
+class _FixtureShard:
+    """Stands in for one shard engine (no GPU here): its bounds and its part cut
+    from the reference's decision fixture (test_decisions_combine._parts)."""
+
+    def __init__(self, bounds, part, want_global):
+        self.bounds, self.part, self.want_global = bounds, part, want_global
+
+    def decision_bounds(self):
+        return list(self.bounds)
+
+    def decisions_part(self, gx):
+        assert gx == self.want_global                 # the element-wise maximum over ranks
+        return self.part
+
+
+def _dec_rank(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import test_decisions_combine as tdc
+        want = open(os.path.join(tdc.GOLD, "fuzz_big_1.mpxd"), "rb").read()
+        parts = tdc._parts(want, [60, 130][:world - 1])
+        nq = sum(len(ds) for ds in mpxd.parse(want))
+        bounds = [[(7 * k + r) % 200 for k in range(nq)] for r in range(world)]
+        gx = [max(col) for col in zip(*bounds)]
+        got = mdist.gather_decisions(_FixtureShard(bounds[rank], parts[rank], gx))
+        q.put((rank, got == want if rank == 0 else got is None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_decisions_over_gloo(world):
+    """mdist.gather_decisions: MAX-reduced bounds reach every rank, the parts come
+    back in rank order and rank 0's merge equals the reference's decisions."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dec_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(r, True) for r in range(world)]
 
 
 def test_bench_filegroup_rendezvous():

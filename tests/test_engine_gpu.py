@@ -517,6 +517,51 @@ def test_engine_decisions_match_oracle_c3(seed, m):
     assert got == want
 
 
+def _sharded_decisions(trace, shards, align=256):
+    """The sharded protocol of include/mpx.h: bounds per shard -> max -> parts -> combine."""
+    from mpx import dist as mdist
+    hd = mpx.trace_header(trace)
+    m = max(hd["num_instances"], 1)
+    engines = []
+    try:
+        for r in range(shards):
+            sb, se = mdist.shard_bounds(m, shards, r, align=align)
+            e = mpx.Engine(hd["num_nodes"], sb, se, semantics=hd["semantics"])
+            engines.append(e)
+            e.submit_trace(trace)
+            e.run()
+        bounds = [e.decision_bounds() for e in engines]
+        assert len({len(b) for b in bounds}) == 1            # the same promise quorums on every shard
+        gx = [max(col) for col in zip(*bounds)]
+        parts = [e.decisions_part(gx) for e in engines]
+    finally:
+        for e in engines:
+            e.close()
+    return mpx.decisions_combine(parts)
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+@pytest.mark.parametrize("name", ["fuzz_big_1", "fuzz_big_2", "c3_faulty_0", "demo_s1", "hm_promise_merge", "fuzz_007"])
+def test_sharded_decisions_match_reference(name, shards):
+    """Phase-2 decisions over instance shards (one engine per range; one
+    all-reduce-MAX of the per-quorum fill bounds, then the parts merged in shard
+    order) == the batch the reference's own OnPrepareReply built (fixture)."""
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxd")
+    assert _sharded_decisions(trace, shards, align=1) == want     # unaligned, non-empty shards of small runs
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_sharded_decisions_match_oracle_c3(shards):
+    from oracles import oracle_decisions
+    t = mpx.generate_trace(mpx.GEN_FAULTY, num_nodes=7, num_instances=1 << 13, seed=84, batch=64, proposers=3,
+                           drop_rate=500, dup_rate=1000, max_delay=500)
+    want = oracle_decisions(t)
+    with mpx.Engine.for_trace(t) as e:
+        e.run()
+        assert e.decisions() == want
+    assert _sharded_decisions(t, shards) == want
+
+
 def test_decisions_refused_for_shards_and_member():
     t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=3, num_instances=1024, batch=256)
     with mpx.Engine(3, 256, 1024) as e:
