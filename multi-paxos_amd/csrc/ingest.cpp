@@ -878,11 +878,11 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             if (!fast) { ht.gp_list.push_back(p); ht.pair_gp[p] = 1; }
         }
     // work-list order: the pairs with no snapshot events and no promise-reply runs
-    // first (multi: k_apply's SIMPLE instantiation takes them), pair order kept
-    // then those with no promise-reply runs (their events are PREPAREs only; k_apply
-    // AM_SNAP), then the rest (promise rounds)
+    // first (k_apply's SIMPLE instantiation takes them), pair order kept
+    // then those with no promise-reply runs (their events are PREPAREs only, member:
+    // and E_EPOCHs; k_apply AM_SNAP), then the rest (promise rounds)
     ht.num_gp_simple = ht.num_gp_snap = 0;
-    if (!member) {
+    {
         auto no_preply = [&](uint64_t p) {
             for (uint64_t f = ht.f_off[p]; f < ht.f_off[p + 1]; ++f)
                 if ((ht.frags[f].flags >> 4) == K_PREPLY) return false;

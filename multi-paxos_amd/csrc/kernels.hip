@@ -1745,7 +1745,13 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             emit_rows(v, hit, g, 0, ref);
                         }
                     } else if (!ROUNDS) {
-                        // (AM_SNAP: a pair without promise-reply runs gets no other event)
+                        // AM_SNAP: a pair without promise-reply runs gets no round events; member:
+                        // an E_EPOCH that deletes / recreates the Acceptor still clears it (below)
+                        if (MEMBER && t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j)
+                                if (!(SF(j) & S_COMMITTED)) { if (DIGEST) sb[j] = 0; SF_SET(j, 0); se[j] = sm[j] = 0; }
+                        }
                     } else if (t8 == MPX_MSG_P_START || (t8 == MPX_MSG_E_EPOCH && (fl & F_PRECLR))) {
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) pre[lane + 64 * j] = u64x2{0, 0};
@@ -2279,10 +2285,19 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (v.semantics == MPX_SEM_MEMBER) {
         // member: every pair walks the general kernel (insert semantics, epoch events)
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
-        if (v.num_gp) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, v.num_gp);
+        // the same three-way split as multi (ingest.cpp orders the list): event-free
+        // pairs, pairs without promise-reply runs (PREPARE / E_EPOCH events), the rest;
+        // knob 65536: one kernel over the whole list, 262144: no AM_SNAP kernel (A/B)
+        const uint64_t ns = (v.knobs & 65536) ? 0 : v.num_gp_simple;
+        const uint64_t nq = (v.knobs & (65536 | 262144)) ? ns : v.num_gp_snap;
+        if (ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
+                  else hipLaunchKernelGGL((k_apply<1, false, true, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
+        if (nq > ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq);
+                  else hipLaunchKernelGGL((k_apply<4, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq); }
+        if (v.num_gp > nq) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
                    // 4 waves / SIMD: C5 2^25 general apply 2.165 vs 2.544 ms unconstrained (variant 1)
-                   else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, v.num_gp);
-                   else hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, v.num_gp); }
+                   else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
+                   else hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
     } else {
         // multi: the lean kernel also writes the chosen log of clean buckets
         // digest runs (verification) take their own instantiation, so the
