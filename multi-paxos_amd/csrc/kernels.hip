@@ -1619,9 +1619,26 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
             }
             first = false;
             const uint32_t fmsg = (uint32_t)fw1;
+            // the window's events that can act (knob 524288: walk every listed event, A/B):
+            // a rejected PREPARE, or a member E_EPOCH that neither deletes nor recreates the
+            // node's Acceptor (nor, with rounds, resets its Proposer), changes nothing here
+            // — member pairs get every marker of their node, most of them such no-ops
+            uint64_t umask = ~0ull;
+            if (!SIMPLE && !(v.knobs & 524288)) {
+                const uint32_t t8l = einfo & 0xFF, fll = einfo >> 8;
+                bool u = t8l == MPX_MSG_PREPARE && (fll & F_GRANTED);
+                if (MEMBER) u = u || (t8l == MPX_MSG_E_EPOCH && (fll & (ROUNDS ? (F_ACCCLR | F_PRECLR) : F_ACCCLR)));
+                if (ROUNDS) u = u || t8l == MPX_MSG_P_START || (t8l == MPX_MSG_PREPARE_REPLY && (fll & F_QUORUM));
+                umask = __ballot(lane < ne && u);
+            }
             // merge-walk fragments and events by message index
             uint32_t a = 0, c = 0;
             for (;;) {
+                if (!SIMPLE) {                            // step over the no-op events
+                    const uint64_t r = c < 64 ? umask >> c : 0;
+                    c = r ? c + (uint32_t)__builtin_ctzll(r) : ne;
+                    if (c > ne) c = ne;
+                }
                 const bool fmore = a < nf, emore = c < ne;
                 if ((!fmore && fi + nf < fe) || (!emore && ei + ne < ee) || (!fmore && !emore)) break;
                 const uint32_t fm = fmore ? rl32(fmsg, a) : NONE32;
