@@ -1706,13 +1706,27 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             }
                     } else if (ROUNDS && kind == K_PREPLY) {
                         if ((mf & F_COUNTED) && !(v.knobs & 8192)) {       // knob 8192: experiment, no merge
+                            if (!(v.knobs & 1048576)) {
+                                // the run's proposal ids all in flight, then the merge
+                                // (knob 1048576: one load per slot in turn, A/B)
+                                uint64_t pid[SPL];
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j)
+                                    if (k[j] >= 0) {
+                                        const u64x2 cur = pre[lane + 64 * j];
+                                        if (!cur.y || pid[j] > cur.x) pre[lane + 64 * j] = u64x2{pid[j], W_PRESENT | (ent + k[j])};   // :1216-1221
+                                    }
+                            } else {
 #pragma unroll 1
-                            for (uint32_t j = 0; j < SPL; ++j)
-                                if (k[j] >= 0) {
-                                    const uint64_t pid = v.r_pid[ent + k[j]];
-                                    const u64x2 cur = pre[lane + 64 * j];
-                                    if (!cur.y || pid > cur.x) pre[lane + 64 * j] = u64x2{pid, W_PRESENT | (ent + k[j])};   // :1216-1221
-                                }
+                                for (uint32_t j = 0; j < SPL; ++j)
+                                    if (k[j] >= 0) {
+                                        const uint64_t pid = v.r_pid[ent + k[j]];
+                                        const u64x2 cur = pre[lane + 64 * j];
+                                        if (!cur.y || pid > cur.x) pre[lane + 64 * j] = u64x2{pid, W_PRESENT | (ent + k[j])};
+                                    }
+                            }
                         }
                     }
                     ++a;
