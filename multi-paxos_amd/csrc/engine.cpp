@@ -86,6 +86,7 @@ struct mpx_engine {
     DevBuf decode_buf;                      // readback scratch (k_decode)
     DevBuf out, out_cursor, partials, viol, summary;
     uint64_t out_cap = 0;
+    uint32_t out_subs = 64;
     DevView view{};
     LaunchGeom geom{};
     uint64_t num_msgs = 0;
@@ -328,9 +329,14 @@ static int finish_view(mpx_engine *e)
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + std::max<uint64_t>(e->geom.chosen_wgs, e->num_cus * 16))));
     TRY(e->viol.alloc(sizeof(DevViolation)));
     TRY(e->summary.alloc(64 * 8));
-    TRY(e->out_cursor.alloc(8ull * OUT_STRIDE * OUT_SUBS));
+    e->out_subs = 64;
+    if (const char *x = std::getenv("MPX_OUT_SUBS")) {  // A/B: snapshot sub-buffers (power of two)
+        const uint32_t k = (uint32_t)std::atoi(x);
+        if (k && !(k & (k - 1)) && k <= OUT_SUBS) e->out_subs = k;
+    }
+    TRY(e->out_cursor.alloc(8ull * OUT_STRIDE * e->out_subs));
     if (!e->out_cap) e->out_cap = 1 << 12;               // records per sub-buffer
-    TRY(e->out.alloc(OUT_SUBS * e->out_cap * sizeof(OutRec)));
+    TRY(e->out.alloc((uint64_t)e->out_subs * e->out_cap * sizeof(OutRec)));
     TRY(e->node_scal.alloc(16ull * N));
     v.st = e->st.p;
     v.st_valid = e->st_valid.as<uint8_t>();
@@ -341,6 +347,7 @@ static int finish_view(mpx_engine *e)
     v.out = e->out.as<OutRec>();
     v.out_cursor = e->out_cursor.as<unsigned long long>();
     v.out_cap = e->out_cap;
+    v.out_subs = e->out_subs;
     v.partials = e->partials.as<unsigned long long>();
     v.viol = e->viol.as<DevViolation>();
     v.summary = e->summary.as<unsigned long long>();
@@ -524,14 +531,14 @@ static int collect(mpx_engine *e)
     HTRY(hipMemcpy(e->last_summary.data(), e->summary.p, 64 * 8, hipMemcpyDeviceToHost));
     uint64_t cursor = 0;
     {
-        std::vector<uint64_t> cur(OUT_STRIDE * OUT_SUBS);
+        std::vector<uint64_t> cur(OUT_STRIDE * e->out_subs);
         HTRY(hipMemcpy(cur.data(), e->out_cursor.p, 8 * cur.size(), hipMemcpyDeviceToHost));
-        for (uint32_t s = 0; s < OUT_SUBS; ++s) cursor = std::max<uint64_t>(cursor, cur[OUT_STRIDE * s]);
+        for (uint32_t s = 0; s < e->out_subs; ++s) cursor = std::max<uint64_t>(cursor, cur[OUT_STRIDE * s]);
     }
     if (cursor > e->out_cap) {
         // a snapshot sub-buffer overflowed: grow and run again (runs are deterministic)
         e->out_cap = cursor + cursor / 4;
-        TRY(e->out.alloc(OUT_SUBS * e->out_cap * sizeof(OutRec)));
+        TRY(e->out.alloc((uint64_t)e->out_subs * e->out_cap * sizeof(OutRec)));
         e->view.out = e->out.as<OutRec>();
         e->view.out_cap = e->out_cap;
         TRY(queue_run(e, e->view.digest != 0));
@@ -817,13 +824,14 @@ static int fetch_results(mpx_engine *e, Results &r)
     TRY(d2h(r.maxseen, e->m_maxseen, G));
     TRY(d2h(r.scal, e->node_scal, 2ull * e->cfg.num_nodes));
     {
-        std::vector<uint64_t> cur(OUT_STRIDE * OUT_SUBS);
+        std::vector<uint64_t> cur(OUT_STRIDE * e->out_subs);
         HTRY(hipMemcpy(cur.data(), e->out_cursor.p, 8 * cur.size(), hipMemcpyDeviceToHost));
         std::vector<OutRec> part;
         const HostTrace &h = e->ht;
         const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
-        for (uint32_t s = 0; s < OUT_SUBS; ++s) {
+        for (uint32_t s = 0; s < e->out_subs; ++s) {
             const uint64_t k = std::min<uint64_t>(cur[OUT_STRIDE * s], e->out_cap);
+            if (!k) continue;
             TRY(d2h(part, e->out, k, (size_t)s * e->out_cap));
             for (const OutRec &o : part) {
                 // resolve the reference (mpx_internal.hpp OutRec) against the host trace

@@ -672,7 +672,7 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
 #pragma unroll
     for (uint32_t j = 0; j < SPL_; ++j) { m[j] = __ballot(want[j]); tot += (uint32_t)__popcll(m[j]); }
     if (!tot) return;
-    const uint32_t sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (OUT_SUBS - 1);
+    const uint32_t sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (v.out_subs - 1);
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(&v.out_cursor[OUT_STRIDE * sub], (unsigned long long)tot);
     base = __shfl(base, 0, 64);
@@ -1941,7 +1941,7 @@ __global__ void k_reset(DevView v, uint32_t n_partials)
     if (i < v.NB) v.chosen_valid[i] = 0;
     if (i < 8ull * n_partials) v.partials[i] = 0;
     if (i < 2ull * v.N) v.node_scal[i] = 0;    // nodes without messages keep promised = max_seen = 0
-    if (i < OUT_SUBS) v.out_cursor[OUT_STRIDE * i] = 0;
+    if (i < v.out_subs) v.out_cursor[OUT_STRIDE * i] = 0;
     if (i == 0) {
         *v.fast_rest = 0;
         v.viol->code = v.viol->node = v.viol->seq = v.viol->iid = v.viol->count = 0;
@@ -2288,6 +2288,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (v.NB > reset_n) reset_n = v.NB;
     if (8ull * n_partials > reset_n) reset_n = 8ull * n_partials;
     if (2ull * v.N > reset_n) reset_n = 2ull * v.N;
+    if (v.out_subs > reset_n) reset_n = v.out_subs;
     // Phase events ride on kernel dispatches (hipExtLaunchKernelGGL start / stop events) where a
     // kernel begins or ends the phase: a separate event record costs a 5-10 us bubble between
     // dependent kernels (rocprof, C4: 16 us of a 395 us step)

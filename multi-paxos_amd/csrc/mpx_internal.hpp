@@ -149,10 +149,11 @@ struct OutEnt {
     uint64_t handle;
 };
 
-// snapshot output: OUT_SUBS sub-buffers with their own cursors, a wave appends
-// to sub (wave id mod OUT_SUBS) — the host sorts records by message and iid, so
+// snapshot output: out_subs (a power of two <= OUT_SUBS, 64 by default; env
+// MPX_OUT_SUBS at create) sub-buffers with their own cursors, a wave appends to
+// sub (wave id mod out_subs) — the host sorts records by message and iid, so
 // their order is free and the append needs no single global atomic
-constexpr uint32_t OUT_SUBS = 64;
+constexpr uint32_t OUT_SUBS = 4096;
 constexpr uint32_t GP_WORDS = 8;
 constexpr uint32_t OUT_STRIDE = 16;
 
@@ -265,6 +266,7 @@ struct DevView {
     OutRec *out;
     unsigned long long *out_cursor;  // OUT_SUBS cursors, one per 128-byte line (stride OUT_STRIDE words)
     uint64_t out_cap;               // records per sub-buffer: sub s owns out[s * out_cap .. (s + 1) * out_cap)
+    uint32_t out_subs;              // sub-buffers in use (power of two <= OUT_SUBS)
     unsigned long long *partials;   // 8 words per apply workgroup, then chosen workgroups
     DevViolation *viol;
     unsigned long long *summary;    // 64 words
