@@ -145,7 +145,7 @@ def c3_leg(args, kind="c3"):
     apply_ms = general_ms + fast_ms
     b_alg = 16 * st["promise_entries"] + 24 * st["accept_apps"] + 16 * st["commit_apps"]
     achieved = b_alg / (apply_ms * 1e-3) / 1e9 if apply_ms else 0.0
-    pmc = None if member else latest_pmc(7, m, 1, workload="C3")
+    pmc = latest_pmc(8 if member else 7, m, 1, workload="C5" if member else "C3")
     ms_step = dt / steps * 1e3
     if member:
         workload = ("C5: 2^%d instances, member semantics, acceptor universe 8, AddAcceptor(1..7) then "
@@ -168,7 +168,8 @@ def c3_leg(args, kind="c3"):
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
                      "traffic_source": ("profiles/%s_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the apply "
-                                        "phase, bench.py --c3-only; not measured inside this process)" % pmc["tag"])
+                                        "phase, bench.py --%s-only; not measured inside this process)"
+                                        % (pmc["tag"], "c5" if member else "c3"))
                      if pmc else None},
         "verified": {"step_state_digest_vs_run": step_ok, "state_digest": chk["state_digest"],
                      "chosen_digest": chk["chosen_digest"]},
@@ -264,7 +265,7 @@ def latest_pmc(n_nodes, instances, world, workload="C4"):
             continue
         if d.get("workload", "C4").split()[0] != workload:
             continue
-        if workload == "C3" or (d.get("nodes") == n_nodes and d.get("instances") == instances and
+        if workload in ("C3", "C5") or (d.get("nodes") == n_nodes and d.get("instances") == instances and
                                 d.get("gpus", 1) == world):
             best = d
     return best

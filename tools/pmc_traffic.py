@@ -12,6 +12,7 @@ profiles/, where bench.py picks them up as roofline.traffic.
 
     python tools/pmc_traffic.py --tag r01 [bench args...]
     python tools/pmc_traffic.py --tag r02_c3 --c3 --sq     (C3 general path, + SQ wave-state pass)
+    python tools/pmc_traffic.py --tag r02_c5 --c5          (C5 member path)
 """
 import argparse
 import csv
@@ -56,9 +57,12 @@ def main():
     ap.add_argument("--instances", type=int, default=1 << 27)
     ap.add_argument("--nodes", type=int, default=9)
     ap.add_argument("--c3", action="store_true", help="the C3 general-path leg (bench.py --c3-only)")
+    ap.add_argument("--c5", action="store_true", help="the C5 member leg (bench.py --c5-only)")
     ap.add_argument("--sq", action="store_true", help="also one pass of SQ wave-state counters")
     a, rest = ap.parse_known_args()
-    if a.c3:
+    if a.c5:
+        bench_args = ["--c5-only", "--c5-steps", "3"] + rest
+    elif a.c3:
         bench_args = ["--c3-only", "--c3-steps", "3"] + rest
     else:
         bench_args = ["--steps", "3", "--warmup", "0", "--instances", str(a.instances), "--nodes", str(a.nodes),
@@ -66,7 +70,8 @@ def main():
     fetch = run_pass(["FETCH_SIZE"], a.outdir, bench_args, a.tag)["FETCH_SIZE"]
     write = run_pass(["WRITE_SIZE"], a.outdir, bench_args, a.tag)["WRITE_SIZE"]
     sq = run_pass(SQ_COUNTERS, a.outdir, bench_args, a.tag) if a.sq else {}
-    out = {"tag": a.tag, "workload": "C3 2^24 x 7 (bench.py --c3-only)" if a.c3 else "C4",
+    out = {"tag": a.tag, "workload": "C5 2^25 member (bench.py --c5-only)" if a.c5 else
+           "C3 2^24 x 7 (bench.py --c3-only)" if a.c3 else "C4",
            "instances": a.instances, "nodes": a.nodes, "gpus": 1, "kernels": {}}
     mean = lambda xs: sum(xs) / len(xs) if xs else 0.0
     for name in sorted(set(fetch) | set(write)):
@@ -83,7 +88,7 @@ def main():
     # C3 adds the general k_apply of the timed steps
     phase = [v for k, v in out["kernels"].items()
              if "k_plan" in k or "k_store" in k or ("k_apply_fast" in k and "true>" in k and "false" in k)
-             or (a.c3 and re.search(r"k_apply<\d+, false", k))]   # k_apply<waves, DIGEST, ...>: not the digested run's
+             or ((a.c3 or a.c5) and re.search(r"k_apply<\d+, false", k))]   # k_apply<waves, DIGEST, ...>: not the digested run's
     out["apply_phase_kernels"] = [k for k, v in out["kernels"].items() if v in phase]
     out["hbm_bytes_per_launch"] = sum(v["hbm_bytes_per_launch"] for v in phase) if phase else None
     out["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"
