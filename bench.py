@@ -77,6 +77,10 @@ def parse():
     ap.add_argument("--c5-instances", type=int, default=1 << 25, help="C5 member-path leg: M (2^25); 0 = skip")
     ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--c5-only", action="store_true", help="only the C5 leg (profiling)")
+    ap.add_argument("--shard-of", type=int, default=8,
+                    help="also time rank 0's shard of the same trace at world G on this GPU (a 1-GPU scaling "
+                         "projection, no RCCL); 0 / 1 = skip")
+    ap.add_argument("--shard-only", action="store_true", help="only the shard projection (profiling)")
     return ap.parse_args()
 
 
@@ -186,9 +190,15 @@ class FileGroup:
 
     def __init__(self, rank, world):
         self.rank, self.world, self.k = rank, world, 0
-        key = "%s_%d" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
-        self.dir = os.path.join("/tmp", "mpx_bench_" + key)
+        # torchrun gives every rank of one launch the same TORCHELASTIC_RUN_ID: a crashed
+        # earlier launch on the same port never shares its directory; without it the ranks'
+        # common parent (one launcher process) keys it
+        rid = os.environ.get("TORCHELASTIC_RUN_ID")
+        key = "%s_%s" % (os.environ.get("MASTER_PORT", "0"), rid if rid else "p%d" % os.getppid())
+        self.dir = os.path.join("/tmp", "mpx_bench_" + re.sub(r"[^A-Za-z0-9_.-]", "_", key))
         os.makedirs(self.dir, exist_ok=True)
+        if os.path.exists(os.path.join(self.dir, "r1_%d" % rank)):
+            raise RuntimeError("rendezvous directory %s holds an earlier run's files" % self.dir)
 
     def _put(self, name, data):
         tmp = os.path.join(self.dir, ".%s.%d" % (name, self.rank))
@@ -253,8 +263,12 @@ def broadcast_bytes(pg, data, rank):
 
 
 def latest_pmc(n_nodes, instances, world, workload="C4"):
-    """HBM bytes per apply-phase launch from the newest profiles/*pmc*.json of this config."""
+    """HBM bytes per apply-phase launch from the newest profiles/*pmc*.json measured on this
+    workload (nodes, instances, GPUs) AND with these kernels (the engine's source digest, as
+    tools/pmc_traffic.py records it); None — reported as traffic null — when no profile matches."""
     best = None
+    digest = mpx.source_digest()
+
     def natural(path):                              # r01_v10 after r01_v9
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
 
@@ -263,10 +277,9 @@ def latest_pmc(n_nodes, instances, world, workload="C4"):
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("workload", "C4").split()[0] != workload:
+        if d.get("workload", "C4").split()[0] != workload or d.get("source_digest") != digest:
             continue
-        if workload in ("C3", "C5") or (d.get("nodes") == n_nodes and d.get("instances") == instances and
-                                d.get("gpus", 1) == world):
+        if d.get("nodes") == n_nodes and d.get("instances") == instances and d.get("gpus", 1) == world:
             best = d
     return best
 
@@ -284,9 +297,30 @@ def clean_expect(n_nodes, sb, se, ballot=1 << 16):
     return a.value, b.value
 
 
+def host_cpus():
+    """(cores this process may run on, nproc, the cgroup CPU quota in cores or None)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return usable, os.cpu_count() or usable, quota
+
+
+def cpu_note():
+    usable, nproc, quota = host_cpus()
+    return "nproc %d, usable %d%s" % (nproc, usable, ", cgroup quota %.1f cores" % quota if quota else "")
+
+
 def cpu_baseline(args, budget_s):
-    """Reference handlers (oracle/_ref) on host cores: node 1's accept+commit stream of a clean trace."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    """Reference handlers (oracle/_ref) on every usable host core: node 1's accept+commit stream
+    of a clean trace, one independent replay per thread."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libmpx_ref.so")
     kind = "reference"
     if not os.path.exists(ref_so):
@@ -301,7 +335,7 @@ def cpu_baseline(args, budget_s):
     t0 = time.perf_counter()
     fn(trace, len(trace), 1, 1)
     one = time.perf_counter() - t0
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = host_cpus()[0]
     reps = max(1, int(budget_s / max(one, 1e-6)))
     done = [0] * threads
 
@@ -321,39 +355,105 @@ def cpu_baseline(args, budget_s):
     return {"value": decisions / dt, "unit": "decisions/s", "cores": threads, "kind": kind,
             "sample": "reference multi/paxos.cpp handlers (-O2) on node 1's stream of a clean C4-shaped trace: "
                       "%d instances x %d passes x %d threads, accept+commit (OnAccept/OnCommit), %.1f s wall; "
-                      "decisions/s = acceptor-instance applications/s / N=%d" % (sample_m, reps, threads, dt, args.nodes),
+                      "decisions/s = acceptor-instance applications/s / N=%d (%s)"
+                      % (sample_m, reps, threads, dt, args.nodes, cpu_note()),
             "node_instance_apps_per_s": apps / dt}
 
 
+def native_oracle():
+    """oracle/mpx_oracle.c compiled here with -O2 -march=native (the CPU
+    restatement built for this host's CPU); the prebuilt generic one when gcc is missing."""
+    import subprocess
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), "mpx_oracle_native_%d.so" % os.getpid())
+    try:
+        subprocess.check_call(["gcc", "-O2", "-march=native", "-std=gnu99", "-fPIC", "-shared", "-o", out,
+                               os.path.join(ROOT, "oracle", "mpx_oracle.c"), "-lpthread"],
+                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        return out, "-O2 -march=native (built on this host)"
+    except (OSError, subprocess.CalledProcessError):
+        return os.path.join(ROOT, "oracle", "_build", "libmpx_oracle.so"), "-O2 generic (gcc unavailable here)"
+
+
 def cpu_port_baseline(args, budget_s):
-    """The build's own CPU restatement (oracle/mpx_oracle.c, gcc -O2) over a clean
-    C4-shaped trace on the host's cores: every node's stream on its own thread, instance shards
-    in parallel (mpxo_run_sharded), counters + digests only.  Not -march=native: the checker is
-    built in the build container and runs on the GPU box's host, whose CPU may differ."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracles import oracle_run_sharded
-    sample_m = 1 << 18
+    """The build's own CPU restatement (oracle/mpx_oracle.c, SURVEY §8(d)(ii): -O2 -march=native,
+    every usable host core) over a clean C4-shaped trace: instance shards in parallel
+    (mpxo_run_sharded), each shard every node's stream on its own thread; counters + digests only."""
+    so, flags = native_oracle()
+    lib = ctypes.CDLL(so)
+    f = lib.mpxo_run_sharded
+    f.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
+    f.restype = ctypes.c_int
+    cores = host_cpus()[0]
+    shards = max(1, cores // args.nodes)              # shards x N node threads = the usable cores
+    sample_m = max(1 << 18, shards << 15)
     trace = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=args.nodes, num_instances=sample_m, batch=256, copy=False)
-    cores = max(1, min(16, os.cpu_count() or 1))      # the box's CPU share per GPU (16)
-    shards = max(1, cores // args.nodes)
+    stats = (ctypes.c_uint64 * 8)()
+
+    def once():
+        if f(trace, len(trace), shards, shards, stats) != 0:
+            raise RuntimeError("mpxo_run_sharded failed")
+
     t0 = time.perf_counter()
-    st = oracle_run_sharded(trace, shards=shards, threads=shards)
+    once()
     one = time.perf_counter() - t0
-    assert st[0] == sample_m
+    assert stats[0] == sample_m
     reps = max(1, int(budget_s / max(one, 1e-6)))
     t0 = time.perf_counter()
     for _ in range(reps):
-        oracle_run_sharded(trace, shards=shards, threads=shards)
+        once()
     dt = time.perf_counter() - t0
+    if so.startswith("/tmp") or "mpx_oracle_native" in so:
+        try:
+            os.remove(so)
+        except OSError:
+            pass
     return {"value": reps * sample_m / dt, "unit": "decisions/s", "cores": shards * args.nodes, "kind": "port",
-            "sample": "oracle/mpx_oracle.c (the build's C restatement, -O2) over a clean C4-shaped trace of %d "
-                      "instances x %d acceptors, every node's stream on its own thread x %d instance shards, "
-                      "%d passes in %.1f s (nproc here: %d; 16 = this GPU's host CPU share)"
-                      % (sample_m, args.nodes, shards, reps, dt, os.cpu_count() or 0)}
+            "sample": "oracle/mpx_oracle.c (the build's C restatement, %s) over a clean C4-shaped trace of %d "
+                      "instances x %d acceptors: %d instance shards x %d node threads, %d passes in %.1f s (%s)"
+                      % (flags, sample_m, args.nodes, shards, args.nodes, reps, dt, cpu_note())}
+
+
+def shard_projection(args, t1_ms):
+    """Rank 0's instance shard of the headline trace at world G, run alone on this GPU: the
+    per-rank work of a G-GPU strong-scaling run without its RCCL all-gather.  eff = T1 / (G * T_shard)
+    is a projection, not a scaling measurement (instance shards are independent)."""
+    G, M, N = args.shard_of, args.instances, args.nodes
+    sb, se = mdist.shard_bounds(M, G, 0)
+    eng = mpx.Engine(N, sb, se)
+    eng.load_clean_device(num_instances=M, batch=args.batch)
+    for _ in range(max(args.warmup, 3)):
+        eng.step()
+    eng.sync()
+    eng.timings()
+    steps = max(args.steps, 50)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.step()
+    eng.sync()
+    dt = time.perf_counter() - t0
+    ph = eng.timings_detail()
+    st = eng.stats()
+    want = clean_expect(N, sb, se)
+    ok = eng.state_digest() == want and st["chosen"] == se - sb
+    eng.close()
+    assert ok, "shard projection: the step's state differs from the closed form"
+    t_shard = dt / steps * 1e3
+    out = {"G": G, "shard": [sb, se], "steps": steps, "T1_ms": t1_ms, "T_shard_ms": t_shard,
+           "eff": t1_ms / (G * t_shard) if t1_ms else None,
+           "phases_ms": {k: sum(p[k] for p in ph) / max(len(ph), 1) for k in mpx.Engine.PHASES},
+           "verified": ok,
+           "note": "projection, no RCCL: rank 0's shard of the same trace timed alone on one GPU"}
+    log("shard-of-%d: %.4f ms per step (T1 %.4f ms): projected efficiency %.3f" %
+        (G, t_shard, t1_ms or 0.0, out["eff"] or 0.0))
+    return out
 
 
 def main():
     args = parse()
+    if args.shard_only:
+        print(json.dumps({"scaling_projection": shard_projection(args, None)}), flush=True)
+        return
     if args.c3_only:
         print(json.dumps({"c3": c3_leg(args)}), flush=True)
         return
@@ -434,12 +534,17 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, args.cpu_seconds)
             cpu_port = cpu_port_baseline(args, args.cpu_seconds / 2)
+        proj = shard_projection(args, ms_per_step) if world == 1 and args.shard_of > 1 else None
         c3 = c3_leg(args) if world == 1 and args.c3_instances else None
         c5 = None
         if world == 1 and args.c5_instances:
-            try:                                    # a secondary leg: its failure is reported, not fatal
-                c5 = c3_leg(args, "c5")
-            except Exception as ex:                 # noqa: BLE001
+            try:                                    # a secondary leg: out of memory is reported, not fatal;
+                c5 = c3_leg(args, "c5")             # a wrong result (AssertionError) or any other error is
+            except MemoryError as ex:               # fatal
+                c5 = {"error": repr(ex)}
+            except mpx.MpxError as ex:
+                if ex.rc != -2:                     # MPX_E_NOMEM
+                    raise
                 c5 = {"error": repr(ex)}
         out = {
             "metric": METRIC,
@@ -476,6 +581,7 @@ def main():
                                  "c3.roofline is the per-slot general path on the survey's bytes"},
             "cpu_baseline": cpu,
             "cpu_baseline_port": cpu_port,
+            **({"scaling_projection": proj} if proj else {}),
             "c3": c3,
             **({"c5": c5} if c5 else {}),
             "verified": {"step_state_digest_vs_closed_form": step_ok, "step_state_digest": step_state,

@@ -156,7 +156,10 @@ typedef struct mpx_stats {
     uint64_t bytes_alg;        /* 16 P + 24 A + 16 L                               */
     uint64_t skipped;          /* submitted records left out: all their entries
                                   belong to other shards (header sharding)       */
-    uint64_t reserved[2];
+    uint64_t general_pairs;    /* (node, bucket) pairs the general per-slot walk
+                                  (k_apply) took in the last run: its work list, or
+                                  in a member step what k_plan_member left to it  */
+    uint64_t reserved[1];
 } mpx_stats;
 
 typedef struct mpx_violation {
@@ -345,6 +348,22 @@ int  mpx_comm_init(mpx_engine *eng, const uint8_t uid[MPX_UID_BYTES],
 /* All-gather every rank's 64-word run summary (mpx_stats words + per-node
  * scalars) over RCCL on the engine's stream; out holds nranks*64 words. */
 int  mpx_allgather_summary(mpx_engine *eng, uint64_t *out);
+/* Element-wise MAX of `n` u64 over every rank of the engine's communicator
+ * (ncclAllReduce over xGMI on the engine's stream), in place in a host buffer.
+ * Without a communicator (or one rank) the values stay as they are. */
+int  mpx_comm_allreduce_max(mpx_engine *eng, uint64_t *vals, uint64_t n);
+/* All-gather of one byte string per rank: *out (malloc'ed; free with mpx_free)
+ * = every rank's string in rank order, lens[r] = rank r's length (nranks
+ * entries).  Lengths go first (one u64 all-gather), then the strings padded to
+ * the longest. */
+int  mpx_comm_allgather_bytes(mpx_engine *eng, const uint8_t *mine, uint64_t len,
+                              uint8_t **out, uint64_t *lens);
+/* Sharded phase-2 decisions over the engine's own communicator (ranks = shards
+ * in instance order): mpx_decisions_bounds, mpx_comm_allreduce_max (also of the
+ * quorum count, which must agree), mpx_read_decisions_part, the parts gathered
+ * with mpx_comm_allgather_bytes and merged with mpx_decisions_combine.  Every
+ * rank receives the whole run's MPXD.  One rank: mpx_read_decisions' bytes. */
+int  mpx_read_decisions_sharded(mpx_engine *eng, uint8_t **out, uint64_t *size);
 
 #ifdef __cplusplus
 }

@@ -83,6 +83,7 @@ struct mpx_engine {
     uint64_t num_frags = 0;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
     DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy, exec_aux, exec_out;
+    DevBuf gp_dyn, gp_dyn_n;                // member plan path: the pairs k_plan_member lists for k_apply
     DevBuf decode_buf;                      // readback scratch (k_decode)
     DevBuf out, out_cursor, partials, viol, summary;
     uint64_t out_cap = 0;
@@ -100,6 +101,7 @@ struct mpx_engine {
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
     DevBuf gather_buf;
+    DevBuf comm_buf, comm_buf2;             // mpx_comm_allreduce_max / mpx_comm_allgather_bytes
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? MPX_OK : MPX_E_HIP; }
@@ -319,6 +321,11 @@ static int finish_view(mpx_engine *e)
     v.frag_w1 = e->frag_w1.as<uint64_t>();
     TRY(e->fast_rest.alloc(8));
     TRY(e->store_dummy.alloc(64 * 1024));
+    // member: k_plan_member lists at most the work list's non-round pairs
+    TRY(e->gp_dyn.alloc(std::max<size_t>(8ull * GP_WORDS * (v.semantics == MPX_SEM_MEMBER ? v.num_gp_snap : 0), 8 * GP_WORDS)));
+    TRY(e->gp_dyn_n.alloc(8));
+    v.gp_dyn = e->gp_dyn.as<uint64_t>();
+    v.gp_dyn_n = e->gp_dyn_n.as<unsigned long long>();
     const uint64_t npairs = (uint64_t)N * e->NB;
     // k_apply_fast holds 5 waves/SIMD (82 VGPRs); 8 workgroups of 4 waves per
     // CU measured best on C4 (tools/ab_apply.py: 2.17 ms vs 2.31 ms at 5)
@@ -551,6 +558,12 @@ static int collect(mpx_engine *e)
     st.skipped = e->device_trace ? 0 : e->ht.dropped;
     st.chosen_digest = s[SW_DCHOSEN]; st.state_digest = s[SW_DSTATE]; st.scalar_digest = s[SW_DSCAL];
     st.bytes_alg = 16 * st.promise_entries + 24 * st.accept_apps + 16 * st.commit_apps;
+    st.general_pairs = e->view.num_gp;
+    if (e->cfg.semantics == MPX_SEM_MEMBER && !e->view.digest && !(e->view.knobs & 64)) {
+        uint64_t listed = 0;                         // k_plan_member's list + the promise-round pairs
+        HTRY(hipMemcpy(&listed, e->gp_dyn_n.p, 8, hipMemcpyDeviceToHost));
+        st.general_pairs = listed + (e->view.num_gp - e->view.num_gp_snap);
+    }
     if (e->ev_used) {
         StepEvents &x = e->ev_pool[e->ev_used - 1];
         float a = 0, r = 0;
@@ -1200,7 +1213,7 @@ extern "C" int mpx_decisions_combine(const uint8_t *const *parts, const uint64_t
     std::vector<P> ps(nparts);
     uint32_t N = 0;
     for (uint32_t i = 0; i < nparts; ++i) {
-        if (!parts[i] || sizes[i] < 20 || std::memcmp(parts[i], "MPXP", 4)) return MPX_E_INVAL;
+        if (!parts[i] || sizes[i] < 20 || std::memcmp(parts[i], "MPXP", 4) || rd32(parts[i] + 4) != 1) return MPX_E_INVAL;
         const uint32_t n = rd32(parts[i] + 8);
         if (i && n != N) return MPX_E_INVAL;
         N = n;
@@ -1231,9 +1244,12 @@ extern "C" int mpx_decisions_combine(const uint8_t *const *parts, const uint64_t
                 if (i && sq != seq) return MPX_E_INVAL;
                 seq = sq;
                 if (!need(ps[i], 16 * m)) return MPX_E_INVAL;
+                // a part holds only its own shard's instances: [its shard_begin, the next part's)
+                const uint64_t lo = ps[i].sb, hi = i + 1 < nparts ? ps[i + 1].sb : ~0ull;
                 for (uint64_t j = 0; j < m; ++j) {
                     const uint64_t iid = rd64(ps[i].p + ps[i].pos), h = rd64(ps[i].p + ps[i].pos + 8);
                     ps[i].pos += 16;
+                    if (iid < lo || iid >= hi) return MPX_E_INVAL;
                     app<uint64_t>(ents, iid);
                     app<uint64_t>(ents, h == NOOP_SLOT ? MPX_HANDLE(node, 1, ++vid) : h);
                 }
@@ -1243,6 +1259,8 @@ extern "C" int mpx_decisions_combine(const uint8_t *const *parts, const uint64_t
             d += ents;
         }
     }
+    for (uint32_t i = 0; i < nparts; ++i)
+        if (ps[i].pos != ps[i].n) return MPX_E_INVAL;                // trailing bytes: another layout
     *out = (uint8_t *)std::malloc(d.size() ? d.size() : 1);
     if (!*out) return MPX_E_NOMEM;
     std::memcpy(*out, d.data(), d.size());
@@ -1589,4 +1607,85 @@ extern "C" int mpx_allgather_summary(mpx_engine *e, uint64_t *out)
     }
     HTRY(hipStreamSynchronize(e->stream));
     return MPX_OK;
+}
+
+extern "C" int mpx_comm_allreduce_max(mpx_engine *e, uint64_t *vals, uint64_t n)
+{
+    if (!e || (n && !vals)) return MPX_E_INVAL;
+    if (!e->comm || e->nranks <= 1 || !n) return MPX_OK;
+    HTRY(hipSetDevice(e->device));
+    TRY(e->comm_buf.alloc(8 * n));
+    HTRY(hipMemcpyAsync(e->comm_buf.p, vals, 8 * n, hipMemcpyHostToDevice, e->stream));
+    if (ncclAllReduce(e->comm_buf.p, e->comm_buf.p, n, ncclUint64, ncclMax, e->comm, e->stream) != ncclSuccess)
+        return MPX_E_COMM;
+    HTRY(hipMemcpyAsync(vals, e->comm_buf.p, 8 * n, hipMemcpyDeviceToHost, e->stream));
+    HTRY(hipStreamSynchronize(e->stream));
+    return MPX_OK;
+}
+
+extern "C" int mpx_comm_allgather_bytes(mpx_engine *e, const uint8_t *mine, uint64_t len, uint8_t **out, uint64_t *lens)
+{
+    if (!e || (len && !mine) || !out || !lens) return MPX_E_INVAL;
+    const int R = e->comm ? e->nranks : 1;
+    if (R <= 1) {
+        *out = (uint8_t *)std::malloc(len ? len : 1);
+        if (!*out) return MPX_E_NOMEM;
+        if (len) std::memcpy(*out, mine, len);
+        lens[0] = len;
+        return MPX_OK;
+    }
+    HTRY(hipSetDevice(e->device));
+    // the lengths, then every string padded to the longest (one all-gather each)
+    TRY(e->comm_buf.alloc(8ull * (R + 1)));
+    uint64_t *dl = e->comm_buf.as<uint64_t>();
+    HTRY(hipMemcpyAsync(dl, &len, 8, hipMemcpyHostToDevice, e->stream));
+    if (ncclAllGather(dl, dl + 1, 1, ncclUint64, e->comm, e->stream) != ncclSuccess) return MPX_E_COMM;
+    HTRY(hipMemcpyAsync(lens, dl + 1, 8ull * R, hipMemcpyDeviceToHost, e->stream));
+    HTRY(hipStreamSynchronize(e->stream));
+    uint64_t mx = 0, tot = 0;
+    for (int r = 0; r < R; ++r) { mx = std::max(mx, lens[r]); tot += lens[r]; }
+    const uint64_t w = (mx + 7) & ~7ull;
+    if (!w) { *out = (uint8_t *)std::malloc(1); return *out ? MPX_OK : MPX_E_NOMEM; }
+    TRY(e->comm_buf2.alloc(w * (R + 1)));
+    uint8_t *db = e->comm_buf2.as<uint8_t>();
+    HTRY(hipMemsetAsync(db, 0, w, e->stream));
+    if (len) HTRY(hipMemcpyAsync(db, mine, len, hipMemcpyHostToDevice, e->stream));
+    if (ncclAllGather(db, db + w, w, ncclUint8, e->comm, e->stream) != ncclSuccess) return MPX_E_COMM;
+    std::vector<uint8_t> all(w * R);
+    HTRY(hipMemcpyAsync(all.data(), db + w, w * R, hipMemcpyDeviceToHost, e->stream));
+    HTRY(hipStreamSynchronize(e->stream));
+    *out = (uint8_t *)std::malloc(tot ? tot : 1);
+    if (!*out) return MPX_E_NOMEM;
+    uint64_t at = 0;
+    for (int r = 0; r < R; ++r) { std::memcpy(*out + at, all.data() + w * r, lens[r]); at += lens[r]; }
+    return MPX_OK;
+}
+
+extern "C" int mpx_read_decisions_sharded(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    const int R = e->comm ? e->nranks : 1;
+    if (R <= 1 && e->cfg.shard_begin == 0) return mpx_read_decisions(e, out, size);
+    uint64_t cnt = 0;
+    TRY(mpx_decisions_bounds(e, nullptr, 0, &cnt));
+    std::vector<uint64_t> b(cnt + 2);
+    TRY(mpx_decisions_bounds(e, b.data(), cnt, &cnt));
+    // the quorum count must agree on every rank: MAX of (count, ~count) gives max and ~min
+    b[cnt] = cnt; b[cnt + 1] = ~cnt;
+    TRY(mpx_comm_allreduce_max(e, b.data(), cnt + 2));
+    if (b[cnt] != cnt || ~b[cnt + 1] != cnt) return MPX_E_INVAL;
+    uint8_t *part = nullptr;
+    uint64_t plen = 0;
+    TRY(mpx_read_decisions_part(e, b.data(), cnt, &part, &plen));
+    std::vector<uint64_t> lens(R);
+    uint8_t *all = nullptr;
+    int rc = mpx_comm_allgather_bytes(e, part, plen, &all, lens.data());
+    std::free(part);
+    if (rc) return rc;
+    std::vector<const uint8_t *> ps(R);
+    uint64_t at = 0;
+    for (int r = 0; r < R; ++r) { ps[r] = all + at; at += lens[r]; }
+    rc = mpx_decisions_combine(ps.data(), lens.data(), (uint32_t)R, out, size);
+    std::free(all);
+    return rc;
 }

@@ -892,6 +892,10 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         ht.num_gp_snap = (uint64_t)(mid - ht.gp_list.begin());
         auto mid2 = std::stable_partition(ht.gp_list.begin(), mid, [&](uint64_t p) { return !ht.pair_ev[p]; });
         ht.num_gp_simple = (uint64_t)(mid2 - ht.gp_list.begin());
+        // member: k_plan_member takes the pairs before `mid` (or lists them for k_apply
+        // itself); the promise-round pairs stay on the host range of the full kernel
+        if (member)
+            for (auto it = mid; it != ht.gp_list.end(); ++it) ht.pair_gp[*it] = GP_ROUNDS;
     }
     // slots for sparse fragments
     if (ht.any_sparse) {

@@ -1260,6 +1260,60 @@ __device__ inline uint64_t plan_pack(const uint32_t (&val)[4], const uint32_t (&
            ((uint64_t)s[0] << 32) | ((uint64_t)s[1] << 41) | ((uint64_t)s[2] << 50);
 }
 
+// The chosen-log plan word of bucket i (row N; k_plan, k_plan_member): every live
+// batch run of the bucket (its votes reached quorum, k_votes) contributes its
+// instances (OnAcceptReply -> Commit, multi/paxos.cpp:1416-1421); when at most
+// four segments describe the bucket and no instance lies under two live runs
+// (k_chosen compares their Values) the word is written and chosen_valid set,
+// else PLAN_SKIP leaves the bucket to k_chosen.
+__device__ inline void plan_chosen(const DevView &v, uint64_t i, unsigned long long &cC)
+{
+    constexpr uint32_t F = PLAN_FRAGS;
+    const uint64_t oc = v.cf_off[i], c1 = v.cf_off[i + 1];
+    const uint32_t len = (uint32_t)(c1 - oc);
+    uint64_t q = PLAN_SKIP;
+    if (len && len <= F && (i + 1) * BS <= v.shard_len) {
+        uint64_t w[F];
+        uint32_t live[F];
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) w[k] = k < len ? frag_w1(v.cfrags + oc + k) : 0;
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) live[k] = k < len ? v.b_chosen[(uint32_t)w[k]] != NONE32 : 0;
+        bool ok = true;
+        uint32_t sp[3] = {BS, BS, BS};
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) {
+            if (k >= len) continue;
+            const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
+            ok = ok && ((w[k] >> 56) & FR_DENSE) && plan_add_split(st0, sp) && plan_add_split(st0 + cnt, sp);
+        }
+        uint32_t val[4];
+        unsigned long long c = 0;
+#pragma unroll
+        for (uint32_t g = 0; g < 4; ++g) {
+            const uint32_t lo = g ? sp[g - 1] : 0, hi = g < 3 ? sp[g] : BS;
+            if (lo >= BS) { val[g] = val[g - 1]; continue; }
+            uint32_t fix = NONE32;
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k) {
+                if (k >= len || !live[k]) continue;
+                const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
+                if (lo < st0 || lo >= st0 + cnt) continue;
+                if (fix != NONE32) ok = false;                    // two chosen runs: k_chosen compares Values
+                else fix = k;
+            }
+            val[g] = fix == NONE32 ? 0 : fix + 1;
+            if (fix != NONE32) c += hi - lo;
+        }
+        if (ok) {
+            q = plan_pack(val, sp);
+            v.chosen_valid[i] = 1;
+            cC = c;
+        }
+    }
+    v.plan[(uint64_t)v.N * v.NB + i] = q;
+}
+
 // Apply split in two (the default for multi runs): k_plan decides every pair
 // with one thread per pair — no per-step chain, so its gathers (CSR offsets,
 // up to PLAN_FRAGS descriptors and scan flags) all overlap — and k_store
@@ -1365,51 +1419,7 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
         if (q == PLAN_SKIP && in_list) rest = 1;
         v.plan[i] = q;
     }
-    if (i < NB) {
-        const uint64_t oc = v.cf_off[i], c1 = v.cf_off[i + 1];
-        const uint32_t len = (uint32_t)(c1 - oc);
-        uint64_t q = PLAN_SKIP;
-        if (len && len <= F && (i + 1) * BS <= v.shard_len) {
-            uint64_t w[F];
-            uint32_t live[F];
-#pragma unroll
-            for (uint32_t k = 0; k < F; ++k) w[k] = k < len ? frag_w1(v.cfrags + oc + k) : 0;
-#pragma unroll
-            for (uint32_t k = 0; k < F; ++k) live[k] = k < len ? v.b_chosen[(uint32_t)w[k]] != NONE32 : 0;
-            bool ok = true;
-            uint32_t sp[3] = {BS, BS, BS};
-#pragma unroll
-            for (uint32_t k = 0; k < F; ++k) {
-                if (k >= len) continue;
-                const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
-                ok = ok && ((w[k] >> 56) & FR_DENSE) && plan_add_split(st0, sp) && plan_add_split(st0 + cnt, sp);
-            }
-            uint32_t val[4];
-            unsigned long long c = 0;
-#pragma unroll
-            for (uint32_t g = 0; g < 4; ++g) {
-                const uint32_t lo = g ? sp[g - 1] : 0, hi = g < 3 ? sp[g] : BS;
-                if (lo >= BS) { val[g] = val[g - 1]; continue; }
-                uint32_t fix = NONE32;
-#pragma unroll
-                for (uint32_t k = 0; k < F; ++k) {
-                    if (k >= len || !live[k]) continue;
-                    const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
-                    if (lo < st0 || lo >= st0 + cnt) continue;
-                    if (fix != NONE32) ok = false;                    // two chosen runs: k_chosen compares Values
-                    else fix = k;
-                }
-                val[g] = fix == NONE32 ? 0 : fix + 1;
-                if (fix != NONE32) c += hi - lo;
-            }
-            if (ok) {
-                q = plan_pack(val, sp);
-                v.chosen_valid[i] = 1;
-                cC = c;
-            }
-        }
-        v.plan[(uint64_t)N * NB + i] = q;
-    }
+    if (i < NB) plan_chosen(v, i, cC);
     unsigned long long cc[3] = {cA, cL, cC};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -1431,6 +1441,193 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
     } else if (threadIdx.x == 3) {
         const uint32_t r = rest_w[0] + rest_w[1] + rest_w[2] + rest_w[3];
         if (r) atomicAdd(v.fast_rest, r);
+    }
+}
+
+// Member plan path (the timed member step): k_plan's reduction for member semantics
+// (member/paxos.cpp:1744-1793 Acceptor::OnAccept / OnLearn, :1029-1060
+// Learner::OnLearn, :1952-1957 Acceptor deletion), one thread per (node, bucket)
+// pair.  Accept and learn are std::map::insert, so per instance the state is fixed
+// by the FIRST learn covering it (the learned Value sticks, and an accepted entry of
+// a learned instance is never made), else by the first granted accept after the
+// last marker that deleted or recreated the node's Acceptor (F_ACCCLR: its accepted
+// map goes, learned entries stay with the Learner).  Runs cut the bucket into at
+// most four segments (plan_add_split); within a segment every run covers all or
+// none of it, so the pair walks its runs and its snapshot events (E_EPOCH markers,
+// PREPAREs) in message order with four segment states instead of 256 slot states,
+// and one plan word (k_store / k_store8 stream it) holds the result.  The counters
+// follow the per-slot walk exactly: A = inserts, L = every learn-covered slot.
+//
+// The pair is listed for k_apply instead (gp_dyn, one append per wave) when:
+// more than MPLAN_FRAGS runs, a run that is not a dense accept / learn run, a fifth
+// segment, a partial last bucket, a granted PREPARE while any segment holds an
+// entry (FilterAcceptedValues emits a snapshot, :1700-1727), an accept / learn over
+// a learned segment whose Value entry differs (the reference's Value check, :1763-
+// 1769), or any other event type.  Promise-round pairs (GP_ROUNDS) are never taken:
+// the host range of the full k_apply has them.  Bucket i < NB also plans its chosen
+// log (plan_chosen).  The staged descriptor words carry the accept runs' scan flag
+// (F_GRANTED) in bit 57 after the gather, so the walk reads only LDS.
+constexpr uint64_t MP_GRANTED = 1ull << 57;
+__global__ __launch_bounds__(256) void k_plan_member(DevView v, uint32_t apply_wgs)
+{
+    constexpr uint32_t F = MPLAN_FRAGS;
+    __shared__ uint64_t w_lds[4][MPLAN_LDS];
+    __shared__ unsigned long long red[4][3];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t N = v.N;
+    const uint64_t NB = v.NB, np = (uint64_t)N * NB;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    unsigned long long cA = 0, cL = 0, cC = 0;
+    const uint64_t ic = i < np ? i : np, in = i < np ? i + 1 : np;
+    const uint64_t oa = v.f_off[ic], o1 = v.f_off[in];
+    const uint64_t e0 = v.ev_off[ic], e1 = v.ev_off[in];
+    const uint8_t gp = i < np ? v.pair_gp[i] : 0;
+    const uint64_t wbase = rl64(oa, 0);
+    {
+        // the wave's runs are one contiguous descriptor range: their second words
+        // into LDS with coalesced loads, all in flight before the LDS writes
+        const uint64_t wend = rl64(o1, 63);
+        const uint32_t R = (uint32_t)(wend - wbase < MPLAN_LDS ? wend - wbase : MPLAN_LDS);
+        constexpr uint32_t K = 4;
+        for (uint32_t r0 = 0; r0 < R; r0 += 64 * K) {
+            uint64_t x[K];
+#pragma unroll
+            for (uint32_t k = 0; k < K; ++k) {
+                const uint32_t r = r0 + lane + 64 * k;
+                x[k] = r < R ? v.frag_w1[wbase + r] : 0;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < K; ++k) {
+                const uint32_t r = r0 + lane + 64 * k;
+                if (r < R) w_lds[wv][r] = x[k];
+            }
+        }
+        wave_lds_fence();
+    }
+    bool fb = false;                                   // list the pair for k_apply
+    if (i < np) {
+        const uint32_t len = (uint32_t)(o1 - oa);
+        const uint64_t rel = oa - wbase, b = i / N;
+        uint64_t q = PLAN_SKIP;
+        if (len && gp == GP_LIST) {
+            bool ok = len <= F && rel + len <= MPLAN_LDS && (b + 1) * BS <= v.shard_len;
+            uint64_t *const W = &w_lds[wv][ok ? rel : 0];
+            uint32_t sp[3] = {BS, BS, BS};
+            if (ok) {
+                for (uint32_t k = 0; k < len; ++k) {
+                    const uint64_t w = W[k];
+                    const uint32_t cnt = (uint32_t)(w >> 32) & 0xFFFF, st0 = (uint32_t)(w >> 48) & 0xFF;
+                    ok = ok && frag_lean(w) && plan_add_split(st0, sp) && plan_add_split(st0 + cnt, sp);
+                }
+            }
+            if (ok) {
+                // the accept runs' scan flags, all in flight, then folded into bit 57
+                uint32_t fg[F];
+#pragma unroll
+                for (uint32_t k = 0; k < F; ++k) {
+                    const uint64_t w = k < len ? W[k] : 0;
+                    fg[k] = k < len && (w >> 60) == K_ACCEPT ? v.m_flags[(uint32_t)w] : 0;
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < F; ++k)
+                    if (k < len && (fg[k] & F_GRANTED)) W[k] |= MP_GRANTED;
+                uint32_t lo[4], sl[4], pres = 0, comm = 0, fix[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (uint32_t g = 0; g < 4; ++g) {
+                    lo[g] = g ? sp[g - 1] : 0;
+                    sl[g] = lo[g] >= BS ? 0 : (g < 3 ? sp[g] : BS) - lo[g];
+                }
+                // the entry index of run k at slot s, minus s (the pool is
+                // content-addressed: equal ones name one Value; read only over a
+                // learned segment)
+                auto ent_at = [&](uint32_t k) -> uint64_t {
+                    return v.frags[oa + k].entry - ((W[k] >> 48) & 0xFF);
+                };
+                auto run = [&](uint32_t k) {
+                    const uint64_t w = W[k];
+                    const uint32_t cnt = (uint32_t)(w >> 32) & 0xFFFF, st0 = (uint32_t)(w >> 48) & 0xFF;
+                    const bool learn = (w >> 60) == K_COMMIT;
+                    if (!learn && !(w & MP_GRANTED)) return;          // a rejected / dropped accept
+#pragma unroll
+                    for (uint32_t g = 0; g < 4; ++g) {
+                        if (!sl[g] || lo[g] < st0 || lo[g] >= st0 + cnt) continue;
+                        if (learn) cL += sl[g];
+                        if ((comm >> g) & 1) {
+                            if (ent_at(k) != ent_at(fix[g])) fb = true;   // the Value check: k_apply
+                        } else if (learn) {
+                            comm |= 1u << g; pres |= 1u << g; fix[g] = k;
+                        } else if (!((pres >> g) & 1)) {
+                            pres |= 1u << g; fix[g] = k; cA += sl[g];
+                        }
+                    }
+                };
+                auto event = [&](uint32_t info) {
+                    const uint32_t t8 = info & 0xFF, fl = info >> 8;
+                    if (t8 == MPX_MSG_E_EPOCH) {
+                        if (fl & F_ACCCLR) pres &= comm;               // the Acceptor's accepted map goes
+                    } else if (t8 == MPX_MSG_PREPARE) {
+                        if ((fl & F_GRANTED) && pres) fb = true;       // a snapshot to emit: k_apply
+                    } else {
+                        fb = true;
+                    }
+                };
+                uint32_t k = 0;
+                for (uint64_t e = e0; e < e1 && !fb; e += 8) {
+                    const uint32_t m = (uint32_t)(e1 - e < 8 ? e1 - e : 8);
+                    uint32_t em[8], ei[8];
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; ++j) em[j] = j < m ? v.ev_msg[e + j] : NONE32;
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; ++j)
+                        ei[j] = j < m ? (uint32_t)v.m_type[em[j]] | ((uint32_t)v.m_flags[em[j]] << 8) : 0;
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; ++j) {
+                        if (j >= m) break;
+                        while (k < len && (uint32_t)W[k] <= em[j]) run(k++);   // a message's runs before its event
+                        event(ei[j]);
+                    }
+                }
+                while (k < len && !fb) run(k++);
+                if (!fb) {
+                    uint32_t val[4];
+#pragma unroll
+                    for (uint32_t g = 0; g < 4; ++g)
+                        val[g] = !sl[g] ? val[g ? g - 1 : 0] : ((pres >> g) & 1) ? fix[g] + 1 : 0;
+                    q = plan_pack(val, sp);
+                    v.st_valid[i] = 1;
+                }
+            } else {
+                fb = true;
+            }
+            if (fb) cA = cL = 0;
+        }
+        v.plan[i] = q;
+    }
+    const uint64_t fm = __ballot(fb);
+    if (fm) {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(v.gp_dyn_n, (unsigned long long)__popcll(fm));
+        base = __shfl(base, 0, 64);
+        if (fb) {
+            uint64_t *w = v.gp_dyn + GP_WORDS * (base + (uint64_t)__popcll(fm & ((1ull << lane) - 1)));
+            w[0] = oa; w[1] = o1; w[2] = e0; w[3] = e1; w[4] = i;
+        }
+    }
+    if (i < NB) plan_chosen(v, i, cC);
+    unsigned long long cc[3] = {cA, cL, cC};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        unsigned long long x = cc[k];
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        cc[k] = x;
+    }
+    if (lane == 0) { red[wv][0] = cc[0]; red[wv][1] = cc[1]; red[wv][2] = cc[2]; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const uint32_t t = threadIdx.x;
+        const unsigned long long x = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+        const int slot = t == 0 ? PC_A : t == 1 ? PC_L : PC_C;
+        if (x) atomicAdd(&v.partials[8 * (blockIdx.x % apply_wgs) + slot], x);
     }
 }
 
@@ -1603,6 +1800,7 @@ enum { AM_FULL = 0, AM_SIMPLE = 1, AM_SNAP = 2 };
 template <int WAVES_PER_EU, bool DIGEST, bool MEMBER, int MODE = AM_FULL>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t it0, uint64_t it1)
 {
+    if (it1 == ~0ull) it1 = *v.gp_dyn_n;          // the device-built list (k_plan_member)
     __shared__ uint16_t lidx_all[4][BS];
     __shared__ u64x2 pre_all[4][BS];           // pre-accepted merge (pid, PRESENT | r-entry): rare, kept in LDS
     __shared__ unsigned long long red[4][8];
@@ -2025,6 +2223,7 @@ __global__ void k_reset(DevView v, uint32_t n_partials)
     if (i < v.out_subs) v.out_cursor[OUT_STRIDE * i] = 0;
     if (i == 0) {
         *v.fast_rest = 0;
+        *v.gp_dyn_n = 0;
         v.viol->code = v.viol->node = v.viol->seq = v.viol->iid = v.viol->count = 0;
     }
 }
@@ -2393,9 +2592,37 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (v.pc_multi) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s, v);
     }
     if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
-    const bool plan_path = v.semantics != MPX_SEM_MEMBER && !v.digest && !(v.knobs & 64) && v.N <= FAST_MAX_NODES;
+    const bool member = v.semantics == MPX_SEM_MEMBER;
+    // member plan path (k_plan_member + store + k_apply over what it lists); knob 64: the
+    // walk of every pair (as the digested run), A/B
+    const bool mplan = member && !v.digest && !(v.knobs & 64);
+    const bool plan_path = (!member && !v.digest && !(v.knobs & 64) && v.N <= FAST_MAX_NODES) || mplan;
     if (ev_apply0 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
-    if (v.semantics == MPX_SEM_MEMBER) {
+    // the plan words of every (row, bucket) -> state rows and the chosen log
+    auto launch_store = [&](hipEvent_t stop) {
+        if (v.slot_w == 1 && (v.knobs & 128))
+            hipExtLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
+        // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64
+        else if (v.slot_w == 1 && (v.knobs & 2048))
+            hipExtLaunchKernelGGL((k_store8<true, 64>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
+        else if (v.slot_w == 1)
+            hipExtLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
+        else
+            hipExtLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
+    };
+    if (mplan) {
+        hipExtLaunchKernelGGL(k_plan_member, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s,
+                              (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+        launch_store((hipEvent_t)ev_apply1);
+        // the pairs k_plan_member listed (their count is on the device), then the promise rounds
+        DevView vd = v;
+        vd.gp_list = v.gp_dyn;
+        hipLaunchKernelGGL((k_apply<4, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
+        if (v.num_gp > v.num_gp_snap) {
+            if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
+            else hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
+        }
+    } else if (member) {
         // member: every pair walks the general kernel (insert semantics, epoch events)
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         // the same three-way split as multi (ingest.cpp orders the list): event-free
@@ -2424,11 +2651,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
             // (the chosen-log buckets on threads of their own after the pairs: 63.5 vs 61.5 us at C4)
             hipExtLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
-            if (v.slot_w == 1 && (v.knobs & 128)) hipLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
-            // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64
-            else if (v.slot_w == 1 && (v.knobs & 2048)) hipLaunchKernelGGL((k_store8<true, 64>), dim3(g.store_wgs), dim3(256), 0, s, v);
-            else if (v.slot_w == 1) hipLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, v);
-            else hipLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, v);
+            launch_store(nullptr);
             hipExtLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s,
                                   (hipEvent_t)nullptr, (hipEvent_t)ev_apply1, 0, v);
         } else switch (g.variant) {

@@ -225,6 +225,10 @@ struct DevView {
     uint64_t num_gp_snap;           // ... then up to here: no promise-reply runs (PREPARE events only)
     const uint64_t *gp_list;        // general-apply work items, GP_WORDS each: the pair's fragment CSR
                                     // range, its event CSR range, the pair q (one coalesced load per item)
+    // member plan path (k_plan_member): the pairs it cannot describe by one plan word are
+    // appended here (GP_WORDS per item, as gp_list) for k_apply; gp_dyn_n counts them
+    uint64_t *gp_dyn;
+    unsigned long long *gp_dyn_n;
     const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
     const uint32_t *ev_msg;
     // promise-quorum chunks (k_prop_chunk / k_prop_node): PROP_CHUNK records of one
@@ -285,6 +289,12 @@ constexpr uint32_t FAST_MAX_FRAGS = 63;
 // events; ingest.cpp / mpx_load_clean_device put every other pair on the work
 // list of the general k_apply (pair_gp = 1).  All static: no run-time flag enters.
 constexpr uint32_t PLAN_FRAGS = 8;
+// member semantics: every pair with runs is on the work list (pair_gp = GP_LIST), the
+// ones with promise-reply runs (promise rounds: k_apply AM_FULL only) are GP_ROUNDS
+enum : uint8_t { GP_LIST = 1, GP_ROUNDS = 2 };
+// k_plan_member: runs per pair it plans (walked from LDS) and runs a wave stages
+constexpr uint32_t MPLAN_FRAGS = 16;
+constexpr uint32_t MPLAN_LDS = 1024;
 // the distinct run boundaries inside (0, 256), sorted into s[0..2] (BS = unused);
 // false once a fourth one appears
 MPX_HD inline bool plan_add_split(uint32_t x, uint32_t (&s)[3])

@@ -49,7 +49,7 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "chosen", "promise_entries", "accept_apps", "commit_apps", "messages", "violations",
         "chosen_digest", "state_digest", "scalar_digest", "device_ns", "apply_ns", "ingest_ns",
-        "bytes_alg", "skipped", "r1", "r2")]
+        "bytes_alg", "skipped", "general_pairs", "r2")]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if not f.startswith("r")}
@@ -115,6 +115,9 @@ def lib():
             "mpx_comm_unique_id": [u8p],
             "mpx_comm_init": [vp, u8p, ctypes.c_int, ctypes.c_int],
             "mpx_allgather_summary": [vp, u64p],
+            "mpx_comm_allreduce_max": [vp, u64p, ctypes.c_uint64],
+            "mpx_comm_allgather_bytes": [vp, ctypes.c_char_p, ctypes.c_uint64, P(u8p), u64p],
+            "mpx_read_decisions_sharded": [vp, P(u8p), u64p],
         }
         for name, args in sig.items():
             f = getattr(L, name)
@@ -362,10 +365,54 @@ class Engine:
         _ck("mpx_comm_init", lib().mpx_comm_init(self.h, buf, rank, nranks))
         self.nranks = nranks
 
+    def allreduce_max(self, vals):
+        """Element-wise MAX over the ranks (RCCL, mpx_comm_allreduce_max); identity without a communicator."""
+        buf = (ctypes.c_uint64 * max(len(vals), 1))(*vals)
+        _ck("mpx_comm_allreduce_max", lib().mpx_comm_allreduce_max(self.h, buf, len(vals)))
+        return list(buf[:len(vals)])
+
+    def allgather_bytes(self, data, nranks=1):
+        """Every rank's byte string, in rank order (RCCL, mpx_comm_allgather_bytes)."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        lens = (ctypes.c_uint64 * max(nranks, 1))()
+        _ck("mpx_comm_allgather_bytes", lib().mpx_comm_allgather_bytes(self.h, bytes(data), len(data),
+                                                                        ctypes.byref(out), lens))
+        blob = _take(out, sum(lens))
+        parts, at = [], 0
+        for n in lens:
+            parts.append(blob[at:at + n])
+            at += n
+        return parts
+
+    def decisions_sharded(self):
+        """The whole run's MPXD from this rank's shard over the engine's communicator
+        (mpx_read_decisions_sharded: bounds all-reduce MAX, parts all-gather, combine)."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_read_decisions_sharded",
+            lib().mpx_read_decisions_sharded(self.h, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
     def allgather_summary(self, nranks=1):
         out = (ctypes.c_uint64 * (64 * nranks))()
         _ck("mpx_allgather_summary", lib().mpx_allgather_summary(self.h, out))
         return [list(out[64 * r: 64 * (r + 1)]) for r in range(nranks)]
+
+
+def source_digest():
+    """16 hex digits of SHA-256 over the engine's sources (csrc/*, include/mpx.h): what a
+    committed PMC profile was measured with (tools/pmc_traffic.py), so bench.py can refuse
+    a profile of other kernels."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(os.path.dirname(HERE), "csrc")
+    for path in sorted(os.listdir(csrc)) + [INCLUDE_H]:
+        full = path if os.path.isabs(path) else os.path.join(csrc, path)
+        if os.path.isfile(full):
+            h.update(os.path.basename(full).encode() + b"\0")
+            with open(full, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def declared_symbols(header=INCLUDE_H):

@@ -51,28 +51,37 @@ def combine(summaries):
     return out
 
 
-def gather_decisions(engine, device="cpu", group=None):
+class EngineExchange:
+    """The two collectives of the sharded decisions over the engine's own RCCL
+    communicator (libmpx: mpx_comm_allreduce_max, mpx_comm_allgather_bytes)."""
+
+    def __init__(self, engine, nranks):
+        self.engine, self.nranks = engine, nranks
+
+    def allreduce_max(self, vals):
+        return self.engine.allreduce_max(vals)
+
+    def allgather(self, data):
+        return self.engine.allgather_bytes(data, self.nranks)
+
+
+def gather_decisions(engine, exchange, rank=0):
     """Phase-2 decisions of a sharded run (include/mpx.h mpx_decisions_bounds /
-    mpx_read_decisions_part / mpx_decisions_combine) over torch.distributed: every
-    rank's per-quorum fill bounds are max-reduced (the noop fill of a quorum reaches
-    the highest committed-or-adopted instance over all shards), each rank writes its
-    part, and rank 0 merges the parts in rank (= shard) order.  Returns the whole
-    run's MPXD on rank 0, None elsewhere.  `device` holds the bound tensor: "cpu"
-    for gloo, the rank's GPU for RCCL."""
-    import torch
-    import torch.distributed as dist
+    mpx_read_decisions_part / mpx_decisions_combine): every rank's per-quorum fill
+    bounds are max-reduced (the noop fill of a quorum reaches the highest
+    committed-or-adopted instance over all shards), each rank writes its part, and
+    the parts are merged in rank (= shard) order.  `exchange` provides
+    allreduce_max(list of u64) and allgather(bytes) -> [bytes per rank]:
+    EngineExchange (RCCL inside libmpx; mpx_read_decisions_sharded is the same flow in
+    one native call) or any other transport.  Returns the whole run's MPXD on rank 0,
+    None elsewhere."""
     from . import decisions_combine
     mine = engine.decision_bounds()
-    n = torch.tensor([len(mine)], dtype=torch.int64, device=device)
-    lo, hi = n.clone(), n.clone()
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
-    if lo.item() != hi.item():
-        raise RuntimeError("ranks disagree on the promise quorums: %d vs %d" % (lo.item(), hi.item()))
-    b = torch.tensor(mine if mine else [0], dtype=torch.int64, device=device)   # bounds <= 2^63 (instance ids)
-    dist.all_reduce(b, op=dist.ReduceOp.MAX, group=group)
-    part = engine.decisions_part([int(x) for x in b.cpu().tolist()[:len(mine)]])
-    world = dist.get_world_size(group)
-    parts = [None] * world
-    dist.all_gather_object(parts, part, group=group)
-    return decisions_combine(parts) if dist.get_rank(group) == 0 else None
+    n = len(mine)
+    # the quorum count must agree: MAX of (n, ~n) yields the max and the complemented min
+    chk = exchange.allreduce_max([n, MASK64 ^ n])
+    if chk[0] != n or (MASK64 ^ chk[1]) != n:
+        raise RuntimeError("ranks disagree on the promise quorums: %d .. %d" % (MASK64 ^ chk[1], chk[0]))
+    bounds = exchange.allreduce_max(mine) if mine else []
+    parts = exchange.allgather(engine.decisions_part(bounds))
+    return decisions_combine(parts) if rank == 0 else None

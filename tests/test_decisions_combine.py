@@ -68,3 +68,23 @@ def test_combine_rejects_mismatched_parts():
         mpx.decisions_combine([a, b[:-8]])                      # truncated
     with pytest.raises(mpx.MpxError):
         mpx.decisions_combine([a, b"MPXD" + b[4:]])             # not a part
+    with pytest.raises(mpx.MpxError):
+        mpx.decisions_combine([a, b + b"\0" * 16])              # trailing bytes
+    with pytest.raises(mpx.MpxError):
+        mpx.decisions_combine([a, b[:4] + struct.pack("<I", 2) + b[8:]])   # another layout version
+
+
+def test_combine_rejects_entries_outside_their_shard():
+    """A part may only hold instances of its own shard: [its shard_begin, the next part's)."""
+    want = open(os.path.join(GOLD, "fuzz_big_1.mpxd"), "rb").read()
+    iids = sorted({i for ds in mpxd.parse(want) for _, ents in ds for i, _ in ents})
+    mid = iids[len(iids) // 2]
+    a, b = _parts(want, [mid])
+    # re-label part b as beginning one past its first instance: its entries now start below it
+    b2 = b[:12] + struct.pack("<Q", mid + 1) + b[20:]
+    with pytest.raises(mpx.MpxError):
+        mpx.decisions_combine([a, b2])
+    # and part a claiming an instance of b's range
+    a2 = _parts(want, [mid + 1])[0]
+    with pytest.raises(mpx.MpxError):
+        mpx.decisions_combine([a2, b])

@@ -95,6 +95,24 @@ class _FixtureShard:
         return self.part
 
 
+class _GlooExchange:
+    """The exchange gather_decisions needs, over torch.distributed gloo (test transport;
+    on GPUs the engine's RCCL communicator does it: mdist.EngineExchange)."""
+
+    def __init__(self, world):
+        self.world = world
+
+    def allreduce_max(self, vals):
+        got = [None] * self.world
+        dist.all_gather_object(got, list(vals))
+        return [max(col) for col in zip(*got)] if vals else []
+
+    def allgather(self, data):
+        got = [None] * self.world
+        dist.all_gather_object(got, bytes(data))
+        return got
+
+
 def _dec_rank(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -106,7 +124,7 @@ def _dec_rank(rank, world, port, q):
         nq = sum(len(ds) for ds in mpxd.parse(want))
         bounds = [[(7 * k + r) % 200 for k in range(nq)] for r in range(world)]
         gx = [max(col) for col in zip(*bounds)]
-        got = mdist.gather_decisions(_FixtureShard(bounds[rank], parts[rank], gx))
+        got = mdist.gather_decisions(_FixtureShard(bounds[rank], parts[rank], gx), _GlooExchange(world), rank)
         q.put((rank, got == want if rank == 0 else got is None))
     finally:
         dist.destroy_process_group()

@@ -319,10 +319,45 @@ def test_engine_matches_oracle_c5_member(seed, u, m, b, drop, dup):
     with mpx.Engine.for_trace(t) as e:
         st = e.run()
         got = e.dump()
-    assert got == want, mpxr.diff(got, want)
+        assert got == want, mpxr.diff(got, want)
+        _step_path(e, want, st)                 # k_plan_member + store + the pairs it listed
     assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
     assert st["chosen"] == m and st["violations"] == 0
+
+
+@pytest.mark.parametrize("seed,u,m,b,drop,dup", [(41, 8, 1 << 15, 256, 100, 100), (42, 6, 20000, 200, 300, 300),
+                                                  (43, 8, 1 << 14, 90, 0, 0), (44, 4, 9000, 33, 500, 500),
+                                                  (45, 8, (1 << 15) + 77, 256, 1000, 1000)])
+def test_member_plan_path(seed, u, m, b, drop, dup):
+    """The member step's plan path (k_plan_member: one plan word per (node, bucket) pair,
+    member/paxos.cpp:1744-1793 insert-first accept / learn, Acceptor deletion at E_EPOCH
+    markers) equals the oracle through the step, and plans most pairs: the general walk
+    takes only what it lists (snapshots to emit, Value checks, > 4 segments or > 16 runs)."""
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=u, num_instances=m, seed=seed, batch=b,
+                           drop_rate=drop, dup_rate=dup, max_delay=64, noop_permille=15)
+    want, ostats, _ = oracle_run(t)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        assert e.dump() == want
+        walked = st["general_pairs"]
+        e.step()
+        e.sync()
+        step = e.stats()
+        assert [step[k] for k in STATS_ORDER[:5]] == ostats[:5]
+        assert e.state_digest() == (ostats[6], ostats[5])
+        assert e.dump() == want
+        if b >= 200:
+            assert step["general_pairs"] * 4 < walked, (step["general_pairs"], walked)
+        # the walk of every pair in the step (knob 64) agrees too
+        os.environ["MPX_KNOBS"] = "64"
+        try:
+            e.step()
+            e.sync()
+            assert e.stats()["general_pairs"] == walked
+            assert e.dump() == want
+        finally:
+            del os.environ["MPX_KNOBS"]
 
 
 def test_engine_member_violations():
@@ -336,6 +371,11 @@ def test_engine_member_violations():
     assert got == want, mpxr.diff(got, want)
     assert st["violations"] == ostats[4] == 3
     assert v["code"] in (3, 6)
+    with mpx.Engine.for_trace(t) as e:              # the step: the plan lists the pairs with Value checks
+        e.step()
+        e.sync()
+        assert e.stats()["violations"] == 3
+        assert e.dump() == want
 
 
 @pytest.mark.parametrize("shards", [2, 3])

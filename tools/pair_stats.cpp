@@ -1,0 +1,115 @@
+// pair_stats.cpp — shape of a generated trace's (node, bucket) pairs after ingest
+// (host only: the generators + ingest.cpp, no GPU).  Used to size the member
+// plan path (how many pairs one plan word can describe, events per pair).
+//   tools/pair_stats <member|faulty> <log2 instances>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "gen.hpp"
+#include "ingest.hpp"
+
+using namespace mpx;
+
+static uint32_t rd32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
+static uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
+
+int main(int argc, char **argv)
+{
+    const bool member = argc > 1 && !std::strcmp(argv[1], "member");
+    const uint32_t lg = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 20;
+    mpx_gen_params p{};
+    p.num_instances = 1ull << lg;
+    if (member) {
+        p.kind = MPX_GEN_MEMBER; p.num_nodes = 8; p.batch = 256; p.drop_rate = 100; p.dup_rate = 100;
+        p.max_delay = 64; p.noop_permille = 15;
+    } else {
+        p.kind = MPX_GEN_FAULTY; p.num_nodes = 7; p.batch = 256; p.proposers = 3; p.drop_rate = 500;
+        p.dup_rate = 1000; p.max_delay = 500;
+    }
+    std::string t;
+    int rc = member ? gen_member(p, t) : gen_faulty(p, t);
+    if (rc) { std::fprintf(stderr, "gen rc %d\n", rc); return 1; }
+    const uint8_t *b = (const uint8_t *)t.data();
+    const uint32_t N = rd32(b + 8), ne = rd32(b + 24);
+    const uint64_t M = rd64(b + 16);
+    std::vector<mpx_epoch> ep(ne);
+    if (ne) std::memcpy(ep.data(), b + 40, (size_t)ne * 24);
+    size_t pos = 40 + (size_t)ne * 24;
+    std::vector<NodeStream> nodes(N);
+    ValueTable vt;
+    vt.member = member;
+    IngestViolation iv;
+    for (uint32_t n = 0; n < N; ++n) {
+        const uint64_t cnt = rd64(b + pos), nb = rd64(b + pos + 8);
+        const uint64_t *offs = reinterpret_cast<const uint64_t *>(b + pos + 16);
+        const uint8_t *bytes = b + pos + 16 + 8 * (cnt + 1);
+        for (uint64_t i = 0; i < cnt; ++i) {
+            rc = member ? decode_record_member(vt, nodes[n], n, bytes + offs[i], offs[i + 1] - offs[i], 0, M, iv)
+                        : decode_record(vt, nodes[n], n, N, bytes + offs[i], offs[i + 1] - offs[i], 0, M, iv);
+            if (rc) { std::fprintf(stderr, "decode rc %d\n", rc); return 1; }
+        }
+        pos += 16 + 8 * (cnt + 1) + nb;
+        pos = (pos + 7) & ~(size_t)7;
+    }
+    HostTrace h;
+    rc = build_trace(nodes, 0, M, member ? ep : std::vector<mpx_epoch>(), h);
+    if (rc) { std::fprintf(stderr, "build rc %d\n", rc); return 1; }
+    const uint64_t NP = (uint64_t)N * h.NB;
+    uint64_t with = 0, gp = 0, preply = 0, sparse = 0, shape_ok = 0, ev_tot = 0, ev_prep = 0, ev_epoch = 0, ev_other = 0;
+    std::map<uint64_t, uint64_t> runs_h, splits_h, ev_h;
+    for (uint64_t q = 0; q < NP; ++q) {
+        const uint64_t f0 = h.f_off[q], nf = h.f_off[q + 1] - f0;
+        if (!nf) continue;
+        ++with;
+        gp += h.pair_gp[q];
+        bool pr = false, sp = false, lean = true;
+        uint32_t s[3] = {BS, BS, BS};
+        uint32_t nsplit_ok = 1;
+        std::vector<uint32_t> bnd;
+        for (uint64_t f = f0; f < f0 + nf; ++f) {
+            const Frag &fr = h.frags[f];
+            const uint32_t kind = fr.flags >> 4;
+            if (kind == K_PREPLY) pr = true;
+            if (!(fr.flags & FR_DENSE)) sp = true;
+            if (kind != K_ACCEPT && kind != K_COMMIT) lean = false;
+            if (fr.start) bnd.push_back(fr.start);
+            if (fr.start + fr.count < BS) bnd.push_back(fr.start + fr.count);
+            if (!plan_add_split(fr.start, s) || !plan_add_split(fr.start + fr.count, s)) nsplit_ok = 0;
+        }
+        std::sort(bnd.begin(), bnd.end());
+        bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+        preply += pr; sparse += sp;
+        shape_ok += lean && !sp && nsplit_ok && nf <= 16;
+        runs_h[nf < 16 ? nf : 16]++;
+        splits_h[bnd.size() < 8 ? bnd.size() : 8]++;
+        const uint64_t e0 = h.ev_off[q], e1 = h.ev_off[q + 1];
+        ev_tot += e1 - e0;
+        ev_h[(e1 - e0) < 64 ? (e1 - e0) / 4 * 4 : 64]++;
+        for (uint64_t e = e0; e < e1; ++e) {
+            const uint8_t ty = h.m_type[h.ev_msg[e]];
+            if (ty == MPX_MSG_PREPARE) ++ev_prep;
+            else if (ty == MPX_MSG_E_EPOCH) ++ev_epoch;
+            else ++ev_other;
+        }
+    }
+    std::printf("N %u NB %u pairs %llu with runs %llu gp %llu (simple %llu snap %llu) preply %llu sparse %llu "
+                "shape_ok(dense acc/commit, <=3 splits, <=16 runs) %llu\n",
+                N, h.NB, (unsigned long long)NP, (unsigned long long)with, (unsigned long long)gp,
+                (unsigned long long)h.num_gp_simple, (unsigned long long)h.num_gp_snap, (unsigned long long)preply,
+                (unsigned long long)sparse, (unsigned long long)shape_ok);
+    std::printf("events %llu (prepare %llu, epoch %llu, other %llu), runs %zu, messages %zu, markers %zu\n",
+                (unsigned long long)ev_tot, (unsigned long long)ev_prep, (unsigned long long)ev_epoch,
+                (unsigned long long)ev_other, h.frags.size(), h.m_type.size(), h.ee_msg.size());
+    std::printf("runs/pair:");
+    for (auto &x : runs_h) std::printf(" %llu:%llu", (unsigned long long)x.first, (unsigned long long)x.second);
+    std::printf("\ninterior boundaries/pair:");
+    for (auto &x : splits_h) std::printf(" %llu:%llu", (unsigned long long)x.first, (unsigned long long)x.second);
+    std::printf("\nevents/pair (bins of 4):");
+    for (auto &x : ev_h) std::printf(" %llu:%llu", (unsigned long long)x.first, (unsigned long long)x.second);
+    std::printf("\n");
+    return 0;
+}

@@ -24,6 +24,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multi-paxos_amd"))
+import mpx  # noqa: E402  (source_digest only: no GPU call)
 # one pass: at most 8 SQ counters (MI355X_MICROARCH.md §rocprofv3 PMC slots); WAIT_ANY +
 # WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES (quad-cycles)
 SQ_COUNTERS = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
@@ -60,19 +62,23 @@ def main():
     ap.add_argument("--c5", action="store_true", help="the C5 member leg (bench.py --c5-only)")
     ap.add_argument("--sq", action="store_true", help="also one pass of SQ wave-state counters")
     a, rest = ap.parse_known_args()
+    # the workload's true size, recorded with the profile (bench.py matches it exactly)
     if a.c5:
-        bench_args = ["--c5-only", "--c5-steps", "3"] + rest
+        a.instances, a.nodes = 1 << 25, 8
+        bench_args = ["--c5-only", "--c5-steps", "3", "--c5-instances", str(a.instances)] + rest
     elif a.c3:
-        bench_args = ["--c3-only", "--c3-steps", "3"] + rest
+        a.instances, a.nodes = 1 << 24, 7
+        bench_args = ["--c3-only", "--c3-steps", "3", "--c3-instances", str(a.instances)] + rest
     else:
         bench_args = ["--steps", "3", "--warmup", "0", "--instances", str(a.instances), "--nodes", str(a.nodes),
                       "--c3-instances", "0"] + rest
     fetch = run_pass(["FETCH_SIZE"], a.outdir, bench_args, a.tag)["FETCH_SIZE"]
     write = run_pass(["WRITE_SIZE"], a.outdir, bench_args, a.tag)["WRITE_SIZE"]
     sq = run_pass(SQ_COUNTERS, a.outdir, bench_args, a.tag) if a.sq else {}
-    out = {"tag": a.tag, "workload": "C5 2^25 member (bench.py --c5-only)" if a.c5 else
-           "C3 2^24 x 7 (bench.py --c3-only)" if a.c3 else "C4",
-           "instances": a.instances, "nodes": a.nodes, "gpus": 1, "kernels": {}}
+    out = {"tag": a.tag, "workload": "C5 2^%d member (bench.py --c5-only)" % (a.instances.bit_length() - 1) if a.c5 else
+           "C3 2^%d x 7 (bench.py --c3-only)" % (a.instances.bit_length() - 1) if a.c3 else "C4",
+           "instances": a.instances, "nodes": a.nodes, "gpus": 1, "source_digest": mpx.source_digest(),
+           "kernels": {}}
     mean = lambda xs: sum(xs) / len(xs) if xs else 0.0
     for name in sorted(set(fetch) | set(write)):
         f = fetch.get(name, [0.0])
