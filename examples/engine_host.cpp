@@ -11,12 +11,19 @@
 //     destination's address, as the handlers' replies do (:888-899,1391-1403);
 //   * the in-order executed Values (mpx_read_executed + mpx_value_bytes) go to
 //     StateMachine::Execute (:1584-1622).
-// It replays an MPXT trace (multi semantics) and prints what the transport and
-// the state machines saw, so a test can compare it with the Python binding.
+// The nodes' addresses are the demo's own paxos::NodeInfoMap (multi/main.cpp:265-268:
+// node i at "0.0.0.0", port i): a reply leaves through SendMessageUDP(ip, port) of the
+// destination's NodeInfo, and the transport maps (ip, port) back to the node by that map.
+// It replays an MPXT trace (multi semantics) and prints what the transport and the state
+// machines saw, so a test can compare it with the Python binding.  With a window count W
+// the engine runs incrementally (MPX_FLAG_INCREMENTAL): each node's stream is received in
+// W slices, and after each slice the engine applies just that window and the replies it
+// produced are sent — the OnReceiveMessage loop of a live host.
 //
-//   engine_host <trace.mpxt>
+//   engine_host <trace.mpxt> [windows]
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iterator>
@@ -36,13 +43,14 @@ uint64_t fnv(uint64_t h, const void *p, size_t n)
     return h;
 }
 
-struct Wire {                         // what the host's transport saw
-    uint64_t count = 0, hash = 1469598103934665603ull;
+struct Wire {                         // what the host's transport saw: count, and a sum of
+    uint64_t count = 0, hash = 0;     // per-send hashes (windows interleave the nodes' sends)
 };
 
 class EngineNetWork : public paxos::NetWork {
 public:
-    EngineNetWork(mpx_engine *eng, uint32_t node, Wire *wire) : eng_(eng), node_(node), wire_(wire) { offs_.push_back(0); }
+    EngineNetWork(mpx_engine *eng, uint32_t node, Wire *wire, const paxos::NodeInfoMap *nodes)
+        : eng_(eng), node_(node), wire_(wire), nodes_(nodes) { offs_.push_back(0); }
 
     void Receive(const char *msg, unsigned len)
     {
@@ -62,16 +70,21 @@ public:
 private:
     void Send(const std::string &ip, unsigned short port, const std::string &msg)
     {
-        const uint32_t src = node_, dst = (uint32_t)(port - 10000);   // the demo's address plan
-        (void)ip;
+        uint32_t dst = ~0u;                                        // the node at (ip, port)
+        for (paxos::NodeInfoMap::const_iterator it = nodes_->begin(); it != nodes_->end(); ++it)
+            if (it->second.ip_ == ip && it->second.port_ == port) dst = it->first;
+        const uint32_t src = node_;
+        uint64_t h = 1469598103934665603ull;
+        h = fnv(h, &src, 4);
+        h = fnv(h, &dst, 4);
+        h = fnv(h, msg.data(), msg.size());
         wire_->count++;
-        wire_->hash = fnv(wire_->hash, &src, 4);
-        wire_->hash = fnv(wire_->hash, &dst, 4);
-        wire_->hash = fnv(wire_->hash, msg.data(), msg.size());
+        wire_->hash += h;
     }
     mpx_engine *eng_;
     uint32_t node_;
     Wire *wire_;
+    const paxos::NodeInfoMap *nodes_;
     std::string buf_;
     std::vector<uint64_t> offs_;
 };
@@ -86,12 +99,14 @@ public:
     uint64_t count = 0, hash = 1469598103934665603ull;
 };
 
-struct DrainCtx { std::vector<EngineNetWork *> *nets; };
+struct DrainCtx { std::vector<EngineNetWork *> *nets; const paxos::NodeInfoMap *nodes; };
 
+// a reply of node src to node dst: out through src's NetWork to dst's address
 void on_send(void *user, uint32_t src, uint32_t dst, const uint8_t *bytes, uint32_t len)
 {
     DrainCtx *c = (DrainCtx *)user;
-    (*c->nets)[src]->SendMessageUDP("127.0.0.1", (unsigned short)(10000 + dst), std::string((const char *)bytes, len));
+    const paxos::NodeInfo &to = c->nodes->find(dst)->second;
+    (*c->nets)[src]->SendMessageUDP(to.ip_, to.port_, std::string((const char *)bytes, len));
 }
 
 template <typename T> T rd(const std::string &s, size_t o)
@@ -105,7 +120,8 @@ template <typename T> T rd(const std::string &s, size_t o)
 
 int main(int argc, char **argv)
 {
-    if (argc < 2) { std::fprintf(stderr, "usage: %s trace.mpxt\n", argv[0]); return 2; }
+    if (argc < 2) { std::fprintf(stderr, "usage: %s trace.mpxt [windows]\n", argv[0]); return 2; }
+    const uint32_t W = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 0;     // 0: one batch run
     std::ifstream f(argv[1], std::ios::binary);
     std::string t((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
     if (t.size() < 40 || t.compare(0, 4, "MPXT") != 0) { std::fprintf(stderr, "not an MPXT trace\n"); return 2; }
@@ -116,27 +132,40 @@ int main(int argc, char **argv)
     std::memset(&cfg, 0, sizeof cfg);
     cfg.abi_version = MPX_ABI_VERSION; cfg.num_nodes = N; cfg.semantics = sem; cfg.device = 0;
     cfg.shard_begin = 0; cfg.shard_end = M ? M : 1;
+    cfg.flags = W ? MPX_FLAG_INCREMENTAL : 0;
     mpx_engine *eng = nullptr;
     int rc = mpx_create(&cfg, &eng);
     if (rc) { std::fprintf(stderr, "mpx_create: %d\n", rc); return 1; }
+    // the demo's addresses (multi/main.cpp:265-268)
+    paxos::NodeInfoMap nodes;
+    for (uint32_t i = 0; i < N; ++i) nodes.insert(std::make_pair(i, paxos::NodeInfo("0.0.0.0", (unsigned short)i)));
     Wire wire;
     std::vector<EngineNetWork *> nets;
-    for (uint32_t n = 0; n < N; ++n) nets.push_back(new EngineNetWork(eng, n, &wire));
+    for (uint32_t n = 0; n < N; ++n) nets.push_back(new EngineNetWork(eng, n, &wire, &nodes));
     // MPXT body: per node {u64 count, u64 nbytes, u64 offsets[count + 1], bytes, pad to 8}
+    std::vector<size_t> offs(N), body(N);
+    std::vector<uint64_t> cnt(N);
     size_t pos = 40;
     for (uint32_t n = 0; n < N; ++n) {
-        const uint64_t cnt = rd<uint64_t>(t, pos), nb = rd<uint64_t>(t, pos + 8);
-        const size_t offs = pos + 16, body = offs + 8 * (cnt + 1);
-        for (uint64_t k = 0; k < cnt; ++k) {
-            const uint64_t a = rd<uint64_t>(t, offs + 8 * k), b = rd<uint64_t>(t, offs + 8 * (k + 1));
-            nets[n]->Receive(t.data() + body + a, (unsigned)(b - a));      // = NetWork::OnReceiveMessage
-        }
-        if ((rc = nets[n]->Flush())) { std::fprintf(stderr, "mpx_submit: %d\n", rc); return 1; }
-        pos = body + ((nb + 7) & ~7ull);
+        cnt[n] = rd<uint64_t>(t, pos);
+        const uint64_t nb = rd<uint64_t>(t, pos + 8);
+        offs[n] = pos + 16; body[n] = offs[n] + 8 * (cnt[n] + 1);
+        pos = body[n] + ((nb + 7) & ~7ull);
     }
-    if ((rc = mpx_run(eng))) { std::fprintf(stderr, "mpx_run: %d\n", rc); return 1; }
-    DrainCtx ctx{&nets};
-    if ((rc = mpx_drain_sends(eng, on_send, &ctx))) { std::fprintf(stderr, "mpx_drain_sends: %d\n", rc); return 1; }
+    DrainCtx ctx{&nets, &nodes};
+    const uint32_t windows = W ? W : 1;
+    for (uint32_t w = 0; w < windows; ++w) {
+        for (uint32_t n = 0; n < N; ++n) {
+            const uint64_t k0 = cnt[n] * w / windows, k1 = cnt[n] * (w + 1) / windows;
+            for (uint64_t k = k0; k < k1; ++k) {
+                const uint64_t a = rd<uint64_t>(t, offs[n] + 8 * k), b = rd<uint64_t>(t, offs[n] + 8 * (k + 1));
+                nets[n]->Receive(t.data() + body[n] + a, (unsigned)(b - a));   // = NetWork::OnReceiveMessage
+            }
+            if ((rc = nets[n]->Flush())) { std::fprintf(stderr, "mpx_submit: %d\n", rc); return 1; }
+        }
+        if ((rc = mpx_run(eng))) { std::fprintf(stderr, "mpx_run: %d\n", rc); return 1; }
+        if ((rc = mpx_drain_sends(eng, on_send, &ctx))) { std::fprintf(stderr, "mpx_drain_sends: %d\n", rc); return 1; }
+    }
     std::printf("sends %llu %016llx\n", (unsigned long long)wire.count, (unsigned long long)wire.hash);
     for (uint32_t n = 0; n < N; ++n) {
         uint64_t frontier = 0, cnt = 0;

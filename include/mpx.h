@@ -132,9 +132,22 @@ typedef struct mpx_config {
     uint64_t shard_begin;      /* this engine owns instances [shard_begin,         */
     uint64_t shard_end;        /*                              shard_end)          */
     uint32_t num_epochs;       /* member only                                      */
-    uint32_t flags;            /* reserved, 0                                      */
+    uint32_t flags;            /* 0, or MPX_FLAG_INCREMENTAL (multi semantics)     */
     const mpx_epoch *epochs;   /* member only, indexed by E_EPOCH's epoch          */
 } mpx_config;
+
+/* Incremental runs (the drop-in for NetWork::OnReceiveMessage, multi/paxos.cpp:1714-1717,
+ * on a live stream).  Each mpx_run applies only the records submitted since
+ * the previous one — a window — to the state the earlier windows left, on the device:
+ * acceptor / learner entries, the chosen log, promised / max_seen, promise rounds with
+ * their pre-accepted maps, and the batches' votes carry over as values.  A window's
+ * host and device work is O(window records + state they touch), not O(history).
+ * mpx_drain_sends returns the window's replies; the mpx_read_* state readbacks and
+ * mpx_state_digest give the cumulative state; mpx_stats counts the window.  Not
+ * available in this mode (MPX_E_STATE): mpx_step / mpx_reset_state (windows are applied
+ * once), mpx_dump_result, the decisions and commits readbacks (they walk the run's
+ * history). */
+#define MPX_FLAG_INCREMENTAL 1u
 
 typedef struct mpx_engine mpx_engine;
 
@@ -158,7 +171,10 @@ typedef struct mpx_stats {
                                   belong to other shards (header sharding)       */
     uint64_t general_pairs;    /* (node, bucket) pairs the general per-slot walk
                                   (k_apply) took in the last run: its work list, or
-                                  in a member step what k_plan_member left to it  */
+                                  in a plan step what k_plan_list left to it       */
+    uint64_t num_runs;         /* message runs (fragments) of the resident trace: an
+                                  entry-carrying message cut per 256-instance bucket */
+    uint64_t slot_bytes;       /* bytes per (node, instance) state slot (1 or 2)   */
     uint64_t reserved[1];
 } mpx_stats;
 
@@ -195,6 +211,26 @@ int  mpx_destroy(mpx_engine *eng);
  */
 int  mpx_submit(mpx_engine *eng, uint32_t node, const uint8_t *bytes,
                 const uint64_t *offsets, uint64_t count);
+/* SoA fast path (multi semantics): `count` records already decoded, as arrays — what
+ * mpx_submit decodes from the wire, without the codec.  Per record: its MPX_MSG_* type,
+ * source id, ballot (proposal id; REJECT: its max id), aux (accept id: ACCEPT /
+ * ACCEPT_REPLY / P_BATCH; commit id: COMMIT / COMMIT_REPLY), and entries
+ * [ent_off[i], ent_off[i+1]) of ent_a / ent_b / ent_pid: ACCEPT / COMMIT / P_BATCH
+ * {iid, handle}, PREPARE_REPLY {iid, handle, accepted proposal id}, PREPARE its ranges
+ * {start, end (exclusive)}.  A handle with no Value bytes yet names the payload-free
+ * Value(proposer, value_id, noop) (MPX_HANDLE).  ent_pid may be NULL (ids 0). */
+typedef struct mpx_soa_records {
+    uint64_t count;
+    const uint8_t *type;
+    const uint32_t *src;
+    const uint64_t *ballot;
+    const uint64_t *aux;
+    const uint64_t *ent_off;     /* count + 1 */
+    const uint64_t *ent_a;
+    const uint64_t *ent_b;
+    const uint64_t *ent_pid;
+} mpx_soa_records;
+int  mpx_submit_soa(mpx_engine *eng, uint32_t node, const mpx_soa_records *records);
 /* Convenience: submit every node of an MPXT trace container (see mpx_trace_*). */
 int  mpx_submit_trace(mpx_engine *eng, const uint8_t *trace, uint64_t size);
 
@@ -310,6 +346,25 @@ int  mpx_decisions_combine(const uint8_t *const *parts, const uint64_t *sizes, u
  * mpx_free.  MPX_E_STATE for member semantics or a shard engine, MPX_E_RANGE
  * for a COMMIT_REPLY naming a learner >= 64. */
 int  mpx_read_commits(mpx_engine *eng, uint8_t **out, uint64_t *size);
+/* Sharded commit reliability (one engine per instance range, shards in rank order).
+ * A commit is created at an accept quorum of a batch (only the shards holding its
+ * instances keep it) or at a promise quorum where the node holds any committed
+ * instance (of any shard), so the creation points are a union over shards:
+ *  1. mpx_commit_points: this engine's creation points, format MPXQ: "MPXQ" u32 1,
+ *     u32 nodes; per node u64 count, {u64 seq, u64 accept_id (~0: promise quorum)}
+ *     ascending by seq (record index in the node's stream);
+ *  2. mpx_commit_points_combine: their union (pure host work);
+ *  3. mpx_read_commits_at, on the engine whose shard starts at instance 0 (header
+ *     sharding keeps every COMMIT_REPLY there): OnCommitReply over the union —
+ *     the MPXC mpx_read_commits writes on one engine holding every instance.
+ * mpx_read_commits_sharded runs 1-3 over the engine's communicator; every rank
+ * receives the MPXC.  MPX_E_STATE for member semantics. */
+int  mpx_commit_points(mpx_engine *eng, uint8_t **out, uint64_t *size);
+int  mpx_commit_points_combine(const uint8_t *const *parts, const uint64_t *sizes, uint32_t nparts,
+                               uint8_t **out, uint64_t *size);
+int  mpx_read_commits_at(mpx_engine *eng, const uint8_t *points, uint64_t points_size,
+                         uint8_t **out, uint64_t *size);
+int  mpx_read_commits_sharded(mpx_engine *eng, uint8_t **out, uint64_t *size);
 /* Encoded reference Value bytes (multi/paxos.cpp:556-598) for a handle. */
 int  mpx_value_bytes(mpx_engine *eng, uint64_t handle, uint8_t *buf,
                      uint32_t cap, uint32_t *len);

@@ -83,7 +83,7 @@ struct mpx_engine {
     uint64_t num_frags = 0;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
     DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy, exec_aux, exec_out;
-    DevBuf gp_dyn, gp_dyn_n;                // member plan path: the pairs k_plan_member lists for k_apply
+    DevBuf gp_dyn, gp_dyn_n;                // list plan path: the pairs k_plan_list lists for k_apply
     DevBuf decode_buf;                      // readback scratch (k_decode)
     DevBuf out, out_cursor, partials, viol, summary;
     uint64_t out_cap = 0;
@@ -102,9 +102,24 @@ struct mpx_engine {
     int rank = 0, nranks = 1;
     DevBuf gather_buf;
     DevBuf comm_buf, comm_buf2;             // mpx_comm_allreduce_max / mpx_comm_allgather_bytes
+    // incremental runs (MPX_FLAG_INCREMENTAL): the host carry between windows,
+    // the device state carried as values, and each node's records in earlier windows
+    bool incremental = false;
+    WindowCarry wc;
+    DevBuf s_bal, s_val, p_pid, p_val, p_round, c_val, scal_base, prop_in, prop_out;
+    DevBuf b_gid, g_mask, g_done, gp_base, cb_list, outv, outv_n;
+    uint64_t g_cap = 0;                     // global batches g_mask / g_done hold
+    std::vector<uint64_t> seq_base, win_seq_base;
+    uint64_t windows = 0;
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? MPX_OK : MPX_E_HIP; }
+template <typename T> static int d2h(std::vector<T> &v, const DevBuf &b, size_t n, size_t off = 0)
+{
+    v.resize(n);
+    if (!n) return MPX_OK;
+    return hip_ok(hipMemcpy(v.data(), (const char *)b.p + off * sizeof(T), n * sizeof(T), hipMemcpyDeviceToHost));
+}
 #define TRY(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
 #define HTRY(x) do { if ((x) != hipSuccess) return MPX_E_HIP; } while (0)
 
@@ -133,6 +148,8 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
     if (cfg->shard_end <= cfg->shard_begin) return MPX_E_INVAL;
     if (cfg->semantics != MPX_SEM_MULTI && cfg->semantics != MPX_SEM_MEMBER) return MPX_E_INVAL;
     if (cfg->semantics == MPX_SEM_MULTI && cfg->num_epochs) return MPX_E_INVAL;
+    if (cfg->flags & ~(uint32_t)MPX_FLAG_INCREMENTAL) return MPX_E_INVAL;
+    if ((cfg->flags & MPX_FLAG_INCREMENTAL) && cfg->semantics != MPX_SEM_MULTI) return MPX_E_INVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPX_E_NODEVICE;
     if (cfg->device < 0 || cfg->device >= n) return MPX_E_NODEVICE;
@@ -151,6 +168,25 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
     e->shard_len = cfg->shard_end - cfg->shard_begin;
     e->NB = (uint32_t)((e->shard_len + BS - 1) >> BSH);
     if ((uint64_t)e->NB * cfg->num_nodes > (1ull << 40)) return MPX_E_RANGE;
+    if (cfg->flags & MPX_FLAG_INCREMENTAL) {
+        // the carried state, as values: 16 B per (node, instance) for the acceptor / learner
+        // entries and 16 B for a promise round's pre-accepted map, 8 B per instance of
+        // chosen log (all zero: the PaxosImpl ctor state, multi/paxos.cpp:323-346)
+        e->incremental = true;
+        e->wc.init(cfg->num_nodes, e->NB);
+        e->seq_base.assign(cfg->num_nodes, 0);
+        const uint64_t NL = (uint64_t)cfg->num_nodes * e->shard_len;
+        DevBuf *bufs[] = {&e->s_bal, &e->s_val, &e->p_pid, &e->p_val};
+        for (DevBuf *b : bufs) TRY(b->alloc(8 * NL));
+        TRY(e->p_round.alloc(8ull * cfg->num_nodes * e->NB)); TRY(e->c_val.alloc(8 * e->shard_len));
+        TRY(e->scal_base.alloc(16ull * cfg->num_nodes));
+        TRY(e->prop_in.alloc(24ull * cfg->num_nodes)); TRY(e->prop_out.alloc(24ull * cfg->num_nodes));
+        TRY(e->outv_n.alloc(8));
+        DevBuf *z[] = {&e->s_bal, &e->s_val, &e->p_pid, &e->p_val, &e->p_round, &e->c_val, &e->scal_base, &e->prop_in,
+                       &e->prop_out};
+        for (DevBuf *b : z) HTRY(hipMemsetAsync(b->p, 0, b->bytes, e->stream));
+        HTRY(hipStreamSynchronize(e->stream));
+    }
     *out = e.release();
     return MPX_OK;
 }
@@ -181,6 +217,31 @@ extern "C" int mpx_submit(mpx_engine *e, uint32_t node, const uint8_t *bytes, co
         int rc = member ? decode_record_member(e->vt, ns, node, m, len, e->cfg.shard_begin, e->cfg.shard_end, e->iv)
                         : decode_record(e->vt, ns, node, e->cfg.num_nodes, m, len, e->cfg.shard_begin, e->cfg.shard_end, e->iv);
         if (rc) return rc;
+    }
+    e->dirty = true;
+    e->stats.ingest_ns += now_ns() - t0;
+    return MPX_OK;
+}
+
+// SoA fast path: records the caller already holds decoded — a synthetic
+// trace generator, or a host that keeps its messages as arrays — skip the wire codec.
+extern "C" int mpx_submit_soa(mpx_engine *e, uint32_t node, const mpx_soa_records *r)
+{
+    if (!e || !r || node >= e->cfg.num_nodes) return MPX_E_INVAL;
+    if (e->device_trace || e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
+    if (r->count && (!r->type || !r->src || !r->ballot || !r->aux || !r->ent_off)) return MPX_E_INVAL;
+    const uint64_t t0 = now_ns();
+    NodeStream &ns = e->nodes[node];
+    for (uint64_t i = 0; i < r->count; ++i) {
+        SoaRecord x{r->type[i], r->src[i], r->ballot[i], r->aux[i], 0, nullptr, nullptr, nullptr};
+        if (r->ent_off[i + 1] < r->ent_off[i]) return MPX_E_INVAL;
+        x.n = r->ent_off[i + 1] - r->ent_off[i];
+        if (x.n) {
+            if (!r->ent_a || !r->ent_b) return MPX_E_INVAL;
+            x.a = r->ent_a + r->ent_off[i]; x.b = r->ent_b + r->ent_off[i];
+            x.pid = r->ent_pid ? r->ent_pid + r->ent_off[i] : nullptr;
+        }
+        TRY(append_record(e->vt, ns, node, x, e->cfg.shard_begin, e->cfg.shard_end, e->iv));
     }
     e->dirty = true;
     e->stats.ingest_ns += now_ns() - t0;
@@ -287,10 +348,11 @@ static int finish_view(mpx_engine *e)
     // 1-byte pair-local index (set by the trace loader), MPX_SLOT_BYTES=2 forces 2
     if (const char *x = std::getenv("MPX_SLOT_BYTES")) if (std::atoi(x) == 2) v.slot_w = 2;
     if (v.slot_w != 1) v.slot_w = 2;
-    TRY(e->st.alloc((size_t)(N + 1) * e->shard_len * v.slot_w));   // row N: the chosen log
-    TRY(e->st_valid.alloc((size_t)N * e->NB));
-    TRY(e->chosen_valid.alloc(e->NB));
-    TRY(e->plan.alloc((size_t)(N + 1) * e->NB * 8));
+    // (incremental windows keep their state as values, DevView s_* / c_val: no slot rows, plans)
+    TRY(e->st.alloc(e->incremental ? 8 : (size_t)(N + 1) * e->shard_len * v.slot_w));   // row N: the chosen log
+    TRY(e->st_valid.alloc(e->incremental ? 8 : (size_t)N * e->NB));
+    TRY(e->chosen_valid.alloc(e->incremental ? 8 : e->NB));
+    TRY(e->plan.alloc(e->incremental ? 8 : (size_t)(N + 1) * e->NB * 8));
     {   // promise-quorum chunks over each node's proposer list (k_prop_chunk / k_prop_node)
         const HostTrace &h = e->ht;
         uint64_t pc = PROP_CHUNK;                       // MPX_PROP_CHUNK: smaller chunks (tests)
@@ -321,8 +383,8 @@ static int finish_view(mpx_engine *e)
     v.frag_w1 = e->frag_w1.as<uint64_t>();
     TRY(e->fast_rest.alloc(8));
     TRY(e->store_dummy.alloc(64 * 1024));
-    // member: k_plan_member lists at most the work list's non-round pairs
-    TRY(e->gp_dyn.alloc(std::max<size_t>(8ull * GP_WORDS * (v.semantics == MPX_SEM_MEMBER ? v.num_gp_snap : 0), 8 * GP_WORDS)));
+    // k_plan_list lists at most the work list's non-round pairs
+    TRY(e->gp_dyn.alloc(std::max<size_t>(8ull * GP_WORDS * v.num_gp_snap, 8 * GP_WORDS)));
     TRY(e->gp_dyn_n.alloc(8));
     v.gp_dyn = e->gp_dyn.as<uint64_t>();
     v.gp_dyn_n = e->gp_dyn_n.as<unsigned long long>();
@@ -367,7 +429,16 @@ static int upload_trace(mpx_engine *e)
     const uint64_t t0 = now_ns();
     const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
     if (member && e->epochs.empty()) return MPX_E_STATE;        // no epoch table yet
-    TRY(build_trace(e->nodes, e->cfg.shard_begin, e->shard_len, member ? e->epochs : std::vector<mpx_epoch>(), e->ht));
+    TRY(build_trace(e->nodes, e->cfg.shard_begin, e->shard_len, member ? e->epochs : std::vector<mpx_epoch>(), e->ht,
+                    e->incremental ? &e->wc : nullptr));
+    if (e->incremental) {
+        // the window is consumed: the next run builds on the carry from only what comes after it
+        e->win_seq_base = e->seq_base;
+        for (uint32_t n = 0; n < e->cfg.num_nodes; ++n) {
+            e->seq_base[n] += e->nodes[n].type.size();
+            e->nodes[n].clear();
+        }
+    }
     e->whole = e->cfg.shard_begin == 0 && e->ht.part_dropped == 0;
     HostTrace &h = e->ht;
     hipStream_t s = e->stream;
@@ -444,6 +515,34 @@ static int upload_trace(mpx_engine *e)
     TRY(upload(e->cf_off, h.cf_off, s)); TRY(upload(e->cfrags, h.cfrags, s));
     e->num_msgs = h.m_type.size();
     DevView &v = e->view;
+    if (e->incremental) {
+        TRY(upload(e->b_gid, h.b_gid, s)); TRY(upload(e->gp_base, h.gp_base, s)); TRY(upload(e->cb_list, h.cb_list, s));
+        if (e->wc.batches > e->g_cap) {                 // the batches' votes, grown geometrically (kept values copied)
+            const uint64_t cap = std::max<uint64_t>(e->wc.batches, 2 * e->g_cap);
+            DevBuf nm, nd;
+            TRY(nm.alloc(8 * cap)); TRY(nd.alloc(cap));
+            HTRY(hipMemsetAsync(nm.p, 0, 8 * cap, s)); HTRY(hipMemsetAsync(nd.p, 0, cap, s));
+            if (e->g_cap) {
+                HTRY(hipMemcpyAsync(nm.p, e->g_mask.p, 8 * e->g_cap, hipMemcpyDeviceToDevice, s));
+                HTRY(hipMemcpyAsync(nd.p, e->g_done.p, e->g_cap, hipMemcpyDeviceToDevice, s));
+            }
+            HTRY(hipStreamSynchronize(s));
+            std::swap(e->g_mask.p, nm.p); std::swap(e->g_mask.bytes, nm.bytes);
+            std::swap(e->g_done.p, nd.p); std::swap(e->g_done.bytes, nd.bytes);
+            e->g_cap = cap;
+        }
+        // snapshot records: at most one per slot of every listed event (PREPARE or quorum)
+        const uint64_t cap = std::max<uint64_t>(BS * h.ev_msg.size(), 1);
+        TRY(e->outv.alloc(cap * sizeof(OutEnt)));
+        v.window = 1;
+        v.s_bal = e->s_bal.as<uint64_t>(); v.s_val = e->s_val.as<uint64_t>();
+        v.p_pid = e->p_pid.as<uint64_t>(); v.p_val = e->p_val.as<uint64_t>(); v.p_round = e->p_round.as<uint64_t>();
+        v.c_val = e->c_val.as<uint64_t>(); v.scal_base = e->scal_base.as<uint64_t>();
+        v.prop_in = e->prop_in.as<uint64_t>(); v.prop_out = e->prop_out.as<uint64_t>();
+        v.b_gid = e->b_gid.as<uint32_t>(); v.g_mask = e->g_mask.as<uint64_t>(); v.g_done = e->g_done.as<uint8_t>();
+        v.gp_base = e->gp_base.as<uint8_t>(); v.cb_list = e->cb_list.as<uint32_t>(); v.num_cb = (uint32_t)h.cb_list.size();
+        v.outv = e->outv.as<OutEnt>(); v.outv_n = e->outv_n.as<unsigned long long>(); v.outv_cap = cap;
+    }
     v.m_type = e->m_type.as<uint8_t>(); v.m_src = e->m_src.as<uint32_t>();
     v.m_ballot = e->m_ballot.as<uint64_t>(); v.m_aux = e->m_aux.as<uint64_t>();
     v.m_ent = e->m_ent.as<uint64_t>(); v.m_cnt = e->m_cnt.as<uint32_t>();
@@ -524,6 +623,10 @@ static int queue_run(mpx_engine *e, bool digest)
     void *evp[5] = {ev->e[0], ev->e[1], ev->e[2], ev->e[3], ev->e[4]};
     int rc = launch_run(e->view, e->stream, g, evp);
     if (rc) return MPX_E_HIP;
+    if (e->incremental) {                              // the next window starts from this one's scalars and rounds
+        HTRY(hipMemcpyAsync(e->scal_base.p, e->node_scal.p, 16ull * e->cfg.num_nodes, hipMemcpyDeviceToDevice, e->stream));
+        HTRY(hipMemcpyAsync(e->prop_in.p, e->prop_out.p, 24ull * e->cfg.num_nodes, hipMemcpyDeviceToDevice, e->stream));
+    }
     // the one cross-GPU exchange: every rank's 64-word summary, over RCCL on
     // the same stream, no host synchronisation
     if (e->comm && ncclAllGather(e->summary.p, e->gather_buf.p, 64, ncclUint64, e->comm, e->stream) != ncclSuccess)
@@ -537,7 +640,13 @@ static int collect(mpx_engine *e)
     e->last_summary.assign(64, 0);
     HTRY(hipMemcpy(e->last_summary.data(), e->summary.p, 64 * 8, hipMemcpyDeviceToHost));
     uint64_t cursor = 0;
-    {
+    if (e->incremental) {
+        // a window is not re-run (its carry has moved on): the record buffer is sized for every
+        // slot of every listed event
+        uint64_t nv = 0;
+        HTRY(hipMemcpy(&nv, e->outv_n.p, 8, hipMemcpyDeviceToHost));
+        if (nv > e->view.outv_cap) return MPX_E_STATE;
+    } else {
         std::vector<uint64_t> cur(OUT_STRIDE * e->out_subs);
         HTRY(hipMemcpy(cur.data(), e->out_cursor.p, 8 * cur.size(), hipMemcpyDeviceToHost));
         for (uint32_t s = 0; s < e->out_subs; ++s) cursor = std::max<uint64_t>(cursor, cur[OUT_STRIDE * s]);
@@ -559,8 +668,20 @@ static int collect(mpx_engine *e)
     st.chosen_digest = s[SW_DCHOSEN]; st.state_digest = s[SW_DSTATE]; st.scalar_digest = s[SW_DSCAL];
     st.bytes_alg = 16 * st.promise_entries + 24 * st.accept_apps + 16 * st.commit_apps;
     st.general_pairs = e->view.num_gp;
-    if (e->cfg.semantics == MPX_SEM_MEMBER && !e->view.digest && !(e->view.knobs & 64)) {
-        uint64_t listed = 0;                         // k_plan_member's list + the promise-round pairs
+    st.num_runs = e->num_frags;
+    st.slot_bytes = e->view.slot_w;
+    const DevView &v = e->view;
+    const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
+    if (!member && !v.digest && !(v.knobs & (64 | 4194304)) && v.N <= FAST_MAX_NODES) {
+        // the multi plan path launches no k_apply_fast after the store: every lean pair must
+        // have been planned (kernels.hip launch_run)
+        uint32_t rest = 0;
+        HTRY(hipMemcpy(&rest, e->fast_rest.p, 4, hipMemcpyDeviceToHost));
+        if (rest) return MPX_E_STATE;
+    }
+    // the plan path with k_plan_list (kernels.hip launch_run): its list + the promise-round pairs
+    if (!v.digest && !(v.knobs & 64) && (member || (v.N <= FAST_MAX_NODES && v.num_gp_snap && !(v.knobs & 8388608)))) {
+        uint64_t listed = 0;
         HTRY(hipMemcpy(&listed, e->gp_dyn_n.p, 8, hipMemcpyDeviceToHost));
         st.general_pairs = listed + (e->view.num_gp - e->view.num_gp_snap);
     }
@@ -578,6 +699,19 @@ static int collect(mpx_engine *e)
 extern "C" int mpx_run(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
+    if (e->incremental) {
+        // one window: the records submitted since the last run, on the carried state
+        e->dirty = true;
+        TRY(queue_run(e, false));
+        TRY(collect(e));
+        // batches chosen in this window need their entries no more
+        std::vector<uint32_t> bc;
+        TRY(d2h(bc, e->b_chosen, e->ht.b_gid.size()));
+        for (size_t j = 0; j < bc.size(); ++j)
+            if (bc[j] != NONE32) e->wc.b_ents.erase(e->ht.b_gid[j]);
+        ++e->windows;
+        return MPX_OK;
+    }
     TRY(queue_run(e, true));
     return collect(e);
 }
@@ -585,6 +719,7 @@ extern "C" int mpx_run(mpx_engine *e)
 extern "C" int mpx_step(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
+    if (e->incremental) return MPX_E_STATE;           // windows are applied once, not replayed
     return queue_run(e, false);
 }
 
@@ -597,6 +732,7 @@ extern "C" int mpx_sync(mpx_engine *e)
 extern "C" int mpx_reset_state(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
+    if (e->incremental) return MPX_E_STATE;
     HTRY(hipSetDevice(e->device));
     if (e->st_valid.p) HTRY(hipMemsetAsync(e->st_valid.p, 0, e->st_valid.bytes, e->stream));
     if (e->chosen_valid.p) HTRY(hipMemsetAsync(e->chosen_valid.p, 0, e->chosen_valid.bytes, e->stream));
@@ -641,12 +777,6 @@ extern "C" int mpx_timings_detail(mpx_engine *e, uint32_t max, double *phases, u
 }
 
 // ---------------------------------------------------------------- readback --
-template <typename T> static int d2h(std::vector<T> &v, const DevBuf &b, size_t n, size_t off = 0)
-{
-    v.resize(n);
-    if (!n) return MPX_OK;
-    return hip_ok(hipMemcpy(v.data(), (const char *)b.p + off * sizeof(T), n * sizeof(T), hipMemcpyDeviceToHost));
-}
 
 static bool have_results(const mpx_engine *e) { return !e->last_summary.empty(); }
 
@@ -657,6 +787,18 @@ static int decode_slots(mpx_engine *e, uint32_t n, uint64_t l0, uint64_t count, 
     out.assign(2 * count, 0);
     if (!count || !have_results(e)) return MPX_OK;
     HTRY(hipSetDevice(e->device));
+    if (e->incremental) {                              // the carried values themselves
+        std::vector<uint64_t> b, w;
+        if (n < e->cfg.num_nodes) {
+            const uint64_t at = (uint64_t)n * e->shard_len + l0;
+            TRY(d2h(b, e->s_bal, count, at)); TRY(d2h(w, e->s_val, count, at));
+        } else {
+            b.assign(count, 0);
+            TRY(d2h(w, e->c_val, count, l0));
+        }
+        for (uint64_t i = 0; i < count; ++i) { out[2 * i] = (w[i] & W_PRESENT) ? b[i] : 0; out[2 * i + 1] = w[i]; }
+        return MPX_OK;
+    }
     TRY(e->decode_buf.alloc(16 * count));
     if (launch_decode(e->view, e->stream, n, l0, count, e->decode_buf.as<uint64_t>()) != 0) return MPX_E_HIP;
     HTRY(hipStreamSynchronize(e->stream));
@@ -675,6 +817,15 @@ static int gpu_executed(mpx_engine *e, uint32_t n, uint64_t &frontier, std::vect
     handles.clear();
     if (!have_results(e)) return MPX_OK;
     HTRY(hipSetDevice(e->device));
+    if (e->incremental) {                              // readback of the carried values (a window keeps no slot rows)
+        std::vector<uint64_t> st;
+        TRY(decode_slots(e, n, 0, e->shard_len, st));
+        while (frontier < e->shard_len && (st[2 * frontier + 1] & W_COMMITTED)) {
+            const uint64_t h = st[2 * frontier + 1] & W_HANDLE;
+            if (!MPX_HANDLE_NOOP(h)) handles.push_back(h);
+            ++frontier;
+        }
+    } else {
     const uint64_t NB = e->NB;
     TRY(e->exec_aux.alloc(8 * (2 * NB + 2)));
     unsigned long long *aux = e->exec_aux.as<unsigned long long>();
@@ -689,6 +840,7 @@ static int gpu_executed(mpx_engine *e, uint32_t n, uint64_t &frontier, std::vect
         if (launch_exec(e->view, e->stream, n, aux, e->exec_out.as<uint64_t>()) != 0) return MPX_E_HIP;
         HTRY(hipStreamSynchronize(e->stream));
         TRY(d2h(handles, e->exec_out, total));
+    }
     }
     {   // Values with no executable payload (membership changes) are not executed
         std::string payload;
@@ -797,7 +949,7 @@ extern "C" int mpx_last_violation(mpx_engine *e, mpx_violation *out)
         const bool msg_seq = d.code == MPX_V_BAD_NODE || d.code == MPX_V_LEARN_VALUE ||
                              (d.code == MPX_V_COMMIT_VALUE && d.seq);
         if (msg_seq && d.node < h.N && h.node_off[d.node] + d.seq < h.m_seq.size())
-            out->seq = h.m_seq[h.node_off[d.node] + d.seq];
+            out->seq = h.m_seq[h.node_off[d.node] + d.seq] + (e->incremental ? e->win_seq_base[d.node] : 0);
     }
     return MPX_OK;
 }
@@ -836,7 +988,11 @@ static int fetch_results(mpx_engine *e, Results &r)
     TRY(d2h(r.flags, e->m_flags, G));
     TRY(d2h(r.maxseen, e->m_maxseen, G));
     TRY(d2h(r.scal, e->node_scal, 2ull * e->cfg.num_nodes));
-    {
+    if (e->incremental) {                              // window records carry their values
+        uint64_t nv = 0;
+        HTRY(hipMemcpy(&nv, e->outv_n.p, 8, hipMemcpyDeviceToHost));
+        TRY(d2h(r.out, e->outv, std::min<uint64_t>(nv, e->view.outv_cap)));
+    } else {
         std::vector<uint64_t> cur(OUT_STRIDE * e->out_subs);
         HTRY(hipMemcpy(cur.data(), e->out_cursor.p, 8 * cur.size(), hipMemcpyDeviceToHost));
         std::vector<OutRec> part;
@@ -852,18 +1008,25 @@ static int fetch_results(mpx_engine *e, Results &r)
                 if (x.kind & 1) {
                     if (o.ref >= h.r_iid.size()) return MPX_E_STATE;
                     x.iid = h.r_iid[o.ref]; x.ballot = h.r_pid[o.ref]; x.handle = h.r_val[o.ref];
+                    r.out.push_back(x);
                 } else {
                     if (o.ref >= h.frags.size()) return MPX_E_STATE;
                     const Frag &f = h.frags[o.ref];
-                    const uint32_t sl = o.aux & (BS - 1);
-                    uint64_t ent = f.entry + (sl - f.start);
-                    if (!(f.flags & FR_DENSE))
-                        for (uint32_t q = 0; q < f.count; ++q)
-                            if (((h.e_iid[f.entry + q] - e->cfg.shard_begin) & (BS - 1)) == sl) { ent = f.entry + q; break; }
-                    x.iid = h.e_iid[ent]; x.handle = h.e_val[ent];
-                    x.ballot = member ? h.e_pid[ent] : h.m_ballot[f.msg];
+                    // one slot, or (OUT_RUN, k_plan_list) a run of slots of a dense fragment
+                    const uint32_t s0 = o.aux & (BS - 1);
+                    const uint32_t ns = (o.aux & OUT_RUN) ? (o.aux >> OUT_RUN_SHIFT) & 0x1FF : 1;
+                    if ((o.aux & OUT_RUN) && (!(f.flags & FR_DENSE) || s0 < f.start || s0 + ns > f.start + f.count))
+                        return MPX_E_STATE;
+                    for (uint32_t sl = s0; sl < s0 + ns; ++sl) {
+                        uint64_t ent = f.entry + (sl - f.start);
+                        if (!(f.flags & FR_DENSE))
+                            for (uint32_t q = 0; q < f.count; ++q)
+                                if (((h.e_iid[f.entry + q] - e->cfg.shard_begin) & (BS - 1)) == sl) { ent = f.entry + q; break; }
+                        x.iid = h.e_iid[ent]; x.handle = h.e_val[ent];
+                        x.ballot = member ? h.e_pid[ent] : h.m_ballot[f.msg];
+                        r.out.push_back(x);
+                    }
                 }
-                r.out.push_back(x);
             }
         }
     }
@@ -937,6 +1100,7 @@ extern "C" int mpx_drain_sends(mpx_engine *e, mpx_send_fn fn, void *user)
 extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
     Results r;
     TRY(fetch_results(e, r));
     const uint32_t N = e->cfg.num_nodes;
@@ -1132,6 +1296,7 @@ static void decide_entries(const DecideEv &ev, uint64_t *vid, std::string &d)
 extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
     if (e->cfg.semantics != MPX_SEM_MULTI || e->cfg.shard_begin != 0) return MPX_E_STATE;
     Results r;
     TRY(fetch_results(e, r));
@@ -1164,6 +1329,7 @@ extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
 extern "C" int mpx_decisions_bounds(mpx_engine *e, uint64_t *bounds, uint64_t cap, uint64_t *count)
 {
     if (!e || !count || (cap && !bounds)) return MPX_E_INVAL;
+    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
     if (e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
     Results r;
     TRY(fetch_results(e, r));
@@ -1178,6 +1344,7 @@ extern "C" int mpx_read_decisions_part(mpx_engine *e, const uint64_t *global_bou
                                        uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size || (count && !global_bounds)) return MPX_E_INVAL;
+    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
     if (e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
     Results r;
     TRY(fetch_results(e, r));
@@ -1277,12 +1444,14 @@ extern "C" int mpx_decisions_combine(const uint8_t *const *parts, const uint64_t
 // order.  k_commits walks the COMMIT_REPLYs of each (node, commit id) on the
 // device: replied_ as a learner mask, retired at |replied_| == N.
 // Format MPXC (include/mpx.h).
-extern "C" int mpx_read_commits(mpx_engine *e, uint8_t **out, uint64_t *size)
+// Commit creation points of one engine, per node in stream order: {seq, accept id}
+// for an accept quorum of a batch this engine kept (its chosen reply), {seq, ~0} for
+// a promise quorum at which the node held a committed instance of this shard.
+// A shard engine sees only its own batches and instances: the union over shards
+// (mpx_commit_points_combine) is the node's whole list.
+typedef std::vector<std::vector<std::pair<uint64_t, uint64_t>>> CommitPoints;
+static int commit_points(mpx_engine *e, const Results &r, CommitPoints &cm)
 {
-    if (!e || !out || !size) return MPX_E_INVAL;
-    if (e->cfg.semantics != MPX_SEM_MULTI || !e->whole) return MPX_E_STATE;
-    Results r;
-    TRY(fetch_results(e, r));
     const HostTrace &h = e->ht;
     const uint32_t N = e->cfg.num_nodes;
     hipStream_t s = e->stream;
@@ -1303,20 +1472,45 @@ extern "C" int mpx_read_commits(mpx_engine *e, uint8_t **out, uint64_t *size)
         HTRY(hipStreamSynchronize(s));
         TRY(d2h(xmax, d_xmax, qn.size()));
     }
-    // commit creation points per node, in message order: (message, accept id | ~0 for a promise quorum)
-    std::vector<std::vector<std::pair<uint32_t, uint64_t>>> cm(N);
+    cm.assign(N, {});
     for (size_t j = 0; j < h.b_msg.size(); ++j)
-        if (r.b_chosen[j] != NONE32) cm[h.m_node[h.b_msg[j]]].push_back({r.b_chosen[j], h.m_aux[h.b_msg[j]]});
+        if (r.b_chosen[j] != NONE32) {
+            const uint32_t n = h.m_node[h.b_msg[j]];
+            cm[n].push_back({seq_of(h, n, r.b_chosen[j]), h.m_aux[h.b_msg[j]]});
+        }
     for (size_t k = 0; k < qn.size(); ++k)
-        if (xmax[k]) cm[qn[k]].push_back({qg[k], ~0ull});
+        if (xmax[k]) cm[qn[k]].push_back({seq_of(h, qn[k], qg[k]), ~0ull});
+    for (auto &l : cm) std::sort(l.begin(), l.end());
+    return MPX_OK;
+}
+
+static int put_bytes(const std::string &d, uint8_t **out, uint64_t *size)
+{
+    *out = (uint8_t *)std::malloc(d.size() ? d.size() : 1);
+    if (!*out) return MPX_E_NOMEM;
+    std::memcpy(*out, d.data(), d.size());
+    *size = d.size();
+    return MPX_OK;
+}
+
+// MPXC from a node's whole list of creation points (ids = rank in stream order) and
+// this engine's COMMIT_REPLYs (it must have kept every one: shard at instance 0)
+static int commits_from_points(mpx_engine *e, const CommitPoints &cm, std::string &d)
+{
+    const HostTrace &h = e->ht;
+    const uint32_t N = e->cfg.num_nodes;
+    hipStream_t s = e->stream;
     std::vector<uint64_t> cm_off(N + 1, 0);
     std::vector<uint32_t> cm_pos;
     for (uint32_t n = 0; n < N; ++n) {
-        std::sort(cm[n].begin(), cm[n].end());
-        for (auto &x : cm[n]) cm_pos.push_back(x.first);
+        for (auto &x : cm[n]) {
+            if (x.first >= NONE32) return MPX_E_RANGE;
+            cm_pos.push_back((uint32_t)x.first);
+        }
         cm_off[n + 1] = cm_pos.size();
     }
-    // reply lists: the COMMIT_REPLYs of each (node, commit id), in processing order
+    // reply lists: the COMMIT_REPLYs of each (node, commit id), in processing order;
+    // positions are record indices in the node's stream (the creation points' unit)
     std::vector<uint64_t> cr_off(1, 0), cr_id;
     std::vector<uint32_t> cr_msg, cr_src, cr_node;
     {
@@ -1337,8 +1531,12 @@ extern "C" int mpx_read_commits(mpx_engine *e, uint8_t **out, uint64_t *size)
                 lists[it->second].push_back((uint32_t)g);
             }
         }
-        for (auto &l : lists) {
-            for (uint32_t g : l) { cr_msg.push_back(g); cr_src.push_back(h.m_src[g]); }
+        for (size_t l = 0; l < lists.size(); ++l) {
+            for (uint32_t g : lists[l]) {
+                const uint64_t sq = seq_of(h, cr_node[l], g);
+                if (sq >= NONE32) return MPX_E_RANGE;
+                cr_msg.push_back((uint32_t)sq); cr_src.push_back(h.m_src[g]);
+            }
             cr_off.push_back(cr_msg.size());
         }
     }
@@ -1349,6 +1547,7 @@ extern "C" int mpx_read_commits(mpx_engine *e, uint8_t **out, uint64_t *size)
         DevBuf d_off, d_id, d_cmoff, d_msg, d_src, d_node, d_pos, d_ret, d_mask;
         TRY(upload(d_off, cr_off, s)); TRY(upload(d_id, cr_id, s)); TRY(upload(d_cmoff, cm_off, s));
         TRY(upload(d_msg, cr_msg, s)); TRY(upload(d_src, cr_src, s)); TRY(upload(d_node, cr_node, s));
+        if (cm_pos.empty()) cm_pos.push_back(0);
         TRY(upload(d_pos, cm_pos, s));
         TRY(d_ret.alloc(4ull * L)); TRY(d_mask.alloc(8ull * L));
         CommitArgs a{L, d_off.as<uint64_t>(), d_id.as<uint64_t>(), d_cmoff.as<uint64_t>(), d_msg.as<uint32_t>(),
@@ -1361,7 +1560,6 @@ extern "C" int mpx_read_commits(mpx_engine *e, uint8_t **out, uint64_t *size)
     // per node, per commit id: the list that names it (if any)
     std::vector<std::map<uint64_t, uint32_t>> by_id(N);
     for (uint32_t l = 0; l < L; ++l) by_id[cr_node[l]][cr_id[l]] = l;
-    std::string d;
     d.append("MPXC", 4);
     app<uint32_t>(d, 1); app<uint32_t>(d, N);
     for (uint32_t n = 0; n < N; ++n) {
@@ -1372,18 +1570,116 @@ extern "C" int mpx_read_commits(mpx_engine *e, uint8_t **out, uint64_t *size)
             const bool has = it != by_id[n].end();
             const uint32_t rg = has ? ret[it->second] : NONE32;
             app<uint64_t>(d, id);
-            app<uint64_t>(d, seq_of(h, n, cm[n][k].first));
+            app<uint64_t>(d, cm[n][k].first);
             app<uint64_t>(d, cm[n][k].second == ~0ull ? 1 : 0);
             app<uint64_t>(d, cm[n][k].second == ~0ull ? 0 : cm[n][k].second);
-            app<uint64_t>(d, rg == NONE32 ? ~0ull : seq_of(h, n, rg));
+            app<uint64_t>(d, rg == NONE32 ? ~0ull : (uint64_t)rg);
             app<uint64_t>(d, has ? mask[it->second] : 0);
         }
     }
-    *out = (uint8_t *)std::malloc(d.size());
-    if (!*out) return MPX_E_NOMEM;
-    std::memcpy(*out, d.data(), d.size());
-    *size = d.size();
     return MPX_OK;
+}
+
+extern "C" int mpx_read_commits(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
+    if (e->cfg.semantics != MPX_SEM_MULTI || !e->whole) return MPX_E_STATE;
+    Results r;
+    TRY(fetch_results(e, r));
+    CommitPoints cm;
+    TRY(commit_points(e, r, cm));
+    std::string d;
+    TRY(commits_from_points(e, cm, d));
+    return put_bytes(d, out, size);
+}
+
+// Sharded commit reliability (include/mpx.h): MPXQ = "MPXQ" u32 1, u32 nodes; per
+// node u64 count, {u64 seq, u64 accept_id | ~0} ascending
+static void points_bytes(const CommitPoints &cm, std::string &d)
+{
+    d.append("MPXQ", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, (uint32_t)cm.size());
+    for (auto &l : cm) {
+        app<uint64_t>(d, l.size());
+        for (auto &x : l) { app<uint64_t>(d, x.first); app<uint64_t>(d, x.second); }
+    }
+}
+
+static int parse_points(const uint8_t *p, uint64_t n, CommitPoints &cm)
+{
+    if (!p || n < 12 || std::memcmp(p, "MPXQ", 4) || rd32(p + 4) != 1) return MPX_E_INVAL;
+    const uint32_t N = rd32(p + 8);
+    if (!N || N > MPX_MAX_NODES) return MPX_E_INVAL;
+    uint64_t pos = 12;
+    cm.assign(N, {});
+    for (uint32_t k = 0; k < N; ++k) {
+        if (pos + 8 > n) return MPX_E_INVAL;
+        const uint64_t c = rd64(p + pos); pos += 8;
+        if (c > (n - pos) / 16) return MPX_E_INVAL;
+        for (uint64_t j = 0; j < c; ++j, pos += 16) {
+            cm[k].push_back({rd64(p + pos), rd64(p + pos + 8)});
+            if (j && cm[k][j] <= cm[k][j - 1]) return MPX_E_INVAL;   // ascending, no repeats
+        }
+    }
+    return pos == n ? MPX_OK : MPX_E_INVAL;
+}
+
+extern "C" int mpx_commit_points(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
+    if (e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
+    // a device-generated shard holds only its own batches' messages: its message positions
+    // are not record indices of the node's whole stream (host traces keep them, m_seq)
+    if (e->device_trace && !e->whole) return MPX_E_STATE;
+    Results r;
+    TRY(fetch_results(e, r));
+    CommitPoints cm;
+    TRY(commit_points(e, r, cm));
+    std::string d;
+    points_bytes(cm, d);
+    return put_bytes(d, out, size);
+}
+
+extern "C" int mpx_commit_points_combine(const uint8_t *const *parts, const uint64_t *sizes, uint32_t nparts,
+                                         uint8_t **out, uint64_t *size)
+{
+    if (!parts || !sizes || !nparts || !out || !size) return MPX_E_INVAL;
+    CommitPoints all;
+    for (uint32_t i = 0; i < nparts; ++i) {
+        CommitPoints cm;
+        TRY(parse_points(parts[i], sizes[i], cm));
+        if (i && cm.size() != all.size()) return MPX_E_INVAL;
+        if (!i) all.assign(cm.size(), {});
+        for (size_t n = 0; n < cm.size(); ++n) all[n].insert(all[n].end(), cm[n].begin(), cm[n].end());
+    }
+    for (auto &l : all) {                 // the union: a batch two shards kept is one point
+        std::sort(l.begin(), l.end());
+        l.erase(std::unique(l.begin(), l.end()), l.end());
+        for (size_t j = 1; j < l.size(); ++j)
+            if (l[j].first == l[j - 1].first) return MPX_E_INVAL;   // one creation per record
+    }
+    std::string d;
+    points_bytes(all, d);
+    return put_bytes(d, out, size);
+}
+
+extern "C" int mpx_read_commits_at(mpx_engine *e, const uint8_t *points, uint64_t points_size,
+                                   uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
+    if (e->cfg.semantics != MPX_SEM_MULTI || e->cfg.shard_begin != 0) return MPX_E_STATE;
+    CommitPoints cm;
+    TRY(parse_points(points, points_size, cm));
+    if (cm.size() != e->cfg.num_nodes) return MPX_E_INVAL;
+    if (!have_results(e)) return MPX_E_STATE;
+    HTRY(hipSetDevice(e->device));
+    TRY(ensure_host_headers(e));
+    std::string d;
+    TRY(commits_from_points(e, cm, d));
+    return put_bytes(d, out, size);
 }
 
 // -------------------------------------------------------------- generators --
@@ -1496,7 +1792,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
         if (f_off[q + 1] > f_off[q] && (N > FAST_MAX_NODES || f_off[q + 1] - f_off[q] > PLAN_FRAGS || (q / N + 1) * BS > L)) {
             const uint64_t w[GP_WORDS] = {f_off[q], f_off[q + 1], 0, 0, q, 0, 0, 0};
             gd.insert(gd.end(), w, w + GP_WORDS);
-            pair_gp[q] = 1;
+            pair_gp[q] = GP_ROUNDS;                     // the full k_apply's host range (num_gp_snap = 0)
         }
     if (gd.empty()) TRY(e->gp_list.alloc(8));
     else TRY(upload(e->gp_list, gd, s));
@@ -1686,6 +1982,51 @@ extern "C" int mpx_read_decisions_sharded(mpx_engine *e, uint8_t **out, uint64_t
     uint64_t at = 0;
     for (int r = 0; r < R; ++r) { ps[r] = all + at; at += lens[r]; }
     rc = mpx_decisions_combine(ps.data(), lens.data(), (uint32_t)R, out, size);
+    std::free(all);
+    return rc;
+}
+
+// Sharded commit reliability over the engine's own communicator: every rank's
+// creation points gathered and merged (mpx_commit_points_combine), the rank whose
+// shard starts at instance 0 (it keeps every COMMIT_REPLY) runs k_commits over the
+// union, and its MPXC is gathered to every rank.  One rank: mpx_read_commits.
+extern "C" int mpx_read_commits_sharded(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    const int R = e->comm ? e->nranks : 1;
+    if (R <= 1) return mpx_read_commits(e, out, size);
+    uint8_t *pts = nullptr;
+    uint64_t plen = 0;
+    TRY(mpx_commit_points(e, &pts, &plen));
+    std::vector<uint64_t> lens(R);
+    uint8_t *all = nullptr;
+    int rc = mpx_comm_allgather_bytes(e, pts, plen, &all, lens.data());
+    std::free(pts);
+    if (rc) return rc;
+    std::vector<const uint8_t *> ps(R);
+    uint64_t at = 0;
+    for (int r = 0; r < R; ++r) { ps[r] = all + at; at += lens[r]; }
+    uint8_t *merged = nullptr;
+    uint64_t mlen = 0;
+    rc = mpx_commit_points_combine(ps.data(), lens.data(), (uint32_t)R, &merged, &mlen);
+    std::free(all);
+    if (rc) return rc;
+    uint8_t *mine = nullptr;
+    uint64_t mylen = 0;
+    if (e->cfg.shard_begin == 0) rc = mpx_read_commits_at(e, merged, mlen, &mine, &mylen);
+    std::free(merged);
+    if (rc) return rc;
+    rc = mpx_comm_allgather_bytes(e, mine, mylen, &all, lens.data());
+    std::free(mine);
+    if (rc) return rc;
+    at = 0;
+    int src = -1;
+    for (int r = 0; r < R; ++r) {
+        if (lens[r]) { if (src >= 0) { std::free(all); return MPX_E_INVAL; } src = r; }
+        if (src < 0) at += lens[r];
+    }
+    if (src < 0) { std::free(all); return MPX_E_STATE; }            // no rank holds instance 0
+    rc = put_bytes(std::string((const char *)all + at, lens[src]), out, size);
     std::free(all);
     return rc;
 }

@@ -140,6 +140,28 @@ long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle)
     return (long)used;
 }
 
+int ValueTable::plain(uint64_t h)
+{
+    if (idx.count(h)) return MPX_OK;
+    if (MPX_HANDLE_PROPOSER(h) >= (1u << 14) || (h & MPX_PRESENT)) return MPX_E_RANGE;
+    // the canonical bytes of Value(proposer, value_id, noop) with an empty payload (FillValue,
+    // multi/paxos.cpp:567-599; member Value_m adds the callback length, :321-408)
+    std::string enc;
+    app<uint32_t>(enc, MPX_HANDLE_PROPOSER(h));
+    app<uint64_t>(enc, MPX_HANDLE_VALUE_ID(h));
+    app<uint8_t>(enc, MPX_HANDLE_NOOP(h) ? 1 : 0);
+    uint32_t eo = 0;
+    if (!MPX_HANDLE_NOOP(h)) {
+        app<uint8_t>(enc, 0);
+        app<uint32_t>(enc, 0);
+        eo = (uint32_t)enc.size();
+        if (member) app<uint32_t>(enc, 0);
+    }
+    idx.emplace(h, Rec{bytes.size(), (uint32_t)enc.size(), eo, 0});
+    bytes += enc;
+    return MPX_OK;
+}
+
 int ValueTable::merge(const ValueTable &o)
 {
     idx.reserve(idx.size() + o.idx.size());
@@ -198,6 +220,9 @@ static void flag(IngestViolation &v, uint64_t code, uint64_t node, uint64_t seq,
     if (!v.code) { v.code = code; v.node = node; v.seq = seq; v.iid = iid; }
 }
 
+static bool sort_entries(std::vector<uint64_t> &iid, std::vector<uint64_t> &pid, std::vector<uint64_t> &val,
+                         size_t first, bool with_pid);
+
 // entries {u64 iid, [u64 pid,] Value}* of an ACCEPT / COMMIT / P_BATCH /
 // PREPARE_REPLY body, sorted by iid (the reference's std::map order)
 static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool with_pid,
@@ -222,12 +247,19 @@ static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool wit
         val.push_back(h);
         ++n_all;
     }
-    // sort this message's entries by iid (stable permutation)
+    dup = sort_entries(iid, pid, val, first, with_pid);
+    return MPX_OK;
+}
+
+// sort one message's entries [first, end) by iid (stable permutation); true when an
+// iid repeats (the reference ASSERTs, multi/paxos.cpp:552)
+static bool sort_entries(std::vector<uint64_t> &iid, std::vector<uint64_t> &pid, std::vector<uint64_t> &val,
+                         size_t first, bool with_pid)
+{
     const size_t n = iid.size() - first;
     bool sorted = true;
     for (size_t k = first + 1; k < iid.size(); ++k)
         if (iid[k - 1] >= iid[k]) { sorted = false; break; }
-    dup = false;
     if (!sorted) {
         std::vector<size_t> perm(n);
         for (size_t k = 0; k < n; ++k) perm[k] = first + k;
@@ -242,9 +274,9 @@ static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool wit
             if (with_pid) pid[first + k] = tp[k];
         }
         for (size_t k = first + 1; k < iid.size(); ++k)
-            if (iid[k - 1] == iid[k]) dup = true;
+            if (iid[k - 1] == iid[k]) return true;
     }
-    return MPX_OK;
+    return false;
 }
 
 int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, const uint8_t *m, size_t len,
@@ -373,6 +405,82 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
     ns.src.push_back(src);
     ns.ballot.push_back(ballot);
     ns.aux.push_back(aux);
+    ns.ent.push_back(ent);
+    ns.cnt.push_back(cnt);
+    return MPX_OK;
+}
+
+int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord &r, uint64_t sb, uint64_t se,
+                  IngestViolation &viol)
+{
+    const uint32_t t = r.type;
+    const uint64_t seq = ns.type.size();
+    uint64_t ent = 0;
+    uint32_t cnt = 0;
+    uint8_t part = 0;
+    auto values = [&]() -> int {
+        for (uint64_t k = 0; k < r.n; ++k) TRY_RC(vt.plain(r.b[k]));
+        return MPX_OK;
+    };
+    auto keep = [&](std::vector<uint64_t> &iid, std::vector<uint64_t> *pid, std::vector<uint64_t> &val, size_t first) {
+        size_t w = first;
+        for (size_t k = first; k < iid.size(); ++k)
+            if (iid[k] >= sb && iid[k] < se) {
+                iid[w] = iid[k]; val[w] = val[k];
+                if (pid) (*pid)[w] = (*pid)[k];
+                ++w;
+            }
+        iid.resize(w); val.resize(w);
+        if (pid) pid->resize(w);
+        return (uint32_t)(w - first);
+    };
+    switch (t) {
+    case MPX_MSG_PREPARE: {                       // ranges [a, b), as decode_record
+        ent = ns.g_a.size();
+        std::vector<std::pair<uint64_t, uint64_t>> g(r.n);
+        for (uint64_t k = 0; k < r.n; ++k) g[k] = {r.a[k], r.b[k]};
+        std::sort(g.begin(), g.end());
+        for (uint64_t k = 0; k < r.n; ++k) {
+            if (k && g[k] == g[k - 1]) flag(viol, MPX_V_DUP_IID, node, seq, g[k].first);
+            if (g[k].first >= g[k].second) continue;
+            if (cnt && g[k].first < ns.g_b.back()) { ns.g_b.back() = std::max(ns.g_b.back(), g[k].second); continue; }
+            ns.g_a.push_back(g[k].first); ns.g_b.push_back(g[k].second);
+            ++cnt;
+        }
+        break;
+    }
+    case MPX_MSG_PREPARE_REPLY: {
+        TRY_RC(values());
+        const size_t first = ns.r_iid.size();
+        for (uint64_t k = 0; k < r.n; ++k) {
+            ns.r_iid.push_back(r.a[k]); ns.r_val.push_back(r.b[k]); ns.r_pid.push_back(r.pid ? r.pid[k] : 0);
+        }
+        if (sort_entries(ns.r_iid, ns.r_pid, ns.r_val, first, true)) flag(viol, MPX_V_DUP_IID, node, seq, 0);
+        ent = first;
+        cnt = keep(ns.r_iid, &ns.r_pid, ns.r_val, first);
+        break;
+    }
+    case MPX_MSG_ACCEPT: case MPX_MSG_COMMIT: case MPX_MSG_P_BATCH: {
+        TRY_RC(values());
+        const size_t first = ns.e_iid.size();
+        std::vector<uint64_t> nopid;
+        for (uint64_t k = 0; k < r.n; ++k) { ns.e_iid.push_back(r.a[k]); ns.e_val.push_back(r.b[k]); }
+        if (sort_entries(ns.e_iid, nopid, ns.e_val, first, false)) flag(viol, MPX_V_DUP_IID, node, seq, 0);
+        ent = first;
+        cnt = keep(ns.e_iid, nullptr, ns.e_val, first);
+        part = r.n && !cnt;
+        break;
+    }
+    case MPX_MSG_REJECT: case MPX_MSG_ACCEPT_REPLY: case MPX_MSG_COMMIT_REPLY: case MPX_MSG_P_START:
+        break;
+    default:
+        return MPX_E_DECODE;
+    }
+    ns.part.push_back(part);
+    ns.type.push_back((uint8_t)t);
+    ns.src.push_back(r.src);
+    ns.ballot.push_back(r.ballot);
+    ns.aux.push_back(r.aux);
     ns.ent.push_back(ent);
     ns.cnt.push_back(cnt);
     return MPX_OK;
@@ -565,9 +673,10 @@ struct EntryPool {
 };
 
 int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen,
-                const std::vector<mpx_epoch> &epochs, HostTrace &ht)
+                const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc)
 {
     const bool member = !epochs.empty();
+    if (wc && (member || !wc->on)) return MPX_E_STATE;            // incremental runs: multi semantics
     ht = HostTrace();
     const uint32_t N = (uint32_t)nodes.size();
     ht.N = N;
@@ -613,6 +722,14 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     std::unordered_map<uint64_t, uint32_t> live;
     std::vector<std::vector<uint32_t>> reps;
     if (member) ht.ee_off.assign(N + 1, 0);
+    // incremental window: batch ids are global (live maps to them); a batch's index in
+    // this window's list, its round ballot, and where a new one's entries are
+    std::unordered_map<uint32_t, uint32_t> gid_local;
+    std::vector<uint64_t> b_bal_w;
+    std::vector<std::pair<uint64_t, uint32_t>> b_ent_w;          // per window batch: pool offset, count (new ones)
+    std::vector<std::pair<uint32_t, uint64_t>> state_new;        // (node, bucket) met by this window's runs
+    const uint64_t gid0 = wc ? wc->batches : 0;
+    uint64_t gid_next = gid0;
 
     for (uint32_t n = 0; n < N; ++n) {
         const NodeStream &ns = nodes[n];
@@ -630,6 +747,38 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         touched.clear(); round_b.clear();
         int64_t maxb = -1;                              // highest bucket with a fragment of this node
         live.clear();
+        uint64_t cur_bal = 0;                           // the ballot of the node's current round
+        if (wc) {                                       // the window starts where the last one ended
+            live = wc->live[n];
+            for (uint64_t b : wc->round_b[n]) { in_round[b] = 1; round_b.push_back(b); }
+            maxb = wc->maxb[n];
+            cur_bal = wc->round_ballot[n];
+        }
+        // window: this window's index of global batch `gid` (an earlier batch joins the list
+        // with its carried entries as chosen-log runs)
+        auto local_batch = [&](uint32_t gid) -> uint32_t {
+            auto it = gid_local.find(gid);
+            if (it != gid_local.end()) return it->second;
+            const uint32_t j = (uint32_t)ht.b_msg.size();
+            gid_local.emplace(gid, j);
+            ht.b_msg.push_back(NONE32); ht.b_pstart.push_back(NONE32); ht.b_gid.push_back(gid);
+            reps.emplace_back();
+            b_bal_w.push_back(wc->b_bal[gid]);
+            b_ent_w.push_back({0, 0});
+            auto be = wc->b_ents.find(gid);
+            if (be != wc->b_ents.end() && !be->second.empty()) {
+                NodeStream tmp;
+                for (auto &x : be->second) { tmp.e_iid.push_back(x.first); tmp.e_val.push_back(x.second); }
+                const uint64_t o = pool.intern(tmp, 0, (uint32_t)tmp.e_iid.size(), ht);
+                cut_runs(ht.e_iid.data(), o, (uint32_t)tmp.e_iid.size(), sb, [&](uint64_t b, uint64_t e0, uint32_t c, uint8_t st, bool dense) {
+                    Frag f{e0, j, (uint16_t)c, st, (uint8_t)((dense ? FR_DENSE : 0) | (K_BATCH << 4))};
+                    if (!dense) ht.any_sparse = true;
+                    cfr.push_back({b, f});
+                    cfcount[b]++;
+                });
+            }
+            return j;
+        };
         bool last_virtual = false;                      // the node's last scan record stands for left-out ACCEPTs
         // member semantics: no role or version logic here — the per-message gate
         // (acceptor incarnation, version filter, proposer presence) is computed on
@@ -651,14 +800,17 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             bool drop = ns.part[k] != 0 || (t == MPX_MSG_COMMIT_REPLY && sb != 0);
             int64_t vote_j = -1;
             if (t == MPX_MSG_P_START) {
+                if (wc)                                  // earlier windows' batches can no longer be chosen
+                    for (auto &x : live) if (x.second < gid0) wc->b_ents.erase(x.second);
                 live.clear();
+                cur_bal = ns.ballot[k];
             } else if (t == MPX_MSG_P_BATCH) {
                 if (drop) live.erase(ns.aux[k]);
-                else live[ns.aux[k]] = (uint32_t)ht.b_msg.size();
+                else live[ns.aux[k]] = wc ? (uint32_t)gid_next : (uint32_t)ht.b_msg.size();
             } else if (t == MPX_MSG_ACCEPT_REPLY) {
                 auto it = live.find(ns.aux[k]);
                 if (it == live.end()) drop = true;   // stale, or its batch is another shard's
-                else vote_j = it->second;
+                else vote_j = wc ? local_batch(it->second) : it->second;
             }
             if (drop) {
                 ++ht.dropped;
@@ -727,6 +879,12 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_E_EPOCH) { pl.push_back(g); pl_cnt[n]++; }
             if (t == MPX_MSG_P_START) pstart = g;
             if (t == MPX_MSG_P_BATCH) {
+                if (wc) {
+                    gid_local.emplace((uint32_t)gid_next, (uint32_t)ht.b_msg.size());
+                    ht.b_gid.push_back((uint32_t)gid_next++);
+                    b_bal_w.push_back(cur_bal);
+                    b_ent_w.push_back({ent, ns.cnt[k]});
+                }
                 ht.b_msg.push_back(g);
                 ht.b_pstart.push_back(pstart);
                 reps.emplace_back();
@@ -739,7 +897,10 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                     if (!dense) ht.any_sparse = true;
                     fr.push_back({b * N + n, f});            // pair index: bucket-major
                     fcount[b * N + n]++;
-                    if (first_frag[b] == NONE32) { first_frag[b] = g; touched.push_back(b); maxb = std::max<int64_t>(maxb, (int64_t)b); }
+                    if (first_frag[b] == NONE32) {
+                        first_frag[b] = g; touched.push_back(b); maxb = std::max<int64_t>(maxb, (int64_t)b);
+                        if (wc && !wc->state_b[n][b]) state_new.push_back({n, b});
+                    }
                     if (kind == K_PREPLY && !in_round[b]) { in_round[b] = 1; round_b.push_back(b); }
                 });
             }
@@ -757,7 +918,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                     // several ranges of one PREPARE can meet in a bucket (holes): list it
                     // once, its aux word = first range (absolute) | ranges meeting it << 32
                     for (uint64_t b = lo; b < hi; ++b) {
-                        if (first_frag[b] >= g) continue;
+                        if (first_frag[b] >= g && !(wc && wc->state_b[n][b])) continue;   // (window: or earlier ones')
                         if (!evp.empty() && evp.back().second == g && b == last_b && evp.back().first == b * N + n) {
                             evx.back() = (evx.back() + (1ull << 32)) & ~EVX_ONE;   // a second range: no interval
                         } else if (evp.empty() || evp.back().second != g || b > last_b) {
@@ -783,7 +944,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                     if (first_frag[b] < g) add_ev(b);
             }
             if (t == MPX_MSG_P_BATCH) {
-                const uint32_t j = (uint32_t)ht.b_msg.size() - 1;
+                const uint32_t j = wc ? gid_local[(uint32_t)(gid_next - 1)] : (uint32_t)ht.b_msg.size() - 1;
                 cut_runs(ht.e_iid.data(), ent, ns.cnt[k], sb, [&](uint64_t b, uint64_t e0, uint32_t c, uint8_t st, bool dense) {
                     Frag f{e0, j, (uint16_t)c, st, (uint8_t)((dense ? FR_DENSE : 0) | (K_BATCH << 4))};
                     if (!dense) ht.any_sparse = true;
@@ -791,6 +952,19 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                     cfcount[b]++;
                 });
             }
+        }
+        if (wc) {                                        // the carry past this node's window
+            wc->live[n] = live;
+            wc->round_b[n] = round_b;
+            wc->maxb[n] = maxb;
+            wc->round_ballot[n] = cur_bal;
+            for (auto &x : live)                         // new batches still open: keep their entries
+                if (x.second >= gid0) {
+                    const auto &be = b_ent_w[gid_local[x.second]];
+                    auto &dst = wc->b_ents[x.second];
+                    dst.clear();
+                    for (uint32_t q = 0; q < be.second; ++q) dst.push_back({ht.e_iid[be.first + q], ht.e_val[be.first + q]});
+                }
         }
     }
     ht.node_off[N] = ht.m_type.size();
@@ -817,7 +991,13 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             ht.b_rsrc[r] = std::min<uint32_t>(ht.m_src[g], 0xFFFF);   // member: epoch bits added on the device
         }
         ht.b_bal.resize(ht.b_msg.size());
-        for (size_t j = 0; j < ht.b_msg.size(); ++j) ht.b_bal[j] = ht.b_pstart[j] == NONE32 ? 0 : ht.m_ballot[ht.b_pstart[j]];
+        for (size_t j = 0; j < ht.b_msg.size(); ++j)
+            ht.b_bal[j] = wc ? b_bal_w[j] : ht.b_pstart[j] == NONE32 ? 0 : ht.m_ballot[ht.b_pstart[j]];
+        if (wc) {
+            for (size_t j = 0; j < ht.b_msg.size(); ++j)
+                if (ht.b_msg[j] != NONE32) wc->b_bal.push_back(b_bal_w[j]);   // new batches, in id order
+            wc->batches = gid_next;
+        }
     }
 
     // fragment CSR per (node, bucket), stable (keeps message order)
@@ -865,7 +1045,23 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     // pairs that are not lean (mpx_internal.hpp plan_shape_ok: one plan word of
     // k_plan) go to the general kernel's work list
     ht.pair_gp.assign(N * NB, 0);
-    for (uint64_t b = 0; b < NB; ++b)
+    if (wc) {
+        // incremental window: every pair with runs or events of the window walks the
+        // window apply kernel (k_apply_win), on the state earlier windows left
+        for (uint64_t b = 0; b < NB; ++b)
+            for (uint32_t n = 0; n < N; ++n) {
+                const uint64_t p = b * N + n;
+                if (ht.f_off[p + 1] == ht.f_off[p] && ht.ev_off[p + 1] == ht.ev_off[p]) continue;
+                ht.gp_list.push_back(p);
+                ht.gp_base.push_back(wc->state_b[n][b]);
+                ht.pair_gp[p] = GP_ROUNDS;
+            }
+        for (auto &x : state_new) wc->state_b[x.first][x.second] = 1;
+        for (uint64_t b = 0; b < NB; ++b)
+            if (ht.cf_off[b + 1] > ht.cf_off[b]) ht.cb_list.push_back((uint32_t)b);
+        ht.num_gp_simple = ht.num_gp_snap = 0;
+    }
+    for (uint64_t b = 0; b < NB && !wc; ++b)
         for (uint32_t n = 0; n < N; ++n) {
             const uint64_t p = b * N + n, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
             if (!nf) continue;
@@ -875,14 +1071,14 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                 for (uint64_t f = 0; f < nf; ++f) std::memcpy(&w1[f], reinterpret_cast<const uint8_t *>(&ht.frags[f0 + f]) + 8, 8);
                 fast = plan_shape_ok(w1, (uint32_t)nf);
             }
-            if (!fast) { ht.gp_list.push_back(p); ht.pair_gp[p] = 1; }
+            if (!fast) { ht.gp_list.push_back(p); ht.pair_gp[p] = GP_LIST; }
         }
     // work-list order: the pairs with no snapshot events and no promise-reply runs
     // first (k_apply's SIMPLE instantiation takes them), pair order kept
     // then those with no promise-reply runs (their events are PREPAREs only, member:
     // and E_EPOCHs; k_apply AM_SNAP), then the rest (promise rounds)
-    ht.num_gp_simple = ht.num_gp_snap = 0;
-    {
+    if (!wc) {
+        ht.num_gp_simple = ht.num_gp_snap = 0;
         auto no_preply = [&](uint64_t p) {
             for (uint64_t f = ht.f_off[p]; f < ht.f_off[p + 1]; ++f)
                 if ((ht.frags[f].flags >> 4) == K_PREPLY) return false;
@@ -892,10 +1088,9 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         ht.num_gp_snap = (uint64_t)(mid - ht.gp_list.begin());
         auto mid2 = std::stable_partition(ht.gp_list.begin(), mid, [&](uint64_t p) { return !ht.pair_ev[p]; });
         ht.num_gp_simple = (uint64_t)(mid2 - ht.gp_list.begin());
-        // member: k_plan_member takes the pairs before `mid` (or lists them for k_apply
-        // itself); the promise-round pairs stay on the host range of the full kernel
-        if (member)
-            for (auto it = mid; it != ht.gp_list.end(); ++it) ht.pair_gp[*it] = GP_ROUNDS;
+        // k_plan_list takes the pairs before `mid` (or lists them for k_apply itself);
+        // the promise-round pairs stay on the host range of the full kernel
+        for (auto it = mid; it != ht.gp_list.end(); ++it) ht.pair_gp[*it] = GP_ROUNDS;
     }
     // slots for sparse fragments
     if (ht.any_sparse) {

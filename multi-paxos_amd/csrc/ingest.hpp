@@ -33,6 +33,8 @@ struct ValueTable {
     // add every Value of `o` (decoded on another thread); MPX_E_VALUE when a
     // handle names different bytes in the two tables
     int merge(const ValueTable &o);
+    // a handle with no bytes yet: the payload-free Value it names (mpx_submit_soa)
+    int plain(uint64_t handle);
 };
 
 // One node's decoded receive stream (submission order).
@@ -51,6 +53,30 @@ struct NodeStream {
 };
 
 struct IngestViolation { uint64_t code = 0, node = 0, seq = 0, iid = 0, count = 0; };
+
+// Incremental runs (MPX_FLAG_INCREMENTAL): what build_trace needs from
+// the windows before the current one to list the current window's snapshot events and
+// vote lists without its history.  O(nodes + buckets with state + live batches).
+struct WindowCarry {
+    bool on = false;
+    uint64_t batches = 0;                                        // batches of earlier windows (global ids 0..)
+    std::vector<std::unordered_map<uint64_t, uint32_t>> live;    // per node: accept id -> global batch id
+    std::vector<uint64_t> round_ballot;                          // per node: its last P_START's ballot (0: none)
+    std::vector<std::vector<uint8_t>> state_b;                   // per node, per bucket: a run of the node met it
+    std::vector<int64_t> maxb;                                   // per node: the highest such bucket (-1: none)
+    std::vector<std::vector<uint64_t>> round_b;                  // per node: buckets with promise-reply runs since
+                                                                 //   its last P_START
+    std::vector<uint64_t> b_bal;                                 // per global batch: its round's ballot
+    // per global batch still live and not chosen: its entries {iid, handle}, for the
+    // chosen log when a later window completes its votes
+    std::unordered_map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> b_ents;
+    void init(uint32_t N, uint64_t NB)
+    {
+        on = true; batches = 0;
+        live.assign(N, {}); round_ballot.assign(N, 0); state_b.assign(N, std::vector<uint8_t>(NB, 0));
+        maxb.assign(N, -1); round_b.assign(N, {}); b_bal.clear(); b_ents.clear();
+    }
+};
 
 // Flattened, bucketed host copy of the trace — mirrors the device arrays.
 struct HostTrace {
@@ -92,6 +118,13 @@ struct HostTrace {
     std::vector<uint64_t> b_rep_off;
     std::vector<uint64_t> cf_off;
     std::vector<Frag> cfrags;
+    // incremental window (build_trace with a WindowCarry): per batch of the window's list
+    // its global id (new batches and earlier ones that get votes here; b_msg = NONE32 for
+    // an earlier one), per work-list pair whether earlier windows left state in it, and the
+    // buckets with chosen-log runs
+    std::vector<uint32_t> b_gid;
+    std::vector<uint8_t> gp_base;
+    std::vector<uint32_t> cb_list;
 };
 
 // Decode one record of `node`'s stream into `ns`.  Entries outside
@@ -99,13 +132,25 @@ struct HostTrace {
 // is marked (`part`) and left out by build_trace (header sharding).
 int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, const uint8_t *m, size_t len,
                   uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol);
+// one record handed over already decoded (mpx_submit_soa, multi semantics): the same
+// NodeStream fields decode_record fills from the wire bytes
+struct SoaRecord {
+    uint32_t type, src;
+    uint64_t ballot, aux;
+    uint64_t n;                                   // entries (PREPARE: ranges)
+    const uint64_t *a, *b, *pid;                  // iid, handle, proposal id (PREPARE: range start, end)
+};
+int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord &r, uint64_t shard_begin,
+                  uint64_t shard_end, IngestViolation &viol);
 // member semantics wire formats (member/paxos.cpp:846-932)
 int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const uint8_t *m, size_t len,
                          uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol);
 
 // Flatten node streams and build every index the kernels walk.  `epochs`
 // non-empty selects member semantics (role / version gates, E_EPOCH events).
+// With `wc` (incremental runs, multi semantics): `nodes` hold one window's records; the
+// window is built on the carried state and the carry is advanced past it.
 int build_trace(const std::vector<NodeStream> &nodes, uint64_t shard_begin, uint64_t shard_len,
-                const std::vector<mpx_epoch> &epochs, HostTrace &ht);
+                const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc = nullptr);
 
 }  // namespace mpx

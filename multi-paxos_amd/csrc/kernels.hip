@@ -349,11 +349,38 @@ __global__ __launch_bounds__(256) void k_gate_votes(DevView v)
 
 constexpr uint32_t SCAN_ROUNDS = SCAN_CHUNK / 256;   // rounds of 64 records per wave
 
+// Per-step reset of what the step accumulates (k_reset, or the head of k_scan_chunk when
+// it is the step's first kernel): thread t of T zeroes its share, grid-stride
+__device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64_t t, uint64_t T)
+{
+    const uint64_t np = (uint64_t)v.N * v.NB;
+    const uint64_t n16 = v.window ? 0 : (np + 15) / 16;     // (a window keeps no slot rows)
+    for (uint64_t i = t; i < n16; i += T) {          // st_valid: 16 bytes per thread, byte tail
+        if (16 * i + 16 <= np) *reinterpret_cast<uint4 *>(v.st_valid + 16 * i) = uint4{0, 0, 0, 0};
+        else for (uint64_t k = 16 * i; k < np; ++k) v.st_valid[k] = 0;
+    }
+    for (uint64_t i = t; i < (v.window ? 0 : v.NB); i += T) v.chosen_valid[i] = 0;
+    for (uint64_t i = t; i < 8ull * n_partials; i += T) v.partials[i] = 0;
+    // nodes without messages keep promised = max_seen = 0 (a window: what the windows before left)
+    for (uint64_t i = t; i < 2ull * v.N; i += T) v.node_scal[i] = v.window ? v.scal_base[i] : 0;
+    for (uint64_t i = t; i < v.out_subs; i += T) v.out_cursor[OUT_STRIDE * i] = 0;
+    if (t == 0) {
+        v.fast_rest[0] = 0;
+        v.fast_rest[1] = 0;                          // k_chosen's last-block ticket
+        *v.gp_dyn_n = 0;
+        if (v.window) *v.outv_n = 0;
+        v.viol->code = v.viol->node = v.viol->seq = v.viol->iid = v.viol->count = 0;
+    }
+}
+
 // Chunk aggregates over the header-scan stream: max of the PREPARE ids and of
 // the max_seen contributions of SCAN_CHUNK records (order-free, coalesced)
-__global__ __launch_bounds__(256) void k_scan_chunk(DevView v)
+// RESET: the step's first kernel also does k_reset's work (one launch less per step)
+template <bool RESET>
+__global__ __launch_bounds__(256) void k_scan_chunk(DevView v, uint32_t n_partials)
 {
     __shared__ uint64_t l[2][4];
+    if (RESET) reset_state(v, n_partials, (uint64_t)blockIdx.x * 256 + threadIdx.x, (uint64_t)gridDim.x * 256);
     const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
     uint64_t lp = 0, ls = 0;
@@ -389,7 +416,7 @@ __global__ __launch_bounds__(256) void k_scan_node(DevView v)
     __shared__ uint64_t l[8];
     const uint32_t n = blockIdx.x;
     const uint32_t c0 = v.node_chunk_off[n], c1 = v.node_chunk_off[n + 1];
-    uint64_t carry_p = 0, carry_s = 0;
+    uint64_t carry_p = v.window ? v.scal_base[2 * n] : 0, carry_s = v.window ? v.scal_base[2 * n + 1] : 0;
     for (uint32_t base = c0; base < c1; base += 256) {
         uint32_t c = base + threadIdx.x;
         uint64_t p = c < c1 ? v.chunk_agg[2 * c] : 0, s = c < c1 ? v.chunk_agg[2 * c + 1] : 0;
@@ -456,6 +483,7 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
     if (v.scan_node_pass) {
         if (threadIdx.x == 0) { xp = v.chunk_carry[2 * c]; xs = v.chunk_carry[2 * c + 1]; }
     } else {
+        if (v.window && threadIdx.x == 0) { xp = v.scal_base[2 * cn]; xs = v.scal_base[2 * cn + 1]; }   // earlier windows
         for (uint32_t k = c0 + threadIdx.x; k < c; k += 256) {
             const uint64_t ap = v.chunk_agg[2 * k], as = v.chunk_agg[2 * k + 1];
             xp = xp > ap ? xp : ap;
@@ -639,6 +667,8 @@ __global__ __launch_bounds__(64) void k_prop_chunk(DevView v)
     const uint32_t n = v.pc_node[c];
     const uint64_t i0 = v.pc_beg[c], i1 = v.pc_end[c];
     PropState st{0, 0, 0, i0 == v.pl_off[n] ? 1u : 0u};
+    if (v.window && st.known)                          // a window's first chunk: the round carried in
+        st = PropState{v.prop_in[3 * n], v.prop_in[3 * n + 1], (uint32_t)v.prop_in[3 * n + 2], 1u};
     uint32_t head;
     prop_range(v, n, i0, i1, st, head);
     if (threadIdx.x == 0) {
@@ -654,7 +684,10 @@ __global__ __launch_bounds__(64) void k_prop_node(DevView v)
     const uint32_t n = blockIdx.x;
     if (n >= v.N) return;
     const uint32_t c0 = v.pc_node_off[n], c1 = v.pc_node_off[n + 1];
-    if (c0 == c1) return;
+    if (c0 == c1) {
+        if (v.window && threadIdx.x < 3) v.prop_out[3 * n + threadIdx.x] = v.prop_in[3 * n + threadIdx.x];
+        return;
+    }
     PropState st{v.pc_state[3 * c0], v.pc_state[3 * c0 + 1], (uint32_t)(v.pc_state[3 * c0 + 2] & 1), 1};
     for (uint32_t c = c0 + 1; c < c1; ++c) {
         const uint64_t i0 = v.pc_beg[c], i1 = v.pc_end[c];
@@ -664,6 +697,9 @@ __global__ __launch_bounds__(64) void k_prop_node(DevView v)
         if (h != ~0u) {
             st.cb = v.pc_state[3 * c]; st.cmask = v.pc_state[3 * c + 1]; st.cprep = (uint32_t)(v.pc_state[3 * c + 2] & 1);
         }
+    }
+    if (v.window && threadIdx.x == 0) {                // the round the next window starts from
+        v.prop_out[3 * n] = st.cb; v.prop_out[3 * n + 1] = st.cmask; v.prop_out[3 * n + 2] = st.cprep;
     }
 }
 
@@ -707,7 +743,12 @@ __global__ __launch_bounds__(256) void k_votes(DevView v)
     const bool member = v.semantics == MPX_SEM_MEMBER;
     uint64_t mask = 0;
     uint64_t chosen_r = ~0ull;
-    for (uint64_t r = rs; r < re; ++r) {
+    // a window: the batch's accepted_ so far, and no more votes once an earlier window chose it
+    // (OnAcceptReply erases the batch at quorum, multi/paxos.cpp:1416-1424)
+    const uint32_t gid = v.window && have ? v.b_gid[j] : 0;
+    const bool done = v.window && have && v.g_done[gid];
+    if (v.window && have) mask = v.g_mask[gid];
+    for (uint64_t r = done ? re : rs; r < re; ++r) {
         const uint64_t o = r - r0;
         const uint64_t b = o < VOTE_LDS ? lbal[wv][o] : v.b_rbal[r];
         const uint32_t x = o < VOTE_LDS ? lsrc[wv][o] : v.b_rsrc[r];
@@ -731,6 +772,10 @@ __global__ __launch_bounds__(256) void k_votes(DevView v)
         if ((uint32_t)__popcll(mask) >= q) { chosen_r = r; break; }   // :1416
     }
     if (have) v.b_chosen[j] = chosen_r == ~0ull ? NONE32 : v.b_rep[chosen_r];
+    if (v.window && have && !done) {
+        v.g_mask[gid] = mask;
+        if (chosen_r != ~0ull) v.g_done[gid] = 1;
+    }
 }
 
 // ------------------------------------------------------------- apply ----
@@ -1444,40 +1489,61 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
     }
 }
 
-// Member plan path (the timed member step): k_plan's reduction for member semantics
-// (member/paxos.cpp:1744-1793 Acceptor::OnAccept / OnLearn, :1029-1060
-// Learner::OnLearn, :1952-1957 Acceptor deletion), one thread per (node, bucket)
-// pair.  Accept and learn are std::map::insert, so per instance the state is fixed
-// by the FIRST learn covering it (the learned Value sticks, and an accepted entry of
-// a learned instance is never made), else by the first granted accept after the
-// last marker that deleted or recreated the node's Acceptor (F_ACCCLR: its accepted
-// map goes, learned entries stay with the Learner).  Runs cut the bucket into at
-// most four segments (plan_add_split); within a segment every run covers all or
-// none of it, so the pair walks its runs and its snapshot events (E_EPOCH markers,
-// PREPAREs) in message order with four segment states instead of 256 slot states,
-// and one plan word (k_store / k_store8 stream it) holds the result.  The counters
-// follow the per-slot walk exactly: A = inserts, L = every learn-covered slot.
+// One snapshot run record (OUT_RUN): slots [lo, lo + len) of a planned pair's bucket, all
+// fixed by fragment `ref`, go into the PREPARE_REPLY of message `msg`; the host expands it
+// slot by slot (engine.cpp fetch_results), so a segment costs one 12-byte record instead
+// of one per slot.
+__device__ inline void emit_run(const DevView &v, uint32_t msg, uint32_t ref, uint32_t lo, uint32_t len)
+{
+    const uint32_t sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (v.out_subs - 1);
+    const unsigned long long at = atomicAdd(&v.out_cursor[OUT_STRIDE * sub], 1ull);
+    if (at < v.out_cap) {
+        OutRec r;
+        r.msg = msg; r.ref = ref; r.aux = OUT_RUN | lo | (len << OUT_RUN_SHIFT);
+        v.out[(uint64_t)sub * v.out_cap + at] = r;
+    }
+}
+
+// List plan path (the timed step for the general work list's pairs without promise
+// rounds): k_plan's reduction extended to pairs with snapshot events, one thread per
+// (node, bucket) pair whose pair_gp is GP_LIST.  Runs cut the bucket into at most four
+// segments (plan_add_split); within a segment every run covers all or none of it, so the
+// pair walks its runs and its events in message order with four segment states instead
+// of 256 slot states, and one plan word (k_store / k_store8 stream it) holds the result.
+//   multi (multi/paxos.cpp:1359-1404 OnAccept, :1494-1518 OnCommit): a granted ACCEPT
+//     overwrites every segment it covers that is not committed, the first COMMIT fixes it;
+//   MEMBER (member/paxos.cpp:1744-1793 Acceptor::OnAccept / OnLearn, :1029-1060
+//     Learner::OnLearn, :1952-1957 Acceptor deletion): accept and learn are
+//     std::map::insert — the FIRST learn covering an instance fixes it, else the first
+//     granted accept after the last marker that deleted or recreated the node's Acceptor
+//     (F_ACCCLR: its accepted map goes, learned entries stay with the Learner).
+// A granted PREPARE while a segment holds an entry is FilterAcceptedValues (multi :902-922,
+// member :1700-1727): per segment meeting the prepare's ranges, one run record (emit_run).
+// The counters follow the per-slot walk exactly (A = applications, L = every learn /
+// commit-covered slot, P = snapshot entries).
 //
-// The pair is listed for k_apply instead (gp_dyn, one append per wave) when:
-// more than MPLAN_FRAGS runs, a run that is not a dense accept / learn run, a fifth
-// segment, a partial last bucket, a granted PREPARE while any segment holds an
-// entry (FilterAcceptedValues emits a snapshot, :1700-1727), an accept / learn over
-// a learned segment whose Value entry differs (the reference's Value check, :1763-
-// 1769), or any other event type.  Promise-round pairs (GP_ROUNDS) are never taken:
-// the host range of the full k_apply has them.  Bucket i < NB also plans its chosen
-// log (plan_chosen).  The staged descriptor words carry the accept runs' scan flag
-// (F_GRANTED) in bit 57 after the gather, so the walk reads only LDS.
+// The pair is listed for k_apply instead (gp_dyn, one append per wave) when: more than
+// MPLAN_FRAGS runs, a run that is not a dense accept / commit run, a fifth segment, a
+// partial last bucket, or a commit / learn (member: also an accept) over a committed
+// segment whose Value entry differs (the reference's Value check: k_apply compares the
+// Values).  Nothing is emitted for a listed pair: the walk runs once to decide, and a second
+// time to emit only when it emits and the pair is kept.  Promise-round pairs (GP_ROUNDS)
+// are never taken: the host range of the full k_apply has them.  MEMBER also plans the
+// chosen log (bucket i < NB, plan_chosen); multi's k_plan did.  The staged descriptor
+// words carry the accept runs' scan flag (F_GRANTED) in bit 57 after the gather, so the
+// walk reads only LDS.
 constexpr uint64_t MP_GRANTED = 1ull << 57;
-__global__ __launch_bounds__(256) void k_plan_member(DevView v, uint32_t apply_wgs)
+template <bool MEMBER>
+__global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs)
 {
     constexpr uint32_t F = MPLAN_FRAGS;
     __shared__ uint64_t w_lds[4][MPLAN_LDS];
-    __shared__ unsigned long long red[4][3];
+    __shared__ unsigned long long red[4][4];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t N = v.N;
     const uint64_t NB = v.NB, np = (uint64_t)N * NB;
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    unsigned long long cA = 0, cL = 0, cC = 0;
+    unsigned long long cA = 0, cL = 0, cC = 0, cP = 0;
     const uint64_t ic = i < np ? i : np, in = i < np ? i + 1 : np;
     const uint64_t oa = v.f_off[ic], o1 = v.f_off[in];
     const uint64_t e0 = v.ev_off[ic], e1 = v.ev_off[in];
@@ -1531,7 +1597,7 @@ __global__ __launch_bounds__(256) void k_plan_member(DevView v, uint32_t apply_w
 #pragma unroll
                 for (uint32_t k = 0; k < F; ++k)
                     if (k < len && (fg[k] & F_GRANTED)) W[k] |= MP_GRANTED;
-                uint32_t lo[4], sl[4], pres = 0, comm = 0, fix[4] = {0, 0, 0, 0};
+                uint32_t lo[4], sl[4];
 #pragma unroll
                 for (uint32_t g = 0; g < 4; ++g) {
                     lo[g] = g ? sp[g - 1] : 0;
@@ -1539,56 +1605,99 @@ __global__ __launch_bounds__(256) void k_plan_member(DevView v, uint32_t apply_w
                 }
                 // the entry index of run k at slot s, minus s (the pool is
                 // content-addressed: equal ones name one Value; read only over a
-                // learned segment)
+                // committed segment)
                 auto ent_at = [&](uint32_t k) -> uint64_t {
                     return v.frags[oa + k].entry - ((W[k] >> 48) & 0xFF);
                 };
-                auto run = [&](uint32_t k) {
-                    const uint64_t w = W[k];
-                    const uint32_t cnt = (uint32_t)(w >> 32) & 0xFFFF, st0 = (uint32_t)(w >> 48) & 0xFF;
-                    const bool learn = (w >> 60) == K_COMMIT;
-                    if (!learn && !(w & MP_GRANTED)) return;          // a rejected / dropped accept
+                const uint64_t blo = v.shard_begin + (b << BSH);
+                // one pass over the pair in message order; EMIT: the second pass, which
+                // writes the snapshot records (the first one decided the pair is kept)
+                auto walk = [&](auto emit_tag, uint32_t &pres, uint32_t &comm, uint32_t (&fix)[4],
+                                unsigned long long &a, unsigned long long &l, unsigned long long &p,
+                                bool &snap) {
+                    constexpr bool EMIT = decltype(emit_tag)::value;
+                    auto run = [&](uint32_t k) {
+                        const uint64_t w = W[k];
+                        const uint32_t cnt = (uint32_t)(w >> 32) & 0xFFFF, st0 = (uint32_t)(w >> 48) & 0xFF;
+                        const bool learn = (w >> 60) == K_COMMIT;
+                        if (!learn && !(w & MP_GRANTED)) return;          // a rejected / dropped accept
 #pragma unroll
-                    for (uint32_t g = 0; g < 4; ++g) {
-                        if (!sl[g] || lo[g] < st0 || lo[g] >= st0 + cnt) continue;
-                        if (learn) cL += sl[g];
-                        if ((comm >> g) & 1) {
-                            if (ent_at(k) != ent_at(fix[g])) fb = true;   // the Value check: k_apply
-                        } else if (learn) {
-                            comm |= 1u << g; pres |= 1u << g; fix[g] = k;
-                        } else if (!((pres >> g) & 1)) {
-                            pres |= 1u << g; fix[g] = k; cA += sl[g];
+                        for (uint32_t g = 0; g < 4; ++g) {
+                            if (!sl[g] || lo[g] < st0 || lo[g] >= st0 + cnt) continue;
+                            if (learn) l += sl[g];
+                            if ((comm >> g) & 1) {
+                                if ((MEMBER || learn) && ent_at(k) != ent_at(fix[g])) fb = true;   // the Value check: k_apply
+                                // (multi: an ACCEPT over a committed instance is skipped, :1380)
+                            } else if (learn) {
+                                comm |= 1u << g; pres |= 1u << g; fix[g] = k;
+                            } else if (MEMBER) {
+                                if (!((pres >> g) & 1)) { pres |= 1u << g; fix[g] = k; a += sl[g]; }   // insert
+                            } else {
+                                pres |= 1u << g; fix[g] = k; a += sl[g];     // multi: the last granted accept
+                            }
+                        }
+                    };
+                    // FilterAcceptedValues over the bucket-local interval [il, ih)
+                    auto snap_iv = [&](uint32_t g8, uint32_t il, uint32_t ih) {
+#pragma unroll
+                        for (uint32_t g = 0; g < 4; ++g) {
+                            if (!((pres >> g) & 1)) continue;
+                            const uint32_t x0 = lo[g] > il ? lo[g] : il, x1 = lo[g] + sl[g] < ih ? lo[g] + sl[g] : ih;
+                            if (x0 >= x1) continue;
+                            p += x1 - x0;
+                            if (EMIT) emit_run(v, g8, (uint32_t)(oa + fix[g]), x0, x1 - x0);
+                        }
+                    };
+                    auto event = [&](uint32_t info, uint32_t g8, uint64_t e) {
+                        const uint32_t t8 = info & 0xFF, fl = info >> 8;
+                        if (MEMBER && t8 == MPX_MSG_E_EPOCH) {
+                            if (fl & F_ACCCLR) pres &= comm;               // the Acceptor's accepted map goes
+                        } else if (t8 == MPX_MSG_PREPARE) {
+                            if (!(fl & F_GRANTED) || !pres) return;
+                            snap = true;
+                            const uint64_t ax = v.ev_aux[e];
+                            if (ax & EVX_ONE) {
+                                snap_iv(g8, (uint32_t)(ax >> 40) & 0x1FF, (uint32_t)(ax >> 49) & 0x1FF);
+                            } else {
+                                const uint32_t r0 = (uint32_t)ax, nr = (uint32_t)(ax >> 32) & 0xFF;
+                                for (uint32_t r = 0; r < nr; ++r) {        // sorted, disjoint ranges
+                                    const uint64_t ra = v.g_a[r0 + r], rb = v.g_b[r0 + r];
+                                    const uint64_t x0 = ra > blo ? ra - blo : 0, x1 = rb < blo + BS ? rb - blo : BS;
+                                    if (rb > blo && ra < blo + BS && x0 < x1) snap_iv(g8, (uint32_t)x0, (uint32_t)x1);
+                                }
+                            }
+                        }
+                        // any other event of a pair without promise-reply runs acts on nothing
+                        // here (k_apply AM_SNAP: a P_START clears an empty merge, a quorum emits it)
+                    };
+                    uint32_t k = 0;
+                    for (uint64_t e = e0; e < e1 && !fb; e += 8) {
+                        const uint32_t m = (uint32_t)(e1 - e < 8 ? e1 - e : 8);
+                        uint32_t em[8], ei[8];
+#pragma unroll
+                        for (uint32_t j = 0; j < 8; ++j) em[j] = j < m ? v.ev_msg[e + j] : NONE32;
+#pragma unroll
+                        for (uint32_t j = 0; j < 8; ++j)
+                            ei[j] = j < m ? (uint32_t)v.m_type[em[j]] | ((uint32_t)v.m_flags[em[j]] << 8) : 0;
+#pragma unroll
+                        for (uint32_t j = 0; j < 8; ++j) {
+                            if (j >= m) break;
+                            while (k < len && (uint32_t)W[k] <= em[j]) run(k++);   // a message's runs before its event
+                            event(ei[j], em[j], e + j);
                         }
                     }
+                    while (k < len && !fb) run(k++);
                 };
-                auto event = [&](uint32_t info) {
-                    const uint32_t t8 = info & 0xFF, fl = info >> 8;
-                    if (t8 == MPX_MSG_E_EPOCH) {
-                        if (fl & F_ACCCLR) pres &= comm;               // the Acceptor's accepted map goes
-                    } else if (t8 == MPX_MSG_PREPARE) {
-                        if ((fl & F_GRANTED) && pres) fb = true;       // a snapshot to emit: k_apply
-                    } else {
-                        fb = true;
-                    }
-                };
-                uint32_t k = 0;
-                for (uint64_t e = e0; e < e1 && !fb; e += 8) {
-                    const uint32_t m = (uint32_t)(e1 - e < 8 ? e1 - e : 8);
-                    uint32_t em[8], ei[8];
-#pragma unroll
-                    for (uint32_t j = 0; j < 8; ++j) em[j] = j < m ? v.ev_msg[e + j] : NONE32;
-#pragma unroll
-                    for (uint32_t j = 0; j < 8; ++j)
-                        ei[j] = j < m ? (uint32_t)v.m_type[em[j]] | ((uint32_t)v.m_flags[em[j]] << 8) : 0;
-#pragma unroll
-                    for (uint32_t j = 0; j < 8; ++j) {
-                        if (j >= m) break;
-                        while (k < len && (uint32_t)W[k] <= em[j]) run(k++);   // a message's runs before its event
-                        event(ei[j]);
-                    }
-                }
-                while (k < len && !fb) run(k++);
+                uint32_t pres = 0, comm = 0, fix[4] = {0, 0, 0, 0};
+                bool snap = false;
+                walk(std::false_type{}, pres, comm, fix, cA, cL, cP, snap);
                 if (!fb) {
+                    if (snap) {                                    // kept: the emitting pass
+                        uint32_t p2 = 0, c2 = 0, f2[4] = {0, 0, 0, 0};
+                        unsigned long long a2 = 0, l2 = 0, pp2 = 0;
+                        bool s2 = false;
+                        walk(std::true_type{}, p2, c2, f2, a2, l2, pp2, s2);
+                    }
                     uint32_t val[4];
 #pragma unroll
                     for (uint32_t g = 0; g < 4; ++g)
@@ -1599,9 +1708,9 @@ __global__ __launch_bounds__(256) void k_plan_member(DevView v, uint32_t apply_w
             } else {
                 fb = true;
             }
-            if (fb) cA = cL = 0;
+            if (fb) cA = cL = cP = 0;
         }
-        v.plan[i] = q;
+        if (gp == GP_LIST || MEMBER) v.plan[i] = q;
     }
     const uint64_t fm = __ballot(fb);
     if (fm) {
@@ -1613,20 +1722,20 @@ __global__ __launch_bounds__(256) void k_plan_member(DevView v, uint32_t apply_w
             w[0] = oa; w[1] = o1; w[2] = e0; w[3] = e1; w[4] = i;
         }
     }
-    if (i < NB) plan_chosen(v, i, cC);
-    unsigned long long cc[3] = {cA, cL, cC};
+    if (MEMBER && i < NB) plan_chosen(v, i, cC);
+    unsigned long long cc[4] = {cA, cL, cC, cP};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 4; ++k) {
         unsigned long long x = cc[k];
         for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
         cc[k] = x;
     }
-    if (lane == 0) { red[wv][0] = cc[0]; red[wv][1] = cc[1]; red[wv][2] = cc[2]; }
+    if (lane == 0) { red[wv][0] = cc[0]; red[wv][1] = cc[1]; red[wv][2] = cc[2]; red[wv][3] = cc[3]; }
     __syncthreads();
-    if (threadIdx.x < 3) {
+    if (threadIdx.x < 4) {
         const uint32_t t = threadIdx.x;
         const unsigned long long x = red[0][t] + red[1][t] + red[2][t] + red[3][t];
-        const int slot = t == 0 ? PC_A : t == 1 ? PC_L : PC_C;
+        const int slot = t == 0 ? PC_A : t == 1 ? PC_L : t == 2 ? PC_C : PC_P;
         if (x) atomicAdd(&v.partials[8 * (blockIdx.x % apply_wgs) + slot], x);
     }
 }
@@ -2133,12 +2242,383 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
 #undef SF_SET
 }
 
-// Chosen log, one wave per bucket, for the buckets k_apply_fast did not
-// write from registers (multi) or every bucket (member: chosen_valid is 0).
-__global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base)
+// ------------------------------------------------------------ windows ----
+// Incremental runs (MPX_FLAG_INCREMENTAL, multi semantics).  The trace
+// arrays hold one window of records; what the windows before left is carried as values:
+// the acceptor / learner state (s_bal, s_val), a promise round's pre-accepted map (p_pid,
+// p_val, tagged per pair with its round's ballot), the chosen log (c_val), the scalars and
+// rounds (scal_base, prop_in) and the batches' votes (g_mask, g_done).
+
+// Snapshot records with their values (OutEnt): lane l's slot j is emitted when want[j];
+// one append per event (a wave-wide atomic on the window cursor).
+__device__ inline void emit_vals(const DevView &v, const bool (&want)[SPL_], uint32_t msg, uint32_t kind,
+                                 uint64_t iid0, const uint64_t (&bal)[SPL_], const uint64_t (&val)[SPL_],
+                                 const uint32_t (&kx)[SPL_])
+{
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t m[SPL_];
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SPL_; ++j) { m[j] = __ballot(want[j]); tot += (uint32_t)__popcll(m[j]); }
+    if (!tot) return;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(v.outv_n, (unsigned long long)tot);
+    base = __shfl(base, 0, 64);
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t off = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SPL_; ++j) {
+        const uint64_t at = base + off + (uint64_t)__popcll(m[j] & below);
+        if (want[j] && at < v.outv_cap) {
+            OutEnt r;
+            r.msg = msg; r.kind = kind | kx[j]; r.iid = iid0 + lane + 64 * j; r.ballot = bal[j]; r.handle = val[j] & W_HANDLE;
+            v.outv[at] = r;
+        }
+        off += (uint32_t)__popcll(m[j]);
+    }
+}
+
+// Window apply: one wave per work-list pair of the window (every pair with runs or events
+// in it), 4 slots per lane.  The pair's runs and events are merge-walked in message order
+// with k_apply's semantics — OnPrepare's FilterAcceptedValues (multi/paxos.cpp:902-922),
+// OnAccept (:1359-1404: a granted ACCEPT overwrites what is not committed), OnCommit
+// (:1494-1518: the first COMMIT fixes the slot, a later one must carry its Value),
+// UpdateByPreAcceptedValues (:1201-1223: the highest proposal id wins, first arrival on
+// ties), the quorum's merged map (:1047-1105) and StartPrepare's clear (:1233-1248) —
+// but the slot state is {ballot, handle | flags} itself, started from what earlier
+// windows left and written back at the end.
+__global__ __launch_bounds__(256) void k_apply_win(DevView v)
 {
     __shared__ uint16_t lidx_all[4][BS];
-    __shared__ unsigned long long red[4][2];
+    __shared__ u64x2 pre_all[4][BS];
+    __shared__ unsigned long long red[4][4];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint16_t *lidx = lidx_all[wv];
+    u64x2 *pre = pre_all[wv];
+#pragma unroll
+    for (uint32_t j = 0; j < SPL; ++j) lidx[lane + 64 * j] = 0xFFFF;
+    wave_lds_fence();
+    uint32_t cA = 0, cL = 0, cP = 0, cQ = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    for (uint64_t it = (uint64_t)blockIdx.x * 4 + wv; it < v.num_gp; it += stride) {
+        const uint64_t w = lane < 5 ? v.gp_list[GP_WORDS * it + lane] : 0;
+        uint64_t fi = rl64(w, 0), ei = rl64(w, 2);
+        const uint64_t fe = rl64(w, 1), ee = rl64(w, 3), q = rl64(w, 4);
+        const uint32_t b = (uint32_t)(q / v.N), n = (uint32_t)(q - (uint64_t)b * v.N);
+        const uint64_t li0 = (uint64_t)b << BSH, row = (uint64_t)n * v.shard_len;
+        const bool base = v.gp_base[it] != 0;
+        // a promise round that spans windows: its pre-accepted map, if this pair's is the round's
+        const uint64_t pr = v.p_round[sv_idx(v, n, b)];
+        const bool pload = pr && v.prop_in[3 * n + 2] && pr == v.prop_in[3 * n];
+        uint64_t sbal[SPL], sval[SPL];
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) {
+            const uint64_t li = li0 + lane + 64 * j;
+            const bool in = li < v.shard_len;
+            sbal[j] = base && in ? v.s_bal[row + li] : 0;
+            sval[j] = base && in ? v.s_val[row + li] : 0;
+            pre[lane + 64 * j] = pload && in ? u64x2{v.p_pid[row + li], v.p_val[row + li]} : u64x2{0, 0};
+        }
+        while (fi < fe || ei < ee) {
+            const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
+            const uint32_t ne = (uint32_t)(ee - ei < 64 ? ee - ei : 64);
+            uint64_t fw0 = 0, fw1 = NONE32, eax = 0, fbal = 0;
+            uint32_t evm = NONE32, fflag = 0, einfo = 0;
+            if (lane < nf) {
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
+                fw0 = x.x; fw1 = x.y;
+            }
+            if (lane < ne) { evm = v.ev_msg[ei + lane]; eax = v.ev_aux[ei + lane]; }
+            if (lane < nf) { fflag = v.m_flags[(uint32_t)fw1]; fbal = v.m_ballot[(uint32_t)fw1]; }
+            if (lane < ne) einfo = (uint32_t)v.m_type[evm] | ((uint32_t)v.m_flags[evm] << 8);
+            const uint32_t fmsg = (uint32_t)fw1;
+            uint32_t a = 0, c = 0;
+            for (;;) {
+                const bool fmore = a < nf, emore = c < ne;
+                if ((!fmore && fi + nf < fe) || (!emore && ei + ne < ee) || (!fmore && !emore)) break;
+                const uint32_t fm = fmore ? rl32(fmsg, a) : NONE32;
+                const uint32_t em = emore ? rl32(evm, c) : NONE32;
+                if (fm <= em) {
+                    const uint64_t ent = rl64(fw0, a), w1 = rl64(fw1, a);
+                    const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                    const uint32_t fl = (uint32_t)(w1 >> 56), kind = fl >> 4;
+                    const uint32_t mf = rl32(fflag, a);
+                    const uint64_t ballot = rl64(fbal, a);
+                    int k[SPL];
+                    frag_slots(lidx, kind == K_PREPLY ? v.r_slot : v.e_slot, ent, cnt, st0, (fl & FR_DENSE) != 0, k);
+                    if (kind == K_ACCEPT) {
+                        if (mf & F_GRANTED) {
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j)
+                                if (k[j] >= 0 && !(sval[j] & W_COMMITTED)) {                  // :1380
+                                    sbal[j] = ballot; sval[j] = W_PRESENT | v.e_val[ent + k[j]];  // :1387
+                                    ++cA;
+                                }
+                        }
+                    } else if (kind == K_COMMIT) {
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j)
+                            if (k[j] >= 0) {
+                                const uint64_t x = v.e_val[ent + k[j]];
+                                if (sval[j] & W_COMMITTED) {                                  // :1508
+                                    if ((sval[j] & W_HANDLE) != x)
+                                        record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
+                                                         v.shard_begin + li0 + lane + 64 * j);
+                                } else {
+                                    sbal[j] = ballot; sval[j] = W_PRESENT | W_COMMITTED | x;   // :1515
+                                }
+                                ++cL;
+                            }
+                    } else if (kind == K_PREPLY && (mf & F_COUNTED)) {
+                        uint64_t pid[SPL], hv[SPL];
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) {
+                            pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
+                            hv[j] = k[j] >= 0 ? v.r_val[ent + k[j]] : 0;
+                        }
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j)
+                            if (k[j] >= 0) {
+                                const u64x2 cur = pre[lane + 64 * j];
+                                if (!cur.y || pid[j] > cur.x) pre[lane + 64 * j] = u64x2{pid[j], W_PRESENT | hv[j]};   // :1216-1221
+                            }
+                    }
+                    ++a;
+                } else {
+                    const uint32_t g = em;
+                    const uint32_t info = rl32(einfo, c);
+                    const uint32_t t8 = info & 0xFF, fl = info >> 8;
+                    bool hit[SPL];
+                    uint64_t hb[SPL], hvv[SPL];
+                    uint32_t kx[SPL];
+                    if (t8 == MPX_MSG_PREPARE) {
+                        bool have = false;
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) have |= (sval[j] & W_PRESENT) != 0;
+                        if ((fl & F_GRANTED) && __ballot(have)) {
+                            const uint64_t ax = rl64(eax, c);
+                            if (ax & EVX_ONE) {
+                                const uint32_t il = (uint32_t)(ax >> 40) & 0x1FF, ih = (uint32_t)(ax >> 49) & 0x1FF;
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j) hit[j] = lane + 64 * j >= il && lane + 64 * j < ih;
+                            } else {
+                                const uint32_t r0 = (uint32_t)ax, nr = (uint32_t)(ax >> 32) & 0xFF;
+                                const uint64_t blo = v.shard_begin + li0;
+                                uint64_t la = 0, lb = 0;
+                                if (lane < nr) { la = v.g_a[r0 + lane]; lb = v.g_b[r0 + lane]; }
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j) hit[j] = false;
+                                for (uint32_t r = 0; r < nr; ++r) {
+                                    const uint64_t ra = rl64(la, r), rb = rl64(lb, r);
+#pragma unroll
+                                    for (uint32_t j = 0; j < SPL; ++j) {
+                                        const uint64_t iid = blo + lane + 64 * j;
+                                        hit[j] |= iid >= ra && iid < rb;
+                                    }
+                                }
+                            }
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j) {
+                                hit[j] = hit[j] && li0 + lane + 64 * j < v.shard_len && (sval[j] & W_PRESENT);
+                                kx[j] = 0;
+                                cP += hit[j];
+                            }
+                            emit_vals(v, hit, g, 0, v.shard_begin + li0, sbal, sval, kx);
+                        }
+                    } else if (t8 == MPX_MSG_P_START) {
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) pre[lane + 64 * j] = u64x2{0, 0};
+                    } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) {
+                            const u64x2 cur = pre[lane + 64 * j];
+                            hit[j] = li0 + lane + 64 * j < v.shard_len && cur.y;
+                            hb[j] = cur.x; hvv[j] = cur.y;
+                            kx[j] = (sval[j] & W_COMMITTED) ? 2u : 0u;                         // not adoptable (:1091)
+                            cQ += hit[j];
+                            pre[lane + 64 * j] = u64x2{0, 0};                                  // :1105
+                        }
+                        emit_vals(v, hit, g, 1, v.shard_begin + li0, hb, hvv, kx);
+                    }
+                    ++c;
+                }
+            }
+            fi += a;
+            ei += c;
+        }
+        // what the next window starts from: the slots, and the pre-accepted map of a round
+        // still preparing after this window (tagged with its ballot)
+        const bool psave = v.prop_out[3 * n + 2] != 0;
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) {
+            const uint64_t li = li0 + lane + 64 * j;
+            if (li >= v.shard_len) continue;
+            v.s_bal[row + li] = sbal[j];
+            v.s_val[row + li] = sval[j];
+            if (psave) {
+                const u64x2 cur = pre[lane + 64 * j];
+                v.p_pid[row + li] = cur.x;
+                v.p_val[row + li] = cur.y;
+            }
+        }
+        if (lane == 0) v.p_round[sv_idx(v, n, b)] = psave ? v.prop_out[3 * n] : 0;
+    }
+    unsigned long long cc[4] = {cA, cL, cP, cQ};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        unsigned long long x = cc[i];
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        cc[i] = x;
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[wv][i] = cc[i];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const uint32_t t = threadIdx.x;
+        const int slot = t == 0 ? PC_A : t == 1 ? PC_L : t == 2 ? PC_P : PC_Q;
+        v.partials[8 * blockIdx.x + slot] += red[0][t] + red[1][t] + red[2][t] + red[3][t];
+    }
+}
+
+// Window chosen log: one wave per bucket with chosen-log runs in the window; the runs of
+// batches whose votes reached quorum in this window (k_votes) write their Values where the
+// log is empty (OnAcceptReply -> Commit, multi/paxos.cpp:1416-1421), and must agree where
+// it is not (safety).  C counts the instances first chosen here.
+__global__ __launch_bounds__(256) void k_chosen_win(DevView v, uint32_t partial_base)
+{
+    __shared__ uint16_t lidx_all[4][BS];
+    __shared__ unsigned long long red[4];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint16_t *lidx = lidx_all[wv];
+#pragma unroll
+    for (uint32_t j = 0; j < SPL; ++j) lidx[lane + 64 * j] = 0xFFFF;
+    wave_lds_fence();
+    unsigned long long cC = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    for (uint64_t it = (uint64_t)blockIdx.x * 4 + wv; it < v.num_cb; it += stride) {
+        const uint64_t b = v.cb_list[it], li0 = b << BSH;
+        const uint64_t off = lane < 2 ? v.cf_off[b + lane] : 0;
+        uint64_t fi = rl64(off, 0);
+        const uint64_t fe = rl64(off, 1);
+        uint64_t cv[SPL];
+        bool had[SPL];
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) {
+            const uint64_t li = li0 + lane + 64 * j;
+            cv[j] = li < v.shard_len ? v.c_val[li] : 0;
+            had[j] = (cv[j] & W_PRESENT) != 0;
+        }
+        while (fi < fe) {
+            const uint32_t nf = (uint32_t)(fe - fi < 64 ? fe - fi : 64);
+            uint64_t fw0 = 0, fw1 = 0;
+            uint32_t live = 0;
+            if (lane < nf) {
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.cfrags + fi + lane);
+                fw0 = x.x; fw1 = x.y;
+                live = v.b_chosen[(uint32_t)fw1] != NONE32;
+            }
+            uint64_t lm = __ballot(live);
+            while (lm) {
+                const uint32_t a = (uint32_t)__builtin_ctzll(lm);
+                lm &= lm - 1;
+                const uint64_t ent = rl64(fw0, a), w1 = rl64(fw1, a);
+                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                int k[SPL];
+                frag_slots(lidx, v.e_slot, ent, cnt, st0, ((w1 >> 56) & FR_DENSE) != 0, k);
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) {
+                    if (k[j] < 0) continue;
+                    const uint64_t x = v.e_val[ent + k[j]];
+                    if (!(cv[j] & W_PRESENT)) cv[j] = W_PRESENT | x;
+                    else if ((cv[j] & W_HANDLE) != x)
+                        record_violation(v, MPX_V_CHOSEN_VALUE, 0, 0, v.shard_begin + li0 + lane + 64 * j);
+                }
+            }
+            fi += nf;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) {
+            const uint64_t li = li0 + lane + 64 * j;
+            if (li < v.shard_len && !had[j] && (cv[j] & W_PRESENT)) { v.c_val[li] = cv[j]; ++cC; }
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) cC += __shfl_xor(cC, d, 64);
+    if (lane == 0) red[wv] = cC;
+    __syncthreads();
+    if (threadIdx.x == 0) v.partials[8 * (partial_base + blockIdx.x) + PC_C] = red[0] + red[1] + red[2] + red[3];
+}
+
+// Digests of the carried state (mpx_state_digest in incremental mode): the same
+// definitions as the batch engine's (mpx_internal.hpp state_digest / chosen_digest)
+__global__ __launch_bounds__(256) void k_state_digest_win(DevView v, unsigned long long *out)
+{
+    const uint64_t total = (uint64_t)(v.N + 1) * v.shard_len;
+    unsigned long long ds = 0, dc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t row = (uint32_t)(i / v.shard_len);
+        const uint64_t li = i - (uint64_t)row * v.shard_len;
+        const uint64_t iid = v.shard_begin + li;
+        if (row < v.N) {
+            const uint64_t x = v.s_val[i];
+            if (x & W_PRESENT) ds += state_digest(row, iid, (x & W_COMMITTED) ? 2 : 1, v.s_bal[i], x & W_HANDLE);
+        } else {
+            const uint64_t x = v.c_val[li];
+            if (x & W_PRESENT) dc += chosen_digest(iid, x & W_HANDLE);
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) { ds += __shfl_xor(ds, d, 64); dc += __shfl_xor(dc, d, 64); }
+    if ((threadIdx.x & 63) == 0) {
+        if (ds) atomicAdd(&out[0], ds);
+        if (dc) atomicAdd(&out[1], dc);
+    }
+}
+
+// The step's summary (mpx_allgather_summary's 64 words) from every workgroup's
+// partial counters: one workgroup of 256 threads
+__device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, unsigned long long (&red)[4][8])
+{
+    const uint32_t t = threadIdx.x;
+    unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 4
+    for (uint32_t w = t; w < n_partials; w += 256)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[i] += __builtin_nontemporal_load(&v.partials[8 * w + i]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        unsigned long long x = s[i];
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        s[i] = x;
+    }
+    if ((t & 63) == 0)
+        for (int i = 0; i < 8; ++i) red[t >> 6][i] = s[i];
+    __syncthreads();
+    if (t == 0) {
+        unsigned long long r[8];
+        for (int i = 0; i < 8; ++i) r[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+        unsigned long long ds = 0;
+        for (uint32_t n = 0; n < v.N; ++n) ds += scalar_digest(n, v.node_scal[2 * n], v.node_scal[2 * n + 1]);
+        unsigned long long *o = v.summary;
+        o[SW_C] = r[PC_C]; o[SW_P] = r[PC_P]; o[SW_A] = r[PC_A]; o[SW_L] = r[PC_L];
+        o[SW_MSGS] = v.num_msgs; o[SW_V] = v.viol->count;
+        o[SW_DCHOSEN] = r[PC_DCHOSEN]; o[SW_DSTATE] = r[PC_DSTATE]; o[SW_DSCAL] = ds; o[SW_Q] = r[PC_Q];
+        for (uint32_t n = 0; n < v.N && n < 24; ++n) {
+            o[SW_NODE_SCAL + 2 * n] = v.node_scal[2 * n];
+            o[SW_NODE_SCAL + 2 * n + 1] = v.node_scal[2 * n + 1];
+        }
+    }
+}
+
+// Chosen log, one wave per bucket, for the buckets k_apply_fast did not
+// write from registers (multi) or every bucket (member: chosen_valid is 0).
+// REDUCE: the last workgroup to finish (a ticket after each one's partials are
+// visible device-wide) also folds every partial into the summary (k_reduce's work)
+template <bool REDUCE>
+__global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base, uint32_t n_partials)
+{
+    __shared__ uint16_t lidx_all[4][BS];
+    __shared__ unsigned long long red[4][8];
+    __shared__ uint32_t last;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint16_t *lidx = lidx_all[wv];
 #pragma unroll
@@ -2173,59 +2653,27 @@ __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base
         unsigned long long s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         v.partials[8 * (partial_base + blockIdx.x) + (t == 0 ? PC_C : PC_DCHOSEN)] = s;
     }
+    if (!REDUCE) return;
+    __threadfence();                             // this workgroup's partials, device-wide (every XCD)
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(&v.fast_rest[1], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();                             // the other workgroups' partials
+    reduce_summary(v, n_partials, red);
+    if (threadIdx.x == 0) v.fast_rest[1] = 0;
 }
 
+// the summary pass (the default; knob 16777216: k_chosen's last block instead, A/B)
 __global__ __launch_bounds__(256) void k_reduce(DevView v, uint32_t n_partials)
 {
     __shared__ unsigned long long red[4][8];
-    const uint32_t t = threadIdx.x;
-    unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 4
-    for (uint32_t w = t; w < n_partials; w += 256)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s[i] += v.partials[8 * w + i];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        unsigned long long x = s[i];
-        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-        s[i] = x;
-    }
-    if ((t & 63) == 0)
-        for (int i = 0; i < 8; ++i) red[t >> 6][i] = s[i];
-    __syncthreads();
-    if (t == 0) {
-        unsigned long long r[8];
-        for (int i = 0; i < 8; ++i) r[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
-        unsigned long long ds = 0;
-        for (uint32_t n = 0; n < v.N; ++n) ds += scalar_digest(n, v.node_scal[2 * n], v.node_scal[2 * n + 1]);
-        unsigned long long *o = v.summary;
-        o[SW_C] = r[PC_C]; o[SW_P] = r[PC_P]; o[SW_A] = r[PC_A]; o[SW_L] = r[PC_L];
-        o[SW_MSGS] = v.num_msgs; o[SW_V] = v.viol->count;
-        o[SW_DCHOSEN] = r[PC_DCHOSEN]; o[SW_DSTATE] = r[PC_DSTATE]; o[SW_DSCAL] = ds; o[SW_Q] = r[PC_Q];
-        for (uint32_t n = 0; n < v.N && n < 24; ++n) {
-            o[SW_NODE_SCAL + 2 * n] = v.node_scal[2 * n];
-            o[SW_NODE_SCAL + 2 * n + 1] = v.node_scal[2 * n + 1];
-        }
-    }
+    reduce_summary(v, n_partials, red);
 }
 
 __global__ void k_reset(DevView v, uint32_t n_partials)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t np = (uint64_t)v.N * v.NB;
-    if (16 * i < np) {                         // st_valid: 16 bytes per thread, byte tail
-        if (16 * i + 16 <= np) *reinterpret_cast<uint4 *>(v.st_valid + 16 * i) = uint4{0, 0, 0, 0};
-        else for (uint64_t k = 16 * i; k < np; ++k) v.st_valid[k] = 0;
-    }
-    if (i < v.NB) v.chosen_valid[i] = 0;
-    if (i < 8ull * n_partials) v.partials[i] = 0;
-    if (i < 2ull * v.N) v.node_scal[i] = 0;    // nodes without messages keep promised = max_seen = 0
-    if (i < v.out_subs) v.out_cursor[OUT_STRIDE * i] = 0;
-    if (i == 0) {
-        *v.fast_rest = 0;
-        *v.gp_dyn_n = 0;
-        v.viol->code = v.viol->node = v.viol->seq = v.viol->iid = v.viol->count = 0;
-    }
+    reset_state(v, n_partials, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
 }
 
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
@@ -2296,6 +2744,10 @@ int launch_state_digest(const DevView &v, void *stream, unsigned long long *out)
     const uint64_t total = (uint64_t)(v.N + 1) * v.shard_len;
     const uint64_t blocks = total / 256 + 1 < 16384 ? total / 256 + 1 : 16384;
     if (hipMemsetAsync(out, 0, 16, (hipStream_t)stream) != hipSuccess) return -1;
+    if (v.window) {
+        hipLaunchKernelGGL(k_state_digest_win, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, v, out);
+        return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(k_state_digest, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, v, out);
     return (int)hipGetLastError();
 }
@@ -2572,8 +3024,11 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     // Phase events ride on kernel dispatches (hipExtLaunchKernelGGL start / stop events) where a
     // kernel begins or ends the phase: a separate event record costs a 5-10 us bubble between
     // dependent kernels (rocprof, C4: 16 us of a 395 us step)
-    hipExtLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s,
-                          (hipEvent_t)ev_begin, (hipEvent_t)nullptr, 0, v, n_partials);
+    // multi: the reset rides on the first header-scan kernel (knob 33554432: its own launch, A/B)
+    const bool fold_reset = v.semantics != MPX_SEM_MEMBER && v.num_chunks && !(v.knobs & 33554432);
+    if (!fold_reset)
+        hipExtLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s,
+                              (hipEvent_t)ev_begin, (hipEvent_t)nullptr, 0, v, n_partials);
     if (v.semantics == MPX_SEM_MEMBER) {
         // member role / version gates from the E_EPOCH markers (k_gate_*)
         hipLaunchKernelGGL(k_gate_epochs, dim3(v.N), dim3(256), 0, s, v);
@@ -2582,21 +3037,35 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (v.num_batches) hipLaunchKernelGGL(k_gate_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
     }
     if (v.num_chunks) {
-        hipLaunchKernelGGL(k_scan_chunk, dim3(v.num_chunks), dim3(256), 0, s, v);
+        if (fold_reset)
+            hipExtLaunchKernelGGL(k_scan_chunk<true>, dim3(v.num_chunks), dim3(256), 0, s,
+                                  (hipEvent_t)ev_begin, (hipEvent_t)nullptr, 0, v, n_partials);
+        else hipLaunchKernelGGL(k_scan_chunk<false>, dim3(v.num_chunks), dim3(256), 0, s, v, n_partials);
         if (v.scan_node_pass) hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);   // long node streams
         if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
         else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
     }
-    if (v.num_pc) {
-        hipLaunchKernelGGL(k_prop_chunk, dim3(v.num_pc), dim3(64), 0, s, v);
-        if (v.pc_multi) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s, v);
-    }
+    if (v.num_pc) hipLaunchKernelGGL(k_prop_chunk, dim3(v.num_pc), dim3(64), 0, s, v);
+    // (a window: every node's round after the window, prop_out, comes from k_prop_node)
+    if ((v.num_pc && v.pc_multi) || v.window) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s, v);
     if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
+    if (v.window) {
+        // incremental window (multi): every pair of the window on the value-state walk, the
+        // chosen log of the batches chosen in it, the summary
+        hipExtLaunchKernelGGL(k_apply_win, dim3(g.apply_wgs), dim3(256), 0, s, (hipEvent_t)ev_apply0,
+                              (hipEvent_t)ev_general, 0, v);
+        if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
+        hipLaunchKernelGGL(k_chosen_win, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
+        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
+        return (int)hipGetLastError();
+    }
     const bool member = v.semantics == MPX_SEM_MEMBER;
-    // member plan path (k_plan_member + store + k_apply over what it lists); knob 64: the
-    // walk of every pair (as the digested run), A/B
-    const bool mplan = member && !v.digest && !(v.knobs & 64);
-    const bool plan_path = (!member && !v.digest && !(v.knobs & 64) && v.N <= FAST_MAX_NODES) || mplan;
+    // plan path (the timed step): k_plan (multi: the lean pairs) / k_plan_list (the work
+    // list's pairs without promise rounds) + store, then k_apply over the pairs k_plan_list
+    // listed and the promise-round pairs; knob 64: every pair walked (as the digested run),
+    // knob 8388608: multi without k_plan_list (the work list on the host-built ranges), A/B
+    const bool plan_path = !v.digest && !(v.knobs & 64) && (member || v.N <= FAST_MAX_NODES);
+    const bool lplan = plan_path && (member || (v.num_gp_snap && !(v.knobs & 8388608)));
     if (ev_apply0 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
     // the plan words of every (row, bucket) -> state rows and the chosen log
     auto launch_store = [&](hipEvent_t stop) {
@@ -2610,21 +3079,62 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         else
             hipExtLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
     };
-    if (mplan) {
-        hipExtLaunchKernelGGL(k_plan_member, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s,
-                              (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
-        launch_store((hipEvent_t)ev_apply1);
-        // the pairs k_plan_member listed (their count is on the device), then the promise rounds
+    const uint32_t plan_blocks = cdiv((uint64_t)v.N * v.NB, 256);
+    if (plan_path) {
+        if (member) {
+            hipExtLaunchKernelGGL(k_plan_list<true>, dim3(plan_blocks), dim3(256), 0, s,
+                                  (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+            launch_store((hipEvent_t)ev_apply1);
+        } else {
+            // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
+            // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
+            // 0.391 vs 0.304 ms apply phase at C4; the compiler drains vmcnt at its loop head)
+            // (the chosen-log buckets on threads of their own after the pairs: 63.5 vs 61.5 us at C4)
+            hipExtLaunchKernelGGL(k_plan, dim3(plan_blocks), dim3(256), 0, s,
+                                  (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+            if (lplan) hipLaunchKernelGGL(k_plan_list<false>, dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
+            // every pair the trace marks lean (pair_gp 0) is one k_plan can describe (ingest.cpp /
+            // mpx_load_clean_device use its predicate, plan_shape_ok), so k_plan leaves nothing to
+            // k_apply_fast (fast_rest 0, checked when the run is collected); knob 4194304 launches
+            // it anyway (it exits at once), A/B
+            if (v.knobs & 4194304) {
+                launch_store(nullptr);
+                hipExtLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s,
+                                      (hipEvent_t)nullptr, (hipEvent_t)ev_apply1, 0, v);
+            } else {
+                launch_store((hipEvent_t)ev_apply1);
+            }
+        }
+    } else if (member) {
+        if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
+    } else {
+        // digest runs (verification) take their own instantiation, so the timed kernel
+        // carries no digest code; the lean kernel also writes the chosen log of clean buckets
+        if (v.digest) hipLaunchKernelGGL((k_apply_fast<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
+        else switch (g.variant) {
+        case 1: hipLaunchKernelGGL((k_apply_fast<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        case 2: hipLaunchKernelGGL((k_apply_fast<5, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
+        }
+        if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
+    }
+    if (lplan) {
+        // the pairs k_plan_list listed (their count is on the device), then the promise rounds
         DevView vd = v;
         vd.gp_list = v.gp_dyn;
-        hipLaunchKernelGGL((k_apply<4, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
+        if (member) hipLaunchKernelGGL((k_apply<4, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
+        else hipLaunchKernelGGL((k_apply<4, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
         if (v.num_gp > v.num_gp_snap) {
-            if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
-            else hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
+            if (member) {
+                if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
+                else hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
+            } else {
+                if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
+                else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
+            }
         }
     } else if (member) {
         // member: every pair walks the general kernel (insert semantics, epoch events)
-        if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         // the same three-way split as multi (ingest.cpp orders the list): event-free
         // pairs, pairs without promise-reply runs (PREPARE / E_EPOCH events), the rest;
         // knob 65536: one kernel over the whole list, 262144: no AM_SNAP kernel (A/B)
@@ -2639,27 +3149,6 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                    else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
                    else hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
     } else {
-        // multi: the lean kernel also writes the chosen log of clean buckets
-        // digest runs (verification) take their own instantiation, so the
-        // timed kernel carries no digest code
-        if (v.digest) hipLaunchKernelGGL((k_apply_fast<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-        else if (!(v.knobs & 64) && v.N <= FAST_MAX_NODES) {
-            // plan + stream, then the per-slot pairs (knob 64: the one-kernel form)
-            // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
-            // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
-            // 0.391 vs 0.304 ms apply phase at C4; the compiler drains vmcnt at its loop head)
-            // (the chosen-log buckets on threads of their own after the pairs: 63.5 vs 61.5 us at C4)
-            hipExtLaunchKernelGGL(k_plan, dim3(cdiv((uint64_t)v.N * v.NB, 256)), dim3(256), 0, s,
-                                  (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
-            launch_store(nullptr);
-            hipExtLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s,
-                                  (hipEvent_t)nullptr, (hipEvent_t)ev_apply1, 0, v);
-        } else switch (g.variant) {
-        case 1: hipLaunchKernelGGL((k_apply_fast<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-        case 2: hipLaunchKernelGGL((k_apply_fast<5, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-        default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-        }
-        if (ev_apply1 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         // the event- and merge-free pairs first (k_apply<..., SIMPLE>), then the rest;
         // knob 65536: one kernel over the whole list (A/B)
         // knob 262144: no AM_SNAP kernel (those pairs go to the full one)
@@ -2680,9 +3169,18 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                    else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
                    else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
     }
-    hipExtLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general, (hipEvent_t)nullptr, 0,
-                          v, g.apply_wgs);
-    hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
+    // the chosen log of the buckets no plan word covered, then the summary (k_reduce); knob
+    // 16777216: the summary in k_chosen's last workgroup instead — measured slower (C4 tail
+    // 0.075 vs 0.015 ms, C3 0.161 vs 0.071 ms: every workgroup's device-scope fence writes
+    // back its XCD's L2 before the ticket), kept for A/B
+    if (!(v.knobs & 16777216)) {
+        hipExtLaunchKernelGGL(k_chosen<false>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
+                              (hipEvent_t)nullptr, 0, v, g.apply_wgs, n_partials);
+        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
+    } else {
+        hipExtLaunchKernelGGL(k_chosen<true>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
+                              (hipEvent_t)ev_end, 0, v, g.apply_wgs, n_partials);
+    }
     return (int)hipGetLastError();
 }
 

@@ -140,6 +140,10 @@ struct OutRec {
 static_assert(sizeof(OutRec) == 12, "OutRec is 12 bytes");
 constexpr uint32_t OUT_K1 = 0x100;
 constexpr uint32_t OUT_CMT = 0x200;
+// kind 0 run record (k_plan_list): slots aux & 0xFF .. + (aux >> OUT_RUN_SHIFT) of the
+// fragment's bucket, all fixed by fragment `ref` (the host expands it)
+constexpr uint32_t OUT_RUN = 0x400;
+constexpr uint32_t OUT_RUN_SHIFT = 16;
 // host form of a snapshot record
 struct OutEnt {
     uint32_t msg;
@@ -225,7 +229,7 @@ struct DevView {
     uint64_t num_gp_snap;           // ... then up to here: no promise-reply runs (PREPARE events only)
     const uint64_t *gp_list;        // general-apply work items, GP_WORDS each: the pair's fragment CSR
                                     // range, its event CSR range, the pair q (one coalesced load per item)
-    // member plan path (k_plan_member): the pairs it cannot describe by one plan word are
+    // list plan path (k_plan_list): the pairs it cannot describe by one plan word are
     // appended here (GP_WORDS per item, as gp_list) for k_apply; gp_dyn_n counts them
     uint64_t *gp_dyn;
     unsigned long long *gp_dyn_n;
@@ -264,7 +268,8 @@ struct DevView {
                                     // half of the descriptor, streamed without the entry words
     uint64_t *plan;                 // (N + 1) * NB: the segments k_store writes over a whole (row, bucket) (plan_idx),
                                     // rows 0..N-1 state, row N chosen log; PLAN_SKIP = not by k_store
-    uint32_t *fast_rest;            // pairs k_plan leaves to k_apply_fast (0: it exits at once)
+    uint32_t *fast_rest;            // [0]: pairs k_plan leaves to k_apply_fast (0: it exits at once);
+                                    // [1]: k_chosen's last-workgroup ticket
     uint32_t *store_dummy;          // 64 KiB sink for k_store's skipped (row, bucket) stores
     // outputs
     OutRec *out;
@@ -274,6 +279,28 @@ struct DevView {
     unsigned long long *partials;   // 8 words per apply workgroup, then chosen workgroups
     DevViolation *viol;
     unsigned long long *summary;    // 64 words
+    // incremental windows (MPX_FLAG_INCREMENTAL, multi): the trace arrays above
+    // hold one window, the state below carries across windows — as values, not as
+    // references to runs of earlier windows (which are gone)
+    uint32_t window;                // 1: a window run (k_apply_win, k_chosen_win, carried scan / rounds / votes)
+    uint64_t *s_bal, *s_val;        // per (node, instance), node-major: the entry's ballot; handle | W_PRESENT |
+                                    //   W_COMMITTED (0: none)
+    uint64_t *p_pid, *p_val;        // per (node, instance): the promise round's pre-accepted entry (proposal id;
+                                    //   handle | W_PRESENT), valid while p_round of its pair is the node's round
+    uint64_t *p_round;              // per pair (sv_idx): ballot of the round p_* belong to (0: none)
+    uint64_t *c_val;                // per instance: the chosen log (handle | W_PRESENT)
+    uint64_t *scal_base;            // 2 per node: promised / max_seen before the window
+    const uint64_t *prop_in;        // 3 per node: the round before the window (ballot, promise mask, preparing)
+    uint64_t *prop_out;             // ... after it (k_prop_node)
+    const uint32_t *b_gid;          // per batch of the window's list: its global id
+    uint64_t *g_mask;               // per global batch: accepted_ (acceptor mask)
+    uint8_t *g_done;                // per global batch: its votes reached quorum in an earlier window
+    const uint8_t *gp_base;         // per work item: earlier windows left state in the pair
+    const uint32_t *cb_list;        // buckets with chosen-log runs in the window
+    uint32_t num_cb;
+    OutEnt *outv;                   // window snapshot records, values inline
+    unsigned long long *outv_n;
+    uint64_t outv_cap;
 };
 
 // k_plan / k_apply_fast take a pair only when its bucket's CSR offsets (N+1,
@@ -289,10 +316,11 @@ constexpr uint32_t FAST_MAX_FRAGS = 63;
 // events; ingest.cpp / mpx_load_clean_device put every other pair on the work
 // list of the general k_apply (pair_gp = 1).  All static: no run-time flag enters.
 constexpr uint32_t PLAN_FRAGS = 8;
-// member semantics: every pair with runs is on the work list (pair_gp = GP_LIST), the
-// ones with promise-reply runs (promise rounds: k_apply AM_FULL only) are GP_ROUNDS
+// pair_gp of the work list's pairs: GP_LIST = no promise-reply runs (k_plan_list plans
+// them or lists them for k_apply), GP_ROUNDS = promise rounds (k_apply AM_FULL only);
+// member: every pair with runs is on the work list
 enum : uint8_t { GP_LIST = 1, GP_ROUNDS = 2 };
-// k_plan_member: runs per pair it plans (walked from LDS) and runs a wave stages
+// k_plan_list: runs per pair it plans (walked from LDS) and runs a wave stages
 constexpr uint32_t MPLAN_FRAGS = 16;
 constexpr uint32_t MPLAN_LDS = 1024;
 // the distinct run boundaries inside (0, 256), sorted into s[0..2] (BS = unused);

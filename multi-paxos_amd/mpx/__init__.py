@@ -18,6 +18,7 @@ INCLUDE_H = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "mpx
 
 ABI_VERSION = 1
 SEM_MULTI, SEM_MEMBER = 0, 1
+FLAG_INCREMENTAL = 1            # mpx_config.flags: each mpx_run applies one window (include/mpx.h)
 GEN_CLEAN, GEN_FAULTY, GEN_MEMBER = 0, 1, 2
 PRESENT = 1 << 63
 UID_BYTES = 128
@@ -49,10 +50,18 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "chosen", "promise_entries", "accept_apps", "commit_apps", "messages", "violations",
         "chosen_digest", "state_digest", "scalar_digest", "device_ns", "apply_ns", "ingest_ns",
-        "bytes_alg", "skipped", "general_pairs", "r2")]
+        "bytes_alg", "skipped", "general_pairs", "num_runs", "slot_bytes", "r2")]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if not f.startswith("r")}
+
+
+class SoaRecords(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint64), ("type", ctypes.POINTER(ctypes.c_uint8)),
+                ("src", ctypes.POINTER(ctypes.c_uint32)), ("ballot", ctypes.POINTER(ctypes.c_uint64)),
+                ("aux", ctypes.POINTER(ctypes.c_uint64)), ("ent_off", ctypes.POINTER(ctypes.c_uint64)),
+                ("ent_a", ctypes.POINTER(ctypes.c_uint64)), ("ent_b", ctypes.POINTER(ctypes.c_uint64)),
+                ("ent_pid", ctypes.POINTER(ctypes.c_uint64))]
 
 
 class Violation(ctypes.Structure):
@@ -92,6 +101,7 @@ def lib():
             "mpx_destroy": [vp],
             "mpx_submit": [vp, ctypes.c_uint32, ctypes.c_char_p, u64p, ctypes.c_uint64],
             "mpx_submit_trace": [vp, ctypes.c_char_p, ctypes.c_uint64],
+            "mpx_submit_soa": [vp, ctypes.c_uint32, P(SoaRecords)],
             "mpx_run": [vp], "mpx_reset_state": [vp], "mpx_step": [vp], "mpx_sync": [vp],
             "mpx_timings": [vp, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_uint32)],
             "mpx_timings_detail": [vp, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_uint32)],
@@ -118,6 +128,10 @@ def lib():
             "mpx_comm_allreduce_max": [vp, u64p, ctypes.c_uint64],
             "mpx_comm_allgather_bytes": [vp, ctypes.c_char_p, ctypes.c_uint64, P(u8p), u64p],
             "mpx_read_decisions_sharded": [vp, P(u8p), u64p],
+            "mpx_commit_points": [vp, P(u8p), u64p],
+            "mpx_commit_points_combine": [P(u8p), u64p, ctypes.c_uint32, P(u8p), u64p],
+            "mpx_read_commits_at": [vp, ctypes.c_char_p, ctypes.c_uint64, P(u8p), u64p],
+            "mpx_read_commits_sharded": [vp, P(u8p), u64p],
         }
         for name, args in sig.items():
             f = getattr(L, name)
@@ -179,13 +193,13 @@ def trace_header(trace):
 class Engine:
     """One engine = one GPU, one instance shard [shard_begin, shard_end)."""
 
-    def __init__(self, num_nodes, shard_begin=0, shard_end=None, device=0, semantics=SEM_MULTI, epochs=()):
+    def __init__(self, num_nodes, shard_begin=0, shard_end=None, device=0, semantics=SEM_MULTI, epochs=(), flags=0):
         L = lib()
         if shard_end is None:
             raise ValueError("shard_end required")
         self._epochs = (Epoch * max(len(epochs), 1))(*[Epoch(v, 0, a, p) for v, a, p in epochs])
         cfg = Config(ABI_VERSION, num_nodes, semantics, device, shard_begin, shard_end,
-                     len(epochs), 0, self._epochs if epochs else None)
+                     len(epochs), flags, self._epochs if epochs else None)
         h = ctypes.c_void_p()
         _ck("mpx_create", L.mpx_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -224,6 +238,23 @@ class Engine:
             offs.append(offs[-1] + len(m))
         arr = (ctypes.c_uint64 * len(offs))(*offs)
         _ck("mpx_submit", lib().mpx_submit(self.h, node, blob, arr, len(messages)))
+
+    def submit_soa(self, node, records):
+        """mpx_submit_soa: records as (type, src, ballot, aux, entries), entries (a, b[, pid])
+        — {iid, handle} / {iid, handle, pid} / PREPARE ranges {start, end}."""
+        n = len(records)
+        offs, ea, eb, ep = [0], [], [], []
+        for r in records:
+            for x in r[4]:
+                ea.append(x[0]); eb.append(x[1]); ep.append(x[2] if len(x) > 2 else 0)
+            offs.append(len(ea))
+        arr = lambda t, v: (t * max(len(v), 1))(*v)
+        keep = [arr(ctypes.c_uint8, [r[0] for r in records]), arr(ctypes.c_uint32, [r[1] for r in records]),
+                arr(ctypes.c_uint64, [r[2] for r in records]), arr(ctypes.c_uint64, [r[3] for r in records]),
+                arr(ctypes.c_uint64, offs), arr(ctypes.c_uint64, ea), arr(ctypes.c_uint64, eb),
+                arr(ctypes.c_uint64, ep)]
+        rec = SoaRecords(n, *[ctypes.cast(k, ctypes.POINTER(k._type_)) for k in keep])   # keep: alive for the call
+        _ck("mpx_submit_soa", lib().mpx_submit_soa(self.h, node, ctypes.byref(rec)))
 
     def submit_trace(self, trace):
         _ck("mpx_submit_trace", lib().mpx_submit_trace(self.h, trace, len(trace)))
@@ -316,6 +347,30 @@ class Engine:
         out = ctypes.POINTER(ctypes.c_uint8)()
         size = ctypes.c_uint64()
         _ck("mpx_read_commits", lib().mpx_read_commits(self.h, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
+    def commit_points(self):
+        """MPXQ bytes: this engine's commit creation points (mpx_commit_points)."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_commit_points", lib().mpx_commit_points(self.h, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
+    def commits_at(self, points):
+        """MPXC bytes from the union of every shard's creation points (mpx_read_commits_at;
+        the engine whose shard starts at instance 0)."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_read_commits_at", lib().mpx_read_commits_at(self.h, bytes(points), len(points), ctypes.byref(out),
+                                                             ctypes.byref(size)))
+        return _take(out, size.value)
+
+    def commits_sharded(self):
+        """The whole run's MPXC from this rank's shard over the engine's communicator
+        (mpx_read_commits_sharded: points all-gather, union, OnCommitReply on the shard at 0)."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_read_commits_sharded", lib().mpx_read_commits_sharded(self.h, ctypes.byref(out), ctypes.byref(size)))
         return _take(out, size.value)
 
     def drain_sends(self):
@@ -432,3 +487,19 @@ def decisions_combine(parts):
     size = ctypes.c_uint64()
     _ck("mpx_decisions_combine", lib().mpx_decisions_combine(arr, sizes, n, ctypes.byref(out), ctypes.byref(size)))
     return _take(out, size.value)
+
+
+def _combine(fn, parts):
+    n = len(parts)
+    raw = [ctypes.create_string_buffer(bytes(p), max(len(p), 1)) for p in parts]   # kept alive for the call
+    arr = (ctypes.POINTER(ctypes.c_uint8) * n)(*[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in raw])
+    sizes = (ctypes.c_uint64 * n)(*[len(p) for p in parts])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    size = ctypes.c_uint64()
+    _ck(fn, getattr(lib(), fn)(arr, sizes, n, ctypes.byref(out), ctypes.byref(size)))
+    return _take(out, size.value)
+
+
+def commit_points_combine(parts):
+    """Union of MPXQ commit creation points of every shard (mpx_commit_points_combine)."""
+    return _combine("mpx_commit_points_combine", parts)

@@ -88,3 +88,37 @@ def test_combine_rejects_entries_outside_their_shard():
     a2 = _parts(want, [mid + 1])[0]
     with pytest.raises(mpx.MpxError):
         mpx.decisions_combine([a2, b])
+
+
+# ---- mpx_commit_points_combine (include/mpx.h: sharded commit reliability) ----
+def _mpxq(nodes):
+    import struct
+    b = b"MPXQ" + struct.pack("<II", 1, len(nodes))
+    for pts in nodes:
+        b += struct.pack("<Q", len(pts))
+        for seq, aid in pts:
+            b += struct.pack("<QQ", seq, aid)
+    return b
+
+
+def test_commit_points_union():
+    """The union of per-shard creation points: a batch kept by two shards is one point,
+    promise-quorum points (~0) merge with accept-quorum points in stream order."""
+    P = (1 << 64) - 1
+    a = _mpxq([[(3, 1), (9, P)], [], [(5, 2)]])
+    b = _mpxq([[(3, 1), (7, 4)], [(2, P)], []])
+    assert mpx.commit_points_combine([a, b]) == _mpxq([[(3, 1), (7, 4), (9, P)], [(2, P)], [(5, 2)]])
+    assert mpx.commit_points_combine([a]) == a
+
+
+def test_commit_points_reject_bad_parts():
+    P = (1 << 64) - 1
+    a = _mpxq([[(3, 1)], []])
+    with pytest.raises(mpx.MpxError):
+        mpx.commit_points_combine([a, _mpxq([[(3, 1)]])])          # node counts differ
+    with pytest.raises(mpx.MpxError):
+        mpx.commit_points_combine([a, _mpxq([[(3, 2)], []])])      # two creations at one record
+    with pytest.raises(mpx.MpxError):
+        mpx.commit_points_combine([a + b"\0" * 8])                 # trailing bytes
+    with pytest.raises(mpx.MpxError):
+        mpx.commit_points_combine([_mpxq([[(4, P), (3, 1)], []])])  # not ascending

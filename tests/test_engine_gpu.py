@@ -14,6 +14,7 @@ import pytest
 
 import mpx
 import mpxr
+import mpxwire
 from oracles import oracle_run
 
 pytestmark = pytest.mark.gpu
@@ -444,7 +445,8 @@ def test_store_chunks_tails_and_partial_pairs(extra):
 
 @pytest.mark.parametrize("env", [("MPX_SCAN_NODE_PASS", "1"), ("MPX_KNOBS", "2048"), ("MPX_PROP_CHUNK", "64"),
                                  ("MPX_PROP_CHUNK", "5"), ("MPX_KNOBS", "65536"), ("MPX_KNOBS", "262144"),
-                                 ("MPX_KNOBS", "131072"), ("MPX_APPLY_VARIANT", "1")])
+                                 ("MPX_KNOBS", "131072"), ("MPX_APPLY_VARIANT", "1"), ("MPX_KNOBS", "8388608"),
+                                 ("MPX_KNOBS", "4194304"), ("MPX_KNOBS", "16777216"), ("MPX_KNOBS", "33554432")])
 @pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "c5_member_3",
                                   "demo_s0", "demo5_s3", "hm_promise_merge"])
 def test_kept_alternative_paths(name, env, monkeypatch):
@@ -453,7 +455,9 @@ def test_kept_alternative_paths(name, env, monkeypatch):
     chunks, promise-quorum chunks small enough that rounds span chunks
     (k_prop_chunk's deferred prefixes, k_prop_node's carry), the general k_apply
     work list without its SIMPLE / SNAP split, PREPARE ranges loaded instead of
-    the inline interval, and the unconstrained (3-wave) k_apply builds."""
+    the inline interval, the unconstrained (3-wave) k_apply builds, multi work lists
+    without k_plan_list, k_apply_fast launched after the store, the summary folded into
+    k_chosen's last workgroup, and k_reset as its own launch."""
     if name not in INDEX:
         pytest.skip("no golden " + name)
     monkeypatch.setenv(*env)
@@ -651,6 +655,191 @@ def test_incremental_submit_matches_whole(name):
         assert got == want, (frac, mpxr.diff(got, want))
 
 
+# ---- SoA submission (mpx_submit_soa) ----
+def _soa_records(stream):
+    """Decode one node's multi wire records (multi/paxos.cpp:741-755,830-856,1282-1297,1345-1357,
+    1429-1444,1481-1492; P_START / P_BATCH) into mpx_submit_soa tuples: Values become handles."""
+    import struct
+
+    def value(b, o):
+        prop, vid, noop = struct.unpack_from("<IQ?", b, o)
+        o += 13
+        if not noop:
+            mem, ln = struct.unpack_from("<?I", b, o)
+            assert not mem
+            o += 5 + ln
+        return mpxwire.handle(prop, vid, noop), o
+
+    out = []
+    for m in stream:
+        t = struct.unpack_from("<I", m)[0]
+        ents = []
+        src = ballot = aux = 0
+        if t == 0:
+            src, ballot, rl = struct.unpack_from("<IQI", m, 4)
+            ents = [struct.unpack_from("<QQ", m, 20 + 16 * k) for k in range(rl // 16)]
+        elif t == 1:
+            src, ballot, vl = struct.unpack_from("<IQI", m, 4)
+            o = 20
+            while o < 20 + vl:
+                iid, pid = struct.unpack_from("<QQ", m, o)
+                h, o = value(m, o + 16)
+                ents.append((iid, h, pid))
+        elif t == 2:
+            ballot = struct.unpack_from("<Q", m, 4)[0]
+        elif t in (3, 5):
+            src, aux, ballot, vl = struct.unpack_from("<IQQI", m, 4)
+            o = 28
+            while o < 28 + vl:
+                iid = struct.unpack_from("<Q", m, o)[0]
+                h, o = value(m, o + 8)
+                ents.append((iid, h))
+        elif t == 4:
+            src, ballot, aux = struct.unpack_from("<IQQ", m, 4)
+        elif t == 6:
+            src, aux = struct.unpack_from("<IQ", m, 4)
+        elif t == 16:
+            ballot = struct.unpack_from("<Q", m, 4)[0]
+        elif t == 17:
+            aux, vl = struct.unpack_from("<QI", m, 4)
+            o = 16
+            while o < 16 + vl:
+                iid = struct.unpack_from("<Q", m, o)[0]
+                h, o = value(m, o + 8)
+                ents.append((iid, h))
+        out.append((t, src, ballot, aux, ents))
+    return out
+
+
+@pytest.mark.parametrize("name", ["fuzz_big_0", "hm_commit_tags", "hm_promise_merge", "c3_faulty_0"])
+def test_submit_soa_matches_wire(name):
+    """The same records through the SoA fast path (no wire codec, payload-free Values) and
+    through mpx_submit: identical state, scalars, counters and digests (both name Values
+    by handle), and the same replies apart from the Value bytes in PREPARE_REPLYs."""
+    trace = _read(name, ".mpxt")
+    hd, _ep, streams = _node_streams(trace)
+    n, m = hd["num_nodes"], max(hd["num_instances"], 1)
+    if hd["semantics"] != mpx.SEM_MULTI:
+        pytest.skip("member trace")
+    want = _whole(trace)
+    with mpx.Engine(n, 0, m) as e:
+        for node, s in enumerate(streams):
+            e.submit_soa(node, _soa_records(s))
+        st = e.run()
+        assert {k: st[k] for k in COUNTERS} == want[1]
+        assert _observe(e, n, m) == want[2]
+        got = [[] for _ in range(n)]
+        for src, dst, b in e.drain_sends():
+            got[src].append((dst, b))
+    for a, b in zip(got, want[0]):
+        assert len(a) == len(b)
+        assert [x for x in a if x[1][:4] != b"\x01\x00\x00\x00"] == [x for x in b if x[1][:4] != b"\x01\x00\x00\x00"]
+
+
+# ---- incremental windows (MPX_FLAG_INCREMENTAL; multi/paxos.cpp:1714-1717, VERDICT r02 item 4) ----
+def _observe(e, n_nodes, m):
+    """Everything a caller can read back after a run: per-node state / scalars / executed
+    stream, the chosen log, the device digests."""
+    return {"state": [e.read_node_state(n, 0, m) for n in range(n_nodes)],
+            "scalars": [e.read_node_scalars(n) for n in range(n_nodes)],
+            "executed": [e.read_executed(n) for n in range(n_nodes)],
+            "chosen": e.read_chosen(0, m), "digests": e.state_digest()}
+
+
+def _whole(trace):
+    hd = mpx.trace_header(trace)
+    n, m = hd["num_nodes"], max(hd["num_instances"], 1)
+    with mpx.Engine.for_trace(trace) as e:
+        st = e.run()
+        sends = [[] for _ in range(n)]
+        for src, dst, b in e.drain_sends():
+            sends[src].append((dst, b))
+        return sends, {k: st[k] for k in COUNTERS}, _observe(e, n, m)
+
+
+def _windows(trace, fracs, times=None):
+    """The trace's node streams cut at `fracs` of each node's records: one mpx_submit per
+    node and window, one incremental mpx_run per window."""
+    import time
+    hd, _epochs, streams = _node_streams(trace)
+    n, m = hd["num_nodes"], max(hd["num_instances"], 1)
+    sends = [[] for _ in range(n)]
+    tot = {k: 0 for k in COUNTERS}
+    with mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL) as e:
+        prev = [0] * n
+        for f in list(fracs) + [1.0]:
+            cut = [len(s) if f >= 1.0 else int(len(s) * f) for s in streams]
+            t0 = time.perf_counter()
+            for node, s in enumerate(streams):
+                if cut[node] > prev[node]:
+                    e.submit(node, s[prev[node]:cut[node]])
+            st = e.run()
+            if times is not None:
+                times.append(time.perf_counter() - t0)
+            prev = cut
+            for k in COUNTERS:
+                tot[k] += st[k]
+            for src, dst, b in e.drain_sends():
+                sends[src].append((dst, b))
+        with pytest.raises(mpx.MpxError):          # windows are applied once: no replay, no history readback
+            e.step()
+        with pytest.raises(mpx.MpxError):
+            e.dump()
+        return sends, tot, _observe(e, n, m)
+
+
+MULTI_GOLDENS = sorted(k for k in INDEX if not k.startswith(("c5_", "mm_")) and "member" not in k)
+
+
+@pytest.mark.parametrize("name", MULTI_GOLDENS)
+def test_incremental_windows_match_whole(name):
+    """Every multi golden cut into 1, 2 and 4 windows: the replies of the windows, node by
+    node, are the whole run's (the reference's: test_engine_goldens), and so are the
+    counters summed over the windows and the final state, scalars, executed streams, chosen
+    log and digests."""
+    trace = _read(name, ".mpxt")
+    if mpx.trace_header(trace)["semantics"] != mpx.SEM_MULTI:
+        pytest.skip("member trace")
+    want = _whole(trace)
+    for fracs in ((), (0.5,), (0.2, 0.45, 0.8)):
+        got = _windows(trace, fracs)
+        assert got[0] == want[0], ("sends", fracs)
+        assert got[1] == want[1], ("counters", fracs)
+        assert got[2] == want[2], ("state", fracs)
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_incremental_windows_c3(seed):
+    """A C3-shaped trace (3 competing proposers, drops, duplicates, reordering: promise
+    rounds and batches that span windows) in 7 windows == the whole run."""
+    t = mpx.generate_trace(mpx.GEN_FAULTY, num_nodes=7, num_instances=1 << 15, seed=seed, batch=64, proposers=3,
+                           drop_rate=500, dup_rate=1000, max_delay=500)
+    want = _whole(t)
+    got = _windows(t, [k / 7 for k in range(1, 7)])
+    assert got[0] == want[0]
+    assert got[1] == want[1]
+    assert got[2] == want[2]
+
+
+def test_incremental_window_cost_is_per_window():
+    """C3 at 2^20 instances in 16 equal windows: each window's host + device time (submit +
+    run) stays within 2x of the second window's as the history grows — O(window), not
+    O(history) — and the windows together give the whole run's digests."""
+    t = mpx.generate_trace(mpx.GEN_FAULTY, num_instances=1 << 20, copy=False, num_nodes=7, seed=0, batch=256,
+                           proposers=3, drop_rate=500, dup_rate=1000, max_delay=500)
+    hd = mpx.trace_header(t)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        want = (st["state_digest"], st["chosen_digest"])
+        want_c = {k: st[k] for k in COUNTERS}
+    times = []
+    _sends, tot, obs = _windows(bytes(t), [k / 16 for k in range(1, 16)], times)
+    assert obs["digests"] == want and tot == want_c
+    print("window times (s):", ["%.3f" % x for x in times])
+    assert max(times[2:]) <= 2.0 * times[1], times
+    assert hd["num_instances"] >= 1 << 20
+
+
 # ---- commit reliability (SURVEY §8 f4; multi/paxos.cpp:1184-1197,1416-1421,1625-1641) ----
 COMMITS = json.load(open(os.path.join(GOLD, "commits.json")))
 
@@ -684,6 +873,53 @@ def test_engine_commits_match_oracle_c3(seed, m):
     assert got == want
 
 
+def _sharded_commits(trace, shards, align=256):
+    """The sharded protocol of include/mpx.h: points per shard -> union -> OnCommitReply
+    on the shard at instance 0."""
+    from mpx import dist as mdist
+    hd = mpx.trace_header(trace)
+    m = max(hd["num_instances"], 1)
+    engines = []
+    try:
+        for r in range(shards):
+            sb, se = mdist.shard_bounds(m, shards, r, align=align)
+            e = mpx.Engine(hd["num_nodes"], sb, se)
+            engines.append(e)
+            e.submit_trace(trace)
+            e.run()
+        pts = mpx.commit_points_combine([e.commit_points() for e in engines])
+        return engines[0].commits_at(pts)
+    finally:
+        for e in engines:
+            e.close()
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+@pytest.mark.parametrize("name", ["fuzz_big_1", "fuzz_big_2", "c3_faulty_0", "demo_s1", "hm_commit_tags", "fuzz_007"])
+def test_sharded_commits_match_reference(name, shards):
+    """Commit reliability over instance shards (each shard's creation points: the batches
+    it kept, the promise quorums where the node held a committed instance of it; their
+    union; OnCommitReply on the shard holding instance 0) == the reference's own
+    committing_values_ bookkeeping (fixture)."""
+    if name not in COMMITS:
+        pytest.skip("no commits fixture " + name)
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxc")
+    assert _sharded_commits(trace, shards, align=1) == want
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_sharded_commits_match_oracle_c3(shards):
+    from oracles import oracle_commits
+    t = mpx.generate_trace(mpx.GEN_FAULTY, num_nodes=7, num_instances=1 << 13, seed=93, batch=64, proposers=3,
+                           drop_rate=500, dup_rate=1000, max_delay=500)
+    want = oracle_commits(t)
+    with mpx.Engine.for_trace(t) as e:
+        e.run()
+        assert e.commit_points() == mpx.commit_points_combine([e.commit_points()])
+        assert e.commits_at(e.commit_points()) == want
+    assert _sharded_commits(t, shards) == want
+
+
 def test_engine_commits_clean_device_trace():
     """Device-generated clean trace: every batch is chosen and every COMMIT is
     answered by all N learners, so every commit retires with the full mask."""
@@ -695,8 +931,14 @@ def test_engine_commits_clean_device_trace():
         p = mpxc.parse(e.commits())
     assert len(p[0]) == M // 256 and all(len(x) == 0 for x in p[1:])
     assert all(r[2] == 0 and r[4] != mpxc.OPEN and r[5] == (1 << N) - 1 for r in p[0])
-    with mpx.Engine(N, 0, M // 2) as e:     # a shard engine drops other shards' batches
-        e.load_clean_device(num_instances=M, batch=256)
+    with mpx.Engine(N, 0, M // 2) as e:     # a device-generated shard keeps only its own batches'
+        e.load_clean_device(num_instances=M, batch=256)   # messages: no stream positions to merge on
         e.run()
         with pytest.raises(mpx.MpxError):
             e.commits()
+        with pytest.raises(mpx.MpxError):
+            e.commit_points()
+    with mpx.Engine(N, 0, M) as e:
+        e.load_clean_device(num_instances=M, batch=256)
+        e.run()
+        assert e.commits_at(e.commit_points()) == e.commits()

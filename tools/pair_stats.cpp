@@ -2,6 +2,7 @@
 // (host only: the generators + ingest.cpp, no GPU).  Used to size the member
 // plan path (how many pairs one plan word can describe, events per pair).
 //   tools/pair_stats <member|faulty> <log2 instances>
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -104,6 +105,33 @@ int main(int argc, char **argv)
     std::printf("events %llu (prepare %llu, epoch %llu, other %llu), runs %zu, messages %zu, markers %zu\n",
                 (unsigned long long)ev_tot, (unsigned long long)ev_prep, (unsigned long long)ev_epoch,
                 (unsigned long long)ev_other, h.frags.size(), h.m_type.size(), h.ee_msg.size());
+    // the AM_SNAP range of the general work list: PREPARE events after the pair's first run
+    // (a snapshot can only be non-empty then), runs per pair
+    {
+        uint64_t snap_pairs = 0, snap_late = 0, snap_late_ev = 0, snap_runs = 0, snap_ev = 0, snap_lean = 0;
+        for (uint64_t it = h.num_gp_simple; it < h.num_gp_snap; ++it) {
+            const uint64_t q = h.gp_list[it];                // host form: the pair itself
+            const uint64_t f0 = h.f_off[q], f1 = h.f_off[q + 1], e0 = h.ev_off[q], e1 = h.ev_off[q + 1];
+            ++snap_pairs; snap_runs += f1 - f0; snap_ev += e1 - e0;
+            bool lean = f1 - f0 <= 16;
+            uint32_t s[3] = {BS, BS, BS};
+            for (uint64_t f = f0; f < f1; ++f) {
+                const Frag &fr = h.frags[f];
+                const uint32_t kind = fr.flags >> 4;
+                if (!(fr.flags & FR_DENSE) || (kind != K_ACCEPT && kind != K_COMMIT)) lean = false;
+                if (!plan_add_split(fr.start, s) || !plan_add_split(fr.start + fr.count, s)) lean = false;
+            }
+            snap_lean += lean;
+            const uint32_t first = f1 > f0 ? h.frags[f0].msg : NONE32;
+            uint64_t late = 0;
+            for (uint64_t e = e0; e < e1; ++e) late += h.ev_msg[e] > first;
+            snap_late += late > 0; snap_late_ev += late;
+        }
+        std::printf("AM_SNAP pairs %llu: runs %llu events %llu, lean-shaped %llu, with a PREPARE after the first run %llu "
+                    "(%llu such events)\n", (unsigned long long)snap_pairs, (unsigned long long)snap_runs,
+                    (unsigned long long)snap_ev, (unsigned long long)snap_lean, (unsigned long long)snap_late,
+                    (unsigned long long)snap_late_ev);
+    }
     std::printf("runs/pair:");
     for (auto &x : runs_h) std::printf(" %llu:%llu", (unsigned long long)x.first, (unsigned long long)x.second);
     std::printf("\ninterior boundaries/pair:");
