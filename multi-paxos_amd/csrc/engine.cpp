@@ -1197,6 +1197,52 @@ extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
 // shard: the promise headers are replicated): the adopted entries in the shard and
 // the shard's noop-fill instances.  gx == nullptr: the fill ends at the shard's own
 // bound (a whole engine); else at gx[k] (absolute), the maximum of every shard's bound.
+// Per promise-quorum event (node en[k], message eg[k]): 1 + the highest shard-local
+// instance the node had committed before the event (0: none).  The first COMMIT over an
+// instance fixes it (multi/paxos.cpp:1501-1515), so "committed before g" is "some COMMIT of
+// the node before g covers it": a node's COMMIT messages in order with a running max of
+// their last in-shard entry (entries are iid-sorted) answer every event with one binary
+// search — O(commits + events log commits) instead of k_decide pass 0's scan of every slot
+// per event, O(events x instances).  A device-generated trace keeps its entry pool on the
+// device only: there (and with MPX_DECIDE_DEVICE=1, for A/B) pass 0 runs.
+static int committed_before(mpx_engine *e, const std::vector<uint32_t> &en, const std::vector<uint32_t> &eg,
+                            std::vector<uint64_t> &xmax)
+{
+    const size_t E = en.size();
+    xmax.assign(E, 0);
+    if (!E) return MPX_OK;
+    const char *dv = std::getenv("MPX_DECIDE_DEVICE");
+    if (e->device_trace || (dv && std::atoi(dv))) {
+        hipStream_t s = e->stream;
+        DevBuf d_node, d_msg, d_xmax;
+        TRY(upload(d_node, en, s)); TRY(upload(d_msg, eg, s));
+        TRY(d_xmax.alloc(8 * E)); HTRY(hipMemsetAsync(d_xmax.p, 0, 8 * E, s));
+        DecideArgs a{};
+        a.E = (uint32_t)E; a.ev_node = d_node.as<uint32_t>(); a.ev_msg = d_msg.as<uint32_t>();
+        a.xmax = d_xmax.as<unsigned long long>();
+        if (launch_decide(e->view, s, 0, a) != 0) return MPX_E_HIP;
+        HTRY(hipStreamSynchronize(s));
+        return d2h(xmax, d_xmax, E);
+    }
+    const HostTrace &h = e->ht;
+    const uint64_t sb = e->cfg.shard_begin;
+    std::vector<std::vector<std::pair<uint32_t, uint64_t>>> pm(e->cfg.num_nodes);   // (commit message, running max)
+    for (uint32_t n = 0; n < e->cfg.num_nodes; ++n) {
+        uint64_t run = 0;
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g)
+            if (h.m_type[g] == MPX_MSG_COMMIT && h.m_cnt[g]) {
+                run = std::max<uint64_t>(run, h.e_iid[h.m_ent[g] + h.m_cnt[g] - 1] - sb + 1);
+                pm[n].push_back({(uint32_t)g, run});
+            }
+    }
+    for (size_t k = 0; k < E; ++k) {
+        const auto &l = pm[en[k]];
+        auto it = std::lower_bound(l.begin(), l.end(), std::make_pair(eg[k], (uint64_t)0));   // first commit at or after g
+        if (it != l.begin()) xmax[k] = std::prev(it)->second;
+    }
+    return MPX_OK;
+}
+
 struct DecideEv { uint32_t node, msg; uint64_t bound; std::vector<const OutEnt *> adopted; std::vector<uint64_t> noops; };
 static int decide_core(mpx_engine *e, const Results &r, const uint64_t *gx, uint64_t ngx, bool bounds_only,
                        std::vector<DecideEv> &evs)
@@ -1224,16 +1270,12 @@ static int decide_core(mpx_engine *e, const Results &r, const uint64_t *gx, uint
     }
     if (!E) return MPX_OK;
     hipStream_t s = e->stream;
-    DevBuf d_node, d_msg, d_xmax, d_xend, d_adoff, d_adli, d_boff, d_bcnt, d_base, d_tot, d_noop;
+    DevBuf d_node, d_msg, d_xend, d_adoff, d_adli, d_boff, d_bcnt, d_base, d_tot, d_noop;
     TRY(upload(d_node, en, s)); TRY(upload(d_msg, eg, s));
-    TRY(d_xmax.alloc(8ull * E)); HTRY(hipMemsetAsync(d_xmax.p, 0, 8ull * E, s));
     DecideArgs a{};
     a.E = E; a.ev_node = d_node.as<uint32_t>(); a.ev_msg = d_msg.as<uint32_t>();
-    a.xmax = d_xmax.as<unsigned long long>();
-    if (launch_decide(e->view, s, 0, a) != 0) return MPX_E_HIP;
     std::vector<uint64_t> xmax;
-    HTRY(hipStreamSynchronize(s));
-    TRY(d2h(xmax, d_xmax, E));
+    TRY(committed_before(e, en, eg, xmax));
     std::vector<uint64_t> boff(E + 1, 0);
     uint64_t maxb = 0;
     for (uint32_t k = 0; k < E; ++k) {
@@ -1454,24 +1496,13 @@ static int commit_points(mpx_engine *e, const Results &r, CommitPoints &cm)
 {
     const HostTrace &h = e->ht;
     const uint32_t N = e->cfg.num_nodes;
-    hipStream_t s = e->stream;
     // promise quorums: did the node hold a committed value there (xmax > 0)
     std::vector<uint32_t> qn, qg;
     for (uint32_t n = 0; n < N; ++n)
         for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g)
             if (h.m_type[g] == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM)) { qn.push_back(n); qg.push_back((uint32_t)g); }
     std::vector<uint64_t> xmax;
-    if (!qn.empty()) {
-        DevBuf d_node, d_msg, d_xmax;
-        TRY(upload(d_node, qn, s)); TRY(upload(d_msg, qg, s));
-        TRY(d_xmax.alloc(8 * qn.size())); HTRY(hipMemsetAsync(d_xmax.p, 0, 8 * qn.size(), s));
-        DecideArgs a{};
-        a.E = (uint32_t)qn.size(); a.ev_node = d_node.as<uint32_t>(); a.ev_msg = d_msg.as<uint32_t>();
-        a.xmax = d_xmax.as<unsigned long long>();
-        if (launch_decide(e->view, s, 0, a) != 0) return MPX_E_HIP;
-        HTRY(hipStreamSynchronize(s));
-        TRY(d2h(xmax, d_xmax, qn.size()));
-    }
+    TRY(committed_before(e, qn, qg, xmax));
     cm.assign(N, {});
     for (size_t j = 0; j < h.b_msg.size(); ++j)
         if (r.b_chosen[j] != NONE32) {

@@ -2576,14 +2576,21 @@ __global__ __launch_bounds__(256) void k_state_digest_win(DevView v, unsigned lo
 
 // The step's summary (mpx_allgather_summary's 64 words) from every workgroup's
 // partial counters: one workgroup of 256 threads
-__device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, unsigned long long (&red)[4][8])
+template <uint32_t W>
+__device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, unsigned long long (&red)[W][8])
 {
+    // one workgroup of 64 W threads: each partial row is 64 bytes, read as four 16-byte loads
     const uint32_t t = threadIdx.x;
     unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 4
-    for (uint32_t w = t; w < n_partials; w += 256)
+    const ulonglong2 *p2 = reinterpret_cast<const ulonglong2 *>(v.partials);
+#pragma unroll 2
+    for (uint32_t w = t; w < n_partials; w += 64 * W) {
+        ulonglong2 x[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) s[i] += __builtin_nontemporal_load(&v.partials[8 * w + i]);
+        for (int i = 0; i < 4; ++i) x[i] = __builtin_nontemporal_load(&p2[4 * (uint64_t)w + i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { s[2 * i] += x[i].x; s[2 * i + 1] += x[i].y; }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         unsigned long long x = s[i];
@@ -2594,8 +2601,9 @@ __device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, uns
         for (int i = 0; i < 8; ++i) red[t >> 6][i] = s[i];
     __syncthreads();
     if (t == 0) {
-        unsigned long long r[8];
-        for (int i = 0; i < 8; ++i) r[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+        unsigned long long r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t k = 0; k < W; ++k)
+            for (int i = 0; i < 8; ++i) r[i] += red[k][i];
         unsigned long long ds = 0;
         for (uint32_t n = 0; n < v.N; ++n) ds += scalar_digest(n, v.node_scal[2 * n], v.node_scal[2 * n + 1]);
         unsigned long long *o = v.summary;
@@ -2665,10 +2673,11 @@ __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base
 }
 
 // the summary pass (the default; knob 16777216: k_chosen's last block instead, A/B)
-__global__ __launch_bounds__(256) void k_reduce(DevView v, uint32_t n_partials)
+// (1024 threads and 16-byte loads over the partial rows: its single workgroup is latency-bound)
+__global__ __launch_bounds__(1024) void k_reduce(DevView v, uint32_t n_partials)
 {
-    __shared__ unsigned long long red[4][8];
-    reduce_summary(v, n_partials, red);
+    __shared__ unsigned long long red[16][8];
+    reduce_summary<16>(v, n_partials, red);
 }
 
 __global__ void k_reset(DevView v, uint32_t n_partials)
@@ -3056,7 +3065,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                               (hipEvent_t)ev_general, 0, v);
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         hipLaunchKernelGGL(k_chosen_win, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
-        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
+        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
         return (int)hipGetLastError();
     }
     const bool member = v.semantics == MPX_SEM_MEMBER;
@@ -3176,7 +3185,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     if (!(v.knobs & 16777216)) {
         hipExtLaunchKernelGGL(k_chosen<false>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)nullptr, 0, v, g.apply_wgs, n_partials);
-        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
+        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
     } else {
         hipExtLaunchKernelGGL(k_chosen<true>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)ev_end, 0, v, g.apply_wgs, n_partials);

@@ -594,6 +594,18 @@ def test_sharded_decisions_match_reference(name, shards):
     assert _sharded_decisions(trace, shards, align=1) == want     # unaligned, non-empty shards of small runs
 
 
+@pytest.mark.parametrize("name", ["fuzz_big_1", "c3_faulty_0", "demo_s1", "hm_promise_merge"])
+def test_committed_before_host_prefix_matches_device_pass(name, monkeypatch):
+    """'Highest instance committed before the quorum' from the node's COMMIT messages in
+    order (host prefix max, the default) == k_decide pass 0's scan of every slot."""
+    trace = _read(name, ".mpxt")
+    with mpx.Engine.for_trace(trace) as e:
+        e.run()
+        d_host, c_host, b_host = e.decisions(), e.commits(), e.decision_bounds()
+        monkeypatch.setenv("MPX_DECIDE_DEVICE", "1")
+        assert (e.decisions(), e.commits(), e.decision_bounds()) == (d_host, c_host, b_host)
+
+
 @pytest.mark.parametrize("shards", [2, 4])
 def test_sharded_decisions_match_oracle_c3(shards):
     from oracles import oracle_decisions
