@@ -81,6 +81,9 @@ def parse():
                     help="also time rank 0's shard of the same trace at world G on this GPU (a 1-GPU scaling "
                          "projection, no RCCL); 0 / 1 = skip")
     ap.add_argument("--shard-only", action="store_true", help="only the shard projection (profiling)")
+    ap.add_argument("--events-every", type=int, default=4,
+                    help="phase events (HIP start / stop timestamps on the kernels) on every k-th timed step of "
+                         "the C4 and shard loops: each costs the step ~1.5-2 us (mpx_timing_every)")
     return ap.parse_args()
 
 
@@ -448,6 +451,7 @@ def shard_projection(args, t1_ms):
         eng.step()
     eng.sync()
     eng.timings()
+    eng.timing_every(max(args.events_every, 1) * 2)
     steps = max(args.steps, 50)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -462,6 +466,7 @@ def shard_projection(args, t1_ms):
     assert ok, "shard projection: the step's state differs from the closed form"
     t_shard = dt / steps * 1e3
     out = {"G": G, "shard": [sb, se], "steps": steps, "T1_ms": t1_ms, "T_shard_ms": t_shard,
+           "phase_events_every": max(args.events_every, 1) * 2,
            "eff": t1_ms / (G * t_shard) if t1_ms else None,
            "phases_ms": {k: sum(p[k] for p in ph) / max(len(ph), 1) for k in mpx.Engine.PHASES},
            "verified": ok,
@@ -499,6 +504,7 @@ def main():
         eng.step()
     eng.sync()
     eng.timings()                                   # drop warmup timings
+    eng.timing_every(max(args.events_every, 1))     # phase events on a sample of the timed steps
 
     barrier(pg)
     eng.sync()
@@ -614,6 +620,7 @@ def main():
             "decisions_per_step": chosen_total,
             "run_ms_device": sum(run_ms) / max(len(run_ms), 1),
             "phases_ms": phases,
+            "phase_events_every": max(args.events_every, 1),
             "trace_materialise_s": t_gen,
         }
         print(json.dumps(out), flush=True)

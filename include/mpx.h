@@ -35,6 +35,9 @@
  *                                                        (+ AcceptRejected's batch clear, :1328-1343)
  *   MPX_MSG_P_BATCH  {u32 type=17, u64 accept_id, u32 len, {u64 iid, Value}*}
  *                                                        a new AcceptingValues, multi/paxos.cpp:1299-1326
+ *   MPX_MSG_P_PROPOSE {u32 type=19, u32 len, payload}     PaxosImpl::Propose(value), :1250-1280: the
+ *                    client value gets the node's next value id; it is proposed at once (the P_BATCH that
+ *                    follows) or, while preparing, at the next promise quorum (mpx_read_decisions)
  *                    (member: entries are {u64 iid, u64 pid, Value_m}, member/paxos.cpp:1158-1160)
  * and, for member semantics only, where the node applied a learned membership
  * change (NodeImpl::ChangeMemberships, member/paxos.cpp:1864-1964):
@@ -87,7 +90,8 @@ enum {
     MPX_MSG_COMMIT_REPLY  = 6,   /* member: LEARN_REPLY (member/paxos.cpp:612) */
     MPX_MSG_P_START       = 16,  /* engine-local proposer marker, see above   */
     MPX_MSG_P_BATCH       = 17,
-    MPX_MSG_E_EPOCH       = 18   /* member only */
+    MPX_MSG_E_EPOCH       = 18,  /* member only */
+    MPX_MSG_P_PROPOSE     = 19   /* multi: a client value reaches Propose, see above */
 };
 
 enum { MPX_SEM_MULTI = 0, MPX_SEM_MEMBER = 1 };
@@ -252,6 +256,10 @@ int  mpx_timings(mpx_engine *eng, uint32_t max, double *apply_ms, double *run_ms
  * pairs), general apply (k_apply: every other pair), chosen log + counters.
  * apply_ms of mpx_timings = phases 2 + 3.  Consumes the timings like mpx_timings. */
 int  mpx_timings_detail(mpx_engine *eng, uint32_t max, double *phases, uint32_t *n);
+/* Record those phase events on every `every`-th run / step only (1: all, the default; 0:
+ * none).  Each event rides on a kernel dispatch and costs the step ~1.5-2 us; a digested
+ * mpx_run is always timed. */
+int  mpx_timing_every(mpx_engine *eng, uint32_t every);
 
 /* ---- outbound ------------------------------------------------------------ */
 /* Replies generated by the acceptor/learner handlers of the last run, in the

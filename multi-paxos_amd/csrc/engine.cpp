@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <thread>
@@ -111,6 +112,7 @@ struct mpx_engine {
     uint64_t g_cap = 0;                     // global batches g_mask / g_done hold
     std::vector<uint64_t> seq_base, win_seq_base;
     uint64_t windows = 0;
+    uint64_t events_every = 1, step_no = 0;   // mpx_timing_every
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? MPX_OK : MPX_E_HIP; }
@@ -393,7 +395,13 @@ static int finish_view(mpx_engine *e)
     // CU measured best on C4 (tools/ab_apply.py: 2.17 ms vs 2.31 ms at 5)
     e->geom.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npairs, (uint64_t)e->num_cus * 8));
     e->geom.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 4));
-    e->geom.store_wgs = e->num_cus * 8;     // k_store: 8 workgroups of 4 waves per CU
+    // k_store: 8 workgroups of 4 waves per CU at C4 size; a smaller shard (fewer 128-bucket
+    // chunks than 2.5 per wave) takes fewer, so each wave still has a next chunk in flight
+    // (C4 shard at world 8: 94 vs 101 us per step, profiles/r03_v7_shard_ab.json)
+    {
+        const uint64_t chunks = (uint64_t)(N + 1) * (e->NB / 128 + 1);
+        e->geom.store_wgs = (uint32_t)std::max<uint64_t>(e->num_cus, std::min<uint64_t>((uint64_t)e->num_cus * 8, chunks / 10));
+    }
 
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + std::max<uint64_t>(e->geom.chosen_wgs, e->num_cus * 16))));
     TRY(e->viol.alloc(sizeof(DevViolation)));
@@ -574,6 +582,22 @@ static int upload_trace(mpx_engine *e)
     v.sc_type = e->sc_type.as<uint8_t>(); v.sc_key = e->sc_key.as<uint64_t>(); v.sc_idx = e->sc_idx.as<uint32_t>();
     v.b_chosen = e->b_chosen.as<uint32_t>();
     v.cf_off = e->cf_off.as<uint64_t>(); v.cfrags = e->cfrags.as<Frag>();
+    {   // plan_chosen's static test over every bucket's chosen-log runs (kernels.hip launch_run)
+        bool ok = true;
+        for (uint64_t b = 0; ok && b + 1 < h.cf_off.size(); ++b) {
+            const uint64_t c0 = h.cf_off[b], c1 = h.cf_off[b + 1];
+            if (c0 == c1) continue;
+            uint32_t sp[3] = {BS, BS, BS};
+            ok = c1 - c0 <= 4 && (b + 1) * BS <= e->shard_len;
+            for (uint64_t k = c0; ok && k < c1; ++k) {
+                const Frag &f = h.cfrags[k];
+                ok = (f.flags & FR_DENSE) && plan_add_split(f.start, sp) && plan_add_split(f.start + f.count, sp);
+                for (uint64_t j = c0; ok && j < k; ++j)
+                    ok = h.cfrags[j].start + h.cfrags[j].count <= f.start || f.start + f.count <= h.cfrags[j].start;
+            }
+        }
+        v.chosen_static = ok ? 1 : 0;
+    }
     {
         uint64_t mx = 0;
         for (size_t i = 0; i + 1 < h.f_off.size(); ++i) mx = std::max<uint64_t>(mx, h.f_off[i + 1] - h.f_off[i]);
@@ -602,8 +626,15 @@ static int queue_run(mpx_engine *e, bool digest)
 {
     HTRY(hipSetDevice(e->device));
     if (e->dirty && !e->device_trace) TRY(upload_trace(e));
-    StepEvents *ev = next_events(e);
-    if (!ev) return MPX_E_HIP;
+    // phase events (per-kernel start / stop timestamps) on every k-th step only
+    // (mpx_timing_every; MPX_EVENTS_EVERY overrides): they cost a step ~1.5-2 us per timed
+    // kernel boundary (C4 shard at world 8: 89 vs 75 us per step)
+    uint64_t every = e->events_every;
+    if (const char *x = std::getenv("MPX_EVENTS_EVERY")) every = std::strtoull(x, nullptr, 10);
+    const bool timed = digest || every == 1 || (every && (e->step_no % every) == 0);
+    ++e->step_no;
+    StepEvents *ev = timed ? next_events(e) : nullptr;
+    if (timed && !ev) return MPX_E_HIP;
     // k_apply build variant / grid for A/B measurements (tools/ab_apply.py);
     // the defaults are the measured best
     LaunchGeom g = e->geom;
@@ -620,7 +651,8 @@ static int queue_run(mpx_engine *e, bool digest)
         g.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(np, (uint64_t)e->num_cus * std::atoi(x)));
         if (g.apply_wgs > e->num_cus * 16) g.apply_wgs = e->num_cus * 16;   // partials are sized for 16 per CU
     }
-    void *evp[5] = {ev->e[0], ev->e[1], ev->e[2], ev->e[3], ev->e[4]};
+    void *evp[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (ev) for (int k = 0; k < 5; ++k) evp[k] = ev->e[k];
     int rc = launch_run(e->view, e->stream, g, evp);
     if (rc) return MPX_E_HIP;
     if (e->incremental) {                              // the next window starts from this one's scalars and rounds
@@ -739,6 +771,14 @@ extern "C" int mpx_reset_state(mpx_engine *e)
     if (e->node_scal.p) HTRY(hipMemsetAsync(e->node_scal.p, 0, e->node_scal.bytes, e->stream));
     HTRY(hipStreamSynchronize(e->stream));
     e->last_summary.clear();
+    return MPX_OK;
+}
+
+extern "C" int mpx_timing_every(mpx_engine *e, uint32_t every)
+{
+    if (!e) return MPX_E_INVAL;
+    e->events_every = every;
+    e->step_no = 0;
     return MPX_OK;
 }
 
@@ -1327,6 +1367,122 @@ static void decide_entries(const DecideEv &ev, uint64_t *vid, std::string &d)
     }
 }
 
+// ---------------------------------------- the proposer's own values (f2) --
+// With client proposals (P_PROPOSE records) the phase-2 batch also carries the node's own
+// values, and value ids are shared between them and the noop fill, so the decision is the
+// proposer's sequential bookkeeping over its stream — host work (control plane, SURVEY §2
+// row 13), fed by what the device computed: the promise quorums (F_QUORUM) and each
+// quorum's merged pre-accepted map (k_apply's records).  The instance-id sets restate
+// AvailableInstanceIDs (multi/paxos.cpp:253-318).
+struct IdSet {
+    std::map<uint64_t, uint64_t> r;                        // start -> end, disjoint, [0, 2^64-1) at first
+    IdSet() { r[0] = ~0ull; }
+    bool contains(uint64_t id) const
+    {
+        auto it = r.upper_bound(id);
+        if (it == r.begin()) return false;
+        --it;
+        return it->first <= id && id < it->second;
+    }
+    void remove(uint64_t id)                               // (callers check contains first)
+    {
+        auto it = std::prev(r.upper_bound(id));
+        const uint64_t a = it->first, b = it->second;
+        r.erase(it);
+        if (a != id) r[a] = id;
+        if (id + 1 != b) r[id + 1] = b;
+    }
+    uint64_t next()
+    {
+        const uint64_t a = r.begin()->first;
+        remove(a);
+        return a;
+    }
+};
+
+// Per node in stream order (multi/paxos.cpp): Propose (:1250-1280: ++value_id_; not preparing
+// -> the next unproposed instance at once, else queued), StartPrepare (P_START), OnCommit
+// (:1494-1570: uncommitted / unproposed ids, an own initial proposal that lost its instance is
+// proposed again — at once, or queued while preparing), and at each promise quorum
+// OnPrepareReply's batch (:1056-1175): the merged values of unproposed instances, noops over
+// every unproposed range but the last (++value_id_ each), the own initial proposals still
+// unproposed, then the queued values at the next unproposed ids.  MPXD as mpx_read_decisions.
+static int proposer_decisions(mpx_engine *e, const Results &r, std::string &d)
+{
+    const HostTrace &h = e->ht;
+    const uint32_t N = e->cfg.num_nodes;
+    d.append("MPXD", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, N);
+    for (uint32_t n = 0; n < N; ++n) {
+        IdSet uncommitted, unproposed;
+        std::map<uint64_t, uint64_t> initial;              // initial_proposals_: instance -> value id
+        std::set<uint64_t> newly, committed;               // newly_proposed_values_; committed instances
+        uint64_t vid = 0;                                   // value_id_ (:335)
+        bool preparing = false;                             // prepare_retry_timeout_ != NULL
+        std::string body;
+        uint64_t count = 0;
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
+            const uint8_t t = h.m_type[g];
+            if (t == MPX_MSG_P_PROPOSE) {
+                ++vid;
+                if (!preparing) initial[unproposed.next()] = vid;
+                else newly.insert(vid);
+            } else if (t == MPX_MSG_P_START) {
+                preparing = true;
+            } else if (t == MPX_MSG_COMMIT) {
+                for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) {
+                    const uint64_t iid = h.e_iid[k], hv = h.e_val[k];
+                    if (committed.insert(iid).second && uncommitted.contains(iid)) uncommitted.remove(iid);
+                    if (unproposed.contains(iid)) unproposed.remove(iid);
+                    auto it = initial.find(iid);
+                    if (it != initial.end()) {
+                        const uint64_t v0 = it->second;
+                        initial.erase(it);
+                        if (MPX_HANDLE_PROPOSER(hv) != n || MPX_HANDLE_VALUE_ID(hv) != v0) {
+                            if (!preparing) initial[unproposed.next()] = v0;
+                            else newly.insert(v0);
+                        }
+                    }
+                }
+            } else if (t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM)) {
+                unproposed = uncommitted;
+                std::vector<std::pair<uint64_t, uint64_t>> b;
+                auto it = r.by_msg[1].find((uint32_t)g);
+                if (it != r.by_msg[1].end())
+                    for (const OutEnt *o : it->second)
+                        if (unproposed.contains(o->iid)) { unproposed.remove(o->iid); b.push_back({o->iid, o->handle}); }
+                while (unproposed.r.size() > 1) {
+                    const auto first = *unproposed.r.begin();
+                    unproposed.r.erase(unproposed.r.begin());
+                    for (uint64_t id = first.first; id != first.second; ++id) b.push_back({id, MPX_HANDLE(n, 1, ++vid)});
+                }
+                for (auto &x : initial)
+                    if (unproposed.contains(x.first)) { unproposed.remove(x.first); b.push_back({x.first, MPX_HANDLE(n, 0, x.second)}); }
+                for (uint64_t v : newly) {
+                    const uint64_t iid = unproposed.next();
+                    initial[iid] = v;
+                    b.push_back({iid, MPX_HANDLE(n, 0, v)});
+                }
+                newly.clear();
+                preparing = false;
+                std::sort(b.begin(), b.end());                 // AcceptingValues::values_ is a map
+                app<uint64_t>(body, seq_of(h, n, g));
+                app<uint64_t>(body, b.size());
+                for (auto &x : b) { app<uint64_t>(body, x.first); app<uint64_t>(body, x.second); }
+                ++count;
+            }
+        }
+        app<uint64_t>(d, count);
+        d += body;
+    }
+    return MPX_OK;
+}
+
+static bool has_proposals(const HostTrace &h)
+{
+    return std::find(h.m_type.begin(), h.m_type.end(), (uint8_t)MPX_MSG_P_PROPOSE) != h.m_type.end();
+}
+
 // ------------------------------------------------- phase-2 decisions (f2) --
 // The batch OnPrepareReply builds at each promise quorum (multi/paxos.cpp:
 // 1056-1130) for a proposer with no client proposals of its own: the device
@@ -1342,6 +1498,17 @@ extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
     if (e->cfg.semantics != MPX_SEM_MULTI || e->cfg.shard_begin != 0) return MPX_E_STATE;
     Results r;
     TRY(fetch_results(e, r));
+    const char *hs = std::getenv("MPX_DECIDE_HOST");     // (A/B: the bookkeeping without proposals too)
+    if (has_proposals(e->ht) || (hs && std::atoi(hs))) {
+        if (!e->whole) return MPX_E_STATE;               // the bookkeeping needs every instance's commits
+        std::string d;
+        TRY(proposer_decisions(e, r, d));
+        *out = (uint8_t *)std::malloc(d.size());
+        if (!*out) return MPX_E_NOMEM;
+        std::memcpy(*out, d.data(), d.size());
+        *size = d.size();
+        return MPX_OK;
+    }
     std::vector<DecideEv> evs;
     TRY(decide_core(e, r, nullptr, 0, false, evs));
     const uint32_t N = e->cfg.num_nodes;
@@ -1375,6 +1542,7 @@ extern "C" int mpx_decisions_bounds(mpx_engine *e, uint64_t *bounds, uint64_t ca
     if (e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
     Results r;
     TRY(fetch_results(e, r));
+    if (has_proposals(e->ht)) return MPX_E_STATE;        // own values: mpx_read_decisions on a whole engine
     std::vector<DecideEv> evs;
     TRY(decide_core(e, r, nullptr, 0, true, evs));
     *count = evs.size();
@@ -1390,6 +1558,7 @@ extern "C" int mpx_read_decisions_part(mpx_engine *e, const uint64_t *global_bou
     if (e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
     Results r;
     TRY(fetch_results(e, r));
+    if (has_proposals(e->ht)) return MPX_E_STATE;        // own values: mpx_read_decisions on a whole engine
     std::vector<DecideEv> evs;
     TRY(decide_core(e, r, global_bounds, count, false, evs));
     const uint32_t N = e->cfg.num_nodes;
@@ -1750,13 +1919,14 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     // per bucket: the batches meeting it (one ACCEPT and one COMMIT run per
     // node each, one chosen-log run) -> the fragment CSR offsets
     std::vector<uint64_t> cf_off(NB + 1, 0), f_off(N * NB + 1, 0);
-    uint64_t max_pair = 0;
+    uint64_t max_pair = 0, max_cb = 0;
     for (uint64_t b = 0; b < NB; ++b) {
         const uint64_t lo = sb + (b << BSH), hi = std::min(lo + BS, se);
         const uint64_t nb = (hi - 1) / B - lo / B + 1;
         cf_off[b + 1] = cf_off[b] + nb;
         for (uint32_t n = 0; n < N; ++n) f_off[b * N + n] = 2 * (N * cf_off[b] + n * nb);
         max_pair = std::max(max_pair, 2 * nb);
+        max_cb = std::max(max_cb, nb);
     }
     f_off[N * NB] = 2ull * N * cf_off[NB];
     if (G >= NONE32 || E > MAX_ENTRIES || f_off[N * NB] > MAX_FRAGS || max_pair > MAX_PAIR_FRAGS) return MPX_E_RANGE;
@@ -1874,6 +2044,9 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.b_chosen = e->b_chosen.as<uint32_t>();
     v.cf_off = e->cf_off.as<uint64_t>(); v.cfrags = e->cfrags.as<Frag>();
     v.slot_w = max_pair <= MAX_PAIR_FRAGS_1 ? 1 : 2;
+    // batches tile the instances: a bucket's chosen-log runs are disjoint and dense, so at most
+    // four of them over a whole bucket pass plan_chosen's static test (no k_chosen walk)
+    v.chosen_static = max_cb <= 4 && L % BS == 0 ? 1 : 0;
     TRY(finish_view(e));
     for (auto &ns : e->nodes) ns.clear();
     e->vt.clear();

@@ -381,6 +381,9 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         if (len < 12) return MPX_E_DECODE;
         ballot = rd64(m + 4);
         break;
+    case MPX_MSG_P_PROPOSE:                       // Propose (:1250-1280): the proposer's bookkeeping only
+        if (len < 8 || 8 + (size_t)rd32(m + 4) > len) return MPX_E_DECODE;
+        break;
     case MPX_MSG_P_BATCH: {
         if (len < 16) return MPX_E_DECODE;
         aux = rd64(m + 4);
@@ -472,6 +475,7 @@ int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord
         break;
     }
     case MPX_MSG_REJECT: case MPX_MSG_ACCEPT_REPLY: case MPX_MSG_COMMIT_REPLY: case MPX_MSG_P_START:
+    case MPX_MSG_P_PROPOSE:
         break;
     default:
         return MPX_E_DECODE;

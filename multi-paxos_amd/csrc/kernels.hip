@@ -441,14 +441,12 @@ __global__ __launch_bounds__(256) void k_scan_node(DevView v)
 // (an exclusive wave scan, only in rounds that hold a PREPARE) and, in rounds
 // with a REJECT, the inclusive max_seen scan.  Flags go to the record's
 // message (m_flags[sc_idx]); messages outside the stream keep their static flags.
+// (the body of one chunk's workgroup: k_scan_apply, or a scan block of k_headers)
 template <bool MEMBER>
-__global__ __launch_bounds__(256) void k_scan_apply(DevView v)
+__device__ inline void scan_apply_chunk(const DevView &v, const uint32_t c, uint64_t (&l)[2][4], uint64_t (&lc)[2][4],
+                                        uint64_t *lky, uint8_t *lty, uint32_t *lix)
 {
-    __shared__ uint64_t l[2][4], lc[2][4];
-    __shared__ uint64_t lky[SCAN_CHUNK];        // phase 2 reads its rounds back from LDS,
-    __shared__ uint8_t lty[SCAN_CHUNK];         // so the round loop needs few registers
-    __shared__ uint32_t lix[SCAN_CHUNK];        // and no dependent load of the message index per round
-    const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
     const uint64_t wb = beg + (uint64_t)w * (SCAN_CHUNK / 4) + lane;
     const uint32_t lb = w * (SCAN_CHUNK / 4) + lane;
@@ -562,6 +560,16 @@ __global__ __launch_bounds__(256) void k_scan_apply(DevView v)
     }
 }
 
+template <bool MEMBER>
+__global__ __launch_bounds__(256) void k_scan_apply(DevView v)
+{
+    __shared__ uint64_t l[2][4], lc[2][4];
+    __shared__ uint64_t lky[SCAN_CHUNK];        // phase 2 reads its rounds back from LDS,
+    __shared__ uint8_t lty[SCAN_CHUNK];         // so the round loop needs few registers
+    __shared__ uint32_t lix[SCAN_CHUNK];        // and no dependent load of the message index per round
+    scan_apply_chunk<MEMBER>(v, blockIdx.x, l, lc, lky, lty, lix);
+}
+
 // --------------------------------------------------------- proposer side --
 // Promise quorum per node (OnPrepareReply, multi/paxos.cpp:1036-1057; member
 // Proposer::OnPrepareReply, member/paxos.cpp:1158-1182): one wave per node over
@@ -661,9 +669,8 @@ __device__ inline void prop_range(const DevView &v, uint32_t n, uint64_t i0, uin
 // :338; not preparing), later ones from their first round head — the records
 // before it wait for k_prop_node.  Writes the chunk's first head and its state
 // after the last record (valid when it has a head or is the node's first).
-__global__ __launch_bounds__(64) void k_prop_chunk(DevView v)
+__device__ inline void prop_chunk_wave(const DevView &v, const uint32_t c)
 {
-    const uint32_t c = blockIdx.x;
     const uint32_t n = v.pc_node[c];
     const uint64_t i0 = v.pc_beg[c], i1 = v.pc_end[c];
     PropState st{0, 0, 0, i0 == v.pl_off[n] ? 1u : 0u};
@@ -671,10 +678,15 @@ __global__ __launch_bounds__(64) void k_prop_chunk(DevView v)
         st = PropState{v.prop_in[3 * n], v.prop_in[3 * n + 1], (uint32_t)v.prop_in[3 * n + 2], 1u};
     uint32_t head;
     prop_range(v, n, i0, i1, st, head);
-    if (threadIdx.x == 0) {
+    if ((threadIdx.x & 63) == 0) {
         v.pc_head[c] = head;
         v.pc_state[3 * c] = st.cb; v.pc_state[3 * c + 1] = st.cmask; v.pc_state[3 * c + 2] = st.cprep | (st.known << 1);
     }
+}
+
+__global__ __launch_bounds__(64) void k_prop_chunk(DevView v)
+{
+    prop_chunk_wave(v, blockIdx.x);
 }
 
 // pass 2: one wave per node, its chunks in order: the records before each
@@ -711,12 +723,11 @@ __global__ __launch_bounds__(64) void k_prop_node(DevView v)
 // headers (ballot, acceptor, epoch: laid out beside the list at ingest), then
 // each lane walks its own batch's replies in order from LDS.
 constexpr uint32_t VOTE_LDS = 768;             // reply headers staged per wave
-__global__ __launch_bounds__(256) void k_votes(DevView v)
+__device__ inline void votes_block(const DevView &v, const uint32_t blk, uint64_t (*lbal)[VOTE_LDS],
+                                   uint32_t (*lsrc)[VOTE_LDS])
 {
-    __shared__ uint64_t lbal[4][VOTE_LDS];
-    __shared__ uint32_t lsrc[4][VOTE_LDS];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t j0 = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    const uint64_t j0 = ((uint64_t)blk * 4 + wv) * 64;
     if (j0 >= v.num_batches) return;
     const uint64_t j = j0 + lane;
     const bool have = j < v.num_batches;
@@ -775,6 +786,39 @@ __global__ __launch_bounds__(256) void k_votes(DevView v)
     if (v.window && have && !done) {
         v.g_mask[gid] = mask;
         if (chosen_r != ~0ull) v.g_done[gid] = 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_votes(DevView v)
+{
+    __shared__ uint64_t lbal[4][VOTE_LDS];
+    __shared__ uint32_t lsrc[4][VOTE_LDS];
+    votes_block(v, blockIdx.x, lbal, lsrc);
+}
+
+// The header kernels that depend only on the scan chunks' aggregates (or on nothing) in
+// one launch — the scan's flag pass (scan_apply_chunk), the promise-quorum chunks (one per
+// wave) and the accept votes (votes_block) — by workgroup range: fewer dependent launches
+// per step (each costs a dispatch and a floor of a few us).  They touch disjoint outputs: the
+// scan's flags on PREPARE / ACCEPT records, the quorum flags on PREPARE_REPLYs, b_chosen.
+// LDS: the larger of the scan's chunk staging and the votes' reply staging, shared.
+constexpr uint32_t HDR_LDS_WORDS = (VOTE_LDS * 4 * 12 + 7) / 8;   // 4 waves x 768 x (8 + 4) bytes
+static_assert(HDR_LDS_WORDS * 8 >= SCAN_CHUNK * 13, "the scan staging fits");
+template <bool MEMBER>
+__global__ __launch_bounds__(256) void k_headers(DevView v, uint32_t nb_scan, uint32_t nb_prop)
+{
+    __shared__ uint64_t raw[HDR_LDS_WORDS];
+    __shared__ uint64_t l[2][4], lc[2][4];
+    const uint32_t b = blockIdx.x;
+    if (b < nb_scan) {
+        scan_apply_chunk<MEMBER>(v, b, l, lc, raw, reinterpret_cast<uint8_t *>(raw + SCAN_CHUNK),
+                                 reinterpret_cast<uint32_t *>(raw + SCAN_CHUNK + SCAN_CHUNK / 8));
+    } else if (b < nb_scan + nb_prop) {
+        const uint32_t c = 4 * (b - nb_scan) + (threadIdx.x >> 6);
+        if (c < v.num_pc) prop_chunk_wave(v, c);
+    } else {
+        votes_block(v, b - nb_scan - nb_prop, reinterpret_cast<uint64_t (*)[VOTE_LDS]>(raw),
+                    reinterpret_cast<uint32_t (*)[VOTE_LDS]>(raw + 4 * VOTE_LDS));
     }
 }
 
@@ -1506,9 +1550,9 @@ __device__ inline void emit_run(const DevView &v, uint32_t msg, uint32_t ref, ui
 
 // List plan path (the timed step for the general work list's pairs without promise
 // rounds): k_plan's reduction extended to pairs with snapshot events, one thread per
-// (node, bucket) pair whose pair_gp is GP_LIST.  Runs cut the bucket into at most four
-// segments (plan_add_split); within a segment every run covers all or none of it, so the
-// pair walks its runs and its events in message order with four segment states instead
+// (node, bucket) pair whose pair_gp is GP_LIST.  Runs cut the bucket into at most LSEG (4)
+// segments (seg_add_split); within a segment every run covers all or none of it, so the
+// pair walks its runs and its events in message order with one state per segment instead
 // of 256 slot states, and one plan word (k_store / k_store8 stream it) holds the result.
 //   multi (multi/paxos.cpp:1359-1404 OnAccept, :1494-1518 OnCommit): a granted ACCEPT
 //     overwrites every segment it covers that is not committed, the first COMMIT fixes it;
@@ -1523,7 +1567,7 @@ __device__ inline void emit_run(const DevView &v, uint32_t msg, uint32_t ref, ui
 // commit-covered slot, P = snapshot entries).
 //
 // The pair is listed for k_apply instead (gp_dyn, one append per wave) when: more than
-// MPLAN_FRAGS runs, a run that is not a dense accept / commit run, a fifth segment, a
+// F (16) runs, a run that is not a dense accept / commit run, a fifth segment, a
 // partial last bucket, or a commit / learn (member: also an accept) over a committed
 // segment whose Value entry differs (the reference's Value check: k_apply compares the
 // Values).  Nothing is emitted for a listed pair: the walk runs once to decide, and a second
@@ -1533,10 +1577,30 @@ __device__ inline void emit_run(const DevView &v, uint32_t msg, uint32_t ref, ui
 // words carry the accept runs' scan flag (F_GRANTED) in bit 57 after the gather, so the
 // walk reads only LDS.
 constexpr uint64_t MP_GRANTED = 1ull << 57;
-template <bool MEMBER>
+// the distinct run boundaries of a pair, sorted into s[0 .. LSEG-2] (BS = unused); false once
+// an LSEG + 1-th segment appears
+template <uint32_t LSEG>
+__device__ inline bool seg_add_split(uint32_t x, uint32_t (&s)[LSEG - 1])
+{
+    if (x == 0 || x >= BS) return true;
+    bool have = false;
+#pragma unroll
+    for (uint32_t k = 0; k < LSEG - 1; ++k) have = have || s[k] == x;
+    if (have) return true;
+    if (s[LSEG - 2] != BS) return false;                      // an LSEG + 1-th segment
+    uint32_t y = x;                                            // insertion: s stays sorted, BS last
+#pragma unroll
+    for (uint32_t k = 0; k < LSEG - 1; ++k)
+        if (y < s[k]) { const uint32_t t = s[k]; s[k] = y; y = t; }
+    return true;
+}
+// LSEG: segments a pair may have — up to 4 fit one plan word (k_store); the LSEG = 8 build
+// (knob 536870912, A/B) writes the slots of a pair with 5..8 segments itself and walks up to
+// F = 32 runs: C3 general apply 1.01 -> 0.80 ms but k_plan_list 0.19 -> 0.40 ms (3 waves per
+// SIMD, the per-thread slot writes), C5 apply 0.335 -> 0.394 ms; the default is 4 / 16.
+template <bool MEMBER, uint32_t LSEG = 4, uint32_t F = MPLAN_FRAGS>
 __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs)
 {
-    constexpr uint32_t F = MPLAN_FRAGS;
     __shared__ uint64_t w_lds[4][MPLAN_LDS];
     __shared__ unsigned long long red[4][4];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1578,12 +1642,14 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
         if (len && gp == GP_LIST) {
             bool ok = len <= F && rel + len <= MPLAN_LDS && (b + 1) * BS <= v.shard_len;
             uint64_t *const W = &w_lds[wv][ok ? rel : 0];
-            uint32_t sp[3] = {BS, BS, BS};
+            uint32_t sp[LSEG - 1];
+#pragma unroll
+            for (uint32_t k = 0; k < LSEG - 1; ++k) sp[k] = BS;
             if (ok) {
                 for (uint32_t k = 0; k < len; ++k) {
                     const uint64_t w = W[k];
                     const uint32_t cnt = (uint32_t)(w >> 32) & 0xFFFF, st0 = (uint32_t)(w >> 48) & 0xFF;
-                    ok = ok && frag_lean(w) && plan_add_split(st0, sp) && plan_add_split(st0 + cnt, sp);
+                    ok = ok && frag_lean(w) && seg_add_split<LSEG>(st0, sp) && seg_add_split<LSEG>(st0 + cnt, sp);
                 }
             }
             if (ok) {
@@ -1597,11 +1663,11 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
 #pragma unroll
                 for (uint32_t k = 0; k < F; ++k)
                     if (k < len && (fg[k] & F_GRANTED)) W[k] |= MP_GRANTED;
-                uint32_t lo[4], sl[4];
+                uint32_t lo[LSEG], sl[LSEG];
 #pragma unroll
-                for (uint32_t g = 0; g < 4; ++g) {
+                for (uint32_t g = 0; g < LSEG; ++g) {
                     lo[g] = g ? sp[g - 1] : 0;
-                    sl[g] = lo[g] >= BS ? 0 : (g < 3 ? sp[g] : BS) - lo[g];
+                    sl[g] = lo[g] >= BS ? 0 : (g < LSEG - 1 ? sp[g] : BS) - lo[g];
                 }
                 // the entry index of run k at slot s, minus s (the pool is
                 // content-addressed: equal ones name one Value; read only over a
@@ -1612,7 +1678,7 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
                 const uint64_t blo = v.shard_begin + (b << BSH);
                 // one pass over the pair in message order; EMIT: the second pass, which
                 // writes the snapshot records (the first one decided the pair is kept)
-                auto walk = [&](auto emit_tag, uint32_t &pres, uint32_t &comm, uint32_t (&fix)[4],
+                auto walk = [&](auto emit_tag, uint32_t &pres, uint32_t &comm, uint32_t (&fix)[LSEG],
                                 unsigned long long &a, unsigned long long &l, unsigned long long &p,
                                 bool &snap) {
                     constexpr bool EMIT = decltype(emit_tag)::value;
@@ -1622,7 +1688,7 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
                         const bool learn = (w >> 60) == K_COMMIT;
                         if (!learn && !(w & MP_GRANTED)) return;          // a rejected / dropped accept
 #pragma unroll
-                        for (uint32_t g = 0; g < 4; ++g) {
+                        for (uint32_t g = 0; g < LSEG; ++g) {
                             if (!sl[g] || lo[g] < st0 || lo[g] >= st0 + cnt) continue;
                             if (learn) l += sl[g];
                             if ((comm >> g) & 1) {
@@ -1640,7 +1706,7 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
                     // FilterAcceptedValues over the bucket-local interval [il, ih)
                     auto snap_iv = [&](uint32_t g8, uint32_t il, uint32_t ih) {
 #pragma unroll
-                        for (uint32_t g = 0; g < 4; ++g) {
+                        for (uint32_t g = 0; g < LSEG; ++g) {
                             if (!((pres >> g) & 1)) continue;
                             const uint32_t x0 = lo[g] > il ? lo[g] : il, x1 = lo[g] + sl[g] < ih ? lo[g] + sl[g] : ih;
                             if (x0 >= x1) continue;
@@ -1688,21 +1754,64 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
                     }
                     while (k < len && !fb) run(k++);
                 };
-                uint32_t pres = 0, comm = 0, fix[4] = {0, 0, 0, 0};
+                uint32_t pres = 0, comm = 0, fix[LSEG];
+#pragma unroll
+                for (uint32_t g = 0; g < LSEG; ++g) fix[g] = 0;
                 bool snap = false;
                 walk(std::false_type{}, pres, comm, fix, cA, cL, cP, snap);
                 if (!fb) {
                     if (snap) {                                    // kept: the emitting pass
-                        uint32_t p2 = 0, c2 = 0, f2[4] = {0, 0, 0, 0};
+                        uint32_t p2 = 0, c2 = 0, f2[LSEG];
+#pragma unroll
+                        for (uint32_t g = 0; g < LSEG; ++g) f2[g] = 0;
                         unsigned long long a2 = 0, l2 = 0, pp2 = 0;
                         bool s2 = false;
                         walk(std::true_type{}, p2, c2, f2, a2, l2, pp2, s2);
                     }
-                    uint32_t val[4];
+                    uint32_t val[LSEG];
 #pragma unroll
-                    for (uint32_t g = 0; g < 4; ++g)
+                    for (uint32_t g = 0; g < LSEG; ++g)
                         val[g] = !sl[g] ? val[g ? g - 1 : 0] : ((pres >> g) & 1) ? fix[g] + 1 : 0;
-                    q = plan_pack(val, sp);
+                    if (LSEG == 4 || sp[LSEG == 4 ? 0 : 3] == BS) {   // <= 4 segments: one plan word for k_store
+                        const uint32_t v4[4] = {val[0], val[1], val[2], val[3]}, s3[3] = {sp[0], sp[1], sp[2]};
+                        q = plan_pack(v4, s3);
+                    } else {
+                        // 5..LSEG segments: the pair's slots written here (k_store skips the bucket)
+                        const uint32_t n = (uint32_t)(i - b * N);
+                        if (v.slot_w == 1) {
+                            uint8_t *dst = static_cast<uint8_t *>(v.st) + (uint64_t)n * v.shard_len + (b << BSH);
+                            for (uint32_t j = 0; j < BS / 16; ++j) {
+                                uint32_t wd[4] = {0, 0, 0, 0};
+                                for (uint32_t t = 0; t < 16; ++t) {
+                                    const uint32_t sl_ = 16 * j + t;
+                                    uint32_t g = 0;
+#pragma unroll
+                                    for (uint32_t k = 0; k < LSEG - 1; ++k) g += sl_ >= sp[k];
+                                    uint32_t x = 0;
+#pragma unroll
+                                    for (uint32_t k = 0; k < LSEG; ++k) x = k == g ? val[k] : x;
+                                    wd[t >> 2] |= x << (8 * (t & 3));
+                                }
+                                *reinterpret_cast<u32x4 *>(dst + 16 * j) = u32x4{wd[0], wd[1], wd[2], wd[3]};
+                            }
+                        } else {
+                            uint16_t *dst = static_cast<uint16_t *>(v.st) + (uint64_t)n * v.shard_len + (b << BSH);
+                            for (uint32_t j = 0; j < BS / 8; ++j) {
+                                uint32_t wd[4] = {0, 0, 0, 0};
+                                for (uint32_t t = 0; t < 8; ++t) {
+                                    const uint32_t sl_ = 8 * j + t;
+                                    uint32_t g = 0;
+#pragma unroll
+                                    for (uint32_t k = 0; k < LSEG - 1; ++k) g += sl_ >= sp[k];
+                                    uint32_t x = 0;
+#pragma unroll
+                                    for (uint32_t k = 0; k < LSEG; ++k) x = k == g ? val[k] : x;
+                                    wd[t >> 1] |= x << (16 * (t & 1));
+                                }
+                                *reinterpret_cast<u32x4 *>(dst + 8 * j) = u32x4{wd[0], wd[1], wd[2], wd[3]};
+                            }
+                        }
+                    }
                     v.st_valid[i] = 1;
                 }
             } else {
@@ -2582,38 +2691,41 @@ __device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, uns
     // one workgroup of 64 W threads: each partial row is 64 bytes, read as four 16-byte loads
     const uint32_t t = threadIdx.x;
     unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const ulonglong2 *p2 = reinterpret_cast<const ulonglong2 *>(v.partials);
-#pragma unroll 2
+    const u64x2 *p2 = reinterpret_cast<const u64x2 *>(v.partials);
+#pragma unroll 1
     for (uint32_t w = t; w < n_partials; w += 64 * W) {
-        ulonglong2 x[4];
+        u64x2 x[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[i] = __builtin_nontemporal_load(&p2[4 * (uint64_t)w + i]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) { s[2 * i] += x[i].x; s[2 * i + 1] += x[i].y; }
     }
-#pragma unroll
+#pragma unroll 1
     for (int i = 0; i < 8; ++i) {
         unsigned long long x = s[i];
         for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-        s[i] = x;
+        if ((t & 63) == 0) red[t >> 6][i] = x;
     }
-    if ((t & 63) == 0)
-        for (int i = 0; i < 8; ++i) red[t >> 6][i] = s[i];
-    __syncthreads();
-    if (t == 0) {
-        unsigned long long r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (uint32_t k = 0; k < W; ++k)
-            for (int i = 0; i < 8; ++i) r[i] += red[k][i];
+    // the per-node scalars, one lane per node (N <= 64): their loads all in flight at once
+    // (a serial loop over the nodes in one thread waited out N memory latencies)
+    unsigned long long *o = v.summary;
+    if (t < 64) {
         unsigned long long ds = 0;
-        for (uint32_t n = 0; n < v.N; ++n) ds += scalar_digest(n, v.node_scal[2 * n], v.node_scal[2 * n + 1]);
-        unsigned long long *o = v.summary;
-        o[SW_C] = r[PC_C]; o[SW_P] = r[PC_P]; o[SW_A] = r[PC_A]; o[SW_L] = r[PC_L];
-        o[SW_MSGS] = v.num_msgs; o[SW_V] = v.viol->count;
-        o[SW_DCHOSEN] = r[PC_DCHOSEN]; o[SW_DSTATE] = r[PC_DSTATE]; o[SW_DSCAL] = ds; o[SW_Q] = r[PC_Q];
-        for (uint32_t n = 0; n < v.N && n < 24; ++n) {
-            o[SW_NODE_SCAL + 2 * n] = v.node_scal[2 * n];
-            o[SW_NODE_SCAL + 2 * n + 1] = v.node_scal[2 * n + 1];
+        if (t < v.N) {
+            const uint64_t p = v.node_scal[2 * t], m = v.node_scal[2 * t + 1];
+            ds = scalar_digest(t, p, m);
+            if (t < 24) { o[SW_NODE_SCAL + 2 * t] = p; o[SW_NODE_SCAL + 2 * t + 1] = m; }
         }
+        for (int d = 32; d >= 1; d >>= 1) ds += __shfl_xor(ds, d, 64);
+        if (t == 0) { o[SW_DSCAL] = ds; o[SW_MSGS] = v.num_msgs; o[SW_V] = v.viol->count; }
+    }
+    __syncthreads();
+    if (t < 8) {
+        unsigned long long r = 0;
+        for (uint32_t k = 0; k < W; ++k) r += red[k][t];
+        const int w = t == PC_C ? SW_C : t == PC_P ? SW_P : t == PC_A ? SW_A : t == PC_L ? SW_L :
+                      t == PC_DCHOSEN ? SW_DCHOSEN : t == PC_DSTATE ? SW_DSTATE : t == PC_Q ? SW_Q : -1;
+        if (w >= 0) o[w] = r;
     }
 }
 
@@ -2673,11 +2785,11 @@ __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base
 }
 
 // the summary pass (the default; knob 16777216: k_chosen's last block instead, A/B)
-// (1024 threads and 16-byte loads over the partial rows: its single workgroup is latency-bound)
-__global__ __launch_bounds__(1024) void k_reduce(DevView v, uint32_t n_partials)
+// (512 threads and 16-byte loads over the partial rows: its single workgroup is latency-bound)
+__global__ __launch_bounds__(512) void k_reduce(DevView v, uint32_t n_partials)
 {
-    __shared__ unsigned long long red[16][8];
-    reduce_summary<16>(v, n_partials, red);
+    __shared__ unsigned long long red[8][8];
+    reduce_summary<8>(v, n_partials, red);
 }
 
 __global__ void k_reset(DevView v, uint32_t n_partials)
@@ -3051,13 +3163,26 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                                   (hipEvent_t)ev_begin, (hipEvent_t)nullptr, 0, v, n_partials);
         else hipLaunchKernelGGL(k_scan_chunk<false>, dim3(v.num_chunks), dim3(256), 0, s, v, n_partials);
         if (v.scan_node_pass) hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);   // long node streams
-        if (v.semantics == MPX_SEM_MEMBER) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
-        else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
     }
-    if (v.num_pc) hipLaunchKernelGGL(k_prop_chunk, dim3(v.num_pc), dim3(64), 0, s, v);
+    // the scan's flag pass, the promise-quorum chunks and the accept votes: one launch
+    // (k_headers); knob 134217728: three launches (A/B)
+    const bool member_sem = v.semantics == MPX_SEM_MEMBER;
+    if (!(v.knobs & 134217728)) {
+        const uint32_t nb_scan = v.num_chunks, nb_prop = cdiv(v.num_pc, 4), nb_votes = cdiv(v.num_batches, 256);
+        if (nb_scan + nb_prop + nb_votes) {
+            if (member_sem) hipLaunchKernelGGL(k_headers<true>, dim3(nb_scan + nb_prop + nb_votes), dim3(256), 0, s, v, nb_scan, nb_prop);
+            else hipLaunchKernelGGL(k_headers<false>, dim3(nb_scan + nb_prop + nb_votes), dim3(256), 0, s, v, nb_scan, nb_prop);
+        }
+    } else {
+        if (v.num_chunks) {
+            if (member_sem) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
+            else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
+        }
+        if (v.num_pc) hipLaunchKernelGGL(k_prop_chunk, dim3(v.num_pc), dim3(64), 0, s, v);
+        if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
+    }
     // (a window: every node's round after the window, prop_out, comes from k_prop_node)
     if ((v.num_pc && v.pc_multi) || v.window) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s, v);
-    if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
     if (v.window) {
         // incremental window (multi): every pair of the window on the value-state walk, the
         // chosen log of the batches chosen in it, the summary
@@ -3065,7 +3190,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                               (hipEvent_t)ev_general, 0, v);
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         hipLaunchKernelGGL(k_chosen_win, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
-        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
+        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(512), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
         return (int)hipGetLastError();
     }
     const bool member = v.semantics == MPX_SEM_MEMBER;
@@ -3091,7 +3216,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     const uint32_t plan_blocks = cdiv((uint64_t)v.N * v.NB, 256);
     if (plan_path) {
         if (member) {
-            hipExtLaunchKernelGGL(k_plan_list<true>, dim3(plan_blocks), dim3(256), 0, s,
+            hipExtLaunchKernelGGL((v.knobs & 536870912) ? k_plan_list<true, 8, 32> : k_plan_list<true>, dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
             launch_store((hipEvent_t)ev_apply1);
         } else {
@@ -3101,7 +3226,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
             // (the chosen-log buckets on threads of their own after the pairs: 63.5 vs 61.5 us at C4)
             hipExtLaunchKernelGGL(k_plan, dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
-            if (lplan) hipLaunchKernelGGL(k_plan_list<false>, dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
+            if (lplan && (v.knobs & 536870912)) hipLaunchKernelGGL((k_plan_list<false, 8, 32>), dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
+            else if (lplan) hipLaunchKernelGGL(k_plan_list<false>, dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
             // every pair the trace marks lean (pair_gp 0) is one k_plan can describe (ingest.cpp /
             // mpx_load_clean_device use its predicate, plan_shape_ok), so k_plan leaves nothing to
             // k_apply_fast (fast_rest 0, checked when the run is collected); knob 4194304 launches
@@ -3178,14 +3304,20 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                    else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
                    else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
     }
-    // the chosen log of the buckets no plan word covered, then the summary (k_reduce); knob
+    // the chosen log of the buckets no plan word covered (none when the trace's chosen-log runs
+    // passed plan_chosen's static test at load: k_chosen is not launched; knob 268435456 launches
+    // it anyway, A/B), then the summary (k_reduce); knob
     // 16777216: the summary in k_chosen's last workgroup instead — measured slower (C4 tail
     // 0.075 vs 0.015 ms, C3 0.161 vs 0.071 ms: every workgroup's device-scope fence writes
     // back its XCD's L2 before the ticket), kept for A/B
-    if (!(v.knobs & 16777216)) {
+    const bool skip_chosen = plan_path && v.chosen_static && !(v.knobs & (16777216 | 268435456));
+    if (skip_chosen) {
+        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(512), 0, s, (hipEvent_t)ev_general, (hipEvent_t)ev_end, 0, v,
+                              n_partials);
+    } else if (!(v.knobs & 16777216)) {
         hipExtLaunchKernelGGL(k_chosen<false>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)nullptr, 0, v, g.apply_wgs, n_partials);
-        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
+        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(512), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
     } else {
         hipExtLaunchKernelGGL(k_chosen<true>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)ev_end, 0, v, g.apply_wgs, n_partials);

@@ -268,6 +268,8 @@ struct DevView {
                                     // half of the descriptor, streamed without the entry words
     uint64_t *plan;                 // (N + 1) * NB: the segments k_store writes over a whole (row, bucket) (plan_idx),
                                     // rows 0..N-1 state, row N chosen log; PLAN_SKIP = not by k_store
+    uint32_t chosen_static;         // every bucket's chosen-log runs pass plan_chosen's static test (<= 4
+                                    // disjoint dense runs, a whole bucket): the plan step needs no k_chosen
     uint32_t *fast_rest;            // [0]: pairs k_plan leaves to k_apply_fast (0: it exits at once);
                                     // [1]: k_chosen's last-workgroup ticket
     uint32_t *store_dummy;          // 64 KiB sink for k_store's skipped (row, bucket) stores

@@ -105,6 +105,7 @@ def lib():
             "mpx_run": [vp], "mpx_reset_state": [vp], "mpx_step": [vp], "mpx_sync": [vp],
             "mpx_timings": [vp, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_uint32)],
             "mpx_timings_detail": [vp, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_uint32)],
+            "mpx_timing_every": [vp, ctypes.c_uint32],
             "mpx_drain_sends": [vp, SEND_FN, vp],
             "mpx_read_chosen": [vp, ctypes.c_uint64, ctypes.c_uint64, u64p],
             "mpx_read_node_scalars": [vp, ctypes.c_uint32, u64p, u64p],
@@ -284,6 +285,10 @@ class Engine:
         n = ctypes.c_uint32()
         _ck("mpx_timings", lib().mpx_timings(self.h, max_n, a, r, ctypes.byref(n)))
         return list(a[: n.value]), list(r[: n.value])
+
+    def timing_every(self, every):
+        """Phase events on every `every`-th run / step only (mpx_timing_every)."""
+        _ck("mpx_timing_every", lib().mpx_timing_every(self.h, every))
 
     PHASES = ("run", "scan", "fast_apply", "general_apply", "tail")
 

@@ -150,6 +150,59 @@ typedef struct { map_t idx; valrec_t *v; size_t n, cap; buf_t bytes; } vtab_t;
 
 enum { OK = 0, E_INVAL = -1, E_DECODE = -4, E_RANGE = -5, E_VALUE = -9, E_NOMEM = -2 };
 
+/* AvailableInstanceIDs (multi/paxos.cpp:253-318): disjoint ranges [a, b), ascending,
+ * [0, 2^64-1) at first — the proposer's unproposed instance ids (client proposals) */
+typedef struct { u64 *a, *b; size_t n, cap; } rng_t;
+static int rng_init(rng_t *r)
+{
+    r->n = 0;
+    if (!r->cap) {
+        r->cap = 16;
+        r->a = (u64 *)malloc(8 * r->cap); r->b = (u64 *)malloc(8 * r->cap);
+        if (!r->a || !r->b) return E_NOMEM;
+    }
+    r->a[0] = 0; r->b[0] = ~0ull; r->n = 1;
+    return OK;
+}
+static size_t rng_find(const rng_t *r, u64 id)        /* index of the range holding id, or n */
+{
+    size_t lo = 0, hi = r->n;
+    while (lo < hi) { size_t mid = (lo + hi) / 2; if (r->b[mid] <= id) lo = mid + 1; else hi = mid; }
+    return lo < r->n && r->a[lo] <= id ? lo : r->n;
+}
+static int rng_contains(const rng_t *r, u64 id) { return rng_find(r, id) < r->n; }
+static int rng_remove(rng_t *r, u64 id)
+{
+    size_t i = rng_find(r, id);
+    if (i == r->n) return OK;
+    u64 a = r->a[i], b = r->b[i];
+    if (a != id && id + 1 != b) {                        /* split: one more range */
+        if (r->n == r->cap) {
+            size_t cc = r->cap * 2;
+            u64 *na = (u64 *)realloc(r->a, 8 * cc), *nb = (u64 *)realloc(r->b, 8 * cc);
+            if (!na || !nb) return E_NOMEM;
+            r->a = na; r->b = nb; r->cap = cc;
+        }
+        memmove(r->a + i + 2, r->a + i + 1, 8 * (r->n - i - 1));
+        memmove(r->b + i + 2, r->b + i + 1, 8 * (r->n - i - 1));
+        r->b[i] = id; r->a[i + 1] = id + 1; r->b[i + 1] = b; r->n++;
+    } else if (a != id) {
+        r->b[i] = id;
+    } else if (id + 1 != b) {
+        r->a[i] = id + 1;
+    } else {
+        memmove(r->a + i, r->a + i + 1, 8 * (r->n - i - 1));
+        memmove(r->b + i, r->b + i + 1, 8 * (r->n - i - 1));
+        r->n--;
+    }
+    return OK;
+}
+static u64 rng_next(rng_t *r) { u64 a = r->a[0]; rng_remove(r, a); return a; }
+static void rng_remove_below(rng_t *r, u64 x)             /* [0, 2^64-1) -> [x, 2^64-1) */
+{
+    if (r->n == 1 && r->a[0] == 0) r->a[0] = x;
+}
+
 /* Parse one Value at p (avail bytes).  Returns bytes used (>0) or <0. */
 /* Parse one Value at p (avail bytes).  Returns bytes used (>0) or <0.
  * t == NULL: length and handle only (an entry outside the oracle's shard). */
@@ -354,6 +407,11 @@ typedef struct {
     int rc;
     /* phase-2 decisions (mpxo_decisions): value_id_ (multi/paxos.cpp:335) and the MPXD records */
     u64 value_id;
+    /* client proposals (P_PROPOSE): unproposed_instance_ids_, initial_proposals_ (iid -> value
+     * id), newly_proposed_values_ (ascending value ids) — multi/paxos.cpp:1132-1175,1250-1280 */
+    rng_t unp;
+    map_t initial;
+    u64 *newly; size_t nnew, cnew;
     buf_t dec; u64 n_dec;
     /* commit reliability (mpxo_commits): committing_values_
      * (multi/paxos.cpp:483), one record per CommittingValues in id order */
@@ -567,7 +625,10 @@ static int on_accept(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     return OK;
 }
 
-/* OnCommit, learner part: multi/paxos.cpp:1494-1518,1572-1622 */
+static int commit_proposals(node_t *n, u64 iid, u64 h);
+
+/* OnCommit: learner part multi/paxos.cpp:1494-1518,1572-1622; proposer part (:1519-1570)
+ * in commit_proposals */
 static int on_commit(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
 {
     if (len < 28) return E_DECODE;
@@ -599,6 +660,14 @@ static int on_commit(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
             pres_add(c, n, iid);
         }
         n->L++;
+        if (c->want_dec) map_put(&n->seen, iid, h, 1);          /* (the proposer part, below, in id order) */
+    }
+    if (c->want_dec && n->seen.n) {
+        size_t k;
+        ent_t *v = map_sorted(&n->seen, &k);
+        for (size_t j = 0; j < k; ++j)
+            if (commit_proposals(n, v[j].key, v[j].a)) { free(v); return E_NOMEM; }
+        free(v);
     }
    
     buf_t r = {0};
@@ -621,16 +690,55 @@ static int on_commit(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     return OK;
 }
 
-/* The phase-2 batch OnPrepareReply builds at a promise quorum
- * (multi/paxos.cpp:1056-1130), for a proposer with no client proposals of its
- * own (initial_proposals_ / newly_proposed_values_ empty; the driver's state):
- * unproposed = uncommitted_instance_ids_ = every id not committed here; every
- * pre-accepted value of an unproposed id is adopted (:1071-1102); then every
- * range of the unproposed set but the last, open one is filled with noops
- * Value(index_, ++value_id_) in id order (:1117-1130).  The last range starts
- * after the highest committed or adopted id, so the fill covers exactly the
- * unproposed, non-adopted ids below it.  Record: seq, count, {iid, handle}
- * ascending (the AcceptingValues map order). */
+/* The phase-2 batch OnPrepareReply builds at a promise quorum (multi/paxos.cpp:1056-1175):
+ * unproposed = uncommitted_instance_ids_ = every id not committed here; every pre-accepted
+ * value of an unproposed id is adopted (:1071-1102); every range of the unproposed set but
+ * the last, open one is filled with noops Value(index_, ++value_id_) in id order (:1117-1130)
+ * — the last range starts after the highest committed or adopted id X, so the fill covers
+ * exactly the unproposed, non-adopted ids below it; then the node's own client values
+ * (:1132-1175, P_PROPOSE records): initial proposals at ids >= X, the queued ones at the
+ * next free ids.  Record: seq, count, {iid, handle} ascending (the AcceptingValues map order). */
+static int add_newly(node_t *n, u64 vid)
+{
+    for (size_t i = 0; i < n->nnew; ++i) if (n->newly[i] == vid) return OK;
+    if (n->nnew == n->cnew) {
+        size_t cc = n->cnew ? 2 * n->cnew : 16;
+        u64 *q = (u64 *)realloc(n->newly, 8 * cc);
+        if (!q) return E_NOMEM;
+        n->newly = q; n->cnew = cc;
+    }
+    size_t i = n->nnew++;
+    while (i && n->newly[i - 1] > vid) { n->newly[i] = n->newly[i - 1]; --i; }   /* a std::set */
+    n->newly[i] = vid;
+    return OK;
+}
+
+/* Propose (:1250-1280): a new value id; not preparing -> the next unproposed instance now
+ * (its AcceptingValues is the trace's P_BATCH), else queued for the next promise quorum */
+static int on_propose(node_t *n)
+{
+    ++n->value_id;
+    if (!n->preparing) { map_put(&n->initial, rng_next(&n->unp), n->value_id, 0); return OK; }
+    return add_newly(n, n->value_id);
+}
+
+/* OnCommit's proposer part (:1519-1570), one committed entry in instance order: the id leaves
+ * the unproposed set; an own initial proposal that lost it is proposed again — at the next
+ * unproposed id now, or queued while preparing */
+static int commit_proposals(node_t *n, u64 iid, u64 h)
+{
+    if (rng_contains(&n->unp, iid)) rng_remove(&n->unp, iid);
+    ent_t *e = map_find(&n->initial, iid);
+    if (!e) return OK;
+    u64 v0 = e->a;
+    map_del(&n->initial, iid);
+    if ((h >> 48) != n->index || (h & ((1ull << 47) - 1)) != v0) {
+        if (!n->preparing) map_put(&n->initial, rng_next(&n->unp), v0, 0);
+        else return add_newly(n, v0);
+    }
+    return OK;
+}
+
 static void decide(node_t *n, const ent_t *pre, size_t k, u64 seq)
 {
     u64 X = 0;
@@ -649,6 +757,32 @@ static void decide(node_t *n, const ent_t *pre, size_t k, u64 seq)
         else bput64(&d, ((u64)n->index << 48) | (1ull << 47) | ++n->value_id);           /* noop */
         ++cnt;
     }
+    /* then the own values (:1132-1175): unproposed is now [X, 2^64-1); the initial proposals
+     * still in it keep their instance, the queued ones take the next free ids */
+    rng_init(&n->unp);
+    rng_remove_below(&n->unp, X);
+    size_t ni = 0, np = 0;
+    ent_t *iv = map_sorted(&n->initial, &ni);
+    u64 *pe = (u64 *)malloc(16 * (ni + n->nnew + 1));
+    for (size_t j = 0; j < ni; ++j)
+        if (rng_contains(&n->unp, iv[j].key)) {
+            rng_remove(&n->unp, iv[j].key);
+            pe[2 * np] = iv[j].key; pe[2 * np + 1] = ((u64)n->index << 48) | iv[j].a; ++np;
+        }
+    free(iv);
+    for (size_t j = 0; j < n->nnew; ++j) {
+        u64 iid = rng_next(&n->unp);
+        map_put(&n->initial, iid, n->newly[j], 0);
+        pe[2 * np] = iid; pe[2 * np + 1] = ((u64)n->index << 48) | n->newly[j]; ++np;
+    }
+    n->nnew = 0;
+    for (size_t a = 1; a < np; ++a)                              /* by instance (the batch is a map) */
+        for (size_t b = a; b > 0 && pe[2 * b - 2] > pe[2 * b]; --b) {
+            u64 t0 = pe[2 * b - 2], t1 = pe[2 * b - 1];
+            pe[2 * b - 2] = pe[2 * b]; pe[2 * b - 1] = pe[2 * b + 1]; pe[2 * b] = t0; pe[2 * b + 1] = t1;
+        }
+    for (size_t j = 0; j < np; ++j) { bput64(&d, pe[2 * j]); bput64(&d, pe[2 * j + 1]); ++cnt; }
+    free(pe);
     bput64(&n->dec, seq);
     bput64(&n->dec, cnt);
     bput(&n->dec, d.p, d.n);
@@ -832,6 +966,9 @@ static int process(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
     case 6:  return on_commit_reply(c, n, m, len, seq);
     case 16: return on_p_start(n, m, len);
     case 17: return on_p_batch(c, n, m, len, seq);
+    case 19:                                                    /* P_PROPOSE: Propose (:1250-1280) moves */
+        if (len < 8 || 8 + (uint64_t)rd32(m + 4) > len) return E_DECODE;   /* no acceptor / learner state */
+        return on_propose(n);
     default: return E_DECODE;                                   /* ASSERT(false), :1672 */
     }
 }
@@ -1324,6 +1461,7 @@ static int run_shard_ex(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64
     for (u32 i = 0; i < c.N && rc == OK; ++i) {
         node_t *n = &c.nodes[i];
         n->index = i;
+        if (rng_init(&n->unp)) { rc = E_NOMEM; break; }
         if (c.sem == 1) {                                  /* genesis roles: epoch 0 */
             n->acc_exists = (int)((c.ep[0].amask >> i) & 1);
             n->prop_exists = (int)((c.ep[0].pmask >> i) & 1);
@@ -1389,6 +1527,7 @@ static int run_shard_ex(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64
         node_t *n = &c.nodes[i];
         map_free(&n->vt.idx); free(n->vt.v); free(n->vt.bytes.p);
         map_free(&n->seen);
+        map_free(&n->initial); free(n->unp.a); free(n->unp.b); free(n->newly);
     }
     free(c.nodes);
     free(c.ep);

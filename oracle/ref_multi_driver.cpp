@@ -15,7 +15,10 @@
 // The proposer control plane (out of scope) is held still: P_START / P_BATCH
 // trace markers set the fields StartPrepare / Accept would set, and batches
 // the reference's own decision code creates after a promise quorum are
-// discarded (their sends are not in-scope replies either).
+// discarded (their sends are not in-scope replies either).  A P_PROPOSE marker
+// calls the reference's own Propose, so its bookkeeping (value_id_,
+// initial_proposals_, newly_proposed_values_) is the real one; the batch it may
+// create is replaced by the trace's P_BATCH with the same accept id.
 //
 // Output: the canonical MPXR result, byte-comparable with
 // oracle/mpx_oracle.c and the engine's mpx_dump_result.
@@ -147,8 +150,8 @@ extern "C" int mpxref_commits(const uint8_t *trace, uint64_t size, uint8_t **out
 
 // The reference's own phase-2 decisions (MPXD): per node, per
 // promise quorum {u64 seq, u64 count, {u64 iid, u64 handle} * count}, the batch
-// OnPrepareReply built with this driver's proposer bookkeeping (no client
-// proposals: initial_proposals_ and newly_proposed_values_ stay empty).
+// OnPrepareReply built with this driver's proposer bookkeeping (client proposals
+// from P_PROPOSE markers: initial_proposals_ / newly_proposed_values_).
 extern "C" int mpxref_decisions(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)
 {
     uint8_t *r = NULL;
@@ -330,6 +333,11 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
                 for (auto &e : p->accepting_values_) e.second->retry_timeout_->Cancel();
                 p->accepting_values_.clear();
                 p->prepare_retry_timeout_ = dummy_prt;
+                break;
+            }
+            case 19: {         // P_PROPOSE: the reference's own Propose (multi/paxos.cpp:1250-1280)
+                const uint32_t pl = rd32(m + 4);
+                p->Propose(paxos::ProposedValue(std::string((const char *)m + 8, pl), &g_nop));
                 break;
             }
             case 17: {         // P_BATCH

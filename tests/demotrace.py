@@ -9,8 +9,9 @@ input — is exactly the server thread's "receive from srv[j]" lines.
 
 What the log does not give directly is where, between two received messages,
 the node's proposer control plane (out of scope) acted.
-Those actions are the engine-local P_START / P_BATCH records (include/mpx.h),
-and the paxos thread logs every one of them:
+Those actions are the engine-local P_START / P_BATCH / P_PROPOSE records
+(include/mpx.h), and the paxos thread logs every one of them:
+  * Propose             "propose: V"                 (multi/paxos.cpp:1253)     -> P_PROPOSE(V);
   * StartPrepare        "add restart prepare timer"  (multi/paxos.cpp:1246) -> P_START,
                         ballot = the next PREPARE this node broadcasts (:814-825);
   * a new AcceptingValues "broadcast accept" (:1310) with an accept id not seen
@@ -166,6 +167,10 @@ def node_stream(n, nd, n_nodes):
             take(find(lambda m: _u32(m, 0) == 6 and _u32(m, 4) == lr and _u64(m, 8) == k, "OnCommitReply"))
         elif func == "UpdateByPreAcceptedValues":
             take(find(lambda m: _u32(m, 0) == 1 and _u64(m, 8) == cur, "OnPrepareReply"))
+        elif func == "Propose" and msg.startswith("propose: "):
+            # a client value reaches PaxosImpl::Propose (:1250-1253; the demo proposes
+            # id2str(id), main.cpp:298-301, and Debug prints it back, :214-219)
+            out.append(W.p_propose(msg[len("propose: "):]))
         elif func == "StartPrepare" and msg.startswith("add restart prepare timer"):
             b = next_send(i, 0)
             if b is None:             # the run ended before this prepare went out:

@@ -1,6 +1,6 @@
 """Hand-written traces, one per reference quirk."""
 from mpxwire import (U64_MAX_EXCL, accept, accept_reply, commit, commit_reply,
-                     container, p_batch, p_start, prepare, prepare_reply,
+                     container, p_batch, p_propose, p_start, prepare, prepare_reply,
                      reject, value)
 
 B1 = (1 << 16) | 0
@@ -75,4 +75,26 @@ def handmade_traces():
         accept_reply(3, B1, 12), accept_reply(0, B1, 12), accept_reply(1, B1, 12),
         commit_reply(2, 1),
     ], [], [], [], []], 4)
+
+    # 7. client proposals (Propose, OnPrepareReply's own / new values, OnCommit re-propose;
+    # multi/paxos.cpp:1132-1175,1250-1280,1524-1570): node 0 of 3
+    a, b, c = value(0, 1, "a"), value(0, 2, "b"), value(0, 6, "c")
+    other = value(1, 7, "x")
+    t["hm_propose"] = container([[
+        p_propose("a"),                                 # not preparing: instance 0 at once (value id 1)
+        p_batch(1, [(0, a)]),
+        p_start(B1),                                    # AcceptRejected -> preparing
+        p_propose("b"),                                 # queued (value id 2)
+        prepare_reply(1, B1, [(3, B1 - 1, other)]),
+        prepare_reply(2, B1),                           # quorum: adopt 3, noops 0..2 (ids 3..5), b at 4
+        commit(1, 5, B1, [(0, value(0, 3, noop=True))]),   # 0 committed as a noop: "a" re-proposed at 5
+        p_batch(3, [(5, a)]),
+        p_propose("c"),                                 # not preparing: instance 6 (value id 6)
+        p_batch(4, [(6, c)]),
+        p_start(B3),
+        prepare_reply(1, B3, [(2, B1, value(1, 8, "y"))]),
+        commit(2, 6, B3, [(1, value(0, 4, noop=True)), (6, other)]),   # 6 lost: "c" queued again
+        prepare_reply(2, B3),                           # quorum: adopt 2, noops 3..5 (own 4, 5 among
+                                                        # them: the fill comes first), c at 7
+    ], [prepare(0, B1), accept(0, 1, B1, [(0, a)])], []], 16)
     return t

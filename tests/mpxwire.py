@@ -77,6 +77,13 @@ def p_batch(batch_id, entries):
     return struct.pack("<IQI", 17, batch_id, len(body)) + body
 
 
+def p_propose(payload):
+    """PaxosImpl::Propose(value) of a client value (multi/paxos.cpp:1250-1280)."""
+    if isinstance(payload, str):
+        payload = payload.encode()
+    return struct.pack("<II", 19, len(payload)) + payload
+
+
 def container(streams, num_instances=0, semantics=0, epochs=()):
     """streams: list (per node) of lists of message bytes, in processing order.
     epochs (member): (version, acceptor_mask, proposer_mask) per epoch."""

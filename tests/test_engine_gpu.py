@@ -446,7 +446,8 @@ def test_store_chunks_tails_and_partial_pairs(extra):
 @pytest.mark.parametrize("env", [("MPX_SCAN_NODE_PASS", "1"), ("MPX_KNOBS", "2048"), ("MPX_PROP_CHUNK", "64"),
                                  ("MPX_PROP_CHUNK", "5"), ("MPX_KNOBS", "65536"), ("MPX_KNOBS", "262144"),
                                  ("MPX_KNOBS", "131072"), ("MPX_APPLY_VARIANT", "1"), ("MPX_KNOBS", "8388608"),
-                                 ("MPX_KNOBS", "4194304"), ("MPX_KNOBS", "16777216"), ("MPX_KNOBS", "33554432")])
+                                 ("MPX_KNOBS", "4194304"), ("MPX_KNOBS", "16777216"), ("MPX_KNOBS", "33554432"),
+                                 ("MPX_KNOBS", "134217728"), ("MPX_KNOBS", "268435456"), ("MPX_KNOBS", "536870912")])
 @pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "c5_member_3",
                                   "demo_s0", "demo5_s3", "hm_promise_merge"])
 def test_kept_alternative_paths(name, env, monkeypatch):
@@ -457,7 +458,9 @@ def test_kept_alternative_paths(name, env, monkeypatch):
     work list without its SIMPLE / SNAP split, PREPARE ranges loaded instead of
     the inline interval, the unconstrained (3-wave) k_apply builds, multi work lists
     without k_plan_list, k_apply_fast launched after the store, the summary folded into
-    k_chosen's last workgroup, and k_reset as its own launch."""
+    k_chosen's last workgroup, k_reset as its own launch, the header kernels as three
+    launches, k_chosen launched where the load found every chosen-log bucket plannable, and
+    the 8-segment / 32-run k_plan_list."""
     if name not in INDEX:
         pytest.skip("no golden " + name)
     monkeypatch.setenv(*env)
@@ -547,6 +550,33 @@ def test_engine_decisions_match_reference(name):
         assert e.decisions() == want
 
 
+PROPOSAL_TRACES = ["demo5_s3", "demo5_s4", "demo_s0", "demo_s1", "demo_s2", "hm_propose"]   # P_PROPOSE records
+
+
+@pytest.mark.parametrize("name", sorted(set(DECISIONS) - set(PROPOSAL_TRACES)))
+def test_proposer_host_sim_matches_device_decisions(name, monkeypatch):
+    """The proposer's sequential bookkeeping on the host (MPX_DECIDE_HOST=1; what a trace with
+    client values takes) == the device decision kernels on traces without client values."""
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxd")
+    with mpx.Engine.for_trace(trace) as e:
+        e.run()
+        assert e.decisions() == want
+        monkeypatch.setenv("MPX_DECIDE_HOST", "1")
+        assert e.decisions() == want
+
+
+@pytest.mark.parametrize("name", ["demo_s1", "hm_propose"])
+def test_proposal_traces_refuse_sharded_decisions(name):
+    """Client values make the batch depend on the whole node's stream (value ids shared with
+    the noop fill): decisions are read from a whole engine; the shard protocol refuses."""
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxd")
+    with mpx.Engine.for_trace(trace) as e:
+        e.run()
+        assert e.decisions() == want
+        with pytest.raises(mpx.MpxError):
+            e.decision_bounds()
+
+
 @pytest.mark.parametrize("seed,m", [(81, 1 << 12), (82, 3000), (83, 1 << 14)])
 def test_engine_decisions_match_oracle_c3(seed, m):
     from oracles import oracle_decisions
@@ -585,7 +615,7 @@ def _sharded_decisions(trace, shards, align=256):
 
 
 @pytest.mark.parametrize("shards", [2, 3])
-@pytest.mark.parametrize("name", ["fuzz_big_1", "fuzz_big_2", "c3_faulty_0", "demo_s1", "hm_promise_merge", "fuzz_007"])
+@pytest.mark.parametrize("name", ["fuzz_big_1", "fuzz_big_2", "c3_faulty_0", "c3_faulty_1", "hm_promise_merge", "fuzz_007"])
 def test_sharded_decisions_match_reference(name, shards):
     """Phase-2 decisions over instance shards (one engine per range; one
     all-reduce-MAX of the per-quorum fill bounds, then the parts merged in shard
@@ -594,7 +624,7 @@ def test_sharded_decisions_match_reference(name, shards):
     assert _sharded_decisions(trace, shards, align=1) == want     # unaligned, non-empty shards of small runs
 
 
-@pytest.mark.parametrize("name", ["fuzz_big_1", "c3_faulty_0", "demo_s1", "hm_promise_merge"])
+@pytest.mark.parametrize("name", ["fuzz_big_1", "c3_faulty_0", "c3_faulty_1", "hm_promise_merge"])
 def test_committed_before_host_prefix_matches_device_pass(name, monkeypatch):
     """'Highest instance committed before the quorum' from the node's COMMIT messages in
     order (host prefix max, the default) == k_decide pass 0's scan of every slot."""

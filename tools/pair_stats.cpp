@@ -132,6 +132,33 @@ int main(int argc, char **argv)
                     (unsigned long long)snap_ev, (unsigned long long)snap_lean, (unsigned long long)snap_late,
                     (unsigned long long)snap_late_ev);
     }
+    // the work list's pairs without promise rounds that a plan walk with up to S segments and
+    // R runs would take (dense accept / commit runs only)
+    {
+        const uint32_t RS[4][2] = {{16, 4}, {32, 8}, {32, 16}, {64, 32}};
+        uint64_t lst = 0, cov[4] = {0, 0, 0, 0};
+        for (uint64_t it = 0; it < h.num_gp_snap; ++it) {
+            const uint64_t q = h.gp_list[it];
+            const uint64_t f0 = h.f_off[q], f1 = h.f_off[q + 1];
+            ++lst;
+            bool dense = true;
+            std::vector<uint32_t> bnd;
+            for (uint64_t f = f0; f < f1; ++f) {
+                const Frag &fr = h.frags[f];
+                const uint32_t kind = fr.flags >> 4;
+                if (!(fr.flags & FR_DENSE) || (kind != K_ACCEPT && kind != K_COMMIT)) dense = false;
+                if (fr.start) bnd.push_back(fr.start);
+                if (fr.start + fr.count < BS) bnd.push_back(fr.start + fr.count);
+            }
+            std::sort(bnd.begin(), bnd.end());
+            bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+            for (int k = 0; k < 4; ++k)
+                cov[k] += dense && f1 - f0 <= RS[k][0] && bnd.size() + 1 <= RS[k][1];
+        }
+        std::printf("list pairs %llu; plannable with (runs, segments) <= (16,4) %llu, (32,8) %llu, (32,16) %llu, (64,32) %llu\n",
+                    (unsigned long long)lst, (unsigned long long)cov[0], (unsigned long long)cov[1],
+                    (unsigned long long)cov[2], (unsigned long long)cov[3]);
+    }
     std::printf("runs/pair:");
     for (auto &x : runs_h) std::printf(" %llu:%llu", (unsigned long long)x.first, (unsigned long long)x.second);
     std::printf("\ninterior boundaries/pair:");
