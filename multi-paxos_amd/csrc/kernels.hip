@@ -349,6 +349,13 @@ __global__ __launch_bounds__(256) void k_gate_votes(DevView v)
 
 constexpr uint32_t SCAN_ROUNDS = SCAN_CHUNK / 256;   // rounds of 64 records per wave
 
+// the summary word a partial-row column adds into (-1: none)
+__device__ inline int summary_word(uint32_t pc)
+{
+    return pc == PC_C ? SW_C : pc == PC_P ? SW_P : pc == PC_A ? SW_A : pc == PC_L ? SW_L :
+           pc == PC_DCHOSEN ? SW_DCHOSEN : pc == PC_DSTATE ? SW_DSTATE : pc == PC_Q ? SW_Q : -1;
+}
+
 // Per-step reset of what the step accumulates (k_reset, or the head of k_scan_chunk when
 // it is the step's first kernel): thread t of T zeroes its share, grid-stride
 __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64_t t, uint64_t T)
@@ -369,6 +376,8 @@ __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64
         v.fast_rest[1] = 0;                          // k_chosen's last-block ticket
         *v.gp_dyn_n = 0;
         if (v.window) *v.outv_n = 0;
+        for (uint32_t pc = 0; pc < 8; ++pc)          // the counter words k_reduce's workgroups add into
+            if (summary_word(pc) >= 0) v.summary[summary_word(pc)] = 0;
         v.viol->code = v.viol->node = v.viol->seq = v.viol->iid = v.viol->count = 0;
     }
 }
@@ -2684,16 +2693,19 @@ __global__ __launch_bounds__(256) void k_state_digest_win(DevView v, unsigned lo
 }
 
 // The step's summary (mpx_allgather_summary's 64 words) from every workgroup's
-// partial counters: one workgroup of 256 threads
+// partial counters: this workgroup (64 W threads) sums the partial rows row0, row0 + stride,
+// ... into the summary's counter words (zeroed by reset_state; integer sums, so the order of
+// the workgroups' atomics does not matter); SCAL: it also writes the node scalars' words
 template <uint32_t W>
-__device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, unsigned long long (&red)[W][8])
+__device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, unsigned long long (&red)[W][8],
+                                      uint32_t row0, uint32_t stride, bool scal)
 {
-    // one workgroup of 64 W threads: each partial row is 64 bytes, read as four 16-byte loads
+    // each partial row is 64 bytes, read as four 16-byte loads
     const uint32_t t = threadIdx.x;
     unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const u64x2 *p2 = reinterpret_cast<const u64x2 *>(v.partials);
 #pragma unroll 1
-    for (uint32_t w = t; w < n_partials; w += 64 * W) {
+    for (uint32_t w = row0 + t; w < n_partials; w += stride) {
         u64x2 x[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[i] = __builtin_nontemporal_load(&p2[4 * (uint64_t)w + i]);
@@ -2709,7 +2721,7 @@ __device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, uns
     // the per-node scalars, one lane per node (N <= 64): their loads all in flight at once
     // (a serial loop over the nodes in one thread waited out N memory latencies)
     unsigned long long *o = v.summary;
-    if (t < 64) {
+    if (scal && t < 64) {
         unsigned long long ds = 0;
         if (t < v.N) {
             const uint64_t p = v.node_scal[2 * t], m = v.node_scal[2 * t + 1];
@@ -2723,9 +2735,8 @@ __device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, uns
     if (t < 8) {
         unsigned long long r = 0;
         for (uint32_t k = 0; k < W; ++k) r += red[k][t];
-        const int w = t == PC_C ? SW_C : t == PC_P ? SW_P : t == PC_A ? SW_A : t == PC_L ? SW_L :
-                      t == PC_DCHOSEN ? SW_DCHOSEN : t == PC_DSTATE ? SW_DSTATE : t == PC_Q ? SW_Q : -1;
-        if (w >= 0) o[w] = r;
+        const int w = summary_word(t);
+        if (w >= 0 && r) atomicAdd(&o[w], r);
     }
 }
 
@@ -2780,16 +2791,18 @@ __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base
     __syncthreads();
     if (!last) return;
     __threadfence();                             // the other workgroups' partials
-    reduce_summary(v, n_partials, red);
+    reduce_summary(v, n_partials, red, 0, 256, true);
     if (threadIdx.x == 0) v.fast_rest[1] = 0;
 }
 
-// the summary pass (the default; knob 16777216: k_chosen's last block instead, A/B)
-// (512 threads and 16-byte loads over the partial rows: its single workgroup is latency-bound)
-__global__ __launch_bounds__(512) void k_reduce(DevView v, uint32_t n_partials)
+// the summary pass (the default; knob 16777216: k_chosen's last block instead, A/B): one
+// partial row per thread, every row's loads in flight at once over cdiv(rows, 256) workgroups
+// (one workgroup of 512 threads looping over the rows waited out six memory latencies in turn:
+// 10.7 us at the C4 shard)
+__global__ __launch_bounds__(256) void k_reduce(DevView v, uint32_t n_partials)
 {
-    __shared__ unsigned long long red[8][8];
-    reduce_summary<8>(v, n_partials, red);
+    __shared__ unsigned long long red[4][8];
+    reduce_summary<4>(v, n_partials, red, 256 * blockIdx.x, 256 * gridDim.x, blockIdx.x == 0);
 }
 
 __global__ void k_reset(DevView v, uint32_t n_partials)
@@ -3190,7 +3203,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                               (hipEvent_t)ev_general, 0, v);
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         hipLaunchKernelGGL(k_chosen_win, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
-        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(512), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
+        hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
         return (int)hipGetLastError();
     }
     const bool member = v.semantics == MPX_SEM_MEMBER;
@@ -3312,12 +3325,12 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     // back its XCD's L2 before the ticket), kept for A/B
     const bool skip_chosen = plan_path && v.chosen_static && !(v.knobs & (16777216 | 268435456));
     if (skip_chosen) {
-        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(512), 0, s, (hipEvent_t)ev_general, (hipEvent_t)ev_end, 0, v,
-                              n_partials);
+        hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)ev_general,
+                              (hipEvent_t)ev_end, 0, v, n_partials);
     } else if (!(v.knobs & 16777216)) {
         hipExtLaunchKernelGGL(k_chosen<false>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)nullptr, 0, v, g.apply_wgs, n_partials);
-        hipExtLaunchKernelGGL(k_reduce, dim3(1), dim3(512), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
+        hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
     } else {
         hipExtLaunchKernelGGL(k_chosen<true>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)ev_end, 0, v, g.apply_wgs, n_partials);
