@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 1u
+#define MPX_ABI_VERSION 2u   /* 2: mpx_epoch carries learner_mask (32 bytes) */
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -120,12 +120,17 @@ enum { MPX_SEM_MULTI = 0, MPX_SEM_MEMBER = 1 };
  * node starts in epoch 0 (Loop: {first} is learner, proposer and acceptor,
  * member/paxos.cpp:738-747).  An acceptor drops PREPARE/ACCEPT whose version
  * differs from its own (:1702,1744); the quorum is |acceptors|/2+1 (:1171,1327).
- * In an MPXT container each entry is 24 bytes, in this layout. */
+ * In an MPXT container (version 2) each entry is 32 bytes, in this layout; a
+ * version-1 container holds 24-byte entries without learner_mask (read as
+ * learner_mask = proposer_mask).  learners_ matter only to learn reliability
+ * (mpx_read_learns): a Proposer retires a learn when |learners_| replied, and
+ * a learner change re-learns (LearnersChanged, member/paxos.cpp:1345-1381,1472-1502). */
 typedef struct mpx_epoch {
     uint32_t version;         /* NodeImpl::version_ in this epoch               */
     uint32_t flags;           /* 0                                              */
     uint64_t acceptor_mask;   /* bit i set: node i is an acceptor (acceptors_)  */
     uint64_t proposer_mask;   /* bit i set: node i runs a Proposer (proposers_) */
+    uint64_t learner_mask;    /* bit i set: node i is a learner (learners_)     */
 } mpx_epoch;
 
 typedef struct mpx_config {
@@ -373,6 +378,25 @@ int  mpx_commit_points_combine(const uint8_t *const *parts, const uint64_t *size
 int  mpx_read_commits_at(mpx_engine *eng, const uint8_t *points, uint64_t points_size,
                          uint8_t **out, uint64_t *size);
 int  mpx_read_commits_sharded(mpx_engine *eng, uint8_t **out, uint64_t *size);
+/* Learn reliability (member semantics, an engine holding every
+ * instance): every LearningValues each node's Proposer created in the last run — at an
+ * accept quorum (OnAcceptReply, member/paxos.cpp:1334-1337), at a promise quorum once its
+ * learner learned anything (OnPrepareReply re-learns all of it, :1299-1307), and at
+ * LearnersChanged while not preparing (every learned and open learn's Value, :1472-1491)
+ * — numbered like learning_id_ (1, 2, ... per Proposer; a node's new Proposer starts
+ * again), and what became of it: OnLearnReply's learned_ set, the record where its
+ * learning_values_for_acceptors_ entry reached |acceptors|/2+1 and Applied ran (replies,
+ * or AcceptorsChanged :1504-1533), the record where every learner had replied (retired),
+ * or where LearnersChanged or the Proposer's deletion (:1916-1942) dropped it.  Learner
+ * and acceptor sets come from the epoch table (mpx_epoch.learner_mask); a membership step
+ * is the E_EPOCH run after the LEARN that applied it.  The replies are walked on the
+ * device (k_learns).  Format MPXL: "MPXL" u32 1, u32 nodes; per node u64 count, per learn
+ * {u64 id, u64 created_seq, u64 kind (0 accept quorum, 1 promise quorum, 2 learners
+ * changed), u64 accept_id (kind 0, else 0), u64 applied_seq, u64 retired_seq, u64
+ * dropped_seq, u64 learned_mask} (~0: did not happen), seqs = record indices in the
+ * node's stream.  *out is malloc'ed; free with mpx_free.  MPX_E_STATE for multi
+ * semantics, a shard engine or an E_EPOCH step that both adds and removes roles. */
+int  mpx_read_learns(mpx_engine *eng, uint8_t **out, uint64_t *size);
 /* Encoded reference Value bytes (multi/paxos.cpp:556-598) for a handle. */
 int  mpx_value_bytes(mpx_engine *eng, uint64_t handle, uint8_t *buf,
                      uint32_t cap, uint32_t *len);

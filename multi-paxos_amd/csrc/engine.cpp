@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 #include <set>
 #include <memory>
 #include <string>
@@ -256,18 +257,23 @@ static inline uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8
 extern "C" int mpx_submit_trace(mpx_engine *e, const uint8_t *t, uint64_t size)
 {
     if (!e || !t || size < 40 || std::memcmp(t, "MPXT", 4)) return MPX_E_INVAL;
-    const uint32_t N = rd32(t + 8), sem = rd32(t + 12), ne = rd32(t + 24);
-    if (N != e->cfg.num_nodes || sem != e->cfg.semantics) return MPX_E_INVAL;
-    if (size < 40 + (uint64_t)ne * 24) return MPX_E_DECODE;
+    const uint32_t N = rd32(t + 8), sem = rd32(t + 12), ne = rd32(t + 24), ver = rd32(t + 4);
+    if (N != e->cfg.num_nodes || sem != e->cfg.semantics || ver < 1 || ver > 2) return MPX_E_INVAL;
+    const uint32_t esz = ver == 1 ? 24 : 32;         // version 1: no learner_mask (= proposer_mask)
+    if (size < 40 + (uint64_t)ne * esz) return MPX_E_DECODE;
     if (ne) {
         // the container's epoch table: adopted by an engine created without
         // one, else it must be the same table
         std::vector<mpx_epoch> ep(ne);
-        std::memcpy(ep.data(), t + 40, (size_t)ne * 24);
+        for (uint32_t k = 0; k < ne; ++k) {
+            const uint8_t *x = t + 40 + (size_t)k * esz;
+            ep[k] = mpx_epoch{rd32(x), rd32(x + 4), rd64(x + 8), rd64(x + 16), esz == 32 ? rd64(x + 24) : rd64(x + 16)};
+        }
         if (e->epochs.empty()) e->epochs = ep;
-        else if (e->epochs.size() != ep.size() || std::memcmp(e->epochs.data(), ep.data(), (size_t)ne * 24)) return MPX_E_INVAL;
+        else if (e->epochs.size() != ep.size() || std::memcmp(e->epochs.data(), ep.data(), (size_t)ne * sizeof(mpx_epoch)))
+            return MPX_E_INVAL;
     }
-    size_t pos = 40 + (size_t)ne * 24;
+    size_t pos = 40 + (size_t)ne * esz;
     std::vector<size_t> at(N);                      // each node's stream: count word
     for (uint32_t n = 0; n < N; ++n) {
         if (pos + 16 > size) return MPX_E_DECODE;
@@ -1791,6 +1797,176 @@ extern "C" int mpx_read_commits(mpx_engine *e, uint8_t **out, uint64_t *size)
     TRY(commit_points(e, r, cm));
     std::string d;
     TRY(commits_from_points(e, cm, d));
+    return put_bytes(d, out, size);
+}
+
+// ------------------------------------------------ learn reliability (f4) --
+// The member Proposer's LearningValues bookkeeping (member/paxos.cpp:1299-1307,1334-1337,
+// 1345-1381,1472-1549,1864-1964).  The host walks each node's stream once for the control
+// plane: which Proposer incarnation runs (its learning_id_ restarts), whether it is
+// preparing, where it creates a learn — at an accept quorum (the batch's chosen reply,
+// k_votes), at a promise quorum once its learner learned anything (F_QUORUM, k_prop_*),
+// at LearnersChanged while not preparing — and where LearnersChanged or the Proposer's
+// deletion drops every open learn; the membership steps come from the E_EPOCH markers
+// that follow the LEARN which applied them (learners gained, then the Proposer created,
+// then acceptors gained; acceptors lost, then the Proposer deleted, then learners lost:
+// the reference's change lists, :638-723).  k_learns then walks each learn's replies and
+// AcceptorsChanged calls on the device.  Format MPXL (include/mpx.h).
+struct LearnPlan {
+    uint32_t node;
+    uint64_t id, created, kind, src;
+    uint8_t facc;
+    uint32_t end = NONE32;
+    std::vector<uint64_t> ev_a, ev_m;
+};
+
+static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnPlan> &out)
+{
+    const HostTrace &h = e->ht;
+    const uint32_t N = e->cfg.num_nodes;
+    const auto &ep = e->epochs;
+    std::unordered_map<uint32_t, uint64_t> chosen_at;          // accept quorum message -> accept id
+    for (size_t j = 0; j < h.b_msg.size(); ++j)
+        if (r.b_chosen[j] != NONE32 && h.b_msg[j] != NONE32) chosen_at[r.b_chosen[j]] = h.m_aux[h.b_msg[j]];
+    for (uint32_t n = 0; n < N; ++n) {
+        uint32_t ei = 0;
+        bool prop = (ep[0].proposer_mask >> n) & 1, preparing = false, learned_any = false;
+        uint64_t lid = 0, amask = ep[0].acceptor_mask;
+        std::vector<size_t> live;                                  // the incarnation's open learns
+        uint64_t K = 0;                                            // the last non-marker record
+        bool idle = false;
+        auto create = [&](uint64_t at, uint64_t kind, uint64_t src, bool facc) {
+            LearnPlan p;
+            p.node = n; p.id = ++lid; p.created = at; p.kind = kind; p.src = src; p.facc = facc;
+            live.push_back(out.size());
+            out.push_back(std::move(p));
+        };
+        auto drop_all = [&](uint64_t at) {
+            for (size_t x : live) out[x].end = (uint32_t)at;
+            live.clear();
+        };
+        auto acc_changed = [&](uint64_t at, uint32_t who, bool add) {     // AcceptorsChanged (:1504-1549)
+            for (size_t x : live)
+                if (out[x].facc) {
+                    out[x].ev_a.push_back(at << 32 | (uint64_t)LEV_ACC << 24 | (uint64_t)add << 23 | who);
+                    out[x].ev_m.push_back(amask);
+                }
+            preparing = true;                                      // RestartPrepare / AcceptRejected
+        };
+        auto learners_changed = [&](uint64_t at) {                 // LearnersChanged (:1472-1502)
+            drop_all(at);
+            if (!preparing) create(at, 2, 0, true);
+        };
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
+            const uint8_t t = h.m_type[g];
+            const uint64_t k = seq_of(h, n, g);
+            if (k >= NONE32) return MPX_E_RANGE;
+            if (t != MPX_MSG_E_EPOCH) {
+                K = k;
+                if (idle) { preparing = false; idle = false; }     // after the marker run (below)
+            }
+            if (t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM)) {
+                preparing = false;                                 // OnPrepareReply's quorum (:1171-1307)
+                if (learned_any) create(k, 1, 0, true);
+            } else if (t == MPX_MSG_ACCEPT_REPLY) {
+                auto it = chosen_at.find((uint32_t)g);
+                if (it != chosen_at.end()) create(k, 0, it->second, false);   // OnAcceptReply (:1327-1342)
+            } else if (t == MPX_MSG_COMMIT_REPLY) {                // LEARN_REPLY -> OnLearnReply
+                if (!prop) continue;
+                if (h.m_src[g] >= 64) return MPX_E_RANGE;
+                for (size_t x : live)
+                    if (out[x].id == h.m_aux[g]) {
+                        out[x].ev_a.push_back(k << 32 | (uint64_t)LEV_REPLY << 24 |
+                                              (uint64_t)__builtin_popcountll(ep[ei].learner_mask) << 8 | h.m_src[g]);
+                        out[x].ev_m.push_back(amask);
+                    }
+            } else if (t == MPX_MSG_P_START) {
+                if (prop) preparing = true;
+            } else if (t == MPX_MSG_COMMIT) {                      // LEARN (Learner::OnLearn, :1029-1060)
+                if (h.m_cnt[g]) learned_any = true;
+            } else if (t == MPX_MSG_E_EPOCH) {
+                const uint32_t ej = h.m_ver[g];
+                if (ej >= ep.size()) return MPX_E_DECODE;
+                const mpx_epoch &o = ep[ei], &x = ep[ej];
+                const bool was = (o.proposer_mask >> n) & 1, now = (x.proposer_mask >> n) & 1;
+                const uint64_t gl = x.learner_mask & ~o.learner_mask, ll = o.learner_mask & ~x.learner_mask;
+                const uint64_t ga = x.acceptor_mask & ~o.acceptor_mask, la = o.acceptor_mask & ~x.acceptor_mask;
+                if ((gl | ga | (now && !was)) && (ll | la | (was && !now))) return MPX_E_STATE;   // not one change list
+                for (uint64_t m = gl; m; m &= m - 1) if (prop) learners_changed(K);
+                if (!was && now) { prop = true; lid = 0; live.clear(); preparing = false; }    // a new Proposer
+                for (uint64_t m = ga; m; m &= m - 1) {
+                    amask |= m & (~m + 1);
+                    if (prop) acc_changed(K, (uint32_t)__builtin_ctzll(m), true);
+                }
+                for (uint64_t m = la; m; m &= m - 1) {
+                    amask &= ~(m & (~m + 1));
+                    if (prop) acc_changed(K, (uint32_t)__builtin_ctzll(m), false);
+                }
+                if (was && !now) { drop_all(K); prop = false; }    // the Proposer deleted (:1916-1942)
+                for (uint64_t m = ll; m; m &= m - 1) if (prop) learners_changed(K);
+                amask = x.acceptor_mask;
+                // the engine model (include/mpx.h): a proposer created, or whose acceptor set
+                // changed, is idle until its next P_START — once every change of the LEARN
+                // has run (all of them happen inside it), i.e. after the marker run
+                if (now && (!was || o.acceptor_mask != x.acceptor_mask)) idle = true;
+                ei = ej;
+            }
+        }
+    }
+    return MPX_OK;
+}
+
+extern "C" int mpx_read_learns(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->cfg.semantics != MPX_SEM_MEMBER || !e->whole) return MPX_E_STATE;
+    Results r;
+    TRY(fetch_results(e, r));
+    std::vector<LearnPlan> lp;
+    TRY(learn_plan(e, r, lp));
+    const uint32_t L = (uint32_t)lp.size();
+    std::vector<uint32_t> applied, retired, ended;
+    std::vector<uint64_t> mask;
+    if (L) {
+        std::vector<uint64_t> ev_off(1, 0), ev_a, ev_m;
+        std::vector<uint8_t> facc;
+        std::vector<uint32_t> end;
+        for (auto &p : lp) {
+            ev_a.insert(ev_a.end(), p.ev_a.begin(), p.ev_a.end());
+            ev_m.insert(ev_m.end(), p.ev_m.begin(), p.ev_m.end());
+            ev_off.push_back(ev_a.size());
+            facc.push_back(p.facc);
+            end.push_back(p.end);
+        }
+        if (ev_a.empty()) { ev_a.push_back(0); ev_m.push_back(0); }
+        hipStream_t s = e->stream;
+        DevBuf d_off, d_a, d_m, d_facc, d_end, d_app, d_ret, d_endo, d_mask;
+        TRY(upload(d_off, ev_off, s)); TRY(upload(d_a, ev_a, s)); TRY(upload(d_m, ev_m, s));
+        TRY(upload(d_facc, facc, s)); TRY(upload(d_end, end, s));
+        TRY(d_app.alloc(4ull * L)); TRY(d_ret.alloc(4ull * L)); TRY(d_endo.alloc(4ull * L)); TRY(d_mask.alloc(8ull * L));
+        LearnArgs a{L, d_off.as<uint64_t>(), d_a.as<uint64_t>(), d_m.as<uint64_t>(), d_facc.as<uint8_t>(),
+                    d_end.as<uint32_t>(), d_app.as<uint32_t>(), d_ret.as<uint32_t>(), d_endo.as<uint32_t>(),
+                    d_mask.as<unsigned long long>()};
+        if (launch_learns(e->view, s, a) != 0) return MPX_E_HIP;
+        HTRY(hipStreamSynchronize(s));
+        TRY(d2h(applied, d_app, L)); TRY(d2h(retired, d_ret, L)); TRY(d2h(ended, d_endo, L)); TRY(d2h(mask, d_mask, L));
+    }
+    const uint32_t N = e->cfg.num_nodes;
+    std::vector<uint64_t> per(N, 0);
+    for (auto &p : lp) per[p.node]++;
+    std::string d;
+    d.append("MPXL", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, N);
+    auto seq = [](uint32_t x) -> uint64_t { return x == NONE32 ? ~0ull : x; };
+    for (uint32_t n = 0; n < N; ++n) {
+        app<uint64_t>(d, per[n]);
+        for (size_t l = 0; l < lp.size(); ++l) {
+            if (lp[l].node != n) continue;
+            app<uint64_t>(d, lp[l].id); app<uint64_t>(d, lp[l].created); app<uint64_t>(d, lp[l].kind);
+            app<uint64_t>(d, lp[l].src); app<uint64_t>(d, seq(applied[l])); app<uint64_t>(d, seq(retired[l]));
+            app<uint64_t>(d, seq(ended[l])); app<uint64_t>(d, mask[l]);
+        }
+    }
     return put_bytes(d, out, size);
 }
 

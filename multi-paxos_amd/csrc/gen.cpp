@@ -18,14 +18,17 @@ void TraceWriter::begin(uint32_t N, uint32_t semantics, uint64_t M, const std::v
 {
     out.clear();
     out.append("MPXT", 4);
-    app<uint32_t>(out, 1);
+    app<uint32_t>(out, epochs.empty() ? 1 : 2);     // version 2: 32-byte epoch entries (learner_mask)
     app<uint32_t>(out, N);
     app<uint32_t>(out, semantics);
     app<uint64_t>(out, M);
     app<uint32_t>(out, (uint32_t)epochs.size());
     app<uint32_t>(out, 0);
     app<uint64_t>(out, 0);
-    for (auto &e : epochs) { app<uint32_t>(out, e.version); app<uint32_t>(out, e.flags); app<uint64_t>(out, e.acceptor_mask); app<uint64_t>(out, e.proposer_mask); }
+    for (auto &e : epochs) {
+        app<uint32_t>(out, e.version); app<uint32_t>(out, e.flags);
+        app<uint64_t>(out, e.acceptor_mask); app<uint64_t>(out, e.proposer_mask); app<uint64_t>(out, e.learner_mask);
+    }
 }
 
 void TraceWriter::node(const std::vector<std::string> &msgs)

@@ -267,7 +267,7 @@ int gen_member(const mpx_gen_params &p, std::string &out)
     g.ep.resize(g.E);
     g.changes.resize(g.E);
     uint64_t set = 1;
-    g.ep[0] = mpx_epoch{0, 0, 1, 1};
+    g.ep[0] = mpx_epoch{0, 0, 1, 1, 1};
     for (uint32_t c = 1; c < g.E; ++c) {
         if (c < U) {
             g.changes[c] = {{c, ADD_LEARNER}, {c, LEARNER_TO_PROPOSER}, {c, PROPOSER_TO_ACCEPTOR}};
@@ -277,7 +277,7 @@ int gen_member(const mpx_gen_params &p, std::string &out)
             g.changes[c] = {{j, ACCEPTOR_TO_PROPOSER}, {j, PROPOSER_TO_LEARNER}, {j, DEL_LEARNER}};
             set &= ~(1ull << j);
         }
-        g.ep[c] = mpx_epoch{c, 0, set, set};
+        g.ep[c] = mpx_epoch{c, 0, set, set, set};   // (the change lists move all three roles at once)
     }
     // instance Values: the epoch ranges, membership Value last in each range
     std::vector<uint64_t> start(g.E + 1);

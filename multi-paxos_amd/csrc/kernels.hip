@@ -3138,6 +3138,53 @@ int launch_commits(const DevView &v, void *stream, const CommitArgs &a)
     return (int)hipGetLastError();
 }
 
+// ------------------------------------------------- learn reliability --
+// member Proposer (member/paxos.cpp:1345-1381, 1504-1533), one lane per
+// LearningValues, over its events in processing order: a LEARN_REPLY adds its learner to
+// learned_ and, while the learn is in learning_values_for_acceptors_, an acceptor of the
+// node's epoch to that set; |set| >= |acceptors|/2+1 runs Applied and drops the entry
+// (:1363-1370); |learned_| == |learners_| retires the learn (:1373-1380).  An
+// AcceptorsChanged call removes a deleted acceptor from the set or adds an added one that
+// had replied, then checks the quorum of the new set (:1507-1533).  A learn neither
+// retired nor open at the end was dropped at `end` (LearnersChanged / the proposer deleted).
+__global__ __launch_bounds__(256) void k_learns(LearnArgs a)
+{
+    const uint64_t l = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (l >= a.L) return;
+    bool facc = a.facc[l] != 0;
+    unsigned long long learned = 0, acc = 0;
+    uint32_t applied = NONE32, retired = NONE32;
+    for (uint64_t k = a.ev_off[l]; k < a.ev_off[l + 1]; ++k) {
+        const uint64_t w = a.ev_a[k];
+        const uint64_t am = a.ev_m[k];
+        const uint32_t pos = (uint32_t)(w >> 32), who = (uint32_t)w & 63;
+        const uint32_t quorum = (uint32_t)__popcll(am) / 2 + 1;
+        if (((w >> 24) & 0xFF) == LEV_REPLY) {
+            learned |= 1ull << who;                                        // :1353
+            if (facc && ((am >> who) & 1)) {                               // :1355-1358
+                acc |= 1ull << who;
+                if ((uint32_t)__popcll(acc) >= quorum) { applied = pos; facc = false; }   // :1363-1370
+            }
+            if ((uint32_t)__popcll(learned) == ((w >> 8) & 0x7F)) { retired = pos; break; }   // :1373-1380
+        } else if (facc) {
+            if ((w >> 23) & 1) { if ((learned >> who) & 1) acc |= 1ull << who; }          // :1518-1519
+            else acc &= ~(1ull << who);                                                      // :1511-1512
+            if ((uint32_t)__popcll(acc) >= quorum) { applied = pos; facc = false; }          // :1521-1528
+        }
+    }
+    a.applied[l] = applied;
+    a.retired[l] = retired;
+    a.ended[l] = retired == NONE32 ? a.end[l] : NONE32;
+    a.mask[l] = learned;
+}
+
+int launch_learns(const DevView &, void *stream, const LearnArgs &a)
+{
+    if (!a.L) return 0;
+    hipLaunchKernelGGL(k_learns, dim3(cdiv(a.L, 256)), dim3(256), 0, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+}
+
 int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, uint64_t count, uint64_t *out)
 {
     if (!count) return 0;

@@ -40,7 +40,10 @@ namespace mpx {
 
 constexpr uint32_t BSH = 8;                  // bucket = 256 instances
 constexpr uint32_t BS = 1u << BSH;
-constexpr uint32_t SCAN_CHUNK = 2048;        // header-scan chunk (messages): 8 per thread
+#ifndef MPX_SCAN_CHUNK
+#define MPX_SCAN_CHUNK 2048                     // (a build knob for A/B: make EXTRA=-DMPX_SCAN_CHUNK=1024)
+#endif
+constexpr uint32_t SCAN_CHUNK = MPX_SCAN_CHUNK;        // header-scan chunk (messages): 8 per thread
 constexpr uint32_t PROP_CHUNK = 512;         // promise-quorum chunk (pl records): 8 windows of 64 (C3 2^24 scan
                                              // phase 0.112 ms vs 0.128 at 2048, 0.134 at 256)
 // k_scan_apply re-reduces a node's earlier chunk aggregates inline (O(chunks^2)
@@ -435,6 +438,23 @@ struct CommitArgs {
     unsigned long long *mask;
 };
 int launch_commits(const DevView &v, void *stream, const CommitArgs &a);
+// Learn reliability (member; mpx_read_learns, kernels.hip k_learns): per
+// learn its events in processing order — LEARN_REPLYs and the AcceptorsChanged calls of
+// its proposer while it is open — as ev_a = pos << 32 | kind << 24 | add << 23 |
+// lcount << 8 | node (kind 0 reply: node = learner, lcount = |learners_|; kind 1
+// AcceptorsChanged: add, node), ev_m = the node's acceptor mask at the event (after the
+// change); facc: the learn has a learning_values_for_acceptors_ entry; end: the record
+// that drops it (NONE32: none)
+enum : uint32_t { LEV_REPLY = 0, LEV_ACC = 1 };
+struct LearnArgs {
+    uint32_t L;
+    const uint64_t *ev_off, *ev_a, *ev_m;
+    const uint8_t *facc;
+    const uint32_t *end;
+    uint32_t *applied, *retired, *ended;
+    unsigned long long *mask;
+};
+int launch_learns(const DevView &v, void *stream, const LearnArgs &a);
 // f_off / cf_off: host-computed prefix counts (per pair, per bucket), read by the generator
 int launch_gen_clean(void *stream, uint32_t N, uint64_t K, uint64_t k0, uint64_t sb, uint64_t se,
                      uint64_t G0, uint64_t G1, uint64_t ballot, uint64_t B, uint32_t NB,

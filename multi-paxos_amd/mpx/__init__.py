@@ -14,9 +14,11 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libmpx.so")
+if os.environ.get("MPX_LIB_VARIANT"):         # A/B builds of the same sources (tools/ab_*.sh)
+    LIB_PATH = os.path.join(os.path.dirname(HERE), "lib_" + os.environ["MPX_LIB_VARIANT"], "libmpx.so")
 INCLUDE_H = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "mpx.h")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 SEM_MULTI, SEM_MEMBER = 0, 1
 FLAG_INCREMENTAL = 1            # mpx_config.flags: each mpx_run applies one window (include/mpx.h)
 GEN_CLEAN, GEN_FAULTY, GEN_MEMBER = 0, 1, 2
@@ -35,7 +37,7 @@ class MpxError(RuntimeError):
 
 class Epoch(ctypes.Structure):
     _fields_ = [("version", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("acceptor_mask", ctypes.c_uint64),
-                ("proposer_mask", ctypes.c_uint64)]
+                ("proposer_mask", ctypes.c_uint64), ("learner_mask", ctypes.c_uint64)]
 
 
 class Config(ctypes.Structure):
@@ -117,6 +119,7 @@ def lib():
             "mpx_dump_result": [vp, P(u8p), u64p],
             "mpx_read_decisions": [vp, P(u8p), u64p],
             "mpx_read_commits": [vp, P(u8p), u64p],
+            "mpx_read_learns": [vp, P(u8p), u64p],
             "mpx_decisions_bounds": [vp, u64p, ctypes.c_uint64, u64p],
             "mpx_read_decisions_part": [vp, u64p, ctypes.c_uint64, P(u8p), u64p],
             "mpx_decisions_combine": [P(u8p), u64p, ctypes.c_uint32, P(u8p), u64p],
@@ -187,8 +190,21 @@ def generate_trace(kind=GEN_CLEAN, num_nodes=5, num_instances=1 << 10, seed=0, b
 def trace_header(trace):
     import struct
     assert trace[:4] == b"MPXT"
-    _, n, sem, m = struct.unpack_from("<IIIQ", trace, 4)
-    return {"num_nodes": n, "semantics": sem, "num_instances": m}
+    ver, n, sem, m = struct.unpack_from("<IIIQ", trace, 4)
+    return {"num_nodes": n, "semantics": sem, "num_instances": m, "version": ver}
+
+
+def trace_epochs(trace):
+    """The container's epoch table: [(version, acceptor_mask, proposer_mask, learner_mask)]
+    (version-1 containers: 24-byte entries, learner_mask = proposer_mask)."""
+    import struct
+    ver, ne = struct.unpack_from("<I", trace, 4)[0], struct.unpack_from("<I", trace, 24)[0]
+    esz = 24 if ver == 1 else 32
+    out = []
+    for i in range(ne):
+        v, a, p = struct.unpack_from("<IxxxxQQ", trace, 40 + esz * i)
+        out.append((v, a, p, struct.unpack_from("<Q", trace, 40 + esz * i + 24)[0] if esz == 32 else p))
+    return out
 
 
 class Engine:
@@ -198,7 +214,9 @@ class Engine:
         L = lib()
         if shard_end is None:
             raise ValueError("shard_end required")
-        self._epochs = (Epoch * max(len(epochs), 1))(*[Epoch(v, 0, a, p) for v, a, p in epochs])
+        # epochs: (version, acceptor_mask, proposer_mask[, learner_mask = proposer_mask])
+        self._epochs = (Epoch * max(len(epochs), 1))(*[Epoch(x[0], 0, x[1], x[2], x[3] if len(x) > 3 else x[2])
+                                                        for x in epochs])
         cfg = Config(ABI_VERSION, num_nodes, semantics, device, shard_begin, shard_end,
                      len(epochs), flags, self._epochs if epochs else None)
         h = ctypes.c_void_p()
@@ -352,6 +370,13 @@ class Engine:
         out = ctypes.POINTER(ctypes.c_uint8)()
         size = ctypes.c_uint64()
         _ck("mpx_read_commits", lib().mpx_read_commits(self.h, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
+    def learns(self):
+        """MPXL bytes: every member LearningValues and what became of it (mpx_read_learns)."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_read_learns", lib().mpx_read_learns(self.h, ctypes.byref(out), ctypes.byref(size)))
         return _take(out, size.value)
 
     def commit_points(self):

@@ -1441,16 +1441,17 @@ static int run_shard_ex(const u8 *trace, u64 size, u64 sb, u64 se, u8 **out, u64
     c.M = rd64(trace + 16);
     u32 ne = rd32(trace + 24);
     if (c.N == 0 || c.N > 64 || c.sem > 1) return -1;
-    if (c.sem == 1 && (ne == 0 || size < HDR + (u64)ne * 24)) return E_DECODE;
-    size_t pos = HDR + (size_t)ne * 24;
+    const size_t esz = rd32(trace + 4) == 1 ? 24 : 32;     /* container version 2: + learner_mask */
+    if (c.sem == 1 && (ne == 0 || size < HDR + (u64)ne * esz)) return E_DECODE;
+    size_t pos = HDR + (size_t)ne * esz;
     c.nodes = (node_t *)calloc(c.N, sizeof(node_t));
     c.ne = ne;
     c.ep = (epoch_t *)calloc(ne ? ne : 1, sizeof(epoch_t));
     if (!c.nodes || !c.ep) { free(c.nodes); free(c.ep); return E_NOMEM; }
     for (u32 e = 0; e < ne; ++e) {
-        c.ep[e].version = rd32(trace + HDR + 24 * e);
-        c.ep[e].amask = rd64(trace + HDR + 24 * e + 8);
-        c.ep[e].pmask = rd64(trace + HDR + 24 * e + 16);
+        c.ep[e].version = rd32(trace + HDR + esz * e);
+        c.ep[e].amask = rd64(trace + HDR + esz * e + 8);
+        c.ep[e].pmask = rd64(trace + HDR + esz * e + 16);
     }
     /* node streams: located sequentially, processed in parallel — a node's
      * handlers touch only its own state (the reference runs one paxos thread

@@ -24,7 +24,15 @@
 // model, include/mpx.h), and batches / learns its own decision code creates are
 // discarded (their sends are proposer broadcasts, not in-scope replies).
 //
-// Output: the canonical MPXR result.
+// Output: the canonical MPXR result; mpxref_member_learns: the
+// proposers' learn reliability bookkeeping as MPXL (include/mpx.h
+// mpx_read_learns): every LearningValues a Proposer created (learning_id_, :1334-1337,
+// 1299-1307, 1487-1491), the record where Applied ran for it (learning_values_for_
+// acceptors_ reached |acceptors|/2+1, :1355-1370,1507-1533), where it retired (every
+// learner replied, :1373-1380) or was dropped (LearnersChanged, :1472-1502, or the
+// Proposer deleted, :1916-1942), and its learned_ set.  The reference's own objects are
+// read after every record; Applied is attributed to its learn by tagging the cb_ of the
+// values of every learn in learning_values_for_acceptors_ around the record.
 
 #include <string.h>
 #include <stdarg.h>
@@ -75,6 +83,14 @@ struct FrozenClock : public Clock {
 
 struct Sent { uint32_t dst; std::string bytes; };
 
+// Callback::Applied capture (the tags name the learn, see above)
+struct CapCb : public paxos::Callback {
+    std::vector<std::string> applied;
+    void Applied(Thread *, const std::string &cb, const std::string *) { applied.push_back(cb); }
+};
+
+struct LearnRec { u64 id, created, kind, src, applied, retired, ended, learned; };
+
 struct CapNet : public paxos::NetWork {
     std::vector<Sent> *out;
     void Send(Thread *, paxos::NodeID node, const std::string &msg) { out->push_back(Sent{node, msg}); }
@@ -90,7 +106,7 @@ template <typename T> void put(std::string &b, T v) { b.append((const char *)&v,
 uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
 u64 rd64(const uint8_t *p) { u64 v; memcpy(&v, p, 8); return v; }
 
-struct Epoch { uint32_t version; u64 amask, pmask; };
+struct Epoch { uint32_t version; u64 amask, pmask, lmask; };
 
 typedef std::map<paxos::InstanceID, paxos::ProposalValue> PVMap;
 
@@ -107,6 +123,8 @@ struct Node {
     std::map<paxos::InstanceID, paxos::ValueID> own_iids;
     uint32_t epoch = 0;
     u64 P = 0, A = 0, L = 0;
+    std::vector<LearnRec> lrec;                      // learn reliability (MPXL), creation order
+    std::map<paxos::LearningID, size_t> llive;       // the current Proposer's open learns
 };
 
 DThread *g_thread;
@@ -123,7 +141,7 @@ u64 set_mask(const std::set<paxos::NodeID> &s)
 bool consistent(const Node &n, uint32_t id, const Epoch &e)
 {
     const paxos::NodeImpl *p = n.impl;
-    return p->version_ == e.version && set_mask(p->acceptors_) == e.amask &&
+    return p->version_ == e.version && set_mask(p->acceptors_) == e.amask && set_mask(p->learners_) == e.lmask &&
            (p->acceptor_ != NULL) == (bool)((e.amask >> id) & 1) &&
            (p->proposer_ != NULL) == (bool)((e.pmask >> id) & 1);
 }
@@ -173,17 +191,19 @@ int parse_pvalues(Logger *lg, const uint8_t *buf, uint32_t len, PVMap *out)
 
 }  // namespace
 
-extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size,
-                                 uint64_t *stats)
+static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size,
+                      uint64_t *stats, uint8_t **lout, uint64_t *lsize)
 {
     if (size < 40 || memcmp(trace, "MPXT", 4)) return -4;
     uint32_t N = rd32(trace + 8), sem = rd32(trace + 12), ne = rd32(trace + 24);
     if (sem != 1 || N == 0 || N > 64 || ne == 0) return -1;
     std::vector<Epoch> ep(ne);
+    const size_t esz = rd32(trace + 4) == 1 ? 24 : 32;    // container version 2: + learner_mask
     for (uint32_t e = 0; e < ne; ++e) {
-        ep[e].version = rd32(trace + 40 + 24 * e);
-        ep[e].amask = rd64(trace + 48 + 24 * e);
-        ep[e].pmask = rd64(trace + 56 + 24 * e);
+        ep[e].version = rd32(trace + 40 + esz * e);
+        ep[e].amask = rd64(trace + 48 + esz * e);
+        ep[e].pmask = rd64(trace + 56 + esz * e);
+        ep[e].lmask = esz == 32 ? rd64(trace + 64 + esz * e) : ep[e].pmask;
     }
     // the reference starts every node in {first} (NodeImpl::Loop, :738-747)
     if (ep[0].amask == 0 || (ep[0].amask & (ep[0].amask - 1)) || ep[0].pmask != ep[0].amask || ep[0].version != 0)
@@ -197,12 +217,12 @@ extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **
     Logger &logger = *new Logger(new DLock, &clock, 7);   // above CRITICAL: silent (ASSERT still crashes)
     Timer &timer = *new Timer(&logger);
     Rand &rand = *new Rand(0);
-    paxos::Callback &cb = *new paxos::Callback;
+    CapCb &cb = *new CapCb;
     paxos::Config cfg;
 
     std::vector<const uint8_t *> offs(N), bytes(N);
     std::vector<u64> cnt(N);
-    size_t pos = 40 + (size_t)ne * 24;
+    size_t pos = 40 + (size_t)ne * esz;
     for (uint32_t i = 0; i < N; ++i) {
         if (pos + 16 > size) return -4;
         cnt[i] = rd64(trace + pos);
@@ -264,6 +284,22 @@ extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **
             if (type != 18 && !consistent(n, i, ep[n.epoch])) return -11;   // an E_EPOCH marker is missing
             size_t before = n.sends.size();
             paxos::Proposer *pr = ni->proposer_;
+            // learn bookkeeping: tag the learns Applied may run for, note the id counter
+            const paxos::LearningID lid0 = pr ? pr->learning_id_ : 0;
+            std::map<paxos::InstanceID, std::string> orig_cb;
+            std::map<paxos::LearningID, u64> prev_mask;
+            if (pr) {
+                for (auto &f : pr->learning_values_for_acceptors_) {
+                    auto it = pr->learning_values_.find(f.first);
+                    if (it == pr->learning_values_.end()) continue;
+                    for (auto &v : it->second->values_) {
+                        orig_cb[v.first] = v.second.value_.cb_;
+                        v.second.value_.cb_ = "\x01" + std::to_string(f.first);
+                    }
+                }
+                for (auto &l : pr->learning_values_) prev_mask[l.first] = set_mask(l.second->learned_);
+            }
+            cb.applied.clear();
             std::set<paxos::AcceptingID> before_b;
             if (pr) for (auto &e : pr->accepting_values_) before_b.insert(e.first);
             switch (type) {
@@ -335,7 +371,8 @@ extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **
                 break;
             }
             case 6:
-                break;     // OnLearnReply: learn-retry bookkeeping, out of scope
+                if (pr) pr->OnLearnReply((const paxos::LearnReplyMsg *)m);
+                break;
             case 16:       // P_START
                 if (pr) {
                     make_idle(pr);
@@ -365,6 +402,46 @@ extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **
                 break;
             }
             default: return -4;
+            }
+            {
+                paxos::Proposer *p1 = ni->proposer_;
+                if (pr && p1 == pr)                    // untag (learns built from tagged copies too)
+                    for (auto &l : pr->learning_values_)
+                        for (auto &v : l.second->values_)
+                            if (!v.second.value_.cb_.empty() && v.second.value_.cb_[0] == '\x01')
+                                v.second.value_.cb_ = orig_cb[v.first];
+                for (auto &a : cb.applied) {
+                    if (a.empty() || a[0] != '\x01') continue;
+                    auto it = n.llive.find(std::stoull(a.substr(1)));
+                    if (it != n.llive.end() && n.lrec[it->second].applied == ~0ull) n.lrec[it->second].applied = k;
+                }
+                if (pr && p1 != pr) {                  // the Proposer was deleted: its open learns end
+                    for (auto &l : n.llive) n.lrec[l.second].ended = k;
+                    n.llive.clear();
+                }
+                if (p1) {
+                    const paxos::LearningID base = p1 == pr ? lid0 : 0;
+                    const u64 kind = type == 4 ? 0 : type == 1 ? 1 : 2;
+                    const u64 src = type == 4 ? ((const paxos::AcceptReplyMsg *)m)->accept_ : 0;
+                    for (paxos::LearningID id = base + 1; id <= p1->learning_id_; ++id) {
+                        n.llive[id] = n.lrec.size();
+                        n.lrec.push_back(LearnRec{id, k, kind, src, ~0ull, ~0ull, ~0ull, 0});
+                    }
+                    for (auto it = n.llive.begin(); it != n.llive.end();) {
+                        LearnRec &r = n.lrec[it->second];
+                        auto lv = p1->learning_values_.find(it->first);
+                        if (lv != p1->learning_values_.end()) {
+                            r.learned = set_mask(lv->second->learned_);
+                            ++it;
+                            continue;
+                        }
+                        if (type == 6) {                   // OnLearnReply: every learner replied
+                            r.retired = k;
+                            r.learned = prev_mask[it->first] | (1ull << ((const paxos::LearnReplyMsg *)m)->learner_);
+                        } else r.ended = k;                // LearnersChanged dropped it
+                        it = n.llive.erase(it);
+                    }
+                }
             }
             // keep only the acceptor / learner replies (types 1,2,4,6)
             std::vector<Sent> keep(n.sends.begin(), n.sends.begin() + before);
@@ -418,10 +495,39 @@ extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **
     put<u64>(r, chosen.size());
     for (auto &e : chosen) { put<u64>(r, e.first); put<u64>(r, e.second); }
     if (stats) { stats[0] = chosen.size(); stats[1] = P; stats[2] = A; stats[3] = L; }
-    *out = (uint8_t *)malloc(r.size());
-    if (!*out) return -2;
-    memcpy(*out, r.data(), r.size());
-    *out_size = r.size();
+    if (out) {
+        *out = (uint8_t *)malloc(r.size());
+        if (!*out) return -2;
+        memcpy(*out, r.data(), r.size());
+        *out_size = r.size();
+    }
+    if (lout) {
+        std::string l;
+        l.append("MPXL", 4);
+        put<uint32_t>(l, 1); put<uint32_t>(l, N);
+        for (uint32_t i = 0; i < N; ++i) {
+            put<u64>(l, ns[i].lrec.size());
+            for (auto &x : ns[i].lrec) {
+                put<u64>(l, x.id); put<u64>(l, x.created); put<u64>(l, x.kind); put<u64>(l, x.src);
+                put<u64>(l, x.applied); put<u64>(l, x.retired); put<u64>(l, x.ended); put<u64>(l, x.learned);
+            }
+        }
+        *lout = (uint8_t *)malloc(l.size());
+        if (!*lout) return -2;
+        memcpy(*lout, l.data(), l.size());
+        *lsize = l.size();
+    }
     // NodeImpl objects are leaked on purpose (their dtors expect a joined thread).
     return 0;
+}
+
+extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size,
+                                 uint64_t *stats)
+{
+    return member_run(trace, size, out, out_size, stats, NULL, NULL);
+}
+
+extern "C" int mpxref_member_learns(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)
+{
+    return member_run(trace, size, NULL, NULL, NULL, out, out_size);
 }

@@ -178,6 +178,28 @@ def member_traces():
         m_learn(0, 2, [(5, B1, mvalue(0, 0, noop=True)), (4, B1, v(4))]),   # noop is not executed
     ]
     t["mm_catchup"] = m.trace()
+
+    # 8. learn reliability (f4): a promise quorum re-learns what was learned (:1299-1307), an
+    #    accept quorum learns its batch (:1334-1337); Applied at |acceptors|/2+1 replies and
+    #    retirement at |learners_| (:1345-1381); AddLearner / DelLearner alone change learners_
+    #    only (LearnersChanged, :1472-1502: drop every open learn, re-learn all)
+    m = Member(4, 2, extra_epochs=[(1, mask(0, 1), mask(0, 1), mask(0, 1, 3)), (1, mask(0, 1), mask(0, 1), mask(0, 1))])
+    m.bootstrap([0])
+    ents = [(1, B1, v(1)), (2, B1, v(2))]
+    al3 = mvalue(0, 20, cb="al3", changes=[(3, ADD_LEARNER)])
+    dl3 = mvalue(0, 21, cb="dl3", changes=[(3, DEL_LEARNER)])
+    m.streams[0] += [
+        # (learn 1: AddAcceptor(1)'s ADD_LEARNER while the bootstrap LEARN applies)
+        p_start(B1), m_prepare_reply(0, B1), m_prepare_reply(1, B1),   # quorum: learn 2 (learned boot value)
+        m_p_batch(5, ents), m_accept_reply(0, 5), m_accept_reply(1, 5),   # chosen: learn 3
+        m_learn_reply(0, 2), m_learn_reply(1, 2),                     # learn 2 applied, retired (2 learners)
+        m_learn(0, 2, ents), m_learn_reply(0, 3),
+        m_learn(0, 3, [(3, B1, al3)]), e_epoch(2),                    # learners {0,1,3}: drops 3, learn 4
+        m_learn_reply(0, 4), m_learn_reply(1, 4), m_learn_reply(2, 4), m_learn_reply(3, 4),   # 2: not a learner
+        m_learn(0, 4, [(4, B1, dl3)]), e_epoch(3),                    # learners {0,1}: learn 5
+        m_learn_reply(1, 5), m_learn_reply(3, 1), m_learn_reply(0, 5),
+    ]
+    t["mm_learners"] = m.trace()
     return t
 
 

@@ -86,14 +86,16 @@ def p_propose(payload):
 
 def container(streams, num_instances=0, semantics=0, epochs=()):
     """streams: list (per node) of lists of message bytes, in processing order.
-    epochs (member): (version, acceptor_mask, proposer_mask) per epoch."""
+    epochs (member): (version, acceptor_mask, proposer_mask[, learner_mask]) per epoch; a
+    member container is version 2 (32-byte entries, learner_mask defaults to proposer_mask)."""
     out = bytearray(b"MPXT")
-    out += struct.pack("<III", 1, len(streams), semantics)
+    out += struct.pack("<III", 2 if epochs else 1, len(streams), semantics)
     out += struct.pack("<QII", num_instances, len(epochs), 0)
     out += struct.pack("<Q", 0)
     assert len(out) == 40
-    for ver, amask, pmask in epochs:
-        out += struct.pack("<IIQQ", ver, 0, amask, pmask)
+    for e in epochs:
+        ver, amask, pmask = e[:3]
+        out += struct.pack("<IIQQQ", ver, 0, amask, pmask, e[3] if len(e) > 3 else pmask)
     for msgs in streams:
         offs = [0]
         for m in msgs:

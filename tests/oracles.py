@@ -144,6 +144,13 @@ def ref_commits(trace):
     return _blob_call(REF_SO, "mpxref_commits", trace)
 
 
+def ref_learns(trace):
+    """The reference's own member LearningValues bookkeeping (MPXL): creation at accept /
+    promise quorums and LearnersChanged, Applied, OnLearnReply retirement, drops
+    (oracle/ref_member_driver.cpp mpxref_member_learns)."""
+    return _blob_call(REF_MEMBER_SO, "mpxref_member_learns", trace)
+
+
 def oracle_commits(trace):
     """The oracle's restatement of the same bookkeeping (mpxo_commits)."""
     return _blob_call(ORACLE_SO, "mpxo_commits", trace)

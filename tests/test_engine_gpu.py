@@ -659,12 +659,11 @@ def test_decisions_refused_for_shards_and_member():
 
 # ---- incremental submission (multi/paxos.cpp:1714-1717) ----
 def _node_streams(trace):
-    """MPXT -> (header, epochs [(version, amask, pmask)], per-node lists of record bytes)."""
+    """MPXT -> (header, epochs [(version, amask, pmask, lmask)], per-node lists of record bytes)."""
     import struct
     hd = mpx.trace_header(trace)
-    ne = struct.unpack_from("<I", trace, 24)[0]
-    epochs = [struct.unpack_from("<IxxxxQQ", trace, 40 + 24 * i) for i in range(ne)]
-    pos = 40 + 24 * ne
+    epochs = mpx.trace_epochs(trace)
+    pos = 40 + (24 if hd["version"] == 1 else 32) * len(epochs)
     streams = []
     for _ in range(hd["num_nodes"]):
         cnt, nb = struct.unpack_from("<QQ", trace, pos)
@@ -884,6 +883,61 @@ def test_incremental_window_cost_is_per_window():
 
 # ---- commit reliability (multi/paxos.cpp:1184-1197,1416-1421,1625-1641) ----
 COMMITS = json.load(open(os.path.join(GOLD, "commits.json")))
+LEARNS = json.load(open(os.path.join(GOLD, "learns.json")))
+
+
+# ---- member learn reliability (member/paxos.cpp:1345-1381,1472-1549) ----
+@pytest.mark.parametrize("name", sorted(LEARNS))
+def test_engine_learns_match_reference(name):
+    """Every LearningValues the member proposers create (accept quorums from k_votes,
+    promise quorums from k_prop_*, LearnersChanged at the epoch markers) and what k_learns
+    makes of their LEARN_REPLYs and AcceptorsChanged calls == the reference's own
+    bookkeeping (fixture, oracle/ref_member_driver.cpp), after run and after a timed step."""
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxl")
+    with mpx.Engine.for_trace(trace) as e:
+        e.run()
+        assert e.learns() == want
+        e.step()
+        e.sync()
+        assert e.learns() == want
+
+
+@pytest.mark.parametrize("seed,m,batch", [(7, 1 << 16, 64), (8, 50000, 256)])
+def test_engine_learns_match_model_c5(seed, m, batch):
+    """C5-shaped traces beyond fixture size: the engine's learn bookkeeping == the Python
+    restatement (tests/learns_model.py, pinned to the reference's fixtures on CPU) fed by
+    the C oracle's promise quorums and chosen batches."""
+    from oracles import oracle_run
+    import learns_model
+    import mpxl
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=8, num_instances=m, seed=seed, batch=batch,
+                           drop_rate=300, dup_rate=300, max_delay=64, noop_permille=15)
+    want = learns_model.learns(t, oracle_run(t)[0])
+    assert sum(len(x) for x in mpxl.parse(want)) > 100
+    with mpx.Engine.for_trace(t) as e:
+        e.run()
+        assert e.learns() == want
+
+
+def test_learns_refused_off_member_and_on_shards():
+    """mpx_read_learns is member bookkeeping of an engine that kept every record: multi
+    semantics and a shard that left records out for another shard are refused; a shard at
+    instance 0 that kept every record (its LEARNs / batches meet it) answers as the whole."""
+    with mpx.Engine.for_trace(_read("hm_clean3", ".mpxt")) as e:
+        e.run()
+        with pytest.raises(mpx.MpxError):
+            e.learns()
+    trace = _read("mm_clean3", ".mpxt")
+    hd = mpx.trace_header(trace)
+    with mpx.Engine(hd["num_nodes"], 0, 8, semantics=hd["semantics"]) as e:
+        e.submit_trace(trace)
+        e.run()
+        assert e.learns() == _read("mm_clean3", ".mpxl")
+    with mpx.Engine(hd["num_nodes"], 3, 64, semantics=hd["semantics"]) as e:
+        e.submit_trace(trace)
+        e.run()
+        with pytest.raises(mpx.MpxError):
+            e.learns()
 
 
 @pytest.mark.parametrize("name", sorted(COMMITS))

@@ -5,8 +5,8 @@ rm -f gpurun_out/ab_shard/*.json
 run() { tag=$1; shift; env "$@" timeout -k 10 120 python bench.py --shard-only > gpurun_out/ab_shard/$tag.json 2> gpurun_out/ab_shard/$tag.err || exit 1; }
 run default X=0
 run events_every1000 MPX_EVENTS_EVERY=1000
-run headers3 MPX_KNOBS=134217728
-run chosen_on MPX_KNOBS=268435456
-run wgs8 MPX_STORE_WGS_PER_CU=8
+run store64 MPX_KNOBS=2048
+run wgs1 MPX_STORE_WGS_PER_CU=1
+run wgs4 MPX_STORE_WGS_PER_CU=4
 run default2 X=0
 for f in gpurun_out/ab_shard/*.json; do python -c "import json,sys; d=json.load(open('$f'))['scaling_projection']; print('$f', round(d['T_shard_ms']*1e3,1), {k: round(v*1e3,1) for k,v in d['phases_ms'].items()})"; done

@@ -37,9 +37,13 @@ int main(int argc, char **argv)
     const uint8_t *b = (const uint8_t *)t.data();
     const uint32_t N = rd32(b + 8), ne = rd32(b + 24);
     const uint64_t M = rd64(b + 16);
+    const size_t esz = rd32(b + 4) == 1 ? 24 : 32;      // container version 2: learner_mask
     std::vector<mpx_epoch> ep(ne);
-    if (ne) std::memcpy(ep.data(), b + 40, (size_t)ne * 24);
-    size_t pos = 40 + (size_t)ne * 24;
+    for (uint32_t k = 0; k < ne; ++k) {
+        std::memcpy(&ep[k], b + 40 + k * esz, 24);
+        ep[k].learner_mask = esz == 32 ? rd64(b + 40 + k * esz + 24) : ep[k].proposer_mask;
+    }
+    size_t pos = 40 + (size_t)ne * esz;
     std::vector<NodeStream> nodes(N);
     ValueTable vt;
     vt.member = member;
