@@ -307,17 +307,25 @@ int  mpx_last_violation(mpx_engine *eng, mpx_violation *out);
  * the CPU oracle and the reference driver also write, so parity is a
  * byte comparison.  *out is malloc'ed; free with mpx_free. */
 int  mpx_dump_result(mpx_engine *eng, uint8_t **out, uint64_t *size);
-/* Phase-2 decisions (multi semantics, an engine whose shard
- * starts at instance 0): for every promise quorum of the last run, the batch
- * OnPrepareReply builds (multi/paxos.cpp:1056-1130) for a proposer with no
- * client proposals of its own — every pre-accepted value of an instance the
- * node has not committed (:1071-1102), then a noop Value(node, ++value_id) for
- * every other uncommitted instance below the highest committed-or-adopted one
- * (:1117-1130; value ids count from 1 per node over its quorums).  Computed on
- * the device from the run's state.  Format MPXD: "MPXD" u32 1, u32 nodes; per
- * node u64 count, per quorum {u64 seq (record index in the node's stream),
- * u64 n, {u64 iid, u64 handle} * n, iid ascending}.  *out is malloc'ed; free
- * with mpx_free.  MPX_E_STATE for member semantics or a shard engine. */
+/* Phase-2 decisions (an engine whose shard starts at instance
+ * 0): for every promise quorum of the last run, the batch OnPrepareReply builds
+ * (multi/paxos.cpp:1056-1175) — every pre-accepted value of an instance the node
+ * has not committed (:1071-1102), then a noop Value(node, ++value_id) for every
+ * other uncommitted instance below the highest committed-or-adopted one
+ * (:1117-1130; value ids count from 1 per node over its quorums), then the node's
+ * own client values (P_PROPOSE records: initial proposals still unproposed, the
+ * queued ones at the next free ids, :1132-1175, with Propose :1250-1280 and the
+ * OnCommit re-propose :1519-1570 kept in order; they share the value ids).
+ * Without client values the noop fill is computed on the device from the run's
+ * state; with them (and for member) it is the proposer's sequential bookkeeping
+ * on the host over the device's quorums and merged maps.  Member semantics
+ * (member/paxos.cpp:1183-1297, an engine that kept every record): the same batch
+ * over the Proposer's unlearned ids, kept by Proposer::OnLearn (:1383-1470); a
+ * Proposer's initial proposals are the node's own Values of the trace not yet
+ * learned when it starts (what Propose would have recorded).  Format MPXD: "MPXD"
+ * u32 1, u32 nodes; per node u64 count, per quorum {u64 seq (record index in the
+ * node's stream), u64 n, {u64 iid, u64 handle} * n, iid ascending}.  *out is
+ * malloc'ed; free with mpx_free.  MPX_E_STATE for a shard engine. */
 int  mpx_read_decisions(mpx_engine *eng, uint8_t **out, uint64_t *size);
 /* Sharded phase-2 decisions (one engine per instance range, shards in rank
  * order).  The fill of each quorum reaches the highest committed-or-adopted

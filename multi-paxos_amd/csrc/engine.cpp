@@ -1489,6 +1489,127 @@ static bool has_proposals(const HostTrace &h)
     return std::find(h.m_type.begin(), h.m_type.end(), (uint8_t)MPX_MSG_P_PROPOSE) != h.m_type.end();
 }
 
+// Member semantics (member/paxos.cpp:1183-1297): the same batch over the proposer's
+// unlearned ids — Proposer::OnLearn (:1383-1470) removes a newly learned id from the
+// unlearned / unproposed sets and re-proposes an initial proposal that lost its id.  A
+// Proposer starts with every id unlearned and preparing (:1074-1082); the engine model
+// idles it at the E_EPOCH run that created it or changed its acceptors (include/mpx.h)
+// and gives it the node's own Values of the trace not yet learned as initial proposals
+// (what Propose would have recorded; the reference driver's prefill).  Host walk over
+// the device's promise quorums (F_QUORUM) and merged maps (k_apply's records).
+static int put_bytes(const std::string &d, uint8_t **out, uint64_t *size);
+
+static int member_decisions(mpx_engine *e, const Results &r, std::string &d)
+{
+    const HostTrace &h = e->ht;
+    const uint32_t N = e->cfg.num_nodes;
+    const auto &ep = e->epochs;
+    d.append("MPXD", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, N);
+    struct Prop {
+        IdSet unlearned, unproposed;
+        std::map<uint64_t, uint64_t> initial;          // initial_proposals_: instance -> value id
+        std::set<uint64_t> newly;                      // newly_proposed_values_
+        uint64_t vid = 0;                              // value_id_
+        bool preparing = true, prefilled = false;
+    };
+    for (uint32_t n = 0; n < N; ++n) {
+        // the node's own non-noop Values, first LEARN occurrence of each value id
+        std::map<uint64_t, uint64_t> own;
+        {
+            std::set<uint64_t> seen;
+            for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
+                if (h.m_type[g] != MPX_MSG_COMMIT) continue;
+                for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) {
+                    const uint64_t hv = h.e_val[k], v = MPX_HANDLE_VALUE_ID(hv);
+                    if (MPX_HANDLE_PROPOSER(hv) != n || MPX_HANDLE_NOOP(hv) || !seen.insert(v).second) continue;
+                    own[h.e_iid[k]] = v;
+                }
+            }
+        }
+        std::unordered_map<uint64_t, uint64_t> learned;      // the learner's learned_values_ (insert-first)
+        std::unique_ptr<Prop> p;
+        auto prefill = [&]() {
+            if (!p || p->prefilled) return;
+            p->prefilled = true;
+            for (auto &x : own)
+                if (!learned.count(x.first)) p->initial.emplace(x.first, x.second);
+        };
+        if ((ep[0].proposer_mask >> n) & 1) { p.reset(new Prop); p->preparing = false; prefill(); }
+        std::string body;
+        uint64_t count = 0;
+        uint32_t ei = 0;
+        bool idle = false;
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
+            const uint8_t t = h.m_type[g];
+            if (t != MPX_MSG_E_EPOCH && idle) {
+                if (p) { p->preparing = false; prefill(); }
+                idle = false;
+            }
+            if (t == MPX_MSG_P_START) {
+                if (p) p->preparing = true;
+            } else if (t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM) && p) {
+                IdSet un = p->unlearned;
+                std::vector<std::pair<uint64_t, uint64_t>> b;
+                auto it = r.by_msg[1].find((uint32_t)g);
+                if (it != r.by_msg[1].end())
+                    for (const OutEnt *o : it->second)
+                        if (un.contains(o->iid)) { un.remove(o->iid); b.push_back({o->iid, o->handle}); }
+                while (un.r.size() > 1) {
+                    const auto first = *un.r.begin();
+                    un.r.erase(un.r.begin());
+                    for (uint64_t id = first.first; id != first.second; ++id) b.push_back({id, MPX_HANDLE(n, 1, ++p->vid)});
+                }
+                for (auto &x : p->initial)
+                    if (un.contains(x.first)) { un.remove(x.first); b.push_back({x.first, MPX_HANDLE(n, 0, x.second)}); }
+                for (uint64_t v : p->newly) {
+                    const uint64_t iid = un.next();
+                    p->initial[iid] = v;
+                    b.push_back({iid, MPX_HANDLE(n, 0, v)});
+                }
+                p->newly.clear();
+                p->unproposed = un;
+                p->preparing = false;
+                std::sort(b.begin(), b.end());
+                app<uint64_t>(body, seq_of(h, n, g));
+                app<uint64_t>(body, b.size());
+                for (auto &x : b) { app<uint64_t>(body, x.first); app<uint64_t>(body, x.second); }
+                ++count;
+            } else if (t == MPX_MSG_COMMIT) {                  // LEARN: Learner::OnLearn (:1029-1060)
+                if (p) {                                       // Proposer::OnLearn (:1383-1470)
+                    std::set<uint64_t> conflicts;
+                    for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) {
+                        const uint64_t iid = h.e_iid[k], hv = h.e_val[k];
+                        if (!learned.count(iid) && p->unlearned.contains(iid)) p->unlearned.remove(iid);
+                        if (p->unproposed.contains(iid)) p->unproposed.remove(iid);
+                        auto in = p->initial.find(iid);
+                        if (in != p->initial.end()) {
+                            if (MPX_HANDLE_PROPOSER(hv) != n || MPX_HANDLE_VALUE_ID(hv) != in->second) conflicts.insert(in->second);
+                            p->initial.erase(in);
+                        }
+                    }
+                    if (!p->preparing) { for (uint64_t v : conflicts) p->initial[p->unproposed.next()] = v; }
+                    else p->newly.insert(conflicts.begin(), conflicts.end());
+                }
+                for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) learned.emplace(h.e_iid[k], h.e_val[k]);
+            } else if (t == MPX_MSG_E_EPOCH) {
+                const uint32_t ej = h.m_ver[g];
+                if (ej >= ep.size()) return MPX_E_DECODE;
+                const mpx_epoch &o = ep[ei], &x = ep[ej];
+                const bool was = (o.proposer_mask >> n) & 1, now = (x.proposer_mask >> n) & 1;
+                if (now && !was) p.reset(new Prop);            // the constructor's StartPrepare
+                if (was && !now) p.reset();
+                if (p && x.acceptor_mask != o.acceptor_mask) p->preparing = true;   // AcceptorsChanged
+                if (now && (!was || o.acceptor_mask != x.acceptor_mask)) idle = true;
+                ei = ej;
+            }
+        }
+        app<uint64_t>(d, count);
+        d += body;
+    }
+    return MPX_OK;
+}
+
 // ------------------------------------------------- phase-2 decisions (f2) --
 // The batch OnPrepareReply builds at each promise quorum (multi/paxos.cpp:
 // 1056-1130) for a proposer with no client proposals of its own: the device
@@ -1501,7 +1622,15 @@ extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
     if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
-    if (e->cfg.semantics != MPX_SEM_MULTI || e->cfg.shard_begin != 0) return MPX_E_STATE;
+    if (e->cfg.shard_begin != 0) return MPX_E_STATE;
+    if (e->cfg.semantics == MPX_SEM_MEMBER) {
+        if (!e->whole) return MPX_E_STATE;               // the learner's whole learned set
+        Results r;
+        TRY(fetch_results(e, r));
+        std::string d;
+        TRY(member_decisions(e, r, d));
+        return put_bytes(d, out, size);
+    }
     Results r;
     TRY(fetch_results(e, r));
     const char *hs = std::getenv("MPX_DECIDE_HOST");     // (A/B: the bookkeeping without proposals too)

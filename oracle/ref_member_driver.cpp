@@ -24,7 +24,8 @@
 // model, include/mpx.h), and batches / learns its own decision code creates are
 // discarded (their sends are proposer broadcasts, not in-scope replies).
 //
-// Output: the canonical MPXR result; mpxref_member_learns: the
+// Output: the canonical MPXR result; mpxref_member_decisions: the
+// ACCEPT batch each promise quorum's OnPrepareReply built (MPXD, :1183-1297); mpxref_member_learns: the
 // proposers' learn reliability bookkeeping as MPXL (include/mpx.h
 // mpx_read_learns): every LearningValues a Proposer created (learning_id_, :1334-1337,
 // 1299-1307, 1487-1491), the record where Applied ran for it (learning_values_for_
@@ -123,6 +124,7 @@ struct Node {
     std::map<paxos::InstanceID, paxos::ValueID> own_iids;
     uint32_t epoch = 0;
     u64 P = 0, A = 0, L = 0;
+    std::string events_d; u64 n_d = 0;               // phase-2 decisions (MPXD)
     std::vector<LearnRec> lrec;                      // learn reliability (MPXL), creation order
     std::map<paxos::LearningID, size_t> llive;       // the current Proposer's open learns
 };
@@ -192,7 +194,7 @@ int parse_pvalues(Logger *lg, const uint8_t *buf, uint32_t len, PVMap *out)
 }  // namespace
 
 static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size,
-                      uint64_t *stats, uint8_t **lout, uint64_t *lsize)
+                      uint64_t *stats, uint8_t **lout, uint64_t *lsize, uint8_t **dout = NULL, uint64_t *dsize = NULL)
 {
     if (size < 40 || memcmp(trace, "MPXT", 4)) return -4;
     uint32_t N = rd32(trace + 8), sem = rd32(trace + 12), ne = rd32(trace + 24);
@@ -332,6 +334,19 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
                     pr->pre_accepted_values_.swap(saved);
                 }
                 pr->OnPrepareReply(msg);
+                if (quorum_next) {
+                    // the phase-2 batch the reference's decision logic built (:1183-1297:
+                    // adopt pre-accepted, noop gap fill, own initial / queued values)
+                    std::string d;
+                    u64 cnt_d = 0;
+                    for (auto &e : pr->accepting_values_)
+                        if (!before_b.count(e.first))
+                            for (auto &v : e.second->values_) {
+                                put<u64>(d, v.first); put<u64>(d, handle_of(v.second.value_)); ++cnt_d;
+                            }
+                    put<u64>(n.events_d, k); put<u64>(n.events_d, cnt_d); n.events_d += d;
+                    n.n_d++;
+                }
                 discard_new_batches(pr, before_b);
                 break;
             }
@@ -501,6 +516,16 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
         memcpy(*out, r.data(), r.size());
         *out_size = r.size();
     }
+    if (dout) {
+        std::string d;
+        d.append("MPXD", 4);
+        put<uint32_t>(d, 1); put<uint32_t>(d, N);
+        for (uint32_t i = 0; i < N; ++i) { put<u64>(d, ns[i].n_d); d += ns[i].events_d; }
+        *dout = (uint8_t *)malloc(d.size());
+        if (!*dout) return -2;
+        memcpy(*dout, d.data(), d.size());
+        *dsize = d.size();
+    }
     if (lout) {
         std::string l;
         l.append("MPXL", 4);
@@ -530,4 +555,9 @@ extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **
 extern "C" int mpxref_member_learns(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)
 {
     return member_run(trace, size, NULL, NULL, NULL, out, out_size);
+}
+
+extern "C" int mpxref_member_decisions(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)
+{
+    return member_run(trace, size, NULL, NULL, NULL, NULL, NULL, out, out_size);
 }

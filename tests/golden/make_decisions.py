@@ -1,7 +1,8 @@
 """Write the phase-2 decision fixtures (tests/golden/<name>.mpxd, format tests/mpxd.py):
-for every multi-semantics golden trace with a promise quorum, the batch the
-REFERENCE's own OnPrepareReply built there (multi/paxos.cpp:1056-1182), recorded
-by oracle/ref_multi_driver.cpp (mpxref_decisions).  Run in the build container.
+for every golden trace with a promise quorum, the batch the REFERENCE's own
+OnPrepareReply built there (multi/paxos.cpp:1056-1182, member/paxos.cpp:1183-1297),
+recorded by oracle/ref_multi_driver.cpp (mpxref_decisions) or
+oracle/ref_member_driver.cpp (mpxref_member_decisions).  Run in the build container.
 
     python tests/golden/make_decisions.py
 """
@@ -13,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 import mpxd  # noqa: E402
-from oracles import ref_available, ref_decisions  # noqa: E402
+from oracles import ref_available, ref_decisions, ref_member_decisions  # noqa: E402
 
 
 def main():
@@ -23,9 +24,7 @@ def main():
     out = {}
     for name in sorted(index):
         trace = open(os.path.join(HERE, name + ".mpxt"), "rb").read()
-        if trace[12:16] != b"\x00\x00\x00\x00":
-            continue
-        d = ref_decisions(trace)
+        d = ref_decisions(trace) if trace[12:16] == b"\x00\x00\x00\x00" else ref_member_decisions(trace)
         parsed = mpxd.parse(d)
         nq = sum(len(x) for x in parsed)
         if not nq:

@@ -1,0 +1,184 @@
+"""Member phase-2 decisions restated in Python — TEST INFRASTRUCTURE.
+
+The batch member Proposer::OnPrepareReply builds at a promise quorum
+(member/paxos.cpp:1183-1297): unproposed = the proposer's unlearned ids; adopt the merged
+pre-accepted value of every unproposed id, noop-fill every unproposed range but the last,
+then its initial proposals still unproposed and its queued values at the next free ids.
+Proposer::OnLearn (:1383-1470) keeps the sets: a learned id leaves unlearned / unproposed,
+an initial proposal that lost its id is proposed again (now, or queued while preparing).
+A Proposer starts with every id unlearned (:1074-1082); the reference driver fills its
+initial proposals with the node's own Values of the trace not yet learned (prefill,
+oracle/ref_member_driver.cpp) and idles it at each E_EPOCH step until its next P_START.
+The promise quorums and merged maps come from an MPXR result (what the device computes).
+Checked against the reference's own decisions (tests/golden/*.mpxd) on CPU; the engine's
+host walk (engine.cpp member_decisions) is the same algorithm.
+"""
+import struct
+
+import mpxr
+from learns_model import _streams
+
+INF = (1 << 64) - 1
+
+
+class IdSet:
+    """AvailableInstanceIDs (multi/paxos.cpp:253-318): disjoint [a, b) ranges."""
+
+    def __init__(self):
+        self.r = [[0, INF]]
+
+    def copy(self):
+        c = IdSet()
+        c.r = [list(x) for x in self.r]
+        return c
+
+    def contains(self, i):
+        return any(a <= i < b for a, b in self.r)
+
+    def remove(self, i):
+        for k, (a, b) in enumerate(self.r):
+            if a <= i < b:
+                rep = ([[a, i]] if a != i else []) + ([[i + 1, b]] if i + 1 != b else [])
+                self.r[k:k + 1] = rep
+                return
+
+    def next(self):
+        a = self.r[0][0]
+        self.remove(a)
+        return a
+
+
+def _value(m, pos):
+    """member Value_m at pos -> (handle, end)"""
+    p, vid, noop = struct.unpack_from("<IQ?", m, pos)
+    pos += 13
+    h = (p << 48) | (int(noop) << 47) | vid
+    if noop:
+        return h, pos
+    mem, ln = struct.unpack_from("<?I", m, pos)
+    pos += 5
+    pos += 8 * ln if mem else ln
+    (cl,) = struct.unpack_from("<I", m, pos)
+    return h, pos + 4 + cl
+
+
+def _learn_entries(m):
+    (ln,) = struct.unpack_from("<I", m, 16)
+    pos, end, out = 20, 20 + ln, []
+    while pos < end:
+        iid = struct.unpack_from("<Q", m, pos)[0]
+        h, pos = _value(m, pos + 16)
+        out.append((iid, h))
+    return sorted(out)
+
+
+def decisions(trace, result):
+    epochs, streams = _streams(trace)
+    res = mpxr.parse(result)
+    b = bytearray(b"MPXD") + struct.pack("<II", 1, len(streams))
+    for n, msgs in enumerate(streams):
+        quorums = {q[0]: q[2] for q in res["nodes"][n]["quorums"]}
+        own = {}                                    # the driver's prefill source: iid -> value id
+        seen = set()
+        for m in msgs:
+            if struct.unpack_from("<I", m)[0] != 5:
+                continue
+            for iid, h in _learn_entries(m):
+                vid = h & ((1 << 47) - 1)
+                if (h >> 48) != n or (h >> 47) & 1 or vid in seen:
+                    continue
+                seen.add(vid)
+                own[iid] = vid
+        learned = {}
+        st = None                                   # the Proposer, if any
+
+        def new_proposer():
+            return {"unlearned": IdSet(), "unproposed": IdSet(), "initial": {}, "newly": set(), "vid": 0,
+                    "prep": True, "prefilled": False}
+
+        def prefill(p):
+            if p["prefilled"]:
+                return
+            p["prefilled"] = True
+            for iid in sorted(own):
+                if iid not in learned and iid not in p["initial"]:
+                    p["initial"][iid] = own[iid]
+
+        if (epochs[0][2] >> n) & 1:
+            st = new_proposer()
+            st["prep"] = False
+            prefill(st)
+        out, ei, idle = [], 0, False
+        for k, m in enumerate(msgs):
+            t = struct.unpack_from("<I", m)[0]
+            if t != 18 and idle:
+                if st:
+                    st["prep"] = False
+                    prefill(st)
+                idle = False
+            if t == 16 and st:
+                st["prep"] = True
+            elif t == 1 and k in quorums and st:
+                un = st["unlearned"].copy()
+                batch = []
+                for iid, _pid, h in quorums[k]:
+                    if un.contains(iid):
+                        un.remove(iid)
+                        batch.append((iid, h))
+                while len(un.r) != 1:
+                    a, e = un.r.pop(0)
+                    for i in range(a, e):
+                        st["vid"] += 1
+                        batch.append((i, (n << 48) | (1 << 47) | st["vid"]))
+                for iid in sorted(st["initial"]):
+                    if un.contains(iid):
+                        un.remove(iid)
+                        batch.append((iid, (n << 48) | st["initial"][iid]))
+                for vid in sorted(st["newly"]):
+                    iid = un.next()
+                    st["initial"][iid] = vid
+                    batch.append((iid, (n << 48) | vid))
+                st["newly"].clear()
+                st["unproposed"] = un
+                st["prep"] = False
+                out.append((k, sorted(batch)))
+            elif t == 5:
+                ents = _learn_entries(m)
+                if st:                              # Proposer::OnLearn (:1383-1470)
+                    conflicts = set()
+                    for iid, h in ents:
+                        if iid not in learned and st["unlearned"].contains(iid):
+                            st["unlearned"].remove(iid)
+                        if st["unproposed"].contains(iid):
+                            st["unproposed"].remove(iid)
+                        if iid in st["initial"]:
+                            v0 = st["initial"].pop(iid)
+                            if (h >> 48) != n or (h & ((1 << 47) - 1)) != v0:
+                                conflicts.add(v0)
+                    if conflicts:
+                        if not st["prep"]:
+                            for vid in sorted(conflicts):
+                                st["initial"][st["unproposed"].next()] = vid
+                        else:
+                            st["newly"] |= conflicts
+                for iid, h in ents:
+                    learned.setdefault(iid, h)
+            elif t == 18:
+                ej = struct.unpack_from("<I", m, 4)[0]
+                o, x = epochs[ei], epochs[ej]
+                was, now = bool((o[2] >> n) & 1), bool((x[2] >> n) & 1)
+                if now and not was:
+                    st = new_proposer()             # the constructor's StartPrepare: preparing
+                if was and not now:
+                    st = None
+                if st and (x[1] != o[1]):
+                    st["prep"] = True               # AcceptorsChanged -> RestartPrepare / AcceptRejected
+                if now and (not was or o[1] != x[1]):
+                    idle = True                     # the driver idles it once the LEARN's changes ran
+                ei = ej
+        b += struct.pack("<Q", len(out))
+        for k, batch in out:
+            b += struct.pack("<QQ", k, len(batch))
+            for iid, h in batch:
+                b += struct.pack("<QQ", iid, h)
+    return bytes(b)

@@ -144,6 +144,12 @@ def ref_commits(trace):
     return _blob_call(REF_SO, "mpxref_commits", trace)
 
 
+def ref_member_decisions(trace):
+    """The reference's own member phase-2 batch at every promise quorum (MPXD),
+    recorded by oracle/ref_member_driver.cpp (mpxref_member_decisions)."""
+    return _blob_call(REF_MEMBER_SO, "mpxref_member_decisions", trace)
+
+
 def ref_learns(trace):
     """The reference's own member LearningValues bookkeeping (MPXL): creation at accept /
     promise quorums and LearnersChanged, Applied, OnLearnReply retirement, drops

@@ -648,7 +648,7 @@ def test_sharded_decisions_match_oracle_c3(shards):
     assert _sharded_decisions(t, shards) == want
 
 
-def test_decisions_refused_for_shards_and_member():
+def test_decisions_refused_for_shards():
     t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=3, num_instances=1024, batch=256)
     with mpx.Engine(3, 256, 1024) as e:
         e.submit_trace(t)
@@ -917,6 +917,23 @@ def test_engine_learns_match_model_c5(seed, m, batch):
     with mpx.Engine.for_trace(t) as e:
         e.run()
         assert e.learns() == want
+
+
+@pytest.mark.parametrize("seed,m,batch", [(9, 1 << 16, 64), (10, 40000, 200)])
+def test_engine_member_decisions_match_model_c5(seed, m, batch):
+    """Member phase-2 decisions beyond fixture size: the engine == the Python restatement
+    (tests/member_decisions_model.py, pinned to the reference's fixtures on CPU) fed by the
+    C oracle's promise quorums and merged maps."""
+    from oracles import oracle_run
+    import member_decisions_model
+    import mpxd
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=8, num_instances=m, seed=seed, batch=batch,
+                           drop_rate=300, dup_rate=300, max_delay=64, noop_permille=15)
+    want = member_decisions_model.decisions(t, oracle_run(t)[0])
+    assert sum(len(x) for x in mpxd.parse(want)) >= 15
+    with mpx.Engine.for_trace(t) as e:
+        e.run()
+        assert e.decisions() == want
 
 
 def test_learns_refused_off_member_and_on_shards():

@@ -1,5 +1,6 @@
-"""Learn reliability (member): the Python restatement of the engine's
-algorithm (tests/learns_model.py) against the reference's own bookkeeping — CPU only."""
+"""Member proposer bookkeeping — learn reliability and phase-2 decisions
+(f2): the Python restatements of the engine's algorithms (tests/learns_model.py,
+tests/member_decisions_model.py) against the reference's own bookkeeping — CPU only."""
 import json
 import os
 import struct
@@ -7,6 +8,7 @@ import struct
 import pytest
 
 import learns_model
+import member_decisions_model
 import mpxl
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -40,3 +42,13 @@ def test_learn_fixtures_cover_every_outcome():
     assert struct.unpack_from("<I", t, 4)[0] == 2
     assert any(struct.unpack_from("<Q", t, 40 + 32 * i + 16) != struct.unpack_from("<Q", t, 40 + 32 * i + 24)
                for i in range(ne))
+
+
+DECISIONS = json.load(open(os.path.join(GOLD, "decisions.json")))
+
+
+@pytest.mark.parametrize("name", sorted(n for n in DECISIONS if n.startswith(("mm_", "c5_"))))
+def test_member_decisions_model_matches_reference_golden(name):
+    """member_decisions_model over the trace and its reference MPXR (promise quorums and their
+    merged maps) == the batch the reference's member OnPrepareReply built (.mpxd fixture)."""
+    assert member_decisions_model.decisions(_read(name, ".mpxt"), _read(name, ".mpxr")) == _read(name, ".mpxd")
