@@ -1,4 +1,4 @@
-"""Learn reliability (member) restated in Python — TEST INFRASTRUCTURE.
+"""Learn reliability (member) restated in Python — TEST INFRASTRUCTURE (oracle/: only tests use it, as the checker).
 
 The engine's mpx_read_learns (engine.cpp learn_plan + kernels.hip k_learns) in plain
 loops over a trace and its MPXR result: the promise quorums and chosen batches the

@@ -1,4 +1,4 @@
-"""Member phase-2 decisions restated in Python — TEST INFRASTRUCTURE.
+"""Member phase-2 decisions restated in Python — TEST INFRASTRUCTURE (oracle/: only tests use it, as the checker).
 
 The batch member Proposer::OnPrepareReply builds at a promise quorum
 (member/paxos.cpp:1183-1297): unproposed = the proposer's unlearned ids; adopt the merged

@@ -5,6 +5,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.join(ROOT, "multi-paxos_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))          # the Python restatements (learns, member decisions)
 
 
 def pytest_configure(config):

@@ -905,7 +905,7 @@ def test_engine_learns_match_reference(name):
 @pytest.mark.parametrize("seed,m,batch", [(7, 1 << 16, 64), (8, 50000, 256)])
 def test_engine_learns_match_model_c5(seed, m, batch):
     """C5-shaped traces beyond fixture size: the engine's learn bookkeeping == the Python
-    restatement (tests/learns_model.py, pinned to the reference's fixtures on CPU) fed by
+    restatement (oracle/learns_model.py, pinned to the reference's fixtures on CPU) fed by
     the C oracle's promise quorums and chosen batches."""
     from oracles import oracle_run
     import learns_model
@@ -922,7 +922,7 @@ def test_engine_learns_match_model_c5(seed, m, batch):
 @pytest.mark.parametrize("seed,m,batch", [(9, 1 << 16, 64), (10, 40000, 200)])
 def test_engine_member_decisions_match_model_c5(seed, m, batch):
     """Member phase-2 decisions beyond fixture size: the engine == the Python restatement
-    (tests/member_decisions_model.py, pinned to the reference's fixtures on CPU) fed by the
+    (oracle/member_decisions_model.py, pinned to the reference's fixtures on CPU) fed by the
     C oracle's promise quorums and merged maps."""
     from oracles import oracle_run
     import member_decisions_model

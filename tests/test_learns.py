@@ -1,6 +1,6 @@
 """Member proposer bookkeeping — learn reliability and phase-2 decisions
-(f2): the Python restatements of the engine's algorithms (tests/learns_model.py,
-tests/member_decisions_model.py) against the reference's own bookkeeping — CPU only."""
+(f2): the Python restatements of the engine's algorithms (oracle/learns_model.py,
+oracle/member_decisions_model.py) against the reference's own bookkeeping — CPU only."""
 import json
 import os
 import struct
