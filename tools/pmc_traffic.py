@@ -71,7 +71,7 @@ def main():
         bench_args = ["--c3-only", "--c3-steps", "3", "--c3-instances", str(a.instances)] + rest
     else:
         bench_args = ["--steps", "3", "--warmup", "0", "--instances", str(a.instances), "--nodes", str(a.nodes),
-                      "--c3-instances", "0"] + rest
+                      "--c3-instances", "0", "--c5-instances", "0", "--shard-of", "0"] + rest
     fetch = run_pass(["FETCH_SIZE"], a.outdir, bench_args, a.tag)["FETCH_SIZE"]
     write = run_pass(["WRITE_SIZE"], a.outdir, bench_args, a.tag)["WRITE_SIZE"]
     sq = run_pass(SQ_COUNTERS, a.outdir, bench_args, a.tag) if a.sq else {}
