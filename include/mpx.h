@@ -457,8 +457,23 @@ int  mpx_comm_allgather_bytes(mpx_engine *eng, const uint8_t *mine, uint64_t len
  * in instance order): mpx_decisions_bounds, mpx_comm_allreduce_max (also of the
  * quorum count, which must agree), mpx_read_decisions_part, the parts gathered
  * with mpx_comm_allgather_bytes and merged with mpx_decisions_combine.  Every
- * rank receives the whole run's MPXD.  One rank: mpx_read_decisions' bytes. */
+ * rank receives the whole run's MPXD.  One rank: mpx_read_decisions' bytes.  A
+ * trace with client values (P_PROPOSE) takes the proposal parts instead
+ * (mpx_proposal_part gathered, mpx_proposal_combine). */
 int  mpx_read_decisions_sharded(mpx_engine *eng, uint8_t **out, uint64_t *size);
+/* Decisions with client values over instance shards (multi semantics, host traces):
+ * the proposer's bookkeeping reads events of its own stream — Propose, StartPrepare,
+ * each COMMIT's entries, each promise quorum's merged map — and a shard holds its own
+ * instances' entries of them.  mpx_proposal_part writes this shard's events, format
+ * MPXE: "MPXE" u32 1, u32 nodes, u64 shard_begin, u64 shard_end; per node u64 count,
+ * per event {u64 seq, u32 type (19 P_PROPOSE, 16 P_START, 5 COMMIT, 1 promise
+ * quorum), u32 n, {u64 iid, u64 handle} * n}.  mpx_proposal_combine takes every
+ * shard's part in shard order (contiguous ranges from 0), merges each node's events
+ * by record (entries concatenated in shard order) and writes the MPXD
+ * mpx_read_decisions writes on one engine holding every instance.  Pure host work. */
+int  mpx_proposal_part(mpx_engine *eng, uint8_t **out, uint64_t *size);
+int  mpx_proposal_combine(const uint8_t *const *parts, const uint64_t *sizes, uint32_t nparts,
+                          uint8_t **out, uint64_t *size);
 
 #ifdef __cplusplus
 }

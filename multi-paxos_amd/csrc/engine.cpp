@@ -1413,10 +1413,43 @@ struct IdSet {
 // OnPrepareReply's batch (:1056-1175): the merged values of unproposed instances, noops over
 // every unproposed range but the last (++value_id_ each), the own initial proposals still
 // unproposed, then the queued values at the next unproposed ids.  MPXD as mpx_read_decisions.
-static int proposer_decisions(mpx_engine *e, const Results &r, std::string &d)
+// The events the bookkeeping reads, per node in stream order: Propose, StartPrepare, a COMMIT
+// with its entries, a promise quorum with its merged map's entries.  One engine holding every
+// instance has them all; instance shards each hold their own instances' entries of the same
+// events (headers are replicated), merged in shard order (mpx_proposal_combine).
+struct PEv {
+    uint64_t seq;
+    uint32_t type;
+    std::vector<std::pair<uint64_t, uint64_t>> ents;      // {iid, handle}, iid ascending
+};
+typedef std::vector<std::vector<PEv>> PEvents;
+
+static void proposer_events(mpx_engine *e, const Results &r, PEvents &ev)
 {
     const HostTrace &h = e->ht;
     const uint32_t N = e->cfg.num_nodes;
+    ev.assign(N, {});
+    for (uint32_t n = 0; n < N; ++n)
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
+            const uint8_t t = h.m_type[g];
+            const bool quorum = t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM);
+            if (t != MPX_MSG_P_PROPOSE && t != MPX_MSG_P_START && t != MPX_MSG_COMMIT && !quorum) continue;
+            PEv x{seq_of(h, n, g), t, {}};
+            if (t == MPX_MSG_COMMIT)
+                for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) x.ents.push_back({h.e_iid[k], h.e_val[k]});
+            if (quorum) {
+                auto it = r.by_msg[1].find((uint32_t)g);
+                if (it != r.by_msg[1].end())
+                    for (const OutEnt *o : it->second) x.ents.push_back({o->iid, o->handle});
+                std::sort(x.ents.begin(), x.ents.end());
+            }
+            ev[n].push_back(std::move(x));
+        }
+}
+
+static void proposer_sim(const PEvents &ev, std::string &d)
+{
+    const uint32_t N = (uint32_t)ev.size();
     d.append("MPXD", 4);
     app<uint32_t>(d, 1); app<uint32_t>(d, N);
     for (uint32_t n = 0; n < N; ++n) {
@@ -1427,8 +1460,8 @@ static int proposer_decisions(mpx_engine *e, const Results &r, std::string &d)
         bool preparing = false;                             // prepare_retry_timeout_ != NULL
         std::string body;
         uint64_t count = 0;
-        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
-            const uint8_t t = h.m_type[g];
+        for (const PEv &x : ev[n]) {
+            const uint32_t t = x.type;
             if (t == MPX_MSG_P_PROPOSE) {
                 ++vid;
                 if (!preparing) initial[unproposed.next()] = vid;
@@ -1436,8 +1469,8 @@ static int proposer_decisions(mpx_engine *e, const Results &r, std::string &d)
             } else if (t == MPX_MSG_P_START) {
                 preparing = true;
             } else if (t == MPX_MSG_COMMIT) {
-                for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) {
-                    const uint64_t iid = h.e_iid[k], hv = h.e_val[k];
+                for (auto &en : x.ents) {
+                    const uint64_t iid = en.first, hv = en.second;
                     if (committed.insert(iid).second && uncommitted.contains(iid)) uncommitted.remove(iid);
                     if (unproposed.contains(iid)) unproposed.remove(iid);
                     auto it = initial.find(iid);
@@ -1450,20 +1483,18 @@ static int proposer_decisions(mpx_engine *e, const Results &r, std::string &d)
                         }
                     }
                 }
-            } else if (t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM)) {
+            } else {                                        // a promise quorum
                 unproposed = uncommitted;
                 std::vector<std::pair<uint64_t, uint64_t>> b;
-                auto it = r.by_msg[1].find((uint32_t)g);
-                if (it != r.by_msg[1].end())
-                    for (const OutEnt *o : it->second)
-                        if (unproposed.contains(o->iid)) { unproposed.remove(o->iid); b.push_back({o->iid, o->handle}); }
+                for (auto &en : x.ents)
+                    if (unproposed.contains(en.first)) { unproposed.remove(en.first); b.push_back(en); }
                 while (unproposed.r.size() > 1) {
                     const auto first = *unproposed.r.begin();
                     unproposed.r.erase(unproposed.r.begin());
                     for (uint64_t id = first.first; id != first.second; ++id) b.push_back({id, MPX_HANDLE(n, 1, ++vid)});
                 }
-                for (auto &x : initial)
-                    if (unproposed.contains(x.first)) { unproposed.remove(x.first); b.push_back({x.first, MPX_HANDLE(n, 0, x.second)}); }
+                for (auto &y : initial)
+                    if (unproposed.contains(y.first)) { unproposed.remove(y.first); b.push_back({y.first, MPX_HANDLE(n, 0, y.second)}); }
                 for (uint64_t v : newly) {
                     const uint64_t iid = unproposed.next();
                     initial[iid] = v;
@@ -1472,15 +1503,22 @@ static int proposer_decisions(mpx_engine *e, const Results &r, std::string &d)
                 newly.clear();
                 preparing = false;
                 std::sort(b.begin(), b.end());                 // AcceptingValues::values_ is a map
-                app<uint64_t>(body, seq_of(h, n, g));
+                app<uint64_t>(body, x.seq);
                 app<uint64_t>(body, b.size());
-                for (auto &x : b) { app<uint64_t>(body, x.first); app<uint64_t>(body, x.second); }
+                for (auto &y : b) { app<uint64_t>(body, y.first); app<uint64_t>(body, y.second); }
                 ++count;
             }
         }
         app<uint64_t>(d, count);
         d += body;
     }
+}
+
+static int proposer_decisions(mpx_engine *e, const Results &r, std::string &d)
+{
+    PEvents ev;
+    proposer_events(e, r, ev);
+    proposer_sim(ev, d);
     return MPX_OK;
 }
 
@@ -2466,11 +2504,111 @@ extern "C" int mpx_comm_allgather_bytes(mpx_engine *e, const uint8_t *mine, uint
     return MPX_OK;
 }
 
+// Decisions with client values over instance shards (include/mpx.h): each shard's part
+// holds the bookkeeping's events with its own instances' entries (MPXE); the combine merges
+// the parts per node by record (headers are replicated, so every shard lists the same
+// Propose / StartPrepare / quorum records; a COMMIT appears where it has entries) and runs
+// the proposer's walk once over the union.
+extern "C" int mpx_proposal_part(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->incremental || e->cfg.semantics != MPX_SEM_MULTI || e->device_trace) return MPX_E_STATE;
+    Results r;
+    TRY(fetch_results(e, r));
+    PEvents ev;
+    proposer_events(e, r, ev);
+    std::string d;
+    d.append("MPXE", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, e->cfg.num_nodes);
+    app<uint64_t>(d, e->cfg.shard_begin); app<uint64_t>(d, e->cfg.shard_end);
+    for (auto &l : ev) {
+        app<uint64_t>(d, l.size());
+        for (auto &x : l) {
+            app<uint64_t>(d, x.seq); app<uint32_t>(d, x.type); app<uint32_t>(d, (uint32_t)x.ents.size());
+            for (auto &en : x.ents) { app<uint64_t>(d, en.first); app<uint64_t>(d, en.second); }
+        }
+    }
+    return put_bytes(d, out, size);
+}
+
+extern "C" int mpx_proposal_combine(const uint8_t *const *parts, const uint64_t *sizes, uint32_t nparts,
+                                    uint8_t **out, uint64_t *size)
+{
+    if (!parts || !sizes || !nparts || !out || !size) return MPX_E_INVAL;
+    uint32_t N = 0;
+    uint64_t prev_end = 0;
+    std::vector<PEvents> ps(nparts);
+    for (uint32_t i = 0; i < nparts; ++i) {
+        const uint8_t *p = parts[i];
+        const uint64_t n = sizes[i];
+        if (!p || n < 28 || std::memcmp(p, "MPXE", 4) || rd32(p + 4) != 1) return MPX_E_INVAL;
+        const uint32_t Ni = rd32(p + 8);
+        const uint64_t sb = rd64(p + 12), se = rd64(p + 20);
+        if (!Ni || Ni > MPX_MAX_NODES || (i && Ni != N) || sb != prev_end || se < sb) return MPX_E_INVAL;   // shard order
+        N = Ni;
+        prev_end = se;
+        uint64_t pos = 28;
+        ps[i].assign(N, {});
+        for (uint32_t k = 0; k < N; ++k) {
+            if (pos + 8 > n) return MPX_E_INVAL;
+            const uint64_t c = rd64(p + pos); pos += 8;
+            for (uint64_t j = 0; j < c; ++j) {
+                if (pos + 16 > n) return MPX_E_INVAL;
+                PEv x{rd64(p + pos), rd32(p + pos + 8), {}};
+                const uint32_t m = rd32(p + pos + 12);
+                pos += 16;
+                if (m > (n - pos) / 16) return MPX_E_INVAL;
+                for (uint32_t q = 0; q < m; ++q, pos += 16) {
+                    const uint64_t iid = rd64(p + pos);
+                    if (iid < sb || iid >= se) return MPX_E_INVAL;
+                    x.ents.push_back({iid, rd64(p + pos + 8)});
+                }
+                if (!ps[i][k].empty() && x.seq <= ps[i][k].back().seq) return MPX_E_INVAL;   // stream order
+                ps[i][k].push_back(std::move(x));
+            }
+        }
+        if (pos != n) return MPX_E_INVAL;
+    }
+    PEvents all(N);
+    for (uint32_t k = 0; k < N; ++k) {
+        std::map<uint64_t, PEv> m;                         // record -> the event, entries in shard order
+        for (uint32_t i = 0; i < nparts; ++i)
+            for (auto &x : ps[i][k]) {
+                auto it = m.find(x.seq);
+                if (it == m.end()) { m.emplace(x.seq, x); continue; }
+                if (it->second.type != x.type) return MPX_E_INVAL;
+                it->second.ents.insert(it->second.ents.end(), x.ents.begin(), x.ents.end());
+            }
+        for (auto &y : m) all[k].push_back(std::move(y.second));
+    }
+    std::string d;
+    proposer_sim(all, d);
+    return put_bytes(d, out, size);
+}
+
 extern "C" int mpx_read_decisions_sharded(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
     const int R = e->comm ? e->nranks : 1;
     if (R <= 1 && e->cfg.shard_begin == 0) return mpx_read_decisions(e, out, size);
+    if (e->cfg.semantics == MPX_SEM_MULTI && has_proposals(e->ht)) {
+        // client values: the proposer's walk over every shard's events (P_PROPOSE is a header:
+        // every rank sees it, so every rank takes this branch)
+        uint8_t *part = nullptr;
+        uint64_t plen = 0;
+        TRY(mpx_proposal_part(e, &part, &plen));
+        std::vector<uint64_t> lens(R);
+        uint8_t *all = nullptr;
+        int rc = mpx_comm_allgather_bytes(e, part, plen, &all, lens.data());
+        std::free(part);
+        if (rc) return rc;
+        std::vector<const uint8_t *> ps(R);
+        uint64_t at = 0;
+        for (int r = 0; r < R; ++r) { ps[r] = all + at; at += lens[r]; }
+        rc = mpx_proposal_combine(ps.data(), lens.data(), (uint32_t)R, out, size);
+        std::free(all);
+        return rc;
+    }
     uint64_t cnt = 0;
     TRY(mpx_decisions_bounds(e, nullptr, 0, &cnt));
     std::vector<uint64_t> b(cnt + 2);

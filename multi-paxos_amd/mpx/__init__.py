@@ -120,6 +120,8 @@ def lib():
             "mpx_read_decisions": [vp, P(u8p), u64p],
             "mpx_read_commits": [vp, P(u8p), u64p],
             "mpx_read_learns": [vp, P(u8p), u64p],
+            "mpx_proposal_part": [vp, P(u8p), u64p],
+            "mpx_proposal_combine": [P(u8p), u64p, ctypes.c_uint32, P(u8p), u64p],
             "mpx_decisions_bounds": [vp, u64p, ctypes.c_uint64, u64p],
             "mpx_read_decisions_part": [vp, u64p, ctypes.c_uint64, P(u8p), u64p],
             "mpx_decisions_combine": [P(u8p), u64p, ctypes.c_uint32, P(u8p), u64p],
@@ -372,6 +374,13 @@ class Engine:
         _ck("mpx_read_commits", lib().mpx_read_commits(self.h, ctypes.byref(out), ctypes.byref(size)))
         return _take(out, size.value)
 
+    def proposal_part(self):
+        """MPXE bytes: this shard's events of the proposer bookkeeping (mpx_proposal_part)."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_proposal_part", lib().mpx_proposal_part(self.h, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
     def learns(self):
         """MPXL bytes: every member LearningValues and what became of it (mpx_read_learns)."""
         out = ctypes.POINTER(ctypes.c_uint8)()
@@ -533,3 +542,8 @@ def _combine(fn, parts):
 def commit_points_combine(parts):
     """Union of MPXQ commit creation points of every shard (mpx_commit_points_combine)."""
     return _combine("mpx_commit_points_combine", parts)
+
+
+def proposal_combine(parts):
+    """Merge MPXE parts (shard order) into the whole run's MPXD with client values (mpx_proposal_combine)."""
+    return _combine("mpx_proposal_combine", parts)

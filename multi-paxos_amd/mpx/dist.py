@@ -85,3 +85,13 @@ def gather_decisions(engine, exchange, rank=0):
     bounds = exchange.allreduce_max(mine) if mine else []
     parts = exchange.allgather(engine.decisions_part(bounds))
     return decisions_combine(parts) if rank == 0 else None
+
+
+def gather_proposal_decisions(engine, exchange, rank=0):
+    """Phase-2 decisions of a sharded run whose trace has client values (include/mpx.h
+    mpx_proposal_part / mpx_proposal_combine): every rank's events of the proposer
+    bookkeeping are gathered and walked once in rank (= shard) order.  Returns the whole
+    run's MPXD on rank 0, None elsewhere."""
+    from . import proposal_combine
+    parts = exchange.allgather(bytes(engine.proposal_part()))
+    return proposal_combine(parts) if rank == 0 else None

@@ -122,3 +122,39 @@ def test_commit_points_reject_bad_parts():
         mpx.commit_points_combine([a + b"\0" * 8])                 # trailing bytes
     with pytest.raises(mpx.MpxError):
         mpx.commit_points_combine([_mpxq([[(4, P), (3, 1)], []])])  # not ascending
+
+
+def _mpxe(parts_events, n_nodes, sb, se):
+    b = bytearray(b"MPXE") + struct.pack("<IIQQ", 1, n_nodes, sb, se)
+    for evs in parts_events:
+        b += struct.pack("<Q", len(evs))
+        for seq, t, ents in evs:
+            b += struct.pack("<QII", seq, t, len(ents))
+            for iid, h in ents:
+                b += struct.pack("<QQ", iid, h)
+    return bytes(b)
+
+
+def test_proposal_combine_walks_client_values():
+    """mpx_proposal_combine (host only): a client value proposed while idle takes the next
+    unproposed id (Propose, multi/paxos.cpp:1250-1280); a COMMIT of another value there
+    re-proposes it (:1519-1570); after StartPrepare a quorum adopts the other shard's
+    pre-accepted value and noop-fills the gap (:1056-1175)."""
+    other = (1 << 48) | 7
+    a = _mpxe([[(0, 19, []), (1, 5, [(0, other)]), (2, 16, []), (3, 1, [])]], 1, 0, 4)
+    b = _mpxe([[(0, 19, []), (2, 16, []), (3, 1, [(5, (1 << 48) | 9)])]], 1, 4, 16)
+    got = mpx.proposal_combine([a, b])
+    # value 1 at instance 0, committed there as another value -> re-proposed at 1 (idle);
+    # the quorum: unproposed = [1, inf) minus adopted 5 -> the noop fill comes first and takes
+    # 1..4 (value ids 2..5), so the own value finds its id gone (it waits for that commit)
+    want = bytearray(b"MPXD") + struct.pack("<IIQ", 1, 1, 1) + struct.pack("<QQ", 3, 5)
+    for iid, h in [(1, (1 << 47) | 2), (2, (1 << 47) | 3), (3, (1 << 47) | 4), (4, (1 << 47) | 5),
+                   (5, (1 << 48) | 9)]:
+        want += struct.pack("<QQ", iid, h)
+    assert got == bytes(want), mpxd.parse(got)
+    with pytest.raises(mpx.MpxError):
+        mpx.proposal_combine([b, a])                       # not in shard order
+    with pytest.raises(mpx.MpxError):
+        mpx.proposal_combine([a, _mpxe([[(3, 5, [])]], 1, 4, 16)])   # record types disagree
+    with pytest.raises(mpx.MpxError):
+        mpx.proposal_combine([a[:-4]])                     # truncated

@@ -577,6 +577,28 @@ def test_proposal_traces_refuse_sharded_decisions(name):
             e.decision_bounds()
 
 
+@pytest.mark.parametrize("shards", [2, 3])
+@pytest.mark.parametrize("name", ["demo_s1", "demo5_s3", "hm_propose"])
+def test_proposal_traces_sharded_decisions(name, shards):
+    """Decisions with client values over instance shards (unaligned): each shard's events
+    (mpx_proposal_part) merged by record in shard order, the proposer's walk once over the
+    union (mpx_proposal_combine) == the reference's own decisions (fixture)."""
+    from mpx import dist as mdist
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxd")
+    hd = mpx.trace_header(trace)
+    m = max(hd["num_instances"], 1)
+    parts = []
+    for r in range(shards):
+        sb, se = mdist.shard_bounds(m, shards, r, align=1)
+        with mpx.Engine(hd["num_nodes"], sb, se) as e:
+            e.submit_trace(trace)
+            e.run()
+            parts.append(e.proposal_part())
+    assert mpx.proposal_combine(parts) == want
+    with pytest.raises(mpx.MpxError):
+        mpx.proposal_combine(parts[::-1])                 # not in shard order
+
+
 @pytest.mark.parametrize("seed,m", [(81, 1 << 12), (82, 3000), (83, 1 << 14)])
 def test_engine_decisions_match_oracle_c3(seed, m):
     from oracles import oracle_decisions
