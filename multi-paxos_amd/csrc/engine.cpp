@@ -39,6 +39,7 @@ struct DevBuf {
         if (n <= bytes && p) return MPX_OK;
         if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
         if (!n) return MPX_OK;
+        n = (n + 63) & ~(size_t)63;     // padded: vector loads may read a tail word past the last element
         if (hipMalloc(&p, n) != hipSuccess) { p = nullptr; return MPX_E_NOMEM; }
         bytes = n;
         return MPX_OK;

@@ -119,6 +119,9 @@ __device__ inline uint64_t block_excl_max(uint64_t x, uint64_t *lds4, uint64_t *
 // (multi/paxos.cpp:862-863,1363-1364,1229-1230); member keys carry the Acceptor
 // incarnation in their top byte, so both restart with each new Acceptor
 // (member/paxos.cpp:1700-1760) and an E_EPOCH record starts the incarnation
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ inline void contrib(uint8_t t, uint64_t key, uint64_t &p, uint64_t &s)
 {
     const uint32_t k = t & SC_KIND;
@@ -385,6 +388,10 @@ __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64
 // Chunk aggregates over the header-scan stream: max of the PREPARE ids and of
 // the max_seen contributions of SCAN_CHUNK records (order-free, coalesced)
 // RESET: the step's first kernel also does k_reset's work (one launch less per step)
+// Loads: four records per thread per round — their types as one aligned u32 and their keys
+// as two 16-byte loads (a wave reads 256 B of types and 4 KiB of keys per round) instead of
+// a byte and a u64 per record; the words may start before the chunk and end after it (the
+// record index decides), and device buffers are padded to 64 bytes (DevBuf::alloc)
 template <bool RESET>
 __global__ __launch_bounds__(256) void k_scan_chunk(DevView v, uint32_t n_partials)
 {
@@ -392,21 +399,32 @@ __global__ __launch_bounds__(256) void k_scan_chunk(DevView v, uint32_t n_partia
     if (RESET) reset_state(v, n_partials, (uint64_t)blockIdx.x * 256 + threadIdx.x, (uint64_t)gridDim.x * 256);
     const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
-    uint64_t lp = 0, ls = 0;
-    uint8_t ty[SCAN_ROUNDS];
-    uint64_t ky[SCAN_ROUNDS];
+    const uint64_t w0 = beg >> 2, w1 = (end + 3) >> 2;
+    constexpr uint32_t WR = (SCAN_CHUNK / 4 + 256) / 256;     // words of a chunk, one slack word
+    const uint32_t *tw = reinterpret_cast<const uint32_t *>(v.sc_type);
+    const u64x2 *kw = reinterpret_cast<const u64x2 *>(v.sc_key);
+    uint32_t ty[WR];
+    u64x2 k0[WR], k1[WR];
 #pragma unroll
-    for (uint32_t i = 0; i < SCAN_ROUNDS; ++i) {          // all loads in flight at once
-        const uint64_t g = beg + threadIdx.x + 256ull * i;
-        ty[i] = SC_NONE; ky[i] = 0;
-        if (g < end) { ty[i] = v.sc_type[g]; ky[i] = v.sc_key[g]; }
+    for (uint32_t i = 0; i < WR; ++i) {                      // all loads in flight at once
+        const uint64_t wd = w0 + threadIdx.x + 256ull * i;
+        ty[i] = (uint32_t)SC_NONE * 0x01010101u;
+        k0[i] = u64x2{0, 0}; k1[i] = u64x2{0, 0};
+        if (wd < w1) { ty[i] = tw[wd]; k0[i] = kw[2 * wd]; k1[i] = kw[2 * wd + 1]; }
     }
+    uint64_t lp = 0, ls = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < SCAN_ROUNDS; ++i) {
-        uint64_t p, s;
-        contrib(ty[i], ky[i], p, s);
-        lp = lp > p ? lp : p;
-        ls = ls > s ? ls : s;
+    for (uint32_t i = 0; i < WR; ++i) {
+        const uint64_t g0 = 4 * (w0 + threadIdx.x + 256ull * i);
+        const uint64_t key[4] = {k0[i].x, k0[i].y, k1[i].x, k1[i].y};
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const bool in = g0 + j >= beg && g0 + j < end;
+            uint64_t p, s;
+            contrib(in ? (uint8_t)(ty[i] >> (8 * j)) : (uint8_t)SC_NONE, key[j], p, s);
+            lp = lp > p ? lp : p;
+            ls = ls > s ? ls : s;
+        }
     }
     lp = wave_max(lp);
     ls = wave_max(ls);
@@ -460,30 +478,27 @@ __device__ inline void scan_apply_chunk(const DevView &v, const uint32_t c, uint
     const uint64_t wb = beg + (uint64_t)w * (SCAN_CHUNK / 4) + lane;
     const uint32_t lb = w * (SCAN_CHUNK / 4) + lane;
     constexpr bool member = MEMBER;
-    uint8_t ty[SCAN_ROUNDS];
-    uint64_t ky[SCAN_ROUNDS];
-    uint32_t ix[SCAN_ROUNDS];
-    uint64_t lp = 0, ls = 0;
+    // staging: the chunk's records into LDS (record g at g - beg), four per thread per
+    // round — their types as one aligned u32, keys and message indices as 16-byte loads
+    // (as k_scan_chunk); the words may start before the chunk and end after it
+    const uint64_t w0 = beg >> 2, w1 = (end + 3) >> 2;
+    constexpr uint32_t WR = (SCAN_CHUNK / 4 + 256) / 256;
+    const uint32_t *tw = reinterpret_cast<const uint32_t *>(v.sc_type);
+    const u64x2 *kw = reinterpret_cast<const u64x2 *>(v.sc_key);
+    const u32x4 *iw = reinterpret_cast<const u32x4 *>(v.sc_idx);
+    uint32_t ty[WR];
+    u64x2 k0[WR], k1[WR];
+    u32x4 ix[WR];
 #pragma unroll
-    for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {             // all loads in flight at once
-        const uint64_t g = wb + 64 * r;
-        ty[r] = SC_NONE; ky[r] = 0; ix[r] = 0;
-        if (g < end) { ty[r] = v.sc_type[g]; ky[r] = v.sc_key[g]; ix[r] = v.sc_idx[g]; }
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
-        uint64_t p, s;
-        contrib(ty[r], ky[r], p, s);
-        lp = lp > p ? lp : p;
-        ls = ls > s ? ls : s;
-        lty[lb + 64 * r] = ty[r];
-        lky[lb + 64 * r] = ky[r];
-        lix[lb + 64 * r] = ix[r];
+    for (uint32_t i = 0; i < WR; ++i) {                      // all loads in flight at once
+        const uint64_t wd = w0 + threadIdx.x + 256ull * i;
+        ty[i] = 0; k0[i] = u64x2{0, 0}; k1[i] = u64x2{0, 0}; ix[i] = u32x4{0, 0, 0, 0};
+        if (wd < w1) { ty[i] = tw[wd]; k0[i] = kw[2 * wd]; k1[i] = kw[2 * wd + 1]; ix[i] = iw[wd]; }
     }
     // carry-in = max over the node's earlier chunk aggregates (k_scan_chunk),
-    // read here from L2 instead of a separate per-node scan kernel
-    // — O(chunks^2) per node, so a node with more than SCAN_INLINE_CHUNKS
-    // chunks reads the carry k_scan_node computed instead (v.scan_node_pass)
+    // read here from L2 instead of a separate per-node scan kernel (its loads in flight
+    // with the staging loads) — O(chunks^2) per node, so a node with more than
+    // SCAN_INLINE_CHUNKS chunks reads the carry k_scan_node computed instead (v.scan_node_pass)
     const uint32_t cn = v.chunk_node[c];
     const uint32_t c0 = v.node_chunk_off[cn], c1 = v.node_chunk_off[cn + 1];
     uint64_t xp = 0, xs = 0;
@@ -496,6 +511,32 @@ __device__ inline void scan_apply_chunk(const DevView &v, const uint32_t c, uint
             xp = xp > ap ? xp : ap;
             xs = xs > as ? xs : as;
         }
+    }
+    const uint32_t len = (uint32_t)(end - beg);
+#pragma unroll
+    for (uint32_t i = 0; i < WR; ++i) {
+        const uint64_t g0 = 4 * (w0 + threadIdx.x + 256ull * i);
+        const uint64_t key[4] = {k0[i].x, k0[i].y, k1[i].x, k1[i].y};
+        const uint32_t idx[4] = {ix[i].x, ix[i].y, ix[i].z, ix[i].w};
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (g0 + j >= beg && g0 + j < end) {
+                const uint32_t o = (uint32_t)(g0 + j - beg);
+                lty[o] = (uint8_t)(ty[i] >> (8 * j));
+                lky[o] = key[j];
+                lix[o] = idx[j];
+            }
+    }
+    for (uint32_t o = len + threadIdx.x; o < SCAN_CHUNK; o += 256) { lty[o] = SC_NONE; lky[o] = 0; }
+    __syncthreads();
+    // the wave's own records (its SCAN_CHUNK / 4, 64 per round): its maxima
+    uint64_t lp = 0, ls = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
+        uint64_t p, s;
+        contrib(lty[lb + 64 * r], lky[lb + 64 * r], p, s);
+        lp = lp > p ? lp : p;
+        ls = ls > s ? ls : s;
     }
     xp = wave_max(xp);
     xs = wave_max(xs);
@@ -519,7 +560,7 @@ __device__ inline void scan_apply_chunk(const DevView &v, const uint32_t c, uint
     for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
         const uint64_t g = wb + 64 * r;
         if (!__ballot(g < end)) break;
-        const uint8_t t = lty[lb + 64 * r];    // written by this lane: no barrier needed
+        const uint8_t t = lty[lb + 64 * r];    // staged above, before the barrier
         const uint64_t key = lky[lb + 64 * r];
         const uint32_t kind = t & SC_KIND;
         uint64_t p, s;
@@ -871,7 +912,6 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
 
 constexpr uint32_t SPL = BS / 64;
 static_assert(SPL == SPL_, "4 slots per lane");
-typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));          // slots per lane: slot = lane + 64 * j
 
 // slots of this lane that fragment (start, count, dense) covers: k[j] = entry
 // offset within the fragment or -1.  Sparse runs scatter through the wave's
@@ -1033,7 +1073,6 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // N <= FAST_MAX_NODES, the pair has at most FAST_MAX_FRAGS fragments, all dense
 // ACCEPT / COMMIT runs and its node has no PREPARE after the first of them —
 // its snapshot events see empty state, so skipping them changes no output.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t FAST_PAIR_FRAGS = 2;      // descriptors a pair lane prefetches
 constexpr uint64_t EV_BIT = 1ull << 63;      // k_apply_fast: pair_gp folded into the lane's CSR offset
 constexpr uint64_t DONE_BIT = 1ull << 62;    // ... and (AFTER_STORE) "k_plan planned this pair"
