@@ -81,7 +81,7 @@ def parse():
                     help="also time rank 0's shard of the same trace at world G on this GPU (a 1-GPU scaling "
                          "projection, no RCCL); 0 / 1 = skip")
     ap.add_argument("--shard-only", action="store_true", help="only the shard projection (profiling)")
-    ap.add_argument("--events-every", type=int, default=4,
+    ap.add_argument("--events-every", type=int, default=8,
                     help="phase events (HIP start / stop timestamps on the kernels) on every k-th timed step of "
                          "the C4 and shard loops: each costs the step ~1.5-2 us (mpx_timing_every)")
     return ap.parse_args()
