@@ -1077,3 +1077,92 @@ def test_engine_commits_clean_device_trace():
         e.load_clean_device(num_instances=M, batch=256)
         e.run()
         assert e.commits_at(e.commit_points()) == e.commits()
+
+
+# ---- closed loop (the engine's decisions drive the next messages) ----
+def test_closed_loop_contending_proposers_match_reference():
+    """mpx.loop.ClosedLoop: node 0 prepares with four client values queued, its phase-2 batch
+    (the engine's decision) reaches only 2 of 5 acceptors; node 1 prepares higher with two
+    values of its own — its quorum adopts node 0's half-accepted values (the engine's merge)
+    and queues its own after them; the batch is chosen and committed.  Every node executes
+    a0..a3, b0, b1 in order; the recorded streams, replayed through the reference's own
+    handlers, give the engine's result and the reference's decisions equal the engine's."""
+    from mpx.loop import ClosedLoop
+    import mpxd
+    L = ClosedLoop(5, 64)
+    try:
+        L.prepare(0, range(5))
+        for i in range(4):
+            L.propose(0, "a%d" % i)
+        L.run(); L.run()                               # promises -> node 0's quorum
+        assert L.accept_decided(0, [0, 1]) == 1        # reaches 2 of 5: no quorum
+        L.run(); L.run()
+        assert not L.commit_chosen(0, range(5))
+        L.prepare(1, range(5))
+        L.propose(1, "b0"); L.propose(1, "b1")
+        L.run(); L.run()                               # node 1's quorum merges node 0's values
+        d1 = mpxd.parse(L.engine.decisions())[1][-1][1]
+        assert [iid for iid, _ in d1] == list(range(6))
+        assert [h >> 48 for _, h in d1] == [0, 0, 0, 0, 1, 1]
+        assert L.accept_decided(1, range(5)) == 1
+        L.run(); L.run()
+        assert L.commit_chosen(1, range(5)) == [1]
+        L.run(); L.run()
+        want = [b"a0", b"a1", b"a2", b"a3", b"b0", b"b1"]
+        for n in range(5):
+            fr, handles = L.engine.read_executed(n)
+            assert fr == 6 and [L.payload[(h >> 48, h & ((1 << 47) - 1))] for h in handles] == want
+        trace = L.trace()
+        from oracles import oracle_run, ref_available
+        assert L.engine.dump() == oracle_run(trace)[0]
+        if ref_available():
+            from oracles import ref_decisions, ref_run
+            assert L.engine.dump() == ref_run(trace)[0]
+            assert L.engine.decisions() == ref_decisions(trace)
+    finally:
+        L.close()
+
+
+@pytest.mark.parametrize("seed", [3, 5, 7])
+def test_closed_loop_random_schedule_matches_oracle(seed):
+    """Random closed-loop schedules: three proposers prepare, propose client values, send the
+    engine's decided batches and commit what the engine found chosen, each to a random subset
+    of the five acceptors.  The streams replayed through the C oracle give the engine's result,
+    decisions and commits; the executed streams are prefixes of one another (safety); with the
+    reference built, its own handlers agree too (these seeds: no ASSERT case, checked on CPU)."""
+    import random
+    from mpx.loop import ClosedLoop
+    from oracles import oracle_commits, oracle_decisions, oracle_run, ref_available
+    rng = random.Random(seed)
+    L = ClosedLoop(5, 256)
+    try:
+        vals = 0
+        for _ in range(40):
+            p = rng.randrange(3)
+            to = sorted(rng.sample(range(5), rng.randint(2, 5)))
+            op = rng.random()
+            if op < 0.2:
+                L.prepare(p, to)
+                for _ in range(rng.randint(0, 3)):
+                    L.propose(p, "v%d" % vals)
+                    vals += 1
+            elif op < 0.65 and L.engine is not None:
+                L.accept_decided(p, to)
+            elif L.engine is not None:
+                L.commit_chosen(p, to)
+            L.run(); L.run()
+        trace = L.trace()
+        want, _st, viol = oracle_run(trace)
+        assert L.engine.dump() == want and viol[0] == 0
+        assert L.engine.decisions() == oracle_decisions(trace)
+        assert L.engine.commits() == oracle_commits(trace)
+        ex = [L.engine.read_executed(n)[1] for n in range(5)]
+        longest = max(ex, key=len)
+        assert all(e == longest[:len(e)] for e in ex)
+        assert len(L.batches) >= 2
+        if ref_available():
+            from oracles import ref_decisions, ref_run
+            assert L.engine.dump() == ref_run(trace)[0]
+            assert L.engine.decisions() == ref_decisions(trace)
+    finally:
+        L.close()
