@@ -13,6 +13,7 @@ The promise quorums and merged maps come from an MPXR result (what the device co
 Checked against the reference's own decisions (tests/golden/*.mpxd) on CPU; the engine's
 host walk (engine.cpp member_decisions) is the same algorithm.
 """
+import bisect
 import struct
 
 import mpxr
@@ -22,30 +23,52 @@ INF = (1 << 64) - 1
 
 
 class IdSet:
-    """AvailableInstanceIDs (multi/paxos.cpp:253-318): disjoint [a, b) ranges."""
+    """AvailableInstanceIDs (multi/paxos.cpp:253-318): disjoint [a, b) ranges, kept as sorted
+    start / end lists (binary search)."""
 
     def __init__(self):
-        self.r = [[0, INF]]
+        self.a, self.b = [0], [INF]
 
     def copy(self):
         c = IdSet()
-        c.r = [list(x) for x in self.r]
+        c.a, c.b = list(self.a), list(self.b)
         return c
 
+    @property
+    def r(self):
+        return list(zip(self.a, self.b))
+
+    def _find(self, i):
+        k = bisect.bisect_right(self.a, i) - 1
+        return k if k >= 0 and i < self.b[k] else -1
+
     def contains(self, i):
-        return any(a <= i < b for a, b in self.r)
+        return self._find(i) >= 0
 
     def remove(self, i):
-        for k, (a, b) in enumerate(self.r):
-            if a <= i < b:
-                rep = ([[a, i]] if a != i else []) + ([[i + 1, b]] if i + 1 != b else [])
-                self.r[k:k + 1] = rep
-                return
+        k = self._find(i)
+        if k < 0:
+            return
+        a, b = self.a[k], self.b[k]
+        if a != i and i + 1 != b:
+            self.b[k] = i
+            self.a.insert(k + 1, i + 1)
+            self.b.insert(k + 1, b)
+        elif a != i:
+            self.b[k] = i
+        elif i + 1 != b:
+            self.a[k] = i + 1
+        else:
+            del self.a[k], self.b[k]
 
     def next(self):
-        a = self.r[0][0]
+        a = self.a[0]
         self.remove(a)
         return a
+
+    def pop_first(self):
+        a, b = self.a.pop(0), self.b.pop(0)
+        return a, b
 
 
 def _value(m, pos):
@@ -125,8 +148,8 @@ def decisions(trace, result):
                     if un.contains(iid):
                         un.remove(iid)
                         batch.append((iid, h))
-                while len(un.r) != 1:
-                    a, e = un.r.pop(0)
+                while len(un.a) != 1:
+                    a, e = un.pop_first()
                     for i in range(a, e):
                         st["vid"] += 1
                         batch.append((i, (n << 48) | (1 << 47) | st["vid"]))

@@ -1166,3 +1166,21 @@ def test_closed_loop_random_schedule_matches_oracle(seed):
             assert L.engine.decisions() == ref_decisions(trace)
     finally:
         L.close()
+
+
+@pytest.mark.timeout(300)
+def test_member_learns_and_decisions_at_2_18_match_restatements():
+    """The member proposer bookkeeping at 2^18 instances (C5's schedule and fault rates, 8 nodes,
+    15 epochs): the engine's learns and phase-2 decisions == the oracle/ restatements (pinned to
+    the reference's fixtures) over the C oracle's quorums — about 2 M decided entries."""
+    from oracles import oracle_run
+    import learns_model
+    import member_decisions_model
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=8, num_instances=1 << 18, seed=0, batch=256,
+                           drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15)
+    r = oracle_run(t)[0]
+    with mpx.Engine.for_trace(t) as e:
+        e.run()
+        assert e.dump() == r
+        assert e.learns() == learns_model.learns(t, r)
+        assert e.decisions() == member_decisions_model.decisions(t, r)
