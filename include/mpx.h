@@ -141,7 +141,7 @@ typedef struct mpx_config {
     uint64_t shard_begin;      /* this engine owns instances [shard_begin,         */
     uint64_t shard_end;        /*                              shard_end)          */
     uint32_t num_epochs;       /* member only                                      */
-    uint32_t flags;            /* 0, or MPX_FLAG_INCREMENTAL (multi semantics)     */
+    uint32_t flags;            /* 0, or MPX_FLAG_INCREMENTAL [| MPX_FLAG_DECISIONS] (multi) */
     const mpx_epoch *epochs;   /* member only, indexed by E_EPOCH's epoch          */
 } mpx_config;
 
@@ -157,6 +157,11 @@ typedef struct mpx_config {
  * once), mpx_dump_result, the decisions and commits readbacks (they walk the run's
  * history). */
 #define MPX_FLAG_INCREMENTAL 1u
+/* With MPX_FLAG_INCREMENTAL: every mpx_run also advances the proposers' phase-2
+ * bookkeeping over the window's events (the quorums' merged maps, COMMIT entries,
+ * client values), so mpx_read_decisions returns the decisions of every window so far —
+ * the MPXD of one run over the whole stream (host work per window, O(window)). */
+#define MPX_FLAG_DECISIONS 2u
 
 typedef struct mpx_engine mpx_engine;
 

@@ -60,6 +60,12 @@ struct StepEvents { hipEvent_t e[5]; };   // launch_run's event points
 
 }  // namespace
 
+struct PropNode;
+static std::vector<PropNode> *prop_new(uint32_t nodes);
+static void prop_free(std::vector<PropNode> *p);
+struct mpx_engine;
+static int prop_window(mpx_engine *e);
+
 struct mpx_engine {
     mpx_config cfg{};
     std::vector<mpx_epoch> epochs;
@@ -113,6 +119,7 @@ struct mpx_engine {
     DevBuf b_gid, g_mask, g_done, gp_base, cb_list, outv, outv_n;
     uint64_t g_cap = 0;                     // global batches g_mask / g_done hold
     std::vector<uint64_t> seq_base, win_seq_base;
+    std::vector<PropNode> *prop = nullptr;           // MPX_FLAG_DECISIONS: the bookkeeping carried across windows
     uint64_t windows = 0;
     uint64_t events_every = 1, step_no = 0;   // mpx_timing_every
 };
@@ -152,7 +159,8 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
     if (cfg->shard_end <= cfg->shard_begin) return MPX_E_INVAL;
     if (cfg->semantics != MPX_SEM_MULTI && cfg->semantics != MPX_SEM_MEMBER) return MPX_E_INVAL;
     if (cfg->semantics == MPX_SEM_MULTI && cfg->num_epochs) return MPX_E_INVAL;
-    if (cfg->flags & ~(uint32_t)MPX_FLAG_INCREMENTAL) return MPX_E_INVAL;
+    if (cfg->flags & ~(uint32_t)(MPX_FLAG_INCREMENTAL | MPX_FLAG_DECISIONS)) return MPX_E_INVAL;
+    if ((cfg->flags & MPX_FLAG_DECISIONS) && !(cfg->flags & MPX_FLAG_INCREMENTAL)) return MPX_E_INVAL;
     if ((cfg->flags & MPX_FLAG_INCREMENTAL) && cfg->semantics != MPX_SEM_MULTI) return MPX_E_INVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPX_E_NODEVICE;
@@ -177,6 +185,7 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
         // entries and 16 B for a promise round's pre-accepted map, 8 B per instance of
         // chosen log (all zero: the PaxosImpl ctor state, multi/paxos.cpp:323-346)
         e->incremental = true;
+        if (cfg->flags & MPX_FLAG_DECISIONS) e->prop = prop_new(cfg->num_nodes);
         e->wc.init(cfg->num_nodes, e->NB);
         e->seq_base.assign(cfg->num_nodes, 0);
         const uint64_t NL = (uint64_t)cfg->num_nodes * e->shard_len;
@@ -203,6 +212,7 @@ extern "C" int mpx_destroy(mpx_engine *e)
     for (auto &s : e->ev_pool) for (auto ev : s.e) (void)hipEventDestroy(ev);
     if (e->comm) ncclCommDestroy(e->comm);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+    prop_free(e->prop);
     delete e;
     return MPX_OK;
 }
@@ -743,6 +753,7 @@ extern "C" int mpx_run(mpx_engine *e)
         e->dirty = true;
         TRY(queue_run(e, false));
         TRY(collect(e));
+        if (e->prop) TRY(prop_window(e));
         // batches chosen in this window need their entries no more
         std::vector<uint32_t> bc;
         TRY(d2h(bc, e->b_chosen, e->ht.b_gid.size()));
@@ -1435,7 +1446,7 @@ static void proposer_events(mpx_engine *e, const Results &r, PEvents &ev)
             const uint8_t t = h.m_type[g];
             const bool quorum = t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM);
             if (t != MPX_MSG_P_PROPOSE && t != MPX_MSG_P_START && t != MPX_MSG_COMMIT && !quorum) continue;
-            PEv x{seq_of(h, n, g), t, {}};
+            PEv x{seq_of(h, n, g) + (e->incremental ? e->win_seq_base[n] : 0), t, {}};
             if (t == MPX_MSG_COMMIT)
                 for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) x.ents.push_back({h.e_iid[k], h.e_val[k]});
             if (quorum) {
@@ -1448,71 +1459,104 @@ static void proposer_events(mpx_engine *e, const Results &r, PEvents &ev)
         }
 }
 
-static void proposer_sim(const PEvents &ev, std::string &d)
+// The proposer's bookkeeping of one node, advanced over its events in stream order (a whole
+// run at once, or window by window: MPX_FLAG_DECISIONS); each promise quorum appends its
+// MPXD record to `body`
+struct PropNode {
+    IdSet uncommitted, unproposed;
+    std::map<uint64_t, uint64_t> initial;              // initial_proposals_: instance -> value id
+    std::set<uint64_t> newly, committed;               // newly_proposed_values_; committed instances
+    uint64_t vid = 0;                                   // value_id_ (:335)
+    bool preparing = false;                             // prepare_retry_timeout_ != NULL
+    std::string body;
+    uint64_t count = 0;
+};
+
+static void prop_advance(PropNode &st, uint32_t n, const std::vector<PEv> &evs)
 {
-    const uint32_t N = (uint32_t)ev.size();
-    d.append("MPXD", 4);
-    app<uint32_t>(d, 1); app<uint32_t>(d, N);
-    for (uint32_t n = 0; n < N; ++n) {
-        IdSet uncommitted, unproposed;
-        std::map<uint64_t, uint64_t> initial;              // initial_proposals_: instance -> value id
-        std::set<uint64_t> newly, committed;               // newly_proposed_values_; committed instances
-        uint64_t vid = 0;                                   // value_id_ (:335)
-        bool preparing = false;                             // prepare_retry_timeout_ != NULL
-        std::string body;
-        uint64_t count = 0;
-        for (const PEv &x : ev[n]) {
-            const uint32_t t = x.type;
-            if (t == MPX_MSG_P_PROPOSE) {
-                ++vid;
-                if (!preparing) initial[unproposed.next()] = vid;
-                else newly.insert(vid);
-            } else if (t == MPX_MSG_P_START) {
-                preparing = true;
-            } else if (t == MPX_MSG_COMMIT) {
-                for (auto &en : x.ents) {
-                    const uint64_t iid = en.first, hv = en.second;
-                    if (committed.insert(iid).second && uncommitted.contains(iid)) uncommitted.remove(iid);
-                    if (unproposed.contains(iid)) unproposed.remove(iid);
-                    auto it = initial.find(iid);
-                    if (it != initial.end()) {
-                        const uint64_t v0 = it->second;
-                        initial.erase(it);
-                        if (MPX_HANDLE_PROPOSER(hv) != n || MPX_HANDLE_VALUE_ID(hv) != v0) {
-                            if (!preparing) initial[unproposed.next()] = v0;
-                            else newly.insert(v0);
-                        }
+    IdSet &uncommitted = st.uncommitted, &unproposed = st.unproposed;
+    auto &initial = st.initial;
+    auto &newly = st.newly, &committed = st.committed;
+    uint64_t &vid = st.vid;
+    bool &preparing = st.preparing;
+    for (const PEv &x : evs) {
+        const uint32_t t = x.type;
+        if (t == MPX_MSG_P_PROPOSE) {
+            ++vid;
+            if (!preparing) initial[unproposed.next()] = vid;
+            else newly.insert(vid);
+        } else if (t == MPX_MSG_P_START) {
+            preparing = true;
+        } else if (t == MPX_MSG_COMMIT) {
+            for (auto &en : x.ents) {
+                const uint64_t iid = en.first, hv = en.second;
+                if (committed.insert(iid).second && uncommitted.contains(iid)) uncommitted.remove(iid);
+                if (unproposed.contains(iid)) unproposed.remove(iid);
+                auto it = initial.find(iid);
+                if (it != initial.end()) {
+                    const uint64_t v0 = it->second;
+                    initial.erase(it);
+                    if (MPX_HANDLE_PROPOSER(hv) != n || MPX_HANDLE_VALUE_ID(hv) != v0) {
+                        if (!preparing) initial[unproposed.next()] = v0;
+                        else newly.insert(v0);
                     }
                 }
-            } else {                                        // a promise quorum
-                unproposed = uncommitted;
-                std::vector<std::pair<uint64_t, uint64_t>> b;
-                for (auto &en : x.ents)
-                    if (unproposed.contains(en.first)) { unproposed.remove(en.first); b.push_back(en); }
-                while (unproposed.r.size() > 1) {
-                    const auto first = *unproposed.r.begin();
-                    unproposed.r.erase(unproposed.r.begin());
-                    for (uint64_t id = first.first; id != first.second; ++id) b.push_back({id, MPX_HANDLE(n, 1, ++vid)});
-                }
-                for (auto &y : initial)
-                    if (unproposed.contains(y.first)) { unproposed.remove(y.first); b.push_back({y.first, MPX_HANDLE(n, 0, y.second)}); }
-                for (uint64_t v : newly) {
-                    const uint64_t iid = unproposed.next();
-                    initial[iid] = v;
-                    b.push_back({iid, MPX_HANDLE(n, 0, v)});
-                }
-                newly.clear();
-                preparing = false;
-                std::sort(b.begin(), b.end());                 // AcceptingValues::values_ is a map
-                app<uint64_t>(body, x.seq);
-                app<uint64_t>(body, b.size());
-                for (auto &y : b) { app<uint64_t>(body, y.first); app<uint64_t>(body, y.second); }
-                ++count;
             }
+        } else {                                        // a promise quorum
+            unproposed = uncommitted;
+            std::vector<std::pair<uint64_t, uint64_t>> b;
+            for (auto &en : x.ents)
+                if (unproposed.contains(en.first)) { unproposed.remove(en.first); b.push_back(en); }
+            while (unproposed.r.size() > 1) {
+                const auto first = *unproposed.r.begin();
+                unproposed.r.erase(unproposed.r.begin());
+                for (uint64_t id = first.first; id != first.second; ++id) b.push_back({id, MPX_HANDLE(n, 1, ++vid)});
+            }
+            for (auto &y : initial)
+                if (unproposed.contains(y.first)) { unproposed.remove(y.first); b.push_back({y.first, MPX_HANDLE(n, 0, y.second)}); }
+            for (uint64_t v : newly) {
+                const uint64_t iid = unproposed.next();
+                initial[iid] = v;
+                b.push_back({iid, MPX_HANDLE(n, 0, v)});
+            }
+            newly.clear();
+            preparing = false;
+            std::sort(b.begin(), b.end());                 // AcceptingValues::values_ is a map
+            app<uint64_t>(st.body, x.seq);
+            app<uint64_t>(st.body, b.size());
+            for (auto &y : b) { app<uint64_t>(st.body, y.first); app<uint64_t>(st.body, y.second); }
+            ++st.count;
         }
-        app<uint64_t>(d, count);
-        d += body;
     }
+}
+
+static std::vector<PropNode> *prop_new(uint32_t nodes) { return new std::vector<PropNode>(nodes); }
+static void prop_free(std::vector<PropNode> *p) { delete p; }
+
+static void prop_bytes(const std::vector<PropNode> &st, std::string &d)
+{
+    d.append("MPXD", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, (uint32_t)st.size());
+    for (auto &x : st) { app<uint64_t>(d, x.count); d += x.body; }
+}
+
+static void proposer_sim(const PEvents &ev, std::string &d)
+{
+    std::vector<PropNode> st(ev.size());
+    for (uint32_t n = 0; n < ev.size(); ++n) prop_advance(st[n], n, ev[n]);
+    prop_bytes(st, d);
+}
+
+// MPX_FLAG_DECISIONS: the proposers' bookkeeping advanced over the last window's events (its
+// quorums' merged maps carry the pre-accepted values of earlier windows, k_apply_win)
+static int prop_window(mpx_engine *e)
+{
+    Results r;
+    TRY(fetch_results(e, r));
+    PEvents ev;
+    proposer_events(e, r, ev);
+    for (uint32_t n = 0; n < e->cfg.num_nodes; ++n) prop_advance((*e->prop)[n], n, ev[n]);
+    return MPX_OK;
 }
 
 static int proposer_decisions(mpx_engine *e, const Results &r, std::string &d)
@@ -1660,7 +1704,12 @@ static int member_decisions(mpx_engine *e, const Results &r, std::string &d)
 extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
-    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
+    if (e->incremental) {                               // windows keep no history of runs, but
+        if (!e->prop || e->cfg.shard_begin != 0) return MPX_E_STATE;   // MPX_FLAG_DECISIONS carries the
+        std::string d;                                  // bookkeeping: every window's quorums so far
+        prop_bytes(*e->prop, d);
+        return put_bytes(d, out, size);
+    }
     if (e->cfg.shard_begin != 0) return MPX_E_STATE;
     if (e->cfg.semantics == MPX_SEM_MEMBER) {
         if (!e->whole) return MPX_E_STATE;               // the learner's whole learned set

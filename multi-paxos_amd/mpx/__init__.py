@@ -21,6 +21,7 @@ INCLUDE_H = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "mpx
 ABI_VERSION = 2
 SEM_MULTI, SEM_MEMBER = 0, 1
 FLAG_INCREMENTAL = 1            # mpx_config.flags: each mpx_run applies one window (include/mpx.h)
+FLAG_DECISIONS = 2              # with FLAG_INCREMENTAL: decisions carried across windows
 GEN_CLEAN, GEN_FAULTY, GEN_MEMBER = 0, 1, 2
 PRESENT = 1 << 63
 UID_BYTES = 128

@@ -17,13 +17,16 @@ every message it sends is made from what the engine computed —
 Deliveries may reach only some acceptors, so rounds of different proposers contend and the next
 quorum adopts what the last one left half-accepted.  The loop only moves bytes: promises,
 quorums, merges, decisions, votes and the chosen log all come from the device.  Each step
-re-runs the engine over the streams so far (an MPXT trace, `trace()`); replayed through the
-reference's own handlers that trace gives the engine's result byte for byte (tests).
+re-runs the engine over the streams so far (an MPXT trace, `trace()`), or with
+`incremental=True` submits only the records added since the last step to one engine
+(MPX_FLAG_INCREMENTAL | MPX_FLAG_DECISIONS: state, promise rounds and the decisions'
+bookkeeping carried across windows, O(window) per step).  Replayed through the reference's
+own handlers the recorded trace gives the engine's result byte for byte (tests).
 """
 import ctypes
 import struct
 
-from . import Engine, lib, _ck
+from . import FLAG_DECISIONS, FLAG_INCREMENTAL, Engine, lib, _ck
 
 INF = (1 << 64) - 1
 
@@ -53,8 +56,10 @@ def _parse_mpxd(b):
 class ClosedLoop:
     """N nodes (multi semantics; every node an acceptor and learner), instances [0, M)."""
 
-    def __init__(self, num_nodes, num_instances):
+    def __init__(self, num_nodes, num_instances, incremental=False):
         self.N, self.M = num_nodes, num_instances
+        self.incremental = incremental
+        self.submitted = [0] * num_nodes              # incremental: records of each stream already submitted
         self.streams = [[] for _ in range(num_nodes)]
         self.delivered = {}                           # src -> replies of src already routed
         self.ballot_count = [0] * num_nodes
@@ -84,7 +89,19 @@ class ClosedLoop:
         return bytes(out)
 
     def run(self):
-        """Re-run the engine over every stream so far; route the new replies to their nodes."""
+        """Re-run the engine over every stream so far (or, incremental, one window of the records
+        added since the last step); route the new replies to their nodes."""
+        if self.incremental:
+            if self.engine is None:
+                self.engine = Engine(self.N, 0, self.M, flags=FLAG_INCREMENTAL | FLAG_DECISIONS)
+            for n, msgs in enumerate(self.streams):
+                if len(msgs) > self.submitted[n]:
+                    self.engine.submit(n, msgs[self.submitted[n]:])
+                    self.submitted[n] = len(msgs)
+            st = self.engine.run()
+            for _src, dst, b in self.engine.drain_sends():   # a window's replies are all new
+                self.streams[dst].append(b)
+            return st
         if self.engine is not None:
             self.engine.close()
         self.engine = Engine.for_trace(self.trace())

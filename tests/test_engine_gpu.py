@@ -854,6 +854,34 @@ def _windows(trace, fracs, times=None):
 MULTI_GOLDENS = sorted(k for k in INDEX if not k.startswith(("c5_", "mm_")) and "member" not in k)
 
 
+@pytest.mark.parametrize("name", sorted(k for k in DECISIONS if not k.startswith(("c5_", "mm_"))))
+def test_incremental_windows_carry_decisions(name):
+    """MPX_FLAG_DECISIONS: every multi golden with a promise quorum (client values included)
+    cut into 2 and 4 windows — the proposers' bookkeeping advanced window by window over the
+    device's quorums and merged maps gives the reference's decisions (fixture); without the
+    flag a window engine keeps no decisions."""
+    want = _read(name, ".mpxd")
+    hd, _epochs, streams = _node_streams(_read(name, ".mpxt"))
+    n, m = hd["num_nodes"], max(hd["num_instances"], 1)
+    for fracs in ((0.5,), (0.2, 0.45, 0.8)):
+        with mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL | mpx.FLAG_DECISIONS) as e:
+            prev = [0] * n
+            for f in list(fracs) + [1.0]:
+                cut = [len(s) if f >= 1.0 else int(len(s) * f) for s in streams]
+                for node, st in enumerate(streams):
+                    if cut[node] > prev[node]:
+                        e.submit(node, st[prev[node]:cut[node]])
+                e.run()
+                prev = cut
+            assert e.decisions() == want, fracs
+    with mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL) as e:
+        for node, st in enumerate(streams):
+            e.submit(node, st)
+        e.run()
+        with pytest.raises(mpx.MpxError):
+            e.decisions()
+
+
 @pytest.mark.parametrize("name", MULTI_GOLDENS)
 def test_incremental_windows_match_whole(name):
     """Every multi golden cut into 1, 2 and 4 windows: the replies of the windows, node by
@@ -1184,3 +1212,42 @@ def test_member_learns_and_decisions_at_2_18_match_restatements():
         assert e.dump() == r
         assert e.learns() == learns_model.learns(t, r)
         assert e.decisions() == member_decisions_model.decisions(t, r)
+
+
+def test_closed_loop_incremental_equals_replay():
+    """The closed loop on one incremental engine (MPX_FLAG_INCREMENTAL | MPX_FLAG_DECISIONS:
+    each step submits only the new records) makes the same moves as the replaying loop: the
+    same streams and decisions, and the streams replayed whole give the C oracle's result."""
+    import random
+    from mpx.loop import ClosedLoop
+    from oracles import oracle_decisions, oracle_run
+
+    def play(incremental):
+        rng = random.Random(5)
+        L = ClosedLoop(5, 256, incremental=incremental)
+        vals = 0
+        for _ in range(40):
+            p = rng.randrange(3)
+            to = sorted(rng.sample(range(5), rng.randint(2, 5)))
+            op = rng.random()
+            if op < 0.2:
+                L.prepare(p, to)
+                for _ in range(rng.randint(0, 3)):
+                    L.propose(p, "v%d" % vals)
+                    vals += 1
+            elif op < 0.65 and L.engine is not None:
+                L.accept_decided(p, to)
+            elif L.engine is not None:
+                L.commit_chosen(p, to)
+            L.run(); L.run()
+        out = (L.trace(), L.engine.decisions(), len(L.batches), len(L.committed))
+        L.close()
+        return out
+
+    a, b = play(False), play(True)
+    assert a == b
+    assert a[2] >= 2
+    assert oracle_decisions(a[0]) == b[1]
+    with mpx.Engine.for_trace(a[0]) as e:
+        e.run()
+        assert e.dump() == oracle_run(a[0])[0]
