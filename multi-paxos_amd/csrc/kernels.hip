@@ -1033,12 +1033,13 @@ __device__ inline uint64_t slot_digest(const DevView &v, uint32_t n, uint64_t ii
 // Wave id with consecutive ids on one XCD: workgroups are dealt round-robin
 // over the 8 XCDs (blockIdx % 8), so id = xcd * (waves per XCD) + local id.
 // Neighbouring buckets then share their XCD's L2 (headers, descriptors).
-__device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
+__device__ inline uint64_t xcd_wave_id_g(uint32_t wv, uint32_t grid, uint32_t knobs = 0)
 {
-    if ((gridDim.x & 7) || (knobs & 1)) return (uint64_t)blockIdx.x * 4 + wv;
-    const uint64_t per = (uint64_t)(gridDim.x >> 3) * 4;
+    if ((grid & 7) || (knobs & 1)) return (uint64_t)blockIdx.x * 4 + wv;
+    const uint64_t per = (uint64_t)(grid >> 3) * 4;
     return (uint64_t)(blockIdx.x & 7) * per + (uint64_t)(blockIdx.x >> 3) * 4 + wv;
 }
+__device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0) { return xcd_wave_id_g(wv, gridDim.x, knobs); }
 
 // Lean acceptor/learner apply plus the chosen log, G consecutive buckets per
 // wave step (fast_group: G * N + 1 <= 64, at most 4).
@@ -1983,17 +1984,31 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
 // of a store is one segment (batch 256) its low half is the 16 bytes; else
 // plan_bytes16 expands the segments.  Tail buckets of a row go through the
 // per-bucket loop.
-template <bool NT, uint32_t C = 64>
-__global__ __launch_bounds__(256) void k_store8(DevView v)
+template <uint32_t W>
+__device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, unsigned long long (&red)[W][8],
+                                      uint32_t row0, uint32_t stride, bool scal);
+
+// REDUCE: workgroups [store_grid, gridDim.x) fold the partials into the summary (k_reduce's
+// work) while the others store — launched when the store is the step's last kernel, so the
+// summary's dependent launch and its ramp leave the chain (the partials are all written by
+// the kernels before it)
+template <bool NT, uint32_t C = 64, bool REDUCE = false>
+__global__ __launch_bounds__(256) void k_store8(DevView v, uint32_t store_grid, uint32_t n_partials)
 {
     static_assert(C == 64 || C == 128, "one or two plan words per lane");
+    if (REDUCE && blockIdx.x >= store_grid) {
+        __shared__ unsigned long long red[4][8];
+        const uint32_t r = blockIdx.x - store_grid, R = gridDim.x - store_grid;
+        reduce_summary<4>(v, n_partials, red, 256 * r, 256 * R, r == 0);
+        return;
+    }
     const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t N = v.N;
 
     const uint64_t whole = v.shard_len >> BSH;
     const uint64_t cpr = whole / C, S = (uint64_t)(N + 1) * cpr;
-    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
-    const uint64_t wid = xcd_wave_id(wv, v.knobs);
+    const uint64_t nwaves = (uint64_t)store_grid * 4;
+    const uint64_t wid = xcd_wave_id_g(wv, store_grid, v.knobs);
     uint8_t *const st = static_cast<uint8_t *>(v.st);
     uint8_t *const sink = reinterpret_cast<uint8_t *>(v.store_dummy) + (wid & 63) * 1024 + 16 * lane;
     const uint32_t p16 = 16 * (lane & 15);                 // the lane's first slot in its bucket
@@ -3300,15 +3315,24 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     const bool plan_path = !v.digest && !(v.knobs & 64) && (member || v.N <= FAST_MAX_NODES);
     const bool lplan = plan_path && (member || (v.num_gp_snap && !(v.knobs & 8388608)));
     if (ev_apply0 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
+    // the summary folded into the store's extra workgroups when the store ends the step (the C4
+    // shape: no general pairs, no k_apply_fast, no k_chosen); knob 1073741824: k_reduce (A/B)
+    const bool skip_chosen = plan_path && v.chosen_static && !(v.knobs & (16777216 | 268435456));
+    const bool fuse_reduce = skip_chosen && !member && !lplan && v.num_gp == 0 && !(v.knobs & (4194304 | 2048 | 128 | 1073741824)) &&
+                             v.slot_w == 1;
+    const uint32_t reduce_wgs = cdiv(n_partials ? n_partials : 1, 256);
     // the plan words of every (row, bucket) -> state rows and the chosen log
     auto launch_store = [&](hipEvent_t stop) {
         if (v.slot_w == 1 && (v.knobs & 128))
             hipExtLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
         // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64
         else if (v.slot_w == 1 && (v.knobs & 2048))
-            hipExtLaunchKernelGGL((k_store8<true, 64>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
+            hipExtLaunchKernelGGL((k_store8<true, 64>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v, g.store_wgs, 0u);
+        else if (v.slot_w == 1 && fuse_reduce)
+            hipExtLaunchKernelGGL((k_store8<true, 128, true>), dim3(g.store_wgs + reduce_wgs), dim3(256), 0, s, nullptr, stop, 0, v,
+                                  g.store_wgs, n_partials);
         else if (v.slot_w == 1)
-            hipExtLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
+            hipExtLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v, g.store_wgs, 0u);
         else
             hipExtLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
     };
@@ -3409,8 +3433,11 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     // 16777216: the summary in k_chosen's last workgroup instead — measured slower (C4 tail
     // 0.075 vs 0.015 ms, C3 0.161 vs 0.071 ms: every workgroup's device-scope fence writes
     // back its XCD's L2 before the ticket), kept for A/B
-    const bool skip_chosen = plan_path && v.chosen_static && !(v.knobs & (16777216 | 268435456));
-    if (skip_chosen) {
+    if (fuse_reduce) {
+        // (phase events: the apply phase ends with the store; the general and tail phases are empty)
+        if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
+        if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, s);
+    } else if (skip_chosen) {
         hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)ev_end, 0, v, n_partials);
     } else if (!(v.knobs & 16777216)) {
