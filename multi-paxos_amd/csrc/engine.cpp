@@ -660,10 +660,6 @@ static int queue_run(mpx_engine *e, bool digest)
     e->view.knobs = 0;
     if (const char *x = std::getenv("MPX_KNOBS")) e->view.knobs = (uint32_t)std::atoi(x);
     if (const char *x = std::getenv("MPX_STORE_WGS_PER_CU")) g.store_wgs = std::max<uint32_t>(1, e->num_cus * (uint32_t)std::atoi(x));
-    g.pipe_stages = 1;                                  // (pipelined plan / store: slower)
-    g.pipe_store_wgs = e->num_cus * 2;
-    if (const char *x = std::getenv("MPX_PIPE_STAGES")) g.pipe_stages = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)std::atoi(x)));
-    if (const char *x = std::getenv("MPX_PIPE_STORE_PER_CU")) g.pipe_store_wgs = std::max<uint32_t>(1, e->num_cus * (uint32_t)std::atoi(x));
     if (const char *x = std::getenv("MPX_CHOSEN_WGS_PER_CU"))     // (partials hold 16 per CU for it too)
         g.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 16),
                                                                           (uint64_t)e->num_cus * std::atoi(x)));

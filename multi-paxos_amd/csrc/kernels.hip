@@ -1033,13 +1033,12 @@ __device__ inline uint64_t slot_digest(const DevView &v, uint32_t n, uint64_t ii
 // Wave id with consecutive ids on one XCD: workgroups are dealt round-robin
 // over the 8 XCDs (blockIdx % 8), so id = xcd * (waves per XCD) + local id.
 // Neighbouring buckets then share their XCD's L2 (headers, descriptors).
-__device__ inline uint64_t xcd_wave_id_g(uint32_t wv, uint32_t grid, uint32_t knobs = 0)
+__device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 {
-    if ((grid & 7) || (knobs & 1)) return (uint64_t)blockIdx.x * 4 + wv;
-    const uint64_t per = (uint64_t)(grid >> 3) * 4;
+    if ((gridDim.x & 7) || (knobs & 1)) return (uint64_t)blockIdx.x * 4 + wv;
+    const uint64_t per = (uint64_t)(gridDim.x >> 3) * 4;
     return (uint64_t)(blockIdx.x & 7) * per + (uint64_t)(blockIdx.x >> 3) * 4 + wv;
 }
-__device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0) { return xcd_wave_id_g(wv, gridDim.x, knobs); }
 
 // Lean acceptor/learner apply plus the chosen log, G consecutive buckets per
 // wave step (fast_group: G * N + 1 <= 64, at most 4).
@@ -1465,20 +1464,16 @@ __device__ inline void plan_chosen(const DevView &v, uint64_t i, unsigned long l
 // same way (bucket-local chosen run + 1).  Pairs with more runs or segments, a
 // re-commit (its Value check) or a partial last bucket are counted in
 // fast_rest and left to k_apply_fast<.., AFTER_STORE>.
-struct PlanLds { unsigned long long red[4][3]; uint32_t rest_w[4]; uint64_t w_lds[4][PLAN_LDS]; };
-
-// pairs [p0, p1) (bucket-major, so a bucket range), workgroup `blk` of them; the chosen-log
-// plan word of bucket i is decided by the thread of pair index i
-__device__ inline void plan_pairs(const DevView &v, uint32_t apply_wgs, PlanLds &L, uint64_t p0, uint64_t np, uint32_t blk)
+__global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
 {
     constexpr uint32_t F = PLAN_FRAGS;
-    auto &red = L.red;
-    auto &rest_w = L.rest_w;
-    auto &w_lds = L.w_lds;
+    __shared__ unsigned long long red[4][3];
+    __shared__ uint32_t rest_w[4];
+    __shared__ uint64_t w_lds[4][PLAN_LDS];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t N = v.N;
-    const uint64_t NB = v.NB;
-    const uint64_t i = p0 + (uint64_t)blk * 256 + threadIdx.x;
+    const uint64_t NB = v.NB, np = (uint64_t)N * NB;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     unsigned long long cA = 0, cL = 0, cC = 0;
     uint32_t rest = 0;
     // the wave's 64 pairs own one contiguous descriptor range: stream its
@@ -1561,7 +1556,7 @@ __device__ inline void plan_pairs(const DevView &v, uint32_t apply_wgs, PlanLds 
         if (q == PLAN_SKIP && in_list) rest = 1;
         v.plan[i] = q;
     }
-    if (i < NB && i < np) plan_chosen(v, i, cC);
+    if (i < NB) plan_chosen(v, i, cC);
     unsigned long long cc[3] = {cA, cL, cC};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -1579,17 +1574,11 @@ __device__ inline void plan_pairs(const DevView &v, uint32_t apply_wgs, PlanLds 
         const uint32_t t = threadIdx.x;
         const unsigned long long x = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         const int slot = t == 0 ? PC_A : t == 1 ? PC_L : PC_C;
-        if (x) atomicAdd(&v.partials[8 * (blk % apply_wgs) + slot], x);
+        if (x) atomicAdd(&v.partials[8 * (blockIdx.x % apply_wgs) + slot], x);
     } else if (threadIdx.x == 3) {
         const uint32_t r = rest_w[0] + rest_w[1] + rest_w[2] + rest_w[3];
         if (r) atomicAdd(v.fast_rest, r);
     }
-}
-
-__global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
-{
-    __shared__ PlanLds L;
-    plan_pairs(v, apply_wgs, L, 0, (uint64_t)v.N * v.NB, blockIdx.x);
 }
 
 // One snapshot run record (OUT_RUN): slots [lo, lo + len) of a planned pair's bucket, all
@@ -1994,32 +1983,26 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
 // of a store is one segment (batch 256) its low half is the 16 bytes; else
 // plan_bytes16 expands the segments.  Tail buckets of a row go through the
 // per-bucket loop.
-template <uint32_t W>
-__device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, unsigned long long (&red)[W][8],
-                                      uint32_t row0, uint32_t stride, bool scal);
-
-// Chunks [c0, c1) of every row (C buckets each) and, with `tails`, the buckets past the last
-// whole chunk, by wave `wid` of `nwaves`
-template <bool NT, uint32_t C>
-__device__ inline void store8_range(const DevView &v, const uint64_t wid, const uint64_t nwaves, const uint64_t c0,
-                                    uint64_t c1, const bool tails)
+template <bool NT, uint32_t C = 64>
+__global__ __launch_bounds__(256) void k_store8(DevView v)
 {
-    const uint32_t lane = threadIdx.x & 63;
+    static_assert(C == 64 || C == 128, "one or two plan words per lane");
+    const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t N = v.N;
 
     const uint64_t whole = v.shard_len >> BSH;
-    const uint64_t cpr = whole / C;
-    if (c1 > cpr) c1 = cpr;
-    const uint64_t cw = c1 > c0 ? c1 - c0 : 0, S = (uint64_t)(N + 1) * cw;
+    const uint64_t cpr = whole / C, S = (uint64_t)(N + 1) * cpr;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    const uint64_t wid = xcd_wave_id(wv, v.knobs);
     uint8_t *const st = static_cast<uint8_t *>(v.st);
     uint8_t *const sink = reinterpret_cast<uint8_t *>(v.store_dummy) + (wid & 63) * 1024 + 16 * lane;
     const uint32_t p16 = 16 * (lane & 15);                 // the lane's first slot in its bucket
     if (wid < S) {
-        uint32_t rn = (uint32_t)(wid / cw), kn = (uint32_t)(wid - (uint64_t)rn * cw);
-        const uint32_t step_r = (uint32_t)(nwaves / cw), step_k = (uint32_t)(nwaves - (uint64_t)step_r * cw);
-        // plan words of bucket (c0 + kk) * C + lane (and + 64) of row rr; past the end: a valid dummy
+        uint32_t rn = (uint32_t)(wid / cpr), kn = (uint32_t)(wid - (uint64_t)rn * cpr);
+        const uint32_t step_r = (uint32_t)(nwaves / cpr), step_k = (uint32_t)(nwaves - (uint64_t)step_r * cpr);
+        // plan words of bucket kk * C + lane (and + 64) of row rr; past the end: a valid dummy
         auto ld = [&](uint64_t cc, uint32_t rr, uint32_t kk, uint32_t off) -> uint64_t {
-            return v.plan[cc < S ? plan_idx(v, rr, (c0 + kk) * C + off + lane) : lane];
+            return v.plan[cc < S ? plan_idx(v, rr, (uint64_t)kk * C + off + lane) : lane];
         };
         uint64_t qn = ld(wid, rn, kn, 0), qn1 = C == 128 ? ld(wid, rn, kn, 64) : 0;
         __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -2027,10 +2010,10 @@ __device__ inline void store8_range(const DevView &v, const uint64_t wid, const 
             const uint64_t qw = qn, qw1 = qn1;
             const uint32_t rc = rn, kc = kn;
             rn += step_r; kn += step_k;
-            if (kn >= cw) { kn -= (uint32_t)cw; ++rn; }
+            if (kn >= cpr) { kn -= (uint32_t)cpr; ++rn; }
             qn = ld(c + nwaves, rn, kn, 0);
             if (C == 128) qn1 = ld(c + nwaves, rn, kn, 64);
-            uint8_t *const base = st + (uint64_t)rc * v.shard_len + ((c0 + kc) * C << BSH) + 16 * lane;
+            uint8_t *const base = st + (uint64_t)rc * v.shard_len + ((uint64_t)kc * C << BSH) + 16 * lane;
 #pragma unroll
             for (uint32_t j = 0; j < C / 4; ++j) {
                 const uint64_t q = __shfl(j < 16 ? qw : qw1, (int)((4 * j + (lane >> 4)) & 63), 64);
@@ -2043,10 +2026,9 @@ __device__ inline void store8_range(const DevView &v, const uint64_t wid, const 
             }
         }
     }
-    if (!tails) return;
     const uint32_t s0 = 4 * lane;
-    const uint64_t tpr = whole - cpr * C, ntails = (uint64_t)(N + 1) * tpr;
-    for (uint64_t t = wid; t < ntails; t += nwaves) {
+    const uint64_t tpr = whole - cpr * C, tails = (uint64_t)(N + 1) * tpr;
+    for (uint64_t t = wid; t < tails; t += nwaves) {
         const uint64_t r = t / tpr, b = cpr * C + (t - r * tpr);
         const uint64_t q = v.plan[plan_idx(v, (uint32_t)r, b)];
         if (q == PLAN_SKIP) continue;
@@ -2054,48 +2036,6 @@ __device__ inline void store8_range(const DevView &v, const uint64_t wid, const 
                                          (uint8_t)plan_slot(q, s0 + 2), (uint8_t)plan_slot(q, s0 + 3)},
                                     reinterpret_cast<u8x4 *>(st + r * v.shard_len + (b << BSH) + s0));
     }
-}
-
-// REDUCE: workgroups [store_grid, gridDim.x) fold the partials into the summary (k_reduce's
-// work) while the others store — launched when the store is the step's last kernel, so the
-// summary's dependent launch and its ramp leave the chain (the partials are all written by
-// the kernels before it)
-template <bool NT, uint32_t C = 64, bool REDUCE = false>
-__global__ __launch_bounds__(256) void k_store8(DevView v, uint32_t store_grid, uint32_t n_partials)
-{
-    static_assert(C == 64 || C == 128, "one or two plan words per lane");
-    if (REDUCE && blockIdx.x >= store_grid) {
-        __shared__ unsigned long long red[4][8];
-        const uint32_t r = blockIdx.x - store_grid, R = gridDim.x - store_grid;
-        reduce_summary<4>(v, n_partials, red, 256 * r, 256 * R, r == 0);
-        return;
-    }
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    store8_range<NT, C>(v, xcd_wave_id_g(wv, store_grid, v.knobs), (uint64_t)store_grid * 4, 0, ~0ull, true);
-}
-
-// One stage of the pipelined C4-shape apply (LaunchGeom::pipe_stages): workgroups [0,
-// store_grid) store chunks [c0, c1) whose plan words the previous launch wrote, the next
-// plan_blocks plan pairs [p0, p1) beside them (the plan is latency-bound, the store
-// bandwidth-bound), the rest fold the summary (the last stage)
-struct PipeStage { uint64_t p0, p1, c0, c1; uint32_t store_grid, plan_blocks, apply_wgs, n_partials, tails; };
-template <bool NT, uint32_t C>
-__global__ __launch_bounds__(256) void k_plan_store(DevView v, PipeStage ps)
-{
-    __shared__ PlanLds L;
-    __shared__ unsigned long long red[4][8];
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (blockIdx.x < ps.store_grid) {
-        store8_range<NT, C>(v, xcd_wave_id_g(wv, ps.store_grid, v.knobs), (uint64_t)ps.store_grid * 4, ps.c0, ps.c1, ps.tails != 0);
-        return;
-    }
-    const uint32_t b = blockIdx.x - ps.store_grid;
-    if (b < ps.plan_blocks) {
-        plan_pairs(v, ps.apply_wgs, L, ps.p0, ps.p1, b);
-        return;
-    }
-    const uint32_t r = b - ps.plan_blocks, R = gridDim.x - ps.store_grid - ps.plan_blocks;
-    reduce_summary<4>(v, ps.n_partials, red, 256 * r, 256 * R, r == 0);
 }
 
 // General apply: one wave owns one (node, bucket) pair of the host-built work
@@ -3360,24 +3300,15 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     const bool plan_path = !v.digest && !(v.knobs & 64) && (member || v.N <= FAST_MAX_NODES);
     const bool lplan = plan_path && (member || (v.num_gp_snap && !(v.knobs & 8388608)));
     if (ev_apply0 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
-    // the summary folded into the store's extra workgroups when the store ends the step (the C4
-    // shape: no general pairs, no k_apply_fast, no k_chosen); knob 1073741824: k_reduce (A/B)
-    const bool skip_chosen = plan_path && v.chosen_static && !(v.knobs & (16777216 | 268435456));
-    const bool fuse_reduce = skip_chosen && !member && !lplan && v.num_gp == 0 && !(v.knobs & (4194304 | 2048 | 128 | 1073741824)) &&
-                             v.slot_w == 1;
-    const uint32_t reduce_wgs = cdiv(n_partials ? n_partials : 1, 256);
     // the plan words of every (row, bucket) -> state rows and the chosen log
     auto launch_store = [&](hipEvent_t stop) {
         if (v.slot_w == 1 && (v.knobs & 128))
             hipExtLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
         // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64
         else if (v.slot_w == 1 && (v.knobs & 2048))
-            hipExtLaunchKernelGGL((k_store8<true, 64>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v, g.store_wgs, 0u);
-        else if (v.slot_w == 1 && fuse_reduce)
-            hipExtLaunchKernelGGL((k_store8<true, 128, true>), dim3(g.store_wgs + reduce_wgs), dim3(256), 0, s, nullptr, stop, 0, v,
-                                  g.store_wgs, n_partials);
+            hipExtLaunchKernelGGL((k_store8<true, 64>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
         else if (v.slot_w == 1)
-            hipExtLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v, g.store_wgs, 0u);
+            hipExtLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
         else
             hipExtLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
     };
@@ -3392,32 +3323,6 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
             // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
             // 0.391 vs 0.304 ms apply phase at C4; the compiler drains vmcnt at its loop head)
             // (the chosen-log buckets on threads of their own after the pairs: 63.5 vs 61.5 us at C4)
-            const uint64_t cpr = (v.shard_len >> BSH) / 128, np = (uint64_t)v.N * v.NB;
-            const uint32_t K = (uint32_t)std::min<uint64_t>(g.pipe_stages, cpr);
-            if (fuse_reduce && K > 1) {
-                // the plan of stage j's buckets beside the store of stage j - 1's (k_plan_store):
-                // K + 1 launches, the first plan only, the last store + tails + summary
-                uint64_t cb[9], pb[9];
-                for (uint32_t j = 0; j <= K; ++j) {
-                    cb[j] = cpr * j / K;
-                    pb[j] = j == K ? np : (uint64_t)v.N * (cb[j] * 128);
-                }
-                for (uint32_t j = 0; j <= K; ++j) {
-                    PipeStage ps{};
-                    if (j < K) { ps.p0 = pb[j]; ps.p1 = pb[j + 1]; ps.plan_blocks = cdiv(pb[j + 1] - pb[j], 256); }
-                    if (j > 0) {
-                        ps.c0 = cb[j - 1];
-                        ps.c1 = j == K ? ~0ull : cb[j];
-                        ps.tails = j == K;
-                        ps.store_grid = j == K ? g.store_wgs : g.pipe_store_wgs;
-                    }
-                    ps.apply_wgs = g.apply_wgs;
-                    ps.n_partials = n_partials;
-                    const uint32_t red_wgs = j == K ? reduce_wgs : 0;
-                    hipExtLaunchKernelGGL((k_plan_store<true, 128>), dim3(ps.store_grid + ps.plan_blocks + red_wgs), dim3(256), 0, s,
-                                          (hipEvent_t)(j == 0 ? ev_apply0 : nullptr), (hipEvent_t)(j == K ? ev_apply1 : nullptr), 0, v, ps);
-                }
-            } else {
             hipExtLaunchKernelGGL(k_plan, dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
             if (lplan && (v.knobs & 536870912)) hipLaunchKernelGGL((k_plan_list<false, 8, 32>), dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
@@ -3432,7 +3337,6 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
                                       (hipEvent_t)nullptr, (hipEvent_t)ev_apply1, 0, v);
             } else {
                 launch_store((hipEvent_t)ev_apply1);
-            }
             }
         }
     } else if (member) {
@@ -3505,11 +3409,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     // 16777216: the summary in k_chosen's last workgroup instead — measured slower (C4 tail
     // 0.075 vs 0.015 ms, C3 0.161 vs 0.071 ms: every workgroup's device-scope fence writes
     // back its XCD's L2 before the ticket), kept for A/B
-    if (fuse_reduce) {
-        // (phase events: the apply phase ends with the store; the general and tail phases are empty)
-        if (ev_general) (void)hipEventRecord((hipEvent_t)ev_general, s);
-        if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, s);
-    } else if (skip_chosen) {
+    const bool skip_chosen = plan_path && v.chosen_static && !(v.knobs & (16777216 | 268435456));
+    if (skip_chosen) {
         hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)ev_end, 0, v, n_partials);
     } else if (!(v.knobs & 16777216)) {

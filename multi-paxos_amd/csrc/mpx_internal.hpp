@@ -387,10 +387,7 @@ MPX_HD inline uint64_t scalar_digest(uint32_t node, uint64_t promised, uint64_t 
 }
 
 // kernels (kernels.hip); every launcher queues on `stream`, returns hipError_t as int
-// pipe_stages: the C4-shape plan + store split into that many bucket ranges, the store of one
-// range overlapping the plan of the next (1: k_plan then k_store8); pipe_store_wgs: the
-// store's workgroups while a plan runs beside it
-struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, variant, store_wgs, pipe_stages, pipe_store_wgs; };
+struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, variant, store_wgs; };
 // ev (hipEvent_t, each may be null): begin, apply phase start (after the header
 // scan / quorum kernels), after the plan / store / fast-apply kernels, after the
 // general k_apply, end
