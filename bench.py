@@ -14,19 +14,18 @@ state: header scan, promise quorum, accept-vote quorum, acceptor/learner apply
 over ranks) / max-over-ranks step time.
 
 roofline: the dominant unit is the apply phase — k_plan (one thread per
-(acceptor, bucket) pair decides which message run fixes it), k_store (streams
-the slots and the chosen log) and k_apply_fast's per-slot pairs (none in C4:
-it exits at once) — bracketed by HIP events on the engine's stream; k_store is
-most of it (profiles/).  achieved = the phase's compulsory bytes (DESIGN.md
-§4: one 1-byte state slot written per (acceptor, instance), one 1-byte
-chosen-log entry per instance, one 16-byte fragment descriptor read per
-(acceptor, bucket, message), and the 4-byte plan word per (row, bucket) written
-and read back — a slot names the message run that fixed it, whose entry in the
-resident pool holds the Value, so no Value is read or copied) / its mean
-duration.  The SURVEY.md §8(d) model (16 P + 24 A + 16 L, which charges
-every acceptor a 16-byte slot plus a read of its own copy of each message) is
-reported beside it.  traffic = HBM bytes per launch from rocprofv3 PMC
-(profiles/, tools/pmc_traffic.py) or null.
+(acceptor, bucket) pair decides which message run fixes it) and k_store8
+(streams the slots and the chosen log) — bracketed by HIP events on the
+engine's stream; k_store8 is most of it (profiles/).  frac is the hardware
+fraction: traffic (HBM bytes per launch of those kernels from rocprofv3 PMC,
+FETCH_SIZE x2 + WRITE_SIZE, committed under profiles/ and matched to these
+sources by digest, tools/pmc_traffic.py) / the phase's mean duration in this
+run / 8 TB/s.  Beside it: the engine's own byte model (1-byte
+slot per (acceptor, instance), 1-byte chosen log, 16-byte descriptors per run,
+plan words; frac_engine_model) and SURVEY.md §8(d)'s 16 P + 24 A + 16 L
+(frac_survey_model, > 1 on the clean trace: a measure of the representation,
+not a bandwidth).  Without a matching profile frac falls back to the engine
+model and roofline.basis says so.
 
 Verification: steps leave the order-independent digests off (mpx_step); after
 the timed region one digested run (mpx_run) is checked against the closed-form
@@ -74,6 +73,10 @@ def parse():
     ap.add_argument("--c3-instances", type=int, default=1 << 24, help="C3 general-path leg: M (2^24); 0 = skip")
     ap.add_argument("--c3-steps", type=int, default=5)
     ap.add_argument("--c3-only", action="store_true", help="only the C3 leg (profiling)")
+    ap.add_argument("--c3-windows", type=int, default=16,
+                    help="the C3 trace again as this many incremental windows (the live OnReceiveMessage path, "
+                         "k_apply_win); 0 = skip")
+    ap.add_argument("--c3-windows-only", action="store_true", help="only the C3 windows leg (profiling)")
     ap.add_argument("--c5-instances", type=int, default=1 << 25, help="C5 member-path leg: M (2^25); 0 = skip")
     ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--c5-only", action="store_true", help="only the C5 leg (profiling)")
@@ -125,6 +128,7 @@ def c3_leg(args, kind="c3"):
     eng.submit_trace(trace)                         # (member: the trace's epoch table comes with it)
     t_ingest = time.perf_counter() - t0
     log("%s: ingested in %.1f s" % (kind, t_ingest))
+    windows_trace = trace if (not member and args.c3_windows and not args.c3_only) else None
     del trace
     t0 = time.perf_counter()
     chk = eng.run()                                 # upload + one digested run (verification)
@@ -160,7 +164,14 @@ def c3_leg(args, kind="c3"):
         16 * (hd["num_nodes"] + 1) * nb_l
     achieved_eng = b_eng / (apply_ms * 1e-3) / 1e9 if apply_ms else 0.0
     pmc = latest_pmc(8 if member else 7, m, 1, workload="C5" if member else "C3")
+    hw = hw_roofline(pmc, apply_ms)
     ms_step = dt / steps * 1e3
+    eng.close()
+    win = None
+    if windows_trace is not None:
+        win = c3_windows_leg(args, windows_trace, (chk["state_digest"], chk["chosen_digest"]),
+                             {k: chk[k] for k in ("chosen", "promise_entries", "accept_apps", "commit_apps")})
+        del windows_trace
     if member:
         workload = ("C5: 2^%d instances, member semantics, acceptor universe 8, AddAcceptor(1..7) then "
                     "DelAcceptor(1..7) = 15 epochs (member/main.cpp:119-141), 1%% loss / 1%% duplicates, "
@@ -182,9 +193,12 @@ def c3_leg(args, kind="c3"):
                      "bytes_alg_per_launch": b_alg, "bytes_model": "SURVEY §8(d): 16 P + 24 A + 16 L",
                      "kernel_ms": apply_ms, "general_ms": general_ms, "fast_ms": fast_ms,
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     # the hardware fraction: PMC HBM bytes of the same kernels / the same mean duration
+                     "frac_hw": hw["frac"] if hw else None, "achieved_hw": hw["achieved"] if hw else None,
                      "bytes_engine_model_per_launch": b_eng,
                      "frac_engine_model": achieved_eng / HBM_PEAK_GBS,
-                     "note": "frac is on SURVEY §8(d)'s bytes (every acceptor's own 16-24 B copy per entry); the "
+                     "note": "frac_hw is what the HBM moved (PMC traffic / kernel_ms / 8 TB/s); "
+                             "frac is on SURVEY §8(d)'s bytes (every acceptor's own 16-24 B copy per entry); the "
                              "engine stores a broadcast once and its slots name the run that fixed them, so it "
                              "moves far fewer bytes: frac > 1 (C5) measures that representation, and "
                              "frac_engine_model (the slots, chosen log, run descriptors and plan words it must "
@@ -200,7 +214,66 @@ def c3_leg(args, kind="c3"):
                      "chosen_digest": chk["chosen_digest"]},
         "host": {"generate_s": t_gen, "ingest_s": t_ingest, "upload_and_first_run_s": t_first,
                  "trace_bytes": trace_bytes},
+        **({"windows": win} if win else {}),
     }
+
+
+def c3_windows_leg(args, trace, want_digests, want_counters):
+    """The live path: the C3 trace as args.c3_windows incremental windows
+    (MPX_FLAG_INCREMENTAL: the drop-in for NetWork::OnReceiveMessage, multi/paxos.cpp:1714-1717).
+    Each window = mpx_submit_trace_range of 1/W of every node's records (host decode) + one
+    mpx_run (k_apply_win over the pairs the window touches, on the value state the earlier
+    windows left).  The windows together must give the batch run's digests and counters."""
+    W = args.c3_windows
+    hd = mpx.trace_header(trace)
+    idx = mpx.trace_index(trace)
+    n, m = hd["num_nodes"], hd["num_instances"]
+    eng = mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL)
+    eng.timing_every(1)
+    host_ms, dev, gp = [], [], []
+    tot = {k: 0 for k in want_counters}
+    prev = [0] * n
+    for w in range(1, W + 1):
+        cut = [c * w // W for (c, _, _) in idx]
+        t0 = time.perf_counter()
+        eng.submit_window(trace, prev, cut)
+        st = eng.run()
+        host_ms.append((time.perf_counter() - t0) * 1e3)
+        ph = eng.timings_detail()
+        dev.append(ph[-1])
+        gp.append(st["general_pairs"])
+        for k in tot:
+            tot[k] += st[k]
+        prev = cut
+    digests = eng.state_digest()
+    eng.close()
+    ok = digests == tuple(want_digests) and tot == want_counters
+    assert ok, "C3 windows: the windows' state differs from the batch run's (%r vs %r, %r vs %r)" % (
+        digests, want_digests, tot, want_counters)
+    run_ms = [p["run"] for p in dev]
+    apply_ms = [p["general_apply"] for p in dev]
+    mean = lambda xs: sum(xs) / max(len(xs), 1)
+    pmc = latest_pmc(7, m, 1, workload="C3W")
+    hw = hw_roofline(pmc, mean(apply_ms))
+    # engine model of a window's apply: each pair it touches reads and writes 256 slots of
+    # 16-B value state (s_bal, s_val) and its runs' 16-B descriptors
+    b_eng = sum(32 * 256 * x for x in gp) / W
+    log("c3 windows: %d windows, host %.1f ms / window (device %.2f), k_apply_win %.3f ms" %
+        (W, mean(host_ms), mean(run_ms), mean(apply_ms)))
+    return {"windows": W, "chosen": tot["chosen"],
+            "value": tot["chosen"] / (sum(host_ms) * 1e-3), "unit": "decisions/s",
+            "value_device": tot["chosen"] / (sum(run_ms) * 1e-3),
+            "note": "value: chosen instances / the windows' host + device wall time (decode, upload, run, "
+                    "readback); value_device: / the device run time alone",
+            "host_ms_per_window": mean(host_ms), "device_ms_per_window": mean(run_ms),
+            "host_ms": host_ms, "device_ms": run_ms, "apply_ms": apply_ms, "pairs_per_window": gp,
+            "roofline": {"bound": "hbm", "kernel": "k_apply_win", "kernel_ms": mean(apply_ms),
+                         "frac_hw": hw["frac"] if hw else None, "achieved_hw": hw["achieved"] if hw else None,
+                         "traffic": hw["traffic"] if hw else None, "traffic_source": hw["source"] if hw else None,
+                         "bytes_engine_model_per_launch": b_eng,
+                         "frac_engine_model": b_eng / (mean(apply_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS if mean(apply_ms) else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s"},
+            "verified": {"digests_vs_batch_run": ok}}
 
 
 class FileGroup:
@@ -339,9 +412,33 @@ def cpu_note():
     return "nproc %d, usable %d%s" % (nproc, usable, ", cgroup quota %.1f cores" % quota if quota else "")
 
 
+def cpu_threads():
+    """Threads the CPU baselines run: every usable core, but no more than the cgroup CPU quota
+    allows (on the GPU box: 256 usable cores under a 16-core quota -> 16 threads; more would only
+    time-slice the same 16 cores and understate the baseline)."""
+    usable, _, quota = host_cpus()
+    if quota:
+        import math
+        return max(1, min(usable, int(math.ceil(quota))))
+    return max(1, usable)
+
+
+def hw_roofline(pmc, kernel_ms):
+    """The hardware fraction: PMC HBM bytes of the timed apply-phase kernels (one launch each,
+    rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) over the
+    phase's mean duration from the HIP events of this run, against the 8 TB/s peak.  None when
+    no committed profile matches this workload and these kernels (source digest)."""
+    if not pmc or not kernel_ms or not pmc.get("hbm_bytes_per_launch"):
+        return None
+    gbps = pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
+    return {"achieved": gbps, "frac": gbps / HBM_PEAK_GBS, "traffic": pmc["hbm_bytes_per_launch"],
+            "source": "profiles/%s_pmc.json" % pmc["tag"]}
+
+
 def cpu_baseline(args, budget_s):
-    """Reference handlers (oracle/_ref) on every usable host core: node 1's accept+commit stream
-    of a clean trace, one independent replay per thread."""
+    """Reference handlers (oracle/_ref) on the host cores this process may use (cpu_threads: the
+    usable cores, capped at the cgroup CPU quota): node 1's accept+commit stream of a clean trace,
+    one independent replay per thread."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libmpx_ref.so")
     kind = "reference"
     if not os.path.exists(ref_so):
@@ -352,7 +449,7 @@ def cpu_baseline(args, budget_s):
     fn.restype = ctypes.c_int64
     sample_m = 1 << 16
     trace = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=args.nodes, num_instances=sample_m, batch=256)
-    threads = host_cpus()[0]
+    threads = cpu_threads()
     done = [0] * threads
 
     def parallel(reps):
@@ -401,15 +498,15 @@ def native_oracle():
 
 def cpu_port_baseline(args, budget_s):
     """The build's own CPU restatement (oracle/mpx_oracle.c, SURVEY §8(d)(ii): -O2 -march=native,
-    every usable host core) over a clean C4-shaped trace: instance shards in parallel
+    the host cores cpu_threads allows) over a clean C4-shaped trace: instance shards in parallel
     (mpxo_run_sharded), each shard every node's stream on its own thread; counters + digests only."""
     so, flags = native_oracle()
     lib = ctypes.CDLL(so)
     f = lib.mpxo_run_sharded
     f.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
     f.restype = ctypes.c_int
-    cores = host_cpus()[0]
-    shards = max(1, cores // args.nodes)              # shards x N node threads = the usable cores
+    cores = cpu_threads()
+    shards = max(1, cores // args.nodes)              # shards x N node threads ~ the cores the quota gives
     sample_m = max(1 << 18, shards << 15)
     trace = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=args.nodes, num_instances=sample_m, batch=256, copy=False)
     stats = (ctypes.c_uint64 * 8)()
@@ -484,6 +581,15 @@ def main():
     if args.c3_only:
         print(json.dumps({"c3": c3_leg(args)}), flush=True)
         return
+    if args.c3_windows_only:
+        trace = mpx.generate_trace(mpx.GEN_FAULTY, num_instances=args.c3_instances, copy=False, **C3)
+        with mpx.Engine.for_trace(trace) as e:
+            chk = e.run()
+        print(json.dumps({"c3_windows": c3_windows_leg(args, trace, (chk["state_digest"], chk["chosen_digest"]),
+                                                       {k: chk[k] for k in ("chosen", "promise_entries",
+                                                                            "accept_apps", "commit_apps")})}),
+              flush=True)
+        return
     if args.c5_only:
         print(json.dumps({"c5": c3_leg(args, "c5")}), flush=True)
         return
@@ -550,11 +656,18 @@ def main():
     runs = sum(((min(b0 + 256, se) - 1) // args.batch - b0 // args.batch + 1)
                for b0 in range(sb, se, 256)) if args.batch != 256 else nb   # batch runs meeting each bucket
     bytes_min = 1 * N * L + 1 * L + 2 * 16 * N * runs + 2 * 8 * (N + 1) * nb
-    achieved = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
+    achieved_eng = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
     pmc = latest_pmc(N, M, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     traffic_src = ("profiles/%s_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of this command, "
                    "committed; not measured inside this process)" % pmc["tag"]) if pmc else None
+    # roofline.frac is the hardware fraction: the PMC bytes the timed
+    # apply-phase kernels move per launch / the phase's mean duration of THIS run / 8 TB/s.
+    # Without a profile at these sources it falls back to the engine's byte model (basis says so).
+    hw = hw_roofline(pmc, apply_mean)
+    achieved = hw["achieved"] if hw else achieved_eng
+    basis = ("pmc: %s traffic / this run's kernel_ms" % hw["source"]) if hw else \
+        "engine_model (no PMC profile at this source digest): DESIGN.md §4 bytes / kernel_ms"
 
     log("C4: %.4f ms per step over %d steps, verified %s" % (dt_max / args.steps * 1e3, args.steps, verified))
     out = None
@@ -594,16 +707,21 @@ def main():
                        "instances": M, "acceptors": N, "batch": args.batch, "shard_per_gpu": se - sb,
                        "parallelism": "instance-shard x%d (RCCL all-gather of 64-word summaries)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "apply phase: k_plan + k_store + k_apply_fast<1,false,true>",
+                         "frac": achieved / HBM_PEAK_GBS, "basis": basis,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "apply phase: k_plan + k_store8",
                          "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_min,
-                         "bytes_model": "DESIGN.md §4: 1-B slot per (acceptor, instance) + 1-B chosen log + "
-                                        "16-B ACCEPT / COMMIT descriptors per run + 8-B plan words",
+                         "achieved_engine_model": achieved_eng,
+                         "frac_engine_model": achieved_eng / HBM_PEAK_GBS,
+                         "bytes_model": "engine model, DESIGN.md §4: 1-B slot per (acceptor, instance) + 1-B chosen "
+                                        "log + 16-B ACCEPT / COMMIT descriptors per run + 8-B plan words",
                          "bytes_survey_model_per_launch": bytes_survey,
                          "survey_model_gbps": bytes_survey / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0,
                          "frac_survey_model": bytes_survey / (apply_mean * 1e-3) / 1e9 / HBM_PEAK_GBS
                          if apply_mean else 0.0,
-                         "note": "the clean trace fixes every (acceptor, bucket) pair with one full run, so its apply "
+                         "note": "frac = PMC traffic / kernel_ms / 8 TB/s (what the HBM moved); frac_survey_model is "
+                                 "NOT a fraction when > 1. "
+                                 "The clean trace fixes every (acceptor, bucket) pair with one full run, so its apply "
                                  "phase reduces to one plan word per pair and a byte stream of slots (k_store8): the "
                                  "survey model's 360 B/instance (16-B slot writes + per-acceptor Value reads) are "
                                  "never moved, and frac_survey_model > 1 measures representation, not bandwidth; "

@@ -63,7 +63,10 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 2u   /* 2: mpx_epoch carries learner_mask (32 bytes) */
+/* 2: mpx_epoch carries learner_mask (32 bytes), and mpx_stats grew from 16 to 18 u64
+ *    words (general_pairs, num_runs, slot_bytes; reserved[] is the extension area from
+ *    here on: the struct stays 144 bytes within ABI 2) */
+#define MPX_ABI_VERSION 2u
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -141,24 +144,30 @@ typedef struct mpx_config {
     uint64_t shard_begin;      /* this engine owns instances [shard_begin,         */
     uint64_t shard_end;        /*                              shard_end)          */
     uint32_t num_epochs;       /* member only                                      */
-    uint32_t flags;            /* 0, or MPX_FLAG_INCREMENTAL [| MPX_FLAG_DECISIONS] (multi) */
+    uint32_t flags;            /* 0, or MPX_FLAG_INCREMENTAL [| MPX_FLAG_DECISIONS (multi)] */
     const mpx_epoch *epochs;   /* member only, indexed by E_EPOCH's epoch          */
 } mpx_config;
 
 /* Incremental runs (the drop-in for NetWork::OnReceiveMessage, multi/paxos.cpp:1714-1717,
- * on a live stream).  Each mpx_run applies only the records submitted since
- * the previous one — a window — to the state the earlier windows left, on the device:
- * acceptor / learner entries, the chosen log, promised / max_seen, promise rounds with
- * their pre-accepted maps, and the batches' votes carry over as values.  A window's
- * host and device work is O(window records + state they touch), not O(history).
+ * and member NetWork::OnReceive, member/paxos.cpp:841-844, on a live stream).
+ * Each mpx_run applies only the records submitted since the previous one — a window — to
+ * the state the earlier windows left, on the device: acceptor / learner entries, the chosen
+ * log, promised / max_seen, promise rounds with their pre-accepted maps, and the batches'
+ * votes carry over as values; member windows also carry each node's roles (epoch, Acceptor
+ * incarnation, Proposer) and which batches a membership step cleared.  A window's host and
+ * device work is O(window records + state they touch), not O(history).
  * mpx_drain_sends returns the window's replies; the mpx_read_* state readbacks and
  * mpx_state_digest give the cumulative state; mpx_stats counts the window.  Not
  * available in this mode (MPX_E_STATE): mpx_step / mpx_reset_state (windows are applied
- * once), mpx_dump_result, the decisions and commits readbacks (they walk the run's
- * history). */
+ * once), mpx_dump_result, the commits / learns readbacks and the sharded decisions (they
+ * walk the run's history).
+ * Errors: a window refused while it is built (MPX_E_RANGE, MPX_E_DECODE, ...) leaves the
+ * engine as it was — its records stay queued and are refused again; a failure after the
+ * window was taken (a HIP error) may leave it partly applied, so the engine is poisoned:
+ * every later mpx_run, submit and readback returns MPX_E_STATE. */
 #define MPX_FLAG_INCREMENTAL 1u
-/* With MPX_FLAG_INCREMENTAL: every mpx_run also advances the proposers' phase-2
- * bookkeeping over the window's events (the quorums' merged maps, COMMIT entries,
+/* With MPX_FLAG_INCREMENTAL (multi semantics): every mpx_run also advances the proposers'
+ * phase-2 bookkeeping over the window's events (the quorums' merged maps, COMMIT entries,
  * client values), so mpx_read_decisions returns the decisions of every window so far —
  * the MPXD of one run over the whole stream (host work per window, O(window)). */
 #define MPX_FLAG_DECISIONS 2u
@@ -247,6 +256,11 @@ typedef struct mpx_soa_records {
 int  mpx_submit_soa(mpx_engine *eng, uint32_t node, const mpx_soa_records *records);
 /* Convenience: submit every node of an MPXT trace container (see mpx_trace_*). */
 int  mpx_submit_trace(mpx_engine *eng, const uint8_t *trace, uint64_t size);
+/* The same for one slice of every node's stream — records [begin[n], end[n]) of node n
+ * (one window of a live stream, MPX_FLAG_INCREMENTAL): = mpx_submit of each node's slice,
+ * decoded on one host thread per node for large slices. */
+int  mpx_submit_trace_range(mpx_engine *eng, const uint8_t *trace, uint64_t size,
+                            const uint64_t *begin, const uint64_t *end);
 
 /* Apply everything submitted since the last run (state carries over). */
 int  mpx_run(mpx_engine *eng);

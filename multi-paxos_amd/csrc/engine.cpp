@@ -28,6 +28,8 @@
 
 using namespace mpx;
 
+static_assert(sizeof(mpx_stats) == 144, "mpx_stats is 18 u64 words within ABI 2 (include/mpx.h)");
+
 namespace {
 
 struct DevBuf {
@@ -115,8 +117,11 @@ struct mpx_engine {
     // the device state carried as values, and each node's records in earlier windows
     bool incremental = false;
     WindowCarry wc;
-    DevBuf s_bal, s_val, p_pid, p_val, p_round, c_val, scal_base, prop_in, prop_out;
-    DevBuf b_gid, g_mask, g_done, gp_base, cb_list, outv, outv_n;
+    DevBuf s_bal, s_val, p_pid, p_val, p_round, c_val, scal_base, scal_key, prop_in, prop_out;
+    DevBuf b_gid, b_node, g_mask, g_done, gp_base, cb_list, outv, outv_n, ee_init, ee_out;
+    bool ee_ready = false;                  // member: ee_init holds the roles the next window starts from
+    uint64_t consumed = 0;                  // windows whose records build_trace took (the carry moved past them)
+    bool poisoned = false;                  // a window failed after it was consumed: state undefined
     uint64_t g_cap = 0;                     // global batches g_mask / g_done hold
     std::vector<uint64_t> seq_base, win_seq_base;
     std::vector<PropNode> *prop = nullptr;           // MPX_FLAG_DECISIONS: the bookkeeping carried across windows
@@ -161,7 +166,7 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
     if (cfg->semantics == MPX_SEM_MULTI && cfg->num_epochs) return MPX_E_INVAL;
     if (cfg->flags & ~(uint32_t)(MPX_FLAG_INCREMENTAL | MPX_FLAG_DECISIONS)) return MPX_E_INVAL;
     if ((cfg->flags & MPX_FLAG_DECISIONS) && !(cfg->flags & MPX_FLAG_INCREMENTAL)) return MPX_E_INVAL;
-    if ((cfg->flags & MPX_FLAG_INCREMENTAL) && cfg->semantics != MPX_SEM_MULTI) return MPX_E_INVAL;
+    if ((cfg->flags & MPX_FLAG_DECISIONS) && cfg->semantics != MPX_SEM_MULTI) return MPX_E_INVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPX_E_NODEVICE;
     if (cfg->device < 0 || cfg->device >= n) return MPX_E_NODEVICE;
@@ -192,7 +197,8 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
         DevBuf *bufs[] = {&e->s_bal, &e->s_val, &e->p_pid, &e->p_val};
         for (DevBuf *b : bufs) TRY(b->alloc(8 * NL));
         TRY(e->p_round.alloc(8ull * cfg->num_nodes * e->NB)); TRY(e->c_val.alloc(8 * e->shard_len));
-        TRY(e->scal_base.alloc(16ull * cfg->num_nodes));
+        TRY(e->scal_base.alloc(16ull * cfg->num_nodes)); TRY(e->scal_key.alloc(16ull * cfg->num_nodes));
+        TRY(e->ee_init.alloc(4ull * cfg->num_nodes)); TRY(e->ee_out.alloc(4ull * cfg->num_nodes));
         TRY(e->prop_in.alloc(24ull * cfg->num_nodes)); TRY(e->prop_out.alloc(24ull * cfg->num_nodes));
         TRY(e->outv_n.alloc(8));
         DevBuf *z[] = {&e->s_bal, &e->s_val, &e->p_pid, &e->p_val, &e->p_round, &e->c_val, &e->scal_base, &e->prop_in,
@@ -220,6 +226,7 @@ extern "C" int mpx_destroy(mpx_engine *e)
 extern "C" int mpx_submit(mpx_engine *e, uint32_t node, const uint8_t *bytes, const uint64_t *offsets, uint64_t count)
 {
     if (!e || node >= e->cfg.num_nodes || (count && (!bytes || !offsets))) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (e->device_trace) return MPX_E_STATE;
     const uint64_t t0 = now_ns();
     NodeStream &ns = e->nodes[node];
@@ -242,6 +249,7 @@ extern "C" int mpx_submit(mpx_engine *e, uint32_t node, const uint8_t *bytes, co
 extern "C" int mpx_submit_soa(mpx_engine *e, uint32_t node, const mpx_soa_records *r)
 {
     if (!e || !r || node >= e->cfg.num_nodes) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (e->device_trace || e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
     if (r->count && (!r->type || !r->src || !r->ballot || !r->aux || !r->ent_off)) return MPX_E_INVAL;
     const uint64_t t0 = now_ns();
@@ -265,9 +273,11 @@ extern "C" int mpx_submit_soa(mpx_engine *e, uint32_t node, const mpx_soa_record
 static inline uint32_t rd32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
 static inline uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 
-extern "C" int mpx_submit_trace(mpx_engine *e, const uint8_t *t, uint64_t size)
+// the records [begin[n], end[n]) of every node's stream of an MPXT container (nullptr: all of them)
+static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, const uint64_t *begin, const uint64_t *end)
 {
     if (!e || !t || size < 40 || std::memcmp(t, "MPXT", 4)) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     const uint32_t N = rd32(t + 8), sem = rd32(t + 12), ne = rd32(t + 24), ver = rd32(t + 4);
     if (N != e->cfg.num_nodes || sem != e->cfg.semantics || ver < 1 || ver > 2) return MPX_E_INVAL;
     const uint32_t esz = ver == 1 ? 24 : 32;         // version 1: no learner_mask (= proposer_mask)
@@ -295,13 +305,20 @@ extern "C" int mpx_submit_trace(mpx_engine *e, const uint8_t *t, uint64_t size)
         pos += 8 * (cnt + 1) + nb;
         pos = (pos + 7) & ~(size_t)7;
     }
+    if (begin && end)
+        for (uint32_t n = 0; n < N; ++n)
+            if (begin[n] > end[n] || end[n] > rd64(t + at[n])) return MPX_E_INVAL;
+    // node n's records [k0, k1): offs[k0 .. k1] index the container's record bytes
     auto stream = [&](uint32_t n, const uint64_t *&offs, const uint8_t *&bytes) {
         const uint64_t cnt = rd64(t + at[n]);
-        offs = reinterpret_cast<const uint64_t *>(t + at[n] + 16);     // 8-aligned in the container
+        const uint64_t k0 = begin ? begin[n] : 0, k1 = end ? end[n] : cnt;
+        offs = reinterpret_cast<const uint64_t *>(t + at[n] + 16) + k0;    // 8-aligned in the container
         bytes = t + at[n] + 16 + 8 * (cnt + 1);
-        return cnt;
+        return k1 - k0;
     };
-    if (N == 1 || size < (1u << 20) || e->device_trace) {
+    uint64_t total = 0;
+    for (uint32_t n = 0; n < N; ++n) { const uint64_t *o; const uint8_t *b; const uint64_t c = stream(n, o, b); if (c) total += o[c] - o[0]; }
+    if (N == 1 || total < (1u << 20) || e->device_trace) {
         for (uint32_t n = 0; n < N; ++n) {
             const uint64_t *offs; const uint8_t *bytes;
             const uint64_t cnt = stream(n, offs, bytes);
@@ -345,6 +362,18 @@ extern "C" int mpx_submit_trace(mpx_engine *e, const uint8_t *t, uint64_t size)
     e->dirty = true;
     e->stats.ingest_ns += now_ns() - t0;
     return MPX_OK;
+}
+
+extern "C" int mpx_submit_trace(mpx_engine *e, const uint8_t *t, uint64_t size)
+{
+    return submit_container(e, t, size, nullptr, nullptr);
+}
+
+extern "C" int mpx_submit_trace_range(mpx_engine *e, const uint8_t *t, uint64_t size, const uint64_t *begin,
+                                      const uint64_t *end)
+{
+    if (!e || !begin || !end) return MPX_E_INVAL;
+    return submit_container(e, t, size, begin, end);
 }
 
 // allocate state / output buffers and fill the kernel view
@@ -458,6 +487,7 @@ static int upload_trace(mpx_engine *e)
                     e->incremental ? &e->wc : nullptr));
     if (e->incremental) {
         // the window is consumed: the next run builds on the carry from only what comes after it
+        ++e->consumed;
         e->win_seq_base = e->seq_base;
         for (uint32_t n = 0; n < e->cfg.num_nodes; ++n) {
             e->seq_base[n] += e->nodes[n].type.size();
@@ -542,6 +572,18 @@ static int upload_trace(mpx_engine *e)
     DevView &v = e->view;
     if (e->incremental) {
         TRY(upload(e->b_gid, h.b_gid, s)); TRY(upload(e->gp_base, h.gp_base, s)); TRY(upload(e->cb_list, h.cb_list, s));
+        TRY(upload(e->b_node, h.b_node, s));
+        if (member && !e->ee_ready) {
+            // the first window starts from the genesis roles (Loop: {first} is learner, proposer
+            // and acceptor, member/paxos.cpp:738-747; epochs[0] of the table)
+            std::vector<uint32_t> g0(e->cfg.num_nodes);
+            for (uint32_t n = 0; n < e->cfg.num_nodes; ++n)
+                g0[n] = (1u << EE_SEG_SHIFT) | (((e->epochs[0].acceptor_mask >> n) & 1) ? EE_ACC : 0) |
+                        (((e->epochs[0].proposer_mask >> n) & 1) ? EE_PROP : 0);
+            TRY(upload(e->ee_init, g0, s));
+            HTRY(hipStreamSynchronize(s));                 // g0 is a local
+            e->ee_ready = true;
+        }
         if (e->wc.batches > e->g_cap) {                 // the batches' votes, grown geometrically (kept values copied)
             const uint64_t cap = std::max<uint64_t>(e->wc.batches, 2 * e->g_cap);
             DevBuf nm, nd;
@@ -562,7 +604,8 @@ static int upload_trace(mpx_engine *e)
         v.window = 1;
         v.s_bal = e->s_bal.as<uint64_t>(); v.s_val = e->s_val.as<uint64_t>();
         v.p_pid = e->p_pid.as<uint64_t>(); v.p_val = e->p_val.as<uint64_t>(); v.p_round = e->p_round.as<uint64_t>();
-        v.c_val = e->c_val.as<uint64_t>(); v.scal_base = e->scal_base.as<uint64_t>();
+        v.c_val = e->c_val.as<uint64_t>(); v.scal_base = e->scal_base.as<uint64_t>(); v.scal_key = e->scal_key.as<uint64_t>();
+        v.b_node = e->b_node.as<uint32_t>(); v.ee_init = e->ee_init.as<uint32_t>(); v.ee_out = e->ee_out.as<uint32_t>();
         v.prop_in = e->prop_in.as<uint64_t>(); v.prop_out = e->prop_out.as<uint64_t>();
         v.b_gid = e->b_gid.as<uint32_t>(); v.g_mask = e->g_mask.as<uint64_t>(); v.g_done = e->g_done.as<uint8_t>();
         v.gp_base = e->gp_base.as<uint8_t>(); v.cb_list = e->cb_list.as<uint32_t>(); v.num_cb = (uint32_t)h.cb_list.size();
@@ -652,13 +695,13 @@ static int queue_run(mpx_engine *e, bool digest)
     ++e->step_no;
     StepEvents *ev = timed ? next_events(e) : nullptr;
     if (timed && !ev) return MPX_E_HIP;
-    // k_apply build variant / grid for A/B measurements (tools/ab_apply.py);
-    // the defaults are the measured best
+    // grid sizes: the defaults are the measured best; the MPX_*_WGS_PER_CU overrides are for
+    // sweeps (tools/)
     LaunchGeom g = e->geom;
-    if (const char *x = std::getenv("MPX_APPLY_VARIANT")) g.variant = (uint32_t)std::atoi(x);
     e->view.digest = digest ? 1 : 0;
-    e->view.knobs = 0;
-    if (const char *x = std::getenv("MPX_KNOBS")) e->view.knobs = (uint32_t)std::atoi(x);
+    // MPX_STEP_WALK=1: a step walks every pair as the digested run does (no plan words)
+    e->view.walk_all = 0;
+    if (const char *x = std::getenv("MPX_STEP_WALK")) e->view.walk_all = std::atoi(x) ? 1 : 0;
     if (const char *x = std::getenv("MPX_STORE_WGS_PER_CU")) g.store_wgs = std::max<uint32_t>(1, e->num_cus * (uint32_t)std::atoi(x));
     if (const char *x = std::getenv("MPX_CHOSEN_WGS_PER_CU"))     // (partials hold 16 per CU for it too)
         g.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 16),
@@ -672,9 +715,11 @@ static int queue_run(mpx_engine *e, bool digest)
     if (ev) for (int k = 0; k < 5; ++k) evp[k] = ev->e[k];
     int rc = launch_run(e->view, e->stream, g, evp);
     if (rc) return MPX_E_HIP;
-    if (e->incremental) {                              // the next window starts from this one's scalars and rounds
-        HTRY(hipMemcpyAsync(e->scal_base.p, e->node_scal.p, 16ull * e->cfg.num_nodes, hipMemcpyDeviceToDevice, e->stream));
+    if (e->incremental) {                              // the next window starts from this one's scalars, rounds, roles
+        HTRY(hipMemcpyAsync(e->scal_base.p, e->scal_key.p, 16ull * e->cfg.num_nodes, hipMemcpyDeviceToDevice, e->stream));
         HTRY(hipMemcpyAsync(e->prop_in.p, e->prop_out.p, 24ull * e->cfg.num_nodes, hipMemcpyDeviceToDevice, e->stream));
+        if (e->cfg.semantics == MPX_SEM_MEMBER)
+            HTRY(hipMemcpyAsync(e->ee_init.p, e->ee_out.p, 4ull * e->cfg.num_nodes, hipMemcpyDeviceToDevice, e->stream));
     }
     // the one cross-GPU exchange: every rank's 64-word summary, over RCCL on
     // the same stream, no host synchronisation
@@ -721,7 +766,7 @@ static int collect(mpx_engine *e)
     st.slot_bytes = e->view.slot_w;
     const DevView &v = e->view;
     const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
-    if (!member && !v.digest && !(v.knobs & (64 | 4194304)) && v.N <= FAST_MAX_NODES) {
+    if (!member && !v.digest && !v.walk_all && v.N <= FAST_MAX_NODES) {
         // the multi plan path launches no k_apply_fast after the store: every lean pair must
         // have been planned (kernels.hip launch_run)
         uint32_t rest = 0;
@@ -729,7 +774,7 @@ static int collect(mpx_engine *e)
         if (rest) return MPX_E_STATE;
     }
     // the plan path with k_plan_list (kernels.hip launch_run): its list + the promise-round pairs
-    if (!v.digest && !(v.knobs & 64) && (member || (v.N <= FAST_MAX_NODES && v.num_gp_snap && !(v.knobs & 8388608)))) {
+    if (!v.digest && !v.walk_all && (member || (v.N <= FAST_MAX_NODES && v.num_gp_snap))) {
         uint64_t listed = 0;
         HTRY(hipMemcpy(&listed, e->gp_dyn_n.p, 8, hipMemcpyDeviceToHost));
         st.general_pairs = listed + (e->view.num_gp - e->view.num_gp_snap);
@@ -745,22 +790,34 @@ static int collect(mpx_engine *e)
     return MPX_OK;
 }
 
+static int run_window(mpx_engine *e)
+{
+    // one window: the records submitted since the last run, on the carried state
+    e->dirty = true;
+    TRY(queue_run(e, false));
+    TRY(collect(e));
+    if (e->prop) TRY(prop_window(e));
+    // batches chosen in this window need their entries no more
+    std::vector<uint32_t> bc;
+    TRY(d2h(bc, e->b_chosen, e->ht.b_gid.size()));
+    for (size_t j = 0; j < bc.size(); ++j)
+        if (bc[j] != NONE32) e->wc.b_ents.erase(e->ht.b_gid[j]);
+    ++e->windows;
+    return MPX_OK;
+}
+
 extern "C" int mpx_run(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
     if (e->incremental) {
-        // one window: the records submitted since the last run, on the carried state
-        e->dirty = true;
-        TRY(queue_run(e, false));
-        TRY(collect(e));
-        if (e->prop) TRY(prop_window(e));
-        // batches chosen in this window need their entries no more
-        std::vector<uint32_t> bc;
-        TRY(d2h(bc, e->b_chosen, e->ht.b_gid.size()));
-        for (size_t j = 0; j < bc.size(); ++j)
-            if (bc[j] != NONE32) e->wc.b_ents.erase(e->ht.b_gid[j]);
-        ++e->windows;
-        return MPX_OK;
+        if (e->poisoned) return MPX_E_STATE;
+        const uint64_t before = e->consumed;
+        const int rc = run_window(e);
+        // a window that failed before build_trace took it leaves the engine as it was (the
+        // records stay queued); one that failed after may be partly applied on the device and
+        // its records are gone: every later call refuses (include/mpx.h MPX_FLAG_INCREMENTAL)
+        if (rc && e->consumed != before) e->poisoned = true;
+        return rc;
     }
     TRY(queue_run(e, true));
     return collect(e);
@@ -914,6 +971,7 @@ extern "C" int mpx_read_executed(mpx_engine *e, uint32_t node, uint64_t *frontie
                                  uint64_t *handles, uint64_t cap)
 {
     if (!e || node >= e->cfg.num_nodes || (cap && !handles)) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     uint64_t fr;
     std::vector<uint64_t> h;
     TRY(gpu_executed(e, node, fr, h));
@@ -926,6 +984,7 @@ extern "C" int mpx_read_executed(mpx_engine *e, uint32_t node, uint64_t *frontie
 extern "C" int mpx_read_chosen(mpx_engine *e, uint64_t first, uint64_t count, uint64_t *out)
 {
     if (!e || (count && !out)) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (first < e->cfg.shard_begin || first + count > e->cfg.shard_end) return MPX_E_RANGE;
     if (!count) return MPX_OK;
     std::vector<uint64_t> d;
@@ -937,6 +996,7 @@ extern "C" int mpx_read_chosen(mpx_engine *e, uint64_t first, uint64_t count, ui
 extern "C" int mpx_read_node_scalars(mpx_engine *e, uint32_t node, uint64_t *promised, uint64_t *max_seen)
 {
     if (!e || node >= e->cfg.num_nodes) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     uint64_t v[2] = {0, 0};
     if (have_results(e)) {
         HTRY(hipSetDevice(e->device));
@@ -951,6 +1011,7 @@ extern "C" int mpx_read_node_state(mpx_engine *e, uint32_t node, uint64_t first,
                                    uint64_t *acc_ballot, uint64_t *acc_value, uint64_t *com_ballot, uint64_t *com_value)
 {
     if (!e || node >= e->cfg.num_nodes) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (first < e->cfg.shard_begin || first + count > e->cfg.shard_end) return MPX_E_RANGE;
     if (!count) return MPX_OK;
     std::vector<uint64_t> st;
@@ -977,6 +1038,7 @@ extern "C" int mpx_stats_get(mpx_engine *e, mpx_stats *out)
 extern "C" int mpx_state_digest(mpx_engine *e, uint64_t *state_digest, uint64_t *chosen_digest)
 {
     if (!e || !state_digest || !chosen_digest) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (!e->st.p) return MPX_E_STATE;
     HTRY(hipSetDevice(e->device));
     TRY(e->exec_aux.alloc(std::max<size_t>(e->exec_aux.bytes, 16)));
@@ -1143,6 +1205,7 @@ static void reply_of(const mpx_engine *e, const Results &r, uint32_t n, uint64_t
 extern "C" int mpx_drain_sends(mpx_engine *e, mpx_send_fn fn, void *user)
 {
     if (!e || !fn) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     Results r;
     TRY(fetch_results(e, r));
     std::string m;
@@ -1704,6 +1767,7 @@ static int member_decisions(mpx_engine *e, const Results &r, std::string &d)
 extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (e->incremental) {                               // windows keep no history of runs, but
         if (!e->prop || e->cfg.shard_begin != 0) return MPX_E_STATE;   // MPX_FLAG_DECISIONS carries the
         std::string d;                                  // bookkeeping: every window's quorums so far
@@ -2136,7 +2200,9 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnPlan> &o
 extern "C" int mpx_read_learns(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (e->cfg.semantics != MPX_SEM_MEMBER || !e->whole) return MPX_E_STATE;
+    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
     Results r;
     TRY(fetch_results(e, r));
     std::vector<LearnPlan> lp;

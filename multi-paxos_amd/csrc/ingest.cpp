@@ -647,15 +647,19 @@ static void cut_runs(const uint64_t *iid, uint64_t first, uint32_t count, uint64
 // each distinct entry list once lets the apply kernel read a bucket's Values
 // once for all nodes (DESIGN.md §Data layout).  Lists are compared in full,
 // the hash only picks the candidates.
+// member pools carry a proposal id per entry (e_pid, index-aligned with e_iid / e_val); a
+// list without ids (a window's carried batch entries, chosen-log runs only) takes id 0
 struct EntryPool {
+    bool member = false;
     std::unordered_multimap<uint64_t, uint64_t> idx;    // hash -> offset in ht.e_*
     uint64_t intern(const NodeStream &ns, uint64_t first, uint32_t cnt, HostTrace &ht)
     {
-        const bool pid = !ns.e_pid.empty();
+        const bool has = !ns.e_pid.empty();
+        auto pid_of = [&](uint32_t i) -> uint64_t { return has ? ns.e_pid[first + i] : 0; };
         uint64_t h = mix64(cnt + 0x51ull);
         for (uint32_t i = 0; i < cnt; ++i) {
             h = mix64(h ^ ns.e_iid[first + i]) + ns.e_val[first + i];
-            if (pid) h = mix64(h ^ ns.e_pid[first + i]);
+            if (member) h = mix64(h ^ pid_of(i));
         }
         auto r = idx.equal_range(h);
         for (auto it = r.first; it != r.second; ++it) {
@@ -664,13 +668,14 @@ struct EntryPool {
             bool same = true;
             for (uint32_t i = 0; same && i < cnt; ++i)
                 same = ht.e_iid[o + i] == ns.e_iid[first + i] && ht.e_val[o + i] == ns.e_val[first + i] &&
-                       (!pid || ht.e_pid[o + i] == ns.e_pid[first + i]);
+                       (!member || ht.e_pid[o + i] == pid_of(i));
             if (same) return o;
         }
         const uint64_t o = ht.e_iid.size();
         ht.e_iid.insert(ht.e_iid.end(), ns.e_iid.begin() + first, ns.e_iid.begin() + first + cnt);
         ht.e_val.insert(ht.e_val.end(), ns.e_val.begin() + first, ns.e_val.begin() + first + cnt);
-        if (pid) ht.e_pid.insert(ht.e_pid.end(), ns.e_pid.begin() + first, ns.e_pid.begin() + first + cnt);
+        if (member)
+            for (uint32_t i = 0; i < cnt; ++i) ht.e_pid.push_back(pid_of(i));
         idx.emplace(h, o);
         return o;
     }
@@ -680,7 +685,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                 const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc)
 {
     const bool member = !epochs.empty();
-    if (wc && (member || !wc->on)) return MPX_E_STATE;            // incremental runs: multi semantics
+    if (wc && !wc->on) return MPX_E_STATE;
     ht = HostTrace();
     const uint32_t N = (uint32_t)nodes.size();
     ht.N = N;
@@ -698,6 +703,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     ht.node_off.assign(N + 1, 0);
 
     EntryPool pool;
+    pool.member = member;
     struct FragKey { uint64_t key; Frag f; };
     std::vector<uint64_t> fcount(N * NB + 1, 0), cfcount(NB + 1, 0);
     std::vector<FragKey> fr, cfr;
@@ -734,6 +740,19 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     std::vector<std::pair<uint32_t, uint64_t>> state_new;        // (node, bucket) met by this window's runs
     const uint64_t gid0 = wc ? wc->batches : 0;
     uint64_t gid_next = gid0;
+    // The carry past this window is collected here and committed to *wc only once every
+    // check below has passed: a window that fails (MPX_E_RANGE, MPX_E_DECODE) leaves the
+    // carry as it was, so its records can be resubmitted or the engine dropped
+    struct NodeCarry {
+        std::unordered_map<uint64_t, uint32_t> live;
+        std::vector<uint64_t> round_b;
+        int64_t maxb = -1;
+        uint64_t ballot = 0;
+        uint32_t markers = 0;
+    };
+    std::vector<NodeCarry> next(wc ? N : 0);
+    std::vector<uint32_t> ents_gone;                             // carried batches no longer live
+    std::unordered_map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> ents_new;
 
     for (uint32_t n = 0; n < N; ++n) {
         const NodeStream &ns = nodes[n];
@@ -766,6 +785,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             const uint32_t j = (uint32_t)ht.b_msg.size();
             gid_local.emplace(gid, j);
             ht.b_msg.push_back(NONE32); ht.b_pstart.push_back(NONE32); ht.b_gid.push_back(gid);
+            ht.b_node.push_back(n);
             reps.emplace_back();
             b_bal_w.push_back(wc->b_bal[gid]);
             b_ent_w.push_back({0, 0});
@@ -805,7 +825,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             int64_t vote_j = -1;
             if (t == MPX_MSG_P_START) {
                 if (wc)                                  // earlier windows' batches can no longer be chosen
-                    for (auto &x : live) if (x.second < gid0) wc->b_ents.erase(x.second);
+                    for (auto &x : live) if (x.second < gid0) ents_gone.push_back(x.second);
                 live.clear();
                 cur_bal = ns.ballot[k];
             } else if (t == MPX_MSG_P_BATCH) {
@@ -886,6 +906,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                 if (wc) {
                     gid_local.emplace((uint32_t)gid_next, (uint32_t)ht.b_msg.size());
                     ht.b_gid.push_back((uint32_t)gid_next++);
+                    ht.b_node.push_back(n);
                     b_bal_w.push_back(cur_bal);
                     b_ent_w.push_back({ent, ns.cnt[k]});
                 }
@@ -943,9 +964,10 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             } else if (t == MPX_MSG_E_EPOCH) {
                 // the marker may delete / recreate the Acceptor or reset the Proposer
                 // (decided on the device): every bucket with state of the node gets the
-                // event (round buckets included), and the round stays listed
+                // event (round buckets included; a window: also state of earlier windows),
+                // and the round stays listed
                 for (uint64_t b = 0; (int64_t)b <= maxb; ++b)
-                    if (first_frag[b] < g) add_ev(b);
+                    if (first_frag[b] < g || (wc && wc->state_b[n][b])) add_ev(b);
             }
             if (t == MPX_MSG_P_BATCH) {
                 const uint32_t j = wc ? gid_local[(uint32_t)(gid_next - 1)] : (uint32_t)ht.b_msg.size() - 1;
@@ -958,17 +980,18 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             }
         }
         if (wc) {                                        // the carry past this node's window
-            wc->live[n] = live;
-            wc->round_b[n] = round_b;
-            wc->maxb[n] = maxb;
-            wc->round_ballot[n] = cur_bal;
+            NodeCarry &c = next[n];
             for (auto &x : live)                         // new batches still open: keep their entries
                 if (x.second >= gid0) {
                     const auto &be = b_ent_w[gid_local[x.second]];
-                    auto &dst = wc->b_ents[x.second];
-                    dst.clear();
+                    auto &dst = ents_new[x.second];
                     for (uint32_t q = 0; q < be.second; ++q) dst.push_back({ht.e_iid[be.first + q], ht.e_val[be.first + q]});
                 }
+            c.live = std::move(live);
+            c.round_b = round_b;
+            c.maxb = maxb;
+            c.ballot = cur_bal;
+            if (member) c.markers = wc->markers[n] + (uint32_t)(ht.ee_msg.size() - ht.ee_off[n]);
         }
     }
     ht.node_off[N] = ht.m_type.size();
@@ -977,7 +1000,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         ht.ee_off[N] = ht.ee_msg.size();
         ht.sc_off = sc_off;
         for (uint32_t n = 0; n < N; ++n)       // the device incarnation (G_SEG) counts at most one per marker
-            if (ht.ee_off[n + 1] - ht.ee_off[n] >= G_SEG) return MPX_E_RANGE;
+            if ((wc ? next[n].markers : ht.ee_off[n + 1] - ht.ee_off[n]) >= G_SEG) return MPX_E_RANGE;
     }
 
     // vote lists (attributed in the walk above)
@@ -997,11 +1020,6 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         ht.b_bal.resize(ht.b_msg.size());
         for (size_t j = 0; j < ht.b_msg.size(); ++j)
             ht.b_bal[j] = wc ? b_bal_w[j] : ht.b_pstart[j] == NONE32 ? 0 : ht.m_ballot[ht.b_pstart[j]];
-        if (wc) {
-            for (size_t j = 0; j < ht.b_msg.size(); ++j)
-                if (ht.b_msg[j] != NONE32) wc->b_bal.push_back(b_bal_w[j]);   // new batches, in id order
-            wc->batches = gid_next;
-        }
     }
 
     // fragment CSR per (node, bucket), stable (keeps message order)
@@ -1060,7 +1078,6 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                 ht.gp_base.push_back(wc->state_b[n][b]);
                 ht.pair_gp[p] = GP_ROUNDS;
             }
-        for (auto &x : state_new) wc->state_b[x.first][x.second] = 1;
         for (uint64_t b = 0; b < NB; ++b)
             if (ht.cf_off[b + 1] > ht.cf_off[b]) ht.cb_list.push_back((uint32_t)b);
         ht.num_gp_simple = ht.num_gp_snap = 0;
@@ -1118,6 +1135,23 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         }
     }
     ht.node_chunk_off[N] = (uint32_t)ht.chunk_node.size();
+    if (wc) {
+        // every check passed: the window is consumed, the carry moves past it
+        for (uint32_t n = 0; n < N; ++n) {
+            NodeCarry &c = next[n];
+            wc->live[n] = std::move(c.live);
+            wc->round_b[n] = std::move(c.round_b);
+            wc->maxb[n] = c.maxb;
+            wc->round_ballot[n] = c.ballot;
+            wc->markers[n] = c.markers;
+        }
+        for (uint32_t gid : ents_gone) wc->b_ents.erase(gid);
+        for (auto &x : ents_new) wc->b_ents[x.first] = std::move(x.second);
+        for (size_t j = 0; j < ht.b_msg.size(); ++j)
+            if (ht.b_msg[j] != NONE32) wc->b_bal.push_back(b_bal_w[j]);   // new batches, in id order
+        wc->batches = gid_next;
+        for (auto &x : state_new) wc->state_b[x.first][x.second] = 1;
+    }
     return MPX_OK;
 }
 

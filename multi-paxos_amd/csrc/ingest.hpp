@@ -67,6 +67,7 @@ struct WindowCarry {
     std::vector<std::vector<uint64_t>> round_b;                  // per node: buckets with promise-reply runs since
                                                                  //   its last P_START
     std::vector<uint64_t> b_bal;                                 // per global batch: its round's ballot
+    std::vector<uint32_t> markers;                               // member, per node: E_EPOCH markers so far
     // per global batch still live and not chosen: its entries {iid, handle}, for the
     // chosen log when a later window completes its votes
     std::unordered_map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> b_ents;
@@ -74,7 +75,7 @@ struct WindowCarry {
     {
         on = true; batches = 0;
         live.assign(N, {}); round_ballot.assign(N, 0); state_b.assign(N, std::vector<uint8_t>(NB, 0));
-        maxb.assign(N, -1); round_b.assign(N, {}); b_bal.clear(); b_ents.clear();
+        maxb.assign(N, -1); round_b.assign(N, {}); b_bal.clear(); b_ents.clear(); markers.assign(N, 0);
     }
 };
 
@@ -122,7 +123,7 @@ struct HostTrace {
     // its global id (new batches and earlier ones that get votes here; b_msg = NONE32 for
     // an earlier one), per work-list pair whether earlier windows left state in it, and the
     // buckets with chosen-log runs
-    std::vector<uint32_t> b_gid;
+    std::vector<uint32_t> b_gid, b_node;
     std::vector<uint8_t> gp_base;
     std::vector<uint32_t> cb_list;
 };
@@ -148,8 +149,8 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
 
 // Flatten node streams and build every index the kernels walk.  `epochs`
 // non-empty selects member semantics (role / version gates, E_EPOCH events).
-// With `wc` (incremental runs, multi semantics): `nodes` hold one window's records; the
-// window is built on the carried state and the carry is advanced past it.
+// With `wc` (incremental runs): `nodes` hold one window's records; the window is built on
+// the carried state and, only when the build succeeds, the carry is advanced past it.
 int build_trace(const std::vector<NodeStream> &nodes, uint64_t shard_begin, uint64_t shard_len,
                 const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc = nullptr);
 

@@ -151,8 +151,10 @@ __device__ inline uint64_t wave_max(uint64_t x)
 // the Acceptor is deleted, :1952-1957, or created, :1897-1901) | G_ACCCLR on that
 // flip | G_PRECLR when the Proposer is deleted, created or sees a new acceptor
 // set (AcceptorsChanged, :1504-1549).  Four passes at the head of every member run.
+// (an incremental window starts from the roles the windows before left, ee_init)
 __device__ inline uint32_t ee_genesis(const DevView &v, uint32_t n)
 {
+    if (v.window) return v.ee_init[n];
     return (1u << EE_SEG_SHIFT) | (((v.ep_amask[0] >> n) & 1) ? EE_ACC : 0) | (((v.ep_pmask[0] >> n) & 1) ? EE_PROP : 0);
 }
 
@@ -173,7 +175,7 @@ __device__ inline uint32_t ee_before(const DevView &v, uint32_t n, uint32_t g)
 // dependent global loads (a trace with more than GATE_LDS markers searches
 // global memory, as ee_before does).
 constexpr uint32_t GATE_LDS = 2048;
-struct GateLds { uint32_t msg[GATE_LDS], state[GATE_LDS]; uint64_t off[MPX_MAX_NODES + 1]; uint64_t am0, pm0; };
+struct GateLds { uint32_t msg[GATE_LDS], state[GATE_LDS]; uint64_t off[MPX_MAX_NODES + 1]; uint32_t init[MPX_MAX_NODES]; };
 __device__ inline bool gate_stage(const DevView &v, GateLds &L)
 {
     const uint64_t E = v.ee_off[v.N];
@@ -181,7 +183,7 @@ __device__ inline bool gate_stage(const DevView &v, GateLds &L)
     if (staged)
         for (uint32_t i = threadIdx.x; i < E; i += blockDim.x) { L.msg[i] = v.ee_msg[i]; L.state[i] = v.ee_state[i]; }
     for (uint32_t i = threadIdx.x; i <= v.N; i += blockDim.x) L.off[i] = v.ee_off[i];
-    if (threadIdx.x == 0) { L.am0 = v.ep_amask[0]; L.pm0 = v.ep_pmask[0]; }
+    for (uint32_t i = threadIdx.x; i < v.N; i += blockDim.x) L.init[i] = ee_genesis(v, i);
     __syncthreads();
     return staged;
 }
@@ -194,8 +196,7 @@ __device__ inline uint32_t ee_before_lds(const DevView &v, const GateLds &L, boo
         const uint32_t mid = (lo + hi) >> 1;
         if (L.msg[mid] < g) lo = mid + 1; else hi = mid;
     }
-    return lo > first ? L.state[lo - 1]
-                      : (1u << EE_SEG_SHIFT) | (((L.am0 >> n) & 1) ? EE_ACC : 0) | (((L.pm0 >> n) & 1) ? EE_PROP : 0);
+    return lo > first ? L.state[lo - 1] : L.init[n];
 }
 
 // pass 1: one block per node; its markers' epochs and role sets are loaded in
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(256) void k_gate_epochs(DevView v)
     const uint32_t n = blockIdx.x, j = threadIdx.x;
     const uint64_t k0 = v.ee_off[n], k1 = v.ee_off[n + 1];
     uint32_t st = ee_genesis(v, n);                      // lane 0's walk state
-    uint64_t am_prev = v.ep_amask[0];                   // the acceptor set of st's epoch
+    uint64_t am_prev = v.ep_amask[st & 0xFFFF];         // the acceptor set of st's epoch
     for (uint64_t c = k0; c < k1; c += 256) {
         const uint32_t m = (uint32_t)(k1 - c < 256 ? k1 - c : 256);
         if (j < m) {
@@ -241,6 +242,7 @@ __global__ __launch_bounds__(256) void k_gate_epochs(DevView v)
         }
         __syncthreads();
     }
+    if (v.window && j == 0) v.ee_out[n] = st;           // the roles the next window starts from
 }
 
 // pass 2: every other record of the trace
@@ -309,7 +311,8 @@ __global__ __launch_bounds__(256) void k_gate_votes(DevView v)
     __shared__ GateLds L;                               // msg: the markers, state: their G_PRECLR bit
     const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     uint32_t g0 = 0, n = 0;
-    if (j < v.num_batches) { g0 = v.b_msg[j]; n = v.m_node[g0]; }
+    // (a window: a batch of an earlier window has no message here, b_msg NONE32; its node is b_node)
+    if (j < v.num_batches) { g0 = v.b_msg[j]; n = v.window ? v.b_node[j] : v.m_node[g0]; }
     const uint64_t E = v.ee_off[v.N];
     const bool staged = E <= GATE_LDS;
     if (staged)
@@ -321,14 +324,19 @@ __global__ __launch_bounds__(256) void k_gate_votes(DevView v)
     __syncthreads();
     if (j >= v.num_batches) return;
     uint32_t kill = NONE32;
-    if (!(v.m_gate[g0] >> G_EPOCH_SHIFT)) {
+    const bool carried = g0 == NONE32;                  // first marker of the window: "after the batch"
+    const uint32_t gid = v.window && j < v.num_batches ? v.b_gid[j] : 0;
+    const uint32_t gs = carried ? 0 : g0;
+    if (carried && (v.g_done[gid] & 2)) {
+        kill = 0;                                       // cleared in an earlier window
+    } else if (!carried && !(v.m_gate[g0] >> G_EPOCH_SHIFT)) {
         kill = g0;
     } else if (staged) {
         uint32_t lo = (uint32_t)L.off[n], hi = (uint32_t)L.off[n + 1];
         const uint32_t end = hi;
         while (lo < hi) {                               // first marker after the batch
             const uint32_t mid = (lo + hi) >> 1;
-            if (L.msg[mid] < g0) lo = mid + 1; else hi = mid;
+            if (L.msg[mid] < gs) lo = mid + 1; else hi = mid;
         }
         for (; lo < end; ++lo)
             if (L.state[lo]) { kill = L.msg[lo]; break; }
@@ -336,11 +344,12 @@ __global__ __launch_bounds__(256) void k_gate_votes(DevView v)
         uint64_t lo = v.ee_off[n], hi = v.ee_off[n + 1];
         while (lo < hi) {                               // first marker after the batch
             const uint64_t mid = (lo + hi) >> 1;
-            if (v.ee_msg[mid] < g0) lo = mid + 1; else hi = mid;
+            if (v.ee_msg[mid] < gs) lo = mid + 1; else hi = mid;
         }
         for (; lo < v.ee_off[n + 1]; ++lo)
             if (v.m_gate[v.ee_msg[lo]] & G_PRECLR) { kill = v.ee_msg[lo]; break; }
     }
+    if (v.window && kill != NONE32) v.g_done[gid] |= 2;   // no vote counts in a later window
     // (the replies one per thread, each finding its batch in the block's offsets:
     // 21.8 vs 15.1 us at C5)
     for (uint64_t r = v.b_rep_off[j]; r < v.b_rep_off[j + 1]; ++r) {
@@ -371,8 +380,13 @@ __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64
     }
     for (uint64_t i = t; i < (v.window ? 0 : v.NB); i += T) v.chosen_valid[i] = 0;
     for (uint64_t i = t; i < 8ull * n_partials; i += T) v.partials[i] = 0;
-    // nodes without messages keep promised = max_seen = 0 (a window: what the windows before left)
-    for (uint64_t i = t; i < 2ull * v.N; i += T) v.node_scal[i] = v.window ? v.scal_base[i] : 0;
+    // nodes without messages keep promised = max_seen = 0 (a window: what the windows before left;
+    // member keys carry the Acceptor's incarnation above LOW56, the readback does not)
+    for (uint64_t i = t; i < 2ull * v.N; i += T) {
+        const uint64_t k = v.window ? v.scal_base[i] : 0;
+        v.node_scal[i] = v.semantics == MPX_SEM_MEMBER ? k & LOW56 : k;
+        if (v.window) v.scal_key[i] = k;
+    }
     for (uint64_t i = t; i < v.out_subs; i += T) v.out_cursor[OUT_STRIDE * i] = 0;
     if (t == 0) {
         v.fast_rest[0] = 0;
@@ -457,6 +471,7 @@ __global__ __launch_bounds__(256) void k_scan_node(DevView v)
         carry_p = carry_p > tp ? carry_p : tp;
         carry_s = carry_s > ts ? carry_s : ts;
     }
+    if (v.window && threadIdx.x == 0) { v.scal_key[2 * n] = carry_p; v.scal_key[2 * n + 1] = carry_s; }
     if (v.semantics == MPX_SEM_MEMBER) { carry_p &= LOW56; carry_s &= LOW56; }   // current incarnation
     if (threadIdx.x == 0) { v.node_scal[2 * n] = carry_p; v.node_scal[2 * n + 1] = carry_s; }
 }
@@ -550,6 +565,7 @@ __device__ inline void scan_apply_chunk(const DevView &v, const uint32_t c, uint
         // the node's last chunk: its promised / max_seen after the whole stream
         uint64_t tp = cp, ts = cs;
         for (uint32_t i = 0; i < 4; ++i) { tp = tp > l[0][i] ? tp : l[0][i]; ts = ts > l[1][i] ? ts : l[1][i]; }
+        if (v.window) { v.scal_key[2 * cn] = tp; v.scal_key[2 * cn + 1] = ts; }   // the next window's carry-in
         if (member) { tp &= LOW56; ts &= LOW56; }   // current incarnation
         v.node_scal[2 * cn] = tp;
         v.node_scal[2 * cn + 1] = ts;
@@ -610,15 +626,6 @@ __device__ inline void scan_apply_chunk(const DevView &v, const uint32_t c, uint
     }
 }
 
-template <bool MEMBER>
-__global__ __launch_bounds__(256) void k_scan_apply(DevView v)
-{
-    __shared__ uint64_t l[2][4], lc[2][4];
-    __shared__ uint64_t lky[SCAN_CHUNK];        // phase 2 reads its rounds back from LDS,
-    __shared__ uint8_t lty[SCAN_CHUNK];         // so the round loop needs few registers
-    __shared__ uint32_t lix[SCAN_CHUNK];        // and no dependent load of the message index per round
-    scan_apply_chunk<MEMBER>(v, blockIdx.x, l, lc, lky, lty, lix);
-}
 
 // --------------------------------------------------------- proposer side --
 // Promise quorum per node (OnPrepareReply, multi/paxos.cpp:1036-1057; member
@@ -734,11 +741,6 @@ __device__ inline void prop_chunk_wave(const DevView &v, const uint32_t c)
     }
 }
 
-__global__ __launch_bounds__(64) void k_prop_chunk(DevView v)
-{
-    prop_chunk_wave(v, blockIdx.x);
-}
-
 // pass 2: one wave per node, its chunks in order: the records before each
 // chunk's first head under the state carried from the chunk before
 __global__ __launch_bounds__(64) void k_prop_node(DevView v)
@@ -807,7 +809,7 @@ __device__ inline void votes_block(const DevView &v, const uint32_t blk, uint64_
     // a window: the batch's accepted_ so far, and no more votes once an earlier window chose it
     // (OnAcceptReply erases the batch at quorum, multi/paxos.cpp:1416-1424)
     const uint32_t gid = v.window && have ? v.b_gid[j] : 0;
-    const bool done = v.window && have && v.g_done[gid];
+    const bool done = v.window && have && (v.g_done[gid] & 1);
     if (v.window && have) mask = v.g_mask[gid];
     for (uint64_t r = done ? re : rs; r < re; ++r) {
         const uint64_t o = r - r0;
@@ -835,15 +837,8 @@ __device__ inline void votes_block(const DevView &v, const uint32_t blk, uint64_
     if (have) v.b_chosen[j] = chosen_r == ~0ull ? NONE32 : v.b_rep[chosen_r];
     if (v.window && have && !done) {
         v.g_mask[gid] = mask;
-        if (chosen_r != ~0ull) v.g_done[gid] = 1;
+        if (chosen_r != ~0ull) v.g_done[gid] |= 1;
     }
-}
-
-__global__ __launch_bounds__(256) void k_votes(DevView v)
-{
-    __shared__ uint64_t lbal[4][VOTE_LDS];
-    __shared__ uint32_t lsrc[4][VOTE_LDS];
-    votes_block(v, blockIdx.x, lbal, lsrc);
 }
 
 // The header kernels that depend only on the scan chunks' aggregates (or on nothing) in
@@ -1033,9 +1028,9 @@ __device__ inline uint64_t slot_digest(const DevView &v, uint32_t n, uint64_t ii
 // Wave id with consecutive ids on one XCD: workgroups are dealt round-robin
 // over the 8 XCDs (blockIdx % 8), so id = xcd * (waves per XCD) + local id.
 // Neighbouring buckets then share their XCD's L2 (headers, descriptors).
-__device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
+__device__ inline uint64_t xcd_wave_id(uint32_t wv)
 {
-    if ((gridDim.x & 7) || (knobs & 1)) return (uint64_t)blockIdx.x * 4 + wv;
+    if (gridDim.x & 7) return (uint64_t)blockIdx.x * 4 + wv;
     const uint64_t per = (uint64_t)(gridDim.x >> 3) * 4;
     return (uint64_t)(blockIdx.x & 7) * per + (uint64_t)(blockIdx.x >> 3) * 4 + wv;
 }
@@ -1075,8 +1070,7 @@ __device__ inline uint64_t xcd_wave_id(uint32_t wv, uint32_t knobs = 0)
 // its snapshot events see empty state, so skipping them changes no output.
 constexpr uint32_t FAST_PAIR_FRAGS = 2;      // descriptors a pair lane prefetches
 constexpr uint64_t EV_BIT = 1ull << 63;      // k_apply_fast: pair_gp folded into the lane's CSR offset
-constexpr uint64_t DONE_BIT = 1ull << 62;    // ... and (AFTER_STORE) "k_plan planned this pair"
-constexpr uint64_t OFF_FLAGS = EV_BIT | DONE_BIT;
+constexpr uint64_t OFF_FLAGS = EV_BIT;
 __host__ __device__ inline uint32_t fast_group(uint32_t N, uint32_t cap = 4)
 {
     return N ? (63 / N < cap ? 63 / N : cap) : 1;
@@ -1089,7 +1083,7 @@ __device__ inline bool frag_lean(uint64_t w1)
 }
 __device__ inline bool frag_full(uint64_t w1) { return ((w1 >> 48) & 0xFF) == 0 && ((w1 >> 32) & 0xFFFF) == BS; }
 
-template <int WAVES_PER_EU, bool DIGEST, bool AFTER_STORE = false>
+template <int WAVES_PER_EU, bool DIGEST>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
 {
     constexpr uint32_t F = FAST_PAIR_FRAGS;
@@ -1099,9 +1093,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
     const uint32_t N = v.N;
     const uint64_t NB = v.NB;
     if (N > FAST_MAX_NODES) return;
-    // after k_plan + k_store only the pairs k_plan counted are left
-    if (AFTER_STORE && *v.fast_rest == 0) return;
-    const uint32_t G = fast_group(N, (v.knobs >> 8) & 15 ? (v.knobs >> 8) & 15 : 4);
+    const uint32_t G = fast_group(N);
     const uint64_t steps = (NB + G - 1) / G;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
@@ -1114,8 +1106,6 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         if (st >= steps) return;
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
         if (lane <= nb * N) oa = v.f_off[b0 * N + lane] | (lane < nb * N && v.pair_gp[b0 * N + lane] ? EV_BIT : 0);
-        if (AFTER_STORE && lane < nb * N && v.st_valid[b0 * N + lane])   // set only by k_plan so far
-            oa |= DONE_BIT;
         if (lane <= nb) oc = v.cf_off[b0 + lane];
     };
     // stage 2 (one step ahead): each pair's first F descriptors, each
@@ -1145,7 +1135,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         }
     };
 
-    uint64_t st_c = xcd_wave_id(wv, v.knobs);
+    uint64_t st_c = xcd_wave_id(wv);
     uint64_t oa_c, oc_c, oa_n, oc_n;
     ld_off(st_c, oa_c, oc_c);
     ld_off(st_c + nwaves, oa_n, oc_n);
@@ -1155,7 +1145,6 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         const uint64_t st = st_c;
         const uint64_t b0 = st * G, nb = NB - b0 < G ? NB - b0 : G;
         const bool pev = (oa_c & EV_BIT) != 0;                 // the pair has snapshot events
-        const bool done = (oa_c & DONE_BIT) != 0;              // k_plan + k_store wrote it
         const uint64_t oa = oa_c & ~OFF_FLAGS;
         const uint64_t pev_m = __ballot(pev);
         uint64_t e[F], w[F];
@@ -1173,13 +1162,13 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         for (uint32_t k = 0; k < F; ++k) fg[k] = (uint32_t)w[k] != NONE32 ? v.m_flags[(uint32_t)w[k]] : 0;
         const uint32_t clive = (uint32_t)cw != NONE32 ? v.b_chosen[(uint32_t)cw] != NONE32 : 0;
         // One wait per step, before its stores (vmcnt(0); expcnt / lgkmcnt free).
-        if (!(v.knobs & 32)) __builtin_amdgcn_s_waitcnt(0x0F70);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
 
         // plan, one pair per lane
         const uint64_t o1 = __shfl(oa, (int)((lane + 1) & 63), 64);
         const bool pair = lane < nb * N;
         const uint32_t len = pair ? (uint32_t)(o1 - oa) : 0;
-        const bool in_list = len && len <= FAST_MAX_FRAGS && !done;         // else: general work list / stored
+        const bool in_list = len && len <= FAST_MAX_FRAGS;                  // else: the general work list
         bool elig = in_list && len <= F, full = true, again = false, comm = false;
         uint32_t fix = NONE32, nA = 0, nL = 0;
 #pragma unroll
@@ -1208,9 +1197,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
                 if (!((uni_m >> p) & 1)) continue;
                 const uint32_t q = rl32(qv, p);
                 const uint32_t sq = rl32(ql, p);
-                if (v.knobs & 16) {
-                    // experiment: no state stores
-                } else if (whole) {
+                if (whole) {
                     st_put4(v, row + g * BS + s0, sq, sq, sq, sq);
                 } else {
 #pragma unroll
@@ -1303,9 +1290,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
             const uint64_t pbase = f_base;             // the pair's first fragment
             const uint32_t l0 = q0 ? (uint32_t)(q0 - pbase) : 0, l1 = q1 ? (uint32_t)(q1 - pbase) : 0,
                            l2 = q2 ? (uint32_t)(q2 - pbase) : 0, l3 = q3 ? (uint32_t)(q3 - pbase) : 0;
-            if (v.knobs & 16) {
-                // experiment: no state stores
-            } else if (li0 + BS <= v.shard_len) {
+            if (li0 + BS <= v.shard_len) {
                 st_put4(v, srow + s0, l0, l1, l2, l3);
             } else {
                 if (li0 + s0 < v.shard_len) st_put(v, srow + s0, l0);
@@ -1319,7 +1304,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply_fast(DevView v)
         }
 
         // chosen log of the buckets whose one live batch is a full run
-        const bool cok = !AFTER_STORE && clive && frag_full(cw) && (b0 + lane + 1) * BS <= v.shard_len;
+        const bool cok = clive && frag_full(cw) && (b0 + lane + 1) * BS <= v.shard_len;
         const uint64_t cok_m = __ballot(cok);
         if (cok) v.chosen_valid[b0 + lane] = 1;
         for (uint64_t m = cok_m; m; m &= m - 1) {
@@ -1956,7 +1941,7 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
     const uint64_t whole = v.shard_len >> BSH;            // buckets wholly inside the shard
     const uint64_t cpr = whole / C, S = (uint64_t)(N + 1) * cpr;   // rows 0..N-1 state, row N chosen log
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
-    const uint64_t wid = xcd_wave_id(wv, v.knobs);
+    const uint64_t wid = xcd_wave_id(wv);
     const uint32_t s0 = 4 * lane;
     uint32_t *const sink = v.store_dummy + (wid & 63) * BS;
     T *const st = static_cast<T *>(v.st);
@@ -1993,7 +1978,7 @@ __global__ __launch_bounds__(256) void k_store8(DevView v)
     const uint64_t whole = v.shard_len >> BSH;
     const uint64_t cpr = whole / C, S = (uint64_t)(N + 1) * cpr;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
-    const uint64_t wid = xcd_wave_id(wv, v.knobs);
+    const uint64_t wid = xcd_wave_id(wv);
     uint8_t *const st = static_cast<uint8_t *>(v.st);
     uint8_t *const sink = reinterpret_cast<uint8_t *>(v.store_dummy) + (wid & 63) * 1024 + 16 * lane;
     const uint32_t p16 = 16 * (lane & 15);                 // the lane's first slot in its bucket
@@ -2164,12 +2149,12 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
             }
             first = false;
             const uint32_t fmsg = (uint32_t)fw1;
-            // the window's events that can act (knob 524288: walk every listed event, A/B):
+            // the window's events that can act:
             // a rejected PREPARE, or a member E_EPOCH that neither deletes nor recreates the
             // node's Acceptor (nor, with rounds, resets its Proposer), changes nothing here
             // — member pairs get every marker of their node, most of them such no-ops
             uint64_t umask = ~0ull;
-            if (!SIMPLE && !(v.knobs & 524288)) {
+            if (!SIMPLE) {
                 const uint32_t t8l = einfo & 0xFF, fll = einfo >> 8;
                 bool u = t8l == MPX_MSG_PREPARE && (fll & F_GRANTED);
                 if (MEMBER) u = u || (t8l == MPX_MSG_E_EPOCH && (fll & (ROUNDS ? (F_ACCCLR | F_PRECLR) : F_ACCCLR)));
@@ -2240,7 +2225,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             if (k[j] >= 0) {
                                 const uint32_t x = (uint32_t)(ent + k[j]);
                                 if (SF(j) & S_COMMITTED) {                            // :1508
-                                    if (se[j] != x && !(v.knobs & 32768) && e_val[se[j]] != e_val[x])   // knob 32768: experiment
+                                    if (se[j] != x && e_val[se[j]] != e_val[x])
                                         record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
                                                          v.shard_begin + li0 + lane + 64 * j);
                                 } else {
@@ -2250,28 +2235,17 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                 ++cL;
                             }
                     } else if (ROUNDS && kind == K_PREPLY) {
-                        if ((mf & F_COUNTED) && !(v.knobs & 8192)) {       // knob 8192: experiment, no merge
-                            if (!(v.knobs & 1048576)) {
-                                // the run's proposal ids all in flight, then the merge
-                                // (knob 1048576: one load per slot in turn, A/B)
-                                uint64_t pid[SPL];
+                        if (mf & F_COUNTED) {
+                            // the run's proposal ids all in flight, then the merge
+                            uint64_t pid[SPL];
 #pragma unroll
-                                for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
+                            for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
 #pragma unroll
-                                for (uint32_t j = 0; j < SPL; ++j)
-                                    if (k[j] >= 0) {
-                                        const u64x2 cur = pre[lane + 64 * j];
-                                        if (!cur.y || pid[j] > cur.x) pre[lane + 64 * j] = u64x2{pid[j], W_PRESENT | (ent + k[j])};   // :1216-1221
-                                    }
-                            } else {
-#pragma unroll 1
-                                for (uint32_t j = 0; j < SPL; ++j)
-                                    if (k[j] >= 0) {
-                                        const uint64_t pid = v.r_pid[ent + k[j]];
-                                        const u64x2 cur = pre[lane + 64 * j];
-                                        if (!cur.y || pid > cur.x) pre[lane + 64 * j] = u64x2{pid, W_PRESENT | (ent + k[j])};
-                                    }
-                            }
+                            for (uint32_t j = 0; j < SPL; ++j)
+                                if (k[j] >= 0) {
+                                    const u64x2 cur = pre[lane + 64 * j];
+                                    if (!cur.y || pid[j] > cur.x) pre[lane + 64 * j] = u64x2{pid[j], W_PRESENT | (ent + k[j])};   // :1216-1221
+                                }
                         }
                     }
                     ++a;
@@ -2279,7 +2253,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                     const uint32_t g = em;
                     const uint32_t info = rl32(einfo, c);
                     const uint32_t t8 = info & 0xFF, fl = info >> 8;
-                    if (t8 == MPX_MSG_PREPARE && !(v.knobs & 4096)) {   // knob 4096: experiment, no snapshots
+                    if (t8 == MPX_MSG_PREPARE) {
                         bool have = false;
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) have |= (SF(j) & S_PRESENT) != 0;
@@ -2288,8 +2262,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             // ingest listed which of them meet this bucket (ev_aux, in the
                             // event window: first range | count, or one range's bucket-local
                             // interval inline — then no range loads at all)
-                            // (knob 131072: A/B against the loaded word and the range loads)
-                            const uint64_t ax = (v.knobs & 131072) ? v.ev_aux[ei + c] & ~EVX_ONE : rl64(eax, c);
+                            const uint64_t ax = rl64(eax, c);
                             bool hit[SPL];
                             if (ax & EVX_ONE) {
                                 const uint32_t il = (uint32_t)(ax >> 40) & 0x1FF, ih = (uint32_t)(ax >> 49) & 0x1FF;
@@ -2342,7 +2315,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j)
                             if (!(SF(j) & S_COMMITTED)) { if (DIGEST) sb[j] = 0; SF_SET(j, 0); se[j] = sm[j] = 0; }
-                    } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM) && !(v.knobs & 16384)) {   // knob 16384: experiment
+                    } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
                         bool hit[SPL];
                         uint32_t ref[SPL], ext[SPL];
 #pragma unroll
@@ -2400,7 +2373,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
 }
 
 // ------------------------------------------------------------ windows ----
-// Incremental runs (MPX_FLAG_INCREMENTAL, multi semantics).  The trace
+// Incremental runs (MPX_FLAG_INCREMENTAL).  The trace
 // arrays hold one window of records; what the windows before left is carried as values:
 // the acceptor / learner state (s_bal, s_val), a promise round's pre-accepted map (p_pid,
 // p_val, tagged per pair with its round's ballot), the chosen log (c_val), the scalars and
@@ -2443,7 +2416,13 @@ __device__ inline void emit_vals(const DevView &v, const bool (&want)[SPL_], uin
 // UpdateByPreAcceptedValues (:1201-1223: the highest proposal id wins, first arrival on
 // ties), the quorum's merged map (:1047-1105) and StartPrepare's clear (:1233-1248) —
 // but the slot state is {ballot, handle | flags} itself, started from what earlier
-// windows left and written back at the end.
+// windows left and written back at the end.  MEMBER: the member Acceptor / Learner
+// (member/paxos.cpp:1744-1793, 1029-1060) — accept and learn insert (the first Value and
+// its proposal id stick), a learned instance takes no accept (its Value must agree), a
+// learn replaces the accepted entry, and an E_EPOCH marker that deletes / recreates the
+// node's Acceptor clears what it accepted (:1952-1957) or, resetting its Proposer, the
+// pre-accepted map (the flags k_gate_epochs wrote from the carried roles).
+template <bool MEMBER>
 __global__ __launch_bounds__(256) void k_apply_win(DevView v)
 {
     __shared__ uint16_t lidx_all[4][BS];
@@ -2503,7 +2482,32 @@ __global__ __launch_bounds__(256) void k_apply_win(DevView v)
                     const uint64_t ballot = rl64(fbal, a);
                     int k[SPL];
                     frag_slots(lidx, kind == K_PREPLY ? v.r_slot : v.e_slot, ent, cnt, st0, (fl & FR_DENSE) != 0, k);
-                    if (kind == K_ACCEPT) {
+                    if (MEMBER && (kind == K_ACCEPT || kind == K_COMMIT)) {
+                        const bool learn = kind == K_COMMIT;
+                        if (learn || (mf & F_GRANTED)) {
+                            uint64_t pid[SPL], hv[SPL];
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j) {
+                                pid[j] = k[j] >= 0 ? v.e_pid[ent + k[j]] : 0;
+                                hv[j] = k[j] >= 0 ? v.e_val[ent + k[j]] : 0;
+                            }
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j) {
+                                if (k[j] < 0) continue;
+                                if (sval[j] & W_COMMITTED) {                                  // :1763-1769, :1398
+                                    if ((sval[j] & W_HANDLE) != hv[j] && (!learn || (mf & F_PROP)))
+                                        record_violation(v, MPX_V_LEARN_VALUE, n, rl32(fmsg, a) - (uint32_t)v.node_off[n],
+                                                         v.shard_begin + li0 + lane + 64 * j);
+                                } else if (learn) {                                           // :1040, :1786-1793
+                                    sbal[j] = pid[j]; sval[j] = W_PRESENT | W_COMMITTED | hv[j];
+                                } else if (!(sval[j] & W_PRESENT)) {                          // :1765 insert
+                                    sbal[j] = pid[j]; sval[j] = W_PRESENT | hv[j];
+                                    ++cA;
+                                }
+                                cL += learn;
+                            }
+                        }
+                    } else if (kind == K_ACCEPT) {
                         if (mf & F_GRANTED) {
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
@@ -2582,9 +2586,20 @@ __global__ __launch_bounds__(256) void k_apply_win(DevView v)
                             }
                             emit_vals(v, hit, g, 0, v.shard_begin + li0, sbal, sval, kx);
                         }
-                    } else if (t8 == MPX_MSG_P_START) {
+                    } else if (t8 == MPX_MSG_P_START || (MEMBER && t8 == MPX_MSG_E_EPOCH && (fl & F_PRECLR))) {
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) pre[lane + 64 * j] = u64x2{0, 0};
+                        if (MEMBER && t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j)
+                                if (!(sval[j] & W_COMMITTED)) { sbal[j] = 0; sval[j] = 0; }
+                        }
+                    } else if (MEMBER && t8 == MPX_MSG_E_EPOCH && (fl & F_ACCCLR)) {
+                        // the Acceptor is deleted / recreated: its accepted values go
+                        // (member/paxos.cpp:1952-1957); learned ones stay with the Learner
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j)
+                            if (!(sval[j] & W_COMMITTED)) { sbal[j] = 0; sval[j] = 0; }
                     } else if (t8 == MPX_MSG_PREPARE_REPLY && (fl & F_QUORUM)) {
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) {
@@ -2781,14 +2796,12 @@ __device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, uns
 
 // Chosen log, one wave per bucket, for the buckets k_apply_fast did not
 // write from registers (multi) or every bucket (member: chosen_valid is 0).
-// REDUCE: the last workgroup to finish (a ticket after each one's partials are
-// visible device-wide) also folds every partial into the summary (k_reduce's work)
-template <bool REDUCE>
-__global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base, uint32_t n_partials)
+// (Folding the summary into its last workgroup was measured slower: every workgroup's
+// device-scope fence writes back its XCD's L2 before the ticket; C4 tail 75 vs 15 us.)
+__global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base)
 {
     __shared__ uint16_t lidx_all[4][BS];
     __shared__ unsigned long long red[4][8];
-    __shared__ uint32_t last;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint16_t *lidx = lidx_all[wv];
 #pragma unroll
@@ -2823,19 +2836,9 @@ __global__ __launch_bounds__(256) void k_chosen(DevView v, uint32_t partial_base
         unsigned long long s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         v.partials[8 * (partial_base + blockIdx.x) + (t == 0 ? PC_C : PC_DCHOSEN)] = s;
     }
-    if (!REDUCE) return;
-    __threadfence();                             // this workgroup's partials, device-wide (every XCD)
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(&v.fast_rest[1], 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();                             // the other workgroups' partials
-    reduce_summary(v, n_partials, red, 0, 256, true);
-    if (threadIdx.x == 0) v.fast_rest[1] = 0;
 }
 
-// the summary pass (the default; knob 16777216: k_chosen's last block instead, A/B): one
-// partial row per thread, every row's loads in flight at once over cdiv(rows, 256) workgroups
+// the summary pass: one partial row per thread, every row's loads in flight at once over cdiv(rows, 256) workgroups
 // (one workgroup of 512 threads looping over the rows waited out six memory latencies in turn:
 // 10.7 us at the C4 shard)
 __global__ __launch_bounds__(256) void k_reduce(DevView v, uint32_t n_partials)
@@ -3236,6 +3239,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     void *ev_begin = ev[0], *ev_apply0 = ev[1], *ev_apply1 = ev[2], *ev_general = ev[3], *ev_end = ev[4];
     hipStream_t s = (hipStream_t)stream_;
     const uint32_t n_partials = g.apply_wgs + g.chosen_wgs;
+    const bool member = v.semantics == MPX_SEM_MEMBER;
     uint64_t reset_n = ((uint64_t)v.N * v.NB + 15) / 16;
     if (v.NB > reset_n) reset_n = v.NB;
     if (8ull * n_partials > reset_n) reset_n = 8ull * n_partials;
@@ -3244,12 +3248,12 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     // Phase events ride on kernel dispatches (hipExtLaunchKernelGGL start / stop events) where a
     // kernel begins or ends the phase: a separate event record costs a 5-10 us bubble between
     // dependent kernels (rocprof, C4: 16 us of a 395 us step)
-    // multi: the reset rides on the first header-scan kernel (knob 33554432: its own launch, A/B)
-    const bool fold_reset = v.semantics != MPX_SEM_MEMBER && v.num_chunks && !(v.knobs & 33554432);
+    // multi: the reset rides on the first header-scan kernel (one launch less per step)
+    const bool fold_reset = !member && v.num_chunks;
     if (!fold_reset)
         hipExtLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s,
                               (hipEvent_t)ev_begin, (hipEvent_t)nullptr, 0, v, n_partials);
-    if (v.semantics == MPX_SEM_MEMBER) {
+    if (member) {
         // member role / version gates from the E_EPOCH markers (k_gate_*)
         hipLaunchKernelGGL(k_gate_epochs, dim3(v.N), dim3(256), 0, s, v);
         if (v.num_msgs) hipLaunchKernelGGL(k_gate_msgs, dim3(cdiv(v.num_msgs, 256)), dim3(256), 0, s, v);
@@ -3263,51 +3267,41 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         else hipLaunchKernelGGL(k_scan_chunk<false>, dim3(v.num_chunks), dim3(256), 0, s, v, n_partials);
         if (v.scan_node_pass) hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);   // long node streams
     }
-    // the scan's flag pass, the promise-quorum chunks and the accept votes: one launch
-    // (k_headers); knob 134217728: three launches (A/B)
-    const bool member_sem = v.semantics == MPX_SEM_MEMBER;
-    if (!(v.knobs & 134217728)) {
+    // the scan's flag pass, the promise-quorum chunks and the accept votes: one launch (k_headers)
+    {
         const uint32_t nb_scan = v.num_chunks, nb_prop = cdiv(v.num_pc, 4), nb_votes = cdiv(v.num_batches, 256);
         if (nb_scan + nb_prop + nb_votes) {
-            if (member_sem) hipLaunchKernelGGL(k_headers<true>, dim3(nb_scan + nb_prop + nb_votes), dim3(256), 0, s, v, nb_scan, nb_prop);
+            if (member) hipLaunchKernelGGL(k_headers<true>, dim3(nb_scan + nb_prop + nb_votes), dim3(256), 0, s, v, nb_scan, nb_prop);
             else hipLaunchKernelGGL(k_headers<false>, dim3(nb_scan + nb_prop + nb_votes), dim3(256), 0, s, v, nb_scan, nb_prop);
         }
-    } else {
-        if (v.num_chunks) {
-            if (member_sem) hipLaunchKernelGGL(k_scan_apply<true>, dim3(v.num_chunks), dim3(256), 0, s, v);
-            else hipLaunchKernelGGL(k_scan_apply<false>, dim3(v.num_chunks), dim3(256), 0, s, v);
-        }
-        if (v.num_pc) hipLaunchKernelGGL(k_prop_chunk, dim3(v.num_pc), dim3(64), 0, s, v);
-        if (v.num_batches) hipLaunchKernelGGL(k_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
     }
     // (a window: every node's round after the window, prop_out, comes from k_prop_node)
     if ((v.num_pc && v.pc_multi) || v.window) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s, v);
     if (v.window) {
-        // incremental window (multi): every pair of the window on the value-state walk, the
-        // chosen log of the batches chosen in it, the summary
-        hipExtLaunchKernelGGL(k_apply_win, dim3(g.apply_wgs), dim3(256), 0, s, (hipEvent_t)ev_apply0,
-                              (hipEvent_t)ev_general, 0, v);
+        // incremental window: every pair of the window on the value-state walk, the chosen log
+        // of the batches chosen in it, the summary
+        if (member) hipExtLaunchKernelGGL(k_apply_win<true>, dim3(g.apply_wgs), dim3(256), 0, s, (hipEvent_t)ev_apply0,
+                                          (hipEvent_t)ev_general, 0, v);
+        else hipExtLaunchKernelGGL(k_apply_win<false>, dim3(g.apply_wgs), dim3(256), 0, s, (hipEvent_t)ev_apply0,
+                                   (hipEvent_t)ev_general, 0, v);
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
         hipLaunchKernelGGL(k_chosen_win, dim3(g.chosen_wgs), dim3(256), 0, s, v, g.apply_wgs);
         hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
         return (int)hipGetLastError();
     }
-    const bool member = v.semantics == MPX_SEM_MEMBER;
     // plan path (the timed step): k_plan (multi: the lean pairs) / k_plan_list (the work
     // list's pairs without promise rounds) + store, then k_apply over the pairs k_plan_list
-    // listed and the promise-round pairs; knob 64: every pair walked (as the digested run),
-    // knob 8388608: multi without k_plan_list (the work list on the host-built ranges), A/B
-    const bool plan_path = !v.digest && !(v.knobs & 64) && (member || v.N <= FAST_MAX_NODES);
-    const bool lplan = plan_path && (member || (v.num_gp_snap && !(v.knobs & 8388608)));
+    // listed and the promise-round pairs.  A digested run (verification) and v.walk_all
+    // (MPX_STEP_WALK=1) walk every pair instead, as do multi traces with more than
+    // FAST_MAX_NODES nodes.
+    const bool plan_path = !v.digest && !v.walk_all && (member || v.N <= FAST_MAX_NODES);
+    const bool lplan = plan_path && (member || v.num_gp_snap);
     if (ev_apply0 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
     // the plan words of every (row, bucket) -> state rows and the chosen log
+    // (1-byte slots: 128-bucket chunks, 32 KiB per row and two plan words per lane, 0.295 vs
+    // 0.315 ms for 64-bucket chunks at C4)
     auto launch_store = [&](hipEvent_t stop) {
-        if (v.slot_w == 1 && (v.knobs & 128))
-            hipExtLaunchKernelGGL((k_store<32, true, uint8_t, u8x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
-        // 128-bucket chunks (32 KiB per row, two plan words per lane): A/B 0.295 vs 0.315 ms for 64
-        else if (v.slot_w == 1 && (v.knobs & 2048))
-            hipExtLaunchKernelGGL((k_store8<true, 64>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
-        else if (v.slot_w == 1)
+        if (v.slot_w == 1)
             hipExtLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
         else
             hipExtLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
@@ -3315,41 +3309,27 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     const uint32_t plan_blocks = cdiv((uint64_t)v.N * v.NB, 256);
     if (plan_path) {
         if (member) {
-            hipExtLaunchKernelGGL((v.knobs & 536870912) ? k_plan_list<true, 8, 32> : k_plan_list<true>, dim3(plan_blocks), dim3(256), 0, s,
+            hipExtLaunchKernelGGL(k_plan_list<true>, dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
-            launch_store((hipEvent_t)ev_apply1);
         } else {
             // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
             // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
             // 0.391 vs 0.304 ms apply phase at C4; the compiler drains vmcnt at its loop head)
-            // (the chosen-log buckets on threads of their own after the pairs: 63.5 vs 61.5 us at C4)
             hipExtLaunchKernelGGL(k_plan, dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
-            if (lplan && (v.knobs & 536870912)) hipLaunchKernelGGL((k_plan_list<false, 8, 32>), dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
-            else if (lplan) hipLaunchKernelGGL(k_plan_list<false>, dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
-            // every pair the trace marks lean (pair_gp 0) is one k_plan can describe (ingest.cpp /
-            // mpx_load_clean_device use its predicate, plan_shape_ok), so k_plan leaves nothing to
-            // k_apply_fast (fast_rest 0, checked when the run is collected); knob 4194304 launches
-            // it anyway (it exits at once), A/B
-            if (v.knobs & 4194304) {
-                launch_store(nullptr);
-                hipExtLaunchKernelGGL((k_apply_fast<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s,
-                                      (hipEvent_t)nullptr, (hipEvent_t)ev_apply1, 0, v);
-            } else {
-                launch_store((hipEvent_t)ev_apply1);
-            }
+            if (lplan) hipLaunchKernelGGL(k_plan_list<false>, dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
         }
+        // every pair the trace marks lean (pair_gp 0) is one k_plan can describe (ingest.cpp /
+        // mpx_load_clean_device use its predicate, plan_shape_ok), so nothing is left for the
+        // lean per-slot kernel after the store (fast_rest 0, checked when the run is collected)
+        launch_store((hipEvent_t)ev_apply1);
     } else if (member) {
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
     } else {
         // digest runs (verification) take their own instantiation, so the timed kernel
         // carries no digest code; the lean kernel also writes the chosen log of clean buckets
         if (v.digest) hipLaunchKernelGGL((k_apply_fast<1, true>), dim3(g.apply_wgs), dim3(256), 0, s, v);
-        else switch (g.variant) {
-        case 1: hipLaunchKernelGGL((k_apply_fast<4, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-        case 2: hipLaunchKernelGGL((k_apply_fast<5, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-        default: hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v); break;
-        }
+        else hipLaunchKernelGGL((k_apply_fast<1, false>), dim3(g.apply_wgs), dim3(256), 0, s, v);
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
     }
     if (lplan) {
@@ -3359,67 +3339,43 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (member) hipLaunchKernelGGL((k_apply<4, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
         else hipLaunchKernelGGL((k_apply<4, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
         if (v.num_gp > v.num_gp_snap) {
-            if (member) {
-                if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
-                else hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
-            } else {
-                if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
-                else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
-            }
+            if (member) hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
+            else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
         }
-    } else if (member) {
-        // member: every pair walks the general kernel (insert semantics, epoch events)
-        // the same three-way split as multi (ingest.cpp orders the list): event-free
-        // pairs, pairs without promise-reply runs (PREPARE / E_EPOCH events), the rest;
-        // knob 65536: one kernel over the whole list, 262144: no AM_SNAP kernel (A/B)
-        const uint64_t ns = (v.knobs & 65536) ? 0 : v.num_gp_simple;
-        const uint64_t nq = (v.knobs & (65536 | 262144)) ? ns : v.num_gp_snap;
-        if (ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
-                  else hipLaunchKernelGGL((k_apply<1, false, true, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
-        if (nq > ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq);
-                  else hipLaunchKernelGGL((k_apply<4, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq); }
-        if (v.num_gp > nq) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
-                   // 4 waves / SIMD: C5 2^25 general apply 2.165 vs 2.544 ms unconstrained (variant 1)
-                   else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
-                   else hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
     } else {
-        // the event- and merge-free pairs first (k_apply<..., SIMPLE>), then the rest;
-        // knob 65536: one kernel over the whole list (A/B)
-        // knob 262144: no AM_SNAP kernel (those pairs go to the full one)
-        const uint64_t ns = (v.knobs & 65536) ? 0 : v.num_gp_simple;
-        const uint64_t nq = (v.knobs & (65536 | 262144)) ? ns : v.num_gp_snap;
-        if (ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
-                  // (capped at 6 / 8 waves per SIMD: 1.415 / 1.458 vs 1.393 ms general apply, C3 2^24)
-                  else hipLaunchKernelGGL((k_apply<1, false, false, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
-        if (nq > ns) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq);
-                  // 4 waves / SIMD (128 VGPRs, 4 spilled): 1.324 ms general apply vs 1.469 unconstrained (133 VGPRs,
-                  // 3 waves), 1.496 at 5 waves (96 VGPRs, 38 spilled) and 1.351 without the AM_SNAP split
-                  // (knob 262144), C3 2^24
-                  else hipLaunchKernelGGL((k_apply<4, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq); }
-        if (v.num_gp > nq) { if (v.digest) hipLaunchKernelGGL((k_apply<1, true, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
-                   // 4 waves / SIMD (128 VGPRs, a few spilled) beats the unconstrained 154 VGPRs at 3:
-                   // C3 2^24 general apply 1.394 vs 1.580 ms; 5 and 6 waves spill more (1.87, 2.36 ms);
-                   // variant 1: the unconstrained build (A/B)
-                   else if (g.variant == 1) hipLaunchKernelGGL((k_apply<1, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
-                   else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
+        // every pair of the host-built work list on the general kernel, in three ranges
+        // (ingest.cpp orders the list): event-free pairs (AM_SIMPLE), pairs without
+        // promise-reply runs (PREPARE / member E_EPOCH events, AM_SNAP), the rest (promise rounds).
+        // Occupancy (C3 2^24 general apply): AM_SNAP at 4 waves / SIMD 1.324 ms vs 1.469
+        // unconstrained (3 waves) and 1.496 at 5 (spills); the full kernel at 4 waves 1.394 vs
+        // 1.580 ms unconstrained; one kernel over the whole list 1.351 ms (C5: 2.165 vs 2.544 ms)
+        const uint64_t ns = v.num_gp_simple, nq = v.num_gp_snap;
+        if (v.digest) {
+            if (ns) { if (member) hipLaunchKernelGGL((k_apply<1, true, true, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
+                      else hipLaunchKernelGGL((k_apply<1, true, false, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
+            if (nq > ns) { if (member) hipLaunchKernelGGL((k_apply<1, true, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq);
+                           else hipLaunchKernelGGL((k_apply<1, true, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq); }
+            if (v.num_gp > nq) { if (member) hipLaunchKernelGGL((k_apply<1, true, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
+                                 else hipLaunchKernelGGL((k_apply<1, true, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
+        } else {
+            if (ns) { if (member) hipLaunchKernelGGL((k_apply<1, false, true, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
+                      else hipLaunchKernelGGL((k_apply<1, false, false, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
+            if (nq > ns) { if (member) hipLaunchKernelGGL((k_apply<4, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq);
+                           else hipLaunchKernelGGL((k_apply<4, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq); }
+            if (v.num_gp > nq) { if (member) hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
+                                 else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
+        }
     }
     // the chosen log of the buckets no plan word covered (none when the trace's chosen-log runs
-    // passed plan_chosen's static test at load: k_chosen is not launched; knob 268435456 launches
-    // it anyway, A/B), then the summary (k_reduce); knob
-    // 16777216: the summary in k_chosen's last workgroup instead — measured slower (C4 tail
-    // 0.075 vs 0.015 ms, C3 0.161 vs 0.071 ms: every workgroup's device-scope fence writes
-    // back its XCD's L2 before the ticket), kept for A/B
-    const bool skip_chosen = plan_path && v.chosen_static && !(v.knobs & (16777216 | 268435456));
+    // passed plan_chosen's static test at load: k_chosen is not launched), then the summary
+    const bool skip_chosen = plan_path && v.chosen_static;
     if (skip_chosen) {
         hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)ev_end, 0, v, n_partials);
-    } else if (!(v.knobs & 16777216)) {
-        hipExtLaunchKernelGGL(k_chosen<false>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
-                              (hipEvent_t)nullptr, 0, v, g.apply_wgs, n_partials);
-        hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
     } else {
-        hipExtLaunchKernelGGL(k_chosen<true>, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
-                              (hipEvent_t)ev_end, 0, v, g.apply_wgs, n_partials);
+        hipExtLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
+                              (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+        hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
     }
     return (int)hipGetLastError();
 }

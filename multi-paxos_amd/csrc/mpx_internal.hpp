@@ -172,7 +172,7 @@ struct DevViolation {
 // Everything a kernel needs, passed by value (kernarg).
 struct DevView {
     uint32_t N, quorum, NB, semantics;
-    uint32_t knobs;                 // experiment switches (MPX_KNOBS, tools/ab_apply.py), 0 = default
+    uint32_t walk_all;              // a step walks every pair like a digested run (MPX_STEP_WALK=1)
     uint32_t digest;                // 1: accumulate the order-independent state / chosen digests
                                     //    (mpx_run; verification only, mpx_step leaves them 0)
     uint64_t shard_begin, shard_len;
@@ -284,7 +284,7 @@ struct DevView {
     unsigned long long *partials;   // 8 words per apply workgroup, then chosen workgroups
     DevViolation *viol;
     unsigned long long *summary;    // 64 words
-    // incremental windows (MPX_FLAG_INCREMENTAL, multi): the trace arrays above
+    // incremental windows (MPX_FLAG_INCREMENTAL): the trace arrays above
     // hold one window, the state below carries across windows — as values, not as
     // references to runs of earlier windows (which are gone)
     uint32_t window;                // 1: a window run (k_apply_win, k_chosen_win, carried scan / rounds / votes)
@@ -294,12 +294,19 @@ struct DevView {
                                     //   handle | W_PRESENT), valid while p_round of its pair is the node's round
     uint64_t *p_round;              // per pair (sv_idx): ballot of the round p_* belong to (0: none)
     uint64_t *c_val;                // per instance: the chosen log (handle | W_PRESENT)
-    uint64_t *scal_base;            // 2 per node: promised / max_seen before the window
+    uint64_t *scal_base;            // 2 per node: promised / max_seen scan keys before the window (member: with
+                                    //   the acceptor incarnation << SEG_SHIFT)
+    uint64_t *scal_key;             // ... after it (the scan's unmasked keys; node_scal holds the readback)
     const uint64_t *prop_in;        // 3 per node: the round before the window (ballot, promise mask, preparing)
     uint64_t *prop_out;             // ... after it (k_prop_node)
     const uint32_t *b_gid;          // per batch of the window's list: its global id
     uint64_t *g_mask;               // per global batch: accepted_ (acceptor mask)
-    uint8_t *g_done;                // per global batch: its votes reached quorum in an earlier window
+    uint8_t *g_done;                // per global batch: bit 0 its votes reached quorum in an earlier window;
+                                    //   bit 1 (member) its proposer's batches were cleared (k_gate_votes)
+    const uint32_t *b_node;         // per batch of the window's list: its node
+    const uint32_t *ee_init;        // member, per node: its roles before the window (EE_* state; genesis
+                                    //   from epochs[0] for the first)
+    uint32_t *ee_out;               // ... after it (k_gate_epochs)
     const uint8_t *gp_base;         // per work item: earlier windows left state in the pair
     const uint32_t *cb_list;        // buckets with chosen-log runs in the window
     uint32_t num_cb;
@@ -387,7 +394,7 @@ MPX_HD inline uint64_t scalar_digest(uint32_t node, uint64_t promised, uint64_t 
 }
 
 // kernels (kernels.hip); every launcher queues on `stream`, returns hipError_t as int
-struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, variant, store_wgs; };
+struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, store_wgs; };
 // ev (hipEvent_t, each may be null): begin, apply phase start (after the header
 // scan / quorum kernels), after the plan / store / fast-apply kernels, after the
 // general k_apply, end

@@ -104,6 +104,7 @@ def lib():
             "mpx_destroy": [vp],
             "mpx_submit": [vp, ctypes.c_uint32, ctypes.c_char_p, u64p, ctypes.c_uint64],
             "mpx_submit_trace": [vp, ctypes.c_char_p, ctypes.c_uint64],
+            "mpx_submit_trace_range": [vp, ctypes.c_char_p, ctypes.c_uint64, u64p, u64p],
             "mpx_submit_soa": [vp, ctypes.c_uint32, P(SoaRecords)],
             "mpx_run": [vp], "mpx_reset_state": [vp], "mpx_step": [vp], "mpx_sync": [vp],
             "mpx_timings": [vp, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_uint32)],
@@ -210,6 +211,28 @@ def trace_epochs(trace):
     return out
 
 
+def _addr(buf):
+    """Address of a bytes object's or ctypes array's data (valid while `buf` lives)."""
+    if isinstance(buf, bytes):
+        return ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p).value
+    return ctypes.addressof(buf)
+
+
+def trace_index(trace):
+    """Per node of an MPXT container: (record count, byte offset of its offsets array, byte
+    offset of its record bytes) — what Engine.submit_range needs."""
+    import struct
+    hd = trace_header(trace)
+    ne = struct.unpack_from("<I", trace, 24)[0]
+    pos = 40 + (24 if hd["version"] == 1 else 32) * ne
+    out = []
+    for _ in range(hd["num_nodes"]):
+        cnt, nb = struct.unpack_from("<QQ", trace, pos)
+        out.append((cnt, pos + 16, pos + 16 + 8 * (cnt + 1)))
+        pos = (pos + 16 + 8 * (cnt + 1) + nb + 7) & ~7
+    return out
+
+
 class Engine:
     """One engine = one GPU, one instance shard [shard_begin, shard_end)."""
 
@@ -280,6 +303,27 @@ class Engine:
 
     def submit_trace(self, trace):
         _ck("mpx_submit_trace", lib().mpx_submit_trace(self.h, trace, len(trace)))
+
+    def submit_window(self, trace, begin, end):
+        """mpx_submit_trace_range: records [begin[n], end[n]) of every node's stream."""
+        n = len(begin)
+        b = (ctypes.c_uint64 * n)(*begin)
+        e = (ctypes.c_uint64 * n)(*end)
+        _ck("mpx_submit_trace_range", lib().mpx_submit_trace_range(self.h, trace, len(trace), b, e))
+
+    def submit_range(self, trace, node, k0, k1, index=None):
+        """mpx_submit of records [k0, k1) of `node`'s stream in an MPXT container, in place (no
+        copy: the bytes and offsets are the container's own; a window of a live stream)."""
+        if k1 <= k0:
+            return
+        idx = index if index is not None else trace_index(trace)
+        base = _addr(trace)
+        cnt, offs_at, body_at = idx[node]
+        if k1 > cnt:
+            raise ValueError("records [%d, %d) of a %d-record stream" % (k0, k1, cnt))
+        f = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_uint64)(("mpx_submit", lib()))
+        _ck("mpx_submit", f(self.h, node, base + body_at, base + offs_at + 8 * k0, k1 - k0))
 
     def load_clean_device(self, **kw):
         p = GenParams(GEN_CLEAN, kw.get("num_nodes", self.num_nodes), kw["num_instances"], kw.get("seed", 0),

@@ -350,15 +350,15 @@ def test_member_plan_path(seed, u, m, b, drop, dup):
         assert e.dump() == want
         if b >= 200:
             assert step["general_pairs"] * 4 < walked, (step["general_pairs"], walked)
-        # the walk of every pair in the step (knob 64) agrees too
-        os.environ["MPX_KNOBS"] = "64"
+        # the walk of every pair in the step (MPX_STEP_WALK=1) agrees too
+        os.environ["MPX_STEP_WALK"] = "1"
         try:
             e.step()
             e.sync()
             assert e.stats()["general_pairs"] == walked
             assert e.dump() == want
         finally:
-            del os.environ["MPX_KNOBS"]
+            del os.environ["MPX_STEP_WALK"]
 
 
 def test_engine_member_violations():
@@ -443,24 +443,17 @@ def test_store_chunks_tails_and_partial_pairs(extra):
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
 
 
-@pytest.mark.parametrize("env", [("MPX_SCAN_NODE_PASS", "1"), ("MPX_KNOBS", "2048"), ("MPX_PROP_CHUNK", "64"),
-                                 ("MPX_PROP_CHUNK", "5"), ("MPX_KNOBS", "65536"), ("MPX_KNOBS", "262144"),
-                                 ("MPX_KNOBS", "131072"), ("MPX_APPLY_VARIANT", "1"), ("MPX_KNOBS", "8388608"),
-                                 ("MPX_KNOBS", "4194304"), ("MPX_KNOBS", "16777216"), ("MPX_KNOBS", "33554432"),
-                                 ("MPX_KNOBS", "134217728"), ("MPX_KNOBS", "268435456"), ("MPX_KNOBS", "536870912")])
+@pytest.mark.parametrize("env", [("MPX_SCAN_NODE_PASS", "1"), ("MPX_PROP_CHUNK", "64"), ("MPX_PROP_CHUNK", "5"),
+                                 ("MPX_STEP_WALK", "1")])
 @pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "c5_member_3",
                                   "demo_s0", "demo5_s3", "hm_promise_merge"])
 def test_kept_alternative_paths(name, env, monkeypatch):
-    """The kept alternatives stay correct: the separate per-node scan pass (taken
-    automatically beyond SCAN_INLINE_CHUNKS chunks per node), 64-bucket k_store8
-    chunks, promise-quorum chunks small enough that rounds span chunks
-    (k_prop_chunk's deferred prefixes, k_prop_node's carry), the general k_apply
-    work list without its SIMPLE / SNAP split, PREPARE ranges loaded instead of
-    the inline interval, the unconstrained (3-wave) k_apply builds, multi work lists
-    without k_plan_list, k_apply_fast launched after the store, the summary folded into
-    k_chosen's last workgroup, k_reset as its own launch, the header kernels as three
-    launches, k_chosen launched where the load found every chosen-log bucket plannable, and
-    the 8-segment / 32-run k_plan_list."""
+    """The supported alternatives stay correct: the separate per-node scan pass (taken
+    automatically beyond SCAN_INLINE_CHUNKS chunks per node), promise-quorum chunks small
+    enough that rounds span chunks (k_prop_chunk's deferred prefixes, k_prop_node's carry),
+    and a step that walks every pair as the digested run does (MPX_STEP_WALK; the path of
+    multi traces with more than FAST_MAX_NODES nodes).  The measured-and-rejected variants
+    of earlier rounds are no longer compiled (their A/B records stay in profiles/)."""
     if name not in INDEX:
         pytest.skip("no golden " + name)
     monkeypatch.setenv(*env)
@@ -824,11 +817,11 @@ def _windows(trace, fracs, times=None):
     """The trace's node streams cut at `fracs` of each node's records: one mpx_submit per
     node and window, one incremental mpx_run per window."""
     import time
-    hd, _epochs, streams = _node_streams(trace)
+    hd, epochs, streams = _node_streams(trace)
     n, m = hd["num_nodes"], max(hd["num_instances"], 1)
     sends = [[] for _ in range(n)]
     tot = {k: 0 for k in COUNTERS}
-    with mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL) as e:
+    with mpx.Engine(n, 0, m, semantics=hd["semantics"], epochs=epochs, flags=mpx.FLAG_INCREMENTAL) as e:
         prev = [0] * n
         for f in list(fracs) + [1.0]:
             cut = [len(s) if f >= 1.0 else int(len(s) * f) for s in streams]
@@ -882,15 +875,15 @@ def test_incremental_windows_carry_decisions(name):
             e.decisions()
 
 
-@pytest.mark.parametrize("name", MULTI_GOLDENS)
+@pytest.mark.parametrize("name", sorted(INDEX))
 def test_incremental_windows_match_whole(name):
-    """Every multi golden cut into 1, 2 and 4 windows: the replies of the windows, node by
-    node, are the whole run's (the reference's: test_engine_goldens), and so are the
-    counters summed over the windows and the final state, scalars, executed streams, chosen
-    log and digests."""
+    """Every golden, multi and member, cut into 1, 2 and 4 windows: the replies of the
+    windows, node by node, are the whole run's (the reference's: test_engine_goldens), and so
+    are the counters summed over the windows and the final state, scalars, executed streams,
+    chosen log and digests.  Member windows carry each node's roles (epoch, Acceptor
+    incarnation, Proposer), its scan keys with the incarnation and the batches a marker
+    cleared (member/paxos.cpp:841-844 OnReceive per message, :1864-1964)."""
     trace = _read(name, ".mpxt")
-    if mpx.trace_header(trace)["semantics"] != mpx.SEM_MULTI:
-        pytest.skip("member trace")
     want = _whole(trace)
     for fracs in ((), (0.5,), (0.2, 0.45, 0.8)):
         got = _windows(trace, fracs)
@@ -910,6 +903,43 @@ def test_incremental_windows_c3(seed):
     assert got[0] == want[0]
     assert got[1] == want[1]
     assert got[2] == want[2]
+
+
+@pytest.mark.parametrize("seed,u,m,b,drop,dup", [(51, 8, 1 << 15, 256, 100, 100), (52, 6, 20000, 90, 500, 500),
+                                                  (53, 5, 9000, 33, 1000, 1000)])
+def test_incremental_windows_member(seed, u, m, b, drop, dup):
+    """C5-shaped member traces (AddAcceptor / DelAcceptor epochs, stale versions, loss and
+    duplicates: markers, Acceptor deletions and Proposer resets in every window) in 7 windows
+    == the whole run."""
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=u, num_instances=m, seed=seed, batch=b,
+                           drop_rate=drop, dup_rate=dup, max_delay=64, noop_permille=15)
+    want = _whole(t)
+    got = _windows(t, [k / 7 for k in range(1, 7)])
+    assert got[0] == want[0]
+    assert got[1] == want[1]
+    assert got[2] == want[2]
+
+
+def test_incremental_window_range_error_keeps_state():
+    """A window the engine cannot encode (MPX_E_RANGE: a member node past 254 E_EPOCH markers,
+    the device incarnation counter) is refused before it touches the carry: the state read back
+    is the earlier windows', and the same records are refused again."""
+    import struct
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=4, num_instances=4096, seed=7, batch=64,
+                           drop_rate=100, dup_rate=100, max_delay=32)
+    hd, epochs, streams = _node_streams(t)
+    n, m = hd["num_nodes"], hd["num_instances"]
+    with mpx.Engine(n, 0, m, semantics=hd["semantics"], epochs=epochs, flags=mpx.FLAG_INCREMENTAL) as e:
+        for node, s in enumerate(streams):
+            e.submit(node, s[:len(s) // 2])
+        e.run()
+        before = _observe(e, n, m)
+        e.submit(0, [struct.pack("<II", 18, 0)] * 300)      # E_EPOCH{epoch 0} x 300
+        for _ in range(2):
+            with pytest.raises(mpx.MpxError) as ex:
+                e.run()
+            assert ex.value.rc == -5                         # MPX_E_RANGE
+        assert _observe(e, n, m) == before
 
 
 def test_incremental_window_cost_is_per_window():
