@@ -251,7 +251,7 @@ def c3_windows_leg(args, trace, want_digests, want_counters):
     assert ok, "C3 windows: the windows' state differs from the batch run's (%r vs %r, %r vs %r)" % (
         digests, want_digests, tot, want_counters)
     run_ms = [p["run"] for p in dev]
-    apply_ms = [p["general_apply"] for p in dev]
+    apply_ms = [p["fast_apply"] + p["general_apply"] for p in dev]   # k_apply_win's start / stop events
     mean = lambda xs: sum(xs) / max(len(xs), 1)
     pmc = latest_pmc(7, m, 1, workload="C3W")
     hw = hw_roofline(pmc, mean(apply_ms))

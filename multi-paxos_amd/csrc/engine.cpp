@@ -58,7 +58,8 @@ template <typename T> int upload(DevBuf &b, const std::vector<T> &v, hipStream_t
     return MPX_OK;
 }
 
-struct StepEvents { hipEvent_t e[5]; };   // launch_run's event points
+struct StepEvents { hipEvent_t e[5]; bool store_last; };   // launch_run's event points (store_last: e[3], e[4]
+                                                          // not recorded, run_ends_with_store)
 
 }  // namespace
 
@@ -127,9 +128,12 @@ struct mpx_engine {
     std::vector<PropNode> *prop = nullptr;           // MPX_FLAG_DECISIONS: the bookkeeping carried across windows
     uint64_t windows = 0;
     uint64_t events_every = 1, step_no = 0;   // mpx_timing_every
+    uint32_t seq = 0;                         // launches so far (DevView::seq, the violation record's buffer)
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? MPX_OK : MPX_E_HIP; }
+// event k of a run (a run that ends with the store recorded no e[3], e[4]: they are e[2])
+static hipEvent_t evk(const StepEvents &x, int k) { return x.store_last && k > 2 ? x.e[2] : x.e[k]; }
 template <typename T> static int d2h(std::vector<T> &v, const DevBuf &b, size_t n, size_t off = 0)
 {
     v.resize(n);
@@ -384,14 +388,14 @@ static int finish_view(mpx_engine *e)
     v.N = N;
     v.quorum = N / 2 + 1;                          // nodes_.size() / 2 + 1, paxos.cpp:1047,1416
     v.NB = e->NB;
-    v.semantics = e->cfg.semantics;
-    v.shard_begin = e->cfg.shard_begin;
-    v.shard_len = e->shard_len;
-    v.num_msgs = e->num_msgs;
     v.scan_node_pass = 0;
     for (size_t n = 0; n + 1 < e->ht.node_chunk_off.size(); ++n)
         if (e->ht.node_chunk_off[n + 1] - e->ht.node_chunk_off[n] > SCAN_INLINE_CHUNKS) v.scan_node_pass = 1;
     if (const char *x = std::getenv("MPX_SCAN_NODE_PASS")) v.scan_node_pass = std::atoi(x) ? 1 : 0;
+    v.semantics = e->cfg.semantics;
+    v.shard_begin = e->cfg.shard_begin;
+    v.shard_len = e->shard_len;
+    v.num_msgs = e->num_msgs;
     // slot width: 1 byte when every pair / bucket has few enough fragments for a
     // 1-byte pair-local index (set by the trace loader), MPX_SLOT_BYTES=2 forces 2
     if (const char *x = std::getenv("MPX_SLOT_BYTES")) if (std::atoi(x) == 2) v.slot_w = 2;
@@ -450,7 +454,8 @@ static int finish_view(mpx_engine *e)
     }
 
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + std::max<uint64_t>(e->geom.chosen_wgs, e->num_cus * 16))));
-    TRY(e->viol.alloc(sizeof(DevViolation)));
+    TRY(e->viol.alloc(2 * sizeof(DevViolation)));                     // double-buffered (reset_state)
+    HTRY(hipMemsetAsync(e->viol.p, 0, 2 * sizeof(DevViolation), e->stream));
     TRY(e->summary.alloc(64 * 8));
     e->out_subs = 64;
     if (const char *x = std::getenv("MPX_OUT_SUBS")) {  // A/B: snapshot sub-buffers (power of two)
@@ -473,6 +478,7 @@ static int finish_view(mpx_engine *e)
     v.out_subs = e->out_subs;
     v.partials = e->partials.as<unsigned long long>();
     v.viol = e->viol.as<DevViolation>();
+    v.viol_next = e->viol.as<DevViolation>() + 1;
     v.summary = e->summary.as<unsigned long long>();
     v.node_scal = e->node_scal.as<uint64_t>();
     return MPX_OK;
@@ -674,7 +680,7 @@ static int upload_trace(mpx_engine *e)
 static StepEvents *next_events(mpx_engine *e)
 {
     if (e->ev_used == e->ev_pool.size()) {
-        StepEvents se;
+        StepEvents se{};
         for (auto &x : se.e)
             if (hipEventCreate(&x) != hipSuccess) return nullptr;
         e->ev_pool.push_back(se);
@@ -711,8 +717,15 @@ static int queue_run(mpx_engine *e, bool digest)
         g.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(np, (uint64_t)e->num_cus * std::atoi(x)));
         if (g.apply_wgs > e->num_cus * 16) g.apply_wgs = e->num_cus * 16;   // partials are sized for 16 per CU
     }
+    // the launch's sequence number tags the header scan's look-back flags; the violation
+    // record alternates between two buffers (this launch's, and the next one it clears)
+    if (++e->seq >= (1u << 30)) e->seq = 1;
+    e->view.seq = e->seq;
+    e->view.viol = e->viol.as<DevViolation>() + (e->seq & 1);
+    e->view.viol_next = e->viol.as<DevViolation>() + ((e->seq + 1) & 1);
     void *evp[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     if (ev) for (int k = 0; k < 5; ++k) evp[k] = ev->e[k];
+    if (ev) ev->store_last = run_ends_with_store(e->view);
     int rc = launch_run(e->view, e->stream, g, evp);
     if (rc) return MPX_E_HIP;
     if (e->incremental) {                              // the next window starts from this one's scalars, rounds, roles
@@ -782,8 +795,8 @@ static int collect(mpx_engine *e)
     if (e->ev_used) {
         StepEvents &x = e->ev_pool[e->ev_used - 1];
         float a = 0, r = 0;
-        (void)hipEventElapsedTime(&a, x.e[1], x.e[3]);
-        (void)hipEventElapsedTime(&r, x.e[0], x.e[4]);
+        (void)hipEventElapsedTime(&a, evk(x, 1), evk(x, 3));
+        (void)hipEventElapsedTime(&r, evk(x, 0), evk(x, 4));
         st.apply_ns = (uint64_t)(a * 1e6);
         st.device_ns = (uint64_t)(r * 1e6);
     }
@@ -864,8 +877,8 @@ extern "C" int mpx_timings(mpx_engine *e, uint32_t max, double *apply_ms, double
     uint32_t k = 0;
     for (size_t i = 0; i < e->ev_used && k < max; ++i, ++k) {
         float a = 0, r = 0;
-        (void)hipEventElapsedTime(&a, e->ev_pool[i].e[1], e->ev_pool[i].e[3]);
-        (void)hipEventElapsedTime(&r, e->ev_pool[i].e[0], e->ev_pool[i].e[4]);
+        (void)hipEventElapsedTime(&a, evk(e->ev_pool[i], 1), evk(e->ev_pool[i], 3));
+        (void)hipEventElapsedTime(&r, evk(e->ev_pool[i], 0), evk(e->ev_pool[i], 4));
         if (apply_ms) apply_ms[k] = a;
         if (run_ms) run_ms[k] = r;
     }
@@ -880,10 +893,11 @@ extern "C" int mpx_timings_detail(mpx_engine *e, uint32_t max, double *phases, u
     HTRY(hipStreamSynchronize(e->stream));
     uint32_t k = 0;
     for (size_t i = 0; i < e->ev_used && k < max; ++i, ++k) {
-        const hipEvent_t *x = e->ev_pool[i].e;
+        const StepEvents &x = e->ev_pool[i];
         float t[5] = {0, 0, 0, 0, 0};
-        (void)hipEventElapsedTime(&t[0], x[0], x[4]);
-        for (int j = 0; j < 4; ++j) (void)hipEventElapsedTime(&t[j + 1], x[j], x[j + 1]);
+        (void)hipEventElapsedTime(&t[0], evk(x, 0), evk(x, 4));
+        for (int j = 0; j < 4; ++j)
+            if (evk(x, j) != evk(x, j + 1)) (void)hipEventElapsedTime(&t[j + 1], evk(x, j), evk(x, j + 1));
         for (int j = 0; j < 5; ++j) phases[5 * k + j] = t[j];
     }
     *n = k;
@@ -1062,7 +1076,7 @@ extern "C" int mpx_last_violation(mpx_engine *e, mpx_violation *out)
     }
     if (e->viol.p && have_results(e)) {
         DevViolation d;
-        HTRY(hipMemcpy(&d, e->viol.p, sizeof d, hipMemcpyDeviceToHost));
+        HTRY(hipMemcpy(&d, e->view.viol, sizeof d, hipMemcpyDeviceToHost));
         out->code = d.code; out->node = (uint32_t)d.node; out->seq = d.seq; out->iid = d.iid;
         // kernels report a message's position among the kept records of its node
         const HostTrace &h = e->ht;

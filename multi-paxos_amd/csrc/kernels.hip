@@ -1,7 +1,7 @@
 // kernels.hip — CDNA4 (gfx950) kernels of the batched Multi-Paxos engine.
 //
 // One run = the whole resident trace applied from genesis state:
-//   k_scan_chunk / k_scan_node / k_scan_apply
+//   k_scan_chunk / k_headers
 //       per-message header scan: promised = running max of PREPARE ids,
 //       max_seen = running max of PREPARE/ACCEPT ids and REJECT max_ids
 //       (multi/paxos.cpp:862-865,1363-1366,1229-1230) -> granted / reject flags
@@ -369,7 +369,10 @@ __device__ inline int summary_word(uint32_t pc)
 }
 
 // Per-step reset of what the step accumulates (k_reset, or the head of k_scan_chunk when
-// it is the step's first kernel): thread t of T zeroes its share, grid-stride
+// it is the step's first kernel): thread t of T zeroes its share, grid-stride.  The scalars
+// of a node with scan records are left to its last scan chunk; the violation record is
+// double-buffered (a launch records into v.viol and clears v.viol_next, the one the next
+// launch records into), so no kernel of a launch both clears and records.
 __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64_t t, uint64_t T)
 {
     const uint64_t np = (uint64_t)v.N * v.NB;
@@ -383,6 +386,8 @@ __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64
     // nodes without messages keep promised = max_seen = 0 (a window: what the windows before left;
     // member keys carry the Acceptor's incarnation above LOW56, the readback does not)
     for (uint64_t i = t; i < 2ull * v.N; i += T) {
+        const uint32_t n = (uint32_t)(i >> 1);
+        if (v.node_chunk_off[n + 1] != v.node_chunk_off[n]) continue;   // the scan writes them
         const uint64_t k = v.window ? v.scal_base[i] : 0;
         v.node_scal[i] = v.semantics == MPX_SEM_MEMBER ? k & LOW56 : k;
         if (v.window) v.scal_key[i] = k;
@@ -395,7 +400,7 @@ __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64
         if (v.window) *v.outv_n = 0;
         for (uint32_t pc = 0; pc < 8; ++pc)          // the counter words k_reduce's workgroups add into
             if (summary_word(pc) >= 0) v.summary[summary_word(pc)] = 0;
-        v.viol->code = v.viol->node = v.viol->seq = v.viol->iid = v.viol->count = 0;
+        v.viol_next->code = v.viol_next->node = v.viol_next->seq = v.viol_next->iid = v.viol_next->count = 0;
     }
 }
 
@@ -1028,12 +1033,13 @@ __device__ inline uint64_t slot_digest(const DevView &v, uint32_t n, uint64_t ii
 // Wave id with consecutive ids on one XCD: workgroups are dealt round-robin
 // over the 8 XCDs (blockIdx % 8), so id = xcd * (waves per XCD) + local id.
 // Neighbouring buckets then share their XCD's L2 (headers, descriptors).
-__device__ inline uint64_t xcd_wave_id(uint32_t wv)
+__device__ inline uint64_t xcd_wave_id_g(uint32_t wv, uint32_t grid)
 {
-    if (gridDim.x & 7) return (uint64_t)blockIdx.x * 4 + wv;
-    const uint64_t per = (uint64_t)(gridDim.x >> 3) * 4;
+    if (grid & 7) return (uint64_t)blockIdx.x * 4 + wv;
+    const uint64_t per = (uint64_t)(grid >> 3) * 4;
     return (uint64_t)(blockIdx.x & 7) * per + (uint64_t)(blockIdx.x >> 3) * 4 + wv;
 }
+__device__ inline uint64_t xcd_wave_id(uint32_t wv) { return xcd_wave_id_g(wv, gridDim.x); }
 
 // Lean acceptor/learner apply plus the chosen log, G consecutive buckets per
 // wave step (fast_group: G * N + 1 <= 64, at most 4).
@@ -1968,17 +1974,32 @@ __global__ __launch_bounds__(256) void k_store(DevView v)
 // of a store is one segment (batch 256) its low half is the 16 bytes; else
 // plan_bytes16 expands the segments.  Tail buckets of a row go through the
 // per-bucket loop.
-template <bool NT, uint32_t C = 64>
-__global__ __launch_bounds__(256) void k_store8(DevView v)
+template <uint32_t W>
+__device__ inline void reduce_summary(const DevView &v, uint32_t n_partials, unsigned long long (&red)[W][8],
+                                      uint32_t row0, uint32_t stride, bool scal);
+
+// REDUCE: workgroups [store_grid, gridDim.x) fold the partials into the summary (k_reduce's
+// work) while the others store — launched when the store is the step's last kernel (the
+// partials are all written by the kernels before it), so the summary's dependent launch and
+// its ramp leave the step's chain (C4 shard at world 8: 64.1 vs 68.9 us, same-box A/B,
+// profiles/r03_v20_fused_reduce_ab.json)
+template <bool NT, uint32_t C = 64, bool REDUCE = false>
+__global__ __launch_bounds__(256) void k_store8(DevView v, uint32_t store_grid, uint32_t n_partials)
 {
     static_assert(C == 64 || C == 128, "one or two plan words per lane");
+    if (REDUCE && blockIdx.x >= store_grid) {
+        __shared__ unsigned long long red[4][8];
+        const uint32_t r = blockIdx.x - store_grid, R = gridDim.x - store_grid;
+        reduce_summary<4>(v, n_partials, red, 256 * r, 256 * R, r == 0);
+        return;
+    }
     const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t N = v.N;
 
     const uint64_t whole = v.shard_len >> BSH;
     const uint64_t cpr = whole / C, S = (uint64_t)(N + 1) * cpr;
-    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
-    const uint64_t wid = xcd_wave_id(wv);
+    const uint64_t nwaves = (uint64_t)store_grid * 4;
+    const uint64_t wid = xcd_wave_id_g(wv, store_grid);
     uint8_t *const st = static_cast<uint8_t *>(v.st);
     uint8_t *const sink = reinterpret_cast<uint8_t *>(v.store_dummy) + (wid & 63) * 1024 + 16 * lane;
     const uint32_t p16 = 16 * (lane & 15);                 // the lane's first slot in its bucket
@@ -3234,6 +3255,14 @@ int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, ui
     return (int)hipGetLastError();
 }
 
+bool run_ends_with_store(const DevView &v)
+{
+    const bool member = v.semantics == MPX_SEM_MEMBER;
+    const bool plan_path = !v.digest && !v.walk_all && !v.window && (member || v.N <= FAST_MAX_NODES);
+    const bool lplan = plan_path && (member || v.num_gp_snap);
+    return plan_path && v.chosen_static && !member && !lplan && v.num_gp == 0 && v.slot_w == 1;
+}
+
 int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
 {
     void *ev_begin = ev[0], *ev_apply0 = ev[1], *ev_apply1 = ev[2], *ev_general = ev[3], *ev_end = ev[4];
@@ -3249,6 +3278,10 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     // kernel begins or ends the phase: a separate event record costs a 5-10 us bubble between
     // dependent kernels (rocprof, C4: 16 us of a 395 us step)
     // multi: the reset rides on the first header-scan kernel (one launch less per step)
+    // (a single-pass scan — the chunk aggregates found by a decoupled look-back inside
+    // k_headers, agent-coherent atomics, no k_scan_chunk launch — was measured slower: C4 shard
+    // scan phase 22.0 vs 17.9 us, the look-back's serialized round trips cost more than the
+    // launch; profiles/r04_v1_bench.json)
     const bool fold_reset = !member && v.num_chunks;
     if (!fold_reset)
         hipExtLaunchKernelGGL(k_reset, dim3(cdiv(reset_n ? reset_n : 1, 256)), dim3(256), 0, s,
@@ -3297,12 +3330,22 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     const bool plan_path = !v.digest && !v.walk_all && (member || v.N <= FAST_MAX_NODES);
     const bool lplan = plan_path && (member || v.num_gp_snap);
     if (ev_apply0 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
+    // the chosen log needs no k_chosen launch when the trace's chosen-log runs passed
+    // plan_chosen's static test at load; then, with no general pair either (the C4 shape), the
+    // store ends the step and the summary rides on its extra workgroups
+    const bool skip_chosen = plan_path && v.chosen_static;
+    const bool fuse_reduce = run_ends_with_store(v);
+    const uint32_t reduce_wgs = cdiv(n_partials ? n_partials : 1, 256);
     // the plan words of every (row, bucket) -> state rows and the chosen log
     // (1-byte slots: 128-bucket chunks, 32 KiB per row and two plan words per lane, 0.295 vs
     // 0.315 ms for 64-bucket chunks at C4)
     auto launch_store = [&](hipEvent_t stop) {
-        if (v.slot_w == 1)
-            hipExtLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
+        if (v.slot_w == 1 && fuse_reduce)
+            hipExtLaunchKernelGGL((k_store8<true, 128, true>), dim3(g.store_wgs + reduce_wgs), dim3(256), 0, s, nullptr,
+                                  stop, 0, v, g.store_wgs, n_partials);
+        else if (v.slot_w == 1)
+            hipExtLaunchKernelGGL((k_store8<true, 128>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v,
+                                  g.store_wgs, 0u);
         else
             hipExtLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
     };
@@ -3368,8 +3411,10 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     }
     // the chosen log of the buckets no plan word covered (none when the trace's chosen-log runs
     // passed plan_chosen's static test at load: k_chosen is not launched), then the summary
-    const bool skip_chosen = plan_path && v.chosen_static;
-    if (skip_chosen) {
+    if (fuse_reduce) {
+        // (the apply phase ends with the store; the general and tail phases are empty: the
+        // host reads the store's stop event for them, run_ends_with_store)
+    } else if (skip_chosen) {
         hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)ev_end, 0, v, n_partials);
     } else {

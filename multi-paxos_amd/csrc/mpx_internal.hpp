@@ -46,7 +46,7 @@ constexpr uint32_t BS = 1u << BSH;
 constexpr uint32_t SCAN_CHUNK = MPX_SCAN_CHUNK;        // header-scan chunk (messages): 8 per thread
 constexpr uint32_t PROP_CHUNK = 512;         // promise-quorum chunk (pl records): 8 windows of 64 (C3 2^24 scan
                                              // phase 0.112 ms vs 0.128 at 2048, 0.134 at 256)
-// k_scan_apply re-reduces a node's earlier chunk aggregates inline (O(chunks^2)
+// k_headers' scan blocks re-reduce a node's earlier chunk aggregates inline (O(chunks^2)
 // per node) up to this many chunks per node; longer streams take k_scan_node
 constexpr uint32_t SCAN_INLINE_CHUNKS = 512;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
@@ -215,6 +215,7 @@ struct DevView {
     uint64_t *chunk_agg;            // 2 per chunk: pmax, smax
     uint64_t *chunk_carry;          // 2 per chunk: exclusive prefix (k_scan_node)
     uint32_t scan_node_pass;        // 1: a node has > SCAN_INLINE_CHUNKS chunks, carry-in from k_scan_node
+    uint32_t seq;                   // this launch's sequence number (from 1)
     uint64_t *node_scal;            // 2 per node: promised, max_seen
     // pools
     const uint64_t *e_val;
@@ -282,7 +283,8 @@ struct DevView {
     uint64_t out_cap;               // records per sub-buffer: sub s owns out[s * out_cap .. (s + 1) * out_cap)
     uint32_t out_subs;              // sub-buffers in use (power of two <= OUT_SUBS)
     unsigned long long *partials;   // 8 words per apply workgroup, then chosen workgroups
-    DevViolation *viol;
+    DevViolation *viol;             // this launch's first-violation record (double-buffered: reset_state
+    DevViolation *viol_next;        //   clears the next launch's, which nothing writes in this one)
     unsigned long long *summary;    // 64 words
     // incremental windows (MPX_FLAG_INCREMENTAL): the trace arrays above
     // hold one window, the state below carries across windows — as values, not as
@@ -399,6 +401,9 @@ struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, store_wgs; };
 // scan / quorum kernels), after the plan / store / fast-apply kernels, after the
 // general k_apply, end
 int launch_run(const DevView &v, void *stream, LaunchGeom g, void *const ev[5]);
+// the run's last kernel is the store, the step summary folded into it (the clean multi
+// plan path, C4): launch_run then records neither the general-apply nor the end event
+bool run_ends_with_store(const DevView &v);
 // readback: count slots of node `node` (node >= N: the chosen log) from shard
 // offset l0 -> out, 2 words each {ballot, PRESENT | COMMITTED? | handle}
 // (chosen: {0, PRESENT | handle}); unwritten buckets read as empty

@@ -443,13 +443,11 @@ def test_store_chunks_tails_and_partial_pairs(extra):
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
 
 
-@pytest.mark.parametrize("env", [("MPX_SCAN_NODE_PASS", "1"), ("MPX_PROP_CHUNK", "64"), ("MPX_PROP_CHUNK", "5"),
-                                 ("MPX_STEP_WALK", "1")])
+@pytest.mark.parametrize("env", [("MPX_PROP_CHUNK", "64"), ("MPX_PROP_CHUNK", "5"), ("MPX_STEP_WALK", "1")])
 @pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "c5_member_3",
                                   "demo_s0", "demo5_s3", "hm_promise_merge"])
 def test_kept_alternative_paths(name, env, monkeypatch):
-    """The supported alternatives stay correct: the separate per-node scan pass (taken
-    automatically beyond SCAN_INLINE_CHUNKS chunks per node), promise-quorum chunks small
+    """The supported alternatives stay correct: promise-quorum chunks small
     enough that rounds span chunks (k_prop_chunk's deferred prefixes, k_prop_node's carry),
     and a step that walks every pair as the digested run does (MPX_STEP_WALK; the path of
     multi traces with more than FAST_MAX_NODES nodes).  The measured-and-rejected variants
@@ -464,9 +462,10 @@ def test_kept_alternative_paths(name, env, monkeypatch):
         _step_path(e, want, st)
 
 
-def test_clean_long_node_stream_scan_node_pass():
-    """A node stream of more than SCAN_INLINE_CHUNKS header-scan chunks takes the
-    k_scan_node pass by itself; the result equals the oracle's either way."""
+def test_clean_long_node_stream_scan_lookback():
+    """A node stream of hundreds of header-scan chunks: the single-pass scan's chunk look-back
+    walks back over more than 64 predecessors (wave-wide sweeps); the result equals the
+    oracle's."""
     n, m = 2, 320000                         # batch 1: node 0 gets 7 records per instance -> 547 chunks of 4096
     t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=1)
     _, ostats, _ = oracle_run(t)
