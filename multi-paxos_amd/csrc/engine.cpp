@@ -440,18 +440,7 @@ static int finish_view(mpx_engine *e)
     TRY(e->gp_dyn_n.alloc(8));
     v.gp_dyn = e->gp_dyn.as<uint64_t>();
     v.gp_dyn_n = e->gp_dyn_n.as<unsigned long long>();
-    const uint64_t npairs = (uint64_t)N * e->NB;
-    // k_apply_fast holds 5 waves/SIMD (82 VGPRs); 8 workgroups of 4 waves per
-    // CU measured best on C4 (tools/ab_apply.py: 2.17 ms vs 2.31 ms at 5)
-    e->geom.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npairs, (uint64_t)e->num_cus * 8));
-    e->geom.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 4));
-    // k_store: 8 workgroups of 4 waves per CU at C4 size; a smaller shard (fewer 128-bucket
-    // chunks than 2.5 per wave) takes fewer, so each wave still has a next chunk in flight
-    // (C4 shard at world 8: 94 vs 101 us per step, profiles/r03_v7_shard_ab.json)
-    {
-        const uint64_t chunks = (uint64_t)(N + 1) * (e->NB / 128 + 1);
-        e->geom.store_wgs = (uint32_t)std::max<uint64_t>(e->num_cus, std::min<uint64_t>((uint64_t)e->num_cus * 8, chunks / 10));
-    }
+    e->geom = launch_geometry(N, e->NB, e->num_cus);
 
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + std::max<uint64_t>(e->geom.chosen_wgs, e->num_cus * 16))));
     TRY(e->viol.alloc(2 * sizeof(DevViolation)));                     // double-buffered (reset_state)
@@ -1651,12 +1640,13 @@ static bool has_proposals(const HostTrace &h)
 
 // Member semantics (member/paxos.cpp:1183-1297): the same batch over the proposer's
 // unlearned ids — Proposer::OnLearn (:1383-1470) removes a newly learned id from the
-// unlearned / unproposed sets and re-proposes an initial proposal that lost its id.  A
-// Proposer starts with every id unlearned and preparing (:1074-1082); the engine model
-// idles it at the E_EPOCH run that created it or changed its acceptors (include/mpx.h)
-// and gives it the node's own Values of the trace not yet learned as initial proposals
-// (what Propose would have recorded; the reference driver's prefill).  Host walk over
-// the device's promise quorums (F_QUORUM) and merged maps (k_apply's records).
+// unlearned / unproposed sets and re-proposes an initial proposal that lost its id; a
+// P_PROPOSE record is Node::Propose -> Proposer::Propose (:1122-1156, value_id_ + 1: the
+// next unproposed id now, or queued while preparing; without a Proposer the value is
+// Unproposable, :786-789).  A Proposer starts with every id unlearned and preparing
+// (:1074-1082); the engine model idles it at the E_EPOCH run that created it or changed
+// its acceptors (include/mpx.h).  Host walk over the device's promise quorums (F_QUORUM)
+// and merged maps (k_apply's records).
 static int put_bytes(const std::string &d, uint8_t **out, uint64_t *size);
 
 static int member_decisions(mpx_engine *e, const Results &r, std::string &d)
@@ -1671,31 +1661,12 @@ static int member_decisions(mpx_engine *e, const Results &r, std::string &d)
         std::map<uint64_t, uint64_t> initial;          // initial_proposals_: instance -> value id
         std::set<uint64_t> newly;                      // newly_proposed_values_
         uint64_t vid = 0;                              // value_id_
-        bool preparing = true, prefilled = false;
+        bool preparing = true;
     };
     for (uint32_t n = 0; n < N; ++n) {
-        // the node's own non-noop Values, first LEARN occurrence of each value id
-        std::map<uint64_t, uint64_t> own;
-        {
-            std::set<uint64_t> seen;
-            for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
-                if (h.m_type[g] != MPX_MSG_COMMIT) continue;
-                for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) {
-                    const uint64_t hv = h.e_val[k], v = MPX_HANDLE_VALUE_ID(hv);
-                    if (MPX_HANDLE_PROPOSER(hv) != n || MPX_HANDLE_NOOP(hv) || !seen.insert(v).second) continue;
-                    own[h.e_iid[k]] = v;
-                }
-            }
-        }
         std::unordered_map<uint64_t, uint64_t> learned;      // the learner's learned_values_ (insert-first)
         std::unique_ptr<Prop> p;
-        auto prefill = [&]() {
-            if (!p || p->prefilled) return;
-            p->prefilled = true;
-            for (auto &x : own)
-                if (!learned.count(x.first)) p->initial.emplace(x.first, x.second);
-        };
-        if ((ep[0].proposer_mask >> n) & 1) { p.reset(new Prop); p->preparing = false; prefill(); }
+        if ((ep[0].proposer_mask >> n) & 1) { p.reset(new Prop); p->preparing = false; }
         std::string body;
         uint64_t count = 0;
         uint32_t ei = 0;
@@ -1703,11 +1674,17 @@ static int member_decisions(mpx_engine *e, const Results &r, std::string &d)
         for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
             const uint8_t t = h.m_type[g];
             if (t != MPX_MSG_E_EPOCH && idle) {
-                if (p) { p->preparing = false; prefill(); }
+                if (p) p->preparing = false;
                 idle = false;
             }
             if (t == MPX_MSG_P_START) {
                 if (p) p->preparing = true;
+            } else if (t == MPX_MSG_P_PROPOSE) {           // Proposer::Propose (:1122-1156)
+                if (p) {
+                    ++p->vid;
+                    if (!p->preparing) p->initial[p->unproposed.next()] = p->vid;
+                    else p->newly.insert(p->vid);
+                }
             } else if (t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM) && p) {
                 IdSet un = p->unlearned;
                 std::vector<std::pair<uint64_t, uint64_t>> b;

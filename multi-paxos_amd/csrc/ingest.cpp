@@ -608,6 +608,9 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         if (len < 8) return MPX_E_DECODE;
         ver = rd32(m + 4);
         break;
+    case MPX_MSG_P_PROPOSE:                       // Node::Propose (:1984, :1122-1156): bookkeeping only
+        if (len < 8 || 8 + (size_t)rd32(m + 4) > len) return MPX_E_DECODE;
+        break;
     default:
         return MPX_E_DECODE;
     }

@@ -3255,6 +3255,23 @@ int launch_decode(const DevView &v, void *stream, uint32_t node, uint64_t l0, ui
     return (int)hipGetLastError();
 }
 
+LaunchGeom launch_geometry(uint32_t N, uint64_t NB, uint32_t num_cus)
+{
+    LaunchGeom g{};
+    const uint64_t npairs = (uint64_t)N * NB;
+    // k_apply_fast holds 5 waves/SIMD (82 VGPRs); 8 workgroups of 4 waves per
+    // CU measured best on C4 (2.17 ms vs 2.31 ms at 5)
+    g.apply_wgs = (uint32_t)(npairs < 1 ? 1 : npairs < (uint64_t)num_cus * 8 ? npairs : (uint64_t)num_cus * 8);
+    g.chosen_wgs = (uint32_t)(NB < 1 ? 1 : NB < (uint64_t)num_cus * 4 ? NB : (uint64_t)num_cus * 4);
+    // k_store: 8 workgroups of 4 waves per CU at C4 size; a smaller shard (fewer 128-bucket
+    // chunks than 2.5 per wave) takes fewer, so each wave still has a next chunk in flight
+    // (C4 shard at world 8: 94 vs 101 us per step, profiles/r03_v7_shard_ab.json)
+    const uint64_t chunks = (uint64_t)(N + 1) * (NB / 128 + 1), want = chunks / 10;
+    const uint64_t hi = (uint64_t)num_cus * 8;
+    g.store_wgs = (uint32_t)(want > hi ? hi : want < num_cus ? num_cus : want);
+    return g;
+}
+
 bool run_ends_with_store(const DevView &v)
 {
     const bool member = v.semantics == MPX_SEM_MEMBER;

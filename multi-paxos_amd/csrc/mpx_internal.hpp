@@ -404,6 +404,8 @@ int launch_run(const DevView &v, void *stream, LaunchGeom g, void *const ev[5]);
 // the run's last kernel is the store, the step summary folded into it (the clean multi
 // plan path, C4): launch_run then records neither the general-apply nor the end event
 bool run_ends_with_store(const DevView &v);
+// the grids of a trace of N nodes x NB buckets on a device with num_cus CUs
+LaunchGeom launch_geometry(uint32_t N, uint64_t NB, uint32_t num_cus);
 // readback: count slots of node `node` (node >= N: the chosen log) from shard
 // offset l0 -> out, 2 words each {ballot, PRESENT | COMMITTED? | handle}
 // (chosen: {0, PRESENT | handle}); unwritten buckets read as empty

@@ -539,18 +539,18 @@ class Engine:
 
 
 def source_digest():
-    """16 hex digits of SHA-256 over the engine's sources (csrc/*, include/mpx.h): what a
-    committed PMC profile was measured with (tools/pmc_traffic.py), so bench.py can refuse
-    a profile of other kernels."""
+    """16 hex digits of SHA-256 over the engine's device sources — the kernels, the device
+    generator, the shared layout header (which also holds the launch code and grids): what a
+    committed PMC profile was measured with (tools/pmc_traffic.py), so bench.py can refuse a
+    profile of other kernels.  Host-only sources (ingest, the C ABI, readbacks) do not enter."""
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(os.path.dirname(HERE), "csrc")
-    for path in sorted(os.listdir(csrc)) + [INCLUDE_H]:
-        full = path if os.path.isabs(path) else os.path.join(csrc, path)
-        if os.path.isfile(full):
-            h.update(os.path.basename(full).encode() + b"\0")
-            with open(full, "rb") as f:
-                h.update(f.read())
+    for name in ("gen_device.hip", "kernels.hip", "mpx_internal.hpp"):
+        full = os.path.join(csrc, name)
+        h.update(name.encode() + b"\0")
+        with open(full, "rb") as f:
+            h.update(f.read())
     return h.hexdigest()[:16]
 
 

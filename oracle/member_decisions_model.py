@@ -6,9 +6,11 @@ pre-accepted value of every unproposed id, noop-fill every unproposed range but 
 then its initial proposals still unproposed and its queued values at the next free ids.
 Proposer::OnLearn (:1383-1470) keeps the sets: a learned id leaves unlearned / unproposed,
 an initial proposal that lost its id is proposed again (now, or queued while preparing).
-A Proposer starts with every id unlearned (:1074-1082); the reference driver fills its
-initial proposals with the node's own Values of the trace not yet learned (prefill,
-oracle/ref_member_driver.cpp) and idles it at each E_EPOCH step until its next P_START.
+A P_PROPOSE record is Node::Propose -> Proposer::Propose (:1122-1156): value_id_ + 1, the
+next unproposed id at once, or queued while preparing (no Proposer: Unproposable).  A
+Proposer starts with every id unlearned (:1074-1082); the engine model and the reference
+driver idle it at each E_EPOCH step that creates it or changes its acceptors until its next
+P_START.
 The promise quorums and merged maps come from an MPXR result (what the device computes).
 Checked against the reference's own decisions (tests/golden/*.mpxd) on CPU; the engine's
 host walk (engine.cpp member_decisions) is the same algorithm.
@@ -101,46 +103,31 @@ def decisions(trace, result):
     b = bytearray(b"MPXD") + struct.pack("<II", 1, len(streams))
     for n, msgs in enumerate(streams):
         quorums = {q[0]: q[2] for q in res["nodes"][n]["quorums"]}
-        own = {}                                    # the driver's prefill source: iid -> value id
-        seen = set()
-        for m in msgs:
-            if struct.unpack_from("<I", m)[0] != 5:
-                continue
-            for iid, h in _learn_entries(m):
-                vid = h & ((1 << 47) - 1)
-                if (h >> 48) != n or (h >> 47) & 1 or vid in seen:
-                    continue
-                seen.add(vid)
-                own[iid] = vid
         learned = {}
         st = None                                   # the Proposer, if any
 
         def new_proposer():
             return {"unlearned": IdSet(), "unproposed": IdSet(), "initial": {}, "newly": set(), "vid": 0,
-                    "prep": True, "prefilled": False}
-
-        def prefill(p):
-            if p["prefilled"]:
-                return
-            p["prefilled"] = True
-            for iid in sorted(own):
-                if iid not in learned and iid not in p["initial"]:
-                    p["initial"][iid] = own[iid]
+                    "prep": True}
 
         if (epochs[0][2] >> n) & 1:
             st = new_proposer()
             st["prep"] = False
-            prefill(st)
         out, ei, idle = [], 0, False
         for k, m in enumerate(msgs):
             t = struct.unpack_from("<I", m)[0]
             if t != 18 and idle:
                 if st:
                     st["prep"] = False
-                    prefill(st)
                 idle = False
             if t == 16 and st:
                 st["prep"] = True
+            elif t == 19 and st:                    # Proposer::Propose (:1122-1156)
+                st["vid"] += 1
+                if not st["prep"]:
+                    st["initial"][st["unproposed"].next()] = st["vid"]
+                else:
+                    st["newly"].add(st["vid"])
             elif t == 1 and k in quorums and st:
                 un = st["unlearned"].copy()
                 batch = []

@@ -1297,6 +1297,8 @@ static int process_member(ctx_t *c, node_t *n, const u8 *m, size_t len, u64 seq)
         return OK;
     case 17: return m_on_p_batch(c, n, m, len, seq);
     case 18: return m_on_epoch(c, n, m, len);
+    case 19:                                               /* P_PROPOSE: the proposer's bookkeeping only */
+        return len < 8 || 8 + (size_t)rd32(m + 4) > len ? E_DECODE : OK;
     default: return E_DECODE;
     }
 }

@@ -119,9 +119,6 @@ struct Node {
     std::string events_q; u64 n_q = 0;
     std::string events_c; u64 n_c = 0;
     std::map<paxos::AcceptingID, std::map<paxos::InstanceID, u64> > batch_values;
-    paxos::Proposer *prefilled = NULL;
-    std::map<paxos::ValueID, paxos::ProposedValue> own_values;   // Values this node proposed (its LEARNs)
-    std::map<paxos::InstanceID, paxos::ValueID> own_iids;
     uint32_t epoch = 0;
     u64 P = 0, A = 0, L = 0;
     std::string events_d; u64 n_d = 0;               // phase-2 decisions (MPXD)
@@ -148,20 +145,34 @@ bool consistent(const Node &n, uint32_t id, const Epoch &e)
            (p->proposer_ != NULL) == (bool)((e.pmask >> id) & 1);
 }
 
-// Proposer bookkeeping Propose() would have filled (Proposer::OnLearn asserts
-// on it, member/paxos.cpp:1402-1424): the Values this node proposed, at the
-// instance each was first learned at.
-void prefill(Node &n)
+// P_PROPOSE body -> the ProposedValue Node::Propose / AddAcceptor / ... hand to the Proposer
+// (member/paxos.cpp:630-733): {u8 membership, u32 n, payload | n x {u32 node, u32 type},
+// u32 cblen, cb}, the Value_m layout after proposer / value id / noop (:330-408)
+bool proposed_value(const uint8_t *b, uint32_t len, paxos::ProposedValue &pv)
 {
-    paxos::Proposer *p = n.impl->proposer_;
-    if (!p || p == n.prefilled) return;
-    n.prefilled = p;
-    const PVMap &learned = n.impl->learner_.learned_values_;
-    for (auto &e : n.own_iids) {
-        if (learned.count(e.first)) continue;
-        p->unlearned_proposed_values_.insert(std::make_pair(e.second, n.own_values[e.second]));
-        p->initial_proposals_.insert(e);
+    if (len < 5) return false;
+    const bool mem = b[0] != 0;
+    const uint32_t n = rd32(b + 1);
+    size_t pos = 5;
+    if (mem) {
+        if ((len - pos) / 8 < n) return false;
+        pv.membership_changes_ = new std::vector<paxos::MembershipChange>();
+        for (uint32_t k = 0; k < n; ++k)
+            pv.membership_changes_->push_back(paxos::MembershipChange(rd32(b + pos + 8 * k),
+                                                                      (paxos::MembershipChangeType)rd32(b + pos + 8 * k + 4)));
+        pos += 8 * (size_t)n;
+    } else {
+        if (len - pos < n) return false;
+        pv.membership_changes_ = NULL;
+        pv.value_.assign((const char *)b + pos, n);
+        pos += n;
     }
+    if (len - pos < 4) return false;
+    const uint32_t cl = rd32(b + pos);
+    pos += 4;
+    if (len - pos < cl) return false;
+    pv.cb_.assign((const char *)b + pos, cl);
+    return true;
 }
 
 void make_idle(paxos::Proposer *p)
@@ -244,23 +255,6 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
         n.impl = new paxos::NodeImpl(g_thread, i, first, &logger, &clock, &timer, &rand, &cb, &n.net, &n.sm, cfg);
         n.impl->thread_ = g_thread;
         n.net.node_ = n.impl;
-        // own Values, first learned position
-        for (u64 k = 0; k < cnt[i]; ++k) {
-            const uint8_t *m = bytes[i] + rd64(offs[i] + 8 * k);
-            if (rd32(m) != 5) continue;
-            PVMap vals;
-            parse_pvalues(&logger, m + 20, rd32(m + 16), &vals);
-            for (auto &e : vals) {
-                const paxos::Value &v = e.second.value_;
-                if (v.proposer_ != i || v.noop_ || n.own_values.count(v.value_id_)) continue;
-                paxos::ProposedValue pv;
-                pv.membership_changes_ = v.membership_changes_ ? new std::vector<paxos::MembershipChange>(*v.membership_changes_) : NULL;
-                pv.value_ = v.value_;
-                pv.cb_ = v.cb_;
-                n.own_values[v.value_id_] = pv;
-                n.own_iids[e.first] = v.value_id_;
-            }
-        }
         // NodeImpl::Loop prologue (:738-747)
         paxos::NodeImpl *p = n.impl;
         p->learners_.insert(first);
@@ -270,7 +264,6 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
             p->proposer_ = new paxos::Proposer(p);
             p->acceptor_ = new paxos::Acceptor(p);
             make_idle(p->proposer_);     // the engine model: idle until P_START
-            prefill(n);
         }
     }
     if (!g_dummy_prt) g_dummy_prt = new paxos::PrepareRetryTimeout(NULL, 1000000);
@@ -413,7 +406,15 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
                 bool was = (o.pmask >> i) & 1, now = (x.pmask >> i) & 1;
                 n.epoch = e;
                 if (now && ni->proposer_ && (!was || o.amask != x.amask)) make_idle(ni->proposer_);
-                prefill(n);
+                break;
+            }
+            case 19: {     // P_PROPOSE: the reference's own Propose (Node::Propose -> :1122-1156)
+                const uint32_t pl = rd32(m + 4);
+                if (b - a < 8 + (u64)pl) return -4;
+                paxos::ProposedValue pv;
+                if (!proposed_value(m + 8, pl, pv)) return -4;
+                if (pr) pr->Propose(pv);                 // (no Proposer: Unproposable, :786-789)
+                discard_new_batches(pr, before_b);       // the trace's P_BATCH is the batch
                 break;
             }
             default: return -4;

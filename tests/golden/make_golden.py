@@ -56,6 +56,13 @@ def main():
         cases["c5_member_%d" % seed] = mpx.generate_trace(
             mpx.GEN_MEMBER, num_nodes=U, num_instances=M, seed=seed, batch=B, drop_rate=drop,
             dup_rate=dup, max_delay=64, noop_permille=noop)
+    # C5 contended: rival proposers' rounds (proposers > 1: multi-ballot promise phases, adopted
+    # values, rejected ACCEPTs, own values proposed again)
+    for seed, (U, M, B, drop, dup, P) in enumerate([(4, 400, 8, 0, 0, 2), (5, 2000, 16, 0, 0, 3),
+                                                    (6, 3000, 32, 500, 200, 3)]):
+        cases["c5_contended_%d" % seed] = mpx.generate_trace(
+            mpx.GEN_MEMBER, num_nodes=U, num_instances=M, seed=seed, batch=B, drop_rate=drop, dup_rate=dup,
+            max_delay=64, proposers=P)
     # C1: the reference's own demo, captured by capture_demo.py (tests/demotrace.py, test_demo.py)
     for path in sorted(glob.glob(os.path.join(HERE, "demo", "*.log.gz"))):
         cases[os.path.basename(path)[:-len(".log.gz")]] = demotrace.to_trace(demotrace.read_log(path))

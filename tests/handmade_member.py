@@ -3,12 +3,15 @@
 Every node starts in epoch 0 = {node 0} (NodeImpl::Loop, member/paxos.cpp:738-747);
 larger acceptor sets are reached the way the reference reaches them: membership
 Values learned in instance order and applied by ChangeMemberships (:1864-1964),
-each version step marked by an E_EPOCH record in the node's stream.
+each version step marked by an E_EPOCH record in the node's stream.  Node 0's own
+Values reach its Proposer as P_PROPOSE records (Node::Propose -> Proposer::Propose,
+:1122-1156) before they are sent, and carry the value ids Propose gives them
+(value_id_ + 1 per Propose and per noop of its own batches).
 """
 from mpxwire import (U64_MAX_EXCL, ADD_LEARNER, LEARNER_TO_PROPOSER, PROPOSER_TO_ACCEPTOR,
                      ACCEPTOR_TO_PROPOSER, PROPOSER_TO_LEARNER, DEL_LEARNER,
                      container, e_epoch, m_accept, m_accept_reply, m_learn, m_learn_reply,
-                     m_p_batch, m_prepare, m_prepare_reply, mvalue, p_start, reject)
+                     m_p_batch, m_p_propose, m_prepare, m_prepare_reply, mvalue, p_start, reject)
 
 B0 = (1 << 16) | 0
 B1 = (2 << 16) | 0
@@ -37,7 +40,8 @@ def v(i, p=0, vid=None, cb="cb"):
 
 
 class Member:
-    """Bootstrap: instances 0..k-1 hold AddAcceptor(1..k) proposed by node 0."""
+    """Bootstrap: instances 0..k-1 hold AddAcceptor(1..k) proposed by node 0 (value ids 1..k,
+    its first Proposes, taken at once: its Proposer is idle, member/paxos.cpp:1131-1150)."""
 
     def __init__(self, n_nodes, n_acceptors, extra_epochs=()):
         self.N = n_nodes
@@ -48,12 +52,20 @@ class Member:
             self.epochs.append((j, m, m))
         self.epochs += list(extra_epochs)
         self.boot = [(j - 1, B0, mvalue(0, j, cb="m%d" % j, changes=add_acceptor(j))) for j in range(1, n_acceptors)]
+        self.vid = self.k                         # node 0's value_id_ after the bootstrap proposals
         self.streams = [[] for _ in range(n_nodes)]
 
     def bootstrap(self, nodes=None):
-        """every listed node learns the bootstrap values and steps its epochs"""
+        """every listed node learns the bootstrap values and steps its epochs; node 0 proposed them"""
         for i in (range(self.N) if nodes is None else nodes):
-            self.streams[i] += [m_learn(0, 1, self.boot)] + [e_epoch(j) for j in range(1, self.k + 1)]
+            pre = [m_p_propose(v) for _i, _p, v in self.boot] if i == 0 else []
+            self.streams[i] += pre + [m_learn(0, 1, self.boot)] + [e_epoch(j) for j in range(1, self.k + 1)]
+
+    def own(self, i, cb="cb", changes=None):
+        """node 0's next own Value (the next value id its Proposer gives) and its P_PROPOSE record"""
+        self.vid += 1
+        val = mvalue(0, self.vid, cb=cb, changes=changes) if changes else mvalue(0, self.vid, str(i), cb)
+        return val, m_p_propose(val)
 
     def trace(self, M=64):
         return container(self.streams, M, semantics=1, epochs=self.epochs)
@@ -66,9 +78,10 @@ def member_traces():
     # 1. clean round with 3 acceptors of 3 nodes
     m = Member(3, 3)
     m.bootstrap()
-    ent = [(2, B1, v(2)), (3, B1, v(3)), (4, B1, v(4))]
+    own = [m.own(i) for i in (2, 3, 4)]
+    ent = [(i, B1, own[i - 2][0]) for i in (2, 3, 4)]
     s0 = m.streams[0]
-    s0 += [p_start(B1), m_prepare(ver, 0, B1, [(2, U64_MAX_EXCL)])]
+    s0 += [p_start(B1)] + [x[1] for x in own] + [m_prepare(ver, 0, B1, [(2, U64_MAX_EXCL)])]
     s0 += [m_prepare_reply(i, B1) for i in range(3)]
     s0 += [m_p_batch(1, ent), m_accept(ver, 0, 1, B1, ent)] + [m_accept_reply(i, 1) for i in range(3)]
     s0 += [m_learn(0, 2, ent)] + [m_learn_reply(i, 2) for i in range(3)]
@@ -118,10 +131,10 @@ def member_traces():
 
     # 5. acceptor reset: AcceptorToProposer(2) then ProposerToAcceptor(2) — the new
     #    Acceptor starts with promised = max = 0 and nothing accepted (:1897-1901,1952-1957)
-    a2p = mvalue(0, 10, cb="a2p", changes=[(2, ACCEPTOR_TO_PROPOSER)])
-    p2a = mvalue(0, 11, cb="p2a", changes=[(2, PROPOSER_TO_ACCEPTOR)])
     m = Member(3, 3, extra_epochs=[(3, mask(0, 1), mask(0, 1, 2)), (4, mask(0, 1, 2), mask(0, 1, 2))])
     m.bootstrap()
+    a2p, pa2p = m.own(2, cb="a2p", changes=[(2, ACCEPTOR_TO_PROPOSER)])
+    p2a, pp2a = m.own(3, cb="p2a", changes=[(2, PROPOSER_TO_ACCEPTOR)])
     m.streams[2] += [
         m_prepare(ver, 0, B2),
         m_accept(ver, 0, 1, B2, [(5, B2, v(5)), (6, B2, v(6))]),
@@ -131,7 +144,7 @@ def member_traces():
         m_accept(4, 0, 2, B0, [(5, B0, v(5, 0, 55))]),    # B0 >= promised(0): accepted
         m_prepare(4, 0, B1),
     ]
-    m.streams[0] += [m_learn(0, 3, [(2, B2, a2p)]), e_epoch(3), m_learn(0, 4, [(3, B2, p2a)]), e_epoch(4)]
+    m.streams[0] += [pa2p, pp2a, m_learn(0, 3, [(2, B2, a2p)]), e_epoch(3), m_learn(0, 4, [(3, B2, p2a)]), e_epoch(4)]
     m.streams[1] += [m_learn(0, 3, [(2, B2, a2p)]), e_epoch(3), m_learn(0, 4, [(3, B2, p2a)]), e_epoch(4)]
     t["mm_acceptor_reset"] = m.trace()
 
@@ -185,21 +198,52 @@ def member_traces():
     #    only (LearnersChanged, :1472-1502: drop every open learn, re-learn all)
     m = Member(4, 2, extra_epochs=[(1, mask(0, 1), mask(0, 1), mask(0, 1, 3)), (1, mask(0, 1), mask(0, 1), mask(0, 1))])
     m.bootstrap([0])
-    ents = [(1, B1, v(1)), (2, B1, v(2))]
-    al3 = mvalue(0, 20, cb="al3", changes=[(3, ADD_LEARNER)])
-    dl3 = mvalue(0, 21, cb="dl3", changes=[(3, DEL_LEARNER)])
+    o1, o2 = m.own(1), m.own(2)
+    ents = [(1, B1, o1[0]), (2, B1, o2[0])]
+    al3, pal3 = m.own(3, cb="al3", changes=[(3, ADD_LEARNER)])
+    dl3, pdl3 = m.own(4, cb="dl3", changes=[(3, DEL_LEARNER)])
     m.streams[0] += [
         # (learn 1: AddAcceptor(1)'s ADD_LEARNER while the bootstrap LEARN applies)
-        p_start(B1), m_prepare_reply(0, B1), m_prepare_reply(1, B1),   # quorum: learn 2 (learned boot value)
+        p_start(B1), o1[1], o2[1],                                    # queued while preparing
+        m_prepare_reply(0, B1), m_prepare_reply(1, B1),               # quorum: learn 2 (learned boot value)
         m_p_batch(5, ents), m_accept_reply(0, 5), m_accept_reply(1, 5),   # chosen: learn 3
         m_learn_reply(0, 2), m_learn_reply(1, 2),                     # learn 2 applied, retired (2 learners)
         m_learn(0, 2, ents), m_learn_reply(0, 3),
+        pal3, pdl3,                                                   # proposed at once: 3, 4
         m_learn(0, 3, [(3, B1, al3)]), e_epoch(2),                    # learners {0,1,3}: drops 3, learn 4
         m_learn_reply(0, 4), m_learn_reply(1, 4), m_learn_reply(2, 4), m_learn_reply(3, 4),   # 2: not a learner
         m_learn(0, 4, [(4, B1, dl3)]), e_epoch(3),                    # learners {0,1}: learn 5
         m_learn_reply(1, 5), m_learn_reply(3, 1), m_learn_reply(0, 5),
     ]
     t["mm_learners"] = m.trace()
+
+    # 9. Propose (f2; member/paxos.cpp:1122-1156, OnPrepareReply :1183-1297, OnLearn :1383-1470):
+    #    values proposed at once and queued while preparing; a quorum adopts another proposer's
+    #    value at an instance node 0 had proposed, so its LEARN is a conflict: the lost value is
+    #    proposed again at once (not preparing), and a second conflict while preparing is queued
+    #    for the next quorum's batch
+    m = Member(3, 3)
+    m.bootstrap()
+    a, b, c, d = m.own(2), m.own(3), m.own(4), m.own(5)
+    x3 = mvalue(1, 7, "x3", "cb")                         # node 1's value at instance 3
+    x5 = mvalue(2, 9, "x5", "cb")                         # node 2's value at instance 5
+    s0 = m.streams[0]
+    s0 += [
+        a[1], b[1],                                       # at once: instances 2, 3
+        m_p_batch(1, [(2, B0, a[0]), (3, B0, b[0])]),
+        p_start(B1), c[1],                                # queued while preparing
+        m_prepare_reply(1, B1, [(2, B0, a[0]), (3, B2, x3)]),
+        m_prepare_reply(2, B1, [(3, B1, b[0])]),          # quorum: adopt 2 = a, 3 = x3 (B2 > B1); c at 4
+        m_p_batch(2, [(2, B1, a[0]), (3, B1, x3), (4, B1, c[0])]),
+        m_learn(1, 3, [(3, B2, x3)]),                     # conflict: b proposed again at once (5)
+        d[1],                                             # at once: 6
+        p_start(B3),
+        m_learn(2, 4, [(5, B2, x5)]),                     # conflict while preparing: b queued
+        m_prepare_reply(0, B3, [(4, B1, c[0]), (6, B1, d[0])]),
+        m_prepare_reply(1, B3),                           # quorum: adopt 4 = c, 6 = d; 2 (unlearned,
+                                                          # no reply holds it): noop; b queued -> 7
+    ]
+    t["mm_propose"] = m.trace()
     return t
 
 

@@ -170,5 +170,13 @@ def m_p_batch(batch_id, entries):
     return struct.pack("<IQI", 17, batch_id, len(body)) + body
 
 
+def m_p_propose(value):
+    """Node::Propose / AddAcceptor / ... reaching the member Proposer (member/paxos.cpp:630-733,
+    1122-1156): the Value_m bytes after proposer / value id / noop (membership flag, payload or
+    change list, cb), as {u32 type=19, u32 len, body}.  `value`: an mvalue (not a noop)."""
+    body = value[13:]
+    return struct.pack("<II", 19, len(body)) + body
+
+
 def e_epoch(epoch):
     return struct.pack("<II", 18, epoch)

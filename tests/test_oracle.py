@@ -94,7 +94,7 @@ def test_member_reference_checks_epoch_markers():
     # node 1 learns AddAcceptor(1) but the trace omits its E_EPOCH marker: the
     # reference driver refuses the trace (the epoch table would be a lie)
     m = Member(2, 2)
-    m.streams[0] += [m_learn(0, 1, m.boot), e_epoch(1)]
+    m.bootstrap([0])
     m.streams[1] += [m_learn(0, 1, m.boot), m_prepare(1, 0, 5 << 16)]
     with pytest.raises(RuntimeError, match="-11"):
         ref_run(m.trace())
