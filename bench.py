@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--c5-instances", type=int, default=1 << 25, help="C5 member-path leg: M (2^25); 0 = skip")
     ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--c5-only", action="store_true", help="only the C5 leg (profiling)")
+    ap.add_argument("--c5c-instances", type=int, default=1 << 25,
+                    help="contended C5 leg (3 member proposers, a rival round per epoch): M (2^25); 0 = skip")
+    ap.add_argument("--c5c-only", action="store_true", help="only the contended C5 leg (profiling)")
     ap.add_argument("--shard-of", type=int, default=8,
                     help="also time rank 0's shard of the same trace at world G on this GPU (a 1-GPU scaling "
                          "projection, no RCCL); 0 / 1 = skip")
@@ -97,6 +100,10 @@ C3 = dict(num_nodes=7, seed=0, batch=256, proposers=3, drop_rate=500, dup_rate=1
 # C5: member semantics, acceptor universe 8, AddAcceptor(1..7) then DelAcceptor(1..7)
 # (member/main.cpp:119-141), 1 % loss / duplicates, stale in-flight ACCEPTs across version changes
 C5 = dict(num_nodes=8, seed=0, batch=256, drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15)
+# contended C5: the same schedule with 3 member proposers — from epoch 2 a
+# rival prepares above the leader over its own unlearned ids (member/paxos.cpp:1158-1182,
+# 1504-1549,1614-1629): promise replies carrying most of the history, merged maps, rejects
+C5C = dict(C5, proposers=3)
 
 
 def log(msg):
@@ -110,13 +117,13 @@ def c3_leg(args, kind="c3"):
     is the same mpx_step the C4 line times.  roofline on SURVEY §8(d)'s bytes
     (16 P + 24 A + 16 L from the engine's counters) over the apply phase.
     kind "c5": the same over the C5 member trace (member role gates, insert-first apply,
-    per-epoch quorums: the member instantiation of k_apply)."""
-    member = kind == "c5"
-    m = args.c5_instances if member else args.c3_instances
+    per-epoch quorums: the member instantiation of k_apply); "c5c": contended C5."""
+    member = kind in ("c5", "c5c")
+    m = args.c5c_instances if kind == "c5c" else args.c5_instances if member else args.c3_instances
     steps = args.c5_steps if member else args.c3_steps
     t0 = time.perf_counter()
     if member:
-        trace = mpx.generate_trace(mpx.GEN_MEMBER, num_instances=m, copy=False, **C5)
+        trace = mpx.generate_trace(mpx.GEN_MEMBER, num_instances=m, copy=False, **(C5C if kind == "c5c" else C5))
     else:
         trace = mpx.generate_trace(mpx.GEN_FAULTY, num_instances=m, copy=False, **C3)
     t_gen = time.perf_counter() - t0
@@ -163,7 +170,7 @@ def c3_leg(args, kind="c3"):
     b_eng = st["slot_bytes"] * (hd["num_nodes"] + 1) * nb_l * 256 + 16 * st["num_runs"] + \
         16 * (hd["num_nodes"] + 1) * nb_l
     achieved_eng = b_eng / (apply_ms * 1e-3) / 1e9 if apply_ms else 0.0
-    pmc = latest_pmc(8 if member else 7, m, 1, workload="C5" if member else "C3")
+    pmc = latest_pmc(8 if member else 7, m, 1, workload=kind.upper())
     hw = hw_roofline(pmc, apply_ms)
     ms_step = dt / steps * 1e3
     eng.close()
@@ -176,6 +183,9 @@ def c3_leg(args, kind="c3"):
         workload = ("C5: 2^%d instances, member semantics, acceptor universe 8, AddAcceptor(1..7) then "
                     "DelAcceptor(1..7) = 15 epochs (member/main.cpp:119-141), 1%% loss / 1%% duplicates, "
                     "batch U[1,256]" % (m.bit_length() - 1))
+        if kind == "c5c":
+            workload += (", contended: 3 member proposers (a rival round above the leader in every epoch from "
+                         "2, over its own unlearned ids; the leader re-prepares)")
     else:
         workload = ("C3: 2^%d instances x 7 acceptors, 3 competing proposers, drop 5%% / dup 10%% (<=3) / "
                     "delay U[0,500) (multi/debug.conf.sample:1), batch U[1,256]" % (m.bit_length() - 1))
@@ -208,7 +218,7 @@ def c3_leg(args, kind="c3"):
                      "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
                      "traffic_source": ("profiles/%s_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the apply "
                                         "phase, bench.py --%s-only; not measured inside this process)"
-                                        % (pmc["tag"], "c5" if member else "c3"))
+                                        % (pmc["tag"], kind))
                      if pmc else None},
         "verified": {"step_state_digest_vs_run": step_ok, "state_digest": chk["state_digest"],
                      "chosen_digest": chk["chosen_digest"]},
@@ -593,6 +603,9 @@ def main():
     if args.c5_only:
         print(json.dumps({"c5": c3_leg(args, "c5")}), flush=True)
         return
+    if args.c5c_only:
+        print(json.dumps({"c5_contended": c3_leg(args, "c5c")}), flush=True)
+        return
     world, rank, local, pg = dist_setup(args)
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
@@ -678,16 +691,17 @@ def main():
             cpu_port = cpu_port_baseline(args, args.cpu_seconds / 2)
         proj = shard_projection(args, ms_per_step) if world == 1 and args.shard_of > 1 else None
         c3 = c3_leg(args) if world == 1 and args.c3_instances else None
-        c5 = None
-        if world == 1 and args.c5_instances:
+        def secondary(kind):
             try:                                    # a secondary leg: out of memory is reported, not fatal;
-                c5 = c3_leg(args, "c5")             # a wrong result (AssertionError) or any other error is
+                return c3_leg(args, kind)           # a wrong result (AssertionError) or any other error is
             except MemoryError as ex:               # fatal
-                c5 = {"error": repr(ex)}
+                return {"error": repr(ex)}
             except mpx.MpxError as ex:
                 if ex.rc != -2:                     # MPX_E_NOMEM
                     raise
-                c5 = {"error": repr(ex)}
+                return {"error": repr(ex)}
+        c5 = secondary("c5") if world == 1 and args.c5_instances else None
+        c5c = secondary("c5c") if world == 1 and args.c5c_instances else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -731,6 +745,7 @@ def main():
             **({"scaling_projection": proj} if proj else {}),
             "c3": c3,
             **({"c5": c5} if c5 else {}),
+            **({"c5_contended": c5c} if c5c else {}),
             "verified": {"step_state_digest_vs_closed_form": step_ok, "step_state_digest": step_state,
                          "step_chosen_digest": step_chosen, "run_digests_vs_closed_form": verified,
                          "state_digest": chk["state_digest"], "chosen_digest": chk["chosen_digest"]},

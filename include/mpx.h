@@ -144,7 +144,7 @@ typedef struct mpx_config {
     uint64_t shard_begin;      /* this engine owns instances [shard_begin,         */
     uint64_t shard_end;        /*                              shard_end)          */
     uint32_t num_epochs;       /* member only                                      */
-    uint32_t flags;            /* 0, or MPX_FLAG_INCREMENTAL [| MPX_FLAG_DECISIONS (multi)] */
+    uint32_t flags;            /* 0, or MPX_FLAG_INCREMENTAL [| MPX_FLAG_DECISIONS]  */
     const mpx_epoch *epochs;   /* member only, indexed by E_EPOCH's epoch          */
 } mpx_config;
 
@@ -159,17 +159,21 @@ typedef struct mpx_config {
  * mpx_drain_sends returns the window's replies; the mpx_read_* state readbacks and
  * mpx_state_digest give the cumulative state; mpx_stats counts the window.  Not
  * available in this mode (MPX_E_STATE): mpx_step / mpx_reset_state (windows are applied
- * once), mpx_dump_result, the commits / learns readbacks and the sharded decisions (they
- * walk the run's history).
+ * once), mpx_dump_result, the commits readback and the sharded decisions (they walk the
+ * run's history), and the decisions / learns readbacks unless MPX_FLAG_DECISIONS carries
+ * their bookkeeping.
  * Errors: a window refused while it is built (MPX_E_RANGE, MPX_E_DECODE, ...) leaves the
  * engine as it was — its records stay queued and are refused again; a failure after the
  * window was taken (a HIP error) may leave it partly applied, so the engine is poisoned:
  * every later mpx_run, submit and readback returns MPX_E_STATE. */
 #define MPX_FLAG_INCREMENTAL 1u
-/* With MPX_FLAG_INCREMENTAL (multi semantics): every mpx_run also advances the proposers'
- * phase-2 bookkeeping over the window's events (the quorums' merged maps, COMMIT entries,
- * client values), so mpx_read_decisions returns the decisions of every window so far —
- * the MPXD of one run over the whole stream (host work per window, O(window)). */
+/* With MPX_FLAG_INCREMENTAL: every mpx_run also advances the proposers' phase-2
+ * bookkeeping over the window's events (the quorums' merged maps, COMMIT / LEARN entries,
+ * client values; member: E_EPOCH role changes), so mpx_read_decisions returns the
+ * decisions of every window so far — the MPXD of one run over the whole stream (host work
+ * per window, O(window)).  Member semantics: the learn bookkeeping (LearningValues
+ * creation, replies, AcceptorsChanged, drops) advances the same way and mpx_read_learns
+ * returns the MPXL of the whole stream (k_learns over every learn at read time). */
 #define MPX_FLAG_DECISIONS 2u
 
 typedef struct mpx_engine mpx_engine;
@@ -486,7 +490,11 @@ int  mpx_read_decisions_sharded(mpx_engine *eng, uint8_t **out, uint64_t *size);
  * instances' entries of them.  mpx_proposal_part writes this shard's events, format
  * MPXE: "MPXE" u32 1, u32 nodes, u64 shard_begin, u64 shard_end; per node u64 count,
  * per event {u64 seq, u32 type (19 P_PROPOSE, 16 P_START, 5 COMMIT, 1 promise
- * quorum), u32 n, {u64 iid, u64 handle} * n}.  mpx_proposal_combine takes every
+ * quorum), u32 n, {u64 iid, u64 handle} * n}.  Member semantics (every member decision
+ * walk, client values or not): "MPXE" u32 2, the same header, then u32 E and E x {u64
+ * acceptor_mask, u64 proposer_mask} (the epoch table), and per event {u64 seq, u32 type
+ * (as above, 5 = LEARN, plus 18 E_EPOCH), u32 n, u64 aux (E_EPOCH: the epoch), entries}.
+ * mpx_proposal_combine takes every
  * shard's part in shard order (contiguous ranges from 0), merges each node's events
  * by record (entries concatenated in shard order) and writes the MPXD
  * mpx_read_decisions writes on one engine holding every instance.  Pure host work. */

@@ -64,8 +64,14 @@ struct StepEvents { hipEvent_t e[5]; bool store_last; };   // launch_run's event
 }  // namespace
 
 struct PropNode;
+struct MPropNode;
 static std::vector<PropNode> *prop_new(uint32_t nodes);
 static void prop_free(std::vector<PropNode> *p);
+static std::vector<MPropNode> *mprop_new(uint32_t nodes);
+static void mprop_free(std::vector<MPropNode> *p);
+struct LearnCarry;
+static LearnCarry *learn_new(uint32_t nodes);
+static void learn_free(LearnCarry *c);
 struct mpx_engine;
 static int prop_window(mpx_engine *e);
 
@@ -113,6 +119,13 @@ struct mpx_engine {
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
     DevBuf gather_buf;
+    // the per-launch summary all-gather runs on its own stream, overlapped with the next
+    // launch's kernels: summaries and gather buffers alternate between two slots, and a launch
+    // waits only for the all-gather that last read its slot (two launches back)
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t sum_ev[2] = {nullptr, nullptr}, ag_ev[2] = {nullptr, nullptr};
+    bool ag_pending[2] = {false, false};
+    uint32_t sum_idx = 0;
     DevBuf comm_buf, comm_buf2;             // mpx_comm_allreduce_max / mpx_comm_allgather_bytes
     // incremental runs (MPX_FLAG_INCREMENTAL): the host carry between windows,
     // the device state carried as values, and each node's records in earlier windows
@@ -126,6 +139,8 @@ struct mpx_engine {
     uint64_t g_cap = 0;                     // global batches g_mask / g_done hold
     std::vector<uint64_t> seq_base, win_seq_base;
     std::vector<PropNode> *prop = nullptr;           // MPX_FLAG_DECISIONS: the bookkeeping carried across windows
+    std::vector<MPropNode> *mprop = nullptr;         //   (member semantics: + the learn bookkeeping)
+    LearnCarry *lrn = nullptr;
     uint64_t windows = 0;
     uint64_t events_every = 1, step_no = 0;   // mpx_timing_every
     uint32_t seq = 0;                         // launches so far (DevView::seq, the violation record's buffer)
@@ -170,7 +185,6 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
     if (cfg->semantics == MPX_SEM_MULTI && cfg->num_epochs) return MPX_E_INVAL;
     if (cfg->flags & ~(uint32_t)(MPX_FLAG_INCREMENTAL | MPX_FLAG_DECISIONS)) return MPX_E_INVAL;
     if ((cfg->flags & MPX_FLAG_DECISIONS) && !(cfg->flags & MPX_FLAG_INCREMENTAL)) return MPX_E_INVAL;
-    if ((cfg->flags & MPX_FLAG_DECISIONS) && cfg->semantics != MPX_SEM_MULTI) return MPX_E_INVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPX_E_NODEVICE;
     if (cfg->device < 0 || cfg->device >= n) return MPX_E_NODEVICE;
@@ -194,7 +208,11 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
         // entries and 16 B for a promise round's pre-accepted map, 8 B per instance of
         // chosen log (all zero: the PaxosImpl ctor state, multi/paxos.cpp:323-346)
         e->incremental = true;
-        if (cfg->flags & MPX_FLAG_DECISIONS) e->prop = prop_new(cfg->num_nodes);
+        if ((cfg->flags & MPX_FLAG_DECISIONS) && cfg->semantics == MPX_SEM_MULTI) e->prop = prop_new(cfg->num_nodes);
+        if ((cfg->flags & MPX_FLAG_DECISIONS) && cfg->semantics == MPX_SEM_MEMBER) {
+            e->mprop = mprop_new(cfg->num_nodes);
+            e->lrn = learn_new(cfg->num_nodes);
+        }
         e->wc.init(cfg->num_nodes, e->NB);
         e->seq_base.assign(cfg->num_nodes, 0);
         const uint64_t NL = (uint64_t)cfg->num_nodes * e->shard_len;
@@ -220,9 +238,17 @@ extern "C" int mpx_destroy(mpx_engine *e)
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (auto &s : e->ev_pool) for (auto ev : s.e) (void)hipEventDestroy(ev);
+    if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
     if (e->comm) ncclCommDestroy(e->comm);
+    for (int k = 0; k < 2; ++k) {
+        if (e->sum_ev[k]) (void)hipEventDestroy(e->sum_ev[k]);
+        if (e->ag_ev[k]) (void)hipEventDestroy(e->ag_ev[k]);
+    }
+    if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     prop_free(e->prop);
+    mprop_free(e->mprop);
+    learn_free(e->lrn);
     delete e;
     return MPX_OK;
 }
@@ -445,7 +471,7 @@ static int finish_view(mpx_engine *e)
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + std::max<uint64_t>(e->geom.chosen_wgs, e->num_cus * 16))));
     TRY(e->viol.alloc(2 * sizeof(DevViolation)));                     // double-buffered (reset_state)
     HTRY(hipMemsetAsync(e->viol.p, 0, 2 * sizeof(DevViolation), e->stream));
-    TRY(e->summary.alloc(64 * 8));
+    TRY(e->summary.alloc(2 * 64 * 8));                                // two slots (comm overlap)
     e->out_subs = 64;
     if (const char *x = std::getenv("MPX_OUT_SUBS")) {  // A/B: snapshot sub-buffers (power of two)
         const uint32_t k = (uint32_t)std::atoi(x);
@@ -468,7 +494,7 @@ static int finish_view(mpx_engine *e)
     v.partials = e->partials.as<unsigned long long>();
     v.viol = e->viol.as<DevViolation>();
     v.viol_next = e->viol.as<DevViolation>() + 1;
-    v.summary = e->summary.as<unsigned long long>();
+    v.summary = e->summary.as<unsigned long long>() + 64 * e->sum_idx;
     v.node_scal = e->node_scal.as<uint64_t>();
     return MPX_OK;
 }
@@ -712,6 +738,11 @@ static int queue_run(mpx_engine *e, bool digest)
     e->view.seq = e->seq;
     e->view.viol = e->viol.as<DevViolation>() + (e->seq & 1);
     e->view.viol_next = e->viol.as<DevViolation>() + ((e->seq + 1) & 1);
+    // this launch's summary slot: free once the all-gather that read it (two launches back) ran
+    const uint32_t idx = e->sum_idx ^ 1;
+    e->sum_idx = idx;
+    e->view.summary = e->summary.as<unsigned long long>() + 64 * idx;
+    if (e->ag_pending[idx]) HTRY(hipStreamWaitEvent(e->stream, e->ag_ev[idx], 0));
     void *evp[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     if (ev) for (int k = 0; k < 5; ++k) evp[k] = ev->e[k];
     if (ev) ev->store_last = run_ends_with_store(e->view);
@@ -723,18 +754,27 @@ static int queue_run(mpx_engine *e, bool digest)
         if (e->cfg.semantics == MPX_SEM_MEMBER)
             HTRY(hipMemcpyAsync(e->ee_init.p, e->ee_out.p, 4ull * e->cfg.num_nodes, hipMemcpyDeviceToDevice, e->stream));
     }
-    // the one cross-GPU exchange: every rank's 64-word summary, over RCCL on
-    // the same stream, no host synchronisation
-    if (e->comm && ncclAllGather(e->summary.p, e->gather_buf.p, 64, ncclUint64, e->comm, e->stream) != ncclSuccess)
-        return MPX_E_COMM;
+    // the one cross-GPU exchange: every rank's 64-word summary, over RCCL, no host
+    // synchronisation — on the comm stream once the launch wrote it, so the
+    // next launch's kernels run while it crosses xGMI
+    if (e->comm) {
+        HTRY(hipEventRecord(e->sum_ev[idx], e->stream));
+        HTRY(hipStreamWaitEvent(e->comm_stream, e->sum_ev[idx], 0));
+        if (ncclAllGather(e->view.summary, e->gather_buf.as<uint64_t>() + 64ull * e->nranks * idx, 64, ncclUint64,
+                          e->comm, e->comm_stream) != ncclSuccess)
+            return MPX_E_COMM;
+        HTRY(hipEventRecord(e->ag_ev[idx], e->comm_stream));
+        e->ag_pending[idx] = true;
+    }
     return MPX_OK;
 }
 
 static int collect(mpx_engine *e)
 {
     HTRY(hipStreamSynchronize(e->stream));
+    if (e->comm_stream) HTRY(hipStreamSynchronize(e->comm_stream));   // the step includes its exchange
     e->last_summary.assign(64, 0);
-    HTRY(hipMemcpy(e->last_summary.data(), e->summary.p, 64 * 8, hipMemcpyDeviceToHost));
+    HTRY(hipMemcpy(e->last_summary.data(), e->summary.as<uint64_t>() + 64 * e->sum_idx, 64 * 8, hipMemcpyDeviceToHost));
     uint64_t cursor = 0;
     if (e->incremental) {
         // a window is not re-run (its carry has moved on): the record buffer is sized for every
@@ -798,7 +838,7 @@ static int run_window(mpx_engine *e)
     e->dirty = true;
     TRY(queue_run(e, false));
     TRY(collect(e));
-    if (e->prop) TRY(prop_window(e));
+    if (e->prop || e->mprop) TRY(prop_window(e));
     // batches chosen in this window need their entries no more
     std::vector<uint32_t> bc;
     TRY(d2h(bc, e->b_chosen, e->ht.b_gid.size()));
@@ -1499,6 +1539,7 @@ struct PEv {
     uint64_t seq;
     uint32_t type;
     std::vector<std::pair<uint64_t, uint64_t>> ents;      // {iid, handle}, iid ascending
+    uint64_t aux = 0;                                     // member E_EPOCH: the epoch index
 };
 typedef std::vector<std::vector<PEv>> PEvents;
 
@@ -1615,11 +1656,20 @@ static void proposer_sim(const PEvents &ev, std::string &d)
 
 // MPX_FLAG_DECISIONS: the proposers' bookkeeping advanced over the last window's events (its
 // quorums' merged maps carry the pre-accepted values of earlier windows, k_apply_win)
+static int member_events(mpx_engine *e, const Results &r, PEvents &ev);
+static int mprop_advance(MPropNode &st, uint32_t n, const std::vector<PEv> &evs, const std::vector<mpx_epoch> &ep);
+static int learn_window(mpx_engine *e, const Results &r);
+
 static int prop_window(mpx_engine *e)
 {
     Results r;
     TRY(fetch_results(e, r));
     PEvents ev;
+    if (e->mprop) {
+        TRY(member_events(e, r, ev));
+        for (uint32_t n = 0; n < e->cfg.num_nodes; ++n) TRY(mprop_advance((*e->mprop)[n], n, ev[n], e->epochs));
+        return learn_window(e, r);
+    }
     proposer_events(e, r, ev);
     for (uint32_t n = 0; n < e->cfg.num_nodes; ++n) prop_advance((*e->prop)[n], n, ev[n]);
     return MPX_OK;
@@ -1649,102 +1699,160 @@ static bool has_proposals(const HostTrace &h)
 // and merged maps (k_apply's records).
 static int put_bytes(const std::string &d, uint8_t **out, uint64_t *size);
 
-static int member_decisions(mpx_engine *e, const Results &r, std::string &d)
+// The member bookkeeping reads, per node in stream order: Propose, StartPrepare, each
+// promise quorum's merged map, each LEARN's entries and the E_EPOCH markers (aux: the
+// epoch).  Headers are replicated over instance shards, entries split (mpx_proposal_part).
+static int member_events(mpx_engine *e, const Results &r, PEvents &ev)
 {
     const HostTrace &h = e->ht;
     const uint32_t N = e->cfg.num_nodes;
-    const auto &ep = e->epochs;
-    d.append("MPXD", 4);
-    app<uint32_t>(d, 1); app<uint32_t>(d, N);
-    struct Prop {
+    ev.assign(N, {});
+    for (uint32_t n = 0; n < N; ++n)
+        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
+            const uint8_t t = h.m_type[g];
+            const bool quorum = t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM);
+            if (t != MPX_MSG_P_PROPOSE && t != MPX_MSG_P_START && t != MPX_MSG_COMMIT && t != MPX_MSG_E_EPOCH && !quorum)
+                continue;
+            PEv x{seq_of(h, n, g) + (e->incremental ? e->win_seq_base[n] : 0), t, {}};
+            if (t == MPX_MSG_E_EPOCH) x.aux = h.m_ver[g];
+            if (t == MPX_MSG_COMMIT)
+                for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) x.ents.push_back({h.e_iid[k], h.e_val[k]});
+            if (quorum) {
+                auto it = r.by_msg[1].find((uint32_t)g);
+                if (it != r.by_msg[1].end())
+                    for (const OutEnt *o : it->second) x.ents.push_back({o->iid, o->handle});
+                std::sort(x.ents.begin(), x.ents.end());
+            }
+            ev[n].push_back(std::move(x));
+        }
+    return MPX_OK;
+}
+
+// One node's member Proposer bookkeeping, advanced over its events (a whole run, window by
+// window under MPX_FLAG_DECISIONS, or over the union of shard parts).  A Proposer starts
+// with every id unlearned and preparing (:1074-1082); the engine model idles it at the
+// E_EPOCH run that created it or changed its acceptors (include/mpx.h) — until the node's
+// next record that is not a marker, which the events stand for (nothing between them reads
+// the flag).
+struct MPropNode {
+    struct P {
         IdSet unlearned, unproposed;
         std::map<uint64_t, uint64_t> initial;          // initial_proposals_: instance -> value id
         std::set<uint64_t> newly;                      // newly_proposed_values_
         uint64_t vid = 0;                              // value_id_
         bool preparing = true;
     };
-    for (uint32_t n = 0; n < N; ++n) {
-        std::unordered_map<uint64_t, uint64_t> learned;      // the learner's learned_values_ (insert-first)
-        std::unique_ptr<Prop> p;
-        if ((ep[0].proposer_mask >> n) & 1) { p.reset(new Prop); p->preparing = false; }
-        std::string body;
-        uint64_t count = 0;
-        uint32_t ei = 0;
-        bool idle = false;
-        for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
-            const uint8_t t = h.m_type[g];
-            if (t != MPX_MSG_E_EPOCH && idle) {
-                if (p) p->preparing = false;
-                idle = false;
-            }
-            if (t == MPX_MSG_P_START) {
-                if (p) p->preparing = true;
-            } else if (t == MPX_MSG_P_PROPOSE) {           // Proposer::Propose (:1122-1156)
-                if (p) {
-                    ++p->vid;
-                    if (!p->preparing) p->initial[p->unproposed.next()] = p->vid;
-                    else p->newly.insert(p->vid);
-                }
-            } else if (t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM) && p) {
-                IdSet un = p->unlearned;
-                std::vector<std::pair<uint64_t, uint64_t>> b;
-                auto it = r.by_msg[1].find((uint32_t)g);
-                if (it != r.by_msg[1].end())
-                    for (const OutEnt *o : it->second)
-                        if (un.contains(o->iid)) { un.remove(o->iid); b.push_back({o->iid, o->handle}); }
-                while (un.r.size() > 1) {
-                    const auto first = *un.r.begin();
-                    un.r.erase(un.r.begin());
-                    for (uint64_t id = first.first; id != first.second; ++id) b.push_back({id, MPX_HANDLE(n, 1, ++p->vid)});
-                }
-                for (auto &x : p->initial)
-                    if (un.contains(x.first)) { un.remove(x.first); b.push_back({x.first, MPX_HANDLE(n, 0, x.second)}); }
-                for (uint64_t v : p->newly) {
-                    const uint64_t iid = un.next();
-                    p->initial[iid] = v;
-                    b.push_back({iid, MPX_HANDLE(n, 0, v)});
-                }
-                p->newly.clear();
-                p->unproposed = un;
-                p->preparing = false;
-                std::sort(b.begin(), b.end());
-                app<uint64_t>(body, seq_of(h, n, g));
-                app<uint64_t>(body, b.size());
-                for (auto &x : b) { app<uint64_t>(body, x.first); app<uint64_t>(body, x.second); }
-                ++count;
-            } else if (t == MPX_MSG_COMMIT) {                  // LEARN: Learner::OnLearn (:1029-1060)
-                if (p) {                                       // Proposer::OnLearn (:1383-1470)
-                    std::set<uint64_t> conflicts;
-                    for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) {
-                        const uint64_t iid = h.e_iid[k], hv = h.e_val[k];
-                        if (!learned.count(iid) && p->unlearned.contains(iid)) p->unlearned.remove(iid);
-                        if (p->unproposed.contains(iid)) p->unproposed.remove(iid);
-                        auto in = p->initial.find(iid);
-                        if (in != p->initial.end()) {
-                            if (MPX_HANDLE_PROPOSER(hv) != n || MPX_HANDLE_VALUE_ID(hv) != in->second) conflicts.insert(in->second);
-                            p->initial.erase(in);
-                        }
-                    }
-                    if (!p->preparing) { for (uint64_t v : conflicts) p->initial[p->unproposed.next()] = v; }
-                    else p->newly.insert(conflicts.begin(), conflicts.end());
-                }
-                for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) learned.emplace(h.e_iid[k], h.e_val[k]);
-            } else if (t == MPX_MSG_E_EPOCH) {
-                const uint32_t ej = h.m_ver[g];
-                if (ej >= ep.size()) return MPX_E_DECODE;
-                const mpx_epoch &o = ep[ei], &x = ep[ej];
-                const bool was = (o.proposer_mask >> n) & 1, now = (x.proposer_mask >> n) & 1;
-                if (now && !was) p.reset(new Prop);            // the constructor's StartPrepare
-                if (was && !now) p.reset();
-                if (p && x.acceptor_mask != o.acceptor_mask) p->preparing = true;   // AcceptorsChanged
-                if (now && (!was || o.acceptor_mask != x.acceptor_mask)) idle = true;
-                ei = ej;
-            }
+    std::unique_ptr<P> p;
+    IdSet notlearned;                                  // the learner's learned_values_, complemented
+    uint32_t ei = 0;
+    bool idle = false, started = false;
+    std::string body;
+    uint64_t count = 0;
+};
+
+static std::vector<MPropNode> *mprop_new(uint32_t nodes) { return new std::vector<MPropNode>(nodes); }
+static void mprop_free(std::vector<MPropNode> *p) { delete p; }
+
+static int mprop_advance(MPropNode &st, uint32_t n, const std::vector<PEv> &evs, const std::vector<mpx_epoch> &ep)
+{
+    if (!st.started) {                                 // the genesis roles (NodeImpl::Loop, :738-747)
+        st.started = true;
+        if ((ep[0].proposer_mask >> n) & 1) { st.p.reset(new MPropNode::P); st.p->preparing = false; }
+    }
+    auto &p = st.p;
+    for (const PEv &x : evs) {
+        const uint32_t t = x.type;
+        if (t != MPX_MSG_E_EPOCH && st.idle) {
+            if (p) p->preparing = false;
+            st.idle = false;
         }
-        app<uint64_t>(d, count);
-        d += body;
+        if (t == MPX_MSG_P_START) {
+            if (p) p->preparing = true;
+        } else if (t == MPX_MSG_P_PROPOSE) {               // Proposer::Propose (:1122-1156)
+            if (p) {
+                ++p->vid;
+                if (!p->preparing) p->initial[p->unproposed.next()] = p->vid;
+                else p->newly.insert(p->vid);
+            }
+        } else if (t == MPX_MSG_PREPARE_REPLY) {           // a promise quorum (:1183-1297)
+            if (!p) continue;
+            IdSet un = p->unlearned;
+            std::vector<std::pair<uint64_t, uint64_t>> b;
+            for (auto &en : x.ents)
+                if (un.contains(en.first)) { un.remove(en.first); b.push_back(en); }
+            while (un.r.size() > 1) {
+                const auto first = *un.r.begin();
+                un.r.erase(un.r.begin());
+                for (uint64_t id = first.first; id != first.second; ++id) b.push_back({id, MPX_HANDLE(n, 1, ++p->vid)});
+            }
+            for (auto &y : p->initial)
+                if (un.contains(y.first)) { un.remove(y.first); b.push_back({y.first, MPX_HANDLE(n, 0, y.second)}); }
+            for (uint64_t v : p->newly) {
+                const uint64_t iid = un.next();
+                p->initial[iid] = v;
+                b.push_back({iid, MPX_HANDLE(n, 0, v)});
+            }
+            p->newly.clear();
+            p->unproposed = un;
+            p->preparing = false;
+            std::sort(b.begin(), b.end());
+            app<uint64_t>(st.body, x.seq);
+            app<uint64_t>(st.body, b.size());
+            for (auto &y : b) { app<uint64_t>(st.body, y.first); app<uint64_t>(st.body, y.second); }
+            ++st.count;
+        } else if (t == MPX_MSG_COMMIT) {                  // LEARN: Learner::OnLearn (:1029-1060)
+            if (p) {                                       // Proposer::OnLearn (:1383-1470)
+                std::set<uint64_t> conflicts;
+                for (auto &en : x.ents) {
+                    const uint64_t iid = en.first, hv = en.second;
+                    if (st.notlearned.contains(iid) && p->unlearned.contains(iid)) p->unlearned.remove(iid);
+                    if (p->unproposed.contains(iid)) p->unproposed.remove(iid);
+                    auto in = p->initial.find(iid);
+                    if (in != p->initial.end()) {
+                        if (MPX_HANDLE_PROPOSER(hv) != n || MPX_HANDLE_VALUE_ID(hv) != in->second) conflicts.insert(in->second);
+                        p->initial.erase(in);
+                    }
+                }
+                if (!p->preparing) { for (uint64_t v : conflicts) p->initial[p->unproposed.next()] = v; }
+                else p->newly.insert(conflicts.begin(), conflicts.end());
+            }
+            for (auto &en : x.ents)
+                if (st.notlearned.contains(en.first)) st.notlearned.remove(en.first);
+        } else if (t == MPX_MSG_E_EPOCH) {
+            const uint64_t ej = x.aux;
+            if (ej >= ep.size()) return MPX_E_DECODE;
+            const mpx_epoch &o = ep[st.ei], &y = ep[ej];
+            const bool was = (o.proposer_mask >> n) & 1, now = (y.proposer_mask >> n) & 1;
+            if (now && !was) p.reset(new MPropNode::P);    // the constructor's StartPrepare
+            if (was && !now) p.reset();
+            if (p && y.acceptor_mask != o.acceptor_mask) p->preparing = true;   // AcceptorsChanged
+            if (now && (!was || o.acceptor_mask != y.acceptor_mask)) st.idle = true;
+            st.ei = (uint32_t)ej;
+        }
     }
     return MPX_OK;
+}
+
+static void mprop_bytes(const std::vector<MPropNode> &st, std::string &d)
+{
+    d.append("MPXD", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, (uint32_t)st.size());
+    for (auto &x : st) { app<uint64_t>(d, x.count); d += x.body; }
+}
+
+static int member_sim(const PEvents &ev, const std::vector<mpx_epoch> &ep, std::string &d)
+{
+    std::vector<MPropNode> st(ev.size());
+    for (uint32_t n = 0; n < ev.size(); ++n) TRY(mprop_advance(st[n], n, ev[n], ep));
+    mprop_bytes(st, d);
+    return MPX_OK;
+}
+
+static int member_decisions(mpx_engine *e, const Results &r, std::string &d)
+{
+    PEvents ev;
+    TRY(member_events(e, r, ev));
+    return member_sim(ev, e->epochs, d);
 }
 
 // ------------------------------------------------- phase-2 decisions (f2) --
@@ -1760,9 +1868,10 @@ extern "C" int mpx_read_decisions(mpx_engine *e, uint8_t **out, uint64_t *size)
     if (!e || !out || !size) return MPX_E_INVAL;
     if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (e->incremental) {                               // windows keep no history of runs, but
-        if (!e->prop || e->cfg.shard_begin != 0) return MPX_E_STATE;   // MPX_FLAG_DECISIONS carries the
-        std::string d;                                  // bookkeeping: every window's quorums so far
-        prop_bytes(*e->prop, d);
+        if ((!e->prop && !e->mprop) || e->cfg.shard_begin != 0) return MPX_E_STATE;   // MPX_FLAG_DECISIONS
+        std::string d;                                  // carries the bookkeeping: every window's quorums so far
+        if (e->mprop) mprop_bytes(*e->mprop, d);
+        else prop_bytes(*e->prop, d);
         return put_bytes(d, out, size);
     }
     if (e->cfg.shard_begin != 0) return MPX_E_STATE;
@@ -2092,21 +2201,42 @@ struct LearnPlan {
     std::vector<uint64_t> ev_a, ev_m;
 };
 
-static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnPlan> &out)
+// one node's walk state (carried across windows under MPX_FLAG_DECISIONS); `live` indexes
+// the incarnation's open learns in the plan list
+struct LearnNode {
+    bool started = false, prop = false, preparing = false, learned_any = false, idle = false;
+    uint32_t ei = 0;
+    uint64_t lid = 0, amask = 0, K = 0;                        // K: the last non-marker record
+    std::vector<size_t> live;
+};
+struct LearnCarry {
+    std::vector<LearnNode> nodes;
+    std::vector<LearnPlan> plans;
+};
+static LearnCarry *learn_new(uint32_t nodes) { LearnCarry *c = new LearnCarry; c->nodes.resize(nodes); return c; }
+static void learn_free(LearnCarry *c) { delete c; }
+
+static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnNode> &nodes, std::vector<LearnPlan> &out)
 {
     const HostTrace &h = e->ht;
     const uint32_t N = e->cfg.num_nodes;
     const auto &ep = e->epochs;
     std::unordered_map<uint32_t, uint64_t> chosen_at;          // accept quorum message -> accept id
+    const bool aid = h.b_aid.size() == h.b_msg.size();         // (a window's earlier batches: carried ids)
     for (size_t j = 0; j < h.b_msg.size(); ++j)
-        if (r.b_chosen[j] != NONE32 && h.b_msg[j] != NONE32) chosen_at[r.b_chosen[j]] = h.m_aux[h.b_msg[j]];
+        if (r.b_chosen[j] != NONE32 && (aid || h.b_msg[j] != NONE32))
+            chosen_at[r.b_chosen[j]] = aid ? h.b_aid[j] : h.m_aux[h.b_msg[j]];
     for (uint32_t n = 0; n < N; ++n) {
-        uint32_t ei = 0;
-        bool prop = (ep[0].proposer_mask >> n) & 1, preparing = false, learned_any = false;
-        uint64_t lid = 0, amask = ep[0].acceptor_mask;
-        std::vector<size_t> live;                                  // the incarnation's open learns
-        uint64_t K = 0;                                            // the last non-marker record
-        bool idle = false;
+        LearnNode &st = nodes[n];
+        if (!st.started) {
+            st.started = true;
+            st.prop = (ep[0].proposer_mask >> n) & 1;
+            st.amask = ep[0].acceptor_mask;
+        }
+        uint32_t &ei = st.ei;
+        bool &prop = st.prop, &preparing = st.preparing, &learned_any = st.learned_any, &idle = st.idle;
+        uint64_t &lid = st.lid, &amask = st.amask, &K = st.K;
+        std::vector<size_t> &live = st.live;
         auto create = [&](uint64_t at, uint64_t kind, uint64_t src, bool facc) {
             LearnPlan p;
             p.node = n; p.id = ++lid; p.created = at; p.kind = kind; p.src = src; p.facc = facc;
@@ -2131,7 +2261,7 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnPlan> &o
         };
         for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
             const uint8_t t = h.m_type[g];
-            const uint64_t k = seq_of(h, n, g);
+            const uint64_t k = seq_of(h, n, g) + (e->incremental ? e->win_seq_base[n] : 0);
             if (k >= NONE32) return MPX_E_RANGE;
             if (t != MPX_MSG_E_EPOCH) {
                 K = k;
@@ -2188,16 +2318,23 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnPlan> &o
     return MPX_OK;
 }
 
+static int learn_window(mpx_engine *e, const Results &r) { return learn_plan(e, r, e->lrn->nodes, e->lrn->plans); }
+
 extern "C" int mpx_read_learns(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
     if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (e->cfg.semantics != MPX_SEM_MEMBER || !e->whole) return MPX_E_STATE;
-    if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
-    Results r;
-    TRY(fetch_results(e, r));
-    std::vector<LearnPlan> lp;
-    TRY(learn_plan(e, r, lp));
+    std::vector<LearnPlan> whole_lp;
+    if (e->incremental) {                               // windows keep no history of runs, but
+        if (!e->lrn) return MPX_E_STATE;                // MPX_FLAG_DECISIONS carries the walk
+    } else {
+        Results r;
+        TRY(fetch_results(e, r));
+        std::vector<LearnNode> nodes(e->cfg.num_nodes);
+        TRY(learn_plan(e, r, nodes, whole_lp));
+    }
+    const std::vector<LearnPlan> &lp = e->incremental ? e->lrn->plans : whole_lp;
     const uint32_t L = (uint32_t)lp.size();
     std::vector<uint32_t> applied, retired, ended;
     std::vector<uint64_t> mask;
@@ -2540,7 +2677,21 @@ extern "C" int mpx_comm_init(mpx_engine *e, const uint8_t uid[MPX_UID_BYTES], in
     if (ncclCommInitRank(&e->comm, nranks, id, rank) != ncclSuccess) return MPX_E_COMM;
     e->rank = rank;
     e->nranks = nranks;
-    TRY(e->gather_buf.alloc(64ull * 8 * nranks));
+    TRY(e->gather_buf.alloc(2 * 64ull * 8 * nranks));
+    HTRY(hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+        HTRY(hipEventCreateWithFlags(&e->sum_ev[k], hipEventDisableTiming));
+        HTRY(hipEventCreateWithFlags(&e->ag_ev[k], hipEventDisableTiming));
+    }
+    return MPX_OK;
+}
+
+// RCCL calls on the engine stream come after every summary all-gather already issued (one
+// order of collectives on every rank)
+static int comm_fence(mpx_engine *e)
+{
+    for (int k = 0; k < 2; ++k)
+        if (e->ag_pending[k]) HTRY(hipStreamWaitEvent(e->stream, e->ag_ev[k], 0));
     return MPX_OK;
 }
 
@@ -2551,9 +2702,11 @@ extern "C" int mpx_allgather_summary(mpx_engine *e, uint64_t *out)
     HTRY(hipSetDevice(e->device));
     if (e->comm) {
         // gathered by the last queued run/step
-        HTRY(hipMemcpyAsync(out, e->gather_buf.p, 64ull * 8 * e->nranks, hipMemcpyDeviceToHost, e->stream));
+        TRY(comm_fence(e));
+        HTRY(hipMemcpyAsync(out, e->gather_buf.as<uint64_t>() + 64ull * e->nranks * e->sum_idx, 64ull * 8 * e->nranks,
+                            hipMemcpyDeviceToHost, e->stream));
     } else {
-        HTRY(hipMemcpyAsync(out, e->summary.p, 64 * 8, hipMemcpyDeviceToHost, e->stream));
+        HTRY(hipMemcpyAsync(out, e->summary.as<uint64_t>() + 64 * e->sum_idx, 64 * 8, hipMemcpyDeviceToHost, e->stream));
     }
     HTRY(hipStreamSynchronize(e->stream));
     return MPX_OK;
@@ -2564,6 +2717,7 @@ extern "C" int mpx_comm_allreduce_max(mpx_engine *e, uint64_t *vals, uint64_t n)
     if (!e || (n && !vals)) return MPX_E_INVAL;
     if (!e->comm || e->nranks <= 1 || !n) return MPX_OK;
     HTRY(hipSetDevice(e->device));
+    TRY(comm_fence(e));
     TRY(e->comm_buf.alloc(8 * n));
     HTRY(hipMemcpyAsync(e->comm_buf.p, vals, 8 * n, hipMemcpyHostToDevice, e->stream));
     if (ncclAllReduce(e->comm_buf.p, e->comm_buf.p, n, ncclUint64, ncclMax, e->comm, e->stream) != ncclSuccess)
@@ -2585,6 +2739,7 @@ extern "C" int mpx_comm_allgather_bytes(mpx_engine *e, const uint8_t *mine, uint
         return MPX_OK;
     }
     HTRY(hipSetDevice(e->device));
+    TRY(comm_fence(e));
     // the lengths, then every string padded to the longest (one all-gather each)
     TRY(e->comm_buf.alloc(8ull * (R + 1)));
     uint64_t *dl = e->comm_buf.as<uint64_t>();
@@ -2619,19 +2774,26 @@ extern "C" int mpx_comm_allgather_bytes(mpx_engine *e, const uint8_t *mine, uint
 extern "C" int mpx_proposal_part(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
-    if (e->incremental || e->cfg.semantics != MPX_SEM_MULTI || e->device_trace) return MPX_E_STATE;
+    if (e->incremental || e->device_trace) return MPX_E_STATE;
+    const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
     Results r;
     TRY(fetch_results(e, r));
     PEvents ev;
-    proposer_events(e, r, ev);
+    if (member) TRY(member_events(e, r, ev));
+    else proposer_events(e, r, ev);
     std::string d;
     d.append("MPXE", 4);
-    app<uint32_t>(d, 1); app<uint32_t>(d, e->cfg.num_nodes);
+    app<uint32_t>(d, member ? 2 : 1); app<uint32_t>(d, e->cfg.num_nodes);
     app<uint64_t>(d, e->cfg.shard_begin); app<uint64_t>(d, e->cfg.shard_end);
+    if (member) {                                       // the epoch table the walk reads
+        app<uint32_t>(d, (uint32_t)e->epochs.size());
+        for (auto &x : e->epochs) { app<uint64_t>(d, x.acceptor_mask); app<uint64_t>(d, x.proposer_mask); }
+    }
     for (auto &l : ev) {
         app<uint64_t>(d, l.size());
         for (auto &x : l) {
             app<uint64_t>(d, x.seq); app<uint32_t>(d, x.type); app<uint32_t>(d, (uint32_t)x.ents.size());
+            if (member) app<uint64_t>(d, x.aux);
             for (auto &en : x.ents) { app<uint64_t>(d, en.first); app<uint64_t>(d, en.second); }
         }
     }
@@ -2642,28 +2804,49 @@ extern "C" int mpx_proposal_combine(const uint8_t *const *parts, const uint64_t 
                                     uint8_t **out, uint64_t *size)
 {
     if (!parts || !sizes || !nparts || !out || !size) return MPX_E_INVAL;
-    uint32_t N = 0;
+    uint32_t N = 0, ver = 0;
     uint64_t prev_end = 0;
     std::vector<PEvents> ps(nparts);
+    std::vector<mpx_epoch> ep;
     for (uint32_t i = 0; i < nparts; ++i) {
         const uint8_t *p = parts[i];
         const uint64_t n = sizes[i];
-        if (!p || n < 28 || std::memcmp(p, "MPXE", 4) || rd32(p + 4) != 1) return MPX_E_INVAL;
-        const uint32_t Ni = rd32(p + 8);
+        if (!p || n < 28 || std::memcmp(p, "MPXE", 4)) return MPX_E_INVAL;
+        const uint32_t vi = rd32(p + 4), Ni = rd32(p + 8);       // 1 multi, 2 member
         const uint64_t sb = rd64(p + 12), se = rd64(p + 20);
+        if ((vi != 1 && vi != 2) || (i && vi != ver)) return MPX_E_INVAL;
         if (!Ni || Ni > MPX_MAX_NODES || (i && Ni != N) || sb != prev_end || se < sb) return MPX_E_INVAL;   // shard order
         N = Ni;
+        ver = vi;
         prev_end = se;
         uint64_t pos = 28;
+        if (ver == 2) {                                  // member: the epoch table, equal on every part
+            if (pos + 4 > n) return MPX_E_INVAL;
+            const uint32_t E = rd32(p + pos);
+            pos += 4;
+            if (!E || E > (n - pos) / 16) return MPX_E_INVAL;
+            std::vector<mpx_epoch> epi(E);
+            for (uint32_t k = 0; k < E; ++k, pos += 16) {
+                epi[k].acceptor_mask = rd64(p + pos);
+                epi[k].proposer_mask = rd64(p + pos + 8);
+            }
+            if (i && (epi.size() != ep.size() ||
+                      !std::equal(epi.begin(), epi.end(), ep.begin(), [](const mpx_epoch &a, const mpx_epoch &b) {
+                          return a.acceptor_mask == b.acceptor_mask && a.proposer_mask == b.proposer_mask; })))
+                return MPX_E_INVAL;
+            ep.swap(epi);
+        }
+        const uint64_t hdr = ver == 2 ? 24 : 16;
         ps[i].assign(N, {});
         for (uint32_t k = 0; k < N; ++k) {
             if (pos + 8 > n) return MPX_E_INVAL;
             const uint64_t c = rd64(p + pos); pos += 8;
             for (uint64_t j = 0; j < c; ++j) {
-                if (pos + 16 > n) return MPX_E_INVAL;
+                if (pos + hdr > n) return MPX_E_INVAL;
                 PEv x{rd64(p + pos), rd32(p + pos + 8), {}};
                 const uint32_t m = rd32(p + pos + 12);
-                pos += 16;
+                if (ver == 2) x.aux = rd64(p + pos + 16);
+                pos += hdr;
                 if (m > (n - pos) / 16) return MPX_E_INVAL;
                 for (uint32_t q = 0; q < m; ++q, pos += 16) {
                     const uint64_t iid = rd64(p + pos);
@@ -2683,13 +2866,14 @@ extern "C" int mpx_proposal_combine(const uint8_t *const *parts, const uint64_t 
             for (auto &x : ps[i][k]) {
                 auto it = m.find(x.seq);
                 if (it == m.end()) { m.emplace(x.seq, x); continue; }
-                if (it->second.type != x.type) return MPX_E_INVAL;
+                if (it->second.type != x.type || it->second.aux != x.aux) return MPX_E_INVAL;
                 it->second.ents.insert(it->second.ents.end(), x.ents.begin(), x.ents.end());
             }
         for (auto &y : m) all[k].push_back(std::move(y.second));
     }
     std::string d;
-    proposer_sim(all, d);
+    if (ver == 2) TRY(member_sim(all, ep, d));
+    else proposer_sim(all, d);
     return put_bytes(d, out, size);
 }
 
@@ -2698,9 +2882,9 @@ extern "C" int mpx_read_decisions_sharded(mpx_engine *e, uint8_t **out, uint64_t
     if (!e || !out || !size) return MPX_E_INVAL;
     const int R = e->comm ? e->nranks : 1;
     if (R <= 1 && e->cfg.shard_begin == 0) return mpx_read_decisions(e, out, size);
-    if (e->cfg.semantics == MPX_SEM_MULTI && has_proposals(e->ht)) {
-        // client values: the proposer's walk over every shard's events (P_PROPOSE is a header:
-        // every rank sees it, so every rank takes this branch)
+    if (e->cfg.semantics == MPX_SEM_MEMBER || has_proposals(e->ht)) {
+        // client values (or member semantics): the proposer's walk over every shard's events
+        // (P_PROPOSE is a header: every rank sees it, so every rank takes this branch)
         uint8_t *part = nullptr;
         uint64_t plen = 0;
         TRY(mpx_proposal_part(e, &part, &plen));

@@ -612,7 +612,7 @@ int gen_member(const mpx_gen_params &p, std::string &out)
     uint32_t rival_k = 0;
     for (uint32_t e = 0; e < g.E; ++e) {
         if (!lead_round()) return MPX_E_INVAL;
-        const uint64_t end = e + 1 < g.E ? target[e + 1] - 1 : Meff;   // the membership Value's instance
+        const uint64_t end = e + 1 < g.E ? target[e + 1] - 1 : g.M;     // the membership Value's instance
         const uint64_t mid = (target[e] + end) / 2;
         bool contended = false, changed = false;
         while (!changed) {
@@ -659,7 +659,7 @@ int gen_member(const mpx_gen_params &p, std::string &out)
             changed = true;
             // batches the leader created after the membership Value and before its own LEARN
             // applied it: in flight across the change (AcceptorsChanged clears them, :1322)
-            const uint64_t lim = e + 2 < g.E ? target[e + 2] - 1 : Meff;
+            const uint64_t lim = e + 2 < g.E ? target[e + 2] - 1 : g.M;
             std::vector<Delivery> fly;
             const size_t extra = g.rng.below(3);
             for (size_t x = 0; x < extra; ++x) {

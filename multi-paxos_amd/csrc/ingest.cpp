@@ -788,6 +788,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             const uint32_t j = (uint32_t)ht.b_msg.size();
             gid_local.emplace(gid, j);
             ht.b_msg.push_back(NONE32); ht.b_pstart.push_back(NONE32); ht.b_gid.push_back(gid);
+            ht.b_aid.push_back(wc->b_aid[gid]);
             ht.b_node.push_back(n);
             reps.emplace_back();
             b_bal_w.push_back(wc->b_bal[gid]);
@@ -914,6 +915,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
                     b_ent_w.push_back({ent, ns.cnt[k]});
                 }
                 ht.b_msg.push_back(g);
+                ht.b_aid.push_back(ns.aux[k]);
                 ht.b_pstart.push_back(pstart);
                 reps.emplace_back();
             }
@@ -1151,7 +1153,10 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         for (uint32_t gid : ents_gone) wc->b_ents.erase(gid);
         for (auto &x : ents_new) wc->b_ents[x.first] = std::move(x.second);
         for (size_t j = 0; j < ht.b_msg.size(); ++j)
-            if (ht.b_msg[j] != NONE32) wc->b_bal.push_back(b_bal_w[j]);   // new batches, in id order
+            if (ht.b_msg[j] != NONE32) {                    // new batches, in id order
+                wc->b_bal.push_back(b_bal_w[j]);
+                wc->b_aid.push_back(ht.b_aid[j]);
+            }
         wc->batches = gid_next;
         for (auto &x : state_new) wc->state_b[x.first][x.second] = 1;
     }

@@ -67,6 +67,7 @@ struct WindowCarry {
     std::vector<std::vector<uint64_t>> round_b;                  // per node: buckets with promise-reply runs since
                                                                  //   its last P_START
     std::vector<uint64_t> b_bal;                                 // per global batch: its round's ballot
+    std::vector<uint64_t> b_aid;                                 // per global batch: its accept id (P_BATCH aux)
     std::vector<uint32_t> markers;                               // member, per node: E_EPOCH markers so far
     // per global batch still live and not chosen: its entries {iid, handle}, for the
     // chosen log when a later window completes its votes
@@ -75,7 +76,7 @@ struct WindowCarry {
     {
         on = true; batches = 0;
         live.assign(N, {}); round_ballot.assign(N, 0); state_b.assign(N, std::vector<uint8_t>(NB, 0));
-        maxb.assign(N, -1); round_b.assign(N, {}); b_bal.clear(); b_ents.clear(); markers.assign(N, 0);
+        maxb.assign(N, -1); round_b.assign(N, {}); b_bal.clear(); b_aid.clear(); b_ents.clear(); markers.assign(N, 0);
     }
 };
 
@@ -116,6 +117,7 @@ struct HostTrace {
     std::vector<uint8_t> pair_gp;                   // per pair: 1 when not lean (mpx_internal.hpp plan_shape_ok)
     std::vector<uint32_t> b_msg, b_pstart, b_rep, b_rsrc;
     std::vector<uint64_t> b_rbal, b_bal;
+    std::vector<uint64_t> b_aid;                    // per batch: its accept id (the P_BATCH's, or carried)
     std::vector<uint64_t> b_rep_off;
     std::vector<uint64_t> cf_off;
     std::vector<Frag> cfrags;

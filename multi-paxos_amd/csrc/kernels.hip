@@ -910,6 +910,62 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
     }
 }
 
+// Snapshot records of one PREPARE of a pair (FilterAcceptedValues, multi/paxos.cpp:902-922):
+// the hit slots in slot order, grouped into segments fixed by one dense fragment — one
+// OUT_RUN record per segment, which the host expands slot by slot (engine.cpp
+// fetch_results) — and one record per slot a sparse fragment fixed.  A promise reply's
+// values mostly come from a few whole runs, so this writes a few records per pair and
+// PREPARE instead of one per slot.
+__device__ inline void emit_snap(const DevView &v, const bool (&hit)[SPL_], uint32_t msg, const uint32_t (&ref)[SPL_],
+                                 const bool (&dense)[SPL_])
+{
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t key[SPL_];                      // segment key: fixing fragment + 1 (dense), 0: a record of its own
+    uint64_t sm[SPL_], em[SPL_];
+#pragma unroll
+    for (uint32_t j = 0; j < SPL_; ++j) key[j] = hit[j] && dense[j] ? ref[j] + 1 : 0;
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SPL_; ++j) {
+        // the previous slot (lane - 1, or lane 63 of row j - 1) and the next one
+        uint32_t pk = __shfl_up(key[j], 1, 64), nk = __shfl_down(key[j], 1, 64);
+        const uint32_t pk_row = j ? __shfl(key[j ? j - 1 : 0], 63, 64) : 0;
+        const uint32_t nk_row = j + 1 < SPL_ ? __shfl(key[j + 1 < SPL_ ? j + 1 : j], 0, 64) : 0;
+        if (lane == 0) pk = pk_row;
+        if (lane == 63) nk = nk_row;
+        sm[j] = __ballot(hit[j] && (key[j] == 0 || pk != key[j]));
+        em[j] = __ballot(hit[j] && (key[j] == 0 || nk != key[j]));
+        tot += (uint32_t)__popcll(sm[j]);
+    }
+    if (!tot) return;
+    const uint32_t sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (v.out_subs - 1);
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&v.out_cursor[OUT_STRIDE * sub], (unsigned long long)tot);
+    base = __shfl(base, 0, 64);
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t off = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SPL_; ++j) {
+        if ((sm[j] >> lane) & 1) {
+            const uint64_t at = base + off + (uint64_t)__popcll(sm[j] & below);
+            uint32_t e = 0;                      // the segment's last slot: the first end at or after it
+#pragma unroll
+            for (uint32_t j2 = SPL_; j2-- > j;) {
+                const uint64_t m = j2 == j ? em[j2] & ~below : em[j2];
+                if (m) e = 64 * j2 + (uint32_t)__builtin_ctzll(m);
+            }
+            const uint32_t s0 = lane + 64 * j;
+            if (at < v.out_cap) {
+                OutRec r;
+                r.msg = msg; r.ref = ref[j];
+                r.aux = key[j] ? OUT_RUN | s0 | ((e - s0 + 1) << OUT_RUN_SHIFT) : s0;
+                v.out[(uint64_t)sub * v.out_cap + at] = r;
+            }
+        }
+        off += (uint32_t)__popcll(sm[j]);
+    }
+}
+
 constexpr uint32_t SPL = BS / 64;
 static_assert(SPL == SPL_, "4 slots per lane");
 
@@ -2089,7 +2145,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
     constexpr bool member = MEMBER;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
-    constexpr uint32_t S_PRESENT = 1, S_COMMITTED = 2;
+    constexpr uint32_t S_PRESENT = 1, S_COMMITTED = 2, S_DENSE = 4;   // S_DENSE: fixed by a dense fragment
 
     // work list: the pairs the lean kernel does not take (ingest.cpp), GP_WORDS
     // per item.  Three-stage software pipeline over this wave's items, issued at
@@ -2202,6 +2258,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                     const uint64_t ballot = DIGEST ? rl64(fbal, a) : 0;
                     const bool dense = fl & FR_DENSE;
                     const uint32_t fq = (uint32_t)(fi + a + 1);
+                    const uint32_t sd = dense ? S_DENSE : 0;
                     int k[SPL];
                     frag_slots(lidx, kind == K_PREPLY ? v.r_slot : v.e_slot, ent, cnt, st0, dense, k);
                     if (member && (kind == K_ACCEPT || kind == K_COMMIT)) {
@@ -2221,10 +2278,10 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                         record_violation(v, MPX_V_LEARN_VALUE, n, seq, v.shard_begin + li0 + lane + 64 * j);
                                 } else if (learn) {
                                     if (DIGEST) sb[j] = v.e_pid[x];
-                                    SF_SET(j, S_PRESENT | S_COMMITTED); se[j] = x; sm[j] = fq;
+                                    SF_SET(j, S_PRESENT | S_COMMITTED | sd); se[j] = x; sm[j] = fq;
                                 } else if (!(SF(j) & S_PRESENT)) {
                                     if (DIGEST) sb[j] = v.e_pid[x];
-                                    SF_SET(j, S_PRESENT); se[j] = x; sm[j] = fq;
+                                    SF_SET(j, S_PRESENT | sd); se[j] = x; sm[j] = fq;
                                     ++cA;
                                 }
                                 cL += learn;
@@ -2236,7 +2293,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             for (uint32_t j = 0; j < SPL; ++j)
                                 if (k[j] >= 0 && !(SF(j) & S_COMMITTED)) {           // :1380
                                     if (DIGEST) sb[j] = ballot;                                   // :1387
-                                    SF_SET(j, S_PRESENT); se[j] = (uint32_t)(ent + k[j]); sm[j] = fq;
+                                    SF_SET(j, S_PRESENT | sd); se[j] = (uint32_t)(ent + k[j]); sm[j] = fq;
                                     ++cA;
                                 }
                         }
@@ -2251,7 +2308,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                                          v.shard_begin + li0 + lane + 64 * j);
                                 } else {
                                     if (DIGEST) sb[j] = ballot;                                   // :1515
-                                    SF_SET(j, S_PRESENT | S_COMMITTED); se[j] = x; sm[j] = fq;
+                                    SF_SET(j, S_PRESENT | S_COMMITTED | sd); se[j] = x; sm[j] = fq;
                                 }
                                 ++cL;
                             }
@@ -2306,13 +2363,19 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                 }
                             }
                             uint32_t ref[SPL];
+                            bool dn[SPL];
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j) {
                                 hit[j] = hit[j] && li0 + lane + 64 * j < v.shard_len && (SF(j) & S_PRESENT);
                                 ref[j] = sm[j] - 1;                 // the fixing fragment (global)
+                                dn[j] = (SF(j) & S_DENSE) != 0;
                                 cP += hit[j];
                             }
-                            emit_rows(v, hit, g, 0, ref);
+#ifdef MPX_SNAP_ROWS
+                            emit_rows(v, hit, g, 0, ref);                 // (A/B build: one record per slot)
+#else
+                            emit_snap(v, hit, g, ref, dn);
+#endif
                         }
                     } else if (!ROUNDS) {
                         // AM_SNAP: a pair without promise-reply runs gets no round events; member:

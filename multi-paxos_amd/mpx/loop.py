@@ -169,10 +169,12 @@ class ClosedLoop:
     def commit_chosen(self, node, to):
         """COMMIT every batch of `node` whose instances are all in the engine's chosen log."""
         done = []
+        chosen = None                                 # the chosen log, read once per call
         for (n, aid), (b, ents) in sorted(self.batches.items()):
             if n != node or (n, aid) in self.committed:
                 continue
-            chosen = self.engine.read_chosen(0, self.M)
+            if chosen is None:
+                chosen = self.engine.read_chosen(0, self.M)
             if not all(chosen[iid] >> 63 for iid, _h in ents):
                 continue
             self.committed.add((n, aid))

@@ -158,3 +158,75 @@ def test_proposal_combine_walks_client_values():
         mpx.proposal_combine([a, _mpxe([[(3, 5, [])]], 1, 4, 16)])   # record types disagree
     with pytest.raises(mpx.MpxError):
         mpx.proposal_combine([a[:-4]])                     # truncated
+
+
+MEMBER_DECISIONS = [k for k in DECISIONS if k.startswith(("c5_", "mm_"))]
+
+
+def _member_mpxe(trace, result, cuts):
+    """Member MPXE parts (version 2, include/mpx.h) of a trace cut at instance boundaries:
+    every shard lists each node's Propose / StartPrepare / E_EPOCH records, its quorums and
+    LEARNs with the entries of its own instances — the quorums' merged maps from the oracle's
+    MPXR result (what the device computes)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle"))
+    import mpxr
+    from learns_model import _streams
+    from member_decisions_model import _learn_entries
+    epochs, streams = _streams(trace)
+    res = mpxr.parse(result)
+    bounds = [0] + list(cuts) + [1 << 62]
+    parts = []
+    for s in range(len(bounds) - 1):
+        sb, se = bounds[s], bounds[s + 1]
+        b = bytearray(b"MPXE") + struct.pack("<IIQQ", 2, len(streams), sb, se)
+        b += struct.pack("<I", len(epochs))
+        for _v, am, pm, _lm in epochs:
+            b += struct.pack("<QQ", am, pm)
+        for n, msgs in enumerate(streams):
+            quorums = {q[0]: q[2] for q in res["nodes"][n]["quorums"]}
+            evs = []
+            for k, m in enumerate(msgs):
+                t = struct.unpack_from("<I", m)[0]
+                if t in (16, 19):
+                    evs.append((k, t, 0, []))
+                elif t == 18:
+                    evs.append((k, t, struct.unpack_from("<I", m, 4)[0], []))
+                elif t == 5:
+                    evs.append((k, t, 0, [e for e in _learn_entries(m) if sb <= e[0] < se]))
+                elif t == 1 and k in quorums:
+                    evs.append((k, t, 0, sorted((i, h) for i, _p, h in quorums[k] if sb <= i < se)))
+            b += struct.pack("<Q", len(evs))
+            for k, t, aux, ents in evs:
+                b += struct.pack("<QIIQ", k, t, len(ents), aux)
+                for iid, h in ents:
+                    b += struct.pack("<QQ", iid, h)
+        parts.append(bytes(b))
+    return parts
+
+
+@pytest.mark.parametrize("name", MEMBER_DECISIONS)
+def test_member_proposal_combine_restores_reference_decisions(name):
+    """The engine's member Proposer walk (engine.cpp mprop_advance, host only) over the union
+    of member MPXE parts — whole, and cut into 2 and 3 instance shards — gives the reference's
+    own decisions (fixture: real Proposer::Propose calls, member/paxos.cpp:1122-1297,1383-1470)."""
+    from oracles import oracle_run
+    trace = open(os.path.join(GOLD, name + ".mpxt"), "rb").read()
+    want = open(os.path.join(GOLD, name + ".mpxd"), "rb").read()
+    result = oracle_run(trace)[0]
+    m = struct.unpack_from("<Q", trace, 16)[0]
+    for cuts in ([], [m // 2], [m // 3, 2 * m // 3]):
+        assert mpx.proposal_combine(_member_mpxe(trace, result, [c for c in cuts if c > 0])) == want, cuts
+
+
+def test_member_proposal_combine_rejects_mixed_parts():
+    from oracles import oracle_run
+    trace = open(os.path.join(GOLD, "mm_propose.mpxt"), "rb").read()
+    parts = _member_mpxe(trace, oracle_run(trace)[0], [3])
+    multi = _mpxe([[(0, 19, [])]], 1, 3, 16)
+    with pytest.raises(mpx.MpxError):
+        mpx.proposal_combine([parts[0], multi])                   # member and multi parts
+    bad = bytearray(parts[1])
+    bad[36] ^= 1                                                   # another epoch table
+    with pytest.raises(mpx.MpxError):
+        mpx.proposal_combine([parts[0], bytes(bad)])

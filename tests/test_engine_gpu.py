@@ -327,6 +327,33 @@ def test_engine_matches_oracle_c5_member(seed, u, m, b, drop, dup):
     assert st["chosen"] == m and st["violations"] == 0
 
 
+@pytest.mark.parametrize("seed,u,m,b,drop,dup,props", [(61, 8, 1 << 14, 64, 100, 100, 3), (62, 6, 20000, 200, 300, 300, 2),
+                                                        (63, 5, 9000, 33, 0, 0, 3)])
+def test_engine_matches_oracle_c5_contended(seed, u, m, b, drop, dup, props):
+    """Contended C5 (gen_member proposers > 1): in every epoch from 2 on a rival member proposer
+    prepares above the leader over its own unlearned ids — promise replies carrying most of the
+    history, merged pre-accepted maps (member/paxos.cpp:1158-1182,1614-1629), rejected ACCEPTs
+    and the leader's re-prepare; the engine == the oracle through the run and the step."""
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=u, num_instances=m, seed=seed, batch=b,
+                           drop_rate=drop, dup_rate=dup, max_delay=64, noop_permille=15, proposers=props)
+    want, ostats, _ = oracle_run(t)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        got = e.dump()
+        assert got == want, mpxr.diff(got, want)
+        _step_path(e, want, st)
+    assert [st[k] for k in STATS_ORDER] == ostats
+    assert st["promise_entries"] > m and st["violations"] == 0
+
+
+def test_c5_contended_2_20_matches_oracle():
+    """Contended C5 at 2^20 instances (acceptor universe 8, 3 proposers, 1 % loss / dup):
+    several million promise entries; counters and digests == the CPU oracle's."""
+    st = _full_size_vs_oracle(mpx.GEN_MEMBER, num_nodes=8, num_instances=1 << 20, seed=0, batch=256,
+                              drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15, proposers=3)
+    assert st["promise_entries"] >= 10 ** 6 and st["violations"] == 0
+
+
 @pytest.mark.parametrize("seed,u,m,b,drop,dup", [(41, 8, 1 << 15, 256, 100, 100), (42, 6, 20000, 200, 300, 300),
                                                   (43, 8, 1 << 14, 90, 0, 0), (44, 4, 9000, 33, 500, 500),
                                                   (45, 8, (1 << 15) + 77, 256, 1000, 1000)])
@@ -480,14 +507,14 @@ STATS_ORDER = ("chosen", "promise_entries", "accept_apps", "commit_apps", "viola
                "chosen_digest", "state_digest", "scalar_digest")
 
 
-def _full_size_vs_oracle(kind, **kw):
+def _full_size_vs_oracle(kind, oracle_threads=1, **kw):
     import time
     from oracles import oracle_run_sharded
     t0 = time.time()
     log = lambda m: print("[full-size] %s: %s (%.0f s)" % (kw.get("num_instances"), m, time.time() - t0), flush=True)
     t = mpx.generate_trace(kind, copy=False, **kw)           # the generator's buffer, no bytes copy
     log("generated %.1f GB" % (len(t) / 1e9))
-    want = oracle_run_sharded(t, shards=1, threads=1)       # node-parallel CPU oracle, digests only
+    want = oracle_run_sharded(t, shards=oracle_threads, threads=oracle_threads)   # CPU oracle, digests only
     log("oracle")
     e = mpx.Engine.for_trace(t)
     del t
@@ -514,6 +541,17 @@ def test_c3_full_size_matches_oracle():
     assert st["chosen"] >= 1 << 24 and st["promise_entries"] > 0 and st["violations"] == 0
 
 
+@pytest.mark.timeout(900)
+def test_c5_contended_full_size_matches_oracle():
+    """Contended C5 at its stated size: 2^25 instances, 3 member proposers (a rival round per
+    epoch from epoch 2, member/paxos.cpp:1158-1182,1504-1549,1614-1629); >= 10^6 promise
+    entries; every counter and digest == the CPU oracle's (node-parallel, 8 threads)."""
+    st = _full_size_vs_oracle(mpx.GEN_MEMBER, num_nodes=8, num_instances=1 << 25, seed=0, batch=256,
+                              drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15, proposers=3,
+                              oracle_threads=8)
+    assert st["promise_entries"] >= 10 ** 6 and st["violations"] == 0
+
+
 def test_c5_full_size_matches_oracle():
     """C5 at its stated size: 2^25 instances, member semantics, acceptor universe 8 —
     AddAcceptor(1..7) then DelAcceptor(1..7), 15 epochs (member/main.cpp:119-141), 1 % loss,
@@ -525,6 +563,7 @@ def test_c5_full_size_matches_oracle():
 
 # ---- phase-2 decisions at promise quorums (multi/paxos.cpp:1056-1130) ----
 DECISIONS = json.load(open(os.path.join(GOLD, "decisions.json")))
+LEARNS = json.load(open(os.path.join(GOLD, "learns.json")))
 
 
 @pytest.mark.parametrize("name", sorted(DECISIONS))
@@ -567,6 +606,33 @@ def test_proposal_traces_refuse_sharded_decisions(name):
         assert e.decisions() == want
         with pytest.raises(mpx.MpxError):
             e.decision_bounds()
+
+
+MEMBER_DECISIONS = sorted(k for k in DECISIONS if k.startswith(("c5_", "mm_")))
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+@pytest.mark.parametrize("name", MEMBER_DECISIONS)
+def test_member_sharded_decisions(name, shards):
+    """Member decisions over instance shards (unaligned): each shard's events — Propose,
+    StartPrepare, E_EPOCH, its instances' entries of each LEARN and promise quorum
+    (mpx_proposal_part, MPXE version 2 with the epoch table) — merged by record in shard
+    order, the member Proposer's walk once over the union (mpx_proposal_combine) == the
+    reference's own decisions (fixture, real Proposer::Propose calls)."""
+    from mpx import dist as mdist
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxd")
+    hd = mpx.trace_header(trace)
+    m = max(hd["num_instances"], 1)
+    parts = []
+    for r in range(shards):
+        sb, se = mdist.shard_bounds(m, shards, r, align=1)
+        with mpx.Engine(hd["num_nodes"], sb, se, semantics=hd["semantics"]) as e:
+            e.submit_trace(trace)
+            e.run()
+            with pytest.raises(mpx.MpxError):
+                e.decisions()                         # a member shard alone cannot decide
+            parts.append(e.proposal_part())
+    assert mpx.proposal_combine(parts) == want
 
 
 @pytest.mark.parametrize("shards", [2, 3])
@@ -846,17 +912,22 @@ def _windows(trace, fracs, times=None):
 MULTI_GOLDENS = sorted(k for k in INDEX if not k.startswith(("c5_", "mm_")) and "member" not in k)
 
 
-@pytest.mark.parametrize("name", sorted(k for k in DECISIONS if not k.startswith(("c5_", "mm_"))))
+@pytest.mark.parametrize("name", sorted(set(DECISIONS) | set(LEARNS)))
 def test_incremental_windows_carry_decisions(name):
-    """MPX_FLAG_DECISIONS: every multi golden with a promise quorum (client values included)
-    cut into 2 and 4 windows — the proposers' bookkeeping advanced window by window over the
-    device's quorums and merged maps gives the reference's decisions (fixture); without the
-    flag a window engine keeps no decisions."""
-    want = _read(name, ".mpxd")
-    hd, _epochs, streams = _node_streams(_read(name, ".mpxt"))
+    """MPX_FLAG_DECISIONS: every golden with a promise quorum (client values included; member:
+    also every one with learns) cut into 1, 2 and 4 windows — the proposers' bookkeeping
+    advanced window by window over the device's quorums and merged maps gives the reference's
+    decisions (fixture); member windows also carry the learn bookkeeping (LearningValues,
+    member/paxos.cpp:1345-1381,1472-1549) and give the reference's learns; without the flag a
+    window engine keeps neither."""
+    trace = _read(name, ".mpxt")
+    want = _read(name, ".mpxd") if name in DECISIONS else None
+    want_l = _read(name, ".mpxl") if name in LEARNS else None
+    hd, epochs, streams = _node_streams(trace)
     n, m = hd["num_nodes"], max(hd["num_instances"], 1)
-    for fracs in ((0.5,), (0.2, 0.45, 0.8)):
-        with mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL | mpx.FLAG_DECISIONS) as e:
+    kw = dict(semantics=hd["semantics"], epochs=epochs) if hd["semantics"] == mpx.SEM_MEMBER else {}
+    for fracs in ((), (0.5,), (0.2, 0.45, 0.8)):
+        with mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL | mpx.FLAG_DECISIONS, **kw) as e:
             prev = [0] * n
             for f in list(fracs) + [1.0]:
                 cut = [len(s) if f >= 1.0 else int(len(s) * f) for s in streams]
@@ -865,13 +936,18 @@ def test_incremental_windows_carry_decisions(name):
                         e.submit(node, st[prev[node]:cut[node]])
                 e.run()
                 prev = cut
-            assert e.decisions() == want, fracs
-    with mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL) as e:
+            if want is not None:
+                assert e.decisions() == want, fracs
+            if want_l is not None:
+                assert e.learns() == want_l, fracs
+    with mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL, **kw) as e:
         for node, st in enumerate(streams):
             e.submit(node, st)
         e.run()
         with pytest.raises(mpx.MpxError):
             e.decisions()
+        with pytest.raises(mpx.MpxError):
+            e.learns()
 
 
 @pytest.mark.parametrize("name", sorted(INDEX))
@@ -919,6 +995,48 @@ def test_incremental_windows_member(seed, u, m, b, drop, dup):
     assert got[2] == want[2]
 
 
+@pytest.mark.parametrize("seed,props", [(71, 1), (72, 3)])
+def test_incremental_windows_member_decisions_and_learns_c5(seed, props):
+    """C5-shaped member traces beyond fixture size (contended too) in 7 windows with
+    MPX_FLAG_DECISIONS: decisions and learns == one engine over the whole trace."""
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=8, num_instances=1 << 14, seed=seed, batch=64,
+                           drop_rate=300, dup_rate=300, max_delay=64, noop_permille=15, proposers=props)
+    with mpx.Engine.for_trace(t) as e:
+        e.run()
+        want, want_l = e.decisions(), e.learns()
+    hd, epochs, streams = _node_streams(t)
+    n, m = hd["num_nodes"], hd["num_instances"]
+    with mpx.Engine(n, 0, m, semantics=hd["semantics"], epochs=epochs,
+                    flags=mpx.FLAG_INCREMENTAL | mpx.FLAG_DECISIONS) as e:
+        prev = [0] * n
+        for f in [k / 7 for k in range(1, 7)] + [1.0]:
+            cut = [len(s) if f >= 1.0 else int(len(s) * f) for s in streams]
+            for node, st in enumerate(streams):
+                if cut[node] > prev[node]:
+                    e.submit(node, st[prev[node]:cut[node]])
+            e.run()
+            prev = cut
+        assert e.decisions() == want
+        assert e.learns() == want_l
+
+
+def test_incremental_window_cost_is_per_window_member():
+    """C5 at 2^20 instances (acceptor universe 8, 15 epochs, loss / dup) in 16 equal windows:
+    each window's host + device time stays within 2x of the second window's as the history
+    grows — O(window), not O(history) — and the windows together give the whole run's digests."""
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_instances=1 << 20, copy=False, num_nodes=8, seed=0, batch=256,
+                           drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        want = (st["state_digest"], st["chosen_digest"])
+        want_c = {k: st[k] for k in COUNTERS}
+    times = []
+    _sends, tot, obs = _windows(bytes(t), [k / 16 for k in range(1, 16)], times)
+    assert obs["digests"] == want and tot == want_c
+    print("window times (s):", ["%.3f" % x for x in times])
+    assert max(times[2:]) <= 2.0 * times[1], times
+
+
 def test_incremental_window_range_error_keeps_state():
     """A window the engine cannot encode (MPX_E_RANGE: a member node past 254 E_EPOCH markers,
     the device incarnation counter) is refused before it touches the carry: the state read back
@@ -962,7 +1080,6 @@ def test_incremental_window_cost_is_per_window():
 
 # ---- commit reliability (multi/paxos.cpp:1184-1197,1416-1421,1625-1641) ----
 COMMITS = json.load(open(os.path.join(GOLD, "commits.json")))
-LEARNS = json.load(open(os.path.join(GOLD, "learns.json")))
 
 
 # ---- member learn reliability (member/paxos.cpp:1345-1381,1472-1549) ----

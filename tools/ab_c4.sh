@@ -4,7 +4,7 @@ mkdir -p gpurun_out/ab_c4
 for rep in 1 2; do
   for v in default "$@"; do
     if [ $v = default ]; then unset MPX_LIB_VARIANT; else export MPX_LIB_VARIANT=$v; fi
-    timeout -k 10 200 python bench.py --no-cpu-baseline --c3-instances 0 --c5-instances 0 > gpurun_out/ab_c4/${v}_$rep.json 2> gpurun_out/ab_c4/${v}_$rep.err || exit 1
+    timeout -k 10 200 python bench.py --no-cpu-baseline --c3-instances 0 --c5-instances 0 --c5c-instances 0 > gpurun_out/ab_c4/${v}_$rep.json 2> gpurun_out/ab_c4/${v}_$rep.err || exit 1
   done
 done
 unset MPX_LIB_VARIANT

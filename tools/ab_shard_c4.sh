@@ -11,7 +11,7 @@ for rep in 1 2 3; do
   for v in default "$@"; do
     if [ $v = default ]; then unset MPX_LIB_VARIANT; else export MPX_LIB_VARIANT=$v; fi
     timeout -k 10 120 python bench.py --shard-only > $out/shard_${v}_$rep.json 2> $out/shard_${v}_$rep.err || { tail -5 $out/shard_${v}_$rep.err; exit 1; }
-    timeout -k 10 200 python bench.py --no-cpu-baseline --c3-instances 0 --c5-instances 0 --shard-of 0 > $out/c4_${v}_$rep.json 2> $out/c4_${v}_$rep.err || { tail -5 $out/c4_${v}_$rep.err; exit 2; }
+    timeout -k 10 200 python bench.py --no-cpu-baseline --c3-instances 0 --c5-instances 0 --c5c-instances 0 --shard-of 0 > $out/c4_${v}_$rep.json 2> $out/c4_${v}_$rep.err || { tail -5 $out/c4_${v}_$rep.err; exit 2; }
   done
 done
 unset MPX_LIB_VARIANT

@@ -14,6 +14,7 @@ profiles/, where bench.py picks them up as roofline.traffic.
     python tools/pmc_traffic.py --tag r02_c3 --c3 --sq     (C3 general path, + SQ wave-state pass)
     python tools/pmc_traffic.py --tag r02_c5 --c5          (C5 member path)
     python tools/pmc_traffic.py --tag r04_c3w --c3w        (C3 as 16 incremental windows: k_apply_win)
+    python tools/pmc_traffic.py --tag r04_c5c --c5c        (contended C5: 3 member proposers)
 """
 import argparse
 import csv
@@ -62,6 +63,7 @@ def main():
     ap.add_argument("--c3", action="store_true", help="the C3 general-path leg (bench.py --c3-only)")
     ap.add_argument("--c5", action="store_true", help="the C5 member leg (bench.py --c5-only)")
     ap.add_argument("--c3w", action="store_true", help="the C3 windows leg (bench.py --c3-windows-only)")
+    ap.add_argument("--c5c", action="store_true", help="the contended C5 leg (bench.py --c5c-only)")
     ap.add_argument("--sq", action="store_true", help="also one pass of SQ wave-state counters")
     a, rest = ap.parse_known_args()
     # the workload's true size, recorded with the profile (bench.py matches it exactly)
@@ -71,17 +73,21 @@ def main():
     elif a.c5:
         a.instances, a.nodes = 1 << 25, 8
         bench_args = ["--c5-only", "--c5-steps", "3", "--c5-instances", str(a.instances)] + rest
+    elif a.c5c:
+        a.instances, a.nodes = 1 << 25, 8
+        bench_args = ["--c5c-only", "--c5-steps", "3", "--c5c-instances", str(a.instances)] + rest
     elif a.c3:
         a.instances, a.nodes = 1 << 24, 7
         bench_args = ["--c3-only", "--c3-steps", "3", "--c3-instances", str(a.instances)] + rest
     else:
         bench_args = ["--steps", "3", "--warmup", "0", "--instances", str(a.instances), "--nodes", str(a.nodes),
-                      "--c3-instances", "0", "--c5-instances", "0", "--shard-of", "0"] + rest
+                      "--c3-instances", "0", "--c5-instances", "0", "--c5c-instances", "0", "--shard-of", "0"] + rest
     fetch = run_pass(["FETCH_SIZE"], a.outdir, bench_args, a.tag)["FETCH_SIZE"]
     write = run_pass(["WRITE_SIZE"], a.outdir, bench_args, a.tag)["WRITE_SIZE"]
     sq = run_pass(SQ_COUNTERS, a.outdir, bench_args, a.tag) if a.sq else {}
     out = {"tag": a.tag, "workload": "C3W 2^%d x 7 in 16 windows (bench.py --c3-windows-only)" % (a.instances.bit_length() - 1)
            if a.c3w else "C5 2^%d member (bench.py --c5-only)" % (a.instances.bit_length() - 1) if a.c5 else
+           "C5C 2^%d member, 3 proposers (bench.py --c5c-only)" % (a.instances.bit_length() - 1) if a.c5c else
            "C3 2^%d x 7 (bench.py --c3-only)" % (a.instances.bit_length() - 1) if a.c3 else "C4",
            "instances": a.instances, "nodes": a.nodes, "gpus": 1, "source_digest": mpx.source_digest(),
            "kernels": {}}
@@ -103,7 +109,7 @@ def main():
     else:
         phase = [v for k, v in out["kernels"].items()
                  if "k_plan" in k or "k_store" in k
-                 or ((a.c3 or a.c5) and re.search(r"k_apply<\d+, false", k))]   # k_apply<waves, DIGEST, ...>: not the digested run's
+                 or ((a.c3 or a.c5 or a.c5c) and re.search(r"k_apply<\d+, false", k))]   # k_apply<waves, DIGEST, ...>: not the digested run's
     out["apply_phase_kernels"] = [k for k, v in out["kernels"].items() if v in phase]
     out["hbm_bytes_per_launch"] = sum(v["hbm_bytes_per_launch"] for v in phase) if phase else None
     out["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"
