@@ -123,6 +123,8 @@ struct mpx_engine {
     // launch's kernels: summaries and gather buffers alternate between two slots, and a launch
     // waits only for the all-gather that last read its slot (two launches back)
     hipStream_t comm_stream = nullptr;
+    hipStream_t stream2 = nullptr;                  // a run's promise-round pairs beside its plan path
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     hipEvent_t sum_ev[2] = {nullptr, nullptr}, ag_ev[2] = {nullptr, nullptr};
     bool ag_pending[2] = {false, false};
     uint32_t sum_idx = 0;
@@ -245,6 +247,10 @@ extern "C" int mpx_destroy(mpx_engine *e)
         if (e->ag_ev[k]) (void)hipEventDestroy(e->ag_ev[k]);
     }
     if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
+    if (e->stream2) (void)hipStreamSynchronize(e->stream2);
+    if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
+    if (e->join_ev) (void)hipEventDestroy(e->join_ev);
+    if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     prop_free(e->prop);
     mprop_free(e->mprop);
@@ -415,6 +421,7 @@ static int finish_view(mpx_engine *e)
     v.quorum = N / 2 + 1;                          // nodes_.size() / 2 + 1, paxos.cpp:1047,1416
     v.NB = e->NB;
     v.scan_node_pass = 0;
+    v.scan_chunk = e->ht.scan_chunk;
     for (size_t n = 0; n + 1 < e->ht.node_chunk_off.size(); ++n)
         if (e->ht.node_chunk_off[n + 1] - e->ht.node_chunk_off[n] > SCAN_INLINE_CHUNKS) v.scan_node_pass = 1;
     if (const char *x = std::getenv("MPX_SCAN_NODE_PASS")) v.scan_node_pass = std::atoi(x) ? 1 : 0;
@@ -746,7 +753,14 @@ static int queue_run(mpx_engine *e, bool digest)
     void *evp[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     if (ev) for (int k = 0; k < 5; ++k) evp[k] = ev->e[k];
     if (ev) ev->store_last = run_ends_with_store(e->view);
-    int rc = launch_run(e->view, e->stream, g, evp);
+    if (!e->stream2) {
+        HTRY(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+        HTRY(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
+        HTRY(hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming));
+    }
+    LaunchSide side{nullptr, nullptr, nullptr};
+    if (!std::getenv("MPX_ONE_STREAM")) side = LaunchSide{e->stream2, e->fork_ev, e->join_ev};
+    int rc = launch_run(e->view, e->stream, g, evp, side);
     if (rc) return MPX_E_HIP;
     if (e->incremental) {                              // the next window starts from this one's scalars, rounds, roles
         HTRY(hipMemcpyAsync(e->scal_base.p, e->scal_key.p, 16ull * e->cfg.num_nodes, hipMemcpyDeviceToDevice, e->stream));
@@ -2526,13 +2540,14 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     for (uint32_t n = 0; n <= N; ++n) h.node_off[n] = n == 0 ? 0 : G0 + (uint64_t)(n - 1) * G1;
     // header-scan stream: per node its PREPARE and K ACCEPTs (gen_device.hip k_gen_scan)
     h.node_chunk_off.assign(N + 1, 0);
+    h.scan_chunk = scan_chunk_for((uint64_t)N * (K + 1));
     for (uint32_t n = 0; n < N; ++n) {
         h.node_chunk_off[n] = (uint32_t)h.chunk_node.size();
         const uint64_t a = (uint64_t)n * (K + 1), b = a + K + 1;
-        for (uint64_t g = a; g < b; g += SCAN_CHUNK) {
+        for (uint64_t g = a; g < b; g += h.scan_chunk) {
             h.chunk_node.push_back(n);
             h.chunk_beg.push_back(g);
-            h.chunk_end.push_back(std::min<uint64_t>(g + SCAN_CHUNK, b));
+            h.chunk_end.push_back(std::min<uint64_t>(g + h.scan_chunk, b));
         }
     }
     h.node_chunk_off[N] = (uint32_t)h.chunk_node.size();

@@ -1131,12 +1131,13 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     ht.pl_msg = std::move(pl);
     // header-scan chunks, over each node's scan stream
     ht.node_chunk_off.assign(N + 1, 0);
+    ht.scan_chunk = scan_chunk_for(sc_off[N]);
     for (uint32_t n = 0; n < N; ++n) {
         ht.node_chunk_off[n] = (uint32_t)ht.chunk_node.size();
-        for (uint64_t g = sc_off[n]; g < sc_off[n + 1]; g += SCAN_CHUNK) {
+        for (uint64_t g = sc_off[n]; g < sc_off[n + 1]; g += ht.scan_chunk) {
             ht.chunk_node.push_back(n);
             ht.chunk_beg.push_back(g);
-            ht.chunk_end.push_back(std::min<uint64_t>(g + SCAN_CHUNK, sc_off[n + 1]));
+            ht.chunk_end.push_back(std::min<uint64_t>(g + ht.scan_chunk, sc_off[n + 1]));
         }
     }
     ht.node_chunk_off[N] = (uint32_t)ht.chunk_node.size();

@@ -92,6 +92,7 @@ struct HostTrace {
     uint64_t dropped = 0;                           // records of other shards left out (header sharding)
     uint64_t part_dropped = 0;                      // ... of them, records whose entries all lie in other shards
     std::vector<uint32_t> chunk_node, node_chunk_off;
+    uint32_t scan_chunk = SCAN_CHUNK;               // records per header-scan chunk (scan_chunk_for)
     std::vector<uint64_t> chunk_beg, chunk_end;
     std::vector<uint8_t> sc_type;                   // header-scan stream (mpx_internal.hpp SC_*)
     std::vector<uint64_t> sc_key;

@@ -359,7 +359,6 @@ __global__ __launch_bounds__(256) void k_gate_votes(DevView v)
     }
 }
 
-constexpr uint32_t SCAN_ROUNDS = SCAN_CHUNK / 256;   // rounds of 64 records per wave
 
 // the summary word a partial-row column adds into (-1: none)
 __device__ inline int summary_word(uint32_t pc)
@@ -405,13 +404,13 @@ __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64
 }
 
 // Chunk aggregates over the header-scan stream: max of the PREPARE ids and of
-// the max_seen contributions of SCAN_CHUNK records (order-free, coalesced)
+// the max_seen contributions of CH records (order-free, coalesced)
 // RESET: the step's first kernel also does k_reset's work (one launch less per step)
 // Loads: four records per thread per round — their types as one aligned u32 and their keys
 // as two 16-byte loads (a wave reads 256 B of types and 4 KiB of keys per round) instead of
 // a byte and a u64 per record; the words may start before the chunk and end after it (the
 // record index decides), and device buffers are padded to 64 bytes (DevBuf::alloc)
-template <bool RESET>
+template <bool RESET, uint32_t CH>
 __global__ __launch_bounds__(256) void k_scan_chunk(DevView v, uint32_t n_partials)
 {
     __shared__ uint64_t l[2][4];
@@ -419,7 +418,7 @@ __global__ __launch_bounds__(256) void k_scan_chunk(DevView v, uint32_t n_partia
     const uint32_t c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
     const uint64_t w0 = beg >> 2, w1 = (end + 3) >> 2;
-    constexpr uint32_t WR = (SCAN_CHUNK / 4 + 256) / 256;     // words of a chunk, one slack word
+    constexpr uint32_t WR = (CH / 4 + 256) / 256;             // words of a chunk, one slack word
     const uint32_t *tw = reinterpret_cast<const uint32_t *>(v.sc_type);
     const u64x2 *kw = reinterpret_cast<const u64x2 *>(v.sc_key);
     uint32_t ty[WR];
@@ -482,27 +481,28 @@ __global__ __launch_bounds__(256) void k_scan_node(DevView v)
 }
 
 // Per scan record: granted / reject flags and the max_seen a REJECT carries.
-// Wave w of the chunk's block owns SCAN_CHUNK / 4 consecutive records, 64 per
+// Wave w of the chunk's block owns CH / 4 consecutive records, 64 per
 // round (coalesced), staged in LDS between the two phases: (1) wave maxima ->
 // the wave's carry-in, (2) per round the promised value before each record
 // (an exclusive wave scan, only in rounds that hold a PREPARE) and, in rounds
 // with a REJECT, the inclusive max_seen scan.  Flags go to the record's
 // message (m_flags[sc_idx]); messages outside the stream keep their static flags.
 // (the body of one chunk's workgroup: k_scan_apply, or a scan block of k_headers)
-template <bool MEMBER>
+template <bool MEMBER, uint32_t CH>
 __device__ inline void scan_apply_chunk(const DevView &v, const uint32_t c, uint64_t (&l)[2][4], uint64_t (&lc)[2][4],
                                         uint64_t *lky, uint8_t *lty, uint32_t *lix)
 {
+    constexpr uint32_t SCAN_ROUNDS = CH / 256;                // rounds of 64 records per wave
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t beg = v.chunk_beg[c], end = v.chunk_end[c];
-    const uint64_t wb = beg + (uint64_t)w * (SCAN_CHUNK / 4) + lane;
-    const uint32_t lb = w * (SCAN_CHUNK / 4) + lane;
+    const uint64_t wb = beg + (uint64_t)w * (CH / 4) + lane;
+    const uint32_t lb = w * (CH / 4) + lane;
     constexpr bool member = MEMBER;
     // staging: the chunk's records into LDS (record g at g - beg), four per thread per
     // round — their types as one aligned u32, keys and message indices as 16-byte loads
     // (as k_scan_chunk); the words may start before the chunk and end after it
     const uint64_t w0 = beg >> 2, w1 = (end + 3) >> 2;
-    constexpr uint32_t WR = (SCAN_CHUNK / 4 + 256) / 256;
+    constexpr uint32_t WR = (CH / 4 + 256) / 256;
     const uint32_t *tw = reinterpret_cast<const uint32_t *>(v.sc_type);
     const u64x2 *kw = reinterpret_cast<const u64x2 *>(v.sc_key);
     const u32x4 *iw = reinterpret_cast<const u32x4 *>(v.sc_idx);
@@ -547,9 +547,9 @@ __device__ inline void scan_apply_chunk(const DevView &v, const uint32_t c, uint
                 lix[o] = idx[j];
             }
     }
-    for (uint32_t o = len + threadIdx.x; o < SCAN_CHUNK; o += 256) { lty[o] = SC_NONE; lky[o] = 0; }
+    for (uint32_t o = len + threadIdx.x; o < CH; o += 256) { lty[o] = SC_NONE; lky[o] = 0; }
     __syncthreads();
-    // the wave's own records (its SCAN_CHUNK / 4, 64 per round): its maxima
+    // the wave's own records (its CH / 4, 64 per round): its maxima
     uint64_t lp = 0, ls = 0;
 #pragma unroll
     for (uint32_t r = 0; r < SCAN_ROUNDS; ++r) {
@@ -854,15 +854,15 @@ __device__ inline void votes_block(const DevView &v, const uint32_t blk, uint64_
 // LDS: the larger of the scan's chunk staging and the votes' reply staging, shared.
 constexpr uint32_t HDR_LDS_WORDS = (VOTE_LDS * 4 * 12 + 7) / 8;   // 4 waves x 768 x (8 + 4) bytes
 static_assert(HDR_LDS_WORDS * 8 >= SCAN_CHUNK * 13, "the scan staging fits");
-template <bool MEMBER>
+template <bool MEMBER, uint32_t CH>
 __global__ __launch_bounds__(256) void k_headers(DevView v, uint32_t nb_scan, uint32_t nb_prop)
 {
     __shared__ uint64_t raw[HDR_LDS_WORDS];
     __shared__ uint64_t l[2][4], lc[2][4];
     const uint32_t b = blockIdx.x;
     if (b < nb_scan) {
-        scan_apply_chunk<MEMBER>(v, b, l, lc, raw, reinterpret_cast<uint8_t *>(raw + SCAN_CHUNK),
-                                 reinterpret_cast<uint32_t *>(raw + SCAN_CHUNK + SCAN_CHUNK / 8));
+        scan_apply_chunk<MEMBER, CH>(v, b, l, lc, raw, reinterpret_cast<uint8_t *>(raw + CH),
+                                     reinterpret_cast<uint32_t *>(raw + CH + CH / 8));
     } else if (b < nb_scan + nb_prop) {
         const uint32_t c = 4 * (b - nb_scan) + (threadIdx.x >> 6);
         if (c < v.num_pc) prop_chunk_wave(v, c);
@@ -894,8 +894,12 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
     if (!tot) return;
     const uint32_t sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (v.out_subs - 1);
     unsigned long long base = 0;
+#ifdef MPX_EXP_NOATOMIC
+    base = 0;                                    // (timing experiment only: records overwrite each other)
+#else
     if (lane == 0) base = atomicAdd(&v.out_cursor[OUT_STRIDE * sub], (unsigned long long)tot);
     base = __shfl(base, 0, 64);
+#endif
     const uint64_t below = (1ull << lane) - 1;
     uint32_t off = 0;
 #pragma unroll
@@ -910,64 +914,81 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
     }
 }
 
-// Snapshot records of one PREPARE of a pair (FilterAcceptedValues, multi/paxos.cpp:902-922):
-// the hit slots in slot order, grouped into segments fixed by one dense fragment — one
-// OUT_RUN record per segment, which the host expands slot by slot (engine.cpp
-// fetch_results) — and one record per slot a sparse fragment fixed.  A promise reply's
-// values mostly come from a few whole runs, so this writes a few records per pair and
-// PREPARE instead of one per slot.
-__device__ inline void emit_snap(const DevView &v, const bool (&hit)[SPL_], uint32_t msg, const uint32_t (&ref)[SPL_],
-                                 const bool (&dense)[SPL_])
-{
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t key[SPL_];                      // segment key: fixing fragment + 1 (dense), 0: a record of its own
-    uint64_t sm[SPL_], em[SPL_];
-#pragma unroll
-    for (uint32_t j = 0; j < SPL_; ++j) key[j] = hit[j] && dense[j] ? ref[j] + 1 : 0;
-    uint32_t tot = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < SPL_; ++j) {
-        // the previous slot (lane - 1, or lane 63 of row j - 1) and the next one
-        uint32_t pk = __shfl_up(key[j], 1, 64), nk = __shfl_down(key[j], 1, 64);
-        const uint32_t pk_row = j ? __shfl(key[j ? j - 1 : 0], 63, 64) : 0;
-        const uint32_t nk_row = j + 1 < SPL_ ? __shfl(key[j + 1 < SPL_ ? j + 1 : j], 0, 64) : 0;
-        if (lane == 0) pk = pk_row;
-        if (lane == 63) nk = nk_row;
-        sm[j] = __ballot(hit[j] && (key[j] == 0 || pk != key[j]));
-        em[j] = __ballot(hit[j] && (key[j] == 0 || nk != key[j]));
-        tot += (uint32_t)__popcll(sm[j]);
+// Snapshot records through a per-wave LDS queue (k_apply): the records of a wave's events are
+// staged in LDS and reserved in the sub-buffer with one atomic per QCAP records instead of one
+// per event; the queue is double-buffered, so a full half's reservation (a returning atomic,
+// a full memory round trip) is in flight while the walk fills the other half, and its records
+// are copied out when that one fills in turn (or at the wave's end).
+constexpr uint32_t QCAP = 128;
+struct EmitQ {
+    uint32_t *q;                 // LDS: [2][QCAP][3] words (msg, ref, aux)
+    uint32_t fill, cur, pend;    // records in the filling half, which half fills, records awaiting their base
+    unsigned long long pbase;    // lane 0: the pending half's reservation
+    uint32_t sub;
+    __device__ void init(const DevView &v, uint32_t *lds)
+    {
+        q = lds; fill = 0; cur = 0; pend = 0; pbase = 0;
+        sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (v.out_subs - 1);
     }
-    if (!tot) return;
-    const uint32_t sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (v.out_subs - 1);
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(&v.out_cursor[OUT_STRIDE * sub], (unsigned long long)tot);
-    base = __shfl(base, 0, 64);
-    const uint64_t below = (1ull << lane) - 1;
-    uint32_t off = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < SPL_; ++j) {
-        if ((sm[j] >> lane) & 1) {
-            const uint64_t at = base + off + (uint64_t)__popcll(sm[j] & below);
-            uint32_t e = 0;                      // the segment's last slot: the first end at or after it
-#pragma unroll
-            for (uint32_t j2 = SPL_; j2-- > j;) {
-                const uint64_t m = j2 == j ? em[j2] & ~below : em[j2];
-                if (m) e = 64 * j2 + (uint32_t)__builtin_ctzll(m);
-            }
-            const uint32_t s0 = lane + 64 * j;
-            if (at < v.out_cap) {
-                OutRec r;
-                r.msg = msg; r.ref = ref[j];
-                r.aux = key[j] ? OUT_RUN | s0 | ((e - s0 + 1) << OUT_RUN_SHIFT) : s0;
-                v.out[(uint64_t)sub * v.out_cap + at] = r;
-            }
+    // copy the pending half out (waits for its reservation), then reserve the filling half
+    __device__ void rotate(const DevView &v)
+    {
+        const uint32_t lane = threadIdx.x & 63;
+        if (pend) {
+            const unsigned long long base = __shfl(pbase, 0, 64);
+            const uint32_t *h = q + 3 * QCAP * (cur ^ 1);
+            for (uint32_t r = lane; r < pend; r += 64)
+                if (base + r < v.out_cap) {
+                    OutRec o;
+                    o.msg = h[3 * r]; o.ref = h[3 * r + 1]; o.aux = h[3 * r + 2];
+                    v.out[(uint64_t)sub * v.out_cap + base + r] = o;
+                }
         }
-        off += (uint32_t)__popcll(sm[j]);
+        pend = fill;
+        if (fill && lane == 0) pbase = atomicAdd(&v.out_cursor[OUT_STRIDE * sub], (unsigned long long)fill);
+        cur ^= 1;
+        fill = 0;
+        wave_lds_fence();
     }
-}
+    __device__ void finish(const DevView &v) { rotate(v); rotate(v); }
+    __device__ void emit(const DevView &v, const bool (&want)[SPL_], uint32_t msg, uint32_t kind_aux,
+                         const uint32_t (&ref)[SPL_], const uint32_t *ext = nullptr)
+    {
+        const uint32_t lane = threadIdx.x & 63;
+        uint64_t m[SPL_];
+        uint32_t tot = 0, idx[SPL_];
+        const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+        for (uint32_t j = 0; j < SPL_; ++j) {
+            m[j] = __ballot(want[j]);
+            idx[j] = tot + (uint32_t)__popcll(m[j] & below);       // the record's rank in the event
+            tot += (uint32_t)__popcll(m[j]);
+        }
+        for (uint32_t done = 0; done < tot;) {
+            if (fill == QCAP) rotate(v);
+            const uint32_t take = tot - done < QCAP - fill ? tot - done : QCAP - fill;
+            uint32_t *h = q + 3 * QCAP * cur;
+#pragma unroll
+            for (uint32_t j = 0; j < SPL_; ++j)
+                if (want[j] && idx[j] >= done && idx[j] < done + take) {
+                    const uint32_t at = fill + idx[j] - done;
+                    h[3 * at] = msg; h[3 * at + 1] = ref[j];
+                    h[3 * at + 2] = kind_aux | (lane + 64 * j) | (ext ? ext[j] : 0);
+                }
+            fill += take;
+            done += take;
+        }
+    }
+};
 
 constexpr uint32_t SPL = BS / 64;
 static_assert(SPL == SPL_, "4 slots per lane");
+#ifndef MPX_PREPLY_PREFETCH
+#define MPX_PREPLY_PREFETCH 0
+#endif
+// k_apply's promise rounds: the proposal ids of this many counted dense promise-reply runs
+// ahead of the walk are in flight (a rolling window over the pair's fragment window)
+constexpr uint32_t PREPLY_PF = MPX_PREPLY_PREFETCH;
 
 // slots of this lane that fragment (start, count, dense) covers: k[j] = entry
 // offset within the fragment or -1.  Sparse runs scatter through the wave's
@@ -2125,6 +2146,14 @@ __global__ __launch_bounds__(256) void k_store8(DevView v, uint32_t store_grid, 
 // never run, so they hold fewer registers and more waves per SIMD hide the
 // descriptor latency.
 enum { AM_FULL = 0, AM_SIMPLE = 1, AM_SNAP = 2 };
+// waves per SIMD the timed instantiations are built for (the register budget: 512 / waves)
+#ifndef MPX_APPLY_WAVES_SNAP
+#define MPX_APPLY_WAVES_SNAP 4
+#endif
+#ifndef MPX_APPLY_WAVES_FULL
+#define MPX_APPLY_WAVES_FULL 4
+#endif
+constexpr int APPLY_WAVES_SNAP = MPX_APPLY_WAVES_SNAP, APPLY_WAVES_FULL = MPX_APPLY_WAVES_FULL;
 template <int WAVES_PER_EU, bool DIGEST, bool MEMBER, int MODE = AM_FULL>
 __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t it0, uint64_t it1)
 {
@@ -2132,6 +2161,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
     __shared__ uint16_t lidx_all[4][BS];
     __shared__ u64x2 pre_all[4][BS];           // pre-accepted merge (pid, PRESENT | r-entry): rare, kept in LDS
     __shared__ unsigned long long red[4][8];
+#ifdef MPX_EMIT_QUEUE
+    __shared__ uint32_t emq_all[4][2 * QCAP * 3];
+    EmitQ emq;
+    emq.init(v, emq_all[threadIdx.x >> 6]);
+#define EMIT(...) emq.emit(v, __VA_ARGS__)
+#else
+#define EMIT(...) emit_rows(v, __VA_ARGS__)
+#endif
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint16_t *lidx = lidx_all[wv];
     u64x2 *pre = pre_all[wv];
@@ -2145,7 +2182,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
     constexpr bool member = MEMBER;
     const uint64_t stride = (uint64_t)gridDim.x * 4;
     const uint64_t *__restrict__ e_val = v.e_val;
-    constexpr uint32_t S_PRESENT = 1, S_COMMITTED = 2, S_DENSE = 4;   // S_DENSE: fixed by a dense fragment
+    constexpr uint32_t S_PRESENT = 1, S_COMMITTED = 2;
 
     // work list: the pairs the lean kernel does not take (ingest.cpp), GP_WORDS
     // per item.  Three-stage software pipeline over this wave's items, issued at
@@ -2226,6 +2263,33 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
             }
             first = false;
             const uint32_t fmsg = (uint32_t)fw1;
+            // promise rounds: the counted dense promise-reply runs of the window, whose proposal
+            // ids the walk merges one run at a time — the next PREPLY_PF of them are loaded ahead
+            // (slot q holds run pfa[q]'s ids), so a run's merge does not wait out its own loads
+            constexpr uint32_t PF = ROUNDS ? (PREPLY_PF ? PREPLY_PF : 1) : 1;
+            uint64_t pfv[PF][SPL];
+            uint32_t pfa[PF];
+            uint64_t pleft = 0;                          // runs not yet issued
+            auto pf_issue = [&](uint32_t q) {
+                pfa[q] = NONE32;
+                if (!pleft) return;
+                const uint32_t x = (uint32_t)__builtin_ctzll(pleft);
+                pleft &= pleft - 1;
+                pfa[q] = x;
+                const uint64_t ent = rl64(fw0, x), w1 = rl64(fw1, x);
+                const int cnt = (int)((w1 >> 32) & 0xFFFF), st0 = (int)((w1 >> 48) & 0xFF);
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) {
+                    const int d = (int)(lane + 64 * j) - st0;
+                    pfv[q][j] = d >= 0 && d < cnt ? v.r_pid[ent + d] : 0;
+                }
+            };
+            if (ROUNDS && PREPLY_PF) {
+                const uint32_t fl0 = (uint32_t)(fw1 >> 56);
+                pleft = __ballot(lane < nf && (fl0 >> 4) == K_PREPLY && (fl0 & FR_DENSE) && (fflag & F_COUNTED));
+#pragma unroll
+                for (uint32_t q = 0; q < PF; ++q) pf_issue(q);
+            }
             // the window's events that can act:
             // a rejected PREPARE, or a member E_EPOCH that neither deletes nor recreates the
             // node's Acceptor (nor, with rounds, resets its Proposer), changes nothing here
@@ -2258,7 +2322,6 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                     const uint64_t ballot = DIGEST ? rl64(fbal, a) : 0;
                     const bool dense = fl & FR_DENSE;
                     const uint32_t fq = (uint32_t)(fi + a + 1);
-                    const uint32_t sd = dense ? S_DENSE : 0;
                     int k[SPL];
                     frag_slots(lidx, kind == K_PREPLY ? v.r_slot : v.e_slot, ent, cnt, st0, dense, k);
                     if (member && (kind == K_ACCEPT || kind == K_COMMIT)) {
@@ -2278,10 +2341,10 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                         record_violation(v, MPX_V_LEARN_VALUE, n, seq, v.shard_begin + li0 + lane + 64 * j);
                                 } else if (learn) {
                                     if (DIGEST) sb[j] = v.e_pid[x];
-                                    SF_SET(j, S_PRESENT | S_COMMITTED | sd); se[j] = x; sm[j] = fq;
+                                    SF_SET(j, S_PRESENT | S_COMMITTED); se[j] = x; sm[j] = fq;
                                 } else if (!(SF(j) & S_PRESENT)) {
                                     if (DIGEST) sb[j] = v.e_pid[x];
-                                    SF_SET(j, S_PRESENT | sd); se[j] = x; sm[j] = fq;
+                                    SF_SET(j, S_PRESENT); se[j] = x; sm[j] = fq;
                                     ++cA;
                                 }
                                 cL += learn;
@@ -2293,7 +2356,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             for (uint32_t j = 0; j < SPL; ++j)
                                 if (k[j] >= 0 && !(SF(j) & S_COMMITTED)) {           // :1380
                                     if (DIGEST) sb[j] = ballot;                                   // :1387
-                                    SF_SET(j, S_PRESENT | sd); se[j] = (uint32_t)(ent + k[j]); sm[j] = fq;
+                                    SF_SET(j, S_PRESENT); se[j] = (uint32_t)(ent + k[j]); sm[j] = fq;
                                     ++cA;
                                 }
                         }
@@ -2308,16 +2371,27 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                                          v.shard_begin + li0 + lane + 64 * j);
                                 } else {
                                     if (DIGEST) sb[j] = ballot;                                   // :1515
-                                    SF_SET(j, S_PRESENT | S_COMMITTED | sd); se[j] = x; sm[j] = fq;
+                                    SF_SET(j, S_PRESENT | S_COMMITTED); se[j] = x; sm[j] = fq;
                                 }
                                 ++cL;
                             }
                     } else if (ROUNDS && kind == K_PREPLY) {
                         if (mf & F_COUNTED) {
-                            // the run's proposal ids all in flight, then the merge
+                            // the run's proposal ids: loaded ahead (a dense run), or all in flight now
                             uint64_t pid[SPL];
+                            bool got = false;
 #pragma unroll
-                            for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
+                            for (uint32_t q = 0; q < PF; ++q)
+                                if (ROUNDS && PREPLY_PF && pfa[q] == a) {
+#pragma unroll
+                                    for (uint32_t j = 0; j < SPL; ++j) pid[j] = pfv[q][j];
+                                    got = true;
+                                    pf_issue(q);                 // the slot takes the next run
+                                }
+                            if (!got) {
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
+                            }
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
                                 if (k[j] >= 0) {
@@ -2363,19 +2437,15 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                 }
                             }
                             uint32_t ref[SPL];
-                            bool dn[SPL];
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j) {
                                 hit[j] = hit[j] && li0 + lane + 64 * j < v.shard_len && (SF(j) & S_PRESENT);
                                 ref[j] = sm[j] - 1;                 // the fixing fragment (global)
-                                dn[j] = (SF(j) & S_DENSE) != 0;
                                 cP += hit[j];
                             }
-#ifdef MPX_SNAP_ROWS
-                            emit_rows(v, hit, g, 0, ref);                 // (A/B build: one record per slot)
-#else
-                            emit_snap(v, hit, g, ref, dn);
-#endif
+                            // (one record per slot: run records — OUT_RUN segments — measured slower,
+                            // 1.015 vs 0.992 ms C3 general apply, profiles/r04_v5_ab_snap_runs.json)
+                            EMIT(hit, g, 0, ref);
                         }
                     } else if (!ROUNDS) {
                         // AM_SNAP: a pair without promise-reply runs gets no round events; member:
@@ -2411,7 +2481,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             cQ += hit[j];
                             pre[lane + 64 * j] = u64x2{0, 0};                        // :1105
                         }
-                        emit_rows(v, hit, g, OUT_K1, ref, ext);
+                        EMIT(hit, g, OUT_K1, ref, ext);
                     }
                     ++c;
                 }
@@ -2433,6 +2503,10 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
             if (lane == 0) v.st_valid[sv_idx(v, n, b)] = 1;
         }
     }
+#ifdef MPX_EMIT_QUEUE
+    emq.finish(v);                               // the wave's last records out
+#endif
+#undef EMIT
     // workgroup reduction of the counters
     unsigned long long cc[5] = {cA, cL, cP, cQ, dig};
 #pragma unroll
@@ -2450,7 +2524,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
         const uint32_t t = threadIdx.x;
         unsigned long long s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         const int slot = t == 0 ? PC_A : t == 1 ? PC_L : t == 2 ? PC_P : t == 3 ? PC_Q : PC_DSTATE;
-        v.partials[8 * blockIdx.x + slot] += s;
+        if (s) atomicAdd(&v.partials[8 * blockIdx.x + slot], s);   // (the rounds launch may run beside the listed pairs')
     }
 #undef SF
 #undef SF_SET
@@ -3343,7 +3417,7 @@ bool run_ends_with_store(const DevView &v)
     return plan_path && v.chosen_static && !member && !lplan && v.num_gp == 0 && v.slot_w == 1;
 }
 
-int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
+int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5], LaunchSide side)
 {
     void *ev_begin = ev[0], *ev_apply0 = ev[1], *ev_apply1 = ev[2], *ev_general = ev[3], *ev_end = ev[4];
     hipStream_t s = (hipStream_t)stream_;
@@ -3373,19 +3447,27 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         if (v.num_sc) hipLaunchKernelGGL(k_gate_scan, dim3(cdiv(v.num_sc, 256)), dim3(256), 0, s, v, v.num_sc);
         if (v.num_batches) hipLaunchKernelGGL(k_gate_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
     }
+    const bool small = v.scan_chunk == SCAN_CHUNK_SMALL;      // (the host cut the chunks: scan_chunk_for)
     if (v.num_chunks) {
-        if (fold_reset)
-            hipExtLaunchKernelGGL(k_scan_chunk<true>, dim3(v.num_chunks), dim3(256), 0, s,
-                                  (hipEvent_t)ev_begin, (hipEvent_t)nullptr, 0, v, n_partials);
-        else hipLaunchKernelGGL(k_scan_chunk<false>, dim3(v.num_chunks), dim3(256), 0, s, v, n_partials);
+        if (fold_reset) {
+            if (small) hipExtLaunchKernelGGL((k_scan_chunk<true, SCAN_CHUNK_SMALL>), dim3(v.num_chunks), dim3(256), 0, s,
+                                             (hipEvent_t)ev_begin, (hipEvent_t)nullptr, 0, v, n_partials);
+            else hipExtLaunchKernelGGL((k_scan_chunk<true, SCAN_CHUNK>), dim3(v.num_chunks), dim3(256), 0, s,
+                                       (hipEvent_t)ev_begin, (hipEvent_t)nullptr, 0, v, n_partials);
+        } else if (small) hipLaunchKernelGGL((k_scan_chunk<false, SCAN_CHUNK_SMALL>), dim3(v.num_chunks), dim3(256), 0, s,
+                                             v, n_partials);
+        else hipLaunchKernelGGL((k_scan_chunk<false, SCAN_CHUNK>), dim3(v.num_chunks), dim3(256), 0, s, v, n_partials);
         if (v.scan_node_pass) hipLaunchKernelGGL(k_scan_node, dim3(v.N), dim3(256), 0, s, v);   // long node streams
     }
     // the scan's flag pass, the promise-quorum chunks and the accept votes: one launch (k_headers)
     {
         const uint32_t nb_scan = v.num_chunks, nb_prop = cdiv(v.num_pc, 4), nb_votes = cdiv(v.num_batches, 256);
         if (nb_scan + nb_prop + nb_votes) {
-            if (member) hipLaunchKernelGGL(k_headers<true>, dim3(nb_scan + nb_prop + nb_votes), dim3(256), 0, s, v, nb_scan, nb_prop);
-            else hipLaunchKernelGGL(k_headers<false>, dim3(nb_scan + nb_prop + nb_votes), dim3(256), 0, s, v, nb_scan, nb_prop);
+            const dim3 grid(nb_scan + nb_prop + nb_votes);
+            if (member && small) hipLaunchKernelGGL((k_headers<true, SCAN_CHUNK_SMALL>), grid, dim3(256), 0, s, v, nb_scan, nb_prop);
+            else if (member) hipLaunchKernelGGL((k_headers<true, SCAN_CHUNK>), grid, dim3(256), 0, s, v, nb_scan, nb_prop);
+            else if (small) hipLaunchKernelGGL((k_headers<false, SCAN_CHUNK_SMALL>), grid, dim3(256), 0, s, v, nb_scan, nb_prop);
+            else hipLaunchKernelGGL((k_headers<false, SCAN_CHUNK>), grid, dim3(256), 0, s, v, nb_scan, nb_prop);
         }
     }
     // (a window: every node's round after the window, prop_out, comes from k_prop_node)
@@ -3409,6 +3491,22 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
     // FAST_MAX_NODES nodes.
     const bool plan_path = !v.digest && !v.walk_all && (member || v.N <= FAST_MAX_NODES);
     const bool lplan = plan_path && (member || v.num_gp_snap);
+    // the promise-round pairs (the host list's tail) depend only on the header kernels: on the
+    // side stream they run beside the plan / store / listed-pair kernels (disjoint pairs, rows
+    // and sub-buffer cursors), joined before the chosen log and the summary
+    const bool rounds = lplan && v.num_gp > v.num_gp_snap;
+    const bool side_rounds = rounds && side.stream2;
+    hipStream_t s2 = side_rounds ? (hipStream_t)side.stream2 : s;
+    if (side_rounds) {
+        (void)hipEventRecord((hipEvent_t)side.fork, s);
+        (void)hipStreamWaitEvent(s2, (hipEvent_t)side.fork, 0);
+    }
+    auto launch_rounds = [&]() {
+        if (member) hipLaunchKernelGGL((k_apply<APPLY_WAVES_FULL, false, true>), dim3(g.apply_wgs), dim3(256), 0, s2, v, v.num_gp_snap, v.num_gp);
+        else hipLaunchKernelGGL((k_apply<APPLY_WAVES_FULL, false, false>), dim3(g.apply_wgs), dim3(256), 0, s2, v, v.num_gp_snap, v.num_gp);
+        if (side_rounds) (void)hipEventRecord((hipEvent_t)side.join, s2);
+    };
+    if (side_rounds) launch_rounds();
     if (ev_apply0 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
     // the chosen log needs no k_chosen launch when the trace's chosen-log runs passed
     // plan_chosen's static test at load; then, with no general pair either (the C4 shape), the
@@ -3459,12 +3557,10 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         // the pairs k_plan_list listed (their count is on the device), then the promise rounds
         DevView vd = v;
         vd.gp_list = v.gp_dyn;
-        if (member) hipLaunchKernelGGL((k_apply<4, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
-        else hipLaunchKernelGGL((k_apply<4, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
-        if (v.num_gp > v.num_gp_snap) {
-            if (member) hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
-            else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, v.num_gp_snap, v.num_gp);
-        }
+        if (member) hipLaunchKernelGGL((k_apply<APPLY_WAVES_SNAP, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
+        else hipLaunchKernelGGL((k_apply<APPLY_WAVES_SNAP, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
+        if (rounds && !side_rounds) launch_rounds();
+        if (side_rounds) (void)hipStreamWaitEvent(s, (hipEvent_t)side.join, 0);
     } else {
         // every pair of the host-built work list on the general kernel, in three ranges
         // (ingest.cpp orders the list): event-free pairs (AM_SIMPLE), pairs without
@@ -3483,10 +3579,10 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5])
         } else {
             if (ns) { if (member) hipLaunchKernelGGL((k_apply<1, false, true, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
                       else hipLaunchKernelGGL((k_apply<1, false, false, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns); }
-            if (nq > ns) { if (member) hipLaunchKernelGGL((k_apply<4, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq);
-                           else hipLaunchKernelGGL((k_apply<4, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq); }
-            if (v.num_gp > nq) { if (member) hipLaunchKernelGGL((k_apply<4, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
-                                 else hipLaunchKernelGGL((k_apply<4, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
+            if (nq > ns) { if (member) hipLaunchKernelGGL((k_apply<APPLY_WAVES_SNAP, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq);
+                           else hipLaunchKernelGGL((k_apply<APPLY_WAVES_SNAP, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, v, ns, nq); }
+            if (v.num_gp > nq) { if (member) hipLaunchKernelGGL((k_apply<APPLY_WAVES_FULL, false, true>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp);
+                                 else hipLaunchKernelGGL((k_apply<APPLY_WAVES_FULL, false, false>), dim3(g.apply_wgs), dim3(256), 0, s, v, nq, v.num_gp); }
         }
     }
     // the chosen log of the buckets no plan word covered (none when the trace's chosen-log runs

@@ -26,6 +26,7 @@
 //       row N of the state array so k_store streams both alike
 #pragma once
 #include <cstdint>
+#include <cstdlib>
 #include <cstddef>
 
 #include "mpx.h"
@@ -44,6 +45,16 @@ constexpr uint32_t BS = 1u << BSH;
 #define MPX_SCAN_CHUNK 2048                     // (a build knob for A/B: make EXTRA=-DMPX_SCAN_CHUNK=1024)
 #endif
 constexpr uint32_t SCAN_CHUNK = MPX_SCAN_CHUNK;        // header-scan chunk (messages): 8 per thread
+// a short scan stream (an instance shard) is cut into half-size chunks: twice the
+// workgroups for the two scan launches, which are latency-bound at that size (C4 shard at
+// world 8: 1024-record chunks -2.7 us per step; at C4 size +2 %, profiles/r03_v11_scan_chunk_ab.json)
+constexpr uint32_t SCAN_CHUNK_SMALL = SCAN_CHUNK / 2;
+constexpr uint64_t SCAN_SMALL_RECORDS = 1ull << 21;
+inline uint32_t scan_chunk_for(uint64_t records)
+{
+    if (const char *x = std::getenv("MPX_SCAN_SMALL")) return std::atoi(x) ? SCAN_CHUNK_SMALL : SCAN_CHUNK;   // (A/B)
+    return records <= SCAN_SMALL_RECORDS ? SCAN_CHUNK_SMALL : SCAN_CHUNK;
+}
 constexpr uint32_t PROP_CHUNK = 512;         // promise-quorum chunk (pl records): 8 windows of 64 (C3 2^24 scan
                                              // phase 0.112 ms vs 0.128 at 2048, 0.134 at 256)
 // k_headers' scan blocks re-reduce a node's earlier chunk aggregates inline (O(chunks^2)
@@ -215,6 +226,7 @@ struct DevView {
     uint64_t *chunk_agg;            // 2 per chunk: pmax, smax
     uint64_t *chunk_carry;          // 2 per chunk: exclusive prefix (k_scan_node)
     uint32_t scan_node_pass;        // 1: a node has > SCAN_INLINE_CHUNKS chunks, carry-in from k_scan_node
+    uint32_t scan_chunk;            // records per header-scan chunk (SCAN_CHUNK or SCAN_CHUNK_SMALL)
     uint32_t seq;                   // this launch's sequence number (from 1)
     uint64_t *node_scal;            // 2 per node: promised, max_seen
     // pools
@@ -400,7 +412,10 @@ struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, store_wgs; };
 // ev (hipEvent_t, each may be null): begin, apply phase start (after the header
 // scan / quorum kernels), after the plan / store / fast-apply kernels, after the
 // general k_apply, end
-int launch_run(const DevView &v, void *stream, LaunchGeom g, void *const ev[5]);
+// a second stream and two events (fork / join, timing off) for kernels of a run that may
+// overlap others of it; nullptr: everything on `stream`
+struct LaunchSide { void *stream2, *fork, *join; };
+int launch_run(const DevView &v, void *stream, LaunchGeom g, void *const ev[5], LaunchSide side);
 // the run's last kernel is the store, the step summary folded into it (the clean multi
 // plan path, C4): launch_run then records neither the general-apply nor the end event
 bool run_ends_with_store(const DevView &v);

@@ -293,19 +293,26 @@ def test_engine_matches_oracle_c3_faulty(seed, m, p, b):
 
 
 def test_rccl_single_rank_allgather():
-    """The RCCL path of a step (communicator + summary all-gather on the engine stream), one rank."""
+    """The RCCL path of a step (communicator + summary all-gather on the comm stream, overlapped
+    with the next launch: two summary slots), one rank: after one step, several queued steps
+    (each slot reused while the other's all-gather may still run) and a digested run, the
+    gathered summary is the last launch's."""
     n, m = 9, 256 * 64
+    from mpx import dist as mdist
     with mpx.Engine(n, 0, m) as e:
         e.comm_init(mpx.Engine.comm_unique_id(), 0, 1)
         e.load_clean_device(num_instances=m)
-        e.step()
-        e.sync()
-        st = e.stats()
-        summ = e.allgather_summary(1)
-    from mpx import dist as mdist
-    tot = mdist.combine(summ)
-    assert tot["chosen"] == m == st["chosen"]
-    assert tot["state_digest"] == st["state_digest"]
+        for steps in (1, 5):
+            for _ in range(steps):
+                e.step()
+            e.sync()
+            st = e.stats()
+            tot = mdist.combine(e.allgather_summary(1))
+            assert tot["chosen"] == m == st["chosen"]
+            assert tot["state_digest"] == st["state_digest"]
+        chk = e.run()
+        tot = mdist.combine(e.allgather_summary(1))
+        assert tot["chosen"] == m == chk["chosen"] and tot["state_digest"] == chk["state_digest"]
 
 
 # ---- member semantics (member/paxos.cpp; SURVEY.md §8 rows a12-a15, config C5) ----
@@ -470,12 +477,15 @@ def test_store_chunks_tails_and_partial_pairs(extra):
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
 
 
-@pytest.mark.parametrize("env", [("MPX_PROP_CHUNK", "64"), ("MPX_PROP_CHUNK", "5"), ("MPX_STEP_WALK", "1")])
+@pytest.mark.parametrize("env", [("MPX_PROP_CHUNK", "64"), ("MPX_PROP_CHUNK", "5"), ("MPX_STEP_WALK", "1"),
+                                 ("MPX_SCAN_SMALL", "0"), ("MPX_SCAN_SMALL", "1")])
 @pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "c5_member_3",
                                   "demo_s0", "demo5_s3", "hm_promise_merge"])
 def test_kept_alternative_paths(name, env, monkeypatch):
     """The supported alternatives stay correct: promise-quorum chunks small
     enough that rounds span chunks (k_prop_chunk's deferred prefixes, k_prop_node's carry),
+    either header-scan chunk size whatever the stream length (MPX_SCAN_SMALL: the size
+    scan_chunk_for picks by length),
     and a step that walks every pair as the digested run does (MPX_STEP_WALK; the path of
     multi traces with more than FAST_MAX_NODES nodes).  The measured-and-rejected variants
     of earlier rounds are no longer compiled (their A/B records stay in profiles/)."""
@@ -629,8 +639,9 @@ def test_member_sharded_decisions(name, shards):
         with mpx.Engine(hd["num_nodes"], sb, se, semantics=hd["semantics"]) as e:
             e.submit_trace(trace)
             e.run()
-            with pytest.raises(mpx.MpxError):
-                e.decisions()                         # a member shard alone cannot decide
+            if sb > 0:
+                with pytest.raises(mpx.MpxError):
+                    e.decisions()                     # a shard past instance 0 cannot decide alone
             parts.append(e.proposal_part())
     assert mpx.proposal_combine(parts) == want
 

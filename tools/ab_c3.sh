@@ -1,7 +1,7 @@
 #!/bin/bash
-# Same-box A/B of build variants (multi-paxos_amd/lib_<v>/libmpx.so) against the default
-# library on the C3 general-path leg (bench.py --c3-only), arms alternated, 3 rounds:
-#   tools/ab_c3.sh <tag> v1 [v2 ...]
+# Same-box A/B on the C3 general-path leg (bench.py --c3-only), arms alternated, 3 rounds:
+#   tools/ab_c3.sh <tag> v1 [v2 ...]       build variants (multi-paxos_amd/lib_<v>/libmpx.so)
+#   tools/ab_c3.sh <tag> VAR=value [...]   environment switches on the default library
 set -o pipefail
 tag=$1; shift
 out=gpurun_out/abc3_$tag
@@ -9,8 +9,11 @@ mkdir -p $out
 rm -f $out/*.json
 for rep in 1 2 3; do
   for v in default "$@"; do
-    if [ $v = default ]; then unset MPX_LIB_VARIANT; else export MPX_LIB_VARIANT=$v; fi
-    timeout -k 10 300 python bench.py --c3-only > $out/c3_${v}_$rep.json 2> $out/c3_${v}_$rep.err || { tail -5 $out/c3_${v}_$rep.err; exit 1; }
+    unset MPX_LIB_VARIANT
+    envs=X=0
+    case $v in default) ;; *=*) envs=$v ;; *) export MPX_LIB_VARIANT=$v ;; esac
+    a=${v//=/_}
+    env $envs timeout -k 10 300 python bench.py --c3-only > $out/c3_${a}_$rep.json 2> $out/c3_${a}_$rep.err || { tail -5 $out/c3_${a}_$rep.err; exit 1; }
   done
 done
 unset MPX_LIB_VARIANT
