@@ -396,6 +396,7 @@ __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64
         v.fast_rest[0] = 0;
         v.fast_rest[1] = 0;                          // k_chosen's last-block ticket
         *v.gp_dyn_n = 0;
+        *v.gp_ext_n = 0;
         if (v.window) *v.outv_n = 0;
         for (uint32_t pc = 0; pc < 8; ++pc)          // the counter words k_reduce's workgroups add into
             if (summary_word(pc) >= 0) v.summary[summary_word(pc)] = 0;
@@ -894,12 +895,8 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
     if (!tot) return;
     const uint32_t sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (v.out_subs - 1);
     unsigned long long base = 0;
-#ifdef MPX_EXP_NOATOMIC
-    base = 0;                                    // (timing experiment only: records overwrite each other)
-#else
     if (lane == 0) base = atomicAdd(&v.out_cursor[OUT_STRIDE * sub], (unsigned long long)tot);
     base = __shfl(base, 0, 64);
-#endif
     const uint64_t below = (1ull << lane) - 1;
     uint32_t off = 0;
 #pragma unroll
@@ -913,73 +910,6 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
         off += (uint32_t)__popcll(m[j]);
     }
 }
-
-// Snapshot records through a per-wave LDS queue (k_apply): the records of a wave's events are
-// staged in LDS and reserved in the sub-buffer with one atomic per QCAP records instead of one
-// per event; the queue is double-buffered, so a full half's reservation (a returning atomic,
-// a full memory round trip) is in flight while the walk fills the other half, and its records
-// are copied out when that one fills in turn (or at the wave's end).
-constexpr uint32_t QCAP = 128;
-struct EmitQ {
-    uint32_t *q;                 // LDS: [2][QCAP][3] words (msg, ref, aux)
-    uint32_t fill, cur, pend;    // records in the filling half, which half fills, records awaiting their base
-    unsigned long long pbase;    // lane 0: the pending half's reservation
-    uint32_t sub;
-    __device__ void init(const DevView &v, uint32_t *lds)
-    {
-        q = lds; fill = 0; cur = 0; pend = 0; pbase = 0;
-        sub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (v.out_subs - 1);
-    }
-    // copy the pending half out (waits for its reservation), then reserve the filling half
-    __device__ void rotate(const DevView &v)
-    {
-        const uint32_t lane = threadIdx.x & 63;
-        if (pend) {
-            const unsigned long long base = __shfl(pbase, 0, 64);
-            const uint32_t *h = q + 3 * QCAP * (cur ^ 1);
-            for (uint32_t r = lane; r < pend; r += 64)
-                if (base + r < v.out_cap) {
-                    OutRec o;
-                    o.msg = h[3 * r]; o.ref = h[3 * r + 1]; o.aux = h[3 * r + 2];
-                    v.out[(uint64_t)sub * v.out_cap + base + r] = o;
-                }
-        }
-        pend = fill;
-        if (fill && lane == 0) pbase = atomicAdd(&v.out_cursor[OUT_STRIDE * sub], (unsigned long long)fill);
-        cur ^= 1;
-        fill = 0;
-        wave_lds_fence();
-    }
-    __device__ void finish(const DevView &v) { rotate(v); rotate(v); }
-    __device__ void emit(const DevView &v, const bool (&want)[SPL_], uint32_t msg, uint32_t kind_aux,
-                         const uint32_t (&ref)[SPL_], const uint32_t *ext = nullptr)
-    {
-        const uint32_t lane = threadIdx.x & 63;
-        uint64_t m[SPL_];
-        uint32_t tot = 0, idx[SPL_];
-        const uint64_t below = (1ull << lane) - 1;
-#pragma unroll
-        for (uint32_t j = 0; j < SPL_; ++j) {
-            m[j] = __ballot(want[j]);
-            idx[j] = tot + (uint32_t)__popcll(m[j] & below);       // the record's rank in the event
-            tot += (uint32_t)__popcll(m[j]);
-        }
-        for (uint32_t done = 0; done < tot;) {
-            if (fill == QCAP) rotate(v);
-            const uint32_t take = tot - done < QCAP - fill ? tot - done : QCAP - fill;
-            uint32_t *h = q + 3 * QCAP * cur;
-#pragma unroll
-            for (uint32_t j = 0; j < SPL_; ++j)
-                if (want[j] && idx[j] >= done && idx[j] < done + take) {
-                    const uint32_t at = fill + idx[j] - done;
-                    h[3 * at] = msg; h[3 * at + 1] = ref[j];
-                    h[3 * at + 2] = kind_aux | (lane + 64 * j) | (ext ? ext[j] : 0);
-                }
-            fill += take;
-            done += take;
-        }
-    }
-};
 
 constexpr uint32_t SPL = BS / 64;
 static_assert(SPL == SPL_, "4 slots per lane");
@@ -1710,12 +1640,13 @@ __device__ inline bool seg_add_split(uint32_t x, uint32_t (&s)[LSEG - 1])
         if (y < s[k]) { const uint32_t t = s[k]; s[k] = y; y = t; }
     return true;
 }
-// LSEG: segments a pair may have — up to 4 fit one plan word (k_store); the LSEG = 8 build
-// (knob 536870912, A/B) writes the slots of a pair with 5..8 segments itself and walks up to
-// F = 32 runs: C3 general apply 1.01 -> 0.80 ms but k_plan_list 0.19 -> 0.40 ms (3 waves per
-// SIMD, the per-thread slot writes), C5 apply 0.335 -> 0.394 ms; the default is 4 / 16.
+// LSEG: segments a pair may have — up to 4 fit one plan word (k_store); a pair with 5..8
+// (multi: LSEG = PLAN_XSEG, up to F = PLAN_XFRAGS runs) goes to the extension list as its split
+// points and segment values, which k_store_ext writes one wave per pair (round 3 measured the
+// same walk writing those slots per thread: C3 general apply 1.01 -> 0.80 ms but k_plan_list
+// 0.19 -> 0.40 ms).
 template <bool MEMBER, uint32_t LSEG = 4, uint32_t F = MPLAN_FRAGS>
-__global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs)
+__global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_wgs)
 {
     __shared__ uint64_t w_lds[4][MPLAN_LDS];
     __shared__ unsigned long long red[4][4];
@@ -1751,6 +1682,8 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
         wave_lds_fence();
     }
     bool fb = false;                                   // list the pair for k_apply
+    bool xt = false;                                   // ... or for k_store_ext (xw0: split points, xw1: values)
+    uint64_t xw0 = 0, xw1 = 0;
     if (i < np) {
         const uint32_t len = (uint32_t)(o1 - oa);
         const uint64_t rel = oa - wbase, b = i / N;
@@ -1769,16 +1702,19 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
                 }
             }
             if (ok) {
-                // the accept runs' scan flags, all in flight, then folded into bit 57
-                uint32_t fg[F];
+                // the accept runs' scan flags, 16 in flight at a time, then folded into bit 57
+                constexpr uint32_t FC = F < 16 ? F : 16;
+                for (uint32_t k0 = 0; k0 < len; k0 += FC) {
+                    uint32_t fg[FC];
 #pragma unroll
-                for (uint32_t k = 0; k < F; ++k) {
-                    const uint64_t w = k < len ? W[k] : 0;
-                    fg[k] = k < len && (w >> 60) == K_ACCEPT ? v.m_flags[(uint32_t)w] : 0;
+                    for (uint32_t k = 0; k < FC; ++k) {
+                        const uint64_t w = k0 + k < len ? W[k0 + k] : 0;
+                        fg[k] = k0 + k < len && (w >> 60) == K_ACCEPT ? v.m_flags[(uint32_t)w] : 0;
+                    }
+#pragma unroll
+                    for (uint32_t k = 0; k < FC; ++k)
+                        if (k0 + k < len && (fg[k] & F_GRANTED)) W[k0 + k] |= MP_GRANTED;
                 }
-#pragma unroll
-                for (uint32_t k = 0; k < F; ++k)
-                    if (k < len && (fg[k] & F_GRANTED)) W[k] |= MP_GRANTED;
                 uint32_t lo[LSEG], sl[LSEG];
 #pragma unroll
                 for (uint32_t g = 0; g < LSEG; ++g) {
@@ -1892,41 +1828,14 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
                         const uint32_t v4[4] = {val[0], val[1], val[2], val[3]}, s3[3] = {sp[0], sp[1], sp[2]};
                         q = plan_pack(v4, s3);
                     } else {
-                        // 5..LSEG segments: the pair's slots written here (k_store skips the bucket)
-                        const uint32_t n = (uint32_t)(i - b * N);
-                        if (v.slot_w == 1) {
-                            uint8_t *dst = static_cast<uint8_t *>(v.st) + (uint64_t)n * v.shard_len + (b << BSH);
-                            for (uint32_t j = 0; j < BS / 16; ++j) {
-                                uint32_t wd[4] = {0, 0, 0, 0};
-                                for (uint32_t t = 0; t < 16; ++t) {
-                                    const uint32_t sl_ = 16 * j + t;
-                                    uint32_t g = 0;
+                        // 5..LSEG segments: the split points and segment values to the extension
+                        // list (k_store_ext writes the slots; k_store skips the bucket)
+                        xw0 = xw1 = 0;
 #pragma unroll
-                                    for (uint32_t k = 0; k < LSEG - 1; ++k) g += sl_ >= sp[k];
-                                    uint32_t x = 0;
+                        for (uint32_t k = 0; k < LSEG - 1 && k < 7; ++k) xw0 |= (uint64_t)(sp[k] & 0x1FF) << (9 * k);
 #pragma unroll
-                                    for (uint32_t k = 0; k < LSEG; ++k) x = k == g ? val[k] : x;
-                                    wd[t >> 2] |= x << (8 * (t & 3));
-                                }
-                                *reinterpret_cast<u32x4 *>(dst + 16 * j) = u32x4{wd[0], wd[1], wd[2], wd[3]};
-                            }
-                        } else {
-                            uint16_t *dst = static_cast<uint16_t *>(v.st) + (uint64_t)n * v.shard_len + (b << BSH);
-                            for (uint32_t j = 0; j < BS / 8; ++j) {
-                                uint32_t wd[4] = {0, 0, 0, 0};
-                                for (uint32_t t = 0; t < 8; ++t) {
-                                    const uint32_t sl_ = 8 * j + t;
-                                    uint32_t g = 0;
-#pragma unroll
-                                    for (uint32_t k = 0; k < LSEG - 1; ++k) g += sl_ >= sp[k];
-                                    uint32_t x = 0;
-#pragma unroll
-                                    for (uint32_t k = 0; k < LSEG; ++k) x = k == g ? val[k] : x;
-                                    wd[t >> 1] |= x << (16 * (t & 1));
-                                }
-                                *reinterpret_cast<u32x4 *>(dst + 8 * j) = u32x4{wd[0], wd[1], wd[2], wd[3]};
-                            }
-                        }
+                        for (uint32_t k = 0; k < LSEG && k < 8; ++k) xw1 |= (uint64_t)(val[k] & 0xFF) << (8 * k);
+                        xt = true;
                     }
                     v.st_valid[i] = 1;
                 }
@@ -1947,6 +1856,16 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
             w[0] = oa; w[1] = o1; w[2] = e0; w[3] = e1; w[4] = i;
         }
     }
+    const uint64_t xm = __ballot(xt && !fb);
+    if (xm) {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(v.gp_ext_n, (unsigned long long)__popcll(xm));
+        base = __shfl(base, 0, 64);
+        if (xt && !fb) {
+            uint64_t *w = v.gp_ext + EXT_WORDS * (base + (uint64_t)__popcll(xm & ((1ull << lane) - 1)));
+            w[0] = i; w[1] = xw0; w[2] = xw1;
+        }
+    }
     if (MEMBER && i < NB) plan_chosen(v, i, cC);
     unsigned long long cc[4] = {cA, cL, cC, cP};
 #pragma unroll
@@ -1962,6 +1881,35 @@ __global__ __launch_bounds__(256) void k_plan_list(DevView v, uint32_t apply_wgs
         const unsigned long long x = red[0][t] + red[1][t] + red[2][t] + red[3][t];
         const int slot = t == 0 ? PC_A : t == 1 ? PC_L : t == 2 ? PC_C : PC_P;
         if (x) atomicAdd(&v.partials[8 * (blockIdx.x % apply_wgs) + slot], x);
+    }
+}
+
+// The slots of the pairs k_plan_list described by 5..8 segments: one wave per pair, 4 slots
+// per lane — the slot's segment is the number of split points at or below it, its value that
+// segment's (pair-local run + 1, or 0).
+__global__ __launch_bounds__(256) void k_store_ext(DevView v)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t n_ext = *v.gp_ext_n, nwaves = (uint64_t)gridDim.x * 4;
+    for (uint64_t x = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < n_ext; x += nwaves) {
+        const uint64_t i = v.gp_ext[EXT_WORDS * x], w0 = v.gp_ext[EXT_WORDS * x + 1], w1 = v.gp_ext[EXT_WORDS * x + 2];
+        const uint64_t b = i / v.N, n = i - b * v.N;
+        uint32_t val[4];
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+            const uint32_t sl = 4 * lane + t;
+            uint32_t g = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 7; ++k) g += sl >= ((w0 >> (9 * k)) & 0x1FF);
+            val[t] = (uint32_t)(w1 >> (8 * g)) & 0xFF;
+        }
+        const uint64_t at = n * v.shard_len + (b << BSH) + 4 * lane;
+        if (v.slot_w == 1)
+            *reinterpret_cast<u8x4 *>(static_cast<uint8_t *>(v.st) + at) =
+                u8x4{(uint8_t)val[0], (uint8_t)val[1], (uint8_t)val[2], (uint8_t)val[3]};
+        else
+            *reinterpret_cast<u16x4 *>(static_cast<uint16_t *>(v.st) + at) =
+                u16x4{(uint16_t)val[0], (uint16_t)val[1], (uint16_t)val[2], (uint16_t)val[3]};
     }
 }
 
@@ -2161,14 +2109,9 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
     __shared__ uint16_t lidx_all[4][BS];
     __shared__ u64x2 pre_all[4][BS];           // pre-accepted merge (pid, PRESENT | r-entry): rare, kept in LDS
     __shared__ unsigned long long red[4][8];
-#ifdef MPX_EMIT_QUEUE
-    __shared__ uint32_t emq_all[4][2 * QCAP * 3];
-    EmitQ emq;
-    emq.init(v, emq_all[threadIdx.x >> 6]);
-#define EMIT(...) emq.emit(v, __VA_ARGS__)
-#else
+// (snapshot records staged in a per-wave LDS queue, one reservation per 128: measured slower,
+// C3 step 1.447 vs 1.388 ms, profiles/r04_v9_ab_emit_queue.json)
 #define EMIT(...) emit_rows(v, __VA_ARGS__)
-#endif
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint16_t *lidx = lidx_all[wv];
     u64x2 *pre = pre_all[wv];
@@ -2503,9 +2446,6 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
             if (lane == 0) v.st_valid[sv_idx(v, n, b)] = 1;
         }
     }
-#ifdef MPX_EMIT_QUEUE
-    emq.finish(v);                               // the wave's last records out
-#endif
 #undef EMIT
     // workgroup reduction of the counters
     unsigned long long cc[5] = {cA, cL, cP, cQ, dig};
@@ -3538,7 +3478,14 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
             // 0.391 vs 0.304 ms apply phase at C4; the compiler drains vmcnt at its loop head)
             hipExtLaunchKernelGGL(k_plan, dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
-            if (lplan) hipLaunchKernelGGL(k_plan_list<false>, dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
+            if (lplan) {
+#ifdef MPX_PLAN_LSEG4
+                hipLaunchKernelGGL((k_plan_list<false>), dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);   // (A/B build)
+#else
+                hipLaunchKernelGGL((k_plan_list<false, PLAN_XSEG, PLAN_XFRAGS>), dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
+                hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);
+#endif
+            }
         }
         // every pair the trace marks lean (pair_gp 0) is one k_plan can describe (ingest.cpp /
         // mpx_load_clean_device use its predicate, plan_shape_ok), so nothing is left for the

@@ -249,6 +249,10 @@ struct DevView {
     // appended here (GP_WORDS per item, as gp_list) for k_apply; gp_dyn_n counts them
     uint64_t *gp_dyn;
     unsigned long long *gp_dyn_n;
+    // ... and the pairs it describes by 5..PLAN_XSEG segments: {pair, split points, values}
+    // (EXT_WORDS per item) for k_store_ext; gp_ext_n counts them
+    uint64_t *gp_ext;
+    unsigned long long *gp_ext_n;
     const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
     const uint32_t *ev_msg;
     // promise-quorum chunks (k_prop_chunk / k_prop_node): PROP_CHUNK records of one
@@ -349,6 +353,9 @@ enum : uint8_t { GP_LIST = 1, GP_ROUNDS = 2 };
 // k_plan_list: runs per pair it plans (walked from LDS) and runs a wave stages
 constexpr uint32_t MPLAN_FRAGS = 16;
 constexpr uint32_t MPLAN_LDS = 1024;
+constexpr uint32_t PLAN_XSEG = 8;            // k_plan_list (multi): up to 8 segments, 32 runs per pair
+constexpr uint32_t PLAN_XFRAGS = 32;
+constexpr uint32_t EXT_WORDS = 3;
 // the distinct run boundaries inside (0, 256), sorted into s[0..2] (BS = unused);
 // false once a fourth one appears
 MPX_HD inline bool plan_add_split(uint32_t x, uint32_t (&s)[3])
