@@ -3470,6 +3470,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
     const uint32_t plan_blocks = cdiv((uint64_t)v.N * v.NB, 256);
     if (plan_path) {
         if (member) {
+            // (member keeps 4 segments: its 8-segment build spills 80 VGPRs — plan_chosen — and
+            // 96 % of member list pairs have at most 4, tools/pair_stats.cpp)
             hipExtLaunchKernelGGL(k_plan_list<true>, dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
         } else {

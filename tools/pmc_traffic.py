@@ -34,10 +34,10 @@ SQ_COUNTERS = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "S
                "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VALU", "SQ_INSTS_SALU"]
 
 
-def run_pass(counters, outdir, bench_args, tag):
+def run_pass(counters, outdir, bench_args, tag, limit=400):
     """One rocprofv3 --pmc pass (kernel trace only); {counter: {kernel: [values per dispatch]}}."""
     d = os.path.join(outdir, "%s_pmc_%s" % (tag, "_".join(c.lower() for c in counters)))
-    cmd = ["timeout", "-s", "KILL", "400", "rocprofv3", "--pmc"] + counters + ["-d", d, "-o", "pmc",
+    cmd = ["timeout", "-s", "KILL", str(limit), "rocprofv3", "--pmc"] + counters + ["-d", d, "-o", "pmc",
            "--output-format", "csv", "--", sys.executable, os.path.join(ROOT, "bench.py"),
            "--no-cpu-baseline"] + bench_args
     subprocess.check_call(cmd, cwd=ROOT)
@@ -82,9 +82,10 @@ def main():
     else:
         bench_args = ["--steps", "3", "--warmup", "0", "--instances", str(a.instances), "--nodes", str(a.nodes),
                       "--c3-instances", "0", "--c5-instances", "0", "--c5c-instances", "0", "--shard-of", "0"] + rest
-    fetch = run_pass(["FETCH_SIZE"], a.outdir, bench_args, a.tag)["FETCH_SIZE"]
-    write = run_pass(["WRITE_SIZE"], a.outdir, bench_args, a.tag)["WRITE_SIZE"]
-    sq = run_pass(SQ_COUNTERS, a.outdir, bench_args, a.tag) if a.sq else {}
+    lim = 480 if a.c5c else 400                     # (the contended trace takes ~2.5 min to generate and ingest)
+    fetch = run_pass(["FETCH_SIZE"], a.outdir, bench_args, a.tag, lim)["FETCH_SIZE"]
+    write = run_pass(["WRITE_SIZE"], a.outdir, bench_args, a.tag, lim)["WRITE_SIZE"]
+    sq = run_pass(SQ_COUNTERS, a.outdir, bench_args, a.tag, lim) if a.sq else {}
     out = {"tag": a.tag, "workload": "C3W 2^%d x 7 in 16 windows (bench.py --c3-windows-only)" % (a.instances.bit_length() - 1)
            if a.c3w else "C5 2^%d member (bench.py --c5-only)" % (a.instances.bit_length() - 1) if a.c5 else
            "C5C 2^%d member, 3 proposers (bench.py --c5c-only)" % (a.instances.bit_length() - 1) if a.c5c else
