@@ -913,12 +913,6 @@ __device__ inline void emit_rows(const DevView &v, const bool (&want)[SPL_], uin
 
 constexpr uint32_t SPL = BS / 64;
 static_assert(SPL == SPL_, "4 slots per lane");
-#ifndef MPX_PREPLY_PREFETCH
-#define MPX_PREPLY_PREFETCH 0
-#endif
-// k_apply's promise rounds: the proposal ids of this many counted dense promise-reply runs
-// ahead of the walk are in flight (a rolling window over the pair's fragment window)
-constexpr uint32_t PREPLY_PF = MPX_PREPLY_PREFETCH;
 
 // slots of this lane that fragment (start, count, dense) covers: k[j] = entry
 // offset within the fragment or -1.  Sparse runs scatter through the wave's
@@ -2206,33 +2200,6 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
             }
             first = false;
             const uint32_t fmsg = (uint32_t)fw1;
-            // promise rounds: the counted dense promise-reply runs of the window, whose proposal
-            // ids the walk merges one run at a time — the next PREPLY_PF of them are loaded ahead
-            // (slot q holds run pfa[q]'s ids), so a run's merge does not wait out its own loads
-            constexpr uint32_t PF = ROUNDS ? (PREPLY_PF ? PREPLY_PF : 1) : 1;
-            uint64_t pfv[PF][SPL];
-            uint32_t pfa[PF];
-            uint64_t pleft = 0;                          // runs not yet issued
-            auto pf_issue = [&](uint32_t q) {
-                pfa[q] = NONE32;
-                if (!pleft) return;
-                const uint32_t x = (uint32_t)__builtin_ctzll(pleft);
-                pleft &= pleft - 1;
-                pfa[q] = x;
-                const uint64_t ent = rl64(fw0, x), w1 = rl64(fw1, x);
-                const int cnt = (int)((w1 >> 32) & 0xFFFF), st0 = (int)((w1 >> 48) & 0xFF);
-#pragma unroll
-                for (uint32_t j = 0; j < SPL; ++j) {
-                    const int d = (int)(lane + 64 * j) - st0;
-                    pfv[q][j] = d >= 0 && d < cnt ? v.r_pid[ent + d] : 0;
-                }
-            };
-            if (ROUNDS && PREPLY_PF) {
-                const uint32_t fl0 = (uint32_t)(fw1 >> 56);
-                pleft = __ballot(lane < nf && (fl0 >> 4) == K_PREPLY && (fl0 & FR_DENSE) && (fflag & F_COUNTED));
-#pragma unroll
-                for (uint32_t q = 0; q < PF; ++q) pf_issue(q);
-            }
             // the window's events that can act:
             // a rejected PREPARE, or a member E_EPOCH that neither deletes nor recreates the
             // node's Acceptor (nor, with rounds, resets its Proposer), changes nothing here
@@ -2320,21 +2287,12 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             }
                     } else if (ROUNDS && kind == K_PREPLY) {
                         if (mf & F_COUNTED) {
-                            // the run's proposal ids: loaded ahead (a dense run), or all in flight now
+                            // the run's proposal ids all in flight, then the merge (loading the next
+                            // runs' ids ahead, 1 or 2 deep, measured slower: C3 step 1.366 / 1.452 vs
+                            // 1.270 ms — the registers spill; profiles/r04_v12_ab_preply_prefetch.json)
                             uint64_t pid[SPL];
-                            bool got = false;
 #pragma unroll
-                            for (uint32_t q = 0; q < PF; ++q)
-                                if (ROUNDS && PREPLY_PF && pfa[q] == a) {
-#pragma unroll
-                                    for (uint32_t j = 0; j < SPL; ++j) pid[j] = pfv[q][j];
-                                    got = true;
-                                    pf_issue(q);                 // the slot takes the next run
-                                }
-                            if (!got) {
-#pragma unroll
-                                for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
-                            }
+                            for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
                                 if (k[j] >= 0) {
