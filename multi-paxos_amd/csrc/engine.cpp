@@ -1562,6 +1562,25 @@ struct PEv {
 };
 typedef std::vector<std::vector<PEv>> PEvents;
 
+// a node's P_PROPOSE records (HostTrace::prop_seq, kept off the device) merged into its
+// events by record index
+static void merge_proposals(const mpx_engine *e, uint32_t n, std::vector<PEv> &evs)
+{
+    const HostTrace &h = e->ht;
+    if (h.prop_off.size() <= n + 1 || h.prop_off[n + 1] == h.prop_off[n]) return;
+    const uint64_t base = e->incremental ? e->win_seq_base[n] : 0;
+    std::vector<PEv> out;
+    out.reserve(evs.size() + (h.prop_off[n + 1] - h.prop_off[n]));
+    size_t i = 0;
+    for (uint64_t k = h.prop_off[n]; k < h.prop_off[n + 1]; ++k) {
+        const uint64_t sq = h.prop_seq[k] + base;
+        while (i < evs.size() && evs[i].seq < sq) out.push_back(std::move(evs[i++]));
+        out.push_back(PEv{sq, MPX_MSG_P_PROPOSE, {}});
+    }
+    while (i < evs.size()) out.push_back(std::move(evs[i++]));
+    evs.swap(out);
+}
+
 static void proposer_events(mpx_engine *e, const Results &r, PEvents &ev)
 {
     const HostTrace &h = e->ht;
@@ -1571,7 +1590,7 @@ static void proposer_events(mpx_engine *e, const Results &r, PEvents &ev)
         for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
             const uint8_t t = h.m_type[g];
             const bool quorum = t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM);
-            if (t != MPX_MSG_P_PROPOSE && t != MPX_MSG_P_START && t != MPX_MSG_COMMIT && !quorum) continue;
+            if (t != MPX_MSG_P_START && t != MPX_MSG_COMMIT && !quorum) continue;
             PEv x{seq_of(h, n, g) + (e->incremental ? e->win_seq_base[n] : 0), t, {}};
             if (t == MPX_MSG_COMMIT)
                 for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) x.ents.push_back({h.e_iid[k], h.e_val[k]});
@@ -1583,6 +1602,7 @@ static void proposer_events(mpx_engine *e, const Results &r, PEvents &ev)
             }
             ev[n].push_back(std::move(x));
         }
+    for (uint32_t n = 0; n < N; ++n) merge_proposals(e, n, ev[n]);
 }
 
 // The proposer's bookkeeping of one node, advanced over its events in stream order (a whole
@@ -1704,7 +1724,7 @@ static int proposer_decisions(mpx_engine *e, const Results &r, std::string &d)
 
 static bool has_proposals(const HostTrace &h)
 {
-    return std::find(h.m_type.begin(), h.m_type.end(), (uint8_t)MPX_MSG_P_PROPOSE) != h.m_type.end();
+    return !h.prop_seq.empty();
 }
 
 // Member semantics (member/paxos.cpp:1183-1297): the same batch over the proposer's
@@ -1730,7 +1750,7 @@ static int member_events(mpx_engine *e, const Results &r, PEvents &ev)
         for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
             const uint8_t t = h.m_type[g];
             const bool quorum = t == MPX_MSG_PREPARE_REPLY && (r.flags[g] & F_QUORUM);
-            if (t != MPX_MSG_P_PROPOSE && t != MPX_MSG_P_START && t != MPX_MSG_COMMIT && t != MPX_MSG_E_EPOCH && !quorum)
+            if (t != MPX_MSG_P_START && t != MPX_MSG_COMMIT && t != MPX_MSG_E_EPOCH && !quorum)
                 continue;
             PEv x{seq_of(h, n, g) + (e->incremental ? e->win_seq_base[n] : 0), t, {}};
             if (t == MPX_MSG_E_EPOCH) x.aux = h.m_ver[g];
@@ -1744,6 +1764,7 @@ static int member_events(mpx_engine *e, const Results &r, PEvents &ev)
             }
             ev[n].push_back(std::move(x));
         }
+    for (uint32_t n = 0; n < N; ++n) merge_proposals(e, n, ev[n]);
     return MPX_OK;
 }
 

@@ -85,6 +85,32 @@ long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle)
     const uint64_t value_id = rd64(p + 4);
     const bool noop = p[12] != 0;
     if (proposer >= (1u << 14) || value_id >= (1ull << 47)) return MPX_E_RANGE;
+    {
+        // the canonical bytes are the wire bytes themselves when every bool is 0 / 1 (a plain
+        // payload Value or a noop): compare / append the span, no encoding buffer
+        size_t used = 0;
+        uint32_t eo = 0, el = 0;
+        if (p[12] == 1) used = 13;
+        else if (p[12] == 0 && avail >= 18 && p[13] == 0) {
+            el = rd32(p + 14);
+            if (avail < 18 + (size_t)el) return MPX_E_DECODE;
+            used = 18 + el;
+            eo = 18;
+        }
+        if (used) {
+            const uint64_t h = MPX_HANDLE(proposer, noop, value_id);
+            auto it = idx.find(h);
+            if (it != idx.end()) {
+                const Rec &r = it->second;
+                if (r.len != used || std::memcmp(bytes.data() + r.off, p, used) != 0) return MPX_E_VALUE;
+            } else {
+                idx.emplace(h, Rec{bytes.size(), (uint32_t)used, eo, el});
+                bytes.append((const char *)p, used);
+            }
+            *handle = h;
+            return (long)used;
+        }
+    }
     std::string enc;
     enc.reserve(32);
     app<uint32_t>(enc, proposer);
@@ -813,9 +839,15 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         // the device from the E_EPOCH markers and the epoch table (kernels.hip
         // k_gate_*); ingest only lists the markers and keeps every record
         if (member) ht.ee_off[n] = ht.ee_msg.size();
+        if (ht.prop_off.empty()) ht.prop_off.assign(N + 1, 0);
+        ht.prop_off[n] = ht.prop_seq.size();
         for (size_t k = 0; k < ns.type.size(); ++k) {
             const uint32_t g = (uint32_t)ht.m_type.size();
             const uint8_t t = ns.type[k];
+            if (t == MPX_MSG_P_PROPOSE) {               // the proposer's bookkeeping only (engine.cpp)
+                ht.prop_seq.push_back((uint32_t)k);
+                continue;
+            }
             if (member && t == MPX_MSG_E_EPOCH && ns.ver[k] >= epochs.size()) return MPX_E_DECODE;
             // Header sharding: a record whose entries all belong to
             // other shards is left out here — ACCEPT / COMMIT / P_BATCH with no
@@ -1001,6 +1033,8 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     }
     ht.node_off[N] = ht.m_type.size();
     sc_off[N] = ht.sc_type.size();
+    if (ht.prop_off.empty()) ht.prop_off.assign(N + 1, 0);
+    ht.prop_off[N] = ht.prop_seq.size();
     if (member) {
         ht.ee_off[N] = ht.ee_msg.size();
         ht.sc_off = sc_off;

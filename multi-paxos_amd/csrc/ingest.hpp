@@ -89,6 +89,11 @@ struct HostTrace {
     std::vector<uint64_t> m_ballot, m_aux, m_ent;
     std::vector<uint64_t> node_off;
     std::vector<uint32_t> m_seq;                    // record index in its node's submitted stream
+    // P_PROPOSE records (the proposers' client values: host bookkeeping only, no device work):
+    // per node [prop_off[n], prop_off[n + 1]) of prop_seq, their record indices; they are not in
+    // the device's message arrays
+    std::vector<uint64_t> prop_off;
+    std::vector<uint32_t> prop_seq;
     uint64_t dropped = 0;                           // records of other shards left out (header sharding)
     uint64_t part_dropped = 0;                      // ... of them, records whose entries all lie in other shards
     std::vector<uint32_t> chunk_node, node_chunk_off;
