@@ -759,7 +759,16 @@ static int queue_run(mpx_engine *e, bool digest)
     if (ev) for (int k = 0; k < 5; ++k) evp[k] = ev->e[k];
     if (ev) ev->store_last = run_ends_with_store(e->view);
     if (!e->stream2) {
-        HTRY(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+        // the side stream gets a hardware queue of its own: a stream of another priority draws
+        // from that priority's queue pool, so it never shares the plan path's queue — which
+        // serialises the two — when the process holds more streams than GPU_MAX_HW_QUEUES
+        // (MPX_SIDE_PRIO=normal|low|high, A/B)
+        int least = 0, greatest = 0;
+        HTRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        const char *sp = std::getenv("MPX_SIDE_PRIO");
+        const std::string pr = sp ? sp : "low";
+        const int prio = pr == "high" ? greatest : pr == "normal" ? 0 : least;
+        HTRY(hipStreamCreateWithPriority(&e->stream2, hipStreamNonBlocking, prio));
         HTRY(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
         HTRY(hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming));
     }
