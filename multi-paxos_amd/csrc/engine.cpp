@@ -103,6 +103,7 @@ struct mpx_engine {
     DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy, exec_aux, exec_out;
     DevBuf gp_dyn, gp_dyn_n;                // list plan path: the pairs k_plan_list lists for k_apply
     DevBuf gp_ext, gp_ext_n;                //   ... and those it describes by 5..8 segments (k_store_ext)
+    DevBuf gp_chk, gp_chk_n;                //   ... and its planned pairs whose re-commits need the Value check
     DevBuf decode_buf;                      // readback scratch (k_decode)
     DevBuf out, out_cursor, partials, viol, summary;
     uint64_t out_cap = 0;
@@ -478,6 +479,10 @@ static int finish_view(mpx_engine *e)
     TRY(e->gp_ext_n.alloc(8));
     v.gp_ext = e->gp_ext.as<uint64_t>();
     v.gp_ext_n = e->gp_ext_n.as<unsigned long long>();
+    TRY(e->gp_chk.alloc(std::max<size_t>(8ull * CHK_WORDS * v.num_gp_snap, 8 * CHK_WORDS)));
+    TRY(e->gp_chk_n.alloc(8));
+    v.gp_chk = e->gp_chk.as<uint64_t>();
+    v.gp_chk_n = e->gp_chk_n.as<unsigned long long>();
     e->geom = launch_geometry(N, e->NB, e->num_cus);
 
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + std::max<uint64_t>(e->geom.chosen_wgs, e->num_cus * 16))));

@@ -397,6 +397,7 @@ __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64
         v.fast_rest[1] = 0;                          // k_chosen's last-block ticket
         *v.gp_dyn_n = 0;
         *v.gp_ext_n = 0;
+        *v.gp_chk_n = 0;
         if (v.window) *v.outv_n = 0;
         for (uint32_t pc = 0; pc < 8; ++pc)          // the counter words k_reduce's workgroups add into
             if (summary_word(pc) >= 0) v.summary[summary_word(pc)] = 0;
@@ -1607,11 +1608,13 @@ __device__ inline void emit_run(const DevView &v, uint32_t msg, uint32_t ref, ui
 // commit-covered slot, P = snapshot entries).
 //
 // The pair is listed for k_apply instead (gp_dyn, one append per wave) when: more than
-// F (16) runs, a run that is not a dense accept / commit run, a fifth segment, a
-// partial last bucket, or a commit / learn (member: also an accept) over a committed
-// segment whose Value entry differs (the reference's Value check: k_apply compares the
-// Values).  Nothing is emitted for a listed pair: the walk runs once to decide, and a second
-// time to emit only when it emits and the pair is kept.  Promise-round pairs (GP_ROUNDS)
+// F (16) runs, a run that is not a dense accept / commit run, a fifth segment or a
+// partial last bucket.  A commit / learn (member: also an accept) over a committed segment
+// through another message's entries changes nothing there, but the reference compares the
+// Values (multi :1508, member :1765,1040): the pair stays planned and goes to the check list
+// (gp_chk, one append per wave), whose slots k_commit_check compares.  Nothing is emitted
+// for a listed pair: the walk runs once to decide, and a second time to emit only when it
+// emits and the pair is kept.  Promise-round pairs (GP_ROUNDS)
 // are never taken: the host range of the full k_apply has them.  MEMBER also plans the
 // chosen log (bucket i < NB, plan_chosen); multi's k_plan did.  The staged descriptor
 // words carry the accept runs' scan flag (F_GRANTED) in bit 57 after the gather, so the
@@ -1676,6 +1679,7 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
         wave_lds_fence();
     }
     bool fb = false;                                   // list the pair for k_apply
+    bool ck = false;                                   // ... planned, its re-commits' Values to check
     bool xt = false;                                   // ... or for k_store_ext (xw0: split points, xw1: values)
     uint64_t xw0 = 0, xw1 = 0;
     if (i < np) {
@@ -1738,7 +1742,7 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
                             if (!sl[g] || lo[g] < st0 || lo[g] >= st0 + cnt) continue;
                             if (learn) l += sl[g];
                             if ((comm >> g) & 1) {
-                                if ((MEMBER || learn) && ent_at(k) != ent_at(fix[g])) fb = true;   // the Value check: k_apply
+                                if ((MEMBER || learn) && ent_at(k) != ent_at(fix[g])) ck = true;   // the Value check: k_commit_check
                                 // (multi: an ACCEPT over a committed instance is skipped, :1380)
                             } else if (learn) {
                                 comm |= 1u << g; pres |= 1u << g; fix[g] = k;
@@ -1850,6 +1854,16 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
             w[0] = oa; w[1] = o1; w[2] = e0; w[3] = e1; w[4] = i;
         }
     }
+    const uint64_t cm = __ballot(ck && !fb);
+    if (cm) {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(v.gp_chk_n, (unsigned long long)__popcll(cm));
+        base = __shfl(base, 0, 64);
+        if (ck && !fb) {
+            uint64_t *w = v.gp_chk + CHK_WORDS * (base + (uint64_t)__popcll(cm & ((1ull << lane) - 1)));
+            w[0] = oa; w[1] = o1; w[2] = i;
+        }
+    }
     const uint64_t xm = __ballot(xt && !fb);
     if (xm) {
         unsigned long long base = 0;
@@ -1904,6 +1918,62 @@ __global__ __launch_bounds__(256) void k_store_ext(DevView v)
         else
             *reinterpret_cast<u16x4 *>(static_cast<uint16_t *>(v.st) + at) =
                 u16x4{(uint16_t)val[0], (uint16_t)val[1], (uint16_t)val[2], (uint16_t)val[3]};
+    }
+}
+
+// The Value check of the planned pairs k_plan_list put on gp_chk, one wave per pair, 4 slots
+// per lane, the pair's runs in message order (k_apply's rules, without its state): the first
+// commit / learn of a slot fixes its entry; a later one through another entry (member: also
+// a granted accept; a learn only when its message is the proposer's own, F_PROP) whose Value
+// differs is the violation k_apply records — MPX_V_COMMIT_VALUE (multi/paxos.cpp:1508),
+// MPX_V_LEARN_VALUE (member/paxos.cpp:1765,1040) — once per slot.  Plan-list pairs hold
+// dense accept / commit runs only.
+template <bool MEMBER>
+__global__ __launch_bounds__(256) void k_commit_check(DevView v)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t n_chk = *v.gp_chk_n, nwaves = (uint64_t)gridDim.x * 4;
+    for (uint64_t x = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < n_chk; x += nwaves) {
+        const uint64_t f0 = v.gp_chk[CHK_WORDS * x], f1 = v.gp_chk[CHK_WORDS * x + 1], i = v.gp_chk[CHK_WORDS * x + 2];
+        const uint32_t b = (uint32_t)(i / v.N), n = (uint32_t)(i - (uint64_t)b * v.N);
+        const uint64_t li0 = (uint64_t)b << BSH;
+        uint32_t se[SPL], cm = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) se[j] = 0;
+        for (uint64_t fi = f0; fi < f1; fi += 64) {
+            const uint32_t nf = (uint32_t)(f1 - fi < 64 ? f1 - fi : 64);
+            uint64_t fw0 = 0, fw1 = 0;
+            uint32_t mf = 0;
+            if (lane < nf) {
+                const ulonglong2 d = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
+                fw0 = d.x; fw1 = d.y;
+                if (MEMBER) mf = v.m_flags[(uint32_t)fw1];
+            }
+            for (uint32_t a = 0; a < nf; ++a) {
+                const uint64_t w1 = rl64(fw1, a);
+                const uint32_t kind = (uint32_t)(w1 >> 60);
+                const bool learn = kind == K_COMMIT;
+                const uint32_t f = MEMBER ? rl32(mf, a) : 0;
+                if (!learn && !(MEMBER && (f & F_GRANTED))) continue;
+                const bool check = MEMBER ? (!learn || (f & F_PROP)) : learn;
+                const uint64_t ent = rl64(fw0, a);
+                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                const uint32_t msg = (uint32_t)w1;
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) {
+                    const int d = (int)(lane + 64 * j) - (int)st0;
+                    if (d < 0 || d >= (int)cnt) continue;
+                    const uint32_t xe = (uint32_t)(ent + d);
+                    if ((cm >> j) & 1) {
+                        if (check && se[j] != xe && v.e_val[se[j]] != v.e_val[xe])
+                            record_violation(v, MEMBER ? MPX_V_LEARN_VALUE : MPX_V_COMMIT_VALUE, n, msg - (uint32_t)v.node_off[n],
+                                             v.shard_begin + li0 + lane + 64 * j);
+                    } else if (learn) {
+                        cm |= 1u << j; se[j] = xe;
+                    }
+                }
+            }
+        }
     }
 }
 
@@ -3432,6 +3502,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
             // 96 % of member list pairs have at most 4, tools/pair_stats.cpp)
             hipExtLaunchKernelGGL(k_plan_list<true>, dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+            hipLaunchKernelGGL(k_commit_check<true>, dim3(g.chosen_wgs), dim3(256), 0, s, v);
         } else {
             // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
             // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
@@ -3445,6 +3516,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
                 hipLaunchKernelGGL((k_plan_list<false, PLAN_XSEG, PLAN_XFRAGS>), dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
                 hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);
 #endif
+                hipLaunchKernelGGL(k_commit_check<false>, dim3(g.chosen_wgs), dim3(256), 0, s, v);
             }
         }
         // every pair the trace marks lean (pair_gp 0) is one k_plan can describe (ingest.cpp /

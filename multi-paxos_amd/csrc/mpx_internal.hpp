@@ -253,6 +253,11 @@ struct DevView {
     // (EXT_WORDS per item) for k_store_ext; gp_ext_n counts them
     uint64_t *gp_ext;
     unsigned long long *gp_ext_n;
+    // ... and the planned pairs where a commit / learn (member: also an accept) meets a committed
+    // segment through another message's entries: {first run, end run, pair} (CHK_WORDS per item)
+    // for k_commit_check, which compares their Values slot by slot; gp_chk_n counts them
+    uint64_t *gp_chk;
+    unsigned long long *gp_chk_n;
     const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
     const uint32_t *ev_msg;
     // promise-quorum chunks (k_prop_chunk / k_prop_node): PROP_CHUNK records of one
@@ -355,6 +360,7 @@ constexpr uint32_t MPLAN_FRAGS = 16;
 constexpr uint32_t MPLAN_LDS = 1024;
 constexpr uint32_t PLAN_XSEG = 8;            // k_plan_list (multi): up to 8 segments, 32 runs per pair
 constexpr uint32_t PLAN_XFRAGS = 32;
+constexpr uint32_t CHK_WORDS = 3;           // gp_chk items
 constexpr uint32_t EXT_WORDS = 3;
 // the distinct run boundaries inside (0, 256), sorted into s[0..2] (BS = unused);
 // false once a fourth one appears

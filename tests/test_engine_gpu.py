@@ -413,6 +413,36 @@ def test_engine_member_violations():
         assert e.dump() == want
 
 
+def test_engine_commit_value_check_on_planned_pairs():
+    """Re-commits through other messages' entries on a whole bucket (the plan path keeps the
+    pair and k_commit_check compares the Values): an equal re-commit is silent, a different
+    Value is MPX_V_COMMIT_VALUE once per slot (multi/paxos.cpp:1508), as in the oracle."""
+    from handmade import B1, B2, B3, v
+    w = mpxwire
+    ent = [(i, v(i)) for i in range(4)]
+    t = w.container([[
+        w.prepare(0, B1),
+        w.accept(0, 1, B1, ent),
+        w.commit(0, 1, B1, ent),
+        w.commit(1, 9, B2, ent[1:3]),                                 # equal Values, other entries
+        w.commit(2, 4, B3, [(2, v(2, 2, 77)), (3, v(3, 2, 78))]),     # two slots differ
+        w.accept(1, 2, B2, [(1, v(1, 1, 90)), (2, v(2, 1, 91))]),     # over committed: skipped
+        w.commit(1, 10, B2, ent[:2]),
+    ], [w.prepare(0, B1), w.accept(0, 1, B1, ent)], []], 256)
+    want, ostats, _ = oracle_run(t)
+    assert ostats[4] == 2
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        assert e.dump() == want
+    assert st["violations"] == 2
+    with mpx.Engine.for_trace(t) as e:
+        e.step()
+        e.sync()
+        st = e.stats()
+        assert st["violations"] == 2 and e.violation()["code"] == 1   # MPX_V_COMMIT_VALUE
+        assert e.dump() == want
+
+
 @pytest.mark.parametrize("shards", [2, 3])
 def test_engine_member_sharded_matches_oracle_restricted(shards):
     """Instance shards of a member trace: headers (and so roles, versions, scalars,

@@ -163,6 +163,90 @@ int main(int argc, char **argv)
                     (unsigned long long)lst, (unsigned long long)cov[0], (unsigned long long)cov[1],
                     (unsigned long long)cov[2], (unsigned long long)cov[3]);
     }
+    // walk lengths (runs + events) of the pairs left on k_apply: the listed pairs a (32, 8) plan
+    // cannot describe (AM_SNAP) and the promise-round pairs (AM_FULL) — tail versus throughput
+    {
+        std::vector<uint64_t> snapw, fullw;
+        for (uint64_t it = 0; it < h.gp_list.size(); ++it) {
+            const uint64_t q = h.gp_list[it];
+            const uint64_t f0 = h.f_off[q], f1 = h.f_off[q + 1], e0 = h.ev_off[q], e1 = h.ev_off[q + 1];
+            if (it >= h.num_gp_snap) { fullw.push_back(f1 - f0 + e1 - e0); continue; }
+            bool dense = true;
+            std::vector<uint32_t> bnd;
+            for (uint64_t f = f0; f < f1; ++f) {
+                const Frag &fr = h.frags[f];
+                const uint32_t kind = fr.flags >> 4;
+                if (!(fr.flags & FR_DENSE) || (kind != K_ACCEPT && kind != K_COMMIT)) dense = false;
+                if (fr.start) bnd.push_back(fr.start);
+                if (fr.start + fr.count < BS) bnd.push_back(fr.start + fr.count);
+            }
+            std::sort(bnd.begin(), bnd.end());
+            bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+            if (!(dense && f1 - f0 <= 32 && bnd.size() + 1 <= 8)) snapw.push_back(f1 - f0 + e1 - e0);
+        }
+        for (int k = 0; k < 2; ++k) {
+            std::vector<uint64_t> &w = k ? fullw : snapw;
+            std::sort(w.begin(), w.end());
+            uint64_t sum = 0;
+            for (uint64_t x : w) sum += x;
+            auto pc = [&](double f) { return w.empty() ? 0ull : (unsigned long long)w[(size_t)(f * (w.size() - 1))]; };
+            std::printf("%s pairs %zu: steps (runs + events) sum %llu, p50 %llu p90 %llu p99 %llu p99.9 %llu max %llu\n",
+                        k ? "AM_FULL" : "AM_SNAP (not (32, 8)-plannable)", w.size(), (unsigned long long)sum, pc(0.5),
+                        pc(0.9), pc(0.99), pc(0.999), pc(1.0));
+        }
+    }
+    // k_plan_list stages a wave's (64 consecutive pairs') descriptor words in LDS, MPLAN_LDS per
+    // wave: the GP_LIST pairs a (32, 8) plan could take that the staging window leaves out
+    {
+        uint64_t over = 0, wmax = 0;
+        for (uint64_t w0 = 0; w0 < NP; w0 += 64) {
+            const uint64_t wb = h.f_off[w0], we = h.f_off[std::min<uint64_t>(w0 + 64, NP)];
+            wmax = std::max<uint64_t>(wmax, we - wb);
+            for (uint64_t q = w0; q < std::min<uint64_t>(w0 + 64, NP); ++q)
+                if (h.pair_gp[q] == GP_LIST && h.f_off[q + 1] - h.f_off[q] <= 32 &&
+                    h.f_off[q + 1] - wb > MPLAN_LDS) ++over;
+        }
+        std::printf("GP_LIST pairs (<= 32 runs) past a wave's %u-word LDS window: %llu (max runs per wave %llu)\n",
+                    MPLAN_LDS, (unsigned long long)over, (unsigned long long)wmax);
+    }
+    // k_plan_list's Value check: a COMMIT over a committed segment whose entry index differs
+    // lists the pair for k_apply; how many (32, 8)-shaped pairs that is, and how many of them
+    // carry equal Values (handles) on every such slot
+    {
+        uint64_t shaped = 0, recommit = 0, equal = 0;
+        for (uint64_t it = 0; it < h.num_gp_snap; ++it) {
+            const uint64_t q = h.gp_list[it];
+            const uint64_t f0 = h.f_off[q], f1 = h.f_off[q + 1];
+            bool dense = f1 - f0 <= 32;
+            std::vector<uint32_t> bnd;
+            for (uint64_t f = f0; f < f1; ++f) {
+                const Frag &fr = h.frags[f];
+                const uint32_t kind = fr.flags >> 4;
+                if (!(fr.flags & FR_DENSE) || (kind != K_ACCEPT && kind != K_COMMIT)) dense = false;
+                if (fr.start) bnd.push_back(fr.start);
+                if (fr.start + fr.count < BS) bnd.push_back(fr.start + fr.count);
+            }
+            std::sort(bnd.begin(), bnd.end());
+            bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+            if (!dense || bnd.size() + 1 > 8) continue;
+            ++shaped;
+            int64_t fix[BS];
+            for (uint32_t s = 0; s < BS; ++s) fix[s] = -1;
+            bool rc = false, eq = true;
+            for (uint64_t f = f0; f < f1; ++f) {
+                const Frag &fr = h.frags[f];
+                if ((fr.flags >> 4) != K_COMMIT) continue;
+                for (uint32_t s = fr.start; s < (uint32_t)fr.start + fr.count; ++s) {
+                    const uint64_t x = fr.entry + (s - fr.start);
+                    if (fix[s] < 0) { fix[s] = (int64_t)x; continue; }
+                    if ((uint64_t)fix[s] != x) { rc = true; eq = eq && h.e_val[fix[s]] == h.e_val[x]; }
+                }
+            }
+            recommit += rc; equal += rc && eq;
+        }
+        std::printf("(32, 8)-shaped list pairs %llu: re-committed with another entry %llu, all such slots equal Values %llu\n",
+                    (unsigned long long)shaped, (unsigned long long)recommit, (unsigned long long)equal);
+    }
     std::printf("runs/pair:");
     for (auto &x : runs_h) std::printf(" %llu:%llu", (unsigned long long)x.first, (unsigned long long)x.second);
     std::printf("\ninterior boundaries/pair:");
