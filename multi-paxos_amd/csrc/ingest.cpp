@@ -710,6 +710,62 @@ struct EntryPool {
     }
 };
 
+// Per pair of dense accept / commit runs (the pairs k_plan_list can plan): a commit / learn
+// (member: also an accept) run whose every slot an earlier commit run of the pair fixed, with
+// the same entries (iid, Value, member: proposal id) over its range, names that run's entries
+// (the pool's content addressing at bucket-run grain: a re-commit of the same Values through
+// another message — another proposer's COMMIT, multi/paxos.cpp:1494-1518 — then shares them);
+// a run that still meets a committed slot through another entry gets FR_VCHK, and only those
+// send their pair to the device's Value check (k_commit_check).
+static void mark_value_checks(HostTrace &ht, bool member)
+{
+    const uint64_t NP = (uint64_t)ht.N * ht.NB;
+    std::vector<uint32_t> fixr(BS);                   // per slot: pair-local committing run + 1
+    for (uint64_t p = 0; p < NP; ++p) {
+        const uint64_t f0 = ht.f_off[p], f1 = ht.f_off[p + 1];
+        if (f1 - f0 < 2) continue;
+        uint32_t commits = 0;
+        bool plain = true;
+        for (uint64_t f = f0; f < f1 && plain; ++f) {
+            const uint32_t kind = ht.frags[f].flags >> 4;
+            plain = (ht.frags[f].flags & FR_DENSE) && (kind == K_ACCEPT || kind == K_COMMIT);
+            commits += kind == K_COMMIT;
+        }
+        if (!plain || !commits || (!member && commits < 2)) continue;
+        std::fill(fixr.begin(), fixr.end(), 0u);
+        for (uint64_t f = f0; f < f1; ++f) {
+            Frag &fr = ht.frags[f];
+            const bool learn = (fr.flags >> 4) == K_COMMIT;
+            const uint32_t st = fr.start, c = fr.count;
+            if (!learn && !member) continue;           // multi: an accept over a commit is skipped
+            const uint32_t j = fixr[st];
+            bool one = j != 0;
+            for (uint32_t s = st + 1; one && s < st + c; ++s) one = fixr[s] == j;
+            if (one) {
+                const Frag &fj = ht.frags[f0 + j - 1];
+                const uint64_t base = fj.entry + (st - fj.start);
+                if (base != fr.entry) {
+                    bool same = true;
+                    for (uint32_t d = 0; same && d < c; ++d)
+                        same = ht.e_iid[base + d] == ht.e_iid[fr.entry + d] && ht.e_val[base + d] == ht.e_val[fr.entry + d] &&
+                               (!member || ht.e_pid[base + d] == ht.e_pid[fr.entry + d]);
+                    if (same) fr.entry = base;
+                }
+            }
+            bool chk = false;
+            for (uint32_t s = st; s < st + c; ++s)
+                if (fixr[s]) {
+                    const Frag &fj = ht.frags[f0 + fixr[s] - 1];
+                    chk = chk || fj.entry - fj.start != fr.entry - fr.start;
+                }
+            if (chk) fr.flags |= FR_VCHK;
+            if (learn)
+                for (uint32_t s = st; s < st + c; ++s)
+                    if (!fixr[s]) fixr[s] = (uint32_t)(f - f0) + 1;
+        }
+    }
+}
+
 int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen,
                 const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc)
 {
@@ -1073,6 +1129,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         std::vector<uint64_t> pos(ht.f_off.begin(), ht.f_off.end() - 1);
         for (auto &x : fr) ht.frags[pos[x.key]++] = x.f;
     }
+    if (!wc) mark_value_checks(ht, member);
     ht.cf_off.assign(NB + 1, 0);
     for (uint64_t i = 0; i < NB; ++i) {
         ht.cf_off[i + 1] = ht.cf_off[i] + cfcount[i];

@@ -1719,12 +1719,6 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
                     lo[g] = g ? sp[g - 1] : 0;
                     sl[g] = lo[g] >= BS ? 0 : (g < LSEG - 1 ? sp[g] : BS) - lo[g];
                 }
-                // the entry index of run k at slot s, minus s (the pool is
-                // content-addressed: equal ones name one Value; read only over a
-                // committed segment)
-                auto ent_at = [&](uint32_t k) -> uint64_t {
-                    return v.frags[oa + k].entry - ((W[k] >> 48) & 0xFF);
-                };
                 const uint64_t blo = v.shard_begin + (b << BSH);
                 // one pass over the pair in message order; EMIT: the second pass, which
                 // writes the snapshot records (the first one decided the pair is kept)
@@ -1742,7 +1736,8 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
                             if (!sl[g] || lo[g] < st0 || lo[g] >= st0 + cnt) continue;
                             if (learn) l += sl[g];
                             if ((comm >> g) & 1) {
-                                if ((MEMBER || learn) && ent_at(k) != ent_at(fix[g])) ck = true;   // the Value check: k_commit_check
+                                // through another entry (ingest's FR_VCHK): the Value check, k_commit_check
+                                if ((MEMBER || learn) && ((w >> 56) & FR_VCHK)) ck = true;
                                 // (multi: an ACCEPT over a committed instance is skipped, :1380)
                             } else if (learn) {
                                 comm |= 1u << g; pres |= 1u << g; fix[g] = k;
@@ -1937,42 +1932,64 @@ __global__ __launch_bounds__(256) void k_commit_check(DevView v)
         const uint64_t f0 = v.gp_chk[CHK_WORDS * x], f1 = v.gp_chk[CHK_WORDS * x + 1], i = v.gp_chk[CHK_WORDS * x + 2];
         const uint32_t b = (uint32_t)(i / v.N), n = (uint32_t)(i - (uint64_t)b * v.N);
         const uint64_t li0 = (uint64_t)b << BSH;
-        uint32_t se[SPL], cm = 0;
+        // plan-list pairs have at most PLAN_XFRAGS (32) runs: one descriptor window
+        const uint32_t nf = (uint32_t)(f1 - f0 < 64 ? f1 - f0 : 64);
+        uint64_t fw0 = 0, fw1 = 0;
+        uint32_t mf = 0;
+        if (lane < nf) {
+            const ulonglong2 d = *reinterpret_cast<const ulonglong2 *>(v.frags + f0 + lane);
+            fw0 = d.x; fw1 = d.y;
+            if (MEMBER) mf = v.m_flags[(uint32_t)fw1];
+        }
+        // pass 1 (no loads): each slot's first commit / learn — its entry and run
+        uint32_t se[SPL], sa[SPL];
 #pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) se[j] = 0;
-        for (uint64_t fi = f0; fi < f1; fi += 64) {
-            const uint32_t nf = (uint32_t)(f1 - fi < 64 ? f1 - fi : 64);
-            uint64_t fw0 = 0, fw1 = 0;
-            uint32_t mf = 0;
-            if (lane < nf) {
-                const ulonglong2 d = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
-                fw0 = d.x; fw1 = d.y;
-                if (MEMBER) mf = v.m_flags[(uint32_t)fw1];
+        for (uint32_t j = 0; j < SPL; ++j) { se[j] = 0; sa[j] = 64; }
+        for (uint32_t a = 0; a < nf; ++a) {
+            const uint64_t w1 = rl64(fw1, a);
+            if ((uint32_t)(w1 >> 60) != K_COMMIT) continue;
+            const uint32_t ent = (uint32_t)rl64(fw0, a);
+            const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+#pragma unroll
+            for (uint32_t j = 0; j < SPL; ++j) {
+                const int d = (int)(lane + 64 * j) - (int)st0;
+                if (d >= 0 && d < (int)cnt && sa[j] == 64) { se[j] = ent + d; sa[j] = a; }
             }
-            for (uint32_t a = 0; a < nf; ++a) {
+        }
+        uint64_t sv[SPL];
+#pragma unroll
+        for (uint32_t j = 0; j < SPL; ++j) sv[j] = sa[j] < 64 ? v.e_val[se[j]] : 0;
+        // pass 2: the later checked runs over committed slots through another entry, four runs'
+        // Values in flight at a time
+        for (uint32_t a0 = 0; a0 < nf; a0 += 4) {
+            uint64_t xv[4][SPL];
+            uint32_t xm[4];
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) {
+                xm[r] = 0;
+                const uint32_t a = a0 + r;
+                if (a >= nf) continue;
                 const uint64_t w1 = rl64(fw1, a);
-                const uint32_t kind = (uint32_t)(w1 >> 60);
-                const bool learn = kind == K_COMMIT;
+                const bool learn = (uint32_t)(w1 >> 60) == K_COMMIT;
                 const uint32_t f = MEMBER ? rl32(mf, a) : 0;
-                if (!learn && !(MEMBER && (f & F_GRANTED))) continue;
-                const bool check = MEMBER ? (!learn || (f & F_PROP)) : learn;
-                const uint64_t ent = rl64(fw0, a);
+                if (!(MEMBER ? (learn ? (f & F_PROP) != 0 : (f & F_GRANTED) != 0) : learn)) continue;
+                const uint32_t ent = (uint32_t)rl64(fw0, a);
                 const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
-                const uint32_t msg = (uint32_t)w1;
 #pragma unroll
                 for (uint32_t j = 0; j < SPL; ++j) {
                     const int d = (int)(lane + 64 * j) - (int)st0;
-                    if (d < 0 || d >= (int)cnt) continue;
-                    const uint32_t xe = (uint32_t)(ent + d);
-                    if ((cm >> j) & 1) {
-                        if (check && se[j] != xe && v.e_val[se[j]] != v.e_val[xe])
-                            record_violation(v, MEMBER ? MPX_V_LEARN_VALUE : MPX_V_COMMIT_VALUE, n, msg - (uint32_t)v.node_off[n],
-                                             v.shard_begin + li0 + lane + 64 * j);
-                    } else if (learn) {
-                        cm |= 1u << j; se[j] = xe;
-                    }
+                    const bool c = d >= 0 && d < (int)cnt && sa[j] < a && ent + d != se[j];
+                    xv[r][j] = c ? v.e_val[ent + d] : 0;
+                    xm[r] |= (uint32_t)c << j;
                 }
             }
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r)
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j)
+                    if (((xm[r] >> j) & 1) && xv[r][j] != sv[j])
+                        record_violation(v, MEMBER ? MPX_V_LEARN_VALUE : MPX_V_COMMIT_VALUE, n,
+                                         (uint32_t)rl64(fw1, a0 + r) - (uint32_t)v.node_off[n], v.shard_begin + li0 + lane + 64 * j);
         }
     }
 }

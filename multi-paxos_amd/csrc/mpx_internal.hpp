@@ -125,7 +125,10 @@ enum : uint8_t {
 
 // fragment kinds (Frag::flags >> 4)
 enum : uint8_t { K_ACCEPT = 0, K_COMMIT = 1, K_PREPLY = 2, K_BATCH = 3 };
-enum : uint8_t { FR_DENSE = 1 };
+// FR_VCHK (ingest): a commit / learn (member: also an accept) run that meets a slot committed
+// earlier in its pair through another entry — the Value check (k_commit_check) has work there.
+// (flags bit 1 stays free: k_plan_list's staged words carry F_GRANTED in it, MP_GRANTED)
+enum : uint8_t { FR_DENSE = 1, FR_VCHK = 4 };
 
 struct Frag {
     uint64_t entry;      // first entry in its pool

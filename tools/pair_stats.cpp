@@ -3,6 +3,7 @@
 // plan path (how many pairs one plan word can describe, events per pair).
 //   tools/pair_stats <member|faulty> <log2 instances>
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -61,8 +62,10 @@ int main(int argc, char **argv)
         pos = (pos + 7) & ~(size_t)7;
     }
     HostTrace h;
+    const auto t_b0 = std::chrono::steady_clock::now();
     rc = build_trace(nodes, 0, M, member ? ep : std::vector<mpx_epoch>(), h);
     if (rc) { std::fprintf(stderr, "build rc %d\n", rc); return 1; }
+    std::printf("build_trace %.3f s\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - t_b0).count());
     const uint64_t NP = (uint64_t)N * h.NB;
     uint64_t with = 0, gp = 0, preply = 0, sparse = 0, shape_ok = 0, ev_tot = 0, ev_prep = 0, ev_epoch = 0, ev_other = 0;
     std::map<uint64_t, uint64_t> runs_h, splits_h, ev_h;
@@ -213,7 +216,7 @@ int main(int argc, char **argv)
     // lists the pair for k_apply; how many (32, 8)-shaped pairs that is, and how many of them
     // carry equal Values (handles) on every such slot
     {
-        uint64_t shaped = 0, recommit = 0, equal = 0;
+        uint64_t shaped = 0, recommit = 0, equal = 0, vchk = 0;
         for (uint64_t it = 0; it < h.num_gp_snap; ++it) {
             const uint64_t q = h.gp_list[it];
             const uint64_t f0 = h.f_off[q], f1 = h.f_off[q + 1];
@@ -243,9 +246,13 @@ int main(int argc, char **argv)
                 }
             }
             recommit += rc; equal += rc && eq;
+            bool vb = false;
+            for (uint64_t f = f0; f < f1; ++f) vb = vb || (h.frags[f].flags & FR_VCHK);
+            vchk += vb;
         }
-        std::printf("(32, 8)-shaped list pairs %llu: re-committed with another entry %llu, all such slots equal Values %llu\n",
-                    (unsigned long long)shaped, (unsigned long long)recommit, (unsigned long long)equal);
+        std::printf("(32, 8)-shaped list pairs %llu: re-committed with another entry %llu, all such slots equal Values %llu; "
+                    "with an FR_VCHK run (after ingest's aliasing) %llu\n",
+                    (unsigned long long)shaped, (unsigned long long)recommit, (unsigned long long)equal, (unsigned long long)vchk);
     }
     std::printf("runs/pair:");
     for (auto &x : runs_h) std::printf(" %llu:%llu", (unsigned long long)x.first, (unsigned long long)x.second);
