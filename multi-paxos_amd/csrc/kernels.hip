@@ -3515,10 +3515,11 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
     const uint32_t plan_blocks = cdiv((uint64_t)v.N * v.NB, 256);
     if (plan_path) {
         if (member) {
-            // (member keeps 4 segments: its 8-segment build spills 80 VGPRs — plan_chosen — and
-            // 96 % of member list pairs have at most 4, tools/pair_stats.cpp)
-            hipExtLaunchKernelGGL(k_plan_list<true>, dim3(plan_blocks), dim3(256), 0, s,
+            // (8 segments / 32 runs since the Value check left the walk — 128 VGPRs, no spill:
+            // C5 0.451 -> 0.384 ms, contended C5 2.745 -> 2.582 ms, profiles/r04_v25_ab_member_plan8.json)
+            hipExtLaunchKernelGGL((k_plan_list<true, PLAN_XSEG, PLAN_XFRAGS>), dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+            hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);
             hipLaunchKernelGGL(k_commit_check<true>, dim3(g.chosen_wgs), dim3(256), 0, s, v);
         } else {
             // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and

@@ -361,7 +361,7 @@ enum : uint8_t { GP_LIST = 1, GP_ROUNDS = 2 };
 // k_plan_list: runs per pair it plans (walked from LDS) and runs a wave stages
 constexpr uint32_t MPLAN_FRAGS = 16;
 constexpr uint32_t MPLAN_LDS = 1024;
-constexpr uint32_t PLAN_XSEG = 8;            // k_plan_list (multi): up to 8 segments, 32 runs per pair
+constexpr uint32_t PLAN_XSEG = 8;            // k_plan_list: up to 8 segments, 32 runs per pair
 constexpr uint32_t PLAN_XFRAGS = 32;
 constexpr uint32_t CHK_WORDS = 3;           // gp_chk items
 constexpr uint32_t EXT_WORDS = 3;

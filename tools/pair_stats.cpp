@@ -27,6 +27,7 @@ int main(int argc, char **argv)
     p.num_instances = 1ull << lg;
     if (member) {
         p.kind = MPX_GEN_MEMBER; p.num_nodes = 8; p.batch = 256; p.drop_rate = 100; p.dup_rate = 100;
+        p.proposers = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 0;
         p.max_delay = 64; p.noop_permille = 15;
     } else {
         p.kind = MPX_GEN_FAULTY; p.num_nodes = 7; p.batch = 256; p.proposers = 3; p.drop_rate = 500;
@@ -197,6 +198,23 @@ int main(int argc, char **argv)
                         k ? "AM_FULL" : "AM_SNAP (not (32, 8)-plannable)", w.size(), (unsigned long long)sum, pc(0.5),
                         pc(0.9), pc(0.99), pc(0.999), pc(1.0));
         }
+    }
+    // the promise-round pairs' runs by kind and density, and their events by type
+    {
+        uint64_t k_n[4] = {0, 0, 0, 0}, k_sp[4] = {0, 0, 0, 0}, k_ent[4] = {0, 0, 0, 0}, evq = 0;
+        for (uint64_t it = h.num_gp_snap; it < h.gp_list.size(); ++it) {
+            const uint64_t q = h.gp_list[it];
+            for (uint64_t f = h.f_off[q]; f < h.f_off[q + 1]; ++f) {
+                const Frag &fr = h.frags[f];
+                const uint32_t kind = (fr.flags >> 4) & 3;
+                k_n[kind]++; k_sp[kind] += !(fr.flags & FR_DENSE); k_ent[kind] += fr.count;
+            }
+            evq += h.ev_off[q + 1] - h.ev_off[q];
+        }
+        for (uint32_t k = 0; k < 4; ++k)
+            std::printf("AM_FULL runs of kind %u: %llu (sparse %llu, entries %llu)\n", k, (unsigned long long)k_n[k],
+                        (unsigned long long)k_sp[k], (unsigned long long)k_ent[k]);
+        std::printf("AM_FULL events %llu\n", (unsigned long long)evq);
     }
     // k_plan_list stages a wave's (64 consecutive pairs') descriptor words in LDS, MPLAN_LDS per
     // wave: the GP_LIST pairs a (32, 8) plan could take that the staging window leaves out
