@@ -1656,19 +1656,30 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
     const uint64_t oa = v.f_off[ic], o1 = v.f_off[in];
     const uint64_t e0 = v.ev_off[ic], e1 = v.ev_off[in];
     const uint8_t gp = i < np ? v.pair_gp[i] : 0;
-    const uint64_t wbase = rl64(oa, 0);
+    // the wave's runs are one contiguous descriptor range, staged MPLAN_LDS words at a time: a
+    // pair whose runs end past the staged window waits for the next window, which starts at
+    // the first such pair (pairs are in lane order, their runs ascend), until every pair of
+    // the wave is decided (each window decides at least its first pair: len <= F)
+    const uint64_t wend = rl64(o1, 63);
+    const uint32_t len = (uint32_t)(o1 - oa);
+    uint64_t sbase = rl64(oa, 0);
+    bool todo = i < np;
+    bool fb = false;                                   // list the pair for k_apply
+    bool ck = false;                                   // ... planned, its re-commits' Values to check
+    bool xt = false;                                   // ... or for k_store_ext (xw0: split points, xw1: values)
+    uint64_t xw0 = 0, xw1 = 0;
+    for (;;) {
     {
-        // the wave's runs are one contiguous descriptor range: their second words
-        // into LDS with coalesced loads, all in flight before the LDS writes
-        const uint64_t wend = rl64(o1, 63);
-        const uint32_t R = (uint32_t)(wend - wbase < MPLAN_LDS ? wend - wbase : MPLAN_LDS);
+        // the window's second words into LDS with coalesced loads, all in flight before the
+        // LDS writes
+        const uint32_t R = (uint32_t)(wend - sbase < MPLAN_LDS ? wend - sbase : MPLAN_LDS);
         constexpr uint32_t K = 4;
         for (uint32_t r0 = 0; r0 < R; r0 += 64 * K) {
             uint64_t x[K];
 #pragma unroll
             for (uint32_t k = 0; k < K; ++k) {
                 const uint32_t r = r0 + lane + 64 * k;
-                x[k] = r < R ? v.frag_w1[wbase + r] : 0;
+                x[k] = r < R ? v.frag_w1[sbase + r] : 0;
             }
 #pragma unroll
             for (uint32_t k = 0; k < K; ++k) {
@@ -1678,13 +1689,11 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
         }
         wave_lds_fence();
     }
-    bool fb = false;                                   // list the pair for k_apply
-    bool ck = false;                                   // ... planned, its re-commits' Values to check
-    bool xt = false;                                   // ... or for k_store_ext (xw0: split points, xw1: values)
-    uint64_t xw0 = 0, xw1 = 0;
-    if (i < np) {
-        const uint32_t len = (uint32_t)(o1 - oa);
-        const uint64_t rel = oa - wbase, b = i / N;
+    const bool wait = MEMBER && todo && len && gp == GP_LIST && len <= F && (i / N + 1) * BS <= v.shard_len &&
+                      oa - sbase + len > MPLAN_LDS;
+    if (todo && !wait) {
+        todo = false;
+        const uint64_t rel = oa - sbase, b = i / N;
         uint64_t q = PLAN_SKIP;
         if (len && gp == GP_LIST) {
             bool ok = len <= F && rel + len <= MPLAN_LDS && (b + 1) * BS <= v.shard_len;
@@ -1838,6 +1847,11 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
             if (fb) cA = cL = cP = 0;
         }
         if (gp == GP_LIST || MEMBER) v.plan[i] = q;
+    }
+    const uint64_t rem = __ballot(todo);
+    if (!rem) break;
+    sbase = rl64(oa, (uint32_t)__builtin_ctzll(rem));
+    wave_lds_fence();                                  // the window is read: restage
     }
     const uint64_t fm = __ballot(fb);
     if (fm) {
