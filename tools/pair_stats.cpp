@@ -47,6 +47,7 @@ int main(int argc, char **argv)
     }
     size_t pos = 40 + (size_t)ne * esz;
     std::vector<NodeStream> nodes(N);
+    const auto t_d0 = std::chrono::steady_clock::now();
     ValueTable vt;
     vt.member = member;
     IngestViolation iv;
@@ -62,6 +63,7 @@ int main(int argc, char **argv)
         pos += 16 + 8 * (cnt + 1) + nb;
         pos = (pos + 7) & ~(size_t)7;
     }
+    std::printf("decode %.3f s (one thread)\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - t_d0).count());
     HostTrace h;
     const auto t_b0 = std::chrono::steady_clock::now();
     rc = build_trace(nodes, 0, M, member ? ep : std::vector<mpx_epoch>(), h);
