@@ -685,19 +685,21 @@ struct EntryPool {
     {
         const bool has = !ns.e_pid.empty();
         auto pid_of = [&](uint32_t i) -> uint64_t { return has ? ns.e_pid[first + i] : 0; };
-        uint64_t h = mix64(cnt + 0x51ull);
-        for (uint32_t i = 0; i < cnt; ++i) {
-            h = mix64(h ^ ns.e_iid[first + i]) + ns.e_val[first + i];
-            if (member) h = mix64(h ^ pid_of(i));
-        }
+        // the hash only picks candidates: four independent lanes (no serial multiply chain
+        // over the list), folded at the end
+        const uint64_t *iv = ns.e_iid.data() + first, *vv = ns.e_val.data() + first;
+        uint64_t l[4] = {mix64(cnt + 0x51ull), 0x9E3779B97F4A7C15ull, 0xC2B2AE3D27D4EB4Full, 0x165667B19E3779F9ull};
+        for (uint32_t i = 0; i < cnt; ++i) l[i & 3] = (l[i & 3] ^ iv[i]) * 0xff51afd7ed558ccdull + vv[i];
+        if (member)
+            for (uint32_t i = 0; i < cnt; ++i) l[i & 3] = (l[i & 3] ^ pid_of(i)) * 0xc4ceb9fe1a85ec53ull;
+        const uint64_t h = mix64(mix64(mix64(l[0] ^ l[1]) ^ l[2]) ^ l[3]);
         auto r = idx.equal_range(h);
         for (auto it = r.first; it != r.second; ++it) {
             const uint64_t o = it->second;
             if (o + cnt > ht.e_iid.size()) continue;
-            bool same = true;
-            for (uint32_t i = 0; same && i < cnt; ++i)
-                same = ht.e_iid[o + i] == ns.e_iid[first + i] && ht.e_val[o + i] == ns.e_val[first + i] &&
-                       (!member || ht.e_pid[o + i] == pid_of(i));
+            bool same = std::memcmp(ht.e_iid.data() + o, iv, 8ull * cnt) == 0 &&
+                        std::memcmp(ht.e_val.data() + o, vv, 8ull * cnt) == 0;
+            for (uint32_t i = 0; same && member && i < cnt; ++i) same = ht.e_pid[o + i] == pid_of(i);
             if (same) return o;
         }
         const uint64_t o = ht.e_iid.size();
