@@ -263,7 +263,9 @@ def c3_windows_leg(args, trace, want_digests, want_counters):
     run_ms = [p["run"] for p in dev]
     apply_ms = [p["fast_apply"] + p["general_apply"] for p in dev]   # k_apply_win's start / stop events
     mean = lambda xs: sum(xs) / max(len(xs), 1)
-    pmc = latest_pmc(7, m, 1, workload="C3W")
+    # profiles record the proposed instance count (2^24), not the trace header's (every
+    # instance a proposer ever touched): look up by the same key as the C3 leg
+    pmc = latest_pmc(7, args.c3_instances, 1, workload="C3W")
     hw = hw_roofline(pmc, mean(apply_ms))
     # engine model of a window's apply: each pair it touches reads and writes 256 slots of
     # 16-B value state (s_bal, s_val) and its runs' 16-B descriptors

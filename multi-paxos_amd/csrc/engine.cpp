@@ -490,7 +490,7 @@ static int finish_view(mpx_engine *e)
     HTRY(hipMemsetAsync(e->viol.p, 0, 2 * sizeof(DevViolation), e->stream));
     TRY(e->summary.alloc(2 * 64 * 8));                                // two slots (comm overlap)
     e->out_subs = 64;
-    if (const char *x = std::getenv("MPX_OUT_SUBS")) {  // A/B: snapshot sub-buffers (power of two)
+    if (const char *x = ab_env("MPX_OUT_SUBS")) {  // A/B: snapshot sub-buffers (power of two)
         const uint32_t k = (uint32_t)std::atoi(x);
         if (k && !(k & (k - 1)) && k <= OUT_SUBS) e->out_subs = k;
     }
@@ -585,7 +585,7 @@ static int upload_trace(mpx_engine *e)
         }
         TRY(upload(e->gp_list, gd, s));
         HTRY(hipStreamSynchronize(s));                 // gd is a local
-        if (std::getenv("MPX_TRACE_STATS")) {          // shape of the general work list (tools)
+        if (ab_env("MPX_TRACE_STATS")) {          // shape of the general work list (tools)
             uint64_t fr = 0, ev = 0, mx = 0, pre = 0;
             for (uint64_t q : h.gp_list) {
                 fr += h.f_off[q + 1] - h.f_off[q]; ev += h.ev_off[q + 1] - h.ev_off[q];
@@ -728,7 +728,7 @@ static int queue_run(mpx_engine *e, bool digest)
     // (mpx_timing_every; MPX_EVENTS_EVERY overrides): they cost a step ~1.5-2 us per timed
     // kernel boundary (C4 shard at world 8: 89 vs 75 us per step)
     uint64_t every = e->events_every;
-    if (const char *x = std::getenv("MPX_EVENTS_EVERY")) every = std::strtoull(x, nullptr, 10);
+    if (const char *x = ab_env("MPX_EVENTS_EVERY")) every = std::strtoull(x, nullptr, 10);
     const bool timed = digest || every == 1 || (every && (e->step_no % every) == 0);
     ++e->step_no;
     StepEvents *ev = timed ? next_events(e) : nullptr;
@@ -740,18 +740,18 @@ static int queue_run(mpx_engine *e, bool digest)
     // MPX_STEP_WALK=1: a step walks every pair as the digested run does (no plan words)
     e->view.walk_all = 0;
     if (const char *x = std::getenv("MPX_STEP_WALK")) e->view.walk_all = std::atoi(x) ? 1 : 0;
-    if (const char *x = std::getenv("MPX_STORE_WGS_PER_CU")) g.store_wgs = std::max<uint32_t>(1, e->num_cus * (uint32_t)std::atoi(x));
-    if (const char *x = std::getenv("MPX_CHOSEN_WGS_PER_CU"))     // (partials hold 16 per CU for it too)
+    if (const char *x = ab_env("MPX_STORE_WGS_PER_CU")) g.store_wgs = std::max<uint32_t>(1, e->num_cus * (uint32_t)std::atoi(x));
+    if (const char *x = ab_env("MPX_CHOSEN_WGS_PER_CU"))     // (partials hold 16 per CU for it too)
         g.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 16),
                                                                           (uint64_t)e->num_cus * std::atoi(x)));
-    if (const char *x = std::getenv("MPX_APPLY_WGS_PER_CU")) {
+    if (const char *x = ab_env("MPX_APPLY_WGS_PER_CU")) {
         const uint64_t np = (uint64_t)e->cfg.num_nodes * e->NB;
         g.apply_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(np, (uint64_t)e->num_cus * std::atoi(x)));
         if (g.apply_wgs > e->num_cus * 16) g.apply_wgs = e->num_cus * 16;   // partials are sized for 16 per CU
     }
     // the launch's sequence number tags the header scan's look-back flags; the violation
     // record alternates between two buffers (this launch's, and the next one it clears)
-    if (++e->seq >= (1u << 30)) e->seq = 1;
+    if (++e->seq >= (1u << 30)) e->seq = 2;             // (wraps to an even number: the parity keeps alternating)
     e->view.seq = e->seq;
     e->view.viol = e->viol.as<DevViolation>() + (e->seq & 1);
     e->view.viol_next = e->viol.as<DevViolation>() + ((e->seq + 1) & 1);
@@ -770,7 +770,7 @@ static int queue_run(mpx_engine *e, bool digest)
         // (MPX_SIDE_PRIO=normal|low|high, A/B)
         int least = 0, greatest = 0;
         HTRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        const char *sp = std::getenv("MPX_SIDE_PRIO");
+        const char *sp = ab_env("MPX_SIDE_PRIO");
         const std::string pr = sp ? sp : "low";
         const int prio = pr == "high" ? greatest : pr == "normal" ? 0 : least;
         HTRY(hipStreamCreateWithPriority(&e->stream2, hipStreamNonBlocking, prio));
@@ -778,7 +778,7 @@ static int queue_run(mpx_engine *e, bool digest)
         HTRY(hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming));
     }
     LaunchSide side{nullptr, nullptr, nullptr};
-    if (!std::getenv("MPX_ONE_STREAM")) side = LaunchSide{e->stream2, e->fork_ev, e->join_ev};
+    if (!ab_env("MPX_ONE_STREAM")) side = LaunchSide{e->stream2, e->fork_ev, e->join_ev};
     int rc = launch_run(e->view, e->stream, g, evp, side);
     if (rc) return MPX_E_HIP;
     if (e->incremental) {                              // the next window starts from this one's scalars, rounds, roles

@@ -1731,6 +1731,11 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
                 const uint64_t blo = v.shard_begin + (b << BSH);
                 // one pass over the pair in message order; EMIT: the second pass, which
                 // writes the snapshot records (the first one decided the pair is kept)
+                // the snapshot run records: counted by the deciding pass, one reservation per pair,
+                // written by the emitting pass (no returning atomic per record)
+                unsigned long long rbase = 0;
+                uint32_t rnext = 0, nrec = 0;
+                const uint32_t rsub = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (v.out_subs - 1);
                 auto walk = [&](auto emit_tag, uint32_t &pres, uint32_t &comm, uint32_t (&fix)[LSEG],
                                 unsigned long long &a, unsigned long long &l, unsigned long long &p,
                                 bool &snap) {
@@ -1765,7 +1770,16 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
                             const uint32_t x0 = lo[g] > il ? lo[g] : il, x1 = lo[g] + sl[g] < ih ? lo[g] + sl[g] : ih;
                             if (x0 >= x1) continue;
                             p += x1 - x0;
-                            if (EMIT) emit_run(v, g8, (uint32_t)(oa + fix[g]), x0, x1 - x0);
+                            if (EMIT) {                            // at the place reserved after the first pass
+                                const unsigned long long at = rbase + rnext++;
+                                if (at < v.out_cap) {
+                                    OutRec r;
+                                    r.msg = g8; r.ref = (uint32_t)(oa + fix[g]); r.aux = OUT_RUN | x0 | ((x1 - x0) << OUT_RUN_SHIFT);
+                                    v.out[(uint64_t)rsub * v.out_cap + at] = r;
+                                }
+                            } else {
+                                ++nrec;
+                            }
                         }
                     };
                     auto event = [&](uint32_t info, uint32_t g8, uint64_t e) {
@@ -1814,6 +1828,7 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
                 bool snap = false;
                 walk(std::false_type{}, pres, comm, fix, cA, cL, cP, snap);
                 if (!fb) {
+                    if (snap && nrec) rbase = atomicAdd(&v.out_cursor[OUT_STRIDE * rsub], (unsigned long long)nrec);
                     if (snap) {                                    // kept: the emitting pass
                         uint32_t p2 = 0, c2 = 0, f2[LSEG];
 #pragma unroll

@@ -39,6 +39,22 @@
 
 namespace mpx {
 
+// Environment knobs.  std::getenv is read only for the alternative paths the GPU tests compare
+// with the default one (MPX_SLOT_BYTES, MPX_PROP_CHUNK, MPX_STEP_WALK, MPX_SCAN_NODE_PASS,
+// MPX_SCAN_SMALL, MPX_DECIDE_HOST, MPX_DECIDE_DEVICE).  Launch-tuning knobs kept for same-box
+// A/B runs (tools/ab_*.sh) go through ab_env: only a variant built with -DMPX_AB
+// (make EXTRA=-DMPX_AB OUT=$PWD/multi-paxos_amd/lib_<v> OBJ=$PWD/multi-paxos_amd/build_<v>) reads them;
+// the product library ignores them.
+inline const char *ab_env(const char *k)
+{
+#ifdef MPX_AB
+    return std::getenv(k);
+#else
+    (void)k;
+    return nullptr;
+#endif
+}
+
 constexpr uint32_t BSH = 8;                  // bucket = 256 instances
 constexpr uint32_t BS = 1u << BSH;
 #ifndef MPX_SCAN_CHUNK

@@ -539,14 +539,15 @@ class Engine:
 
 
 def source_digest():
-    """16 hex digits of SHA-256 over the engine's device sources — the kernels, the device
-    generator, the shared layout header (which also holds the launch code and grids): what a
+    """16 hex digits of SHA-256 over the sources that decide the device traffic — the kernels,
+    the device generator, the shared layout header, the launch code (engine.cpp: grids, which
+    kernels run) and ingest (which runs share entries, which pairs go to which kernel): what a
     committed PMC profile was measured with (tools/pmc_traffic.py), so bench.py can refuse a
-    profile of other kernels.  Host-only sources (ingest, the C ABI, readbacks) do not enter."""
+    profile of other kernels or another trace layout."""
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(os.path.dirname(HERE), "csrc")
-    for name in ("gen_device.hip", "kernels.hip", "mpx_internal.hpp"):
+    for name in ("gen_device.hip", "kernels.hip", "mpx_internal.hpp", "engine.cpp", "ingest.cpp", "ingest.hpp"):
         full = os.path.join(csrc, name)
         h.update(name.encode() + b"\0")
         with open(full, "rb") as f:

@@ -109,7 +109,7 @@ def main():
         phase = [v for k, v in out["kernels"].items() if "k_apply_win" in k]
     else:
         phase = [v for k, v in out["kernels"].items()
-                 if "k_plan" in k or "k_store" in k
+                 if "k_plan" in k or "k_store" in k or "k_commit_check" in k   # (the Value check: timed steps only)
                  or ((a.c3 or a.c5 or a.c5c) and re.search(r"k_apply<\d+, false", k))]   # k_apply<waves, DIGEST, ...>: not the digested run's
     out["apply_phase_kernels"] = [k for k, v in out["kernels"].items() if v in phase]
     out["hbm_bytes_per_launch"] = sum(v["hbm_bytes_per_launch"] for v in phase) if phase else None
