@@ -144,7 +144,8 @@ typedef struct mpx_config {
     uint64_t shard_begin;      /* this engine owns instances [shard_begin,         */
     uint64_t shard_end;        /*                              shard_end)          */
     uint32_t num_epochs;       /* member only                                      */
-    uint32_t flags;            /* 0, or MPX_FLAG_INCREMENTAL [| MPX_FLAG_DECISIONS]  */
+    uint32_t flags;            /* 0, MPX_FLAG_INCREMENTAL [| MPX_FLAG_DECISIONS],  */
+                               /* member: [| MPX_FLAG_LEARN_EPOCHS]                */
     const mpx_epoch *epochs;   /* member only, indexed by E_EPOCH's epoch          */
 } mpx_config;
 
@@ -175,6 +176,23 @@ typedef struct mpx_config {
  * creation, replies, AcceptorsChanged, drops) advances the same way and mpx_read_learns
  * returns the MPXL of the whole stream (k_learns over every learn at read time). */
 #define MPX_FLAG_DECISIONS 2u
+/* Member semantics: membership learned at run time, as the reference does it — a node's
+ * Learner applies learned Values in instance order and a membership Value (Node::AddAcceptor
+ * ... ProposerToLearner, member/paxos.cpp:635-721) changes the node's roles when it is applied
+ * (Learner::Apply -> NodeImpl::ChangeMemberships, :1062-1073,1864-1964).  The engine is created
+ * with the genesis epoch only (num_epochs = 1: {first} learner, proposer and acceptor, version 0,
+ * :738-747); at ingest it tracks every node's apply frontier over its LEARN entries (all of
+ * them, whatever the shard), and after a LEARN that makes the node apply membership Values it
+ * places one E_EPOCH record per Value, the node's view after that change, in its stream.  The
+ * epoch table grows as the nodes apply membership Values (epoch k = the view after the k-th
+ * membership Value in instance order; every node reaches the same sequence, MPX_E_STATE if two
+ * disagree) and mpx_read_epochs returns it.  Submitted E_EPOCH records are ignored, so a live host
+ * submits exactly what NetWork::OnReceive receives (member/paxos.cpp:841-844); combines with
+ * MPX_FLAG_INCREMENTAL (the frontier and the views carry over between windows).  Record indices
+ * (sends' and events' seq) count the engine's E_EPOCH records.  A change the reference ASSERTs
+ * on (a member added twice, an absent one removed, the last acceptor removed) fails the submit
+ * with MPX_E_STATE. */
+#define MPX_FLAG_LEARN_EPOCHS 4u
 
 typedef struct mpx_engine mpx_engine;
 
@@ -301,6 +319,10 @@ int  mpx_drain_sends(mpx_engine *eng, mpx_send_fn fn, void *user);
 /* chosen log: out[i] = MPX_PRESENT | handle, or 0 if instance first+i is not
  * chosen yet (instances outside the shard are an error). */
 int  mpx_read_chosen(mpx_engine *eng, uint64_t first, uint64_t count, uint64_t *out);
+/* The member epoch table: with MPX_FLAG_LEARN_EPOCHS the epochs learned so far (genesis first),
+ * else the table the engine was created with or took from a container.  Writes min(cap, total)
+ * entries, *count = total. */
+int  mpx_read_epochs(mpx_engine *eng, mpx_epoch *out, uint32_t cap, uint32_t *count);
 /* per-node scalars: promised_proposal_id_ and max_proposal_id_
  * (multi/paxos.cpp:492,460) */
 /* In-order executor of one node, on the device (replaces the

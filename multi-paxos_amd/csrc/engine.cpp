@@ -83,6 +83,7 @@ struct mpx_engine {
     uint32_t num_cus = 256;
     ValueTable vt;
     std::vector<NodeStream> nodes;
+    std::vector<EpochLearn> elearn;                  // MPX_FLAG_LEARN_EPOCHS: per node (ingest.hpp)
     IngestViolation iv;
     HostTrace ht;
     bool dirty = true;
@@ -187,7 +188,9 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
     if (cfg->shard_end <= cfg->shard_begin) return MPX_E_INVAL;
     if (cfg->semantics != MPX_SEM_MULTI && cfg->semantics != MPX_SEM_MEMBER) return MPX_E_INVAL;
     if (cfg->semantics == MPX_SEM_MULTI && cfg->num_epochs) return MPX_E_INVAL;
-    if (cfg->flags & ~(uint32_t)(MPX_FLAG_INCREMENTAL | MPX_FLAG_DECISIONS)) return MPX_E_INVAL;
+    if (cfg->flags & ~(uint32_t)(MPX_FLAG_INCREMENTAL | MPX_FLAG_DECISIONS | MPX_FLAG_LEARN_EPOCHS)) return MPX_E_INVAL;
+    if ((cfg->flags & MPX_FLAG_LEARN_EPOCHS) &&
+        (cfg->semantics != MPX_SEM_MEMBER || cfg->num_epochs != 1 || !cfg->epochs)) return MPX_E_INVAL;
     if ((cfg->flags & MPX_FLAG_DECISIONS) && !(cfg->flags & MPX_FLAG_INCREMENTAL)) return MPX_E_INVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPX_E_NODEVICE;
@@ -203,6 +206,10 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
     if (hipGetDeviceProperties(&prop, e->device) == hipSuccess && prop.multiProcessorCount > 0)
         e->num_cus = (uint32_t)prop.multiProcessorCount;
     e->nodes.resize(cfg->num_nodes);
+    if (cfg->flags & MPX_FLAG_LEARN_EPOCHS) {        // every node starts in the genesis epoch
+        e->elearn.resize(cfg->num_nodes);
+        for (auto &l : e->elearn) l.view = e->epochs[0];
+    }
     e->vt.member = cfg->semantics == MPX_SEM_MEMBER;
     e->shard_len = cfg->shard_end - cfg->shard_begin;
     e->NB = (uint32_t)((e->shard_len + BS - 1) >> BSH);
@@ -261,6 +268,32 @@ extern "C" int mpx_destroy(mpx_engine *e)
     return MPX_OK;
 }
 
+// MPX_FLAG_LEARN_EPOCHS: the epochs each node reached (EpochLearn::steps) extend the table;
+// nodes apply the same membership Values in the same instance order, so a node's k-th step
+// must equal every other node's (the reference's safety: one chosen Value per instance)
+static int merge_epochs(mpx_engine *e)
+{
+    for (const EpochLearn &l : e->elearn)
+        for (size_t k = 0; k < l.steps.size(); ++k) {
+            if (k + 1 < e->epochs.size()) {
+                const mpx_epoch &a = e->epochs[k + 1], &b = l.steps[k];
+                if (a.version != b.version || a.acceptor_mask != b.acceptor_mask || a.proposer_mask != b.proposer_mask ||
+                    a.learner_mask != b.learner_mask) return MPX_E_STATE;
+            } else {
+                e->epochs.push_back(l.steps[k]);
+            }
+        }
+    return MPX_OK;
+}
+
+extern "C" int mpx_read_epochs(mpx_engine *e, mpx_epoch *out, uint32_t cap, uint32_t *count)
+{
+    if (!e || !count || (cap && !out)) return MPX_E_INVAL;
+    *count = (uint32_t)e->epochs.size();
+    for (uint32_t k = 0; k < cap && k < e->epochs.size(); ++k) out[k] = e->epochs[k];
+    return MPX_OK;
+}
+
 extern "C" int mpx_submit(mpx_engine *e, uint32_t node, const uint8_t *bytes, const uint64_t *offsets, uint64_t count)
 {
     if (!e || node >= e->cfg.num_nodes || (count && (!bytes || !offsets))) return MPX_E_INVAL;
@@ -273,10 +306,12 @@ extern "C" int mpx_submit(mpx_engine *e, uint32_t node, const uint8_t *bytes, co
         if (offsets[i + 1] < offsets[i]) return MPX_E_INVAL;
         const uint8_t *m = bytes + offsets[i];
         const size_t len = (size_t)(offsets[i + 1] - offsets[i]);
-        int rc = member ? decode_record_member(e->vt, ns, node, m, len, e->cfg.shard_begin, e->cfg.shard_end, e->iv)
+        int rc = member ? decode_record_member(e->vt, ns, node, m, len, e->cfg.shard_begin, e->cfg.shard_end, e->iv,
+                                               e->elearn.empty() ? nullptr : &e->elearn[node])
                         : decode_record(e->vt, ns, node, e->cfg.num_nodes, m, len, e->cfg.shard_begin, e->cfg.shard_end, e->iv);
         if (rc) return rc;
     }
+    TRY(merge_epochs(e));
     e->dirty = true;
     e->stats.ingest_ns += now_ns() - t0;
     return MPX_OK;
@@ -320,9 +355,9 @@ static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, cons
     if (N != e->cfg.num_nodes || sem != e->cfg.semantics || ver < 1 || ver > 2) return MPX_E_INVAL;
     const uint32_t esz = ver == 1 ? 24 : 32;         // version 1: no learner_mask (= proposer_mask)
     if (size < 40 + (uint64_t)ne * esz) return MPX_E_DECODE;
-    if (ne) {
+    if (ne && e->elearn.empty()) {
         // the container's epoch table: adopted by an engine created without
-        // one, else it must be the same table
+        // one, else it must be the same table (MPX_FLAG_LEARN_EPOCHS: the engine learns its own)
         std::vector<mpx_epoch> ep(ne);
         for (uint32_t k = 0; k < ne; ++k) {
             const uint8_t *x = t + 40 + (size_t)k * esz;
@@ -383,7 +418,8 @@ static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, cons
                 if (offs[i + 1] < offs[i]) { rcs[n] = MPX_E_INVAL; break; }
                 const uint8_t *m = bytes + offs[i];
                 const size_t len = (size_t)(offs[i + 1] - offs[i]);
-                rcs[n] = member ? decode_record_member(vts[n], ns, n, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n])
+                rcs[n] = member ? decode_record_member(vts[n], ns, n, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n],
+                                                       e->elearn.empty() ? nullptr : &e->elearn[n])
                                 : decode_record(vts[n], ns, n, N, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n]);
             }
         });
@@ -397,6 +433,7 @@ static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, cons
             e->iv.count += ivs[n].count;
         }
     }
+    TRY(merge_epochs(e));
     e->dirty = true;
     e->stats.ingest_ns += now_ns() - t0;
     return MPX_OK;

@@ -77,6 +77,7 @@ long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle)
         } else {
             idx.emplace(h, Rec{bytes.size(), (uint32_t)enc.size(), eo, el});
             bytes += enc;
+            if (eo == NONE32) membership.insert(h);
         }
         *handle = h;
         return used;
@@ -201,6 +202,43 @@ int ValueTable::merge(const ValueTable &o)
         }
         idx.emplace(kv.first, Rec{bytes.size(), r.len, r.exec_off, r.exec_len});
         bytes.append(o.bytes, r.off, r.len);
+    }
+    membership.insert(o.membership.begin(), o.membership.end());
+    return MPX_OK;
+}
+
+bool ValueTable::changes(uint64_t h, std::vector<std::pair<uint32_t, uint32_t>> &out) const
+{
+    out.clear();
+    auto it = idx.find(h);
+    if (it == idx.end() || it->second.exec_off != NONE32) return false;
+    // canonical Value_m bytes (parse_member): ... u8 membership @13, u32 n @14, n x {u32 node, u32 type} @18
+    const uint8_t *p = (const uint8_t *)bytes.data() + it->second.off;
+    const uint32_t n = rd32(p + 14);
+    for (uint32_t k = 0; k < n; ++k) out.emplace_back(rd32(p + 18 + 8 * k), rd32(p + 22 + 8 * k));
+    return true;
+}
+
+// NodeImpl::ChangeMemberships (member/paxos.cpp:1864-1964) on a node's view: the six change
+// types, version_ bumped by each acceptor change; a change the reference ASSERTs on (adding a
+// member twice, removing an absent one, the last acceptor) is refused (MPX_E_STATE)
+static int change_memberships(mpx_epoch &v, const std::vector<std::pair<uint32_t, uint32_t>> &ch)
+{
+    enum { ADD_LEARNER, LEARNER_TO_PROPOSER, PROPOSER_TO_ACCEPTOR, DEL_LEARNER, PROPOSER_TO_LEARNER, ACCEPTOR_TO_PROPOSER };
+    for (const auto &c : ch) {
+        if (c.first >= 64) return MPX_E_RANGE;
+        const uint64_t b = 1ull << c.first;
+        switch (c.second) {
+        case ADD_LEARNER: if (v.learner_mask & b) return MPX_E_STATE; v.learner_mask |= b; break;          // :1872-1880
+        case LEARNER_TO_PROPOSER: if (v.proposer_mask & b) return MPX_E_STATE; v.proposer_mask |= b; break;   // :1881-1892
+        case PROPOSER_TO_ACCEPTOR: if (v.acceptor_mask & b) return MPX_E_STATE; v.acceptor_mask |= b; ++v.version; break;   // :1893-1905
+        case DEL_LEARNER: if (!(v.learner_mask & b)) return MPX_E_STATE; v.learner_mask &= ~b; break;      // :1906-1915
+        case PROPOSER_TO_LEARNER: if (!(v.proposer_mask & b)) return MPX_E_STATE; v.proposer_mask &= ~b; break;   // :1916-1943
+        case ACCEPTOR_TO_PROPOSER:                                                                          // :1944-1960
+            if (!(v.acceptor_mask & b) || v.acceptor_mask == b) return MPX_E_STATE;
+            v.acceptor_mask &= ~b; ++v.version; break;
+        default: return MPX_E_DECODE;
+        }
     }
     return MPX_OK;
 }
@@ -517,7 +555,7 @@ int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord
 }
 
 int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const uint8_t *m, size_t len,
-                         uint64_t sb, uint64_t se, IngestViolation &viol)
+                         uint64_t sb, uint64_t se, IngestViolation &viol, EpochLearn *el)
 {
     if (len < 4) return MPX_E_DECODE;
     const uint32_t t = rd32(m);
@@ -536,6 +574,24 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         ns.e_iid.resize(w); ns.e_val.resize(w); ns.e_pid.resize(w);
         return (uint32_t)(w - first);
     };
+    std::vector<uint64_t> applied;                // (el) membership Values this LEARN makes the node apply
+    // the Learner's apply loop over one LEARN's entries, every instance (not only the shard's)
+    auto learn = [&](size_t first, size_t end) {
+        for (size_t k = first; k < end; ++k) {
+            const uint64_t i = ns.e_iid[k];
+            if (i < el->front) continue;                          // applied already (insert: no change)
+            if (i > el->front) { el->above.emplace(i, ns.e_val[k]); continue; }
+            uint64_t h = ns.e_val[k];
+            for (;;) {                                            // apply at the frontier, then what waited above it
+                if (vt.is_membership(h)) applied.push_back(h);
+                ++el->front;
+                auto it = el->above.begin();
+                if (it == el->above.end() || it->first != el->front) break;
+                h = it->second;
+                el->above.erase(it);
+            }
+        }
+    };
     // {u64 iid, u64 pid, Value_m}* (ExtractProposalValues, member/paxos.cpp:421-433)
     auto entries = [&](const uint8_t *b, size_t l) -> int {
         const size_t first = ns.e_iid.size();
@@ -543,6 +599,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         int rc = decode_entries(vt, b, l, true, ns.e_iid, ns.e_pid, ns.e_val, n_all, dup);
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
+        if (el && t == MPX_MSG_COMMIT) learn(first, ns.e_iid.size());
         ent = first;
         cnt = keep_shard(first);
         part = n_all && !cnt;
@@ -632,6 +689,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
     }
     case MPX_MSG_E_EPOCH:
         if (len < 8) return MPX_E_DECODE;
+        if (el) return MPX_OK;                    // (learned epochs: the engine places its own)
         ver = rd32(m + 4);
         break;
     case MPX_MSG_P_PROPOSE:                       // Node::Propose (:1984, :1122-1156): bookkeeping only
@@ -649,6 +707,22 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
     ns.ent.push_back(ent);
     ns.cnt.push_back(cnt);
     ns.ver.push_back(ver);
+    // the membership Values this LEARN applied, in instance order: one E_EPOCH each, right after
+    // it (the reference changes the roles inside OnLearn, before the node's next record)
+    std::vector<std::pair<uint32_t, uint32_t>> ch;
+    for (const uint64_t h : applied) {
+        if (!vt.changes(h, ch)) return MPX_E_STATE;
+        TRY_RC(change_memberships(el->view, ch));
+        el->steps.push_back(el->view);
+        ns.part.push_back(0);
+        ns.type.push_back((uint8_t)MPX_MSG_E_EPOCH);
+        ns.src.push_back(0);
+        ns.ballot.push_back(0);
+        ns.aux.push_back(0);
+        ns.ent.push_back(0);
+        ns.cnt.push_back(0);
+        ns.ver.push_back((uint32_t)el->steps.size());
+    }
     return MPX_OK;
 }
 

@@ -2,8 +2,10 @@
 // instance bucketing into fragments.
 #pragma once
 #include <cstdint>
+#include <map>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "mpx.h"
@@ -35,6 +37,27 @@ struct ValueTable {
     int merge(const ValueTable &o);
     // a handle with no bytes yet: the payload-free Value it names (mpx_submit_soa)
     int plain(uint64_t handle);
+    // member: the handles of membership Values (Value_m with a change list) and their lists
+    std::unordered_set<uint64_t> membership;
+    bool is_membership(uint64_t h) const { return !membership.empty() && membership.count(h) != 0; }
+    // {node, MembershipChangeType} of a membership Value, in its order (member/paxos.cpp:365-390)
+    bool changes(uint64_t h, std::vector<std::pair<uint32_t, uint32_t>> &out) const;
+};
+
+// Membership discovered at run time (MPX_FLAG_LEARN_EPOCHS, member semantics): every node's
+// Learner applies learned Values in instance order (Learner::OnLearn, member/paxos.cpp:1040-1053;
+// a LEARN is handled whatever the node's roles, Loop :771-772), and applying a membership Value
+// runs NodeImpl::ChangeMemberships (Learner::Apply :1062-1073, :1864-1964).  Per node: the apply
+// frontier (next_id_to_apply_), the instances learned above it with their first Value (insert:
+// the first learned Value sticks, :1040), the node's membership view, and the epochs it stepped
+// through.  Epoch k = the view after the k-th membership Value in instance order; every node
+// applies the same Values in the same order (one chosen Value per instance), so the per-node
+// lists agree on their common prefix (checked when they are merged, mpx_engine::epochs).
+struct EpochLearn {
+    uint64_t front = 0;
+    std::map<uint64_t, uint64_t> above;           // learned, not yet applied: iid -> handle
+    mpx_epoch view{};                             // NodeImpl's version_ / acceptors_ / proposers_ / learners_
+    std::vector<mpx_epoch> steps;                 // epochs 1.. this node reached
 };
 
 // One node's decoded receive stream (submission order).
@@ -151,9 +174,11 @@ struct SoaRecord {
 };
 int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord &r, uint64_t shard_begin,
                   uint64_t shard_end, IngestViolation &viol);
-// member semantics wire formats (member/paxos.cpp:846-932)
+// member semantics wire formats (member/paxos.cpp:846-932).  With `el` (MPX_FLAG_LEARN_EPOCHS)
+// the record's E_EPOCH markers come from the engine: a submitted E_EPOCH is dropped, and a LEARN
+// that makes the node apply membership Values is followed by one E_EPOCH per Value
 int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const uint8_t *m, size_t len,
-                         uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol);
+                         uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol, EpochLearn *el = nullptr);
 
 // Flatten node streams and build every index the kernels walk.  `epochs`
 // non-empty selects member semantics (role / version gates, E_EPOCH events).

@@ -1,0 +1,139 @@
+#!/usr/bin/env python3
+"""Full-size parity pinned to the REFERENCE itself (TEST INFRASTRUCTURE; VERDICT r04 item 3,
+SURVEY.md §8(c)(ii), §7 step 4): counters + order-independent digests of the stated configs,
+computed by the reference's own handlers (oracle/_ref, multi/paxos.cpp and member/paxos.cpp
+compiled in place) per instance shard, summed, and kept in tests/golden/full_size.json.  The GPU
+tests test_*_full_size_matches_oracle assert the engine equals these values, beside the C
+restatement's.
+
+Per shard [sb, se) the reference driver (mpxref_run_shard / mpxref_member_run_shard) processes
+every record's header and only the shard's entries (cut with the reference's own codec), so one
+shard needs only its share of the reference's std::map state; shards run as separate processes
+(the reference's objects are not made for concurrent use in one process).  The shard mode is
+checked against the whole-trace reference on every golden (tests/test_oracle.py
+test_ref_shard_mode_matches_whole).
+
+The trace comes from the same deterministic generator the GPU tests call (libmpx
+mpx_trace_generate, host code); its size and xxh3-64 are recorded so a test can tell that it
+judged the same bytes.  Only where /root/reference exists (oracle/_ref is built there).
+
+    python oracle/ref_full_size.py c3 [--shards 16] [--procs 8]      (c2 | c3 | c5 | c5c)
+"""
+import argparse
+import ctypes
+import json
+import mmap
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multi-paxos_amd"))
+OUT = os.path.join(ROOT, "tests", "golden", "full_size.json")
+
+# the GPU tests' parameters (tests/test_engine_gpu.py test_*_full_size_matches_oracle)
+CONFIGS = {
+    "c2": dict(kind="GEN_CLEAN", num_nodes=5, num_instances=1 << 20, seed=0, batch=256),
+    "c3": dict(kind="GEN_FAULTY", num_nodes=7, num_instances=1 << 24, seed=0, batch=256, proposers=3,
+               drop_rate=500, dup_rate=1000, max_delay=500),
+    "c5": dict(kind="GEN_MEMBER", num_nodes=8, num_instances=1 << 25, seed=0, batch=256, drop_rate=100,
+               dup_rate=100, max_delay=64, noop_permille=15),
+    "c5c": dict(kind="GEN_MEMBER", num_nodes=8, num_instances=1 << 25, seed=0, batch=256, drop_rate=100,
+                dup_rate=100, max_delay=64, noop_permille=15, proposers=3),
+}
+STATS = ("chosen", "promise_entries", "accept_apps", "commit_apps", "violations",
+         "chosen_digest", "state_digest", "scalar_digest")
+
+
+def trace_fingerprint(buf):
+    import xxhash
+    return xxhash.xxh3_64_intdigest(memoryview(buf))
+
+
+def _worker(args):
+    path, member, sb, se = args
+    so = os.path.join(ROOT, "oracle", "_ref", "libmpx_ref_member.so" if member else "libmpx_ref.so")
+    f = getattr(ctypes.CDLL(so), "mpxref_member_run_shard" if member else "mpxref_run_shard")
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    f.restype = ctypes.c_int
+    with open(path, "rb") as fh:
+        mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_COPY)     # shared pages, never written
+    addr = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+    st = (ctypes.c_uint64 * 8)()
+    t0 = time.time()
+    rc = f(addr, len(mm), sb, se, st)
+    return rc, list(st), time.time() - t0, sb
+
+
+def run(cfg, shards, procs, tmpdir):
+    import mpx
+    p = dict(CONFIGS[cfg])
+    kind = getattr(mpx, p.pop("kind"))
+    t0 = time.time()
+    t = mpx.generate_trace(kind, copy=False, **p)
+    size = len(t)
+    fp = trace_fingerprint(t)
+    hd = mpx.trace_header(t)
+    path = os.path.join(tmpdir, "mpx_full_%s.mpxt" % cfg)
+    with open(path, "wb") as fh:
+        fh.write(memoryview(t))
+    del t
+    print("[%s] generated %.2f GB (xxh3 %016x) in %.0f s" % (cfg, size / 1e9, fp, time.time() - t0), flush=True)
+    # the C restatement on the same bytes, for the record (the GPU tests compare the engine with both)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracles import oracle_run_sharded
+    t2 = time.time()
+    with open(path, "rb") as fh:
+        mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_COPY)
+    oracle = oracle_run_sharded((ctypes.c_char * size).from_buffer(mm), shards=procs, threads=procs)
+    del mm
+    print("[%s] C oracle (restatement) in %.0f s" % (cfg, time.time() - t2), flush=True)
+    member = hd["semantics"] == 1
+    M = hd["num_instances"]
+    per = -(-M // shards)
+    jobs = [(path, member, k * per, (k + 1) * per if k + 1 < shards else (1 << 64) - 1) for k in range(shards)]
+    tot, scal, secs = [0] * 8, None, []
+    t1 = time.time()
+    with mp.get_context("fork").Pool(procs, maxtasksperchild=1) as pool:
+        for rc, st, dt, sb in pool.imap_unordered(_worker, jobs):
+            if rc:
+                raise SystemExit("[%s] shard at %d: reference driver returned %d" % (cfg, sb, rc))
+            for w in range(7):
+                tot[w] = (tot[w] + st[w]) % (1 << 64)
+            if scal is None:
+                scal = st[7]
+            elif scal != st[7]:
+                raise SystemExit("[%s] per-node scalars differ between shards" % cfg)
+            secs.append(dt)
+            print("[%s] shard %d done in %.0f s (%d/%d)" % (cfg, sb // per, dt, len(secs), shards), flush=True)
+    tot[7] = scal
+    os.unlink(path)
+    if oracle[:4] + oracle[5:] != tot[:4] + tot[5:]:
+        print("[%s] NOTE: the C restatement differs from the reference: %r vs %r" % (cfg, oracle, tot), flush=True)
+    return {"params": CONFIGS[cfg], "trace_bytes": size, "trace_xxh3": "%016x" % fp, "trace_instances": M,
+            "shards": shards, "procs": procs, "cpu_s": round(sum(secs), 1), "wall_s": round(time.time() - t1, 1),
+            "stats": dict(zip(STATS, tot)),
+            "c_oracle_equal": oracle[:4] + oracle[5:] == tot[:4] + tot[5:],
+            "source": "oracle/_ref (the reference's handlers compiled in place), mpxref%s_run_shard over %d "
+                      "instance shards" % ("_member" if member else "", shards)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="+", choices=sorted(CONFIGS))
+    ap.add_argument("--shards", type=int, default=16)
+    ap.add_argument("--procs", type=int, default=8)
+    ap.add_argument("--tmpdir", default="/tmp")
+    ap.add_argument("--out", default=OUT)
+    a = ap.parse_args()
+    res = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    for cfg in a.configs:
+        res[cfg] = run(cfg, a.shards, a.procs, a.tmpdir)
+        print(json.dumps({cfg: res[cfg]}, indent=1), flush=True)
+        with open(a.out, "w") as fh:
+            json.dump(res, fh, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -202,11 +202,98 @@ int parse_pvalues(Logger *lg, const uint8_t *buf, uint32_t len, PVMap *out)
     return 0;
 }
 
+
+// mix64 / the digests of oracle/mpx_oracle.c dump() (shard runs sum them)
+u64 mix64(u64 x)
+{
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    x ^= x >> 31; return x;
+}
+
+// One record with its entries outside [sb, se) removed (shard runs), walked with the reference's
+// own ExtractValue; iid-sorted lists (FillProposalValues walks a std::map) keep one byte range,
+// which is what ExtractProposalValues -> erase -> FillProposalValues writes; others take that path.
+const uint8_t *shard_cut(const uint8_t *m, size_t len, u64 sb, u64 se, std::string &buf, Logger *lg)
+{
+    size_t lo = 0, vo = 0;
+    switch (rd32(m)) {
+    case 1: lo = offsetof(paxos::PrepareReplyMsg, len_); vo = offsetof(paxos::PrepareReplyMsg, values_); break;
+    case 3: lo = offsetof(paxos::AcceptMsg, len_); vo = offsetof(paxos::AcceptMsg, values_); break;
+    case 5: lo = offsetof(paxos::LearnMsg, len_); vo = offsetof(paxos::LearnMsg, values_); break;
+    case 17: lo = 12; vo = 16; break;            // P_BATCH {u32 type, u64 accept id, u32 len, values}
+    default: return m;
+    }
+    if (len < vo) return m;
+    const char *v = (const char *)m + vo;
+    const unsigned int vl = rd32(m + lo);
+    unsigned int cur = 0, a = vl, b = vl;
+    u64 prev = 0;
+    bool sorted = true;
+    while (cur != vl) {
+        const unsigned int at = cur;
+        const u64 iid = rd64((const uint8_t *)v + cur);
+        if (at && iid <= prev) sorted = false;
+        prev = iid;
+        cur += 16;
+        paxos::ExtractValue(v, cur);
+        if (iid >= sb && a == vl) a = at;
+        if (iid >= se && b == vl) b = at;
+    }
+    if (a > b) a = b;
+    if (sorted && a == 0 && b == vl) return m;
+    buf.assign((const char *)m, vo);
+    unsigned int nl = 0;
+    if (sorted) {
+        nl = b - a;
+        buf.append(v + a, nl);
+    } else {
+        PVMap x, keep;
+        paxos::ExtractProposalValues(lg, g_thread, v, vl, &x);
+        keep.insert(x.lower_bound(sb), x.lower_bound(se));
+        nl = paxos::CalcProposalValuesLength(keep);
+        buf.resize(vo + nl);
+        paxos::FillProposalValues(&buf[vo], keep);
+    }
+    memcpy(&buf[lo], &nl, 4);
+    return (const uint8_t *)buf.data();
+}
+
+// The change list of a membership step from one epoch to the next (shard runs: the learned
+// membership Values are applied by the marker, see member_run), in the order the reference's own
+// lists use (Node::AddAcceptor / DelAcceptor ..., member/paxos.cpp:635-721): gains, then losses
+std::vector<paxos::MembershipChange> epoch_changes(const Epoch &o, const Epoch &x)
+{
+    std::vector<paxos::MembershipChange> ch;
+    for (uint32_t j = 0; j < 64; ++j) {
+        const u64 b = 1ull << j;
+        if ((x.lmask & b) && !(o.lmask & b)) ch.push_back(paxos::MembershipChange(j, paxos::ADD_LEARNER));
+        if ((x.pmask & b) && !(o.pmask & b)) ch.push_back(paxos::MembershipChange(j, paxos::LEARNER_TO_PROPOSER));
+        if ((x.amask & b) && !(o.amask & b)) ch.push_back(paxos::MembershipChange(j, paxos::PROPOSER_TO_ACCEPTOR));
+    }
+    for (uint32_t j = 0; j < 64; ++j) {
+        const u64 b = 1ull << j;
+        if ((o.amask & b) && !(x.amask & b)) ch.push_back(paxos::MembershipChange(j, paxos::ACCEPTOR_TO_PROPOSER));
+        if ((o.pmask & b) && !(x.pmask & b)) ch.push_back(paxos::MembershipChange(j, paxos::PROPOSER_TO_LEARNER));
+        if ((o.lmask & b) && !(x.lmask & b)) ch.push_back(paxos::MembershipChange(j, paxos::DEL_LEARNER));
+    }
+    return ch;
+}
+
 }  // namespace
 
 static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size,
-                      uint64_t *stats, uint8_t **lout, uint64_t *lsize, uint8_t **dout = NULL, uint64_t *dsize = NULL)
+                      uint64_t *stats, uint8_t **lout, uint64_t *lsize, uint8_t **dout = NULL, uint64_t *dsize = NULL,
+                      u64 sb = 0, u64 se = ~0ull, bool digest = false)
 {
+    // digest (mpxref_member_run_shard): counters and digests of the instance shard [sb, se) only
+    // (SURVEY.md §8(c)(ii)).  Every record's header is processed; entries outside the shard are cut
+    // with the reference's own codec.  A shard never learns the instances below it, so its Learner
+    // would never apply a membership Value (Learner::Apply runs in instance order, :1042-1053): here
+    // nothing is applied (next_id_to_apply_ parked) and each E_EPOCH marker — which whole runs
+    // CHECK against what Apply did, at the record after the LEARN that applied it — calls the
+    // reference's own NodeImpl::ChangeMemberships with that step's change list.  The consistency
+    // check below still holds the node to the marker's epoch before every record.
     if (size < 40 || memcmp(trace, "MPXT", 4)) return -4;
     uint32_t N = rd32(trace + 8), sem = rd32(trace + 12), ne = rd32(trace + 24);
     if (sem != 1 || N == 0 || N > 64 || ne == 0) return -1;
@@ -265,16 +352,30 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
             p->acceptor_ = new paxos::Acceptor(p);
             make_idle(p->proposer_);     // the engine model: idle until P_START
         }
+        if (digest) p->learner_.next_id_to_apply_ = ~0ull;
     }
     if (!g_dummy_prt) g_dummy_prt = new paxos::PrepareRetryTimeout(NULL, 1000000);
 
+    std::string cutbuf;
     for (uint32_t i = 0; i < N; ++i) {
         Node &n = ns[i];
         paxos::NodeImpl *ni = n.impl;
+        paxos::Proposer *shard_prop = NULL;              // (digest: the Proposer whose id sets start at sb)
         for (u64 k = 0; k < cnt[i]; ++k) {
             u64 a = rd64(offs[i] + 8 * k), b = rd64(offs[i] + 8 * k + 8);
             const uint8_t *m = bytes[i] + a;
             if (b - a < 4) return -4;
+            if (digest) {
+                m = shard_cut(m, b - a, sb, se, cutbuf, &logger);
+                if (ni->proposer_ && ni->proposer_ != shard_prop) {
+                    // a new Proposer's unlearned ids (:552, [0, 2^64-1)) start at the shard: ids
+                    // below it are never learned here, and a noop fill of [0, sb) at every promise
+                    // quorum would only build batches the driver discards (proposer-side)
+                    shard_prop = ni->proposer_;
+                    shard_prop->unlearned_instance_ids_.ids_.clear();
+                    shard_prop->unlearned_instance_ids_.ids_.insert(std::make_pair((paxos::InstanceID)sb, (paxos::InstanceID)-1));
+                }
+            }
             uint32_t type = rd32(m);
             if (type != 18 && !consistent(n, i, ep[n.epoch])) return -11;   // an E_EPOCH marker is missing
             size_t before = n.sends.size();
@@ -283,7 +384,7 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
             const paxos::LearningID lid0 = pr ? pr->learning_id_ : 0;
             std::map<paxos::InstanceID, std::string> orig_cb;
             std::map<paxos::LearningID, u64> prev_mask;
-            if (pr) {
+            if (pr && !digest) {
                 for (auto &f : pr->learning_values_for_acceptors_) {
                     auto it = pr->learning_values_.find(f.first);
                     if (it == pr->learning_values_.end()) continue;
@@ -305,7 +406,7 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
                 if (!pr) break;
                 const paxos::PrepareReplyMsg *msg = (const paxos::PrepareReplyMsg *)m;
                 bool live = pr->prepare_retry_timeout_ && msg->id_ == pr->proposal_id_;
-                bool quorum_next = live && [&] {
+                bool quorum_next = !digest && live && [&] {
                     std::set<paxos::NodeID> s = pr->prepare_promised_;
                     s.insert(msg->acceptor_);
                     return s.size() >= ni->acceptors_.size() / 2 + 1;
@@ -373,7 +474,27 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
             }
             case 5: {
                 const paxos::LearnMsg *msg = (const paxos::LearnMsg *)m;
-                n.L += [&] { PVMap v; parse_pvalues(&logger, (const uint8_t *)msg->values_, msg->len_, &v); return (u64)v.size(); }();
+                PVMap lv;
+                parse_pvalues(&logger, (const uint8_t *)msg->values_, msg->len_, &lv);
+                n.L += lv.size();
+                if (digest && pr) {
+                    // (digest runs do not replay Propose: a node's own Value is registered as
+                    // proposed at the instance it is first learned at, which is all Proposer::OnLearn
+                    // asks of it, :1398-1425 — proposer-side bookkeeping, out of the digested state)
+                    const PVMap &learned = ni->learner_.learned_values_;
+                    for (auto &e : lv) {
+                        const paxos::Value &x = e.second.value_;
+                        if (x.proposer_ != i || x.noop_ || learned.count(e.first) ||
+                            pr->unlearned_proposed_values_.count(x.value_id_))
+                            continue;
+                        paxos::ProposedValue pv;
+                        if (x.membership_changes_) pv.membership_changes_ = new std::vector<paxos::MembershipChange>(*x.membership_changes_);
+                        pv.value_ = x.value_;
+                        pv.cb_ = x.cb_;
+                        pr->unlearned_proposed_values_.insert(std::make_pair(x.value_id_, pv));
+                        pr->initial_proposals_.insert(std::make_pair(e.first, x.value_id_));
+                    }
+                }
                 ni->learner_.OnLearn(msg);
                 discard_new_batches(ni->proposer_ == pr ? pr : NULL, before_b);
                 break;
@@ -403,6 +524,7 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
                 uint32_t e = rd32(m + 4);
                 if (e >= ne) return -4;
                 const Epoch &o = ep[n.epoch], &x = ep[e];
+                if (digest) ni->ChangeMemberships(epoch_changes(o, x));
                 bool was = (o.pmask >> i) & 1, now = (x.pmask >> i) & 1;
                 n.epoch = e;
                 if (now && ni->proposer_ && (!was || o.amask != x.amask)) make_idle(ni->proposer_);
@@ -413,11 +535,25 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
                 if (b - a < 8 + (u64)pl) return -4;
                 paxos::ProposedValue pv;
                 if (!proposed_value(m + 8, pl, pv)) return -4;
-                if (pr) pr->Propose(pv);                 // (no Proposer: Unproposable, :786-789)
+                // (digest runs skip it: Propose only moves the proposer's id bookkeeping, which
+                // numbers instances across shards; the digested state and the chosen log come from
+                // the trace's P_BATCH / ACCEPT / LEARN records)
+                if (pr && !digest) pr->Propose(pv);      // (no Proposer: Unproposable, :786-789)
                 discard_new_batches(pr, before_b);       // the trace's P_BATCH is the batch
                 break;
             }
             default: return -4;
+            }
+            if (digest) {                      // counters only: P from this record's PREPARE_REPLYs
+                for (size_t j = before; j < n.sends.size(); ++j)
+                    if (rd32((const uint8_t *)n.sends[j].bytes.data()) == 1) {
+                        const paxos::PrepareReplyMsg *r = (const paxos::PrepareReplyMsg *)n.sends[j].bytes.data();
+                        PVMap vals;
+                        parse_pvalues(&logger, (const uint8_t *)r->values_, r->len_, &vals);
+                        n.P += vals.size();
+                    }
+                n.sends.clear();
+                continue;
             }
             {
                 paxos::Proposer *p1 = ni->proposer_;
@@ -476,6 +612,33 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
         if (!consistent(n, i, ep[n.epoch])) return -11;
     }
 
+    if (digest) {
+        // [C, P, A, L, V, chosen digest, state digest, scalar digest] as oracle/mpx_oracle.c dump()
+        u64 P = 0, A = 0, L = 0, ds = 0, dsc = 0, dc = 0;
+        std::map<u64, u64> chosen;
+        for (uint32_t i = 0; i < N; ++i) {
+            Node &n = ns[i];
+            paxos::NodeImpl *ni = n.impl;
+            paxos::Acceptor *ac = ni->acceptor_;
+            dsc += mix64(mix64((u64)i * 0x9E3779B97F4A7C15ull ^ (ac ? ac->promised_proposal_id_ : 0)) ^
+                         (ac ? ac->max_proposal_id_ : 0));
+            for (int pass = 0; pass < 2; ++pass) {
+                if (!pass && !ac) continue;
+                for (auto &e : pass ? ni->learner_.learned_values_ : ac->accepted_values_)
+                    ds += mix64(mix64(mix64(e.first + (u64)i * 0x9E3779B97F4A7C15ull) ^ e.second.proposal_id_)
+                                ^ (handle_of(e.second.value_) + (pass ? 2 : 1) * 0xD6E8FEB86659FD93ull));
+            }
+            P += n.P; A += n.A; L += n.L;
+            for (u64 k = 0; k < n.n_c; ++k) {
+                u64 bid = rd64((const uint8_t *)n.events_c.data() + 16 * k + 8);
+                for (auto &e : n.batch_values[bid])
+                    if (chosen.insert(e).second) dc += mix64(mix64(e.first) ^ e.second);
+            }
+        }
+        stats[0] = chosen.size(); stats[1] = P; stats[2] = A; stats[3] = L; stats[4] = 0;
+        stats[5] = dc; stats[6] = ds; stats[7] = dsc;
+        return 0;
+    }
     // canonical MPXR dump
     std::string r;
     r.append("MPXR", 4);
@@ -551,6 +714,14 @@ extern "C" int mpxref_member_run(const uint8_t *trace, uint64_t size, uint8_t **
                                  uint64_t *stats)
 {
     return member_run(trace, size, out, out_size, stats, NULL, NULL);
+}
+
+// Counters and digests of the instance shard [sb, se) of a member trace (the 8 words of
+// mpxo_run; see member_run), for full-size parity per instance shard (oracle/ref_full_size.py).
+extern "C" int mpxref_member_run_shard(const uint8_t *trace, uint64_t size, uint64_t sb, uint64_t se, uint64_t *stats)
+{
+    if (!stats || se <= sb) return -3;
+    return member_run(trace, size, NULL, NULL, stats, NULL, NULL, NULL, NULL, sb, se, true);
 }
 
 extern "C" int mpxref_member_learns(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)

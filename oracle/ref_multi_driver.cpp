@@ -75,7 +75,9 @@ struct CapNet : public paxos::NetWork {
 
 struct RecSM : public paxos::StateMachine {
     std::vector<std::string> executed;
-    void Execute(const std::string &v) { executed.push_back(v); }
+    bool keep = true;                        // (digest runs only count: mpxref_run_shard)
+    u64 n_exec = 0;
+    void Execute(const std::string &v) { ++n_exec; if (keep) executed.push_back(v); }
 };
 
 struct NopCallback : public paxos::Callback { void Run() {} };
@@ -121,8 +123,75 @@ static void scan_values(const uint8_t *m, size_t len, std::map<u64, paxos::Value
     for (auto &e : av) vals.insert(std::make_pair(handle_of(e.second.value_), e.second.value_));
 }
 
+
+// mix64 / the digests of oracle/mpx_oracle.c dump() (counters + order-independent digests of a
+// result, the engine's mpx_stats): shard runs sum them over instance shards
+static u64 mix64(u64 x)
+{
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    x ^= x >> 31; return x;
+}
+
+// One record with its entries outside [sb, se) removed (shard runs).  Entries are walked with the
+// reference's own ExtractValue; the wire lists them iid-sorted (Fill* walks a std::map), so the
+// shard's entries are one byte range and keeping that range is what Extract* -> erase -> Fill*
+// would write; an unsorted list takes exactly that path.
+static const uint8_t *shard_cut(const uint8_t *m, size_t len, u64 sb, u64 se, std::string &buf, Logger *lg)
+{
+    size_t lo = 0, vo = 0;
+    bool pid = false;                            // AcceptedValues (iid, proposal id, Value)
+    switch (rd32(m)) {
+    case 1: lo = offsetof(paxos::PrepareReplyMsg, len_); vo = offsetof(paxos::PrepareReplyMsg, values_); pid = true; break;
+    case 3: lo = offsetof(paxos::AcceptMsg, len_); vo = offsetof(paxos::AcceptMsg, values_); break;
+    case 5: lo = offsetof(paxos::CommitMsg, len_); vo = offsetof(paxos::CommitMsg, values_); break;
+    case 17: lo = 12; vo = 16; break;            // P_BATCH {u32 type, u64 accept id, u32 len, values}
+    default: return m;
+    }
+    if (len < vo) return m;
+    const char *v = (const char *)m + vo;
+    const unsigned int vl = rd32(m + lo);
+    unsigned int cur = 0, a = vl, b = vl;
+    u64 prev = 0;
+    bool sorted = true;
+    while (cur != vl) {
+        const unsigned int at = cur;
+        const u64 iid = rd64((const uint8_t *)v + cur);
+        if (at && iid <= prev) sorted = false;
+        prev = iid;
+        cur += pid ? 16 : 8;
+        paxos::ExtractValue(v, cur);
+        if (iid >= sb && a == vl) a = at;
+        if (iid >= se && b == vl) b = at;
+    }
+    if (a > b) a = b;
+    if (sorted && a == 0 && b == vl) return m;   // every entry in the shard
+    buf.assign((const char *)m, vo);
+    unsigned int nl = 0;
+    if (sorted) {
+        nl = b - a;
+        buf.append(v + a, nl);
+    } else if (pid) {
+        std::map<paxos::InstanceID, paxos::AcceptedValue> x, keep;
+        paxos::ExtractAcceptedValues(lg, v, vl, &x);
+        keep.insert(x.lower_bound(sb), x.lower_bound(se));
+        nl = paxos::CalcAcceptedValuesLength(&keep);
+        buf.resize(vo + nl);
+        paxos::FillAcceptedValues(&buf[vo], &keep);
+    } else {
+        std::map<paxos::InstanceID, paxos::Value> x, keep;
+        paxos::ExtractInstanceValues(lg, v, vl, &x);
+        keep.insert(x.lower_bound(sb), x.lower_bound(se));
+        nl = paxos::CalcInstanceValuesLength(&keep);
+        buf.resize(vo + nl);
+        paxos::FillInstanceValues(&buf[vo], &keep);
+    }
+    memcpy(&buf[lo], &nl, 4);
+    return (const uint8_t *)buf.data();
+}
+
 static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size, uint64_t *stats,
-                    std::string *decisions, std::string *commits = NULL);
+                    std::string *decisions, std::string *commits = NULL, u64 sb = 0, u64 se = ~0ull);
 
 extern "C" int mpxref_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size, uint64_t *stats)
 {
@@ -168,8 +237,14 @@ extern "C" int mpxref_decisions(const uint8_t *trace, uint64_t size, uint8_t **o
 }
 
 static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size, uint64_t *stats,
-                    std::string *decisions, std::string *commits)
+                    std::string *decisions, std::string *commits, u64 sb, u64 se)
 {
+    // Instance shard [sb, se) (mpxref_run_shard, out == NULL): what one GPU rank ingests
+    //  — every record's header is processed, the entries of
+    // PREPARE_REPLY / ACCEPT / COMMIT / P_BATCH outside the shard are cut with the reference's
+    // own codec (Extract* -> erase -> Calc* / Fill*); only counters and digests are kept.
+    const bool shard = sb != 0 || se != ~0ull;
+    const bool digest = out == NULL;
     if (size < 40 || memcmp(trace, "MPXT", 4)) return -4;
     uint32_t N = rd32(trace + 8), sem = rd32(trace + 12), ne = rd32(trace + 24);
     if (sem != 0 || N == 0 || N > 64) return -1;
@@ -200,18 +275,27 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
         if (pos > size + 7) return -4;
     }
     std::map<u64, paxos::Value> allvals;
-    for (uint32_t i = 0; i < N; ++i)
-        for (u64 k = 0; k < cnt[i]; ++k) {
-            u64 a = rd64(offs[i] + 8 * k), b = rd64(offs[i] + 8 * k + 8);
-            scan_values(bytes[i] + a, b - a, allvals, &logger);
-        }
+    if (!shard)
+        for (uint32_t i = 0; i < N; ++i)
+            for (u64 k = 0; k < cnt[i]; ++k) {
+                u64 a = rd64(offs[i] + 8 * k), b = rd64(offs[i] + 8 * k + 8);
+                scan_values(bytes[i] + a, b - a, allvals, &logger);
+            }
 
     std::vector<Node> ns(N);
     for (uint32_t i = 0; i < N; ++i) {
         Node &n = ns[i];
         n.net.out = &n.sends;
+        n.sm.keep = !digest;
         n.impl = new paxos::PaxosImpl(&logger, "ref", &clock, &timer, &rand, nodes, i,
                                       &n.net, &n.sm, cfg, NULL);
+        if (shard) {
+            // the proposer's id sets start at the shard: instances below it are never committed
+            // here, and a noop fill of [0, sb) at every promise quorum (:1117-1130) would only
+            // build batches the driver discards (proposer-side, out of the digested state)
+            n.impl->uncommitted_instance_ids_.ids_.clear();
+            n.impl->uncommitted_instance_ids_.ids_.insert(std::make_pair((paxos::InstanceID)sb, (paxos::InstanceID)-1));
+        }
         for (auto &v : allvals)
             if (v.second.proposer_ == i && !v.second.noop_)
                 n.impl->uncommitted_proposed_values_.insert(
@@ -219,13 +303,16 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
     }
 
     static paxos::PrepareRetryTimeout *dummy_prt = NULL;
+    std::string cutbuf;
     for (uint32_t i = 0; i < N; ++i) {
         Node &n = ns[i];
         paxos::PaxosImpl *p = n.impl;
         if (!dummy_prt) dummy_prt = new paxos::PrepareRetryTimeout(p, 1000000);
+        std::set<paxos::ValueID> registered;            // (shard runs: own Values seen at a COMMIT)
         for (u64 k = 0; k < cnt[i]; ++k) {
             u64 a = rd64(offs[i] + 8 * k), b = rd64(offs[i] + 8 * k + 8);
             const uint8_t *m = bytes[i] + a;
+            if (shard) m = shard_cut(m, b - a, sb, se, cutbuf, &logger);
             uint32_t type = rd32(m);
             size_t before = n.sends.size();
             const paxos::CommittingID cid0 = p->committing_id_;
@@ -253,7 +340,23 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
                         s.insert(msg->acceptor_);
                         return s.size() >= nodes.size() / 2 + 1;
                     }();
-                if (quorum_next) {
+                if (quorum_next && digest) {
+                    // (digest runs: no snapshot or decision record; the re-commit of every committed
+                    // value a promise quorum creates, :1184-1197, is proposer-side and would copy the
+                    // whole committed map per quorum: it sees an empty map here)
+                    std::map<paxos::InstanceID, paxos::AcceptedValue> held;
+                    held.swap(p->committed_values_);
+                    std::set<paxos::AcceptingID> before_b;
+                    for (auto &e : p->accepting_values_) before_b.insert(e.first);
+                    p->OnPrepareReply(msg);
+                    held.swap(p->committed_values_);
+                    for (auto it = p->accepting_values_.begin(); it != p->accepting_values_.end();) {
+                        if (!before_b.count(it->first)) {
+                            it->second->retry_timeout_->Cancel();
+                            it = p->accepting_values_.erase(it);
+                        } else ++it;
+                    }
+                } else if (quorum_next) {
                     // snapshot the merged map with the reference's own merge
                     std::map<paxos::InstanceID, paxos::AcceptedValue> saved = p->pre_accepted_values_;
                     std::map<paxos::InstanceID, paxos::AcceptedValue> vals;
@@ -322,6 +425,11 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
                 std::map<paxos::InstanceID, paxos::Value> vals;
                 paxos::ExtractInstanceValues(&logger, msg->values_, msg->len_, &vals);
                 n.L += vals.size();
+                if (shard)   // the prefill, per shard: a node's own Value exists before its first COMMIT
+                    for (auto &e : vals)
+                        if (e.second.proposer_ == i && !e.second.noop_ && registered.insert(e.second.value_id_).second)
+                            p->uncommitted_proposed_values_.insert(
+                                std::make_pair(e.second.value_id_, paxos::ProposedValue(e.second.value_, &g_nop)));
                 p->OnCommit(msg);
                 break;
             }
@@ -336,6 +444,10 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
                 break;
             }
             case 19: {         // P_PROPOSE: the reference's own Propose (multi/paxos.cpp:1250-1280)
+                // (shard runs skip it: Propose only moves the proposer's id bookkeeping, which
+                // numbers instances across shards; the digested acceptor / learner state and the
+                // chosen log come from the trace's P_BATCH / ACCEPT / COMMIT records)
+                if (shard) break;
                 const uint32_t pl = rd32(m + 4);
                 p->Propose(paxos::ProposedValue(std::string((const char *)m + 8, pl), &g_nop));
                 break;
@@ -353,6 +465,17 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
                 break;
             }
             default: return -4;
+            }
+            if (digest) {                      // counters only: P from this record's PREPARE_REPLYs
+                for (size_t j = before; j < n.sends.size(); ++j)
+                    if (rd32((const uint8_t *)n.sends[j].bytes.data()) == 1) {
+                        const paxos::PrepareReplyMsg *r = (const paxos::PrepareReplyMsg *)n.sends[j].bytes.data();
+                        std::map<paxos::InstanceID, paxos::AcceptedValue> vals;
+                        paxos::ExtractAcceptedValues(&logger, r->values_, r->len_, &vals);
+                        n.P += vals.size();
+                    }
+                n.sends.clear();
+                continue;
             }
             for (paxos::CommittingID id = cid0 + 1; id <= p->committing_id_; ++id) {
                 const u64 acc = type == 4 ? ((const paxos::AcceptReplyMsg *)m)->accept_ : 0;
@@ -378,6 +501,30 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
         }
     }
 
+    if (digest) {
+        // [C, P, A, L, V, chosen digest, state digest, scalar digest] as oracle/mpx_oracle.c dump()
+        u64 P = 0, A = 0, L = 0, ds = 0, dsc = 0, dc = 0;
+        std::map<u64, u64> chosen;
+        for (uint32_t i = 0; i < N; ++i) {
+            Node &n = ns[i];
+            paxos::PaxosImpl *p = n.impl;
+            dsc += mix64(mix64((u64)i * 0x9E3779B97F4A7C15ull ^ p->promised_proposal_id_) ^ p->max_proposal_id_);
+            for (int pass = 0; pass < 2; ++pass)
+                for (auto &e : pass ? p->committed_values_ : p->accepted_values_)
+                    ds += mix64(mix64(mix64(e.first + (u64)i * 0x9E3779B97F4A7C15ull) ^ e.second.proposal_id_)
+                                ^ (handle_of(e.second.value_) + (pass ? 2 : 1) * 0xD6E8FEB86659FD93ull));
+            P += n.P; A += n.A; L += n.L;
+            for (u64 k = 0; k < n.n_c; ++k) {
+                u64 bid = rd64((const uint8_t *)n.events_c.data() + 16 * k + 8);
+                for (auto &e : n.batch_values[bid])
+                    if (chosen.insert(std::make_pair(e.first, handle_of(e.second))).second)
+                        dc += mix64(mix64(e.first) ^ handle_of(e.second));
+            }
+        }
+        stats[0] = chosen.size(); stats[1] = P; stats[2] = A; stats[3] = L; stats[4] = 0;
+        stats[5] = dc; stats[6] = ds; stats[7] = dsc;
+        return 0;
+    }
     // canonical MPXR dump
     std::string r;
     r.append("MPXR", 4);
@@ -440,6 +587,17 @@ static int run_impl(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t
     // PaxosImpl objects are leaked on purpose: their dtor joins the (never
     // started) paxos thread and the timers hold raw pointers into them.
     return 0;
+}
+
+// Counters and digests of the instance shard [sb, se) of a trace, from the reference's own
+// handlers (full-size parity per (node, instance shard)); stats = the 8
+// words of oracle/mpx_oracle.c mpxo_run: C, P, A, L, violations (0: the reference would have
+// crashed), chosen / state / scalar digests.  Counters and digests of disjoint shards add up;
+// the scalar digest is the same on every shard.  oracle/ref_full_size.py runs the shards.
+extern "C" int mpxref_run_shard(const uint8_t *trace, uint64_t size, uint64_t sb, uint64_t se, uint64_t *stats)
+{
+    if (!stats || se <= sb) return -3;
+    return run_impl(trace, size, NULL, NULL, stats, NULL, NULL, sb, se);
 }
 
 // Timing entry for bench.py's cpu_baseline leg: apply `reps` passes of one

@@ -160,3 +160,37 @@ def ref_learns(trace):
 def oracle_commits(trace):
     """The oracle's restatement of the same bookkeeping (mpxo_commits)."""
     return _blob_call(ORACLE_SO, "mpxo_commits", trace)
+
+
+_ref_shard = {}
+
+
+def ref_run_shards(trace, shards):
+    """Counters + digests of a trace from the REFERENCE's own handlers, summed over `shards`
+    instance shards (oracle/_ref mpxref_run_shard / mpxref_member_run_shard: each shard's entries
+    only, every record's header; oracle/ref_full_size.py runs them at full size) ->
+    [C,P,A,L,0,chosen_digest,state_digest,scalar_digest] (the reference counts no violations)."""
+    member = trace[12:16] == b"\x01\x00\x00\x00"
+    name = "mpxref_member_run_shard" if member else "mpxref_run_shard"
+    if name not in _ref_shard:
+        f = getattr(ctypes.CDLL(REF_MEMBER_SO if member else REF_SO), name)
+        f.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                      ctypes.POINTER(ctypes.c_uint64)]
+        f.restype = ctypes.c_int
+        _ref_shard[name] = f
+    m = int.from_bytes(bytes(trace[16:24]), "little")
+    per = -(-m // shards)
+    tot, scal = [0] * 8, None
+    for k in range(shards):
+        st = (ctypes.c_uint64 * 8)()
+        se = (k + 1) * per if k + 1 < shards else (1 << 64) - 1
+        rc = _ref_shard[name](trace, len(trace), k * per, se, st)
+        if rc != 0:
+            raise RuntimeError("%s failed: %d" % (name, rc))
+        for w in range(7):
+            tot[w] = (tot[w] + st[w]) % (1 << 64)
+        if scal is not None and scal != st[7]:
+            raise RuntimeError("per-node scalars differ between shards")
+        scal = st[7]
+    tot[7] = scal
+    return tot

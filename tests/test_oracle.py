@@ -15,7 +15,7 @@ import pytest
 import mpxr
 from fuzztrace import fuzz_trace
 from mpxwire import container, value
-from oracles import oracle_run, ref_available, ref_run
+from oracles import oracle_run, ref_available, ref_run, ref_run_shards
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 INDEX = json.load(open(os.path.join(GOLD, "index.json")))
@@ -33,6 +33,24 @@ def test_oracle_matches_reference_golden(name):
     assert got == want, mpxr.diff(got, want)
     meta = INDEX[name]
     assert stats[:4] == [meta["C"], meta["P"], meta["A"], meta["L"]]
+
+
+@pytest.mark.ref
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("name", sorted(INDEX))
+def test_ref_shard_mode_matches_whole(name):
+    """The reference's instance-shard mode (oracle/ref_full_size.py: the full-size values in
+    tests/golden/full_size.json) sums to the whole-trace result over 1, 3 and 7 unaligned shards:
+    each shard's entries cut with the reference's own codec; member shards apply the marker's
+    membership step with the reference's own ChangeMemberships (a shard never learns the
+    instances below it, so Learner::Apply cannot); proposer-only bookkeeping (Propose, the id sets
+    below the shard) differs and stays out of the digests.  Whole == oracle stats here, and the
+    oracle == the reference's bytes on this golden (test_oracle_matches_reference_golden)."""
+    trace = _read(name, ".mpxt")
+    _, want, _ = oracle_run(trace)
+    want[4] = 0                                    # (violations: the reference would have crashed)
+    for shards in (1, 3, 7):
+        assert ref_run_shards(trace, shards) == want, shards
 
 
 def test_codec_unittest_vectors():

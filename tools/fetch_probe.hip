@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t *buf, uint64_t *si
     const T *p = reinterpret_cast<const T *>(buf);
     const uint64_t n = STREAM_BYTES / W, stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t acc = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) acc ^= fold<W>(p[i]);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) acc = acc * 31 + fold<W>(p[i]);
     if (acc == 0x0123456789abcdefull) sink[0] = acc;
 }
 
@@ -59,7 +59,8 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t *buf, uint64_t *si
     for (uint64_t t = tid; t < GROUPS * G; t += stride) {
         const uint64_t g = t / G, k = t % G;
         const uint64_t c = mix(g ^ salt) % chunks;
-        acc ^= fold<W>(*reinterpret_cast<const T *>(buf + c * (uint64_t)(W * G) + k * W));
+        // (a multiply, not a xor: with 4-B loads the guard's upper half must stay reachable)
+        acc = acc * 31 + fold<W>(*reinterpret_cast<const T *>(buf + c * (uint64_t)(W * G) + k * W));
     }
     if (acc == 0x0123456789abcdefull) sink[0] = acc;
 }
