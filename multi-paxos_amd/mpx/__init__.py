@@ -22,6 +22,7 @@ ABI_VERSION = 2
 SEM_MULTI, SEM_MEMBER = 0, 1
 FLAG_INCREMENTAL = 1            # mpx_config.flags: each mpx_run applies one window (include/mpx.h)
 FLAG_DECISIONS = 2              # with FLAG_INCREMENTAL: decisions carried across windows
+FLAG_LEARN_EPOCHS = 4           # member: roles from the applied membership Values (include/mpx.h)
 GEN_CLEAN, GEN_FAULTY, GEN_MEMBER = 0, 1, 2
 PRESENT = 1 << 63
 UID_BYTES = 128
@@ -112,6 +113,7 @@ def lib():
             "mpx_timing_every": [vp, ctypes.c_uint32],
             "mpx_drain_sends": [vp, SEND_FN, vp],
             "mpx_read_chosen": [vp, ctypes.c_uint64, ctypes.c_uint64, u64p],
+            "mpx_read_epochs": [vp, P(Epoch), ctypes.c_uint32, P(ctypes.c_uint32)],
             "mpx_read_node_scalars": [vp, ctypes.c_uint32, u64p, u64p],
             "mpx_read_executed": [vp, ctypes.c_uint32, u64p, u64p, u64p, ctypes.c_uint64],
             "mpx_read_node_state": [vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, u64p, u64p, u64p, u64p],
@@ -252,11 +254,24 @@ class Engine:
         self.shard_begin, self.shard_end = shard_begin, shard_end
 
     @classmethod
-    def for_trace(cls, trace, device=0):
+    def for_trace(cls, trace, device=0, flags=0):
+        """An engine for a whole MPXT trace.  flags FLAG_LEARN_EPOCHS (member): created with the
+        container's genesis epoch only; the engine learns the rest and ignores the container's
+        E_EPOCH records."""
         hd = trace_header(trace)
-        e = cls(hd["num_nodes"], 0, max(hd["num_instances"], 1), device=device, semantics=hd["semantics"])
+        epochs = trace_epochs(trace)[:1] if flags & FLAG_LEARN_EPOCHS else ()
+        e = cls(hd["num_nodes"], 0, max(hd["num_instances"], 1), device=device, semantics=hd["semantics"],
+                epochs=epochs, flags=flags)
         e.submit_trace(trace)
         return e
+
+    def epochs(self):
+        """The member epoch table [(version, acceptor_mask, proposer_mask, learner_mask)] (mpx_read_epochs)."""
+        n = ctypes.c_uint32()
+        _ck("mpx_read_epochs", lib().mpx_read_epochs(self.h, None, 0, ctypes.byref(n)))
+        arr = (Epoch * max(n.value, 1))()
+        _ck("mpx_read_epochs", lib().mpx_read_epochs(self.h, arr, n.value, ctypes.byref(n)))
+        return [(x.version, x.acceptor_mask, x.proposer_mask, x.learner_mask) for x in arr[: n.value]]
 
     def close(self):
         if self.h:

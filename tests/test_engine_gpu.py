@@ -148,6 +148,9 @@ def test_engine_c2_full_size_digests():
     assert [st["chosen"], st["promise_entries"], st["accept_apps"], st["commit_apps"], st["violations"],
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
     assert st["chosen"] == m and st["bytes_alg"] == 40 * n * m
+    import xxhash                                            # and == the reference's own handlers (full_size.json)
+    assert (len(t), "%016x" % xxhash.xxh3_64_intdigest(t)) == (FULL_SIZE["c2"]["trace_bytes"], FULL_SIZE["c2"]["trace_xxh3"])
+    assert {k: st[k] for k in STATS_ORDER} == FULL_SIZE["c2"]["stats"]
 
 
 def test_sends_match_dump():
@@ -547,15 +550,27 @@ STATS_ORDER = ("chosen", "promise_entries", "accept_apps", "commit_apps", "viola
                "chosen_digest", "state_digest", "scalar_digest")
 
 
-def _full_size_vs_oracle(kind, oracle_threads=1, **kw):
+# the same configs judged by the REFERENCE's own handlers, per instance shard (oracle/ref_full_size.py,
+# VERDICT r04 item 3): counters + digests, with the size and xxh3 of the trace they judged
+FULL_SIZE = json.load(open(os.path.join(GOLD, "full_size.json")))
+
+
+def _full_size_vs_oracle(kind, oracle_threads=1, ref=None, **kw):
     import time
     from oracles import oracle_run_sharded
     t0 = time.time()
     log = lambda m: print("[full-size] %s: %s (%.0f s)" % (kw.get("num_instances"), m, time.time() - t0), flush=True)
     t = mpx.generate_trace(kind, copy=False, **kw)           # the generator's buffer, no bytes copy
     log("generated %.1f GB" % (len(t) / 1e9))
+    if ref is not None:
+        import xxhash
+        r = FULL_SIZE[ref]
+        # the reference judged these very bytes (the generator is deterministic)
+        assert (len(t), "%016x" % xxhash.xxh3_64_intdigest(memoryview(t))) == (r["trace_bytes"], r["trace_xxh3"])
     want = oracle_run_sharded(t, shards=oracle_threads, threads=oracle_threads)   # CPU oracle, digests only
     log("oracle")
+    if ref is not None:                                      # restatement == reference at full size
+        assert want[:4] + want[5:] == [FULL_SIZE[ref]["stats"][k] for k in STATS_ORDER if k != "violations"]
     e = mpx.Engine.for_trace(t)
     del t
     log("ingested")
@@ -577,7 +592,7 @@ def test_c3_full_size_matches_oracle():
     drop 5 % / dup 10 % (<=3) / delay U[0,500) (multi/debug.conf.sample:1), batch U[1,256];
     every counter and order-independent digest equals the CPU oracle's."""
     st = _full_size_vs_oracle(mpx.GEN_FAULTY, num_nodes=7, num_instances=1 << 24, seed=0, batch=256,
-                              proposers=3, drop_rate=500, dup_rate=1000, max_delay=500)
+                              proposers=3, drop_rate=500, dup_rate=1000, max_delay=500, ref="c3")
     assert st["chosen"] >= 1 << 24 and st["promise_entries"] > 0 and st["violations"] == 0
 
 
@@ -588,7 +603,7 @@ def test_c5_contended_full_size_matches_oracle():
     entries; every counter and digest == the CPU oracle's (node-parallel, 8 threads)."""
     st = _full_size_vs_oracle(mpx.GEN_MEMBER, num_nodes=8, num_instances=1 << 25, seed=0, batch=256,
                               drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15, proposers=3,
-                              oracle_threads=8)
+                              oracle_threads=8, ref="c5c" if "c5c" in FULL_SIZE else None)
     assert st["promise_entries"] >= 10 ** 6 and st["violations"] == 0
 
 
@@ -597,7 +612,8 @@ def test_c5_full_size_matches_oracle():
     AddAcceptor(1..7) then DelAcceptor(1..7), 15 epochs (member/main.cpp:119-141), 1 % loss,
     1 % duplicates, stale in-flight ACCEPTs across version changes."""
     st = _full_size_vs_oracle(mpx.GEN_MEMBER, num_nodes=8, num_instances=1 << 25, seed=0, batch=256,
-                              drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15)
+                              drop_rate=100, dup_rate=100, max_delay=64, noop_permille=15,
+                              ref="c5" if "c5" in FULL_SIZE else None)
     assert st["chosen"] == 1 << 25 and st["violations"] == 0
 
 
@@ -1438,3 +1454,96 @@ def test_closed_loop_incremental_equals_replay():
     with mpx.Engine.for_trace(a[0]) as e:
         e.run()
         assert e.dump() == oracle_run(a[0])[0]
+
+
+# ---- membership learned at run time (MPX_FLAG_LEARN_EPOCHS; member/paxos.cpp:1040-1073,1864-1964) ----
+MEMBER_GOLDENS = sorted(k for k in INDEX if k.startswith(("c5_", "mm_")))
+
+
+def _strip_markers(streams):
+    """What NetWork::OnReceive hands a live node: the trace's records without the E_EPOCH markers."""
+    return [[r for r in s if r[:4] != b"\x12\x00\x00\x00"] for s in streams]
+
+
+@pytest.mark.parametrize("name", MEMBER_GOLDENS)
+def test_learned_epochs_match_reference(name):
+    """Every member golden on an engine created with the genesis epoch only: the engine applies the
+    membership Values its nodes' Learners apply (ingest EpochLearn) and places its own E_EPOCH
+    records — the result is the reference's byte for byte (its roles come from the reference's
+    own ChangeMemberships), the learned epoch table is the trace's, and the decisions and learns
+    are the reference's fixtures."""
+    trace, want = _read(name, ".mpxt"), _read(name, ".mpxr")
+    table = mpx.trace_epochs(trace)
+    with mpx.Engine.for_trace(trace, flags=mpx.FLAG_LEARN_EPOCHS) as e:
+        e.run()
+        assert e.dump() == want
+        got = e.epochs()
+        assert got == table[:len(got)] and len(got) > 1
+        if name in DECISIONS:
+            assert e.decisions() == _read(name, ".mpxd")
+        if name in LEARNS:
+            assert e.learns() == _read(name, ".mpxl")
+
+
+@pytest.mark.parametrize("name", ["c5_member_2", "c5_member_3", "c5_contended_2", "mm_learners", "mm_acceptor_reset"])
+def test_learned_epochs_in_windows_marker_free(name):
+    """A live member host: every node's stream WITHOUT its E_EPOCH markers, in 4 and 7 incremental
+    windows, on an engine that knows only the genesis epoch (MPX_FLAG_LEARN_EPOCHS): the epoch
+    table grows window by window as the nodes apply membership Values, and the windows give the
+    whole run's replies, counters, state, executed streams and chosen log, and the reference's
+    decisions and learns (MPXD / MPXL fixtures)."""
+    trace = _read(name, ".mpxt")
+    want = _whole(trace)
+    hd, epochs, streams = _node_streams(trace)
+    live = _strip_markers(streams)
+    n, m = hd["num_nodes"], max(hd["num_instances"], 1)
+    for W in (4, 7):
+        sends = [[] for _ in range(n)]
+        tot = {k: 0 for k in COUNTERS}
+        sizes = []
+        with mpx.Engine(n, 0, m, semantics=mpx.SEM_MEMBER, epochs=epochs[:1],
+                        flags=mpx.FLAG_INCREMENTAL | mpx.FLAG_DECISIONS | mpx.FLAG_LEARN_EPOCHS) as e:
+            prev = [0] * n
+            for w in range(1, W + 1):
+                cut = [len(s) * w // W for s in live]
+                for node, s in enumerate(live):
+                    if cut[node] > prev[node]:
+                        e.submit(node, s[prev[node]:cut[node]])
+                st = e.run()
+                prev = cut
+                for k in COUNTERS:
+                    tot[k] += st[k]
+                for src, dst, b in e.drain_sends():
+                    sends[src].append((dst, b))
+                sizes.append(len(e.epochs()))
+            assert e.epochs() == epochs[:sizes[-1]] and sizes[-1] > 1
+            assert sizes == sorted(sizes), sizes
+            if name.startswith("c5_"):
+                assert len(set(sizes)) >= 3, sizes                  # the table grows window by window
+            assert sends == want[0] and tot == want[1]
+            assert _observe(e, n, m) == want[2]
+            if name in DECISIONS:
+                assert e.decisions() == _read(name, ".mpxd")
+            if name in LEARNS:
+                assert e.learns() == _read(name, ".mpxl")
+
+
+@pytest.mark.parametrize("seed,props", [(81, 1), (82, 3)])
+def test_learned_epochs_c5_generated(seed, props):
+    """C5-shaped traces beyond fixture size (2^16 instances, contended too): the marker-free streams
+    on a genesis-only engine == the whole run with the generator's markers (state, digests,
+    decisions, learns), and every one of the schedule's 15 epochs is learned."""
+    t = mpx.generate_trace(mpx.GEN_MEMBER, num_nodes=8, num_instances=1 << 16, seed=seed, batch=128,
+                           drop_rate=200, dup_rate=200, max_delay=64, noop_permille=15, proposers=props)
+    with mpx.Engine.for_trace(t) as e:
+        st = e.run()
+        want = ({k: st[k] for k in COUNTERS}, e.state_digest(), e.decisions(), e.learns())
+    hd, epochs, streams = _node_streams(t)
+    live = _strip_markers(streams)
+    with mpx.Engine(8, 0, hd["num_instances"], semantics=mpx.SEM_MEMBER, epochs=epochs[:1],
+                    flags=mpx.FLAG_LEARN_EPOCHS) as e:
+        for node, s in enumerate(live):
+            e.submit(node, s)
+        st = e.run()
+        assert ({k: st[k] for k in COUNTERS}, e.state_digest(), e.decisions(), e.learns()) == want
+        assert e.epochs() == epochs and len(epochs) == 15
