@@ -128,6 +128,8 @@ struct mpx_engine {
     hipStream_t comm_stream = nullptr;
     hipStream_t stream2 = nullptr;                  // a run's promise-round pairs beside its plan path
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    hipStream_t stream3 = nullptr;                  // the listed pairs and the chosen log beside the store chain
+    hipEvent_t fork3a = nullptr, fork3b = nullptr, join3 = nullptr;
     hipEvent_t sum_ev[2] = {nullptr, nullptr}, ag_ev[2] = {nullptr, nullptr};
     bool ag_pending[2] = {false, false};
     uint32_t sum_idx = 0;
@@ -260,6 +262,9 @@ extern "C" int mpx_destroy(mpx_engine *e)
     if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
     if (e->join_ev) (void)hipEventDestroy(e->join_ev);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
+    if (e->stream3) (void)hipStreamSynchronize(e->stream3);
+    for (hipEvent_t x : {e->fork3a, e->fork3b, e->join3}) if (x) (void)hipEventDestroy(x);
+    if (e->stream3) (void)hipStreamDestroy(e->stream3);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     prop_free(e->prop);
     mprop_free(e->mprop);
@@ -400,16 +405,15 @@ static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, cons
         return MPX_OK;
     }
     // large traces: the nodes' streams are independent records, decoded on one
-    // host thread each (own value table, merged after; the same MPX_E_VALUE
-    // check across nodes), so ingest scales with the node count
+    // host thread each into the one value table (sharded, a lock per shard: the same
+    // MPX_E_VALUE check across nodes), so ingest scales with the node count
     const uint64_t t0 = now_ns();
-    std::vector<ValueTable> vts(N);
     std::vector<IngestViolation> ivs(N);
     std::vector<int> rcs(N, MPX_OK);
+    SectionCache sc;                                 // (one decode per distinct entry list, this call)
     const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
     std::vector<std::thread> th;
     for (uint32_t n = 0; n < N; ++n) {
-        vts[n].member = member;
         th.emplace_back([&, n]() {
             const uint64_t *offs; const uint8_t *bytes;
             const uint64_t cnt = stream(n, offs, bytes);
@@ -418,16 +422,15 @@ static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, cons
                 if (offs[i + 1] < offs[i]) { rcs[n] = MPX_E_INVAL; break; }
                 const uint8_t *m = bytes + offs[i];
                 const size_t len = (size_t)(offs[i + 1] - offs[i]);
-                rcs[n] = member ? decode_record_member(vts[n], ns, n, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n],
-                                                       e->elearn.empty() ? nullptr : &e->elearn[n])
-                                : decode_record(vts[n], ns, n, N, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n]);
+                rcs[n] = member ? decode_record_member(e->vt, ns, n, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n],
+                                                       e->elearn.empty() ? nullptr : &e->elearn[n], &sc)
+                                : decode_record(e->vt, ns, n, N, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n], &sc);
             }
         });
     }
     for (auto &x : th) x.join();
     for (uint32_t n = 0; n < N; ++n) {
         TRY(rcs[n]);
-        TRY(e->vt.merge(vts[n]));
         if (ivs[n].count) {                          // first violation in node order
             if (!e->iv.code) { e->iv.code = ivs[n].code; e->iv.node = ivs[n].node; e->iv.seq = ivs[n].seq; e->iv.iid = ivs[n].iid; }
             e->iv.count += ivs[n].count;
@@ -813,9 +816,21 @@ static int queue_run(mpx_engine *e, bool digest)
         HTRY(hipStreamCreateWithPriority(&e->stream2, hipStreamNonBlocking, prio));
         HTRY(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
         HTRY(hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming));
+        // the third stream at the highest priority: its own hardware-queue pool again, so neither
+        // side stream shares the plan path's queue (MPX_SIDE3_PRIO=normal|low|high, A/B)
+        const char *sp3 = ab_env("MPX_SIDE3_PRIO");
+        const std::string pr3 = sp3 ? sp3 : "high";
+        const int prio3 = pr3 == "high" ? greatest : pr3 == "normal" ? 0 : least;
+        HTRY(hipStreamCreateWithPriority(&e->stream3, hipStreamNonBlocking, prio3));
+        HTRY(hipEventCreate(&e->fork3a));           // (ride on kernel launches as their stop events)
+        HTRY(hipEventCreate(&e->fork3b));
+        HTRY(hipEventCreateWithFlags(&e->join3, hipEventDisableTiming));
     }
-    LaunchSide side{nullptr, nullptr, nullptr};
-    if (!ab_env("MPX_ONE_STREAM")) side = LaunchSide{e->stream2, e->fork_ev, e->join_ev};
+    LaunchSide side{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (!ab_env("MPX_ONE_STREAM")) side = LaunchSide{e->stream2, e->fork_ev, e->join_ev, nullptr, nullptr, nullptr, nullptr};
+    if (!ab_env("MPX_ONE_STREAM") && !ab_env("MPX_TWO_STREAMS")) {
+        side.stream3 = e->stream3; side.fork3a = e->fork3a; side.fork3b = e->fork3b; side.join3 = e->join3;
+    }
     int rc = launch_run(e->view, e->stream, g, evp, side);
     if (rc) return MPX_E_HIP;
     if (e->incremental) {                              // the next window starts from this one's scalars, rounds, roles

@@ -594,6 +594,11 @@ int gen_member(const mpx_gen_params &p, std::string &out)
     g.chosen_h.assign(g.cap, 0);
     g.nd.resize(U);
     for (uint32_t n = 0; n < U; ++n) g.nd[n].learned_pid.assign(g.cap, 0);
+    // address space for each node's stream up front, somewhat above its mean size (C5: 82 B per
+    // instance, contended 152 B; pages are only touched as they are written): a stream that grew by
+    // doubling copied itself and held both copies at once — 2^25 contended traces (41 GB) peaked
+    // past 60 GB of resident memory that way
+    for (uint32_t n = 0; n < U; ++n) g.nd[n].bytes.reserve((size_t)std::min<uint64_t>(g.M, 1ull << 30) * (p.proposers > 1 ? 224 : 128));
     SimNode &L = g.nd[0];
     L.acc = true;
     L.learners = 1;

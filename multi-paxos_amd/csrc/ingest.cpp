@@ -9,6 +9,7 @@
 #include "ingest.hpp"
 
 #include <algorithm>
+#include <thread>
 #include <cstring>
 
 #include "mpx.h"
@@ -18,6 +19,7 @@ namespace mpx {
 static inline uint32_t rd32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
 static inline uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 template <typename T> static inline void app(std::string &s, T v) { s.append((const char *)&v, sizeof v); }
+#define TRY_RC(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
 
 // member Value_m (FillValue / ExtractValue, member/paxos.cpp:330-408): the
 // multi layout plus a membership change list {u32 node, u32 type}* in place of
@@ -56,10 +58,134 @@ static long parse_member(const uint8_t *p, size_t avail, std::string &enc, uint3
     return (long)used;
 }
 
-long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle)
+static inline size_t slot_of(uint64_t h, size_t mask) { return (size_t)((h * 0xD6E8FEB86659FD93ull) >> 20) & mask; }
+
+const ValueTable::Rec *ValueTable::Shard::find(uint64_t h) const
+{
+    if (key.empty()) return nullptr;
+    const size_t mask = key.size() - 1;
+    for (size_t i = slot_of(h, mask);; i = (i + 1) & mask) {
+        if (key[i] == h) return &rec[i];
+        if (key[i] == EMPTY) return nullptr;
+    }
+}
+
+ValueTable::Rec *ValueTable::Shard::insert(uint64_t h, bool &fresh)
+{
+    if (2 * (count + 1) > key.size()) {                       // grow: at most half full
+        std::vector<uint64_t> k2(key.empty() ? 1024 : 2 * key.size(), EMPTY);
+        std::vector<Rec> r2(k2.size());
+        const size_t m2 = k2.size() - 1;
+        for (size_t i = 0; i < key.size(); ++i) {
+            if (key[i] == EMPTY) continue;
+            size_t j = slot_of(key[i], m2);
+            while (k2[j] != EMPTY) j = (j + 1) & m2;
+            k2[j] = key[i]; r2[j] = rec[i];
+        }
+        key.swap(k2); rec.swap(r2);
+    }
+    const size_t mask = key.size() - 1;
+    size_t i = slot_of(h, mask);
+    while (key[i] != EMPTY && key[i] != h) i = (i + 1) & mask;
+    fresh = key[i] == EMPTY;
+    if (fresh) { key[i] = h; ++count; }
+    return &rec[i];
+}
+
+int ValueTable::intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_off, uint32_t exec_len)
+{
+    Shard &x = sh[shard_of(h)];
+    std::lock_guard<std::mutex> g(x.mu);
+    bool fresh = false;
+    Rec *r = x.insert(h, fresh);
+    if (!fresh) return r->len != len || std::memcmp(r->p, b, len) != 0 ? MPX_E_VALUE : MPX_OK;
+    char *dst;
+    if (len > BLOCK / 4) {                                   // (a long value: a block of its own)
+        x.blocks.emplace_back(new char[len]);
+        dst = x.blocks.back().get();
+        if (x.blocks.size() > 1) std::swap(x.blocks.back(), x.blocks[x.blocks.size() - 2]);   // (the arena block stays last)
+    } else {
+        if (x.used + len > BLOCK || x.blocks.empty()) { x.blocks.emplace_back(new char[BLOCK]); x.used = 0; }
+        dst = x.blocks.back().get() + x.used;
+        x.used += len;
+    }
+    std::memcpy(dst, b, len);
+    *r = Rec{dst, len, exec_off, exec_len};
+    return MPX_OK;
+}
+
+// the key of a section: its length and sampled bytes (the candidates are compared in full)
+static uint64_t section_key(const uint8_t *b, size_t len, bool with_pid)
+{
+    uint64_t h = (len * 0x9E3779B97F4A7C15ull) ^ (with_pid ? 0x5851F42D4C957F2Dull : 0);
+    auto mix = [&](uint64_t x) { h ^= x; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 31; };
+    const size_t k = len < 64 ? len / 8 : 8;
+    for (size_t i = 0; i < k; ++i) { uint64_t x; std::memcpy(&x, b + 8 * i, 8); mix(x); }
+    for (size_t i = 0; len >= 128 && i < 8; ++i) { uint64_t x; std::memcpy(&x, b + len - 64 + 8 * i, 8); mix(x); }
+    return h;
+}
+
+bool SectionCache::claim(const uint8_t *b, size_t len, bool with_pid)
+{
+    const uint64_t key = section_key(b, len, with_pid);
+    Shard &x = sh[(key * 0x9E3779B97F4A7C15ull) >> 58];
+    std::lock_guard<std::mutex> g(x.mu);
+    auto r = x.m.equal_range(key);
+    for (auto it = r.first; it != r.second; ++it) {
+        const Ent &c = it->second;
+        if (c.len == len && c.with_pid == with_pid && (c.b == b || std::memcmp(c.b, b, len) == 0)) return false;
+    }
+    x.m.emplace(key, Ent{b, len, with_pid});
+    return true;
+}
+
+// One Value's handle, length and kind off the wire without the table (a section another thread
+// interns): the same layout checks as ValueTable::parse, FillValue / ExtractValue
+// (multi/paxos.cpp:556-644; member Value_m, member/paxos.cpp:330-408)
+static long skim(const uint8_t *p, size_t avail, bool member, uint64_t *handle, bool *mem)
+{
+    if (avail < 13) return MPX_E_DECODE;
+    const uint32_t proposer = rd32(p);
+    const uint64_t value_id = rd64(p + 4);
+    if (proposer >= (1u << 14) || value_id >= (1ull << 47)) return MPX_E_RANGE;
+    const bool noop = p[12] != 0;
+    *handle = MPX_HANDLE(proposer, noop, value_id);
+    if (mem) *mem = false;
+    if (noop) return 13;
+    if (avail < 14) return MPX_E_DECODE;
+    const bool m = p[13] != 0;
+    if (member) {
+        if (avail < 18) return MPX_E_DECODE;
+        const uint32_t n = rd32(p + 14);
+        size_t used = 18;
+        if (m) { if ((avail - used) / 8 < n) return MPX_E_DECODE; used += 8 * (size_t)n; }
+        else { if (avail - used < n) return MPX_E_DECODE; used += n; }
+        if (avail - used < 4) return MPX_E_DECODE;
+        const uint32_t cbl = rd32(p + used);
+        used += 4;
+        if (avail - used < cbl) return MPX_E_DECODE;
+        if (mem) *mem = m;
+        return (long)(used + cbl);
+    }
+    if (m) {
+        if (avail < 19) return MPX_E_DECODE;
+        if (p[18] == 0) return 19;
+        if (avail < 23) return MPX_E_DECODE;
+        const uint32_t iplen = rd32(p + 19);
+        if (avail < 25 + (size_t)iplen) return MPX_E_DECODE;
+        return (long)(25 + iplen);
+    }
+    if (avail < 18) return MPX_E_DECODE;
+    const uint32_t len = rd32(p + 14);
+    if (avail < 18 + (size_t)len) return MPX_E_DECODE;
+    return (long)(18 + len);
+}
+
+long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle, bool *mem)
 {
     // FillValue / ExtractValue layout, multi/paxos.cpp:556-644
     if (avail < 13) return MPX_E_DECODE;
+    if (mem) *mem = false;
     if (member) {
         const uint32_t proposer = rd32(p);
         const uint64_t value_id = rd64(p + 4);
@@ -69,16 +195,8 @@ long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle)
         const long used = parse_member(p, avail, enc, eo, el);
         if (used < 0) return used;
         const uint64_t h = MPX_HANDLE(proposer, p[12] != 0, value_id);
-        auto it = idx.find(h);
-        if (it != idx.end()) {
-            const Rec &r = it->second;
-            if (r.len != enc.size() || std::memcmp(bytes.data() + r.off, enc.data(), enc.size()) != 0)
-                return MPX_E_VALUE;
-        } else {
-            idx.emplace(h, Rec{bytes.size(), (uint32_t)enc.size(), eo, el});
-            bytes += enc;
-            if (eo == NONE32) membership.insert(h);
-        }
+        TRY_RC(intern(h, enc.data(), (uint32_t)enc.size(), eo, el));
+        if (mem) *mem = eo == NONE32;
         *handle = h;
         return used;
     }
@@ -100,14 +218,7 @@ long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle)
         }
         if (used) {
             const uint64_t h = MPX_HANDLE(proposer, noop, value_id);
-            auto it = idx.find(h);
-            if (it != idx.end()) {
-                const Rec &r = it->second;
-                if (r.len != used || std::memcmp(bytes.data() + r.off, p, used) != 0) return MPX_E_VALUE;
-            } else {
-                idx.emplace(h, Rec{bytes.size(), (uint32_t)used, eo, el});
-                bytes.append((const char *)p, used);
-            }
+            TRY_RC(intern(h, (const char *)p, (uint32_t)used, eo, el));
             *handle = h;
             return (long)used;
         }
@@ -153,23 +264,18 @@ long ValueTable::parse(const uint8_t *p, size_t avail, uint64_t *handle)
         }
     }
     const uint64_t h = MPX_HANDLE(proposer, noop, value_id);
-    auto it = idx.find(h);
-    if (it != idx.end()) {
-        const Rec &r = it->second;
-        if (r.len != enc.size() || std::memcmp(bytes.data() + r.off, enc.data(), enc.size()) != 0)
-            return MPX_E_VALUE;
-    } else {
-        Rec r{bytes.size(), (uint32_t)enc.size(), exec_off, exec_len};
-        bytes += enc;
-        idx.emplace(h, r);
-    }
+    TRY_RC(intern(h, enc.data(), (uint32_t)enc.size(), exec_off, exec_len));
     *handle = h;
     return (long)used;
 }
 
 int ValueTable::plain(uint64_t h)
 {
-    if (idx.count(h)) return MPX_OK;
+    {
+        Shard &x = sh[shard_of(h)];
+        std::lock_guard<std::mutex> g(x.mu);
+        if (x.find(h)) return MPX_OK;
+    }
     if (MPX_HANDLE_PROPOSER(h) >= (1u << 14) || (h & MPX_PRESENT)) return MPX_E_RANGE;
     // the canonical bytes of Value(proposer, value_id, noop) with an empty payload (FillValue,
     // multi/paxos.cpp:567-599; member Value_m adds the callback length, :321-408)
@@ -184,36 +290,18 @@ int ValueTable::plain(uint64_t h)
         eo = (uint32_t)enc.size();
         if (member) app<uint32_t>(enc, 0);
     }
-    idx.emplace(h, Rec{bytes.size(), (uint32_t)enc.size(), eo, 0});
-    bytes += enc;
-    return MPX_OK;
+    return intern(h, enc.data(), (uint32_t)enc.size(), eo, 0);
 }
 
-int ValueTable::merge(const ValueTable &o)
-{
-    idx.reserve(idx.size() + o.idx.size());
-    for (const auto &kv : o.idx) {
-        const Rec &r = kv.second;
-        auto it = idx.find(kv.first);
-        if (it != idx.end()) {
-            const Rec &q = it->second;
-            if (q.len != r.len || std::memcmp(bytes.data() + q.off, o.bytes.data() + r.off, r.len) != 0) return MPX_E_VALUE;
-            continue;
-        }
-        idx.emplace(kv.first, Rec{bytes.size(), r.len, r.exec_off, r.exec_len});
-        bytes.append(o.bytes, r.off, r.len);
-    }
-    membership.insert(o.membership.begin(), o.membership.end());
-    return MPX_OK;
-}
-
-bool ValueTable::changes(uint64_t h, std::vector<std::pair<uint32_t, uint32_t>> &out) const
+bool ValueTable::changes(uint64_t h, std::vector<std::pair<uint32_t, uint32_t>> &out)
 {
     out.clear();
-    auto it = idx.find(h);
-    if (it == idx.end() || it->second.exec_off != NONE32) return false;
+    Shard &x = sh[shard_of(h)];
+    std::lock_guard<std::mutex> g(x.mu);                  // (other decode threads may append to the shard)
+    const Rec *r = x.find(h);
+    if (!r || r->exec_off != NONE32) return false;
     // canonical Value_m bytes (parse_member): ... u8 membership @13, u32 n @14, n x {u32 node, u32 type} @18
-    const uint8_t *p = (const uint8_t *)bytes.data() + it->second.off;
+    const uint8_t *p = (const uint8_t *)r->p;
     const uint32_t n = rd32(p + 14);
     for (uint32_t k = 0; k < n; ++k) out.emplace_back(rd32(p + 18 + 8 * k), rd32(p + 22 + 8 * k));
     return true;
@@ -245,9 +333,8 @@ static int change_memberships(mpx_epoch &v, const std::vector<std::pair<uint32_t
 
 bool ValueTable::encode(uint64_t h, std::string &out) const
 {
-    auto it = idx.find(h);
-    if (it != idx.end()) {
-        out.append(bytes.data() + it->second.off, it->second.len);
+    if (const Rec *r = find(h)) {
+        out.append(r->p, r->len);
         return true;
     }
     if (synthetic_clean && MPX_HANDLE_PROPOSER(h) == 0 && !MPX_HANDLE_NOOP(h)) {
@@ -263,10 +350,9 @@ bool ValueTable::encode(uint64_t h, std::string &out) const
 
 bool ValueTable::exec_payload(uint64_t h, std::string &out) const
 {
-    auto it = idx.find(h);
-    if (it != idx.end()) {
-        if (it->second.exec_off == NONE32) return false;     // member: ChangeMemberships
-        out.assign(bytes.data() + it->second.off + it->second.exec_off, it->second.exec_len);
+    if (const Rec *r = find(h)) {
+        if (r->exec_off == NONE32) return false;             // member: ChangeMemberships
+        out.assign(r->p + r->exec_off, r->exec_len);
         return true;
     }
     if (synthetic_clean && MPX_HANDLE_PROPOSER(h) == 0 && !MPX_HANDLE_NOOP(h)) {
@@ -275,8 +361,6 @@ bool ValueTable::exec_payload(uint64_t h, std::string &out) const
     }
     return false;
 }
-
-#define TRY_RC(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
 
 static void flag(IngestViolation &v, uint64_t code, uint64_t node, uint64_t seq, uint64_t iid)
 {
@@ -291,8 +375,11 @@ static bool sort_entries(std::vector<uint64_t> &iid, std::vector<uint64_t> &pid,
 // PREPARE_REPLY body, sorted by iid (the reference's std::map order)
 static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool with_pid,
                           std::vector<uint64_t> &iid, std::vector<uint64_t> &pid,
-                          std::vector<uint64_t> &val, size_t &n_all, bool &dup)
+                          std::vector<uint64_t> &val, size_t &n_all, bool &dup,
+                          std::vector<uint64_t> *memh = nullptr, SectionCache *sc = nullptr)
 {
+    // the first thread to meet these bytes interns their Values, the others skim them
+    const bool own = !sc || !len || sc->claim(b, len, with_pid);
     size_t cur = 0;
     const size_t first = iid.size();
     n_all = 0;
@@ -303,8 +390,10 @@ static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool wit
         const uint64_t pd = with_pid ? rd64(b + cur + 8) : 0;
         cur += need;
         uint64_t h;
-        const long u = vt.parse(b + cur, len - cur, &h);
+        bool mem = false;
+        const long u = own ? vt.parse(b + cur, len - cur, &h, &mem) : skim(b + cur, len - cur, vt.member, &h, &mem);
         if (u < 0) return (int)u;
+        if (mem && memh) memh->push_back(h);          // (member membership Values: MPX_FLAG_LEARN_EPOCHS)
         cur += (size_t)u;
         iid.push_back(i);
         if (with_pid) pid.push_back(pd);
@@ -344,7 +433,7 @@ static bool sort_entries(std::vector<uint64_t> &iid, std::vector<uint64_t> &pid,
 }
 
 int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, const uint8_t *m, size_t len,
-                  uint64_t sb, uint64_t se, IngestViolation &viol)
+                  uint64_t sb, uint64_t se, IngestViolation &viol, SectionCache *sc)
 {
     if (len < 4) return MPX_E_DECODE;
     const uint32_t t = rd32(m);
@@ -405,7 +494,7 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         if (20 + (size_t)vl > len) return MPX_E_DECODE;
         const size_t first = ns.r_iid.size();
         size_t n_all; bool dup;
-        int rc = decode_entries(vt, m + 20, vl, true, ns.r_iid, ns.r_pid, ns.r_val, n_all, dup);
+        int rc = decode_entries(vt, m + 20, vl, true, ns.r_iid, ns.r_pid, ns.r_val, n_all, dup, nullptr, sc);
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
@@ -425,7 +514,7 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         const size_t first = ns.e_iid.size();
         size_t n_all; bool dup;
         std::vector<uint64_t> nopid;
-        int rc = decode_entries(vt, m + 28, vl, false, ns.e_iid, nopid, ns.e_val, n_all, dup);
+        int rc = decode_entries(vt, m + 28, vl, false, ns.e_iid, nopid, ns.e_val, n_all, dup, nullptr, sc);
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
@@ -456,7 +545,7 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         const size_t first = ns.e_iid.size();
         size_t n_all; bool dup;
         std::vector<uint64_t> nopid;
-        int rc = decode_entries(vt, m + 16, vl, false, ns.e_iid, nopid, ns.e_val, n_all, dup);
+        int rc = decode_entries(vt, m + 16, vl, false, ns.e_iid, nopid, ns.e_val, n_all, dup, nullptr, sc);
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
@@ -555,7 +644,7 @@ int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord
 }
 
 int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const uint8_t *m, size_t len,
-                         uint64_t sb, uint64_t se, IngestViolation &viol, EpochLearn *el)
+                         uint64_t sb, uint64_t se, IngestViolation &viol, EpochLearn *el, SectionCache *sc)
 {
     if (len < 4) return MPX_E_DECODE;
     const uint32_t t = rd32(m);
@@ -575,19 +664,24 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         return (uint32_t)(w - first);
     };
     std::vector<uint64_t> applied;                // (el) membership Values this LEARN makes the node apply
+    std::vector<uint64_t> memh;                   // (el) the membership Values among this record's entries
     // the Learner's apply loop over one LEARN's entries, every instance (not only the shard's)
     auto learn = [&](size_t first, size_t end) {
         for (size_t k = first; k < end; ++k) {
             const uint64_t i = ns.e_iid[k];
             if (i < el->front) continue;                          // applied already (insert: no change)
-            if (i > el->front) { el->above.emplace(i, ns.e_val[k]); continue; }
-            uint64_t h = ns.e_val[k];
+            const uint64_t h0 = ns.e_val[k];
+            const bool m0 = !memh.empty() && std::find(memh.begin(), memh.end(), h0) != memh.end();
+            if (i > el->front) { el->above.emplace(i, std::make_pair(h0, m0)); continue; }
+            uint64_t h = h0;
+            bool mem = m0;
             for (;;) {                                            // apply at the frontier, then what waited above it
-                if (vt.is_membership(h)) applied.push_back(h);
+                if (mem) applied.push_back(h);
                 ++el->front;
                 auto it = el->above.begin();
                 if (it == el->above.end() || it->first != el->front) break;
-                h = it->second;
+                h = it->second.first;
+                mem = it->second.second;
                 el->above.erase(it);
             }
         }
@@ -596,7 +690,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
     auto entries = [&](const uint8_t *b, size_t l) -> int {
         const size_t first = ns.e_iid.size();
         size_t n_all; bool dup;
-        int rc = decode_entries(vt, b, l, true, ns.e_iid, ns.e_pid, ns.e_val, n_all, dup);
+        int rc = decode_entries(vt, b, l, true, ns.e_iid, ns.e_pid, ns.e_val, n_all, dup, el ? &memh : nullptr, sc);
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         if (el && t == MPX_MSG_COMMIT) learn(first, ns.e_iid.size());
@@ -633,7 +727,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         if (20 + (size_t)vl > len) return MPX_E_DECODE;
         const size_t first = ns.r_iid.size();
         size_t n_all; bool dup;
-        int rc = decode_entries(vt, m + 20, vl, true, ns.r_iid, ns.r_pid, ns.r_val, n_all, dup);
+        int rc = decode_entries(vt, m + 20, vl, true, ns.r_iid, ns.r_pid, ns.r_val, n_all, dup, nullptr, sc);
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;

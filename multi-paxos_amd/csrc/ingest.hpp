@@ -1,8 +1,11 @@
 // ingest.hpp — host side of mpx_submit: wire decode into SoA, value table,
 // instance bucketing into fragments.
 #pragma once
+#include <atomic>
 #include <cstdint>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -15,33 +18,73 @@
 namespace mpx {
 
 // Interned reference Values: handle -> canonical FillValue bytes
-// (multi/paxos.cpp:556-598) and what StateMachine::Execute receives.
+// (multi/paxos.cpp:556-598) and what StateMachine::Execute receives.  Sharded by handle, each
+// shard behind its own lock, so the node-parallel decode threads intern into one table (no
+// per-thread tables merged afterwards); the readers (encode, exec_payload) run when no decode
+// is in flight.
 struct ValueTable {
-    struct Rec { uint64_t off; uint32_t len; uint32_t exec_off; uint32_t exec_len; };
-    std::unordered_map<uint64_t, Rec> idx;
-    std::string bytes;
+    struct Rec { const char *p; uint32_t len; uint32_t exec_off; uint32_t exec_len; };
+    static constexpr uint32_t SHARDS = 64;
+    static constexpr size_t BLOCK = 1 << 20;
+    static constexpr uint64_t EMPTY = ~0ull;            // (no handle: proposer < 2^14 keeps bits 62-63 clear)
+    // open addressing, linear probing, at most half full: no allocation per Value (a node-based
+    // map spent ~190 ns per insert at C3 window sizes, most of the host's decode time)
+    struct Shard {
+        std::mutex mu;
+        std::vector<uint64_t> key;
+        std::vector<Rec> rec;
+        size_t count = 0;
+        std::vector<std::unique_ptr<char[]>> blocks;     // canonical bytes: stable addresses, no regrowth copies
+        size_t used = BLOCK;                             // bytes used in the last block
+        const Rec *find(uint64_t h) const;
+        Rec *insert(uint64_t h, bool &fresh);
+    };
+    std::unique_ptr<Shard[]> sh{new Shard[SHARDS]};
     // synthetic resolver for device-generated clean traces: value_id v of
     // proposer 0 is the decimal string of v-1
     bool synthetic_clean = false;
     // member Value_m codec (member/paxos.cpp:321-408): + cb, membership list
     bool member = false;
-    // parse one Value; returns bytes used (>0) or a negative MPX_E_* code
-    long parse(const uint8_t *p, size_t avail, uint64_t *handle);
+    static uint32_t shard_of(uint64_t h) { return (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> 58); }
+    // parse one Value; returns bytes used (>0) or a negative MPX_E_* code; *mem: a member
+    // membership Value (a change list instead of a payload)
+    long parse(const uint8_t *p, size_t avail, uint64_t *handle, bool *mem = nullptr);
     bool encode(uint64_t handle, std::string &out) const;    // canonical bytes
     // what StateMachine::Execute / Apply receives; false for unknown handles
     // and for member membership Values (applied by ChangeMemberships instead)
     bool exec_payload(uint64_t handle, std::string &out) const;
-    void clear() { idx.clear(); bytes.clear(); synthetic_clean = false; }
-    // add every Value of `o` (decoded on another thread); MPX_E_VALUE when a
-    // handle names different bytes in the two tables
-    int merge(const ValueTable &o);
+    void clear()
+    {
+        for (uint32_t k = 0; k < SHARDS; ++k) {
+            Shard &x = sh[k];
+            x.key.clear(); x.rec.clear(); x.count = 0; x.blocks.clear(); x.used = BLOCK;
+        }
+        synthetic_clean = false;
+    }
     // a handle with no bytes yet: the payload-free Value it names (mpx_submit_soa)
     int plain(uint64_t handle);
-    // member: the handles of membership Values (Value_m with a change list) and their lists
-    std::unordered_set<uint64_t> membership;
-    bool is_membership(uint64_t h) const { return !membership.empty() && membership.count(h) != 0; }
     // {node, MembershipChangeType} of a membership Value, in its order (member/paxos.cpp:365-390)
-    bool changes(uint64_t h, std::vector<std::pair<uint32_t, uint32_t>> &out) const;
+    bool changes(uint64_t h, std::vector<std::pair<uint32_t, uint32_t>> &out);
+    // the canonical bytes of handle h, interned (thread-safe): MPX_E_VALUE when h already names
+    // other bytes (a Value is named by (proposer, value_id), multi/paxos.cpp:439)
+    int intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_off, uint32_t exec_len);
+    const Rec *find(uint64_t h) const { return sh[shard_of(h)].find(h); }
+};
+
+// One submit call's value sections (the entry lists of ACCEPT / COMMIT / P_BATCH / PREPARE_REPLY
+// bodies) already interned: a broadcast reaches every node with the same bytes, and a batch's
+// ACCEPT, COMMIT and P_BATCH carry the same list, so the first decode thread to meet a section
+// interns its Values (ValueTable::parse) and every other one only reads its entries off the wire
+// (the handle is (proposer, noop, value_id) itself) — no thread waits for another, and the table
+// sees each distinct Value about once.  Sections are compared in full (the key only picks
+// candidates) and point into the submitted buffers: the set lives for one submit call.
+struct SectionCache {
+    struct Ent { const uint8_t *b; size_t len; bool with_pid; };
+    static constexpr uint32_t SHARDS = 64;
+    struct Shard { std::mutex mu; std::unordered_multimap<uint64_t, Ent> m; };
+    std::unique_ptr<Shard[]> sh{new Shard[SHARDS]};
+    // true for the first caller with these bytes (it interns them)
+    bool claim(const uint8_t *b, size_t len, bool with_pid);
 };
 
 // Membership discovered at run time (MPX_FLAG_LEARN_EPOCHS, member semantics): every node's
@@ -55,7 +98,7 @@ struct ValueTable {
 // lists agree on their common prefix (checked when they are merged, mpx_engine::epochs).
 struct EpochLearn {
     uint64_t front = 0;
-    std::map<uint64_t, uint64_t> above;           // learned, not yet applied: iid -> handle
+    std::map<uint64_t, std::pair<uint64_t, bool>> above;   // learned, not yet applied: iid -> (handle, membership)
     mpx_epoch view{};                             // NodeImpl's version_ / acceptors_ / proposers_ / learners_
     std::vector<mpx_epoch> steps;                 // epochs 1.. this node reached
 };
@@ -72,7 +115,12 @@ struct NodeStream {
     std::vector<uint64_t> r_iid, r_pid, r_val;    // PREPARE_REPLY entries (in shard)
     std::vector<uint64_t> g_a, g_b;               // PREPARE ranges (all), sorted by start
     std::vector<uint8_t> part;                    // 1: the record carried entries, none in the shard
-    void clear() { *this = NodeStream(); }
+    // (keeps the capacity: a live engine decodes window after window into the same streams)
+    void clear()
+    {
+        type.clear(); src.clear(); ballot.clear(); aux.clear(); ent.clear(); cnt.clear(); e_iid.clear(); e_val.clear();
+        e_pid.clear(); ver.clear(); r_iid.clear(); r_pid.clear(); r_val.clear(); g_a.clear(); g_b.clear(); part.clear();
+    }
 };
 
 struct IngestViolation { uint64_t code = 0, node = 0, seq = 0, iid = 0, count = 0; };
@@ -163,7 +211,7 @@ struct HostTrace {
 // [shard_begin, shard_end) are dropped; a record whose entries all lie outside
 // is marked (`part`) and left out by build_trace (header sharding).
 int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, const uint8_t *m, size_t len,
-                  uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol);
+                  uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol, SectionCache *sc = nullptr);
 // one record handed over already decoded (mpx_submit_soa, multi semantics): the same
 // NodeStream fields decode_record fills from the wire bytes
 struct SoaRecord {
@@ -178,7 +226,8 @@ int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord
 // the record's E_EPOCH markers come from the engine: a submitted E_EPOCH is dropped, and a LEARN
 // that makes the node apply membership Values is followed by one E_EPOCH per Value
 int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const uint8_t *m, size_t len,
-                         uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol, EpochLearn *el = nullptr);
+                         uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol, EpochLearn *el = nullptr,
+                         SectionCache *sc = nullptr);
 
 // Flatten node streams and build every index the kernels walk.  `epochs`
 // non-empty selects member semantics (role / version gates, E_EPOCH events).

@@ -1957,39 +1957,60 @@ __global__ __launch_bounds__(256) void k_commit_check(DevView v)
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t n_chk = *v.gp_chk_n, nwaves = (uint64_t)gridDim.x * 4;
-    for (uint64_t x = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < n_chk; x += nwaves) {
-        const uint64_t f0 = v.gp_chk[CHK_WORDS * x], f1 = v.gp_chk[CHK_WORDS * x + 1], i = v.gp_chk[CHK_WORDS * x + 2];
+    // Software pipeline over the wave's pairs (the chain item words -> run descriptors -> member
+    // scan flags -> Values is one dependent round trip per link): the next pair's descriptors and
+    // the pair after's item words are in flight while a pair is checked, its flags one pair
+    // ahead, so a pair waits only for its Values — the first commit's and the checked runs', four
+    // runs per round trip, the first group issued with the first commits'.
+    // (r05: 289 -> see profiles/r05_* for contended C5, 80 k pairs; the serial chain took 5 round trips)
+    auto words = [&](uint64_t x) -> uint64_t { return x < n_chk && lane < CHK_WORDS ? v.gp_chk[CHK_WORDS * x + lane] : 0; };
+    struct Desc { uint64_t fw0, fw1; };
+    auto descr = [&](uint64_t w) -> Desc {
+        Desc d{0, 0};
+        const uint64_t f0 = rl64(w, 0), f1 = rl64(w, 1);
+        if (lane < f1 - f0 && lane < 64) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + f0 + lane);
+            d.fw0 = x.x; d.fw1 = x.y;
+        }
+        return d;
+    };
+    auto flags = [&](const Desc &d) -> uint32_t { return MEMBER && d.fw1 ? v.m_flags[(uint32_t)d.fw1] : 0; };
+    uint64_t x = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    uint64_t w0 = words(x), w1 = words(x + nwaves), w2 = words(x + 2 * nwaves);
+    Desc d0 = descr(w0), d1 = descr(w1);
+    uint32_t m0 = flags(d0);
+    for (; x < n_chk; x += nwaves) {
+        const uint64_t w = w0;
+        const Desc d = d0;
+        const uint32_t mf = m0;
+        m0 = flags(d1);                                           // pair x + 1
+        d0 = d1; d1 = descr(w2);                                  // pair x + 2
+        w0 = w1; w1 = w2; w2 = words(x + 3 * nwaves);             // pair x + 3
+        const uint64_t f0 = rl64(w, 0), f1 = rl64(w, 1), i = rl64(w, 2);
+        const uint64_t fw0 = d.fw0, fw1 = d.fw1;
         const uint32_t b = (uint32_t)(i / v.N), n = (uint32_t)(i - (uint64_t)b * v.N);
         const uint64_t li0 = (uint64_t)b << BSH;
         // plan-list pairs have at most PLAN_XFRAGS (32) runs: one descriptor window
         const uint32_t nf = (uint32_t)(f1 - f0 < 64 ? f1 - f0 : 64);
-        uint64_t fw0 = 0, fw1 = 0;
-        uint32_t mf = 0;
-        if (lane < nf) {
-            const ulonglong2 d = *reinterpret_cast<const ulonglong2 *>(v.frags + f0 + lane);
-            fw0 = d.x; fw1 = d.y;
-            if (MEMBER) mf = v.m_flags[(uint32_t)fw1];
-        }
         // pass 1 (no loads): each slot's first commit / learn — its entry and run
         uint32_t se[SPL], sa[SPL];
 #pragma unroll
         for (uint32_t j = 0; j < SPL; ++j) { se[j] = 0; sa[j] = 64; }
         for (uint32_t a = 0; a < nf; ++a) {
-            const uint64_t w1 = rl64(fw1, a);
-            if ((uint32_t)(w1 >> 60) != K_COMMIT) continue;
-            const uint32_t ent = (uint32_t)rl64(fw0, a);
-            const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+            const uint64_t wv1 = rl64(fw1, a);
+            if ((uint32_t)(wv1 >> 60) != K_COMMIT) continue;
+            const uint32_t ent = (uint32_t)rl64(fw0, a);      // (entries < MAX_ENTRIES < 2^32: ingest refuses more)
+            const uint32_t cnt = (uint32_t)(wv1 >> 32) & 0xFFFF, st0 = (uint32_t)(wv1 >> 48) & 0xFF;
 #pragma unroll
             for (uint32_t j = 0; j < SPL; ++j) {
-                const int d = (int)(lane + 64 * j) - (int)st0;
-                if (d >= 0 && d < (int)cnt && sa[j] == 64) { se[j] = ent + d; sa[j] = a; }
+                const int dd = (int)(lane + 64 * j) - (int)st0;
+                if (dd >= 0 && dd < (int)cnt && sa[j] == 64) { se[j] = ent + dd; sa[j] = a; }
             }
         }
-        uint64_t sv[SPL];
-#pragma unroll
-        for (uint32_t j = 0; j < SPL; ++j) sv[j] = sa[j] < 64 ? v.e_val[se[j]] : 0;
         // pass 2: the later checked runs over committed slots through another entry, four runs'
-        // Values in flight at a time
+        // Values in flight at a time (the first group together with the first commits' Values)
+        uint64_t sv[SPL];
+        bool sv_loaded = false;
         for (uint32_t a0 = 0; a0 < nf; a0 += 4) {
             uint64_t xv[4][SPL];
             uint32_t xm[4];
@@ -1998,19 +2019,25 @@ __global__ __launch_bounds__(256) void k_commit_check(DevView v)
                 xm[r] = 0;
                 const uint32_t a = a0 + r;
                 if (a >= nf) continue;
-                const uint64_t w1 = rl64(fw1, a);
-                const bool learn = (uint32_t)(w1 >> 60) == K_COMMIT;
+                const uint64_t wv1 = rl64(fw1, a);
+                const bool learn = (uint32_t)(wv1 >> 60) == K_COMMIT;
                 const uint32_t f = MEMBER ? rl32(mf, a) : 0;
                 if (!(MEMBER ? (learn ? (f & F_PROP) != 0 : (f & F_GRANTED) != 0) : learn)) continue;
                 const uint32_t ent = (uint32_t)rl64(fw0, a);
-                const uint32_t cnt = (uint32_t)(w1 >> 32) & 0xFFFF, st0 = (uint32_t)(w1 >> 48) & 0xFF;
+                const uint32_t cnt = (uint32_t)(wv1 >> 32) & 0xFFFF, st0 = (uint32_t)(wv1 >> 48) & 0xFF;
 #pragma unroll
                 for (uint32_t j = 0; j < SPL; ++j) {
-                    const int d = (int)(lane + 64 * j) - (int)st0;
-                    const bool c = d >= 0 && d < (int)cnt && sa[j] < a && ent + d != se[j];
-                    xv[r][j] = c ? v.e_val[ent + d] : 0;
+                    const int dd = (int)(lane + 64 * j) - (int)st0;
+                    const bool c = dd >= 0 && dd < (int)cnt && sa[j] < a && ent + dd != se[j];
+                    xv[r][j] = c ? v.e_val[ent + dd] : 0;
                     xm[r] |= (uint32_t)c << j;
                 }
+            }
+            if (!__ballot(xm[0] | xm[1] | xm[2] | xm[3])) continue;    // nothing to compare in this group
+            if (!sv_loaded) {
+#pragma unroll
+                for (uint32_t j = 0; j < SPL; ++j) sv[j] = sa[j] < 64 ? v.e_val[se[j]] : 0;
+                sv_loaded = true;
             }
 #pragma unroll
             for (uint32_t r = 0; r < 4; ++r)
@@ -3484,8 +3511,31 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
             else hipLaunchKernelGGL((k_headers<false, SCAN_CHUNK>), grid, dim3(256), 0, s, v, nb_scan, nb_prop);
         }
     }
+    // plan path (the timed step): k_plan (multi: the lean pairs) / k_plan_list (the work
+    // list's pairs without promise rounds) + store, then k_apply over the pairs k_plan_list
+    // listed and the promise-round pairs.  A digested run (verification) and v.walk_all
+    // (MPX_STEP_WALK=1) walk every pair instead, as do multi traces with more than
+    // FAST_MAX_NODES nodes.
+    const bool plan_path = !v.digest && !v.walk_all && !v.window && (member || v.N <= FAST_MAX_NODES);
+    const bool lplan = plan_path && (member || v.num_gp_snap);
+    // Three streams on the list plan path (the kernels are latency-bound walks, so running them
+    // side by side hides their round trips behind each other's):
+    //   s  : k_plan -> k_plan_list -> k_store_ext -> k_commit_check -> store          (planned pairs)
+    //   s2 : [k_prop_node ->] k_apply AM_FULL  from the end of the header kernels     (promise rounds)
+    //   s3 : k_chosen from the end of the plan of its buckets, k_apply AM_SNAP from the end of
+    //        k_plan_list (the pairs it listed)
+    // Each writes its own pairs / rows (a listed pair has no plan word; k_chosen walks only the
+    // buckets plan_chosen left, whose row-N plan word is PLAN_SKIP) and adds counters with
+    // atomics; all joined before the summary.  k_prop_node feeds only the promise-round walk
+    // (k_plan / k_plan_list pairs have no promise-reply runs).
+    const bool rounds = lplan && v.num_gp > v.num_gp_snap;
+    const bool side_rounds = rounds && side.stream2;
+    const bool side3 = lplan && side.stream3;
+    hipStream_t s2 = side_rounds ? (hipStream_t)side.stream2 : s;
+    hipStream_t s3 = side3 ? (hipStream_t)side.stream3 : s;
+    const bool prop = (v.num_pc && v.pc_multi) || v.window;
     // (a window: every node's round after the window, prop_out, comes from k_prop_node)
-    if ((v.num_pc && v.pc_multi) || v.window) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s, v);
+    if (prop && !side_rounds) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s, v);
     if (v.window) {
         // incremental window: every pair of the window on the value-state walk, the chosen log
         // of the batches chosen in it, the summary
@@ -3498,22 +3548,10 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
         hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
         return (int)hipGetLastError();
     }
-    // plan path (the timed step): k_plan (multi: the lean pairs) / k_plan_list (the work
-    // list's pairs without promise rounds) + store, then k_apply over the pairs k_plan_list
-    // listed and the promise-round pairs.  A digested run (verification) and v.walk_all
-    // (MPX_STEP_WALK=1) walk every pair instead, as do multi traces with more than
-    // FAST_MAX_NODES nodes.
-    const bool plan_path = !v.digest && !v.walk_all && (member || v.N <= FAST_MAX_NODES);
-    const bool lplan = plan_path && (member || v.num_gp_snap);
-    // the promise-round pairs (the host list's tail) depend only on the header kernels: on the
-    // side stream they run beside the plan / store / listed-pair kernels (disjoint pairs, rows
-    // and sub-buffer cursors), joined before the chosen log and the summary
-    const bool rounds = lplan && v.num_gp > v.num_gp_snap;
-    const bool side_rounds = rounds && side.stream2;
-    hipStream_t s2 = side_rounds ? (hipStream_t)side.stream2 : s;
     if (side_rounds) {
         (void)hipEventRecord((hipEvent_t)side.fork, s);
         (void)hipStreamWaitEvent(s2, (hipEvent_t)side.fork, 0);
+        if (prop) hipLaunchKernelGGL(k_prop_node, dim3(v.N), dim3(64), 0, s2, v);
     }
     auto launch_rounds = [&]() {
         if (member) hipLaunchKernelGGL((k_apply<APPLY_WAVES_FULL, false, true>), dim3(g.apply_wgs), dim3(256), 0, s2, v, v.num_gp_snap, v.num_gp);
@@ -3528,6 +3566,16 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
     const bool skip_chosen = plan_path && v.chosen_static;
     const bool fuse_reduce = run_ends_with_store(v);
     const uint32_t reduce_wgs = cdiv(n_partials ? n_partials : 1, 256);
+    auto launch_chosen = [&](hipStream_t cs, hipEvent_t start) {
+        hipExtLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, cs, start, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+    };
+    // the pairs k_plan_list listed (their count is on the device)
+    auto launch_listed = [&](hipStream_t ls) {
+        DevView vd = v;
+        vd.gp_list = v.gp_dyn;
+        if (member) hipLaunchKernelGGL((k_apply<APPLY_WAVES_SNAP, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, ls, vd, 0ull, ~0ull);
+        else hipLaunchKernelGGL((k_apply<APPLY_WAVES_SNAP, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, ls, vd, 0ull, ~0ull);
+    };
     // the plan words of every (row, bucket) -> state rows and the chosen log
     // (1-byte slots: 128-bucket chunks, 32 KiB per row and two plan words per lane, 0.295 vs
     // 0.315 ms for 64-bucket chunks at C4)
@@ -3542,28 +3590,52 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
             hipExtLaunchKernelGGL((k_store<32, true, uint16_t, u16x4>), dim3(g.store_wgs), dim3(256), 0, s, nullptr, stop, 0, v);
     };
     const uint32_t plan_blocks = cdiv((uint64_t)v.N * v.NB, 256);
+    bool chosen_done = false;                            // k_chosen launched on s3 already
     if (plan_path) {
         if (member) {
             // (8 segments / 32 runs since the Value check left the walk — 128 VGPRs, no spill:
             // C5 0.451 -> 0.384 ms, contended C5 2.745 -> 2.582 ms, profiles/r04_v25_ab_member_plan8.json)
             hipExtLaunchKernelGGL((k_plan_list<true, PLAN_XSEG, PLAN_XFRAGS>), dim3(plan_blocks), dim3(256), 0, s,
-                                  (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+                                  (hipEvent_t)ev_apply0, side3 ? (hipEvent_t)side.fork3b : (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+            if (side3) {                                 // member k_plan_list planned the chosen log too
+                (void)hipStreamWaitEvent(s3, (hipEvent_t)side.fork3b, 0);
+                launch_listed(s3);
+                if (!skip_chosen) { launch_chosen(s3, nullptr); chosen_done = true; }
+                (void)hipEventRecord((hipEvent_t)side.join3, s3);
+            }
             hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);
-            hipLaunchKernelGGL(k_commit_check<true>, dim3(g.chosen_wgs), dim3(256), 0, s, v);
+            hipLaunchKernelGGL(k_commit_check<true>, dim3(g.apply_wgs), dim3(256), 0, s, v);
         } else {
             // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
             // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
             // 0.391 vs 0.304 ms apply phase at C4; the compiler drains vmcnt at its loop head)
-            hipExtLaunchKernelGGL(k_plan, dim3(plan_blocks), dim3(256), 0, s,
-                                  (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+            hipExtLaunchKernelGGL(k_plan, dim3(plan_blocks), dim3(256), 0, s, (hipEvent_t)ev_apply0,
+                                  side3 ? (hipEvent_t)side.fork3a : (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+            if (side3 && !skip_chosen) {                 // k_plan decided which buckets' chosen log it plans
+                (void)hipStreamWaitEvent(s3, (hipEvent_t)side.fork3a, 0);
+                launch_chosen(s3, nullptr);
+                chosen_done = true;
+            }
             if (lplan) {
 #ifdef MPX_PLAN_LSEG4
-                hipLaunchKernelGGL((k_plan_list<false>), dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);   // (A/B build)
+                hipExtLaunchKernelGGL((k_plan_list<false>), dim3(plan_blocks), dim3(256), 0, s, (hipEvent_t)nullptr,
+                                      side3 ? (hipEvent_t)side.fork3b : (hipEvent_t)nullptr, 0, v, g.apply_wgs);   // (A/B build)
 #else
-                hipLaunchKernelGGL((k_plan_list<false, PLAN_XSEG, PLAN_XFRAGS>), dim3(plan_blocks), dim3(256), 0, s, v, g.apply_wgs);
+                hipExtLaunchKernelGGL((k_plan_list<false, PLAN_XSEG, PLAN_XFRAGS>), dim3(plan_blocks), dim3(256), 0, s,
+                                      (hipEvent_t)nullptr, side3 ? (hipEvent_t)side.fork3b : (hipEvent_t)nullptr, 0, v,
+                                      g.apply_wgs);
+#endif
+                if (side3) {
+                    (void)hipStreamWaitEvent(s3, (hipEvent_t)side.fork3b, 0);
+                    launch_listed(s3);
+                    (void)hipEventRecord((hipEvent_t)side.join3, s3);
+                }
+#ifndef MPX_PLAN_LSEG4
                 hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);
 #endif
-                hipLaunchKernelGGL(k_commit_check<false>, dim3(g.chosen_wgs), dim3(256), 0, s, v);
+                hipLaunchKernelGGL(k_commit_check<false>, dim3(g.apply_wgs), dim3(256), 0, s, v);
+            } else if (side3) {
+                (void)hipEventRecord((hipEvent_t)side.join3, s3);
             }
         }
         // every pair the trace marks lean (pair_gp 0) is one k_plan can describe (ingest.cpp /
@@ -3580,13 +3652,10 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
     }
     if (lplan) {
-        // the pairs k_plan_list listed (their count is on the device), then the promise rounds
-        DevView vd = v;
-        vd.gp_list = v.gp_dyn;
-        if (member) hipLaunchKernelGGL((k_apply<APPLY_WAVES_SNAP, false, true, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
-        else hipLaunchKernelGGL((k_apply<APPLY_WAVES_SNAP, false, false, AM_SNAP>), dim3(g.apply_wgs), dim3(256), 0, s, vd, 0ull, ~0ull);
+        if (!side3) launch_listed(s);
         if (rounds && !side_rounds) launch_rounds();
         if (side_rounds) (void)hipStreamWaitEvent(s, (hipEvent_t)side.join, 0);
+        if (side3) (void)hipStreamWaitEvent(s, (hipEvent_t)side.join3, 0);
     } else {
         // every pair of the host-built work list on the general kernel, in three ranges
         // (ingest.cpp orders the list): event-free pairs (AM_SIMPLE), pairs without
@@ -3594,6 +3663,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
         // Occupancy (C3 2^24 general apply): AM_SNAP at 4 waves / SIMD 1.324 ms vs 1.469
         // unconstrained (3 waves) and 1.496 at 5 (spills); the full kernel at 4 waves 1.394 vs
         // 1.580 ms unconstrained; one kernel over the whole list 1.351 ms (C5: 2.165 vs 2.544 ms)
+        if (side3) (void)hipStreamWaitEvent(s, (hipEvent_t)side.join3, 0);   // (a multi plan path without list pairs)
         const uint64_t ns = v.num_gp_simple, nq = v.num_gp_snap;
         if (v.digest) {
             if (ns) { if (member) hipLaunchKernelGGL((k_apply<1, true, true, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);
@@ -3616,12 +3686,11 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
     if (fuse_reduce) {
         // (the apply phase ends with the store; the general and tail phases are empty: the
         // host reads the store's stop event for them, run_ends_with_store)
-    } else if (skip_chosen) {
+    } else if (skip_chosen || chosen_done) {
         hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)ev_general,
                               (hipEvent_t)ev_end, 0, v, n_partials);
     } else {
-        hipExtLaunchKernelGGL(k_chosen, dim3(g.chosen_wgs), dim3(256), 0, s, (hipEvent_t)ev_general,
-                              (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+        launch_chosen(s, (hipEvent_t)ev_general);
         hipExtLaunchKernelGGL(k_reduce, dim3(cdiv(n_partials ? n_partials : 1, 256)), dim3(256), 0, s, (hipEvent_t)nullptr, (hipEvent_t)ev_end, 0, v, n_partials);
     }
     return (int)hipGetLastError();

@@ -446,7 +446,10 @@ struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, store_wgs; };
 // general k_apply, end
 // a second stream and two events (fork / join, timing off) for kernels of a run that may
 // overlap others of it; nullptr: everything on `stream`
-struct LaunchSide { void *stream2, *fork, *join; };
+// side streams of a run (nullptr: one stream): stream2 takes the promise-round pairs (after the
+// header kernels), stream3 the chosen log (after the plan of its buckets) and the pairs k_plan_list
+// lists (after it); both joined before the summary
+struct LaunchSide { void *stream2, *fork, *join, *stream3, *fork3a, *fork3b, *join3; };
 int launch_run(const DevView &v, void *stream, LaunchGeom g, void *const ev[5], LaunchSide side);
 // the run's last kernel is the store, the step summary folded into it (the clean multi
 // plan path, C4): launch_run then records neither the general-apply nor the end event

@@ -119,6 +119,18 @@ def run(cfg, shards, procs, tmpdir):
                       "instance shards" % ("_member" if member else "", shards)}
 
 
+def _heartbeat(every=50):
+    """A progress line every `every` s (a run on the GPU box is killed after 180 s of silence)."""
+    import threading
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(every)
+            print("[ref_full_size] %.0f s" % (time.time() - t0), flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="+", choices=sorted(CONFIGS))
@@ -126,7 +138,10 @@ def main():
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--tmpdir", default="/tmp")
     ap.add_argument("--out", default=OUT)
+    ap.add_argument("--heartbeat", action="store_true", help="print a progress line every 50 s")
     a = ap.parse_args()
+    if a.heartbeat:
+        _heartbeat()
     res = json.load(open(a.out)) if os.path.exists(a.out) else {}
     for cfg in a.configs:
         res[cfg] = run(cfg, a.shards, a.procs, a.tmpdir)
