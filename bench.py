@@ -240,13 +240,14 @@ def c3_windows_leg(args, trace, want_digests, want_counters):
     n, m = hd["num_nodes"], hd["num_instances"]
     eng = mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL)
     eng.timing_every(1)
-    host_ms, dev, gp = [], [], []
+    host_ms, sub_ms, dev, gp = [], [], [], []
     tot = {k: 0 for k in want_counters}
     prev = [0] * n
     for w in range(1, W + 1):
         cut = [c * w // W for (c, _, _) in idx]
         t0 = time.perf_counter()
         eng.submit_window(trace, prev, cut)
+        sub_ms.append((time.perf_counter() - t0) * 1e3)
         st = eng.run()
         host_ms.append((time.perf_counter() - t0) * 1e3)
         ph = eng.timings_detail()
@@ -270,14 +271,15 @@ def c3_windows_leg(args, trace, want_digests, want_counters):
     # engine model of a window's apply: each pair it touches reads and writes 256 slots of
     # 16-B value state (s_bal, s_val) and its runs' 16-B descriptors
     b_eng = sum(32 * 256 * x for x in gp) / W
-    log("c3 windows: %d windows, host %.1f ms / window (device %.2f), k_apply_win %.3f ms" %
-        (W, mean(host_ms), mean(run_ms), mean(apply_ms)))
+    log("c3 windows: %d windows, host %.1f ms / window (submit %.1f; device %.2f), k_apply_win %.3f ms" %
+        (W, mean(host_ms), mean(sub_ms), mean(run_ms), mean(apply_ms)))
     return {"windows": W, "chosen": tot["chosen"],
             "value": tot["chosen"] / (sum(host_ms) * 1e-3), "unit": "decisions/s",
             "value_device": tot["chosen"] / (sum(run_ms) * 1e-3),
             "note": "value: chosen instances / the windows' host + device wall time (decode, upload, run, "
                     "readback); value_device: / the device run time alone",
-            "host_ms_per_window": mean(host_ms), "device_ms_per_window": mean(run_ms),
+            "host_ms_per_window": mean(host_ms), "submit_ms_per_window": mean(sub_ms),
+            "device_ms_per_window": mean(run_ms),
             "host_ms": host_ms, "device_ms": run_ms, "apply_ms": apply_ms, "pairs_per_window": gp,
             "roofline": {"bound": "hbm", "kernel": "k_apply_win", "kernel_ms": mean(apply_ms),
                          "frac_hw": hw["frac"] if hw else None, "achieved_hw": hw["achieved"] if hw else None,

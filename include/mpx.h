@@ -166,7 +166,13 @@ typedef struct mpx_config {
  * Errors: a window refused while it is built (MPX_E_RANGE, MPX_E_DECODE, ...) leaves the
  * engine as it was — its records stay queued and are refused again; a failure after the
  * window was taken (a HIP error) may leave it partly applied, so the engine is poisoned:
- * every later mpx_run, submit and readback returns MPX_E_STATE. */
+ * every later mpx_run, submit and readback returns MPX_E_STATE.
+ * Limits that count over the whole live stream, not per window: member semantics allow at
+ * most 254 E_EPOCH records per node over the stream (the device's Acceptor incarnation
+ * counter, G_SEG); the window that would place a node's 255th is refused with MPX_E_RANGE
+ * and, as above, stays queued, so that stream cannot advance (start a new engine).  With
+ * MPX_FLAG_DECISIONS a node's record index (sends' and events' seq) is 32-bit over the
+ * stream (< 2^32 - 1 records per node, else MPX_E_RANGE). */
 #define MPX_FLAG_INCREMENTAL 1u
 /* With MPX_FLAG_INCREMENTAL: every mpx_run also advances the proposers' phase-2
  * bookkeeping over the window's events (the quorums' merged maps, COMMIT / LEARN entries,

@@ -77,6 +77,7 @@ static int prop_window(mpx_engine *e);
 
 struct mpx_engine {
     mpx_config cfg{};
+    uint64_t ab_build_ns = 0;                  // (MPX_HOST_TIMES, A/B builds: build_trace's share of upload_trace)
     std::vector<mpx_epoch> epochs;
     int device = 0;
     hipStream_t stream = nullptr;
@@ -563,6 +564,7 @@ static int upload_trace(mpx_engine *e)
     if (member && e->epochs.empty()) return MPX_E_STATE;        // no epoch table yet
     TRY(build_trace(e->nodes, e->cfg.shard_begin, e->shard_len, member ? e->epochs : std::vector<mpx_epoch>(), e->ht,
                     e->incremental ? &e->wc : nullptr));
+    e->ab_build_ns = now_ns() - t0;
     if (e->incremental) {
         // the window is consumed: the next run builds on the carry from only what comes after it
         ++e->consumed;
@@ -921,15 +923,24 @@ static int run_window(mpx_engine *e)
 {
     // one window: the records submitted since the last run, on the carried state
     e->dirty = true;
+    const uint64_t t0 = now_ns(), u0 = e->stats.ingest_ns;
     TRY(queue_run(e, false));
+    const uint64_t t1 = now_ns();
     TRY(collect(e));
+    const uint64_t t2 = now_ns();
     if (e->prop || e->mprop) TRY(prop_window(e));
+    const uint64_t t3 = now_ns();
     // batches chosen in this window need their entries no more
     std::vector<uint32_t> bc;
     TRY(d2h(bc, e->b_chosen, e->ht.b_gid.size()));
     for (size_t j = 0; j < bc.size(); ++j)
         if (bc[j] != NONE32) e->wc.b_ents.erase(e->ht.b_gid[j]);
     ++e->windows;
+    if (ab_env("MPX_HOST_TIMES"))
+        std::fprintf(stderr, "[mpx] window %llu: build_trace %.1f ms, upload %.1f ms, launch %.1f ms, collect %.1f ms, "
+                     "proposer %.1f ms, release %.1f ms\n", (unsigned long long)e->windows, e->ab_build_ns * 1e-6,
+                     (e->stats.ingest_ns - u0 - e->ab_build_ns) * 1e-6, (t1 - t0 - (e->stats.ingest_ns - u0)) * 1e-6,
+                     (t2 - t1) * 1e-6, (t3 - t2) * 1e-6, (now_ns() - t3) * 1e-6);
     return MPX_OK;
 }
 

@@ -83,6 +83,9 @@ ValueTable::Rec *ValueTable::Shard::insert(uint64_t h, bool &fresh)
             k2[j] = key[i]; r2[j] = rec[i];
         }
         key.swap(k2); rec.swap(r2);
+        kp.store(key.data(), std::memory_order_relaxed);
+        rp.store(rec.data(), std::memory_order_relaxed);
+        kmask.store(key.size() - 1, std::memory_order_relaxed);
     }
     const size_t mask = key.size() - 1;
     size_t i = slot_of(h, mask);
@@ -90,6 +93,16 @@ ValueTable::Rec *ValueTable::Shard::insert(uint64_t h, bool &fresh)
     fresh = key[i] == EMPTY;
     if (fresh) { key[i] = h; ++count; }
     return &rec[i];
+}
+
+void ValueTable::prefetch_slot(uint64_t h) const
+{
+    const Shard &x = sh[shard_of(h)];
+    const uint64_t *k = x.kp.load(std::memory_order_relaxed);
+    if (!k) return;
+    const size_t i = slot_of(h, x.kmask.load(std::memory_order_relaxed));
+    __builtin_prefetch(k + i);
+    __builtin_prefetch(x.rp.load(std::memory_order_relaxed) + i);
 }
 
 int ValueTable::intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_off, uint32_t exec_len)
@@ -293,20 +306,6 @@ int ValueTable::plain(uint64_t h)
     return intern(h, enc.data(), (uint32_t)enc.size(), eo, 0);
 }
 
-bool ValueTable::changes(uint64_t h, std::vector<std::pair<uint32_t, uint32_t>> &out)
-{
-    out.clear();
-    Shard &x = sh[shard_of(h)];
-    std::lock_guard<std::mutex> g(x.mu);                  // (other decode threads may append to the shard)
-    const Rec *r = x.find(h);
-    if (!r || r->exec_off != NONE32) return false;
-    // canonical Value_m bytes (parse_member): ... u8 membership @13, u32 n @14, n x {u32 node, u32 type} @18
-    const uint8_t *p = (const uint8_t *)r->p;
-    const uint32_t n = rd32(p + 14);
-    for (uint32_t k = 0; k < n; ++k) out.emplace_back(rd32(p + 18 + 8 * k), rd32(p + 22 + 8 * k));
-    return true;
-}
-
 // NodeImpl::ChangeMemberships (member/paxos.cpp:1864-1964) on a node's view: the six change
 // types, version_ bumped by each acceptor change; a change the reference ASSERTs on (adding a
 // member twice, removing an absent one, the last acceptor) is refused (MPX_E_STATE)
@@ -376,13 +375,25 @@ static bool sort_entries(std::vector<uint64_t> &iid, std::vector<uint64_t> &pid,
 static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool with_pid,
                           std::vector<uint64_t> &iid, std::vector<uint64_t> &pid,
                           std::vector<uint64_t> &val, size_t &n_all, bool &dup,
-                          std::vector<uint64_t> *memh = nullptr, SectionCache *sc = nullptr)
+                          std::vector<std::pair<uint64_t, const uint8_t *>> *memh = nullptr, SectionCache *sc = nullptr)
 {
     // the first thread to meet these bytes interns their Values, the others skim them
     const bool own = !sc || !len || sc->claim(b, len, with_pid);
     size_t cur = 0;
     const size_t first = iid.size();
     n_all = 0;
+    if (own && len >= 512) {                          // touch the Values' table slots first (see prefetch_slot)
+        for (size_t c = 0; c < len;) {
+            const size_t need = with_pid ? 16 : 8;
+            if (len - c < need) break;
+            c += need;
+            uint64_t h;
+            const long u = skim(b + c, len - c, vt.member, &h, nullptr);
+            if (u < 0) break;                             // (the decode below reports it)
+            vt.prefetch_slot(h);
+            c += (size_t)u;
+        }
+    }
     while (cur < len) {
         const size_t need = with_pid ? 16 : 8;
         if (len - cur < need) return MPX_E_DECODE;
@@ -393,7 +404,7 @@ static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool wit
         bool mem = false;
         const long u = own ? vt.parse(b + cur, len - cur, &h, &mem) : skim(b + cur, len - cur, vt.member, &h, &mem);
         if (u < 0) return (int)u;
-        if (mem && memh) memh->push_back(h);          // (member membership Values: MPX_FLAG_LEARN_EPOCHS)
+        if (mem && memh) memh->push_back({h, b + cur});   // (member membership Values: MPX_FLAG_LEARN_EPOCHS)
         cur += (size_t)u;
         iid.push_back(i);
         if (with_pid) pid.push_back(pd);
@@ -663,25 +674,34 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         ns.e_iid.resize(w); ns.e_val.resize(w); ns.e_pid.resize(w);
         return (uint32_t)(w - first);
     };
-    std::vector<uint64_t> applied;                // (el) membership Values this LEARN makes the node apply
-    std::vector<uint64_t> memh;                   // (el) the membership Values among this record's entries
+    std::vector<EpochLearn::Changes> applied;     // (el) the membership Values this LEARN makes the node apply
+    // (el) the membership Values among this record's entries and their wire bytes: the change list
+    // is read off the wire (the same layout as the canonical bytes, parse_member), not the shared
+    // table, which another decode thread may still be filling for this section (SectionCache)
+    std::vector<std::pair<uint64_t, const uint8_t *>> memh;
+    auto changes_of = [&](uint64_t h, EpochLearn::Changes &ch) {
+        for (const auto &x : memh)
+            if (x.first == h) {
+                const uint32_t n = rd32(x.second + 14);            // (bounds checked by the decode)
+                for (uint32_t k = 0; k < n; ++k) ch.emplace_back(rd32(x.second + 18 + 8 * k), rd32(x.second + 22 + 8 * k));
+                return true;
+            }
+        return false;
+    };
     // the Learner's apply loop over one LEARN's entries, every instance (not only the shard's)
     auto learn = [&](size_t first, size_t end) {
         for (size_t k = first; k < end; ++k) {
             const uint64_t i = ns.e_iid[k];
             if (i < el->front) continue;                          // applied already (insert: no change)
-            const uint64_t h0 = ns.e_val[k];
-            const bool m0 = !memh.empty() && std::find(memh.begin(), memh.end(), h0) != memh.end();
-            if (i > el->front) { el->above.emplace(i, std::make_pair(h0, m0)); continue; }
-            uint64_t h = h0;
-            bool mem = m0;
+            EpochLearn::Learned cur{false, {}};
+            if (!memh.empty()) cur.mem = changes_of(ns.e_val[k], cur.ch);
+            if (i > el->front) { el->above.emplace(i, std::move(cur)); continue; }
             for (;;) {                                            // apply at the frontier, then what waited above it
-                if (mem) applied.push_back(h);
+                if (cur.mem) applied.push_back(std::move(cur.ch));
                 ++el->front;
                 auto it = el->above.begin();
                 if (it == el->above.end() || it->first != el->front) break;
-                h = it->second.first;
-                mem = it->second.second;
+                cur = std::move(it->second);
                 el->above.erase(it);
             }
         }
@@ -803,9 +823,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
     ns.ver.push_back(ver);
     // the membership Values this LEARN applied, in instance order: one E_EPOCH each, right after
     // it (the reference changes the roles inside OnLearn, before the node's next record)
-    std::vector<std::pair<uint32_t, uint32_t>> ch;
-    for (const uint64_t h : applied) {
-        if (!vt.changes(h, ch)) return MPX_E_STATE;
+    for (const auto &ch : applied) {
         TRY_RC(change_memberships(el->view, ch));
         el->steps.push_back(el->view);
         ns.part.push_back(0);

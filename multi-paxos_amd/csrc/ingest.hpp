@@ -36,6 +36,10 @@ struct ValueTable {
         size_t count = 0;
         std::vector<std::unique_ptr<char[]>> blocks;     // canonical bytes: stable addresses, no regrowth copies
         size_t used = BLOCK;                             // bytes used in the last block
+        // the arrays' current addresses, published under mu for prefetch_slot (read without it)
+        std::atomic<const uint64_t *> kp{nullptr};
+        std::atomic<const Rec *> rp{nullptr};
+        std::atomic<size_t> kmask{0};
         const Rec *find(uint64_t h) const;
         Rec *insert(uint64_t h, bool &fresh);
     };
@@ -58,17 +62,20 @@ struct ValueTable {
         for (uint32_t k = 0; k < SHARDS; ++k) {
             Shard &x = sh[k];
             x.key.clear(); x.rec.clear(); x.count = 0; x.blocks.clear(); x.used = BLOCK;
+            x.kp = nullptr; x.rp = nullptr; x.kmask = 0;
         }
         synthetic_clean = false;
     }
     // a handle with no bytes yet: the payload-free Value it names (mpx_submit_soa)
     int plain(uint64_t handle);
-    // {node, MembershipChangeType} of a membership Value, in its order (member/paxos.cpp:365-390)
-    bool changes(uint64_t h, std::vector<std::pair<uint32_t, uint32_t>> &out);
     // the canonical bytes of handle h, interned (thread-safe): MPX_E_VALUE when h already names
     // other bytes (a Value is named by (proposer, value_id), multi/paxos.cpp:439)
     int intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_off, uint32_t exec_len);
     const Rec *find(uint64_t h) const { return sh[shard_of(h)].find(h); }
+    // prefetch h's home slot (key and record): a section's Values are looked up one after another,
+    // each a likely cache miss, so the decode touches them all first (no lock: a stale address
+    // after a concurrent growth only wastes the prefetch)
+    void prefetch_slot(uint64_t h) const;
 };
 
 // One submit call's value sections (the entry lists of ACCEPT / COMMIT / P_BATCH / PREPARE_REPLY
@@ -97,8 +104,10 @@ struct SectionCache {
 // applies the same Values in the same order (one chosen Value per instance), so the per-node
 // lists agree on their common prefix (checked when they are merged, mpx_engine::epochs).
 struct EpochLearn {
+    using Changes = std::vector<std::pair<uint32_t, uint32_t>>;   // {node, MembershipChangeType}*
+    struct Learned { bool mem; Changes ch; };
     uint64_t front = 0;
-    std::map<uint64_t, std::pair<uint64_t, bool>> above;   // learned, not yet applied: iid -> (handle, membership)
+    std::map<uint64_t, Learned> above;            // learned, not yet applied: iid -> (membership?, its changes)
     mpx_epoch view{};                             // NodeImpl's version_ / acceptors_ / proposers_ / learners_
     std::vector<mpx_epoch> steps;                 // epochs 1.. this node reached
 };

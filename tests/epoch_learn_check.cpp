@@ -7,7 +7,8 @@
 // and with an EpochLearn from the genesis epoch, fed in `windows` slices (the learner state carries
 // over, as across MPX_FLAG_INCREMENTAL windows).  The learned run must place the same E_EPOCH
 // records at the same stream positions with the same epochs, and the epochs it learned must be the
-// container's table.  Prints "ok <records> <markers> <epochs>" or the first difference.
+// container's table.  The learned pass skims every value section (another thread's claim, SectionCache).
+// Prints "ok <records> <markers> <epochs>" or the first difference.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -75,10 +76,21 @@ int main(int argc, char **argv)
             if (int rc = decode_record_member(v1, as_is, n, bytes + offs[i], offs[i + 1] - offs[i], 0, M, iv)) {
                 std::printf("FAIL decode rc %d\n", rc); return 1;
             }
+        // the learned pass skims every value section (as a decode thread does when another thread
+        // claimed the section and may not have interned it yet): its table stays empty, so the
+        // learner must read membership changes off the wire
+        SectionCache sc;
+        {
+            NodeStream sink;
+            ValueTable v3;
+            v3.member = true;
+            for (uint64_t i = 0; i < cnt; ++i)
+                decode_record_member(v3, sink, n, bytes + offs[i], offs[i + 1] - offs[i], 0, M, iv, nullptr, &sc);
+        }
         for (uint32_t w = 0; w < W; ++w) {                   // windows: the learner state carries over
             NodeStream part;
             for (uint64_t i = cnt * w / W; i < cnt * (w + 1) / W; ++i)
-                if (int rc = decode_record_member(v2, part, n, bytes + offs[i], offs[i + 1] - offs[i], 0, M, iv, &el)) {
+                if (int rc = decode_record_member(v2, part, n, bytes + offs[i], offs[i + 1] - offs[i], 0, M, iv, &el, &sc)) {
                     std::printf("FAIL learned decode rc %d node %u record %llu\n", rc, n, (unsigned long long)i);
                     return 1;
                 }

@@ -966,6 +966,26 @@ def _windows(trace, fracs, times=None):
         return sends, tot, _observe(e, n, m)
 
 
+def test_incremental_member_marker_limit_covers_the_stream():
+    """The member incarnation counter (G_SEG: at most 254 E_EPOCH records per node) counts over
+    the whole live stream, not per window (include/mpx.h MPX_FLAG_INCREMENTAL, DESIGN.md §9;
+    ADVICE r04).  Windows of 127 markers on node 0: two are applied (254 so far), the third
+    window's one more marker is refused with MPX_E_RANGE, stays queued (refused again on the
+    next run) and leaves the engine readable (not poisoned)."""
+    epochs = [(k, 1, 1, 1) for k in range(300)]
+    with mpx.Engine(2, 0, 64, semantics=mpx.SEM_MEMBER, epochs=epochs, flags=mpx.FLAG_INCREMENTAL) as e:
+        for k0 in (1, 128):
+            e.submit(0, [mpxwire.e_epoch(k) for k in range(k0, k0 + 127)])
+            e.run()
+        d = e.state_digest()
+        e.submit(0, [mpxwire.e_epoch(255)])
+        for _ in range(2):
+            with pytest.raises(mpx.MpxError) as ex:
+                e.run()
+            assert ex.value.rc == -5
+        assert e.state_digest() == d
+
+
 MULTI_GOLDENS = sorted(k for k in INDEX if not k.startswith(("c5_", "mm_")) and "member" not in k)
 
 
