@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
@@ -84,6 +85,7 @@ struct mpx_engine {
     uint32_t num_cus = 256;
     ValueTable vt;
     std::vector<NodeStream> nodes;
+    std::vector<NodeStream> parts;             // submit_container's record chunks past each node's first (capacity kept)
     std::vector<EpochLearn> elearn;                  // MPX_FLAG_LEARN_EPOCHS: per node (ingest.hpp)
     IngestViolation iv;
     HostTrace ht;
@@ -405,38 +407,14 @@ static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, cons
         }
         return MPX_OK;
     }
-    // large traces: the nodes' streams are independent records, decoded on one
-    // host thread each into the one value table (sharded, a lock per shard: the same
-    // MPX_E_VALUE check across nodes), so ingest scales with the node count
+    // large traces: every node's stream cut into chunks decoded on a pool of host threads
+    // (ingest.cpp decode_parallel)
     const uint64_t t0 = now_ns();
-    std::vector<IngestViolation> ivs(N);
-    std::vector<int> rcs(N, MPX_OK);
-    SectionCache sc;                                 // (one decode per distinct entry list, this call)
-    const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
-    std::vector<std::thread> th;
-    for (uint32_t n = 0; n < N; ++n) {
-        th.emplace_back([&, n]() {
-            const uint64_t *offs; const uint8_t *bytes;
-            const uint64_t cnt = stream(n, offs, bytes);
-            NodeStream &ns = e->nodes[n];
-            for (uint64_t i = 0; i < cnt && rcs[n] == MPX_OK; ++i) {
-                if (offs[i + 1] < offs[i]) { rcs[n] = MPX_E_INVAL; break; }
-                const uint8_t *m = bytes + offs[i];
-                const size_t len = (size_t)(offs[i + 1] - offs[i]);
-                rcs[n] = member ? decode_record_member(e->vt, ns, n, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n],
-                                                       e->elearn.empty() ? nullptr : &e->elearn[n], &sc)
-                                : decode_record(e->vt, ns, n, N, m, len, e->cfg.shard_begin, e->cfg.shard_end, ivs[n], &sc);
-            }
-        });
-    }
-    for (auto &x : th) x.join();
-    for (uint32_t n = 0; n < N; ++n) {
-        TRY(rcs[n]);
-        if (ivs[n].count) {                          // first violation in node order
-            if (!e->iv.code) { e->iv.code = ivs[n].code; e->iv.node = ivs[n].node; e->iv.seq = ivs[n].seq; e->iv.iid = ivs[n].iid; }
-            e->iv.count += ivs[n].count;
-        }
-    }
+    std::vector<StreamSlice> sl(N);
+    for (uint32_t n = 0; n < N; ++n) sl[n].cnt = stream(n, sl[n].offs, sl[n].bytes);
+    TRY(decode_parallel(e->vt, e->nodes, e->parts, sl, e->cfg.semantics == MPX_SEM_MEMBER,
+                        e->elearn.empty() ? nullptr : &e->elearn, e->cfg.shard_begin, e->cfg.shard_end, e->iv,
+                        std::max(1u, std::min(16u, std::thread::hardware_concurrency())), 0));
     TRY(merge_epochs(e));
     e->dirty = true;
     e->stats.ingest_ns += now_ns() - t0;

@@ -9,8 +9,11 @@
 #include "ingest.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <thread>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 
 #include "mpx.h"
 
@@ -62,47 +65,53 @@ static inline size_t slot_of(uint64_t h, size_t mask) { return (size_t)((h * 0xD
 
 const ValueTable::Rec *ValueTable::Shard::find(uint64_t h) const
 {
-    if (key.empty()) return nullptr;
-    const size_t mask = key.size() - 1;
-    for (size_t i = slot_of(h, mask);; i = (i + 1) & mask) {
-        if (key[i] == h) return &rec[i];
-        if (key[i] == EMPTY) return nullptr;
+    if (slot.empty()) return nullptr;
+    const uint64_t gk = h >> GSH;
+    const size_t mask = slot.size() - 1;
+    for (size_t i = slot_of(gk, mask);; i = (i + 1) & mask) {
+        if (slot[i].key == gk) {
+            const Rec *r = &slot[i].g->r[h & (GN - 1)];
+            return r->p ? r : nullptr;
+        }
+        if (slot[i].key == EMPTY) return nullptr;
     }
 }
 
 ValueTable::Rec *ValueTable::Shard::insert(uint64_t h, bool &fresh)
 {
-    if (2 * (count + 1) > key.size()) {                       // grow: at most half full
-        std::vector<uint64_t> k2(key.empty() ? 1024 : 2 * key.size(), EMPTY);
-        std::vector<Rec> r2(k2.size());
-        const size_t m2 = k2.size() - 1;
-        for (size_t i = 0; i < key.size(); ++i) {
-            if (key[i] == EMPTY) continue;
-            size_t j = slot_of(key[i], m2);
-            while (k2[j] != EMPTY) j = (j + 1) & m2;
-            k2[j] = key[i]; r2[j] = rec[i];
+    const uint64_t gk = h >> GSH;
+    if (2 * (count + 1) > slot.size()) {                      // grow: at most half full
+        std::vector<GSlot> s2(slot.empty() ? 256 : 2 * slot.size(), GSlot{EMPTY, nullptr});
+        const size_t m2 = s2.size() - 1;
+        for (const GSlot &x : slot) {
+            if (x.key == EMPTY) continue;
+            size_t j = slot_of(x.key, m2);
+            while (s2[j].key != EMPTY) j = (j + 1) & m2;
+            s2[j] = x;
         }
-        key.swap(k2); rec.swap(r2);
-        kp.store(key.data(), std::memory_order_relaxed);
-        rp.store(rec.data(), std::memory_order_relaxed);
-        kmask.store(key.size() - 1, std::memory_order_relaxed);
+        slot.swap(s2);
+        sp.store(slot.data(), std::memory_order_relaxed);
+        smask.store(m2, std::memory_order_relaxed);
     }
-    const size_t mask = key.size() - 1;
-    size_t i = slot_of(h, mask);
-    while (key[i] != EMPTY && key[i] != h) i = (i + 1) & mask;
-    fresh = key[i] == EMPTY;
-    if (fresh) { key[i] = h; ++count; }
-    return &rec[i];
+    const size_t mask = slot.size() - 1;
+    size_t i = slot_of(gk, mask);
+    while (slot[i].key != EMPTY && slot[i].key != gk) i = (i + 1) & mask;
+    if (slot[i].key == EMPTY) {
+        constexpr size_t CHUNK = 1024;                        // groups per chunk (384 KiB)
+        if (gchunks.empty() || gused == CHUNK) { gchunks.emplace_back(new Group[CHUNK]()); gused = 0; }
+        slot[i] = GSlot{gk, &gchunks.back()[gused++]};
+        ++count;
+    }
+    Rec *r = &slot[i].g->r[h & (GN - 1)];
+    fresh = r->p == nullptr;
+    return r;
 }
 
 void ValueTable::prefetch_slot(uint64_t h) const
 {
     const Shard &x = sh[shard_of(h)];
-    const uint64_t *k = x.kp.load(std::memory_order_relaxed);
-    if (!k) return;
-    const size_t i = slot_of(h, x.kmask.load(std::memory_order_relaxed));
-    __builtin_prefetch(k + i);
-    __builtin_prefetch(x.rp.load(std::memory_order_relaxed) + i);
+    const GSlot *s = x.sp.load(std::memory_order_relaxed);
+    if (s) __builtin_prefetch(s + slot_of(h >> GSH, x.smask.load(std::memory_order_relaxed)));
 }
 
 int ValueTable::intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_off, uint32_t exec_len)
@@ -123,7 +132,7 @@ int ValueTable::intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_of
         x.used += len;
     }
     std::memcpy(dst, b, len);
-    *r = Rec{dst, len, exec_off, exec_len};
+    r->p = dst; r->len = len; r->exec_off = exec_off; r->exec_len = exec_len;
     return MPX_OK;
 }
 
@@ -383,6 +392,7 @@ static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool wit
     const size_t first = iid.size();
     n_all = 0;
     if (own && len >= 512) {                          // touch the Values' table slots first (see prefetch_slot)
+        uint64_t last = ValueTable::EMPTY;
         for (size_t c = 0; c < len;) {
             const size_t need = with_pid ? 16 : 8;
             if (len - c < need) break;
@@ -390,7 +400,8 @@ static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool wit
             uint64_t h;
             const long u = skim(b + c, len - c, vt.member, &h, nullptr);
             if (u < 0) break;                             // (the decode below reports it)
-            vt.prefetch_slot(h);
+            if ((h >> ValueTable::GSH) != last) vt.prefetch_slot(h);
+            last = h >> ValueTable::GSH;
             c += (size_t)u;
         }
     }
@@ -1440,6 +1451,100 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         wc->batches = gid_next;
         for (auto &x : state_new) wc->state_b[x.first][x.second] = 1;
     }
+    return MPX_OK;
+}
+
+int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<NodeStream> &parts,
+                    const std::vector<StreamSlice> &sl, bool member, std::vector<EpochLearn> *el,
+                    uint64_t sb, uint64_t se, IngestViolation &iv, uint32_t threads, uint64_t chunk_bytes)
+{
+    const uint32_t N = (uint32_t)sl.size();
+    if (nodes.size() < N) return MPX_E_INVAL;
+    threads = std::max(1u, threads);
+    struct Chunk { uint32_t n; uint64_t k0, k1; };
+    std::vector<Chunk> chunks;
+    {
+        uint64_t total = 0;
+        for (const auto &x : sl) if (x.cnt) total += x.offs[x.cnt] - x.offs[0];
+        const uint64_t target = el ? ~0ull : chunk_bytes ? chunk_bytes : std::max<uint64_t>(total / (4ull * threads), 1u << 20);
+        for (uint32_t n = 0; n < N; ++n) {
+            const StreamSlice &x = sl[n];
+            uint64_t k = 0;
+            do {
+                uint64_t k1 = x.cnt;
+                if (target != ~0ull && x.offs[x.cnt] - x.offs[k] > target) {
+                    // (a bad offset table is caught by the decode: offs[i + 1] < offs[i])
+                    k1 = (uint64_t)(std::upper_bound(x.offs + k, x.offs + x.cnt, x.offs[k] + target) - x.offs);
+                    k1 = std::min(x.cnt, std::max(k1, k + 1));
+                }
+                chunks.push_back({n, k, k1});
+                k = k1;
+            } while (k < x.cnt);
+        }
+    }
+    if (parts.size() < chunks.size()) parts.resize(chunks.size());
+    std::vector<IngestViolation> ivs(chunks.size());
+    std::vector<int> rcs(chunks.size(), MPX_OK);
+    SectionCache sc;                                 // (one decode per distinct entry list, this call)
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t c; (c = next.fetch_add(1)) < chunks.size();) {
+            const Chunk &ch = chunks[c];
+            const StreamSlice &x = sl[ch.n];
+            NodeStream &ns = ch.k0 == 0 ? nodes[ch.n] : parts[c];
+            if (ch.k0) ns.clear();
+            for (uint64_t i = ch.k0; i < ch.k1; ++i) {
+                if (x.offs[i + 1] < x.offs[i]) { rcs[c] = MPX_E_INVAL; break; }
+                const uint8_t *m = x.bytes + x.offs[i];
+                const size_t len = (size_t)(x.offs[i + 1] - x.offs[i]);
+                rcs[c] = member ? decode_record_member(vt, ns, ch.n, m, len, sb, se, ivs[c], el ? &(*el)[ch.n] : nullptr, &sc)
+                                : decode_record(vt, ns, ch.n, N, m, len, sb, se, ivs[c], &sc);
+                if (rcs[c]) break;
+            }
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (uint32_t k = 1; k < std::min<size_t>(threads, chunks.size()); ++k) th.emplace_back(work);
+        work();
+        for (auto &t : th) t.join();
+    }
+    for (size_t c = 0; c < chunks.size(); ++c) TRY_RC(rcs[c]);
+    // every node's later chunks in order (a thread per node): entry offsets and violation
+    // record indices rebased
+    auto append = [&](uint32_t n) {
+        NodeStream &ns = nodes[n];
+        for (size_t c = 0; c < chunks.size(); ++c) {
+            if (chunks[c].n != n || chunks[c].k0 == 0) continue;
+            const NodeStream &p = parts[c];
+            const uint64_t rb = ns.type.size(), eb = ns.e_iid.size(), qb = ns.r_iid.size(), gb = ns.g_a.size();
+            ivs[c].seq += rb;
+            auto cat = [](auto &dst, const auto &src) { dst.insert(dst.end(), src.begin(), src.end()); };
+            cat(ns.type, p.type); cat(ns.src, p.src); cat(ns.ballot, p.ballot); cat(ns.aux, p.aux);
+            cat(ns.cnt, p.cnt); cat(ns.ver, p.ver); cat(ns.part, p.part);
+            cat(ns.e_iid, p.e_iid); cat(ns.e_val, p.e_val); cat(ns.e_pid, p.e_pid);
+            cat(ns.r_iid, p.r_iid); cat(ns.r_pid, p.r_pid); cat(ns.r_val, p.r_val);
+            cat(ns.g_a, p.g_a); cat(ns.g_b, p.g_b);
+            ns.ent.reserve(ns.ent.size() + p.ent.size());
+            for (size_t k = 0; k < p.ent.size(); ++k) {
+                const uint8_t t = p.type[k];
+                const uint64_t base = t == MPX_MSG_PREPARE ? gb : t == MPX_MSG_PREPARE_REPLY ? qb :
+                                      (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_P_BATCH) ? eb : 0;
+                ns.ent.push_back(p.ent[k] + base);
+            }
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (uint32_t n = 1; n < N; ++n) th.emplace_back(append, n);
+        if (N) append(0);
+        for (auto &t : th) t.join();
+    }
+    for (size_t c = 0; c < chunks.size(); ++c)       // first violation in record order
+        if (ivs[c].count) {
+            if (!iv.code) { iv.code = ivs[c].code; iv.node = ivs[c].node; iv.seq = ivs[c].seq; iv.iid = ivs[c].iid; }
+            iv.count += ivs[c].count;
+        }
     return MPX_OK;
 }
 

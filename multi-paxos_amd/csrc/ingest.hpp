@@ -23,33 +23,43 @@ namespace mpx {
 // per-thread tables merged afterwards); the readers (encode, exec_payload) run when no decode
 // is in flight.
 struct ValueTable {
-    struct Rec { const char *p; uint32_t len; uint32_t exec_off; uint32_t exec_len; };
+    struct Rec { const char *p; uint32_t len; uint32_t exec_off; uint32_t exec_len; };   // p == nullptr: absent
     static constexpr uint32_t SHARDS = 64;
     static constexpr size_t BLOCK = 1 << 20;
-    static constexpr uint64_t EMPTY = ~0ull;            // (no handle: proposer < 2^14 keeps bits 62-63 clear)
-    // open addressing, linear probing, at most half full: no allocation per Value (a node-based
-    // map spent ~190 ns per insert at C3 window sizes, most of the host's decode time)
+    static constexpr uint64_t EMPTY = ~0ull;            // (no group key: proposer < 2^14 keeps bits 62-63 clear)
+    // A proposer numbers its Values 1, 2, 3, ... and a batch's instances carry consecutive ids, so
+    // the records sit in groups of 16 consecutive handles (h >> 4): a section's lookups walk a
+    // group's 384 contiguous bytes instead of one random slot per Value.  Groups are found through
+    // an open-addressing table (at most half full) of {group key, group} and allocated in chunks.
+    static constexpr uint32_t GSH = 4, GN = 1u << GSH;
+    struct Group { Rec r[GN]; };
+    struct GSlot { uint64_t key; Group *g; };
     struct Shard {
         std::mutex mu;
-        std::vector<uint64_t> key;
-        std::vector<Rec> rec;
-        size_t count = 0;
+        std::vector<GSlot> slot;
+        size_t count = 0;                                // groups
+        std::vector<std::unique_ptr<Group[]>> gchunks;   // group storage: stable addresses
+        size_t gused = 0;                                // groups used in the last chunk
         std::vector<std::unique_ptr<char[]>> blocks;     // canonical bytes: stable addresses, no regrowth copies
         size_t used = BLOCK;                             // bytes used in the last block
-        // the arrays' current addresses, published under mu for prefetch_slot (read without it)
-        std::atomic<const uint64_t *> kp{nullptr};
-        std::atomic<const Rec *> rp{nullptr};
-        std::atomic<size_t> kmask{0};
+        // the slot array's current address and mask, published under mu for prefetch_slot
+        std::atomic<const GSlot *> sp{nullptr};
+        std::atomic<size_t> smask{0};
         const Rec *find(uint64_t h) const;
         Rec *insert(uint64_t h, bool &fresh);
+        void release()
+        {
+            slot.clear(); slot.shrink_to_fit(); count = 0; gchunks.clear(); gused = 0;
+            sp.store(nullptr, std::memory_order_relaxed); smask.store(0, std::memory_order_relaxed);
+        }
     };
+    static uint32_t shard_of(uint64_t h) { return (uint32_t)(((h >> GSH) * 0x9E3779B97F4A7C15ull) >> 58); }
     std::unique_ptr<Shard[]> sh{new Shard[SHARDS]};
     // synthetic resolver for device-generated clean traces: value_id v of
     // proposer 0 is the decimal string of v-1
     bool synthetic_clean = false;
     // member Value_m codec (member/paxos.cpp:321-408): + cb, membership list
     bool member = false;
-    static uint32_t shard_of(uint64_t h) { return (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> 58); }
     // parse one Value; returns bytes used (>0) or a negative MPX_E_* code; *mem: a member
     // membership Value (a change list instead of a payload)
     long parse(const uint8_t *p, size_t avail, uint64_t *handle, bool *mem = nullptr);
@@ -61,8 +71,7 @@ struct ValueTable {
     {
         for (uint32_t k = 0; k < SHARDS; ++k) {
             Shard &x = sh[k];
-            x.key.clear(); x.rec.clear(); x.count = 0; x.blocks.clear(); x.used = BLOCK;
-            x.kp = nullptr; x.rp = nullptr; x.kmask = 0;
+            x.release(); x.blocks.clear(); x.used = BLOCK;
         }
         synthetic_clean = false;
     }
@@ -133,6 +142,9 @@ struct NodeStream {
 };
 
 struct IngestViolation { uint64_t code = 0, node = 0, seq = 0, iid = 0, count = 0; };
+
+// One node's records to decode: offs[0 .. cnt] index bytes (an MPXT stream, or a slice of one).
+struct StreamSlice { const uint64_t *offs = nullptr; const uint8_t *bytes = nullptr; uint64_t cnt = 0; };
 
 // Incremental runs (MPX_FLAG_INCREMENTAL): what build_trace needs from
 // the windows before the current one to list the current window's snapshot events and
@@ -237,6 +249,18 @@ int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord
 int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const uint8_t *m, size_t len,
                          uint64_t shard_begin, uint64_t shard_end, IngestViolation &viol, EpochLearn *el = nullptr,
                          SectionCache *sc = nullptr);
+
+// Decode every node's slice sl[n], appended to nodes[n], on `threads` host threads: each stream is
+// cut into chunks of about `chunk_bytes` (0: the total over 4 x threads, at least 1 MiB) decoded
+// independently into the one value table — a node's first chunk straight into its stream, the
+// later ones into `parts` (scratch, capacity kept), appended in record order with their entry
+// offsets rebased — so the result is the serial decode's record for record.  `el` (learned
+// epochs): one chunk per node, the Learner's apply frontier walks its records in order.  The
+// violations are merged into `iv` in record order; the first failing chunk's code is returned.
+int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<NodeStream> &parts,
+                    const std::vector<StreamSlice> &sl, bool member, std::vector<EpochLearn> *el,
+                    uint64_t shard_begin, uint64_t shard_end, IngestViolation &iv, uint32_t threads,
+                    uint64_t chunk_bytes);
 
 // Flatten node streams and build every index the kernels walk.  `epochs`
 // non-empty selects member semantics (role / version gates, E_EPOCH events).

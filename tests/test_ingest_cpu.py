@@ -67,3 +67,52 @@ def test_learned_epochs_on_generated_c5(epoch_checker, lg, proposers, windows):
                        text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
     assert int(r.stdout.split()[3]) == 15          # every step of the C5 schedule learned
+
+
+# ---- chunked multi-threaded decode (ingest.cpp decode_parallel, submit_container) ----
+@pytest.fixture(scope="module")
+def par_checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("pdec") / "parallel_decode_check")
+    src = [os.path.join(ROOT, "tests", "parallel_decode_check.cpp")] + \
+          [os.path.join(CSRC, f) for f in ("ingest.cpp", "gen.cpp", "gen_faulty.cpp", "gen_member.cpp")]
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I" + CSRC, "-I" + os.path.join(ROOT, "include")] + src +
+                   ["-o", exe], check=True, timeout=600)
+    return exe
+
+
+@pytest.mark.parametrize("kind,lg,proposers,chunk,threads", [("faulty", 15, 3, 4096, 5), ("faulty", 14, 0, 1 << 16, 8),
+                                                             ("member", 14, 3, 2048, 6), ("member", 13, 0, 512, 3)])
+def test_parallel_decode_equals_serial_generated(par_checker, kind, lg, proposers, chunk, threads):
+    """decode_parallel (a node's stream in chunks on a thread pool, later chunks appended with their
+    entry offsets rebased) gives the serial decode array for array, after records already queued."""
+    r = subprocess.run([par_checker, kind, str(lg), str(proposers), str(chunk), str(threads)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("ok "), r.stdout + r.stderr
+    assert int(r.stdout.split()[2]) > 1          # several chunks per node
+
+
+def test_parallel_decode_equals_serial_goldens(par_checker):
+    for f in sorted(os.listdir(GOLD)):
+        if f.endswith(".mpxt"):
+            r = subprocess.run([par_checker, os.path.join(GOLD, f), "0", "0", "64", "4"], capture_output=True,
+                               text=True, timeout=120)
+            assert r.returncode == 0 and r.stdout.startswith("ok"), f + ": " + r.stdout + r.stderr
+
+
+def test_parallel_decode_violations_in_record_order(par_checker, tmp_path):
+    """Duplicate iids (MPX_V_DUP_IID, the reference ASSERTs) in later chunks of several nodes: the
+    first violation (node, record index) and the count are the serial decode's."""
+    import mpxwire as w
+    streams = []
+    for n in range(3):
+        s = [w.accept(0, k, 5, [(2 * k, w.value(0, 2 * k + 1, "x" * 40)), (2 * k + 1, w.value(0, 2 * k + 2, "y"))])
+             for k in range(60)]
+        if n:
+            s[40 + n] = w.accept(0, 99, 5, [(7, w.value(0, 500, "a")), (7, w.value(0, 501, "b"))])
+            s[50] = w.prepare(1, 9, ((0, 10), (0, 10)))
+        streams.append(s)
+    p = tmp_path / "dup.mpxt"
+    p.write_bytes(w.container(streams, 256))
+    r = subprocess.run([par_checker, str(p), "0", "0", "256", "4"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.startswith("ok "), r.stdout + r.stderr
+    assert int(r.stdout.split()[3]) == 4
