@@ -965,8 +965,227 @@ static void mark_value_checks(HostTrace &ht, bool member)
     }
 }
 
-int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen,
-                const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc)
+namespace {
+struct FragKey { uint64_t key; Frag f; };
+// a window's carry past one node (committed to the WindowCarry only when the build succeeds)
+struct NodeCarry {
+    std::unordered_map<uint64_t, uint32_t> live;
+    std::vector<uint64_t> round_b;
+    int64_t maxb = -1;
+    uint64_t ballot = 0;
+    uint32_t markers = 0;
+};
+// what the walk over the nodes' records hands to finish_trace
+struct Walk {
+    std::vector<uint64_t> fcount, cfcount;        // runs per (bucket, node) pair / per bucket's chosen list
+    std::vector<FragKey> fr, cfr;                 // the runs, in walk order
+    std::vector<uint32_t> pl;                     // proposer lists (messages)
+    std::vector<uint64_t> pl_cnt;
+    std::vector<std::pair<uint64_t, uint32_t>> evp;   // snapshot events (pair, message)
+    std::vector<uint64_t> evx;
+    std::vector<uint64_t> sc_off;
+    std::vector<std::vector<uint32_t>> reps;      // per batch: its vote messages
+    std::vector<uint64_t> b_bal_w;                // (window) per batch: its round's ballot
+    std::vector<std::pair<uint32_t, uint64_t>> state_new;
+    std::vector<NodeCarry> next;
+    std::vector<uint32_t> ents_gone;
+    std::unordered_map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> ents_new;
+    uint64_t gid_next = 0;
+};
+}  // namespace
+
+// Everything after the walk over the nodes' records: the vote lists, the run / event CSRs, the
+// work lists, the scan chunks, and (a window) the carry, committed only when every check passed.
+static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_t sb, uint64_t slen, bool member,
+                        WindowCarry *wc)
+{
+    auto &fcount = W.fcount, &cfcount = W.cfcount;
+    auto &fr = W.fr, &cfr = W.cfr;
+    auto &pl = W.pl;
+    auto &pl_cnt = W.pl_cnt;
+    auto &evp = W.evp;
+    auto &evx = W.evx;
+    auto &sc_off = W.sc_off;
+    auto &reps = W.reps;
+    auto &b_bal_w = W.b_bal_w;
+    auto &state_new = W.state_new;
+    auto &next = W.next;
+    auto &ents_gone = W.ents_gone;
+    auto &ents_new = W.ents_new;
+    const uint64_t gid_next = W.gid_next;
+    (void)sb;
+    ht.node_off[N] = ht.m_type.size();
+    sc_off[N] = ht.sc_type.size();
+    if (ht.prop_off.empty()) ht.prop_off.assign(N + 1, 0);
+    ht.prop_off[N] = ht.prop_seq.size();
+    if (member) {
+        ht.ee_off[N] = ht.ee_msg.size();
+        ht.sc_off = sc_off;
+        for (uint32_t n = 0; n < N; ++n)       // the device incarnation (G_SEG) counts at most one per marker
+            if ((wc ? next[n].markers : ht.ee_off[n + 1] - ht.ee_off[n]) >= G_SEG) return MPX_E_RANGE;
+    }
+
+    // vote lists (attributed in the walk above)
+    {
+        ht.b_rep_off.assign(ht.b_msg.size() + 1, 0);
+        for (size_t j = 0; j < reps.size(); ++j) ht.b_rep_off[j + 1] = ht.b_rep_off[j] + reps[j].size();
+        ht.b_rep.reserve(ht.b_rep_off.back());
+        for (auto &r : reps) ht.b_rep.insert(ht.b_rep.end(), r.begin(), r.end());
+        // the replies' headers beside the list (read in order by k_votes, no gathers)
+        ht.b_rbal.resize(ht.b_rep.size());
+        ht.b_rsrc.resize(ht.b_rep.size());
+        for (size_t r = 0; r < ht.b_rep.size(); ++r) {
+            const uint32_t g = ht.b_rep[r];
+            ht.b_rbal[r] = ht.m_ballot[g];
+            ht.b_rsrc[r] = std::min<uint32_t>(ht.m_src[g], 0xFFFF);   // member: epoch bits added on the device
+        }
+        ht.b_bal.resize(ht.b_msg.size());
+        for (size_t j = 0; j < ht.b_msg.size(); ++j)
+            ht.b_bal[j] = wc ? b_bal_w[j] : ht.b_pstart[j] == NONE32 ? 0 : ht.m_ballot[ht.b_pstart[j]];
+    }
+
+    // fragment CSR per (node, bucket), stable (keeps message order)
+    ht.f_off.assign(N * NB + 1, 0);
+    for (uint64_t i = 0; i < N * NB; ++i) {
+        ht.f_off[i + 1] = ht.f_off[i] + fcount[i];
+        if (fcount[i] > MAX_PAIR_FRAGS) return MPX_E_RANGE;   // 2-byte state slots (mpx_internal.hpp)
+    }
+    if (fr.size() > MAX_FRAGS) return MPX_E_RANGE;             // 4-byte state slots (mpx_internal.hpp)
+    ht.frags.resize(fr.size());
+    {
+        std::vector<uint64_t> pos(ht.f_off.begin(), ht.f_off.end() - 1);
+        for (auto &x : fr) ht.frags[pos[x.key]++] = x.f;
+    }
+    if (!wc) mark_value_checks(ht, member);
+    ht.cf_off.assign(NB + 1, 0);
+    for (uint64_t i = 0; i < NB; ++i) {
+        ht.cf_off[i + 1] = ht.cf_off[i] + cfcount[i];
+        if (cfcount[i] > MAX_PAIR_FRAGS) return MPX_E_RANGE;  // 2-byte chosen log (mpx_internal.hpp)
+    }
+    ht.cfrags.resize(cfr.size());
+    {
+        std::vector<uint64_t> pos(ht.cf_off.begin(), ht.cf_off.end() - 1);
+        for (auto &x : cfr) ht.cfrags[pos[x.key]++] = x.f;
+    }
+    // per-pair event CSR (stable: message order within a pair)
+    ht.ev_off.assign(N * NB + 1, 0);
+    ht.pair_ev.assign(N * NB, 0);
+    for (auto &x : evp) ht.ev_off[x.first + 1]++;
+    for (uint64_t i = 0; i < N * NB; ++i) {
+        ht.pair_ev[i] = ht.ev_off[i + 1] ? 1 : 0;
+        ht.ev_off[i + 1] += ht.ev_off[i];
+    }
+    ht.ev_msg.resize(evp.size());
+    ht.ev_aux.resize(evp.size());
+    {
+        std::vector<uint64_t> pos(ht.ev_off.begin(), ht.ev_off.end() - 1);
+        for (size_t i = 0; i < evp.size(); ++i) {
+            const uint64_t at = pos[evp[i].first]++;
+            ht.ev_msg[at] = evp[i].second;
+            ht.ev_aux[at] = evx[i];
+        }
+    }
+    std::vector<uint64_t>().swap(evx);
+    std::vector<std::pair<uint64_t, uint32_t>>().swap(evp);
+    // pairs that are not lean (mpx_internal.hpp plan_shape_ok: one plan word of
+    // k_plan) go to the general kernel's work list
+    ht.pair_gp.assign(N * NB, 0);
+    if (wc) {
+        // incremental window: every pair with runs or events of the window walks the
+        // window apply kernel (k_apply_win), on the state earlier windows left
+        for (uint64_t b = 0; b < NB; ++b)
+            for (uint32_t n = 0; n < N; ++n) {
+                const uint64_t p = b * N + n;
+                if (ht.f_off[p + 1] == ht.f_off[p] && ht.ev_off[p + 1] == ht.ev_off[p]) continue;
+                ht.gp_list.push_back(p);
+                ht.gp_base.push_back(wc->state_b[n][b]);
+                ht.pair_gp[p] = GP_ROUNDS;
+            }
+        for (uint64_t b = 0; b < NB; ++b)
+            if (ht.cf_off[b + 1] > ht.cf_off[b]) ht.cb_list.push_back((uint32_t)b);
+        ht.num_gp_simple = ht.num_gp_snap = 0;
+    }
+    for (uint64_t b = 0; b < NB && !wc; ++b)
+        for (uint32_t n = 0; n < N; ++n) {
+            const uint64_t p = b * N + n, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
+            if (!nf) continue;
+            bool fast = !member && N <= FAST_MAX_NODES && nf <= PLAN_FRAGS && !ht.pair_ev[p] && (b + 1) * BS <= slen;
+            if (fast) {
+                uint64_t w1[PLAN_FRAGS];
+                for (uint64_t f = 0; f < nf; ++f) std::memcpy(&w1[f], reinterpret_cast<const uint8_t *>(&ht.frags[f0 + f]) + 8, 8);
+                fast = plan_shape_ok(w1, (uint32_t)nf);
+            }
+            if (!fast) { ht.gp_list.push_back(p); ht.pair_gp[p] = GP_LIST; }
+        }
+    // work-list order: the pairs with no snapshot events and no promise-reply runs
+    // first (k_apply's SIMPLE instantiation takes them), pair order kept
+    // then those with no promise-reply runs (their events are PREPAREs only, member:
+    // and E_EPOCHs; k_apply AM_SNAP), then the rest (promise rounds)
+    if (!wc) {
+        ht.num_gp_simple = ht.num_gp_snap = 0;
+        auto no_preply = [&](uint64_t p) {
+            for (uint64_t f = ht.f_off[p]; f < ht.f_off[p + 1]; ++f)
+                if ((ht.frags[f].flags >> 4) == K_PREPLY) return false;
+            return true;
+        };
+        auto mid = std::stable_partition(ht.gp_list.begin(), ht.gp_list.end(), no_preply);
+        ht.num_gp_snap = (uint64_t)(mid - ht.gp_list.begin());
+        auto mid2 = std::stable_partition(ht.gp_list.begin(), mid, [&](uint64_t p) { return !ht.pair_ev[p]; });
+        ht.num_gp_simple = (uint64_t)(mid2 - ht.gp_list.begin());
+        // k_plan_list takes the pairs before `mid` (or lists them for k_apply itself);
+        // the promise-round pairs stay on the host range of the full kernel
+        for (auto it = mid; it != ht.gp_list.end(); ++it) ht.pair_gp[*it] = GP_ROUNDS;
+    }
+    // slots for sparse fragments
+    if (ht.any_sparse) {
+        ht.e_slot.resize(ht.e_iid.size());
+        for (size_t k = 0; k < ht.e_iid.size(); ++k) ht.e_slot[k] = (uint8_t)((ht.e_iid[k] - sb) & (BS - 1));
+        ht.r_slot.resize(ht.r_iid.size());
+        for (size_t k = 0; k < ht.r_iid.size(); ++k) ht.r_slot[k] = (uint8_t)((ht.r_iid[k] - sb) & (BS - 1));
+    }
+    // proposer lists
+    ht.pl_off.assign(N + 1, 0);
+    for (uint32_t n = 0; n < N; ++n) ht.pl_off[n + 1] = ht.pl_off[n] + pl_cnt[n];
+    ht.pl_msg = std::move(pl);
+    // header-scan chunks, over each node's scan stream
+    ht.node_chunk_off.assign(N + 1, 0);
+    ht.scan_chunk = scan_chunk_for(sc_off[N]);
+    for (uint32_t n = 0; n < N; ++n) {
+        ht.node_chunk_off[n] = (uint32_t)ht.chunk_node.size();
+        for (uint64_t g = sc_off[n]; g < sc_off[n + 1]; g += ht.scan_chunk) {
+            ht.chunk_node.push_back(n);
+            ht.chunk_beg.push_back(g);
+            ht.chunk_end.push_back(std::min<uint64_t>(g + ht.scan_chunk, sc_off[n + 1]));
+        }
+    }
+    ht.node_chunk_off[N] = (uint32_t)ht.chunk_node.size();
+    if (wc) {
+        // every check passed: the window is consumed, the carry moves past it
+        for (uint32_t n = 0; n < N; ++n) {
+            NodeCarry &c = next[n];
+            wc->live[n] = std::move(c.live);
+            wc->round_b[n] = std::move(c.round_b);
+            wc->maxb[n] = c.maxb;
+            wc->round_ballot[n] = c.ballot;
+            wc->markers[n] = c.markers;
+        }
+        for (uint32_t gid : ents_gone) wc->b_ents.erase(gid);
+        for (auto &x : ents_new) wc->b_ents[x.first] = std::move(x.second);
+        for (size_t j = 0; j < ht.b_msg.size(); ++j)
+            if (ht.b_msg[j] != NONE32) {                    // new batches, in id order
+                wc->b_bal.push_back(b_bal_w[j]);
+                wc->b_aid.push_back(ht.b_aid[j]);
+            }
+        wc->batches = gid_next;
+        for (auto &x : state_new) wc->state_b[x.first][x.second] = 1;
+    }
+    return MPX_OK;
+}
+
+// The one-thread build (the reference for build_trace's node-parallel walk: tests and tools compare
+// the two HostTraces field by field).
+int build_trace_serial(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen,
+                       const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc)
 {
     const bool member = !epochs.empty();
     if (wc && !wc->on) return MPX_E_STATE;
@@ -988,11 +1207,12 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
 
     EntryPool pool;
     pool.member = member;
-    struct FragKey { uint64_t key; Frag f; };
-    std::vector<uint64_t> fcount(N * NB + 1, 0), cfcount(NB + 1, 0);
-    std::vector<FragKey> fr, cfr;
-    std::vector<uint32_t> pl;
-    std::vector<uint64_t> pl_cnt(N, 0);
+    Walk W;
+    W.fcount.assign(N * NB + 1, 0); W.cfcount.assign(NB + 1, 0); W.pl_cnt.assign(N, 0);
+    auto &fcount = W.fcount, &cfcount = W.cfcount;
+    auto &fr = W.fr, &cfr = W.cfr;
+    auto &pl = W.pl;
+    auto &pl_cnt = W.pl_cnt;
     // Snapshot events (PREPARE, PREPARE_REPLY, P_START, E_EPOCH) are listed per
     // (bucket, node) pair, only where they can act on the pair's state:
     //   PREPARE       FilterAcceptedValues (multi/paxos.cpp:902-922) reads accepted /
@@ -1004,39 +1224,35 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
     //   E_EPOCH       (member) the same, plus every bucket with state when the node's
     //                 Acceptor is deleted / recreated (member/paxos.cpp:1897-1901,1952-1957).
     // So a pair walks O(events that touch it), not every event of its node.
-    std::vector<std::pair<uint64_t, uint32_t>> evp;          // (pair, message)
-    std::vector<uint64_t> evx;                               // its aux word (PREPARE: the ranges meeting the bucket)
+    auto &evp = W.evp;                                       // (pair, message)
+    auto &evx = W.evx;                                       // its aux word (PREPARE: the ranges meeting the bucket)
     std::vector<uint32_t> first_frag(NB, NONE32);            // per bucket: the node's first fragment message
     std::vector<uint64_t> touched, round_b;
     std::vector<uint8_t> in_round(NB, 0);
-    std::vector<uint64_t> sc_off(N + 1, 0);                 // each node's scan-stream range
+    W.sc_off.assign(N + 1, 0);
+    auto &sc_off = W.sc_off;                                 // each node's scan-stream range
     // vote lists: an ACCEPT_REPLY counts for the live batch of its node with the
     // same accept id (OnAcceptReply, multi/paxos.cpp:1406-1410); member: only at a
     // node whose Proposer exists (Loop, member/paxos.cpp:763-790)
     std::unordered_map<uint64_t, uint32_t> live;
-    std::vector<std::vector<uint32_t>> reps;
+    auto &reps = W.reps;
     if (member) ht.ee_off.assign(N + 1, 0);
     // incremental window: batch ids are global (live maps to them); a batch's index in
     // this window's list, its round ballot, and where a new one's entries are
     std::unordered_map<uint32_t, uint32_t> gid_local;
-    std::vector<uint64_t> b_bal_w;
+    auto &b_bal_w = W.b_bal_w;
     std::vector<std::pair<uint64_t, uint32_t>> b_ent_w;          // per window batch: pool offset, count (new ones)
-    std::vector<std::pair<uint32_t, uint64_t>> state_new;        // (node, bucket) met by this window's runs
+    auto &state_new = W.state_new;                               // (node, bucket) met by this window's runs
     const uint64_t gid0 = wc ? wc->batches : 0;
-    uint64_t gid_next = gid0;
+    W.gid_next = gid0;
+    auto &gid_next = W.gid_next;
     // The carry past this window is collected here and committed to *wc only once every
     // check below has passed: a window that fails (MPX_E_RANGE, MPX_E_DECODE) leaves the
     // carry as it was, so its records can be resubmitted or the engine dropped
-    struct NodeCarry {
-        std::unordered_map<uint64_t, uint32_t> live;
-        std::vector<uint64_t> round_b;
-        int64_t maxb = -1;
-        uint64_t ballot = 0;
-        uint32_t markers = 0;
-    };
-    std::vector<NodeCarry> next(wc ? N : 0);
-    std::vector<uint32_t> ents_gone;                             // carried batches no longer live
-    std::unordered_map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> ents_new;
+    W.next.resize(wc ? N : 0);
+    auto &next = W.next;
+    auto &ents_gone = W.ents_gone;                               // carried batches no longer live
+    auto &ents_new = W.ents_new;
 
     for (uint32_t n = 0; n < N; ++n) {
         const NodeStream &ns = nodes[n];
@@ -1286,172 +1502,533 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             if (member) c.markers = wc->markers[n] + (uint32_t)(ht.ee_msg.size() - ht.ee_off[n]);
         }
     }
-    ht.node_off[N] = ht.m_type.size();
-    sc_off[N] = ht.sc_type.size();
-    if (ht.prop_off.empty()) ht.prop_off.assign(N + 1, 0);
-    ht.prop_off[N] = ht.prop_seq.size();
-    if (member) {
-        ht.ee_off[N] = ht.ee_msg.size();
-        ht.sc_off = sc_off;
-        for (uint32_t n = 0; n < N; ++n)       // the device incarnation (G_SEG) counts at most one per marker
-            if ((wc ? next[n].markers : ht.ee_off[n + 1] - ht.ee_off[n]) >= G_SEG) return MPX_E_RANGE;
-    }
+    return finish_trace(ht, W, N, NB, sb, slen, member, wc);
+}
 
-    // vote lists (attributed in the walk above)
-    {
-        ht.b_rep_off.assign(ht.b_msg.size() + 1, 0);
-        for (size_t j = 0; j < reps.size(); ++j) ht.b_rep_off[j + 1] = ht.b_rep_off[j] + reps[j].size();
-        ht.b_rep.reserve(ht.b_rep_off.back());
-        for (auto &r : reps) ht.b_rep.insert(ht.b_rep.end(), r.begin(), r.end());
-        // the replies' headers beside the list (read in order by k_votes, no gathers)
-        ht.b_rbal.resize(ht.b_rep.size());
-        ht.b_rsrc.resize(ht.b_rep.size());
-        for (size_t r = 0; r < ht.b_rep.size(); ++r) {
-            const uint32_t g = ht.b_rep[r];
-            ht.b_rbal[r] = ht.m_ballot[g];
-            ht.b_rsrc[r] = std::min<uint32_t>(ht.m_src[g], 0xFFFF);   // member: epoch bits added on the device
-        }
-        ht.b_bal.resize(ht.b_msg.size());
-        for (size_t j = 0; j < ht.b_msg.size(); ++j)
-            ht.b_bal[j] = wc ? b_bal_w[j] : ht.b_pstart[j] == NONE32 ? 0 : ht.m_ballot[ht.b_pstart[j]];
-    }
+// ---- build_trace: the walk over the nodes' records, node-parallel ----
+//
+// Phase A (a thread per node): the serial walk's per-node work in node-local coordinates —
+// kept messages numbered from 0, batches from 0 in first-reference order, entry lists by the
+// node's own arrays, each list to intern (ACCEPT / COMMIT / P_BATCH, a window's carried batch
+// entries) hashed.  Phase B: the entry pool — first occurrences in walk order (node, list),
+// found per hash shard on a thread each, lists compared in full; then their offsets in order.
+// Phase C (a thread per node): the parts rebased into the HostTrace (message, batch, pool, range
+// and promise-reply offsets).  The result is build_trace_serial's, field for field.
+namespace {
+struct PoolItem {
+    uint32_t node;
+    uint32_t batch;                     // carried batch list: its local batch (NONE32: a message's list)
+    uint64_t first;                     // the node's e_* index (carried: 0)
+    uint32_t cnt;
+    uint64_t hash;
+    const std::vector<std::pair<uint64_t, uint64_t>> *carried;
+    uint64_t off;                       // phase B: pool offset
+    bool is_first;
+};
+struct NodePart {
+    int rc = MPX_OK;
+    std::vector<uint8_t> m_type, m_flags0;
+    std::vector<uint32_t> m_src, m_cnt, m_ver, m_seq;
+    std::vector<uint64_t> m_ballot, m_aux, m_ent;   // m_ent: g_a / r index (node-local), or pool item
+    std::vector<uint8_t> sc_type;
+    std::vector<uint64_t> sc_key;
+    std::vector<uint32_t> sc_idx, sc_ver;            // sc_idx: local message, NONE32 = literal 0
+    std::vector<uint32_t> ee_msg, pl, prop_seq;
+    uint64_t dropped = 0, part_dropped = 0;
+    bool any_sparse = false;
+    // batches in first-reference order
+    std::vector<uint32_t> b_msg, b_pstart, b_gid, b_item;   // b_gid: carried: global; new: gid0 + local new index
+    std::vector<uint64_t> b_aid, b_bal;
+    std::vector<std::pair<uint64_t, uint32_t>> b_ent;       // new batches: their list (node e_* index, count)
+    std::vector<std::vector<uint32_t>> reps;
+    uint32_t new_batches = 0;
+    std::vector<PoolItem> items;
+    // runs: Frag.entry relative to its list (fr_item / cfr_item), or a node-local r index (NONE32)
+    std::vector<FragKey> fr, cfr;
+    std::vector<uint32_t> fr_item, cfr_item;
+    std::vector<uint64_t> fcount, cfcount;                   // (sparse: touched pairs only, see below)
+    std::vector<std::pair<uint64_t, uint32_t>> evp;
+    std::vector<uint64_t> evx;
+    std::vector<uint64_t> state_b;                           // (window) buckets first met
+    NodeCarry carry;
+    std::vector<uint32_t> ents_gone;
+    std::vector<std::pair<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>>> ents_new;   // (gid, entries)
+};
 
-    // fragment CSR per (node, bucket), stable (keeps message order)
-    ht.f_off.assign(N * NB + 1, 0);
-    for (uint64_t i = 0; i < N * NB; ++i) {
-        ht.f_off[i + 1] = ht.f_off[i] + fcount[i];
-        if (fcount[i] > MAX_PAIR_FRAGS) return MPX_E_RANGE;   // 2-byte state slots (mpx_internal.hpp)
-    }
-    if (fr.size() > MAX_FRAGS) return MPX_E_RANGE;             // 4-byte state slots (mpx_internal.hpp)
-    ht.frags.resize(fr.size());
-    {
-        std::vector<uint64_t> pos(ht.f_off.begin(), ht.f_off.end() - 1);
-        for (auto &x : fr) ht.frags[pos[x.key]++] = x.f;
-    }
-    if (!wc) mark_value_checks(ht, member);
-    ht.cf_off.assign(NB + 1, 0);
-    for (uint64_t i = 0; i < NB; ++i) {
-        ht.cf_off[i + 1] = ht.cf_off[i] + cfcount[i];
-        if (cfcount[i] > MAX_PAIR_FRAGS) return MPX_E_RANGE;  // 2-byte chosen log (mpx_internal.hpp)
-    }
-    ht.cfrags.resize(cfr.size());
-    {
-        std::vector<uint64_t> pos(ht.cf_off.begin(), ht.cf_off.end() - 1);
-        for (auto &x : cfr) ht.cfrags[pos[x.key]++] = x.f;
-    }
-    // per-pair event CSR (stable: message order within a pair)
-    ht.ev_off.assign(N * NB + 1, 0);
-    ht.pair_ev.assign(N * NB, 0);
-    for (auto &x : evp) ht.ev_off[x.first + 1]++;
-    for (uint64_t i = 0; i < N * NB; ++i) {
-        ht.pair_ev[i] = ht.ev_off[i + 1] ? 1 : 0;
-        ht.ev_off[i + 1] += ht.ev_off[i];
-    }
-    ht.ev_msg.resize(evp.size());
-    ht.ev_aux.resize(evp.size());
-    {
-        std::vector<uint64_t> pos(ht.ev_off.begin(), ht.ev_off.end() - 1);
-        for (size_t i = 0; i < evp.size(); ++i) {
-            const uint64_t at = pos[evp[i].first]++;
-            ht.ev_msg[at] = evp[i].second;
-            ht.ev_aux[at] = evx[i];
-        }
-    }
-    std::vector<uint64_t>().swap(evx);
-    std::vector<std::pair<uint64_t, uint32_t>>().swap(evp);
-    // pairs that are not lean (mpx_internal.hpp plan_shape_ok: one plan word of
-    // k_plan) go to the general kernel's work list
-    ht.pair_gp.assign(N * NB, 0);
+static uint64_t list_hash(const uint64_t *iv, const uint64_t *vv, const uint64_t *pv, uint32_t cnt, bool member)
+{
+    // EntryPool::intern's hash (content-equal lists hash equal)
+    uint64_t l[4] = {mix64(cnt + 0x51ull), 0x9E3779B97F4A7C15ull, 0xC2B2AE3D27D4EB4Full, 0x165667B19E3779F9ull};
+    for (uint32_t i = 0; i < cnt; ++i) l[i & 3] = (l[i & 3] ^ iv[i]) * 0xff51afd7ed558ccdull + vv[i];
+    if (member)
+        for (uint32_t i = 0; i < cnt; ++i) l[i & 3] = (l[i & 3] ^ (pv ? pv[i] : 0)) * 0xc4ceb9fe1a85ec53ull;
+    return mix64(mix64(mix64(l[0] ^ l[1]) ^ l[2]) ^ l[3]);
+}
+
+static void walk_node(const NodeStream &ns, uint32_t n, uint32_t N, uint64_t sb, uint64_t slen, uint64_t NB,
+                      bool member, size_t num_epochs, const WindowCarry *wc, NodePart &P)
+{
+    const uint64_t gid0 = wc ? wc->batches : 0;
+    std::vector<uint32_t> first_frag(NB, NONE32);            // per bucket: the node's first fragment message
+    std::vector<uint8_t> in_round(NB, 0);
+    std::vector<uint64_t> round_b;
+    int64_t maxb = -1;
+    std::unordered_map<uint64_t, uint32_t> live;              // accept id -> batch (window: global id)
+    uint64_t cur_bal = 0;
+    std::unordered_map<uint32_t, uint32_t> gid_local;         // (window) batch id -> local batch
     if (wc) {
-        // incremental window: every pair with runs or events of the window walks the
-        // window apply kernel (k_apply_win), on the state earlier windows left
-        for (uint64_t b = 0; b < NB; ++b)
-            for (uint32_t n = 0; n < N; ++n) {
-                const uint64_t p = b * N + n;
-                if (ht.f_off[p + 1] == ht.f_off[p] && ht.ev_off[p + 1] == ht.ev_off[p]) continue;
-                ht.gp_list.push_back(p);
-                ht.gp_base.push_back(wc->state_b[n][b]);
-                ht.pair_gp[p] = GP_ROUNDS;
-            }
-        for (uint64_t b = 0; b < NB; ++b)
-            if (ht.cf_off[b + 1] > ht.cf_off[b]) ht.cb_list.push_back((uint32_t)b);
-        ht.num_gp_simple = ht.num_gp_snap = 0;
+        live = wc->live[n];
+        for (uint64_t b : wc->round_b[n]) { in_round[b] = 1; round_b.push_back(b); }
+        maxb = wc->maxb[n];
+        cur_bal = wc->round_ballot[n];
     }
-    for (uint64_t b = 0; b < NB && !wc; ++b)
-        for (uint32_t n = 0; n < N; ++n) {
-            const uint64_t p = b * N + n, f0 = ht.f_off[p], nf = ht.f_off[p + 1] - f0;
-            if (!nf) continue;
-            bool fast = !member && N <= FAST_MAX_NODES && nf <= PLAN_FRAGS && !ht.pair_ev[p] && (b + 1) * BS <= slen;
-            if (fast) {
-                uint64_t w1[PLAN_FRAGS];
-                for (uint64_t f = 0; f < nf; ++f) std::memcpy(&w1[f], reinterpret_cast<const uint8_t *>(&ht.frags[f0 + f]) + 8, 8);
-                fast = plan_shape_ok(w1, (uint32_t)nf);
-            }
-            if (!fast) { ht.gp_list.push_back(p); ht.pair_gp[p] = GP_LIST; }
+    const bool has_pid = !ns.e_pid.empty();
+    auto add_item = [&](uint32_t batch, uint64_t first, uint32_t cnt,
+                        const std::vector<std::pair<uint64_t, uint64_t>> *carried) -> uint32_t {
+        PoolItem it{n, batch, first, cnt, 0, carried, 0, false};
+        if (carried) {
+            std::vector<uint64_t> iv(cnt), vv(cnt);
+            for (uint32_t q = 0; q < cnt; ++q) { iv[q] = (*carried)[q].first; vv[q] = (*carried)[q].second; }
+            it.hash = list_hash(iv.data(), vv.data(), nullptr, cnt, member);
+        } else {
+            it.hash = list_hash(ns.e_iid.data() + first, ns.e_val.data() + first, has_pid ? ns.e_pid.data() + first : nullptr,
+                                cnt, member);
         }
-    // work-list order: the pairs with no snapshot events and no promise-reply runs
-    // first (k_apply's SIMPLE instantiation takes them), pair order kept
-    // then those with no promise-reply runs (their events are PREPAREs only, member:
-    // and E_EPOCHs; k_apply AM_SNAP), then the rest (promise rounds)
-    if (!wc) {
-        ht.num_gp_simple = ht.num_gp_snap = 0;
-        auto no_preply = [&](uint64_t p) {
-            for (uint64_t f = ht.f_off[p]; f < ht.f_off[p + 1]; ++f)
-                if ((ht.frags[f].flags >> 4) == K_PREPLY) return false;
+        P.items.push_back(it);
+        return (uint32_t)P.items.size() - 1;
+    };
+    auto local_batch = [&](uint32_t gid) -> uint32_t {
+        auto it = gid_local.find(gid);
+        if (it != gid_local.end()) return it->second;
+        const uint32_t j = (uint32_t)P.b_msg.size();
+        gid_local.emplace(gid, j);
+        P.b_msg.push_back(NONE32); P.b_pstart.push_back(NONE32); P.b_gid.push_back(gid);
+        P.b_aid.push_back(wc->b_aid[gid]);
+        P.b_bal.push_back(wc->b_bal[gid]);
+        P.b_ent.push_back({0, 0});
+        P.b_item.push_back(NONE32);
+        P.reps.emplace_back();
+        auto be = wc->b_ents.find(gid);
+        if (be != wc->b_ents.end() && !be->second.empty()) {
+            const uint32_t cnt = (uint32_t)be->second.size();
+            const uint32_t item = add_item(j, 0, cnt, &be->second);
+            P.b_item[j] = item;
+            std::vector<uint64_t> iv(cnt);
+            for (uint32_t q = 0; q < cnt; ++q) iv[q] = be->second[q].first;
+            cut_runs(iv.data(), 0, cnt, sb, [&](uint64_t b, uint64_t e0, uint32_t c, uint8_t st, bool dense) {
+                Frag f{e0, j, (uint16_t)c, st, (uint8_t)((dense ? FR_DENSE : 0) | (K_BATCH << 4))};
+                if (!dense) P.any_sparse = true;
+                P.cfr.push_back({b, f});
+                P.cfr_item.push_back(item);
+            });
+        }
+        return j;
+    };
+    uint32_t pstart = NONE32;
+    bool last_virtual = false;
+    for (size_t k = 0; k < ns.type.size(); ++k) {
+        const uint32_t g = (uint32_t)P.m_type.size();
+        const uint8_t t = ns.type[k];
+        if (t == MPX_MSG_P_PROPOSE) { P.prop_seq.push_back((uint32_t)k); continue; }
+        if (member && t == MPX_MSG_E_EPOCH && ns.ver[k] >= num_epochs) { P.rc = MPX_E_DECODE; return; }
+        bool drop = ns.part[k] != 0 || (t == MPX_MSG_COMMIT_REPLY && sb != 0);
+        int64_t vote_j = -1;
+        if (t == MPX_MSG_P_START) {
+            if (wc)
+                for (auto &x : live) if (x.second < gid0) P.ents_gone.push_back(x.second);
+            live.clear();
+            cur_bal = ns.ballot[k];
+        } else if (t == MPX_MSG_P_BATCH) {
+            if (drop) live.erase(ns.aux[k]);
+            else live[ns.aux[k]] = wc ? (uint32_t)(gid0 + P.new_batches) : (uint32_t)P.b_msg.size();
+        } else if (t == MPX_MSG_ACCEPT_REPLY) {
+            auto it = live.find(ns.aux[k]);
+            if (it == live.end()) drop = true;
+            else vote_j = wc ? local_batch(it->second) : it->second;
+        }
+        if (drop) {
+            ++P.dropped;
+            if (ns.part[k] != 0) ++P.part_dropped;
+            if (t == MPX_MSG_ACCEPT && member) {
+                P.sc_type.push_back(SC_SONLY | SC_VIRT); P.sc_key.push_back(ns.ballot[k]);
+                P.sc_idx.push_back(g); P.sc_ver.push_back(ns.ver[k]);
+                last_virtual = false;
+            } else if (t == MPX_MSG_ACCEPT) {
+                if (last_virtual) P.sc_key.back() = std::max(P.sc_key.back(), ns.ballot[k]);
+                else { P.sc_type.push_back(SC_SONLY); P.sc_key.push_back(ns.ballot[k]); P.sc_idx.push_back(NONE32); }
+                last_virtual = true;
+            }
+            continue;
+        }
+        if (member) {
+            P.m_ver.push_back(ns.ver[k]);
+            if (t == MPX_MSG_E_EPOCH) P.ee_msg.push_back(g);
+        }
+        P.m_seq.push_back((uint32_t)k);
+        if (vote_j >= 0) P.reps[vote_j].push_back(g);
+        uint64_t ent = ns.ent[k];                    // node-local g_a / r / e index
+        uint32_t item = NONE32;
+        if (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_P_BATCH) item = add_item(NONE32, ent, ns.cnt[k], nullptr);
+        P.m_type.push_back(t);
+        P.m_src.push_back(ns.src[k]);
+        P.m_ballot.push_back(ns.ballot[k]);
+        P.m_aux.push_back(ns.aux[k]);
+        P.m_ent.push_back(item != NONE32 ? item : ent);
+        P.m_cnt.push_back(ns.cnt[k]);
+        {   // header-scan stream and static flags (as build_trace_serial)
+            const bool badsrc = ns.src[k] >= N;
+            uint8_t f0 = 0;
+            int sct = -1;
+            uint64_t key = ns.ballot[k];
+            if (member) {
+                if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
+                    sct = t == MPX_MSG_PREPARE ? SC_PREP : SC_ACC;
+                    if (badsrc) sct |= SC_BAD;
+                } else if (t == MPX_MSG_E_EPOCH) {
+                    sct = SC_PS;
+                    key = 0;
+                } else if (t == MPX_MSG_COMMIT && badsrc) {
+                    f0 = F_BADNODE; sct = SC_NONE | SC_BAD;
+                }
+            } else if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
+                sct = t == MPX_MSG_PREPARE ? SC_PREP : SC_ACC;
+                if (badsrc) { f0 |= F_BADNODE; sct |= SC_BAD; }
+            } else if (t == MPX_MSG_REJECT) {
+                sct = SC_SONLY;
+            } else if (t == MPX_MSG_COMMIT && badsrc) {
+                f0 = F_BADNODE; sct = SC_NONE | SC_BAD;
+            }
+            P.m_flags0.push_back(f0);
+            if (sct >= 0) {
+                P.sc_type.push_back((uint8_t)sct); P.sc_key.push_back(key); P.sc_idx.push_back(g);
+                if (member) P.sc_ver.push_back(ns.ver[k]);
+                last_virtual = false;
+            }
+        }
+        if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_E_EPOCH) P.pl.push_back(g);
+        if (t == MPX_MSG_P_START) pstart = g;
+        if (t == MPX_MSG_P_BATCH) {
+            const uint32_t j = (uint32_t)P.b_msg.size();
+            if (wc) gid_local.emplace((uint32_t)(gid0 + P.new_batches), j);
+            P.b_gid.push_back((uint32_t)(gid0 + P.new_batches));
+            ++P.new_batches;
+            P.b_bal.push_back(cur_bal);
+            P.b_ent.push_back({ent, ns.cnt[k]});
+            P.b_item.push_back(item);
+            P.b_msg.push_back(g);
+            P.b_aid.push_back(ns.aux[k]);
+            P.b_pstart.push_back(pstart);
+            P.reps.emplace_back();
+        }
+        if (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_PREPARE_REPLY) {
+            const uint8_t kind = t == MPX_MSG_ACCEPT ? K_ACCEPT : t == MPX_MSG_COMMIT ? K_COMMIT : K_PREPLY;
+            const uint64_t *iid = t == MPX_MSG_PREPARE_REPLY ? ns.r_iid.data() : ns.e_iid.data();
+            cut_runs(iid, ent, ns.cnt[k], sb, [&](uint64_t b, uint64_t e0, uint32_t c, uint8_t st, bool dense) {
+                Frag f{item != NONE32 ? e0 - ent : e0, g, (uint16_t)c, st, (uint8_t)((dense ? FR_DENSE : 0) | (kind << 4))};
+                if (!dense) P.any_sparse = true;
+                P.fr.push_back({b * N + n, f});
+                P.fr_item.push_back(item);
+                if (first_frag[b] == NONE32) {
+                    first_frag[b] = g; maxb = std::max<int64_t>(maxb, (int64_t)b);
+                    if (wc && !wc->state_b[n][b]) P.state_b.push_back(b);
+                }
+                if (kind == K_PREPLY && !in_round[b]) { in_round[b] = 1; round_b.push_back(b); }
+            });
+        }
+        auto add_ev = [&](uint64_t b) { P.evp.push_back({b * N + n, g}); P.evx.push_back(0); };
+        auto clear_round = [&]() { for (uint64_t b : round_b) in_round[b] = 0; round_b.clear(); };
+        if (t == MPX_MSG_PREPARE && maxb >= 0) {
+            uint64_t last_b = 0;
+            for (uint32_t r = 0; r < ns.cnt[k]; ++r) {
+                const uint64_t a = ns.g_a[ent + r], e = ns.g_b[ent + r];
+                if (e <= sb || a >= sb + slen) continue;
+                const uint64_t lo = (std::max(a, sb) - sb) >> BSH;
+                const uint64_t hi = std::min<uint64_t>((std::min(e, sb + slen) - sb + BS - 1) >> BSH, (uint64_t)maxb + 1);
+                for (uint64_t b = lo; b < hi; ++b) {
+                    if (first_frag[b] >= g && !(wc && wc->state_b[n][b])) continue;
+                    if (!P.evp.empty() && P.evp.back().second == g && b == last_b && P.evp.back().first == b * N + n) {
+                        P.evx.back() = (P.evx.back() + (1ull << 32)) & ~EVX_ONE;
+                    } else if (P.evp.empty() || P.evp.back().second != g || b > last_b) {
+                        add_ev(b);
+                        const uint64_t blo = sb + (b << BSH);
+                        const uint64_t il = std::max(a, blo) - blo, ih = std::min(e, blo + BS) - blo;
+                        P.evx.back() = (ent + r) | (1ull << 32) | (il << 40) | (ih << 49) | EVX_ONE;   // (g_a index: rebased)
+                        last_b = b;
+                    }
+                }
+            }
+        } else if (t == MPX_MSG_PREPARE_REPLY) {
+            for (uint64_t b : round_b) add_ev(b);
+        } else if (t == MPX_MSG_P_START) {
+            for (uint64_t b : round_b) add_ev(b);
+            clear_round();
+        } else if (t == MPX_MSG_E_EPOCH) {
+            for (uint64_t b = 0; (int64_t)b <= maxb; ++b)
+                if (first_frag[b] < g || (wc && wc->state_b[n][b])) add_ev(b);
+        }
+        if (t == MPX_MSG_P_BATCH) {
+            const uint32_t j = (uint32_t)P.b_msg.size() - 1;
+            cut_runs(ns.e_iid.data(), ent, ns.cnt[k], sb, [&](uint64_t b, uint64_t e0, uint32_t c, uint8_t st, bool dense) {
+                Frag f{e0 - ent, j, (uint16_t)c, st, (uint8_t)((dense ? FR_DENSE : 0) | (K_BATCH << 4))};
+                if (!dense) P.any_sparse = true;
+                P.cfr.push_back({b, f});
+                P.cfr_item.push_back(item);
+            });
+        }
+    }
+    if (wc) {
+        NodeCarry &c = P.carry;
+        for (auto &x : live)                         // new batches still open: keep their entries
+            if (x.second >= gid0) {
+                const auto &be = P.b_ent[gid_local[x.second]];
+                std::vector<std::pair<uint64_t, uint64_t>> dst(be.second);
+                for (uint32_t q = 0; q < be.second; ++q) dst[q] = {ns.e_iid[be.first + q], ns.e_val[be.first + q]};
+                P.ents_new.push_back({x.second, std::move(dst)});
+            }
+        c.live = std::move(live);
+        c.round_b = round_b;
+        c.maxb = maxb;
+        c.ballot = cur_bal;
+        if (member) c.markers = wc->markers[n] + (uint32_t)P.ee_msg.size();
+    }
+}
+}  // namespace
+
+int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen,
+                const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc, uint32_t threads)
+{
+    const bool member = !epochs.empty();
+    if (wc && !wc->on) return MPX_E_STATE;
+    if (!threads) threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    ht = HostTrace();
+    const uint32_t N = (uint32_t)nodes.size();
+    ht.N = N;
+    ht.shard_begin = sb;
+    ht.shard_len = slen;
+    ht.NB = (uint32_t)((slen + BS - 1) >> BSH);
+    const uint64_t NB = ht.NB;
+    uint64_t G = 0, E = 0;
+    for (auto &ns : nodes) { G += ns.type.size(); E += ns.e_iid.size(); }
+    if (G >= NONE32 || E > MAX_ENTRIES) return MPX_E_RANGE;     // chosen log (mpx_internal.hpp)
+    auto parallel = [&](uint32_t count, const auto &fn) {      // fn(k) for k < count on up to `threads` threads
+        std::atomic<uint32_t> next{0};
+        auto work = [&]() { for (uint32_t k; (k = next.fetch_add(1)) < count;) fn(k); };
+        std::vector<std::thread> th;
+        for (uint32_t t = 1; t < std::min(threads, count); ++t) th.emplace_back(work);
+        work();
+        for (auto &x : th) x.join();
+    };
+    // phase A
+    std::vector<NodePart> parts(N);
+    parallel(N, [&](uint32_t n) { walk_node(nodes[n], n, N, sb, slen, NB, member, epochs.size(), wc, parts[n]); });
+    for (uint32_t n = 0; n < N; ++n) TRY_RC(parts[n].rc);
+    // phase B: the entry pool (EntryPool's content addressing, first occurrence in walk order)
+    {
+        const uint32_t S = std::max(1u, threads);
+        auto same = [&](const PoolItem &a, const PoolItem &b) {
+            if (a.cnt != b.cnt) return false;
+            if (!a.carried && !b.carried) {                    // (the common case: two messages' lists)
+                const NodeStream &x = nodes[a.node], &y = nodes[b.node];
+                const size_t bytes = 8ull * a.cnt;
+                if (std::memcmp(x.e_iid.data() + a.first, y.e_iid.data() + b.first, bytes) ||
+                    std::memcmp(x.e_val.data() + a.first, y.e_val.data() + b.first, bytes))
+                    return false;
+                if (!member) return true;
+                for (uint32_t q = 0; q < a.cnt; ++q)
+                    if ((x.e_pid.empty() ? 0 : x.e_pid[a.first + q]) != (y.e_pid.empty() ? 0 : y.e_pid[b.first + q])) return false;
+                return true;
+            }
+            for (uint32_t q = 0; q < a.cnt; ++q) {
+                const uint64_t ai = a.carried ? (*a.carried)[q].first : nodes[a.node].e_iid[a.first + q];
+                const uint64_t bi = b.carried ? (*b.carried)[q].first : nodes[b.node].e_iid[b.first + q];
+                const uint64_t av = a.carried ? (*a.carried)[q].second : nodes[a.node].e_val[a.first + q];
+                const uint64_t bv = b.carried ? (*b.carried)[q].second : nodes[b.node].e_val[b.first + q];
+                if (ai != bi || av != bv) return false;
+                if (member) {
+                    const auto &pa = nodes[a.node].e_pid, &pb = nodes[b.node].e_pid;
+                    const uint64_t ap = a.carried || pa.empty() ? 0 : pa[a.first + q];
+                    const uint64_t bp = b.carried || pb.empty() ? 0 : pb[b.first + q];
+                    if (ap != bp) return false;
+                }
+            }
             return true;
         };
-        auto mid = std::stable_partition(ht.gp_list.begin(), ht.gp_list.end(), no_preply);
-        ht.num_gp_snap = (uint64_t)(mid - ht.gp_list.begin());
-        auto mid2 = std::stable_partition(ht.gp_list.begin(), mid, [&](uint64_t p) { return !ht.pair_ev[p]; });
-        ht.num_gp_simple = (uint64_t)(mid2 - ht.gp_list.begin());
-        // k_plan_list takes the pairs before `mid` (or lists them for k_apply itself);
-        // the promise-round pairs stay on the host range of the full kernel
-        for (auto it = mid; it != ht.gp_list.end(); ++it) ht.pair_gp[*it] = GP_ROUNDS;
-    }
-    // slots for sparse fragments
-    if (ht.any_sparse) {
-        ht.e_slot.resize(ht.e_iid.size());
-        for (size_t k = 0; k < ht.e_iid.size(); ++k) ht.e_slot[k] = (uint8_t)((ht.e_iid[k] - sb) & (BS - 1));
-        ht.r_slot.resize(ht.r_iid.size());
-        for (size_t k = 0; k < ht.r_iid.size(); ++k) ht.r_slot[k] = (uint8_t)((ht.r_iid[k] - sb) & (BS - 1));
-    }
-    // proposer lists
-    ht.pl_off.assign(N + 1, 0);
-    for (uint32_t n = 0; n < N; ++n) ht.pl_off[n + 1] = ht.pl_off[n] + pl_cnt[n];
-    ht.pl_msg = std::move(pl);
-    // header-scan chunks, over each node's scan stream
-    ht.node_chunk_off.assign(N + 1, 0);
-    ht.scan_chunk = scan_chunk_for(sc_off[N]);
-    for (uint32_t n = 0; n < N; ++n) {
-        ht.node_chunk_off[n] = (uint32_t)ht.chunk_node.size();
-        for (uint64_t g = sc_off[n]; g < sc_off[n + 1]; g += ht.scan_chunk) {
-            ht.chunk_node.push_back(n);
-            ht.chunk_beg.push_back(g);
-            ht.chunk_end.push_back(std::min<uint64_t>(g + ht.scan_chunk, sc_off[n + 1]));
-        }
-    }
-    ht.node_chunk_off[N] = (uint32_t)ht.chunk_node.size();
-    if (wc) {
-        // every check passed: the window is consumed, the carry moves past it
-        for (uint32_t n = 0; n < N; ++n) {
-            NodeCarry &c = next[n];
-            wc->live[n] = std::move(c.live);
-            wc->round_b[n] = std::move(c.round_b);
-            wc->maxb[n] = c.maxb;
-            wc->round_ballot[n] = c.ballot;
-            wc->markers[n] = c.markers;
-        }
-        for (uint32_t gid : ents_gone) wc->b_ents.erase(gid);
-        for (auto &x : ents_new) wc->b_ents[x.first] = std::move(x.second);
-        for (size_t j = 0; j < ht.b_msg.size(); ++j)
-            if (ht.b_msg[j] != NONE32) {                    // new batches, in id order
-                wc->b_bal.push_back(b_bal_w[j]);
-                wc->b_aid.push_back(ht.b_aid[j]);
+        // per item: the (node, index) of its list's first occurrence (itself when first)
+        std::vector<std::vector<uint64_t>> first_of(N);
+        for (uint32_t n = 0; n < N; ++n) first_of[n].assign(parts[n].items.size(), 0);
+        parallel(S, [&](uint32_t s) {
+            std::unordered_multimap<uint64_t, uint64_t> seen;      // hash -> (node << 32 | index)
+            for (uint32_t n = 0; n < N; ++n)
+                for (size_t i = 0; i < parts[n].items.size(); ++i) {
+                    const PoolItem &it = parts[n].items[i];
+                    if (mix64(it.hash ^ 0x2545F4914F6CDD1Dull) % S != s) continue;
+                    uint64_t f = ((uint64_t)n << 32) | i;
+                    auto r = seen.equal_range(it.hash);
+                    for (auto x = r.first; x != r.second; ++x)
+                        if (same(parts[x->second >> 32].items[(uint32_t)x->second], it)) { f = x->second; break; }
+                    if (f == (((uint64_t)n << 32) | i)) seen.emplace(it.hash, f);
+                    first_of[n][i] = f;
+                }
+        });
+        uint64_t off = 0;                                   // offsets in walk order
+        for (uint32_t n = 0; n < N; ++n)
+            for (size_t i = 0; i < parts[n].items.size(); ++i) {
+                PoolItem &it = parts[n].items[i];
+                const uint64_t f = first_of[n][i];
+                it.is_first = f == (((uint64_t)n << 32) | i);
+                if (it.is_first) { it.off = off; off += it.cnt; }
+                else it.off = parts[f >> 32].items[(uint32_t)f].off;
             }
-        wc->batches = gid_next;
-        for (auto &x : state_new) wc->state_b[x.first][x.second] = 1;
+        E = off;
     }
-    return MPX_OK;
+    // phase C: offsets of every node's part, then the parts rebased into the trace
+    std::vector<uint64_t> g_off(N + 1, 0), j_off(N + 1, 0), new_off(N + 1, 0), r_off(N + 1, 0), ga_off(N + 1, 0),
+        sc_o(N + 1, 0), ee_o(N + 1, 0), pl_o(N + 1, 0), pr_o(N + 1, 0), fr_o(N + 1, 0), cfr_o(N + 1, 0), ev_o(N + 1, 0),
+        rep_o(N + 1, 0);
+    for (uint32_t n = 0; n < N; ++n) {
+        const NodePart &P = parts[n];
+        g_off[n + 1] = g_off[n] + P.m_type.size();
+        j_off[n + 1] = j_off[n] + P.b_msg.size();
+        new_off[n + 1] = new_off[n] + P.new_batches;
+        r_off[n + 1] = r_off[n] + nodes[n].r_iid.size();
+        ga_off[n + 1] = ga_off[n] + nodes[n].g_a.size();
+        sc_o[n + 1] = sc_o[n] + P.sc_type.size();
+        ee_o[n + 1] = ee_o[n] + P.ee_msg.size();
+        pl_o[n + 1] = pl_o[n] + P.pl.size();
+        pr_o[n + 1] = pr_o[n] + P.prop_seq.size();
+        fr_o[n + 1] = fr_o[n] + P.fr.size();
+        cfr_o[n + 1] = cfr_o[n] + P.cfr.size();
+        ev_o[n + 1] = ev_o[n] + P.evp.size();
+        ht.dropped += P.dropped;
+        ht.part_dropped += P.part_dropped;
+        ht.any_sparse = ht.any_sparse || P.any_sparse;
+    }
+    const uint64_t GK = g_off[N], JB = j_off[N];
+    ht.m_type.resize(GK); ht.m_src.resize(GK); ht.m_cnt.resize(GK); ht.m_node.resize(GK);
+    ht.m_ballot.resize(GK); ht.m_aux.resize(GK); ht.m_ent.resize(GK); ht.m_seq.resize(GK); ht.m_flags0.resize(GK);
+    if (member) { ht.m_ver.resize(GK); ht.ee_msg.resize(ee_o[N]); ht.sc_ver.resize(sc_o[N]); ht.ee_off.assign(N + 1, 0); }
+    ht.sc_type.resize(sc_o[N]); ht.sc_key.resize(sc_o[N]); ht.sc_idx.resize(sc_o[N]);
+    ht.prop_seq.resize(pr_o[N]); ht.prop_off.assign(N + 1, 0);
+    ht.e_iid.resize(E); ht.e_val.resize(E);
+    if (member) ht.e_pid.resize(E);
+    ht.r_pid.resize(r_off[N]); ht.r_val.resize(r_off[N]); ht.r_iid.resize(r_off[N]);
+    ht.g_a.resize(ga_off[N]); ht.g_b.resize(ga_off[N]);
+    ht.node_off.assign(N + 1, 0);
+    ht.b_msg.resize(JB); ht.b_pstart.resize(JB); ht.b_aid.resize(JB);
+    if (wc) { ht.b_gid.resize(JB); ht.b_node.resize(JB); }
+    Walk W;
+    W.fcount.assign(N * NB + 1, 0); W.cfcount.assign(NB + 1, 0); W.pl_cnt.assign(N, 0);
+    W.fr.resize(fr_o[N]); W.cfr.resize(cfr_o[N]); W.pl.resize(pl_o[N]);
+    W.evp.resize(ev_o[N]); W.evx.resize(ev_o[N]);
+    W.sc_off.assign(N + 1, 0);
+    W.reps.resize(JB);
+    W.b_bal_w.resize(JB);
+    W.next.resize(wc ? N : 0);
+    const uint64_t gid0 = wc ? wc->batches : 0;
+    W.gid_next = gid0 + new_off[N];
+    for (uint32_t n = 0; n <= N; ++n) {
+        ht.node_off[n] = g_off[n]; W.sc_off[n] = sc_o[n]; ht.prop_off[n] = pr_o[n];
+        if (member) ht.ee_off[n] = ee_o[n];
+    }
+    {   // the pool's lists, copied from their first occurrences (mostly the first node's: split evenly)
+        std::vector<const PoolItem *> firsts;
+        for (uint32_t n = 0; n < N; ++n)
+            for (const PoolItem &it : parts[n].items) if (it.is_first) firsts.push_back(&it);
+        const uint32_t C = std::max<uint32_t>(1, std::min<uint32_t>(4 * threads, (uint32_t)firsts.size()));
+        parallel(C, [&](uint32_t c) {
+            for (size_t i = firsts.size() * c / C; i < firsts.size() * (c + 1) / C; ++i) {
+                const PoolItem &it = *firsts[i];
+                const NodeStream &ns = nodes[it.node];
+                if (it.carried) {
+                    for (uint32_t q = 0; q < it.cnt; ++q) {
+                        ht.e_iid[it.off + q] = (*it.carried)[q].first;
+                        ht.e_val[it.off + q] = (*it.carried)[q].second;
+                        if (member) ht.e_pid[it.off + q] = 0;
+                    }
+                    continue;
+                }
+                std::memcpy(ht.e_iid.data() + it.off, ns.e_iid.data() + it.first, 8ull * it.cnt);
+                std::memcpy(ht.e_val.data() + it.off, ns.e_val.data() + it.first, 8ull * it.cnt);
+                if (member) {
+                    if (ns.e_pid.empty()) std::fill(ht.e_pid.begin() + it.off, ht.e_pid.begin() + it.off + it.cnt, 0);
+                    else std::memcpy(ht.e_pid.data() + it.off, ns.e_pid.data() + it.first, 8ull * it.cnt);
+                }
+            }
+        });
+    }
+    parallel(N, [&](uint32_t n) {
+        const NodePart &P = parts[n];
+        const NodeStream &ns = nodes[n];
+        const uint64_t go = g_off[n], jo = j_off[n], ro = r_off[n], gao = ga_off[n];
+        std::copy(ns.r_pid.begin(), ns.r_pid.end(), ht.r_pid.begin() + ro);
+        std::copy(ns.r_val.begin(), ns.r_val.end(), ht.r_val.begin() + ro);
+        std::copy(ns.r_iid.begin(), ns.r_iid.end(), ht.r_iid.begin() + ro);
+        std::copy(ns.g_a.begin(), ns.g_a.end(), ht.g_a.begin() + gao);
+        std::copy(ns.g_b.begin(), ns.g_b.end(), ht.g_b.begin() + gao);
+        for (size_t g = 0; g < P.m_type.size(); ++g) {
+            const uint64_t G2 = go + g;
+            const uint8_t t = P.m_type[g];
+            ht.m_type[G2] = t; ht.m_src[G2] = P.m_src[g]; ht.m_cnt[G2] = P.m_cnt[g]; ht.m_node[G2] = n;
+            ht.m_ballot[G2] = P.m_ballot[g]; ht.m_aux[G2] = P.m_aux[g]; ht.m_seq[G2] = P.m_seq[g];
+            ht.m_flags0[G2] = P.m_flags0[g];
+            if (member) ht.m_ver[G2] = P.m_ver[g];
+            const uint64_t e = P.m_ent[g];
+            ht.m_ent[G2] = t == MPX_MSG_PREPARE ? e + gao : t == MPX_MSG_PREPARE_REPLY ? e + ro :
+                           (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_P_BATCH) ? P.items[e].off : e;
+        }
+        for (size_t i = 0; i < P.sc_type.size(); ++i) {
+            ht.sc_type[sc_o[n] + i] = P.sc_type[i]; ht.sc_key[sc_o[n] + i] = P.sc_key[i];
+            ht.sc_idx[sc_o[n] + i] = P.sc_idx[i] == NONE32 ? 0 : (uint32_t)(go + P.sc_idx[i]);
+            if (member) ht.sc_ver[sc_o[n] + i] = P.sc_ver[i];
+        }
+        for (size_t i = 0; i < P.ee_msg.size(); ++i) ht.ee_msg[ee_o[n] + i] = (uint32_t)(go + P.ee_msg[i]);
+        for (size_t i = 0; i < P.pl.size(); ++i) W.pl[pl_o[n] + i] = (uint32_t)(go + P.pl[i]);
+        W.pl_cnt[n] = P.pl.size();
+        std::copy(P.prop_seq.begin(), P.prop_seq.end(), ht.prop_seq.begin() + pr_o[n]);
+        for (size_t j = 0; j < P.b_msg.size(); ++j) {
+            const uint64_t J = jo + j;
+            ht.b_msg[J] = P.b_msg[j] == NONE32 ? NONE32 : (uint32_t)(go + P.b_msg[j]);
+            ht.b_pstart[J] = P.b_pstart[j] == NONE32 ? NONE32 : (uint32_t)(go + P.b_pstart[j]);
+            ht.b_aid[J] = P.b_aid[j];
+            const uint32_t gid = P.b_gid[j] >= gid0 ? (uint32_t)(P.b_gid[j] + new_off[n]) : P.b_gid[j];
+            if (wc) { ht.b_gid[J] = gid; ht.b_node[J] = n; }
+            W.b_bal_w[J] = P.b_bal[j];
+            auto &rp = W.reps[J];
+            rp.resize(P.reps[j].size());
+            for (size_t q = 0; q < rp.size(); ++q) rp[q] = (uint32_t)(go + P.reps[j][q]);
+        }
+        for (size_t i = 0; i < P.fr.size(); ++i) {
+            FragKey x = P.fr[i];
+            x.f.msg = (uint32_t)(go + x.f.msg);
+            x.f.entry = P.fr_item[i] == NONE32 ? x.f.entry + ro : P.items[P.fr_item[i]].off + x.f.entry;
+            W.fr[fr_o[n] + i] = x;
+        }
+        for (size_t i = 0; i < P.cfr.size(); ++i) {
+            FragKey x = P.cfr[i];
+            x.f.msg = (uint32_t)(jo + x.f.msg);
+            x.f.entry = P.items[P.cfr_item[i]].off + x.f.entry;
+            W.cfr[cfr_o[n] + i] = x;
+        }
+        for (size_t i = 0; i < P.evp.size(); ++i) {
+            const uint32_t g = P.evp[i].second;
+            W.evp[ev_o[n] + i] = {P.evp[i].first, (uint32_t)(go + g)};
+            W.evx[ev_o[n] + i] = P.m_type[g] == MPX_MSG_PREPARE ? P.evx[i] + gao : P.evx[i];
+        }
+    });
+    // (counts and the window's carry: serial, small)
+    for (const FragKey &x : W.fr) W.fcount[x.key]++;
+    for (const FragKey &x : W.cfr) W.cfcount[x.key]++;
+    if (wc)
+        for (uint32_t n = 0; n < N; ++n) {
+            NodePart &P = parts[n];
+            for (uint64_t b : P.state_b) W.state_new.push_back({n, b});
+            NodeCarry &c = W.next[n];
+            c = std::move(P.carry);
+            for (auto &x : c.live) if (x.second >= gid0) x.second = (uint32_t)(x.second + new_off[n]);
+            W.ents_gone.insert(W.ents_gone.end(), P.ents_gone.begin(), P.ents_gone.end());
+            for (auto &x : P.ents_new) W.ents_new[(uint32_t)(x.first + new_off[n])] = std::move(x.second);
+        }
+    return finish_trace(ht, W, N, NB, sb, slen, member, wc);
 }
 
 int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<NodeStream> &parts,

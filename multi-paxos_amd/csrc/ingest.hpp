@@ -266,7 +266,11 @@ int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<
 // non-empty selects member semantics (role / version gates, E_EPOCH events).
 // With `wc` (incremental runs): `nodes` hold one window's records; the window is built on
 // the carried state and, only when the build succeeds, the carry is advanced past it.
+// The walk over the nodes' records runs a thread per node (`threads`: at most that many; 0: up
+// to 16) and the result is build_trace_serial's, field for field (tests/build_check.cpp).
 int build_trace(const std::vector<NodeStream> &nodes, uint64_t shard_begin, uint64_t shard_len,
-                const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc = nullptr);
+                const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc = nullptr, uint32_t threads = 0);
+int build_trace_serial(const std::vector<NodeStream> &nodes, uint64_t shard_begin, uint64_t shard_len,
+                       const std::vector<mpx_epoch> &epochs, HostTrace &ht, WindowCarry *wc = nullptr);
 
 }  // namespace mpx

@@ -116,3 +116,36 @@ def test_parallel_decode_violations_in_record_order(par_checker, tmp_path):
     r = subprocess.run([par_checker, str(p), "0", "0", "256", "4"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and r.stdout.startswith("ok "), r.stdout + r.stderr
     assert int(r.stdout.split()[3]) == 4
+
+
+# ---- node-parallel build (ingest.cpp build_trace vs build_trace_serial) ----
+@pytest.fixture(scope="module")
+def build_checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("bchk") / "build_check")
+    src = [os.path.join(ROOT, "tests", "build_check.cpp")] + \
+          [os.path.join(CSRC, f) for f in ("ingest.cpp", "gen.cpp", "gen_faulty.cpp", "gen_member.cpp")]
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I" + CSRC, "-I" + os.path.join(ROOT, "include")] + src +
+                   ["-o", exe], check=True, timeout=600)
+    return exe
+
+
+@pytest.mark.parametrize("kind,lg,proposers,windows,threads,shard", [
+    ("faulty", 15, 3, 1, 4, 0), ("faulty", 15, 3, 6, 8, 0), ("faulty", 14, 2, 3, 3, 1), ("faulty", 14, 0, 2, 2, 0),
+    ("member", 14, 3, 1, 4, 0), ("member", 14, 3, 5, 6, 1), ("member", 13, 0, 3, 3, 0)])
+def test_parallel_build_equals_serial_generated(build_checker, kind, lg, proposers, windows, threads, shard):
+    """build_trace's node-parallel walk (per-node parts rebased, the entry pool's first occurrences
+    found per hash shard) gives build_trace_serial's HostTrace field for field — whole, window by
+    window with the carry, and on a shard of the instances."""
+    r = subprocess.run([build_checker, kind, str(lg), str(proposers), str(windows), str(threads), str(shard)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("ok "), r.stdout + r.stderr
+
+
+def test_parallel_build_equals_serial_goldens(build_checker):
+    for f in sorted(os.listdir(GOLD)):
+        if not f.endswith(".mpxt"):
+            continue
+        for args in (("0", "0", "1", "3", "0"), ("0", "0", "3", "3", "0"), ("0", "0", "2", "2", "1")):
+            r = subprocess.run([build_checker, os.path.join(GOLD, f)] + list(args), capture_output=True, text=True,
+                               timeout=120)
+            assert r.returncode == 0 and r.stdout.startswith("ok"), f + " %r: " % (args,) + r.stdout + r.stderr
