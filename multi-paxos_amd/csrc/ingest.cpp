@@ -114,12 +114,12 @@ void ValueTable::prefetch_slot(uint64_t h) const
     if (s) __builtin_prefetch(s + slot_of(h >> GSH, x.smask.load(std::memory_order_relaxed)));
 }
 
-int ValueTable::intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_off, uint32_t exec_len)
+// one Value into its (locked) shard
+static int intern_locked(ValueTable::Shard &x, uint64_t h, const char *b, uint32_t len, uint32_t exec_off, uint32_t exec_len)
 {
-    Shard &x = sh[shard_of(h)];
-    std::lock_guard<std::mutex> g(x.mu);
+    constexpr size_t BLOCK = ValueTable::BLOCK;
     bool fresh = false;
-    Rec *r = x.insert(h, fresh);
+    ValueTable::Rec *r = x.insert(h, fresh);
     if (!fresh) return r->len != len || std::memcmp(r->p, b, len) != 0 ? MPX_E_VALUE : MPX_OK;
     char *dst;
     if (len > BLOCK / 4) {                                   // (a long value: a block of its own)
@@ -136,6 +136,25 @@ int ValueTable::intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_of
     return MPX_OK;
 }
 
+int ValueTable::intern_batch(const Pending *v, size_t n)
+{
+    for (size_t i = 0; i < n;) {
+        const uint32_t s = shard_of(v[i].h);
+        Shard &x = sh[s];
+        std::lock_guard<std::mutex> g(x.mu);
+        for (; i < n && shard_of(v[i].h) == s; ++i)
+            if (int rc = intern_locked(x, v[i].h, v[i].b, v[i].len, v[i].exec_off, v[i].exec_len)) return rc;
+    }
+    return MPX_OK;
+}
+
+int ValueTable::intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_off, uint32_t exec_len)
+{
+    Shard &x = sh[shard_of(h)];
+    std::lock_guard<std::mutex> g(x.mu);
+    return intern_locked(x, h, b, len, exec_off, exec_len);
+}
+
 // the key of a section: its length and sampled bytes (the candidates are compared in full)
 static uint64_t section_key(const uint8_t *b, size_t len, bool with_pid)
 {
@@ -147,18 +166,41 @@ static uint64_t section_key(const uint8_t *b, size_t len, bool with_pid)
     return h;
 }
 
-bool SectionCache::claim(const uint8_t *b, size_t len, bool with_pid)
+SectionCache::Result *SectionCache::claim(const uint8_t *b, size_t len, bool with_pid, bool &own)
 {
     const uint64_t key = section_key(b, len, with_pid);
     Shard &x = sh[(key * 0x9E3779B97F4A7C15ull) >> 58];
-    std::lock_guard<std::mutex> g(x.mu);
-    auto r = x.m.equal_range(key);
-    for (auto it = r.first; it != r.second; ++it) {
-        const Ent &c = it->second;
-        if (c.len == len && c.with_pid == with_pid && (c.b == b || std::memcmp(c.b, b, len) == 0)) return false;
+    // candidates under the lock, the full compares outside it (Results are never removed while
+    // the cache lives; two threads that both miss a new section both decode it — equal results)
+    Result *cand[8];
+    uint32_t nc = 0;
+    bool more = false;
+    {
+        std::lock_guard<std::mutex> g(x.mu);
+        auto r = x.m.equal_range(key);
+        for (auto it = r.first; it != r.second; ++it) {
+            if (nc == 8) { more = true; break; }
+            cand[nc++] = it->second.get();
+        }
     }
-    x.m.emplace(key, Ent{b, len, with_pid});
-    return true;
+    auto match = [&](const Result *c) {
+        return c->len == len && c->with_pid == with_pid && (c->b == b || std::memcmp(c->b, b, len) == 0);
+    };
+    for (uint32_t k = 0; k < nc; ++k)
+        if (match(cand[k])) { own = false; return cand[k]; }
+    std::lock_guard<std::mutex> g(x.mu);
+    if (more) {                                           // (a crowded key: compare the rest under the lock)
+        auto r = x.m.equal_range(key);
+        for (auto it = r.first; it != r.second; ++it)
+            if (match(it->second.get())) { own = false; return it->second.get(); }
+    }
+    std::unique_ptr<Result> res(new Result());
+    res->b = b; res->len = len; res->with_pid = with_pid;
+    res->id = id_base + next_id.fetch_add(1, std::memory_order_relaxed);
+    Result *out = res.get();
+    x.m.emplace(key, std::move(res));
+    own = true;
+    return out;
 }
 
 // One Value's handle, length and kind off the wire without the table (a section another thread
@@ -381,13 +423,44 @@ static bool sort_entries(std::vector<uint64_t> &iid, std::vector<uint64_t> &pid,
 
 // entries {u64 iid, [u64 pid,] Value}* of an ACCEPT / COMMIT / P_BATCH /
 // PREPARE_REPLY body, sorted by iid (the reference's std::map order)
-static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool with_pid,
-                          std::vector<uint64_t> &iid, std::vector<uint64_t> &pid,
-                          std::vector<uint64_t> &val, size_t &n_all, bool &dup,
-                          std::vector<std::pair<uint64_t, const uint8_t *>> *memh = nullptr, SectionCache *sc = nullptr)
+// One Value off the wire for the batched intern: its handle, length, executed span and whether
+// its canonical bytes are the wire bytes themselves (every bool 0 / 1 and no membership change in
+// the multi codec); 0 when the caller must take ValueTable::parse instead, < 0 on a bad layout
+static long value_span(const uint8_t *p, size_t avail, bool member, ValueTable::Pending &v, bool &mem)
 {
-    // the first thread to meet these bytes interns their Values, the others skim them
-    const bool own = !sc || !len || sc->claim(b, len, with_pid);
+    if (avail < 13) return 0;
+    const uint32_t proposer = rd32(p);
+    const uint64_t value_id = rd64(p + 4);
+    if (proposer >= (1u << 14) || value_id >= (1ull << 47)) return 0;
+    mem = false;
+    v.h = MPX_HANDLE(proposer, p[12] != 0, value_id);
+    v.b = (const char *)p;
+    v.exec_off = v.exec_len = 0;
+    if (p[12] == 1) { v.len = 13; return 13; }
+    if (p[12] != 0 || avail < 18 || p[13] > 1) return 0;
+    const uint32_t n = rd32(p + 14);
+    if (!member) {
+        if (p[13] != 0 || avail - 18 < n) return 0;
+        v.len = 18 + n; v.exec_off = 18; v.exec_len = n;
+        return (long)v.len;
+    }
+    size_t used = 18;
+    if (p[13]) { if ((avail - used) / 8 < n) return 0; used += 8 * (size_t)n; v.exec_off = NONE32; mem = true; }
+    else { if (avail - used < n) return 0; v.exec_off = 18; v.exec_len = n; used += n; }
+    if (avail - used < 4) return 0;
+    const uint32_t cbl = rd32(p + used);
+    used += 4;
+    if (avail - used < cbl) return 0;
+    v.len = (uint32_t)(used + cbl);
+    return (long)v.len;
+}
+
+// entries {u64 iid, [u64 pid,] Value}* of one section appended and sorted; `own`: intern the
+// Values (else skim them off the wire)
+static int parse_section(ValueTable &vt, const uint8_t *b, size_t len, bool with_pid, bool own,
+                         std::vector<uint64_t> &iid, std::vector<uint64_t> &pid, std::vector<uint64_t> &val,
+                         size_t &n_all, bool &dup, std::vector<std::pair<uint64_t, const uint8_t *>> *memh)
+{
     size_t cur = 0;
     const size_t first = iid.size();
     n_all = 0;
@@ -405,6 +478,10 @@ static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool wit
             c += (size_t)u;
         }
     }
+    // own: Values whose canonical bytes are their wire bytes go to the table in batches (one lock
+    // per shard run, intern_batch); the rest one by one (ValueTable::parse)
+    ValueTable::Pending pend[64];
+    size_t np = 0;
     while (cur < len) {
         const size_t need = with_pid ? 16 : 8;
         if (len - cur < need) return MPX_E_DECODE;
@@ -413,7 +490,19 @@ static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool wit
         cur += need;
         uint64_t h;
         bool mem = false;
-        const long u = own ? vt.parse(b + cur, len - cur, &h, &mem) : skim(b + cur, len - cur, vt.member, &h, &mem);
+        long u;
+        if (own) {
+            u = value_span(b + cur, len - cur, vt.member, pend[np], mem);
+            if (u > 0) {
+                h = pend[np].h;
+                if (++np == 64) { TRY_RC(vt.intern_batch(pend, np)); np = 0; }
+            } else {
+                if (np) { TRY_RC(vt.intern_batch(pend, np)); np = 0; }   // (table order: as the wire)
+                u = vt.parse(b + cur, len - cur, &h, &mem);
+            }
+        } else {
+            u = skim(b + cur, len - cur, vt.member, &h, &mem);
+        }
         if (u < 0) return (int)u;
         if (mem && memh) memh->push_back({h, b + cur});   // (member membership Values: MPX_FLAG_LEARN_EPOCHS)
         cur += (size_t)u;
@@ -422,7 +511,45 @@ static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool wit
         val.push_back(h);
         ++n_all;
     }
+    if (np) TRY_RC(vt.intern_batch(pend, np));
     dup = sort_entries(iid, pid, val, first, with_pid);
+    return MPX_OK;
+}
+
+// decode a section for its first claimer: its Result (or its error) for every other one
+static void publish_section(ValueTable &vt, SectionCache &sc, SectionCache::Result *r)
+{
+    std::vector<std::pair<uint64_t, const uint8_t *>> mh;
+    r->rc = parse_section(vt, r->b, r->len, r->with_pid, true, r->iid, r->pid, r->val, r->n_all, r->dup,
+                          vt.member ? &mh : nullptr);
+    for (const auto &x : mh) r->memh.push_back({x.first, (uint32_t)(x.second - r->b)});
+    if (!r->rc && !sc.share) return;                  // (never marked ready: others skim)
+    r->ready.store(1, std::memory_order_release);
+}
+
+// entries {u64 iid, [u64 pid,] Value}* of an ACCEPT / COMMIT / P_BATCH / PREPARE_REPLY body,
+// sorted by iid (the reference's std::map order); with `sc`, from the section's Result when it is
+// ready, else decoded (and published by the first claimer)
+static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool with_pid,
+                          std::vector<uint64_t> &iid, std::vector<uint64_t> &pid,
+                          std::vector<uint64_t> &val, size_t &n_all, bool &dup,
+                          std::vector<std::pair<uint64_t, const uint8_t *>> *memh = nullptr, SectionCache *sc = nullptr,
+                          uint64_t *sec = nullptr)
+{
+    if (!sc || !len) return parse_section(vt, b, len, with_pid, true, iid, pid, val, n_all, dup, memh);
+    bool own = false;
+    SectionCache::Result *r = sc->claim(b, len, with_pid, own);
+    if (sec) *sec = r->id;
+    if (own) publish_section(vt, *sc, r);
+    if (!r->ready.load(std::memory_order_acquire))   // (claimed elsewhere, not decoded yet: skim)
+        return parse_section(vt, b, len, with_pid, false, iid, pid, val, n_all, dup, memh);
+    if (r->rc) return r->rc;
+    iid.insert(iid.end(), r->iid.begin(), r->iid.end());
+    if (with_pid) pid.insert(pid.end(), r->pid.begin(), r->pid.end());
+    val.insert(val.end(), r->val.begin(), r->val.end());
+    if (memh) for (const auto &x : r->memh) memh->push_back({x.first, b + x.second});
+    n_all = r->n_all;
+    dup = r->dup;
     return MPX_OK;
 }
 
@@ -463,7 +590,8 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
     uint32_t src = 0;
     uint64_t ballot = 0, aux = 0, ent = 0;
     uint32_t cnt = 0;
-    uint8_t part = 0;                             // entries, none in the shard: another rank's record
+    uint8_t part = 0;
+    uint64_t sec = 0;                             // (SectionCache) the value section's id                             // entries, none in the shard: another rank's record
     (void)N;
     auto keep_shard = [&](std::vector<uint64_t> &iid, std::vector<uint64_t> *pid, std::vector<uint64_t> &val,
                           size_t first) {
@@ -516,7 +644,7 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         if (20 + (size_t)vl > len) return MPX_E_DECODE;
         const size_t first = ns.r_iid.size();
         size_t n_all; bool dup;
-        int rc = decode_entries(vt, m + 20, vl, true, ns.r_iid, ns.r_pid, ns.r_val, n_all, dup, nullptr, sc);
+        int rc = decode_entries(vt, m + 20, vl, true, ns.r_iid, ns.r_pid, ns.r_val, n_all, dup);   // (unique per reply: no section cache)
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
@@ -536,7 +664,7 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         const size_t first = ns.e_iid.size();
         size_t n_all; bool dup;
         std::vector<uint64_t> nopid;
-        int rc = decode_entries(vt, m + 28, vl, false, ns.e_iid, nopid, ns.e_val, n_all, dup, nullptr, sc);
+        int rc = decode_entries(vt, m + 28, vl, false, ns.e_iid, nopid, ns.e_val, n_all, dup, nullptr, sc, &sec);
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
@@ -567,7 +695,7 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         const size_t first = ns.e_iid.size();
         size_t n_all; bool dup;
         std::vector<uint64_t> nopid;
-        int rc = decode_entries(vt, m + 16, vl, false, ns.e_iid, nopid, ns.e_val, n_all, dup, nullptr, sc);
+        int rc = decode_entries(vt, m + 16, vl, false, ns.e_iid, nopid, ns.e_val, n_all, dup, nullptr, sc, &sec);
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
@@ -579,6 +707,7 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
         return MPX_E_DECODE;                      // ASSERT(false), :1671-1672
     }
     ns.part.push_back(part);
+    ns.sec.push_back(sec);
     ns.type.push_back((uint8_t)t);
     ns.src.push_back(src);
     ns.ballot.push_back(ballot);
@@ -596,6 +725,7 @@ int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord
     uint64_t ent = 0;
     uint32_t cnt = 0;
     uint8_t part = 0;
+    uint64_t sec = 0;                             // (SectionCache) the value section's id
     auto values = [&]() -> int {
         for (uint64_t k = 0; k < r.n; ++k) TRY_RC(vt.plain(r.b[k]));
         return MPX_OK;
@@ -656,6 +786,7 @@ int append_record(ValueTable &vt, NodeStream &ns, uint32_t node, const SoaRecord
         return MPX_E_DECODE;
     }
     ns.part.push_back(part);
+    ns.sec.push_back(sec);
     ns.type.push_back((uint8_t)t);
     ns.src.push_back(r.src);
     ns.ballot.push_back(r.ballot);
@@ -675,6 +806,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
     uint64_t ballot = 0, aux = 0, ent = 0;
     uint32_t cnt = 0;
     uint8_t part = 0;
+    uint64_t sec = 0;                             // (SectionCache) the value section's id
     auto keep_shard = [&](size_t first) {
         size_t w = first;
         for (size_t k = first; k < ns.e_iid.size(); ++k)
@@ -721,7 +853,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
     auto entries = [&](const uint8_t *b, size_t l) -> int {
         const size_t first = ns.e_iid.size();
         size_t n_all; bool dup;
-        int rc = decode_entries(vt, b, l, true, ns.e_iid, ns.e_pid, ns.e_val, n_all, dup, el ? &memh : nullptr, sc);
+        int rc = decode_entries(vt, b, l, true, ns.e_iid, ns.e_pid, ns.e_val, n_all, dup, el ? &memh : nullptr, sc, &sec);
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         if (el && t == MPX_MSG_COMMIT) learn(first, ns.e_iid.size());
@@ -758,7 +890,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         if (20 + (size_t)vl > len) return MPX_E_DECODE;
         const size_t first = ns.r_iid.size();
         size_t n_all; bool dup;
-        int rc = decode_entries(vt, m + 20, vl, true, ns.r_iid, ns.r_pid, ns.r_val, n_all, dup, nullptr, sc);
+        int rc = decode_entries(vt, m + 20, vl, true, ns.r_iid, ns.r_pid, ns.r_val, n_all, dup);   // (unique per reply: no section cache)
         if (rc) return rc;
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
@@ -825,6 +957,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
     }
     if ((t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) && ballot > LOW56) return MPX_E_RANGE;   // see G_SEG
     ns.part.push_back(part);
+    ns.sec.push_back(sec);
     ns.type.push_back((uint8_t)t);
     ns.src.push_back(src);
     ns.ballot.push_back(ballot);
@@ -839,6 +972,7 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         el->steps.push_back(el->view);
         ns.part.push_back(0);
         ns.type.push_back((uint8_t)MPX_MSG_E_EPOCH);
+        ns.sec.push_back(0);
         ns.src.push_back(0);
         ns.ballot.push_back(0);
         ns.aux.push_back(0);
@@ -1521,6 +1655,7 @@ struct PoolItem {
     uint64_t first;                     // the node's e_* index (carried: 0)
     uint32_t cnt;
     uint64_t hash;
+    uint64_t sec;                       // the list's value-section id (0: none; equal ids = equal lists)
     const std::vector<std::pair<uint64_t, uint64_t>> *carried;
     uint64_t off;                       // phase B: pool offset
     bool is_first;
@@ -1585,7 +1720,7 @@ static void walk_node(const NodeStream &ns, uint32_t n, uint32_t N, uint64_t sb,
     const bool has_pid = !ns.e_pid.empty();
     auto add_item = [&](uint32_t batch, uint64_t first, uint32_t cnt,
                         const std::vector<std::pair<uint64_t, uint64_t>> *carried) -> uint32_t {
-        PoolItem it{n, batch, first, cnt, 0, carried, 0, false};
+        PoolItem it{n, batch, first, cnt, 0, 0, carried, 0, false};
         if (carried) {
             std::vector<uint64_t> iv(cnt), vv(cnt);
             for (uint32_t q = 0; q < cnt; ++q) { iv[q] = (*carried)[q].first; vv[q] = (*carried)[q].second; }
@@ -1668,7 +1803,10 @@ static void walk_node(const NodeStream &ns, uint32_t n, uint32_t N, uint64_t sb,
         if (vote_j >= 0) P.reps[vote_j].push_back(g);
         uint64_t ent = ns.ent[k];                    // node-local g_a / r / e index
         uint32_t item = NONE32;
-        if (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_P_BATCH) item = add_item(NONE32, ent, ns.cnt[k], nullptr);
+        if (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_P_BATCH) {
+            item = add_item(NONE32, ent, ns.cnt[k], nullptr);
+            if (!ns.sec.empty()) P.items[item].sec = ns.sec[k];
+        }
         P.m_type.push_back(t);
         P.m_src.push_back(ns.src[k]);
         P.m_ballot.push_back(ns.ballot[k]);
@@ -1827,6 +1965,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         const uint32_t S = std::max(1u, threads);
         auto same = [&](const PoolItem &a, const PoolItem &b) {
             if (a.cnt != b.cnt) return false;
+            if (a.sec && a.sec == b.sec) return true;          // (byte-equal sections, one shard filter)
             if (!a.carried && !b.carried) {                    // (the common case: two messages' lists)
                 const NodeStream &x = nodes[a.node], &y = nodes[b.node];
                 const size_t bytes = 8ull * a.cnt;
@@ -2063,6 +2202,7 @@ int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<
     std::vector<IngestViolation> ivs(chunks.size());
     std::vector<int> rcs(chunks.size(), MPX_OK);
     SectionCache sc;                                 // (one decode per distinct entry list, this call)
+    sc.id_base = vt.sections.fetch_add(1ull << 40);
     std::atomic<size_t> next{0};
     auto work = [&]() {
         for (size_t c; (c = next.fetch_add(1)) < chunks.size();) {
@@ -2098,7 +2238,7 @@ int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<
             ivs[c].seq += rb;
             auto cat = [](auto &dst, const auto &src) { dst.insert(dst.end(), src.begin(), src.end()); };
             cat(ns.type, p.type); cat(ns.src, p.src); cat(ns.ballot, p.ballot); cat(ns.aux, p.aux);
-            cat(ns.cnt, p.cnt); cat(ns.ver, p.ver); cat(ns.part, p.part);
+            cat(ns.cnt, p.cnt); cat(ns.ver, p.ver); cat(ns.part, p.part); cat(ns.sec, p.sec);
             cat(ns.e_iid, p.e_iid); cat(ns.e_val, p.e_val); cat(ns.e_pid, p.e_pid);
             cat(ns.r_iid, p.r_iid); cat(ns.r_pid, p.r_pid); cat(ns.r_val, p.r_val);
             cat(ns.g_a, p.g_a); cat(ns.g_b, p.g_b);

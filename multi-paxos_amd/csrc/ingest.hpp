@@ -60,6 +60,8 @@ struct ValueTable {
     bool synthetic_clean = false;
     // member Value_m codec (member/paxos.cpp:321-408): + cb, membership list
     bool member = false;
+    // section id ranges handed to the submit calls' SectionCaches (ids unique over the engine)
+    std::atomic<uint64_t> sections{0};
     // parse one Value; returns bytes used (>0) or a negative MPX_E_* code; *mem: a member
     // membership Value (a change list instead of a payload)
     long parse(const uint8_t *p, size_t avail, uint64_t *handle, bool *mem = nullptr);
@@ -80,6 +82,10 @@ struct ValueTable {
     // the canonical bytes of handle h, interned (thread-safe): MPX_E_VALUE when h already names
     // other bytes (a Value is named by (proposer, value_id), multi/paxos.cpp:439)
     int intern(uint64_t h, const char *b, uint32_t len, uint32_t exec_off, uint32_t exec_len);
+    // a run of Values whose canonical bytes are their wire bytes, interned with one lock per run of
+    // the same shard (a section's consecutive handles share groups, hence shards)
+    struct Pending { uint64_t h; const char *b; uint32_t len, exec_off, exec_len; };
+    int intern_batch(const Pending *v, size_t n);
     const Rec *find(uint64_t h) const { return sh[shard_of(h)].find(h); }
     // prefetch h's home slot (key and record): a section's Values are looked up one after another,
     // each a likely cache miss, so the decode touches them all first (no lock: a stale address
@@ -87,20 +93,34 @@ struct ValueTable {
     void prefetch_slot(uint64_t h) const;
 };
 
-// One submit call's value sections (the entry lists of ACCEPT / COMMIT / P_BATCH / PREPARE_REPLY
-// bodies) already interned: a broadcast reaches every node with the same bytes, and a batch's
-// ACCEPT, COMMIT and P_BATCH carry the same list, so the first decode thread to meet a section
-// interns its Values (ValueTable::parse) and every other one only reads its entries off the wire
-// (the handle is (proposer, noop, value_id) itself) — no thread waits for another, and the table
-// sees each distinct Value about once.  Sections are compared in full (the key only picks
-// candidates) and point into the submitted buffers: the set lives for one submit call.
+// One submit call's value sections (the entry lists of ACCEPT / COMMIT / P_BATCH bodies): a
+// broadcast reaches every node with the same bytes, and a batch's ACCEPT, COMMIT and P_BATCH carry
+// the same list.  The first decode thread to claim a section interns its Values (in batches, one
+// lock per shard run) and keeps the sorted entries as the section's Result; a thread that meets
+// the section later copies them, and one that meets it while it is still being decoded reads its
+// entries off the wire (skim: the handle is (proposer, noop, value_id) itself) — no thread waits
+// for another.  Every record notes its section's id (NodeStream::sec), which build_trace's entry
+// pool takes as list equality.  Sections are compared in full (the key only picks candidates)
+// and point into the submitted buffers: the set lives for one submit call.
 struct SectionCache {
-    struct Ent { const uint8_t *b; size_t len; bool with_pid; };
+    struct Result {
+        const uint8_t *b; size_t len; bool with_pid;
+        uint64_t id;                                      // the section's identity (NodeStream::sec)
+        std::atomic<int> ready{0};
+        int rc = MPX_OK;                                  // the section's decode error (reported in record order)
+        std::vector<uint64_t> iid, pid, val;              // sorted by iid (sort_entries)
+        std::vector<std::pair<uint64_t, uint32_t>> memh;  // member: membership Values, offset in the section
+        size_t n_all = 0;
+        bool dup = false;
+    };
     static constexpr uint32_t SHARDS = 64;
-    struct Shard { std::mutex mu; std::unordered_multimap<uint64_t, Ent> m; };
+    struct Shard { std::mutex mu; std::unordered_multimap<uint64_t, std::unique_ptr<Result>> m; };
     std::unique_ptr<Shard[]> sh{new Shard[SHARDS]};
-    // true for the first caller with these bytes (it interns them)
-    bool claim(const uint8_t *b, size_t len, bool with_pid);
+    bool share = true;                                    // (tests: false = owners keep no Result, others skim)
+    uint64_t id_base = 0;                                 // section ids: id_base + k (ValueTable::sections)
+    std::atomic<uint64_t> next_id{1};
+    // the section's Result; own = the caller is the first with these bytes (it decodes them)
+    Result *claim(const uint8_t *b, size_t len, bool with_pid, bool &own);
 };
 
 // Membership discovered at run time (MPX_FLAG_LEARN_EPOCHS, member semantics): every node's
@@ -133,11 +153,14 @@ struct NodeStream {
     std::vector<uint64_t> r_iid, r_pid, r_val;    // PREPARE_REPLY entries (in shard)
     std::vector<uint64_t> g_a, g_b;               // PREPARE ranges (all), sorted by start
     std::vector<uint8_t> part;                    // 1: the record carried entries, none in the shard
+    std::vector<uint64_t> sec;                    // its value section's id (SectionCache; 0: none / unknown):
+                                                  //   equal ids = byte-equal sections = equal entry lists
     // (keeps the capacity: a live engine decodes window after window into the same streams)
     void clear()
     {
         type.clear(); src.clear(); ballot.clear(); aux.clear(); ent.clear(); cnt.clear(); e_iid.clear(); e_val.clear();
         e_pid.clear(); ver.clear(); r_iid.clear(); r_pid.clear(); r_val.clear(); g_a.clear(); g_b.clear(); part.clear();
+        sec.clear();
     }
 };
 

@@ -125,15 +125,18 @@ int main(int argc, char **argv)
     if (W > 1) { wa.init(N, NB); wb.init(N, NB); }
     uint64_t msgs = 0, runs = 0;
     for (uint32_t w = 0; w < W; ++w) {
-        std::vector<NodeStream> nodes(N);
-        for (uint32_t n = 0; n < N; ++n)
-            for (uint64_t k = all[n].cnt * w / W; k < all[n].cnt * (w + 1) / W; ++k) {
-                const uint8_t *m = all[n].bytes + all[n].offs[k];
-                const size_t len = all[n].offs[k + 1] - all[n].offs[k];
-                const int rc = member ? decode_record_member(vt, nodes[n], n, m, len, sb, se, iv)
-                                      : decode_record(vt, nodes[n], n, N, m, len, sb, se, iv);
-                if (rc) { std::printf("ok-decode-error %d\n", rc); return 0; }
-            }
+        // (decode_parallel: the records carry their value sections' ids, which the parallel build's
+        // entry pool takes as equality; the serial build compares every list)
+        std::vector<NodeStream> nodes(N), parts;
+        std::vector<StreamSlice> sl(N);
+        for (uint32_t n = 0; n < N; ++n) {
+            const uint64_t k0 = all[n].cnt * w / W, k1 = all[n].cnt * (w + 1) / W;
+            sl[n] = StreamSlice{all[n].offs + k0, all[n].bytes, k1 - k0};
+        }
+        if (int rc = decode_parallel(vt, nodes, parts, sl, member, nullptr, sb, se, iv, 3, 4096)) {
+            std::printf("ok-decode-error %d\n", rc);
+            return 0;
+        }
         HostTrace ha, hb;
         const std::vector<mpx_epoch> e = member ? ep : std::vector<mpx_epoch>();
         const int ra = build_trace_serial(nodes, sb, se - sb, e, ha, W > 1 ? &wa : nullptr);

@@ -7,7 +7,8 @@
 // and with an EpochLearn from the genesis epoch, fed in `windows` slices (the learner state carries
 // over, as across MPX_FLAG_INCREMENTAL windows).  The learned run must place the same E_EPOCH
 // records at the same stream positions with the same epochs, and the epochs it learned must be the
-// container's table.  The learned pass skims every value section (another thread's claim, SectionCache).
+// container's table.  The learned pass runs skimming every value section and copying every
+// section's decode (SectionCache).
 // Prints "ok <records> <markers> <epochs>" or the first difference.
 #include <cstdio>
 #include <cstdlib>
@@ -66,20 +67,26 @@ int main(int argc, char **argv)
         const uint64_t cnt = rd64(b + pos), nb = rd64(b + pos + 8);
         const uint64_t *offs = reinterpret_cast<const uint64_t *>(b + pos + 16);
         const uint8_t *bytes = b + pos + 16 + 8 * (cnt + 1);
-        NodeStream as_is, got;
-        ValueTable v1, v2;
-        v1.member = v2.member = true;
+        NodeStream as_is;
+        ValueTable v1;
+        v1.member = true;
         IngestViolation iv;
-        EpochLearn el;
-        el.view = ep[0];
         for (uint64_t i = 0; i < cnt; ++i)
             if (int rc = decode_record_member(v1, as_is, n, bytes + offs[i], offs[i + 1] - offs[i], 0, M, iv)) {
                 std::printf("FAIL decode rc %d\n", rc); return 1;
             }
-        // the learned pass skims every value section (as a decode thread does when another thread
-        // claimed the section and may not have interned it yet): its table stays empty, so the
-        // learner must read membership changes off the wire
+        // the learned pass twice: once skimming every value section (as a decode thread does when
+        // another thread claimed the section and has not decoded it yet: its table stays empty, so
+        // the learner must read membership changes off the wire), once copying every section from
+        // another decode's Result (SectionCache, the membership Values' wire offsets with it)
+        for (int share = 0; share < 2; ++share) {
+        NodeStream got;
+        ValueTable v2;
+        v2.member = true;
+        EpochLearn el;
+        el.view = ep[0];
         SectionCache sc;
+        sc.share = share != 0;
         {
             NodeStream sink;
             ValueTable v3;
@@ -109,12 +116,13 @@ int main(int argc, char **argv)
                             got.type[k], got.ver[k], as_is.type[k], as_is.ver[k]);
                 return 1;
             }
-            markers += got.type[k] == MPX_MSG_E_EPOCH;
+            markers += share && got.type[k] == MPX_MSG_E_EPOCH;
         }
         for (size_t k = 0; k < el.steps.size(); ++k) {
             if (k + 1 < learned.size()) {
                 if (!same(learned[k + 1], el.steps[k])) { std::printf("FAIL node %u step %zu disagrees\n", n, k); return 1; }
             } else learned.push_back(el.steps[k]);
+        }
         }
         records += cnt;
         pos += 16 + 8 * (cnt + 1) + nb;
