@@ -715,6 +715,8 @@ static int upload_trace(mpx_engine *e)
             }
         }
         v.chosen_static = ok ? 1 : 0;
+        v.any_vchk = 0;                              // (ingest marks only runs whose Values can differ)
+        for (const Frag &f : h.frags) if (f.flags & FR_VCHK) { v.any_vchk = 1; break; }
     }
     {
         uint64_t mx = 0;
@@ -2730,6 +2732,7 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     // batches tile the instances: a bucket's chosen-log runs are disjoint and dense, so at most
     // four of them over a whole bucket pass plan_chosen's static test (no k_chosen walk)
     v.chosen_static = max_cb <= 4 && L % BS == 0 ? 1 : 0;
+    v.any_vchk = 0;                                  // (a clean trace: no re-commit through another entry)
     TRY(finish_view(e));
     for (auto &ns : e->nodes) ns.clear();
     e->vt.clear();

@@ -1048,8 +1048,8 @@ struct EntryPool {
 // the same entries (iid, Value, member: proposal id) over its range, names that run's entries
 // (the pool's content addressing at bucket-run grain: a re-commit of the same Values through
 // another message — another proposer's COMMIT, multi/paxos.cpp:1494-1518 — then shares them);
-// a run that still meets a committed slot through another entry gets FR_VCHK, and only those
-// send their pair to the device's Value check (k_commit_check).
+// a run that still meets a committed slot through another entry with another Value gets FR_VCHK,
+// and only those send their pair to the device's Value check (k_commit_check).
 static void mark_value_checks(HostTrace &ht, bool member)
 {
     const uint64_t NP = (uint64_t)ht.N * ht.NB;
@@ -1085,11 +1085,15 @@ static void mark_value_checks(HostTrace &ht, bool member)
                     if (same) fr.entry = base;
                 }
             }
+            // the device's check compares the Values (k_commit_check: a later run's e_val against the
+            // fixing run's); through another entry with the same Value it can never fire, so only a
+            // slot whose Values differ sends the pair to it
             bool chk = false;
-            for (uint32_t s = st; s < st + c; ++s)
+            for (uint32_t s = st; s < st + c && !chk; ++s)
                 if (fixr[s]) {
                     const Frag &fj = ht.frags[f0 + fixr[s] - 1];
-                    chk = chk || fj.entry - fj.start != fr.entry - fr.start;
+                    chk = fj.entry - fj.start != fr.entry - fr.start &&
+                          ht.e_val[fj.entry + (s - fj.start)] != ht.e_val[fr.entry + (s - st)];
                 }
             if (chk) fr.flags |= FR_VCHK;
             if (learn)
@@ -1131,7 +1135,7 @@ struct Walk {
 // Everything after the walk over the nodes' records: the vote lists, the run / event CSRs, the
 // work lists, the scan chunks, and (a window) the carry, committed only when every check passed.
 static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_t sb, uint64_t slen, bool member,
-                        WindowCarry *wc)
+                        WindowCarry *wc, uint32_t threads)
 {
     auto &fcount = W.fcount, &cfcount = W.cfcount;
     auto &fr = W.fr, &cfr = W.cfr;
@@ -1148,6 +1152,29 @@ static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_
     auto &ents_new = W.ents_new;
     const uint64_t gid_next = W.gid_next;
     (void)sb;
+    // (the CSR scatters and the slot bytes on a few threads: each takes a range of keys and scans
+    // the whole list, so every key's items keep their order)
+    const uint32_t T = std::max(1u, threads);
+    auto parallel = [&](uint32_t count, const auto &fn) {
+        std::atomic<uint32_t> next{0};
+        auto work = [&]() { for (uint32_t k; (k = next.fetch_add(1)) < count;) fn(k); };
+        std::vector<std::thread> th;
+        for (uint32_t t = 1; t < std::min(T, count); ++t) th.emplace_back(work);
+        work();
+        for (auto &x : th) x.join();
+    };
+    // items[i] goes to off[key(i)] + (its rank among that key's items)
+    auto scatter = [&](size_t n, uint64_t nkeys, const std::vector<uint64_t> &off, const auto &key, const auto &put) {
+        const uint32_t P = n < 4096 ? 1 : T;
+        parallel(P, [&](uint32_t p) {
+            const uint64_t k0 = nkeys * p / P, k1 = nkeys * (p + 1) / P;
+            std::vector<uint64_t> pos(off.begin() + k0, off.begin() + k1);
+            for (size_t i = 0; i < n; ++i) {
+                const uint64_t k = key(i);
+                if (k >= k0 && k < k1) put(i, pos[k - k0]++);
+            }
+        });
+    };
     ht.node_off[N] = ht.m_type.size();
     sc_off[N] = ht.sc_type.size();
     if (ht.prop_off.empty()) ht.prop_off.assign(N + 1, 0);
@@ -1186,10 +1213,8 @@ static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_
     }
     if (fr.size() > MAX_FRAGS) return MPX_E_RANGE;             // 4-byte state slots (mpx_internal.hpp)
     ht.frags.resize(fr.size());
-    {
-        std::vector<uint64_t> pos(ht.f_off.begin(), ht.f_off.end() - 1);
-        for (auto &x : fr) ht.frags[pos[x.key]++] = x.f;
-    }
+    scatter(fr.size(), (uint64_t)N * NB, ht.f_off, [&](size_t i) { return fr[i].key; },
+            [&](size_t i, uint64_t at) { ht.frags[at] = fr[i].f; });
     if (!wc) mark_value_checks(ht, member);
     ht.cf_off.assign(NB + 1, 0);
     for (uint64_t i = 0; i < NB; ++i) {
@@ -1197,10 +1222,8 @@ static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_
         if (cfcount[i] > MAX_PAIR_FRAGS) return MPX_E_RANGE;  // 2-byte chosen log (mpx_internal.hpp)
     }
     ht.cfrags.resize(cfr.size());
-    {
-        std::vector<uint64_t> pos(ht.cf_off.begin(), ht.cf_off.end() - 1);
-        for (auto &x : cfr) ht.cfrags[pos[x.key]++] = x.f;
-    }
+    scatter(cfr.size(), NB, ht.cf_off, [&](size_t i) { return cfr[i].key; },
+            [&](size_t i, uint64_t at) { ht.cfrags[at] = cfr[i].f; });
     // per-pair event CSR (stable: message order within a pair)
     ht.ev_off.assign(N * NB + 1, 0);
     ht.pair_ev.assign(N * NB, 0);
@@ -1211,14 +1234,8 @@ static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_
     }
     ht.ev_msg.resize(evp.size());
     ht.ev_aux.resize(evp.size());
-    {
-        std::vector<uint64_t> pos(ht.ev_off.begin(), ht.ev_off.end() - 1);
-        for (size_t i = 0; i < evp.size(); ++i) {
-            const uint64_t at = pos[evp[i].first]++;
-            ht.ev_msg[at] = evp[i].second;
-            ht.ev_aux[at] = evx[i];
-        }
-    }
+    scatter(evp.size(), (uint64_t)N * NB, ht.ev_off, [&](size_t i) { return evp[i].first; },
+            [&](size_t i, uint64_t at) { ht.ev_msg[at] = evp[i].second; ht.ev_aux[at] = evx[i]; });
     std::vector<uint64_t>().swap(evx);
     std::vector<std::pair<uint64_t, uint32_t>>().swap(evp);
     // pairs that are not lean (mpx_internal.hpp plan_shape_ok: one plan word of
@@ -1273,9 +1290,16 @@ static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_
     // slots for sparse fragments
     if (ht.any_sparse) {
         ht.e_slot.resize(ht.e_iid.size());
-        for (size_t k = 0; k < ht.e_iid.size(); ++k) ht.e_slot[k] = (uint8_t)((ht.e_iid[k] - sb) & (BS - 1));
         ht.r_slot.resize(ht.r_iid.size());
-        for (size_t k = 0; k < ht.r_iid.size(); ++k) ht.r_slot[k] = (uint8_t)((ht.r_iid[k] - sb) & (BS - 1));
+        const size_t E = ht.e_iid.size(), R = ht.r_iid.size(), C = 1u << 18;
+        const uint32_t ce = (uint32_t)((E + C - 1) / C), cr = (uint32_t)((R + C - 1) / C);
+        parallel(ce + cr, [&](uint32_t c) {
+            const bool e = c < ce;
+            const std::vector<uint64_t> &iv = e ? ht.e_iid : ht.r_iid;
+            std::vector<uint8_t> &sl = e ? ht.e_slot : ht.r_slot;
+            const size_t a = (size_t)(e ? c : c - ce) * C, b = std::min(iv.size(), a + C);
+            for (size_t k = a; k < b; ++k) sl[k] = (uint8_t)((iv[k] - sb) & (BS - 1));
+        });
     }
     // proposer lists
     ht.pl_off.assign(N + 1, 0);
@@ -1636,7 +1660,7 @@ int build_trace_serial(const std::vector<NodeStream> &nodes, uint64_t sb, uint64
             if (member) c.markers = wc->markers[n] + (uint32_t)(ht.ee_msg.size() - ht.ee_off[n]);
         }
     }
-    return finish_trace(ht, W, N, NB, sb, slen, member, wc);
+    return finish_trace(ht, W, N, NB, sb, slen, member, wc, 1);
 }
 
 // ---- build_trace: the walk over the nodes' records, node-parallel ----
@@ -2167,7 +2191,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             W.ents_gone.insert(W.ents_gone.end(), P.ents_gone.begin(), P.ents_gone.end());
             for (auto &x : P.ents_new) W.ents_new[(uint32_t)(x.first + new_off[n])] = std::move(x.second);
         }
-    return finish_trace(ht, W, N, NB, sb, slen, member, wc);
+    return finish_trace(ht, W, N, NB, sb, slen, member, wc, threads);
 }
 
 int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<NodeStream> &parts,

@@ -3604,7 +3604,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
                 (void)hipEventRecord((hipEvent_t)side.join3, s3);
             }
             hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);
-            hipLaunchKernelGGL(k_commit_check<true>, dim3(g.apply_wgs), dim3(256), 0, s, v);
+            if (v.any_vchk) hipLaunchKernelGGL(k_commit_check<true>, dim3(g.apply_wgs), dim3(256), 0, s, v);
         } else {
             // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
             // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
@@ -3633,7 +3633,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
 #ifndef MPX_PLAN_LSEG4
                 hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);
 #endif
-                hipLaunchKernelGGL(k_commit_check<false>, dim3(g.apply_wgs), dim3(256), 0, s, v);
+                if (v.any_vchk) hipLaunchKernelGGL(k_commit_check<false>, dim3(g.apply_wgs), dim3(256), 0, s, v);
             } else if (side3) {
                 (void)hipEventRecord((hipEvent_t)side.join3, s3);
             }

@@ -142,7 +142,8 @@ enum : uint8_t {
 // fragment kinds (Frag::flags >> 4)
 enum : uint8_t { K_ACCEPT = 0, K_COMMIT = 1, K_PREPLY = 2, K_BATCH = 3 };
 // FR_VCHK (ingest): a commit / learn (member: also an accept) run that meets a slot committed
-// earlier in its pair through another entry — the Value check (k_commit_check) has work there.
+// earlier in its pair through another entry holding another Value — the Value check
+// (k_commit_check) may find a violation there (equal Values through another entry cannot).
 // (flags bit 1 stays free: k_plan_list's staged words carry F_GRANTED in it, MP_GRANTED)
 enum : uint8_t { FR_DENSE = 1, FR_VCHK = 4 };
 
@@ -314,6 +315,7 @@ struct DevView {
                                     // rows 0..N-1 state, row N chosen log; PLAN_SKIP = not by k_store
     uint32_t chosen_static;         // every bucket's chosen-log runs pass plan_chosen's static test (<= 4
                                     // disjoint dense runs, a whole bucket): the plan step needs no k_chosen
+    uint32_t any_vchk;              // some run carries FR_VCHK: k_commit_check has pairs (else not launched)
     uint32_t *fast_rest;            // [0]: pairs k_plan leaves to k_apply_fast (0: it exits at once);
                                     // [1]: k_chosen's last-workgroup ticket
     uint32_t *store_dummy;          // 64 KiB sink for k_store's skipped (row, bucket) stores

@@ -6,8 +6,9 @@
 //   1. the entries the run names are its message's own (iid, Value, member: proposal id) on every
 //      slot it covers — aliasing onto another run's entries never changes what the run says;
 //   2. FR_VCHK is set exactly when a commit / learn (member: also an accept) covers a slot an
-//      earlier commit / learn of the pair fixed through another entry index (the pairs whose
-//      re-commits the device's Value check has to compare), on the pairs k_plan_list can plan;
+//      earlier commit / learn of the pair fixed through another entry index holding another Value
+//      (the re-commits the device's Value check could find different), on the pairs k_plan_list
+//      can plan;
 //   3. aliasing took effect: no unmarked run names other entries than its slot's fixing run.
 // Prints "ok <runs> <aliased> <marked>" or the first failure.
 #include <cstdio>
@@ -110,7 +111,7 @@ int main(int argc, char **argv)
             if (learn || member)
                 for (uint32_t d = 0; d < fr.count; ++d) {
                     const int64_t j = fix[fr.start + d];
-                    want = want || (j >= 0 && (uint64_t)j != fr.entry + d);
+                    want = want || (j >= 0 && (uint64_t)j != fr.entry + d && h.e_val[j] != h.e_val[fr.entry + d]);
                 }
             const bool got = (fr.flags & FR_VCHK) != 0;
             marked += got;
