@@ -789,11 +789,15 @@ static int queue_run(mpx_engine *e, bool digest)
         // the side stream gets a hardware queue of its own: a stream of another priority draws
         // from that priority's queue pool, so it never shares the plan path's queue — which
         // serialises the two — when the process holds more streams than GPU_MAX_HW_QUEUES
-        // (MPX_SIDE_PRIO=normal|low|high, A/B)
+        // (MPX_SIDE_PRIO=normal|low|high, A/B).  The longer chain gets the high-priority stream:
+        // multi, the promise-round walk (C3 0.886 -> 0.854 ms with s2 high / s3 low); member, the
+        // plan list and the listed pairs' walk (contended C5 2.019 vs 2.106 ms the other way;
+        // profiles/r05_v12_ab_stream_prio.json)
+        const bool rounds_first = e->cfg.semantics == MPX_SEM_MULTI;
         int least = 0, greatest = 0;
         HTRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
         const char *sp = ab_env("MPX_SIDE_PRIO");
-        const std::string pr = sp ? sp : "low";
+        const std::string pr = sp ? sp : rounds_first ? "high" : "low";
         const int prio = pr == "high" ? greatest : pr == "normal" ? 0 : least;
         HTRY(hipStreamCreateWithPriority(&e->stream2, hipStreamNonBlocking, prio));
         HTRY(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
@@ -801,7 +805,7 @@ static int queue_run(mpx_engine *e, bool digest)
         // the third stream at the highest priority: its own hardware-queue pool again, so neither
         // side stream shares the plan path's queue (MPX_SIDE3_PRIO=normal|low|high, A/B)
         const char *sp3 = ab_env("MPX_SIDE3_PRIO");
-        const std::string pr3 = sp3 ? sp3 : "high";
+        const std::string pr3 = sp3 ? sp3 : rounds_first ? "low" : "high";
         const int prio3 = pr3 == "high" ? greatest : pr3 == "normal" ? 0 : least;
         HTRY(hipStreamCreateWithPriority(&e->stream3, hipStreamNonBlocking, prio3));
         HTRY(hipEventCreate(&e->fork3a));           // (ride on kernel launches as their stop events)
@@ -1245,9 +1249,14 @@ static int fetch_results(mpx_engine *e, Results &r)
                 // resolve the reference (mpx_internal.hpp OutRec) against the host trace
                 OutEnt x{o.msg, ((o.aux & OUT_K1) ? 1u : 0u) | ((o.aux & OUT_CMT) ? 2u : 0u), 0, 0, 0};
                 if (x.kind & 1) {
-                    if (o.ref >= h.r_iid.size()) return MPX_E_STATE;
-                    x.iid = h.r_iid[o.ref]; x.ballot = h.r_pid[o.ref]; x.handle = h.r_val[o.ref];
-                    r.out.push_back(x);
+                    // one slot, or (OUT_RUN, a quorum's merged map) a run of slots whose entries follow
+                    // one another in one reply run
+                    const uint32_t ns = (o.aux & OUT_RUN) ? (o.aux >> OUT_RUN_SHIFT) & 0x1FF : 1;
+                    if ((uint64_t)o.ref + ns > h.r_iid.size()) return MPX_E_STATE;
+                    for (uint32_t i = 0; i < ns; ++i) {
+                        x.iid = h.r_iid[o.ref + i]; x.ballot = h.r_pid[o.ref + i]; x.handle = h.r_val[o.ref + i];
+                        r.out.push_back(x);
+                    }
                 } else {
                     if (o.ref >= h.frags.size()) return MPX_E_STATE;
                     const Frag &f = h.frags[o.ref];

@@ -2525,7 +2525,46 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             cQ += hit[j];
                             pre[lane + 64 * j] = u64x2{0, 0};                        // :1105
                         }
-                        EMIT(hit, g, OUT_K1, ref, ext);
+                        // the merged map leaves as run records: consecutive slots whose entries are
+                        // consecutive (one reply run) with the same OUT_CMT bit are one record
+                        // (OUT_RUN: slot, length; the host expands entry ref + i to slot + i)
+                        bool cont[SPL];
+                        uint64_t cm[SPL];
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) {
+                            uint32_t pr = __shfl_up(ref[j], 1, 64), pe = __shfl_up(ext[j], 1, 64);
+                            int ph = __shfl_up((int)hit[j], 1, 64);
+                            if (j) {                                                 // lane 0: the previous strip's lane 63
+                                const uint32_t r63 = __shfl(ref[j - 1], 63, 64), e63 = __shfl(ext[j - 1], 63, 64);
+                                const int h63 = __shfl((int)hit[j - 1], 63, 64);
+                                if (lane == 0) { pr = r63; pe = e63; ph = h63; }
+                            } else if (lane == 0) {
+                                ph = 0;
+                            }
+                            cont[j] = hit[j] && ph && pr + 1 == ref[j] && pe == ext[j];
+                            cm[j] = __ballot(cont[j]);
+                        }
+                        bool start[SPL];
+                        uint32_t ext2[SPL];
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) {
+                            start[j] = hit[j] && !cont[j];
+                            uint32_t len = 1;
+                            if (start[j]) {
+                                uint32_t p = lane + 64 * j + 1;                      // count the continuation bits after it
+                                while (p < BS) {
+                                    const uint64_t w = cm[p >> 6] >> (p & 63);
+                                    const uint32_t room = 64 - (p & 63);
+                                    const uint32_t ones = ~w ? (uint32_t)__builtin_ctzll(~w) : 64;
+                                    const uint32_t take = ones < room ? ones : room;
+                                    len += take;
+                                    if (take < room) break;
+                                    p += take;
+                                }
+                            }
+                            ext2[j] = ext[j] | OUT_RUN | (len << OUT_RUN_SHIFT);
+                        }
+                        EMIT(start, g, OUT_K1, ref, ext2);
                     }
                     ++c;
                 }
@@ -3558,7 +3597,15 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
         else hipLaunchKernelGGL((k_apply<APPLY_WAVES_FULL, false, false>), dim3(g.apply_wgs), dim3(256), 0, s2, v, v.num_gp_snap, v.num_gp);
         if (side_rounds) (void)hipEventRecord((hipEvent_t)side.join, s2);
     };
-    if (side_rounds) launch_rounds();
+    // (A/B: MPX_FULL_LATE starts the promise-round walk at the end of k_plan_list instead, so the
+    // plan runs alone)
+    const bool full_late = side_rounds && side.stream3 && ab_env("MPX_FULL_LATE") != nullptr;
+    if (side_rounds && !full_late) launch_rounds();
+    auto launch_rounds_late = [&]() {
+        if (!full_late) return;
+        (void)hipStreamWaitEvent(s2, (hipEvent_t)side.fork3b, 0);
+        launch_rounds();
+    };
     if (ev_apply0 && !plan_path) (void)hipEventRecord((hipEvent_t)ev_apply0, s);
     // the chosen log needs no k_chosen launch when the trace's chosen-log runs passed
     // plan_chosen's static test at load; then, with no general pair either (the C4 shape), the
@@ -3597,14 +3644,17 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
             // C5 0.451 -> 0.384 ms, contended C5 2.745 -> 2.582 ms, profiles/r04_v25_ab_member_plan8.json)
             hipExtLaunchKernelGGL((k_plan_list<true, PLAN_XSEG, PLAN_XFRAGS>), dim3(plan_blocks), dim3(256), 0, s,
                                   (hipEvent_t)ev_apply0, side3 ? (hipEvent_t)side.fork3b : (hipEvent_t)nullptr, 0, v, g.apply_wgs);
-            if (side3) {                                 // member k_plan_list planned the chosen log too
+            if (side3) {                                 // (the listed pairs' walk, the step's longest chain)
                 (void)hipStreamWaitEvent(s3, (hipEvent_t)side.fork3b, 0);
                 launch_listed(s3);
-                if (!skip_chosen) { launch_chosen(s3, nullptr); chosen_done = true; }
                 (void)hipEventRecord((hipEvent_t)side.join3, s3);
+                launch_rounds_late();
             }
             hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);
             if (v.any_vchk) hipLaunchKernelGGL(k_commit_check<true>, dim3(g.apply_wgs), dim3(256), 0, s, v);
+            // member k_plan_list planned the chosen log too: k_chosen walks the rest beside the listed
+            // pairs (it reads only the votes and the chosen-log runs)
+            if (side3 && !skip_chosen) { launch_chosen(s, nullptr); chosen_done = true; }
         } else {
             // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
             // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
@@ -3629,6 +3679,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
                     (void)hipStreamWaitEvent(s3, (hipEvent_t)side.fork3b, 0);
                     launch_listed(s3);
                     (void)hipEventRecord((hipEvent_t)side.join3, s3);
+                    launch_rounds_late();
                 }
 #ifndef MPX_PLAN_LSEG4
                 hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);

@@ -175,7 +175,8 @@ static_assert(sizeof(OutRec) == 12, "OutRec is 12 bytes");
 constexpr uint32_t OUT_K1 = 0x100;
 constexpr uint32_t OUT_CMT = 0x200;
 // kind 0 run record (k_plan_list): slots aux & 0xFF .. + (aux >> OUT_RUN_SHIFT) of the
-// fragment's bucket, all fixed by fragment `ref` (the host expands it)
+// fragment's bucket, all fixed by fragment `ref` (the host expands it); kind 1 run record (a
+// quorum's merged map, k_apply): slot aux & 0xFF + i takes PREPARE_REPLY entry ref + i
 constexpr uint32_t OUT_RUN = 0x400;
 constexpr uint32_t OUT_RUN_SHIFT = 16;
 // host form of a snapshot record
