@@ -9,6 +9,8 @@
 #include "ingest.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <atomic>
 #include <thread>
 #include <cstdlib>
@@ -1980,10 +1982,15 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
         work();
         for (auto &x : th) x.join();
     };
+    // (MPX_BUILD_TIMES, A/B builds: the phases' wall times on stderr)
+    const bool times = ab_env("MPX_BUILD_TIMES") != nullptr;
+    auto wall = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double tp[5] = {times ? wall() : 0, 0, 0, 0, 0};
     // phase A
     std::vector<NodePart> parts(N);
     parallel(N, [&](uint32_t n) { walk_node(nodes[n], n, N, sb, slen, NB, member, epochs.size(), wc, parts[n]); });
     for (uint32_t n = 0; n < N; ++n) TRY_RC(parts[n].rc);
+    if (times) tp[1] = wall();
     // phase B: the entry pool (EntryPool's content addressing, first occurrence in walk order)
     {
         const uint32_t S = std::max(1u, threads);
@@ -2044,6 +2051,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             }
         E = off;
     }
+    if (times) tp[2] = wall();
     // phase C: offsets of every node's part, then the parts rebased into the trace
     std::vector<uint64_t> g_off(N + 1, 0), j_off(N + 1, 0), new_off(N + 1, 0), r_off(N + 1, 0), ga_off(N + 1, 0),
         sc_o(N + 1, 0), ee_o(N + 1, 0), pl_o(N + 1, 0), pr_o(N + 1, 0), fr_o(N + 1, 0), cfr_o(N + 1, 0), ev_o(N + 1, 0),
@@ -2178,6 +2186,7 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             W.evx[ev_o[n] + i] = P.m_type[g] == MPX_MSG_PREPARE ? P.evx[i] + gao : P.evx[i];
         }
     });
+    if (times) tp[3] = wall();
     // (counts and the window's carry: serial, small)
     for (const FragKey &x : W.fr) W.fcount[x.key]++;
     for (const FragKey &x : W.cfr) W.cfcount[x.key]++;
@@ -2191,7 +2200,13 @@ int build_trace(const std::vector<NodeStream> &nodes, uint64_t sb, uint64_t slen
             W.ents_gone.insert(W.ents_gone.end(), P.ents_gone.begin(), P.ents_gone.end());
             for (auto &x : P.ents_new) W.ents_new[(uint32_t)(x.first + new_off[n])] = std::move(x.second);
         }
-    return finish_trace(ht, W, N, NB, sb, slen, member, wc, threads);
+    if (!times) return finish_trace(ht, W, N, NB, sb, slen, member, wc, threads);
+    tp[4] = wall();
+    const int rc = finish_trace(ht, W, N, NB, sb, slen, member, wc, threads);
+    const double te = wall();
+    std::fprintf(stderr, "[mpx] build_trace: walk %.1f ms, pool %.1f ms, rebase %.1f ms, carry %.1f ms, finish %.1f ms\n",
+                 (tp[1] - tp[0]) * 1e3, (tp[2] - tp[1]) * 1e3, (tp[3] - tp[2]) * 1e3, (tp[4] - tp[3]) * 1e3, (te - tp[4]) * 1e3);
+    return rc;
 }
 
 int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<NodeStream> &parts,

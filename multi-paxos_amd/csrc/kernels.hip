@@ -1962,7 +1962,8 @@ __global__ __launch_bounds__(256) void k_commit_check(DevView v)
     // the pair after's item words are in flight while a pair is checked, its flags one pair
     // ahead, so a pair waits only for its Values — the first commit's and the checked runs', four
     // runs per round trip, the first group issued with the first commits'.
-    // (r05: 289 -> see profiles/r05_* for contended C5, 80 k pairs; the serial chain took 5 round trips)
+    // (Since ingest marks only the re-commits whose Values differ, FR_VCHK, valid traces put no pair
+    // here and the kernel is not launched, any_vchk; it runs on violation traces, the goldens.)
     auto words = [&](uint64_t x) -> uint64_t { return x < n_chk && lane < CHK_WORDS ? v.gp_chk[CHK_WORDS * x + lane] : 0; };
     struct Desc { uint64_t fw0, fw1; };
     auto descr = [&](uint64_t w) -> Desc {
