@@ -1136,6 +1136,36 @@ struct Walk {
 
 // Everything after the walk over the nodes' records: the vote lists, the run / event CSRs, the
 // work lists, the scan chunks, and (a window) the carry, committed only when every check passed.
+// FR_VEQ: every slot a commit / learn / accept run covers that an earlier commit / learn of its
+// pair fixed holds the same Value through the run's entry (or the same entry). A committed slot's
+// entry is its first commit run's in message order — accepts never replace it, member Acceptor
+// resets keep it — so this is static, and the walks (k_apply) skip their Value compare there
+// (two dependent loads per slot: contended C5's rivals re-learn equal Values under their own ids,
+// through other entries, on most slots of their walked pairs).
+static void mark_equal_values(HostTrace &ht, uint64_t p0, uint64_t p1)
+{
+    std::vector<int64_t> fix(BS);
+    for (uint64_t p = p0; p < p1; ++p) {
+        const uint64_t f0 = ht.f_off[p], f1 = ht.f_off[p + 1];
+        std::fill(fix.begin(), fix.end(), -1);
+        for (uint64_t f = f0; f < f1; ++f) {
+            Frag &fr = ht.frags[f];
+            const uint32_t kind = fr.flags >> 4;
+            if (kind != K_ACCEPT && kind != K_COMMIT) continue;
+            const bool dense = fr.flags & FR_DENSE;
+            bool eq = true;
+            for (uint32_t d = 0; d < fr.count; ++d) {
+                const uint64_t x = fr.entry + d;
+                const uint32_t s = dense ? fr.start + d : (uint32_t)((ht.e_iid[x] - ht.shard_begin) & (BS - 1));
+                const int64_t j = fix[s];
+                if (j >= 0 && (uint64_t)j != x && ht.e_val[j] != ht.e_val[x]) eq = false;
+                if (kind == K_COMMIT && j < 0) fix[s] = (int64_t)x;
+            }
+            if (eq) fr.flags |= FR_VEQ;
+        }
+    }
+}
+
 static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_t sb, uint64_t slen, bool member,
                         WindowCarry *wc, uint32_t threads)
 {
@@ -1217,7 +1247,12 @@ static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_
     ht.frags.resize(fr.size());
     scatter(fr.size(), (uint64_t)N * NB, ht.f_off, [&](size_t i) { return fr[i].key; },
             [&](size_t i, uint64_t at) { ht.frags[at] = fr[i].f; });
-    if (!wc) mark_value_checks(ht, member);
+    if (!wc) {
+        mark_value_checks(ht, member);
+        const uint64_t NP = (uint64_t)N * NB;
+        const uint32_t P = NP < 4096 ? 1 : T;
+        parallel(P, [&](uint32_t k) { mark_equal_values(ht, NP * k / P, NP * (k + 1) / P); });
+    }
     ht.cf_off.assign(NB + 1, 0);
     for (uint64_t i = 0; i < NB; ++i) {
         ht.cf_off[i + 1] = ht.cf_off[i] + cfcount[i];

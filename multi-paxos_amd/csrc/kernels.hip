@@ -2391,7 +2391,8 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                 if (k[j] < 0) continue;
                                 const uint32_t x = (uint32_t)(ent + k[j]);
                                 if (SF(j) & S_COMMITTED) {
-                                    if (se[j] != x && e_val[se[j]] != e_val[x] && (!learn || (mf & F_PROP)))
+                                    // (FR_VEQ: ingest found every such Value equal — no loads)
+                                    if (!(fl & FR_VEQ) && se[j] != x && e_val[se[j]] != e_val[x] && (!learn || (mf & F_PROP)))
                                         record_violation(v, MPX_V_LEARN_VALUE, n, seq, v.shard_begin + li0 + lane + 64 * j);
                                 } else if (learn) {
                                     if (DIGEST) sb[j] = v.e_pid[x];
@@ -2420,7 +2421,7 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             if (k[j] >= 0) {
                                 const uint32_t x = (uint32_t)(ent + k[j]);
                                 if (SF(j) & S_COMMITTED) {                            // :1508
-                                    if (se[j] != x && e_val[se[j]] != e_val[x])
+                                    if (!(fl & FR_VEQ) && se[j] != x && e_val[se[j]] != e_val[x])
                                         record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
                                                          v.shard_begin + li0 + lane + 64 * j);
                                 } else {

@@ -145,7 +145,9 @@ enum : uint8_t { K_ACCEPT = 0, K_COMMIT = 1, K_PREPLY = 2, K_BATCH = 3 };
 // earlier in its pair through another entry holding another Value — the Value check
 // (k_commit_check) may find a violation there (equal Values through another entry cannot).
 // (flags bit 1 stays free: k_plan_list's staged words carry F_GRANTED in it, MP_GRANTED)
-enum : uint8_t { FR_DENSE = 1, FR_VCHK = 4 };
+// FR_VEQ (ingest): every slot the run meets that an earlier commit / learn of its pair fixed holds
+// an equal Value — the walks (k_apply) skip their Value compare (ingest.cpp mark_equal_values).
+enum : uint8_t { FR_DENSE = 1, FR_VCHK = 4, FR_VEQ = 8 };
 
 struct Frag {
     uint64_t entry;      // first entry in its pool

@@ -9,7 +9,8 @@
 //      earlier commit / learn of the pair fixed through another entry index holding another Value
 //      (the re-commits the device's Value check could find different), on the pairs k_plan_list
 //      can plan;
-//   3. aliasing took effect: no unmarked run names other entries than its slot's fixing run.
+//   3. aliasing took effect: no unmarked run names other entries than its slot's fixing run;
+//   4. FR_VEQ is set exactly on the runs whose every earlier-committed slot holds an equal Value.
 // Prints "ok <runs> <aliased> <marked>" or the first failure.
 #include <cstdio>
 #include <cstdlib>
@@ -72,7 +73,7 @@ int main(int argc, char **argv)
     rc = build_trace(nodes, 0, M, member ? ep : std::vector<mpx_epoch>(), h);
     if (rc) { std::printf("FAIL build rc %d\n", rc); return 1; }
     const uint64_t NP = (uint64_t)N * h.NB;
-    uint64_t runs = 0, aliased = 0, marked = 0;
+    uint64_t runs = 0, aliased = 0, marked = 0, veq = 0;
     std::vector<int64_t> fix(BS);
     for (uint64_t q = 0; q < NP; ++q) {
         const uint64_t f0 = h.f_off[q], f1 = h.f_off[q + 1], bk = q / N;
@@ -124,7 +125,29 @@ int main(int argc, char **argv)
                 for (uint32_t d = 0; d < fr.count; ++d)
                     if (fix[fr.start + d] < 0) fix[fr.start + d] = (int64_t)(fr.entry + d);
         }
+        // 4. FR_VEQ on every accept / commit run (dense or sparse): set exactly when each slot it
+        //    covers that an earlier commit of the pair fixed holds the same Value through its entry
+        std::vector<int64_t> fx(BS, -1);
+        for (uint64_t f = f0; f < f1; ++f) {
+            const Frag &fr = h.frags[f];
+            const uint32_t kind = fr.flags >> 4;
+            if (kind != K_ACCEPT && kind != K_COMMIT) continue;
+            bool eq = true;
+            for (uint32_t d = 0; d < fr.count; ++d) {
+                const uint64_t x = fr.entry + d;
+                const uint32_t sl = (fr.flags & FR_DENSE) ? fr.start + d : (uint32_t)(h.e_iid[x] & (BS - 1));
+                if (fx[sl] >= 0 && (uint64_t)fx[sl] != x && h.e_val[fx[sl]] != h.e_val[x]) eq = false;
+                if (kind == K_COMMIT && fx[sl] < 0) fx[sl] = (int64_t)x;
+            }
+            veq += eq;
+            if (eq != ((fr.flags & FR_VEQ) != 0)) {
+                std::printf("FAIL equal-Value mark pair %llu run %llu: FR_VEQ %d, want %d\n", (unsigned long long)q,
+                            (unsigned long long)(f - f0), (int)((fr.flags & FR_VEQ) != 0), (int)eq);
+                return 1;
+            }
+        }
     }
-    std::printf("ok %llu %llu %llu\n", (unsigned long long)runs, (unsigned long long)aliased, (unsigned long long)marked);
+    std::printf("ok %llu %llu %llu %llu\n", (unsigned long long)runs, (unsigned long long)aliased, (unsigned long long)marked,
+                (unsigned long long)veq);
     return 0;
 }
