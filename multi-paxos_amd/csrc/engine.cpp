@@ -105,6 +105,7 @@ struct mpx_engine {
     uint64_t num_frags = 0;
     DevBuf b_msg, b_pstart, b_rep_off, b_rep, b_chosen, cf_off, cfrags;
     DevBuf st, st_valid, chosen, chosen_valid, plan, fast_rest, store_dummy, exec_aux, exec_out;
+    DevBuf f_pid;                           // per run: an FR_UPID promise-reply run's proposal id
     DevBuf gp_dyn, gp_dyn_n;                // list plan path: the pairs k_plan_list lists for k_apply
     DevBuf gp_ext, gp_ext_n;                //   ... and those it describes by 5..8 segments (k_store_ext)
     DevBuf gp_chk, gp_chk_n;                //   ... and its planned pairs whose re-commits need the Value check
@@ -595,7 +596,7 @@ static int upload_trace(mpx_engine *e)
     TRY(upload(e->e_val, h.e_val, s)); TRY(upload(e->e_slot, h.e_slot, s));
     TRY(upload(e->r_pid, h.r_pid, s)); TRY(upload(e->r_val, h.r_val, s)); TRY(upload(e->r_slot, h.r_slot, s));
     TRY(upload(e->g_a, h.g_a, s)); TRY(upload(e->g_b, h.g_b, s));
-    TRY(upload(e->f_off, h.f_off, s)); TRY(upload(e->frags, h.frags, s));
+    TRY(upload(e->f_off, h.f_off, s)); TRY(upload(e->frags, h.frags, s)); TRY(upload(e->f_pid, h.f_pid, s));
     {   // work items of the general k_apply: {f_off[q], f_off[q + 1], ev_off[q], ev_off[q + 1], q}
         std::vector<uint64_t> gd(GP_WORDS * h.gp_list.size(), 0);
         for (size_t i = 0; i < h.gp_list.size(); ++i) {
@@ -688,7 +689,7 @@ static int upload_trace(mpx_engine *e)
     v.e_val = e->e_val.as<uint64_t>(); v.e_slot = e->e_slot.as<uint8_t>();
     v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
-    v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
+    v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>(); v.f_pid = e->f_pid.as<uint64_t>();
     e->num_frags = h.frags.size();
     v.num_gp = h.gp_list.size(); v.gp_list = e->gp_list.as<uint64_t>(); v.num_gp_simple = h.num_gp_simple; v.num_gp_snap = h.num_gp_snap;
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>(); v.ev_aux = e->ev_aux.as<uint64_t>();
@@ -2726,6 +2727,8 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
+    TRY(e->f_pid.alloc(8));                          // (no promise-reply runs: never read)
+    v.f_pid = e->f_pid.as<uint64_t>();
     e->num_frags = f_off[N * NB];
     v.num_gp = gd.size() / GP_WORDS; v.gp_list = e->gp_list.as<uint64_t>(); v.num_gp_simple = 0; v.num_gp_snap = 0;
     v.ev_off = e->ev_off.as<uint64_t>(); v.ev_msg = e->ev_msg.as<uint32_t>(); v.ev_aux = e->ev_aux.as<uint64_t>();

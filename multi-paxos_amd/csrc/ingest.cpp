@@ -1166,6 +1166,20 @@ static void mark_equal_values(HostTrace &ht, uint64_t p0, uint64_t p1)
     }
 }
 
+// FR_UPID / f_pid: a promise-reply run whose entries all carry one proposal id (typically every
+// instance of it accepted by one ACCEPT) gives the promise-round walk that id with its descriptor
+static void mark_uniform_pids(HostTrace &ht, uint64_t f0, uint64_t f1)
+{
+    for (uint64_t f = f0; f < f1; ++f) {
+        Frag &fr = ht.frags[f];
+        if ((fr.flags >> 4) != K_PREPLY || !fr.count) continue;
+        const uint64_t p0 = ht.r_pid[fr.entry];
+        bool u = true;
+        for (uint32_t d = 1; d < fr.count && u; ++d) u = ht.r_pid[fr.entry + d] == p0;
+        if (u) { fr.flags |= FR_UPID; ht.f_pid[f] = p0; }
+    }
+}
+
 static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_t sb, uint64_t slen, bool member,
                         WindowCarry *wc, uint32_t threads)
 {
@@ -1252,6 +1266,10 @@ static int finish_trace(HostTrace &ht, Walk &W, uint32_t N, uint64_t NB, uint64_
         const uint64_t NP = (uint64_t)N * NB;
         const uint32_t P = NP < 4096 ? 1 : T;
         parallel(P, [&](uint32_t k) { mark_equal_values(ht, NP * k / P, NP * (k + 1) / P); });
+        ht.f_pid.assign(ht.frags.size(), 0);
+        const uint64_t NF = ht.frags.size();
+        const uint32_t PF = NF < 4096 ? 1 : T;
+        parallel(PF, [&](uint32_t k) { mark_uniform_pids(ht, NF * k / PF, NF * (k + 1) / PF); });
     }
     ht.cf_off.assign(NB + 1, 0);
     for (uint64_t i = 0; i < NB; ++i) {

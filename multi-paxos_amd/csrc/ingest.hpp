@@ -228,6 +228,7 @@ struct HostTrace {
     bool any_sparse = false;
     std::vector<uint64_t> f_off;
     std::vector<Frag> frags;
+    std::vector<uint64_t> f_pid;                    // per run: the common proposal id of an FR_UPID promise-reply run
     std::vector<uint64_t> gp_list;                  // (node, bucket) pairs for the general apply kernel
     uint64_t num_gp_simple = 0;                     // ... the first of them: no events, no promise-reply runs
     uint64_t num_gp_snap = 0;                       // ... then up to here: no promise-reply runs

@@ -2275,13 +2275,16 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
         return v.gp_list[GP_WORDS * i + lane];          // lanes 0..4: fi, fe, ei, ee, q
     };
     // the event window carries each event's aux word (PREPARE: its ranges in the bucket)
-    struct Win { uint64_t fw0, fw1; uint32_t evm; uint64_t eax; };
+    // (ROUNDS: with each run's uniform proposal id, f_pid, so a promise-reply run whose entries
+    // share one — FR_UPID — merges without loading its slots' ids)
+    struct Win { uint64_t fw0, fw1; uint32_t evm; uint64_t eax; uint64_t fpid; };
     auto rt2 = [&](uint64_t off) -> Win {
-        Win w{0, NONE32, NONE32, 0};
+        Win w{0, NONE32, NONE32, 0, 0};
         const uint64_t fi = rl64(off, 0), fe = rl64(off, 1), ei = rl64(off, 2), ee = rl64(off, 3);
         if (lane < fe - fi && lane < 64) {
             const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
             w.fw0 = x.x; w.fw1 = x.y;
+            if (ROUNDS) w.fpid = v.f_pid[fi + lane];
         }
         if (!SIMPLE && lane < ee - ei && lane < 64) { w.evm = v.ev_msg[ei + lane]; w.eax = v.ev_aux[ei + lane]; }
         return w;
@@ -2327,19 +2330,20 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
             const uint32_t ne = SIMPLE ? 0 : (uint32_t)(ee - ei < 64 ? ee - ei : 64);
             // descriptors (one per lane) and their scan flags: the pipelined
             // first window, then loaded here for the rare longer pairs
-            uint64_t fw0 = win.fw0, fw1 = win.fw1, eax = win.eax;
+            uint64_t fw0 = win.fw0, fw1 = win.fw1, eax = win.eax, fpid = win.fpid;
             uint32_t evm = win.evm;
             uint32_t fflag = flg.fflag, einfo = flg.einfo;
             uint64_t fbal = flg.fbal;
             if (!first) {
-                Win w2{0, NONE32, NONE32, 0};
+                Win w2{0, NONE32, NONE32, 0, 0};
                 if (lane < nf) {
                     const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(v.frags + fi + lane);
                     w2.fw0 = x.x; w2.fw1 = x.y;
+                    if (ROUNDS) w2.fpid = v.f_pid[fi + lane];
                 }
                 if (!SIMPLE && lane < ne) { w2.evm = v.ev_msg[ei + lane]; w2.eax = v.ev_aux[ei + lane]; }
                 const Flg f2 = rt3(w2);
-                fw0 = w2.fw0; fw1 = w2.fw1; evm = w2.evm; eax = w2.eax;
+                fw0 = w2.fw0; fw1 = w2.fw1; evm = w2.evm; eax = w2.eax; fpid = w2.fpid;
                 fflag = f2.fflag; einfo = f2.einfo; fbal = f2.fbal;
             }
             first = false;
@@ -2436,8 +2440,14 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             // runs' ids ahead, 1 or 2 deep, measured slower: C3 step 1.366 / 1.452 vs
                             // 1.270 ms — the registers spill; profiles/r04_v12_ab_preply_prefetch.json)
                             uint64_t pid[SPL];
+                            if (fl & FR_UPID) {                        // one id for the run, from the window
+                                const uint64_t pu = rl64(fpid, a);
 #pragma unroll
-                            for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
+                                for (uint32_t j = 0; j < SPL; ++j) pid[j] = pu;
+                            } else {
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
+                            }
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
                                 if (k[j] >= 0) {

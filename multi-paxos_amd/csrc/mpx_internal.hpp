@@ -147,7 +147,10 @@ enum : uint8_t { K_ACCEPT = 0, K_COMMIT = 1, K_PREPLY = 2, K_BATCH = 3 };
 // (flags bit 1 stays free: k_plan_list's staged words carry F_GRANTED in it, MP_GRANTED)
 // FR_VEQ (ingest): every slot the run meets that an earlier commit / learn of its pair fixed holds
 // an equal Value — the walks (k_apply) skip their Value compare (ingest.cpp mark_equal_values).
-enum : uint8_t { FR_DENSE = 1, FR_VCHK = 4, FR_VEQ = 8 };
+// FR_UPID (ingest, on a promise-reply run; the same bit as FR_VEQ, which only accept / commit runs
+// carry): every entry of the run has the same proposal id, f_pid[run] (the promise-round walk takes
+// it with the run's descriptor instead of loading each slot's id).
+enum : uint8_t { FR_DENSE = 1, FR_VCHK = 4, FR_VEQ = 8, FR_UPID = 8 };
 
 struct Frag {
     uint64_t entry;      // first entry in its pool
@@ -312,6 +315,7 @@ struct DevView {
     uint8_t *st_valid;              // per (node, bucket) pair: bucket * N + node (sv_idx)
     // chosen log: row N of st (per instance: the bucket's chosen fragment (cf_off) + 1)
     uint8_t *chosen_valid;          // per bucket
+    const uint64_t *f_pid;          // per run: its entries' common proposal id (FR_UPID promise-reply runs), else 0
     const uint64_t *frag_w1;        // frags[i]'s second word (message, count, start, flags): k_plan's
                                     // half of the descriptor, streamed without the entry words
     uint64_t *plan;                 // (N + 1) * NB: the segments k_store writes over a whole (row, bucket) (plan_idx),

@@ -59,7 +59,7 @@ static void compare(const HostTrace &a, const HostTrace &b)
     C(e_val); C(e_iid); C(e_pid); C(r_pid); C(r_val); C(r_iid); C(g_a); C(g_b); C(e_slot); C(r_slot);
     C(f_off); C(gp_list); C(ev_off); C(pl_off); C(ev_msg); C(pl_msg); C(ev_aux); C(pair_ev); C(pair_gp);
     C(b_msg); C(b_pstart); C(b_rep); C(b_rsrc); C(b_rbal); C(b_bal); C(b_aid); C(b_rep_off); C(cf_off);
-    C(b_gid); C(b_node); C(gp_base); C(cb_list);
+    C(b_gid); C(b_node); C(gp_base); C(cb_list); C(f_pid);
     cmpf("frags", a.frags, b.frags); cmpf("cfrags", a.cfrags, b.cfrags);
 #undef C
 }

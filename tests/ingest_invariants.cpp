@@ -10,7 +10,8 @@
 //      (the re-commits the device's Value check could find different), on the pairs k_plan_list
 //      can plan;
 //   3. aliasing took effect: no unmarked run names other entries than its slot's fixing run;
-//   4. FR_VEQ is set exactly on the runs whose every earlier-committed slot holds an equal Value.
+//   4. FR_VEQ is set exactly on the runs whose every earlier-committed slot holds an equal Value;
+//   5. FR_UPID is set exactly on the promise-reply runs whose entries share one proposal id (f_pid).
 // Prints "ok <runs> <aliased> <marked>" or the first failure.
 #include <cstdio>
 #include <cstdlib>
@@ -73,7 +74,7 @@ int main(int argc, char **argv)
     rc = build_trace(nodes, 0, M, member ? ep : std::vector<mpx_epoch>(), h);
     if (rc) { std::printf("FAIL build rc %d\n", rc); return 1; }
     const uint64_t NP = (uint64_t)N * h.NB;
-    uint64_t runs = 0, aliased = 0, marked = 0, veq = 0;
+    uint64_t runs = 0, aliased = 0, marked = 0, veq = 0, upid = 0;
     std::vector<int64_t> fix(BS);
     for (uint64_t q = 0; q < NP; ++q) {
         const uint64_t f0 = h.f_off[q], f1 = h.f_off[q + 1], bk = q / N;
@@ -146,8 +147,22 @@ int main(int argc, char **argv)
                 return 1;
             }
         }
+        // 5. FR_UPID on every promise-reply run: set exactly when its entries share one proposal id,
+        //    which f_pid holds for the run
+        for (uint64_t f = f0; f < f1; ++f) {
+            const Frag &fr = h.frags[f];
+            if ((fr.flags >> 4) != K_PREPLY || !fr.count) continue;
+            bool u = true;
+            for (uint32_t d = 1; d < fr.count; ++d) u = u && h.r_pid[fr.entry + d] == h.r_pid[fr.entry];
+            upid += u;
+            if (u != ((fr.flags & FR_UPID) != 0) || (u && h.f_pid[f] != h.r_pid[fr.entry])) {
+                std::printf("FAIL uniform-id mark pair %llu run %llu: FR_UPID %d, want %d\n", (unsigned long long)q,
+                            (unsigned long long)(f - f0), (int)((fr.flags & FR_UPID) != 0), (int)u);
+                return 1;
+            }
+        }
     }
-    std::printf("ok %llu %llu %llu %llu\n", (unsigned long long)runs, (unsigned long long)aliased, (unsigned long long)marked,
-                (unsigned long long)veq);
+    std::printf("ok %llu %llu %llu %llu %llu\n", (unsigned long long)runs, (unsigned long long)aliased,
+                (unsigned long long)marked, (unsigned long long)veq, (unsigned long long)upid);
     return 0;
 }

@@ -25,10 +25,11 @@ def checker(tmp_path_factory):
 def test_run_aliasing_and_value_check_marks(checker, kind, lg, proposers):
     r = subprocess.run([checker, kind, str(lg), str(proposers)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
-    runs, aliased, marked = map(int, r.stdout.split()[1:4])
-    assert runs > 0
+    runs, aliased, marked, veq, upid = map(int, r.stdout.split()[1:6])
+    assert runs > 0 and veq > 0
     if kind == "faulty":
         assert aliased > 0          # competing proposers' re-commits of equal Values share entries
+        assert upid > 0             # promise replies to a contending proposer's prepare
 
 
 # ---- membership learned at run time (MPX_FLAG_LEARN_EPOCHS, ingest.cpp EpochLearn) ----
