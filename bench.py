@@ -87,6 +87,11 @@ def parse():
                     help="also time rank 0's shard of the same trace at world G on this GPU (a 1-GPU scaling "
                          "projection, no RCCL); 0 / 1 = skip")
     ap.add_argument("--shard-only", action="store_true", help="only the shard projection (profiling)")
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="the full result (every leg's notes, per-window times) is written here; the JSON line on "
+                         "stdout carries the headline figures of every leg")
+    ap.add_argument("--leg-cpu-instances", type=int, default=1 << 17,
+                    help="instances of the sampled trace each leg's reference cpu_baseline replays")
     ap.add_argument("--events-every", type=int, default=8,
                     help="phase events (HIP start / stop timestamps on the kernels) on every k-th timed step of "
                          "the C4 and shard loops: each costs the step ~1.5-2 us (mpx_timing_every)")
@@ -392,6 +397,22 @@ def latest_pmc(n_nodes, instances, world, workload="C4"):
     return best
 
 
+def reference_c4(M, N, batch):
+    """The reference's own verdict on the clean trace (tests/golden/full_size.json "c4": multi/paxos.cpp's
+    handlers over 128 instance shards, oracle/ref_full_size.py) when this run is that configuration."""
+    path = os.path.join(ROOT, "tests", "golden", "full_size.json")
+    try:
+        c4 = json.load(open(path)).get("c4")
+    except (OSError, ValueError):
+        return None
+    if not c4:
+        return None
+    p = c4["params"]
+    if (p["num_instances"], p["num_nodes"], p["batch"]) != (M, N, batch):
+        return None
+    return c4["stats"]
+
+
 def clean_expect(n_nodes, sb, se, ballot=1 << 16):
     """(state_digest, chosen_digest) of the clean trace's final state over [sb, se) — closed form, oracle C."""
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libmpx_oracle.so"))
@@ -493,6 +514,84 @@ def cpu_baseline(args, budget_s):
                       "decisions/s = acceptor-instance applications/s / N=%d (%s)"
                       % (sample_m, reps, threads, dt, args.nodes, cpu_note()),
             "node_instance_apps_per_s": apps / dt}
+
+
+def leg_cpu_baseline(leg, instances=1 << 17):
+    """The reference's own handlers (oracle/_ref, -O2) on the leg's own generator configuration
+    (bench's C3 / C5 / C5C parameters and seed, sampled at `instances`), one forked process per
+    core the quota gives, each replaying the whole sampled trace (oracle/ref_leg_rate.py, run as a
+    child process: the reference's objects are not made for concurrent use in one process, and this
+    process holds the GPU).  Rank 0, N = 1, the default run only (not the --*-only profiling modes)."""
+    import subprocess
+    so = os.path.join(ROOT, "oracle", "_ref", "libmpx_ref.so" if leg == "c3" else "libmpx_ref_member.so")
+    if not os.path.exists(so):
+        return None
+    procs = cpu_threads()
+    cmd = [sys.executable, os.path.join(ROOT, "oracle", "ref_leg_rate.py"), leg, "--instances", str(instances),
+           "--procs", str(procs)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    if r.returncode:
+        log("%s cpu_baseline failed: %s" % (leg, r.stderr.strip()[-300:]))
+        return {"error": "rc %d" % r.returncode}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    fs = d.get("full_size_check")
+    return {"value": d["value"], "unit": "decisions/s", "cores": procs, "kind": "reference",
+            "sample": "reference %s handlers (-O2, oracle/_ref) over the leg's own generator configuration at "
+                      "%d instances (%d chosen, %.0f MB), %d processes each replaying the whole trace, slowest "
+                      "%.1f s (%s)" % ("member/paxos.cpp" if leg != "c3" else "multi/paxos.cpp", instances,
+                                       d["chosen"], d["trace_bytes"] / 1e6, procs, d["slowest_s"], cpu_note()),
+            "full_size_ref_per_core": fs["per_core"] if fs else None}
+
+
+def compact_leg(d):
+    """The leg's headline figures for the JSON line (the full leg goes to --detail)."""
+    if not d or "error" in d:
+        return d
+    r = d["roofline"]
+    out = {"ms_per_step": round(d["ms_per_step"], 4), "value": d["value"], "decisions_per_step": d["decisions_per_step"],
+           "kernel_ms": round(r["kernel_ms"], 4), "frac_hw": r["frac_hw"] and round(r["frac_hw"], 4),
+           "traffic": r["traffic"], "frac_survey_model": round(r["frac"], 3),
+           "frac_engine_model": round(r["frac_engine_model"], 4),
+           "verified": d["verified"]["step_state_digest_vs_run"]}
+    cb = d.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "error") if k in cb}
+        if cb.get("value"):
+            out["vs_cpu"] = round(d["value"] / cb["value"], 1)
+    w = d.get("windows")
+    if w:
+        out["windows"] = {"windows": w["windows"], "host_ms_per_window": round(w["host_ms_per_window"], 2),
+                          "submit_ms_per_window": round(w["submit_ms_per_window"], 2),
+                          "device_ms_per_window": round(w["device_ms_per_window"], 4), "value": w["value"],
+                          "value_device": w["value_device"], "kernel_ms": round(w["roofline"]["kernel_ms"], 4),
+                          "frac_hw": w["roofline"]["frac_hw"] and round(w["roofline"]["frac_hw"], 4),
+                          "verified": w["verified"]["digests_vs_batch_run"]}
+        for k in ("host_phases_ms",):
+            if k in w:
+                out["windows"][k] = w[k]
+    return out
+
+
+def log_leg(name, d):
+    if not d or "error" in d:
+        log("leg %s: %r" % (name, d))
+        return
+    r = d["roofline"]
+    cb = d.get("cpu_baseline") or {}
+    log("leg %s: ms_per_step %.4f, %.3f G decisions/s, apply kernel_ms %.4f, frac_hw %s, cpu_baseline %s" % (
+        name, d["ms_per_step"], d["value"] / 1e9, r["kernel_ms"],
+        "%.3f" % r["frac_hw"] if r["frac_hw"] else "null",
+        "%.3g decisions/s on %s cores (%s)" % (cb["value"], cb["cores"], cb["kind"]) if cb.get("value") else "none"))
+    w = d.get("windows")
+    if w:
+        log("leg %s.windows: host %.2f ms / window (submit %.2f), device %.4f ms, %.3g decisions/s end to end, "
+            "%.3g on the device, k_apply_win %.4f ms, frac_hw %s" % (
+                name, w["host_ms_per_window"], w["submit_ms_per_window"], w["device_ms_per_window"], w["value"],
+                w["value_device"], w["roofline"]["kernel_ms"],
+                "%.3f" % w["roofline"]["frac_hw"] if w["roofline"]["frac_hw"] else "null"))
 
 
 def native_oracle():
@@ -655,6 +754,18 @@ def main():
     step_ok = (step_state, step_chosen) == (want_state, want_chosen) and \
         st["accept_apps"] == N * (se - sb) == st["commit_apps"]
     assert step_ok, "the timed step's final state differs from the clean trace's closed form"
+    # (3) the reference's own handlers on the same C4 trace (oracle/ref_full_size.py: 128 instance
+    # shards of multi/paxos.cpp compiled in place, tests/golden/full_size.json["c4"]) — the shards'
+    # digests add up to the whole trace's (sums of per-entry hashes mod 2^64)
+    import struct
+    parts = pg.exchange(struct.pack("<QQ", step_state, step_chosen)) if pg is not None else \
+        [struct.pack("<QQ", step_state, step_chosen)]
+    tot_state = sum(struct.unpack("<QQ", b)[0] for b in parts) & ((1 << 64) - 1)
+    tot_chosen = sum(struct.unpack("<QQ", b)[1] for b in parts) & ((1 << 64) - 1)
+    ref_c4 = reference_c4(M, N, args.batch)
+    step_vs_ref = None if ref_c4 is None else \
+        (tot_state, tot_chosen) == (ref_c4["state_digest"], ref_c4["chosen_digest"])
+    assert step_vs_ref is not False, "the timed step's digests differ from the reference's own handlers"
     chk = eng.run()
     eng.timings()
     verified = (chk["state_digest"] == want_state and chk["chosen_digest"] == want_chosen and
@@ -686,7 +797,8 @@ def main():
     basis = ("pmc: %s traffic / this run's kernel_ms" % hw["source"]) if hw else \
         "engine_model (no PMC profile at this source digest): DESIGN.md §4 bytes / kernel_ms"
 
-    log("C4: %.4f ms per step over %d steps, verified %s" % (dt_max / args.steps * 1e3, args.steps, verified))
+    log("C4: %.4f ms per step over %d steps, verified %s (closed form), step digests vs the reference's own "
+        "handlers %s" % (dt_max / args.steps * 1e3, args.steps, verified, step_vs_ref))
     out = None
     if rank == 0:
         cpu = cpu_port = None
@@ -706,6 +818,13 @@ def main():
                 return {"error": repr(ex)}
         c5 = secondary("c5") if world == 1 and args.c5_instances else None
         c5c = secondary("c5c") if world == 1 and args.c5c_instances else None
+        # every leg's same-workload reference CPU rate
+        for name, leg in (("c3", c3), ("c5", c5), ("c5c", c5c)):
+            if leg and "error" not in leg and world == 1 and not args.no_cpu_baseline:
+                leg["cpu_baseline"] = leg_cpu_baseline(name, args.leg_cpu_instances)
+                if leg["cpu_baseline"] and leg["cpu_baseline"].get("value"):
+                    leg["vs_cpu"] = leg["value"] / leg["cpu_baseline"]["value"]
+            log_leg(name, leg)
         out = {
             "metric": METRIC,
             "value": value,
@@ -750,7 +869,8 @@ def main():
             "c3": c3,
             **({"c5": c5} if c5 else {}),
             **({"c5_contended": c5c} if c5c else {}),
-            "verified": {"step_state_digest_vs_closed_form": step_ok, "step_state_digest": step_state,
+            "verified": {"step_state_digest_vs_closed_form": step_ok, "step_digests_vs_reference": step_vs_ref,
+                         "step_state_digest": step_state,
                          "step_chosen_digest": step_chosen, "run_digests_vs_closed_form": verified,
                          "state_digest": chk["state_digest"], "chosen_digest": chk["chosen_digest"]},
             "hbm_gbps_alg_step": bytes_min * world / (dt_max / args.steps) / 1e9,
@@ -760,7 +880,34 @@ def main():
             "phase_events_every": max(args.events_every, 1),
             "trace_materialise_s": t_gen,
         }
-        print(json.dumps(out), flush=True)
+        if args.detail:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+                with open(args.detail, "w") as fh:
+                    json.dump(out, fh, indent=1)
+            except OSError as ex:
+                log("detail not written: %r" % ex)
+        # the JSON line: the contract's keys, the headline roofline and CPU baseline, then every
+        # leg's headline figures — short enough that a driver's tail of stdout holds all of it
+        keep_roof = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms",
+                     "bytes_alg_per_launch", "frac_engine_model", "frac_survey_model")
+        line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                    "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
+        line["roofline"] = dict({k: out["roofline"][k] for k in keep_roof},
+                                basis=out["roofline"]["basis"].split(" traffic")[0])
+        line["cpu_baseline"] = cpu
+        line["legs"] = {"c3": compact_leg(c3), "c5": compact_leg(c5), "c5_contended": compact_leg(c5c)}
+        if proj:
+            line["scaling_projection"] = {k: proj[k] for k in ("G", "T1_ms", "T_shard_ms", "eff", "verified")}
+        line["cpu_baseline_port"] = {k: cpu_port[k] for k in ("value", "unit", "cores", "kind")} if cpu_port else None
+        line["verified"] = {k: out["verified"][k] for k in ("step_state_digest_vs_closed_form",
+                                                            "run_digests_vs_closed_form")}
+        for k in ("step_digests_vs_reference",):
+            if k in out["verified"]:
+                line["verified"][k] = out["verified"][k]
+        line["phases_ms"] = {k: round(v, 4) for k, v in phases.items()}
+        line["detail"] = args.detail
+        print(json.dumps(line), flush=True)
     eng.close()
     if pg is not None:
         pg.close()

@@ -16,13 +16,14 @@
 //   * the executed Values (mpx_read_executed + mpx_value_bytes) go to StateMachine::Apply in
 //     instance order as each window makes them applicable — membership and noop Values are
 //     not passed, as Learner::Apply does not (:1062-1073);
-//   * Callback::Accepted / Applied from the learn bookkeeping (mpx_read_learns with
-//     MPX_FLAG_DECISIONS): a learn created at an accept quorum (kind 0) is the batch whose
-//     values Proposer::OnAcceptReply passes to Accepted (:1327-1332), and its applied point is
-//     where OnLearnReply passes them to Applied (:1360-1368); the batch's values are the host's
-//     own P_BATCH record of that accept id (the proposer's batches are the host's).
-//     Applied for learns a promise quorum or a learner change created (kinds 1, 2: every learned
-//     value re-sent) is not reported here.
+//   * Callback::Accepted / Applied / Unproposable from the learn bookkeeping (mpx_read_learns
+//     + mpx_read_learn_values with MPX_FLAG_DECISIONS): a learn created at an accept quorum (kind
+//     0) is the batch whose values Proposer::OnAcceptReply passes to Accepted (:1327-1332); a
+//     learn created at a promise quorum or a learner change (kinds 1, 2: the whole learned map,
+//     plus the open learns' values) passes its values to Applied at its applied record — an
+//     acceptor quorum of repliers, OnLearnReply or AcceptorsChanged (:1360-1368,1523-1526); a
+//     P_PROPOSE the node received without a Proposer is Unproposable (:784-787).  The cb strings
+//     come from the Values' own bytes (mpx_value_bytes).
 // It replays a member MPXT trace, dropping its E_EPOCH markers, in W windows (an incremental
 // engine: the OnReceive loop of a live host), and prints what the transport, the state machines
 // and the callbacks saw, plus the epochs the engine learned, so a test can compare them with the
@@ -111,7 +112,8 @@ class CountingCallback : public paxos::Callback {
 public:
     void Accepted(Thread *, const std::string &cb) { accepted.add(fnv(1469598103934665603ull, cb.data(), cb.size())); }
     void Applied(Thread *, const std::string &cb, const std::string *) { applied.add(fnv(1469598103934665603ull, cb.data(), cb.size())); }
-    Tally accepted, applied;
+    void Unproposable(Thread *, const std::string &cb) { unproposable.add(fnv(1469598103934665603ull, cb.data(), cb.size())); }
+    Tally accepted, applied, unproposable;
 };
 
 struct DrainCtx { std::vector<EngineNetWork *> *nets; };
@@ -122,36 +124,34 @@ void on_send(void *user, uint32_t src, uint32_t dst, const uint8_t *bytes, uint3
     (*c->nets)[src]->Send(nullptr, dst, std::string((const char *)bytes, len));
 }
 
-// the callback strings of a P_BATCH's values: {u32 type, u64 accept id, u32 len, {u64 iid, u64 pid,
-// Value_m}*}; Value_m = u32 proposer, u64 value_id, u8 noop [, u8 membership, u32 n, payload or n
-// changes, u32 cb length, cb] (FillValue, member/paxos.cpp:330-363), in instance order
-bool batch_cbs(const uint8_t *m, size_t len, uint64_t &aid, std::vector<std::string> &cbs)
+// the cb string of a member Value_m: u32 proposer, u64 value_id, u8 noop [, u8 membership, u32 n,
+// payload or n changes, u32 cb length, cb] (FillValue, member/paxos.cpp:330-363); "" for a noop
+bool value_cb(const uint8_t *v, size_t len, std::string &cb)
 {
-    if (len < 16) return false;
-    aid = rd<uint64_t>(m + 4);
-    const uint32_t vl = rd<uint32_t>(m + 12);
-    size_t p = 16, end = 16 + (size_t)vl;
-    if (end > len) return false;
-    std::map<uint64_t, std::string> byiid;
-    while (p < end) {
-        const uint64_t iid = rd<uint64_t>(m + p);
-        p += 16;
-        const bool noop = m[p + 12] != 0;
-        p += 13;
-        std::string cb;
-        if (!noop) {
-            const bool mem = m[p] != 0;
-            const uint32_t n = rd<uint32_t>(m + p + 1);
-            p += 5 + (mem ? 8 * (size_t)n : (size_t)n);
-            const uint32_t cl = rd<uint32_t>(m + p);
-            cb.assign((const char *)m + p + 4, cl);
-            p += 4 + cl;
-        }
-        if (!noop) byiid[iid] = cb;
+    cb.clear();
+    if (len < 13) return false;
+    if (v[12]) return true;
+    if (len < 18) return false;
+    const bool mem = v[13] != 0;
+    const uint32_t n = rd<uint32_t>(v + 14);
+    const size_t p = 18 + (mem ? 8 * (size_t)n : (size_t)n);
+    if (p + 4 > len) return false;
+    const uint32_t cl = rd<uint32_t>(v + p);
+    if (p + 4 + cl > len) return false;
+    cb.assign((const char *)v + p + 4, cl);
+    return true;
+}
+
+bool handle_cb(mpx_engine *eng, uint64_t h, std::string &cb)
+{
+    std::vector<uint8_t> buf(256);
+    uint32_t len = 0;
+    if (mpx_value_bytes(eng, h, buf.data(), (uint32_t)buf.size(), &len)) return false;
+    if (len > buf.size()) {
+        buf.resize(len);
+        if (mpx_value_bytes(eng, h, buf.data(), (uint32_t)buf.size(), &len)) return false;
     }
-    cbs.clear();
-    for (auto &x : byiid) cbs.push_back(x.second);
-    return p == end;
+    return value_cb(buf.data(), len, cb);
 }
 
 }  // namespace
@@ -196,13 +196,11 @@ int main(int argc, char **argv)
         pos = body[n] + ((nb + 7) & ~7ull);
     }
     DrainCtx ctx{&nets};
-    // per node: accept id -> its P_BATCH records {stream position, callback strings}; a new Proposer
-    // numbers its batches from 1 again, so a learn takes the last one before it was created.  The
-    // engine's record indices count its own E_EPOCH records, which it places where the reference
+    // The engine's record indices count its own E_EPOCH records, which it places where the reference
     // applies a membership Value — here, where the trace's markers were: positions count them too
-    std::vector<std::map<uint64_t, std::vector<std::pair<uint64_t, std::vector<std::string>>>>> batches(N);
     std::vector<uint64_t> applied_sm(N, 0);          // executed values handed to Apply so far
     std::vector<std::map<uint64_t, std::pair<bool, bool>>> seen(N);   // learn -> (accepted, applied) reported
+    std::vector<uint64_t> unprop_seen(N, 0);         // Unproposable records reported
     std::vector<uint32_t> epochs_after;              // the learned table's size after each window
     for (uint32_t w = 0; w < W; ++w) {
         for (uint32_t n = 0; n < N; ++n) {
@@ -212,12 +210,6 @@ int main(int argc, char **argv)
                 const uint8_t *m = tb + body[n] + a;
                 const uint32_t type = rd<uint32_t>(m);
                 if (type == MPX_MSG_E_EPOCH) continue;            // the engine learns the membership itself
-                if (type == MPX_MSG_P_BATCH) {                    // the host's own batch: its callbacks
-                    uint64_t aid = 0;
-                    std::vector<std::string> c;
-                    if (!batch_cbs(m, b - a, aid, c)) { std::fprintf(stderr, "bad P_BATCH\n"); return 1; }
-                    batches[n][aid].emplace_back(k, c);
-                }
                 nets[n]->Receive(std::string((const char *)m, b - a));
             }
             if ((rc = nets[n]->Flush())) { std::fprintf(stderr, "mpx_submit: %d\n", rc); return 1; }
@@ -240,29 +232,47 @@ int main(int argc, char **argv)
             }
             applied_sm[n] = c;
         }
-        // Callback::Accepted / Applied from the learns (MPXL) this window created or applied
-        uint8_t *ml = nullptr;
-        uint64_t ms = 0;
+        // Callback::Accepted / Applied / Unproposable from the learns (MPXL) and their Values (MPXV)
+        // this window created or applied
+        uint8_t *ml = nullptr, *mv = nullptr;
+        uint64_t ms = 0, mvs = 0;
         if ((rc = mpx_read_learns(eng, &ml, &ms))) { std::fprintf(stderr, "mpx_read_learns: %d\n", rc); return 1; }
-        size_t p = 12;
+        if ((rc = mpx_read_learn_values(eng, &mv, &mvs))) { std::fprintf(stderr, "mpx_read_learn_values: %d\n", rc); return 1; }
+        size_t p = 12, q = 12;
+        std::string cb;
         for (uint32_t n = 0; n < N; ++n) {
             const uint64_t nl = rd<uint64_t>(ml + p);
-            p += 8;
+            if (rd<uint64_t>(mv + q) != nl) { std::fprintf(stderr, "MPXV / MPXL differ\n"); return 1; }
+            p += 8; q += 8;
             for (uint64_t k = 0; k < nl; ++k, p += 64) {
-                const uint64_t created = rd<uint64_t>(ml + p + 8), kind = rd<uint64_t>(ml + p + 16);
-                const uint64_t aid = rd<uint64_t>(ml + p + 24), applied = rd<uint64_t>(ml + p + 32);
-                if (kind != 0) continue;
+                const uint64_t kind = rd<uint64_t>(ml + p + 16), applied = rd<uint64_t>(ml + p + 32);
+                const uint64_t nv = rd<uint64_t>(mv + q);
+                const uint8_t *vals = mv + q + 8;                    // {u64 iid, u64 handle}*
+                q += 8 + 16 * nv;
                 auto &s = seen[n][k];                                // (MPXL: every learn so far, in creation order)
-                auto it = batches[n].find(aid);
-                if (it == batches[n].end()) continue;
-                const std::vector<std::string> *vals = nullptr;
-                for (auto &b : it->second) if (b.first < created) vals = &b.second;
-                if (!vals) continue;
-                if (!s.first) { for (auto &cb : *vals) cbs[n].Accepted(nullptr, cb); s.first = true; }
-                if (!s.second && applied != ~0ull) { for (auto &cb : *vals) cbs[n].Applied(nullptr, cb, nullptr); s.second = true; }
+                const bool acc = kind == 0 && !s.first, app = kind != 0 && !s.second && applied != ~0ull;
+                if (!acc && !app) continue;
+                for (uint64_t j = 0; j < nv; ++j) {
+                    if (!handle_cb(eng, rd<uint64_t>(vals + 16 * j + 8), cb)) { std::fprintf(stderr, "bad Value\n"); return 1; }
+                    if (acc) cbs[n].Accepted(nullptr, cb);
+                    else cbs[n].Applied(nullptr, cb, nullptr);
+                }
+                (acc ? s.first : s.second) = true;
             }
+            const uint64_t nu = rd<uint64_t>(mv + q);
+            q += 8;
+            for (uint64_t j = unprop_seen[n]; j < nu; ++j) {          // the host's own P_PROPOSE record
+                const uint64_t k = rd<uint64_t>(mv + q + 8 * j);
+                if (k >= cnt[n]) { std::fprintf(stderr, "bad Unproposable record\n"); return 1; }
+                const uint64_t a = rd<uint64_t>(tb + offs[n] + 8 * k), b = rd<uint64_t>(tb + offs[n] + 8 * (k + 1));
+                if (b - a < 8 || !value_cb(tb + body[n] + a + 8, b - a - 8, cb)) { std::fprintf(stderr, "bad P_PROPOSE\n"); return 1; }
+                cbs[n].Unproposable(nullptr, cb);
+            }
+            unprop_seen[n] = nu;
+            q += 8 * nu;
         }
         mpx_free(ml);
+        mpx_free(mv);
         uint32_t ec = 0;
         if ((rc = mpx_read_epochs(eng, nullptr, 0, &ec))) return 1;
         epochs_after.push_back(ec);
@@ -273,9 +283,10 @@ int main(int argc, char **argv)
         if ((rc = mpx_read_executed(eng, n, &frontier, &c, nullptr, 0))) return 1;
         std::printf("applied %u %llu %llu %016llx\n", n, (unsigned long long)frontier, (unsigned long long)sms[n].count,
                     (unsigned long long)sms[n].hash);
-        std::printf("callbacks %u %llu %016llx %llu %016llx\n", n, (unsigned long long)cbs[n].accepted.count,
+        std::printf("callbacks %u %llu %016llx %llu %016llx %llu %016llx\n", n, (unsigned long long)cbs[n].accepted.count,
                     (unsigned long long)cbs[n].accepted.hash, (unsigned long long)cbs[n].applied.count,
-                    (unsigned long long)cbs[n].applied.hash);
+                    (unsigned long long)cbs[n].applied.hash, (unsigned long long)cbs[n].unproposable.count,
+                    (unsigned long long)cbs[n].unproposable.hash);
     }
     uint32_t ec = 0;
     mpx_read_epochs(eng, nullptr, 0, &ec);

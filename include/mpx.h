@@ -456,6 +456,18 @@ int  mpx_read_commits_sharded(mpx_engine *eng, uint8_t **out, uint64_t *size);
  * node's stream.  *out is malloc'ed; free with mpx_free.  MPX_E_STATE for multi
  * semantics, a shard engine or an E_EPOCH step that both adds and removes roles. */
 int  mpx_read_learns(mpx_engine *eng, uint8_t **out, uint64_t *size);
+/* The Values of the same learns, for the host's paxos::Callback (member/paxos.h:142-164):
+ * LearningValues::values_ in instance order — kind 0: the chosen batch (the cb strings
+ * Callback::Accepted receives at creation, :1327-1332); kinds 1 and 2: the node's Learner's
+ * learned values at creation (:1299-1301, :1476), kind 2 with every open learn's values
+ * added (std::map::insert, id order, :1477-1482) — what Applied receives at applied_seq
+ * (:1360-1368, :1523-1526); and the records where a P_PROPOSE found the node without a
+ * Proposer (Node::Propose -> Callback::Unproposable, NodeImpl::Loop :784-787).  Format MPXV:
+ * "MPXV" u32 1, u32 nodes; per node u64 count (= MPXL's), per learn {u64 n, n x {u64 iid,
+ * u64 handle}}, then u64 u, u x u64 unproposable_seq.  Replaces the reference's
+ * Callback calls from Proposer::OnAcceptReply / OnLearnReply / AcceptorsChanged (member/
+ * paxos.cpp:1317-1381,1504-1533).  Same state requirements as mpx_read_learns. */
+int  mpx_read_learn_values(mpx_engine *eng, uint8_t **out, uint64_t *size);
 /* Encoded reference Value bytes (multi/paxos.cpp:556-598) for a handle. */
 int  mpx_value_bytes(mpx_engine *eng, uint64_t handle, uint8_t *buf,
                      uint32_t cap, uint32_t *len);

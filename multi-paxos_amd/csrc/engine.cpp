@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <functional>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -146,7 +147,8 @@ struct mpx_engine {
     DevBuf b_gid, b_node, g_mask, g_done, gp_base, cb_list, outv, outv_n, ee_init, ee_out;
     bool ee_ready = false;                  // member: ee_init holds the roles the next window starts from
     uint64_t consumed = 0;                  // windows whose records build_trace took (the carry moved past them)
-    bool poisoned = false;                  // a window failed after it was consumed: state undefined
+    bool poisoned = false;                  // a window failed after it was consumed, or a LEARN_EPOCHS submit
+                                            // failed mid-stream: state undefined, every later call MPX_E_STATE
     uint64_t g_cap = 0;                     // global batches g_mask / g_done hold
     std::vector<uint64_t> seq_base, win_seq_base;
     std::vector<PropNode> *prop = nullptr;           // MPX_FLAG_DECISIONS: the bookkeeping carried across windows
@@ -280,18 +282,25 @@ extern "C" int mpx_destroy(mpx_engine *e)
 // MPX_FLAG_LEARN_EPOCHS: the epochs each node reached (EpochLearn::steps) extend the table;
 // nodes apply the same membership Values in the same instance order, so a node's k-th step
 // must equal every other node's (the reference's safety: one chosen Value per instance)
+// (every node is checked against the table and against the longest node before anything is
+// appended, so a disagreement leaves the table as it was)
 static int merge_epochs(mpx_engine *e)
 {
+    auto same = [](const mpx_epoch &a, const mpx_epoch &b) {
+        return a.version == b.version && a.acceptor_mask == b.acceptor_mask && a.proposer_mask == b.proposer_mask &&
+               a.learner_mask == b.learner_mask;
+    };
+    const EpochLearn *longest = nullptr;
+    for (const EpochLearn &l : e->elearn)
+        if (!longest || l.steps.size() > longest->steps.size()) longest = &l;
+    if (!longest) return MPX_OK;
     for (const EpochLearn &l : e->elearn)
         for (size_t k = 0; k < l.steps.size(); ++k) {
-            if (k + 1 < e->epochs.size()) {
-                const mpx_epoch &a = e->epochs[k + 1], &b = l.steps[k];
-                if (a.version != b.version || a.acceptor_mask != b.acceptor_mask || a.proposer_mask != b.proposer_mask ||
-                    a.learner_mask != b.learner_mask) return MPX_E_STATE;
-            } else {
-                e->epochs.push_back(l.steps[k]);
-            }
+            if (k + 1 < e->epochs.size() && !same(e->epochs[k + 1], l.steps[k])) return MPX_E_STATE;
+            if (!same(longest->steps[k], l.steps[k])) return MPX_E_STATE;
         }
+    for (size_t k = e->epochs.size() ? e->epochs.size() - 1 : 0; k < longest->steps.size(); ++k)
+        e->epochs.push_back(longest->steps[k]);
     return MPX_OK;
 }
 
@@ -318,9 +327,15 @@ extern "C" int mpx_submit(mpx_engine *e, uint32_t node, const uint8_t *bytes, co
         int rc = member ? decode_record_member(e->vt, ns, node, m, len, e->cfg.shard_begin, e->cfg.shard_end, e->iv,
                                                e->elearn.empty() ? nullptr : &e->elearn[node])
                         : decode_record(e->vt, ns, node, e->cfg.num_nodes, m, len, e->cfg.shard_begin, e->cfg.shard_end, e->iv);
-        if (rc) return rc;
+        if (rc) {
+            // MPX_FLAG_LEARN_EPOCHS: the Learner's apply frontier, the node's view and its placed
+            // E_EPOCH records may already have moved past the failing record: no
+            // later call may run on that half-learned state
+            if (!e->elearn.empty()) e->poisoned = true;
+            return rc;
+        }
     }
-    TRY(merge_epochs(e));
+    if (int rc = merge_epochs(e)) { e->poisoned = true; return rc; }
     e->dirty = true;
     e->stats.ingest_ns += now_ns() - t0;
     return MPX_OK;
@@ -413,10 +428,13 @@ static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, cons
     const uint64_t t0 = now_ns();
     std::vector<StreamSlice> sl(N);
     for (uint32_t n = 0; n < N; ++n) sl[n].cnt = stream(n, sl[n].offs, sl[n].bytes);
-    TRY(decode_parallel(e->vt, e->nodes, e->parts, sl, e->cfg.semantics == MPX_SEM_MEMBER,
-                        e->elearn.empty() ? nullptr : &e->elearn, e->cfg.shard_begin, e->cfg.shard_end, e->iv,
-                        std::max(1u, std::min(16u, std::thread::hardware_concurrency())), 0));
-    TRY(merge_epochs(e));
+    if (int rc = decode_parallel(e->vt, e->nodes, e->parts, sl, e->cfg.semantics == MPX_SEM_MEMBER,
+                                 e->elearn.empty() ? nullptr : &e->elearn, e->cfg.shard_begin, e->cfg.shard_end, e->iv,
+                                 std::max(1u, std::min(16u, std::thread::hardware_concurrency())), 0)) {
+        if (!e->elearn.empty()) e->poisoned = true;  // (see mpx_submit)
+        return rc;
+    }
+    if (int rc = merge_epochs(e)) { e->poisoned = true; return rc; }
     e->dirty = true;
     e->stats.ingest_ns += now_ns() - t0;
     return MPX_OK;
@@ -932,8 +950,8 @@ static int run_window(mpx_engine *e)
 extern "C" int mpx_run(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
+    if (e->poisoned) return MPX_E_STATE;            // (a failed window, or a failed LEARN_EPOCHS submit)
     if (e->incremental) {
-        if (e->poisoned) return MPX_E_STATE;
         const uint64_t before = e->consumed;
         const int rc = run_window(e);
         // a window that failed before build_trace took it leaves the engine as it was (the
@@ -949,7 +967,7 @@ extern "C" int mpx_run(mpx_engine *e)
 extern "C" int mpx_step(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
-    if (e->incremental) return MPX_E_STATE;           // windows are applied once, not replayed
+    if (e->incremental || e->poisoned) return MPX_E_STATE;   // windows are applied once, not replayed
     return queue_run(e, false);
 }
 
@@ -2306,6 +2324,13 @@ struct LearnPlan {
     uint8_t facc;
     uint32_t end = NONE32;
     std::vector<uint64_t> ev_a, ev_m;
+    // its values_ (mpx_read_learn_values): kind 0 the batch's {iid, handle}; kinds 1 and 2 the
+    // Learner's learned values then — the first log_len of the node's learn log (:1299-1301,
+    // :1476) — and kind 2 also every open learn's values (`parents`, id order; one that had
+    // retired by then is skipped at read time, retirement being k_learns' finding, :1477-1482)
+    uint64_t log_len = 0;
+    std::vector<uint32_t> parents;
+    std::vector<std::pair<uint64_t, uint64_t>> batch;
 };
 
 // one node's walk state (carried across windows under MPX_FLAG_DECISIONS); `live` indexes
@@ -2315,6 +2340,11 @@ struct LearnNode {
     uint32_t ei = 0;
     uint64_t lid = 0, amask = 0, K = 0;                        // K: the last non-marker record
     std::vector<size_t> live;
+    // the Learner's learned_values_ (insert: the first Value of an instance sticks, :1040) in
+    // the order it learned them, and a bit per shard instance learned
+    std::vector<std::pair<uint64_t, uint64_t>> llog;
+    std::vector<uint64_t> lbits;
+    std::vector<uint64_t> unprop;                              // Unproposable P_PROPOSE records (:784-787)
 };
 struct LearnCarry {
     std::vector<LearnNode> nodes;
@@ -2328,11 +2358,23 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnNode> &n
     const HostTrace &h = e->ht;
     const uint32_t N = e->cfg.num_nodes;
     const auto &ep = e->epochs;
-    std::unordered_map<uint32_t, uint64_t> chosen_at;          // accept quorum message -> accept id
+    std::unordered_map<uint32_t, std::pair<uint64_t, uint32_t>> chosen_at;   // accept quorum message -> (accept id, batch)
     const bool aid = h.b_aid.size() == h.b_msg.size();         // (a window's earlier batches: carried ids)
     for (size_t j = 0; j < h.b_msg.size(); ++j)
         if (r.b_chosen[j] != NONE32 && (aid || h.b_msg[j] != NONE32))
-            chosen_at[r.b_chosen[j]] = aid ? h.b_aid[j] : h.m_aux[h.b_msg[j]];
+            chosen_at[r.b_chosen[j]] = {aid ? h.b_aid[j] : h.m_aux[h.b_msg[j]], (uint32_t)j};
+    // a chosen batch's values (its P_BATCH's entries; a window's earlier batch: the carried ones)
+    auto batch_values = [&](uint32_t j, std::vector<std::pair<uint64_t, uint64_t>> &v) {
+        const uint32_t g = h.b_msg[j];
+        if (g != NONE32) {
+            for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) v.push_back({h.e_iid[k], h.e_val[k]});
+        } else if (e->incremental && j < h.b_gid.size()) {
+            auto it = e->wc.b_ents.find(h.b_gid[j]);
+            if (it != e->wc.b_ents.end()) v = it->second;
+        }
+        std::sort(v.begin(), v.end());
+    };
+    const uint64_t lwords = (h.shard_len + 63) / 64;
     for (uint32_t n = 0; n < N; ++n) {
         LearnNode &st = nodes[n];
         if (!st.started) {
@@ -2347,6 +2389,7 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnNode> &n
         auto create = [&](uint64_t at, uint64_t kind, uint64_t src, bool facc) {
             LearnPlan p;
             p.node = n; p.id = ++lid; p.created = at; p.kind = kind; p.src = src; p.facc = facc;
+            p.log_len = st.llog.size();
             live.push_back(out.size());
             out.push_back(std::move(p));
         };
@@ -2363,13 +2406,27 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnNode> &n
             preparing = true;                                      // RestartPrepare / AcceptRejected
         };
         auto learners_changed = [&](uint64_t at) {                 // LearnersChanged (:1472-1502)
+            const std::vector<size_t> open = live;
             drop_all(at);
-            if (!preparing) create(at, 2, 0, true);
+            if (!preparing) {
+                create(at, 2, 0, true);
+                for (size_t x : open) out.back().parents.push_back((uint32_t)x);
+            }
+        };
+        // P_PROPOSE records are host bookkeeping only (not in the device's message arrays): merged
+        // in by record index, Node::Propose without a Proposer is Unproposable (NodeImpl::Loop, :784-787)
+        const uint64_t sbase = e->incremental ? e->win_seq_base[n] : 0;
+        uint64_t pp = n + 1 < h.prop_off.size() ? h.prop_off[n] : 0;
+        const uint64_t pe = n + 1 < h.prop_off.size() ? h.prop_off[n + 1] : 0;
+        auto proposes_before = [&](uint64_t k) {
+            for (; pp < pe && h.prop_seq[pp] + sbase < k; ++pp)
+                if (!prop) st.unprop.push_back(h.prop_seq[pp] + sbase);
         };
         for (uint64_t g = h.node_off[n]; g < h.node_off[n + 1]; ++g) {
             const uint8_t t = h.m_type[g];
-            const uint64_t k = seq_of(h, n, g) + (e->incremental ? e->win_seq_base[n] : 0);
+            const uint64_t k = seq_of(h, n, g) + sbase;
             if (k >= NONE32) return MPX_E_RANGE;
+            proposes_before(k);
             if (t != MPX_MSG_E_EPOCH) {
                 K = k;
                 if (idle) { preparing = false; idle = false; }     // after the marker run (below)
@@ -2379,7 +2436,10 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnNode> &n
                 if (learned_any) create(k, 1, 0, true);
             } else if (t == MPX_MSG_ACCEPT_REPLY) {
                 auto it = chosen_at.find((uint32_t)g);
-                if (it != chosen_at.end()) create(k, 0, it->second, false);   // OnAcceptReply (:1327-1342)
+                if (it != chosen_at.end()) {                       // OnAcceptReply (:1327-1342)
+                    create(k, 0, it->second.first, false);
+                    batch_values(it->second.second, out.back().batch);
+                }
             } else if (t == MPX_MSG_COMMIT_REPLY) {                // LEARN_REPLY -> OnLearnReply
                 if (!prop) continue;
                 if (h.m_src[g] >= 64) return MPX_E_RANGE;
@@ -2393,6 +2453,13 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnNode> &n
                 if (prop) preparing = true;
             } else if (t == MPX_MSG_COMMIT) {                      // LEARN (Learner::OnLearn, :1029-1060)
                 if (h.m_cnt[g]) learned_any = true;
+                if (h.m_cnt[g] && st.lbits.empty()) st.lbits.assign(lwords, 0);
+                for (uint64_t x = h.m_ent[g]; x < h.m_ent[g] + h.m_cnt[g]; ++x) {   // learned_values_.insert (:1040)
+                    const uint64_t li = h.e_iid[x] - h.shard_begin;
+                    if (li >= h.shard_len || (st.lbits[li >> 6] >> (li & 63) & 1)) continue;
+                    st.lbits[li >> 6] |= 1ull << (li & 63);
+                    st.llog.push_back({h.e_iid[x], h.e_val[x]});
+                }
             } else if (t == MPX_MSG_E_EPOCH) {
                 const uint32_t ej = h.m_ver[g];
                 if (ej >= ep.size()) return MPX_E_DECODE;
@@ -2421,30 +2488,43 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnNode> &n
                 ei = ej;
             }
         }
+        proposes_before(~0ull);
     }
     return MPX_OK;
 }
 
 static int learn_window(mpx_engine *e, const Results &r) { return learn_plan(e, r, e->lrn->nodes, e->lrn->plans); }
 
-extern "C" int mpx_read_learns(mpx_engine *e, uint8_t **out, uint64_t *size)
+// Every learn so far with what k_learns found for it: the plans (a whole engine walks its run
+// now; windows carry the walk, MPX_FLAG_DECISIONS) and, per plan, applied / retired / ended
+// record and the learned mask
+struct LearnsOut {
+    std::vector<LearnPlan> whole_lp;
+    std::vector<LearnNode> whole_nodes;
+    const std::vector<LearnPlan> *lp = nullptr;
+    const std::vector<LearnNode> *nodes = nullptr;
+    std::vector<uint32_t> applied, retired, ended;
+    std::vector<uint64_t> mask;
+};
+
+static int learns_compute(mpx_engine *e, LearnsOut &o)
 {
-    if (!e || !out || !size) return MPX_E_INVAL;
     if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (e->cfg.semantics != MPX_SEM_MEMBER || !e->whole) return MPX_E_STATE;
-    std::vector<LearnPlan> whole_lp;
     if (e->incremental) {                               // windows keep no history of runs, but
         if (!e->lrn) return MPX_E_STATE;                // MPX_FLAG_DECISIONS carries the walk
+        o.lp = &e->lrn->plans;
+        o.nodes = &e->lrn->nodes;
     } else {
         Results r;
         TRY(fetch_results(e, r));
-        std::vector<LearnNode> nodes(e->cfg.num_nodes);
-        TRY(learn_plan(e, r, nodes, whole_lp));
+        o.whole_nodes.assign(e->cfg.num_nodes, LearnNode());
+        TRY(learn_plan(e, r, o.whole_nodes, o.whole_lp));
+        o.lp = &o.whole_lp;
+        o.nodes = &o.whole_nodes;
     }
-    const std::vector<LearnPlan> &lp = e->incremental ? e->lrn->plans : whole_lp;
+    const std::vector<LearnPlan> &lp = *o.lp;
     const uint32_t L = (uint32_t)lp.size();
-    std::vector<uint32_t> applied, retired, ended;
-    std::vector<uint64_t> mask;
     if (L) {
         std::vector<uint64_t> ev_off(1, 0), ev_a, ev_m;
         std::vector<uint8_t> facc;
@@ -2467,8 +2547,17 @@ extern "C" int mpx_read_learns(mpx_engine *e, uint8_t **out, uint64_t *size)
                     d_mask.as<unsigned long long>()};
         if (launch_learns(e->view, s, a) != 0) return MPX_E_HIP;
         HTRY(hipStreamSynchronize(s));
-        TRY(d2h(applied, d_app, L)); TRY(d2h(retired, d_ret, L)); TRY(d2h(ended, d_endo, L)); TRY(d2h(mask, d_mask, L));
+        TRY(d2h(o.applied, d_app, L)); TRY(d2h(o.retired, d_ret, L)); TRY(d2h(o.ended, d_endo, L)); TRY(d2h(o.mask, d_mask, L));
     }
+    return MPX_OK;
+}
+
+extern "C" int mpx_read_learns(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    LearnsOut o;
+    TRY(learns_compute(e, o));
+    const std::vector<LearnPlan> &lp = *o.lp;
     const uint32_t N = e->cfg.num_nodes;
     std::vector<uint64_t> per(N, 0);
     for (auto &p : lp) per[p.node]++;
@@ -2481,9 +2570,60 @@ extern "C" int mpx_read_learns(mpx_engine *e, uint8_t **out, uint64_t *size)
         for (size_t l = 0; l < lp.size(); ++l) {
             if (lp[l].node != n) continue;
             app<uint64_t>(d, lp[l].id); app<uint64_t>(d, lp[l].created); app<uint64_t>(d, lp[l].kind);
-            app<uint64_t>(d, lp[l].src); app<uint64_t>(d, seq(applied[l])); app<uint64_t>(d, seq(retired[l]));
-            app<uint64_t>(d, seq(ended[l])); app<uint64_t>(d, mask[l]);
+            app<uint64_t>(d, lp[l].src); app<uint64_t>(d, seq(o.applied[l])); app<uint64_t>(d, seq(o.retired[l]));
+            app<uint64_t>(d, seq(o.ended[l])); app<uint64_t>(d, o.mask[l]);
         }
+    }
+    return put_bytes(d, out, size);
+}
+
+// The Values of every learn (LearningValues::values_, in instance order), what the Proposer's
+// Callback::Accepted (kind 0, at creation, :1327-1332) and Applied (kinds 1 and 2, at the applied
+// record, :1360-1368,1523-1526) iterate, and the records where Node::Propose found no Proposer
+// (Unproposable, :784-787).  Format MPXV (include/mpx.h).
+extern "C" int mpx_read_learn_values(mpx_engine *e, uint8_t **out, uint64_t *size)
+{
+    if (!e || !out || !size) return MPX_E_INVAL;
+    LearnsOut o;
+    TRY(learns_compute(e, o));
+    const std::vector<LearnPlan> &lp = *o.lp;
+    const std::vector<LearnNode> &nodes = *o.nodes;
+    // values_ of plan l: a kind-2 learn's map is the learned values, then each open learn's values
+    // inserted in id order (std::map::insert: the first Value of an instance stays, :1476-1482)
+    std::vector<std::unique_ptr<std::map<uint64_t, uint64_t>>> memo(lp.size());
+    std::function<const std::map<uint64_t, uint64_t> &(size_t)> values = [&](size_t l) -> const std::map<uint64_t, uint64_t> & {
+        if (memo[l]) return *memo[l];
+        auto m = std::make_unique<std::map<uint64_t, uint64_t>>();
+        const LearnPlan &p = lp[l];
+        if (p.kind == 0) {
+            for (auto &x : p.batch) m->insert(x);
+        } else {
+            const auto &lg = nodes[p.node].llog;
+            for (uint64_t k = 0; k < p.log_len && k < lg.size(); ++k) m->insert(lg[k]);
+            for (uint32_t q : p.parents)                 // (retired before it was created: gone by then)
+                if (o.retired[q] == NONE32 || o.retired[q] > p.created)
+                    for (auto &x : values(q)) m->insert(x);
+        }
+        memo[l] = std::move(m);
+        return *memo[l];
+    };
+    const uint32_t N = e->cfg.num_nodes;
+    std::string d;
+    d.append("MPXV", 4);
+    app<uint32_t>(d, 1); app<uint32_t>(d, N);
+    for (uint32_t n = 0; n < N; ++n) {
+        uint64_t per = 0;
+        for (auto &p : lp) per += p.node == n;
+        app<uint64_t>(d, per);
+        for (size_t l = 0; l < lp.size(); ++l) {
+            if (lp[l].node != n) continue;
+            const auto &m = values(l);
+            app<uint64_t>(d, m.size());
+            for (auto &x : m) { app<uint64_t>(d, x.first); app<uint64_t>(d, x.second); }
+        }
+        const auto &u = nodes[n].unprop;
+        app<uint64_t>(d, u.size());
+        for (uint64_t k : u) app<uint64_t>(d, k);
     }
     return put_bytes(d, out, size);
 }
@@ -2582,10 +2722,16 @@ extern "C" int mpx_trace_generate(const mpx_gen_params *p, uint8_t **out, uint64
     if (!p || !out || !size) return MPX_E_INVAL;
     std::string t;
     int rc;
-    if (p->kind == MPX_GEN_CLEAN) rc = gen_clean(*p, t);
-    else if (p->kind == MPX_GEN_FAULTY) rc = gen_faulty(*p, t);
-    else if (p->kind == MPX_GEN_MEMBER) rc = gen_member(*p, t);
-    else rc = MPX_E_INVAL;
+    try {                                            // (no C++ exception crosses the C ABI)
+        if (p->kind == MPX_GEN_CLEAN) rc = gen_clean(*p, t);
+        else if (p->kind == MPX_GEN_FAULTY) rc = gen_faulty(*p, t);
+        else if (p->kind == MPX_GEN_MEMBER) rc = gen_member(*p, t);
+        else rc = MPX_E_INVAL;
+    } catch (const std::bad_alloc &) {
+        return MPX_E_NOMEM;
+    } catch (const std::length_error &) {
+        return MPX_E_NOMEM;
+    }
     if (rc) return rc;
     *out = (uint8_t *)std::malloc(t.size());
     if (!*out) return MPX_E_NOMEM;

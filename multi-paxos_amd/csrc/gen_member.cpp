@@ -598,7 +598,11 @@ int gen_member(const mpx_gen_params &p, std::string &out)
     // instance, contended 152 B; pages are only touched as they are written): a stream that grew by
     // doubling copied itself and held both copies at once — 2^25 contended traces (41 GB) peaked
     // past 60 GB of resident memory that way
-    for (uint32_t n = 0; n < U; ++n) g.nd[n].bytes.reserve((size_t)std::min<uint64_t>(g.M, 1ull << 30) * (p.proposers > 1 ? 224 : 128));
+    // a first guess at each node's stream (it grows past it as needed), capped at 8 GB per node: an
+    // up-front reservation of M x 224 B is hundreds of GB at large M
+    for (uint32_t n = 0; n < U; ++n)
+        g.nd[n].bytes.reserve((size_t)std::min<uint64_t>(std::min<uint64_t>(g.M, 1ull << 30) * (p.proposers > 1 ? 224 : 128),
+                                                         8ull << 30));
     SimNode &L = g.nd[0];
     L.acc = true;
     L.learners = 1;

@@ -2565,7 +2565,13 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                             if (start[j]) {
                                 uint32_t p = lane + 64 * j + 1;                      // count the continuation bits after it
                                 while (p < BS) {
-                                    const uint64_t w = cm[p >> 6] >> (p & 63);
+                                    // (the word by an unrolled select, not cm[p >> 6]: a run-time index
+                                    // would put cm in scratch)
+                                    uint64_t cw = 0;
+#pragma unroll
+                                    for (uint32_t jj = 0; jj < SPL; ++jj)
+                                        if (jj == (p >> 6)) cw = cm[jj];
+                                    const uint64_t w = cw >> (p & 63);
                                     const uint32_t room = 64 - (p & 63);
                                     const uint32_t ones = ~w ? (uint32_t)__builtin_ctzll(~w) : 64;
                                     const uint32_t take = ones < room ? ones : room;
@@ -3697,8 +3703,6 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
                 hipLaunchKernelGGL(k_store_ext, dim3(g.chosen_wgs), dim3(256), 0, s, v);
 #endif
                 if (v.any_vchk) hipLaunchKernelGGL(k_commit_check<false>, dim3(g.apply_wgs), dim3(256), 0, s, v);
-            } else if (side3) {
-                (void)hipEventRecord((hipEvent_t)side.join3, s3);
             }
         }
         // every pair the trace marks lean (pair_gp 0) is one k_plan can describe (ingest.cpp /
@@ -3726,7 +3730,6 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
         // Occupancy (C3 2^24 general apply): AM_SNAP at 4 waves / SIMD 1.324 ms vs 1.469
         // unconstrained (3 waves) and 1.496 at 5 (spills); the full kernel at 4 waves 1.394 vs
         // 1.580 ms unconstrained; one kernel over the whole list 1.351 ms (C5: 2.165 vs 2.544 ms)
-        if (side3) (void)hipStreamWaitEvent(s, (hipEvent_t)side.join3, 0);   // (a multi plan path without list pairs)
         const uint64_t ns = v.num_gp_simple, nq = v.num_gp_snap;
         if (v.digest) {
             if (ns) { if (member) hipLaunchKernelGGL((k_apply<1, true, true, AM_SIMPLE>), dim3(g.apply_wgs), dim3(256), 0, s, v, 0ull, ns);

@@ -124,6 +124,7 @@ def lib():
             "mpx_read_decisions": [vp, P(u8p), u64p],
             "mpx_read_commits": [vp, P(u8p), u64p],
             "mpx_read_learns": [vp, P(u8p), u64p],
+            "mpx_read_learn_values": [vp, P(u8p), u64p],
             "mpx_proposal_part": [vp, P(u8p), u64p],
             "mpx_proposal_combine": [P(u8p), u64p, ctypes.c_uint32, P(u8p), u64p],
             "mpx_decisions_bounds": [vp, u64p, ctypes.c_uint64, u64p],
@@ -446,6 +447,26 @@ class Engine:
         out = ctypes.POINTER(ctypes.c_uint8)()
         size = ctypes.c_uint64()
         _ck("mpx_read_learns", lib().mpx_read_learns(self.h, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
+    def value_bytes(self, handle):
+        """The canonical wire bytes of the Value a handle names (mpx_value_bytes)."""
+        cap = 1 << 12
+        while True:
+            buf = (ctypes.c_uint8 * cap)()
+            n = ctypes.c_uint32()
+            rc = lib().mpx_value_bytes(self.h, handle, buf, cap, ctypes.byref(n))
+            if rc == 0 and n.value <= cap:
+                return bytes(buf[:n.value])
+            if rc != 0 and n.value <= cap:
+                _ck("mpx_value_bytes", rc)
+            cap = n.value
+
+    def learn_values(self):
+        """MPXV bytes: every learn's Values and the Unproposable records (mpx_read_learn_values)."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_read_learn_values", lib().mpx_read_learn_values(self.h, ctypes.byref(out), ctypes.byref(size)))
         return _take(out, size.value)
 
     def commit_points(self):

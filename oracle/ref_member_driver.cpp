@@ -84,10 +84,18 @@ struct FrozenClock : public Clock {
 
 struct Sent { uint32_t dst; std::string bytes; };
 
-// Callback::Applied capture (the tags name the learn, see above)
+// Callback capture: Applied (the tags name the learn, see above) and, for the callback
+// fixture (mpxref_member_callbacks), every Accepted / Applied / Unproposable call in order
 struct CapCb : public paxos::Callback {
     std::vector<std::string> applied;
-    void Applied(Thread *, const std::string &cb, const std::string *) { applied.push_back(cb); }
+    std::vector<std::pair<int, std::string> > calls;     // {0 Accepted | 1 Applied | 2 Unproposable, cb}
+    void Accepted(Thread *, const std::string &cb) { calls.push_back(std::make_pair(0, cb)); }
+    void Applied(Thread *, const std::string &cb, const std::string *)
+    {
+        applied.push_back(cb);
+        calls.push_back(std::make_pair(1, cb));
+    }
+    void Unproposable(Thread *, const std::string &cb) { calls.push_back(std::make_pair(2, cb)); }
 };
 
 struct LearnRec { u64 id, created, kind, src, applied, retired, ended, learned; };
@@ -123,6 +131,7 @@ struct Node {
     u64 P = 0, A = 0, L = 0;
     std::string events_d; u64 n_d = 0;               // phase-2 decisions (MPXD)
     std::vector<LearnRec> lrec;                      // learn reliability (MPXL), creation order
+    std::string events_b; u64 n_b = 0;               // the Callback calls (MPXB): {seq, kind, cb}
     std::map<paxos::LearningID, size_t> llive;       // the current Proposer's open learns
 };
 
@@ -284,7 +293,7 @@ std::vector<paxos::MembershipChange> epoch_changes(const Epoch &o, const Epoch &
 
 static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size,
                       uint64_t *stats, uint8_t **lout, uint64_t *lsize, uint8_t **dout = NULL, uint64_t *dsize = NULL,
-                      u64 sb = 0, u64 se = ~0ull, bool digest = false)
+                      u64 sb = 0, u64 se = ~0ull, bool digest = false, uint8_t **bout = NULL, uint64_t *bsize = NULL)
 {
     // digest (mpxref_member_run_shard): counters and digests of the instance shard [sb, se) only
     // (SURVEY.md §8(c)(ii)).  Every record's header is processed; entries outside the shard are cut
@@ -382,20 +391,22 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
             paxos::Proposer *pr = ni->proposer_;
             // learn bookkeeping: tag the learns Applied may run for, note the id counter
             const paxos::LearningID lid0 = pr ? pr->learning_id_ : 0;
-            std::map<paxos::InstanceID, std::string> orig_cb;
+            std::map<std::string, std::string> orig_cb;      // tag -> the value's own cb
             std::map<paxos::LearningID, u64> prev_mask;
             if (pr && !digest) {
                 for (auto &f : pr->learning_values_for_acceptors_) {
                     auto it = pr->learning_values_.find(f.first);
                     if (it == pr->learning_values_.end()) continue;
                     for (auto &v : it->second->values_) {
-                        orig_cb[v.first] = v.second.value_.cb_;
-                        v.second.value_.cb_ = "\x01" + std::to_string(f.first);
+                        const std::string tag = "\x01" + std::to_string(f.first) + "." + std::to_string(v.first);
+                        orig_cb[tag] = v.second.value_.cb_;
+                        v.second.value_.cb_ = tag;
                     }
                 }
                 for (auto &l : pr->learning_values_) prev_mask[l.first] = set_mask(l.second->learned_);
             }
             cb.applied.clear();
+            cb.calls.clear();
             std::set<paxos::AcceptingID> before_b;
             if (pr) for (auto &e : pr->accepting_values_) before_b.insert(e.first);
             switch (type) {
@@ -538,7 +549,8 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
                 // (digest runs skip it: Propose only moves the proposer's id bookkeeping, which
                 // numbers instances across shards; the digested state and the chosen log come from
                 // the trace's P_BATCH / ACCEPT / LEARN records)
-                if (pr && !digest) pr->Propose(pv);      // (no Proposer: Unproposable, :786-789)
+                if (pr && !digest) pr->Propose(pv);
+                else if (!pr && !digest) cb.Unproposable(g_thread, pv.cb_);    // NodeImpl::Loop, :784-787
                 discard_new_batches(pr, before_b);       // the trace's P_BATCH is the batch
                 break;
             }
@@ -561,7 +573,18 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
                     for (auto &l : pr->learning_values_)
                         for (auto &v : l.second->values_)
                             if (!v.second.value_.cb_.empty() && v.second.value_.cb_[0] == '\x01')
-                                v.second.value_.cb_ = orig_cb[v.first];
+                                v.second.value_.cb_ = orig_cb[v.second.value_.cb_];
+                for (auto &c : cb.calls) {             // the fixture: every call, Applied untagged
+                    std::string x = c.second;
+                    if (c.first == 1 && !x.empty() && x[0] == '\x01') {
+                        auto o = orig_cb.find(x);
+                        if (o == orig_cb.end()) return -12;
+                        x = o->second;
+                    }
+                    put<u64>(n.events_b, k); put<u64>(n.events_b, (u64)c.first);
+                    put<uint32_t>(n.events_b, (uint32_t)x.size()); n.events_b += x;
+                    n.n_b++;
+                }
                 for (auto &a : cb.applied) {
                     if (a.empty() || a[0] != '\x01') continue;
                     auto it = n.llive.find(std::stoull(a.substr(1)));
@@ -690,6 +713,16 @@ static int member_run(const uint8_t *trace, uint64_t size, uint8_t **out, uint64
         memcpy(*dout, d.data(), d.size());
         *dsize = d.size();
     }
+    if (bout) {
+        std::string b;
+        b.append("MPXB", 4);
+        put<uint32_t>(b, 1); put<uint32_t>(b, N);
+        for (uint32_t i = 0; i < N; ++i) { put<u64>(b, ns[i].n_b); b += ns[i].events_b; }
+        *bout = (uint8_t *)malloc(b.size());
+        if (!*bout) return -2;
+        memcpy(*bout, b.data(), b.size());
+        *bsize = b.size();
+    }
     if (lout) {
         std::string l;
         l.append("MPXL", 4);
@@ -727,6 +760,13 @@ extern "C" int mpxref_member_run_shard(const uint8_t *trace, uint64_t size, uint
 extern "C" int mpxref_member_learns(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)
 {
     return member_run(trace, size, NULL, NULL, NULL, out, out_size);
+}
+
+// Every Callback call the reference's nodes made (MPXB): per node u64 count, {u64 record, u64 kind
+// (0 Accepted :1332, 1 Applied :1368,1526, 2 Unproposable :787), u32 len, cb bytes} in call order
+extern "C" int mpxref_member_callbacks(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)
+{
+    return member_run(trace, size, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 0, ~0ull, false, out, out_size);
 }
 
 extern "C" int mpxref_member_decisions(const uint8_t *trace, uint64_t size, uint8_t **out, uint64_t *out_size)

@@ -157,6 +157,12 @@ def ref_learns(trace):
     return _blob_call(REF_MEMBER_SO, "mpxref_member_learns", trace)
 
 
+def ref_callbacks(trace):
+    """Every Callback call the REFERENCE's member nodes made — Accepted, Applied, Unproposable — as
+    MPXB (oracle/ref_member_driver.cpp mpxref_member_callbacks; parse: tests/mpxb.py)."""
+    return _blob_call(REF_MEMBER_SO, "mpxref_member_callbacks", trace)
+
+
 def oracle_commits(trace):
     """The oracle's restatement of the same bookkeeping (mpxo_commits)."""
     return _blob_call(ORACLE_SO, "mpxo_commits", trace)

@@ -1281,7 +1281,7 @@ def _sharded_commits(trace, shards, align=256):
 
 
 @pytest.mark.parametrize("shards", [2, 3])
-@pytest.mark.parametrize("name", ["fuzz_big_1", "fuzz_big_2", "c3_faulty_0", "demo_s1", "hm_commit_tags", "fuzz_007"])
+@pytest.mark.parametrize("name", ["fuzz_big_1", "fuzz_big_2", "c3_faulty_0", "demo_s1", "fuzz_007"])
 def test_sharded_commits_match_reference(name, shards):
     """Commit reliability over instance shards (each shard's creation points: the batches
     it kept, the promise quorums where the node held a committed instance of it; their
@@ -1546,6 +1546,125 @@ def test_learned_epochs_in_windows_marker_free(name):
                 assert e.decisions() == _read(name, ".mpxd")
             if name in LEARNS:
                 assert e.learns() == _read(name, ".mpxl")
+
+
+# ---- the member host's Callback calls (member/paxos.h:142-164) ----
+CALLBACKS = json.load(open(os.path.join(GOLD, "callbacks.json")))
+
+
+def _cb_of(vb):
+    """The cb string of a member Value_m (FillValue, member/paxos.cpp:330-363); b"" for a noop."""
+    import struct
+    if vb[12]:
+        return b""
+    mem, n = vb[13] != 0, struct.unpack_from("<I", vb, 14)[0]
+    p = 18 + (8 * n if mem else n)
+    cl = struct.unpack_from("<I", vb, p)[0]
+    return bytes(vb[p + 4:p + 4 + cl])
+
+
+def _engine_callbacks(e, streams):
+    """Every Callback call a member host makes from the engine's readbacks, per node sorted
+    (record, kind, cb): Accepted for a kind-0 learn's values at its creation, Applied for a
+    kind-1 / kind-2 learn's values at its applied record (MPXL + MPXV), Unproposable for the
+    P_PROPOSE records MPXV names (the cb of the host's own record)."""
+    import mpxl
+    import mpxv
+    learns, vals = mpxl.parse(e.learns()), mpxv.parse(e.learn_values())
+    cache = {}
+
+    def cb(h):
+        if h not in cache:
+            cache[h] = _cb_of(e.value_bytes(h))
+        return cache[h]
+    out = []
+    for n, (rows, (vs, unprop)) in enumerate(zip(learns, vals)):
+        assert len(rows) == len(vs)
+        calls = []
+        for row, v in zip(rows, vs):
+            kind, created, applied = row[2], row[1], row[4]
+            if kind == 0:
+                calls += [(created, 0, cb(h)) for _i, h in v]
+            elif applied != mpxl.NONE:
+                calls += [(applied, 1, cb(h)) for _i, h in v]
+        calls += [(k, 2, _cb_of(streams[n][k][8:])) for k in unprop]
+        out.append(sorted(calls))
+    return out
+
+
+def _reference_callbacks(name):
+    import mpxb
+    return [sorted(x) for x in mpxb.parse(_read(name, ".mpxb"))]
+
+
+@pytest.mark.parametrize("name", sorted(CALLBACKS))
+def test_member_callbacks_match_reference(name):
+    """Every paxos::Callback call the reference's nodes made (Accepted at an accept quorum,
+    member/paxos.cpp:1327-1332; Applied for the values of a learn created at a promise quorum or a
+    learner change once an acceptor quorum learned it, :1360-1368,1523-1526 — the whole learned map
+    for those; Unproposable, :784-787), by record and cb string, equals what the engine's learns
+    and their Values (mpx_read_learns + mpx_read_learn_values) make a host call: whole run, and
+    marker-free in 4 incremental windows on a genesis-only engine (MPX_FLAG_LEARN_EPOCHS)."""
+    trace = _read(name, ".mpxt")
+    want = _reference_callbacks(name)
+    _hd, epochs, streams = _node_streams(trace)
+    with mpx.Engine.for_trace(trace) as e:
+        e.run()
+        assert _engine_callbacks(e, streams) == want
+    live = _strip_markers(streams)
+    hd = mpx.trace_header(trace)
+    n, m = hd["num_nodes"], max(hd["num_instances"], 1)
+    with mpx.Engine(n, 0, m, semantics=mpx.SEM_MEMBER, epochs=epochs[:1],
+                    flags=mpx.FLAG_INCREMENTAL | mpx.FLAG_DECISIONS | mpx.FLAG_LEARN_EPOCHS) as e:
+        prev = [0] * n
+        for w in range(1, 5):
+            cut = [len(s) * w // 4 for s in live]
+            for node, s in enumerate(live):
+                if cut[node] > prev[node]:
+                    e.submit(node, s[prev[node]:cut[node]])
+            e.run()
+            prev = cut
+        assert _engine_callbacks(e, streams) == want
+
+
+def test_member_unproposable_reported():
+    """Node::Propose on a node without a Proposer calls Callback::Unproposable (NodeImpl::Loop,
+    member/paxos.cpp:784-787): a P_PROPOSE at node 1 (no Proposer in the genesis epoch) is named by
+    MPXV, one at node 0 (the genesis Proposer) is not — as the reference's own nodes do (MPXB)."""
+    from mpxwire import container, m_p_propose, mvalue
+    import mpxb
+    import mpxv
+    from oracles import ref_available, ref_callbacks
+    streams = [[m_p_propose(mvalue(0, 1, "a", cb="c0"))], [m_p_propose(mvalue(1, 1, "b", cb="c1"))]]
+    trace = container(streams, 16, semantics=1, epochs=[(0, 1, 1)])
+    with mpx.Engine.for_trace(trace) as e:
+        e.run()
+        v = mpxv.parse(e.learn_values())
+    assert [x[1] for x in v] == [[], [0]]
+    if ref_available():
+        assert [[(k, kind, cb) for k, kind, cb in x] for x in mpxb.parse(ref_callbacks(trace))] == [[], [(0, 2, b"c1")]]
+
+
+def test_learned_epochs_refused_change_poisons_engine():
+    """A membership Value the reference ASSERTs on (AddAcceptor of a node that already is one,
+    NodeImpl::ChangeMemberships, member/paxos.cpp:1864-1964) fails the submit with MPX_E_STATE, and
+    the engine — whose Learner frontier and view may have moved past that record — refuses every
+    later call: no run or read on half-learned epochs; the epoch table is unchanged."""
+    from handmade_member import B0, add_acceptor
+    from mpxwire import m_learn, mvalue
+    ok = [(0, B0, mvalue(0, 1, cb="m1", changes=add_acceptor(1)))]
+    twice = [(1, B0, mvalue(0, 2, cb="m2", changes=add_acceptor(1)))]    # node 1 is an acceptor already
+    with mpx.Engine(2, 0, 64, semantics=mpx.SEM_MEMBER, epochs=[(0, 1, 1)], flags=mpx.FLAG_LEARN_EPOCHS) as e:
+        e.submit(0, [m_learn(0, 1, ok)])
+        assert len(e.epochs()) == 2
+        with pytest.raises(mpx.MpxError) as ex:
+            e.submit(0, [m_learn(0, 2, twice)])
+        assert ex.value.rc == -6                            # MPX_E_STATE
+        assert len(e.epochs()) == 2
+        for call in (e.run, lambda: e.submit(1, [m_learn(0, 1, ok)])):
+            with pytest.raises(mpx.MpxError) as ex:
+                call()
+            assert ex.value.rc == -6
 
 
 @pytest.mark.parametrize("seed,props", [(81, 1), (82, 3)])

@@ -72,38 +72,17 @@ def test_member_example_links_libmpx():
     assert r.returncode == 2 and "usage" in r.stderr
 
 
-def _batch_cbs(rec):
-    """P_BATCH {u32 type, u64 accept id, u32 len, {u64 iid, u64 pid, Value_m}*} -> (accept id, the
-    non-noop values' callback strings in instance order) (Value_m: member/paxos.cpp:330-363)."""
-    import struct
-    aid, vl = struct.unpack_from("<QI", rec, 4)
-    p, end, cbs = 16, 16 + vl, {}
-    while p < end:
-        iid = struct.unpack_from("<Q", rec, p)[0]
-        p += 16
-        noop = rec[p + 12] != 0
-        p += 13
-        if noop:
-            continue
-        mem, n = rec[p] != 0, struct.unpack_from("<I", rec, p + 1)[0]
-        p += 5 + (8 * n if mem else n)
-        cl = struct.unpack_from("<I", rec, p)[0]
-        cbs[iid] = bytes(rec[p + 4:p + 4 + cl])
-        p += 4 + cl
-    return aid, [cbs[k] for k in sorted(cbs)]
-
-
 def _member_expect(name):
     """What the reference's own node showed its host, from its fixtures: the replies it sent and
-    the values StateMachine::Apply received (.mpxr), and the Callback::Accepted / Applied calls of
-    every learn an accept quorum created (.mpxl: Proposer::OnAcceptReply, OnLearnReply,
-    member/paxos.cpp:1327-1332,1360-1368) with the callback strings of that batch's values."""
-    import mpxl
+    the values StateMachine::Apply received (.mpxr), and every Callback call its nodes made —
+    Accepted, Applied, Unproposable, each learn kind counted (.mpxb: a recording Callback in
+    oracle/ref_member_driver.cpp, member/paxos.cpp:784-787,1327-1332,1360-1368,1523-1526)."""
+    import mpxb
     from test_engine_gpu import _node_streams
     trace = open(os.path.join(GOLD, name + ".mpxt"), "rb").read()
     ref = mpxr.parse(open(os.path.join(GOLD, name + ".mpxr"), "rb").read())
-    learns = mpxl.parse(open(os.path.join(GOLD, name + ".mpxl"), "rb").read())
-    _hd, epochs, streams = _node_streams(trace)
+    calls = mpxb.parse(open(os.path.join(GOLD, name + ".mpxb"), "rb").read())
+    _hd, epochs, _streams = _node_streams(trace)
     h = 0
     count = 0
     for src, nd in enumerate(ref["nodes"]):
@@ -115,35 +94,27 @@ def _member_expect(name):
         hx = 1469598103934665603
         for p in nd["executed"]:
             hx = _fnv(hx, p)
-        batches = {}
-        for k, r in enumerate(streams[n]):
-            if r[:4] == b"\x11\x00\x00\x00":
-                aid, cbs = _batch_cbs(r)
-                batches.setdefault(aid, []).append((k, cbs))
-        acc, app = [0, 0], [0, 0]
-        for (_id, created, kind, aid, applied, _ret, _drop, _mask) in learns[n]:
-            cands = [c for (k, c) in batches.get(aid, []) if k < created] if kind == 0 else []
-            if not cands:
-                continue
-            for cb in cands[-1]:
-                x = _fnv(1469598103934665603, cb)
-                acc = [acc[0] + 1, (acc[1] + x) % (1 << 64)]
-                if applied != NONE:
-                    app = [app[0] + 1, (app[1] + x) % (1 << 64)]
+        tally = [[0, 0] for _ in range(3)]                # Accepted, Applied, Unproposable
+        for _seq, kind, cb in calls[n]:
+            t = tally[kind]
+            t[0] += 1
+            t[1] = (t[1] + _fnv(1469598103934665603, cb)) % (1 << 64)
         lines.append(("applied", n, len(nd["executed"]), hx))
-        lines.append("callbacks %d %d %016x %d %016x" % (n, acc[0], acc[1], app[0], app[1]))
+        lines.append("callbacks %d %s" % (n, " ".join("%d %016x" % (c, x) for c, x in tally)))
     return lines, epochs
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("windows", [1, 4])
-@pytest.mark.parametrize("name", ["mm_clean3", "mm_learners", "mm_acceptor_reset", "c5_member_2", "c5_contended_1"])
+@pytest.mark.parametrize("name", ["mm_clean3", "mm_learners", "mm_acceptor_reset", "c5_member_2", "c5_member_4",
+                                  "c5_contended_1", "c5_contended_2"])
 def test_member_host_matches_reference(name, windows):
     """The reference's member/paxos.h NetWork / StateMachine / Callback classes on libmpx: a live
     host submits only what NetWork::OnReceive receives (no markers; the engine learns the
     membership from the Values its Learners apply, MPX_FLAG_LEARN_EPOCHS), whole and in 4
     incremental windows; its transport, state machines and callbacks see what the reference's own
-    node showed its host (fixtures), and the epochs the engine learned are the trace's."""
+    node showed its host (fixtures: every Accepted / Applied / Unproposable call, all learn kinds),
+    and the epochs the engine learned are the trace's."""
     if not os.path.exists(MBIN):
         pytest.fail("examples/_build/member_host missing: build() builds it where /root/reference exists")
     path = os.path.join(GOLD, name + ".mpxt")

@@ -53,6 +53,31 @@ def test_ref_shard_mode_matches_whole(name):
         assert ref_run_shards(trace, shards) == want, shards
 
 
+@pytest.mark.ref
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("n,m,shards", [(9, 1 << 16, 4), (5, 40000, 3)])
+def test_ref_c4_shard_generation_matches_whole_trace_shard(n, m, shards):
+    """oracle/ref_full_size.py's C4 entry (the whole 2^27 x 9 trace is ~85 GB): each shard process
+    generates only its shard of the clean trace (every record, entries outside the shard left out).
+    The reference's shard mode over those bytes must equal its shard mode over the WHOLE trace, shard
+    by shard — so the sum over generated shards is the reference's verdict on the whole C4 trace."""
+    import ctypes
+    from oracles import REF_SO
+    f = ctypes.CDLL(REF_SO).mpxref_run_shard
+    f.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    whole = _mpx.generate_trace(_mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=256)
+    per = -(-m // shards)
+    per = -(-per // 256) * 256
+    for k in range(shards):
+        sb, se = k * per, min(m, (k + 1) * per)
+        part = _mpx.generate_trace(_mpx.GEN_CLEAN, num_nodes=n, num_instances=m, batch=256, shard_begin=sb,
+                                   shard_end=se)
+        a, b = (ctypes.c_uint64 * 8)(), (ctypes.c_uint64 * 8)()
+        assert f(whole, len(whole), sb, se, a) == 0 and f(part, len(part), sb, se, b) == 0
+        assert list(a) == list(b), (sb, se)
+        assert a[0] == se - sb
+
+
 def test_codec_unittest_vectors():
     # multi/paxos.cpp:1753-1777: Value(1,2) encodes to 13 bytes, Value(1,2,"123") to 21
     assert len(value(1, 2, noop=True)) == 13

@@ -5,6 +5,7 @@ set -o pipefail
 out=gpurun_out/${1:-fetch}
 mkdir -p $out
 export TMPDIR=/tmp
+hipcc --offload-arch=gfx950 -O2 -o tools/fetch_probe tools/fetch_probe.hip || exit 9
 timeout -k 10 60 tools/fetch_probe > $out/probe.jsonl || exit 1
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $out/fetch -o fp --output-format csv -- tools/fetch_probe > $out/fetch.log 2>&1 || exit 2
 timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -d $out/rdreq -o fp --output-format csv -- tools/fetch_probe > $out/rdreq.log 2>&1 || exit 3
