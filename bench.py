@@ -83,6 +83,11 @@ def parse():
     ap.add_argument("--c5c-instances", type=int, default=1 << 25,
                     help="contended C5 leg (3 member proposers, a rival round per epoch): M (2^25); 0 = skip")
     ap.add_argument("--c5c-only", action="store_true", help="only the contended C5 leg (profiling)")
+    ap.add_argument("--loop-values", type=int, default=1 << 16,
+                    help="closed-loop leg (libmpx's own proposer loop, mpx_loop_leader_rounds): client values per "
+                         "round; 0 = skip")
+    ap.add_argument("--loop-rounds", type=int, default=4)
+    ap.add_argument("--loop-only", action="store_true", help="only the closed-loop leg")
     ap.add_argument("--shard-of", type=int, default=8,
                     help="also time rank 0's shard of the same trace at world G on this GPU (a 1-GPU scaling "
                          "projection, no RCCL); 0 / 1 = skip")
@@ -293,6 +298,52 @@ def c3_windows_leg(args, trace, want_digests, want_counters):
                          "frac_engine_model": b_eng / (mean(apply_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS if mean(apply_ms) else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s"},
             "verified": {"digests_vs_batch_run": ok}}
+
+
+def secondary_loop(args):
+    try:
+        return closed_loop_leg(args)
+    except mpx.MpxError as ex:
+        if ex.rc != -2:
+            raise
+        return {"error": repr(ex)}
+
+
+def closed_loop_leg(args):
+    """The closed loop: libmpx's own proposer loop over one
+    incremental engine (csrc/loop.cpp) — node 0 leads 7 acceptors/learners; per round it starts a
+    prepare with --loop-values client values queued (Propose while preparing, multi/paxos.cpp:
+    1250-1280), and the engine's promise quorum decision becomes the ACCEPT, its chosen log the COMMIT,
+    with no Python between windows (5 windows per round).  decisions/s = values chosen, committed and
+    executed on every node / wall time of the rounds (host encode + decode + build, device run)."""
+    from mpx.loop import NativeLoop
+    N, V, R = 7, args.loop_values, args.loop_rounds
+    L = NativeLoop(N, (R + 1) * V)
+    try:
+        L.leader_rounds(0, range(N), 1, V)                  # warm-up round (allocations, first window)
+        s0 = L.stats()
+        t0 = time.perf_counter()
+        L.leader_rounds(0, range(N), R, V)
+        dt = time.perf_counter() - t0
+        s1 = L.stats()
+        ex = [L.engine.read_executed(n) for n in range(N)]
+        ok = all(fr == (R + 1) * V and len(h) == (R + 1) * V for fr, h in ex) and all(h == ex[0][1] for _, h in ex)
+        assert ok, "closed loop: not every value was executed in order on every node"
+        d = {k: s1[k] - s0[k] for k in s1}
+    finally:
+        L.close()
+    w = max(d["windows"], 1)
+    out = {"workload": "closed loop: 7 nodes, leader 0, %d rounds x %d client values (prepare with values "
+                       "queued -> the engine's decided batch -> ACCEPT -> chosen -> COMMIT), libmpx mpx_loop_*" % (R, V),
+           "value": d["committed_instances"] / dt, "unit": "decisions/s", "rounds": R, "values_per_round": V,
+           "windows": d["windows"], "ms_per_window": dt / w * 1e3,
+           "host_split_ms_per_window": {"submit": d["submit_ns"] / w / 1e6, "run": d["run_ns"] / w / 1e6,
+                                        "drain": d["drain_ns"] / w / 1e6},
+           "verified": {"executed_in_order_on_every_node": ok}}
+    log("closed loop: %d rounds x %d values in %.3f s: %.3g decisions/s (%.2f ms / window: submit %.2f, run %.2f, "
+        "drain %.2f)" % (R, V, dt, out["value"], out["ms_per_window"], out["host_split_ms_per_window"]["submit"],
+                         out["host_split_ms_per_window"]["run"], out["host_split_ms_per_window"]["drain"]))
+    return out
 
 
 class FileGroup:
@@ -706,6 +757,9 @@ def main():
     if args.c5_only:
         print(json.dumps({"c5": c3_leg(args, "c5")}), flush=True)
         return
+    if args.loop_only:
+        print(json.dumps({"closed_loop": closed_loop_leg(args)}), flush=True)
+        return
     if args.c5c_only:
         print(json.dumps({"c5_contended": c3_leg(args, "c5c")}), flush=True)
         return
@@ -818,6 +872,7 @@ def main():
                 return {"error": repr(ex)}
         c5 = secondary("c5") if world == 1 and args.c5_instances else None
         c5c = secondary("c5c") if world == 1 and args.c5c_instances else None
+        loop = secondary_loop(args) if world == 1 and args.loop_values else None
         # every leg's same-workload reference CPU rate
         for name, leg in (("c3", c3), ("c5", c5), ("c5c", c5c)):
             if leg and "error" not in leg and world == 1 and not args.no_cpu_baseline:
@@ -869,6 +924,7 @@ def main():
             "c3": c3,
             **({"c5": c5} if c5 else {}),
             **({"c5_contended": c5c} if c5c else {}),
+            **({"closed_loop": loop} if loop else {}),
             "verified": {"step_state_digest_vs_closed_form": step_ok, "step_digests_vs_reference": step_vs_ref,
                          "step_state_digest": step_state,
                          "step_chosen_digest": step_chosen, "run_digests_vs_closed_form": verified,
@@ -897,6 +953,9 @@ def main():
                                 basis=out["roofline"]["basis"].split(" traffic")[0])
         line["cpu_baseline"] = cpu
         line["legs"] = {"c3": compact_leg(c3), "c5": compact_leg(c5), "c5_contended": compact_leg(c5c)}
+        if loop:
+            line["legs"]["closed_loop"] = {k: loop[k] for k in ("value", "unit", "windows", "ms_per_window",
+                                                                "verified") if k in loop} if "error" not in loop else loop
         if proj:
             line["scaling_projection"] = {k: proj[k] for k in ("G", "T1_ms", "T_shard_ms", "eff", "verified")}
         line["cpu_baseline_port"] = {k: cpu_port[k] for k in ("value", "unit", "cores", "kind")} if cpu_port else None

@@ -542,6 +542,37 @@ int  mpx_proposal_part(mpx_engine *eng, uint8_t **out, uint64_t *size);
 int  mpx_proposal_combine(const uint8_t *const *parts, const uint64_t *sizes, uint32_t nparts,
                           uint8_t **out, uint64_t *size);
 
+/* ---- the closed loop (the engine generates its own accepts and commits) ----
+ * A proposer control plane over one incremental engine (MPX_FLAG_INCREMENTAL |
+ * MPX_FLAG_DECISIONS, multi semantics, every node an acceptor and learner): each message it
+ * sends is made from the engine's results — StartPrepare (P_START + PREPARE over [0, 2^64-1),
+ * multi/paxos.cpp:1233-1248), Propose (P_PROPOSE, :1250-1280), the phase-2 batch the engine
+ * decided at the proposer's promise quorum (mpx_read_decisions -> P_BATCH + ACCEPT,
+ * :1056-1175,1299-1326), COMMIT of a batch the chosen log holds (:1429-1444); the acceptors'
+ * replies are the engine's drained sends, appended to their destinations' streams.  `to`:
+ * a bit mask of the nodes a message is delivered to.  mpx_loop_step submits every stream's new
+ * records as one window and runs it.  mpx_loop_trace: the recorded streams as MPXT (replayable
+ * through the reference's handlers).  mpx_loop_leader_rounds: `rounds` rounds of node `leader`
+ * with `values` client values queued each (5 windows per round).  Replaces what the reference's
+ * Proposer does between its receive and send calls (multi/paxos.cpp:1036-1343,1406-1444) for
+ * the decisions the engine computes; the timers stay the caller's. */
+typedef struct mpx_loop mpx_loop;
+typedef struct mpx_loop_stats {
+    uint64_t windows, records, batches, committed_batches, committed_instances, proposed;
+    uint64_t submit_ns, run_ns, drain_ns;
+} mpx_loop_stats;
+int  mpx_loop_create(uint32_t num_nodes, uint64_t num_instances, int device, mpx_loop **out);
+int  mpx_loop_destroy(mpx_loop *loop);
+mpx_engine *mpx_loop_engine(mpx_loop *loop);
+int  mpx_loop_prepare(mpx_loop *loop, uint32_t node, uint64_t to);
+int  mpx_loop_propose(mpx_loop *loop, uint32_t node, const uint8_t *payload, uint32_t len);
+int  mpx_loop_step(mpx_loop *loop);
+int  mpx_loop_accept_decided(mpx_loop *loop, uint32_t node, uint64_t to, uint64_t *accept_id);
+int  mpx_loop_commit_chosen(mpx_loop *loop, uint32_t node, uint64_t to, uint32_t *count);
+int  mpx_loop_leader_rounds(mpx_loop *loop, uint32_t leader, uint64_t to, uint32_t rounds, uint32_t values);
+int  mpx_loop_stats_get(mpx_loop *loop, mpx_loop_stats *out);
+int  mpx_loop_trace(mpx_loop *loop, uint8_t **out, uint64_t *size);
+
 #ifdef __cplusplus
 }
 #endif

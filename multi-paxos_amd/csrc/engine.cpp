@@ -2363,16 +2363,30 @@ static int learn_plan(mpx_engine *e, const Results &r, std::vector<LearnNode> &n
     for (size_t j = 0; j < h.b_msg.size(); ++j)
         if (r.b_chosen[j] != NONE32 && (aid || h.b_msg[j] != NONE32))
             chosen_at[r.b_chosen[j]] = {aid ? h.b_aid[j] : h.m_aux[h.b_msg[j]], (uint32_t)j};
-    // a chosen batch's values (its P_BATCH's entries; a window's earlier batch: the carried ones)
+    // a chosen batch's values: its P_BATCH's entries; a window's earlier batch (b_msg NONE32): the
+    // chosen-log runs build_trace cut from its carried entries (the carry itself may have let them go
+    // already — a P_START later in the window ends the batch, after its votes completed)
+    std::unordered_map<uint32_t, std::vector<uint32_t>> carried;
+    bool carried_ready = false;
     auto batch_values = [&](uint32_t j, std::vector<std::pair<uint64_t, uint64_t>> &v) {
         const uint32_t g = h.b_msg[j];
         if (g != NONE32) {
             for (uint64_t k = h.m_ent[g]; k < h.m_ent[g] + h.m_cnt[g]; ++k) v.push_back({h.e_iid[k], h.e_val[k]});
-        } else if (e->incremental && j < h.b_gid.size()) {
-            auto it = e->wc.b_ents.find(h.b_gid[j]);
-            if (it != e->wc.b_ents.end()) v = it->second;
+        } else {
+            if (!carried_ready) {
+                carried_ready = true;
+                for (size_t f = 0; f < h.cfrags.size(); ++f)
+                    if (h.cfrags[f].msg < h.b_msg.size() && h.b_msg[h.cfrags[f].msg] == NONE32)
+                        carried[h.cfrags[f].msg].push_back((uint32_t)f);
+            }
+            auto it = carried.find(j);
+            if (it != carried.end())
+                for (uint32_t f : it->second)
+                    for (uint32_t q = 0; q < h.cfrags[f].count; ++q)
+                        v.push_back({h.e_iid[h.cfrags[f].entry + q], h.e_val[h.cfrags[f].entry + q]});
         }
         std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
     };
     const uint64_t lwords = (h.shard_len + 63) / 64;
     for (uint32_t n = 0; n < N; ++n) {

@@ -597,7 +597,9 @@ int decode_record(ValueTable &vt, NodeStream &ns, uint32_t node, uint32_t N, con
     (void)N;
     auto keep_shard = [&](std::vector<uint64_t> &iid, std::vector<uint64_t> *pid, std::vector<uint64_t> &val,
                           size_t first) {
-        // drop entries outside this engine's shard (headers stay: SURVEY §8(e))
+        // drop entries outside this engine's shard (headers stay: SURVEY §8(e)); entries are sorted,
+        // so a list inside the shard is kept as it is (no pass over it)
+        if (iid.size() == first || (iid[first] >= sb && iid.back() < se)) return iid.size() - first;
         size_t w = first;
         for (size_t k = first; k < iid.size(); ++k) {
             if (iid[k] >= sb && iid[k] < se) {
@@ -810,6 +812,8 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
     uint8_t part = 0;
     uint64_t sec = 0;                             // (SectionCache) the value section's id
     auto keep_shard = [&](size_t first) {
+        if (ns.e_iid.size() == first || (ns.e_iid[first] >= sb && ns.e_iid.back() < se))
+            return (uint32_t)(ns.e_iid.size() - first);          // (sorted, inside the shard: kept as it is)
         size_t w = first;
         for (size_t k = first; k < ns.e_iid.size(); ++k)
             if (ns.e_iid[k] >= sb && ns.e_iid[k] < se) {
@@ -897,7 +901,8 @@ int decode_record_member(ValueTable &vt, NodeStream &ns, uint32_t node, const ui
         if (dup) flag(viol, MPX_V_DUP_IID, node, seq, 0);
         ent = first;
         size_t w = first;
-        for (size_t k = first; k < ns.r_iid.size(); ++k)
+        if (ns.r_iid.size() > first && ns.r_iid[first] >= sb && ns.r_iid.back() < se) w = ns.r_iid.size();
+        else for (size_t k = first; k < ns.r_iid.size(); ++k)
             if (ns.r_iid[k] >= sb && ns.r_iid[k] < se) {
                 ns.r_iid[w] = ns.r_iid[k]; ns.r_val[w] = ns.r_val[k]; ns.r_pid[w] = ns.r_pid[k];
                 ++w;
@@ -2295,6 +2300,9 @@ int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<
     std::vector<int> rcs(chunks.size(), MPX_OK);
     SectionCache sc;                                 // (one decode per distinct entry list, this call)
     sc.id_base = vt.sections.fetch_add(1ull << 40);
+    const bool times = ab_env("MPX_DECODE_TIMES") != nullptr;
+    auto wall = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = times ? wall() : 0;
     std::atomic<size_t> next{0};
     auto work = [&]() {
         for (size_t c; (c = next.fetch_add(1)) < chunks.size();) {
@@ -2319,6 +2327,7 @@ int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<
         for (auto &t : th) t.join();
     }
     for (size_t c = 0; c < chunks.size(); ++c) TRY_RC(rcs[c]);
+    const double t1 = times ? wall() : 0;
     // every node's later chunks in order (a thread per node): entry offsets and violation
     // record indices rebased
     auto append = [&](uint32_t n) {
@@ -2349,6 +2358,9 @@ int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<
         if (N) append(0);
         for (auto &t : th) t.join();
     }
+    if (times)
+        std::fprintf(stderr, "[mpx] decode_parallel: %zu chunks on %u threads: records %.1f ms, append %.1f ms\n",
+                     chunks.size(), threads, (t1 - t0) * 1e3, (wall() - t1) * 1e3);
     for (size_t c = 0; c < chunks.size(); ++c)       // first violation in record order
         if (ivs[c].count) {
             if (!iv.code) { iv.code = ivs[c].code; iv.node = ivs[c].node; iv.seq = ivs[c].seq; iv.iid = ivs[c].iid; }

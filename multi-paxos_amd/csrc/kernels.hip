@@ -1620,6 +1620,13 @@ __device__ inline void emit_run(const DevView &v, uint32_t msg, uint32_t ref, ui
 // words carry the accept runs' scan flag (F_GRANTED) in bit 57 after the gather, so the
 // walk reads only LDS.
 constexpr uint64_t MP_GRANTED = 1ull << 57;
+// descriptor-window staging loads in flight per lane, and scan-flag gathers in flight (A/B knobs)
+#ifndef MPX_PL_STAGE_K
+#define MPX_PL_STAGE_K 4
+#endif
+#ifndef MPX_PL_FLAG_C
+#define MPX_PL_FLAG_C 16
+#endif
 // the distinct run boundaries of a pair, sorted into s[0 .. LSEG-2] (BS = unused); false once
 // an LSEG + 1-th segment appears
 template <uint32_t LSEG>
@@ -1673,7 +1680,7 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
         // the window's second words into LDS with coalesced loads, all in flight before the
         // LDS writes
         const uint32_t R = (uint32_t)(wend - sbase < MPLAN_LDS ? wend - sbase : MPLAN_LDS);
-        constexpr uint32_t K = 4;
+        constexpr uint32_t K = MPX_PL_STAGE_K;
         for (uint32_t r0 = 0; r0 < R; r0 += 64 * K) {
             uint64_t x[K];
 #pragma unroll
@@ -1710,7 +1717,7 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
             }
             if (ok) {
                 // the accept runs' scan flags, 16 in flight at a time, then folded into bit 57
-                constexpr uint32_t FC = F < 16 ? F : 16;
+                constexpr uint32_t FC = F < MPX_PL_FLAG_C ? F : MPX_PL_FLAG_C;
                 for (uint32_t k0 = 0; k0 < len; k0 += FC) {
                     uint32_t fg[FC];
 #pragma unroll

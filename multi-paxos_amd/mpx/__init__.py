@@ -37,6 +37,12 @@ class MpxError(RuntimeError):
         self.rc = rc
 
 
+class LoopStats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in ("windows", "records", "batches", "committed_batches",
+                                               "committed_instances", "proposed", "submit_ns", "run_ns",
+                                               "drain_ns")]
+
+
 class Epoch(ctypes.Structure):
     _fields_ = [("version", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("acceptor_mask", ctypes.c_uint64),
                 ("proposer_mask", ctypes.c_uint64), ("learner_mask", ctypes.c_uint64)]
@@ -143,11 +149,23 @@ def lib():
             "mpx_commit_points_combine": [P(u8p), u64p, ctypes.c_uint32, P(u8p), u64p],
             "mpx_read_commits_at": [vp, ctypes.c_char_p, ctypes.c_uint64, P(u8p), u64p],
             "mpx_read_commits_sharded": [vp, P(u8p), u64p],
+            "mpx_loop_create": [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, P(vp)],
+            "mpx_loop_destroy": [vp],
+            "mpx_loop_prepare": [vp, ctypes.c_uint32, ctypes.c_uint64],
+            "mpx_loop_propose": [vp, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32],
+            "mpx_loop_step": [vp],
+            "mpx_loop_accept_decided": [vp, ctypes.c_uint32, ctypes.c_uint64, u64p],
+            "mpx_loop_commit_chosen": [vp, ctypes.c_uint32, ctypes.c_uint64, P(ctypes.c_uint32)],
+            "mpx_loop_leader_rounds": [vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32],
+            "mpx_loop_stats_get": [vp, P(LoopStats)],
+            "mpx_loop_trace": [vp, P(u8p), u64p],
         }
         for name, args in sig.items():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = ctypes.c_int
+        L.mpx_loop_engine.argtypes = [vp]
+        L.mpx_loop_engine.restype = vp
         L.mpx_free.argtypes = [vp]
         L.mpx_free.restype = None
         _lib = L

@@ -190,3 +190,71 @@ class ClosedLoop:
         if self.engine is not None:
             self.engine.close()
             self.engine = None
+
+
+def _mask(to):
+    m = 0
+    for a in to:
+        m |= 1 << a
+    return m
+
+
+class NativeLoop:
+    """The same driver inside libmpx (mpx_loop_*, csrc/loop.cpp): ClosedLoop's moves in C++ on one
+    incremental engine, no Python between a window's decisions / chosen log and the next window's
+    P_BATCH / ACCEPT / COMMIT records.  Same method names and arguments as ClosedLoop(...,
+    incremental=True); for one schedule both record identical streams."""
+
+    def __init__(self, num_nodes, num_instances, device=0):
+        from . import LoopStats  # noqa: F401
+        self.N, self.M = num_nodes, num_instances
+        h = ctypes.c_void_p()
+        _ck("mpx_loop_create", lib().mpx_loop_create(num_nodes, num_instances, device, ctypes.byref(h)))
+        self.h = h
+        self.engine = Engine.__new__(Engine)              # a view of the loop's engine (the loop owns it)
+        self.engine.h = ctypes.c_void_p(lib().mpx_loop_engine(h))
+        self.engine.num_nodes = num_nodes
+        self.engine.shard_begin, self.engine.shard_end = 0, num_instances
+        self.engine.close = lambda: None
+
+    def prepare(self, node, to):
+        _ck("mpx_loop_prepare", lib().mpx_loop_prepare(self.h, node, _mask(to)))
+
+    def propose(self, node, payload):
+        if isinstance(payload, str):
+            payload = payload.encode()
+        _ck("mpx_loop_propose", lib().mpx_loop_propose(self.h, node, payload, len(payload)))
+
+    def run(self):
+        _ck("mpx_loop_step", lib().mpx_loop_step(self.h))
+
+    def accept_decided(self, node, to):
+        aid = ctypes.c_uint64()
+        _ck("mpx_loop_accept_decided", lib().mpx_loop_accept_decided(self.h, node, _mask(to), ctypes.byref(aid)))
+        return aid.value or None
+
+    def commit_chosen(self, node, to):
+        c = ctypes.c_uint32()
+        _ck("mpx_loop_commit_chosen", lib().mpx_loop_commit_chosen(self.h, node, _mask(to), ctypes.byref(c)))
+        return c.value
+
+    def leader_rounds(self, leader, to, rounds, values):
+        _ck("mpx_loop_leader_rounds", lib().mpx_loop_leader_rounds(self.h, leader, _mask(to), rounds, values))
+
+    def stats(self):
+        from . import LoopStats
+        st = LoopStats()
+        _ck("mpx_loop_stats_get", lib().mpx_loop_stats_get(self.h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in LoopStats._fields_}
+
+    def trace(self):
+        from . import _take
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_uint64()
+        _ck("mpx_loop_trace", lib().mpx_loop_trace(self.h, ctypes.byref(out), ctypes.byref(size)))
+        return _take(out, size.value)
+
+    def close(self):
+        if self.h:
+            lib().mpx_loop_destroy(self.h)
+            self.h = None

@@ -1476,6 +1476,82 @@ def test_closed_loop_incremental_equals_replay():
         assert e.dump() == oracle_run(a[0])[0]
 
 
+def _loop_schedule(L, seed, steps=40):
+    import random
+    rng = random.Random(seed)
+    vals = 0
+    started = False
+    for _ in range(steps):
+        p = rng.randrange(3)
+        to = sorted(rng.sample(range(5), rng.randint(2, 5)))
+        op = rng.random()
+        if op < 0.2:
+            L.prepare(p, to)
+            for _ in range(rng.randint(0, 3)):
+                L.propose(p, "v%d" % vals)
+                vals += 1
+        elif op < 0.65 and started:
+            L.accept_decided(p, to)
+        elif started:
+            L.commit_chosen(p, to)
+        L.run(); L.run()
+        started = True
+
+
+@pytest.mark.parametrize("seed", [5, 11])
+def test_native_loop_equals_python_loop(seed):
+    """The closed loop inside libmpx (mpx_loop_*) makes the Python driver's moves
+    (mpx.loop.ClosedLoop on one incremental engine) for the same schedule: identical recorded streams
+    and decisions; replayed through the C oracle and, built, the reference's own handlers, the
+    streams give the native loop's engine result and decisions."""
+    from mpx.loop import ClosedLoop, NativeLoop
+    from oracles import oracle_decisions, oracle_run, ref_available
+    py, nat = ClosedLoop(5, 256, incremental=True), NativeLoop(5, 256)
+    try:
+        _loop_schedule(py, seed)
+        _loop_schedule(nat, seed)
+        t = nat.trace()
+        assert t == py.trace()
+        assert nat.engine.decisions() == py.engine.decisions() == oracle_decisions(t)
+        assert nat.stats()["batches"] == len(py.batches) >= 1
+        with mpx.Engine.for_trace(t) as e:
+            e.run()
+            assert e.dump() == oracle_run(t)[0]
+            if ref_available():
+                from oracles import ref_decisions, ref_run
+                assert e.dump() == ref_run(t)[0] and e.decisions() == ref_decisions(t)
+    finally:
+        py.close()
+        nat.close()
+
+
+def test_native_loop_leader_rounds_match_reference():
+    """mpx_loop_leader_rounds: a leader's rounds (StartPrepare with client values queued, the engine's
+    decided batch accepted, chosen and committed to every node) entirely in libmpx; every value is
+    chosen and executed in order on every node, and the recorded streams replayed through the
+    reference's own handlers give the engine's result and decisions."""
+    from mpx.loop import NativeLoop
+    from oracles import oracle_run, ref_available
+    L = NativeLoop(5, 4096)
+    try:
+        L.leader_rounds(0, range(5), 4, 300)
+        st = L.stats()
+        assert st["committed_instances"] == 1200 and st["windows"] == 20
+        chosen = L.engine.read_chosen(0, 1200)
+        assert all(c >> 63 for c in chosen)
+        ex = [L.engine.read_executed(n)[1] for n in range(5)]
+        assert all(len(x) == 1200 and x == ex[0] for x in ex)
+        t = L.trace()
+        with mpx.Engine.for_trace(t) as e:
+            e.run()
+            assert e.dump() == oracle_run(t)[0]
+            if ref_available():
+                from oracles import ref_decisions, ref_run
+                assert e.dump() == ref_run(t)[0] and e.decisions() == ref_decisions(t)
+    finally:
+        L.close()
+
+
 # ---- membership learned at run time (MPX_FLAG_LEARN_EPOCHS; member/paxos.cpp:1040-1073,1864-1964) ----
 MEMBER_GOLDENS = sorted(k for k in INDEX if k.startswith(("c5_", "mm_")))
 
