@@ -271,6 +271,26 @@ def c3_windows_leg(args, trace, want_digests, want_counters):
     ok = digests == tuple(want_digests) and tot == want_counters
     assert ok, "C3 windows: the windows' state differs from the batch run's (%r vs %r, %r vs %r)" % (
         digests, want_digests, tot, want_counters)
+    # the pipelined live loop: window k + 1 decoded on a host thread (mpx_submit_trace_range_async)
+    # while window k is built and run — wall time of the whole loop
+    eng = mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL)
+    cuts = [[c * w // W for (c, _, _) in idx] for w in range(W + 1)]
+    ptot = {k: 0 for k in want_counters}
+    t0 = time.perf_counter()
+    eng.submit_window(trace, cuts[0], cuts[1])
+    for w in range(1, W + 1):
+        if w < W:
+            eng.submit_window_async(trace, cuts[w], cuts[w + 1])
+        st = eng.run()
+        for k in ptot:
+            ptot[k] += st[k]
+    pipe_s = time.perf_counter() - t0
+    pdig = eng.state_digest()
+    eng.close()
+    pok = pdig == tuple(want_digests) and ptot == want_counters
+    assert pok, "C3 windows (pipelined): the state differs from the batch run's"
+    log("c3 windows pipelined: %.1f ms / window, %.3g decisions/s end to end" % (pipe_s / W * 1e3,
+                                                                                  ptot["chosen"] / pipe_s))
     run_ms = [p["run"] for p in dev]
     apply_ms = [p["fast_apply"] + p["general_apply"] for p in dev]   # k_apply_win's start / stop events
     mean = lambda xs: sum(xs) / max(len(xs), 1)
@@ -284,11 +304,15 @@ def c3_windows_leg(args, trace, want_digests, want_counters):
     log("c3 windows: %d windows, host %.1f ms / window (submit %.1f; device %.2f), k_apply_win %.3f ms" %
         (W, mean(host_ms), mean(sub_ms), mean(run_ms), mean(apply_ms)))
     return {"windows": W, "chosen": tot["chosen"],
-            "value": tot["chosen"] / (sum(host_ms) * 1e-3), "unit": "decisions/s",
+            "value": ptot["chosen"] / pipe_s, "unit": "decisions/s",
+            "value_sequential": tot["chosen"] / (sum(host_ms) * 1e-3),
             "value_device": tot["chosen"] / (sum(run_ms) * 1e-3),
-            "note": "value: chosen instances / the windows' host + device wall time (decode, upload, run, "
-                    "readback); value_device: / the device run time alone",
-            "host_ms_per_window": mean(host_ms), "submit_ms_per_window": mean(sub_ms),
+            "note": "value: chosen instances / the wall time of the pipelined window loop (window k + 1 decoded "
+                    "on a host thread while window k is built, uploaded and run: mpx_submit_trace_range_async); "
+                    "value_sequential: the same with each window's decode, build, upload and run in turn; "
+                    "value_device: / the device run time alone",
+            "host_ms_per_window": pipe_s / W * 1e3, "host_ms_per_window_sequential": mean(host_ms),
+            "submit_ms_per_window": mean(sub_ms),
             "device_ms_per_window": mean(run_ms),
             "host_ms": host_ms, "device_ms": run_ms, "apply_ms": apply_ms, "pairs_per_window": gp,
             "roofline": {"bound": "hbm", "kernel": "k_apply_win", "kernel_ms": mean(apply_ms),
@@ -297,7 +321,7 @@ def c3_windows_leg(args, trace, want_digests, want_counters):
                          "bytes_engine_model_per_launch": b_eng,
                          "frac_engine_model": b_eng / (mean(apply_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS if mean(apply_ms) else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s"},
-            "verified": {"digests_vs_batch_run": ok}}
+            "verified": {"digests_vs_batch_run": ok and pok}}
 
 
 def secondary_loop(args):
@@ -330,6 +354,12 @@ def closed_loop_leg(args):
         ok = all(fr == (R + 1) * V and len(h) == (R + 1) * V for fr, h in ex) and all(h == ex[0][1] for _, h in ex)
         assert ok, "closed loop: not every value was executed in order on every node"
         d = {k: s1[k] - s0[k] for k in s1}
+        trace_file = None
+        if not args.no_cpu_baseline:                         # the streams the loop sent, for the reference
+            import tempfile
+            trace_file = os.path.join(tempfile.gettempdir(), "mpx_loop_%d.mpxt" % os.getpid())
+            with open(trace_file, "wb") as fh:
+                fh.write(L.trace())
     finally:
         L.close()
     w = max(d["windows"], 1)
@@ -340,6 +370,13 @@ def closed_loop_leg(args):
            "host_split_ms_per_window": {"submit": d["submit_ns"] / w / 1e6, "run": d["run_ns"] / w / 1e6,
                                         "drain": d["drain_ns"] / w / 1e6},
            "verified": {"executed_in_order_on_every_node": ok}}
+    if trace_file:
+        cb = leg_cpu_baseline("loop", trace_file=trace_file)
+        os.remove(trace_file)
+        if cb and cb.get("value"):
+            # the reference replays all R + 1 rounds' streams (the warm-up round too): rate per chosen instance
+            out["cpu_baseline"] = cb
+            out["vs_cpu"] = out["value"] / cb["value"]
     log("closed loop: %d rounds x %d values in %.3f s: %.3g decisions/s (%.2f ms / window: submit %.2f, run %.2f, "
         "drain %.2f)" % (R, V, dt, out["value"], out["ms_per_window"], out["host_split_ms_per_window"]["submit"],
                          out["host_split_ms_per_window"]["run"], out["host_split_ms_per_window"]["drain"]))
@@ -567,7 +604,7 @@ def cpu_baseline(args, budget_s):
             "node_instance_apps_per_s": apps / dt}
 
 
-def leg_cpu_baseline(leg, instances=1 << 17):
+def leg_cpu_baseline(leg, instances=1 << 17, trace_file=None):
     """The reference's own handlers (oracle/_ref, -O2) on the leg's own generator configuration
     (bench's C3 / C5 / C5C parameters and seed, sampled at `instances`), one forked process per
     core the quota gives, each replaying the whole sampled trace (oracle/ref_leg_rate.py, run as a
@@ -579,7 +616,7 @@ def leg_cpu_baseline(leg, instances=1 << 17):
         return None
     procs = cpu_threads()
     cmd = [sys.executable, os.path.join(ROOT, "oracle", "ref_leg_rate.py"), leg, "--instances", str(instances),
-           "--procs", str(procs)]
+           "--procs", str(procs)] + (["--trace", trace_file] if trace_file else [])
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     except subprocess.TimeoutExpired:
@@ -590,10 +627,12 @@ def leg_cpu_baseline(leg, instances=1 << 17):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     fs = d.get("full_size_check")
     return {"value": d["value"], "unit": "decisions/s", "cores": procs, "kind": "reference",
-            "sample": "reference %s handlers (-O2, oracle/_ref) over the leg's own generator configuration at "
-                      "%d instances (%d chosen, %.0f MB), %d processes each replaying the whole trace, slowest "
-                      "%.1f s (%s)" % ("member/paxos.cpp" if leg != "c3" else "multi/paxos.cpp", instances,
-                                       d["chosen"], d["trace_bytes"] / 1e6, procs, d["slowest_s"], cpu_note()),
+            "sample": ("reference %s handlers (-O2, oracle/_ref) over %s (%d chosen, %.0f MB), %d processes each "
+                       "replaying the whole trace, slowest %.1f s (%s)"
+                       % ("member/paxos.cpp" if leg in ("c5", "c5c") else "multi/paxos.cpp",
+                          "the closed loop's own recorded streams" if leg == "loop" else
+                          "the leg's own generator configuration at %d instances" % instances,
+                          d["chosen"], d["trace_bytes"] / 1e6, procs, d["slowest_s"], cpu_note())),
             "full_size_ref_per_core": fs["per_core"] if fs else None}
 
 
@@ -615,14 +654,17 @@ def compact_leg(d):
     w = d.get("windows")
     if w:
         out["windows"] = {"windows": w["windows"], "host_ms_per_window": round(w["host_ms_per_window"], 2),
+                          "host_ms_per_window_sequential": round(w["host_ms_per_window_sequential"], 2),
+                          "value_sequential": w["value_sequential"],
                           "submit_ms_per_window": round(w["submit_ms_per_window"], 2),
                           "device_ms_per_window": round(w["device_ms_per_window"], 4), "value": w["value"],
                           "value_device": w["value_device"], "kernel_ms": round(w["roofline"]["kernel_ms"], 4),
                           "frac_hw": w["roofline"]["frac_hw"] and round(w["roofline"]["frac_hw"], 4),
                           "verified": w["verified"]["digests_vs_batch_run"]}
-        for k in ("host_phases_ms",):
-            if k in w:
-                out["windows"][k] = w[k]
+        if cb:                                   # (the same C3 workload, fed window by window)
+            out["windows"]["cpu_baseline"] = out["cpu_baseline"]
+            if cb.get("value"):
+                out["windows"]["vs_cpu"] = round(w["value"] / cb["value"], 2)
     return out
 
 
@@ -638,9 +680,10 @@ def log_leg(name, d):
         "%.3g decisions/s on %s cores (%s)" % (cb["value"], cb["cores"], cb["kind"]) if cb.get("value") else "none"))
     w = d.get("windows")
     if w:
-        log("leg %s.windows: host %.2f ms / window (submit %.2f), device %.4f ms, %.3g decisions/s end to end, "
-            "%.3g on the device, k_apply_win %.4f ms, frac_hw %s" % (
-                name, w["host_ms_per_window"], w["submit_ms_per_window"], w["device_ms_per_window"], w["value"],
+        log("leg %s.windows: host %.2f ms / window pipelined (%.2f sequential, submit %.2f), device %.4f ms, "
+            "%.3g decisions/s end to end, %.3g on the device, k_apply_win %.4f ms, frac_hw %s" % (
+                name, w["host_ms_per_window"], w["host_ms_per_window_sequential"], w["submit_ms_per_window"],
+                w["device_ms_per_window"], w["value"],
                 w["value_device"], w["roofline"]["kernel_ms"],
                 "%.3f" % w["roofline"]["frac_hw"] if w["roofline"]["frac_hw"] else "null"))
 
@@ -955,7 +998,11 @@ def main():
         line["legs"] = {"c3": compact_leg(c3), "c5": compact_leg(c5), "c5_contended": compact_leg(c5c)}
         if loop:
             line["legs"]["closed_loop"] = {k: loop[k] for k in ("value", "unit", "windows", "ms_per_window",
-                                                                "verified") if k in loop} if "error" not in loop else loop
+                                                                "verified", "vs_cpu") if k in loop} \
+                if "error" not in loop else loop
+            if loop.get("cpu_baseline"):
+                line["legs"]["closed_loop"]["cpu_baseline"] = {k: loop["cpu_baseline"].get(k) for k in
+                                                              ("value", "unit", "cores", "kind")}
         if proj:
             line["scaling_projection"] = {k: proj[k] for k in ("G", "T1_ms", "T_shard_ms", "eff", "verified")}
         line["cpu_baseline_port"] = {k: cpu_port[k] for k in ("value", "unit", "cores", "kind")} if cpu_port else None

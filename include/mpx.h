@@ -289,6 +289,16 @@ int  mpx_submit_trace(mpx_engine *eng, const uint8_t *trace, uint64_t size);
  * decoded on one host thread per node for large slices. */
 int  mpx_submit_trace_range(mpx_engine *eng, const uint8_t *trace, uint64_t size,
                             const uint64_t *begin, const uint64_t *end);
+/* The same slice decoded on a background host thread: the call returns at once and the decode
+ * overlaps the build and device run of the window queued before it — the pipelined live loop
+ * submit_async(k + 1), mpx_run(k), ... (MPX_FLAG_INCREMENTAL, multi semantics, no
+ * MPX_FLAG_LEARN_EPOCHS; MPX_E_STATE otherwise).  mpx_run joins the decode only when nothing else
+ * is queued; every submit and every call that reads Values (mpx_drain_sends, mpx_value_bytes,
+ * mpx_read_executed, mpx_dump_result) joins it first, so records keep their submission order.  A
+ * decode error is returned by the call that joins it (that window is dropped, the engine stays
+ * usable).  `trace` must stay valid until then. */
+int  mpx_submit_trace_range_async(mpx_engine *eng, const uint8_t *trace, uint64_t size,
+                                  const uint64_t *begin, const uint64_t *end);
 
 /* Apply everything submitted since the last run (state carries over). */
 int  mpx_run(mpx_engine *eng);

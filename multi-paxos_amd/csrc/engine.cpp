@@ -89,6 +89,14 @@ struct mpx_engine {
     std::vector<NodeStream> parts;             // submit_container's record chunks past each node's first (capacity kept)
     std::vector<EpochLearn> elearn;                  // MPX_FLAG_LEARN_EPOCHS: per node (ingest.hpp)
     IngestViolation iv;
+    // mpx_submit_trace_range_async: the next window's records decoded on a host thread while the
+    // current one is built and run (pf_join moves them into `nodes`)
+    std::thread pf_thread;
+    bool pf_pending = false;
+    int pf_rc = MPX_OK;
+    std::vector<NodeStream> pf_nodes, pf_parts;
+    IngestViolation pf_iv;
+    uint64_t pf_ns = 0;
     HostTrace ht;
     bool dirty = true;
     bool device_trace = false;       // trace materialised by a device generator
@@ -254,6 +262,7 @@ extern "C" int mpx_create(const mpx_config *cfg, mpx_engine **out)
 extern "C" int mpx_destroy(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
+    if (e->pf_pending) { e->pf_thread.join(); e->pf_pending = false; }
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (auto &s : e->ev_pool) for (auto ev : s.e) (void)hipEventDestroy(ev);
@@ -304,6 +313,43 @@ static int merge_epochs(mpx_engine *e)
     return MPX_OK;
 }
 
+// the pending background decode (mpx_submit_trace_range_async): joined, and its records queued
+// behind any already queued (a node's queue is empty whenever a window was run in between, the
+// pipelined use; otherwise the records are appended with their entry offsets rebased)
+static int pf_join(mpx_engine *e)
+{
+    if (!e->pf_pending) return MPX_OK;
+    e->pf_thread.join();
+    e->pf_pending = false;
+    e->stats.ingest_ns += e->pf_ns;
+    if (e->pf_rc) return e->pf_rc;                  // (nothing consumed: the window is dropped, the engine stays)
+    for (uint32_t n = 0; n < e->cfg.num_nodes; ++n) {
+        NodeStream &ns = e->nodes[n], &p = e->pf_nodes[n];
+        if (ns.type.empty()) { std::swap(ns, p); p.clear(); continue; }
+        const uint64_t eb = ns.e_iid.size(), qb = ns.r_iid.size(), gb = ns.g_a.size();
+        auto cat = [](auto &dst, const auto &src) { dst.insert(dst.end(), src.begin(), src.end()); };
+        cat(ns.type, p.type); cat(ns.src, p.src); cat(ns.ballot, p.ballot); cat(ns.aux, p.aux);
+        cat(ns.cnt, p.cnt); cat(ns.ver, p.ver); cat(ns.part, p.part); cat(ns.sec, p.sec);
+        cat(ns.e_iid, p.e_iid); cat(ns.e_val, p.e_val); cat(ns.e_pid, p.e_pid);
+        cat(ns.r_iid, p.r_iid); cat(ns.r_pid, p.r_pid); cat(ns.r_val, p.r_val);
+        cat(ns.g_a, p.g_a); cat(ns.g_b, p.g_b);
+        for (size_t k = 0; k < p.ent.size(); ++k) {
+            const uint8_t t = p.type[k];
+            const uint64_t base = t == MPX_MSG_PREPARE ? gb : t == MPX_MSG_PREPARE_REPLY ? qb :
+                                  (t == MPX_MSG_ACCEPT || t == MPX_MSG_COMMIT || t == MPX_MSG_P_BATCH) ? eb : 0;
+            ns.ent.push_back(p.ent[k] + base);
+        }
+        p.clear();
+    }
+    if (e->pf_iv.count) {
+        if (!e->iv.code) e->iv = e->pf_iv;
+        else e->iv.count += e->pf_iv.count;
+    }
+    e->pf_iv = IngestViolation();
+    e->dirty = true;
+    return MPX_OK;
+}
+
 extern "C" int mpx_read_epochs(mpx_engine *e, mpx_epoch *out, uint32_t cap, uint32_t *count)
 {
     if (!e || !count || (cap && !out)) return MPX_E_INVAL;
@@ -317,6 +363,7 @@ extern "C" int mpx_submit(mpx_engine *e, uint32_t node, const uint8_t *bytes, co
     if (!e || node >= e->cfg.num_nodes || (count && (!bytes || !offsets))) return MPX_E_INVAL;
     if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (e->device_trace) return MPX_E_STATE;
+    TRY(pf_join(e));                                // (records queue in submission order)
     const uint64_t t0 = now_ns();
     NodeStream &ns = e->nodes[node];
     const bool member = e->cfg.semantics == MPX_SEM_MEMBER;
@@ -348,6 +395,7 @@ extern "C" int mpx_submit_soa(mpx_engine *e, uint32_t node, const mpx_soa_record
     if (!e || !r || node >= e->cfg.num_nodes) return MPX_E_INVAL;
     if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     if (e->device_trace || e->cfg.semantics != MPX_SEM_MULTI) return MPX_E_STATE;
+    TRY(pf_join(e));
     if (r->count && (!r->type || !r->src || !r->ballot || !r->aux || !r->ent_off)) return MPX_E_INVAL;
     const uint64_t t0 = now_ns();
     NodeStream &ns = e->nodes[node];
@@ -371,10 +419,12 @@ static inline uint32_t rd32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4
 static inline uint64_t rd64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
 
 // the records [begin[n], end[n]) of every node's stream of an MPXT container (nullptr: all of them)
-static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, const uint64_t *begin, const uint64_t *end)
+static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, const uint64_t *begin, const uint64_t *end,
+                            bool async = false)
 {
     if (!e || !t || size < 40 || std::memcmp(t, "MPXT", 4)) return MPX_E_INVAL;
     if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
+    TRY(pf_join(e));                                // (records queue in submission order)
     const uint32_t N = rd32(t + 8), sem = rd32(t + 12), ne = rd32(t + 24), ver = rd32(t + 4);
     if (N != e->cfg.num_nodes || sem != e->cfg.semantics || ver < 1 || ver > 2) return MPX_E_INVAL;
     const uint32_t esz = ver == 1 ? 24 : 32;         // version 1: no learner_mask (= proposer_mask)
@@ -415,6 +465,26 @@ static int submit_container(mpx_engine *e, const uint8_t *t, uint64_t size, cons
     };
     uint64_t total = 0;
     for (uint32_t n = 0; n < N; ++n) { const uint64_t *o; const uint8_t *b; const uint64_t c = stream(n, o, b); if (c) total += o[c] - o[0]; }
+    if (async) {
+        // the window's records decoded on a host thread (into pf_nodes) while the caller runs the
+        // windows queued before it; multi semantics (no learned epochs: the decode would move the
+        // epoch table under a running window)
+        std::vector<StreamSlice> sl(N);
+        for (uint32_t n = 0; n < N; ++n) sl[n].cnt = stream(n, sl[n].offs, sl[n].bytes);
+        if (e->pf_nodes.size() < N) e->pf_nodes.resize(N);
+        for (auto &x : e->pf_nodes) x.clear();
+        e->pf_iv = IngestViolation();
+        e->pf_rc = MPX_OK;
+        e->pf_pending = true;
+        e->pf_thread = std::thread([e, sl]() {
+            const uint64_t t0 = now_ns();
+            e->pf_rc = decode_parallel(e->vt, e->pf_nodes, e->pf_parts, sl, false, nullptr, e->cfg.shard_begin,
+                                       e->cfg.shard_end, e->pf_iv,
+                                       std::max(1u, std::min(16u, std::thread::hardware_concurrency())), 0);
+            e->pf_ns = now_ns() - t0;
+        });
+        return MPX_OK;
+    }
     if (N == 1 || total < (1u << 20) || e->device_trace) {
         for (uint32_t n = 0; n < N; ++n) {
             const uint64_t *offs; const uint8_t *bytes;
@@ -450,6 +520,19 @@ extern "C" int mpx_submit_trace_range(mpx_engine *e, const uint8_t *t, uint64_t 
 {
     if (!e || !begin || !end) return MPX_E_INVAL;
     return submit_container(e, t, size, begin, end);
+}
+
+// The same records decoded in the background: the call returns at once, and the decode overlaps
+// the build and device run of the windows queued before it (mpx_run joins it only when nothing
+// else is queued; every call that reads the value table or adds records joins it first).
+// Incremental multi-semantics engines; the caller keeps `t` alive until the records are joined.
+extern "C" int mpx_submit_trace_range_async(mpx_engine *e, const uint8_t *t, uint64_t size, const uint64_t *begin,
+                                            const uint64_t *end)
+{
+    if (!e || !begin || !end) return MPX_E_INVAL;
+    if (!e->incremental || e->cfg.semantics != MPX_SEM_MULTI || !e->elearn.empty() || e->device_trace)
+        return MPX_E_STATE;
+    return submit_container(e, t, size, begin, end, true);
 }
 
 // allocate state / output buffers and fill the kernel view
@@ -951,6 +1034,11 @@ extern "C" int mpx_run(mpx_engine *e)
 {
     if (!e) return MPX_E_INVAL;
     if (e->poisoned) return MPX_E_STATE;            // (a failed window, or a failed LEARN_EPOCHS submit)
+    if (e->pf_pending) {                            // (a prefetched window runs when nothing else is queued)
+        bool queued = false;
+        for (auto &ns : e->nodes) queued = queued || !ns.type.empty();
+        if (!queued) TRY(pf_join(e));
+    }
     if (e->incremental) {
         const uint64_t before = e->consumed;
         const int rc = run_window(e);
@@ -1113,6 +1201,7 @@ extern "C" int mpx_read_executed(mpx_engine *e, uint32_t node, uint64_t *frontie
                                  uint64_t *handles, uint64_t cap)
 {
     if (!e || node >= e->cfg.num_nodes || (cap && !handles)) return MPX_E_INVAL;
+    TRY(pf_join(e));                                // (the value table: no decode in flight)
     if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     uint64_t fr;
     std::vector<uint64_t> h;
@@ -1219,6 +1308,7 @@ extern "C" int mpx_last_violation(mpx_engine *e, mpx_violation *out)
 extern "C" int mpx_value_bytes(mpx_engine *e, uint64_t handle, uint8_t *buf, uint32_t cap, uint32_t *len)
 {
     if (!e || !len) return MPX_E_INVAL;
+    TRY(pf_join(e));                                // (the value table: no decode in flight)
     std::string s;
     if (!e->vt.encode(handle & ~MPX_PRESENT, s)) return MPX_E_RANGE;
     *len = (uint32_t)s.size();
@@ -1352,6 +1442,7 @@ static void reply_of(const mpx_engine *e, const Results &r, uint32_t n, uint64_t
 extern "C" int mpx_drain_sends(mpx_engine *e, mpx_send_fn fn, void *user)
 {
     if (!e || !fn) return MPX_E_INVAL;
+    TRY(pf_join(e));                                // (the value table: no decode in flight)
     if (e->poisoned) return MPX_E_STATE;            // (MPX_FLAG_INCREMENTAL: a failed window)
     Results r;
     TRY(fetch_results(e, r));
@@ -1368,6 +1459,7 @@ extern "C" int mpx_drain_sends(mpx_engine *e, mpx_send_fn fn, void *user)
 extern "C" int mpx_dump_result(mpx_engine *e, uint8_t **out, uint64_t *size)
 {
     if (!e || !out || !size) return MPX_E_INVAL;
+    TRY(pf_join(e));                                // (the value table: no decode in flight)
     if (e->incremental) return MPX_E_STATE;             // windows keep no history of runs
     Results r;
     TRY(fetch_results(e, r));

@@ -532,20 +532,34 @@ static void publish_section(ValueTable &vt, SectionCache &sc, SectionCache::Resu
 // entries {u64 iid, [u64 pid,] Value}* of an ACCEPT / COMMIT / P_BATCH / PREPARE_REPLY body,
 // sorted by iid (the reference's std::map order); with `sc`, from the section's Result when it is
 // ready, else decoded (and published by the first claimer)
+#ifdef MPX_DECODE_PROF
+}  // namespace mpx
+#include <x86intrin.h>
+namespace mpx {
+std::atomic<uint64_t> g_prof[8];                    // claim, own parse, skim, copy, no-cache parse (cycles); counts
+struct ProfT { uint64_t t = __rdtsc(); int k; explicit ProfT(int k_) : k(k_) {} ~ProfT() { g_prof[k] += __rdtsc() - t; } };
+#define PROF(k) ProfT prof_##k(k)
+#else
+#define PROF(k)
+#endif
 static int decode_entries(ValueTable &vt, const uint8_t *b, size_t len, bool with_pid,
                           std::vector<uint64_t> &iid, std::vector<uint64_t> &pid,
                           std::vector<uint64_t> &val, size_t &n_all, bool &dup,
                           std::vector<std::pair<uint64_t, const uint8_t *>> *memh = nullptr, SectionCache *sc = nullptr,
                           uint64_t *sec = nullptr)
 {
-    if (!sc || !len) return parse_section(vt, b, len, with_pid, true, iid, pid, val, n_all, dup, memh);
+    if (!sc || !len) { PROF(4); return parse_section(vt, b, len, with_pid, true, iid, pid, val, n_all, dup, memh); }
     bool own = false;
-    SectionCache::Result *r = sc->claim(b, len, with_pid, own);
+    SectionCache::Result *r;
+    { PROF(0); r = sc->claim(b, len, with_pid, own); }
     if (sec) *sec = r->id;
-    if (own) publish_section(vt, *sc, r);
-    if (!r->ready.load(std::memory_order_acquire))   // (claimed elsewhere, not decoded yet: skim)
+    if (own) { PROF(1); publish_section(vt, *sc, r); }
+    if (!r->ready.load(std::memory_order_acquire)) {  // (claimed elsewhere, not decoded yet: skim)
+        PROF(2);
         return parse_section(vt, b, len, with_pid, false, iid, pid, val, n_all, dup, memh);
+    }
     if (r->rc) return r->rc;
+    PROF(3);
     iid.insert(iid.end(), r->iid.begin(), r->iid.end());
     if (with_pid) pid.insert(pid.end(), r->pid.begin(), r->pid.end());
     val.insert(val.end(), r->val.begin(), r->val.end());
@@ -2361,6 +2375,11 @@ int decode_parallel(ValueTable &vt, std::vector<NodeStream> &nodes, std::vector<
     if (times)
         std::fprintf(stderr, "[mpx] decode_parallel: %zu chunks on %u threads: records %.1f ms, append %.1f ms\n",
                      chunks.size(), threads, (t1 - t0) * 1e3, (wall() - t1) * 1e3);
+#ifdef MPX_DECODE_PROF
+    std::fprintf(stderr, "[mpx] decode cycles (M): claim %.0f own %.0f skim %.0f copy %.0f nocache %.0f\n",
+                 g_prof[0] * 1e-6, g_prof[1] * 1e-6, g_prof[2] * 1e-6, g_prof[3] * 1e-6, g_prof[4] * 1e-6);
+    for (auto &x : g_prof) x = 0;
+#endif
     for (size_t c = 0; c < chunks.size(); ++c)       // first violation in record order
         if (ivs[c].count) {
             if (!iv.code) { iv.code = ivs[c].code; iv.node = ivs[c].node; iv.seq = ivs[c].seq; iv.iid = ivs[c].iid; }

@@ -112,6 +112,7 @@ def lib():
             "mpx_submit": [vp, ctypes.c_uint32, ctypes.c_char_p, u64p, ctypes.c_uint64],
             "mpx_submit_trace": [vp, ctypes.c_char_p, ctypes.c_uint64],
             "mpx_submit_trace_range": [vp, ctypes.c_char_p, ctypes.c_uint64, u64p, u64p],
+            "mpx_submit_trace_range_async": [vp, ctypes.c_char_p, ctypes.c_uint64, u64p, u64p],
             "mpx_submit_soa": [vp, ctypes.c_uint32, P(SoaRecords)],
             "mpx_run": [vp], "mpx_reset_state": [vp], "mpx_step": [vp], "mpx_sync": [vp],
             "mpx_timings": [vp, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_uint32)],
@@ -344,6 +345,14 @@ class Engine:
         b = (ctypes.c_uint64 * n)(*begin)
         e = (ctypes.c_uint64 * n)(*end)
         _ck("mpx_submit_trace_range", lib().mpx_submit_trace_range(self.h, trace, len(trace), b, e))
+
+    def submit_window_async(self, trace, begin, end):
+        """mpx_submit_trace_range_async: the same window decoded on a background host thread (joined by
+        the next submit, a Value read, or mpx_run when nothing else is queued); `trace` must outlive it."""
+        n = len(begin)
+        b = (ctypes.c_uint64 * n)(*begin)
+        e = (ctypes.c_uint64 * n)(*end)
+        _ck("mpx_submit_trace_range_async", lib().mpx_submit_trace_range_async(self.h, trace, len(trace), b, e))
 
     def submit_range(self, trace, node, k0, k1, index=None):
         """mpx_submit of records [k0, k1) of `node`'s stream in an MPXT container, in place (no

@@ -18,6 +18,7 @@ headers and entries per decision.  tests/golden/full_size.json's cpu_s (the refe
 full-size traces, 16 shards) is reported beside it as a cross-check.
 
     python oracle/ref_leg_rate.py c3 --instances 131072 --procs 16      (c3 | c5 | c5c)
+    python oracle/ref_leg_rate.py loop --trace loop.mpxt --procs 16      (the closed loop's streams)
 prints one JSON object.
 """
 import argparse
@@ -58,17 +59,24 @@ def _worker(member):
 def main():
     global _TRACE
     ap = argparse.ArgumentParser()
-    ap.add_argument("leg", choices=sorted(LEGS))
+    ap.add_argument("leg", choices=sorted(LEGS) + ["loop"])
     ap.add_argument("--instances", type=int, default=1 << 17)
     ap.add_argument("--procs", type=int, default=16)
+    ap.add_argument("--trace", help="leg 'loop': the closed loop's recorded streams (an MPXT file) instead of "
+                                    "a generated trace")
     a = ap.parse_args()
-    import mpx
-    p = dict(LEGS[a.leg])
-    kind = getattr(mpx, p.pop("kind"))
     t0 = time.perf_counter()
-    _TRACE = mpx.generate_trace(kind, num_instances=a.instances, copy=False, **p)
+    if a.leg == "loop":
+        data = open(a.trace, "rb").read()
+        _TRACE = (ctypes.c_char * len(data)).from_buffer_copy(data)
+        a.instances = int.from_bytes(data[16:24], "little")
+    else:
+        import mpx
+        p = dict(LEGS[a.leg])
+        kind = getattr(mpx, p.pop("kind"))
+        _TRACE = mpx.generate_trace(kind, num_instances=a.instances, copy=False, **p)
     t_gen = time.perf_counter() - t0
-    member = a.leg != "c3"
+    member = a.leg not in ("c3", "loop")
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(a.procs) as pool:
         res = pool.map(_worker, [member] * a.procs, chunksize=1)

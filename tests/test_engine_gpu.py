@@ -1057,6 +1057,53 @@ def test_incremental_windows_c3(seed):
     assert got[2] == want[2]
 
 
+@pytest.mark.parametrize("seed,W,drain", [(5, 7, False), (6, 5, True), (7, 16, False)])
+def test_incremental_async_submit_equals_whole(seed, W, drain):
+    """The pipelined live loop (mpx_submit_trace_range_async: window k + 1 decoded on a host thread
+    while window k is built and run; mpx_run joins it when nothing else is queued, a Value readback
+    joins it first) == the whole run: counters summed over the windows, replies (drained per window,
+    which joins the decode in flight) and the final state, scalars, executed streams, chosen log and
+    digests, and the decisions of MPX_FLAG_DECISIONS."""
+    t = mpx.generate_trace(mpx.GEN_FAULTY, num_nodes=7, num_instances=1 << 15, seed=seed, batch=64, proposers=3,
+                           drop_rate=500, dup_rate=1000, max_delay=500)
+    want = _whole(t)
+    with mpx.Engine.for_trace(t) as e:
+        e.run()
+        want_dec = e.decisions()
+    hd = mpx.trace_header(t)
+    idx = mpx.trace_index(t)
+    n, m = hd["num_nodes"], max(hd["num_instances"], 1)
+    cuts = [[c * w // W for (c, _, _) in idx] for w in range(W + 1)]
+    tot = {k: 0 for k in COUNTERS}
+    sends = [[] for _ in range(n)]
+    with mpx.Engine(n, 0, m, flags=mpx.FLAG_INCREMENTAL | mpx.FLAG_DECISIONS) as e:
+        e.submit_window(t, cuts[0], cuts[1])
+        for w in range(1, W + 1):
+            if w < W:
+                e.submit_window_async(t, cuts[w], cuts[w + 1])
+            st = e.run()
+            for k in COUNTERS:
+                tot[k] += st[k]
+            if drain:
+                for src, dst, b in e.drain_sends():
+                    sends[src].append((dst, b))
+        assert tot == want[1]
+        if drain:
+            assert sends == want[0]
+        assert _observe(e, n, m) == want[2]
+        assert e.decisions() == want_dec
+
+
+def test_incremental_async_submit_refused_without_incremental():
+    """mpx_submit_trace_range_async needs an incremental multi-semantics engine (MPX_E_STATE)."""
+    t = mpx.generate_trace(mpx.GEN_CLEAN, num_nodes=3, num_instances=512, batch=256)
+    idx = mpx.trace_index(t)
+    with mpx.Engine(3, 0, 512) as e:
+        with pytest.raises(mpx.MpxError) as ex:
+            e.submit_window_async(t, [0] * 3, [c for (c, _, _) in idx])
+        assert ex.value.rc == -6
+
+
 @pytest.mark.parametrize("seed,u,m,b,drop,dup", [(51, 8, 1 << 15, 256, 100, 100), (52, 6, 20000, 90, 500, 500),
                                                   (53, 5, 9000, 33, 1000, 1000)])
 def test_incremental_windows_member(seed, u, m, b, drop, dup):

@@ -81,7 +81,8 @@ def main():
         bench_args = ["--c3-only", "--c3-steps", "3", "--c3-instances", str(a.instances)] + rest
     else:
         bench_args = ["--steps", "3", "--warmup", "0", "--instances", str(a.instances), "--nodes", str(a.nodes),
-                      "--c3-instances", "0", "--c5-instances", "0", "--c5c-instances", "0", "--shard-of", "0"] + rest
+                      "--c3-instances", "0", "--c5-instances", "0", "--c5c-instances", "0", "--shard-of", "0",
+                      "--loop-values", "0"] + rest
     lim = 480 if a.c5c else 400                     # (the contended trace takes ~2.5 min to generate and ingest)
     fetch = run_pass(["FETCH_SIZE"], a.outdir, bench_args, a.tag, lim)["FETCH_SIZE"]
     write = run_pass(["WRITE_SIZE"], a.outdir, bench_args, a.tag, lim)["WRITE_SIZE"]
