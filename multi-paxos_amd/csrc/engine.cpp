@@ -118,6 +118,7 @@ struct mpx_engine {
     DevBuf gp_dyn, gp_dyn_n;                // list plan path: the pairs k_plan_list lists for k_apply
     DevBuf gp_ext, gp_ext_n;                //   ... and those it describes by 5..8 segments (k_store_ext)
     DevBuf gp_chk, gp_chk_n;                //   ... and its planned pairs whose re-commits need the Value check
+    DevBuf gp_rt, gp_rt_n;                  //   ... and (member) its 9..16-segment pairs, planned again
     DevBuf decode_buf;                      // readback scratch (k_decode)
     DevBuf out, out_cursor, partials, viol, summary;
     uint64_t out_cap = 0;
@@ -604,6 +605,10 @@ static int finish_view(mpx_engine *e)
     TRY(e->gp_chk_n.alloc(8));
     v.gp_chk = e->gp_chk.as<uint64_t>();
     v.gp_chk_n = e->gp_chk_n.as<unsigned long long>();
+    TRY(e->gp_rt.alloc(std::max<size_t>(8ull * v.num_gp_snap, 8)));
+    TRY(e->gp_rt_n.alloc(8));
+    v.gp_rt = e->gp_rt.as<uint64_t>();
+    v.gp_rt_n = e->gp_rt_n.as<unsigned long long>();
     e->geom = launch_geometry(N, e->NB, e->num_cus);
 
     TRY(e->partials.alloc(8ull * 8 * ((uint64_t)e->num_cus * 16 + std::max<uint64_t>(e->geom.chosen_wgs, e->num_cus * 16))));

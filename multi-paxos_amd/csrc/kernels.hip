@@ -398,6 +398,7 @@ __device__ inline void reset_state(const DevView &v, uint32_t n_partials, uint64
         *v.gp_dyn_n = 0;
         *v.gp_ext_n = 0;
         *v.gp_chk_n = 0;
+        *v.gp_rt_n = 0;
         if (v.window) *v.outv_n = 0;
         for (uint32_t pc = 0; pc < 8; ++pc)          // the counter words k_reduce's workgroups add into
             if (summary_word(pc) >= 0) v.summary[summary_word(pc)] = 0;
@@ -1649,15 +1650,26 @@ __device__ inline bool seg_add_split(uint32_t x, uint32_t (&s)[LSEG - 1])
 // points and segment values, which k_store_ext writes one wave per pair (round 3 measured the
 // same walk writing those slots per thread: C3 general apply 1.01 -> 0.80 ms but k_plan_list
 // 0.19 -> 0.40 ms).
-template <bool MEMBER, uint32_t LSEG = 4, uint32_t F = MPLAN_FRAGS>
-__global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_wgs)
+// RETRY (member): the pairs the (LSEG = 8) plan listed only for having more segments, planned again
+// with up to 16 (the retry list gp_rt, one lane per pair, each lane's runs staged in its own LDS
+// row); what still does not fit goes to the listed-pair walk as before.  Contended C5: the walk's
+// pairs with more than 8 segments (one kernel at 16 segments needs 215
+// VGPRs and runs at 2 waves per SIMD over every pair: slower, profiles/r06_ab_member_plan16_2waves.txt).
+template <bool MEMBER, uint32_t LSEG = 4, uint32_t F = MPLAN_FRAGS, int WAVES = 4, bool RETRY = false>
+__global__ __launch_bounds__(256, WAVES) void k_plan_list(DevView v, uint32_t apply_wgs)
 {
-    __shared__ uint64_t w_lds[4][MPLAN_LDS];
+    constexpr uint32_t LDSW = RETRY ? 64 * F : MPLAN_LDS;
+    __shared__ uint64_t w_lds[4][LDSW];
     __shared__ unsigned long long red[4][4];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t N = v.N;
     const uint64_t NB = v.NB, np = (uint64_t)N * NB;
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (RETRY) {
+        const uint64_t nrt = *v.gp_rt_n;
+        if ((uint64_t)blockIdx.x * 256 >= nrt) return;      // (the grid covers every list pair: most blocks idle)
+        i = i < nrt ? v.gp_rt[i] : np;
+    }
     unsigned long long cA = 0, cL = 0, cC = 0, cP = 0;
     const uint64_t ic = i < np ? i : np, in = i < np ? i + 1 : np;
     const uint64_t oa = v.f_off[ic], o1 = v.f_off[in];
@@ -1669,14 +1681,30 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
     // the wave is decided (each window decides at least its first pair: len <= F)
     const uint64_t wend = rl64(o1, 63);
     const uint32_t len = (uint32_t)(o1 - oa);
-    uint64_t sbase = rl64(oa, 0);
+    uint64_t sbase = RETRY ? oa - (uint64_t)lane * F : rl64(oa, 0);
     bool todo = i < np;
     bool fb = false;                                   // list the pair for k_apply
+    bool rt = false;                                   // ... or for the retry at 16 segments (RETRY: never)
     bool ck = false;                                   // ... planned, its re-commits' Values to check
-    bool xt = false;                                   // ... or for k_store_ext (xw0: split points, xw1: values)
-    uint64_t xw0 = 0, xw1 = 0;
+    bool xt = false;                                   // ... or for k_store_ext (k_store_ext's item formats)
+    uint64_t xw0 = 0, xw1 = 0, xw2 = 0, xw3 = 0;
+    uint32_t xns = EXT_LEGACY;
     for (;;) {
-    {
+    if (RETRY) {
+        // each lane's own runs into its own LDS row (rel = lane * F), loads all in flight
+        const uint32_t L = todo && len <= F ? len : 0;
+        constexpr uint32_t K8 = 8;                             // (8 in flight at a time: no private array)
+        for (uint32_t k0 = 0; k0 < L; k0 += K8) {
+            uint64_t x0 = k0 + 0 < L ? v.frag_w1[oa + k0 + 0] : 0, x1 = k0 + 1 < L ? v.frag_w1[oa + k0 + 1] : 0;
+            uint64_t x2 = k0 + 2 < L ? v.frag_w1[oa + k0 + 2] : 0, x3 = k0 + 3 < L ? v.frag_w1[oa + k0 + 3] : 0;
+            uint64_t x4 = k0 + 4 < L ? v.frag_w1[oa + k0 + 4] : 0, x5 = k0 + 5 < L ? v.frag_w1[oa + k0 + 5] : 0;
+            uint64_t x6 = k0 + 6 < L ? v.frag_w1[oa + k0 + 6] : 0, x7 = k0 + 7 < L ? v.frag_w1[oa + k0 + 7] : 0;
+            uint64_t *d = &w_lds[wv][lane * F + k0];
+            d[0] = x0; if (k0 + 1 < L) d[1] = x1; if (k0 + 2 < L) d[2] = x2; if (k0 + 3 < L) d[3] = x3;
+            if (k0 + 4 < L) d[4] = x4; if (k0 + 5 < L) d[5] = x5; if (k0 + 6 < L) d[6] = x6; if (k0 + 7 < L) d[7] = x7;
+        }
+        wave_lds_fence();
+    } else {
         // the window's second words into LDS with coalesced loads, all in flight before the
         // LDS writes
         const uint32_t R = (uint32_t)(wend - sbase < MPLAN_LDS ? wend - sbase : MPLAN_LDS);
@@ -1696,24 +1724,29 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
         }
         wave_lds_fence();
     }
-    const bool wait = MEMBER && todo && len && gp == GP_LIST && len <= F && (i / N + 1) * BS <= v.shard_len &&
+    const bool wait = !RETRY && MEMBER && todo && len && gp == GP_LIST && len <= F && (i / N + 1) * BS <= v.shard_len &&
                       oa - sbase + len > MPLAN_LDS;
     if (todo && !wait) {
         todo = false;
         const uint64_t rel = oa - sbase, b = i / N;
         uint64_t q = PLAN_SKIP;
         if (len && gp == GP_LIST) {
-            bool ok = len <= F && rel + len <= MPLAN_LDS && (b + 1) * BS <= v.shard_len;
+            bool ok = len <= F && rel + len <= LDSW && (b + 1) * BS <= v.shard_len;
             uint64_t *const W = &w_lds[wv][ok ? rel : 0];
             uint32_t sp[LSEG - 1];
 #pragma unroll
             for (uint32_t k = 0; k < LSEG - 1; ++k) sp[k] = BS;
             if (ok) {
+                bool lean_all = true, fit_all = true;
                 for (uint32_t k = 0; k < len; ++k) {
                     const uint64_t w = W[k];
                     const uint32_t cnt = (uint32_t)(w >> 32) & 0xFFFF, st0 = (uint32_t)(w >> 48) & 0xFF;
-                    ok = ok && frag_lean(w) && seg_add_split<LSEG>(st0, sp) && seg_add_split<LSEG>(st0 + cnt, sp);
+                    lean_all = lean_all && frag_lean(w);
+                    if (lean_all && fit_all) fit_all = seg_add_split<LSEG>(st0, sp) && seg_add_split<LSEG>(st0 + cnt, sp);
                 }
+                // a pair that failed only on its segment count (every run lean): the retry
+                if (MEMBER && !RETRY && PLAN_RETRY) rt = lean_all && !fit_all;
+                ok = lean_all && fit_all;
             }
             if (ok) {
                 // the accept runs' scan flags, 16 in flight at a time, then folded into bit 57
@@ -1854,11 +1887,32 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
                     } else {
                         // 5..LSEG segments: the split points and segment values to the extension
                         // list (k_store_ext writes the slots; k_store skips the bucket)
-                        xw0 = xw1 = 0;
+                        if constexpr (LSEG <= 8) {
+                            // split points as 7 x 9 bits (BS = unused), segment values as bytes
+                            xw0 = xw1 = 0;
 #pragma unroll
-                        for (uint32_t k = 0; k < LSEG - 1 && k < 7; ++k) xw0 |= (uint64_t)(sp[k] & 0x1FF) << (9 * k);
+                            for (uint32_t k = 0; k < LSEG - 1 && k < 7; ++k) xw0 |= (uint64_t)(sp[k] & 0x1FF) << (9 * k);
 #pragma unroll
-                        for (uint32_t k = 0; k < LSEG && k < 8; ++k) xw1 |= (uint64_t)(val[k] & 0xFF) << (8 * k);
+                            for (uint32_t k = 0; k < LSEG && k < 8; ++k) xw1 |= (uint64_t)(val[k] & 0xFF) << (8 * k);
+                        } else {
+                            // up to 15 split points (1..255) as bytes, their count in the item's top byte;
+                            // up to 16 segment values as bytes
+                            xw0 = xw1 = xw2 = xw3 = 0;
+                            uint32_t ns = 0;
+#pragma unroll
+                            for (uint32_t k = 0; k < LSEG - 1; ++k) {
+                                if (sp[k] >= BS) continue;
+                                ++ns;
+                                if (k < 8) xw0 |= (uint64_t)(sp[k] & 0xFF) << (8 * k);
+                                else xw1 |= (uint64_t)(sp[k] & 0xFF) << (8 * (k - 8));
+                            }
+#pragma unroll
+                            for (uint32_t k = 0; k < LSEG; ++k) {
+                                if (k < 8) xw2 |= (uint64_t)(val[k] & 0xFF) << (8 * k);
+                                else xw3 |= (uint64_t)(val[k] & 0xFF) << (8 * (k - 8));
+                            }
+                            xns = ns;
+                        }
                         xt = true;
                     }
                     v.st_valid[i] = 1;
@@ -1868,12 +1922,23 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
             }
             if (fb) cA = cL = cP = 0;
         }
-        if (gp == GP_LIST || MEMBER) v.plan[i] = q;
+        if (!RETRY && (gp == GP_LIST || MEMBER)) v.plan[i] = q;
+        else if (RETRY && q != PLAN_SKIP) v.plan[i] = q;       // (the first plan wrote PLAN_SKIP)
     }
     const uint64_t rem = __ballot(todo);
-    if (!rem) break;
+    if (!rem || RETRY) break;
     sbase = rl64(oa, (uint32_t)__builtin_ctzll(rem));
     wave_lds_fence();                                  // the window is read: restage
+    }
+    if (!RETRY && MEMBER && PLAN_RETRY) {              // the retry list: fb pairs that failed only on segments
+        const uint64_t rm = __ballot(rt && fb);
+        if (rm) {
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(v.gp_rt_n, (unsigned long long)__popcll(rm));
+            base = __shfl(base, 0, 64);
+            if (rt && fb) v.gp_rt[base + (uint64_t)__popcll(rm & ((1ull << lane) - 1))] = i;
+        }
+        fb = fb && !rt;
     }
     const uint64_t fm = __ballot(fb);
     if (fm) {
@@ -1902,10 +1967,10 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
         base = __shfl(base, 0, 64);
         if (xt && !fb) {
             uint64_t *w = v.gp_ext + EXT_WORDS * (base + (uint64_t)__popcll(xm & ((1ull << lane) - 1)));
-            w[0] = i; w[1] = xw0; w[2] = xw1;
+            w[0] = i | (uint64_t)xns << 56; w[1] = xw0; w[2] = xw1; w[3] = xw2; w[4] = xw3;
         }
     }
-    if (MEMBER && i < NB) plan_chosen(v, i, cC);
+    if (MEMBER && !RETRY && i < NB) plan_chosen(v, i, cC);
     unsigned long long cc[4] = {cA, cL, cC, cP};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1923,24 +1988,41 @@ __global__ __launch_bounds__(256, 4) void k_plan_list(DevView v, uint32_t apply_
     }
 }
 
-// The slots of the pairs k_plan_list described by 5..8 segments: one wave per pair, 4 slots
-// per lane — the slot's segment is the number of split points at or below it, its value that
-// segment's (pair-local run + 1, or 0).
+// The slots of the pairs k_plan_list described by 5..PLAN_XSEG (multi) / PLAN_XSEG_MEMBER (member)
+// segments: one wave per pair, 4 slots per lane — the slot's segment is the number of split points
+// at or below it, its value that segment's (pair-local run + 1, or 0).  Items (EXT_WORDS words):
+// up to 8 segments {pair | EXT_LEGACY << 56, 7 x 9-bit split points (BS = unused), 8 value bytes};
+// up to 16 {pair | splits << 56, 15 split-point bytes (ascending) in two words, 16 value bytes in two}.
 __global__ __launch_bounds__(256) void k_store_ext(DevView v)
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t n_ext = *v.gp_ext_n, nwaves = (uint64_t)gridDim.x * 4;
     for (uint64_t x = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < n_ext; x += nwaves) {
-        const uint64_t i = v.gp_ext[EXT_WORDS * x], w0 = v.gp_ext[EXT_WORDS * x + 1], w1 = v.gp_ext[EXT_WORDS * x + 2];
+        const uint64_t *it = v.gp_ext + EXT_WORDS * x;
+        const uint64_t w = it[0], s0 = it[1], s1 = it[2], v0 = it[3], v1 = it[4];
+        const uint64_t i = w & ((1ull << 56) - 1);
+        const uint32_t ns = (uint32_t)(w >> 56);
         const uint64_t b = i / v.N, n = i - b * v.N;
         uint32_t val[4];
+        if (ns == EXT_LEGACY) {
 #pragma unroll
-        for (uint32_t t = 0; t < 4; ++t) {
-            const uint32_t sl = 4 * lane + t;
-            uint32_t g = 0;
+            for (uint32_t t = 0; t < 4; ++t) {
+                const uint32_t sl = 4 * lane + t;
+                uint32_t g = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < 7; ++k) g += sl >= ((w0 >> (9 * k)) & 0x1FF);
-            val[t] = (uint32_t)(w1 >> (8 * g)) & 0xFF;
+                for (uint32_t k = 0; k < 7; ++k) g += sl >= ((s0 >> (9 * k)) & 0x1FF);
+                val[t] = (uint32_t)(s1 >> (8 * g)) & 0xFF;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t) {
+                const uint32_t sl = 4 * lane + t;
+                uint32_t g = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < 15; ++k)
+                    g += k < ns && sl >= (uint32_t)(((k < 8 ? s0 : s1) >> (8 * (k & 7))) & 0xFF);
+                val[t] = (uint32_t)((g < 8 ? v0 : v1) >> (8 * (g & 7))) & 0xFF;
+            }
         }
         const uint64_t at = n * v.shard_len + (b << BSH) + 4 * lane;
         if (v.slot_w == 1)
@@ -3667,8 +3749,19 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
         if (member) {
             // (8 segments / 32 runs since the Value check left the walk — 128 VGPRs, no spill:
             // C5 0.451 -> 0.384 ms, contended C5 2.745 -> 2.582 ms, profiles/r04_v25_ab_member_plan8.json)
-            hipExtLaunchKernelGGL((k_plan_list<true, PLAN_XSEG, PLAN_XFRAGS>), dim3(plan_blocks), dim3(256), 0, s,
-                                  (hipEvent_t)ev_apply0, side3 ? (hipEvent_t)side.fork3b : (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+            if constexpr (PLAN_RETRY) {
+                // the 9..16-segment pairs planned again (one lane per listed pair, 2 waves per SIMD);
+                // the listed-pair walk starts after it
+                hipExtLaunchKernelGGL((k_plan_list<true, PLAN_XSEG_MEMBER, PLAN_XFRAGS, PLAN_WAVES_MEMBER>), dim3(plan_blocks),
+                                      dim3(256), 0, s, (hipEvent_t)ev_apply0, (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+                hipExtLaunchKernelGGL((k_plan_list<true, PLAN_RETRY_SEG, PLAN_XFRAGS, 2, true>), dim3(cdiv(v.num_gp_snap ? v.num_gp_snap : 1, 256)), dim3(256), 0,
+                                      s, (hipEvent_t)nullptr, side3 ? (hipEvent_t)side.fork3b : (hipEvent_t)nullptr, 0, v,
+                                      g.apply_wgs);
+            } else {
+                hipExtLaunchKernelGGL((k_plan_list<true, PLAN_XSEG_MEMBER, PLAN_XFRAGS, PLAN_WAVES_MEMBER>), dim3(plan_blocks),
+                                      dim3(256), 0, s, (hipEvent_t)ev_apply0,
+                                      side3 ? (hipEvent_t)side.fork3b : (hipEvent_t)nullptr, 0, v, g.apply_wgs);
+            }
             if (side3) {                                 // (the listed pairs' walk, the step's longest chain)
                 (void)hipStreamWaitEvent(s3, (hipEvent_t)side.fork3b, 0);
                 launch_listed(s3);

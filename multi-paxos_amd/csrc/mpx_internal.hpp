@@ -284,6 +284,10 @@ struct DevView {
     // for k_commit_check, which compares their Values slot by slot; gp_chk_n counts them
     uint64_t *gp_chk;
     unsigned long long *gp_chk_n;
+    // ... and (member) the pairs it listed only for having more than PLAN_XSEG_MEMBER segments: their
+    // pair indices, planned again with up to 16 by k_plan_list<..., RETRY>; gp_rt_n counts them
+    uint64_t *gp_rt;
+    unsigned long long *gp_rt_n;
     const uint64_t *ev_off;         // N * NB + 1: snapshot events per pair (ingest.cpp), message order
     const uint32_t *ev_msg;
     // promise-quorum chunks (k_prop_chunk / k_prop_node): PROP_CHUNK records of one
@@ -388,8 +392,28 @@ constexpr uint32_t MPLAN_FRAGS = 16;
 constexpr uint32_t MPLAN_LDS = 1024;
 constexpr uint32_t PLAN_XSEG = 8;            // k_plan_list: up to 8 segments, 32 runs per pair
 constexpr uint32_t PLAN_XFRAGS = 32;
+#ifndef MPX_PLAN_XSEG_MEMBER
+#define MPX_PLAN_XSEG_MEMBER 8
+#endif
+// member k_plan_list: segments and waves per SIMD (A/B knobs: 16 segments need 215 VGPRs, 2 waves —
+// contended C5 1.791 vs 1.515 ms at 8 / 4, profiles/r06_ab_member_plan16_2waves.txt)
+constexpr uint32_t PLAN_XSEG_MEMBER = MPX_PLAN_XSEG_MEMBER;
+#ifndef MPX_PLAN_WAVES_MEMBER
+#define MPX_PLAN_WAVES_MEMBER 4
+#endif
+constexpr int PLAN_WAVES_MEMBER = MPX_PLAN_WAVES_MEMBER;
+// member: the 9..16-segment retry of the pairs the plan lists for their segment count (k_plan_list
+// RETRY, an A/B build variant: contended C5 2.405 vs 1.515 ms, C5 0.525 vs 0.387 ms without it — the
+// retry kernel spills 1.4 KB per lane at 16 segments and its launch sits on the plan -> listed-walk
+// chain; profiles/r06_ab_member_retry.txt)
+#ifndef MPX_PLAN_RETRY
+#define MPX_PLAN_RETRY 0
+#endif
+constexpr bool PLAN_RETRY = MPX_PLAN_RETRY != 0;
+constexpr uint32_t PLAN_RETRY_SEG = 16;
 constexpr uint32_t CHK_WORDS = 3;           // gp_chk items
-constexpr uint32_t EXT_WORDS = 3;
+constexpr uint32_t EXT_WORDS = 5;
+constexpr uint32_t EXT_LEGACY = 0xFF;       // k_store_ext item of <= 8 segments (9-bit split points)
 // the distinct run boundaries inside (0, 256), sorted into s[0..2] (BS = unused);
 // false once a fourth one appears
 MPX_HD inline bool plan_add_split(uint32_t x, uint32_t (&s)[3])
