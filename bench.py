@@ -13,16 +13,18 @@ state: header scan, promise quorum, accept-vote quorum, acceptor/learner apply
 64-word per-shard summary.  decisions/s = chosen instances per step (summed
 over ranks) / max-over-ranks step time.
 
-roofline: the dominant unit is the apply phase — k_plan (one thread per
-(acceptor, bucket) pair decides which message run fixes it) and k_store8
-(streams the slots and the chosen log) — bracketed by HIP events on the
-engine's stream; k_store8 is most of it (profiles/).  frac is the hardware
+roofline: the dominant unit is the apply phase — k_plan_store8, one launch:
+per 32-bucket group, one thread per (acceptor, bucket) pair decides which
+message run fixes it into LDS while other waves of the workgroup stream the
+previous group's slots and chosen log (before round 6: k_plan + k_store8,
+the plan words through HBM) — bracketed by HIP events on the engine's
+stream.  frac is the hardware
 fraction: traffic (HBM bytes per launch of those kernels from rocprofv3 PMC,
 FETCH_SIZE x2 + WRITE_SIZE, committed under profiles/ and matched to these
 sources by digest, tools/pmc_traffic.py) / the phase's mean duration in this
 run / 8 TB/s.  Beside it: the engine's own byte model (1-byte
-slot per (acceptor, instance), 1-byte chosen log, 16-byte descriptors per run,
-plan words; frac_engine_model) and SURVEY.md §8(d)'s 16 P + 24 A + 16 L
+slot per (acceptor, instance), 1-byte chosen log, 16-byte descriptors per run;
+frac_engine_model) and SURVEY.md §8(d)'s 16 P + 24 A + 16 L
 (frac_survey_model, > 1 on the clean trace: a measure of the representation,
 not a bandwidth).  Without a matching profile frac falls back to the engine
 model and roofline.basis says so.
@@ -844,8 +846,8 @@ def main():
     chosen_total = tot["chosen"]
     assert chosen_total == M, "chosen %d != %d instances" % (chosen_total, M)
     assert tot["violations"] == 0
-    # verification, outside the timed region: (1) the state the last TIMED step's kernels
-    # (k_plan + k_store8) wrote, digested by a separate device pass; (2) one digested run
+    # verification, outside the timed region: (1) the state the last TIMED step's kernel
+    # (k_plan_store8) wrote, digested by a separate device pass; (2) one digested run
     want_state, want_chosen = clean_expect(N, sb, se)
     step_state, step_chosen = eng.state_digest()
     step_ok = (step_state, step_chosen) == (want_state, want_chosen) and \
@@ -876,11 +878,12 @@ def main():
     L = se - sb
     # 1-B state slots + 1-B chosen log (the device-generated clean trace has 2 runs per pair, so
     # mpx_load_clean_device picks 1-byte slots) + the ACCEPT and COMMIT descriptors of every (node, bucket)
-    # + the plan word of every (row, bucket), written by k_plan and read by k_store
+    # (k_plan_store8 keeps the plan words in LDS; before round 6, k_plan wrote them and k_store8 read them back:
+    # + 16 B per (row, bucket))
     nb = (L + 255) // 256
     runs = sum(((min(b0 + 256, se) - 1) // args.batch - b0 // args.batch + 1)
                for b0 in range(sb, se, 256)) if args.batch != 256 else nb   # batch runs meeting each bucket
-    bytes_min = 1 * N * L + 1 * L + 2 * 16 * N * runs + 2 * 8 * (N + 1) * nb
+    bytes_min = 1 * N * L + 1 * L + 2 * 16 * N * runs
     achieved_eng = bytes_min / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0
     pmc = latest_pmc(N, M, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
@@ -944,12 +947,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "basis": basis,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "apply phase: k_plan + k_store8",
+                         "kernel": "apply phase: k_plan_store8 (plan in LDS + store, one launch)",
                          "kernel_ms": apply_mean, "bytes_alg_per_launch": bytes_min,
                          "achieved_engine_model": achieved_eng,
                          "frac_engine_model": achieved_eng / HBM_PEAK_GBS,
                          "bytes_model": "engine model, DESIGN.md §4: 1-B slot per (acceptor, instance) + 1-B chosen "
-                                        "log + 16-B ACCEPT / COMMIT descriptors per run + 8-B plan words",
+                                        "log + 16-B ACCEPT / COMMIT descriptors per run (plan words stay in LDS)",
                          "bytes_survey_model_per_launch": bytes_survey,
                          "survey_model_gbps": bytes_survey / (apply_mean * 1e-3) / 1e9 if apply_mean else 0.0,
                          "frac_survey_model": bytes_survey / (apply_mean * 1e-3) / 1e9 / HBM_PEAK_GBS
@@ -957,7 +960,7 @@ def main():
                          "note": "frac = PMC traffic / kernel_ms / 8 TB/s (what the HBM moved); frac_survey_model is "
                                  "NOT a fraction when > 1. "
                                  "The clean trace fixes every (acceptor, bucket) pair with one full run, so its apply "
-                                 "phase reduces to one plan word per pair and a byte stream of slots (k_store8): the "
+                                 "phase reduces to one plan word per pair and a byte stream of slots (k_plan_store8): the "
                                  "survey model's 360 B/instance (16-B slot writes + per-acceptor Value reads) are "
                                  "never moved, and frac_survey_model > 1 measures representation, not bandwidth; "
                                  "c3.roofline is the per-slot general path on the survey's bytes"},

@@ -45,6 +45,12 @@ struct DevBuf {
         if (!n) return MPX_OK;
         n = (n + 63) & ~(size_t)63;     // padded: vector loads may read a tail word past the last element
         if (hipMalloc(&p, n) != hipSuccess) { p = nullptr; return MPX_E_NOMEM; }
+#ifdef MPX_AB
+        if (ab_env("MPX_POISON")) {                     // (A/B builds: find reads of unwritten memory; the
+            (void)hipMemset(p, 0xA5, n);                // null stream does not order the non-blocking
+            (void)hipDeviceSynchronize();               // engine streams, so wait here)
+        }
+#endif
         bytes = n;
         return MPX_OK;
     }
@@ -870,6 +876,9 @@ static int queue_run(mpx_engine *e, bool digest)
     e->view.walk_all = 0;
     if (const char *x = std::getenv("MPX_STEP_WALK")) e->view.walk_all = std::atoi(x) ? 1 : 0;
     if (const char *x = ab_env("MPX_STORE_WGS_PER_CU")) g.store_wgs = std::max<uint32_t>(1, e->num_cus * (uint32_t)std::atoi(x));
+    // MPX_PLAN_STORE=0: the C4 shape takes k_plan + k_store8 (the path before k_plan_store8)
+    if (const char *x = std::getenv("MPX_PLAN_STORE")) if (!std::atoi(x)) g.ps_wgs = 0;
+    if (const char *x = ab_env("MPX_PS_WGS_PER_CU")) g.ps_wgs = std::max<uint32_t>(1, e->num_cus * (uint32_t)std::atoi(x));
     if (const char *x = ab_env("MPX_CHOSEN_WGS_PER_CU"))     // (partials hold 16 per CU for it too)
         g.chosen_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(e->NB, (uint64_t)e->num_cus * 16),
                                                                           (uint64_t)e->num_cus * std::atoi(x)));
@@ -2984,7 +2993,10 @@ extern "C" int mpx_load_clean_device(mpx_engine *e, const mpx_gen_params *p)
     v.r_pid = e->r_pid.as<uint64_t>(); v.r_val = e->r_val.as<uint64_t>(); v.r_slot = e->r_slot.as<uint8_t>();
     v.g_a = e->g_a.as<uint64_t>(); v.g_b = e->g_b.as<uint64_t>();
     v.f_off = e->f_off.as<uint64_t>(); v.frags = e->frags.as<Frag>();
-    TRY(e->f_pid.alloc(8));                          // (no promise-reply runs: never read)
+    // (no promise-reply runs, so no proposal id is used — but the promise-round walk, k_apply
+    // AM_FULL, loads f_pid beside every descriptor of the pairs it takes: the work-list pairs
+    // here, a partial last bucket or more than FAST_MAX_NODES nodes, need it sized like frags)
+    TRY(e->f_pid.alloc(gd.empty() ? 8 : 8 * (f_off[N * NB] + 1)));
     v.f_pid = e->f_pid.as<uint64_t>();
     e->num_frags = f_off[N * NB];
     v.num_gp = gd.size() / GP_WORDS; v.gp_list = e->gp_list.as<uint64_t>(); v.num_gp_simple = 0; v.num_gp_snap = 0;

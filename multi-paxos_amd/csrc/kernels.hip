@@ -1397,10 +1397,9 @@ __device__ inline uint64_t plan_pack(const uint32_t (&val)[4], const uint32_t (&
 // four segments describe the bucket and no instance lies under two live runs
 // (k_chosen compares their Values) the word is written and chosen_valid set,
 // else PLAN_SKIP leaves the bucket to k_chosen.
-__device__ inline void plan_chosen(const DevView &v, uint64_t i, unsigned long long &cC)
+__device__ inline uint64_t plan_chosen_at(const DevView &v, uint64_t i, uint64_t oc, uint64_t c1, unsigned long long &cC)
 {
     constexpr uint32_t F = PLAN_FRAGS;
-    const uint64_t oc = v.cf_off[i], c1 = v.cf_off[i + 1];
     const uint32_t len = (uint32_t)(c1 - oc);
     uint64_t q = PLAN_SKIP;
     if (len && len <= F && (i + 1) * BS <= v.shard_len) {
@@ -1442,7 +1441,70 @@ __device__ inline void plan_chosen(const DevView &v, uint64_t i, unsigned long l
             cC = c;
         }
     }
-    v.plan[(uint64_t)v.N * v.NB + i] = q;
+    return q;
+}
+__device__ inline uint64_t plan_chosen_word(const DevView &v, uint64_t i, unsigned long long &cC)
+{
+    return plan_chosen_at(v, i, v.cf_off[i], v.cf_off[i + 1], cC);
+}
+__device__ inline void plan_chosen(const DevView &v, uint64_t i, unsigned long long &cC)
+{
+    v.plan[(uint64_t)v.N * v.NB + i] = plan_chosen_word(v, i, cC);
+}
+
+// k_plan's reduction of lean multi pair i (bucket b, len runs): its plan word, or PLAN_SKIP
+// (rest = 1 when the pair is in the list but no plan word describes it).  ldw(k) loads the
+// pair's k-th run descriptor word.
+template <typename LoadW>
+__device__ inline uint64_t plan_lean(const DevView &v, uint64_t i, uint64_t b, uint32_t len, bool in_list, LoadW ldw,
+                                     unsigned long long &cA, unsigned long long &cL, uint32_t &rest)
+{
+    constexpr uint32_t F = PLAN_FRAGS;
+    uint64_t q = PLAN_SKIP;
+    if (in_list && len <= F) {
+        uint64_t w[F];
+        uint32_t fg[F];
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) w[k] = k >= len ? 0 : ldw(k);
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k)   // a COMMIT run's scan flag is never read
+            fg[k] = k < len && (w[k] >> 60) != K_COMMIT ? v.m_flags[(uint32_t)w[k]] : 0;
+        bool ok = (b + 1) * BS <= v.shard_len;
+        uint32_t sp[3] = {BS, BS, BS};
+#pragma unroll
+        for (uint32_t k = 0; k < F; ++k) {
+            if (k >= len) continue;
+            const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
+            ok = ok && frag_lean(w[k]) && plan_add_split(st0, sp) && plan_add_split(st0 + cnt, sp);
+        }
+        uint32_t val[4];
+        unsigned long long a = 0, l = 0;
+#pragma unroll
+        for (uint32_t g = 0; g < 4; ++g) {
+            const uint32_t lo = g ? sp[g - 1] : 0, hi = g < 3 ? sp[g] : BS;
+            if (lo >= BS) { val[g] = val[g - 1]; continue; }
+            bool comm = false;
+            uint32_t fix = NONE32, nA = 0, nL = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k) {
+                if (k >= len) continue;
+                const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
+                if (lo < st0 || lo >= st0 + cnt) continue;          // segments lie inside or outside a run
+                if ((w[k] >> 60) == K_COMMIT) { ++nL; if (comm) ok = false; else { comm = true; fix = k; } }
+                else if (!comm && (fg[k] & F_GRANTED)) { ++nA; fix = k; }
+            }
+            val[g] = fix == NONE32 ? 0 : fix + 1;               // the slot as stored: pair-local fragment + 1
+            a += (unsigned long long)nA * (hi - lo);
+            l += (unsigned long long)nL * (hi - lo);
+        }
+        if (ok) {
+            q = plan_pack(val, sp);
+            v.st_valid[i] = 1;
+            cA += a; cL += l;
+        }
+    }
+    if (q == PLAN_SKIP && in_list) ++rest;
+    return q;
 }
 
 // Apply split in two (the default for multi runs): k_plan decides every pair
@@ -1460,7 +1522,6 @@ __device__ inline void plan_chosen(const DevView &v, uint64_t i, unsigned long l
 // fast_rest and left to k_apply_fast<.., AFTER_STORE>.
 __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
 {
-    constexpr uint32_t F = PLAN_FRAGS;
     __shared__ unsigned long long red[4][3];
     __shared__ uint32_t rest_w[4];
     __shared__ uint64_t w_lds[4][PLAN_LDS];
@@ -1502,53 +1563,10 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
 
         const uint32_t len = (uint32_t)(o1 - oa);
         const bool in_list = len && len <= FAST_MAX_FRAGS && !gp;
-        uint64_t q = PLAN_SKIP;
-        if (in_list && len <= F) {
-            uint64_t w[F];
-            uint32_t fg[F];
-            const uint64_t rel = oa - wbase;                 // past the staged words: global loads (rare)
-#pragma unroll
-            for (uint32_t k = 0; k < F; ++k)
-                w[k] = k >= len ? 0 : rel + k < PLAN_LDS ? w_lds[wv][rel + k] : v.frag_w1[oa + k];
-#pragma unroll
-            for (uint32_t k = 0; k < F; ++k)   // a COMMIT run's scan flag is never read
-                fg[k] = k < len && (w[k] >> 60) != K_COMMIT ? v.m_flags[(uint32_t)w[k]] : 0;
-            bool ok = (b + 1) * BS <= v.shard_len;
-            uint32_t sp[3] = {BS, BS, BS};
-#pragma unroll
-            for (uint32_t k = 0; k < F; ++k) {
-                if (k >= len) continue;
-                const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
-                ok = ok && frag_lean(w[k]) && plan_add_split(st0, sp) && plan_add_split(st0 + cnt, sp);
-            }
-            uint32_t val[4];
-            unsigned long long a = 0, l = 0;
-#pragma unroll
-            for (uint32_t g = 0; g < 4; ++g) {
-                const uint32_t lo = g ? sp[g - 1] : 0, hi = g < 3 ? sp[g] : BS;
-                if (lo >= BS) { val[g] = val[g - 1]; continue; }
-                bool comm = false;
-                uint32_t fix = NONE32, nA = 0, nL = 0;
-#pragma unroll
-                for (uint32_t k = 0; k < F; ++k) {
-                    if (k >= len) continue;
-                    const uint32_t cnt = (uint32_t)(w[k] >> 32) & 0xFFFF, st0 = (uint32_t)(w[k] >> 48) & 0xFF;
-                    if (lo < st0 || lo >= st0 + cnt) continue;          // segments lie inside or outside a run
-                    if ((w[k] >> 60) == K_COMMIT) { ++nL; if (comm) ok = false; else { comm = true; fix = k; } }
-                    else if (!comm && (fg[k] & F_GRANTED)) { ++nA; fix = k; }
-                }
-                val[g] = fix == NONE32 ? 0 : fix + 1;               // the slot as stored: pair-local fragment + 1
-                a += (unsigned long long)nA * (hi - lo);
-                l += (unsigned long long)nL * (hi - lo);
-            }
-            if (ok) {
-                q = plan_pack(val, sp);
-                v.st_valid[i] = 1;
-                cA = a; cL = l;
-            }
-        }
-        if (q == PLAN_SKIP && in_list) rest = 1;
-        v.plan[i] = q;
+        const uint64_t rel = oa - wbase;                     // past the staged words: global loads (rare)
+        v.plan[i] = plan_lean(v, i, b, len, in_list,
+                              [&](uint32_t k) { return rel + k < PLAN_LDS ? w_lds[wv][rel + k] : v.frag_w1[oa + k]; },
+                              cA, cL, rest);
     }
     if (i < NB) plan_chosen(v, i, cC);
     unsigned long long cc[3] = {cA, cL, cC};
@@ -2293,6 +2311,130 @@ __global__ __launch_bounds__(256) void k_store8(DevView v, uint32_t store_grid, 
         __builtin_nontemporal_store(u8x4{(uint8_t)plan_slot(q, s0), (uint8_t)plan_slot(q, s0 + 1),
                                          (uint8_t)plan_slot(q, s0 + 2), (uint8_t)plan_slot(q, s0 + 3)},
                                     reinterpret_cast<u8x4 *>(st + r * v.shard_len + (b << BSH) + s0));
+    }
+}
+
+// Plan and store in one launch (the C4 shape only — every pair lean, the chosen log planned
+// statically, the store ends the step: run_ends_with_store — with 1-byte slots).  A workgroup
+// of 8 waves takes groups of PS_G buckets: waves 0 .. PS_PW-1 plan a group into one LDS buffer
+// — lane t < PS_G * N the group's pair t (plan_lean, its descriptors loaded straight from
+// frag_w1: the group's pairs are consecutive), the lanes of the last planner wave its buckets'
+// chosen-log words (plan_chosen_word, no divergence with the pair lanes) — while the other
+// waves store the previous group's rows from the other buffer (1 KiB nontemporal stores of 4
+// buckets each); then all cross a barrier that orders LDS only (the stores stay in flight) and
+// swap buffers.  No plan words go through HBM, there is no k_plan launch, and a group's
+// dependent descriptor / flag loads run under the previous group's stores — so a group's store
+// has to outlast a plan's three dependent round trips under that write traffic (PS_G: C4 shard
+// 62.1 -> 53.4 us, C4 0.364 -> 0.344 ms at 32 buckets / 6 planner waves; 16 / 24 / 28 / 40
+// buckets slower, as is loading the next group's offsets a group ahead (one round trip less
+// per plan, 73 VGPRs: shard 54.2 us, C4 0.361 ms), profiles/r06_ab_plan_store.json).  The
+// plan counters go straight to the summary words (one atomic per counter and workgroup);
+// workgroups [ps_grid, gridDim.x) fold the partial rows of the kernels before (k_store8<..,
+// REDUCE>'s split).  
+#ifndef MPX_PS_G
+#define MPX_PS_G 32
+#endif
+#ifndef MPX_PS_PW
+#define MPX_PS_PW 6
+#endif
+constexpr uint32_t PS_G = MPX_PS_G, PS_PW = MPX_PS_PW, PS_CHOSEN = 64 * (PS_PW - 1);
+static_assert(PS_G % 4 == 0 && PS_G <= 64 && PS_PW >= 2 && PS_PW <= 7, "k_plan_store8 shape");
+__device__ inline void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// (72 VGPRs: 3 workgroups per CU; MPX_PS_WAVES=8 forces 64 with a 28-B spill, A/B build)
+#ifndef MPX_PS_WAVES
+#define MPX_PS_WAVES 6
+#endif
+#ifndef MPX_PS_WPC
+#define MPX_PS_WPC (MPX_PS_WAVES / 2)
+#endif
+__global__ __launch_bounds__(512, MPX_PS_WAVES) void k_plan_store8(DevView v, uint32_t ps_grid, uint32_t n_partials)
+{
+    constexpr uint32_t S = 8 - PS_PW, KPR = PS_G / 4;        // storer waves, KiB stores per row
+    __shared__ uint64_t pw[2][64 * PS_PW];
+    __shared__ unsigned long long red[8][8];
+    if (blockIdx.x >= ps_grid) {
+        const uint32_t r = blockIdx.x - ps_grid, R = gridDim.x - ps_grid;
+        reduce_summary<8>(v, n_partials, red, 512 * r, 512 * R, r == 0);
+        return;
+    }
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const bool planner = wv < PS_PW;
+    const uint32_t N = v.N;
+    const uint64_t NB = v.NB, ngroups = (NB + PS_G - 1) / PS_G;
+    uint8_t *const st = static_cast<uint8_t *>(v.st);
+    unsigned long long cA = 0, cL = 0, cC = 0;
+    uint32_t rest = 0;
+    auto plan_group = [&](uint64_t g, uint64_t *out) {
+        const uint64_t b0 = g * PS_G;
+        uint64_t q = PLAN_SKIP;
+        if (t < PS_G * N) {
+            const uint64_t i = b0 * N + t, b = b0 + t / N;
+            if (b < NB) {
+                const uint64_t oa = v.f_off[i], o1 = v.f_off[i + 1];
+                const uint8_t gp = v.pair_gp[i];
+                const uint32_t len = (uint32_t)(o1 - oa);
+                const bool in_list = len && len <= FAST_MAX_FRAGS && !gp;
+                q = plan_lean(v, i, b, len, in_list, [&](uint32_t k) { return v.frag_w1[oa + k]; }, cA, cL, rest);
+            }
+        } else if (t >= PS_CHOSEN && t < PS_CHOSEN + PS_G) {
+            const uint64_t b = b0 + (t - PS_CHOSEN);
+            if (b < NB) {
+                unsigned long long c = 0;
+                q = plan_chosen_word(v, b, c);
+                cC += c;
+            }
+        }
+        out[t] = q;
+    };
+    auto store_group = [&](uint64_t g, const uint64_t *in) {
+        const uint32_t p16 = 16 * (lane & 15);
+        uint8_t *const base = st + ((g * PS_G) << BSH) + p16;
+        for (uint32_t u = wv - PS_PW; u < (N + 1) * KPR; u += S) {
+            const uint32_t r = u / KPR, bl = 4 * (u - r * KPR) + (lane >> 4);
+            const uint64_t q = in[r < N ? bl * N + r : PS_CHOSEN + bl];   // (PLAN_SKIP past NB)
+            if (q == PLAN_SKIP) continue;
+            u32x4 x;
+            if (__ballot((uint32_t)(q >> 32) != PLAN_UNI)) x = plan_bytes16(q, p16);
+            else x = u32x4{(uint32_t)q, (uint32_t)q, (uint32_t)q, (uint32_t)q};
+            __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(base + (uint64_t)r * v.shard_len + ((uint64_t)bl << BSH)));
+        }
+    };
+    uint64_t g = blockIdx.x;                                  // (uniform: every wave crosses every barrier)
+    uint32_t buf = 0;
+    if (planner && g < ngroups) plan_group(g, pw[0]);
+    lds_barrier();
+    for (; g < ngroups; g += ps_grid) {
+        const uint64_t gn = g + ps_grid;
+        if (planner) {
+            if (gn < ngroups) plan_group(gn, pw[buf ^ 1]);
+        } else {
+            store_group(g, pw[buf]);
+        }
+        lds_barrier();
+        buf ^= 1;
+    }
+    if (planner) {
+        unsigned long long cc[4] = {cA, cL, cC, rest};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            unsigned long long x = cc[k];
+            for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+            if (lane == 0) red[wv][k] = x;
+        }
+    }
+    __syncthreads();
+    if (t < 4) {
+        unsigned long long x = 0;
+        for (uint32_t k = 0; k < PS_PW; ++k) x += red[k][t];
+        if (x) {
+            if (t == 3) atomicAdd(v.fast_rest, (uint32_t)x);
+            else atomicAdd(&v.summary[summary_word(t == 0 ? PC_A : t == 1 ? PC_L : PC_C)], x);
+        }
     }
 }
 
@@ -3593,6 +3735,9 @@ LaunchGeom launch_geometry(uint32_t N, uint64_t NB, uint32_t num_cus)
     const uint64_t chunks = (uint64_t)(N + 1) * (NB / 128 + 1), want = chunks / 10;
     const uint64_t hi = (uint64_t)num_cus * 8;
     g.store_wgs = (uint32_t)(want > hi ? hi : want < num_cus ? num_cus : want);
+    // k_plan_store8: MPX_PS_WPC workgroups of 8 waves per CU (all resident), at most one per group
+    const uint64_t groups = (NB + PS_G - 1) / PS_G, ps = (uint64_t)num_cus * MPX_PS_WPC;
+    g.ps_wgs = (uint32_t)(groups < 1 ? 1 : groups < ps ? groups : ps);
     return g;
 }
 
@@ -3745,6 +3890,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
     };
     const uint32_t plan_blocks = cdiv((uint64_t)v.N * v.NB, 256);
     bool chosen_done = false;                            // k_chosen launched on s3 already
+    // plan and store in one launch (k_plan_store8) where the store ends the step
+    const bool plan_store = PLAN_STORE && fuse_reduce && v.slot_w == 1 && PS_G * v.N <= PS_CHOSEN && g.ps_wgs;
     if (plan_path) {
         if (member) {
             // (8 segments / 32 runs since the Value check left the walk — 128 VGPRs, no spill:
@@ -3773,6 +3920,9 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
             // member k_plan_list planned the chosen log too: k_chosen walks the rest beside the listed
             // pairs (it reads only the votes and the chosen-log runs)
             if (side3 && !skip_chosen) { launch_chosen(s, nullptr); chosen_done = true; }
+        } else if (plan_store) {
+            hipExtLaunchKernelGGL(k_plan_store8, dim3(g.ps_wgs + cdiv(n_partials ? n_partials : 1, 512)), dim3(512), 0, s,
+                                  (hipEvent_t)ev_apply0, (hipEvent_t)ev_apply1, 0, v, g.ps_wgs, n_partials);
         } else {
             // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
             // written as NN + 1 KiB stores, loads three / two / one step ahead — measured slower:
@@ -3808,7 +3958,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
         // every pair the trace marks lean (pair_gp 0) is one k_plan can describe (ingest.cpp /
         // mpx_load_clean_device use its predicate, plan_shape_ok), so nothing is left for the
         // lean per-slot kernel after the store (fast_rest 0, checked when the run is collected)
-        launch_store((hipEvent_t)ev_apply1);
+        if (!plan_store) launch_store((hipEvent_t)ev_apply1);
     } else if (member) {
         if (ev_apply1) (void)hipEventRecord((hipEvent_t)ev_apply1, s);
     } else {

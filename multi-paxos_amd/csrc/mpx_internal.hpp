@@ -473,7 +473,12 @@ MPX_HD inline uint64_t scalar_digest(uint32_t node, uint64_t promised, uint64_t 
 }
 
 // kernels (kernels.hip); every launcher queues on `stream`, returns hipError_t as int
-struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, store_wgs; };
+// k_plan_store8 (kernels.hip) in place of k_plan + k_store8 on the C4 shape (A/B build flag)
+#ifndef MPX_PLAN_STORE
+#define MPX_PLAN_STORE 1
+#endif
+constexpr bool PLAN_STORE = MPX_PLAN_STORE != 0;
+struct LaunchGeom { uint32_t apply_wgs, chosen_wgs, store_wgs, ps_wgs; };
 // ev (hipEvent_t, each may be null): begin, apply phase start (after the header
 // scan / quorum kernels), after the plan / store / fast-apply kernels, after the
 // general k_apply, end

@@ -198,6 +198,29 @@ def test_device_generator_matches_host(n, m, b):
             st["chosen_digest"], st["state_digest"], st["scalar_digest"]] == ostats
 
 
+@pytest.mark.parametrize("n,m,b,sb", [(9, 1 << 23, 256, 0), (9, (1 << 23) + 256 * 7 + 13, 100, 0), (10, 1 << 22, 255, 0), (11, 1 << 21, 256, 0),
+                                      (5, 1 << 23, 256, 256 * 1000), (9, 1 << 20, 256, 0), (2, 256 * 33, 256, 0)])
+def test_plan_store_matches_plan_then_store(n, m, b, sb, monkeypatch):
+    """k_plan_store8 (the C4 shape's one-launch plan + store: workgroups looping over
+    32-bucket groups, a partial last group, shard offsets) leaves the same state and chosen
+    log as k_plan + k_store8 (MPX_PLAN_STORE=0) and as the digested run, with the same
+    counters."""
+    res = []
+    for ps in ("1", "0"):
+        monkeypatch.setenv("MPX_PLAN_STORE", ps)
+        with mpx.Engine(n, sb, m) as e:
+            e.load_clean_device(num_instances=m, batch=b)
+            st = e.run()
+            e.step()
+            e.sync()
+            got = e.stats()
+            assert e.state_digest() == (st["state_digest"], st["chosen_digest"])
+            assert [got[k] for k in COUNTERS] == [st[k] for k in COUNTERS]
+            assert got["chosen"] == m - sb
+            res.append((e.state_digest(), e.read_chosen(m - 300, 300)))
+    assert res[0] == res[1]
+
+
 @pytest.mark.parametrize("shards,b", [(2, 256), (3, 256), (8, 256), (3, 100), (8, 255)])
 def test_sharded_device_generator_sums_to_whole(shards, b):
     """Instance sharding: per-shard counters and digests add
@@ -511,7 +534,7 @@ def test_store_chunks_tails_and_partial_pairs(extra):
 
 
 @pytest.mark.parametrize("env", [("MPX_PROP_CHUNK", "64"), ("MPX_PROP_CHUNK", "5"), ("MPX_STEP_WALK", "1"),
-                                 ("MPX_SCAN_SMALL", "0"), ("MPX_SCAN_SMALL", "1")])
+                                 ("MPX_SCAN_SMALL", "0"), ("MPX_SCAN_SMALL", "1"), ("MPX_PLAN_STORE", "0")])
 @pytest.mark.parametrize("name", ["fuzz_big_0", "c3_faulty_1", "c2_clean_n9_b100", "c5_member_1", "c5_member_3",
                                   "demo_s0", "demo5_s3", "hm_promise_merge"])
 def test_kept_alternative_paths(name, env, monkeypatch):
