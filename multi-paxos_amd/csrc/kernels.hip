@@ -1397,6 +1397,10 @@ __device__ inline uint64_t plan_pack(const uint32_t (&val)[4], const uint32_t (&
 // four segments describe the bucket and no instance lies under two live runs
 // (k_chosen compares their Values) the word is written and chosen_valid set,
 // else PLAN_SKIP leaves the bucket to k_chosen.
+// CLAMPED: the vote loads take clamped indices and no branch, so they are all in flight at once
+// (under a lane condition each was issued and waited for in turn); k_plan_store8 keeps the
+// conditional loads — one live run per bucket there, and 8 more VGPRs cost it occupancy
+template <bool CLAMPED = true>
 __device__ inline uint64_t plan_chosen_at(const DevView &v, uint64_t i, uint64_t oc, uint64_t c1, unsigned long long &cC)
 {
     constexpr uint32_t F = PLAN_FRAGS;
@@ -1407,8 +1411,15 @@ __device__ inline uint64_t plan_chosen_at(const DevView &v, uint64_t i, uint64_t
         uint32_t live[F];
 #pragma unroll
         for (uint32_t k = 0; k < F; ++k) w[k] = k < len ? frag_w1(v.cfrags + oc + k) : 0;
+        if (CLAMPED) {
 #pragma unroll
-        for (uint32_t k = 0; k < F; ++k) live[k] = k < len ? v.b_chosen[(uint32_t)w[k]] != NONE32 : 0;
+            for (uint32_t k = 0; k < F; ++k) live[k] = v.b_chosen[k < len ? (uint32_t)w[k] : 0];
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k) live[k] = k < len && live[k] != NONE32;
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k) live[k] = k < len ? v.b_chosen[(uint32_t)w[k]] != NONE32 : 0;
+        }
         bool ok = true;
         uint32_t sp[3] = {BS, BS, BS};
 #pragma unroll
@@ -1443,9 +1454,10 @@ __device__ inline uint64_t plan_chosen_at(const DevView &v, uint64_t i, uint64_t
     }
     return q;
 }
+template <bool CLAMPED = true>
 __device__ inline uint64_t plan_chosen_word(const DevView &v, uint64_t i, unsigned long long &cC)
 {
-    return plan_chosen_at(v, i, v.cf_off[i], v.cf_off[i + 1], cC);
+    return plan_chosen_at<CLAMPED>(v, i, v.cf_off[i], v.cf_off[i + 1], cC);
 }
 __device__ inline void plan_chosen(const DevView &v, uint64_t i, unsigned long long &cC)
 {
@@ -1454,8 +1466,8 @@ __device__ inline void plan_chosen(const DevView &v, uint64_t i, unsigned long l
 
 // k_plan's reduction of lean multi pair i (bucket b, len runs): its plan word, or PLAN_SKIP
 // (rest = 1 when the pair is in the list but no plan word describes it).  ldw(k) loads the
-// pair's k-th run descriptor word.
-template <typename LoadW>
+// pair's k-th run descriptor word.  CLAMPED: the scan-flag loads all in flight (plan_chosen_at).
+template <bool CLAMPED, typename LoadW>
 __device__ inline uint64_t plan_lean(const DevView &v, uint64_t i, uint64_t b, uint32_t len, bool in_list, LoadW ldw,
                                      unsigned long long &cA, unsigned long long &cL, uint32_t &rest)
 {
@@ -1466,9 +1478,16 @@ __device__ inline uint64_t plan_lean(const DevView &v, uint64_t i, uint64_t b, u
         uint32_t fg[F];
 #pragma unroll
         for (uint32_t k = 0; k < F; ++k) w[k] = k >= len ? 0 : ldw(k);
+        if (CLAMPED) {                     // a COMMIT run's scan flag is never read
 #pragma unroll
-        for (uint32_t k = 0; k < F; ++k)   // a COMMIT run's scan flag is never read
-            fg[k] = k < len && (w[k] >> 60) != K_COMMIT ? v.m_flags[(uint32_t)w[k]] : 0;
+            for (uint32_t k = 0; k < F; ++k) fg[k] = v.m_flags[k < len && (w[k] >> 60) != K_COMMIT ? (uint32_t)w[k] : 0];
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k) fg[k] = k < len && (w[k] >> 60) != K_COMMIT ? fg[k] : 0;
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < F; ++k)
+                fg[k] = k < len && (w[k] >> 60) != K_COMMIT ? v.m_flags[(uint32_t)w[k]] : 0;
+        }
         bool ok = (b + 1) * BS <= v.shard_len;
         uint32_t sp[3] = {BS, BS, BS};
 #pragma unroll
@@ -1564,7 +1583,7 @@ __global__ __launch_bounds__(256) void k_plan(DevView v, uint32_t apply_wgs)
         const uint32_t len = (uint32_t)(o1 - oa);
         const bool in_list = len && len <= FAST_MAX_FRAGS && !gp;
         const uint64_t rel = oa - wbase;                     // past the staged words: global loads (rare)
-        v.plan[i] = plan_lean(v, i, b, len, in_list,
+        v.plan[i] = plan_lean<true>(v, i, b, len, in_list,
                               [&](uint32_t k) { return rel + k < PLAN_LDS ? w_lds[wv][rel + k] : v.frag_w1[oa + k]; },
                               cA, cL, rest);
     }
@@ -1768,17 +1787,24 @@ __global__ __launch_bounds__(256, WAVES) void k_plan_list(DevView v, uint32_t ap
             }
             if (ok) {
                 // the accept runs' scan flags, 16 in flight at a time, then folded into bit 57
+                // (the loads take clamped indices and no branch: a load under a lane condition
+                // was issued and waited for one at a time, a memory round trip per run)
                 constexpr uint32_t FC = F < MPX_PL_FLAG_C ? F : MPX_PL_FLAG_C;
                 for (uint32_t k0 = 0; k0 < len; k0 += FC) {
-                    uint32_t fg[FC];
+                    uint32_t ix[FC], fg[FC];
+                    uint32_t acc = 0;
 #pragma unroll
                     for (uint32_t k = 0; k < FC; ++k) {
                         const uint64_t w = k0 + k < len ? W[k0 + k] : 0;
-                        fg[k] = k0 + k < len && (w >> 60) == K_ACCEPT ? v.m_flags[(uint32_t)w] : 0;
+                        const bool a = k0 + k < len && (w >> 60) == K_ACCEPT;
+                        ix[k] = a ? (uint32_t)w : 0;
+                        acc |= (uint32_t)a << k;
                     }
 #pragma unroll
+                    for (uint32_t k = 0; k < FC; ++k) fg[k] = v.m_flags[ix[k]];
+#pragma unroll
                     for (uint32_t k = 0; k < FC; ++k)
-                        if (k0 + k < len && (fg[k] & F_GRANTED)) W[k0 + k] |= MP_GRANTED;
+                        if (((acc >> k) & 1) && (fg[k] & F_GRANTED)) W[k0 + k] |= MP_GRANTED;
                 }
                 uint32_t lo[LSEG], sl[LSEG];
 #pragma unroll
@@ -1868,9 +1894,15 @@ __global__ __launch_bounds__(256, WAVES) void k_plan_list(DevView v, uint32_t ap
                         uint32_t em[8], ei[8];
 #pragma unroll
                         for (uint32_t j = 0; j < 8; ++j) em[j] = j < m ? v.ev_msg[e + j] : NONE32;
+                        uint32_t et[8], ef[8];
 #pragma unroll
-                        for (uint32_t j = 0; j < 8; ++j)
-                            ei[j] = j < m ? (uint32_t)v.m_type[em[j]] | ((uint32_t)v.m_flags[em[j]] << 8) : 0;
+                        for (uint32_t j = 0; j < 8; ++j) {       // (clamped, unconditional: all in flight)
+                            const uint32_t x = j < m ? em[j] : 0;
+                            et[j] = v.m_type[x];
+                            ef[j] = v.m_flags[x];
+                        }
+#pragma unroll
+                        for (uint32_t j = 0; j < 8; ++j) ei[j] = j < m ? et[j] | (ef[j] << 8) : 0;
 #pragma unroll
                         for (uint32_t j = 0; j < 8; ++j) {
                             if (j >= m) break;
@@ -2379,13 +2411,13 @@ __global__ __launch_bounds__(512, MPX_PS_WAVES) void k_plan_store8(DevView v, ui
                 const uint8_t gp = v.pair_gp[i];
                 const uint32_t len = (uint32_t)(o1 - oa);
                 const bool in_list = len && len <= FAST_MAX_FRAGS && !gp;
-                q = plan_lean(v, i, b, len, in_list, [&](uint32_t k) { return v.frag_w1[oa + k]; }, cA, cL, rest);
+                q = plan_lean<false>(v, i, b, len, in_list, [&](uint32_t k) { return v.frag_w1[oa + k]; }, cA, cL, rest);
             }
         } else if (t >= PS_CHOSEN && t < PS_CHOSEN + PS_G) {
             const uint64_t b = b0 + (t - PS_CHOSEN);
             if (b < NB) {
                 unsigned long long c = 0;
-                q = plan_chosen_word(v, b, c);
+                q = plan_chosen_word<false>(v, b, c);
                 cC += c;
             }
         }
@@ -2651,14 +2683,32 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                 }
                         }
                     } else if (kind == K_COMMIT) {
+                        // the re-commit Value check (:1508): the slots' two Values loaded together
+                        // (clamped indices, no branch per slot: one round trip, not one per slot)
+                        uint32_t chk = 0;
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j)
+                            chk |= (uint32_t)(k[j] >= 0 && (SF(j) & S_COMMITTED) && !(fl & FR_VEQ) &&
+                                              se[j] != (uint32_t)(ent + k[j])) << j;
+                        if (__ballot(chk)) {
+                            uint64_t va[SPL], vb[SPL];
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j) {
+                                const bool c = (chk >> j) & 1;
+                                va[j] = e_val[c ? se[j] : 0];
+                                vb[j] = e_val[c ? (uint32_t)(ent + k[j]) : 0];
+                            }
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j)
+                                if (((chk >> j) & 1) && va[j] != vb[j])
+                                    record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
+                                                     v.shard_begin + li0 + lane + 64 * j);
+                        }
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j)
                             if (k[j] >= 0) {
                                 const uint32_t x = (uint32_t)(ent + k[j]);
-                                if (SF(j) & S_COMMITTED) {                            // :1508
-                                    if (!(fl & FR_VEQ) && se[j] != x && e_val[se[j]] != e_val[x])
-                                        record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
-                                                         v.shard_begin + li0 + lane + 64 * j);
+                                if (SF(j) & S_COMMITTED) {                            // :1508 (checked above)
                                 } else {
                                     if (DIGEST) sb[j] = ballot;                                   // :1515
                                     SF_SET(j, S_PRESENT | S_COMMITTED); se[j] = x; sm[j] = fq;
@@ -2677,7 +2727,8 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                                 for (uint32_t j = 0; j < SPL; ++j) pid[j] = pu;
                             } else {
 #pragma unroll
-                                for (uint32_t j = 0; j < SPL; ++j) pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
+                                for (uint32_t j = 0; j < SPL; ++j)   // (clamped index, no branch: all in flight)
+                                    pid[j] = v.r_pid[ent + (k[j] >= 0 ? k[j] : 0)];
                             }
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
