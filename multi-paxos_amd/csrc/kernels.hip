@@ -2369,8 +2369,12 @@ __global__ __launch_bounds__(256) void k_store8(DevView v, uint32_t store_grid, 
 #ifndef MPX_PS_PW
 #define MPX_PS_PW 6
 #endif
-constexpr uint32_t PS_G = MPX_PS_G, PS_PW = MPX_PS_PW, PS_CHOSEN = 64 * (PS_PW - 1);
-static_assert(PS_G % 4 == 0 && PS_G <= 64 && PS_PW >= 2 && PS_PW <= 7, "k_plan_store8 shape");
+#ifndef MPX_PS_WG
+#define MPX_PS_WG 8
+#endif
+// PS_WG waves per workgroup, PS_PW of them planners
+constexpr uint32_t PS_G = MPX_PS_G, PS_PW = MPX_PS_PW, PS_WG = MPX_PS_WG, PS_CHOSEN = 64 * (PS_PW - 1);
+static_assert(PS_G % 4 == 0 && PS_G <= 64 && PS_PW >= 2 && PS_PW < PS_WG && PS_WG <= 16, "k_plan_store8 shape");
 __device__ inline void lds_barrier()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -2382,16 +2386,16 @@ __device__ inline void lds_barrier()
 #define MPX_PS_WAVES 6
 #endif
 #ifndef MPX_PS_WPC
-#define MPX_PS_WPC (MPX_PS_WAVES / 2)
+#define MPX_PS_WPC (MPX_PS_WAVES * 4 / MPX_PS_WG)
 #endif
-__global__ __launch_bounds__(512, MPX_PS_WAVES) void k_plan_store8(DevView v, uint32_t ps_grid, uint32_t n_partials)
+__global__ __launch_bounds__(64 * PS_WG, MPX_PS_WAVES) void k_plan_store8(DevView v, uint32_t ps_grid, uint32_t n_partials)
 {
-    constexpr uint32_t S = 8 - PS_PW, KPR = PS_G / 4;        // storer waves, KiB stores per row
+    constexpr uint32_t S = PS_WG - PS_PW, KPR = PS_G / 4;    // storer waves, KiB stores per row
     __shared__ uint64_t pw[2][64 * PS_PW];
-    __shared__ unsigned long long red[8][8];
+    __shared__ unsigned long long red[PS_WG][8];
     if (blockIdx.x >= ps_grid) {
         const uint32_t r = blockIdx.x - ps_grid, R = gridDim.x - ps_grid;
-        reduce_summary<8>(v, n_partials, red, 512 * r, 512 * R, r == 0);
+        reduce_summary<PS_WG>(v, n_partials, red, 64 * PS_WG * r, 64 * PS_WG * R, r == 0);
         return;
     }
     const uint32_t t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2653,14 +2657,34 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void k_apply(DevView v, uint64_t
                         const bool learn = kind == K_COMMIT;
                         if (learn || (mf & F_GRANTED)) {
                             const uint32_t seq = rl32(fmsg, a) - (uint32_t)v.node_off[n];
+                            // the learned-Value check of every slot at once (FR_VEQ: ingest found every
+                            // such Value equal — no loads; clamped indices, no branch per slot)
+                            uint32_t chk = 0;
+                            if (!(fl & FR_VEQ) && (!learn || (mf & F_PROP))) {
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j)
+                                    chk |= (uint32_t)(k[j] >= 0 && (SF(j) & S_COMMITTED) &&
+                                                      se[j] != (uint32_t)(ent + k[j])) << j;
+                            }
+                            if (__ballot(chk)) {
+                                uint64_t va[SPL], vb[SPL];
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j) {
+                                    const bool c = (chk >> j) & 1;
+                                    va[j] = e_val[c ? se[j] : 0];
+                                    vb[j] = e_val[c ? (uint32_t)(ent + k[j]) : 0];
+                                }
+#pragma unroll
+                                for (uint32_t j = 0; j < SPL; ++j)
+                                    if (((chk >> j) & 1) && va[j] != vb[j])
+                                        record_violation(v, MPX_V_LEARN_VALUE, n, seq, v.shard_begin + li0 + lane + 64 * j);
+                            }
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j) {
                                 if (k[j] < 0) continue;
                                 const uint32_t x = (uint32_t)(ent + k[j]);
                                 if (SF(j) & S_COMMITTED) {
-                                    // (FR_VEQ: ingest found every such Value equal — no loads)
-                                    if (!(fl & FR_VEQ) && se[j] != x && e_val[se[j]] != e_val[x] && (!learn || (mf & F_PROP)))
-                                        record_violation(v, MPX_V_LEARN_VALUE, n, seq, v.shard_begin + li0 + lane + 64 * j);
+                                    // (checked above)
                                 } else if (learn) {
                                     if (DIGEST) sb[j] = v.e_pid[x];
                                     SF_SET(j, S_PRESENT | S_COMMITTED); se[j] = x; sm[j] = fq;
@@ -3025,9 +3049,9 @@ __global__ __launch_bounds__(256) void k_apply_win(DevView v)
                         if (learn || (mf & F_GRANTED)) {
                             uint64_t pid[SPL], hv[SPL];
 #pragma unroll
-                            for (uint32_t j = 0; j < SPL; ++j) {
-                                pid[j] = k[j] >= 0 ? v.e_pid[ent + k[j]] : 0;
-                                hv[j] = k[j] >= 0 ? v.e_val[ent + k[j]] : 0;
+                            for (uint32_t j = 0; j < SPL; ++j) {   // (clamped, no branch: all in flight)
+                                pid[j] = v.e_pid[ent + (k[j] >= 0 ? k[j] : 0)];
+                                hv[j] = v.e_val[ent + (k[j] >= 0 ? k[j] : 0)];
                             }
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j) {
@@ -3047,18 +3071,24 @@ __global__ __launch_bounds__(256) void k_apply_win(DevView v)
                         }
                     } else if (kind == K_ACCEPT) {
                         if (mf & F_GRANTED) {
+                            uint64_t hv[SPL];
+#pragma unroll
+                            for (uint32_t j = 0; j < SPL; ++j) hv[j] = v.e_val[ent + (k[j] >= 0 ? k[j] : 0)];
 #pragma unroll
                             for (uint32_t j = 0; j < SPL; ++j)
                                 if (k[j] >= 0 && !(sval[j] & W_COMMITTED)) {                  // :1380
-                                    sbal[j] = ballot; sval[j] = W_PRESENT | v.e_val[ent + k[j]];  // :1387
+                                    sbal[j] = ballot; sval[j] = W_PRESENT | hv[j];             // :1387
                                     ++cA;
                                 }
                         }
                     } else if (kind == K_COMMIT) {
+                        uint64_t hv[SPL];
+#pragma unroll
+                        for (uint32_t j = 0; j < SPL; ++j) hv[j] = v.e_val[ent + (k[j] >= 0 ? k[j] : 0)];
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j)
                             if (k[j] >= 0) {
-                                const uint64_t x = v.e_val[ent + k[j]];
+                                const uint64_t x = hv[j];
                                 if (sval[j] & W_COMMITTED) {                                  // :1508
                                     if ((sval[j] & W_HANDLE) != x)
                                         record_violation(v, MPX_V_COMMIT_VALUE, n, rl32(fmsg, a) - v.node_off[n],
@@ -3072,8 +3102,8 @@ __global__ __launch_bounds__(256) void k_apply_win(DevView v)
                         uint64_t pid[SPL], hv[SPL];
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j) {
-                            pid[j] = k[j] >= 0 ? v.r_pid[ent + k[j]] : 0;
-                            hv[j] = k[j] >= 0 ? v.r_val[ent + k[j]] : 0;
+                            pid[j] = v.r_pid[ent + (k[j] >= 0 ? k[j] : 0)];
+                            hv[j] = v.r_val[ent + (k[j] >= 0 ? k[j] : 0)];
                         }
 #pragma unroll
                         for (uint32_t j = 0; j < SPL; ++j)
@@ -3972,7 +4002,7 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
             // pairs (it reads only the votes and the chosen-log runs)
             if (side3 && !skip_chosen) { launch_chosen(s, nullptr); chosen_done = true; }
         } else if (plan_store) {
-            hipExtLaunchKernelGGL(k_plan_store8, dim3(g.ps_wgs + cdiv(n_partials ? n_partials : 1, 512)), dim3(512), 0, s,
+            hipExtLaunchKernelGGL(k_plan_store8, dim3(g.ps_wgs + cdiv(n_partials ? n_partials : 1, 64 * PS_WG)), dim3(64 * PS_WG), 0, s,
                                   (hipEvent_t)ev_apply0, (hipEvent_t)ev_apply1, 0, v, g.ps_wgs, n_partials);
         } else {
             // (a fused plan-and-store kernel — four buckets' plan words decided per wave step and
