@@ -245,62 +245,94 @@ __global__ __launch_bounds__(256) void k_gate_epochs(DevView v)
     if (v.window && j == 0) v.ee_out[n] = st;           // the roles the next window starts from
 }
 
-// pass 2: every other record of the trace
+// pass 2: every other record of the trace.  GATE_PER records per thread, their loads all issued
+// before the block's marker staging (one occupancy round of blocks instead of several, each
+// paying the staging and three dependent round trips: C5 45.8 us with one record per thread)
+#ifndef MPX_GATE_PER
+#define MPX_GATE_PER 4
+#endif
+constexpr uint32_t GATE_PER = MPX_GATE_PER;
 __global__ __launch_bounds__(256) void k_gate_msgs(DevView v)
 {
     __shared__ GateLds L;
-    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    uint8_t t = MPX_MSG_E_EPOCH;
-    uint32_t n = 0;
-    if (g < v.num_msgs) { t = v.m_type[g]; n = v.m_node[g]; }   // in flight during the staging
-    const bool staged = gate_stage(v, L);
-    if (g >= v.num_msgs || t == MPX_MSG_E_EPOCH) return;
-    const uint32_t st = ee_before_lds(v, L, staged, n, (uint32_t)g), ep = st & 0xFFFF;
-    const bool acc = st & EE_ACC, prop = st & EE_PROP;
-    uint32_t gate = 0;
-    if (t == MPX_MSG_PREPARE || t == MPX_MSG_ACCEPT) {
-        gate = acc && v.m_ver[g] == v.ep_ver[ep] ? (st >> EE_SEG_SHIFT) & G_SEG : 0;
-    } else if (t == MPX_MSG_COMMIT) {
-        gate = prop ? G_PROP : 0;
-        if (prop) v.m_flags[g] |= F_PROP;
-    } else if (t == MPX_MSG_PREPARE_REPLY || t == MPX_MSG_ACCEPT_REPLY || t == MPX_MSG_P_START || t == MPX_MSG_P_BATCH) {
-        gate = prop ? (ep + 1) << G_EPOCH_SHIFT : 0;
+    const uint64_t g0 = (uint64_t)blockIdx.x * 256 * GATE_PER + threadIdx.x;
+    uint8_t t[GATE_PER], f[GATE_PER];
+    uint32_t n[GATE_PER], ver[GATE_PER];
+#pragma unroll
+    for (uint32_t k = 0; k < GATE_PER; ++k) {           // (clamped, no branch: in flight during the staging)
+        const uint64_t g = g0 + 256 * k, gc = g < v.num_msgs ? g : 0;
+        t[k] = v.m_type[gc]; n[k] = v.m_node[gc]; ver[k] = v.m_ver[gc]; f[k] = v.m_flags[gc];
     }
-    v.m_gate[g] = gate;
+    const bool staged = gate_stage(v, L);
+#pragma unroll
+    for (uint32_t k = 0; k < GATE_PER; ++k) {
+        const uint64_t g = g0 + 256 * k;
+        if (g >= v.num_msgs || t[k] == MPX_MSG_E_EPOCH) continue;
+        const uint32_t st = ee_before_lds(v, L, staged, n[k], (uint32_t)g), ep = st & 0xFFFF;
+        const bool acc = st & EE_ACC, prop = st & EE_PROP;
+        uint32_t gate = 0;
+        if (t[k] == MPX_MSG_PREPARE || t[k] == MPX_MSG_ACCEPT) {
+            gate = acc && ver[k] == v.ep_ver[ep] ? (st >> EE_SEG_SHIFT) & G_SEG : 0;
+        } else if (t[k] == MPX_MSG_COMMIT) {
+            gate = prop ? G_PROP : 0;
+            if (prop) v.m_flags[g] = f[k] | F_PROP;
+        } else if (t[k] == MPX_MSG_PREPARE_REPLY || t[k] == MPX_MSG_ACCEPT_REPLY || t[k] == MPX_MSG_P_START ||
+                   t[k] == MPX_MSG_P_BATCH) {
+            gate = prop ? (ep + 1) << G_EPOCH_SHIFT : 0;
+        }
+        v.m_gate[g] = gate;
+    }
 }
 
 // pass 3: the header-scan stream — a PREPARE / ACCEPT of a node without an
 // Acceptor of its version leaves the stream (SC_NONE), the others (and the
 // left-out ACCEPTs of header sharding, SC_VIRT) take the incarnation in their key,
 // so one prefix max restarts with every new Acceptor; a marker's key is its
-// incarnation.  Idempotent (a rerun finds the same keys and types).
+// incarnation.  Idempotent (a rerun finds the same keys and types).  GATE_PER records
+// per thread as k_gate_msgs.
 __global__ __launch_bounds__(256) void k_gate_scan(DevView v, uint64_t num_sc)
 {
     __shared__ GateLds L;
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t i0 = (uint64_t)blockIdx.x * 256 * GATE_PER + threadIdx.x;
+    uint8_t t[GATE_PER];
+    uint32_t g[GATE_PER], ver[GATE_PER];
+    uint64_t key[GATE_PER];
+#pragma unroll
+    for (uint32_t k = 0; k < GATE_PER; ++k) {           // (clamped, no branch: in flight during the staging)
+        const uint64_t i = i0 + 256 * k, ic = i < num_sc ? i : 0;
+        t[k] = v.sc_type[ic]; g[k] = v.sc_idx[ic]; ver[k] = v.sc_ver[ic]; key[k] = v.sc_key[ic];
+    }
+    uint32_t gate[GATE_PER], nd[GATE_PER];
+#pragma unroll
+    for (uint32_t k = 0; k < GATE_PER; ++k) {
+        const uint32_t gc = g[k] < v.num_msgs ? g[k] : 0;
+        gate[k] = v.m_gate[gc]; nd[k] = v.m_node[gc];
+    }
     const bool staged = gate_stage(v, L);
-    if (i >= num_sc) return;
-    const uint8_t t = v.sc_type[i];
-    const uint32_t kind = t & SC_KIND;
-    if (kind == SC_PS) {
-        v.sc_key[i] = (uint64_t)(v.m_gate[v.sc_idx[i]] & G_SEG) << SEG_SHIFT;
-        return;
+#pragma unroll
+    for (uint32_t k = 0; k < GATE_PER; ++k) {
+        const uint64_t i = i0 + 256 * k;
+        if (i >= num_sc) continue;
+        const uint32_t kind = t[k] & SC_KIND;
+        if (kind == SC_PS) {
+            v.sc_key[i] = (uint64_t)(gate[k] & G_SEG) << SEG_SHIFT;
+            continue;
+        }
+        if (!(kind == SC_PREP || kind == SC_ACC || (kind == SC_SONLY && (t[k] & SC_VIRT)))) continue;
+        uint32_t n;
+        if (t[k] & SC_VIRT) {                           // the node whose scan range holds i
+            uint32_t lo = 0, hi = v.N;
+            while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (v.sc_off[mid] <= i) lo = mid; else hi = mid; }
+            n = lo;
+        } else {
+            n = nd[k];
+        }
+        const uint32_t st = ee_before_lds(v, L, staged, n, g[k]), ep = st & 0xFFFF;
+        if ((st & EE_ACC) && ver[k] == v.ep_ver[ep])
+            v.sc_key[i] = (key[k] & LOW56) | ((uint64_t)((st >> EE_SEG_SHIFT) & G_SEG) << SEG_SHIFT);
+        else
+            v.sc_type[i] = SC_NONE;                     // dropped silently (:1702,1744)
     }
-    if (!(kind == SC_PREP || kind == SC_ACC || (kind == SC_SONLY && (t & SC_VIRT)))) return;
-    const uint32_t g = v.sc_idx[i];
-    uint32_t n;
-    if (t & SC_VIRT) {                                  // the node whose scan range holds i
-        uint32_t lo = 0, hi = v.N;
-        while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (v.sc_off[mid] <= i) lo = mid; else hi = mid; }
-        n = lo;
-    } else {
-        n = v.m_node[g];
-    }
-    const uint32_t st = ee_before_lds(v, L, staged, n, g), ep = st & 0xFFFF;
-    if ((st & EE_ACC) && v.sc_ver[i] == v.ep_ver[ep])
-        v.sc_key[i] = (v.sc_key[i] & LOW56) | ((uint64_t)((st >> EE_SEG_SHIFT) & G_SEG) << SEG_SHIFT);
-    else
-        v.sc_type[i] = SC_NONE;                         // dropped silently (:1702,1744)
 }
 
 // pass 4: vote lists — a reply counts only while its node has a Proposer
@@ -3856,8 +3888,8 @@ int launch_run(const DevView &v, void *stream_, LaunchGeom g, void *const ev[5],
     if (member) {
         // member role / version gates from the E_EPOCH markers (k_gate_*)
         hipLaunchKernelGGL(k_gate_epochs, dim3(v.N), dim3(256), 0, s, v);
-        if (v.num_msgs) hipLaunchKernelGGL(k_gate_msgs, dim3(cdiv(v.num_msgs, 256)), dim3(256), 0, s, v);
-        if (v.num_sc) hipLaunchKernelGGL(k_gate_scan, dim3(cdiv(v.num_sc, 256)), dim3(256), 0, s, v, v.num_sc);
+        if (v.num_msgs) hipLaunchKernelGGL(k_gate_msgs, dim3(cdiv(v.num_msgs, 256 * GATE_PER)), dim3(256), 0, s, v);
+        if (v.num_sc) hipLaunchKernelGGL(k_gate_scan, dim3(cdiv(v.num_sc, 256 * GATE_PER)), dim3(256), 0, s, v, v.num_sc);
         if (v.num_batches) hipLaunchKernelGGL(k_gate_votes, dim3(cdiv(v.num_batches, 256)), dim3(256), 0, s, v);
     }
     const bool small = v.scan_chunk == SCAN_CHUNK_SMALL;      // (the host cut the chunks: scan_chunk_for)

@@ -8,7 +8,7 @@ mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "${SEL:-c3 or c5 or golden or member or plan or clean}" > $out/tests.txt 2>&1 || { tail -30 $out/tests.txt; exit 1; }
 tail -1 $out/tests.txt
-bash tools/ab_legs.sh $tag head c3 c5 c5c || exit 2
-bash tools/ab_legs.sh ${tag}b head c3 c5c || exit 3
+bash tools/ab_legs.sh $tag head ${LEGS:-c3 c5 c5c} || exit 2
+bash tools/ab_legs.sh ${tag}b head ${LEGS2:-c3 c5c} || exit 3
 [ -z "$SKIP_C4" ] && { bash tools/ab_shard_c4.sh $tag head || exit 4; }
 true
